@@ -1,0 +1,1133 @@
+/*
+ * tfbs_oracle.c -- CPU restatement of find-tfbs's per-haplotype TFBS scoring path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle and the "port" CPU
+ * baseline.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+ * may load it; the product library (find-tfbs_amd/) never links or calls it.
+ *
+ * Parity status: pinned.  Checked against every offline-runnable vector the
+ * reference's own tests hold: haplotype.rs:172-254,
+ * pattern.rs:268-301 (+ the RC vectors of pattern.rs:192-260), main.rs:570-671,
+ * bed.rs:67-96, range.rs:93-107 and the decompressed text of
+ * test_data/expected_output_{1,2}.vcf.gz (tests/test_oracle_*.py).
+ *
+ * Each function cites the reference file:line it restates (paths relative to the
+ * find-tfbs v1.0.1 tree).  Deliberate determinism where the reference is random
+ * (HashMap iteration order):
+ *   D1 haplotype groups are processed in ascending Vec<Diff> order; when two
+ *      groups patch to the same sequence the later one overwrites the earlier
+ *      (HashMap::insert semantics, haplotype.rs:84) and the loser's ids stay in
+ *      the reference set (main.rs:103-105, 129-137).
+ *   D2 rows of one region are emitted sorted by (inner.start, inner.end, bed name,
+ *      pattern_id); POS numbers rows consecutively from 1 (main.rs:329, 424-425).
+ *   D3 DS is printed with printf("%.4f") of the exact f32 value (ties to even).
+ *
+ * Arithmetic follows a Rust --release build: i32 scores and u32 counts wrap.
+ */
+#define _GNU_SOURCE
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <ctype.h>
+
+#define ORC_OK 0
+#define ORC_E_BADBASE (-1)     /* util.rs:15 panic            */
+#define ORC_E_REFMISMATCH (-2) /* haplotype.rs:126-128 panic  */
+#define ORC_E_MNP (-3)         /* haplotype.rs:141-142 panic  */
+#define ORC_E_PLOIDY (-4)      /* haplotype.rs:32 assert      */
+#define ORC_E_RANGE (-5)       /* main.rs:407 u64 underflow   */
+#define ORC_E_PARSE (-6)       /* pattern.rs unwrap/expect    */
+#define ORC_E_IO (-7)
+#define ORC_E_ARG (-8)
+#define ORC_E_ALLELES (-9)     /* haplotype.rs:22 alleles[1] on a 1-allele record */
+#define ORC_E_ZEROLEN (-10)    /* pattern.rs:150-156 index past end for L = 0 */
+
+/* ------------------------------------------------------------------------- */
+/* small growable buffers                                                     */
+/* ------------------------------------------------------------------------- */
+typedef struct { char *p; size_t n, cap; } sbuf;
+static void sb_put(sbuf *b, const char *s, size_t n) {
+    if (b->n + n + 1 > b->cap) {
+        size_t c = b->cap ? b->cap * 2 : 256;
+        while (c < b->n + n + 1) c *= 2;
+        b->p = (char *)realloc(b->p, c);
+        b->cap = c;
+    }
+    memcpy(b->p + b->n, s, n);
+    b->n += n;
+    b->p[b->n] = 0;
+}
+static void sb_puts(sbuf *b, const char *s) { sb_put(b, s, strlen(s)); }
+
+#define VEC_PUSH(arr, n, cap, val)                                           \
+    do {                                                                     \
+        if ((n) == (cap)) {                                                  \
+            (cap) = (cap) ? (cap) * 2 : 8;                                   \
+            (arr) = realloc((arr), (size_t)(cap) * sizeof(*(arr)));          \
+        }                                                                    \
+        (arr)[(n)++] = (val);                                                \
+    } while (0)
+
+/* ------------------------------------------------------------------------- */
+/* types.rs / util.rs / range.rs                                              */
+/* ------------------------------------------------------------------------- */
+/* Nucleotide enum order A,C,G,T,N = weight index (types.rs:5-8, pattern.rs:119-123). */
+int orc_to_nucleotide(uint8_t l) { /* util.rs:4-16 */
+    switch (l) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    case 'N': case 'n': return 4;
+    default: return ORC_E_BADBASE;
+    }
+}
+
+typedef struct { uint64_t start, end; } orc_range; /* range.rs:4-8, inclusive */
+
+/* range.rs:18-21 -- asymmetric: are other's endpoints inside self? */
+int orc_range_overlaps(uint64_t ss, uint64_t se, uint64_t os, uint64_t oe) {
+    return (os >= ss && os <= se) || (oe >= ss && oe <= se);
+}
+
+/* range.rs:43-87 RangeStack::from_iter: stable sort by start, then merge while
+ * last.overlaps(next).  In/out arrays; returns the merged count. */
+static int cmp_range_start(const void *a, const void *b) {
+    const orc_range *x = (const orc_range *)a, *y = (const orc_range *)b;
+    if (x->start < y->start) return -1;
+    if (x->start > y->start) return 1;
+    return 0;
+}
+int orc_merge_ranges(const uint64_t *starts, const uint64_t *ends, int n, uint64_t *out_s, uint64_t *out_e) {
+    orc_range *r = (orc_range *)malloc(sizeof(orc_range) * (n ? n : 1));
+    for (int i = 0; i < n; i++) { r[i].start = starts[i]; r[i].end = ends[i]; }
+    /* stable insertion-merge sort to keep Rust's stable sort_by semantics */
+    for (int i = 1; i < n; i++) {
+        orc_range k = r[i];
+        int j = i - 1;
+        while (j >= 0 && cmp_range_start(&r[j], &k) > 0) { r[j + 1] = r[j]; j--; }
+        r[j + 1] = k;
+    }
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        if (m > 0 && orc_range_overlaps(out_s[m - 1], out_e[m - 1], r[i].start, r[i].end)) {
+            if (r[i].start < out_s[m - 1]) out_s[m - 1] = r[i].start; /* range.rs:31-34 */
+            if (r[i].end > out_e[m - 1]) out_e[m - 1] = r[i].end;
+        } else {
+            out_s[m] = r[i].start; out_e[m] = r[i].end; m++;
+        }
+    }
+    free(r);
+    return m;
+}
+
+/* ------------------------------------------------------------------------- */
+/* pattern.rs parsing                                                          */
+/* ------------------------------------------------------------------------- */
+/* Rust's f32::from_str grammar (decimal, optional sign, optional exponent,
+ * inf/infinity/nan); no hex, no surrounding whitespace.  Returns 0 on success. */
+static int rust_parse_f32(const char *s, float *out) {
+    const char *p = s;
+    if (*p == '+' || *p == '-') p++;
+    if (!strcasecmp(p, "inf") || !strcasecmp(p, "infinity") || !strcasecmp(p, "nan")) {
+        *out = strtof(s, NULL);
+        return 0;
+    }
+    int digits = 0;
+    while (isdigit((unsigned char)*p)) { p++; digits++; }
+    if (*p == '.') { p++; while (isdigit((unsigned char)*p)) { p++; digits++; } }
+    if (!digits) return -1;
+    if (*p == 'e' || *p == 'E') {
+        p++;
+        if (*p == '+' || *p == '-') p++;
+        if (!isdigit((unsigned char)*p)) return -1;
+        while (isdigit((unsigned char)*p)) p++;
+    }
+    if (*p) return -1;
+    *out = strtof(s, NULL);
+    return 0;
+}
+
+/* pattern.rs:13-16: (x_f32 * 1000.0_f32).round() as i32 (saturating cast, NaN -> 0). */
+static int32_t weight_from_f32(float x) {
+    float y = x * 1000.0f;
+    float r = roundf(y);
+    if (r != r) return 0;
+    if (r >= 2147483647.0f) return INT32_MAX;
+    if (r <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)r;
+}
+int orc_parse_weight(const char *s, int32_t *out) {
+    float x;
+    if (rust_parse_f32(s, &x)) return ORC_E_PARSE;
+    *out = weight_from_f32(x);
+    return ORC_OK;
+}
+
+/* split_whitespace into at most maxf fields (counts all fields). */
+static int split_ws(char *line, char **f, int maxf) {
+    int n = 0;
+    char *p = line;
+    while (*p) {
+        while (*p && isspace((unsigned char)*p)) p++;
+        if (!*p) break;
+        char *st = p;
+        while (*p && !isspace((unsigned char)*p)) p++;
+        if (n < maxf) f[n] = st;
+        n++;
+        if (*p) { *p = 0; p++; }
+    }
+    return n;
+}
+
+/* pattern.rs:18-35 parse_threshold_file: the LAST line with exactly two fields
+ * whose p-value (f32) is > pwm_threshold (f32) wins.  1 found, 0 none, <0 error. */
+int orc_parse_threshold_file(const char *path, float pwm_threshold, int32_t *out) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return ORC_E_IO; /* pattern.rs:116 expect -> panic */
+    char *line = NULL;
+    size_t cap = 0;
+    ssize_t n;
+    int found = 0;
+    while ((n = getline(&line, &cap, f)) >= 0) {
+        char *fl[3];
+        if (split_ws(line, fl, 3) == 2) {
+            int32_t w;
+            float pv;
+            if (orc_parse_weight(fl[0], &w)) { found = ORC_E_PARSE; break; }
+            if (rust_parse_f32(fl[1], &pv)) { found = ORC_E_PARSE; break; }
+            if (pv > pwm_threshold) { *out = w; found = 1; }
+        }
+    }
+    free(line);
+    fclose(f);
+    return found;
+}
+
+typedef struct {
+    int kind;           /* 0 = PWM, 1 = OtherPattern (types.rs:86-90) */
+    int direction;      /* 0 = P, 1 = N (types.rs:72-75) */
+    uint16_t pattern_id;
+    int32_t min_score;
+    int len;
+    int32_t *w;         /* len x 5, [A,C,G,T,N=0] (types.rs:103-114) */
+    char *name;
+} orc_pattern;
+
+typedef struct {
+    orc_pattern *p;
+    int n, cap;
+} orc_patterns;
+
+static void pat_push(orc_patterns *ps, int kind, int dir, uint16_t id, int32_t min, int len, const int32_t *w5, const char *name) {
+    orc_pattern q;
+    q.kind = kind; q.direction = dir; q.pattern_id = id; q.min_score = min; q.len = len;
+    q.w = (int32_t *)malloc(sizeof(int32_t) * 5 * (len ? len : 1));
+    if (len) memcpy(q.w, w5, sizeof(int32_t) * 5 * len);
+    q.name = strdup(name ? name : "");
+    VEC_PUSH(ps->p, ps->n, ps->cap, q);
+}
+
+/* pattern.rs:89-101 parse_pwm_definition over one '>'-chunk (modified in place). */
+static int parse_pwm_definition(char *chunk, char **name, int32_t **w5, int *len) {
+    /* lines = chunk.split("\n").filter(|x| x.len() > 0) */
+    char **lines = NULL;
+    int nl = 0, cl = 0;
+    char *p = chunk;
+    for (;;) {
+        char *e = strchr(p, '\n');
+        if (e) *e = 0;
+        if (*p) VEC_PUSH(lines, nl, cl, p);
+        if (!e) break;
+        p = e + 1;
+    }
+    if (nl == 0) { free(lines); return ORC_E_PARSE; } /* lines[0] panics */
+    *name = lines[0];
+    int32_t *w = (int32_t *)malloc(sizeof(int32_t) * 5 * nl);
+    int L = 0;
+    for (int i = 1; i < nl; i++) {
+        char *fl[5];
+        char *tmp = strdup(lines[i]);
+        int nf = split_ws(tmp, fl, 5);
+        if (nf == 4) {
+            int32_t a, c, g, t;
+            if (orc_parse_weight(fl[0], &a) || orc_parse_weight(fl[1], &c) || orc_parse_weight(fl[2], &g) ||
+                orc_parse_weight(fl[3], &t)) {
+                free(tmp); free(w); free(lines);
+                return ORC_E_PARSE;
+            }
+            w[L * 5 + 0] = a; w[L * 5 + 1] = c; w[L * 5 + 2] = g; w[L * 5 + 3] = t; w[L * 5 + 4] = 0;
+            L++;
+        }
+        free(tmp);
+    }
+    free(lines);
+    *w5 = w;
+    *len = L;
+    return ORC_OK;
+}
+
+/* pattern.rs:103-112: reverse the columns, then [a,c,g,t] -> [t,g,c,a]. */
+void orc_reverse_complement(const int32_t *w5, int len, int32_t *out5) {
+    for (int j = 0; j < len; j++) {
+        const int32_t *x = w5 + 5 * (len - 1 - j);
+        out5[5 * j + 0] = x[3];
+        out5[5 * j + 1] = x[2];
+        out5[5 * j + 2] = x[1];
+        out5[5 * j + 3] = x[0];
+        out5[5 * j + 4] = 0;
+    }
+}
+
+orc_patterns *orc_patterns_new(void) { return (orc_patterns *)calloc(1, sizeof(orc_patterns)); }
+void orc_patterns_free(orc_patterns *ps) {
+    if (!ps) return;
+    for (int i = 0; i < ps->n; i++) { free(ps->p[i].w); free(ps->p[i].name); }
+    free(ps->p);
+    free(ps);
+}
+int orc_patterns_count(const orc_patterns *ps) { return ps->n; }
+int orc_pattern_info(const orc_patterns *ps, int i, int *kind, int *dir, int *pid, int32_t *min, int *len) {
+    if (i < 0 || i >= ps->n) return ORC_E_ARG;
+    *kind = ps->p[i].kind; *dir = ps->p[i].direction; *pid = ps->p[i].pattern_id;
+    *min = ps->p[i].min_score; *len = ps->p[i].len;
+    return ORC_OK;
+}
+const int32_t *orc_pattern_weights(const orc_patterns *ps, int i) { return ps->p[i].w; }
+const char *orc_pattern_name(const orc_patterns *ps, int i) { return ps->p[i].name; }
+void orc_patterns_add(orc_patterns *ps, int kind, int dir, int pid, int32_t min, int len, const int32_t *w5, const char *name) {
+    pat_push(ps, kind, dir, (uint16_t)pid, min, len, w5, name);
+}
+
+/* pattern.rs:37-87 parse_pwm_files.  names_csv is the comma-joined wanted list
+ * (main.rs:197).  Returns the count of patterns or an error. */
+int orc_parse_pwm_files(const char *pwm_file, const char *threshold_dir, float pwm_threshold, const char *names_csv,
+                        int add_reverse, orc_patterns *out) {
+    /* wanted names (split(',')) */
+    char *nc = strdup(names_csv);
+    char **wanted = NULL;
+    int nw = 0, cw = 0;
+    {
+        char *p = nc;
+        for (;;) {
+            char *e = strchr(p, ',');
+            if (e) *e = 0;
+            VEC_PUSH(wanted, nw, cw, p);
+            if (!e) break;
+            p = e + 1;
+        }
+    }
+    /* thresholds (pattern.rs:40-50) */
+    int32_t *thr = (int32_t *)malloc(sizeof(int32_t) * nw);
+    int *has = (int *)calloc(nw, sizeof(int));
+    /* trim_end_matches("/") */
+    char *dir = strdup(threshold_dir);
+    size_t dl = strlen(dir);
+    while (dl > 0 && dir[dl - 1] == '/') dir[--dl] = 0;
+    int rc = ORC_OK;
+    for (int i = 0; i < nw && rc == ORC_OK; i++) {
+        char path[4096];
+        snprintf(path, sizeof path, "%s/%s.thr", dir, wanted[i]);
+        int32_t v;
+        int r = orc_parse_threshold_file(path, pwm_threshold, &v);
+        if (r < 0) rc = r;
+        else if (r == 1) { thr[i] = v; has[i] = 1; }
+    }
+    if (rc != ORC_OK) goto done;
+    {
+        FILE *f = fopen(pwm_file, "rb");
+        if (!f) { rc = ORC_E_IO; goto done; } /* pattern.rs:64 exit(1) */
+        fseek(f, 0, SEEK_END);
+        long sz = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        char *content = (char *)malloc(sz + 1);
+        if (fread(content, 1, sz, f) != (size_t)sz) { fclose(f); free(content); rc = ORC_E_IO; goto done; }
+        content[sz] = 0;
+        fclose(f);
+        uint16_t pattern_id = 0;
+        char *p = content;
+        for (;;) {
+            char *e = strchr(p, '>');
+            if (e) *e = 0;
+            if (strlen(p) >= 1) { /* pattern.rs:67 */
+                char *name;
+                int32_t *w5;
+                int L;
+                int r = parse_pwm_definition(p, &name, &w5, &L);
+                if (r) { rc = r; free(content); goto done; }
+                int wi = -1; /* wanted_pwms.contains(&name): thresholds keyed by name (last insert wins) */
+                for (int i = 0; i < nw; i++)
+                    if (!strcmp(wanted[i], name)) wi = i;
+                if (wi >= 0) {
+                    int hasthr = 0;
+                    int32_t ms = 0;
+                    for (int i = 0; i < nw; i++)
+                        if (!strcmp(wanted[i], name) && has[i]) { hasthr = 1; ms = thr[i]; }
+                    if (hasthr) {
+                        pat_push(out, 0, 0, pattern_id, ms, L, w5, name);
+                        if (add_reverse) {
+                            int32_t *rc5 = (int32_t *)malloc(sizeof(int32_t) * 5 * (L ? L : 1));
+                            orc_reverse_complement(w5, L, rc5);
+                            pat_push(out, 0, 1, pattern_id, ms, L, rc5, name);
+                            free(rc5);
+                        }
+                    }
+                    pattern_id = (uint16_t)(pattern_id + 1); /* pattern.rs:81 */
+                }
+                free(w5);
+            }
+            if (!e) break;
+            p = e + 1;
+        }
+        free(content);
+    }
+done:
+    free(dir); free(thr); free(has); free(wanted); free(nc);
+    return rc == ORC_OK ? out->n : rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* haplotype.rs                                                               */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    uint64_t pos;
+    uint8_t *ref; int nref;
+    uint8_t *alt; int nalt;
+} orc_diff; /* types.rs:39-44 */
+
+/* derived Ord on Diff: pos, then reference Vec, then alternative Vec (lexicographic). */
+static int cmp_nucvec(const uint8_t *a, int na, const uint8_t *b, int nb) {
+    int n = na < nb ? na : nb;
+    for (int i = 0; i < n; i++)
+        if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+static int cmp_diff(const orc_diff *a, const orc_diff *b) {
+    if (a->pos != b->pos) return a->pos < b->pos ? -1 : 1;
+    int c = cmp_nucvec(a->ref, a->nref, b->ref, b->nref);
+    if (c) return c;
+    return cmp_nucvec(a->alt, a->nalt, b->alt, b->nalt);
+}
+static int cmp_diffptr(const void *a, const void *b) {
+    return cmp_diff(*(const orc_diff *const *)a, *(const orc_diff *const *)b);
+}
+
+typedef struct { uint8_t *nuc; uint64_t *pos; int n, cap; } nucpos_vec; /* Vec<NucleotidePos> */
+static void np_push(nucpos_vec *v, uint8_t nuc, uint64_t pos) {
+    if (v->n == v->cap) {
+        v->cap = v->cap ? v->cap * 2 : 64;
+        v->nuc = (uint8_t *)realloc(v->nuc, v->cap);
+        v->pos = (uint64_t *)realloc(v->pos, sizeof(uint64_t) * v->cap);
+    }
+    v->nuc[v->n] = nuc;
+    v->pos[v->n] = pos;
+    v->n++;
+}
+
+/* haplotype.rs:90-92 get(): filter the reference window by pos in [s, e]. */
+static void get_range(uint64_t s, uint64_t e, const uint8_t *rn, const uint64_t *rp, int nr, nucpos_vec *out) {
+    for (int i = 0; i < nr; i++)
+        if (rp[i] >= s && rp[i] <= e) np_push(out, rn[i], rp[i]);
+}
+
+/* haplotype.rs:94-156 patch_haplotype; the recursion of next_chunk is unrolled
+ * into a loop with identical case order. */
+static int patch_haplotype_impl(uint64_t rs, uint64_t re, orc_diff *const *diffs, int nd, const uint8_t *rn,
+                                const uint64_t *rp, int nr, nucpos_vec *out) {
+    orc_diff **sd = (orc_diff **)malloc(sizeof(orc_diff *) * (nd ? nd : 1));
+    int n = 0;
+    for (int i = 0; i < nd; i++)
+        if (diffs[i]->pos >= rs && diffs[i]->pos <= re) sd[n++] = diffs[i];
+    qsort(sd, n, sizeof(orc_diff *), cmp_diffptr); /* equal diffs are indistinguishable: stability irrelevant */
+    uint64_t ref_position = rs;
+    int k = 0;
+    int rc = ORC_OK;
+    for (;;) {
+        if (k == n) { /* 100-108 */
+            if (ref_position <= re) get_range(ref_position, re, rn, rp, nr, out);
+            break;
+        }
+        const orc_diff *d = sd[k];
+        if (d->pos > ref_position) { /* 110-114 */
+            get_range(ref_position, d->pos - 1, rn, rp, nr, out);
+            ref_position = d->pos;
+            continue;
+        } else if (d->pos == ref_position && d->nref == 1) { /* 115-135 SNV or insertion */
+            uint8_t nuc = 4; /* Nucleotide::N */
+            for (int i = 0; i < nr; i++)
+                if (rp[i] == ref_position) nuc = rn[i];
+            if (d->ref[0] != nuc) { rc = ORC_E_REFMISMATCH; break; }
+            for (int i = 0; i < d->nalt; i++) np_push(out, d->alt[i], ref_position);
+            ref_position += 1;
+            k++;
+        } else if (d->pos == ref_position && d->nalt == 1) { /* 136-140 deletion */
+            np_push(out, d->alt[0], ref_position);
+            ref_position += (uint64_t)d->nref;
+            k++;
+        } else if (d->pos == ref_position) { /* 141-143 */
+            rc = ORC_E_MNP;
+            break;
+        } else if (ref_position >= re) { /* 144-146 */
+            get_range(ref_position, ref_position, rn, rp, nr, out);
+            break;
+        } else { /* 147-149: overlapping diffs truncate the haplotype */
+            break;
+        }
+    }
+    free(sd);
+    return rc;
+}
+
+/* C-ABI for unit tests: diffs given as flat arrays (ref/alt as nucleotide codes). */
+int orc_patch_haplotype(uint64_t rs, uint64_t re, int nd, const uint64_t *dpos, const uint8_t *dref, const int *dnref,
+                        const uint8_t *dalt, const int *dnalt, const uint8_t *rn, const uint64_t *rp, int nr,
+                        uint8_t *out_nuc, uint64_t *out_pos, int cap) {
+    orc_diff *ds = (orc_diff *)malloc(sizeof(orc_diff) * (nd ? nd : 1));
+    orc_diff **pp = (orc_diff **)malloc(sizeof(orc_diff *) * (nd ? nd : 1));
+    int ro = 0, ao = 0;
+    for (int i = 0; i < nd; i++) {
+        ds[i].pos = dpos[i];
+        ds[i].ref = (uint8_t *)dref + ro; ds[i].nref = dnref[i]; ro += dnref[i];
+        ds[i].alt = (uint8_t *)dalt + ao; ds[i].nalt = dnalt[i]; ao += dnalt[i];
+        pp[i] = &ds[i];
+    }
+    nucpos_vec out = {0};
+    int rc = patch_haplotype_impl(rs, re, pp, nd, rn, rp, nr, &out);
+    if (rc == ORC_OK) {
+        if (out.n > cap) rc = ORC_E_ARG;
+        else {
+            memcpy(out_nuc, out.nuc, out.n);
+            memcpy(out_pos, out.pos, sizeof(uint64_t) * out.n);
+            rc = out.n;
+        }
+    }
+    free(out.nuc); free(out.pos); free(ds); free(pp);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* pattern.rs matching                                                        */
+/* ------------------------------------------------------------------------- */
+/* pattern.rs:141-171 matches() + 125-135 apply_pwm(): every window start i with
+ * score > min_score (strict) yields Match{[pos_i, pos_i + L - 1]}.  Callback style. */
+typedef void (*match_cb)(void *ctx, uint64_t s, uint64_t e);
+static int matches_impl(const orc_pattern *p, const uint8_t *nuc, const uint64_t *pos, int n, match_cb cb, void *ctx) {
+    if (p->kind != 0) return ORC_OK; /* OtherPattern: no matches (pattern.rs:166-168) */
+    int L = p->len;
+    if (n < L) return ORC_OK;
+    for (int i = 0; i <= n - L; i++) {
+        uint32_t score = 0; /* i32 sum, wrapping as in --release */
+        for (int j = 0; j < L; j++) score += (uint32_t)p->w[j * 5 + nuc[i + j]];
+        if ((int32_t)score > p->min_score) {
+            if (L == 0 && i == n) return ORC_E_ZEROLEN; /* haplotype[i] out of bounds */
+            cb(ctx, pos[i], pos[i] + (uint64_t)L - 1);
+        }
+    }
+    return ORC_OK;
+}
+
+typedef struct { uint64_t *s, *e; int n, cap; } mlist;
+static void mlist_cb(void *ctx, uint64_t s, uint64_t e) {
+    mlist *m = (mlist *)ctx;
+    if (m->n == m->cap) {
+        m->cap = m->cap ? m->cap * 2 : 16;
+        m->s = (uint64_t *)realloc(m->s, sizeof(uint64_t) * m->cap);
+        m->e = (uint64_t *)realloc(m->e, sizeof(uint64_t) * m->cap);
+    }
+    m->s[m->n] = s; m->e[m->n] = e; m->n++;
+}
+
+/* C-ABI: one pattern over one haplotype -> match ranges. */
+int orc_matches(const int32_t *w5, int len, int32_t min_score, int kind, const uint8_t *nuc, const uint64_t *pos, int n,
+                uint64_t *out_s, uint64_t *out_e, int cap) {
+    orc_pattern p;
+    p.kind = kind; p.len = len; p.w = (int32_t *)w5; p.min_score = min_score;
+    mlist m = {0};
+    int rc = matches_impl(&p, nuc, pos, n, mlist_cb, &m);
+    if (rc == ORC_OK) {
+        if (m.n > cap) rc = ORC_E_ARG;
+        else {
+            memcpy(out_s, m.s, sizeof(uint64_t) * m.n);
+            memcpy(out_e, m.e, sizeof(uint64_t) * m.n);
+            rc = m.n;
+        }
+    }
+    free(m.s); free(m.e);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
+/* main.rs:439-498 counts_as_genotypes                                        */
+/* ------------------------------------------------------------------------- */
+static int cmp_u32(const void *a, const void *b) {
+    uint32_t x = *(const uint32_t *)a, y = *(const uint32_t *)b;
+    return x < y ? -1 : (x > y ? 1 : 0);
+}
+/* Returns 1 and fills the INFO/genotype strings if the counts vary, else 0. */
+static int counts_as_genotypes_impl(const uint32_t *v1, const uint32_t *v2, int n, uint32_t *maf, sbuf *info,
+                                    sbuf *gts) {
+    if (n == 0) return 0;
+    uint32_t *v = (uint32_t *)malloc(sizeof(uint32_t) * n);
+    for (int i = 0; i < n; i++) v[i] = v1[i] + v2[i];
+    uint32_t lowest = v[0], highest = v[0];
+    for (int i = 1; i < n; i++) {
+        if (v[i] < lowest) lowest = v[i];
+        if (v[i] > highest) highest = v[i];
+    }
+    if (lowest == highest) { free(v); return 0; }
+    uint32_t i1 = (lowest * 1000u * 3u + highest * 1000u) / 4u;
+    uint32_t i3 = (lowest * 1000u + highest * 1000u * 3u) / 4u;
+    uint32_t *all = (uint32_t *)malloc(sizeof(uint32_t) * (n + 2));
+    int na = 0;
+    all[na++] = lowest; all[na++] = highest;
+    uint32_t zero = 0, one = 0, two = 0;
+    float lowf = (float)lowest;
+    float spread = (float)highest - lowf;
+    char tmp[64];
+    for (int i = 0; i < n; i++) {
+        uint32_t x = v[i];
+        if (x == lowest) { sb_puts(gts, "\t0|0:0.0"); zero++; }
+        else if (x == highest) { sb_puts(gts, "\t1|1:2.0"); two++; }
+        else {
+            int seen = 0;
+            for (int j = 0; j < na; j++) if (all[j] == x) { seen = 1; break; }
+            if (!seen) all[na++] = x;
+            uint32_t x1000 = x * 1000u;
+            if (x1000 < i1) { sb_puts(gts, "\t0|0"); zero++; }
+            else if (x1000 < i3) { sb_puts(gts, "\t0|1"); one++; }
+            else { sb_puts(gts, "\t1|1"); two++; }
+            float ds = (((float)x - lowf) * 2.0f) / spread;
+            snprintf(tmp, sizeof tmp, ":%.4f", (double)ds);
+            sb_puts(gts, tmp);
+        }
+    }
+    if (zero >= one && zero >= two) *maf = one + two;
+    else if (two >= zero && two >= one) *maf = zero + one;
+    else *maf = zero + two;
+    qsort(all, na, sizeof(uint32_t), cmp_u32);
+    sb_puts(info, "COUNTS=");
+    for (int j = 0; j < na; j++) {
+        snprintf(tmp, sizeof tmp, j ? ",%u" : "%u", all[j]);
+        sb_puts(info, tmp);
+    }
+    snprintf(tmp, sizeof tmp, ";freqs=%u/%u/%u", zero, one, two);
+    sb_puts(info, tmp);
+    free(all); free(v);
+    return 1;
+}
+
+/* C-ABI: returns 1 (row) / 0 (no variation); writes NUL-terminated strings. */
+int orc_counts_as_genotypes(const uint32_t *v1, const uint32_t *v2, int n, uint32_t *maf, char *info, size_t info_cap,
+                            char *gts, size_t gts_cap) {
+    sbuf a = {0}, b = {0};
+    int r = counts_as_genotypes_impl(v1, v2, n, maf, &a, &b);
+    if (r == 1) {
+        if (a.n + 1 > info_cap || b.n + 1 > gts_cap) r = ORC_E_ARG;
+        else { memcpy(info, a.p, a.n + 1); memcpy(gts, b.p, b.n + 1); }
+    }
+    free(a.p); free(b.p);
+    return r;
+}
+
+/* ------------------------------------------------------------------------- */
+/* main.rs:500-534 count_matches_by_sample (exposed for main.rs:570-671)      */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    int bed;            /* index of the bed basename */
+    uint64_t s, e;      /* inner range (value identity) */
+    uint16_t pid;
+    uint32_t *l, *r;
+} orc_key;
+
+typedef struct { orc_key *k; int n, cap; int nsamp; } keymap;
+
+static orc_key *key_get(keymap *m, int bed, uint64_t s, uint64_t e, uint16_t pid) {
+    for (int i = 0; i < m->n; i++) {
+        orc_key *k = &m->k[i];
+        if (k->bed == bed && k->s == s && k->e == e && k->pid == pid) return k;
+    }
+    orc_key nk;
+    nk.bed = bed; nk.s = s; nk.e = e; nk.pid = pid;
+    nk.l = (uint32_t *)calloc(m->nsamp ? m->nsamp : 1, sizeof(uint32_t));
+    nk.r = (uint32_t *)calloc(m->nsamp ? m->nsamp : 1, sizeof(uint32_t));
+    VEC_PUSH(m->k, m->n, m->cap, nk);
+    return &m->k[m->n - 1];
+}
+static void keymap_free(keymap *m) {
+    for (int i = 0; i < m->n; i++) { free(m->k[i].l); free(m->k[i].r); }
+    free(m->k);
+    m->k = NULL; m->n = m->cap = 0;
+}
+
+/* haplotype id = 2*sample_id + side (0 = Left, 1 = Right). */
+static void count_one_match(keymap *m, int nbeds, const int *inner_bed, const uint64_t *inner_s, const uint64_t *inner_e,
+                            int ninner, uint64_t ms, uint64_t me, uint16_t pid, const uint32_t *ids, int nids) {
+    (void)nbeds;
+    for (int i = 0; i < ninner; i++) {
+        if (!orc_range_overlaps(inner_s[i], inner_e[i], ms, me)) continue; /* main.rs:503 */
+        orc_key *k = key_get(m, inner_bed[i], inner_s[i], inner_e[i], pid);
+        for (int j = 0; j < nids; j++) {
+            uint32_t h = ids[j];
+            if (h & 1) k->r[h >> 1] += 1;
+            else k->l[h >> 1] += 1;
+        }
+    }
+}
+
+/* C-ABI mirror of count_matches_by_sample for the reference's unit test.
+ * matches: (start, end, pid, id offset, id count) over a flat id array.
+ * inner peaks: flat (bed index, start, end) list; duplicates double-count.
+ * Output: keys sorted (s, e, bed, pid); caller reads them via orc_keys_*. */
+typedef struct { keymap m; } orc_keys;
+static int cmp_key(const void *a, const void *b) {
+    const orc_key *x = (const orc_key *)a, *y = (const orc_key *)b;
+    if (x->s != y->s) return x->s < y->s ? -1 : 1;
+    if (x->e != y->e) return x->e < y->e ? -1 : 1;
+    if (x->bed != y->bed) return x->bed < y->bed ? -1 : 1;
+    if (x->pid != y->pid) return x->pid < y->pid ? -1 : 1;
+    return 0;
+}
+orc_keys *orc_count_matches_by_sample(int nsamp, int nmatch, const uint64_t *ms, const uint64_t *me, const uint16_t *mpid,
+                                      const int *id_off, const int *id_cnt, const uint32_t *ids, int ninner,
+                                      const int *inner_bed, const uint64_t *inner_s, const uint64_t *inner_e) {
+    orc_keys *k = (orc_keys *)calloc(1, sizeof(orc_keys));
+    k->m.nsamp = nsamp;
+    for (int i = 0; i < nmatch; i++)
+        count_one_match(&k->m, 0, inner_bed, inner_s, inner_e, ninner, ms[i], me[i], mpid[i], ids + id_off[i], id_cnt[i]);
+    qsort(k->m.k, k->m.n, sizeof(orc_key), cmp_key);
+    return k;
+}
+int orc_keys_count(const orc_keys *k) { return k->m.n; }
+int orc_keys_get(const orc_keys *k, int i, int *bed, uint64_t *s, uint64_t *e, int *pid, uint32_t *l, uint32_t *r) {
+    if (i < 0 || i >= k->m.n) return ORC_E_ARG;
+    const orc_key *q = &k->m.k[i];
+    *bed = q->bed; *s = q->s; *e = q->e; *pid = q->pid;
+    if (l) memcpy(l, q->l, sizeof(uint32_t) * k->m.nsamp);
+    if (r) memcpy(r, q->r, sizeof(uint32_t) * k->m.nsamp);
+    return ORC_OK;
+}
+void orc_keys_free(orc_keys *k) {
+    if (!k) return;
+    keymap_free(&k->m);
+    free(k);
+}
+
+/* ------------------------------------------------------------------------- */
+/* Region job: main.rs:395-436 process_peak + 94-154 find_all_matches +        */
+/* haplotype.rs:13-88 load_diffs / group_by_diffs / load_haplotypes            */
+/* ------------------------------------------------------------------------- */
+typedef struct {
+    char *name;                   /* bed basename (bed.rs:49-60) */
+    uint64_t *s, *e; int n, cap;  /* peaks after the after_position filter, file order */
+} orc_bed;
+
+typedef struct {
+    uint64_t pos;
+    int n_alleles;
+    uint8_t *ref; int nref;
+    uint8_t *alt; int nalt;
+    uint32_t *carriers; int ncar, ccar; /* haplotype ids carrying the alt */
+} orc_record;
+
+typedef struct orc_job {
+    int nsamp;
+    char *chrom;
+    uint32_t min_maf;
+    orc_patterns pats;
+    char **pid_name; int npid_name;
+    orc_bed *beds; int nbeds, cbeds;
+    /* current region */
+    uint64_t ms, me, es, ee;
+    uint8_t *ref_nuc; uint64_t *ref_pos; int nref;
+    orc_record *rec; int nrec, crec;
+    int status;
+    /* outputs */
+    sbuf rows;
+    uint32_t fake_position;
+    keymap keys;                 /* keys of the last region, sorted */
+    int last_haplotypes;         /* number_of_haplotypes (main.rs:97-130) */
+    int last_variants;           /* variant_count (haplotype.rs:25) */
+    uint64_t last_matches;       /* sum of haplotype ids over matches (main.rs:431) */
+} orc_job;
+
+orc_job *orc_job_new(int nsamp, const char *chrom, uint32_t min_maf) {
+    orc_job *j = (orc_job *)calloc(1, sizeof(orc_job));
+    j->nsamp = nsamp;
+    j->chrom = strdup(chrom);
+    j->min_maf = min_maf;
+    j->fake_position = 1;
+    j->keys.nsamp = nsamp;
+    return j;
+}
+void orc_job_free(orc_job *j) {
+    if (!j) return;
+    for (int i = 0; i < j->pats.n; i++) { free(j->pats.p[i].w); free(j->pats.p[i].name); }
+    free(j->pats.p);
+    for (int i = 0; i < j->npid_name; i++) free(j->pid_name[i]);
+    free(j->pid_name);
+    for (int i = 0; i < j->nbeds; i++) { free(j->beds[i].name); free(j->beds[i].s); free(j->beds[i].e); }
+    free(j->beds);
+    for (int i = 0; i < j->nrec; i++) { free(j->rec[i].ref); free(j->rec[i].alt); free(j->rec[i].carriers); }
+    free(j->rec);
+    free(j->ref_nuc); free(j->ref_pos);
+    free(j->rows.p);
+    keymap_free(&j->keys);
+    free(j->chrom);
+    free(j);
+}
+/* Add a pattern; pattern_id -> name dictionary as main.rs:239-250 (last wins). */
+void orc_job_add_pattern(orc_job *j, int kind, int dir, int pid, int32_t min, int len, const int32_t *w5, const char *name) {
+    pat_push(&j->pats, kind, dir, (uint16_t)pid, min, len, w5, name);
+    if (pid >= j->npid_name) {
+        j->pid_name = (char **)realloc(j->pid_name, sizeof(char *) * (pid + 1));
+        for (int i = j->npid_name; i <= pid; i++) j->pid_name[i] = NULL;
+        j->npid_name = pid + 1;
+    }
+    free(j->pid_name[pid]);
+    j->pid_name[pid] = strdup(name ? name : "");
+}
+void orc_job_add_patterns(orc_job *j, const orc_patterns *ps) {
+    for (int i = 0; i < ps->n; i++) {
+        const orc_pattern *p = &ps->p[i];
+        orc_job_add_pattern(j, p->kind, p->direction, p->pattern_id, p->min_score, p->len, p->w, p->name);
+    }
+}
+/* bed.rs:25-47: one entry of the (basename-keyed) peak map, file order. */
+int orc_job_add_bed(orc_job *j, const char *basename, const uint64_t *s, const uint64_t *e, int n) {
+    orc_bed b;
+    memset(&b, 0, sizeof b);
+    b.name = strdup(basename);
+    b.s = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+    b.e = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+    for (int i = 0; i < n; i++) { b.s[i] = s[i]; b.e[i] = e[i]; }
+    b.n = b.cap = n;
+    VEC_PUSH(j->beds, j->nbeds, j->cbeds, b);
+    return j->nbeds - 1;
+}
+
+/* main.rs:404-407: L_max over all patterns; ext = [s - L + 1, e + L - 1]. */
+int orc_job_ext(const orc_job *j, uint64_t ms, uint64_t me, uint64_t *es, uint64_t *ee) {
+    uint64_t L = 0;
+    for (int i = 0; i < j->pats.n; i++) {
+        uint64_t l = j->pats.p[i].kind == 0 ? (uint64_t)j->pats.p[i].len : 0; /* types.rs:92-101 */
+        if (l > L) L = l;
+    }
+    if (j->pats.n == 0) return ORC_E_ARG; /* main.rs:238 assert */
+    if (ms + 1 < L) return ORC_E_RANGE;
+    *es = ms + 1 - L; /* u64 wrapping as in --release (L = 0 gives [s+1, e-1]) */
+    *ee = me + L - 1;
+    return ORC_OK;
+}
+
+/* Begin a merged region.  ref_ascii are the FASTA bases starting at ext.start
+ * (main.rs:156-161; may be shorter than the window at a contig end). */
+int orc_region_begin(orc_job *j, uint64_t ms, uint64_t me, const char *ref_ascii, int nref) {
+    for (int i = 0; i < j->nrec; i++) { free(j->rec[i].ref); free(j->rec[i].alt); free(j->rec[i].carriers); }
+    j->nrec = 0;
+    j->ms = ms; j->me = me;
+    int rc = orc_job_ext(j, ms, me, &j->es, &j->ee);
+    j->status = rc;
+    if (rc) return rc;
+    free(j->ref_nuc); free(j->ref_pos);
+    j->ref_nuc = (uint8_t *)malloc(nref ? nref : 1);
+    j->ref_pos = (uint64_t *)malloc(sizeof(uint64_t) * (nref ? nref : 1));
+    j->nref = nref;
+    for (int i = 0; i < nref; i++) { /* util.rs:22-31 */
+        int c = orc_to_nucleotide((uint8_t)ref_ascii[i]);
+        if (c < 0) { j->status = ORC_E_BADBASE; return ORC_E_BADBASE; }
+        j->ref_nuc[i] = (uint8_t)c;
+        j->ref_pos[i] = j->es + (uint64_t)i;
+    }
+    return ORC_OK;
+}
+
+static int to_nucs(const char *s, uint8_t **out, int *n) {
+    int l = (int)strlen(s);
+    *out = (uint8_t *)malloc(l ? l : 1);
+    for (int i = 0; i < l; i++) {
+        int c = orc_to_nucleotide((uint8_t)s[i]);
+        if (c < 0) return ORC_E_BADBASE;
+        (*out)[i] = (uint8_t)c;
+    }
+    *n = l;
+    return ORC_OK;
+}
+
+/* haplotype.rs:16-60 load_diffs, one record.  gt holds 2 raw BCF GT ints per
+ * selected sample (BCF sample order), with INT32_MIN+1 as vector_end.  A record
+ * with n_alleles < 2 panics at alleles[1] (line 22). */
+#define ORC_VECTOR_END (INT32_MIN + 1)
+int orc_region_add_record_gt(orc_job *j, uint64_t pos, int n_alleles, const char *ref, const char *alt, const int32_t *gt) {
+    if (j->status) return j->status;
+    if (n_alleles < 2) return j->status = ORC_E_ALLELES;
+    orc_record r;
+    memset(&r, 0, sizeof r);
+    r.pos = pos; r.n_alleles = n_alleles;
+    if (to_nucs(ref, &r.ref, &r.nref) || to_nucs(alt, &r.alt, &r.nalt)) {
+        free(r.ref); free(r.alt);
+        return j->status = ORC_E_BADBASE;
+    }
+    if (n_alleles == 2) {
+        for (int s = 0; s < j->nsamp; s++) {
+            int32_t g0 = gt[2 * s], g1 = gt[2 * s + 1];
+            int glen = (g0 == ORC_VECTOR_END) ? 0 : (g1 == ORC_VECTOR_END ? 1 : 2);
+            if (glen != n_alleles) { free(r.ref); free(r.alt); free(r.carriers); return j->status = ORC_E_PLOIDY; }
+            /* GenotypeAllele::Unphased(1) <=> raw 4; Phased(1) <=> raw 5 (rust-htslib 0.26.1) */
+            if (g0 == 4) VEC_PUSH(r.carriers, r.ncar, r.ccar, (uint32_t)(2 * s));
+            if (g1 == 5) VEC_PUSH(r.carriers, r.ncar, r.ccar, (uint32_t)(2 * s + 1));
+        }
+    }
+    VEC_PUSH(j->rec, j->nrec, j->crec, r);
+    return ORC_OK;
+}
+/* Same, with the carrying haplotype ids given directly (synthetic phased data). */
+int orc_region_add_record_carriers(orc_job *j, uint64_t pos, const char *ref, const char *alt, const uint32_t *hap_ids,
+                                   int n) {
+    if (j->status) return j->status;
+    orc_record r;
+    memset(&r, 0, sizeof r);
+    r.pos = pos; r.n_alleles = 2;
+    if (to_nucs(ref, &r.ref, &r.nref) || to_nucs(alt, &r.alt, &r.nalt)) {
+        free(r.ref); free(r.alt);
+        return j->status = ORC_E_BADBASE;
+    }
+    for (int i = 0; i < n; i++) VEC_PUSH(r.carriers, r.ncar, r.ccar, hap_ids[i]);
+    VEC_PUSH(j->rec, j->nrec, j->crec, r);
+    return ORC_OK;
+}
+
+typedef struct {
+    orc_diff **d; int nd, cd;      /* diff list (push order = record order) */
+} hap_diffs;
+
+typedef struct {
+    orc_diff **d; int nd;          /* the group's diff list */
+    uint32_t *ids; int nids, cids; /* haplotype ids */
+} group_t;
+
+static int cmp_difflist(orc_diff *const *a, int na, orc_diff *const *b, int nb) {
+    int n = na < nb ? na : nb;
+    for (int i = 0; i < n; i++) {
+        int c = cmp_diff(a[i], b[i]);
+        if (c) return c;
+    }
+    return na < nb ? -1 : (na > nb ? 1 : 0);
+}
+static int cmp_group(const void *a, const void *b) {
+    const group_t *x = (const group_t *)a, *y = (const group_t *)b;
+    return cmp_difflist(x->d, x->nd, y->d, y->nd);
+}
+
+typedef struct {
+    nucpos_vec seq;
+    group_t *g;  /* winning group */
+} distinct_t;
+
+typedef struct {
+    orc_job *j;
+    const uint32_t *ids; int nids;
+    uint16_t pid;
+    int ninner; const int *ib; const uint64_t *is; const uint64_t *ie;
+    uint64_t nmatch_ids;
+} scan_ctx;
+static void scan_cb(void *ctx, uint64_t s, uint64_t e) {
+    scan_ctx *c = (scan_ctx *)ctx;
+    c->nmatch_ids += (uint64_t)c->nids;
+    count_one_match(&c->j->keys, 0, c->ib, c->is, c->ie, c->ninner, s, e, c->pid, c->ids, c->nids);
+}
+
+
+/* Finish the region: find_all_matches + count_matches_by_sample +
+ * counts_as_genotypes + row emission (main.rs:395-436). */
+int orc_region_end(orc_job *j) {
+    if (j->status) return j->status;
+    keymap_free(&j->keys);
+    j->keys.nsamp = j->nsamp;
+    int H = 2 * j->nsamp;
+
+    /* load_diffs: HashMap<HaplotypeId, Vec<Diff>> built in record order. */
+    orc_diff *diffs = (orc_diff *)malloc(sizeof(orc_diff) * (j->nrec ? j->nrec : 1));
+    hap_diffs *hd = (hap_diffs *)calloc(H ? H : 1, sizeof(hap_diffs));
+    int variants = 0;
+    for (int r = 0; r < j->nrec; r++) {
+        orc_record *rec = &j->rec[r];
+        variants++;
+        diffs[r].pos = rec->pos; diffs[r].ref = rec->ref; diffs[r].nref = rec->nref;
+        diffs[r].alt = rec->alt; diffs[r].nalt = rec->nalt;
+        if (rec->n_alleles != 2) continue; /* haplotype.rs:53-55 */
+        for (int c = 0; c < rec->ncar; c++) {
+            uint32_t h = rec->carriers[c];
+            if ((int)h >= H) continue;
+            VEC_PUSH(hd[h].d, hd[h].nd, hd[h].cd, &diffs[r]);
+        }
+    }
+    /* group_by_diffs (haplotype.rs:65-75): by diff-list VALUE. */
+    group_t *groups = NULL;
+    int ng = 0, cg = 0;
+    {
+        /* sort haplotypes by diff list, then run-length group */
+        int *order = (int *)malloc(sizeof(int) * (H ? H : 1));
+        int no = 0;
+        for (int h = 0; h < H; h++) if (hd[h].nd > 0) order[no++] = h;
+        /* simple stable merge sort on diff lists */
+        int *tmp = (int *)malloc(sizeof(int) * (no ? no : 1));
+        for (int w = 1; w < no; w *= 2) {
+            for (int lo = 0; lo < no; lo += 2 * w) {
+                int mid = lo + w < no ? lo + w : no, hi = lo + 2 * w < no ? lo + 2 * w : no;
+                int a = lo, b = mid, k = lo;
+                while (a < mid && b < hi) {
+                    if (cmp_difflist(hd[order[b]].d, hd[order[b]].nd, hd[order[a]].d, hd[order[a]].nd) < 0)
+                        tmp[k++] = order[b++];
+                    else tmp[k++] = order[a++];
+                }
+                while (a < mid) tmp[k++] = order[a++];
+                while (b < hi) tmp[k++] = order[b++];
+            }
+            memcpy(order, tmp, sizeof(int) * no);
+        }
+        free(tmp);
+        for (int i = 0; i < no; i++) {
+            int h = order[i];
+            if (ng == 0 || cmp_difflist(groups[ng - 1].d, groups[ng - 1].nd, hd[h].d, hd[h].nd) != 0) {
+                group_t g;
+                memset(&g, 0, sizeof g);
+                g.d = hd[h].d; g.nd = hd[h].nd;
+                VEC_PUSH(groups, ng, cg, g);
+            }
+            VEC_PUSH(groups[ng - 1].ids, groups[ng - 1].nids, groups[ng - 1].cids, (uint32_t)h);
+        }
+        free(order);
+        qsort(groups, ng, sizeof(group_t), cmp_group); /* D1: already sorted; kept explicit */
+    }
+    /* load_haplotypes (haplotype.rs:77-88): patch, dedup by sequence (D1). */
+    distinct_t *dist = NULL;
+    int ndist = 0, cdist = 0;
+    int rc = ORC_OK;
+    for (int g = 0; g < ng && rc == ORC_OK; g++) {
+        nucpos_vec seq = {0};
+        rc = patch_haplotype_impl(j->es, j->ee, groups[g].d, groups[g].nd, j->ref_nuc, j->ref_pos, j->nref, &seq);
+        if (rc) { free(seq.nuc); free(seq.pos); break; }
+        int found = -1;
+        for (int k = 0; k < ndist; k++) {
+            if (dist[k].seq.n == seq.n && !memcmp(dist[k].seq.nuc, seq.nuc, seq.n) &&
+                !memcmp(dist[k].seq.pos, seq.pos, sizeof(uint64_t) * seq.n)) { found = k; break; }
+        }
+        if (found >= 0) { /* HashMap::insert on an existing key: the value is replaced */
+            dist[found].g = &groups[g];
+            free(seq.nuc); free(seq.pos);
+        } else {
+            distinct_t d;
+            d.seq = seq; d.g = &groups[g];
+            VEC_PUSH(dist, ndist, cdist, d);
+        }
+    }
+    /* inner peaks: select_inner_peaks (main.rs:62-72), flattened with bed index. */
+    int ninner = 0, cin = 0;
+    int *ib = NULL; uint64_t *is = NULL, *ie = NULL;
+    int cis = 0, cie = 0, nis = 0, nie = 0;
+    for (int b = 0; b < j->nbeds; b++) {
+        for (int p = 0; p < j->beds[b].n; p++) {
+            if (orc_range_overlaps(j->beds[b].s[p], j->beds[b].e[p], j->ms, j->me)) {
+                VEC_PUSH(ib, ninner, cin, b);
+                VEC_PUSH(is, nis, cis, j->beds[b].s[p]);
+                VEC_PUSH(ie, nie, cie, j->beds[b].e[p]);
+            }
+        }
+    }
+    /* find_all_matches (main.rs:94-154) */
+    uint64_t nmatch_ids = 0;
+    int nhap = 0;
+    if (rc == ORC_OK) {
+        uint8_t *in_ref = (uint8_t *)malloc(H ? H : 1);
+        memset(in_ref, 1, H);
+        for (int k = 0; k < ndist && rc == ORC_OK; k++) {
+            nhap++;
+            group_t *g = dist[k].g;
+            for (int i = 0; i < g->nids; i++) in_ref[g->ids[i]] = 0;
+            for (int p = 0; p < j->pats.n && rc == ORC_OK; p++) {
+                scan_ctx c = {j, g->ids, g->nids, j->pats.p[p].pattern_id, ninner, ib, is, ie, 0};
+                rc = matches_impl(&j->pats.p[p], dist[k].seq.nuc, dist[k].seq.pos, dist[k].seq.n, scan_cb, &c);
+                nmatch_ids += c.nmatch_ids;
+            }
+        }
+        uint32_t *rids = (uint32_t *)malloc(sizeof(uint32_t) * (H ? H : 1));
+        int nr = 0;
+        for (int h = 0; h < H; h++) if (in_ref[h]) rids[nr++] = (uint32_t)h;
+        if (nr > 0 && rc == ORC_OK) {
+            nhap++;
+            for (int p = 0; p < j->pats.n && rc == ORC_OK; p++) {
+                scan_ctx c = {j, rids, nr, j->pats.p[p].pattern_id, ninner, ib, is, ie, 0};
+                rc = matches_impl(&j->pats.p[p], j->ref_nuc, j->ref_pos, j->nref, scan_cb, &c);
+                nmatch_ids += c.nmatch_ids;
+            }
+        }
+        free(rids);
+        free(in_ref);
+    }
+    /* rows (main.rs:415-429), D2 order */
+    if (rc == ORC_OK) {
+        qsort(j->keys.k, j->keys.n, sizeof(orc_key), cmp_key);
+        /* chromosome.replace("chr", "") */
+        sbuf chr = {0};
+        {
+            const char *c = j->chrom;
+            while (*c) {
+                if (!strncmp(c, "chr", 3)) c += 3;
+                else { sb_put(&chr, c, 1); c++; }
+            }
+            if (!chr.p) sb_puts(&chr, "");
+        }
+        for (int k = 0; k < j->keys.n; k++) {
+            orc_key *q = &j->keys.k[k];
+            uint32_t maf;
+            sbuf info = {0}, gts = {0};
+            if (counts_as_genotypes_impl(q->l, q->r, j->nsamp, &maf, &info, &gts) == 1 && maf >= j->min_maf) {
+                char head[512];
+                const char *pname = (q->pid < j->npid_name && j->pid_name[q->pid]) ? j->pid_name[q->pid] : "";
+                snprintf(head, sizeof head, "%s\t%u\t%s,%s,%llu-%llu\t.\t.\t.\tPASS\t", chr.p, j->fake_position,
+                         j->beds[q->bed].name, pname, (unsigned long long)q->s, (unsigned long long)q->e);
+                sb_puts(&j->rows, head);
+                sb_put(&j->rows, info.p, info.n);
+                sb_puts(&j->rows, "\tGT:DS");
+                if (gts.n) sb_put(&j->rows, gts.p, gts.n);
+                sb_puts(&j->rows, "\n");
+                j->fake_position++;
+            }
+            free(info.p); free(gts.p);
+        }
+        free(chr.p);
+    }
+    j->last_haplotypes = nhap;
+    j->last_variants = variants;
+    j->last_matches = nmatch_ids;
+
+    for (int k = 0; k < ndist; k++) { free(dist[k].seq.nuc); free(dist[k].seq.pos); }
+    free(dist);
+    for (int g = 0; g < ng; g++) free(groups[g].ids);
+    free(groups);
+    for (int h = 0; h < H; h++) free(hd[h].d);
+    free(hd);
+    free(diffs);
+    free(ib); free(is); free(ie);
+    for (int i = 0; i < j->nrec; i++) { free(j->rec[i].ref); free(j->rec[i].alt); free(j->rec[i].carriers); }
+    j->nrec = 0;
+    return rc;
+}
+
+const char *orc_job_rows(const orc_job *j) { return j->rows.p ? j->rows.p : ""; }
+size_t orc_job_rows_len(const orc_job *j) { return j->rows.n; }
+void orc_job_clear_rows(orc_job *j) { j->rows.n = 0; if (j->rows.p) j->rows.p[0] = 0; }
+int orc_job_nkeys(const orc_job *j) { return j->keys.n; }
+int orc_job_key(const orc_job *j, int i, int *bed, uint64_t *s, uint64_t *e, int *pid, uint32_t *l, uint32_t *r) {
+    if (i < 0 || i >= j->keys.n) return ORC_E_ARG;
+    const orc_key *q = &j->keys.k[i];
+    *bed = q->bed; *s = q->s; *e = q->e; *pid = q->pid;
+    if (l) memcpy(l, q->l, sizeof(uint32_t) * j->nsamp);
+    if (r) memcpy(r, q->r, sizeof(uint32_t) * j->nsamp);
+    return ORC_OK;
+}
+void orc_job_stats(const orc_job *j, int *nhap, int *nvar, uint64_t *nmatch) {
+    *nhap = j->last_haplotypes; *nvar = j->last_variants; *nmatch = j->last_matches;
+}
