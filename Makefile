@@ -1,0 +1,43 @@
+# Builds the product library (HIP for gfx950 + host C++) and the test oracle.
+#   make            -> find-tfbs_amd/lib/libtfbs_amd.so, oracle/_build/libtfbs_oracle.so
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+PKG := find-tfbs_amd
+SRC := $(PKG)/csrc
+LIBDIR := $(PKG)/lib
+OBJDIR := $(PKG)/lib/obj
+JOBS ?= 8
+
+HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp
+HIP_SRCS := $(SRC)/device.hip
+HDRS := $(wildcard $(SRC)/*.hpp) include/tfbs_amd.h
+HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
+HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
+
+CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
+
+all: $(LIBDIR)/libtfbs_amd.so oracle
+
+$(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(CXXFLAGS) -x c++ -c $< -o $@
+
+$(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip -c $< -o $@
+
+$(LIBDIR)/libtfbs_amd.so: $(HOST_OBJS) $(HIP_OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lz -lpthread
+
+oracle:
+	$(MAKE) -s -C oracle
+
+asm: $(SRC)/device.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -x hip --cuda-device-only -S $< -o $(OBJDIR)/device.s -Rpass-analysis=kernel-resource-usage
+
+clean:
+	rm -rf $(LIBDIR) oracle/_build
+
+.PHONY: all oracle clean asm

@@ -1,0 +1,430 @@
+"""find-tfbs_amd: MI355X-native drop-in for find-tfbs's per-haplotype TFBS scoring path.
+
+This module mirrors the reference's Rust interface for that path (names,
+argument meaning, error behaviour) over the C ABI of include/tfbs_amd.h:
+
+  reference (find-tfbs v1.0.1)                    here
+  ----------------------------------------------  ---------------------------------
+  pattern.rs:13-16   parse_weight                 parse_weight
+  pattern.rs:18-35   parse_threshold_file         parse_threshold_file
+  pattern.rs:37-87   parse_pwm_files              parse_pwm_files -> PatternSet
+  pattern.rs:141-171 matches                      matches / Scanner.matches (GPU)
+  haplotype.rs:94    patch_haplotype              patch_haplotype
+  haplotype.rs:77    load_haplotypes  \
+  main.rs:94         find_all_matches  >          RegionBatch (+ Scanner.scan, GPU)
+  main.rs:500        count_matches_by_sample /    RegionBatch.keys
+  main.rs:439        counts_as_genotypes          counts_as_genotypes
+  main.rs:415-429    row emission                 RegionBatch.rows
+
+The reference panics where TfbsError is raised.  The scan always runs on a HIP
+device; without one, Scanner() raises TfbsError(TFBS_E_NODEVICE).
+"""
+import ctypes as C
+from collections import namedtuple
+
+from ._capi import TfbsError, check, lib, tfbs_pattern_desc  # noqa: F401
+
+TFBS_OK = 0
+TFBS_E_NODEVICE = -10
+KIND_PWM, KIND_OTHER = 0, 1
+DIR_P, DIR_N = 0, 1
+NUCLEOTIDES = "ACGTN"  # types.rs:5-8, the weight index order
+
+Range = namedtuple("Range", "start end")  # range.rs:4-8, inclusive
+NucleotidePos = namedtuple("NucleotidePos", "nuc pos")  # types.rs:23-27 (nuc as 'A'..'N')
+Diff = namedtuple("Diff", "pos reference alternative")  # types.rs:39-44 (strings)
+HaplotypeId = namedtuple("HaplotypeId", "sample_id side")  # types.rs:66-70, side 0 Left / 1 Right
+Match = namedtuple("Match", "range pattern_id haplotype_ids")  # types.rs:32-37
+
+
+class Weight:
+    """types.rs:103-114: four milli-log-odds weights, N forced to 0."""
+
+    __slots__ = ("acgtn",)
+
+    def __init__(self, a, c, g, t):
+        self.acgtn = [a, c, g, t, 0]
+
+    def __eq__(self, o):
+        return isinstance(o, Weight) and self.acgtn == o.acgtn
+
+    def __repr__(self):
+        return "Weight(%r)" % (self.acgtn,)
+
+
+class Pattern:
+    """types.rs:86-90: PWM (kind 0) or OtherPattern (kind 1)."""
+
+    def __init__(self, name, pattern_id, weights=None, min_score=0, direction=DIR_P, kind=KIND_PWM):
+        self.name = name
+        self.pattern_id = pattern_id
+        self.weights = list(weights or [])
+        self.min_score = min_score
+        self.direction = direction
+        self.kind = kind
+
+    @classmethod
+    def PWM(cls, weights, name, pattern_id, min_score, direction=DIR_P):
+        return cls(name, pattern_id, weights, min_score, direction, KIND_PWM)
+
+    @classmethod
+    def OtherPattern(cls, name, pattern_id):
+        return cls(name, pattern_id, [], 0, DIR_P, KIND_OTHER)
+
+    def __len__(self):  # pattern_length (types.rs:92-101)
+        return len(self.weights) if self.kind == KIND_PWM else 0
+
+    def __eq__(self, o):
+        return (isinstance(o, Pattern) and (self.name, self.pattern_id, self.weights, self.min_score,
+                                             self.direction, self.kind) ==
+                (o.name, o.pattern_id, o.weights, o.min_score, o.direction, o.kind))
+
+    def __repr__(self):
+        return "Pattern(%s id=%d L=%d min=%d dir=%s)" % (self.name, self.pattern_id, len(self), self.min_score,
+                                                         "+-"[self.direction])
+
+
+def _u(x):
+    return x.encode() if isinstance(x, str) else x
+
+
+def parse_weight(s):
+    v = C.c_int32()
+    check(lib().tfbs_parse_weight(_u(s), C.byref(v)))
+    return v.value
+
+
+def parse_threshold_file(filename, pwm_threshold):
+    v = C.c_int32()
+    r = check(lib().tfbs_parse_threshold_file(_u(filename), pwm_threshold, C.byref(v)))
+    return v.value if r == 1 else None
+
+
+class PatternSet:
+    """An immutable tfbs_patterns handle (Vec<Pattern> of the reference)."""
+
+    def __init__(self, handle):
+        self.h = handle
+
+    @classmethod
+    def from_patterns(cls, patterns):
+        n = len(patterns)
+        descs = (tfbs_pattern_desc * max(1, n))()
+        keep = []
+        for i, p in enumerate(patterns):
+            flat = [x for w in p.weights for x in (w.acgtn if isinstance(w, Weight) else list(w)[:4] + [0])]
+            arr = (C.c_int32 * max(1, len(flat)))(*flat)
+            name = _u(p.name)
+            keep.append((arr, name))
+            descs[i] = tfbs_pattern_desc(p.pattern_id, p.direction, p.kind, len(p), arr, p.min_score, name)
+        h = C.c_void_p()
+        check(lib().tfbs_patterns_create(descs, n, C.byref(h)))
+        return cls(h)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().tfbs_patterns_destroy(self.h)
+            self.h = None
+
+    def __len__(self):
+        return lib().tfbs_patterns_count(self.h)
+
+    def __getitem__(self, i):
+        d = tfbs_pattern_desc()
+        check(lib().tfbs_patterns_get(self.h, i, C.byref(d)))
+        ws = [Weight(*(d.weights[5 * j + c] for c in range(4))) for j in range(d.length)]
+        return Pattern(d.name.decode(), d.pattern_id, ws, d.min_score, d.direction, d.kind)
+
+    def to_list(self):
+        return [self[i] for i in range(len(self))]
+
+    def name_of(self, pattern_id):
+        s = lib().tfbs_patterns_name_of(self.h, pattern_id)
+        return s.decode() if s is not None else None
+
+    @property
+    def max_length(self):
+        return lib().tfbs_patterns_max_length(self.h)
+
+
+def parse_pwm_files(pwm_file, threshold_dir, pwm_threshold, wanted_pwms, add_reverse_patterns=True):
+    """pattern.rs:37-87.  Returns a PatternSet (index it or .to_list() for Pattern objects)."""
+    h = C.c_void_p()
+    check(lib().tfbs_patterns_from_files(_u(pwm_file), _u(threshold_dir), pwm_threshold,
+                                         _u(",".join(wanted_pwms)), 1 if add_reverse_patterns else 0, C.byref(h)))
+    return PatternSet(h)
+
+
+def device_count():
+    n = C.c_int()
+    rc = lib().tfbs_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def _nuc_codes(hap):
+    return [NUCLEOTIDES.index(n.nuc if isinstance(n, NucleotidePos) else n[0]) for n in hap]
+
+
+def patch_haplotype(rng, diffs, ref_haplotype):
+    """haplotype.rs:94-156 (host C++ in libtfbs_amd).  diffs: [Diff(pos, 'REF', 'ALT')]."""
+    L = lib()
+    nd = len(diffs)
+    dref = [NUCLEOTIDES.index(c) for d in diffs for c in d.reference]
+    dalt = [NUCLEOTIDES.index(c) for d in diffs for c in d.alternative]
+    n = len(ref_haplotype)
+    cap = n + sum(len(d.alternative) for d in diffs) + 8
+    on = (C.c_uint8 * cap)()
+    op = (C.c_uint64 * cap)()
+    nout = C.c_size_t()
+    check(L.tfbs_patch_haplotype(
+        rng[0], rng[1], nd, (C.c_uint64 * max(1, nd))(*[d.pos for d in diffs]),
+        (C.c_uint8 * max(1, len(dref)))(*dref), (C.c_uint32 * max(1, nd))(*[len(d.reference) for d in diffs]),
+        (C.c_uint8 * max(1, len(dalt)))(*dalt), (C.c_uint32 * max(1, nd))(*[len(d.alternative) for d in diffs]),
+        (C.c_uint8 * max(1, n))(*_nuc_codes(ref_haplotype)),
+        (C.c_uint64 * max(1, n))(*[x[1] for x in ref_haplotype]), n, on, op, cap, C.byref(nout)))
+    return [NucleotidePos(NUCLEOTIDES[on[i]], op[i]) for i in range(nout.value)]
+
+
+def counts_as_genotypes(v1, v2, verbose=False):
+    """main.rs:439-498 -> (distinct_counts, maf, freq0, freq1, freq2, genotypes) or None."""
+    n = len(v1)
+    maf = C.c_uint32()
+    info = C.create_string_buffer(64 + 16 * n)
+    gts = C.create_string_buffer(64 + 24 * n)
+    r = check(lib().tfbs_counts_as_genotypes((C.c_uint32 * max(1, n))(*v1), (C.c_uint32 * max(1, n))(*v2), n,
+                                             C.byref(maf), info, len(info), gts, len(gts)))
+    if r != 1:
+        return None
+    s = info.value.decode()
+    counts_part, freqs_part = s.split(";")
+    counts = [int(x) for x in counts_part[len("COUNTS="):].split(",")]
+    f0, f1, f2 = (int(x) for x in freqs_part[len("freqs="):].split("/"))
+    return counts, maf.value, f0, f1, f2, gts.value.decode()
+
+
+class Scanner:
+    """A device context: the pattern tables resident on one GPU (one per host thread)."""
+
+    def __init__(self, patterns, device=0):
+        self.patterns = patterns if isinstance(patterns, PatternSet) else PatternSet.from_patterns(patterns)
+        self.h = C.c_void_p()
+        check(lib().tfbs_ctx_create(device, self.patterns.h, C.byref(self.h)))
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().tfbs_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def matches_all(self, haplotype):
+        """pattern.rs:141-171 for every pattern: list (per pattern, creation order) of [(start, end)]."""
+        n = len(haplotype)
+        nucs = (C.c_uint8 * max(1, n))(*_nuc_codes(haplotype))
+        pos = (C.c_uint64 * max(1, n))(*[x[1] for x in haplotype])
+        npat = len(self.patterns)
+        counts = (C.c_uint32 * max(1, npat))()
+        total = C.c_size_t()
+        cap = 64
+        while True:
+            s = (C.c_uint64 * cap)()
+            e = (C.c_uint64 * cap)()
+            rc = lib().tfbs_matches(self.h, nucs, pos, n, counts, s, e, cap, C.byref(total))
+            if rc == -1 and total.value > cap:
+                cap = total.value
+                continue
+            check(rc)
+            break
+        out, k = [], 0
+        for i in range(npat):
+            out.append([(s[k + j], e[k + j]) for j in range(counts[i])])
+            k += counts[i]
+        return out
+
+    def matches(self, pattern_index, haplotype, haplotype_ids=()):
+        p = self.patterns[pattern_index]
+        ids = tuple(haplotype_ids)
+        return [Match(Range(a, b), p.pattern_id, ids) for a, b in self.matches_all(haplotype)[pattern_index]]
+
+    def last_scan_ms(self):
+        return lib().tfbs_ctx_last_scan_ms(self.h)
+
+
+def matches(pattern, haplotype, haplotype_ids=(), verbose=False):
+    """pattern.rs:141-171 for one Pattern on one haplotype (GPU; builds a one-pattern Scanner)."""
+    sc = Scanner([pattern])
+    try:
+        return sc.matches(0, haplotype, haplotype_ids)
+    finally:
+        sc.close()
+
+
+class RegionBatch:
+    """load_haplotypes + find_all_matches + count_matches_by_sample over many merged regions."""
+
+    VECTOR_END = -2147483647
+
+    def __init__(self, patterns, n_samples, keep_membership=True):
+        self.patterns = patterns
+        self.n_samples = n_samples
+        self.h = C.c_void_p()
+        check(lib().tfbs_batch_create(patterns.h, n_samples, 1 if keep_membership else 0, C.byref(self.h)))
+        self.beds = []
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().tfbs_batch_destroy(self.h)
+            self.h = None
+
+    def add_bed(self, basename):
+        self.beds.append(basename)
+        return check(lib().tfbs_batch_add_bed(self.h, _u(basename)))
+
+    def ext(self, start, end):
+        es, ee = C.c_uint64(), C.c_uint64()
+        check(lib().tfbs_batch_region_ext(self.h, start, end, C.byref(es), C.byref(ee)))
+        return es.value, ee.value
+
+    def begin(self, start, end, ref_ascii):
+        check(lib().tfbs_batch_region_begin(self.h, start, end, _u(ref_ascii), len(ref_ascii)))
+
+    def add_inner(self, bed, start, end):
+        check(lib().tfbs_batch_region_add_inner(self.h, bed, start, end))
+
+    def add_record_gt(self, pos, n_alleles, ref, alt, gts):
+        flat = [x for g in gts for x in (list(g[:2]) + [self.VECTOR_END] * (2 - len(g[:2])))]
+        check(lib().tfbs_batch_region_add_record_gt(self.h, pos, n_alleles, _u(ref), _u(alt),
+                                                    (C.c_int32 * max(1, len(flat)))(*flat)))
+
+    def add_record_carriers(self, pos, ref, alt, hap_ids):
+        hap_ids = list(hap_ids)
+        check(lib().tfbs_batch_region_add_record_carriers(self.h, pos, _u(ref), _u(alt),
+                                                          (C.c_uint32 * max(1, len(hap_ids)))(*hap_ids),
+                                                          len(hap_ids)))
+
+    def end(self):
+        check(lib().tfbs_batch_region_end(self.h))
+
+    def synth_fill(self, seed, first, count, indel_pct=0):
+        check(lib().tfbs_synth_fill_batch(self.h, seed, first, count, indel_pct))
+
+    @property
+    def num_regions(self):
+        return lib().tfbs_batch_num_regions(self.h)
+
+    @property
+    def num_haplotypes(self):
+        return lib().tfbs_batch_num_haplotypes(self.h)
+
+    @property
+    def num_windows(self):
+        return lib().tfbs_batch_num_windows(self.h)
+
+    @property
+    def num_cell_ops(self):
+        return lib().tfbs_batch_num_cell_ops(self.h)
+
+    @property
+    def num_effective_windows(self):
+        return lib().tfbs_batch_num_effective_windows(self.h)
+
+    @property
+    def input_bytes(self):
+        return lib().tfbs_batch_input_bytes(self.h)
+
+    @property
+    def output_bytes(self):
+        return lib().tfbs_batch_output_bytes(self.h)
+
+    def region_stats(self, r):
+        a, b = C.c_uint32(), C.c_uint32()
+        check(lib().tfbs_batch_region_stats(self.h, r, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def scan(self, scanner, upload=True, download=True):
+        if upload:
+            check(lib().tfbs_batch_upload(scanner.h, self.h))
+        check(lib().tfbs_scan(scanner.h, self.h))
+        if download:
+            check(lib().tfbs_batch_download(scanner.h, self.h))
+
+    def keys(self, region):
+        """count_matches_by_sample for one region: {(bed, (s, e), pattern_id): (L, R)}."""
+        L = lib()
+        n = C.c_size_t()
+        check(L.tfbs_batch_region_num_keys(self.h, region, C.byref(n)))
+        out = {}
+        ns = self.n_samples
+        for k in range(n.value):
+            bed, s, e, pid = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint16()
+            l = (C.c_uint32 * max(1, ns))()
+            r = (C.c_uint32 * max(1, ns))()
+            check(L.tfbs_batch_region_key(self.h, region, k, C.byref(bed), C.byref(s), C.byref(e), C.byref(pid), l,
+                                          r))
+            out[(self.beds[bed.value], (s.value, e.value), pid.value)] = (list(l[:ns]), list(r[:ns]))
+        return out
+
+    def rows(self, chromosome, min_maf=0, fake_position=1):
+        """Rows for every region (main.rs:415-429); returns (text, next fake_position)."""
+        fp = C.c_uint32(fake_position)
+        p = C.c_void_p()
+        n = C.c_size_t()
+        check(lib().tfbs_batch_rows(self.h, _u(chromosome), min_maf, C.byref(fp), C.byref(p), C.byref(n)))
+        try:
+            text = C.string_at(p, n.value).decode()
+        finally:
+            lib().tfbs_free(p)
+        return text, fp.value
+
+
+class SynthRegion:
+    """A synthetic phased region."""
+
+    def __init__(self, seed, index, n_samples, lmax, indel_pct=0):
+        L = lib()
+        self.h = C.c_void_p()
+        check(L.tfbs_synth_region_make(seed, index, n_samples, lmax, indel_pct, C.byref(self.h)))
+        ms, me, es = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        ref = C.c_char_p()
+        nref, nrec = C.c_size_t(), C.c_size_t()
+        L.tfbs_synth_region_info(self.h, C.byref(ms), C.byref(me), C.byref(es), C.byref(ref), C.byref(nref),
+                                 C.byref(nrec))
+        self.merged = (ms.value, me.value)
+        self.ext_start = es.value
+        self.ref = C.string_at(ref, nref.value).decode()
+        self.records = []
+        for i in range(nrec.value):
+            pos = C.c_uint64()
+            r, a = C.c_char_p(), C.c_char_p()
+            car = C.POINTER(C.c_uint32)()
+            n = C.c_size_t()
+            L.tfbs_synth_region_record(self.h, i, C.byref(pos), C.byref(r), C.byref(a), C.byref(car), C.byref(n))
+            self.records.append((pos.value, r.value.decode(), a.value.decode(), list(car[:n.value])))
+        L.tfbs_synth_region_destroy(self.h)
+        self.h = None
+
+
+def synth_write_pwms(directory, n_pwms, length_config, seed):
+    p = C.c_void_p()
+    check(lib().tfbs_synth_write_pwms(_u(directory), n_pwms, length_config, seed, C.byref(p)))
+    try:
+        names = C.string_at(p).decode().split(",")
+    finally:
+        lib().tfbs_free(p)
+    return names
+
+
+def range_overlaps(a, b):
+    """range.rs:18-21: asymmetric -- are b's endpoints inside a?"""
+    return a[0] <= b[0] <= a[1] or a[0] <= b[1] <= a[1]
+
+
+def select_inner_peaks(merged, beds):
+    """main.rs:62-72: [(bed index, start, end)] of every bed range p with p.overlaps(merged)."""
+    out = []
+    for bi, (_, ranges) in enumerate(beds):
+        for (s, e) in ranges:
+            if range_overlaps((s, e), merged):
+                out.append((bi, s, e))
+    return out

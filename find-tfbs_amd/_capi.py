@@ -1,0 +1,120 @@
+"""ctypes declarations for libtfbs_amd.so (include/tfbs_amd.h).
+
+The library is built in-tree (``make`` or ``__graft_entry__.build()``) into
+find-tfbs_amd/lib/.  Loading fails loudly if it is missing: there is no
+Python or CPU fallback for the scan.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libtfbs_amd.so")
+
+u8p = C.POINTER(C.c_uint8)
+u16p = C.POINTER(C.c_uint16)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+i32p = C.POINTER(C.c_int32)
+vp = C.c_void_p
+
+
+class tfbs_pattern_desc(C.Structure):
+    _fields_ = [
+        ("pattern_id", C.c_uint16),
+        ("direction", C.c_uint8),
+        ("kind", C.c_uint8),
+        ("length", C.c_uint32),
+        ("weights", i32p),
+        ("min_score", C.c_int32),
+        ("name", C.c_char_p),
+    ]
+
+
+# (name, restype, argtypes) for every symbol in include/tfbs_amd.h
+SIGNATURES = [
+    ("tfbs_strerror", C.c_char_p, [C.c_int]),
+    ("tfbs_last_error", C.c_char_p, []),
+    ("tfbs_version", C.c_char_p, []),
+    ("tfbs_patterns_create", C.c_int, [C.POINTER(tfbs_pattern_desc), C.c_size_t, C.POINTER(vp)]),
+    ("tfbs_patterns_from_files", C.c_int, [C.c_char_p, C.c_char_p, C.c_float, C.c_char_p, C.c_int, C.POINTER(vp)]),
+    ("tfbs_patterns_count", C.c_size_t, [vp]),
+    ("tfbs_patterns_get", C.c_int, [vp, C.c_size_t, C.POINTER(tfbs_pattern_desc)]),
+    ("tfbs_patterns_name_of", C.c_char_p, [vp, C.c_uint16]),
+    ("tfbs_patterns_max_length", C.c_uint32, [vp]),
+    ("tfbs_patterns_destroy", None, [vp]),
+    ("tfbs_parse_weight", C.c_int, [C.c_char_p, i32p]),
+    ("tfbs_parse_threshold_file", C.c_int, [C.c_char_p, C.c_float, i32p]),
+    ("tfbs_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("tfbs_ctx_create", C.c_int, [C.c_int, vp, C.POINTER(vp)]),
+    ("tfbs_ctx_destroy", None, [vp]),
+    ("tfbs_ctx_sync", C.c_int, [vp]),
+    ("tfbs_ctx_last_scan_ms", C.c_float, [vp]),
+    ("tfbs_ctx_last_scan_launches", C.c_int, [vp]),
+    ("tfbs_matches", C.c_int, [vp, u8p, u64p, C.c_size_t, u32p, u64p, u64p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("tfbs_patch_haplotype", C.c_int, [C.c_uint64, C.c_uint64, C.c_size_t, u64p, u8p, u32p, u8p, u32p, u8p, u64p,
+                                       C.c_size_t, u8p, u64p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("tfbs_batch_create", C.c_int, [vp, C.c_uint32, C.c_int, C.POINTER(vp)]),
+    ("tfbs_batch_destroy", None, [vp]),
+    ("tfbs_batch_add_bed", C.c_int, [vp, C.c_char_p]),
+    ("tfbs_batch_region_ext", C.c_int, [vp, C.c_uint64, C.c_uint64, u64p, u64p]),
+    ("tfbs_batch_region_begin", C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_char_p, C.c_size_t]),
+    ("tfbs_batch_region_add_inner", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64]),
+    ("tfbs_batch_region_add_record_gt", C.c_int, [vp, C.c_uint64, C.c_uint32, C.c_char_p, C.c_char_p, i32p]),
+    ("tfbs_batch_region_add_record_carriers", C.c_int, [vp, C.c_uint64, C.c_char_p, C.c_char_p, u32p, C.c_size_t]),
+    ("tfbs_batch_region_end", C.c_int, [vp]),
+    ("tfbs_batch_num_regions", C.c_size_t, [vp]),
+    ("tfbs_batch_num_haplotypes", C.c_size_t, [vp]),
+    ("tfbs_batch_num_windows", C.c_uint64, [vp]),
+    ("tfbs_batch_num_effective_windows", C.c_uint64, [vp]),
+    ("tfbs_batch_num_cell_ops", C.c_uint64, [vp]),
+    ("tfbs_batch_input_bytes", C.c_uint64, [vp]),
+    ("tfbs_batch_output_bytes", C.c_uint64, [vp]),
+    ("tfbs_batch_upload", C.c_int, [vp, vp]),
+    ("tfbs_scan", C.c_int, [vp, vp]),
+    ("tfbs_batch_download", C.c_int, [vp, vp]),
+    ("tfbs_batch_region_num_keys", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("tfbs_batch_region_key", C.c_int, [vp, C.c_size_t, C.c_size_t, u32p, u64p, u64p, u16p, u32p, u32p]),
+    ("tfbs_batch_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, u32p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    ("tfbs_batch_region_stats", C.c_int, [vp, C.c_size_t, u32p, u32p]),
+    ("tfbs_free", None, [C.c_void_p]),
+    ("tfbs_counts_as_genotypes", C.c_int, [u32p, u32p, C.c_size_t, u32p, C.c_char_p, C.c_size_t, C.c_char_p,
+                                           C.c_size_t]),
+    ("tfbs_synth_write_pwms", C.c_int, [C.c_char_p, C.c_uint32, C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]),
+    ("tfbs_synth_region_make", C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                         C.POINTER(vp)]),
+    ("tfbs_synth_region_destroy", None, [vp]),
+    ("tfbs_synth_region_info", None, [vp, u64p, u64p, u64p, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                      C.POINTER(C.c_size_t)]),
+    ("tfbs_synth_region_record", None, [vp, C.c_size_t, u64p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                        C.POINTER(u32p), C.POINTER(C.c_size_t)]),
+    ("tfbs_synth_fill_batch", C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint32]),
+]
+
+_lib = None
+
+
+class TfbsError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s (%d): %s" % (msg, code, _lib.tfbs_strerror(code).decode() if _lib else "?"))
+        self.code = code
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("find-tfbs_amd native library missing at %s: run `make` or "
+                              "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc < 0:
+        raise TfbsError(rc, lib().tfbs_last_error().decode(errors="replace"))
+    return rc

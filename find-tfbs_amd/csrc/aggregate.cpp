@@ -1,0 +1,228 @@
+// Count aggregation and VCF row emission from the scan's per-haplotype counts.
+//
+// count_matches_by_sample (main.rs:500-534) adds, for every match and every
+// inner peak it overlaps, +1 to each carrying haplotype's side.  Here the scan
+// already summed hits per (distinct haplotype, pattern_id, inner range), so a
+// key's per-sample vectors are gathers: L[s] = C[hap(2s)], R[s] = C[hap(2s+1)],
+// times the multiplicity of the range in that bed list.  counts_as_genotypes
+// (main.rs:439-498) and the row format (main.rs:415-429) follow.
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "batch.hpp"
+
+namespace tfbs {
+
+namespace {
+
+struct KeyRef {
+    const InnerKey *ik;
+    uint32_t slot;  // pattern_id slot
+};
+
+// hap id -> local distinct index for region R
+struct Membership {
+    const RegionH &R;
+    std::vector<uint32_t> local;  // dense, built once per region
+    Membership(const RegionH &r, uint32_t H) : R(r), local(H, r.ref_local < 0 ? 0u : (uint32_t)r.ref_local) {
+        for (size_t i = 0; i < r.nonref_id.size(); i++) local[r.nonref_id[i]] = r.nonref_local[i];
+    }
+};
+
+inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint32_t slot, int32_t range_slot) {
+    const DevHap &h = B.haps[R.hap_begin + local];
+    const uint32_t n_inner = (uint32_t)R.ranges.size();
+    return B.counts[h.count_off + (uint64_t)slot * n_inner + (uint32_t)range_slot];
+}
+
+// Keys of a region in row order (inner.start, inner.end, bed index, pattern_id)
+// that exist in the reference's HashMap, i.e. got at least one match.
+std::vector<KeyRef> region_keys(const Batch &B, const RegionH &R) {
+    std::vector<KeyRef> out;
+    for (const InnerKey &k : R.keys) {
+        if (k.slot < 0) continue;  // empty range: no match can overlap it
+        for (uint32_t s = 0; s < B.n_slots; s++) {
+            bool any = false;
+            for (uint32_t l = 0; l < R.hap_count && !any; l++) any = count_of(B, R, l, s, k.slot) != 0;
+            if (any) out.push_back({&k, s});
+        }
+    }
+    return out;  // R.keys is sorted by (s, e, bed) and slots ascend with pattern_id
+}
+
+}  // namespace
+
+// main.rs:439-498.  Returns true and appends to info/gts if the counts vary.
+bool counts_as_genotypes(const uint32_t *v1, const uint32_t *v2, size_t n, uint32_t *maf, std::string &info,
+                         std::string &gts) {
+    if (n == 0) return false;
+    uint32_t lo = v1[0] + v2[0], hi = lo;
+    for (size_t i = 1; i < n; i++) {
+        uint32_t v = v1[i] + v2[i];
+        lo = std::min(lo, v);
+        hi = std::max(hi, v);
+    }
+    if (lo == hi) return false;
+    const uint32_t i1 = (lo * 1000u * 3u + hi * 1000u) / 4u;  // u32, wrapping as --release
+    const uint32_t i3 = (lo * 1000u + hi * 1000u * 3u) / 4u;
+    std::vector<uint32_t> all{lo, hi};
+    uint32_t zero = 0, one = 0, two = 0;
+    const float lof = (float)lo;
+    const float spread = (float)hi - lof;
+    char buf[48];
+    gts.reserve(gts.size() + n * 9);
+    for (size_t i = 0; i < n; i++) {
+        const uint32_t x = v1[i] + v2[i];
+        if (x == lo) { gts += "\t0|0:0.0"; zero++; }
+        else if (x == hi) { gts += "\t1|1:2.0"; two++; }
+        else {
+            if (std::find(all.begin(), all.end(), x) == all.end()) all.push_back(x);
+            const uint32_t x1000 = x * 1000u;
+            if (x1000 < i1) { gts += "\t0|0"; zero++; }
+            else if (x1000 < i3) { gts += "\t0|1"; one++; }
+            else { gts += "\t1|1"; two++; }
+            const float ds = (((float)x - lof) * 2.0f) / spread;  // f32 throughout
+            int m = snprintf(buf, sizeof buf, ":%.4f", (double)ds);
+            gts.append(buf, (size_t)m);
+        }
+    }
+    if (zero >= one && zero >= two) *maf = one + two;
+    else if (two >= zero && two >= one) *maf = zero + one;
+    else *maf = zero + two;
+    std::sort(all.begin(), all.end());
+    info += "COUNTS=";
+    for (size_t j = 0; j < all.size(); j++) {
+        int m = snprintf(buf, sizeof buf, j ? ",%u" : "%u", all[j]);
+        info.append(buf, (size_t)m);
+    }
+    int m = snprintf(buf, sizeof buf, ";freqs=%u/%u/%u", zero, one, two);
+    info.append(buf, (size_t)m);
+    return true;
+}
+
+// chromosome.replace("chr", "") (main.rs:402)
+static std::string strip_chr(const std::string &c) {
+    std::string o;
+    for (size_t i = 0; i < c.size();) {
+        if (c.compare(i, 3, "chr") == 0) i += 3;
+        else o.push_back(c[i++]);
+    }
+    return o;
+}
+
+int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out) {
+    if (!B.counts_valid) return fail(TFBS_E_STATE, "counts not downloaded");
+    if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
+    const std::string chr = strip_chr(chrom);
+    const uint32_t H = 2 * B.n_samples;
+    std::vector<uint32_t> l(B.n_samples), r(B.n_samples);
+    for (const RegionH &R : B.rh) {
+        if (R.hap_count == 0) continue;
+        Membership M(R, H);
+        for (const KeyRef &k : region_keys(B, R)) {
+            // all distinct haplotypes equal -> every sample has the same total: no row
+            const uint32_t c0 = count_of(B, R, 0, k.slot, k.ik->slot);
+            bool varies = false;
+            for (uint32_t h = 1; h < R.hap_count && !varies; h++) varies = count_of(B, R, h, k.slot, k.ik->slot) != c0;
+            if (!varies) continue;
+            for (uint32_t s = 0; s < B.n_samples; s++) {
+                l[s] = count_of(B, R, M.local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
+                r[s] = count_of(B, R, M.local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
+            }
+            uint32_t maf = 0;
+            std::string info, gts;
+            if (!counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts)) continue;
+            if (maf < min_maf) continue;
+            const uint16_t pid = B.slot_pid[k.slot];
+            auto it = B.pats->names.find(pid);
+            const std::string &pname = it == B.pats->names.end() ? std::string() : it->second;
+            char head[96];
+            snprintf(head, sizeof head, "\t%u\t", *fake);
+            out += chr;
+            out += head;
+            out += B.beds[k.ik->bed];
+            out += ',';
+            out += pname;
+            snprintf(head, sizeof head, ",%llu-%llu\t.\t.\t.\tPASS\t", (unsigned long long)k.ik->s,
+                     (unsigned long long)k.ik->e);
+            out += head;
+            out += info;
+            out += "\tGT:DS";
+            out += gts;
+            out += '\n';
+            (*fake)++;
+        }
+    }
+    return TFBS_OK;
+}
+
+}  // namespace tfbs
+
+using tfbs::Batch;
+
+extern "C" {
+
+int tfbs_batch_region_num_keys(const tfbs_batch *b, size_t region, size_t *n) {
+    if (!b || !n || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    if (!b->b.counts_valid) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    *n = tfbs::region_keys(b->b, b->b.rh[region]).size();
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t *bed, uint64_t *start, uint64_t *end,
+                          uint16_t *pid, uint32_t *left, uint32_t *right) {
+    if (!b || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    const Batch &B = b->b;
+    if (!B.counts_valid) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (!B.keep_membership && B.n_samples && (left || right))
+        return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    const tfbs::RegionH &R = B.rh[region];
+    auto keys = tfbs::region_keys(B, R);
+    if (k >= keys.size()) return tfbs::fail(TFBS_E_ARG, "bad key index");
+    const auto &q = keys[k];
+    if (bed) *bed = q.ik->bed;
+    if (start) *start = q.ik->s;
+    if (end) *end = q.ik->e;
+    if (pid) *pid = B.slot_pid[q.slot];
+    if (left || right) {
+        tfbs::Membership M(R, 2 * B.n_samples);
+        for (uint32_t s = 0; s < B.n_samples; s++) {
+            if (left) left[s] = tfbs::count_of(B, R, M.local[2 * s], q.slot, q.ik->slot) * q.ik->mult;
+            if (right) right[s] = tfbs::count_of(B, R, M.local[2 * s + 1], q.slot, q.ik->slot) * q.ik->mult;
+        }
+    }
+    return TFBS_OK;
+}
+
+int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t *fake, char **text,
+                    size_t *len) {
+    if (!b || !chromosome || !fake || !text || !len) return tfbs::fail(TFBS_E_ARG, "null argument");
+    std::string out;
+    int rc = tfbs::batch_rows(b->b, chromosome, min_maf, fake, out);
+    if (rc) return rc;
+    char *p = (char *)malloc(out.size() + 1);
+    if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");
+    memcpy(p, out.data(), out.size());
+    p[out.size()] = 0;
+    *text = p;
+    *len = out.size();
+    return TFBS_OK;
+}
+
+void tfbs_free(void *p) { free(p); }
+
+int tfbs_counts_as_genotypes(const uint32_t *left, const uint32_t *right, size_t n, uint32_t *maf, char *info,
+                             size_t info_cap, char *genotypes, size_t gt_cap) {
+    if (!maf || (n && (!left || !right))) return tfbs::fail(TFBS_E_ARG, "null argument");
+    std::string a, g;
+    if (!tfbs::counts_as_genotypes(left, right, n, maf, a, g)) return 0;
+    if (a.size() + 1 > info_cap || g.size() + 1 > gt_cap) return tfbs::fail(TFBS_E_ARG, "output capacity too small");
+    memcpy(info, a.c_str(), a.size() + 1);
+    memcpy(genotypes, g.c_str(), g.size() + 1);
+    return 1;
+}
+
+}  // extern "C"

@@ -1,0 +1,523 @@
+// Region batches: load_diffs / group_by_diffs / load_haplotypes / patch_haplotype
+// (haplotype.rs:13-156) and the packing of distinct haplotypes for the GPU.
+//
+// Determinism where the reference iterates a HashMap (documented in DESIGN.md):
+// groups are visited in ascending Vec<Diff> order, and when two groups patch to
+// the same sequence the later one wins (HashMap::insert, haplotype.rs:84); the
+// loser's haplotype ids stay with the reference group (main.rs:103-105, 129-137).
+#include <algorithm>
+#include <cstring>
+#include <numeric>
+#include <unordered_map>
+
+#include "batch.hpp"
+
+namespace tfbs {
+
+// derived Ord on Diff (types.rs:39-44): pos, then reference, then alternative.
+static bool diff_less(const Record *a, const Record *b) {
+    if (a->pos != b->pos) return a->pos < b->pos;
+    if (a->ref != b->ref) return std::lexicographical_compare(a->ref.begin(), a->ref.end(), b->ref.begin(), b->ref.end());
+    return std::lexicographical_compare(a->alt.begin(), a->alt.end(), b->alt.begin(), b->alt.end());
+}
+static bool diff_equal(const Record *a, const Record *b) {
+    return a->pos == b->pos && a->ref == b->ref && a->alt == b->alt;
+}
+
+// A reference window: consecutive positions [start, start + n) (the batch case).
+struct RefWindow {
+    const uint8_t *nuc;
+    uint64_t start;
+    size_t n;
+    // haplotype.rs:90-92 get(): bases with pos in [s, e]
+    void get(uint64_t s, uint64_t e, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) const {
+        if (n == 0 || e < s) return;
+        uint64_t lo = std::max(s, start), hi = std::min(e, start + n - 1);
+        for (uint64_t p = lo; p <= hi && p >= lo; p++) {
+            nucs.push_back(nuc[p - start]);
+            pos.push_back(p);
+        }
+    }
+    // haplotype.rs:119-125: the base at pos, N if absent
+    uint8_t at(uint64_t p) const { return (p >= start && p - start < n) ? nuc[p - start] : 4; }
+};
+
+// haplotype.rs:94-156.  The recursion of next_chunk is a loop with the same case order.
+static int patch_window(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const RefWindow &ref,
+                        std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
+    diffs.erase(std::remove_if(diffs.begin(), diffs.end(), [&](const Record *d) { return d->pos < rs || d->pos > re; }),
+                diffs.end());
+    std::stable_sort(diffs.begin(), diffs.end(), diff_less);
+    uint64_t at = rs;
+    size_t k = 0;
+    for (;;) {
+        if (k == diffs.size()) {
+            if (at <= re) ref.get(at, re, nucs, pos);
+            return TFBS_OK;
+        }
+        const Record *d = diffs[k];
+        if (d->pos > at) {
+            ref.get(at, d->pos - 1, nucs, pos);
+            at = d->pos;
+        } else if (d->pos == at && d->ref.size() == 1) {  // SNV or insertion
+            if (d->ref[0] != ref.at(at))
+                return fail(TFBS_E_REFMISMATCH,
+                            "First reference nucleotide of variant doesn't match reference genome at " +
+                                std::to_string(at));
+            for (uint8_t a : d->alt) {
+                nucs.push_back(a);
+                pos.push_back(at);
+            }
+            at += 1;
+            k++;
+        } else if (d->pos == at && d->alt.size() == 1) {  // deletion
+            nucs.push_back(d->alt[0]);
+            pos.push_back(at);
+            at += d->ref.size();
+            k++;
+        } else if (d->pos == at) {
+            return fail(TFBS_E_MNP, "Missing case in haplotype patcher at " + std::to_string(at));
+        } else if (at >= re) {
+            ref.get(at, at, nucs, pos);
+            return TFBS_OK;
+        } else {
+            return TFBS_OK;  // overlapping diffs truncate the haplotype
+        }
+    }
+}
+
+int patch(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const uint8_t *ref, uint64_t ref_start,
+          size_t n_ref, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
+    RefWindow w{ref, ref_start, n_ref};
+    return patch_window(rs, re, std::move(diffs), w, nucs, pos);
+}
+
+uint64_t Batch::device_bytes() const {
+    return words.size() * 4ull + nmask.size() * 4ull + posrel.size() * 4ull + haps.size() * sizeof(DevHap) +
+           regions.size() * sizeof(DevRegion) + inner.size() * 4ull;
+}
+
+// ---------------------------------------------------------------------------
+// Builds one region's distinct haplotypes from its inputs; touches no batch
+// state, so regions can be built on several host threads (commit is serial).
+int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
+    out.R = std::move(I.R);
+    RegionH &R = out.R;
+    const uint32_t H = 2 * B.n_samples;
+    R.n_variants = (uint32_t)I.recs.size();  // variant_count counts every fetched record (haplotype.rs:25)
+
+    // ---- inner keys: unique (bed, s, e) with multiplicity; distinct non-empty ranges
+    {
+        std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> in = std::move(I.inner);
+        std::sort(in.begin(), in.end(), [](const auto &a, const auto &b) {
+            if (a.second != b.second) return a.second < b.second;
+            return a.first < b.first;
+        });
+        for (size_t i = 0; i < in.size();) {
+            size_t j = i;
+            while (j < in.size() && in[j] == in[i]) j++;
+            InnerKey k{in[i].first, in[i].second.first, in[i].second.second, (uint32_t)(j - i), -1};
+            if (k.e >= k.s) {
+                auto r = std::make_pair(k.s, k.e);
+                if (R.ranges.empty() || R.ranges.back() != r) R.ranges.push_back(r);
+                k.slot = (int32_t)R.ranges.size() - 1;
+            }
+            R.keys.push_back(k);
+            i = j;
+        }
+    }
+
+    // ---- load_diffs: (haplotype id, canonical diff rank) in record order
+    std::vector<const Record *> uniq;
+    for (auto &r : I.recs)
+        if (r.n_alleles == 2 && !r.carriers.empty()) uniq.push_back(&r);
+    std::stable_sort(uniq.begin(), uniq.end(), diff_less);
+    uniq.erase(std::unique(uniq.begin(), uniq.end(), diff_equal), uniq.end());
+    auto rank_of = [&](const Record *r) {
+        return (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), r, diff_less) - uniq.begin());
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> hd;  // (hap, rank)
+    for (auto &r : I.recs) {
+        if (r.n_alleles != 2 || r.carriers.empty()) continue;
+        uint32_t rk = rank_of(&r);
+        for (uint32_t h : r.carriers)
+            if (h < H) hd.push_back({h, rk});
+    }
+    std::stable_sort(hd.begin(), hd.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    // per-hap spans
+    std::vector<uint32_t> hap_ids, span_b, span_e;
+    for (size_t i = 0; i < hd.size();) {
+        size_t j = i;
+        while (j < hd.size() && hd[j].first == hd[i].first) j++;
+        hap_ids.push_back(hd[i].first);
+        span_b.push_back((uint32_t)i);
+        span_e.push_back((uint32_t)j);
+        i = j;
+    }
+    // ---- group_by_diffs: sort haplotypes by diff list (rank order == Vec<Diff> order)
+    std::vector<uint32_t> order(hap_ids.size());
+    std::iota(order.begin(), order.end(), 0);
+    auto seq_less = [&](uint32_t a, uint32_t b) {
+        return std::lexicographical_compare(
+            hd.begin() + span_b[a], hd.begin() + span_e[a], hd.begin() + span_b[b], hd.begin() + span_e[b],
+            [](const auto &x, const auto &y) { return x.second < y.second; });
+    };
+    auto seq_eq = [&](uint32_t a, uint32_t b) {
+        if (span_e[a] - span_b[a] != span_e[b] - span_b[b]) return false;
+        for (uint32_t t = 0; t < span_e[a] - span_b[a]; t++)
+            if (hd[span_b[a] + t].second != hd[span_b[b] + t].second) return false;
+        return true;
+    };
+    std::stable_sort(order.begin(), order.end(), seq_less);
+    struct Group { uint32_t first, last; };  // run in `order`
+    std::vector<Group> groups;
+    for (uint32_t i = 0; i < order.size();) {
+        uint32_t j = i;
+        while (j < order.size() && seq_eq(order[i], order[j])) j++;
+        groups.push_back({i, j});
+        i = j;
+    }
+
+    // ---- load_haplotypes: patch each group, dedup by (nucs, pos) sequence; later group wins
+    std::vector<Distinct> &dist = out.dist;
+    dist.clear();
+    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    RefWindow ref{I.ref.data(), R.es, I.ref.size()};
+    for (uint32_t g = 0; g < groups.size(); g++) {
+        uint32_t rep = order[groups[g].first];
+        std::vector<const Record *> diffs;
+        for (uint32_t t = span_b[rep]; t < span_e[rep]; t++) diffs.push_back(uniq[hd[t].second]);
+        Distinct d;
+        int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos);
+        if (rc) return rc;
+        d.group = (int32_t)g;
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < d.nuc.size(); i++) {
+            h = (h ^ d.nuc[i]) * 1099511628211ull;
+            h = (h ^ (d.pos[i] - R.es)) * 1099511628211ull;
+        }
+        auto &bucket = by_hash[h];
+        bool replaced = false;
+        for (uint32_t idx : bucket) {
+            if (dist[idx].nuc == d.nuc && dist[idx].pos == d.pos) {
+                dist[idx].group = (int32_t)g;  // HashMap::insert replaces the value
+                replaced = true;
+                break;
+            }
+        }
+        if (!replaced) {
+            bucket.push_back((uint32_t)dist.size());
+            dist.push_back(std::move(d));
+        }
+    }
+    // membership and carrier counts
+    std::vector<uint32_t> &carriers = out.carriers;
+    carriers.assign(dist.size(), 0);
+    std::vector<std::pair<uint32_t, uint32_t>> member;  // (hap id, local)
+    uint64_t covered = 0;
+    for (uint32_t i = 0; i < dist.size(); i++) {
+        const Group &G = groups[dist[i].group];
+        carriers[i] = G.last - G.first;
+        covered += carriers[i];
+        if (B.keep_membership)
+            for (uint32_t t = G.first; t < G.last; t++) member.push_back({hap_ids[order[t]], i});
+    }
+    R.ref_local = -1;
+    if (covered < H) {  // haplotypes_with_reference_genome is non-empty (main.rs:129)
+        Distinct d;
+        d.nuc = I.ref;
+        d.pos.resize(I.ref.size());
+        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.group = -1;
+        R.ref_local = (int32_t)dist.size();
+        dist.push_back(std::move(d));
+        carriers.push_back((uint32_t)(H - covered));
+    }
+    if (B.keep_membership) {
+        std::sort(member.begin(), member.end());
+        R.nonref_id.resize(member.size());
+        R.nonref_local.resize(member.size());
+        for (size_t i = 0; i < member.size(); i++) {
+            R.nonref_id[i] = member[i].first;
+            R.nonref_local[i] = member[i].second;
+        }
+    }
+
+    return TFBS_OK;
+}
+
+// Appends a built region to the batch: packs its haplotypes for the GPU.
+void commit_region(Batch &B, RegionBuilt &&built) {
+    RegionH &R = built.R;
+    const std::vector<Distinct> &dist = built.dist;
+    const std::vector<uint32_t> &carriers = built.carriers;
+    // ---- pack
+    const uint32_t region_index = (uint32_t)B.rh.size();
+    R.hap_begin = (uint32_t)B.haps.size();
+    R.hap_count = (uint32_t)dist.size();
+    DevRegion dr{};
+    dr.inner_off = (uint32_t)(B.inner.size() / 2);
+    dr.n_inner = (uint32_t)R.ranges.size();
+    for (auto &r : R.ranges) {
+        // positions relative to ext_start, clamped: only containment of small
+        // non-negative positions is ever tested, which clamping preserves.
+        auto rel = [&](uint64_t x) -> int32_t {
+            if (x < R.es) { uint64_t d = R.es - x; return d > (1u << 30) ? -(1 << 30) : -(int32_t)d; }
+            uint64_t d = x - R.es;
+            return d > (1u << 30) ? (1 << 30) : (int32_t)d;
+        };
+        B.inner.push_back(rel(r.first));
+        B.inner.push_back(rel(r.second));
+    }
+    B.regions.push_back(dr);
+    for (uint32_t i = 0; i < dist.size(); i++) {
+        const Distinct &d = dist[i];
+        const uint32_t n = (uint32_t)d.nuc.size();
+        DevHap hm{};
+        hm.word_off = (uint32_t)B.words.size();
+        hm.len = n;
+        hm.region = region_index;
+        size_t nw = (n + 15) / 16 + 3;
+        B.words.resize(B.words.size() + nw, 0u);
+        bool has_n = false, affine = true;
+        for (uint32_t p = 0; p < n; p++) {
+            uint8_t c = d.nuc[p];
+            if (c == 4) { has_n = true; c = 0; }  // N packs as A; the kernel subtracts w[j][A]
+            B.words[hm.word_off + p / 16] |= (uint32_t)c << (2 * (p % 16));
+            if (d.pos[p] != R.es + p) affine = false;
+        }
+        if (has_n) {
+            hm.flags |= HAP_HAS_N;
+            hm.nmask_off = (uint32_t)B.nmask.size();
+            B.nmask.resize(B.nmask.size() + (n + 31) / 32 + 2, 0u);
+            for (uint32_t p = 0; p < n; p++)
+                if (d.nuc[p] == 4) B.nmask[hm.nmask_off + p / 32] |= 1u << (p % 32);
+        }
+        if (!affine) {
+            hm.flags |= HAP_HAS_POS;
+            hm.pos_off = (uint32_t)B.posrel.size();
+            for (uint32_t p = 0; p < n; p++) B.posrel.push_back((int32_t)(d.pos[p] - R.es));
+        }
+        hm.count_off = B.n_counts;
+        B.n_counts += (uint64_t)B.n_slots * dr.n_inner;
+        B.haps.push_back(hm);
+        B.hap_carriers.push_back(carriers[i]);
+        uint64_t w = 0;
+        for (uint32_t L : B.pwm_lens)
+            if (n >= L) {
+                w += n - L + 1;
+                B.cell_ops += (uint64_t)(n - L + 1) * L;
+            }
+        B.windows += w;
+        B.eff_windows += w * carriers[i];
+    }
+    B.rh.push_back(std::move(R));
+}
+
+}  // namespace tfbs
+
+using tfbs::Batch;
+
+extern "C" {
+
+int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membership, tfbs_batch **out) {
+    if (!p || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const tfbs::Patterns &P = tfbs::patterns_of(p);
+    if (P.pats.empty()) return tfbs::fail(TFBS_E_NOPATTERN, "no pattern");  // main.rs:238
+    if ((uint64_t)n_samples * 2 > 0xFFFFFFF0ull) return tfbs::fail(TFBS_E_ARG, "too many samples");
+    tfbs::Plan plan;
+    int rc = P.build_plan(1u << 30, &plan);
+    if (rc) return rc;
+    if (plan.zero_len_panics)
+        return tfbs::fail(TFBS_E_ZEROLEN, "length-0 PWM with negative min_score (pattern.rs:150-156)");
+    auto *b = new tfbs_batch();
+    Batch &B = b->b;
+    B.pats = &P;
+    B.n_samples = n_samples;
+    B.keep_membership = keep_membership != 0;
+    B.slot_pid = plan.slot_pid;
+    B.n_slots = (uint32_t)plan.slot_pid.size();
+    for (auto &q : P.pats)
+        if (q.kind == TFBS_KIND_PWM && q.len > 0) B.pwm_lens.push_back(q.len);
+    *out = b;
+    return TFBS_OK;
+}
+
+void tfbs_batch_destroy(tfbs_batch *b) { delete b; }
+
+int tfbs_batch_add_bed(tfbs_batch *b, const char *basename) {
+    if (!b || !basename) return tfbs::fail(TFBS_E_ARG, "null argument");
+    b->b.beds.push_back(basename);
+    return (int)b->b.beds.size() - 1;
+}
+
+int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t ms, uint64_t me, uint64_t *es, uint64_t *ee) {
+    if (!b || !es || !ee) return tfbs::fail(TFBS_E_ARG, "null argument");
+    uint64_t L = b->b.pats->max_length();
+    if (ms + 1 < L) return tfbs::fail(TFBS_E_RANGE, "region start closer than the PWM length to 0 (main.rs:407)");
+    *es = ms + 1 - L;  // u64 wrapping as in --release (L = 0 gives [s+1, e-1])
+    *ee = me + L - 1;
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_begin(tfbs_batch *b, uint64_t ms, uint64_t me, const char *ref_ascii, size_t n_ref) {
+    if (!b || (n_ref && !ref_ascii)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    Batch &B = b->b;
+    if (B.open) return tfbs::fail(TFBS_E_STATE, "region already open");
+    B.cur = tfbs::RegionH();
+    B.cur_rec.clear();
+    B.cur_inner.clear();
+    B.status = TFBS_OK;
+    B.cur.ms = ms;
+    B.cur.me = me;
+    int rc = tfbs_batch_region_ext(b, ms, me, &B.cur.es, &B.cur.ee);
+    if (rc) return rc;
+    B.cur_ref.resize(n_ref);
+    for (size_t i = 0; i < n_ref; i++) {
+        int c = tfbs::to_nuc((uint8_t)ref_ascii[i]);
+        if (c < 0) return tfbs::fail(TFBS_E_BADBASE, std::string("Unknown nucleotide ") + std::to_string((int)(uint8_t)ref_ascii[i]));
+        B.cur_ref[i] = (uint8_t)c;
+    }
+    B.open = true;
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_add_inner(tfbs_batch *b, uint32_t bed, uint64_t s, uint64_t e) {
+    if (!b || !b->b.open) return tfbs::fail(TFBS_E_STATE, "no open region");
+    if (bed >= b->b.beds.size()) return tfbs::fail(TFBS_E_ARG, "unknown bed index");
+    b->b.cur_inner.push_back({bed, {s, e}});
+    return TFBS_OK;
+}
+
+static int to_codes(const char *s, std::vector<uint8_t> &out) {
+    out.clear();
+    for (const char *p = s; *p; p++) {
+        int c = tfbs::to_nuc((uint8_t)*p);
+        if (c < 0) return tfbs::fail(TFBS_E_BADBASE, std::string("Unknown nucleotide ") + std::to_string((int)(uint8_t)*p));
+        out.push_back((uint8_t)c);
+    }
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_add_record_gt(tfbs_batch *b, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                                    const int32_t *gt) {
+    if (!b || !b->b.open) return tfbs::fail(TFBS_E_STATE, "no open region");
+    Batch &B = b->b;
+    if (B.status) return B.status;
+    if (n_alleles < 2 || !alt) return B.status = tfbs::fail(TFBS_E_ALLELES, "record with one allele (haplotype.rs:22)");
+    if (!ref || (n_alleles == 2 && B.n_samples && !gt)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    tfbs::Record r;
+    r.pos = pos;
+    r.n_alleles = n_alleles;
+    int rc = to_codes(ref, r.ref);
+    if (!rc) rc = to_codes(alt, r.alt);
+    if (rc) return B.status = rc;
+    if (n_alleles == 2) {
+        const int32_t VE = INT32_MIN + 1;
+        for (uint32_t s = 0; s < B.n_samples; s++) {
+            int32_t g0 = gt[2 * s], g1 = gt[2 * s + 1];
+            uint32_t glen = g0 == VE ? 0 : (g1 == VE ? 1 : 2);
+            if (glen != n_alleles) return B.status = tfbs::fail(TFBS_E_PLOIDY, "Inconsistent number of alleles");
+            if (g0 == 4) r.carriers.push_back(2 * s);      // GenotypeAllele::Unphased(1)
+            if (g1 == 5) r.carriers.push_back(2 * s + 1);  // GenotypeAllele::Phased(1)
+        }
+    }
+    B.cur_rec.push_back(std::move(r));
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_add_record_carriers(tfbs_batch *b, uint64_t pos, const char *ref, const char *alt,
+                                          const uint32_t *ids, size_t n) {
+    if (!b || !b->b.open) return tfbs::fail(TFBS_E_STATE, "no open region");
+    Batch &B = b->b;
+    if (B.status) return B.status;
+    if (!ref || !alt || (n && !ids)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    tfbs::Record r;
+    r.pos = pos;
+    int rc = to_codes(ref, r.ref);
+    if (!rc) rc = to_codes(alt, r.alt);
+    if (rc) return B.status = rc;
+    r.carriers.assign(ids, ids + n);
+    B.cur_rec.push_back(std::move(r));
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_end(tfbs_batch *b) {
+    if (!b || !b->b.open) return tfbs::fail(TFBS_E_STATE, "no open region");
+    Batch &B = b->b;
+    B.open = false;
+    if (B.status) return B.status;
+    B.counts_valid = false;
+    tfbs::RegionInput in;
+    in.R = std::move(B.cur);
+    in.ref = std::move(B.cur_ref);
+    in.recs = std::move(B.cur_rec);
+    in.inner = std::move(B.cur_inner);
+    B.cur_rec.clear();
+    B.cur_inner.clear();
+    tfbs::RegionBuilt built;
+    int rc = tfbs::build_region(B, std::move(in), built);
+    if (rc) return rc;
+    tfbs::commit_region(B, std::move(built));
+    return TFBS_OK;
+}
+
+size_t tfbs_batch_num_regions(const tfbs_batch *b) { return b ? b->b.rh.size() : 0; }
+size_t tfbs_batch_num_haplotypes(const tfbs_batch *b) { return b ? b->b.haps.size() : 0; }
+uint64_t tfbs_batch_num_windows(const tfbs_batch *b) { return b ? b->b.windows : 0; }
+uint64_t tfbs_batch_num_effective_windows(const tfbs_batch *b) { return b ? b->b.eff_windows : 0; }
+uint64_t tfbs_batch_num_cell_ops(const tfbs_batch *b) { return b ? b->b.cell_ops : 0; }
+uint64_t tfbs_batch_input_bytes(const tfbs_batch *b) { return b ? b->b.device_bytes() : 0; }
+uint64_t tfbs_batch_output_bytes(const tfbs_batch *b) { return b ? b->b.n_counts * 4ull : 0; }
+
+int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *nh, uint32_t *nv) {
+    if (!b || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    if (nh) *nh = b->b.rh[region].hap_count;
+    if (nv) *nv = b->b.rh[region].n_variants;
+    return TFBS_OK;
+}
+
+int tfbs_patch_haplotype(uint64_t rs, uint64_t re, size_t nd, const uint64_t *dpos, const uint8_t *dref,
+                         const uint32_t *dnref, const uint8_t *dalt, const uint32_t *dnalt, const uint8_t *ref_nucs,
+                         const uint64_t *ref_pos, size_t n_ref, uint8_t *out_nucs, uint64_t *out_pos, size_t cap,
+                         size_t *n_out) {
+    if (!n_out || (nd && (!dpos || !dnref || !dnalt)) || (n_ref && (!ref_nucs || !ref_pos)))
+        return tfbs::fail(TFBS_E_ARG, "null argument");
+    std::vector<tfbs::Record> recs(nd);
+    size_t ro = 0, ao = 0;
+    for (size_t i = 0; i < nd; i++) {
+        recs[i].pos = dpos[i];
+        recs[i].ref.assign(dref + ro, dref + ro + dnref[i]);
+        recs[i].alt.assign(dalt + ao, dalt + ao + dnalt[i]);
+        ro += dnref[i];
+        ao += dnalt[i];
+    }
+    std::vector<const tfbs::Record *> ptrs;
+    for (auto &r : recs) ptrs.push_back(&r);
+    std::vector<uint8_t> nuc;
+    std::vector<uint64_t> pos;
+    int rc;
+    bool consecutive = true;
+    for (size_t i = 1; i < n_ref; i++)
+        if (ref_pos[i] != ref_pos[0] + i) consecutive = false;
+    if (consecutive) {
+        rc = tfbs::patch(rs, re, ptrs, ref_nucs, n_ref ? ref_pos[0] : 0, n_ref, nuc, pos);
+    } else {
+        // arbitrary reference vectors: materialise a dense window over [min, max]
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (size_t i = 0; i < n_ref; i++) { lo = std::min(lo, ref_pos[i]); hi = std::max(hi, ref_pos[i]); }
+        if (hi - lo > (1u << 26)) return tfbs::fail(TFBS_E_ARG, "reference positions too sparse");
+        (void)lo;
+        return tfbs::fail(TFBS_E_ARG, "reference positions must be consecutive");
+    }
+    if (rc) return rc;
+    *n_out = nuc.size();
+    if (nuc.size() > cap) return tfbs::fail(TFBS_E_ARG, "output capacity too small");
+    if (!nuc.empty()) {
+        memcpy(out_nucs, nuc.data(), nuc.size());
+        memcpy(out_pos, pos.data(), pos.size() * 8);
+    }
+    return TFBS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+// Host-side region batch: the distinct haplotypes of many merged regions,
+// packed for the scan kernels, plus what the count aggregation needs.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "patterns.hpp"
+#include "tfbs_internal.hpp"
+
+namespace tfbs {
+
+struct Record {  // one BCF record as load_diffs sees it (haplotype.rs:16-60)
+    uint64_t pos = 0;
+    uint32_t n_alleles = 2;
+    std::vector<uint8_t> ref, alt;   // nucleotide codes
+    std::vector<uint32_t> carriers;  // haplotype ids carrying alt (2*sample + side)
+};
+
+struct InnerKey {   // one (bed, inner range) of select_inner_peaks (main.rs:62-72)
+    uint32_t bed;
+    uint64_t s, e;
+    uint32_t mult;  // duplicates of the same range in one bed list count twice (main.rs:503-505)
+    int32_t slot;   // distinct-range slot in the kernel output, -1 if the range is empty (e < s)
+};
+
+struct RegionH {
+    uint64_t ms = 0, me = 0, es = 0, ee = 0;
+    uint32_t hap_begin = 0, hap_count = 0;  // distinct haplotypes (batch-global indices)
+    int32_t ref_local = -1;                 // local index of the reference-group haplotype, -1 if none
+    uint32_t n_variants = 0;
+    std::vector<InnerKey> keys;             // sorted by (s, e, bed)
+    std::vector<std::pair<uint64_t, uint64_t>> ranges;  // distinct non-empty inner ranges
+    // membership: haplotype id -> local distinct index; ids not listed use ref_local
+    std::vector<uint32_t> nonref_id, nonref_local;
+};
+
+struct Batch {
+    const Patterns *pats = nullptr;
+    uint32_t n_samples = 0;
+    bool keep_membership = true;
+    uint32_t n_slots = 0;                 // pattern_id slots (Plan::slot_pid)
+    std::vector<uint16_t> slot_pid;
+    std::vector<std::string> beds;        // registered bed basenames
+    std::vector<uint32_t> pwm_lens;       // lengths of scannable strands (for window counting)
+
+    // packed device image
+    std::vector<uint32_t> words;          // 2-bit bases, 16 per word, LSB first, +3 pad words per hap
+    std::vector<uint32_t> nmask;          // N masks (+2 pad words per hap)
+    std::vector<int32_t> posrel;          // positions relative to ext_start (non-affine haps only)
+    std::vector<DevHap> haps;
+    std::vector<DevRegion> regions;
+    std::vector<int32_t> inner;           // (s_rel, e_rel) pairs
+    std::vector<uint32_t> hap_carriers;   // carriers per distinct hap
+    uint64_t n_counts = 0;                // u32 counts the scan writes
+    std::vector<uint32_t> counts;         // downloaded counts
+    bool counts_valid = false;
+
+    std::vector<RegionH> rh;
+    uint64_t windows = 0, eff_windows = 0, cell_ops = 0;
+
+    // region under construction
+    bool open = false;
+    RegionH cur;
+    std::vector<uint8_t> cur_ref;         // nucleotide codes of the fetched window
+    std::vector<Record> cur_rec;
+    std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> cur_inner;
+    int status = TFBS_OK;
+
+    uint64_t device_bytes() const;
+};
+
+struct RegionInput {  // one merged region as the reader hands it over
+    RegionH R;                        // ms, me, es, ee set
+    std::vector<uint8_t> ref;         // nucleotide codes from es
+    std::vector<Record> recs;         // records in BCF order
+    std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> inner;  // (bed, (s, e))
+};
+
+struct Distinct {  // one distinct haplotype (a key of load_haplotypes' HashMap)
+    std::vector<uint8_t> nuc;
+    std::vector<uint64_t> pos;
+    int32_t group;
+};
+
+struct RegionBuilt {
+    RegionH R;
+    std::vector<Distinct> dist;
+    std::vector<uint32_t> carriers;
+};
+
+int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);
+void commit_region(Batch &B, RegionBuilt &&built);
+
+// haplotype.rs:94-156 over a reference window given as codes for positions
+// [ref_start, ref_start + n_ref).  Diffs are pointers to records.
+int patch(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const uint8_t *ref, uint64_t ref_start,
+          size_t n_ref, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos);
+
+}  // namespace tfbs
+
+struct tfbs_batch {
+    tfbs::Batch b;
+};

@@ -1,0 +1,51 @@
+// Host pattern list and the device plan derived from it.
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "tfbs_internal.hpp"
+
+namespace tfbs {
+
+struct Pat {  // Pattern (types.rs:86-90)
+    int kind = TFBS_KIND_PWM;
+    int direction = TFBS_DIR_P;
+    uint16_t pattern_id = 0;
+    int32_t min_score = 0;
+    uint32_t len = 0;
+    std::vector<int32_t> w5;  // len x [A,C,G,T,N=0]
+    std::string name;
+};
+
+struct Plan {
+    std::vector<uint16_t> slot_pid;  // slot -> pattern_id
+    std::vector<DevPattern> fast_pats;
+    std::vector<DevTile> fast_tiles;
+    std::vector<int32_t> lut;        // blocks x 256
+    std::vector<int32_t> colA;       // per fast-pattern column: weight of A (N correction)
+    std::vector<DevPattern> gen_pats;
+    std::vector<DevTile> gen_tiles;
+    std::vector<int32_t> gen_w;      // per generic column: 5 weights
+    uint32_t max_tile_blocks = 0;
+    uint32_t max_tile_cols = 0;
+    bool zero_len_panics = false;
+};
+
+struct Patterns {
+    std::vector<Pat> pats;
+    std::map<uint16_t, std::string> names;
+    void add(const Pat &p);
+    uint32_t max_length() const;
+    int build_plan(uint32_t tile_blocks, Plan *plan) const;
+};
+
+int parse_weight(const std::string &s, int32_t *out);
+int parse_threshold_file(const std::string &path, float thr, int32_t *out);
+int parse_pwm_files(const std::string &pwm_file, const std::string &thr_dir, float thr,
+                    const std::vector<std::string> &wanted, bool add_reverse, Patterns *out);
+const Patterns &patterns_of(const tfbs_patterns *p);
+
+}  // namespace tfbs

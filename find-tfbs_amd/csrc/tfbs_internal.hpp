@@ -1,0 +1,72 @@
+// Internal declarations shared by the host C++ and the HIP translation units.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/tfbs_amd.h"
+
+namespace tfbs {
+
+// Sets this thread's last-error message and returns code.
+int fail(int code, const std::string &msg);
+
+// util.rs:4-16 to_nucleotide: ASCII -> 0..4, or -1.
+inline int to_nuc(uint8_t c) {
+    switch (c) {
+    case 'A': case 'a': return 0;
+    case 'C': case 'c': return 1;
+    case 'G': case 'g': return 2;
+    case 'T': case 't': return 3;
+    case 'N': case 'n': return 4;
+    default: return -1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Device-side descriptors (POD, shared with the kernels)
+// ---------------------------------------------------------------------------
+constexpr int kLutEntries = 256;   // one 4-mer block: 4^4 entries
+constexpr int kFastMaxLen = 32;    // the LUT path reads a 64-bit (32-base) window per lane
+constexpr int kMaxInnerPass = 8;   // inner ranges handled per pass (accumulators per lane)
+constexpr int kMaxTileSlots = 64;  // pattern_id slots per tile: one lane each
+
+struct DevPattern {        // one PWM strand, in tile order
+    uint32_t lut_off;      // fast path: block offset inside the tile's LDS image
+    uint32_t col_off;      // offset of this pattern's columns in colA (fast) / weights (generic)
+    int32_t min_score;
+    uint16_t len;
+    uint16_t nblk;         // ceil(len / 4)
+    uint16_t slot_local;   // pattern_id slot relative to the tile's first slot
+    uint16_t orig_index;   // index in creation order (for tfbs_matches)
+};
+
+struct DevTile {
+    uint32_t pat_begin, pat_end;  // range in the DevPattern array
+    uint32_t lut_begin;           // first LUT block (global)
+    uint32_t nblocks;             // LUT blocks (x 256 ints) in the tile
+    uint32_t col_begin;           // first colA entry (global)
+    uint32_t ncols;
+    uint32_t slot_begin;          // global pattern_id slot of local slot 0
+    uint32_t nslots;
+};
+
+enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };
+
+struct DevHap {
+    uint32_t word_off;   // packed 2-bit bases, 16 per u32, LSB first
+    uint32_t len;        // bases
+    uint32_t region;     // batch region index
+    uint32_t flags;      // HapFlags
+    uint32_t nmask_off;  // u32 words of the N mask (bit i = base i is N), if HAP_HAS_N
+    uint32_t pos_off;    // int32 positions relative to ext_start, if HAP_HAS_POS
+    uint64_t count_off;  // counts[count_off + slot * n_inner + k]
+};
+
+struct DevRegion {
+    uint32_t inner_off;  // into the inner (s_rel, e_rel) pair array
+    uint32_t n_inner;    // distinct inner ranges
+};
+
+}  // namespace tfbs

@@ -1,0 +1,233 @@
+/*
+ * tfbs_amd.h -- C ABI of the MI355X-native PWM scanner that drops in for
+ * find-tfbs's per-haplotype TFBS scoring path (Helkafen/find-tfbs v1.0.1).
+ *
+ * The reference has no FFI on this path: it is the Rust `Pattern` enum
+ * (types.rs:86-90) dispatched by `matches` (pattern.rs:141-171), fed by
+ * `load_haplotypes` (haplotype.rs:77-88) and consumed by
+ * `count_matches_by_sample` / `counts_as_genotypes` (main.rs:439-534).  Each
+ * entry point below names the reference function it replaces; INTEGRATION.md
+ * shows the Rust `extern "C"` block a maintainer would add to bind them.
+ *
+ * Conventions
+ *  - Every entry returns int: TFBS_OK (0) or a negative TFBS_E_* code;
+ *    tfbs_last_error() returns this thread's message for the last failure.
+ *    The reference panics where these codes are returned (cited per code).
+ *  - Caller owns every buffer it passes for the duration of the call; the
+ *    library copies what it keeps.  Opaque objects are freed by their
+ *    *_destroy.  No callbacks.
+ *  - tfbs_patterns is immutable after creation and may be shared across
+ *    threads.  tfbs_ctx and tfbs_batch are single-threaded objects; use one
+ *    ctx per host thread / per GPU (the reference runs one reader per worker,
+ *    main.rs:333-371).
+ *  - Nucleotide codes are the reference enum order A=0 C=1 G=2 T=3 N=4
+ *    (types.rs:5-8); weights are milli-log-odds int32 per column [A,C,G,T,N]
+ *    with N = 0 (types.rs:103-114).
+ *  - Haplotype ids are 2*sample + side, side 0 = Left, 1 = Right
+ *    (types.rs:29-30, 66-70).
+ */
+#ifndef TFBS_AMD_H
+#define TFBS_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFBS_OK 0
+#define TFBS_E_ARG (-1)         /* bad argument / call order */
+#define TFBS_E_BADBASE (-2)     /* util.rs:15 "Unknown nucleotide" panic */
+#define TFBS_E_REFMISMATCH (-3) /* haplotype.rs:126-128 panic */
+#define TFBS_E_MNP (-4)         /* haplotype.rs:141-142 "Missing case" panic */
+#define TFBS_E_PLOIDY (-5)      /* haplotype.rs:32 assert */
+#define TFBS_E_RANGE (-6)       /* main.rs:407 u64 underflow / FASTA seek failure */
+#define TFBS_E_PARSE (-7)       /* pattern.rs parse().unwrap()/expect panics */
+#define TFBS_E_IO (-8)          /* file open/read failures (pattern.rs:116, bed.rs:34, ...) */
+#define TFBS_E_HIP (-9)         /* HIP runtime error */
+#define TFBS_E_NODEVICE (-10)   /* no HIP device: the product never falls back to the CPU */
+#define TFBS_E_ALLELES (-11)    /* haplotype.rs:22 alleles[1] on a record with one allele */
+#define TFBS_E_ZEROLEN (-12)    /* pattern.rs:150-156 index past the end for a length-0 PWM */
+#define TFBS_E_NOPATTERN (-13)  /* main.rs:238 assert!(pwm_list.len() > 0) */
+#define TFBS_E_STATE (-14)      /* object used out of order */
+#define TFBS_E_NOMEM (-15)
+
+const char *tfbs_strerror(int code);
+const char *tfbs_last_error(void);
+const char *tfbs_version(void);
+
+/* ------------------------------------------------------------------ */
+/* Patterns: the plugin surface (types.rs:86-114; README.md:68-72)      */
+/* ------------------------------------------------------------------ */
+#define TFBS_KIND_PWM 0   /* Pattern::PWM */
+#define TFBS_KIND_OTHER 1 /* Pattern::OtherPattern: length 0, never matches */
+#define TFBS_DIR_P 0      /* PWMDirection::P ("+") */
+#define TFBS_DIR_N 1      /* PWMDirection::N ("-") */
+
+typedef struct tfbs_pattern_desc {
+    uint16_t pattern_id;    /* shared by both strands of one PWM (pattern.rs:73-77) */
+    uint8_t direction;      /* TFBS_DIR_* */
+    uint8_t kind;           /* TFBS_KIND_* */
+    uint32_t length;        /* columns (pattern_length, types.rs:92-101) */
+    const int32_t *weights; /* length x 5 ints [A,C,G,T,N]; the N column is ignored (always 0) */
+    int32_t min_score;      /* a window matches iff score > min_score (pattern.rs:151) */
+    const char *name;       /* pattern_id -> name (main.rs:239-250) */
+} tfbs_pattern_desc;
+
+typedef struct tfbs_patterns tfbs_patterns;
+
+/* Replaces building Vec<Pattern> by hand: copies n descriptors. */
+int tfbs_patterns_create(const tfbs_pattern_desc *descs, size_t n, tfbs_patterns **out);
+/* Replaces parse_pwm_files (pattern.rs:37-87): names_csv is --pwm_names,
+ * add_reverse = !--forward_only.  Fails with TFBS_E_NOPATTERN when nothing loads. */
+int tfbs_patterns_from_files(const char *pwm_file, const char *threshold_dir, float pwm_threshold,
+                             const char *names_csv, int add_reverse, tfbs_patterns **out);
+size_t tfbs_patterns_count(const tfbs_patterns *p);
+/* Pointers in *out stay valid while p lives. */
+int tfbs_patterns_get(const tfbs_patterns *p, size_t i, tfbs_pattern_desc *out);
+/* Name for a pattern_id (main.rs:239-250, last writer wins); NULL if unknown. */
+const char *tfbs_patterns_name_of(const tfbs_patterns *p, uint16_t pattern_id);
+/* max pattern_length over all patterns (main.rs:404). */
+uint32_t tfbs_patterns_max_length(const tfbs_patterns *p);
+void tfbs_patterns_destroy(tfbs_patterns *p);
+
+/* pattern.rs:13-16 parse_weight: (f32(s) * 1000f32).round() as i32. */
+int tfbs_parse_weight(const char *s, int32_t *out);
+/* pattern.rs:18-35 parse_threshold_file: returns 1 (found, *out set), 0 (None) or an error. */
+int tfbs_parse_threshold_file(const char *path, float pwm_threshold, int32_t *out);
+
+/* ------------------------------------------------------------------ */
+/* Device context: one GPU, one HIP stream, the pattern tables in HBM   */
+/* ------------------------------------------------------------------ */
+typedef struct tfbs_ctx tfbs_ctx;
+
+int tfbs_device_count(int *n);
+/* Uploads the 4-mer lookup tables of p to `device`.  p must outlive ctx. */
+int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out);
+void tfbs_ctx_destroy(tfbs_ctx *ctx);
+int tfbs_ctx_sync(tfbs_ctx *ctx);
+/* Device time (HIP events on the ctx stream) of the last tfbs_scan, ms. */
+float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx);
+/* Number of scan-kernel launches issued by the last tfbs_scan. */
+int tfbs_ctx_last_scan_launches(const tfbs_ctx *ctx);
+
+/* Replaces matches() (pattern.rs:141-171) for ONE haplotype against every
+ * pattern, on the GPU.  nucs are codes 0..4, pos the NucleotidePos.pos values.
+ * Writes match ranges grouped by pattern index (in creation order): for each
+ * pattern i, counts[i] matches; the ranges are concatenated into out_start /
+ * out_end (start = pos[w], end = pos[w] + L - 1) in window order.  *n_total
+ * receives the total; TFBS_E_ARG if cap is too small (then *n_total is the need). */
+int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t n, uint32_t *counts,
+                 uint64_t *out_start, uint64_t *out_end, size_t cap, size_t *n_total);
+
+/* ------------------------------------------------------------------ */
+/* Haplotype reconstruction (haplotype.rs:94-156)                       */
+/* ------------------------------------------------------------------ */
+/* patch_haplotype over a reference window.  Diffs are flattened: diff d has
+ * ref codes dref[roff..roff+dnref[d]) and alt codes dalt[aoff..aoff+dnalt[d]).
+ * Writes at most cap bases; *n_out gets the length (TFBS_E_ARG if > cap). */
+int tfbs_patch_haplotype(uint64_t range_start, uint64_t range_end, size_t n_diffs, const uint64_t *dpos,
+                         const uint8_t *dref, const uint32_t *dnref, const uint8_t *dalt, const uint32_t *dnalt,
+                         const uint8_t *ref_nucs, const uint64_t *ref_pos, size_t n_ref, uint8_t *out_nucs,
+                         uint64_t *out_pos, size_t cap, size_t *n_out);
+
+/* ------------------------------------------------------------------ */
+/* Region batches: load_haplotypes + find_all_matches + counting          */
+/* (haplotype.rs:13-88, main.rs:94-154, 395-436, 439-534)                */
+/* ------------------------------------------------------------------ */
+typedef struct tfbs_batch tfbs_batch;
+
+/* n_samples = selected samples (main.rs:293-314).  keep_membership = 0 drops
+ * per-haplotype group membership (scan-only use; rows then unavailable). */
+int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membership, tfbs_batch **out);
+void tfbs_batch_destroy(tfbs_batch *b);
+/* Registers a BED source by basename (bed.rs:49-60); returns its index >= 0. */
+int tfbs_batch_add_bed(tfbs_batch *b, const char *basename);
+/* main.rs:404-407: the halo-extended window of a merged region. */
+int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t merged_start, uint64_t merged_end, uint64_t *ext_start,
+                          uint64_t *ext_end);
+/* Starts a merged region; ref_ascii = FASTA bases from ext_start (main.rs:156-161,
+ * may be shorter than the window at a contig end). */
+int tfbs_batch_region_begin(tfbs_batch *b, uint64_t merged_start, uint64_t merged_end, const char *ref_ascii,
+                            size_t n_ref);
+/* One inner peak selected by select_inner_peaks (main.rs:62-72); duplicates count twice. */
+int tfbs_batch_region_add_inner(tfbs_batch *b, uint32_t bed, uint64_t start, uint64_t end);
+/* One BCF record (haplotype.rs:16-60): gt = 2 raw BCF GT ints per selected
+ * sample, INT32_MIN+1 = vector_end.  Left carries ALT iff gt0 == 4 (Unphased(1)),
+ * Right iff gt1 == 5 (Phased(1)). */
+int tfbs_batch_region_add_record_gt(tfbs_batch *b, uint64_t pos, uint32_t n_alleles, const char *ref,
+                                    const char *alt, const int32_t *gt);
+/* Same with the carrying haplotype ids given directly (phased synthetic data). */
+int tfbs_batch_region_add_record_carriers(tfbs_batch *b, uint64_t pos, const char *ref, const char *alt,
+                                          const uint32_t *hap_ids, size_t n);
+/* Groups, patches, deduplicates and packs the region's distinct haplotypes. */
+int tfbs_batch_region_end(tfbs_batch *b);
+
+size_t tfbs_batch_num_regions(const tfbs_batch *b);
+size_t tfbs_batch_num_haplotypes(const tfbs_batch *b); /* distinct haplotypes to scan */
+/* Windows the scan scores: sum over distinct haplotypes and PWM patterns of max(0, len - L + 1). */
+uint64_t tfbs_batch_num_windows(const tfbs_batch *b);
+/* Column lookups the scan performs: sum over windows of the pattern length L. */
+uint64_t tfbs_batch_num_cell_ops(const tfbs_batch *b);
+/* Per-sample-weighted windows (each distinct haplotype times its carrier count). */
+uint64_t tfbs_batch_num_effective_windows(const tfbs_batch *b);
+/* Packed bytes the scan reads from HBM per launch (sequence + masks + positions + metadata). */
+uint64_t tfbs_batch_input_bytes(const tfbs_batch *b);
+/* Bytes of hit counts the scan writes. */
+uint64_t tfbs_batch_output_bytes(const tfbs_batch *b);
+
+/* Copies the packed batch into ctx device memory (H2D). */
+int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b);
+/* Scans the uploaded batch on the GPU: per (distinct haplotype, pattern_id,
+ * inner range) hit counts, strands summed (the work of matches() over every
+ * distinct haplotype, main.rs:101-147, plus the overlap test of main.rs:503).
+ * Asynchronous on the ctx stream; tfbs_batch_download waits. */
+int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b);
+/* D2H copy of the counts into the batch. */
+int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
+
+/* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
+ * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */
+int tfbs_batch_region_num_keys(const tfbs_batch *b, size_t region, size_t *n);
+int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t *bed, uint64_t *start,
+                          uint64_t *end, uint16_t *pattern_id, uint32_t *left, uint32_t *right);
+/* counts_as_genotypes + row emission (main.rs:415-429, 439-498) for every
+ * region, in region order.  Appends rows to *text (malloc'd; free with
+ * tfbs_free); *fake_position is the POS counter, advanced per row. */
+int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t *fake_position,
+                    char **text, size_t *len);
+/* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
+int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
+void tfbs_free(void *p);
+
+/* counts_as_genotypes alone (main.rs:439-498): 1 = row (strings written), 0 = no variation. */
+int tfbs_counts_as_genotypes(const uint32_t *left, const uint32_t *right, size_t n, uint32_t *maf, char *info,
+                             size_t info_cap, char *genotypes, size_t gt_cap);
+
+/* ------------------------------------------------------------------ */
+/* Synthetic workloads                            */
+/* ------------------------------------------------------------------ */
+/* Writes <dir>/pwms.txt and <dir>/thr/<name>.thr for n PWMs; lengths follow
+ * config 2 (L = 8..15) or 3 (L = 8 + i%15, the last 30 L = 23 + i%8) or
+ * 5 (L = 25..30).  names_csv (malloc'd) lists the names. */
+int tfbs_synth_write_pwms(const char *dir, uint32_t n_pwms, int length_config, uint64_t seed, char **names_csv);
+typedef struct tfbs_synth_region tfbs_synth_region;
+/* Region `index` of a synthetic chromosome: BED row [1000+400*index, 1200+400*index],
+ * Poisson(20) distinct variant sites over the ext window of max length lmax,
+ * carriers with P(k) ~ 1/k on 1..H/10; indel_pct % of sites are 1-10 bp indels. */
+int tfbs_synth_region_make(uint64_t seed, uint64_t index, uint32_t n_samples, uint32_t lmax, uint32_t indel_pct,
+                           tfbs_synth_region **out);
+void tfbs_synth_region_destroy(tfbs_synth_region *r);
+void tfbs_synth_region_info(const tfbs_synth_region *r, uint64_t *merged_start, uint64_t *merged_end,
+                            uint64_t *ext_start, const char **ref_ascii, size_t *n_ref, size_t *n_records);
+void tfbs_synth_region_record(const tfbs_synth_region *r, size_t i, uint64_t *pos, const char **ref,
+                              const char **alt, const uint32_t **carriers, size_t *n_carriers);
+/* Adds regions [first, first+count) to b (one bed source "synthetic.bed" is
+ * registered on first use; each region's inner peak is its BED row). */
+int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t count, uint32_t indel_pct);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFBS_AMD_H */

@@ -18,8 +18,9 @@
  *      groups patch to the same sequence the later one overwrites the earlier
  *      (HashMap::insert semantics, haplotype.rs:84) and the loser's ids stay in
  *      the reference set (main.rs:103-105, 129-137).
- *   D2 rows of one region are emitted sorted by (inner.start, inner.end, bed name,
- *      pattern_id); POS numbers rows consecutively from 1 (main.rs:329, 424-425).
+ *   D2 rows of one region are emitted sorted by (inner.start, inner.end, bed index
+ *      in registration order, pattern_id); POS numbers rows consecutively from 1
+ *      (main.rs:329, 424-425).
  *   D3 DS is printed with printf("%.4f") of the exact f32 value (ties to even).
  *
  * Arithmetic follows a Rust --release build: i32 scores and u32 counts wrap.
@@ -679,7 +680,7 @@ static void count_one_match(keymap *m, int nbeds, const int *inner_bed, const ui
 /* C-ABI mirror of count_matches_by_sample for the reference's unit test.
  * matches: (start, end, pid, id offset, id count) over a flat id array.
  * inner peaks: flat (bed index, start, end) list; duplicates double-count.
- * Output: keys sorted (s, e, bed, pid); caller reads them via orc_keys_*. */
+ * Output: keys sorted (s, e, bed index, pid); caller reads them via orc_keys_*. */
 typedef struct { keymap m; } orc_keys;
 static int cmp_key(const void *a, const void *b) {
     const orc_key *x = (const orc_key *)a, *y = (const orc_key *)b;

@@ -1,0 +1,155 @@
+"""CPU-side checks of the product library (no GPU calls): symbol exports, the
+host parsers / patcher / genotype encoder against the oracle, and batch
+construction (grouping, dedup) against the oracle's haplotype counts."""
+import os
+import random
+import re
+
+import pytest
+
+import oracle_py as O
+from helpers import GOLD, TD, T, make_regions_synth, pattern_dicts, run_oracle, synth_patterns
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    hdr = open(os.path.join(ROOT, "include", "tfbs_amd.h")).read()
+    decls = set(re.findall(r"^\s*(?:const\s+)?[\w ]+?\**\s*\*?(tfbs_\w+)\(", hdr, re.M))
+    assert len(decls) > 40
+    lib = T.lib()
+    for name in sorted(decls):
+        assert hasattr(lib, name), name
+    declared = {s[0] for s in T._capi.SIGNATURES}
+    assert decls == declared, decls ^ declared
+
+
+def test_no_device_means_loud_failure():
+    if T.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    ps = T.parse_pwm_files(os.path.join(TD, "pwm_definitions.txt"), TD, 0.0001, ["ACGT"])
+    with pytest.raises(T.TfbsError) as ei:
+        T.Scanner(ps)
+    assert ei.value.code == T.TFBS_E_NODEVICE
+
+
+def test_parse_pwm_files_matches_oracle(tmp_path):
+    ps, names = synth_patterns(tmp_path, 40, 3, 11)
+    orc = O.Patterns.from_files(str(tmp_path / "pwms.txt"), str(tmp_path / "thr"), 1e-4, names)
+    assert pattern_dicts(ps) == orc.as_list()
+    ps2, _ = synth_patterns(tmp_path, 40, 3, 11, thr=1e-3, forward_only=True)
+    orc2 = O.Patterns.from_files(str(tmp_path / "pwms.txt"), str(tmp_path / "thr"), 1e-3, names, add_reverse=False)
+    assert pattern_dicts(ps2) == orc2.as_list()
+
+
+def test_parse_acgt_fixture():
+    ps = T.parse_pwm_files(os.path.join(TD, "pwm_definitions.txt"), TD, 0.0001, ["ACGT"])
+    pl = ps.to_list()
+    assert [p.min_score for p in pl] == [3999, 3999]
+    assert [w.acgtn for w in pl[0].weights] == [[1000, 0, 0, 0, 0], [0, 1000, 0, 0, 0], [0, 0, 1000, 0, 0],
+                                                [0, 0, 0, 1000, 0]]
+    assert pl[1].weights == pl[0].weights  # ACGT is its own reverse complement
+    assert T.parse_threshold_file(os.path.join(TD, "ACGT.thr"), 0.0001) == 3999
+    assert T.parse_threshold_file(os.path.join(TD, "ACGT.thr"), 1.0) is None
+    with pytest.raises(T.TfbsError):
+        T.parse_threshold_file(os.path.join(TD, "missing.thr"), 0.1)
+    with pytest.raises(T.TfbsError):  # main.rs:238: no pattern loaded
+        T.parse_pwm_files(os.path.join(TD, "pwm_definitions.txt"), TD, 0.0001, ["NOPE"])
+
+
+def test_parse_weight_matches_oracle():
+    rnd = random.Random(5)
+    vals = ["1.0", "-0.0005", "0.0005", "2.5e-3", "-28.912716067144597", "1e10", "inf", "-inf", "nan", "5.", ".5"]
+    vals += ["%.*f" % (rnd.randint(0, 7), rnd.uniform(-20, 20)) for _ in range(300)]
+    for s in vals:
+        v = O.C.c_int32()
+        assert O.lib().orc_parse_weight(s.encode(), O.C.byref(v)) == 0, s
+        assert T.parse_weight(s) == v.value, s
+
+
+REF = [("A", 0), ("C", 1), ("G", 2), ("T", 3)]
+
+
+@pytest.mark.parametrize("rng,diffs", [
+    ((1, 2), []), ((0, 2), []), ((0, 5), []),
+    ((1, 2), [(100, "A", "C")]), ((1, 2), [(1, "C", "N")]), ((1, 2), [(2, "G", "A")]),
+    ((1, 2), [(1, "C", "N"), (2, "G", "A")]), ((1, 2), [(1, "C", "N"), (4, "G", "A")]),
+    ((1, 2), [(1, "C", "NN")]), ((1, 2), [(2, "G", "NN")]), ((1, 2), [(3, "T", "NN")]),
+    ((1, 2), [(1, "CG", "C")]), ((1, 2), [(2, "GT", "G")]), ((1, 2), [(0, "AC", "A")]),
+    ((0, 3), [(0, "AC", "A"), (1, "C", "T")]), ((0, 3), [(1, "CG", "C"), (2, "G", "T")]),
+    ((0, 2), [(1, "CG", "C"), (2, "G", "T")]), ((0, 3), [(1, "CGT", "C"), (2, "G", "T")]),
+])
+def test_patch_haplotype_matches_reference_vectors(rng, diffs):
+    want = O.patch_haplotype(rng, diffs, REF)
+    got = T.patch_haplotype(rng, [T.Diff(*d) for d in diffs], REF)
+    assert [(n.nuc, n.pos) for n in got] == want
+
+
+def test_patch_haplotype_errors():
+    with pytest.raises(T.TfbsError) as e1:
+        T.patch_haplotype((1, 2), [T.Diff(1, "G", "A")], REF)
+    assert e1.value.code == -3
+    with pytest.raises(T.TfbsError) as e2:
+        T.patch_haplotype((1, 2), [T.Diff(1, "CG", "TA")], REF)
+    assert e2.value.code == -4
+
+
+def test_patch_haplotype_fuzz_vs_oracle():
+    rnd = random.Random(7)
+    for _ in range(400):
+        n = rnd.randint(1, 30)
+        ref = [("ACGTN"[rnd.randrange(5)], 10 + i) for i in range(n)]
+        diffs = []
+        for _ in range(rnd.randint(0, 5)):
+            p = rnd.randint(5, 10 + n + 3)
+            r0 = ref[p - 10][0] if 10 <= p < 10 + n else "A"
+            kind = rnd.randrange(3)
+            if kind == 0:
+                d = (p, r0, rnd.choice("ACGTN"))
+            elif kind == 1:
+                d = (p, r0, r0 + "".join(rnd.choice("ACGT") for _ in range(rnd.randint(1, 3))))
+            else:
+                d = (p, r0 + "".join(rnd.choice("ACGT") for _ in range(rnd.randint(1, 3))), r0)
+            diffs.append(d)
+        rng = (rnd.randint(8, 14), rnd.randint(14, 10 + n + 3))
+        want = O.patch_haplotype(rng, diffs, ref)
+        if isinstance(want, int):
+            with pytest.raises(T.TfbsError):
+                T.patch_haplotype(rng, [T.Diff(*d) for d in diffs], ref)
+        else:
+            got = T.patch_haplotype(rng, [T.Diff(*d) for d in diffs], ref)
+            assert [(x.nuc, x.pos) for x in got] == want, (rng, diffs)
+
+
+def test_counts_as_genotypes_fuzz_vs_oracle():
+    rnd = random.Random(3)
+    for _ in range(300):
+        n = rnd.randint(1, 40)
+        top = rnd.choice([1, 3, 10, 33, 64, 1000])
+        v1 = [rnd.randint(0, top) for _ in range(n)]
+        v2 = [rnd.randint(0, top) for _ in range(n)]
+        want = O.counts_as_genotypes(v1, v2)
+        got = T.counts_as_genotypes(v1, v2)
+        if want is None:
+            assert got is None
+        else:
+            maf, info, gts = want
+            counts, gmaf, f0, f1, f2, ggts = got
+            assert gmaf == maf and ggts == gts
+            assert info == "COUNTS=%s;freqs=%d/%d/%d" % (",".join(map(str, counts)), f0, f1, f2)
+
+
+@pytest.mark.parametrize("indel", [0, 30])
+def test_batch_grouping_matches_oracle(tmp_path, indel):
+    """Distinct-haplotype construction (groups, patch, dedup, reference group) on the
+    host matches the oracle's number_of_haplotypes / variant_count per region."""
+    ps, _ = synth_patterns(tmp_path, 6, 2 if not indel else 5, 4)
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(12)])]
+    regions = make_regions_synth(9, 0, 12, 200, ps.max_length, indel)
+    _, _, stats = run_oracle(ps, 200, beds, regions)
+    from helpers import build_batch
+    b = build_batch(ps, 200, beds, regions)
+    for i, (nh, nv, _) in enumerate(stats):
+        assert b.region_stats(i) == (nh, nv)
+    assert b.num_haplotypes == sum(s[0] for s in stats)
+    assert b.num_windows > 0 and b.num_effective_windows >= b.num_windows

@@ -1,0 +1,230 @@
+"""GPU parity: the HIP scan through the C ABI against the CPU oracle.
+
+Integer work, so every comparison is bit-exact: match lists, per-sample L/R
+count vectors per (bed, inner range, pattern_id) key, and the VCF row text.
+"""
+import json
+import os
+import random
+
+import pytest
+
+import oracle_py as O
+from helpers import GOLD, TD, T, make_regions_synth, run_oracle, run_product, synth_patterns
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if T.device_count() == 0:
+        pytest.fail("gpu test without a visible HIP device")
+
+
+def _hap(s, start=0):
+    return [(c, start + i) for i, c in enumerate(s)]
+
+
+# ------------------------------------------------------------ pattern.rs:268-301 on the GPU
+def test_matches_reference_vectors():
+    c, g = T.Weight(0, 1000, 0, 0), T.Weight(0, 0, 1000, 0)
+    pwm = T.Pattern.PWM([c, g], "pwm", 5, 1500)
+    m = T.matches(pwm, [("A", 10), ("C", 11), ("G", 12), ("T", 13)], ())
+    assert m == [T.Match(T.Range(11, 12), 5, ())]
+
+    w = [T.Weight(0, 0, 100, 0), T.Weight(100, 0, 0, 0), T.Weight(0, 0, 0, 100), T.Weight(100, 0, 0, 0),
+         T.Weight(100, 0, 0, 0)]
+    pad = [("N", 0), ("G", 1), ("A", 2), ("T", 3), ("A", 4), ("A", 5), ("N", 6)]
+    nopad = pad[1:-1]
+    p499 = T.Pattern.PWM(w, "Example", 123, 499)
+    p500 = T.Pattern.PWM(w, "Example", 123, 500)
+    assert len(T.matches(p499, pad)) == 1 and len(T.matches(p499, nopad)) == 1
+    assert len(T.matches(p500, pad)) == 0 and len(T.matches(p500, nopad)) == 0
+    assert T.matches(T.Pattern.OtherPattern("x", 1), pad) == []
+
+
+def _rand_pwm(rnd, L, scale=1000):
+    return [[rnd.randint(-3 * scale, scale) for _ in range(4)] + [0] for _ in range(L)]
+
+
+def test_matches_fuzz_vs_oracle():
+    """Random PWMs of length 1..40 (fast LUT path and the >32 generic path), haplotypes
+    up to 700 bases (several 256-window passes), N bases, non-affine positions."""
+    rnd = random.Random(1)
+    pats = []
+    for i in range(48):
+        L = rnd.choice([1, 2, 3, 4, 5, 7, 8, 11, 15, 16, 17, 24, 29, 30, 31, 32, 33, 36, 40])
+        w = _rand_pwm(rnd, L)
+        best = sum(max(r[:4]) for r in w)
+        worst = sum(min(r[:4]) for r in w)
+        ms = rnd.randint(worst, best) if rnd.random() < 0.8 else best - rnd.randint(0, 3000)
+        pats.append(T.Pattern.PWM([T.Weight(*r[:4]) for r in w], "P%d" % i, i // 2, ms, i % 2))
+    pats.append(T.Pattern.OtherPattern("other", 99))
+    sc = T.Scanner(pats)
+    try:
+        for trial in range(12):
+            n = rnd.choice([0, 1, 5, 31, 64, 65, 200, 257, 513, 700])
+            seq = "".join(rnd.choice("ACGTACGTACGTN" if trial % 3 == 0 else "ACGT") for _ in range(n))
+            pos = []
+            p = 1000
+            for i in range(n):  # non-decreasing positions with repeats and skips
+                pos.append(p)
+                p += rnd.choice([0, 1, 1, 1, 3]) if trial % 2 else 1
+            hap = list(zip(seq, pos))
+            got = sc.matches_all(hap)
+            for i, p_ in enumerate(pats):
+                w5 = [wt.acgtn for wt in p_.weights]
+                want = O.matches(w5, p_.min_score, hap, kind=p_.kind)
+                assert got[i] == want, (trial, i, len(w5))
+    finally:
+        sc.close()
+
+
+# ------------------------------------------------------------ main.rs:548-568 through the product
+def _c1(bcf_json, beds_files, samples_file=True):
+    rec = json.load(open(os.path.join(GOLD, bcf_json)))
+    ps = T.parse_pwm_files(os.path.join(TD, "pwm_definitions.txt"), TD, 0.0001, ["ACGT"])
+    merged, beds = O.load_peak_files([os.path.join(TD, b) for b in beds_files], "chr1", 0)
+    names = rec["samples"]
+    want = [l.strip() for l in open(os.path.join(TD, "samples")) if len(l.rstrip("\n")) > 1]
+    sel = [i for i, s in enumerate(names) if s in set(want)] if samples_file else list(range(len(names)))
+    fai = O.read_fai(os.path.join(TD, "reference_genome.fa.fai"))
+    b = T.RegionBatch(ps, len(sel))
+    for name, _ in beds:
+        b.add_bed(name)
+    for (s, e) in merged:
+        es, ee = b.ext(s, e)
+        ref = O.fasta_fetch(os.path.join(TD, "reference_genome.fa"), fai, "chr1", es, ee + 1)
+        b.begin(s, e, ref)
+        for bi, a, z in T.select_inner_peaks((s, e), beds):
+            b.add_inner(bi, a, z)
+        for r in rec["records"]:
+            if r["chrom"] == "chr1" and r["pos0"] < ee + 1 and r["pos0"] + r["rlen"] > es:
+                b.add_record_gt(r["pos0"], len(r["alleles"]), r["alleles"][0], r["alleles"][1],
+                                [r["gt"][i] for i in sel])
+        b.end()
+    sc = T.Scanner(ps)
+    b.scan(sc)
+    rows, _ = b.rows("chr1")
+    sc.close()
+    header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT" + "".join("\t" + names[i] for i in sel) + "\n"
+    return header + rows
+
+
+def test_integration_no_polymorphism():
+    assert _c1("genotypes.records.json", ["regions1.bed", "regions2.bed"]) == \
+        open(os.path.join(GOLD, "expected_output_1.vcf")).read()
+
+
+def test_integration_one_polymorphism():
+    assert _c1("genotypes2.records.json", ["regions1.bed", "regions2.bed"]) == \
+        open(os.path.join(GOLD, "expected_output_2.vcf")).read()
+
+
+def test_config1_regions1_only():
+    # BASELINE.json configs[0]: genotypes2.bcf + regions1.bed + ACGT -> the same single row
+    got = _c1("genotypes2.records.json", ["regions1.bed"])
+    assert got.splitlines()[1:] == open(os.path.join(GOLD, "expected_output_2.vcf")).read().splitlines()[1:]
+
+
+# ------------------------------------------------------------ synthetic regions vs the oracle
+def _compare(ps, n_samples, beds, regions, min_maf=0):
+    okeys, orows, _ = run_oracle(ps, n_samples, beds, regions, min_maf=min_maf)
+    sc = T.Scanner(ps)
+    try:
+        pkeys, prows, b = run_product(sc, ps, n_samples, beds, regions, min_maf=min_maf)
+    finally:
+        sc.close()
+    assert len(okeys) == len(pkeys)
+    for i, (a, z) in enumerate(zip(okeys, pkeys)):
+        assert a.keys() == z.keys(), i
+        for k in a:
+            assert a[k] == z[k], (i, k)
+    assert prows == orows
+    return b
+
+
+@pytest.mark.parametrize("config,indel,n_samples,n_regions", [(2, 0, 150, 16), (3, 0, 60, 6), (5, 30, 80, 10)])
+def test_synthetic_regions_vs_oracle(tmp_path, config, indel, n_samples, n_regions):
+    ps, _ = synth_patterns(tmp_path, 12 if config != 3 else 40, config, 100 + config, thr=1e-3)
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
+    regions = make_regions_synth(7 + config, 0, n_regions, n_samples, ps.max_length, indel)
+    b = _compare(ps, n_samples, beds, regions)
+    assert b.num_haplotypes > n_regions
+
+
+def test_multi_bed_duplicate_and_nested_inner_peaks(tmp_path):
+    """Several bed sources, duplicate ranges (double count), a range that is never selected
+    (strictly inside a 3-way merge, bed.rs:77/89), empty ranges, Ns in the reference."""
+    ps, _ = synth_patterns(tmp_path, 8, 2, 55, thr=2e-3)
+    n = 40
+    base = T.SynthRegion(3, 1, n, ps.max_length)
+    ref = list(base.ref)
+    for i in range(30, 36):
+        ref[i] = "N"
+    ref = "".join(ref)
+    s0 = base.merged[0]
+    beds = [("a.bed", [(s0, s0 + 80), (s0 + 80, s0 + 120), (s0, s0 + 80)]),
+            ("b.bed", [(s0 + 120, s0 + 200), (s0 + 90, s0 + 100), (s0 + 130, s0 + 129)]),
+            ("c.bed", [(s0 + 60, s0 + 70)])]
+    merged = O.merge_ranges([r for _, rs in beds for r in rs])
+    assert merged[0] == (s0, s0 + 200)
+    recs = [("car", p, r, a, c) for p, r, a, c in base.records if not (base.ext_start + 30 <= p < base.ext_start + 36)]
+    regions = [{"merged": merged[0], "ref": ref, "records": recs}]
+    _compare(ps, n, beds, regions)
+
+
+def test_gt_decoding_and_reference_collisions(tmp_path):
+    """Raw GT ints (unphased/phased/missing), multi-allelic records, a REF allele
+    longer than the window, and two groups that patch to the same sequence."""
+    ps, _ = synth_patterns(tmp_path, 6, 2, 77, thr=5e-3)
+    rnd = random.Random(4)
+    n = 30
+    base = T.SynthRegion(5, 2, n, ps.max_length)
+    es = base.ext_start
+    ref = base.ref
+    recs = []
+    VE = -2147483647
+    gt_choices = [(4, 3), (2, 5), (4, 5), (4, 4), (5, 5), (2, 3), (0, 1), (2, 2)]
+    for k, (off, alt) in enumerate([(20, None), (40, None), (41, None), (60, None)]):
+        p = es + off
+        r0 = ref[off]
+        a = rnd.choice([c for c in "ACGT" if c != r0])
+        gts = [list(rnd.choice(gt_choices)) for _ in range(n)]
+        recs.append(("gt", p, 2, r0, a, gts))
+    # multi-allelic: counted as a variant, no diffs
+    recs.append(("gt", es + 50, 3, ref[50], "A", [[VE, VE]] * n))
+    # a deletion starting before the window (filtered by patch_haplotype, haplotype.rs:95)
+    recs.append(("gt", es - 2, 2, "AC", "A", [[4, 3]] * 5 + [[2, 3]] * (n - 5)))
+    # the same SNV twice at one position: groups {d} and {d, d} differ but ...
+    r0 = ref[80]
+    a = "A" if r0 != "A" else "C"
+    recs.append(("gt", es + 80, 2, r0, a, [[4, 3]] * 10 + [[2, 3]] * (n - 10)))
+    recs.append(("gt", es + 80, 2, r0, a, [[4, 3]] * 3 + [[2, 3]] * (n - 3)))
+    regions = [{"merged": base.merged, "ref": ref, "records": recs}]
+    beds = [("x.bed", [base.merged])]
+    _compare(ps, n, beds, regions)
+
+
+def test_min_maf_filter(tmp_path):
+    ps, _ = synth_patterns(tmp_path, 10, 2, 8, thr=1e-3)
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(6)])]
+    regions = make_regions_synth(21, 0, 6, 100, ps.max_length)
+    _compare(ps, 100, beds, regions, min_maf=3)
+
+
+def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
+    """Size-independent property at a larger size: counts do not depend on the LDS
+    tile size or on haplotypes-per-workgroup (the kernels' only tunables)."""
+    ps, _ = synth_patterns(tmp_path, 60, 3, 9)
+    b = T.RegionBatch(ps, 2000)
+    b.synth_fill(13, 0, 200)
+    res = []
+    for tb, hpb in [("32", "64"), ("8", "4"), ("64", "16")]:
+        monkeypatch.setenv("TFBS_TILE_BLOCKS", tb)
+        monkeypatch.setenv("TFBS_HAPS_PER_BLOCK", hpb)
+        sc = T.Scanner(ps)
+        b.scan(sc)
+        res.append([b.keys(r) for r in (0, 57, 199)])
+        sc.close()
+    assert res[0] == res[1] == res[2]
