@@ -308,6 +308,8 @@ class RegionBatch:
 
     def synth_fill(self, seed, first, count, indel_pct=0):
         check(lib().tfbs_synth_fill_batch(self.h, seed, first, count, indel_pct))
+        if "synthetic.bed" not in self.beds:  # registered by the library on first use
+            self.beds.append("synthetic.bed")
 
     @property
     def num_regions(self):
