@@ -11,12 +11,13 @@
 // Design (DESIGN.md has the numbers):
 //  * Haplotypes are packed 2 bits/base (16 bases per u32).  A lane owns one
 //    window start i and funnel-shifts a 64-bit image of bases i..i+31 out of
-//    three words, once per haplotype, into eight 4-mer codes.
-//  * Each PWM strand of length L <= 32 is a list of ceil(L/4) 4-mer lookup
-//    tables (256 int32 each; entry = sum of the 4 column weights, i32 wrap).
-//    A workgroup stages one tile of tables (several pattern_ids, both strands)
-//    in LDS and every wave scores its haplotypes against the whole tile: one
-//    LDS read + two VALU adds per 4 columns per window.
+//    three words, once per (haplotype, tile), into eight 4-mer codes.
+//  * Each PWM strand of length L <= 32 is ceil(L/4) 4-mer lookup tables (entry
+//    = sum of the 4 column weights, i32 wrap).  Four strands of similar length
+//    form a quad whose tables are interleaved, so ONE ds_read_b128 per 4-mer
+//    returns the four strands' partial sums (16 columns of work per LDS read).
+//  * A 512-thread workgroup stages one tile of quads (whole pattern_id groups,
+//    both strands) in LDS; each of its 8 waves scores haplotypes against it.
 //  * N (weight 0 in every column, types.rs:110) packs as A; haplotypes that
 //    contain an N carry a bit mask and subtract w[j][A] for each N column.
 //  * Hits are rare (p ~ 1e-4): a ballot of the threshold compare gates the
@@ -47,9 +48,9 @@ using namespace tfbs;
 
 namespace {
 
-constexpr int kBlock = 256;     // 4 waves
-constexpr int kWaves = kBlock / 64;
-constexpr int kChunks = 4;      // 64-window chunks per lane group (256 windows per pass)
+constexpr int kFastBlock = 512;  // 8 waves share one LDS tile
+constexpr int kGenBlock = 256;
+constexpr int kChunks = 4;       // 64-window chunks per lane group (256 windows per pass)
 
 struct Inner {
     int32_t s;
@@ -59,7 +60,8 @@ struct Inner {
 // Count, for every inner range of this pass, the hit windows whose match range
 // overlaps it (main.rs:503 with Range::overlaps, range.rs:18-21), and add the
 // counts to the lane that owns the pattern_id slot.
-__device__ __forceinline__ void count_hits(const uint64_t (&hit)[kChunks], const int32_t (&pos)[kChunks], uint32_t L,
+template <int NCH>
+__device__ __forceinline__ void count_hits(const uint64_t (&hit)[NCH], const int32_t (&pos)[NCH], uint32_t L,
                                            const Inner *in, uint32_t n_pass, uint32_t slot, uint32_t lane,
                                            uint32_t (&acc)[kMaxInnerPass]) {
 #pragma unroll
@@ -69,7 +71,7 @@ __device__ __forceinline__ void count_hits(const uint64_t (&hit)[kChunks], const
         const uint32_t span = in[kk].span;
         uint32_t cnt = 0;
 #pragma unroll
-        for (int c = 0; c < kChunks; c++) {
+        for (int c = 0; c < NCH; c++) {
             if (!hit[c]) continue;
             const bool ov = (uint32_t)(pos[c] - s) <= span || (uint32_t)(pos[c] + (int32_t)L - 1 - s) <= span;
             cnt += __popcll(hit[c] & __ballot(ov));
@@ -78,46 +80,159 @@ __device__ __forceinline__ void count_hits(const uint64_t (&hit)[kChunks], const
     }
 }
 
+__device__ __forceinline__ uint32_t comp(const uint4 &v, int s) {
+    return s == 0 ? v.x : s == 1 ? v.y : s == 2 ? v.z : v.w;
+}
+
+struct ScanArgs {
+    const DevTile *tiles;
+    uint32_t n_tiles;
+    const DevQuad *quads;
+    const int32_t *lut;
+    const int32_t *colA;
+    const DevHap *haps;
+    uint32_t n_haps;
+    const DevRegion *regions;
+    const int32_t *inner;
+    const uint32_t *words;
+    const uint32_t *nmask;
+    const int32_t *posrel;
+    uint32_t *counts;
+    uint32_t haps_per_block;
+    unsigned long long *hits;  // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
+    uint32_t hits_wpp;
+    uint32_t n_patterns_total;
+};
+
+// Score NCH 64-window chunks starting at window cg against every quad of the tile.
+template <int NCH>
+__device__ __forceinline__ void scan_chunks(const ScanArgs &A, const DevTile &t, const char *s_lut,
+                                            const int32_t *s_col, const DevHap &hm, uint32_t h, uint32_t cg,
+                                            const Inner *in, uint32_t n_pass, bool write_hits, uint32_t lane,
+                                            uint32_t (&acc)[kMaxInnerPass]) {
+    const bool has_n = (hm.flags & HAP_HAS_N) != 0;
+    const bool has_pos = (hm.flags & HAP_HAS_POS) != 0;
+    uint32_t code16[NCH][8];  // byte offsets of the eight 4-mer codes in a quad-block (code * 16)
+    int32_t rem[NCH], pos[NCH];
+    uint32_t nm[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        const uint32_t i = cg + 64 * c + lane;
+        const uint32_t ic = min(i, hm.len);  // keep reads inside the +3 word pad
+        const uint32_t *w = A.words + hm.word_off + (ic >> 4);
+        const uint32_t sh = 2 * (ic & 15);
+        const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+        const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
+        const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            code16[c][b] = ((lo >> (8 * b)) & 0xFFu) << 4;
+            code16[c][b + 4] = ((hi >> (8 * b)) & 0xFFu) << 4;
+        }
+        rem[c] = (int32_t)hm.len - (int32_t)i;
+        pos[c] = has_pos ? (i < hm.len ? A.posrel[hm.pos_off + i] : 0) : (int32_t)i;
+        if (has_n) {
+            const uint32_t *m = A.nmask + hm.nmask_off + (ic >> 5);
+            nm[c] = __builtin_amdgcn_alignbit(m[1], m[0], ic & 31);
+        } else {
+            nm[c] = 0;
+        }
+    }
+    for (uint32_t qi = t.first; qi < t.last; qi++) {
+        const DevQuad &Q = A.quads[qi];
+        const char *base = s_lut + (size_t)Q.lut_off * (kQuadBlockInts * 4);
+        uint4 sc[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) sc[c] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            if (b >= Q.nblk) break;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(base + b * (kQuadBlockInts * 4) + code16[c][b]);
+                sc[c].x += v.x;
+                sc[c].y += v.y;
+                sc[c].z += v.z;
+                sc[c].w += v.w;
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < kQuad; s++) {
+            if (s >= Q.nstrand) break;
+            const uint32_t L = Q.len[s];
+            int32_t score[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) score[c] = (int32_t)comp(sc[c], s);
+            if (has_n) {
+                const uint32_t lmask = L >= 32 ? 0xFFFFFFFFu : ((1u << L) - 1u);
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    uint32_t m = nm[c] & lmask;
+                    while (m) {
+                        const uint32_t j = __builtin_ctz(m);
+                        score[c] = (int32_t)((uint32_t)score[c] - (uint32_t)s_col[Q.col_off[s] + j]);
+                        m &= m - 1;
+                    }
+                }
+            }
+            uint64_t hit[NCH];
+            uint64_t any = 0;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                hit[c] = __ballot(score[c] > Q.min_score[s] && rem[c] >= (int32_t)L);
+                any |= hit[c];
+            }
+            if (write_hits && lane == 0) {
+#pragma unroll
+                for (int c = 0; c < NCH; c++) {
+                    const uint32_t wi = cg / 64 + c;
+                    if (wi < A.hits_wpp)
+                        A.hits[((size_t)h * A.n_patterns_total + Q.orig_index[s]) * A.hits_wpp + wi] = hit[c];
+                }
+            }
+            if (any) count_hits<NCH>(hit, pos, L, in, n_pass, Q.slot_local[s], lane, acc);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
-// Fast kernel: PWM strands of length <= 32 via 4-mer LUTs staged in LDS.
-// Grid: n_tiles x ceil(n_haps / haps_per_block); block 256 threads.
+// Fast kernel: PWM strands of length <= 32 via interleaved 4-mer LUTs in LDS.
+// Grid: n_tiles x ceil(n_haps / haps_per_block); block 512 threads.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void scan_fast_kernel(
-    const DevTile *__restrict__ tiles, uint32_t n_tiles, const DevPattern *__restrict__ pats,
-    const int32_t *__restrict__ lut, const int32_t *__restrict__ colA, const DevHap *__restrict__ haps,
-    uint32_t n_haps, const DevRegion *__restrict__ regions, const int32_t *__restrict__ inner,
-    const uint32_t *__restrict__ words, const uint32_t *__restrict__ nmask, const int32_t *__restrict__ posrel,
-    uint32_t *__restrict__ counts, uint32_t haps_per_block, unsigned long long *__restrict__ hits,
-    uint32_t hits_wpp, uint32_t n_patterns_total) {
+// MINW = minimum waves per SIMD (the register budget: 2 -> up to 256 VGPRs, one
+// workgroup per CU; 4 -> 128 VGPRs, two workgroups per CU).
+template <int MINW>
+__global__ __launch_bounds__(kFastBlock, MINW) void scan_fast_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) int32_t smem[];
-    const uint32_t tile_idx = blockIdx.x % n_tiles;
-    const uint32_t hg = blockIdx.x / n_tiles;
-    const DevTile t = tiles[tile_idx];
+    const uint32_t tile_idx = blockIdx.x % A.n_tiles;
+    const uint32_t hg = blockIdx.x / A.n_tiles;
+    const DevTile t = A.tiles[tile_idx];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
+    constexpr uint32_t kWaves = kFastBlock / 64;
 
-    // stage the tile's LUT blocks and A columns (16-byte loads)
+    // stage the tile's quad-blocks and A columns (16-byte loads)
     {
-        const int4 *src = reinterpret_cast<const int4 *>(lut + (size_t)t.lut_begin * kLutEntries);
-        int4 *dst = reinterpret_cast<int4 *>(smem);
-        const uint32_t n4 = t.nblocks * (kLutEntries / 4);
-        for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
-        int32_t *scol = smem + t.nblocks * kLutEntries;
-        for (uint32_t i = threadIdx.x; i < t.ncols; i += kBlock) scol[i] = colA[t.col_begin + i];
+        const uint4 *src = reinterpret_cast<const uint4 *>(A.lut + (size_t)t.lut_begin * kQuadBlockInts);
+        uint4 *dst = reinterpret_cast<uint4 *>(smem);
+        const uint32_t n4 = t.nblocks * (kQuadBlockInts / 4);
+        for (uint32_t i = threadIdx.x; i < n4; i += kFastBlock) dst[i] = src[i];
+        int32_t *scol = smem + t.nblocks * kQuadBlockInts;
+        for (uint32_t i = threadIdx.x; i < t.ncols; i += kFastBlock) scol[i] = A.colA[t.col_begin + i];
     }
     __syncthreads();
     const char *s_lut = reinterpret_cast<const char *>(smem);
-    const int32_t *s_col = smem + t.nblocks * kLutEntries;
+    const int32_t *s_col = smem + t.nblocks * kQuadBlockInts;
 
-    for (uint32_t hh = wave; hh < haps_per_block; hh += kWaves) {
-        const uint32_t h = hg * haps_per_block + hh;
-        if (h >= n_haps) break;
-        const DevHap hm = haps[h];
-        const DevRegion rg = regions[hm.region];
+    for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
+        const uint32_t h = hg * A.haps_per_block + hh;
+        if (h >= A.n_haps) break;
+        const DevHap hm = A.haps[h];
+        const DevRegion rg = A.regions[hm.region];
         const uint32_t n_inner = rg.n_inner;
-        const bool has_n = (hm.flags & HAP_HAS_N) != 0;
-        const bool has_pos = (hm.flags & HAP_HAS_POS) != 0;
-        const uint32_t n_passes = n_inner == 0 ? (hits ? 1u : 0u) : (n_inner + kMaxInnerPass - 1) / kMaxInnerPass;
+        const uint32_t nwin = hm.len >= t.lmin ? hm.len - t.lmin + 1 : 0;
+        const uint32_t n_passes =
+            n_inner == 0 ? (A.hits ? 1u : 0u) : (n_inner + kMaxInnerPass - 1) / kMaxInnerPass;
         for (uint32_t pass = 0; pass < n_passes; pass++) {
             const uint32_t k0 = pass * kMaxInnerPass;
             const uint32_t n_pass = n_inner > k0 ? min((uint32_t)kMaxInnerPass, n_inner - k0) : 0u;
@@ -125,8 +240,8 @@ __global__ __launch_bounds__(kBlock) void scan_fast_kernel(
 #pragma unroll
             for (int kk = 0; kk < kMaxInnerPass; kk++) {
                 if ((uint32_t)kk < n_pass) {
-                    const int32_t s = inner[2 * (rg.inner_off + k0 + kk)];
-                    const int32_t e = inner[2 * (rg.inner_off + k0 + kk) + 1];
+                    const int32_t s = A.inner[2 * (rg.inner_off + k0 + kk)];
+                    const int32_t e = A.inner[2 * (rg.inner_off + k0 + kk) + 1];
                     in[kk].s = s;
                     in[kk].span = (uint32_t)(e - s);
                 } else {
@@ -137,81 +252,18 @@ __global__ __launch_bounds__(kBlock) void scan_fast_kernel(
             uint32_t acc[kMaxInnerPass];
 #pragma unroll
             for (int kk = 0; kk < kMaxInnerPass; kk++) acc[kk] = 0;
-
-            for (uint32_t cg = 0; cg < hm.len; cg += 64 * kChunks) {
-                uint32_t code4[kChunks][8];  // byte offsets of the 8 4-mer codes (code * 4)
-                int32_t rem[kChunks], pos[kChunks];
-                uint32_t nm[kChunks];
-#pragma unroll
-                for (int c = 0; c < kChunks; c++) {
-                    const uint32_t i = cg + 64 * c + lane;
-                    const uint32_t ic = min(i, hm.len);  // keep reads inside the +3 word pad
-                    const uint32_t *w = words + hm.word_off + (ic >> 4);
-                    const uint32_t sh = 2 * (ic & 15);
-                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-                    const uint32_t lo = __builtin_amdgcn_alignbit(w1, w0, sh);
-                    const uint32_t hi = __builtin_amdgcn_alignbit(w2, w1, sh);
-#pragma unroll
-                    for (int b = 0; b < 4; b++) {
-                        code4[c][b] = ((lo >> (8 * b)) & 0xFFu) << 2;
-                        code4[c][b + 4] = ((hi >> (8 * b)) & 0xFFu) << 2;
-                    }
-                    rem[c] = (int32_t)hm.len - (int32_t)i;
-                    pos[c] = has_pos ? (i < hm.len ? posrel[hm.pos_off + i] : 0) : (int32_t)i;
-                    if (has_n) {
-                        const uint32_t *m = nmask + hm.nmask_off + (ic >> 5);
-                        nm[c] = __builtin_amdgcn_alignbit(m[1], m[0], ic & 31);
-                    } else {
-                        nm[c] = 0;
-                    }
-                }
-                for (uint32_t pi = t.pat_begin; pi < t.pat_end; pi++) {
-                    const DevPattern p = pats[pi];
-                    const char *base = s_lut + (size_t)p.lut_off * (kLutEntries * 4);
-                    int32_t sc[kChunks];
-#pragma unroll
-                    for (int c = 0; c < kChunks; c++) sc[c] = 0;
-#pragma unroll
-                    for (int b = 0; b < 8; b++) {
-                        if (b >= p.nblk) break;
-#pragma unroll
-                        for (int c = 0; c < kChunks; c++)
-                            sc[c] = (int32_t)((uint32_t)sc[c] +
-                                              (uint32_t)*reinterpret_cast<const int32_t *>(
-                                                  base + b * (kLutEntries * 4) + code4[c][b]));
-                    }
-                    if (has_n) {
-                        const uint32_t lmask = p.len >= 32 ? 0xFFFFFFFFu : ((1u << p.len) - 1u);
-#pragma unroll
-                        for (int c = 0; c < kChunks; c++) {
-                            uint32_t m = nm[c] & lmask;
-                            while (m) {
-                                const uint32_t j = __builtin_ctz(m);
-                                sc[c] = (int32_t)((uint32_t)sc[c] - (uint32_t)s_col[p.col_off + j]);
-                                m &= m - 1;
-                            }
-                        }
-                    }
-                    uint64_t hit[kChunks];
-                    uint64_t any = 0;
-#pragma unroll
-                    for (int c = 0; c < kChunks; c++) {
-                        hit[c] = __ballot(sc[c] > p.min_score && rem[c] >= (int32_t)p.len);
-                        any |= hit[c];
-                    }
-                    if (hits && pass == 0 && lane == 0) {
-#pragma unroll
-                        for (int c = 0; c < kChunks; c++) {
-                            const uint32_t wi = cg / 64 + c;
-                            if (wi < hits_wpp)
-                                hits[((size_t)h * n_patterns_total + p.orig_index) * hits_wpp + wi] = hit[c];
-                        }
-                    }
-                    if (any) count_hits(hit, pos, p.len, in, n_pass, p.slot_local, lane, acc);
-                }
+            const bool write_hits = A.hits != nullptr && pass == 0;
+            for (uint32_t cg = 0; cg < nwin; cg += 64 * kChunks) {
+                const uint32_t nch = min((uint32_t)kChunks, (nwin - cg + 63) / 64);
+                if (nch >= 3)  // a 3-chunk tail scores one chunk of invalid windows (rem < L)
+                    scan_chunks<4>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
+                else if (nch == 2)
+                    scan_chunks<2>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
+                else
+                    scan_chunks<1>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
             }
             if (n_pass && lane < t.nslots) {
-                uint32_t *out = counts + hm.count_off + (size_t)(t.slot_begin + lane) * n_inner + k0;
+                uint32_t *out = A.counts + hm.count_off + (size_t)(t.slot_begin + lane) * n_inner + k0;
 #pragma unroll
                 for (int kk = 0; kk < kMaxInnerPass; kk++)
                     if ((uint32_t)kk < n_pass) out[kk] = acc[kk];
@@ -225,34 +277,50 @@ __global__ __launch_bounds__(kBlock) void scan_fast_kernel(
 // 32 columns; column-wise scoring with weights read through the cache.
 // Grid: n_gen_tiles x ceil(n_haps / haps_per_block).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void scan_generic_kernel(
-    const DevTile *__restrict__ tiles, uint32_t n_tiles, const DevPattern *__restrict__ pats,
-    const int32_t *__restrict__ gw, const DevHap *__restrict__ haps, uint32_t n_haps,
-    const DevRegion *__restrict__ regions, const int32_t *__restrict__ inner, const uint32_t *__restrict__ words,
-    const uint32_t *__restrict__ nmask, const int32_t *__restrict__ posrel, uint32_t *__restrict__ counts,
-    uint32_t haps_per_block, unsigned long long *__restrict__ hits, uint32_t hits_wpp, uint32_t n_patterns_total) {
-    const uint32_t tile_idx = blockIdx.x % n_tiles;
-    const uint32_t hg = blockIdx.x / n_tiles;
-    const DevTile t = tiles[tile_idx];
+struct GenArgs {
+    const DevTile *tiles;
+    uint32_t n_tiles;
+    const DevPattern *pats;
+    const int32_t *gw;
+    const DevHap *haps;
+    uint32_t n_haps;
+    const DevRegion *regions;
+    const int32_t *inner;
+    const uint32_t *words;
+    const uint32_t *nmask;
+    const int32_t *posrel;
+    uint32_t *counts;
+    uint32_t haps_per_block;
+    unsigned long long *hits;
+    uint32_t hits_wpp;
+    uint32_t n_patterns_total;
+};
+
+__global__ __launch_bounds__(kGenBlock) void scan_generic_kernel(GenArgs A) {
+    const uint32_t tile_idx = blockIdx.x % A.n_tiles;
+    const uint32_t hg = blockIdx.x / A.n_tiles;
+    const DevTile t = A.tiles[tile_idx];
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = threadIdx.x >> 6;
-    for (uint32_t hh = wave; hh < haps_per_block; hh += kWaves) {
-        const uint32_t h = hg * haps_per_block + hh;
-        if (h >= n_haps) break;
-        const DevHap hm = haps[h];
-        const DevRegion rg = regions[hm.region];
+    constexpr uint32_t kWaves = kGenBlock / 64;
+    for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
+        const uint32_t h = hg * A.haps_per_block + hh;
+        if (h >= A.n_haps) break;
+        const DevHap hm = A.haps[h];
+        const DevRegion rg = A.regions[hm.region];
         const uint32_t n_inner = rg.n_inner;
         const bool has_n = (hm.flags & HAP_HAS_N) != 0;
         const bool has_pos = (hm.flags & HAP_HAS_POS) != 0;
-        const uint32_t n_passes = n_inner == 0 ? (hits ? 1u : 0u) : (n_inner + kMaxInnerPass - 1) / kMaxInnerPass;
+        const uint32_t n_passes =
+            n_inner == 0 ? (A.hits ? 1u : 0u) : (n_inner + kMaxInnerPass - 1) / kMaxInnerPass;
         for (uint32_t pass = 0; pass < n_passes; pass++) {
             const uint32_t k0 = pass * kMaxInnerPass;
             const uint32_t n_pass = n_inner > k0 ? min((uint32_t)kMaxInnerPass, n_inner - k0) : 0u;
             Inner in[kMaxInnerPass];
             for (int kk = 0; kk < kMaxInnerPass; kk++) {
                 if ((uint32_t)kk < n_pass) {
-                    in[kk].s = inner[2 * (rg.inner_off + k0 + kk)];
-                    in[kk].span = (uint32_t)(inner[2 * (rg.inner_off + k0 + kk) + 1] - in[kk].s);
+                    in[kk].s = A.inner[2 * (rg.inner_off + k0 + kk)];
+                    in[kk].span = (uint32_t)(A.inner[2 * (rg.inner_off + k0 + kk) + 1] - in[kk].s);
                 } else {
                     in[kk].s = 0;
                     in[kk].span = 0;
@@ -266,10 +334,10 @@ __global__ __launch_bounds__(kBlock) void scan_generic_kernel(
                 for (int c = 0; c < kChunks; c++) {
                     const uint32_t i = cg + 64 * c + lane;
                     rem[c] = (int32_t)hm.len - (int32_t)i;
-                    pos[c] = has_pos ? (i < hm.len ? posrel[hm.pos_off + i] : 0) : (int32_t)i;
+                    pos[c] = has_pos ? (i < hm.len ? A.posrel[hm.pos_off + i] : 0) : (int32_t)i;
                 }
-                for (uint32_t pi = t.pat_begin; pi < t.pat_end; pi++) {
-                    const DevPattern p = pats[pi];
+                for (uint32_t pi = t.first; pi < t.last; pi++) {
+                    const DevPattern p = A.pats[pi];
                     uint64_t hit[kChunks];
                     uint64_t any = 0;
 #pragma unroll
@@ -280,26 +348,26 @@ __global__ __launch_bounds__(kBlock) void scan_generic_kernel(
                         if (valid) {
                             for (uint32_t j = 0; j < p.len; j++) {
                                 const uint32_t q = i + j;
-                                uint32_t code = (words[hm.word_off + (q >> 4)] >> (2 * (q & 15))) & 3u;
-                                if (has_n && ((nmask[hm.nmask_off + (q >> 5)] >> (q & 31)) & 1u)) code = 4;
-                                sc += (uint32_t)gw[(size_t)(p.col_off + j) * 5 + code];
+                                uint32_t code = (A.words[hm.word_off + (q >> 4)] >> (2 * (q & 15))) & 3u;
+                                if (has_n && ((A.nmask[hm.nmask_off + (q >> 5)] >> (q & 31)) & 1u)) code = 4;
+                                sc += (uint32_t)A.gw[(size_t)(p.col_off + j) * 5 + code];
                             }
                         }
                         hit[c] = __ballot(valid && (int32_t)sc > p.min_score);
                         any |= hit[c];
                     }
-                    if (hits && pass == 0 && lane == 0) {
+                    if (A.hits && pass == 0 && lane == 0) {
                         for (int c = 0; c < kChunks; c++) {
                             const uint32_t wi = cg / 64 + c;
-                            if (wi < hits_wpp)
-                                hits[((size_t)h * n_patterns_total + p.orig_index) * hits_wpp + wi] = hit[c];
+                            if (wi < A.hits_wpp)
+                                A.hits[((size_t)h * A.n_patterns_total + p.orig_index) * A.hits_wpp + wi] = hit[c];
                         }
                     }
-                    if (any) count_hits(hit, pos, p.len, in, n_pass, p.slot_local, lane, acc);
+                    if (any) count_hits<kChunks>(hit, pos, p.len, in, n_pass, p.slot_local, lane, acc);
                 }
             }
             if (n_pass && lane == 0) {
-                uint32_t *out = counts + hm.count_off + (size_t)t.slot_begin * n_inner + k0;
+                uint32_t *out = A.counts + hm.count_off + (size_t)t.slot_begin * n_inner + k0;
                 for (int kk = 0; kk < kMaxInnerPass; kk++)
                     if ((uint32_t)kk < n_pass) out[kk] = acc[kk];
             }
@@ -345,10 +413,12 @@ struct tfbs_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const Patterns *pats = nullptr;
     Plan plan;
-    uint32_t tile_blocks = 32;
+    uint32_t tile_qblocks = 16;   // quad-blocks (4 KiB each) per LDS tile
     uint32_t haps_per_block = 64;
+    int fast_minw = 2;            // scan_fast_kernel<MINW> instantiation
     size_t lds_bytes = 0;
-    DevBuf<DevPattern> fast_pats, gen_pats;
+    DevBuf<DevQuad> fast_quads;
+    DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
     DevBuf<int32_t> lut, colA, gen_w;
     // batch image
@@ -363,9 +433,9 @@ struct tfbs_ctx {
     bool timing_pending = false;
 };
 
-static int env_u32(const char *name, uint32_t dflt) {
+static int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
-    if (!v || !*v) return (int)dflt;
+    if (!v || !*v) return dflt;
     return atoi(v);
 }
 
@@ -383,12 +453,28 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         for (uint64_t g0 = 0; g0 < n_hg; g0 += max_hg) {
             const uint32_t ng = (uint32_t)std::min<uint64_t>(max_hg, n_hg - g0);
             const uint32_t h0 = (uint32_t)(g0 * hpb);
-            const uint32_t nh = std::min<uint32_t>(n_haps - h0, ng * hpb);
-            hipLaunchKernelGGL(scan_fast_kernel, dim3(nt * ng), dim3(kBlock), ctx->lds_bytes, ctx->stream,
-                               ctx->fast_tiles.p, nt, ctx->fast_pats.p, ctx->lut.p, ctx->colA.p, ctx->haps.p + h0, nh,
-                               ctx->regions.p, ctx->inner.p, ctx->words.p, ctx->nmask.p, ctx->posrel.p,
-                               ctx->counts.p, hpb, hits ? hits + (size_t)h0 * n_pat_total * hits_wpp : nullptr,
-                               hits_wpp, n_pat_total);
+            ScanArgs a{};
+            a.tiles = ctx->fast_tiles.p;
+            a.n_tiles = nt;
+            a.quads = ctx->fast_quads.p;
+            a.lut = ctx->lut.p;
+            a.colA = ctx->colA.p;
+            a.haps = ctx->haps.p + h0;
+            a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
+            a.regions = ctx->regions.p;
+            a.inner = ctx->inner.p;
+            a.words = ctx->words.p;
+            a.nmask = ctx->nmask.p;
+            a.posrel = ctx->posrel.p;
+            a.counts = ctx->counts.p;
+            a.haps_per_block = hpb;
+            a.hits = hits ? hits + (size_t)h0 * n_pat_total * hits_wpp : nullptr;
+            a.hits_wpp = hits_wpp;
+            a.n_patterns_total = n_pat_total;
+            if (ctx->fast_minw == 4)
+                hipLaunchKernelGGL(scan_fast_kernel<4>, dim3(nt * ng), dim3(kFastBlock), ctx->lds_bytes, ctx->stream, a);
+            else
+                hipLaunchKernelGGL(scan_fast_kernel<2>, dim3(nt * ng), dim3(kFastBlock), ctx->lds_bytes, ctx->stream, a);
             launches++;
         }
     }
@@ -398,11 +484,24 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         for (uint64_t g0 = 0; g0 < n_hg; g0 += max_hg) {
             const uint32_t ng = (uint32_t)std::min<uint64_t>(max_hg, n_hg - g0);
             const uint32_t h0 = (uint32_t)(g0 * hpb);
-            const uint32_t nh = std::min<uint32_t>(n_haps - h0, ng * hpb);
-            hipLaunchKernelGGL(scan_generic_kernel, dim3(nt * ng), dim3(kBlock), 0, ctx->stream, ctx->gen_tiles.p, nt,
-                               ctx->gen_pats.p, ctx->gen_w.p, ctx->haps.p + h0, nh, ctx->regions.p, ctx->inner.p,
-                               ctx->words.p, ctx->nmask.p, ctx->posrel.p, ctx->counts.p, hpb,
-                               hits ? hits + (size_t)h0 * n_pat_total * hits_wpp : nullptr, hits_wpp, n_pat_total);
+            GenArgs a{};
+            a.tiles = ctx->gen_tiles.p;
+            a.n_tiles = nt;
+            a.pats = ctx->gen_pats.p;
+            a.gw = ctx->gen_w.p;
+            a.haps = ctx->haps.p + h0;
+            a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
+            a.regions = ctx->regions.p;
+            a.inner = ctx->inner.p;
+            a.words = ctx->words.p;
+            a.nmask = ctx->nmask.p;
+            a.posrel = ctx->posrel.p;
+            a.counts = ctx->counts.p;
+            a.haps_per_block = hpb;
+            a.hits = hits ? hits + (size_t)h0 * n_pat_total * hits_wpp : nullptr;
+            a.hits_wpp = hits_wpp;
+            a.n_patterns_total = n_pat_total;
+            hipLaunchKernelGGL(scan_generic_kernel, dim3(nt * ng), dim3(kGenBlock), 0, ctx->stream, a);
             launches++;
         }
     }
@@ -428,7 +527,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    ctx->fast_pats.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
+    ctx->fast_quads.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->colA.release(); ctx->gen_w.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
@@ -447,10 +546,18 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     auto *ctx = new tfbs_ctx();
     ctx->device = device;
     ctx->pats = &tfbs::patterns_of(p);
-    ctx->tile_blocks = (uint32_t)std::max(8, env_u32("TFBS_TILE_BLOCKS", 32));
-    ctx->haps_per_block = (uint32_t)std::max(4, env_u32("TFBS_HAPS_PER_BLOCK", 64));
-    rc = ctx->pats->build_plan(ctx->tile_blocks, &ctx->plan);
-    if (rc) { delete ctx; return rc; }
+    ctx->tile_qblocks = (uint32_t)std::min(36, std::max(8, env_int("TFBS_TILE_QBLOCKS", 16)));
+    ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 64));
+    ctx->fast_minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
+    rc = ctx->pats->build_plan(ctx->tile_qblocks, &ctx->plan);
+    if (rc) {
+        delete ctx;
+        return rc;
+    }
+    if (ctx->plan.zero_len_panics) {
+        delete ctx;
+        return tfbs::fail(TFBS_E_ZEROLEN, "length-0 PWM with negative min_score (pattern.rs:150-156)");
+    }
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
@@ -460,16 +567,23 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         return tfbs::fail(TFBS_E_HIP, std::string("HIP init: ") + hipGetErrorString(e));
     }
     const Plan &P = ctx->plan;
-    ctx->lds_bytes = (size_t)P.max_tile_blocks * kLutEntries * 4 + (size_t)P.max_tile_cols * 4 + 16;
+    ctx->lds_bytes = (size_t)P.max_tile_blocks * kQuadBlockInts * 4 + (size_t)P.max_tile_cols * 4 + 16;
+    if (ctx->lds_bytes > 160 * 1024) {
+        tfbs_ctx_destroy(ctx);
+        return tfbs::fail(TFBS_E_ARG, "pattern tile exceeds the 160 KiB LDS");
+    }
     if (ctx->lds_bytes > 64 * 1024) {
-        e = hipFuncSetAttribute((const void *)scan_fast_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        e = hipFuncSetAttribute((const void *)scan_fast_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)ctx->lds_bytes);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void *)scan_fast_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)ctx->lds_bytes);
         if (e != hipSuccess) {
             tfbs_ctx_destroy(ctx);
             return tfbs::fail(TFBS_E_HIP, std::string("LDS attribute: ") + hipGetErrorString(e));
         }
     }
-    if ((rc = ctx->fast_pats.put(P.fast_pats, ctx->stream)) || (rc = ctx->fast_tiles.put(P.fast_tiles, ctx->stream)) ||
+    if ((rc = ctx->fast_quads.put(P.fast_quads, ctx->stream)) || (rc = ctx->fast_tiles.put(P.fast_tiles, ctx->stream)) ||
         (rc = ctx->lut.put(P.lut, ctx->stream)) || (rc = ctx->colA.put(P.colA, ctx->stream)) ||
         (rc = ctx->gen_pats.put(P.gen_pats, ctx->stream)) || (rc = ctx->gen_tiles.put(P.gen_tiles, ctx->stream)) ||
         (rc = ctx->gen_w.put(P.gen_w, ctx->stream))) {
@@ -512,6 +626,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     Batch &B = b->b;
     if (B.pats != ctx->pats) return tfbs::fail(TFBS_E_ARG, "batch and ctx use different pattern sets");
     if (B.open) return tfbs::fail(TFBS_E_STATE, "region still open");
+    if (B.slot_pid != ctx->plan.slot_pid) return tfbs::fail(TFBS_E_STATE, "batch slot order differs from the ctx plan");
     HIP_TRY(hipSetDevice(ctx->device));
     int rc;
     if ((rc = ctx->words.put(B.words, ctx->stream)) || (rc = ctx->nmask.put(B.nmask, ctx->stream)) ||
@@ -562,7 +677,10 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
     for (size_t i = 0; i < n; i++) {
         if (nucs[i] > 4) return tfbs::fail(TFBS_E_BADBASE, "nucleotide code > 4");
         uint32_t c = nucs[i];
-        if (c == 4) { has_n = true; c = 0; }
+        if (c == 4) {
+            has_n = true;
+            c = 0;
+        }
         words[i / 16] |= c << (2 * (i % 16));
     }
     DevHap hm{};

@@ -200,12 +200,18 @@ int parse_pwm_files(const std::string &pwm_file, const std::string &thr_dir, flo
 // ---------------------------------------------------------------------------
 // Device plan
 // ---------------------------------------------------------------------------
-int Patterns::build_plan(uint32_t tile_blocks, Plan *plan) const {
+// Strands are grouped by pattern_id (both strands of a PWM share it and their
+// hits add into one count, main.rs:505).  Groups are ordered by (needs the
+// generic kernel, longest strand, pattern_id) -- this order defines the count
+// slots -- so neighbouring strands have similar lengths and pack into quads
+// with little padding.  Fast tiles are runs of whole groups whose quad-blocks
+// fit the LDS budget and span at most 64 slots.
+int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
     *plan = Plan();
     // Scannable strands: PWM with length >= 1.  A length-0 PWM with a negative
     // min_score panics in the reference at the first region (pattern.rs:150-156
     // reads haplotype[len]); with min_score >= 0 it never matches.
-    std::vector<int> scan_idx;
+    std::map<uint16_t, std::vector<int>> by_pid;
     for (size_t i = 0; i < pats.size(); i++) {
         const Pat &p = pats[i];
         if (p.kind != TFBS_KIND_PWM) continue;
@@ -213,118 +219,149 @@ int Patterns::build_plan(uint32_t tile_blocks, Plan *plan) const {
             if (p.min_score < 0) plan->zero_len_panics = true;
             continue;
         }
-        scan_idx.push_back((int)i);
+        by_pid[p.pattern_id].push_back((int)i);
     }
-    // pattern_id slots (ascending ids)
-    std::vector<uint16_t> ids;
-    for (int i : scan_idx) ids.push_back(pats[i].pattern_id);
-    std::sort(ids.begin(), ids.end());
-    ids.erase(std::unique(ids.begin(), ids.end()), ids.end());
-    plan->slot_pid = ids;
-    std::map<uint16_t, uint32_t> slot_of;
-    for (size_t s = 0; s < ids.size(); s++) slot_of[ids[s]] = (uint32_t)s;
-    // group strands by pattern_id (stable); a group with any strand longer than
-    // the fast path's 32-base window goes to the generic kernel.
-    std::map<uint16_t, std::vector<int>> groups;
-    for (int i : scan_idx) groups[pats[i].pattern_id].push_back(i);
+    if (pats.size() > 65535) return fail(TFBS_E_ARG, "more than 65535 patterns");
+    struct Group { uint16_t pid; bool generic; uint32_t maxlen; std::vector<int> strands; };
+    std::vector<Group> groups;
+    for (auto &kv : by_pid) {
+        Group g{kv.first, false, 0, kv.second};
+        for (int i : g.strands) {
+            g.maxlen = std::max(g.maxlen, pats[i].len);
+            if (pats[i].len > (uint32_t)kFastMaxLen) g.generic = true;
+        }
+        groups.push_back(std::move(g));
+    }
+    std::stable_sort(groups.begin(), groups.end(), [](const Group &a, const Group &b) {
+        if (a.generic != b.generic) return !a.generic;
+        if (a.maxlen != b.maxlen) return a.maxlen < b.maxlen;
+        return a.pid < b.pid;
+    });
+    for (auto &g : groups) plan->slot_pid.push_back(g.pid);
     auto nblk_of = [](uint32_t L) { return (L + 3) / 4; };
 
     // --- fast tiles
-    DevTile cur{};
-    bool open = false;
-    auto close_tile = [&]() {
-        if (open) {
-            cur.pat_end = (uint32_t)plan->fast_pats.size();
-            cur.nblocks = (uint32_t)(plan->lut.size() / kLutEntries) - cur.lut_begin;
-            cur.ncols = (uint32_t)plan->colA.size() - cur.col_begin;
-            plan->fast_tiles.push_back(cur);
-            open = false;
+    // quad-blocks a tile needs when its strands (in order) are cut into quads
+    auto quad_blocks = [&](const std::vector<int> &strands) {
+        uint32_t total = 0;
+        for (size_t q = 0; q < strands.size(); q += kQuad) {
+            uint32_t m = 0;
+            for (size_t s = q; s < std::min(strands.size(), q + kQuad); s++) m = std::max(m, nblk_of(pats[strands[s]].len));
+            total += m;
         }
+        return total;
     };
-    for (auto &g : groups) {
-        bool fast = true;
-        uint32_t gblocks = 0;
-        for (int i : g.second) {
-            if (pats[i].len > (uint32_t)kFastMaxLen) fast = false;
-            gblocks += nblk_of(pats[i].len);
-        }
-        if (!fast) continue;
-        uint32_t slot = slot_of[g.first];
-        if (open) {
-            uint32_t used = (uint32_t)(plan->lut.size() / kLutEntries) - cur.lut_begin;
-            if (used + gblocks > tile_blocks || slot - cur.slot_begin + 1 > (uint32_t)kMaxTileSlots) close_tile();
-        }
-        if (!open) {
-            cur = DevTile{};
-            cur.pat_begin = (uint32_t)plan->fast_pats.size();
-            cur.lut_begin = (uint32_t)(plan->lut.size() / kLutEntries);
-            cur.col_begin = (uint32_t)plan->colA.size();
-            cur.slot_begin = slot;
-            open = true;
-        }
-        cur.nslots = slot - cur.slot_begin + 1;
-        for (int i : g.second) {
-            const Pat &p = pats[i];
-            DevPattern d{};
-            d.lut_off = (uint32_t)(plan->lut.size() / kLutEntries) - cur.lut_begin;
-            d.col_off = (uint32_t)plan->colA.size() - cur.col_begin;
-            d.min_score = p.min_score;
-            d.len = (uint16_t)p.len;
-            d.nblk = (uint16_t)nblk_of(p.len);
-            d.slot_local = (uint16_t)(slot - cur.slot_begin);
-            d.orig_index = (uint16_t)i;
-            plan->fast_pats.push_back(d);
-            // 4-mer LUT: entry[b][code] = sum_{j<4, 4b+j<L} w[4b+j][(code >> 2j) & 3]
-            // (wrapping i32, as the reference's i32 sum in --release).
-            for (uint32_t b = 0; b < d.nblk; b++) {
-                for (int code = 0; code < kLutEntries; code++) {
-                    uint32_t s = 0;
-                    for (uint32_t j = 0; j < 4; j++) {
-                        uint32_t col = 4 * b + j;
-                        if (col >= p.len) break;
-                        s += (uint32_t)p.w5[5 * col + ((code >> (2 * j)) & 3)];
-                    }
-                    plan->lut.push_back((int32_t)s);
+    std::vector<int> cur;                 // strands of the open tile
+    std::vector<uint32_t> cur_slot;       // their global slots
+    uint32_t cur_slot_begin = 0;
+    auto close_tile = [&]() {
+        if (cur.empty()) return;
+        DevTile t{};
+        t.first = (uint32_t)plan->fast_quads.size();
+        t.lut_begin = (uint32_t)(plan->lut.size() / kQuadBlockInts);
+        t.col_begin = (uint32_t)plan->colA.size();
+        t.slot_begin = cur_slot_begin;
+        t.lmin = UINT32_MAX;
+        uint32_t maxslot = 0;
+        for (size_t q0 = 0; q0 < cur.size(); q0 += kQuad) {
+            DevQuad Q{};
+            Q.lut_off = (uint32_t)(plan->lut.size() / kQuadBlockInts) - t.lut_begin;
+            const size_t n = std::min<size_t>(kQuad, cur.size() - q0);
+            Q.nstrand = (uint16_t)n;
+            for (size_t s = 0; s < kQuad; s++) {
+                if (s < n) {
+                    const Pat &p = pats[cur[q0 + s]];
+                    Q.nblk = (uint16_t)std::max<uint32_t>(Q.nblk, nblk_of(p.len));
+                    Q.min_score[s] = p.min_score;
+                    Q.len[s] = (uint16_t)p.len;
+                    Q.slot_local[s] = (uint16_t)(cur_slot[q0 + s] - cur_slot_begin);
+                    Q.orig_index[s] = (uint16_t)cur[q0 + s];
+                    Q.col_off[s] = (uint32_t)plan->colA.size() - t.col_begin;
+                    for (uint32_t j = 0; j < p.len; j++) plan->colA.push_back(p.w5[5 * j + 0]);
+                    t.lmin = std::min<uint32_t>(t.lmin, p.len);
+                    maxslot = std::max(maxslot, cur_slot[q0 + s]);
+                } else {  // padding strand: never matches
+                    Q.min_score[s] = INT32_MAX;
+                    Q.len[s] = 0;
+                    Q.slot_local[s] = 0;
+                    Q.orig_index[s] = 0xFFFF;
+                    Q.col_off[s] = 0;
                 }
             }
-            for (uint32_t j = 0; j < p.len; j++) plan->colA.push_back(p.w5[5 * j + 0]);
+            // interleaved 4-mer tables: entry[b][code][s] = sum_{j<4, 4b+j<L_s} w_s[4b+j][(code >> 2j) & 3]
+            // (i32 wrapping, as the reference's i32 sum in --release)
+            for (uint32_t b = 0; b < Q.nblk; b++) {
+                for (int code = 0; code < kLutEntries; code++) {
+                    for (size_t s = 0; s < kQuad; s++) {
+                        uint32_t v = 0;
+                        if (s < n) {
+                            const Pat &p = pats[cur[q0 + s]];
+                            for (uint32_t j = 0; j < 4; j++) {
+                                const uint32_t col = 4 * b + j;
+                                if (col >= p.len) break;
+                                v += (uint32_t)p.w5[5 * col + ((code >> (2 * j)) & 3)];
+                            }
+                        }
+                        plan->lut.push_back((int32_t)v);
+                    }
+                }
+            }
+            plan->fast_quads.push_back(Q);
+        }
+        t.last = (uint32_t)plan->fast_quads.size();
+        t.nblocks = (uint32_t)(plan->lut.size() / kQuadBlockInts) - t.lut_begin;
+        t.ncols = (uint32_t)plan->colA.size() - t.col_begin;
+        t.nslots = maxslot - cur_slot_begin + 1;
+        plan->fast_tiles.push_back(t);
+        cur.clear();
+        cur_slot.clear();
+    };
+    for (uint32_t gi = 0; gi < groups.size(); gi++) {
+        const Group &g = groups[gi];
+        if (g.generic) continue;
+        if (!cur.empty()) {
+            std::vector<int> trial = cur;
+            trial.insert(trial.end(), g.strands.begin(), g.strands.end());
+            if (quad_blocks(trial) > tile_quad_blocks || gi - cur_slot_begin + 1 > (uint32_t)kMaxTileSlots)
+                close_tile();
+        }
+        if (cur.empty()) cur_slot_begin = gi;
+        for (int i : g.strands) {
+            cur.push_back(i);
+            cur_slot.push_back(gi);
         }
     }
     close_tile();
-    // --- generic (long) strands: one "tile" per pattern_id group, weights x5
-    for (auto &g : groups) {
-        bool fast = true;
-        for (int i : g.second)
-            if (pats[i].len > (uint32_t)kFastMaxLen) fast = false;
-        if (fast) continue;
+    // --- generic (long) strands: one tile per pattern_id group, weights x5
+    for (uint32_t gi = 0; gi < groups.size(); gi++) {
+        const Group &g = groups[gi];
+        if (!g.generic) continue;
         DevTile t{};
-        t.pat_begin = (uint32_t)plan->gen_pats.size();
-        t.slot_begin = slot_of[g.first];
+        t.first = (uint32_t)plan->gen_pats.size();
+        t.slot_begin = gi;
         t.nslots = 1;
-        for (int i : g.second) {
+        t.lmin = UINT32_MAX;
+        for (int i : g.strands) {
             const Pat &p = pats[i];
+            if (p.len > 65535) return fail(TFBS_E_ARG, "pattern longer than 65535 columns");
             DevPattern d{};
-            d.col_off = (uint32_t)plan->gen_w.size() / 5;
+            d.col_off = (uint32_t)(plan->gen_w.size() / 5);
             d.min_score = p.min_score;
-            d.len = (uint16_t)std::min<uint32_t>(p.len, 65535);
-            d.nblk = 0;
+            d.len = (uint16_t)p.len;
             d.slot_local = 0;
             d.orig_index = (uint16_t)i;
-            if (p.len > 65535) return fail(TFBS_E_ARG, "pattern longer than 65535 columns");
+            t.lmin = std::min<uint32_t>(t.lmin, p.len);
             plan->gen_pats.push_back(d);
             for (uint32_t j = 0; j < p.len; j++)
                 for (int c = 0; c < 5; c++) plan->gen_w.push_back(c == 4 ? 0 : p.w5[5 * j + c]);
         }
-        t.pat_end = (uint32_t)plan->gen_pats.size();
+        t.last = (uint32_t)plan->gen_pats.size();
         plan->gen_tiles.push_back(t);
     }
-    if (pats.size() > 65535) return fail(TFBS_E_ARG, "more than 65535 patterns");
-    uint32_t maxb = 0;
-    for (auto &t : plan->fast_tiles) maxb = std::max(maxb, t.nblocks);
-    uint32_t maxc = 0;
-    for (auto &t : plan->fast_tiles) maxc = std::max(maxc, t.ncols);
-    plan->max_tile_blocks = maxb;
-    plan->max_tile_cols = maxc;
+    for (auto &t : plan->fast_tiles) {
+        plan->max_tile_blocks = std::max(plan->max_tile_blocks, t.nblocks);
+        plan->max_tile_cols = std::max(plan->max_tile_cols, t.ncols);
+    }
     return TFBS_OK;
 }
 

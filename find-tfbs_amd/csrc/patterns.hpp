@@ -22,10 +22,10 @@ struct Pat {  // Pattern (types.rs:86-90)
 
 struct Plan {
     std::vector<uint16_t> slot_pid;  // slot -> pattern_id
-    std::vector<DevPattern> fast_pats;
+    std::vector<DevQuad> fast_quads;
     std::vector<DevTile> fast_tiles;
-    std::vector<int32_t> lut;        // blocks x 256
-    std::vector<int32_t> colA;       // per fast-pattern column: weight of A (N correction)
+    std::vector<int32_t> lut;        // quad-blocks x 256 codes x 4 strands
+    std::vector<int32_t> colA;       // per fast-strand column: weight of A (N correction)
     std::vector<DevPattern> gen_pats;
     std::vector<DevTile> gen_tiles;
     std::vector<int32_t> gen_w;      // per generic column: 5 weights
@@ -39,7 +39,7 @@ struct Patterns {
     std::map<uint16_t, std::string> names;
     void add(const Pat &p);
     uint32_t max_length() const;
-    int build_plan(uint32_t tile_blocks, Plan *plan) const;
+    int build_plan(uint32_t tile_quad_blocks, Plan *plan) const;
 };
 
 int parse_weight(const std::string &s, int32_t *out);

@@ -27,29 +27,44 @@ inline int to_nuc(uint8_t c) {
 // ---------------------------------------------------------------------------
 // Device-side descriptors (POD, shared with the kernels)
 // ---------------------------------------------------------------------------
-constexpr int kLutEntries = 256;   // one 4-mer block: 4^4 entries
+constexpr int kLutEntries = 256;   // one 4-mer block: 4^4 codes
+constexpr int kQuad = 4;           // strands interleaved per LUT entry (one ds_read_b128)
+constexpr int kQuadBlockInts = kLutEntries * kQuad;  // 4 KiB per quad-block
 constexpr int kFastMaxLen = 32;    // the LUT path reads a 64-bit (32-base) window per lane
 constexpr int kMaxInnerPass = 8;   // inner ranges handled per pass (accumulators per lane)
 constexpr int kMaxTileSlots = 64;  // pattern_id slots per tile: one lane each
 
-struct DevPattern {        // one PWM strand, in tile order
-    uint32_t lut_off;      // fast path: block offset inside the tile's LDS image
-    uint32_t col_off;      // offset of this pattern's columns in colA (fast) / weights (generic)
+// Four PWM strands scored together: their 4-mer tables are interleaved so one
+// 16-byte LDS read returns the four strands' partial sums for a code.
+struct DevQuad {
+    uint32_t lut_off;          // quad-block offset inside the tile's LDS image
+    uint16_t nblk;             // max ceil(len / 4) over the strands
+    uint16_t nstrand;          // 1..4 real strands (the rest never match)
+    int32_t min_score[kQuad];
+    uint16_t len[kQuad];
+    uint16_t slot_local[kQuad];  // pattern_id slot relative to the tile's first slot
+    uint16_t orig_index[kQuad];  // index in creation order (tfbs_matches)
+    uint32_t col_off[kQuad];     // A-weight columns (N correction) inside the tile's colA image
+};
+
+struct DevPattern {        // one long strand (generic kernel)
+    uint32_t col_off;      // offset of this pattern's columns in the generic weights (x5)
     int32_t min_score;
     uint16_t len;
-    uint16_t nblk;         // ceil(len / 4)
-    uint16_t slot_local;   // pattern_id slot relative to the tile's first slot
-    uint16_t orig_index;   // index in creation order (for tfbs_matches)
+    uint16_t slot_local;
+    uint16_t orig_index;
+    uint16_t pad;
 };
 
 struct DevTile {
-    uint32_t pat_begin, pat_end;  // range in the DevPattern array
-    uint32_t lut_begin;           // first LUT block (global)
-    uint32_t nblocks;             // LUT blocks (x 256 ints) in the tile
+    uint32_t first, last;         // quad range (fast) or pattern range (generic)
+    uint32_t lut_begin;           // first quad-block (global)
+    uint32_t nblocks;             // quad-blocks in the tile
     uint32_t col_begin;           // first colA entry (global)
     uint32_t ncols;
     uint32_t slot_begin;          // global pattern_id slot of local slot 0
     uint32_t nslots;
+    uint32_t lmin;                // shortest strand (bounds the windows to scan)
 };
 
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };
