@@ -44,13 +44,13 @@ std::vector<KeyRef> region_keys(const Batch &B, const RegionH &R) {
     std::vector<KeyRef> out;
     for (const InnerKey &k : R.keys) {
         if (k.slot < 0) continue;  // empty range: no match can overlap it
-        for (uint32_t s = 0; s < B.n_slots; s++) {
+        for (uint32_t s : B.slots_by_pid) {
             bool any = false;
             for (uint32_t l = 0; l < R.hap_count && !any; l++) any = count_of(B, R, l, s, k.slot) != 0;
             if (any) out.push_back({&k, s});
         }
     }
-    return out;  // R.keys is sorted by (s, e, bed) and slots ascend with pattern_id
+    return out;  // R.keys is sorted by (s, e, bed); slots_by_pid ascends with pattern_id
 }
 
 }  // namespace

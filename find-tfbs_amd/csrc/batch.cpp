@@ -336,6 +336,10 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     B.n_samples = n_samples;
     B.keep_membership = keep_membership != 0;
     B.slot_pid = plan.slot_pid;
+    B.slots_by_pid.resize(B.slot_pid.size());
+    std::iota(B.slots_by_pid.begin(), B.slots_by_pid.end(), 0u);
+    std::sort(B.slots_by_pid.begin(), B.slots_by_pid.end(),
+              [&](uint32_t a, uint32_t b) { return B.slot_pid[a] < B.slot_pid[b]; });
     B.n_slots = (uint32_t)plan.slot_pid.size();
     for (auto &q : P.pats)
         if (q.kind == TFBS_KIND_PWM && q.len > 0) B.pwm_lens.push_back(q.len);

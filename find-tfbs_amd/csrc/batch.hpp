@@ -41,7 +41,8 @@ struct Batch {
     uint32_t n_samples = 0;
     bool keep_membership = true;
     uint32_t n_slots = 0;                 // pattern_id slots (Plan::slot_pid)
-    std::vector<uint16_t> slot_pid;
+    std::vector<uint16_t> slot_pid;       // slot -> pattern_id (slots ordered for the kernels)
+    std::vector<uint32_t> slots_by_pid;   // slots in ascending pattern_id (row order)
     std::vector<std::string> beds;        // registered bed basenames
     std::vector<uint32_t> pwm_lens;       // lengths of scannable strands (for window counting)
 
