@@ -57,6 +57,7 @@ struct Inner {
     uint32_t span;  // e - s
 };
 
+
 // Count, for every inner range of this pass, the hit windows whose match range
 // overlaps it (main.rs:503 with Range::overlaps, range.rs:18-21), and add the
 // counts to the lane that owns the pattern_id slot.
@@ -73,7 +74,9 @@ __device__ __forceinline__ void count_hits(const uint64_t (&hit)[NCH], const int
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             if (!hit[c]) continue;
-            const bool ov = (uint32_t)(pos[c] - s) <= span || (uint32_t)(pos[c] + (int32_t)L - 1 - s) <= span;
+            int32_t p = pos[c];
+            asm volatile("" : "+v"(p));  // keep the (rare) overlap test here, not hoisted into the hot loop
+            const bool ov = (uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span;
             cnt += __popcll(hit[c] & __ballot(ov));
         }
         acc[kk] += (lane == slot) ? cnt : 0u;
@@ -104,10 +107,105 @@ struct ScanArgs {
     uint32_t n_patterns_total;
 };
 
+// Partial sums of one quad over NCH chunks: nblk interleaved 4-mer lookups per
+// window (ds_read_b128 each).  NB > 0 fixes the block count at compile time so
+// every read can be issued ahead of its add; NB == 0 loops over Q.nblk.
+template <int NCH>
+struct Sums {
+    uint4 v[NCH];
+};
+
+template <int NCH, int NB>
+__device__ __forceinline__ Sums<NCH> quad_sums(const char *base, uint32_t nblk, const uint32_t (&code16)[NCH][8]) {
+    Sums<NCH> r;
+    uint4 (&sc)[NCH] = r.v;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) sc[c] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        if (NB > 0 ? b >= NB : (uint32_t)b >= nblk) break;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            const uint4 v = *reinterpret_cast<const uint4 *>(base + b * (kQuadBlockInts * 4) + code16[c][b]);
+            sc[c].x += v.x;
+            sc[c].y += v.y;
+            sc[c].z += v.z;
+            sc[c].w += v.w;
+        }
+    }
+    return r;
+}
+
+// One quad of strands over NCH chunks: the lookups, then per strand the
+// threshold ballot and, on a hit, the inner-range counting.
+template <int NCH>
+__device__ __forceinline__ void quad_body(const ScanArgs &A, const DevQuad &Q, const char *s_lut,
+                                          const int32_t *s_col, const uint32_t (&code16)[NCH][8],
+                                          const int32_t (&rem)[NCH], const int32_t (&pos)[NCH],
+                                          const uint32_t (&nm)[NCH], bool has_n, uint32_t h, uint32_t cg,
+                                          const Inner *in, uint32_t n_pass, bool write_hits, uint32_t lane,
+                                          uint32_t (&acc)[kMaxInnerPass]) {
+    const char *base = s_lut + (size_t)Q.lut_off * (kQuadBlockInts * 4);
+    const uint32_t nblk = Q.nblk;
+    Sums<NCH> S;
+    if (NCH == 4) {
+        switch (nblk) {
+        case 1: S = quad_sums<NCH, 1>(base, nblk, code16); break;
+        case 2: S = quad_sums<NCH, 2>(base, nblk, code16); break;
+        case 3: S = quad_sums<NCH, 3>(base, nblk, code16); break;
+        case 4: S = quad_sums<NCH, 4>(base, nblk, code16); break;
+        case 5: S = quad_sums<NCH, 5>(base, nblk, code16); break;
+        case 6: S = quad_sums<NCH, 6>(base, nblk, code16); break;
+        case 7: S = quad_sums<NCH, 7>(base, nblk, code16); break;
+        default: S = quad_sums<NCH, 8>(base, nblk, code16); break;
+        }
+    } else {
+        S = quad_sums<NCH, 0>(base, nblk, code16);
+    }
+    const uint4 (&sc)[NCH] = S.v;
+#pragma unroll
+    for (int s = 0; s < kQuad; s++) {
+        if (s >= Q.nstrand) break;
+        const uint32_t L = Q.len[s];
+        int32_t score[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) score[c] = (int32_t)comp(sc[c], s);
+        if (has_n) {
+            const uint32_t lmask = L >= 32 ? 0xFFFFFFFFu : ((1u << L) - 1u);
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                uint32_t m = nm[c] & lmask;
+                while (m) {
+                    const uint32_t j = __builtin_ctz(m);
+                    score[c] = (int32_t)((uint32_t)score[c] - (uint32_t)s_col[Q.col_off[s] + j]);
+                    m &= m - 1;
+                }
+            }
+        }
+        uint64_t hit[NCH];
+        uint64_t any = 0;
+        const int32_t ms = Q.min_score[s];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            hit[c] = __ballot(score[c] > ms && rem[c] >= (int32_t)L);
+            any |= hit[c];
+        }
+        if (__builtin_expect(write_hits, 0) && lane == 0) {
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                const uint32_t wi = cg / 64 + c;
+                if (wi < A.hits_wpp)
+                    A.hits[((size_t)h * A.n_patterns_total + Q.orig_index[s]) * A.hits_wpp + wi] = hit[c];
+            }
+        }
+        if (__builtin_expect(any != 0, 0)) count_hits<NCH>(hit, pos, L, in, n_pass, Q.slot_local[s], lane, acc);
+    }
+}
+
 // Score NCH 64-window chunks starting at window cg against every quad of the tile.
 template <int NCH>
 __device__ __forceinline__ void scan_chunks(const ScanArgs &A, const DevTile &t, const char *s_lut,
-                                            const int32_t *s_col, const DevHap &hm, uint32_t h, uint32_t cg,
+                                            const DevQuad *s_quads, const int32_t *s_col, const DevHap &hm, uint32_t h, uint32_t cg,
                                             const Inner *in, uint32_t n_pass, bool write_hits, uint32_t lane,
                                             uint32_t (&acc)[kMaxInnerPass]) {
     const bool has_n = (hm.flags & HAP_HAS_N) != 0;
@@ -139,59 +237,8 @@ __device__ __forceinline__ void scan_chunks(const ScanArgs &A, const DevTile &t,
         }
     }
     for (uint32_t qi = t.first; qi < t.last; qi++) {
-        const DevQuad &Q = A.quads[qi];
-        const char *base = s_lut + (size_t)Q.lut_off * (kQuadBlockInts * 4);
-        uint4 sc[NCH];
-#pragma unroll
-        for (int c = 0; c < NCH; c++) sc[c] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            if (b >= Q.nblk) break;
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(base + b * (kQuadBlockInts * 4) + code16[c][b]);
-                sc[c].x += v.x;
-                sc[c].y += v.y;
-                sc[c].z += v.z;
-                sc[c].w += v.w;
-            }
-        }
-#pragma unroll
-        for (int s = 0; s < kQuad; s++) {
-            if (s >= Q.nstrand) break;
-            const uint32_t L = Q.len[s];
-            int32_t score[NCH];
-#pragma unroll
-            for (int c = 0; c < NCH; c++) score[c] = (int32_t)comp(sc[c], s);
-            if (has_n) {
-                const uint32_t lmask = L >= 32 ? 0xFFFFFFFFu : ((1u << L) - 1u);
-#pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    uint32_t m = nm[c] & lmask;
-                    while (m) {
-                        const uint32_t j = __builtin_ctz(m);
-                        score[c] = (int32_t)((uint32_t)score[c] - (uint32_t)s_col[Q.col_off[s] + j]);
-                        m &= m - 1;
-                    }
-                }
-            }
-            uint64_t hit[NCH];
-            uint64_t any = 0;
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                hit[c] = __ballot(score[c] > Q.min_score[s] && rem[c] >= (int32_t)L);
-                any |= hit[c];
-            }
-            if (write_hits && lane == 0) {
-#pragma unroll
-                for (int c = 0; c < NCH; c++) {
-                    const uint32_t wi = cg / 64 + c;
-                    if (wi < A.hits_wpp)
-                        A.hits[((size_t)h * A.n_patterns_total + Q.orig_index[s]) * A.hits_wpp + wi] = hit[c];
-                }
-            }
-            if (any) count_hits<NCH>(hit, pos, L, in, n_pass, Q.slot_local[s], lane, acc);
-        }
+        const DevQuad &Q = s_quads[qi - t.first];
+        quad_body<NCH>(A, Q, s_lut, s_col, code16, rem, pos, nm, has_n, h, cg, in, n_pass, write_hits, lane, acc);
     }
 }
 
@@ -217,12 +264,18 @@ __global__ __launch_bounds__(kFastBlock, MINW) void scan_fast_kernel(ScanArgs A)
         uint4 *dst = reinterpret_cast<uint4 *>(smem);
         const uint32_t n4 = t.nblocks * (kQuadBlockInts / 4);
         for (uint32_t i = threadIdx.x; i < n4; i += kFastBlock) dst[i] = src[i];
-        int32_t *scol = smem + t.nblocks * kQuadBlockInts;
+        // the tile's quad descriptors: read by every wave at uniform addresses (LDS broadcast)
+        const uint32_t nq = t.last - t.first;
+        const uint32_t *qsrc = reinterpret_cast<const uint32_t *>(A.quads + t.first);
+        uint32_t *qdst = reinterpret_cast<uint32_t *>(smem + t.nblocks * kQuadBlockInts);
+        for (uint32_t i = threadIdx.x; i < nq * (sizeof(DevQuad) / 4); i += kFastBlock) qdst[i] = qsrc[i];
+        int32_t *scol = smem + t.nblocks * kQuadBlockInts + nq * (sizeof(DevQuad) / 4);
         for (uint32_t i = threadIdx.x; i < t.ncols; i += kFastBlock) scol[i] = A.colA[t.col_begin + i];
     }
     __syncthreads();
     const char *s_lut = reinterpret_cast<const char *>(smem);
-    const int32_t *s_col = smem + t.nblocks * kQuadBlockInts;
+    const DevQuad *s_quads = reinterpret_cast<const DevQuad *>(smem + t.nblocks * kQuadBlockInts);
+    const int32_t *s_col = smem + t.nblocks * kQuadBlockInts + (t.last - t.first) * (sizeof(DevQuad) / 4);
 
     for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
         const uint32_t h = hg * A.haps_per_block + hh;
@@ -256,11 +309,11 @@ __global__ __launch_bounds__(kFastBlock, MINW) void scan_fast_kernel(ScanArgs A)
             for (uint32_t cg = 0; cg < nwin; cg += 64 * kChunks) {
                 const uint32_t nch = min((uint32_t)kChunks, (nwin - cg + 63) / 64);
                 if (nch >= 3)  // a 3-chunk tail scores one chunk of invalid windows (rem < L)
-                    scan_chunks<4>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
+                    scan_chunks<4>(A, t, s_lut, s_quads, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
                 else if (nch == 2)
-                    scan_chunks<2>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
+                    scan_chunks<2>(A, t, s_lut, s_quads, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
                 else
-                    scan_chunks<1>(A, t, s_lut, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
+                    scan_chunks<1>(A, t, s_lut, s_quads, s_col, hm, h, cg, in, n_pass, write_hits, lane, acc);
             }
             if (n_pass && lane < t.nslots) {
                 uint32_t *out = A.counts + hm.count_off + (size_t)(t.slot_begin + lane) * n_inner + k0;
@@ -567,7 +620,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         return tfbs::fail(TFBS_E_HIP, std::string("HIP init: ") + hipGetErrorString(e));
     }
     const Plan &P = ctx->plan;
-    ctx->lds_bytes = (size_t)P.max_tile_blocks * kQuadBlockInts * 4 + (size_t)P.max_tile_cols * 4 + 16;
+    ctx->lds_bytes = (size_t)P.max_tile_blocks * kQuadBlockInts * 4 + (size_t)P.max_tile_quads * sizeof(DevQuad) +
+                     (size_t)P.max_tile_cols * 4 + 16;
     if (ctx->lds_bytes > 160 * 1024) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "pattern tile exceeds the 160 KiB LDS");

@@ -361,6 +361,7 @@ int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
     for (auto &t : plan->fast_tiles) {
         plan->max_tile_blocks = std::max(plan->max_tile_blocks, t.nblocks);
         plan->max_tile_cols = std::max(plan->max_tile_cols, t.ncols);
+        plan->max_tile_quads = std::max(plan->max_tile_quads, t.last - t.first);
     }
     return TFBS_OK;
 }

@@ -31,6 +31,7 @@ struct Plan {
     std::vector<int32_t> gen_w;      // per generic column: 5 weights
     uint32_t max_tile_blocks = 0;
     uint32_t max_tile_cols = 0;
+    uint32_t max_tile_quads = 0;
     bool zero_len_panics = false;
 };
 
