@@ -8,7 +8,7 @@ LIBDIR := $(PKG)/lib
 OBJDIR := $(PKG)/lib/obj
 JOBS ?= 8
 
-HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp
+HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
 HIP_SRCS := $(SRC)/device.hip
 HDRS := $(wildcard $(SRC)/*.hpp) include/tfbs_amd.h
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
@@ -17,7 +17,7 @@ HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
 CXXFLAGS := -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
 HIPFLAGS := $(CXXFLAGS) --offload-arch=$(ARCH) -munsafe-fp-atomics
 
-all: $(LIBDIR)/libtfbs_amd.so oracle
+all: $(LIBDIR)/libtfbs_amd.so $(PKG)/bin/find-tfbs-amd oracle
 
 $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -30,6 +30,10 @@ $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 $(LIBDIR)/libtfbs_amd.so: $(HOST_OBJS) $(HIP_OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -lz -lpthread
 
+$(PKG)/bin/find-tfbs-amd: $(SRC)/cli.cpp include/tfbs_amd.h $(LIBDIR)/libtfbs_amd.so
+	@mkdir -p $(PKG)/bin
+	$(HIPCC) $(CXXFLAGS) -x c++ $< -o $@ -L$(LIBDIR) -ltfbs_amd -Wl,-rpath,'$$ORIGIN/../lib'
+
 oracle:
 	$(MAKE) -s -C oracle
 
@@ -38,6 +42,6 @@ asm: $(SRC)/device.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -x hip --cuda-device-only -S $< -o $(OBJDIR)/device.s -Rpass-analysis=kernel-resource-usage
 
 clean:
-	rm -rf $(LIBDIR) oracle/_build
+	rm -rf $(LIBDIR) $(PKG)/bin oracle/_build
 
 .PHONY: all oracle clean asm

@@ -22,6 +22,7 @@ device; without one, Scanner() raises TfbsError(TFBS_E_NODEVICE).
 import ctypes as C
 from collections import namedtuple
 
+from . import _capi
 from ._capi import TfbsError, check, lib, tfbs_pattern_desc  # noqa: F401
 
 TFBS_OK = 0
@@ -430,3 +431,90 @@ def select_inner_peaks(merged, beds):
             if range_overlaps((s, e), merged):
                 out.append((bi, s, e))
     return out
+
+
+def run(chromosome, bcf, bed_files, reference_genome_file, wanted_samples, pwm_file, pwm_threshold_directory,
+        pwm_threshold, wanted_pwms, output_file, forward_only=False, run_tabix=False, min_maf=0, threads=1,
+        after_position=0, verbose=False, device=0, regions_per_batch=0):
+    """main.rs:234-393 `run` with the reference's argument order; writes the BGZF VCF."""
+    a = _capi.tfbs_run_args()
+    keep = [_u(x) if x is not None else None for x in (chromosome, bcf, ",".join(bed_files), reference_genome_file,
+                                                        wanted_samples, pwm_file, pwm_threshold_directory,
+                                                        ",".join(wanted_pwms), output_file)]
+    (a.chromosome, a.bcf, a.bed_files, a.reference, a.samples_file, a.pwm_file, a.pwm_threshold_dir, a.pwm_names,
+     a.output) = keep
+    a.pwm_threshold = pwm_threshold
+    a.forward_only = 1 if forward_only else 0
+    a.min_maf = min_maf
+    a.threads = threads
+    a.after_position = after_position
+    a.tabix = 1 if run_tabix else 0
+    a.verbose = 1 if verbose else 0
+    a.device = device
+    a.regions_per_batch = regions_per_batch
+    check(lib().tfbs_run(C.byref(a)))
+
+
+class BcfReader:
+    """Minimal BCF2 reader (f2): IndexedReader::from_path + fetch + records (raw GT)."""
+
+    def __init__(self, path):
+        self.h = C.c_void_p()
+        check(lib().tfbs_bcf_open(_u(path), C.byref(self.h)))
+        n = lib().tfbs_bcf_num_samples(self.h)
+        self.samples = [lib().tfbs_bcf_sample_name(self.h, i).decode() for i in range(n)]
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().tfbs_bcf_close(self.h)
+            self.h = None
+
+    def fetch(self, chrom, beg, end):
+        n = C.c_size_t()
+        check(lib().tfbs_bcf_fetch(self.h, _u(chrom), beg, end, C.byref(n)))
+        out = []
+        ns = len(self.samples)
+        for i in range(n.value):
+            pos, rlen, na = C.c_uint64(), C.c_uint32(), C.c_uint32()
+            ref, alt = C.c_char_p(), C.c_char_p()
+            gt = _capi.i32p()
+            check(lib().tfbs_bcf_record(self.h, i, C.byref(pos), C.byref(rlen), C.byref(na), C.byref(ref),
+                                        C.byref(alt), C.byref(gt)))
+            out.append({"pos0": pos.value, "rlen": rlen.value, "n_alleles": na.value, "ref": ref.value.decode(),
+                        "alt": alt.value.decode() if alt.value is not None else None,
+                        "gt": [[gt[2 * s], gt[2 * s + 1]] for s in range(ns)]})
+        return out
+
+
+def fasta_fetch(path, chrom, start, stop):
+    p = C.c_void_p()
+    n = C.c_size_t()
+    check(lib().tfbs_fasta_fetch(_u(path), _u(chrom), start, stop, C.byref(p), C.byref(n)))
+    try:
+        return C.string_at(p, n.value).decode()
+    finally:
+        lib().tfbs_free(p)
+
+
+def bgzf_write(path, text, flushes=0):
+    b = _u(text)
+    check(lib().tfbs_bgzf_write_file(_u(path), b, len(b), flushes))
+
+
+def bgzf_read(path):
+    p = C.c_void_p()
+    n = C.c_size_t()
+    check(lib().tfbs_bgzf_read_file(_u(path), C.byref(p), C.byref(n)))
+    try:
+        return C.string_at(p, n.value).decode()
+    finally:
+        lib().tfbs_free(p)
+
+
+def merge_ranges(ranges):
+    n = len(ranges)
+    os_, oe = (C.c_uint64 * max(1, n))(), (C.c_uint64 * max(1, n))()
+    m = C.c_size_t()
+    check(lib().tfbs_merge_ranges((C.c_uint64 * max(1, n))(*[r[0] for r in ranges]),
+                                  (C.c_uint64 * max(1, n))(*[r[1] for r in ranges]), n, os_, oe, C.byref(m)))
+    return [(os_[i], oe[i]) for i in range(m.value)]

@@ -30,6 +30,16 @@ class tfbs_pattern_desc(C.Structure):
     ]
 
 
+class tfbs_run_args(C.Structure):
+    _fields_ = [
+        ("chromosome", C.c_char_p), ("bcf", C.c_char_p), ("bed_files", C.c_char_p), ("reference", C.c_char_p),
+        ("samples_file", C.c_char_p), ("pwm_file", C.c_char_p), ("pwm_threshold_dir", C.c_char_p),
+        ("pwm_names", C.c_char_p), ("output", C.c_char_p), ("pwm_threshold", C.c_float), ("forward_only", C.c_int),
+        ("min_maf", C.c_uint32), ("threads", C.c_uint32), ("after_position", C.c_uint64), ("tabix", C.c_int),
+        ("verbose", C.c_int), ("device", C.c_int), ("regions_per_batch", C.c_uint32),
+    ]
+
+
 # (name, restype, argtypes) for every symbol in include/tfbs_amd.h
 SIGNATURES = [
     ("tfbs_strerror", C.c_char_p, [C.c_int]),
@@ -79,6 +89,19 @@ SIGNATURES = [
     ("tfbs_free", None, [C.c_void_p]),
     ("tfbs_counts_as_genotypes", C.c_int, [u32p, u32p, C.c_size_t, u32p, C.c_char_p, C.c_size_t, C.c_char_p,
                                            C.c_size_t]),
+    ("tfbs_run", C.c_int, [C.c_void_p]),
+    ("tfbs_bcf_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),
+    ("tfbs_bcf_close", None, [vp]),
+    ("tfbs_bcf_num_samples", C.c_size_t, [vp]),
+    ("tfbs_bcf_sample_name", C.c_char_p, [vp, C.c_size_t]),
+    ("tfbs_bcf_fetch", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_size_t)]),
+    ("tfbs_bcf_record", C.c_int, [vp, C.c_size_t, u64p, u32p, u32p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
+                                  C.POINTER(i32p)]),
+    ("tfbs_fasta_fetch", C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p),
+                                   C.POINTER(C.c_size_t)]),
+    ("tfbs_bgzf_write_file", C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t, C.c_int]),
+    ("tfbs_bgzf_read_file", C.c_int, [C.c_char_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    ("tfbs_merge_ranges", C.c_int, [u64p, u64p, C.c_size_t, u64p, u64p, C.POINTER(C.c_size_t)]),
     ("tfbs_synth_write_pwms", C.c_int, [C.c_char_p, C.c_uint32, C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]),
     ("tfbs_synth_region_make", C.c_int, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.POINTER(vp)]),

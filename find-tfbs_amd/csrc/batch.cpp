@@ -6,8 +6,10 @@
 // the same sequence the later one wins (HashMap::insert, haplotype.rs:84); the
 // loser's haplotype ids stay with the reference group (main.rs:103-105, 129-137).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <unordered_map>
 
 #include "batch.hpp"
@@ -403,29 +405,71 @@ static int to_codes(const char *s, std::vector<uint8_t> &out) {
     return TFBS_OK;
 }
 
+}  // extern "C"
+
+namespace tfbs {
+// haplotype.rs:16-60 for one record: alleles[0]/[1] decode (may panic on a bad
+// base even for multi-allelic records, line 20-22); for bi-allelic records the
+// ploidy assert (line 32) and Left = Unphased(1) = raw 4, Right = Phased(1) = raw 5.
+int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                   const int32_t *gt, Record &r) {
+    if (n_alleles < 2 || !alt) return fail(TFBS_E_ALLELES, "record with one allele (haplotype.rs:22)");
+    if (!ref || (n_alleles == 2 && n_samples && !gt)) return fail(TFBS_E_ARG, "null argument");
+    r = Record();
+    r.pos = pos;
+    r.n_alleles = n_alleles;
+    int rc = to_codes(ref, r.ref);
+    if (!rc) rc = to_codes(alt, r.alt);
+    if (rc) return rc;
+    if (n_alleles == 2) {
+        const int32_t VE = INT32_MIN + 1;
+        for (uint32_t s = 0; s < n_samples; s++) {
+            const int32_t g0 = gt[2 * s], g1 = gt[2 * s + 1];
+            const uint32_t glen = g0 == VE ? 0 : (g1 == VE ? 1 : 2);
+            if (glen != n_alleles) return fail(TFBS_E_PLOIDY, "Inconsistent number of alleles");
+            if (g0 == 4) r.carriers.push_back(2 * s);      // GenotypeAllele::Unphased(1)
+            if (g1 == 5) r.carriers.push_back(2 * s + 1);  // GenotypeAllele::Phased(1)
+        }
+    }
+    return TFBS_OK;
+}
+
+// Builds regions on up to `threads` host threads, commits them in order.
+int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads) {
+    const size_t n = ins.size();
+    std::vector<RegionBuilt> built(n);
+    std::vector<int> rcs(n, TFBS_OK);
+    std::atomic<size_t> next(0);
+    auto work = [&]() {
+        for (;;) {
+            const size_t j = next.fetch_add(1);
+            if (j >= n) break;
+            rcs[j] = build_region(B, std::move(ins[j]), built[j]);
+        }
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
+    work();
+    for (auto &t : ts) t.join();
+    B.counts_valid = false;
+    for (size_t j = 0; j < n; j++) {
+        if (rcs[j]) return rcs[j];
+        commit_region(B, std::move(built[j]));
+    }
+    return TFBS_OK;
+}
+}  // namespace tfbs
+
+extern "C" {
+
 int tfbs_batch_region_add_record_gt(tfbs_batch *b, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
                                     const int32_t *gt) {
     if (!b || !b->b.open) return tfbs::fail(TFBS_E_STATE, "no open region");
     Batch &B = b->b;
     if (B.status) return B.status;
-    if (n_alleles < 2 || !alt) return B.status = tfbs::fail(TFBS_E_ALLELES, "record with one allele (haplotype.rs:22)");
-    if (!ref || (n_alleles == 2 && B.n_samples && !gt)) return tfbs::fail(TFBS_E_ARG, "null argument");
     tfbs::Record r;
-    r.pos = pos;
-    r.n_alleles = n_alleles;
-    int rc = to_codes(ref, r.ref);
-    if (!rc) rc = to_codes(alt, r.alt);
+    int rc = tfbs::make_record_gt(B.n_samples, pos, n_alleles, ref, alt, gt, r);
     if (rc) return B.status = rc;
-    if (n_alleles == 2) {
-        const int32_t VE = INT32_MIN + 1;
-        for (uint32_t s = 0; s < B.n_samples; s++) {
-            int32_t g0 = gt[2 * s], g1 = gt[2 * s + 1];
-            uint32_t glen = g0 == VE ? 0 : (g1 == VE ? 1 : 2);
-            if (glen != n_alleles) return B.status = tfbs::fail(TFBS_E_PLOIDY, "Inconsistent number of alleles");
-            if (g0 == 4) r.carriers.push_back(2 * s);      // GenotypeAllele::Unphased(1)
-            if (g1 == 5) r.carriers.push_back(2 * s + 1);  // GenotypeAllele::Phased(1)
-        }
-    }
     B.cur_rec.push_back(std::move(r));
     return TFBS_OK;
 }

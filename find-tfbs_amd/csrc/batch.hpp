@@ -93,6 +93,9 @@ struct RegionBuilt {
 
 int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);
 void commit_region(Batch &B, RegionBuilt &&built);
+int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads);
+int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                   const int32_t *gt, Record &r);
 
 // haplotype.rs:94-156 over a reference window given as codes for positions
 // [ref_start, ref_start + n_ref).  Diffs are pointers to records.

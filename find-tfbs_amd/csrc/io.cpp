@@ -1,0 +1,425 @@
+// Inputs and outputs around the scoring path:
+// a BGZF/BCF2 reader with region fetch (replaces rust-htslib 0.26.1 IndexedReader,
+// haplotype.rs:16-24, 78-79), a FASTA/.fai reader (bio 0.28.2, main.rs:156-161),
+// a BED reader (bed.rs:9-19) and a BGZF writer (bgzip 0.0.3, main.rs:264-276).
+//
+// The BCF reader decodes the whole file once and keeps each contig's records in
+// file order; fetch(contig, beg, end) returns the records overlapping the
+// 0-based half-open [beg, end) the way htslib's region iterator does
+// (pos < end && pos + rlen > beg).  GT values are kept raw (BCF2 encoding
+// (allele + 1) << 1 | phased) with vector_end normalised to INT32_MIN + 1.
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "tfbs_internal.hpp"
+#include "io.hpp"
+
+namespace tfbs {
+
+static int read_file(const std::string &path, std::string &out) {
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return fail(TFBS_E_IO, "Could not open file " + path);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    out = ss.str();
+    return TFBS_OK;
+}
+
+// Inflate a concatenation of gzip members (BGZF blocks are gzip members).
+int bgzf_inflate(const std::string &in, std::string &out) {
+    out.clear();
+    size_t off = 0;
+    std::vector<char> buf(1 << 16);
+    while (off < in.size()) {
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) return fail(TFBS_E_IO, "inflateInit2 failed");
+        zs.next_in = (Bytef *)(in.data() + off);
+        zs.avail_in = (uInt)std::min<size_t>(in.size() - off, 0x7FFFFFFF);
+        int rc;
+        do {
+            zs.next_out = (Bytef *)buf.data();
+            zs.avail_out = (uInt)buf.size();
+            rc = inflate(&zs, Z_NO_FLUSH);
+            if (rc != Z_OK && rc != Z_STREAM_END) {
+                inflateEnd(&zs);
+                return fail(TFBS_E_IO, "corrupt gzip/BGZF data");
+            }
+            out.append(buf.data(), buf.size() - zs.avail_out);
+        } while (rc != Z_STREAM_END);
+        off += zs.total_in;
+        inflateEnd(&zs);
+        if (zs.total_in == 0) break;
+    }
+    return TFBS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// BGZF writer: <= 65280 input bytes per block, raw deflate, BC extra field,
+// CRC32 + ISIZE trailer; flush() ends the current block; close() appends the
+// standard 28-byte EOF block (the layout expected_output_*.vcf.gz shows).
+// ---------------------------------------------------------------------------
+static const unsigned char kBgzfEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                                           2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+int bgzf_block(const char *data, size_t n, std::string &out) {
+    std::vector<unsigned char> comp(compressBound((uLong)n) + 64);
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (deflateInit2(&zs, Z_DEFAULT_COMPRESSION, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK)
+        return fail(TFBS_E_IO, "deflateInit2 failed");
+    zs.next_in = (Bytef *)data;
+    zs.avail_in = (uInt)n;
+    zs.next_out = comp.data();
+    zs.avail_out = (uInt)comp.size();
+    int rc = deflate(&zs, Z_FINISH);
+    deflateEnd(&zs);
+    if (rc != Z_STREAM_END) return fail(TFBS_E_IO, "deflate failed");
+    const size_t clen = zs.total_out;
+    const size_t bsize = 18 + clen + 8;  // header + data + trailer
+    if (bsize > 65536) return fail(TFBS_E_IO, "BGZF block too large");
+    unsigned char hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0, 0, 0};
+    hdr[16] = (unsigned char)((bsize - 1) & 0xff);
+    hdr[17] = (unsigned char)((bsize - 1) >> 8);
+    out.append((const char *)hdr, 18);
+    out.append((const char *)comp.data(), clen);
+    uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), (const Bytef *)data, (uInt)n);
+    unsigned char tr[8];
+    for (int i = 0; i < 4; i++) tr[i] = (unsigned char)(crc >> (8 * i));
+    for (int i = 0; i < 4; i++) tr[4 + i] = (unsigned char)(((uint32_t)n) >> (8 * i));
+    out.append((const char *)tr, 8);
+    return TFBS_OK;
+}
+
+int BgzfWriter::open(const std::string &path) {
+    f = fopen(path.c_str(), "wb");
+    if (!f) return fail(TFBS_E_IO, "Could not create output file " + path);
+    return TFBS_OK;
+}
+int BgzfWriter::write(const char *p, size_t n) {
+    while (n) {
+        const size_t take = std::min(n, kBlock - buf.size());
+        buf.append(p, take);
+        p += take;
+        n -= take;
+        if (buf.size() == kBlock) {
+            int rc = emit();
+            if (rc) return rc;
+        }
+    }
+    return TFBS_OK;
+}
+int BgzfWriter::emit() {
+    std::string blk;
+    int rc = bgzf_block(buf.data(), buf.size(), blk);
+    if (rc) return rc;
+    if (fwrite(blk.data(), 1, blk.size(), f) != blk.size()) return fail(TFBS_E_IO, "write failed");
+    buf.clear();
+    return TFBS_OK;
+}
+int BgzfWriter::flush() { return emit(); }  // like BGzWriter::flush: ends the block (empty block if nothing buffered)
+int BgzfWriter::close() {
+    if (!f) return TFBS_OK;
+    int rc = TFBS_OK;
+    if (!buf.empty()) rc = emit();
+    if (!rc && fwrite(kBgzfEof, 1, sizeof kBgzfEof, f) != sizeof kBgzfEof) rc = fail(TFBS_E_IO, "write failed");
+    fclose(f);
+    f = nullptr;
+    return rc;
+}
+BgzfWriter::~BgzfWriter() {
+    if (f) fclose(f);
+}
+
+// ---------------------------------------------------------------------------
+// BCF2
+// ---------------------------------------------------------------------------
+namespace {
+struct Cur {
+    const unsigned char *p, *e;
+    bool ok = true;
+    bool need(size_t n) {
+        if ((size_t)(e - p) < n) ok = false;
+        return ok;
+    }
+};
+// typed value descriptor: returns (type, count)
+bool typed(Cur &c, int &type, uint32_t &count);
+bool read_int(Cur &c, int type, int64_t &v) {
+    switch (type) {
+    case 1: if (!c.need(1)) return false; v = (int8_t)c.p[0]; c.p += 1; return true;
+    case 2: if (!c.need(2)) return false; { int16_t x; memcpy(&x, c.p, 2); v = x; } c.p += 2; return true;
+    case 3: if (!c.need(4)) return false; { int32_t x; memcpy(&x, c.p, 4); v = x; } c.p += 4; return true;
+    default: return false;
+    }
+}
+bool typed(Cur &c, int &type, uint32_t &count) {
+    if (!c.need(1)) return false;
+    const unsigned char d = *c.p++;
+    type = d & 0x0F;
+    count = d >> 4;
+    if (count == 15) {
+        int t2;
+        uint32_t n2;
+        if (!typed(c, t2, n2) || n2 != 1) return false;
+        int64_t v;
+        if (!read_int(c, t2, v) || v < 0) return false;
+        count = (uint32_t)v;
+    }
+    return true;
+}
+size_t type_size(int t) {
+    switch (t) {
+    case 0: return 0;
+    case 1: case 7: return 1;
+    case 2: return 2;
+    case 3: case 5: return 4;
+    default: return 0;
+    }
+}
+}  // namespace
+
+int Bcf::open(const std::string &path) {
+    std::string raw, data;
+    int rc = read_file(path, raw);
+    if (rc) return rc;
+    rc = bgzf_inflate(raw, data);
+    if (rc) return rc;
+    if (data.size() < 9 || memcmp(data.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
+    uint32_t l_text;
+    memcpy(&l_text, data.data() + 5, 4);
+    if (9ull + l_text > data.size()) return fail(TFBS_E_PARSE, "truncated BCF header");
+    std::string text(data.data() + 9, l_text);
+    // header dictionaries (VCF 4.3 / BCF2): strings PASS + FILTER/INFO/FORMAT (IDX= wins), contigs
+    std::map<int, std::string> sdict;
+    sdict[0] = "PASS";
+    int next = 1, cnext = 0;
+    std::istringstream hs(text);
+    std::string line;
+    auto field = [](const std::string &l, const std::string &key) -> std::string {
+        size_t a = l.find(key + "=");
+        if (a == std::string::npos) return "";
+        a += key.size() + 1;
+        size_t b = a;
+        while (b < l.size() && l[b] != ',' && l[b] != '>') b++;
+        return l.substr(a, b - a);
+    };
+    while (std::getline(hs, line)) {
+        if (!line.empty() && line.back() == '\0') line.pop_back();
+        if (line.rfind("##contig=<", 0) == 0) {
+            std::string id = field(line, "ID"), idx = field(line, "IDX");
+            int i = idx.empty() ? cnext : atoi(idx.c_str());
+            if ((int)contigs.size() <= i) contigs.resize(i + 1);
+            contigs[i] = id;
+            cnext = i + 1;
+        } else if (line.rfind("##FILTER=<", 0) == 0 || line.rfind("##INFO=<", 0) == 0 ||
+                   line.rfind("##FORMAT=<", 0) == 0) {
+            std::string id = field(line, "ID"), idx = field(line, "IDX");
+            if (id == "PASS") continue;
+            int i = idx.empty() ? next : atoi(idx.c_str());
+            if (!sdict.count(i)) sdict[i] = id;
+            next = std::max(next, i + 1);
+        } else if (line.rfind("#CHROM", 0) == 0) {
+            std::vector<std::string> cols;
+            std::string col;
+            std::istringstream ls(line);
+            while (std::getline(ls, col, '\t')) cols.push_back(col);
+            for (size_t i = 9; i < cols.size(); i++) samples.push_back(cols[i]);
+        }
+    }
+    int gt_key = -1;
+    for (auto &kv : sdict)
+        if (kv.second == "GT") gt_key = kv.first;
+    per_contig.assign(contigs.size(), {});
+    const unsigned char *p = (const unsigned char *)data.data() + 9 + l_text;
+    const unsigned char *end = (const unsigned char *)data.data() + data.size();
+    const size_t ns = samples.size();
+    while (p + 8 <= end) {
+        uint32_t l_shared, l_indiv;
+        memcpy(&l_shared, p, 4);
+        memcpy(&l_indiv, p + 4, 4);
+        p += 8;
+        if ((size_t)(end - p) < (size_t)l_shared + l_indiv) return fail(TFBS_E_PARSE, "truncated BCF record");
+        Cur sh{p, p + l_shared};
+        Cur in{p + l_shared, p + l_shared + l_indiv};
+        p += l_shared + l_indiv;
+        BcfRecord r;
+        int32_t chrom, pos, rlen;
+        uint32_t nai, nfs;
+        if (!sh.need(24)) return fail(TFBS_E_PARSE, "short BCF record");
+        memcpy(&chrom, sh.p, 4);
+        memcpy(&pos, sh.p + 4, 4);
+        memcpy(&rlen, sh.p + 8, 4);
+        memcpy(&nai, sh.p + 16, 4);
+        memcpy(&nfs, sh.p + 20, 4);
+        sh.p += 24;
+        r.pos = (uint64_t)(int64_t)pos;
+        r.rlen = (uint32_t)std::max(rlen, 0);
+        const uint32_t n_allele = nai >> 16;
+        const uint32_t n_fmt = nfs >> 24;
+        r.n_alleles = n_allele;
+        int t;
+        uint32_t n;
+        if (!typed(sh, t, n) || !sh.need(n * type_size(t))) return fail(TFBS_E_PARSE, "bad BCF ID");
+        sh.p += n * type_size(t);
+        for (uint32_t a = 0; a < n_allele; a++) {
+            if (!typed(sh, t, n) || !sh.need(n)) return fail(TFBS_E_PARSE, "bad BCF allele");
+            std::string al((const char *)sh.p, n);
+            sh.p += n;
+            while (!al.empty() && al.back() == '\0') al.pop_back();
+            if (a == 0) r.ref = al;
+            else if (a == 1) r.alt = al;
+        }
+        r.gt.assign(2 * ns, INT32_MIN + 1);
+        for (uint32_t f = 0; f < n_fmt; f++) {
+            int kt;
+            uint32_t kn;
+            int64_t key;
+            if (!typed(in, kt, kn) || kn != 1 || !read_int(in, kt, key)) return fail(TFBS_E_PARSE, "bad FORMAT key");
+            int vt;
+            uint32_t vn;
+            if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
+            const size_t sz = type_size(vt);
+            if (!in.need(sz * vn * ns)) return fail(TFBS_E_PARSE, "truncated FORMAT data");
+            if (key == gt_key && vt >= 1 && vt <= 3) {
+                const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
+                for (size_t s = 0; s < ns; s++) {
+                    for (uint32_t k = 0; k < vn; k++) {
+                        int64_t v;
+                        read_int(in, vt, v);
+                        if (k < 2) r.gt[2 * s + k] = v == ve ? INT32_MIN + 1 : (int32_t)v;
+                    }
+                }
+            } else {
+                in.p += sz * vn * ns;
+            }
+        }
+        if (chrom < 0 || (size_t)chrom >= contigs.size()) return fail(TFBS_E_PARSE, "BCF record with unknown contig");
+        per_contig[chrom].push_back(std::move(r));
+    }
+    // overlap queries: per contig the running max of pos + rlen allows a binary search
+    max_end.assign(contigs.size(), {});
+    for (size_t c = 0; c < per_contig.size(); c++) {
+        auto &v = per_contig[c];
+        std::stable_sort(v.begin(), v.end(), [](const BcfRecord &a, const BcfRecord &b) { return a.pos < b.pos; });
+        uint64_t m = 0;
+        for (auto &r : v) {
+            m = std::max(m, r.pos + r.rlen);
+            max_end[c].push_back(m);
+        }
+    }
+    return TFBS_OK;
+}
+
+int Bcf::contig_index(const std::string &name) const {
+    for (size_t i = 0; i < contigs.size(); i++)
+        if (contigs[i] == name) return (int)i;
+    return -1;
+}
+
+void Bcf::fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out) const {
+    out.clear();
+    if (contig < 0 || (size_t)contig >= per_contig.size()) return;
+    const auto &v = per_contig[contig];
+    const auto &me = max_end[contig];
+    // first record whose running max end exceeds beg
+    size_t lo = (size_t)(std::upper_bound(me.begin(), me.end(), beg) - me.begin());
+    for (size_t i = lo; i < v.size() && v[i].pos < end; i++)
+        if (v[i].pos + v[i].rlen > beg) out.push_back(&v[i]);
+}
+
+// ---------------------------------------------------------------------------
+// FASTA (.fai)
+// ---------------------------------------------------------------------------
+int Fasta::open(const std::string &path) {
+    this->path = path;
+    std::ifstream fi(path + ".fai");
+    if (!fi) return fail(TFBS_E_IO, "Error while opening the reference genome '" + path + "' (.fai missing)");
+    std::string line;
+    while (std::getline(fi, line)) {
+        std::istringstream ls(line);
+        std::string name;
+        FaiEntry e;
+        if (std::getline(ls, name, '\t') && (ls >> e.len >> e.off >> e.lbases >> e.lwidth)) idx[name] = e;
+    }
+    f = fopen(path.c_str(), "rb");
+    if (!f) return fail(TFBS_E_IO, "Error while opening the reference genome '" + path + "'");
+    return TFBS_OK;
+}
+Fasta::~Fasta() {
+    if (f) fclose(f);
+}
+int Fasta::fetch(const std::string &chrom, uint64_t start, uint64_t stop, std::string &out) {
+    out.clear();
+    auto it = idx.find(chrom);
+    if (it == idx.end()) return fail(TFBS_E_RANGE, "Error while seeking in reference genome file: unknown " + chrom);
+    const FaiEntry &e = it->second;
+    if (start > e.len) return fail(TFBS_E_RANGE, "Error while seeking in reference genome file");
+    stop = std::min(stop, e.len);
+    uint64_t pos = start;
+    while (pos < stop) {
+        const uint64_t line = pos / e.lbases, col = pos % e.lbases;
+        const uint64_t take = std::min<uint64_t>(e.lbases - col, stop - pos);
+        if (fseeko(f, (off_t)(e.off + line * e.lwidth + col), SEEK_SET)) return fail(TFBS_E_IO, "seek failed");
+        const size_t old = out.size();
+        out.resize(old + take);
+        if (fread(&out[old], 1, take, f) != take) return fail(TFBS_E_IO, "short FASTA read");
+        pos += take;
+    }
+    return TFBS_OK;
+}
+
+// ---------------------------------------------------------------------------
+// BED (bed.rs:9-19): tab separated chrom, start, end[, ...]; raw start/end kept
+// as an inclusive Range.  Empty lines and '#'/track/browser lines are skipped.
+// ---------------------------------------------------------------------------
+int load_bed(const std::string &path, const std::string &chrom, std::vector<std::pair<uint64_t, uint64_t>> &out) {
+    std::ifstream in(path);
+    if (!in) return fail(TFBS_E_IO, "Bed file " + path + " does not exist");
+    std::string line;
+    while (std::getline(in, line)) {
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        if (line.empty() || line[0] == '#' || line.rfind("track", 0) == 0 || line.rfind("browser", 0) == 0) continue;
+        std::vector<std::string> f;
+        std::string x;
+        std::istringstream ls(line);
+        while (std::getline(ls, x, '\t')) f.push_back(x);
+        if (f.size() < 3) return fail(TFBS_E_PARSE, "bad BED line in " + path);
+        if (f[0] != chrom) continue;
+        char *e1 = nullptr, *e2 = nullptr;
+        unsigned long long s = strtoull(f[1].c_str(), &e1, 10), e = strtoull(f[2].c_str(), &e2, 10);
+        if (*e1 || *e2 || f[1].empty() || f[2].empty()) return fail(TFBS_E_PARSE, "bad BED coordinates in " + path);
+        out.push_back({s, e});
+    }
+    return TFBS_OK;
+}
+
+// range.rs:43-87 RangeStack: stable sort by start, merge while last.overlaps(next).
+std::vector<std::pair<uint64_t, uint64_t>> merge_ranges(std::vector<std::pair<uint64_t, uint64_t>> r) {
+    std::stable_sort(r.begin(), r.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+    std::vector<std::pair<uint64_t, uint64_t>> out;
+    for (auto &x : r) {
+        if (!out.empty()) {
+            auto &l = out.back();
+            const bool ov = (x.first >= l.first && x.first <= l.second) || (x.second >= l.first && x.second <= l.second);
+            if (ov) {
+                l.first = std::min(l.first, x.first);
+                l.second = std::max(l.second, x.second);
+                continue;
+            }
+        }
+        out.push_back(x);
+    }
+    return out;
+}
+
+}  // namespace tfbs

@@ -1,0 +1,327 @@
+// The find-tfbs command flow (main.rs:234-393) on top of the batch + GPU scan:
+// PWM load, BED load/merge, BCF + FASTA reads, distinct haplotypes per merged
+// region, the scan, count aggregation and the pseudo-VCF rows through a BGZF
+// writer, renamed from <out>.part at the end (or bgzip + tabix'ed).
+//
+// Differences from the reference that are choices, not gaps:
+// regions are processed in merged-peak order in batches of `regions_per_batch`
+// (the reference spreads 50-peak chunks over threads and emits rows in thread
+// interleaving / HashMap order); rows within a region are sorted (D2); the
+// POS counter is therefore deterministic.
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "batch.hpp"
+#include "io.hpp"
+#include "patterns.hpp"
+
+namespace tfbs {
+int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out);
+}
+
+namespace {
+
+std::vector<std::string> split(const std::string &s, char sep) {
+    std::vector<std::string> out;
+    size_t a = 0;
+    for (;;) {
+        size_t c = s.find(sep, a);
+        out.push_back(s.substr(a, c == std::string::npos ? std::string::npos : c - a));
+        if (c == std::string::npos) break;
+        a = c + 1;
+    }
+    return out;
+}
+
+std::string basename_of(const std::string &p) {
+    size_t k = p.find_last_of('/');
+    return k == std::string::npos ? p : p.substr(k + 1);
+}
+
+bool in_path(const char *prog) {
+    const char *path = getenv("PATH");
+    if (!path) return false;
+    for (auto &d : split(path, ':')) {
+        std::string f = d + "/" + prog;
+        if (access(f.c_str(), X_OK) == 0) return true;
+    }
+    return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfbs_run(const tfbs_run_args *a) {
+    using namespace tfbs;
+    if (!a || !a->chromosome || !a->bcf || !a->bed_files || !a->reference || !a->pwm_file || !a->pwm_threshold_dir ||
+        !a->pwm_names || !a->output)
+        return fail(TFBS_E_ARG, "missing required argument");
+    const std::string chrom = a->chromosome;
+    if (a->tabix && (!in_path("bgzip") || !in_path("tabix")))
+        return fail(TFBS_E_IO, "bgzip/tabix cannot be found in PATH");  // main.rs:220-223
+
+    // patterns (main.rs:237-250)
+    tfbs_patterns *pp = nullptr;
+    int rc = tfbs_patterns_from_files(a->pwm_file, a->pwm_threshold_dir, a->pwm_threshold, a->pwm_names,
+                                      a->forward_only ? 0 : 1, &pp);
+    if (rc) return rc;
+    std::unique_ptr<tfbs_patterns, void (*)(tfbs_patterns *)> pguard(pp, tfbs_patterns_destroy);
+
+    // BED sources (bed.rs:25-47): keyed by path (a repeated path counts once), merged
+    // over all of them, inner peaks keyed by basename (a later file with the same
+    // basename replaces an earlier one).
+    std::vector<std::string> paths;
+    for (auto &b : split(a->bed_files, ','))
+        if (std::find(paths.begin(), paths.end(), b) == paths.end()) paths.push_back(b);
+    std::vector<std::pair<uint64_t, uint64_t>> all;
+    std::vector<std::pair<std::string, std::vector<std::pair<uint64_t, uint64_t>>>> beds;
+    for (auto &path : paths) {
+        struct stat st;
+        if (stat(path.c_str(), &st) != 0) return fail(TFBS_E_IO, "Bed file " + path + " does not exist");
+        std::vector<std::pair<uint64_t, uint64_t>> peaks, kept;
+        rc = load_bed(path, chrom, peaks);
+        if (rc) return rc;
+        for (auto &p : peaks)
+            if (p.first >= a->after_position) kept.push_back(p);
+        all.insert(all.end(), kept.begin(), kept.end());
+        const std::string bn = basename_of(path);
+        bool replaced = false;
+        for (auto &b : beds)
+            if (b.first == bn) { b.second = kept; replaced = true; }
+        if (!replaced) beds.push_back({bn, kept});
+    }
+    const auto merged = merge_ranges(all);
+
+    // BCF + samples (main.rs:255, 293-314)
+    Bcf bcf;
+    rc = bcf.open(a->bcf);
+    if (rc) return rc;
+    std::vector<size_t> sel;
+    if (a->samples_file && *a->samples_file) {
+        std::ifstream sf(a->samples_file);
+        if (!sf) return fail(TFBS_E_IO, std::string("Could not open sample file ") + a->samples_file);
+        std::set<std::string> want;
+        std::string l;
+        while (std::getline(sf, l))
+            if (l.size() > 1) want.insert(l);
+        for (size_t i = 0; i < bcf.samples.size(); i++)
+            if (want.count(bcf.samples[i])) sel.push_back(i);
+    } else {
+        for (size_t i = 0; i < bcf.samples.size(); i++) sel.push_back(i);
+    }
+    const int rid = bcf.contig_index(chrom);
+    Fasta fasta;
+    rc = fasta.open(a->reference);
+    if (rc) return rc;
+
+    // output (main.rs:264-290, 320-324)
+    const std::string out = a->output, part = out + ".part";
+    BgzfWriter w;
+    rc = w.open(part);
+    if (rc) return rc;
+    std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+    for (size_t i : sel) header += "\t" + bcf.samples[i];
+    header += "\n";
+    rc = w.write(header.data(), header.size());
+    if (rc) return rc;
+
+    tfbs_ctx *ctx = nullptr;
+    if (!merged.empty()) {
+        rc = tfbs_ctx_create(a->device, pp, &ctx);
+        if (rc) return rc;
+    }
+    std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
+    const uint32_t threads = std::max(1u, a->threads);
+    const size_t per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
+    uint32_t fake = 1;
+    std::vector<int32_t> gt(2 * sel.size());
+    std::vector<const BcfRecord *> recs;
+    for (size_t r0 = 0; r0 < merged.size(); r0 += per_batch) {
+        tfbs_batch *bb = nullptr;
+        rc = tfbs_batch_create(pp, (uint32_t)sel.size(), 1, &bb);
+        if (rc) return rc;
+        std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)> bguard(bb, tfbs_batch_destroy);
+        Batch &B = bb->b;
+        for (auto &b : beds) B.beds.push_back(b.first);
+        std::vector<RegionInput> ins;
+        for (size_t r = r0; r < std::min(merged.size(), r0 + per_batch); r++) {
+            const auto &m = merged[r];
+            RegionInput in;
+            in.R.ms = m.first;
+            in.R.me = m.second;
+            rc = tfbs_batch_region_ext(bb, m.first, m.second, &in.R.es, &in.R.ee);
+            if (rc) return rc;
+            std::string ref;
+            rc = fasta.fetch(chrom, in.R.es, in.R.ee + 1, ref);  // main.rs:156-161
+            if (rc) return rc;
+            in.ref.resize(ref.size());
+            for (size_t i = 0; i < ref.size(); i++) {
+                const int c = to_nuc((uint8_t)ref[i]);
+                if (c < 0) return fail(TFBS_E_BADBASE, "Unknown nucleotide " + std::to_string((int)(uint8_t)ref[i]));
+                in.ref[i] = (uint8_t)c;
+            }
+            // select_inner_peaks (main.rs:62-72): p.overlaps(merged)
+            for (size_t bi = 0; bi < beds.size(); bi++)
+                for (auto &p : beds[bi].second) {
+                    const bool ov = (m.first >= p.first && m.first <= p.second) ||
+                                    (m.second >= p.first && m.second <= p.second);
+                    if (ov) in.inner.push_back({(uint32_t)bi, {p.first, p.second}});
+                }
+            // load_diffs (haplotype.rs:78-80): name2rid(chrom).unwrap() panics on an unknown contig
+            if (rid < 0) return fail(TFBS_E_ARG, "chromosome " + chrom + " not in the BCF header");
+            bcf.fetch(rid, in.R.es, in.R.ee + 1, recs);
+            for (const BcfRecord *br : recs) {
+                for (size_t k = 0; k < sel.size(); k++) {
+                    gt[2 * k] = br->gt[2 * sel[k]];
+                    gt[2 * k + 1] = br->gt[2 * sel[k] + 1];
+                }
+                Record rec;
+                rc = make_record_gt((uint32_t)sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
+                                    br->n_alleles >= 2 ? br->alt.c_str() : nullptr, gt.data(), rec);
+                if (rc) return rc;
+                in.recs.push_back(std::move(rec));
+            }
+            ins.push_back(std::move(in));
+        }
+        rc = add_regions(B, ins, threads);
+        if (rc) return rc;
+        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_download(ctx, bb)))
+            return rc;
+        std::string rows;
+        rc = batch_rows(B, chrom, a->min_maf, &fake, rows);
+        if (rc) return rc;
+        rc = w.write(rows.data(), rows.size());
+        if (rc) return rc;
+        if (a->verbose) {
+            for (size_t r = 0; r < B.rh.size(); r++)
+                fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", r0 + r + 1, merged.size(),
+                        (unsigned long long)B.rh[r].ms, (unsigned long long)B.rh[r].me, B.rh[r].hap_count,
+                        B.rh[r].n_variants);
+        }
+    }
+    // the reference flushes twice before drop (main.rs:271, 275): two empty blocks
+    if ((rc = w.flush()) || (rc = w.flush()) || (rc = w.close())) return rc;
+    if (a->tabix) {
+        const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +
+                                part + "'";
+        if (system(cmd.c_str()) != 0) fprintf(stdout, "Failed to tabix file %s\n", out.c_str());
+    } else if (rename(part.c_str(), out.c_str()) != 0) {
+        return fail(TFBS_E_IO, "Could not rename " + part + " into " + out);
+    }
+    return TFBS_OK;
+}
+
+// ----------------------------------------------------------------------------
+// File-format entry points (f2-f4), for tests and embedding.
+// ----------------------------------------------------------------------------
+struct tfbs_bcf {
+    tfbs::Bcf b;
+    std::vector<const tfbs::BcfRecord *> cur;
+};
+
+int tfbs_bcf_open(const char *path, tfbs_bcf **out) {
+    if (!path || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    auto *b = new tfbs_bcf();
+    int rc = b->b.open(path);
+    if (rc) {
+        delete b;
+        return rc;
+    }
+    *out = b;
+    return TFBS_OK;
+}
+void tfbs_bcf_close(tfbs_bcf *b) { delete b; }
+size_t tfbs_bcf_num_samples(const tfbs_bcf *b) { return b ? b->b.samples.size() : 0; }
+const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i) {
+    return (b && i < b->b.samples.size()) ? b->b.samples[i].c_str() : nullptr;
+}
+int tfbs_bcf_fetch(tfbs_bcf *b, const char *chrom, uint64_t beg, uint64_t end, size_t *n) {
+    if (!b || !chrom || !n) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const int rid = b->b.contig_index(chrom);
+    if (rid < 0) return tfbs::fail(TFBS_E_ARG, std::string("unknown contig ") + chrom);
+    b->b.fetch(rid, beg, end, b->cur);
+    *n = b->cur.size();
+    return TFBS_OK;
+}
+int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, uint32_t *n_alleles, const char **ref,
+                    const char **alt, const int32_t **gt) {
+    if (!b || i >= b->cur.size()) return tfbs::fail(TFBS_E_ARG, "bad record index");
+    const tfbs::BcfRecord *r = b->cur[i];
+    if (pos) *pos = r->pos;
+    if (rlen) *rlen = r->rlen;
+    if (n_alleles) *n_alleles = r->n_alleles;
+    if (ref) *ref = r->ref.c_str();
+    if (alt) *alt = r->n_alleles >= 2 ? r->alt.c_str() : nullptr;
+    if (gt) *gt = r->gt.data();
+    return TFBS_OK;
+}
+
+int tfbs_fasta_fetch(const char *path, const char *chrom, uint64_t start, uint64_t stop, char **out, size_t *n) {
+    if (!path || !chrom || !out || !n) return tfbs::fail(TFBS_E_ARG, "null argument");
+    tfbs::Fasta f;
+    int rc = f.open(path);
+    if (rc) return rc;
+    std::string s;
+    rc = f.fetch(chrom, start, stop, s);
+    if (rc) return rc;
+    char *p = (char *)malloc(s.size() + 1);
+    memcpy(p, s.data(), s.size());
+    p[s.size()] = 0;
+    *out = p;
+    *n = s.size();
+    return TFBS_OK;
+}
+
+int tfbs_bgzf_write_file(const char *path, const char *text, size_t n, int flushes) {
+    if (!path || (n && !text)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    tfbs::BgzfWriter w;
+    int rc = w.open(path);
+    if (!rc) rc = w.write(text, n);
+    for (int i = 0; !rc && i < flushes; i++) rc = w.flush();
+    if (!rc) rc = w.close();
+    return rc;
+}
+
+int tfbs_bgzf_read_file(const char *path, char **out, size_t *n) {
+    if (!path || !out || !n) return tfbs::fail(TFBS_E_ARG, "null argument");
+    std::ifstream in(path, std::ios::binary);
+    if (!in) return tfbs::fail(TFBS_E_IO, std::string("Could not open file ") + path);
+    std::string raw((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>()), txt;
+    int rc = tfbs::bgzf_inflate(raw, txt);
+    if (rc) return rc;
+    char *p = (char *)malloc(txt.size() + 1);
+    memcpy(p, txt.data(), txt.size());
+    p[txt.size()] = 0;
+    *out = p;
+    *n = txt.size();
+    return TFBS_OK;
+}
+
+int tfbs_merge_ranges(const uint64_t *starts, const uint64_t *ends, size_t n, uint64_t *out_s, uint64_t *out_e,
+                      size_t *n_out) {
+    if (!n_out || (n && (!starts || !ends || !out_s || !out_e))) return tfbs::fail(TFBS_E_ARG, "null argument");
+    std::vector<std::pair<uint64_t, uint64_t>> r(n);
+    for (size_t i = 0; i < n; i++) r[i] = {starts[i], ends[i]};
+    auto m = tfbs::merge_ranges(r);
+    for (size_t i = 0; i < m.size(); i++) {
+        out_s[i] = m[i].first;
+        out_e[i] = m[i].second;
+    }
+    *n_out = m.size();
+    return TFBS_OK;
+}
+
+}  // extern "C"

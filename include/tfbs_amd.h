@@ -206,6 +206,54 @@ int tfbs_counts_as_genotypes(const uint32_t *left, const uint32_t *right, size_t
                              size_t info_cap, char *genotypes, size_t gt_cap);
 
 /* ------------------------------------------------------------------ */
+/* The find-tfbs command flow (main.rs:163-393) and its file formats     */
+/* (f2 BCF, f3 CLI + BGZF writer, f4 FASTA/BED)  */
+/* ------------------------------------------------------------------ */
+typedef struct tfbs_run_args {
+    const char *chromosome;        /* --chromosome */
+    const char *bcf;               /* --input */
+    const char *bed_files;         /* --bed (comma list) */
+    const char *reference;         /* --reference (FASTA with .fai) */
+    const char *samples_file;      /* --samples, NULL = all BCF samples */
+    const char *pwm_file;          /* --pwm_file */
+    const char *pwm_threshold_dir; /* --pwm_threshold_directory */
+    const char *pwm_names;         /* --pwm_names (comma list) */
+    const char *output;            /* --output (BGZF VCF) */
+    float pwm_threshold;           /* --pwm_threshold */
+    int forward_only;              /* --forward_only */
+    uint32_t min_maf;              /* --min_maf */
+    uint32_t threads;              /* --threads: host threads building regions */
+    uint64_t after_position;       /* --after_position */
+    int tabix;                     /* --tabix */
+    int verbose;                   /* --verbose */
+    int device;                    /* HIP device */
+    uint32_t regions_per_batch;    /* merged regions per GPU batch (0 = 512) */
+} tfbs_run_args;
+/* Replaces run() (main.rs:234-393): writes <output>.part, renames it to output. */
+int tfbs_run(const tfbs_run_args *args);
+
+typedef struct tfbs_bcf tfbs_bcf;
+/* Replaces rust-htslib IndexedReader::from_path / header().samples() (main.rs:46-52, 255). */
+int tfbs_bcf_open(const char *path, tfbs_bcf **out);
+void tfbs_bcf_close(tfbs_bcf *b);
+size_t tfbs_bcf_num_samples(const tfbs_bcf *b);
+const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i);
+/* Replaces reader.fetch(rid, beg, end) (haplotype.rs:79): records with pos < end && pos + rlen > beg. */
+int tfbs_bcf_fetch(tfbs_bcf *b, const char *chrom, uint64_t beg, uint64_t end, size_t *n_records);
+/* Record i of the last fetch: raw GT ints, 2 per BCF sample, INT32_MIN+1 = vector_end; alt NULL
+ * for a single-allele record. */
+int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, uint32_t *n_alleles, const char **ref,
+                    const char **alt, const int32_t **gt);
+/* Replaces bio fasta IndexedReader fetch(chrom, start, stop) + read (main.rs:156-161). */
+int tfbs_fasta_fetch(const char *fasta, const char *chrom, uint64_t start, uint64_t stop, char **out, size_t *n);
+/* BGZF writer as BGzWriter (main.rs:267-276): data blocks, `flushes` empty blocks, EOF block. */
+int tfbs_bgzf_write_file(const char *path, const char *text, size_t n, int flushes);
+int tfbs_bgzf_read_file(const char *path, char **out, size_t *n);
+/* RangeStack (range.rs:43-87): out arrays need n entries. */
+int tfbs_merge_ranges(const uint64_t *starts, const uint64_t *ends, size_t n, uint64_t *out_s, uint64_t *out_e,
+                      size_t *n_out);
+
+/* ------------------------------------------------------------------ */
 /* Synthetic workloads                            */
 /* ------------------------------------------------------------------ */
 /* Writes <dir>/pwms.txt and <dir>/thr/<name>.thr for n PWMs; lengths follow

@@ -121,6 +121,40 @@ def test_integration_one_polymorphism():
         open(os.path.join(GOLD, "expected_output_2.vcf")).read()
 
 
+@pytest.mark.parametrize("bcf,expected", [("genotypes.bcf", 1), ("genotypes2.bcf", 2)])
+def test_run_end_to_end_matches_reference_outputs(tmp_path, bcf, expected):
+    """main.rs:548-568 through the native flow (BCF reader, FASTA, BED merge, GPU scan,
+    BGZF writer): decompressed text identical to the reference's expected_output_N."""
+    out = tmp_path / "out.vcf.gz"
+    T.run("chr1", os.path.join(TD, bcf), [os.path.join(TD, "regions1.bed"), os.path.join(TD, "regions2.bed")],
+          os.path.join(TD, "reference_genome.fa"), os.path.join(TD, "samples"),
+          os.path.join(TD, "pwm_definitions.txt"), TD, 0.0001, ["ACGT"], str(out), False, False, 0, 1, 0, False)
+    want = open(os.path.join(GOLD, "expected_output_%d.vcf" % expected)).read()
+    assert T.bgzf_read(str(out)) == want
+    assert not os.path.exists(str(out) + ".part")
+
+
+def test_cli_binary(tmp_path):
+    import subprocess
+    exe = os.path.join(os.path.dirname(T.__file__), "bin", "find-tfbs-amd")
+    out = tmp_path / "cli.vcf.gz"
+    r = subprocess.run([exe, "--chromosome", "chr1", "--input", os.path.join(TD, "genotypes2.bcf"),
+                        "--bed", os.path.join(TD, "regions1.bed") + "," + os.path.join(TD, "regions2.bed"),
+                        "--reference", os.path.join(TD, "reference_genome.fa"), "--samples",
+                        os.path.join(TD, "samples"), "--pwm_file", os.path.join(TD, "pwm_definitions.txt"),
+                        "--pwm_threshold_directory", TD, "--pwm_threshold", "0.0001", "--pwm_names", "ACGT",
+                        "--output", str(out), "--threads", "2"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert T.bgzf_read(str(out)) == open(os.path.join(GOLD, "expected_output_2.vcf")).read()
+    # a missing bed file fails like bed.rs:34's panic (non-zero exit)
+    r2 = subprocess.run([exe, "--chromosome", "chr1", "--input", os.path.join(TD, "genotypes2.bcf"), "--bed",
+                         "/nonexistent.bed", "--reference", os.path.join(TD, "reference_genome.fa"), "--pwm_file",
+                         os.path.join(TD, "pwm_definitions.txt"), "--pwm_threshold_directory", TD,
+                         "--pwm_threshold", "0.0001", "--pwm_names", "ACGT", "--output", str(tmp_path / "y.gz")],
+                        capture_output=True, text=True, timeout=120)
+    assert r2.returncode != 0
+
+
 def test_config1_regions1_only():
     # BASELINE.json configs[0]: genotypes2.bcf + regions1.bed + ACGT -> the same single row
     got = _c1("genotypes2.records.json", ["regions1.bed"])
