@@ -8,8 +8,8 @@ LIBDIR := $(PKG)/lib
 OBJDIR := $(PKG)/lib/obj
 JOBS ?= 8
 
-HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
-HIP_SRCS := $(SRC)/device.hip
+HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/plan.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
+HIP_SRCS := $(SRC)/device.hip $(SRC)/scan_kernels.hip
 HDRS := $(wildcard $(SRC)/*.hpp) include/tfbs_amd.h
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
@@ -37,9 +37,9 @@ $(PKG)/bin/find-tfbs-amd: $(SRC)/cli.cpp include/tfbs_amd.h $(LIBDIR)/libtfbs_am
 oracle:
 	$(MAKE) -s -C oracle
 
-asm: $(SRC)/device.hip $(HDRS)
+asm: $(SRC)/scan_kernels.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
-	$(HIPCC) $(HIPFLAGS) -x hip --cuda-device-only -S $< -o $(OBJDIR)/device.s -Rpass-analysis=kernel-resource-usage
+	$(HIPCC) $(HIPFLAGS) -x hip --cuda-device-only -S $< -o $(OBJDIR)/scan_kernels.s -Rpass-analysis=kernel-resource-usage
 
 clean:
 	rm -rf $(LIBDIR) $(PKG)/bin oracle/_build

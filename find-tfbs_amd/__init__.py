@@ -147,6 +147,12 @@ class PatternSet:
     def max_length(self):
         return lib().tfbs_patterns_max_length(self.h)
 
+    def plan_stats(self, tile_blocks=16):
+        """Host-side summary of the device plan (octet/quad/generic strands, tiles)."""
+        st = _capi.tfbs_plan_stats()
+        check(lib().tfbs_patterns_plan_stats(self.h, tile_blocks, C.byref(st)))
+        return {n: getattr(st, n) for n, _ in st._fields_}
+
 
 def parse_pwm_files(pwm_file, threshold_dir, pwm_threshold, wanted_pwms, add_reverse_patterns=True):
     """pattern.rs:37-87.  Returns a PatternSet (index it or .to_list() for Pattern objects)."""

@@ -200,13 +200,20 @@ int parse_pwm_files(const std::string &pwm_file, const std::string &thr_dir, flo
 // ---------------------------------------------------------------------------
 // Device plan
 // ---------------------------------------------------------------------------
+struct Group { uint16_t pid; bool generic; uint32_t maxlen; std::vector<int> strands; };
+static std::vector<SlotGroup> groups_fast(const std::vector<Group> &groups) {
+    std::vector<SlotGroup> out;
+    for (uint32_t gi = 0; gi < groups.size(); gi++)
+        if (!groups[gi].generic) out.push_back({gi, groups[gi].strands});
+    return out;
+}
 // Strands are grouped by pattern_id (both strands of a PWM share it and their
 // hits add into one count, main.rs:505).  Groups are ordered by (needs the
 // generic kernel, longest strand, pattern_id) -- this order defines the count
-// slots -- so neighbouring strands have similar lengths and pack into quads
-// with little padding.  Fast tiles are runs of whole groups whose quad-blocks
+// slots -- so neighbouring strands have similar lengths and pack into units
+// with little padding.  Fast tiles are runs of whole groups whose table blocks
 // fit the LDS budget and span at most 64 slots.
-int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
+int Patterns::build_plan(uint32_t tile_blocks, Plan *plan) const {
     *plan = Plan();
     // Scannable strands: PWM with length >= 1.  A length-0 PWM with a negative
     // min_score panics in the reference at the first region (pattern.rs:150-156
@@ -222,7 +229,6 @@ int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
         by_pid[p.pattern_id].push_back((int)i);
     }
     if (pats.size() > 65535) return fail(TFBS_E_ARG, "more than 65535 patterns");
-    struct Group { uint16_t pid; bool generic; uint32_t maxlen; std::vector<int> strands; };
     std::vector<Group> groups;
     for (auto &kv : by_pid) {
         Group g{kv.first, false, 0, kv.second};
@@ -238,100 +244,7 @@ int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
         return a.pid < b.pid;
     });
     for (auto &g : groups) plan->slot_pid.push_back(g.pid);
-    auto nblk_of = [](uint32_t L) { return (L + 3) / 4; };
-
-    // --- fast tiles
-    // quad-blocks a tile needs when its strands (in order) are cut into quads
-    auto quad_blocks = [&](const std::vector<int> &strands) {
-        uint32_t total = 0;
-        for (size_t q = 0; q < strands.size(); q += kQuad) {
-            uint32_t m = 0;
-            for (size_t s = q; s < std::min(strands.size(), q + kQuad); s++) m = std::max(m, nblk_of(pats[strands[s]].len));
-            total += m;
-        }
-        return total;
-    };
-    std::vector<int> cur;                 // strands of the open tile
-    std::vector<uint32_t> cur_slot;       // their global slots
-    uint32_t cur_slot_begin = 0;
-    auto close_tile = [&]() {
-        if (cur.empty()) return;
-        DevTile t{};
-        t.first = (uint32_t)plan->fast_quads.size();
-        t.lut_begin = (uint32_t)(plan->lut.size() / kQuadBlockInts);
-        t.col_begin = (uint32_t)plan->colA.size();
-        t.slot_begin = cur_slot_begin;
-        t.lmin = UINT32_MAX;
-        uint32_t maxslot = 0;
-        for (size_t q0 = 0; q0 < cur.size(); q0 += kQuad) {
-            DevQuad Q{};
-            Q.lut_off = (uint32_t)(plan->lut.size() / kQuadBlockInts) - t.lut_begin;
-            const size_t n = std::min<size_t>(kQuad, cur.size() - q0);
-            Q.nstrand = (uint16_t)n;
-            for (size_t s = 0; s < kQuad; s++) {
-                if (s < n) {
-                    const Pat &p = pats[cur[q0 + s]];
-                    Q.nblk = (uint16_t)std::max<uint32_t>(Q.nblk, nblk_of(p.len));
-                    Q.min_score[s] = p.min_score;
-                    Q.len[s] = (uint16_t)p.len;
-                    Q.slot_local[s] = (uint16_t)(cur_slot[q0 + s] - cur_slot_begin);
-                    Q.orig_index[s] = (uint16_t)cur[q0 + s];
-                    Q.col_off[s] = (uint32_t)plan->colA.size() - t.col_begin;
-                    for (uint32_t j = 0; j < p.len; j++) plan->colA.push_back(p.w5[5 * j + 0]);
-                    t.lmin = std::min<uint32_t>(t.lmin, p.len);
-                    maxslot = std::max(maxslot, cur_slot[q0 + s]);
-                } else {  // padding strand: never matches
-                    Q.min_score[s] = INT32_MAX;
-                    Q.len[s] = 0;
-                    Q.slot_local[s] = 0;
-                    Q.orig_index[s] = 0xFFFF;
-                    Q.col_off[s] = 0;
-                }
-            }
-            // interleaved 4-mer tables: entry[b][code][s] = sum_{j<4, 4b+j<L_s} w_s[4b+j][(code >> 2j) & 3]
-            // (i32 wrapping, as the reference's i32 sum in --release)
-            for (uint32_t b = 0; b < Q.nblk; b++) {
-                for (int code = 0; code < kLutEntries; code++) {
-                    for (size_t s = 0; s < kQuad; s++) {
-                        uint32_t v = 0;
-                        if (s < n) {
-                            const Pat &p = pats[cur[q0 + s]];
-                            for (uint32_t j = 0; j < 4; j++) {
-                                const uint32_t col = 4 * b + j;
-                                if (col >= p.len) break;
-                                v += (uint32_t)p.w5[5 * col + ((code >> (2 * j)) & 3)];
-                            }
-                        }
-                        plan->lut.push_back((int32_t)v);
-                    }
-                }
-            }
-            plan->fast_quads.push_back(Q);
-        }
-        t.last = (uint32_t)plan->fast_quads.size();
-        t.nblocks = (uint32_t)(plan->lut.size() / kQuadBlockInts) - t.lut_begin;
-        t.ncols = (uint32_t)plan->colA.size() - t.col_begin;
-        t.nslots = maxslot - cur_slot_begin + 1;
-        plan->fast_tiles.push_back(t);
-        cur.clear();
-        cur_slot.clear();
-    };
-    for (uint32_t gi = 0; gi < groups.size(); gi++) {
-        const Group &g = groups[gi];
-        if (g.generic) continue;
-        if (!cur.empty()) {
-            std::vector<int> trial = cur;
-            trial.insert(trial.end(), g.strands.begin(), g.strands.end());
-            if (quad_blocks(trial) > tile_quad_blocks || gi - cur_slot_begin + 1 > (uint32_t)kMaxTileSlots)
-                close_tile();
-        }
-        if (cur.empty()) cur_slot_begin = gi;
-        for (int i : g.strands) {
-            cur.push_back(i);
-            cur_slot.push_back(gi);
-        }
-    }
-    close_tile();
+    build_fast_tiles(*this, groups_fast(groups), tile_blocks, plan);
     // --- generic (long) strands: one tile per pattern_id group, weights x5
     for (uint32_t gi = 0; gi < groups.size(); gi++) {
         const Group &g = groups[gi];
@@ -347,9 +260,9 @@ int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
             DevPattern d{};
             d.col_off = (uint32_t)(plan->gen_w.size() / 5);
             d.min_score = p.min_score;
-            d.len = (uint16_t)p.len;
+            d.len = p.len;
             d.slot_local = 0;
-            d.orig_index = (uint16_t)i;
+            d.orig_index = (uint32_t)i;
             t.lmin = std::min<uint32_t>(t.lmin, p.len);
             plan->gen_pats.push_back(d);
             for (uint32_t j = 0; j < p.len; j++)
@@ -358,11 +271,7 @@ int Patterns::build_plan(uint32_t tile_quad_blocks, Plan *plan) const {
         t.last = (uint32_t)plan->gen_pats.size();
         plan->gen_tiles.push_back(t);
     }
-    for (auto &t : plan->fast_tiles) {
-        plan->max_tile_blocks = std::max(plan->max_tile_blocks, t.nblocks);
-        plan->max_tile_cols = std::max(plan->max_tile_cols, t.ncols);
-        plan->max_tile_quads = std::max(plan->max_tile_quads, t.last - t.first);
-    }
+    for (auto &t : plan->fast_tiles) plan->max_tile_blocks = std::max(plan->max_tile_blocks, t.nblocks);
     return TFBS_OK;
 }
 
@@ -491,6 +400,23 @@ const char *tfbs_patterns_name_of(const tfbs_patterns *p, uint16_t pid) {
 uint32_t tfbs_patterns_max_length(const tfbs_patterns *p) { return p ? p->p.max_length() : 0; }
 
 void tfbs_patterns_destroy(tfbs_patterns *p) { delete p; }
+
+int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, tfbs_plan_stats *out) {
+    if (!p || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    tfbs::Plan plan;
+    int rc = p->p.build_plan(tile_blocks, &plan);
+    if (rc) return rc;
+    *out = tfbs_plan_stats{};
+    out->n_octet_strands = plan.n_octet_strands;
+    out->n_quad_strands = plan.n_quad_strands;
+    out->n_generic_strands = (uint32_t)plan.gen_pats.size();
+    out->n_fast_tiles = (uint32_t)plan.fast_tiles.size();
+    out->n_fast_units = (uint32_t)plan.fast_units.size();
+    out->n_generic_tiles = (uint32_t)plan.gen_tiles.size();
+    out->max_tile_blocks = plan.max_tile_blocks;
+    out->lut_bytes = (uint64_t)plan.lut.size() * 4;
+    return TFBS_OK;
+}
 
 }  // extern "C"
 

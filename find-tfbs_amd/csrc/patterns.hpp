@@ -22,16 +22,16 @@ struct Pat {  // Pattern (types.rs:86-90)
 
 struct Plan {
     std::vector<uint16_t> slot_pid;  // slot -> pattern_id
-    std::vector<DevQuad> fast_quads;
+    std::vector<DevUnit> fast_units;
     std::vector<DevTile> fast_tiles;
-    std::vector<int32_t> lut;        // quad-blocks x 256 codes x 4 strands
-    std::vector<int32_t> colA;       // per fast-strand column: weight of A (N correction)
+    std::vector<int32_t> lut;        // blocks x 256 codes x 16 bytes (8 x int16 or 4 x int32)
+    std::vector<int32_t> wfull;      // per fast-strand column: [A,C,G,T] weights (windows containing N)
     std::vector<DevPattern> gen_pats;
     std::vector<DevTile> gen_tiles;
     std::vector<int32_t> gen_w;      // per generic column: 5 weights
     uint32_t max_tile_blocks = 0;
-    uint32_t max_tile_cols = 0;
-    uint32_t max_tile_quads = 0;
+    uint32_t n_octet_strands = 0;
+    uint32_t n_quad_strands = 0;
     bool zero_len_panics = false;
 };
 
@@ -40,8 +40,14 @@ struct Patterns {
     std::map<uint16_t, std::string> names;
     void add(const Pat &p);
     uint32_t max_length() const;
-    int build_plan(uint32_t tile_quad_blocks, Plan *plan) const;
+    int build_plan(uint32_t tile_blocks, Plan *plan) const;
 };
+
+struct SlotGroup {  // the strands of one pattern_id and its count slot
+    uint32_t slot;
+    std::vector<int> strands;
+};
+void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t tile_blocks, Plan *plan);
 
 int parse_weight(const std::string &s, int32_t *out);
 int parse_threshold_file(const std::string &path, float thr, int32_t *out);

@@ -1,0 +1,48 @@
+// Launch interface of the scan kernels (scan_kernels.hip), used by device.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "tfbs_internal.hpp"
+
+namespace tfbs {
+
+// Everything a scan launch reads or writes (device pointers).
+struct ScanArgs {
+    const DevTile *tiles;
+    uint32_t n_tiles;
+    const DevUnit *units;       // fast path: units; generic path: unused
+    const DevPattern *gpats;    // generic path
+    const int32_t *lut;         // fast path: 4 KiB table blocks
+    const int32_t *wfull;       // fast path: [A,C,G,T] per column (windows containing N)
+    const int32_t *gw;          // generic path: 5 weights per column
+    const DevHap *haps;
+    uint32_t n_haps;
+    const DevRegion *regions;
+    const int32_t *inner;
+    const uint32_t *words;
+    const uint32_t *nmask;
+    const int32_t *posrel;
+    uint32_t *counts;
+    uint32_t haps_per_block;
+    unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
+    uint32_t hits_wpp;
+    uint32_t n_patterns_total;
+};
+
+struct LaunchConfig {
+    uint32_t fast_block = 512;  // threads per fast workgroup
+    int minw = 2;               // __launch_bounds__ min waves per SIMD of the fast kernel
+    size_t lds_bytes = 0;       // dynamic LDS of the fast kernel
+};
+
+// Enqueues the fast and/or generic scan over n_haps haplotypes on `stream`
+// (grids split below 2^31 workgroups).  Returns launches issued or <0.
+int launch_fast(const ScanArgs &a, const LaunchConfig &cfg, uint32_t n_haps, hipStream_t stream);
+int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
+// Opts the fast kernel into more than 64 KiB of dynamic LDS.
+int fast_kernel_set_lds(const LaunchConfig &cfg);
+
+}  // namespace tfbs

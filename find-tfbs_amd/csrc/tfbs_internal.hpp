@@ -25,46 +25,59 @@ inline int to_nuc(uint8_t c) {
 }
 
 // ---------------------------------------------------------------------------
-// Device-side descriptors (POD, shared with the kernels)
+// Device-side descriptors (POD, shared with the kernels).  All fields are
+// 32-bit: the kernels read descriptors at wave-uniform addresses and gfx950
+// scalar loads (s_load) exist only at dword granularity.
 // ---------------------------------------------------------------------------
 constexpr int kLutEntries = 256;   // one 4-mer block: 4^4 codes
-constexpr int kQuad = 4;           // strands interleaved per LUT entry (one ds_read_b128)
-constexpr int kQuadBlockInts = kLutEntries * kQuad;  // 4 KiB per quad-block
+constexpr int kBlockBytes = 4096;  // one table block: 256 codes x 16 bytes (one ds_read_b128 per lookup)
+constexpr int kBlockInts = kBlockBytes / 4;
+constexpr int kUnitMax = 8;        // strands per unit (octet)
 constexpr int kFastMaxLen = 32;    // the LUT path reads a 64-bit (32-base) window per lane
 constexpr int kMaxInnerPass = 8;   // inner ranges handled per pass (accumulators per lane)
 constexpr int kMaxTileSlots = 64;  // pattern_id slots per tile: one lane each
 
-// Four PWM strands scored together: their 4-mer tables are interleaved so one
-// 16-byte LDS read returns the four strands' partial sums for a code.
-struct DevQuad {
-    uint32_t lut_off;          // quad-block offset inside the tile's LDS image
-    uint16_t nblk;             // max ceil(len / 4) over the strands
-    uint16_t nstrand;          // 1..4 real strands (the rest never match)
-    int32_t min_score[kQuad];
-    uint16_t len[kQuad];
-    uint16_t slot_local[kQuad];  // pattern_id slot relative to the tile's first slot
-    uint16_t orig_index[kQuad];  // index in creation order (tfbs_matches)
-    uint32_t col_off[kQuad];     // A-weight columns (N correction) inside the tile's colA image
+enum UnitKind : uint32_t {
+    // 8 strands, int16 partial sums biased to <= 0 per block, saturating packed adds:
+    // hit iff sum > thr where thr = min_score - sum(block maxima) (exact, see plan)
+    UNIT_OCTET16 = 0,
+    // 4 strands, int32 partial sums (wrapping like the reference's i32)
+    UNIT_QUAD32 = 1,
+};
+
+// A unit of strands scored together: their 4-mer tables are interleaved so one
+// 16-byte LDS read returns every strand's partial sum for a code.
+struct DevUnit {
+    uint32_t lut_off;              // block offset inside the tile's LDS image
+    uint32_t nblk;                 // max ceil(len / 4) over the strands
+    uint32_t nstrand;              // real strands (the rest never match)
+    uint32_t kind;                 // UnitKind
+    uint32_t init[4];              // OCTET16: packed accumulator start -(thr + 1) per strand
+    int32_t thr[kUnitMax];         // OCTET16: biased threshold; QUAD32: min_score
+    int32_t min_score[kUnitMax];   // pattern.rs:151 threshold (windows containing N)
+    uint32_t len[kUnitMax];
+    uint32_t slot_local[kUnitMax]; // pattern_id slot relative to the tile's first slot
+    uint32_t orig_index[kUnitMax]; // index in creation order (tfbs_matches)
+    uint32_t wofs[kUnitMax];       // first column of the strand in the full weight table
 };
 
 struct DevPattern {        // one long strand (generic kernel)
     uint32_t col_off;      // offset of this pattern's columns in the generic weights (x5)
     int32_t min_score;
-    uint16_t len;
-    uint16_t slot_local;
-    uint16_t orig_index;
-    uint16_t pad;
+    uint32_t len;
+    uint32_t slot_local;
+    uint32_t orig_index;
+    uint32_t pad;
 };
 
 struct DevTile {
-    uint32_t first, last;         // quad range (fast) or pattern range (generic)
-    uint32_t lut_begin;           // first quad-block (global)
-    uint32_t nblocks;             // quad-blocks in the tile
-    uint32_t col_begin;           // first colA entry (global)
-    uint32_t ncols;
+    uint32_t first, last;         // unit range (fast) or pattern range (generic)
+    uint32_t lut_begin;           // first block (global)
+    uint32_t nblocks;             // blocks in the tile
     uint32_t slot_begin;          // global pattern_id slot of local slot 0
     uint32_t nslots;
     uint32_t lmin;                // shortest strand (bounds the windows to scan)
+    uint32_t pad;
 };
 
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };

@@ -153,3 +153,33 @@ def test_batch_grouping_matches_oracle(tmp_path, indel):
         assert b.region_stats(i) == (nh, nv)
     assert b.num_haplotypes == sum(s[0] for s in stats)
     assert b.num_windows > 0 and b.num_effective_windows >= b.num_windows
+
+
+def _plan(w4, ms):
+    p = T.Pattern.PWM([T.Weight(*r) for r in w4], "x", 0, ms, 0)
+    return T.PatternSet.from_patterns([p]).plan_stats()
+
+
+def test_plan_octet_eligibility():
+    """plan.cpp: a strand takes the 16-bit octet path iff every 4-column block spans
+    <= 32767, no i32 wrap is possible and min_score - sum(block maxima) >= -32768."""
+    w = [[0, -1000, -500, -2000]] * 8          # best 0, worst -16000
+    assert _plan(w, -32768)["n_octet_strands"] == 1
+    assert _plan(w, -32769)["n_quad_strands"] == 1
+    assert _plan(w, 10**6)["n_octet_strands"] == 1  # threshold above the best: thr clamps to 0
+    span = [[0, -32767, 0, 0]] + [[0, 0, 0, 0]] * 3
+    assert _plan(span, -100)["n_octet_strands"] == 1
+    span = [[0, -32768, 0, 0]] + [[0, 0, 0, 0]] * 3
+    assert _plan(span, -100)["n_quad_strands"] == 1
+    assert _plan([[2**30, 0, 0, 0]] * 2, 0)["n_quad_strands"] == 1
+    long = [[0, 1, 2, 3]] * 33
+    st = _plan(long, 5)
+    assert st["n_generic_strands"] == 1 and st["n_fast_tiles"] == 0
+
+
+def test_plan_tiles_cover_every_strand(tmp_path):
+    ps, _ = synth_patterns(tmp_path, 120, 3, 4)
+    for tb in (8, 16, 32):
+        st = ps.plan_stats(tb)
+        assert st["n_octet_strands"] + st["n_quad_strands"] + st["n_generic_strands"] == len(ps)
+        assert st["max_tile_blocks"] <= max(tb, 8)

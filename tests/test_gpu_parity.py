@@ -80,6 +80,71 @@ def test_matches_fuzz_vs_oracle():
         sc.close()
 
 
+def _scores(w4, seq):
+    """Window scores of pattern.rs:125-135 (N = 0), i32 wrapping."""
+    L = len(w4)
+    out = []
+    for i in range(len(seq) - L + 1):
+        s = 0
+        for j in range(L):
+            c = "ACGTN".index(seq[i + j])
+            s += w4[j][c] if c < 4 else 0
+        out.append(((s + 2**31) % 2**32) - 2**31)
+    return out
+
+
+def octet_boundary_patterns(rnd, seq):
+    """PWMs placed on the edges of the 16-bit octet path (plan.cpp): thresholds tied
+    with / one below a real window score, biased thresholds of exactly -32768 and
+    -32769, block ranges of 32767 and 32768, i32-wrapping weights, thresholds above
+    the best score."""
+    pats = []
+
+    def add(w4, ms):
+        pats.append(T.Pattern.PWM([T.Weight(*r) for r in w4], "B%d" % len(pats), len(pats) // 2, ms,
+                                  len(pats) % 2))
+
+    for L in (1, 4, 9, 16, 23, 32):
+        w4 = [[rnd.randint(-2100, 0) for _ in range(4)] for _ in range(L)]
+        best = sum(max(r) for r in w4)
+        sc = sorted(_scores(w4, seq.replace("N", "A")))
+        top = sc[-1 - rnd.randint(0, 5)]
+        add(w4, top)          # tie: never a hit for that window
+        add(w4, top - 1)      # one below: a hit
+        add(w4, best - 32768)  # biased threshold exactly -32768 (octet)
+        add(w4, best - 32769)  # -32769: quad
+        add(w4, best)          # nothing can exceed the best score
+        add(w4, best + 5)
+    # a block whose range is exactly 32767 (octet) / 32768 (quad)
+    for span in (32767, 32768):
+        w4 = [[0, -span, 0, 0]] + [[0, 0, 0, 0]] * 3 + [[rnd.randint(-50, 50) for _ in range(4)] for _ in range(4)]
+        add(w4, -span + 10)
+        add(w4, 20)
+    # i32 wrap (pattern.rs sums in i32): quad path must wrap like the reference
+    w4 = [[2**30, 2**30 - 7, -2**31, 5] for _ in range(6)]
+    add(w4, 0)
+    add(w4, -2**31)
+    return pats
+
+
+def test_octet_boundaries_vs_oracle():
+    rnd = random.Random(5)
+    base = "".join(rnd.choice("ACGT") for _ in range(700))
+    pats = octet_boundary_patterns(rnd, base)
+    st = T.PatternSet.from_patterns(pats).plan_stats()
+    assert st["n_octet_strands"] > 0 and st["n_quad_strands"] > 0, st
+    sc = T.Scanner(pats)
+    try:
+        for trial, seq in enumerate([base, base[:300] + "N" + base[301:520] + "NN" + base[522:], base[:33], ""]):
+            hap = _hap(seq, 5000)
+            got = sc.matches_all(hap)
+            for i, p_ in enumerate(pats):
+                w5 = [wt.acgtn for wt in p_.weights]
+                assert got[i] == O.matches(w5, p_.min_score, hap, kind=p_.kind), (trial, i)
+    finally:
+        sc.close()
+
+
 # ------------------------------------------------------------ main.rs:548-568 through the product
 def _c1(bcf_json, beds_files, samples_file=True):
     rec = json.load(open(os.path.join(GOLD, bcf_json)))
