@@ -63,7 +63,7 @@ struct tfbs_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     const Patterns *pats = nullptr;
     Plan plan;
-    uint32_t tile_blocks = 16;    // table blocks (4 KiB each) per LDS tile
+    uint32_t tile_blocks = 20;    // table blocks (4 KiB each) per LDS tile: 80 KiB, two workgroups per CU
     uint32_t haps_per_block = 128;
     LaunchConfig cfg;
     DevBuf<DevUnit> fast_units;
@@ -166,7 +166,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     auto *ctx = new tfbs_ctx();
     ctx->device = device;
     ctx->pats = &tfbs::patterns_of(p);
-    ctx->tile_blocks = (uint32_t)std::min(36, std::max(8, env_int("TFBS_TILE_BLOCKS", 16)));
+    ctx->tile_blocks = (uint32_t)std::min(36, std::max(8, env_int("TFBS_TILE_BLOCKS", 20)));
     ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 128));
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     rc = ctx->pats->build_plan(ctx->tile_blocks, &ctx->plan);
@@ -187,9 +187,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         return tfbs::fail(TFBS_E_HIP, std::string("HIP init: ") + hipGetErrorString(e));
     }
     const Plan &P = ctx->plan;
-    size_t max_units = 0;
-    for (const DevTile &t : P.fast_tiles) max_units = std::max<size_t>(max_units, t.last - t.first);
-    ctx->cfg.lds_bytes = (size_t)P.max_tile_blocks * kBlockBytes + max_units * sizeof(DevUnit);
+    ctx->cfg.lds_bytes = (size_t)P.max_tile_blocks * kBlockBytes;
     if (ctx->cfg.lds_bytes > 160 * 1024) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "pattern tile exceeds the 160 KiB LDS");

@@ -34,7 +34,12 @@
 namespace tfbs {
 namespace {
 
-constexpr int kChunks = 4;  // 64-window chunks per lane group (256 windows per pass)
+constexpr int kChunks = 4;
+
+// Unit descriptors are read through the constant address space so that the
+// wave-uniform field loads become scalar loads (s_load) even though the kernel
+// also stores to global memory.
+typedef const __attribute__((address_space(4))) DevUnit CUnit;  // 64-window chunks per lane group (256 windows per pass)
 constexpr int kGenBlock = 256;
 
 // Count, for every inner range of this pass, the hit windows whose match range
@@ -91,10 +96,11 @@ __device__ __forceinline__ uint32_t pk_add_sat_i16(uint32_t a, uint32_t b) {
     return r;
 }
 
+// Table lookups of NB blocks for NCH chunks, added into sum.
 // Threshold test of strand s of a unit for every chunk (hit ballots), with the
 // windows that contain an N rescored exactly, then the counting on a hit.
 template <int NCH, bool OCT>
-__device__ __forceinline__ void strand_hits(const ScanArgs &A, const DevUnit &U, int s, const uint32_t (&sum)[NCH][4],
+__device__ __forceinline__ void strand_hits(const ScanArgs &A, CUnit &U, int s, const uint32_t (&sum)[NCH][4],
                                             const Win<NCH> &W, const DevHap &hm, bool has_n, uint32_t h, uint32_t cg,
                                             const int32_t *inner, uint32_t n_pass, bool write_hits, uint32_t lane,
                                             uint32_t (&acc)[kMaxInnerPass]) {
@@ -135,7 +141,7 @@ __device__ __forceinline__ void strand_hits(const ScanArgs &A, const DevUnit &U,
 // a clear sign bit iff some strand of some window may hit -- one wave-uniform
 // test gates the per-strand work.  QUAD32: per-strand compares.
 template <int NCH, bool OCT>
-__device__ __forceinline__ void unit_body(const ScanArgs &A, const DevUnit &U, const char *s_lut, const Win<NCH> &W,
+__device__ __forceinline__ void unit_body(const ScanArgs &A, CUnit &U, const char *s_lut, const Win<NCH> &W,
                                           const DevHap &hm, bool has_n, uint32_t h, uint32_t cg, const int32_t *inner,
                                           uint32_t n_pass, bool write_hits, uint32_t lane,
                                           uint32_t (&acc)[kMaxInnerPass]) {
@@ -183,7 +189,7 @@ __device__ __forceinline__ void unit_body(const ScanArgs &A, const DevUnit &U, c
 // Score NCH 64-window chunks starting at window cg against every unit of the tile.
 template <int NCH>
 __device__ __forceinline__ void scan_chunks(const ScanArgs &A, const DevTile &t, const char *s_lut,
-                                            const DevUnit *s_units, const DevHap &hm, uint32_t h, uint32_t cg,
+                                            CUnit *s_units, const DevHap &hm, uint32_t h, uint32_t cg,
                                             const int32_t *inner, uint32_t n_pass, bool write_hits, uint32_t lane,
                                             uint32_t (&acc)[kMaxInnerPass]) {
     const bool has_n = (hm.flags & HAP_HAS_N) != 0;
@@ -213,7 +219,7 @@ __device__ __forceinline__ void scan_chunks(const ScanArgs &A, const DevTile &t,
         }
     }
     for (uint32_t ui = 0; ui < t.last - t.first; ui++) {
-        const DevUnit &U = s_units[ui];
+        CUnit &U = s_units[ui];
         if (U.kind == UNIT_OCTET16)
             unit_body<NCH, true>(A, U, s_lut, W, hm, has_n, h, cg, inner, n_pass, write_hits, lane, acc);
         else
@@ -239,14 +245,11 @@ __global__ __launch_bounds__(512, MINW) void scan_fast_kernel(ScanArgs A) {
         uint4 *dst = reinterpret_cast<uint4 *>(smem);
         const uint32_t n4 = t.nblocks * (kBlockInts / 4);
         for (uint32_t i = threadIdx.x; i < n4; i += kBlock) dst[i] = src[i];
-        const uint32_t *usrc = reinterpret_cast<const uint32_t *>(A.units + t.first);
-        uint32_t *udst = reinterpret_cast<uint32_t *>(smem + t.nblocks * kBlockInts);
-        const uint32_t nu = (t.last - t.first) * (uint32_t)(sizeof(DevUnit) / 4);
-        for (uint32_t i = threadIdx.x; i < nu; i += kBlock) udst[i] = usrc[i];
     }
     __syncthreads();
     const char *s_lut = reinterpret_cast<const char *>(smem);
-    const DevUnit *s_units = reinterpret_cast<const DevUnit *>(smem + t.nblocks * kBlockInts);
+    // unit descriptors stay in global memory: wave-uniform, read with scalar loads
+    CUnit *s_units = (CUnit *)(A.units + t.first);
 
     for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
         const uint32_t h = hg * A.haps_per_block + hh;
