@@ -148,6 +148,14 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
 
+    # after the timed region: the two ways the counts leave the GPU
+    t_red = time.perf_counter()
+    T.check(L.tfbs_batch_reduce(sc.h, batch.h))
+    t_red = time.perf_counter() - t_red
+    t_dense = time.perf_counter()
+    T.check(L.tfbs_batch_download(sc.h, batch.h))
+    t_dense = time.perf_counter() - t_dense
+
     windows = batch.num_windows
     regions = batch.num_regions
     if dist is not None:
@@ -204,6 +212,8 @@ def main():
             "kernel_ms_avg": kms,
             "host_prep_s": t_prep,
             "upload_s": t_up,
+            "key_reduce_s": t_red,
+            "dense_download_s": t_dense,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "note": "algorithmic bytes/launch = packed haplotypes + metadata + pattern tables "

@@ -351,11 +351,15 @@ class RegionBatch:
         check(lib().tfbs_batch_region_stats(self.h, r, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def scan(self, scanner, upload=True, download=True):
+    def scan(self, scanner, upload=True, download=True, reduce=False):
+        """tfbs_scan; then either download the dense counts or (reduce=True) classify the
+        keys on the GPU and fetch only what row emission needs (tfbs_batch_reduce)."""
         if upload:
             check(lib().tfbs_batch_upload(scanner.h, self.h))
         check(lib().tfbs_scan(scanner.h, self.h))
-        if download:
+        if reduce:
+            check(lib().tfbs_batch_reduce(scanner.h, self.h))
+        elif download:
             check(lib().tfbs_batch_download(scanner.h, self.h))
 
     def keys(self, region):

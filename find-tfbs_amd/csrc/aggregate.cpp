@@ -32,11 +32,41 @@ struct Membership {
     }
 };
 
-inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint32_t slot, int32_t range_slot) {
-    const DevHap &h = B.haps[R.hap_begin + local];
-    const uint32_t n_inner = (uint32_t)R.ranges.size();
-    return B.counts[h.count_off + (uint64_t)slot * n_inner + (uint32_t)range_slot];
+inline uint64_t key_of(const Batch &B, const RegionH &R, uint32_t slot, int32_t range_slot) {
+    return R.key_off + (uint64_t)slot * R.ranges.size() + (uint32_t)range_slot;
 }
+
+// Count of distinct haplotype `local` for a key, from the dense download or
+// from the device key reduction (tfbs_batch_reduce).
+inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint32_t slot, int32_t range_slot) {
+    if (B.counts_valid) {
+        const DevHap &h = B.haps[R.hap_begin + local];
+        const uint32_t n_inner = (uint32_t)R.ranges.size();
+        return B.counts[h.count_off + (uint64_t)slot * n_inner + (uint32_t)range_slot];
+    }
+    const uint64_t k = key_of(B, R, slot, range_slot);
+    const uint32_t off = B.var_off[k];
+    return off == UINT32_MAX ? B.key_first[k] : B.var_counts[off + local];
+}
+
+// Some distinct haplotype matched (the key exists in the reference's HashMap).
+inline bool key_any(const Batch &B, const RegionH &R, uint32_t slot, int32_t range_slot) {
+    if (!B.counts_valid) return (B.key_flags[key_of(B, R, slot, range_slot)] & KEY_ANY) != 0;
+    bool any = false;
+    for (uint32_t l = 0; l < R.hap_count && !any; l++) any = count_of(B, R, l, slot, range_slot) != 0;
+    return any;
+}
+
+// Distinct haplotypes disagree (otherwise every sample has the same total: no row).
+inline bool key_varies(const Batch &B, const RegionH &R, uint32_t slot, int32_t range_slot) {
+    if (!B.counts_valid) return (B.key_flags[key_of(B, R, slot, range_slot)] & KEY_VARIES) != 0;
+    const uint32_t c0 = count_of(B, R, 0, slot, range_slot);
+    for (uint32_t h = 1; h < R.hap_count; h++)
+        if (count_of(B, R, h, slot, range_slot) != c0) return true;
+    return false;
+}
+
+inline bool have_counts(const Batch &B) { return B.counts_valid || B.reduced; }
 
 // Keys of a region in row order (inner.start, inner.end, bed index, pattern_id)
 // that exist in the reference's HashMap, i.e. got at least one match.
@@ -44,11 +74,8 @@ std::vector<KeyRef> region_keys(const Batch &B, const RegionH &R) {
     std::vector<KeyRef> out;
     for (const InnerKey &k : R.keys) {
         if (k.slot < 0) continue;  // empty range: no match can overlap it
-        for (uint32_t s : B.slots_by_pid) {
-            bool any = false;
-            for (uint32_t l = 0; l < R.hap_count && !any; l++) any = count_of(B, R, l, s, k.slot) != 0;
-            if (any) out.push_back({&k, s});
-        }
+        for (uint32_t s : B.slots_by_pid)
+            if (key_any(B, R, s, k.slot)) out.push_back({&k, s});
     }
     return out;  // R.keys is sorted by (s, e, bed); slots_by_pid ascends with pattern_id
 }
@@ -114,7 +141,7 @@ static std::string strip_chr(const std::string &c) {
 }
 
 int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out) {
-    if (!B.counts_valid) return fail(TFBS_E_STATE, "counts not downloaded");
+    if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
     const std::string chr = strip_chr(chrom);
     const uint32_t H = 2 * B.n_samples;
@@ -123,11 +150,7 @@ int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint3
         if (R.hap_count == 0) continue;
         Membership M(R, H);
         for (const KeyRef &k : region_keys(B, R)) {
-            // all distinct haplotypes equal -> every sample has the same total: no row
-            const uint32_t c0 = count_of(B, R, 0, k.slot, k.ik->slot);
-            bool varies = false;
-            for (uint32_t h = 1; h < R.hap_count && !varies; h++) varies = count_of(B, R, h, k.slot, k.ik->slot) != c0;
-            if (!varies) continue;
+            if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
             for (uint32_t s = 0; s < B.n_samples; s++) {
                 l[s] = count_of(B, R, M.local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
                 r[s] = count_of(B, R, M.local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
@@ -167,7 +190,7 @@ extern "C" {
 
 int tfbs_batch_region_num_keys(const tfbs_batch *b, size_t region, size_t *n) {
     if (!b || !n || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
-    if (!b->b.counts_valid) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (!tfbs::have_counts(b->b)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
     *n = tfbs::region_keys(b->b, b->b.rh[region]).size();
     return TFBS_OK;
 }
@@ -176,7 +199,7 @@ int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t
                           uint16_t *pid, uint32_t *left, uint32_t *right) {
     if (!b || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     const Batch &B = b->b;
-    if (!B.counts_valid) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples && (left || right))
         return tfbs::fail(TFBS_E_STATE, "batch created without membership");
     const tfbs::RegionH &R = B.rh[region];

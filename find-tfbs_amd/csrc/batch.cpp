@@ -260,6 +260,9 @@ void commit_region(Batch &B, RegionBuilt &&built) {
     DevRegion dr{};
     dr.inner_off = (uint32_t)(B.inner.size() / 2);
     dr.n_inner = (uint32_t)R.ranges.size();
+    dr.hap_begin = R.hap_begin;
+    dr.hap_count = R.hap_count;
+    R.key_off = (uint64_t)dr.inner_off * B.n_slots;
     for (auto &r : R.ranges) {
         // positions relative to ext_start, clamped: only containment of small
         // non-negative positions is ever tested, which clamping preserves.
@@ -451,7 +454,7 @@ int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads) {
     for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
     work();
     for (auto &t : ts) t.join();
-    B.counts_valid = false;
+    B.counts_valid = B.reduced = false;
     for (size_t j = 0; j < n; j++) {
         if (rcs[j]) return rcs[j];
         commit_region(B, std::move(built[j]));
@@ -495,7 +498,7 @@ int tfbs_batch_region_end(tfbs_batch *b) {
     Batch &B = b->b;
     B.open = false;
     if (B.status) return B.status;
-    B.counts_valid = false;
+    B.counts_valid = B.reduced = false;
     tfbs::RegionInput in;
     in.R = std::move(B.cur);
     in.ref = std::move(B.cur_ref);

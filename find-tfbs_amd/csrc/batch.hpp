@@ -30,6 +30,7 @@ struct RegionH {
     uint32_t hap_begin = 0, hap_count = 0;  // distinct haplotypes (batch-global indices)
     int32_t ref_local = -1;                 // local index of the reference-group haplotype, -1 if none
     uint32_t n_variants = 0;
+    uint64_t key_off = 0;                   // first key (slot * n_inner + range) in the reduced arrays
     std::vector<InnerKey> keys;             // sorted by (s, e, bed)
     std::vector<std::pair<uint64_t, uint64_t>> ranges;  // distinct non-empty inner ranges
     // membership: haplotype id -> local distinct index; ids not listed use ref_local
@@ -57,6 +58,15 @@ struct Batch {
     uint64_t n_counts = 0;                // u32 counts the scan writes
     std::vector<uint32_t> counts;         // downloaded counts
     bool counts_valid = false;
+    // on-device key reduction (tfbs_batch_reduce): per key
+    // (region, slot, range) the first distinct haplotype's count and flags
+    // (KEY_ANY: some count != 0, KEY_VARIES: counts differ); varying keys keep
+    // every distinct haplotype's count at var_off[key] in var_counts.
+    std::vector<uint32_t> key_first;
+    std::vector<uint8_t> key_flags;
+    std::vector<uint32_t> var_off;        // UINT32_MAX unless the key varies
+    std::vector<uint32_t> var_counts;
+    bool reduced = false;
 
     std::vector<RegionH> rh;
     uint64_t windows = 0, eff_windows = 0, cell_ops = 0;
@@ -71,6 +81,8 @@ struct Batch {
 
     uint64_t device_bytes() const;
 };
+
+enum KeyFlags : uint8_t { KEY_ANY = 1, KEY_VARIES = 2 };
 
 struct RegionInput {  // one merged region as the reader hands it over
     RegionH R;                        // ms, me, es, ee set

@@ -12,6 +12,7 @@
 
 #include "batch.hpp"
 #include "patterns.hpp"
+#include "keys.hpp"
 #include "scan.hpp"
 #include "tfbs_internal.hpp"
 
@@ -76,6 +77,10 @@ struct tfbs_ctx {
     DevBuf<DevHap> haps;
     DevBuf<DevRegion> regions;
     DevBuf<unsigned long long> hits;
+    // key reduction (tfbs_batch_reduce)
+    DevBuf<uint32_t> key_first, var_counts;
+    DevBuf<uint8_t> key_flags;
+    DevBuf<DevVarKey> var_keys;
     const tfbs_batch *resident = nullptr;
     float last_ms = 0.f;
     int last_launches = 0;
@@ -151,6 +156,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
+    ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -262,7 +268,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
     ctx->timing_pending = true;
-    b->b.counts_valid = false;
+    b->b.counts_valid = b->b.reduced = false;
     return TFBS_OK;
 }
 
@@ -276,6 +282,53 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
         HIP_TRY(hipMemcpyAsync(B.counts.data(), ctx->counts.p, B.n_counts * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.counts_valid = true;
+    return TFBS_OK;
+}
+
+int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    HIP_TRY(hipSetDevice(ctx->device));
+    Batch &B = b->b;
+    const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
+    int rc;
+    if ((rc = ctx->key_first.ensure(n_keys)) || (rc = ctx->key_flags.ensure(n_keys))) return rc;
+    if ((rc = launch_key_reduce(ctx->haps.p, ctx->regions.p, (uint32_t)B.regions.size(), ctx->counts.p, B.n_slots,
+                                ctx->key_first.p, ctx->key_flags.p, ctx->stream)))
+        return rc;
+    B.key_first.resize(n_keys);
+    B.key_flags.resize(n_keys);
+    if (n_keys) {
+        HIP_TRY(hipMemcpyAsync(B.key_first.data(), ctx->key_first.p, n_keys * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(B.key_flags.data(), ctx->key_flags.p, n_keys, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // columns of the varying keys, one count per distinct haplotype
+    std::vector<DevVarKey> vk;
+    B.var_off.assign(n_keys, UINT32_MAX);
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < B.regions.size(); r++) {
+        const DevRegion &rg = B.regions[r];
+        const uint64_t ko = (uint64_t)rg.inner_off * B.n_slots;
+        const uint32_t K = B.n_slots * rg.n_inner;
+        for (uint32_t j = 0; j < K; j++)
+            if (B.key_flags[ko + j] & KEY_VARIES) {
+                if (total + rg.hap_count >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
+                B.var_off[ko + j] = (uint32_t)total;
+                vk.push_back(DevVarKey{r, j, total});
+                total += rg.hap_count;
+            }
+    }
+    B.var_counts.resize(total);
+    if (!vk.empty()) {
+        if ((rc = ctx->var_keys.put(vk, ctx->stream)) || (rc = ctx->var_counts.ensure(total))) return rc;
+        if ((rc = launch_key_gather(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->var_keys.p,
+                                    (uint32_t)vk.size(), ctx->var_counts.p, ctx->stream)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(B.var_counts.data(), ctx->var_counts.p, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    B.reduced = true;
     return TFBS_OK;
 }
 
@@ -305,7 +358,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
             if (nucs[i] == 4) nmask[i / 32] |= 1u << (i % 32);
     }
     std::vector<DevHap> haps{hm};
-    std::vector<DevRegion> regions{DevRegion{0, 0}};
+    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1}};
     std::vector<int32_t> inner{0, 0}, posrel{0};
     const uint32_t wpp = (uint32_t)((n + 255) / 256 * 4);
     HIP_TRY(hipSetDevice(ctx->device));

@@ -198,7 +198,7 @@ int tfbs_run(const tfbs_run_args *a) {
         }
         rc = add_regions(B, ins, threads);
         if (rc) return rc;
-        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_download(ctx, bb)))
+        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)))
             return rc;
         std::string rows;
         rc = batch_rows(B, chrom, a->min_maf, &fake, rows);

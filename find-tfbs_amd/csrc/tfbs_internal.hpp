@@ -95,6 +95,16 @@ struct DevHap {
 struct DevRegion {
     uint32_t inner_off;  // into the inner (s_rel, e_rel) pair array
     uint32_t n_inner;    // distinct inner ranges
+    uint32_t hap_begin;  // first distinct haplotype (their count blocks are consecutive)
+    uint32_t hap_count;
+};
+
+// One key (region, slot * n_inner + range) whose distinct-haplotype counts differ;
+// the gather copies its hap_count counts to out_off (tfbs_batch_reduce).
+struct DevVarKey {
+    uint32_t region;
+    uint32_t j;
+    uint64_t out_off;
 };
 
 }  // namespace tfbs

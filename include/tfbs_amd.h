@@ -195,6 +195,13 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b);
 int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b);
 /* D2H copy of the counts into the batch. */
 int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
+/* Alternative to tfbs_batch_download for row emission (the gather half of
+ * count_matches_by_sample, main.rs:500-534, moved to the device): classifies
+ * every (region, pattern_id, inner range) key on the GPU (some distinct
+ * haplotype matched / distinct haplotypes disagree) and downloads only the
+ * flags, one count per key and the per-haplotype counts of the disagreeing
+ * keys.  The key / row functions below then work as after a download. */
+int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
 
 /* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
  * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */

@@ -70,9 +70,9 @@ def build_batch(pset, n_samples, beds, regions):
     return b
 
 
-def run_product(scanner, pset, n_samples, beds, regions, chrom="chr1", min_maf=0):
+def run_product(scanner, pset, n_samples, beds, regions, chrom="chr1", min_maf=0, reduce=False):
     b = build_batch(pset, n_samples, beds, regions)
-    b.scan(scanner)
+    b.scan(scanner, reduce=reduce)
     keys = [b.keys(i) for i in range(b.num_regions)]
     rows, _ = b.rows(chrom, min_maf)
     return keys, rows, b

@@ -231,15 +231,17 @@ def _compare(ps, n_samples, beds, regions, min_maf=0):
     okeys, orows, _ = run_oracle(ps, n_samples, beds, regions, min_maf=min_maf)
     sc = T.Scanner(ps)
     try:
-        pkeys, prows, b = run_product(sc, ps, n_samples, beds, regions, min_maf=min_maf)
+        # dense download, and the device key reduction (f1) the run flow uses
+        for reduce in (False, True):
+            pkeys, prows, b = run_product(sc, ps, n_samples, beds, regions, min_maf=min_maf, reduce=reduce)
+            assert len(okeys) == len(pkeys)
+            for i, (a, z) in enumerate(zip(okeys, pkeys)):
+                assert a.keys() == z.keys(), (reduce, i)
+                for k in a:
+                    assert a[k] == z[k], (reduce, i, k)
+            assert prows == orows, reduce
     finally:
         sc.close()
-    assert len(okeys) == len(pkeys)
-    for i, (a, z) in enumerate(zip(okeys, pkeys)):
-        assert a.keys() == z.keys(), i
-        for k in a:
-            assert a[k] == z[k], (i, k)
-    assert prows == orows
     return b
 
 
@@ -325,5 +327,10 @@ def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
         sc = T.Scanner(ps)
         b.scan(sc)
         res.append([b.keys(r) for r in (0, 57, 199)])
+        rows_dense, _ = b.rows("chr1")
+        b.scan(sc, upload=False, reduce=True)  # device key reduction gives the same keys and rows
+        assert [b.keys(r) for r in (0, 57, 199)] == res[-1]
+        assert b.rows("chr1")[0] == rows_dense
         sc.close()
     assert res[0] == res[1] == res[2]
+    assert rows_dense.count("\n") > 0
