@@ -8,8 +8,8 @@ LIBDIR := $(PKG)/lib
 OBJDIR := $(PKG)/lib/obj
 JOBS ?= 8
 
-HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/plan.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
-HIP_SRCS := $(SRC)/device.hip $(SRC)/scan_kernels.hip $(SRC)/key_kernels.hip
+HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/plan.cpp $(SRC)/mfma.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
+HIP_SRCS := $(SRC)/device.hip $(SRC)/scan_kernels.hip $(SRC)/scan_mfma.hip $(SRC)/key_kernels.hip
 HDRS := $(wildcard $(SRC)/*.hpp) include/tfbs_amd.h
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS := $(patsubst $(SRC)/%.hip,$(OBJDIR)/%.o,$(HIP_SRCS))
@@ -22,6 +22,10 @@ all: $(LIBDIR)/libtfbs_amd.so $(PKG)/bin/find-tfbs-amd oracle
 $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS) -x c++ -c $< -o $@
+
+# MFMA results straight into VGPRs (gfx950's unified register file): the
+# threshold test reads every accumulator, so AGPR copies would cost 16 VALU per tile
+$(OBJDIR)/scan_mfma.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
 $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -147,10 +147,10 @@ class PatternSet:
     def max_length(self):
         return lib().tfbs_patterns_max_length(self.h)
 
-    def plan_stats(self, tile_blocks=16):
-        """Host-side summary of the device plan (octet/quad/generic strands, tiles)."""
+    def plan_stats(self, tile_blocks=20, mfma=False):
+        """Host-side summary of the device plan (octet/quad/generic/MFMA strands, tiles)."""
         st = _capi.tfbs_plan_stats()
-        check(lib().tfbs_patterns_plan_stats(self.h, tile_blocks, C.byref(st)))
+        check(lib().tfbs_patterns_plan_stats(self.h, tile_blocks, 1 if mfma else 0, C.byref(st)))
         return {n: getattr(st, n) for n, _ in st._fields_}
 
 

@@ -33,7 +33,8 @@ class tfbs_pattern_desc(C.Structure):
 class tfbs_plan_stats(C.Structure):
     _fields_ = [(n, C.c_uint32) for n in ("n_octet_strands", "n_quad_strands", "n_generic_strands",
                                            "n_fast_tiles", "n_fast_units", "n_generic_tiles",
-                                           "max_tile_blocks")] + [("lut_bytes", C.c_uint64)]
+                                           "max_tile_blocks")] + [("lut_bytes", C.c_uint64)] + \
+        [(n, C.c_uint32) for n in ("n_mfma_strands", "n_mfma_tiles", "n_mfma_supers")]
 
 
 class tfbs_run_args(C.Structure):
@@ -58,7 +59,7 @@ SIGNATURES = [
     ("tfbs_patterns_name_of", C.c_char_p, [vp, C.c_uint16]),
     ("tfbs_patterns_max_length", C.c_uint32, [vp]),
     ("tfbs_patterns_destroy", None, [vp]),
-    ("tfbs_patterns_plan_stats", C.c_int, [vp, C.c_uint32, C.POINTER(tfbs_plan_stats)]),
+    ("tfbs_patterns_plan_stats", C.c_int, [vp, C.c_uint32, C.c_int, C.POINTER(tfbs_plan_stats)]),
     ("tfbs_parse_weight", C.c_int, [C.c_char_p, i32p]),
     ("tfbs_parse_threshold_file", C.c_int, [C.c_char_p, C.c_float, i32p]),
     ("tfbs_device_count", C.c_int, [C.POINTER(C.c_int)]),

@@ -330,8 +330,10 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     const tfbs::Patterns &P = tfbs::patterns_of(p);
     if (P.pats.empty()) return tfbs::fail(TFBS_E_NOPATTERN, "no pattern");  // main.rs:238
     if ((uint64_t)n_samples * 2 > 0xFFFFFFF0ull) return tfbs::fail(TFBS_E_ARG, "too many samples");
-    tfbs::Plan plan;
-    int rc = P.build_plan(1u << 30, &plan);
+    tfbs::Plan plan;  // only its slot order is used (independent of the tile options)
+    tfbs::PlanOptions opt;
+    opt.tile_blocks = 1u << 30;
+    int rc = P.build_plan(opt, &plan);
     if (rc) return rc;
     if (plan.zero_len_panics)
         return tfbs::fail(TFBS_E_ZEROLEN, "length-0 PWM with negative min_score (pattern.rs:150-156)");

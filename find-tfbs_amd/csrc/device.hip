@@ -70,7 +70,10 @@ struct tfbs_ctx {
     DevBuf<DevUnit> fast_units;
     DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
-    DevBuf<int32_t> lut, wfull, gen_w;
+    DevBuf<int32_t> lut, wfull, gen_w, m_image;
+    DevBuf<DevMSuper> m_supers;
+    bool mfma = false;
+    uint32_t mfma_lds = 64 * 1024;
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
     DevBuf<int32_t> posrel, inner;
@@ -110,6 +113,16 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
     a.hits_wpp = hits_wpp;
     a.n_patterns_total = (uint32_t)ctx->pats->pats.size();
     int launches = 0;
+    if (!P.m_supers.empty()) {  // atomic adds: zero its slots first (the other kernels store theirs)
+        if (ctx->counts.n) HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, ctx->counts.n * 4, ctx->stream));
+        ScanArgs m = a;
+        m.msupers = ctx->m_supers.p;
+        m.n_msupers = (uint32_t)P.m_supers.size();
+        m.mimage = ctx->m_image.p;
+        const int n = launch_mfma(m, P.max_super_bytes, n_haps, ctx->stream);
+        if (n < 0) return n;
+        launches += n;
+    }
     if (!P.fast_tiles.empty()) {
         ScanArgs f = a;
         f.tiles = ctx->fast_tiles.p;
@@ -154,6 +167,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
+    ctx->m_image.release(); ctx->m_supers.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
@@ -175,7 +189,13 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->tile_blocks = (uint32_t)std::min(36, std::max(8, env_int("TFBS_TILE_BLOCKS", 20)));
     ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 128));
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
-    rc = ctx->pats->build_plan(ctx->tile_blocks, &ctx->plan);
+    ctx->mfma = env_int("TFBS_MFMA", 0) != 0;
+    ctx->mfma_lds = (uint32_t)std::min(160, std::max(8, env_int("TFBS_MFMA_LDS_KB", 64))) * 1024u;
+    PlanOptions opt;
+    opt.tile_blocks = ctx->tile_blocks;
+    opt.mfma = ctx->mfma;
+    opt.mfma_lds_bytes = ctx->mfma_lds;
+    rc = ctx->pats->build_plan(opt, &ctx->plan);
     if (rc) {
         delete ctx;
         return rc;
@@ -198,14 +218,19 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "pattern tile exceeds the 160 KiB LDS");
     }
-    if ((rc = fast_kernel_set_lds(ctx->cfg))) {
+    if (P.max_super_bytes > 160 * 1024) {
+        tfbs_ctx_destroy(ctx);
+        return tfbs::fail(TFBS_E_ARG, "MFMA super tile exceeds the 160 KiB LDS");
+    }
+    if ((rc = fast_kernel_set_lds(ctx->cfg)) || (rc = mfma_kernel_set_lds(P.max_super_bytes))) {
         tfbs_ctx_destroy(ctx);
         return rc;
     }
     if ((rc = ctx->fast_units.put(P.fast_units, ctx->stream)) || (rc = ctx->fast_tiles.put(P.fast_tiles, ctx->stream)) ||
         (rc = ctx->lut.put(P.lut, ctx->stream)) || (rc = ctx->wfull.put(P.wfull, ctx->stream)) ||
         (rc = ctx->gen_pats.put(P.gen_pats, ctx->stream)) || (rc = ctx->gen_tiles.put(P.gen_tiles, ctx->stream)) ||
-        (rc = ctx->gen_w.put(P.gen_w, ctx->stream))) {
+        (rc = ctx->gen_w.put(P.gen_w, ctx->stream)) || (rc = ctx->m_image.put(P.m_image, ctx->stream)) ||
+        (rc = ctx->m_supers.put(P.m_supers, ctx->stream))) {
         tfbs_ctx_destroy(ctx);
         return rc;
     }

@@ -213,7 +213,10 @@ static std::vector<SlotGroup> groups_fast(const std::vector<Group> &groups) {
 // slots -- so neighbouring strands have similar lengths and pack into units
 // with little padding.  Fast tiles are runs of whole groups whose table blocks
 // fit the LDS budget and span at most 64 slots.
-int Patterns::build_plan(uint32_t tile_blocks, Plan *plan) const {
+// With opt.mfma, groups whose strands all pass mfma_eligible are scored on the
+// matrix cores instead (32-strand tiles, any slot mix: that kernel adds its
+// counts atomically).
+int Patterns::build_plan(const PlanOptions &opt, Plan *plan) const {
     *plan = Plan();
     // Scannable strands: PWM with length >= 1.  A length-0 PWM with a negative
     // min_score panics in the reference at the first region (pattern.rs:150-156
@@ -244,7 +247,14 @@ int Patterns::build_plan(uint32_t tile_blocks, Plan *plan) const {
         return a.pid < b.pid;
     });
     for (auto &g : groups) plan->slot_pid.push_back(g.pid);
-    build_fast_tiles(*this, groups_fast(groups), tile_blocks, plan);
+    std::vector<SlotGroup> fast = groups_fast(groups), lut, mat;
+    for (SlotGroup &g : fast) {
+        bool m = opt.mfma;
+        for (int i : g.strands) m = m && mfma_eligible(pats[i]);
+        (m ? mat : lut).push_back(std::move(g));
+    }
+    build_fast_tiles(*this, lut, opt.tile_blocks, plan);
+    build_mfma_tiles(*this, mat, opt.mfma_lds_bytes, plan);
     // --- generic (long) strands: one tile per pattern_id group, weights x5
     for (uint32_t gi = 0; gi < groups.size(); gi++) {
         const Group &g = groups[gi];
@@ -401,10 +411,13 @@ uint32_t tfbs_patterns_max_length(const tfbs_patterns *p) { return p ? p->p.max_
 
 void tfbs_patterns_destroy(tfbs_patterns *p) { delete p; }
 
-int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, tfbs_plan_stats *out) {
+int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, int mfma, tfbs_plan_stats *out) {
     if (!p || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
     tfbs::Plan plan;
-    int rc = p->p.build_plan(tile_blocks, &plan);
+    tfbs::PlanOptions opt;
+    opt.tile_blocks = tile_blocks;
+    opt.mfma = mfma != 0;
+    int rc = p->p.build_plan(opt, &plan);
     if (rc) return rc;
     *out = tfbs_plan_stats{};
     out->n_octet_strands = plan.n_octet_strands;
@@ -415,6 +428,9 @@ int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, tfbs_
     out->n_generic_tiles = (uint32_t)plan.gen_tiles.size();
     out->max_tile_blocks = plan.max_tile_blocks;
     out->lut_bytes = (uint64_t)plan.lut.size() * 4;
+    out->n_mfma_strands = plan.n_mfma_strands;
+    out->n_mfma_tiles = plan.n_mfma_tiles;
+    out->n_mfma_supers = (uint32_t)plan.m_supers.size();
     return TFBS_OK;
 }
 

@@ -32,7 +32,19 @@ struct Plan {
     uint32_t max_tile_blocks = 0;
     uint32_t n_octet_strands = 0;
     uint32_t n_quad_strands = 0;
+    // matrix-core path (mfma.cpp, scan_mfma.hip)
+    std::vector<DevMSuper> m_supers;
+    uint32_t n_mfma_tiles = 0;
+    std::vector<int32_t> m_image;    // per super tile: B fragments + strand metadata (LDS image)
+    uint32_t max_super_bytes = 0;
+    uint32_t n_mfma_strands = 0;
     bool zero_len_panics = false;
+};
+
+struct PlanOptions {
+    uint32_t tile_blocks = 20;          // LUT tile: 4 KiB table blocks per workgroup
+    bool mfma = false;                  // score eligible strands on the matrix cores
+    uint32_t mfma_lds_bytes = 64 * 1024;  // LDS image budget of one MFMA super tile
 };
 
 struct Patterns {
@@ -40,7 +52,7 @@ struct Patterns {
     std::map<uint16_t, std::string> names;
     void add(const Pat &p);
     uint32_t max_length() const;
-    int build_plan(uint32_t tile_blocks, Plan *plan) const;
+    int build_plan(const PlanOptions &opt, Plan *plan) const;
 };
 
 struct SlotGroup {  // the strands of one pattern_id and its count slot
@@ -48,6 +60,10 @@ struct SlotGroup {  // the strands of one pattern_id and its count slot
     std::vector<int> strands;
 };
 void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t tile_blocks, Plan *plan);
+// Strands the int8 one-hot formulation scores exactly (L <= 32, every weight
+// splits as 64 a + b with a, b int8).
+bool mfma_eligible(const Pat &p);
+void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t lds_bytes, Plan *plan);
 
 int parse_weight(const std::string &s, int32_t *out);
 int parse_threshold_file(const std::string &path, float thr, int32_t *out);

@@ -27,6 +27,9 @@ struct ScanArgs {
     const int32_t *posrel;
     uint32_t *counts;
     uint32_t haps_per_block;
+    const DevMSuper *msupers;   // matrix-core path
+    uint32_t n_msupers;
+    const int32_t *mimage;
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;
     uint32_t n_patterns_total;
@@ -44,5 +47,8 @@ int launch_fast(const ScanArgs &a, const LaunchConfig &cfg, uint32_t n_haps, hip
 int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
 // Opts the fast kernel into more than 64 KiB of dynamic LDS.
 int fast_kernel_set_lds(const LaunchConfig &cfg);
+// Matrix-core scan (scan_mfma.hip); counts must be zeroed first (atomic adds).
+int launch_mfma(const ScanArgs &a, size_t lds_bytes, uint32_t n_haps, hipStream_t stream);
+int mfma_kernel_set_lds(size_t lds_bytes);
 
 }  // namespace tfbs

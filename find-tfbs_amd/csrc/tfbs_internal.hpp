@@ -80,6 +80,30 @@ struct DevTile {
     uint32_t pad;
 };
 
+// Matrix-core path (scan_mfma.hip).  A strand's weights split as w = 64 a + b
+// (a, b int8); the score of 32 windows x 32 strands is one-hot(window bases) x
+// [b; a] with the one-hot entries 1 and 64, summed exactly in int32 by
+// v_mfma_i32_32x32x32_i8.  K chunk = 8 columns x 4 bases.
+constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
+constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
+constexpr int kMChunkCols = 8;     // columns per K chunk of 32
+constexpr int kMMaxChunks = 4;     // L <= 32
+constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
+constexpr int kMMetaBytes = 512;   // per tile: thr[32], len[32], slot[32], orig[32]
+
+// The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
+// depth nk; tile t's B fragments at t * nk * 2 KiB ([chunk][digit lo, hi][lane
+// 64][16 bytes]), its metadata at meta_off + t * 512.
+struct DevMSuper {
+    uint32_t tile_count;
+    uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
+    uint32_t img_off;   // byte offset of the LDS image in Plan::m_image
+    uint32_t img_bytes;
+    uint32_t meta_off;  // byte offset of tile 0's metadata in the image
+    uint32_t lmin;      // shortest strand
+    uint32_t pad0, pad1;
+};
+
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };
 
 struct DevHap {

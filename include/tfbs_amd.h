@@ -92,14 +92,16 @@ const char *tfbs_patterns_name_of(const tfbs_patterns *p, uint16_t pattern_id);
 uint32_t tfbs_patterns_max_length(const tfbs_patterns *p);
 void tfbs_patterns_destroy(tfbs_patterns *p);
 /* Host-only diagnostics of the device plan the scan would use with tiles of
- * tile_blocks 4 KiB table blocks: strands on the 16-bit octet path, on the
- * 32-bit quad path, on the generic (L > 32) kernel, and fast tiles. */
+ * tile_blocks 4 KiB table blocks (and, if mfma, the matrix-core path): strands
+ * on the 16-bit octet path, the 32-bit quad path, the generic (L > 32) kernel
+ * and the int8 MFMA path, and their tiles. */
 typedef struct tfbs_plan_stats {
     uint32_t n_octet_strands, n_quad_strands, n_generic_strands;
     uint32_t n_fast_tiles, n_fast_units, n_generic_tiles, max_tile_blocks;
     uint64_t lut_bytes;
+    uint32_t n_mfma_strands, n_mfma_tiles, n_mfma_supers;
 } tfbs_plan_stats;
-int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, tfbs_plan_stats *out);
+int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, int mfma, tfbs_plan_stats *out);
 
 /* pattern.rs:13-16 parse_weight: (f32(s) * 1000f32).round() as i32. */
 int tfbs_parse_weight(const char *s, int32_t *out);

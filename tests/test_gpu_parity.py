@@ -47,9 +47,12 @@ def _rand_pwm(rnd, L, scale=1000):
     return [[rnd.randint(-3 * scale, scale) for _ in range(4)] + [0] for _ in range(L)]
 
 
-def test_matches_fuzz_vs_oracle():
-    """Random PWMs of length 1..40 (fast LUT path and the >32 generic path), haplotypes
-    up to 700 bases (several 256-window passes), N bases, non-affine positions."""
+@pytest.mark.parametrize("mfma", ["0", "1"])
+def test_matches_fuzz_vs_oracle(monkeypatch, mfma):
+    """Random PWMs of length 1..40 (fast LUT path and the >32 generic path, or the
+    matrix-core path), haplotypes up to 700 bases (several 256-window passes), N bases,
+    non-affine positions."""
+    monkeypatch.setenv("TFBS_MFMA", mfma)
     rnd = random.Random(1)
     pats = []
     for i in range(48):
@@ -127,12 +130,19 @@ def octet_boundary_patterns(rnd, seq):
     return pats
 
 
-def test_octet_boundaries_vs_oracle():
+@pytest.mark.parametrize("mfma", ["0", "1"])
+def test_octet_boundaries_vs_oracle(monkeypatch, mfma):
+    """With TFBS_MFMA=1 the same patterns split between the matrix-core path (weights
+    within the two int8 digits) and the LUT path (the rest)."""
+    monkeypatch.setenv("TFBS_MFMA", mfma)
     rnd = random.Random(5)
     base = "".join(rnd.choice("ACGT") for _ in range(700))
     pats = octet_boundary_patterns(rnd, base)
-    st = T.PatternSet.from_patterns(pats).plan_stats()
-    assert st["n_octet_strands"] > 0 and st["n_quad_strands"] > 0, st
+    st = T.PatternSet.from_patterns(pats).plan_stats(mfma=mfma == "1")
+    if mfma == "1":
+        assert st["n_mfma_strands"] > 0 and st["n_quad_strands"] > 0, st
+    else:
+        assert st["n_octet_strands"] > 0 and st["n_quad_strands"] > 0, st
     sc = T.Scanner(pats)
     try:
         for trial, seq in enumerate([base, base[:300] + "N" + base[301:520] + "NN" + base[522:], base[:33], ""]):
@@ -245,8 +255,11 @@ def _compare(ps, n_samples, beds, regions, min_maf=0):
     return b
 
 
+@pytest.mark.parametrize("mfma", ["0", "1"])
 @pytest.mark.parametrize("config,indel,n_samples,n_regions", [(2, 0, 150, 16), (3, 0, 60, 6), (5, 30, 80, 10)])
-def test_synthetic_regions_vs_oracle(tmp_path, config, indel, n_samples, n_regions):
+def test_synthetic_regions_vs_oracle(tmp_path, monkeypatch, config, indel, n_samples, n_regions, mfma):
+    """Both scan paths: the LUT kernels and (TFBS_MFMA=1) the int8 matrix-core kernel."""
+    monkeypatch.setenv("TFBS_MFMA", mfma)
     ps, _ = synth_patterns(tmp_path, 12 if config != 3 else 40, config, 100 + config, thr=1e-3)
     beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
     regions = make_regions_synth(7 + config, 0, n_regions, n_samples, ps.max_length, indel)
