@@ -74,6 +74,7 @@ struct tfbs_ctx {
     DevBuf<DevMSuper> m_supers;
     bool mfma = false;
     uint32_t mfma_lds = 64 * 1024;
+    int mfma_pipe = 1;            // scan_mfma_kernel<PIPE> instantiation
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
     DevBuf<int32_t> posrel, inner;
@@ -119,7 +120,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
-        const int n = launch_mfma(m, P.max_super_bytes, n_haps, ctx->stream);
+        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_pipe, n_haps, ctx->stream);
         if (n < 0) return n;
         launches += n;
     }
@@ -191,6 +192,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 0) != 0;
     ctx->mfma_lds = (uint32_t)std::min(160, std::max(8, env_int("TFBS_MFMA_LDS_KB", 64))) * 1024u;
+    ctx->mfma_pipe = env_int("TFBS_MFMA_PIPE", 1) != 0;
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -222,7 +224,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "MFMA super tile exceeds the 160 KiB LDS");
     }
-    if ((rc = fast_kernel_set_lds(ctx->cfg)) || (rc = mfma_kernel_set_lds(P.max_super_bytes))) {
+    if ((rc = fast_kernel_set_lds(ctx->cfg)) || (rc = mfma_kernel_set_lds(P.max_super_bytes, ctx->mfma_pipe))) {
         tfbs_ctx_destroy(ctx);
         return rc;
     }

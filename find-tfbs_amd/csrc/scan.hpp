@@ -48,7 +48,7 @@ int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
 // Opts the fast kernel into more than 64 KiB of dynamic LDS.
 int fast_kernel_set_lds(const LaunchConfig &cfg);
 // Matrix-core scan (scan_mfma.hip); counts must be zeroed first (atomic adds).
-int launch_mfma(const ScanArgs &a, size_t lds_bytes, uint32_t n_haps, hipStream_t stream);
-int mfma_kernel_set_lds(size_t lds_bytes);
+int launch_mfma(const ScanArgs &a, size_t lds_bytes, int pipe, uint32_t n_haps, hipStream_t stream);
+int mfma_kernel_set_lds(size_t lds_bytes, int pipe);
 
 }  // namespace tfbs

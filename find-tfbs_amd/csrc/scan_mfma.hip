@@ -38,26 +38,44 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kMBlock = 256;  // 4 waves, one per SIMD
 
-// One-hot A fragments (entries 1 and 64) of the 32-window tile starting at i0:
-// lane l covers window i0 + (l & 31) and, in chunk kc, columns 8 kc + 4 (l >> 5) + t.
+// The packed words (and N-mask words) a lane needs for its window of the
+// 32-window tile at i0: lane l covers window i0 + (l & 31).  Issued one tile
+// ahead of use so the global-load latency overlaps the previous tile's MFMAs.
+struct WinWords {
+    uint32_t w[3], m[2];
+};
+
+__device__ __forceinline__ void load_window(const ScanArgs &A, const DevHap &hm, uint32_t i0, uint32_t lane,
+                                            WinWords &ww) {
+    const uint32_t ic = min(i0 + (lane & 31), hm.len);  // reads stay inside the +3 word pad
+    const uint32_t *w = A.words + hm.word_off + (ic >> 4);
+    ww.w[0] = w[0];
+    ww.w[1] = w[1];
+    ww.w[2] = w[2];
+    if (hm.flags & HAP_HAS_N) {
+        const uint32_t *m = A.nmask + hm.nmask_off + (ic >> 5);
+        ww.m[0] = m[0];
+        ww.m[1] = m[1];
+    } else {
+        ww.m[0] = ww.m[1] = 0;
+    }
+}
+
+// One-hot A fragments (entries 1 and 64) of the 32-window tile at i0: in chunk
+// kc, lane l covers columns 8 kc + 4 (l >> 5) + t of its window.
 template <int NK>
-__device__ __forceinline__ void build_onehot(const ScanArgs &A, const DevHap &hm, uint32_t i0, uint32_t lane,
+__device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint32_t lane, const WinWords &ww,
                                              v4i (&alo)[NK], v4i (&ahi)[NK]) {
     const uint32_t i = i0 + (lane & 31);
     const uint32_t h = lane >> 5;
-    const uint32_t ic = min(i, hm.len);  // reads stay inside the +3 word pad
-    const uint32_t *w = A.words + hm.word_off + (ic >> 4);
+    const uint32_t ic = min(i, hm.len);
     const uint32_t sh = 2 * (ic & 15);
-    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-    const uint32_t img_lo = __builtin_amdgcn_alignbit(w1, w0, sh);  // bases i .. i+15
-    const uint32_t img_hi = __builtin_amdgcn_alignbit(w2, w1, sh);  // bases i+16 .. i+31
+    const uint32_t img_lo = __builtin_amdgcn_alignbit(ww.w[1], ww.w[0], sh);  // bases i .. i+15
+    const uint32_t img_hi = __builtin_amdgcn_alignbit(ww.w[2], ww.w[1], sh);  // bases i+16 .. i+31
     // bases that exist and are not N
     const int32_t rem = (int32_t)hm.len - (int32_t)i;
     uint32_t vm = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
-    if (hm.flags & HAP_HAS_N) {
-        const uint32_t *m = A.nmask + hm.nmask_off + (ic >> 5);
-        vm &= ~__builtin_amdgcn_alignbit(m[1], m[0], ic & 31);
-    }
+    vm &= ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31);
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) {
         const uint32_t img = kc < 2 ? img_lo : img_hi;
@@ -108,41 +126,51 @@ struct HapCtx {
     const int32_t *inner;
 };
 
-// Threshold test of one strand tile: the max of the lane's 16 scores against its
-// strand's min_score, one ballot.  On a hit (rare) one ballot per score register
-// finds the registers holding hits, and only those windows run the validity
-// test (i + L <= len), the inner-range overlap test (range.rs:18-21 as
+// The rare path of check_tile, out of line so that its registers do not
+// constrain the hot loop; everything by value (an address-taken argument would
+// route the caller's haplotype state through scratch).  One ballot per score
+// register finds the registers holding hits; only those windows run the
+// validity test (i + L <= len), the inner-range overlap test (range.rs:18-21 as
 // main.rs:503 uses it) and the atomic count of the strand's pattern_id slot.
+__device__ __noinline__ void tile_hits(v16i acc, int32_t thr, const int32_t *meta, uint32_t len, uint32_t flags,
+                                       uint32_t pos_off, uint64_t count_off, uint32_t hap, uint32_t i0, uint32_t lane,
+                                       const int32_t *inner, uint32_t n_inner, uint32_t *counts, const int32_t *posrel,
+                                       unsigned long long *hits, uint32_t hits_wpp, uint32_t n_pat) {
+    const uint32_t n = lane & 31, h = lane >> 5;
+    const uint32_t L = (uint32_t)meta[32 + n];
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const bool hit = acc[r] > thr && i + L <= len;
+        if (__ballot(hit) == 0) continue;
+        if (hit) {
+            const uint32_t slot = (uint32_t)meta[64 + n];
+            const int32_t p = (flags & HAP_HAS_POS) ? posrel[pos_off + i] : (int32_t)i;
+            for (uint32_t k = 0; k < n_inner; k++) {
+                const int32_t s = inner[2 * k];
+                const uint32_t span = (uint32_t)(inner[2 * k + 1] - s);
+                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
+                    atomicAdd(counts + count_off + (uint64_t)slot * n_inner + k, 1u);
+            }
+            if (hits && i / 64 < hits_wpp)
+                atomicOr(hits + ((size_t)hap * n_pat + (uint32_t)meta[96 + n]) * hits_wpp + i / 64, 1ull << (i & 63));
+        }
+    }
+}
+
+// Threshold test of one strand tile: the max of the lane's 16 scores against its
+// strand's min_score, one ballot; hits go to tile_hits.
 template <int NK>
 __device__ __forceinline__ void check_tile(const ScanArgs &A, const DevMSuper &S, const char *s_img, uint32_t ti,
                                            const v16i &acc, int32_t thr, const HapCtx &H, uint32_t i0, uint32_t lane) {
     int32_t m = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])), max(max(acc[4], acc[5]), max(acc[6], acc[7])));
     m = max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
     if (__builtin_expect(__ballot(m > thr) == 0, 1)) return;
-    const int32_t *meta = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes);
-    const uint32_t n = lane & 31, h = lane >> 5;
-    const uint32_t L = (uint32_t)meta[32 + n];
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-        const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const bool hit = acc[r] > thr && i + L <= H.hm.len;
-        if (__ballot(hit) == 0) continue;
-        if (hit) {
-            const uint32_t slot = (uint32_t)meta[64 + n];
-            const int32_t p = (H.hm.flags & HAP_HAS_POS) ? A.posrel[H.hm.pos_off + i] : (int32_t)i;
-            for (uint32_t k = 0; k < H.n_inner; k++) {
-                const int32_t s = H.inner[2 * k];
-                const uint32_t span = (uint32_t)(H.inner[2 * k + 1] - s);
-                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-                    atomicAdd(A.counts + H.hm.count_off + (uint64_t)slot * H.n_inner + k, 1u);
-            }
-            if (A.hits && i / 64 < A.hits_wpp)
-                atomicOr(A.hits + ((size_t)H.hap * A.n_patterns_total + (uint32_t)meta[96 + n]) * A.hits_wpp + i / 64,
-                         1ull << (i & 63));
-        }
-    }
+    tile_hits(acc, thr, reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes), H.hm.len, H.hm.flags,
+              H.hm.pos_off, H.hm.count_off, H.hap, i0, lane, H.inner, H.n_inner, A.counts, A.posrel, A.hits,
+              A.hits_wpp, A.n_patterns_total);
 }
-template <int NK>
+template <int NK, bool PIPE>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img, uint32_t hg,
                                            uint32_t lane, uint32_t wave) {
     constexpr uint32_t kWaves = kMBlock / 64;
@@ -157,9 +185,22 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         H.inner = A.inner + 2 * (size_t)rg.inner_off;
         H.n_inner = rg.n_inner;
         const uint32_t nwin = H.hm.len - S.lmin + 1;
+        WinWords ww;
+        load_window(A, H.hm, 0, lane, ww);
         for (uint32_t i0 = 0; i0 < nwin; i0 += kMWindows) {
             v4i alo[NK], ahi[NK];
-            build_onehot<NK>(A, H.hm, i0, lane, alo, ahi);
+            build_onehot<NK>(H.hm, i0, lane, ww, alo, ahi);
+            if (i0 + kMWindows < nwin) load_window(A, H.hm, i0 + kMWindows, lane, ww);  // next tile's words
+            if (!PIPE) {  // one tile at a time; the other waves of the SIMD hide the latencies
+                for (uint32_t ti = 0; ti < nt; ti++) {
+                    BFrag<NK> f;
+                    load_tile<NK>(s_img, S, ti, lane, f);
+                    __builtin_amdgcn_sched_barrier(0);  // every B read of the tile issues before its MFMAs
+                    const v16i acc = tile_scores<NK>(alo, ahi, f);
+                    check_tile<NK>(A, S, s_img, ti, acc, f.thr, H, i0, lane);
+                }
+                continue;
+            }
             // two-stage pipeline over the strand tiles: scores of tile t + 1 are
             // in flight on the matrix core while tile t is tested
             BFrag<NK> fa, fb;
@@ -189,7 +230,10 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block); dynamic LDS = the largest image.
-__global__ __launch_bounds__(kMBlock) void scan_mfma_kernel(ScanArgs A) {
+// PIPE: software-pipelined tile loop, two workgroups (waves) per SIMD;
+// otherwise a plain loop under a 4-waves-per-SIMD register budget.
+template <bool PIPE>
+__global__ __launch_bounds__(kMBlock, PIPE ? 2 : 4) void scan_mfma_kernel(ScanArgs A) {
     extern __shared__ __attribute__((aligned(16))) int32_t smem[];
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
@@ -203,24 +247,27 @@ __global__ __launch_bounds__(kMBlock) void scan_mfma_kernel(ScanArgs A) {
     const char *s_img = reinterpret_cast<const char *>(smem);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     switch (S.nk) {
-    case 1: scan_super<1>(A, S, s_img, hg, lane, wave); break;
-    case 2: scan_super<2>(A, S, s_img, hg, lane, wave); break;
-    case 3: scan_super<3>(A, S, s_img, hg, lane, wave); break;
-    default: scan_super<4>(A, S, s_img, hg, lane, wave); break;
+    case 1: scan_super<1, PIPE>(A, S, s_img, hg, lane, wave); break;
+    case 2: scan_super<2, PIPE>(A, S, s_img, hg, lane, wave); break;
+    case 3: scan_super<3, PIPE>(A, S, s_img, hg, lane, wave); break;
+    default: scan_super<4, PIPE>(A, S, s_img, hg, lane, wave); break;
     }
 }
 
+typedef void (*MfmaKernel)(ScanArgs);
+MfmaKernel mfma_variant(int pipe) { return pipe ? scan_mfma_kernel<true> : scan_mfma_kernel<false>; }
+
 }  // namespace
 
-int mfma_kernel_set_lds(size_t lds_bytes) {
+int mfma_kernel_set_lds(size_t lds_bytes, int pipe) {
     if (lds_bytes <= 64 * 1024) return TFBS_OK;
-    hipError_t e = hipFuncSetAttribute((const void *)scan_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void *)mfma_variant(pipe), hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds_bytes);
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("MFMA LDS attribute: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 
-int launch_mfma(const ScanArgs &a0, size_t lds_bytes, uint32_t n_haps, hipStream_t stream) {
+int launch_mfma(const ScanArgs &a0, size_t lds_bytes, int pipe, uint32_t n_haps, hipStream_t stream) {
     if (n_haps == 0 || a0.n_msupers == 0) return 0;
     const uint32_t hpb = a0.haps_per_block;
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
@@ -233,7 +280,7 @@ int launch_mfma(const ScanArgs &a0, size_t lds_bytes, uint32_t n_haps, hipStream
         a.haps = a0.haps + h0;
         a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
         a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
-        hipLaunchKernelGGL(scan_mfma_kernel, dim3(a0.n_msupers * ng), dim3(kMBlock), lds_bytes, stream, a);
+        hipLaunchKernelGGL(mfma_variant(pipe), dim3(a0.n_msupers * ng), dim3(kMBlock), lds_bytes, stream, a);
         launches++;
     }
     hipError_t e = hipGetLastError();
