@@ -74,7 +74,7 @@ struct tfbs_ctx {
     DevBuf<DevMSuper> m_supers;
     bool mfma = false;
     uint32_t mfma_lds = 64 * 1024;
-    int mfma_pipe = 1;            // scan_mfma_kernel<PIPE> instantiation
+    uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
     DevBuf<int32_t> posrel, inner;
@@ -120,7 +120,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
-        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_pipe, n_haps, ctx->stream);
+        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_group_words, n_haps, ctx->stream);
         if (n < 0) return n;
         launches += n;
     }
@@ -192,7 +192,6 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 0) != 0;
     ctx->mfma_lds = (uint32_t)std::min(160, std::max(8, env_int("TFBS_MFMA_LDS_KB", 64))) * 1024u;
-    ctx->mfma_pipe = env_int("TFBS_MFMA_PIPE", 1) != 0;
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -220,11 +219,11 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "pattern tile exceeds the 160 KiB LDS");
     }
-    if (P.max_super_bytes > 160 * 1024) {
+    if (P.max_super_bytes + mfma_lds_fixed() > 160 * 1024) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_ARG, "MFMA super tile exceeds the 160 KiB LDS");
     }
-    if ((rc = fast_kernel_set_lds(ctx->cfg)) || (rc = mfma_kernel_set_lds(P.max_super_bytes, ctx->mfma_pipe))) {
+    if ((rc = fast_kernel_set_lds(ctx->cfg))) {
         tfbs_ctx_destroy(ctx);
         return rc;
     }
@@ -282,6 +281,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
         return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->resident = b;
+    ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->haps_per_block);
     return TFBS_OK;
 }
 
@@ -396,6 +396,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
         (rc = ctx->counts.ensure(1)))
         return rc;
     ctx->resident = nullptr;
+    ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->haps_per_block);
     const size_t nh = (size_t)P.pats.size() * wpp;
     if ((rc = ctx->hits.ensure(std::max<size_t>(nh, 1)))) return rc;
     if (nh) HIP_TRY(hipMemsetAsync(ctx->hits.p, 0, nh * 8, ctx->stream));

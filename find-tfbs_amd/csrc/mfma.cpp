@@ -5,9 +5,9 @@
 // With the window's bases one-hot encoded (4 entries per column, all zero for
 // N), that is a dot product of a 0/1 vector with the strand's weights.  The
 // weights are split exactly as w = 64 a + b, b = ((w + 32) mod 64) - 32 in
-// [-32, 31], a in [-128, 127]; the A operand carries the one-hot twice, once
-// with entries 1 (against b) and once with entries 64 (against a), so both
-// products accumulate into the same int32 score.  |score| <= 32 * 8224, so no
+// [-32, 31], a in [-128, 127]; each K chunk of 32 covers 4 columns twice, the
+// one-hot with entries 1 against b and with entries 64 against a, so one MFMA
+// per 4 columns accumulates the exact int32 score.  |score| <= 32 * 8224, so no
 // intermediate wraps and the sum equals the reference's i32 sum.
 #include <algorithm>
 #include <climits>
@@ -42,7 +42,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
     for (const SlotGroup &g : groups)
         for (int i : g.strands) strands.push_back({i, g.slot});
     if (strands.empty()) return;
-    lds_bytes = std::max<uint32_t>(lds_bytes, 2 * kMMaxChunks * kMFragBytes + kMMetaBytes);
+    lds_bytes = std::max<uint32_t>(lds_bytes, kMMaxChunks * kMFragBytes + kMMetaBytes);
 
     struct TileSrc { size_t first, count; uint32_t nk, lmin; };
     std::vector<TileSrc> tiles;
@@ -59,21 +59,25 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
     while (ti < tiles.size()) {
         // a super tile: consecutive tiles of the same K depth within the LDS budget
         const uint32_t nk = tiles[ti].nk;
-        const uint32_t per = nk * 2 * kMFragBytes + kMMetaBytes;
-        size_t tj = ti + 1;
-        while (tj < tiles.size() && tiles[tj].nk == nk && (tj - ti + 1) * per <= lds_bytes) tj++;
+        const uint32_t per = nk * kMFragBytes + kMMetaBytes;
+        // the run of tiles with this depth, split into equal super tiles
+        size_t run = ti;
+        while (run < tiles.size() && tiles[run].nk == nk) run++;
+        const size_t max_per_super = std::max<size_t>(1, lds_bytes / per);
+        const size_t n_super = (run - ti + max_per_super - 1) / max_per_super;
+        const size_t tj = ti + (run - ti + n_super - 1) / n_super;
         const uint32_t count = (uint32_t)(tj - ti);
         DevMSuper S{};
         S.tile_count = count;
         S.nk = nk;
         S.img_off = (uint32_t)(plan->m_image.size() * 4);
         S.img_bytes = count * per;
-        S.meta_off = count * nk * 2 * kMFragBytes;
+        S.meta_off = count * nk * kMFragBytes;
         S.lmin = UINT32_MAX;
         std::vector<uint8_t> img(S.img_bytes, 0);
         for (uint32_t k = 0; k < count; k++) {
             const TileSrc &t = tiles[ti + k];
-            const uint32_t b_off = k * nk * 2 * kMFragBytes, meta_off = S.meta_off + k * kMMetaBytes;
+            const uint32_t b_off = k * nk * kMFragBytes, meta_off = S.meta_off + k * kMMetaBytes;
             S.lmin = std::min(S.lmin, t.lmin);
             int32_t *thr = reinterpret_cast<int32_t *>(&img[meta_off]);
             uint32_t *len = reinterpret_cast<uint32_t *>(&img[meta_off + 128]);
@@ -95,24 +99,24 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
                     orig[n] = 0xFFFFFFFFu;
                 }
             }
-            // B fragments: lane l holds column n = l & 31, k = 16 (l >> 5) + j,
-            // j = 4 t + c <-> strand column 8 kc + 4 (l >> 5) + t, base c
+            // B fragments: lane l holds column n = l & 31, k = 16 d + j with
+            // d = l >> 5 the digit (0: b, 1: a), j = 4 t + c <-> strand column
+            // 4 kc + t, base c
             for (uint32_t kc = 0; kc < nk; kc++)
-                for (int digit = 0; digit < 2; digit++)
-                    for (int l = 0; l < 64; l++) {
-                        const int n = l & 31, h = l >> 5;
-                        int8_t *frag = reinterpret_cast<int8_t *>(&img[b_off + (kc * 2 + digit) * kMFragBytes + l * 16]);
-                        if ((size_t)n >= t.count) continue;
-                        const Pat &p = P.pats[strands[t.first + n].first];
-                        for (int tt = 0; tt < 4; tt++) {
-                            const uint32_t col = kc * kMChunkCols + 4 * h + tt;
-                            if (col >= p.len) continue;
-                            for (int c = 0; c < 4; c++) {
-                                const int32_t w = p.w5[5 * col + c];
-                                frag[4 * tt + c] = (int8_t)(digit == 0 ? lo_digit(w) : hi_digit(w));
-                            }
+                for (int l = 0; l < 64; l++) {
+                    const int n = l & 31, digit = l >> 5;
+                    int8_t *frag = reinterpret_cast<int8_t *>(&img[b_off + kc * kMFragBytes + l * 16]);
+                    if ((size_t)n >= t.count) continue;
+                    const Pat &p = P.pats[strands[t.first + n].first];
+                    for (int tt = 0; tt < 4; tt++) {
+                        const uint32_t col = kc * kMChunkCols + tt;
+                        if (col >= p.len) continue;
+                        for (int c = 0; c < 4; c++) {
+                            const int32_t w = p.w5[5 * col + c];
+                            frag[4 * tt + c] = (int8_t)(digit == 0 ? lo_digit(w) : hi_digit(w));
                         }
                     }
+                }
         }
         const size_t at = plan->m_image.size();
         plan->m_image.resize(at + (S.img_bytes + 3) / 4, 0);

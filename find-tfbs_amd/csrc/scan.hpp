@@ -30,6 +30,7 @@ struct ScanArgs {
     const DevMSuper *msupers;   // matrix-core path
     uint32_t n_msupers;
     const int32_t *mimage;
+    uint32_t mimg_max;          // LDS bytes reserved for the largest super tile image
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;
     uint32_t n_patterns_total;
@@ -48,7 +49,9 @@ int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
 // Opts the fast kernel into more than 64 KiB of dynamic LDS.
 int fast_kernel_set_lds(const LaunchConfig &cfg);
 // Matrix-core scan (scan_mfma.hip); counts must be zeroed first (atomic adds).
-int launch_mfma(const ScanArgs &a, size_t lds_bytes, int pipe, uint32_t n_haps, hipStream_t stream);
-int mfma_kernel_set_lds(size_t lds_bytes, int pipe);
+// group_words: the most packed words any haplotype group of haps_per_block spans.
+int launch_mfma(const ScanArgs &a, size_t img_bytes, uint32_t group_words, uint32_t n_haps, hipStream_t stream);
+uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
+size_t mfma_lds_fixed();  // LDS bytes the MFMA kernel needs besides the image and words
 
 }  // namespace tfbs

@@ -83,17 +83,18 @@ struct DevTile {
 // Matrix-core path (scan_mfma.hip).  A strand's weights split as w = 64 a + b
 // (a, b int8); the score of 32 windows x 32 strands is one-hot(window bases) x
 // [b; a] with the one-hot entries 1 and 64, summed exactly in int32 by
-// v_mfma_i32_32x32x32_i8.  K chunk = 8 columns x 4 bases.
+// v_mfma_i32_32x32x32_i8.  K chunk (32) = 4 columns x 4 bases x 2 digits:
+// k = 16 d + 4 t + c, d = 0 (entry 1, digit b) or 1 (entry 64, digit a).
 constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
-constexpr int kMChunkCols = 8;     // columns per K chunk of 32
-constexpr int kMMaxChunks = 4;     // L <= 32
+constexpr int kMChunkCols = 4;     // columns per K chunk of 32
+constexpr int kMMaxChunks = 8;     // L <= 32
 constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
 constexpr int kMMetaBytes = 512;   // per tile: thr[32], len[32], slot[32], orig[32]
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk * 2 KiB ([chunk][digit lo, hi][lane
-// 64][16 bytes]), its metadata at meta_off + t * 512.
+// depth nk; tile t's B fragments at t * nk * 1 KiB ([chunk][lane 64][16
+// bytes]), its metadata at meta_off + t * 512.
 struct DevMSuper {
     uint32_t tile_count;
     uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
