@@ -26,6 +26,10 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TOPS = 78.64      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
+MFMA_I8_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense BF16 rate (MI355X_MICROARCH.md, MFMA table)
+# int8 ops of the one-hot formulation per (window, strand, column): 4 bases x 2
+# digits = 8 multiply-adds (scan_mfma.hip); padding (K, windows, strands) excluded
+MFMA_OPS_PER_CELL = 16
 
 
 def parse():
@@ -95,6 +99,28 @@ def cpu_baseline(T, ps, args, budget_s):
                                        threads, wall)}
 
 
+def shard_batch(T, ps, args, rank):
+    """Rank r's share: merged regions [r R, (r+1) R) of the synthetic
+    chromosome, reduced to distinct haplotypes and packed on the host."""
+    batch = T.RegionBatch(ps, args.samples, keep_membership=False)
+    batch.synth_fill(args.seed, rank * args.regions, args.regions, args.indel_pct)
+    return batch
+
+
+def job_totals(dist, elapsed, windows, regions, eff, device):
+    """Max-over-ranks wall time and whole-job sums.  Regions shard with no exchange, so
+    the only collectives are these scalar reductions around the timed region."""
+    if dist is None:
+        return elapsed, float(windows), float(regions), float(eff)
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    w = torch.tensor([windows, regions, eff], dtype=torch.float64, device=device)
+    dist.all_reduce(w, op=dist.ReduceOp.SUM)
+    tot = [float(x) for x in w.tolist()]
+    return float(t.item()), tot[0], tot[1], tot[2]
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -116,8 +142,7 @@ def main():
     ps = T.parse_pwm_files(os.path.join(work, "pwms.txt"), os.path.join(work, "thr"), args.threshold, names)
     sc = T.Scanner(ps, device=local)
     t_prep = time.perf_counter()
-    batch = T.RegionBatch(ps, args.samples, keep_membership=False)
-    batch.synth_fill(args.seed, rank * args.regions, args.regions, args.indel_pct)
+    batch = shard_batch(T, ps, args, rank)
     t_prep = time.perf_counter() - t_prep
     t_up = time.perf_counter()
     batch.scan(sc, upload=True, download=False)
@@ -136,11 +161,12 @@ def main():
             dist.barrier()
 
     barrier()
-    kernel_ms = []
+    kernel_ms, mfma_ms = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         T.check(L.tfbs_scan(sc.h, batch.h))
         kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # waits for this step's end event
+        mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
     T.check(L.tfbs_ctx_sync(sc.h))
     if dist is not None:
         import torch
@@ -158,16 +184,8 @@ def main():
 
     windows = batch.num_windows
     regions = batch.num_regions
-    if dist is not None:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        w = torch.tensor([windows, regions, batch.num_effective_windows], dtype=torch.float64, device="cuda")
-        dist.all_reduce(w, op=dist.ReduceOp.SUM)
-        tot_windows, tot_regions, tot_eff = (float(x) for x in w.tolist())
-    else:
-        tot_windows, tot_regions, tot_eff = float(windows), float(regions), float(batch.num_effective_windows)
+    elapsed, tot_windows, tot_regions, tot_eff = job_totals(dist, elapsed, windows, regions,
+                                                             batch.num_effective_windows, "cuda")
 
     if rank == 0:
         steps = args.steps
@@ -182,11 +200,27 @@ def main():
         if os.path.exists(args.pmc_summary):
             try:
                 pm = json.load(open(args.pmc_summary))
-                if pm.get("workload") == "C3" and pm.get("regions") == args.regions:
+                if (pm.get("workload") == "C3" and pm.get("regions") == args.regions
+                        and pm.get("scan_path") == ("mfma" if min(mfma_ms) > 0 else "lut")):
                     traffic = pm.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         cell_tops = batch.num_cell_ops / (kms / 1e3) / 1e12
+        mms = sum(mfma_ms) / len(mfma_ms)
+        hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+               "note": "algorithmic bytes/launch = packed haplotypes + metadata + pattern tables + u32 counts; "
+                       "the scan is compute bound"}
+        if mms > 0:  # the matrix-core kernel scored every strand of this workload
+            mops = MFMA_OPS_PER_CELL * batch.num_cell_ops / (mms / 1e3) / 1e12
+            roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS",
+                    "frac": mops / MFMA_I8_PEAK_TOPS, "traffic": traffic, "kernel": "scan_mfma_kernel",
+                    "kernel_ms": mms,
+                    "note": "achieved = 16 int8 ops per (window, strand, column) of the one-hot x weight-digit "
+                            "GEMM / the kernel's HIP-event time; traffic = HBM bytes per launch from PMC"}
+        else:
+            roof = hbm
+        path = "mfma" if mms > 0 else "lut"
         out = {
             "metric": "haplotype-windows scored/sec",
             "value": value,
@@ -198,7 +232,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int32",
+            "dtype": "int8->int32" if path == "mfma" else "int32",
             "data": "synthetic (SURVEY.md 8d generator; no HOCOMOCO/BCF download possible)",
             "config": {
                 "workload": "C3" if (args.samples, args.pwms, args.length_config) == (50000, 600, 3) else "custom",
@@ -206,6 +240,7 @@ def main():
                 "region_bp": 201, "pwms": args.pwms, "patterns": len(ps), "threshold": args.threshold,
                 "indel_pct": args.indel_pct, "distinct_haplotypes_per_gpu": batch.num_haplotypes,
                 "windows_per_step": int(tot_windows), "parallelism": "region shard x%d" % world,
+                "scan_path": path,
             },
             "regions_per_s": tot_regions * steps / elapsed,
             "effective_windows_per_s": tot_eff * steps / elapsed,
@@ -214,10 +249,8 @@ def main():
             "upload_s": t_up,
             "key_reduce_s": t_red,
             "dense_download_s": t_dense,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "note": "algorithmic bytes/launch = packed haplotypes + metadata + pattern tables "
-                                 "+ u32 counts written; the scan is VALU/LDS-issue bound (see valu_roofline)"},
+            "roofline": roof,
+            "hbm_roofline": hbm,
             "valu_roofline": {"bound": "valu", "achieved": cell_tops, "peak": VALU_PEAK_TOPS,
                               "unit": "T column-lookups/s vs T int32 lane-ops/s",
                               "frac": cell_tops / VALU_PEAK_TOPS},

@@ -62,6 +62,9 @@ struct tfbs_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the dominant kernel (the MFMA launches)
+    bool kernel_timed = false;
+    float last_kernel_ms = 0.f;
     const Patterns *pats = nullptr;
     Plan plan;
     uint32_t tile_blocks = 20;    // table blocks (4 KiB each) per LDS tile: 80 KiB, two workgroups per CU
@@ -72,8 +75,9 @@ struct tfbs_ctx {
     DevBuf<DevTile> fast_tiles, gen_tiles;
     DevBuf<int32_t> lut, wfull, gen_w, m_image;
     DevBuf<DevMSuper> m_supers;
-    bool mfma = false;
-    uint32_t mfma_lds = 64 * 1024;
+    bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
+    uint32_t mfma_lds = 28 * 1024;  // LDS image budget of one MFMA super tile
+    uint32_t mfma_hpb = 32;         // haplotypes per MFMA workgroup
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
@@ -120,8 +124,12 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
+        m.haps_per_block = ctx->mfma_hpb;
+        HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_group_words, n_haps, ctx->stream);
         if (n < 0) return n;
+        HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
+        ctx->kernel_timed = true;
         launches += n;
     }
     if (!P.fast_tiles.empty()) {
@@ -174,6 +182,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+    if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
+    if (ctx->evk1) (void)hipEventDestroy(ctx->evk1);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -190,8 +200,9 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->tile_blocks = (uint32_t)std::min(36, std::max(8, env_int("TFBS_TILE_BLOCKS", 20)));
     ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 128));
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
-    ctx->mfma = env_int("TFBS_MFMA", 0) != 0;
-    ctx->mfma_lds = (uint32_t)std::min(160, std::max(8, env_int("TFBS_MFMA_LDS_KB", 64))) * 1024u;
+    ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
+    ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 28))) * 1024u;
+    ctx->mfma_hpb = (uint32_t)std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32));
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -209,6 +220,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->evk0);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
     if (e != hipSuccess) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_HIP, std::string("HIP init: ") + hipGetErrorString(e));
@@ -258,6 +271,8 @@ float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx) {
         if (hipEventSynchronize(c->ev1) == hipSuccess) {
             float ms = 0.f;
             if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->last_ms = ms;
+            ms = 0.f;
+            if (c->kernel_timed && hipEventElapsedTime(&ms, c->evk0, c->evk1) == hipSuccess) c->last_kernel_ms = ms;
         }
         c->timing_pending = false;
     }
@@ -265,6 +280,12 @@ float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx) {
 }
 
 int tfbs_ctx_last_scan_launches(const tfbs_ctx *ctx) { return ctx ? ctx->last_launches : 0; }
+
+float tfbs_ctx_last_mfma_ms(const tfbs_ctx *ctx) {
+    if (!ctx) return -1.f;
+    tfbs_ctx_last_scan_ms(ctx);  // resolves the pending events
+    return ctx->kernel_timed ? ctx->last_kernel_ms : -1.f;
+}
 
 int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
@@ -281,7 +302,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
         return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->resident = b;
-    ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->haps_per_block);
+    ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     return TFBS_OK;
 }
 
@@ -290,6 +311,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not uploaded to this ctx");
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    ctx->kernel_timed = false;
     int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
@@ -396,7 +418,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
         (rc = ctx->counts.ensure(1)))
         return rc;
     ctx->resident = nullptr;
-    ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->haps_per_block);
+    ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->mfma_hpb);
     const size_t nh = (size_t)P.pats.size() * wpp;
     if ((rc = ctx->hits.ensure(std::max<size_t>(nh, 1)))) return rc;
     if (nh) HIP_TRY(hipMemsetAsync(ctx->hits.p, 0, nh * 8, ctx->stream));

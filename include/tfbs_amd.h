@@ -122,6 +122,9 @@ int tfbs_ctx_sync(tfbs_ctx *ctx);
 float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx);
 /* Number of scan-kernel launches issued by the last tfbs_scan. */
 int tfbs_ctx_last_scan_launches(const tfbs_ctx *ctx);
+/* Device time (ms) of the last tfbs_scan's matrix-core kernel launches alone
+ * (HIP events on the ctx stream), or -1 if the scan ran no MFMA tile. */
+float tfbs_ctx_last_mfma_ms(const tfbs_ctx *ctx);
 
 /* Replaces matches() (pattern.rs:141-171) for ONE haplotype against every
  * pattern, on the GPU.  nucs are codes 0..4, pos the NucleotidePos.pos values.

@@ -334,9 +334,13 @@ def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
     b = T.RegionBatch(ps, 2000)
     b.synth_fill(13, 0, 200)
     res = []
-    for tb, hpb in [("32", "64"), ("8", "4"), ("64", "16")]:
+    for mfma, tb, hpb in [("0", "32", "64"), ("0", "8", "4"), ("0", "64", "16"), ("1", "12", "5"),
+                          ("1", "64", "64"), ("1", "28", "32")]:
+        monkeypatch.setenv("TFBS_MFMA", mfma)
         monkeypatch.setenv("TFBS_TILE_BLOCKS", tb)
         monkeypatch.setenv("TFBS_HAPS_PER_BLOCK", hpb)
+        monkeypatch.setenv("TFBS_MFMA_LDS_KB", tb)
+        monkeypatch.setenv("TFBS_MFMA_HAPS_PER_BLOCK", hpb)
         sc = T.Scanner(ps)
         b.scan(sc)
         res.append([b.keys(r) for r in (0, 57, 199)])
@@ -345,5 +349,5 @@ def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
         assert [b.keys(r) for r in (0, 57, 199)] == res[-1]
         assert b.rows("chr1")[0] == rows_dense
         sc.close()
-    assert res[0] == res[1] == res[2]
+    assert all(r == res[0] for r in res)
     assert rows_dense.count("\n") > 0

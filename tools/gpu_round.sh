@@ -14,5 +14,5 @@ cat $OUT/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o trace --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu "$@" > $OUT/prof.log 2>&1 || { echo "rocprof trace failed"; tail -20 $OUT/prof.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o pmc -- python3 bench.py --steps 2 --warmup 0 --no-cpu "$@" > $OUT/pmc_fetch.log 2>&1 || { echo "pmc fetch failed"; tail -20 $OUT/pmc_fetch.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o pmc -- python3 bench.py --steps 2 --warmup 0 --no-cpu "$@" > $OUT/pmc_write.log 2>&1 || { echo "pmc write failed"; tail -20 $OUT/pmc_write.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_BUSY_CYCLES --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 2 --warmup 0 --no-cpu "$@" > $OUT/pmc_sq.log 2>&1 || { echo "pmc sq failed"; tail -20 $OUT/pmc_sq.log; }
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc_sq -o pmc -- python3 bench.py --steps 2 --warmup 0 --no-cpu "$@" > $OUT/pmc_sq.log 2>&1 || { echo "pmc sq failed"; tail -20 $OUT/pmc_sq.log; }
 find $OUT -name "*.csv" | head -20
