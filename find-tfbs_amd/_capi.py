@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libtfbs_amd.so")
+# TFBS_LIB overrides the in-tree build (e.g. a host-AddressSanitizer build of the same sources)
+LIB_PATH = os.environ.get("TFBS_LIB") or os.path.join(HERE, "lib", "libtfbs_amd.so")
 
 u8p = C.POINTER(C.c_uint8)
 u16p = C.POINTER(C.c_uint16)
