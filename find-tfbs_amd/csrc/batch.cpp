@@ -6,6 +6,7 @@
 // the same sequence the later one wins (HashMap::insert, haplotype.rs:84); the
 // loser's haplotype ids stay with the reference group (main.rs:103-105, 129-137).
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <cstring>
 #include <numeric>
@@ -138,46 +139,97 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     auto rank_of = [&](const Record *r) {
         return (uint32_t)(std::lower_bound(uniq.begin(), uniq.end(), r, diff_less) - uniq.begin());
     };
+    // Result of load_diffs + group_by_diffs: hap_ids ascending, each haplotype's
+    // diff ranks ascending in hd[span_b[k], span_e[k]), and the groups as runs of
+    // `order` (indices into hap_ids), in ascending Vec<Diff> order.
     std::vector<std::pair<uint32_t, uint32_t>> hd;  // (hap, rank)
-    for (auto &r : I.recs) {
-        if (r.n_alleles != 2 || r.carriers.empty()) continue;
-        uint32_t rk = rank_of(&r);
-        for (uint32_t h : r.carriers)
-            if (h < H) hd.push_back({h, rk});
-    }
-    std::stable_sort(hd.begin(), hd.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
-    // per-hap spans
-    std::vector<uint32_t> hap_ids, span_b, span_e;
-    for (size_t i = 0; i < hd.size();) {
-        size_t j = i;
-        while (j < hd.size() && hd[j].first == hd[i].first) j++;
-        hap_ids.push_back(hd[i].first);
-        span_b.push_back((uint32_t)i);
-        span_e.push_back((uint32_t)j);
-        i = j;
-    }
-    // ---- group_by_diffs: sort haplotypes by diff list (rank order == Vec<Diff> order)
-    std::vector<uint32_t> order(hap_ids.size());
-    std::iota(order.begin(), order.end(), 0);
-    auto seq_less = [&](uint32_t a, uint32_t b) {
-        return std::lexicographical_compare(
-            hd.begin() + span_b[a], hd.begin() + span_e[a], hd.begin() + span_b[b], hd.begin() + span_e[b],
-            [](const auto &x, const auto &y) { return x.second < y.second; });
-    };
-    auto seq_eq = [&](uint32_t a, uint32_t b) {
-        if (span_e[a] - span_b[a] != span_e[b] - span_b[b]) return false;
-        for (uint32_t t = 0; t < span_e[a] - span_b[a]; t++)
-            if (hd[span_b[a] + t].second != hd[span_b[b] + t].second) return false;
-        return true;
-    };
-    std::stable_sort(order.begin(), order.end(), seq_less);
+    std::vector<uint32_t> hap_ids, span_b, span_e, order;
     struct Group { uint32_t first, last; };  // run in `order`
     std::vector<Group> groups;
-    for (uint32_t i = 0; i < order.size();) {
-        uint32_t j = i;
-        while (j < order.size() && seq_eq(order[i], order[j])) j++;
-        groups.push_back({i, j});
-        i = j;
+    if (uniq.size() <= 64) {
+        // every haplotype's diff list as a 64-bit rank mask: one pass over the
+        // carrier lists, one pass over the haplotypes, a hash of the distinct masks
+        thread_local std::vector<uint64_t> sig;
+        if (sig.size() < H) sig.assign(H, 0);
+        for (auto &r : I.recs) {
+            if (r.n_alleles != 2 || r.carriers.empty()) continue;
+            const uint64_t bit = 1ull << rank_of(&r);
+            for (uint32_t h : r.carriers)
+                if (h < H) sig[h] |= bit;
+        }
+        std::unordered_map<uint64_t, uint32_t> gid;  // mask -> distinct mask index
+        std::vector<uint64_t> masks;
+        std::vector<std::vector<uint32_t>> members;  // indices into hap_ids, ascending
+        for (uint32_t h = 0; h < H; h++) {
+            const uint64_t m = sig[h];
+            if (!m) continue;
+            sig[h] = 0;
+            const uint32_t k = (uint32_t)hap_ids.size();
+            hap_ids.push_back(h);
+            span_b.push_back((uint32_t)hd.size());
+            for (uint64_t x = m; x; x &= x - 1) hd.push_back({h, (uint32_t)__builtin_ctzll(x)});
+            span_e.push_back((uint32_t)hd.size());
+            auto it = gid.find(m);
+            if (it == gid.end()) {
+                it = gid.emplace(m, (uint32_t)masks.size()).first;
+                masks.push_back(m);
+                members.emplace_back();
+            }
+            members[it->second].push_back(k);
+        }
+        // Vec<Diff> order of the masks' ascending rank lists
+        auto lex_less = [](uint64_t a, uint64_t b) {
+            const uint64_t d = a ^ b;
+            if (!d) return false;
+            const uint64_t low = d & (~d + 1);  // lowest rank in exactly one list
+            const uint64_t above = ~((low << 1) - 1);
+            return (a & low) ? (b & above) != 0 : (a & above) == 0;
+        };
+        std::vector<uint32_t> gs(masks.size());
+        std::iota(gs.begin(), gs.end(), 0u);
+        std::sort(gs.begin(), gs.end(), [&](uint32_t x, uint32_t y) { return lex_less(masks[x], masks[y]); });
+        for (uint32_t g : gs) {
+            groups.push_back({(uint32_t)order.size(), (uint32_t)(order.size() + members[g].size())});
+            order.insert(order.end(), members[g].begin(), members[g].end());
+        }
+    } else {
+        for (auto &r : I.recs) {
+            if (r.n_alleles != 2 || r.carriers.empty()) continue;
+            uint32_t rk = rank_of(&r);
+            for (uint32_t h : r.carriers)
+                if (h < H) hd.push_back({h, rk});
+        }
+        std::stable_sort(hd.begin(), hd.end(), [](const auto &a, const auto &b) { return a.first < b.first; });
+        // per-hap spans
+        for (size_t i = 0; i < hd.size();) {
+            size_t j = i;
+            while (j < hd.size() && hd[j].first == hd[i].first) j++;
+            hap_ids.push_back(hd[i].first);
+            span_b.push_back((uint32_t)i);
+            span_e.push_back((uint32_t)j);
+            i = j;
+        }
+        // ---- group_by_diffs: sort haplotypes by diff list (rank order == Vec<Diff> order)
+        order.resize(hap_ids.size());
+        std::iota(order.begin(), order.end(), 0);
+        auto seq_less = [&](uint32_t a, uint32_t b) {
+            return std::lexicographical_compare(
+                hd.begin() + span_b[a], hd.begin() + span_e[a], hd.begin() + span_b[b], hd.begin() + span_e[b],
+                [](const auto &x, const auto &y) { return x.second < y.second; });
+        };
+        auto seq_eq = [&](uint32_t a, uint32_t b) {
+            if (span_e[a] - span_b[a] != span_e[b] - span_b[b]) return false;
+            for (uint32_t t = 0; t < span_e[a] - span_b[a]; t++)
+                if (hd[span_b[a] + t].second != hd[span_b[b] + t].second) return false;
+            return true;
+        };
+        std::stable_sort(order.begin(), order.end(), seq_less);
+        for (uint32_t i = 0; i < order.size();) {
+            uint32_t j = i;
+            while (j < order.size() && seq_eq(order[i], order[j])) j++;
+            groups.push_back({i, j});
+            i = j;
+        }
     }
 
     // ---- load_haplotypes: patch each group, dedup by (nucs, pos) sequence; later group wins
@@ -308,10 +360,10 @@ void commit_region(Batch &B, RegionBuilt &&built) {
         B.haps.push_back(hm);
         B.hap_carriers.push_back(carriers[i]);
         uint64_t w = 0;
-        for (uint32_t L : B.pwm_lens)
-            if (n >= L) {
-                w += n - L + 1;
-                B.cell_ops += (uint64_t)(n - L + 1) * L;
+        for (const auto &lc : B.pwm_len_hist)
+            if (n >= lc.first) {
+                w += (uint64_t)(n - lc.first + 1) * lc.second;
+                B.cell_ops += (uint64_t)(n - lc.first + 1) * lc.first * lc.second;
             }
         B.windows += w;
         B.eff_windows += w * carriers[i];
@@ -348,8 +400,10 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     std::sort(B.slots_by_pid.begin(), B.slots_by_pid.end(),
               [&](uint32_t a, uint32_t b) { return B.slot_pid[a] < B.slot_pid[b]; });
     B.n_slots = (uint32_t)plan.slot_pid.size();
+    std::map<uint32_t, uint32_t> lens;
     for (auto &q : P.pats)
-        if (q.kind == TFBS_KIND_PWM && q.len > 0) B.pwm_lens.push_back(q.len);
+        if (q.kind == TFBS_KIND_PWM && q.len > 0) lens[q.len]++;
+    B.pwm_len_hist.assign(lens.begin(), lens.end());
     *out = b;
     return TFBS_OK;
 }

@@ -45,7 +45,7 @@ struct Batch {
     std::vector<uint16_t> slot_pid;       // slot -> pattern_id (slots ordered for the kernels)
     std::vector<uint32_t> slots_by_pid;   // slots in ascending pattern_id (row order)
     std::vector<std::string> beds;        // registered bed basenames
-    std::vector<uint32_t> pwm_lens;       // lengths of scannable strands (for window counting)
+    std::vector<std::pair<uint32_t, uint32_t>> pwm_len_hist;  // (length, strands) of scannable strands
 
     // packed device image
     std::vector<uint32_t> words;          // 2-bit bases, 16 per word, LSB first, +3 pad words per hap

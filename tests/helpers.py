@@ -1,5 +1,6 @@
 """Shared helpers: run the oracle and the product on the same region inputs."""
 import os
+import random
 
 import oracle_py as O
 import tfbs_pkg
@@ -82,3 +83,31 @@ def synth_patterns(tmpdir, n_pwms, config, seed, thr=1e-4, forward_only=False):
     names = T.synth_write_pwms(str(tmpdir), n_pwms, config, seed)
     return T.parse_pwm_files(os.path.join(str(tmpdir), "pwms.txt"), os.path.join(str(tmpdir), "thr"), thr, names,
                              not forward_only), names
+
+
+def many_variant_regions(n_samples, lmax, n_sites=(64, 90), seed=12):
+    """Regions whose distinct diff count straddles 64 (batch.cpp groups haplotypes by
+    a 64-bit diff mask up to 64 distinct diffs and by sorted diff lists beyond):
+    SNVs at distinct positions, a few exact duplicate records (one diff), random
+    carrier sets, and pairs of records carried by the same haplotypes."""
+    rnd = random.Random(seed)
+    regs = []
+    for j, ns in enumerate(n_sites):
+        base = T.SynthRegion(seed, j, n_samples, lmax)
+        ref = base.ref
+        s, e = base.merged
+        es = s - lmax + 1
+        positions = rnd.sample(range(len(ref)), ns)
+        recs = []
+        H = 2 * n_samples
+        for k, p in enumerate(positions):
+            rb = ref[p]
+            if rb == "N":
+                continue
+            alt = rnd.choice([c for c in "ACGT" if c != rb])
+            car = sorted(rnd.sample(range(H), rnd.randint(1, max(1, H // 8))))
+            recs.append(("car", es + p, rb, alt, car))
+            if k % 17 == 0:  # the same diff again with other carriers (one rank)
+                recs.append(("car", es + p, rb, alt, sorted(rnd.sample(range(H), 3))))
+        regs.append({"merged": (s, e), "ref": ref, "records": recs})
+    return regs

@@ -183,3 +183,18 @@ def test_plan_tiles_cover_every_strand(tmp_path):
         st = ps.plan_stats(tb)
         assert st["n_octet_strands"] + st["n_quad_strands"] + st["n_generic_strands"] == len(ps)
         assert st["max_tile_blocks"] <= max(tb, 8)
+
+
+def test_batch_grouping_beyond_64_distinct_diffs(tmp_path):
+    """The 64-bit diff-mask grouping and the sorted-list fallback (> 64 distinct
+    diffs in a region) agree with the oracle's distinct-haplotype counts."""
+    from helpers import build_batch, many_variant_regions
+    ps, _ = synth_patterns(tmp_path, 4, 2, 6)
+    n = 120
+    regions = many_variant_regions(n, ps.max_length)
+    beds = [("synthetic.bed", [tuple(r["merged"]) for r in regions])]
+    _, _, stats = run_oracle(ps, n, beds, regions)
+    b = build_batch(ps, n, beds, regions)
+    for i, (nh, nv, _) in enumerate(stats):
+        assert b.region_stats(i) == (nh, nv)
+    assert max(s[1] for s in stats) > 64

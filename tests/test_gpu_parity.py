@@ -351,3 +351,14 @@ def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
         sc.close()
     assert all(r == res[0] for r in res)
     assert rows_dense.count("\n") > 0
+
+
+def test_many_variant_regions_vs_oracle(tmp_path):
+    """Regions with 64 and ~90 distinct diffs: both haplotype-grouping paths of the
+    host (64-bit diff masks / sorted diff lists) through the GPU scan vs the oracle."""
+    from helpers import many_variant_regions
+    ps, _ = synth_patterns(tmp_path, 10, 2, 31, thr=2e-3)
+    n = 120
+    regions = many_variant_regions(n, ps.max_length)
+    beds = [("synthetic.bed", [tuple(r["merged"]) for r in regions])]
+    _compare(ps, n, beds, regions)
