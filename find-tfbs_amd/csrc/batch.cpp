@@ -146,17 +146,33 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     std::vector<uint32_t> hap_ids, span_b, span_e, order;
     struct Group { uint32_t first, last; };  // run in `order`
     std::vector<Group> groups;
-    if (uniq.size() <= 64) {
+    bool masks_ok = uniq.size() <= 64;
+    thread_local std::vector<uint64_t> sig;
+    if (masks_ok) {
         // every haplotype's diff list as a 64-bit rank mask: one pass over the
-        // carrier lists, one pass over the haplotypes, a hash of the distinct masks
-        thread_local std::vector<uint64_t> sig;
+        // carrier lists, one pass over the haplotypes, a hash of the distinct masks.
+        // A haplotype carrying one diff twice (duplicate records) has the list
+        // [d, d], not [d] (haplotype.rs:65-75): masks cannot say so, so such a
+        // region takes the sorted-list path.
         if (sig.size() < H) sig.assign(H, 0);
+        bool dup = false;
         for (auto &r : I.recs) {
             if (r.n_alleles != 2 || r.carriers.empty()) continue;
             const uint64_t bit = 1ull << rank_of(&r);
             for (uint32_t h : r.carriers)
-                if (h < H) sig[h] |= bit;
+                if (h < H) {
+                    dup |= (sig[h] & bit) != 0;
+                    sig[h] |= bit;
+                }
         }
+        if (dup) {
+            for (auto &r : I.recs)
+                for (uint32_t h : r.carriers)
+                    if (h < H) sig[h] = 0;
+            masks_ok = false;
+        }
+    }
+    if (masks_ok) {
         std::unordered_map<uint64_t, uint32_t> gid;  // mask -> distinct mask index
         std::vector<uint64_t> masks;
         std::vector<std::vector<uint32_t>> members;  // indices into hap_ids, ascending

@@ -107,7 +107,7 @@ def many_variant_regions(n_samples, lmax, n_sites=(64, 90), seed=12):
             alt = rnd.choice([c for c in "ACGT" if c != rb])
             car = sorted(rnd.sample(range(H), rnd.randint(1, max(1, H // 8))))
             recs.append(("car", es + p, rb, alt, car))
-            if k % 17 == 0:  # the same diff again with other carriers (one rank)
+            if k % 17 == 0 and ns > 64:  # the same diff again with other carriers (one rank)
                 recs.append(("car", es + p, rb, alt, sorted(rnd.sample(range(H), 3))))
         regs.append({"merged": (s, e), "ref": ref, "records": recs})
     return regs
