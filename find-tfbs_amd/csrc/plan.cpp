@@ -85,11 +85,9 @@ StrandTab make_tab(const Pat &p) {
 
 void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t tile_blocks, Plan *plan) {
     std::vector<StrandTab> tabs(P.pats.size());
-    std::vector<bool> have(P.pats.size(), false);
     for (auto &g : groups)
         for (int i : g.strands) {
             tabs[i] = make_tab(P.pats[i]);
-            have[i] = true;
         }
     // blocks a tile needs: octet-eligible strands in chunks of 8, the rest in chunks of 4
     auto need = [&](const std::vector<int> &strands) {
@@ -205,7 +203,6 @@ void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
         }
     }
     close_tile();
-    (void)have;
 }
 
 }  // namespace tfbs

@@ -37,7 +37,6 @@ struct ScanArgs {
 };
 
 struct LaunchConfig {
-    uint32_t fast_block = 512;  // threads per fast workgroup
     int minw = 2;               // __launch_bounds__ min waves per SIMD of the fast kernel
     size_t lds_bytes = 0;       // dynamic LDS of the fast kernel
 };
