@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for the timing reductions (gloo: rehearse several ranks on one GPU)")
     ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -131,8 +133,10 @@ def main():
         import torch
         import torch.distributed as dist
 
+        if args.dist_backend == "gloo":  # rehearsal: ranks may share a GPU
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
 
     import tfbs_pkg
 
@@ -185,7 +189,8 @@ def main():
     windows = batch.num_windows
     regions = batch.num_regions
     elapsed, tot_windows, tot_regions, tot_eff = job_totals(dist, elapsed, windows, regions,
-                                                             batch.num_effective_windows, "cuda")
+                                                             batch.num_effective_windows,
+                                                             "cuda" if args.dist_backend == "nccl" else "cpu")
 
     if rank == 0:
         steps = args.steps
