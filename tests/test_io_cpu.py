@@ -4,6 +4,7 @@ import gzip
 import json
 import os
 import random
+import sys
 
 import oracle_py as O
 from helpers import GOLD, TD, T
@@ -57,3 +58,19 @@ def test_merge_ranges_matches_oracle():
     for _ in range(200):
         rs = [(s, s + rnd.randint(0, 30)) for s in (rnd.randint(0, 300) for _ in range(rnd.randint(0, 20)))]
         assert T.merge_ranges(rs) == O.merge_ranges(rs)
+
+
+def test_synthetic_bcf_roundtrip(tmp_path):
+    """tools/synth_dataset.py writes a BGZF BCF2 file; the native reader (f2) returns
+    the same records, alleles and raw GT pairs (unphased/phased 0/1 encodings)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path), n_samples=40, n_regions=6, indel_pct=20)
+    r = T.BcfReader(d["bcf"])
+    assert r.samples == d["samples"]
+    got = r.fetch("chr1", 0, 10 ** 9)
+    assert len(got) == len(d["records"]) > 0
+    for g, w in zip(got, d["records"]):
+        assert (g["pos0"], g["rlen"], g["ref"], g["alt"], g["n_alleles"]) == \
+            (w["pos0"], w["rlen"], w["alleles"][0], w["alleles"][1], 2)
+        assert g["gt"] == w["gt"].astype(int).tolist()

@@ -1,0 +1,136 @@
+#!/usr/bin/env python3
+"""Synthetic find-tfbs input set: FASTA (+.fai), BED, BCF (BGZF, BCF2 GT), samples
+file and HOCOMOCO-format PWMs + thresholds, from the SURVEY.md 8(d) generator
+(the same regions bench.py scans).  Used by the run-flow parity test
+(tests/test_gpu_parity.py) and by tools/bench_run.py.
+
+Layout of the synthetic chromosome "chr1": merged region j is [1000 + 400 j,
+1200 + 400 j]; the bases of every region's extended window come from the
+generator; the rest of the chromosome is A.  Variants: the generator's records,
+each sample's GT written as phased pairs (left alt = 1 -> GT[0] = 4 (Unphased(1)),
+right alt -> GT[1] = 5 (Phased(1)), references 2 / 3), which load_diffs
+(haplotype.rs:34-41) reads back as the same carrier sets.
+
+Usage: python tools/synth_dataset.py OUTDIR [--samples N] [--regions R] [--pwms P]
+       [--length-config C] [--seed S] [--indel-pct I]
+"""
+import argparse
+import os
+import struct
+import sys
+import zlib
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def bgzf_blocks(data):
+    """BGZF framing (SAM spec 4.1): <= 64 KiB-input deflate blocks + the EOF block."""
+    out = bytearray()
+    for i in range(0, len(data), 65280):
+        chunk = bytes(data[i:i + 65280])
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        comp = co.compress(chunk) + co.flush()
+        bsize = len(comp) + 25
+        out += struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize)
+        out += comp
+        out += struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    return bytes(out)
+
+
+def typed_str(s):
+    b = s.encode()
+    if len(b) < 15:
+        return bytes([(len(b) << 4) | 7]) + b
+    return bytes([0xF7, 0x11, len(b)]) + b  # length as a typed int8
+
+
+def bcf_record(chrom, pos0, ref, alt, gt_pairs):
+    """One BCF2 record: no QUAL/ID/FILTER/INFO, FORMAT GT as int8 pairs."""
+    n_sample = gt_pairs.shape[0]
+    shared = struct.pack("<iiif", chrom, pos0, len(ref), struct.unpack("<f", struct.pack("<I", 0x7F800001))[0])
+    shared += struct.pack("<II", (2 << 16) | 0, (1 << 24) | n_sample)
+    shared += typed_str("") + typed_str(ref) + typed_str(alt) + bytes([0x00])  # ID '.', alleles, FILTER none
+    indiv = bytes([0x11, 1, 0x21]) + gt_pairs.astype(np.int8).tobytes()  # key GT (dict index 1), 2 x int8
+    return struct.pack("<II", len(shared), len(indiv)) + shared + indiv
+
+
+def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0):
+    import tfbs_pkg
+    T = tfbs_pkg.load()
+    os.makedirs(out, exist_ok=True)
+    names = T.synth_write_pwms(out, n_pwms, length_config, seed)
+    ps = T.parse_pwm_files(os.path.join(out, "pwms.txt"), os.path.join(out, "thr"), 1e-4, names)
+    lmax = ps.max_length
+    samples = ["S%05d" % i for i in range(n_samples)]
+    H = 2 * n_samples
+    regions, records = [], []
+    chrom_len = 1000 + 400 * n_regions + 1000
+    seq = bytearray(b"A" * chrom_len)
+    for j in range(n_regions):
+        r = T.SynthRegion(seed, j, n_samples, lmax, indel_pct)
+        s, e = r.merged
+        regions.append((s, e))
+        es = r.ext_start
+        seq[es:es + len(r.ref)] = r.ref.encode()
+        for pos, ref, alt, car in r.records:
+            gt = np.empty((n_samples, 2), dtype=np.int8)
+            gt[:, 0] = 2
+            gt[:, 1] = 3
+            car = np.asarray(car, dtype=np.int64)
+            car = car[car < H]
+            gt[car[car % 2 == 0] // 2, 0] = 4
+            gt[car[car % 2 == 1] // 2, 1] = 5
+            records.append({"chrom": "chr1", "pos0": pos, "rlen": len(ref), "alleles": [ref, alt], "gt": gt})
+    records.sort(key=lambda x: x["pos0"])
+    # FASTA + .fai
+    fa = os.path.join(out, "genome.fa")
+    with open(fa, "w") as f:
+        f.write(">chr1\n")
+        for i in range(0, chrom_len, 60):
+            f.write(seq[i:i + 60].decode() + "\n")
+    with open(fa + ".fai", "w") as f:
+        f.write("chr1\t%d\t6\t60\t61\n" % chrom_len)
+    # BED (half-open in the file; find-tfbs reads [start, end] inclusive, bed.rs:15)
+    bed = os.path.join(out, "regions.bed")
+    with open(bed, "w") as f:
+        for s, e in regions:
+            f.write("chr1\t%d\t%d\n" % (s, e))
+    with open(os.path.join(out, "samples"), "w") as f:
+        f.write("\n".join(samples) + "\n")
+    # BCF
+    header = ("##fileformat=VCFv4.2\n##FILTER=<ID=PASS,Description=\"All filters passed\">\n"
+              "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+              "##contig=<ID=chr1,length=%d>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t%s\n"
+              % (chrom_len, "\t".join(samples))).encode() + b"\0"
+    body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+    for rec in records:
+        body += bcf_record(0, rec["pos0"], rec["alleles"][0], rec["alleles"][1], rec["gt"])
+    bcf = os.path.join(out, "genotypes.bcf")
+    with open(bcf, "wb") as f:
+        f.write(bgzf_blocks(body))
+    return {"dir": out, "fasta": fa, "bed": bed, "bcf": bcf, "samples": samples, "names": names,
+            "pwm_file": os.path.join(out, "pwms.txt"), "thr_dir": os.path.join(out, "thr"),
+            "records": records, "regions": regions}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("out")
+    ap.add_argument("--samples", type=int, default=200)
+    ap.add_argument("--regions", type=int, default=20)
+    ap.add_argument("--pwms", type=int, default=8)
+    ap.add_argument("--length-config", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=3)
+    ap.add_argument("--indel-pct", type=int, default=0)
+    a = ap.parse_args()
+    d = make_dataset(a.out, a.samples, a.regions, a.pwms, a.length_config, a.seed, a.indel_pct)
+    print("wrote %s: %d records, %d regions, %d samples" % (d["bcf"], len(d["records"]), len(d["regions"]),
+                                                           len(d["samples"])))
+
+
+if __name__ == "__main__":
+    main()
