@@ -188,18 +188,9 @@ size_t type_size(int t) {
 }
 }  // namespace
 
-int Bcf::open(const std::string &path) {
-    std::string raw, data;
-    int rc = read_file(path, raw);
-    if (rc) return rc;
-    rc = bgzf_inflate(raw, data);
-    if (rc) return rc;
-    if (data.size() < 9 || memcmp(data.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
-    uint32_t l_text;
-    memcpy(&l_text, data.data() + 5, 4);
-    if (9ull + l_text > data.size()) return fail(TFBS_E_PARSE, "truncated BCF header");
-    std::string text(data.data() + 9, l_text);
-    // header dictionaries (VCF 4.3 / BCF2): strings PASS + FILTER/INFO/FORMAT (IDX= wins), contigs
+// Header dictionaries (VCF 4.3 / BCF2): strings PASS + FILTER/INFO/FORMAT (IDX= wins), contigs.
+static void parse_bcf_header(const std::string &text, std::vector<std::string> &samples,
+                             std::vector<std::string> &contigs, int &gt_key) {
     std::map<int, std::string> sdict;
     sdict[0] = "PASS";
     int next = 1, cnext = 0;
@@ -236,73 +227,101 @@ int Bcf::open(const std::string &path) {
             for (size_t i = 9; i < cols.size(); i++) samples.push_back(cols[i]);
         }
     }
-    int gt_key = -1;
+    gt_key = -1;
     for (auto &kv : sdict)
         if (kv.second == "GT") gt_key = kv.first;
+}
+
+// One BCF2 record (l_shared, l_indiv, shared, indiv) at p.  GT is kept raw for
+// the samples in sel (all samples if sel is null): 2 ints each, vector_end and
+// absent values as INT32_MIN + 1.
+static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, size_t ns, int gt_key,
+                             const std::vector<size_t> *sel, BcfRecord &r, int32_t &chrom) {
+    uint32_t l_shared, l_indiv;
+    memcpy(&l_shared, p, 4);
+    memcpy(&l_indiv, p + 4, 4);
+    p += 8;
+    if ((size_t)(end - p) < (size_t)l_shared + l_indiv) return fail(TFBS_E_PARSE, "truncated BCF record");
+    Cur sh{p, p + l_shared};
+    Cur in{p + l_shared, p + l_shared + l_indiv};
+    p += l_shared + l_indiv;
+    int32_t pos, rlen;
+    uint32_t nai, nfs;
+    if (!sh.need(24)) return fail(TFBS_E_PARSE, "short BCF record");
+    memcpy(&chrom, sh.p, 4);
+    memcpy(&pos, sh.p + 4, 4);
+    memcpy(&rlen, sh.p + 8, 4);
+    memcpy(&nai, sh.p + 16, 4);
+    memcpy(&nfs, sh.p + 20, 4);
+    sh.p += 24;
+    r.pos = (uint64_t)(int64_t)pos;
+    r.rlen = (uint32_t)std::max(rlen, 0);
+    const uint32_t n_allele = nai >> 16;
+    const uint32_t n_fmt = nfs >> 24;
+    r.n_alleles = n_allele;
+    r.ref.clear();
+    r.alt.clear();
+    int t;
+    uint32_t n;
+    if (!typed(sh, t, n) || !sh.need(n * type_size(t))) return fail(TFBS_E_PARSE, "bad BCF ID");
+    sh.p += n * type_size(t);
+    for (uint32_t a = 0; a < n_allele; a++) {
+        if (!typed(sh, t, n) || !sh.need(n)) return fail(TFBS_E_PARSE, "bad BCF allele");
+        std::string al((const char *)sh.p, n);
+        sh.p += n;
+        while (!al.empty() && al.back() == '\0') al.pop_back();
+        if (a == 0) r.ref = al;
+        else if (a == 1) r.alt = al;
+    }
+    const size_t nk = sel ? sel->size() : ns;
+    r.gt.assign(2 * nk, INT32_MIN + 1);
+    for (uint32_t f = 0; f < n_fmt; f++) {
+        int kt;
+        uint32_t kn;
+        int64_t key;
+        if (!typed(in, kt, kn) || kn != 1 || !read_int(in, kt, key)) return fail(TFBS_E_PARSE, "bad FORMAT key");
+        int vt;
+        uint32_t vn;
+        if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
+        const size_t sz = type_size(vt);
+        if (!in.need(sz * vn * ns)) return fail(TFBS_E_PARSE, "truncated FORMAT data");
+        if (key == gt_key && vt >= 1 && vt <= 3) {
+            const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
+            const unsigned char *base = in.p;
+            for (size_t k = 0; k < nk; k++) {
+                const size_t s = sel ? (*sel)[k] : k;
+                Cur c{base + sz * vn * s, base + sz * vn * (s + 1)};
+                for (uint32_t q = 0; q < vn && q < 2; q++) {
+                    int64_t v;
+                    read_int(c, vt, v);
+                    r.gt[2 * k + q] = v == ve ? INT32_MIN + 1 : (int32_t)v;
+                }
+            }
+        }
+        in.p += sz * vn * ns;
+    }
+    return TFBS_OK;
+}
+
+int Bcf::open(const std::string &path) {
+    std::string raw, data;
+    int rc = read_file(path, raw);
+    if (rc) return rc;
+    rc = bgzf_inflate(raw, data);
+    if (rc) return rc;
+    if (data.size() < 9 || memcmp(data.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
+    uint32_t l_text;
+    memcpy(&l_text, data.data() + 5, 4);
+    if (9ull + l_text > data.size()) return fail(TFBS_E_PARSE, "truncated BCF header");
+    int gt_key = -1;
+    parse_bcf_header(std::string(data.data() + 9, l_text), samples, contigs, gt_key);
     per_contig.assign(contigs.size(), {});
     const unsigned char *p = (const unsigned char *)data.data() + 9 + l_text;
     const unsigned char *end = (const unsigned char *)data.data() + data.size();
-    const size_t ns = samples.size();
     while (p + 8 <= end) {
-        uint32_t l_shared, l_indiv;
-        memcpy(&l_shared, p, 4);
-        memcpy(&l_indiv, p + 4, 4);
-        p += 8;
-        if ((size_t)(end - p) < (size_t)l_shared + l_indiv) return fail(TFBS_E_PARSE, "truncated BCF record");
-        Cur sh{p, p + l_shared};
-        Cur in{p + l_shared, p + l_shared + l_indiv};
-        p += l_shared + l_indiv;
         BcfRecord r;
-        int32_t chrom, pos, rlen;
-        uint32_t nai, nfs;
-        if (!sh.need(24)) return fail(TFBS_E_PARSE, "short BCF record");
-        memcpy(&chrom, sh.p, 4);
-        memcpy(&pos, sh.p + 4, 4);
-        memcpy(&rlen, sh.p + 8, 4);
-        memcpy(&nai, sh.p + 16, 4);
-        memcpy(&nfs, sh.p + 20, 4);
-        sh.p += 24;
-        r.pos = (uint64_t)(int64_t)pos;
-        r.rlen = (uint32_t)std::max(rlen, 0);
-        const uint32_t n_allele = nai >> 16;
-        const uint32_t n_fmt = nfs >> 24;
-        r.n_alleles = n_allele;
-        int t;
-        uint32_t n;
-        if (!typed(sh, t, n) || !sh.need(n * type_size(t))) return fail(TFBS_E_PARSE, "bad BCF ID");
-        sh.p += n * type_size(t);
-        for (uint32_t a = 0; a < n_allele; a++) {
-            if (!typed(sh, t, n) || !sh.need(n)) return fail(TFBS_E_PARSE, "bad BCF allele");
-            std::string al((const char *)sh.p, n);
-            sh.p += n;
-            while (!al.empty() && al.back() == '\0') al.pop_back();
-            if (a == 0) r.ref = al;
-            else if (a == 1) r.alt = al;
-        }
-        r.gt.assign(2 * ns, INT32_MIN + 1);
-        for (uint32_t f = 0; f < n_fmt; f++) {
-            int kt;
-            uint32_t kn;
-            int64_t key;
-            if (!typed(in, kt, kn) || kn != 1 || !read_int(in, kt, key)) return fail(TFBS_E_PARSE, "bad FORMAT key");
-            int vt;
-            uint32_t vn;
-            if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
-            const size_t sz = type_size(vt);
-            if (!in.need(sz * vn * ns)) return fail(TFBS_E_PARSE, "truncated FORMAT data");
-            if (key == gt_key && vt >= 1 && vt <= 3) {
-                const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
-                for (size_t s = 0; s < ns; s++) {
-                    for (uint32_t k = 0; k < vn; k++) {
-                        int64_t v;
-                        read_int(in, vt, v);
-                        if (k < 2) r.gt[2 * s + k] = v == ve ? INT32_MIN + 1 : (int32_t)v;
-                    }
-                }
-            } else {
-                in.p += sz * vn * ns;
-            }
-        }
+        int32_t chrom;
+        if ((rc = decode_bcf_record(p, end, samples.size(), gt_key, nullptr, r, chrom))) return rc;
         if (chrom < 0 || (size_t)chrom >= contigs.size()) return fail(TFBS_E_PARSE, "BCF record with unknown contig");
         per_contig[chrom].push_back(std::move(r));
     }
