@@ -466,13 +466,22 @@ def run(chromosome, bcf, bed_files, reference_genome_file, wanted_samples, pwm_f
 
 
 class BcfReader:
-    """Minimal BCF2 reader (f2): IndexedReader::from_path + fetch + records (raw GT)."""
+    """Streaming BCF2 reader (f2): IndexedReader::from_path + fetch + records (raw GT).
+    fetch() with nondecreasing beg on one contig reads the file once."""
 
     def __init__(self, path):
         self.h = C.c_void_p()
         check(lib().tfbs_bcf_open(_u(path), C.byref(self.h)))
         n = lib().tfbs_bcf_num_samples(self.h)
         self.samples = [lib().tfbs_bcf_sample_name(self.h, i).decode() for i in range(n)]
+        self.selected = list(range(n))
+
+    def select(self, idx):
+        """Decode GT only for these sample indices, in this order."""
+        idx = [int(i) for i in idx]
+        arr = (C.c_size_t * max(1, len(idx)))(*idx)
+        check(lib().tfbs_bcf_select(self.h, arr, len(idx)))
+        self.selected = idx
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -483,7 +492,7 @@ class BcfReader:
         n = C.c_size_t()
         check(lib().tfbs_bcf_fetch(self.h, _u(chrom), beg, end, C.byref(n)))
         out = []
-        ns = len(self.samples)
+        ns = len(self.selected)
         for i in range(n.value):
             pos, rlen, na = C.c_uint64(), C.c_uint32(), C.c_uint32()
             ref, alt = C.c_char_p(), C.c_char_p()

@@ -103,6 +103,7 @@ SIGNATURES = [
     ("tfbs_run", C.c_int, [C.c_void_p]),
     ("tfbs_bcf_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),
     ("tfbs_bcf_close", None, [vp]),
+    ("tfbs_bcf_select", C.c_int, [vp, C.POINTER(C.c_size_t), C.c_size_t]),
     ("tfbs_bcf_num_samples", C.c_size_t, [vp]),
     ("tfbs_bcf_sample_name", C.c_char_p, [vp, C.c_size_t]),
     ("tfbs_bcf_fetch", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_size_t)]),

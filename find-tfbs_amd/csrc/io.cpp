@@ -18,6 +18,7 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "tfbs_internal.hpp"
@@ -285,7 +286,16 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
         const size_t sz = type_size(vt);
         if (!in.need(sz * vn * ns)) return fail(TFBS_E_PARSE, "truncated FORMAT data");
-        if (key == gt_key && vt >= 1 && vt <= 3) {
+        if (key == gt_key && vt == 1 && vn == 2) {  // the common diploid int8 layout
+            const int8_t *g = (const int8_t *)in.p;
+            int32_t *o = r.gt.data();
+            for (size_t k = 0; k < nk; k++) {
+                const size_t s = sel ? (*sel)[k] : k;
+                const int8_t a = g[2 * s], b = g[2 * s + 1];
+                o[2 * k] = a == -127 ? INT32_MIN + 1 : a;
+                o[2 * k + 1] = b == -127 ? INT32_MIN + 1 : b;
+            }
+        } else if (key == gt_key && vt >= 1 && vt <= 3) {
             const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
             const unsigned char *base = in.p;
             for (size_t k = 0; k < nk; k++) {
@@ -303,39 +313,213 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
     return TFBS_OK;
 }
 
-int Bcf::open(const std::string &path) {
-    std::string raw, data;
-    int rc = read_file(path, raw);
+// run fn(t) for t in [0, n) on up to `threads` threads
+template <class F> static void par_for(size_t n, uint32_t threads, F fn) {
+    const size_t T = std::min<size_t>(std::max<uint32_t>(threads, 1), n);
+    if (T <= 1) {
+        for (size_t i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < T; t++)
+        ts.emplace_back([&, t] {
+            for (size_t i = t * n / T; i < (t + 1) * n / T; i++) fn(i);
+        });
+    for (auto &x : ts) x.join();
+}
+
+Bcf::~Bcf() {
+    if (f) fclose(f);
+}
+
+int Bcf::open(const std::string &p, uint32_t nthreads) {
+    path = p;
+    threads = nthreads ? nthreads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("TFBS_BCF_CHUNK_KB")) chunk = std::max<size_t>(1, (size_t)atoll(e)) << 10;
+    int rc = rewind();
     if (rc) return rc;
-    rc = bgzf_inflate(raw, data);
-    if (rc) return rc;
-    if (data.size() < 9 || memcmp(data.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
+    sel.resize(samples.size());
+    for (size_t i = 0; i < sel.size(); i++) sel[i] = i;
+    all_samples = true;
+    return TFBS_OK;
+}
+
+int Bcf::select(const std::vector<size_t> &s) {
+    for (size_t i : s)
+        if (i >= samples.size()) return fail(TFBS_E_ARG, "sample index out of range");
+    sel = s;
+    all_samples = sel.size() == samples.size();
+    for (size_t i = 0; all_samples && i < sel.size(); i++) all_samples = sel[i] == i;
+    cur = -1;  // decoded GT columns change: drop the window
+    return rewind();
+}
+
+// (Re)start at the first record: header parsed again, window emptied.
+int Bcf::rewind() {
+    if (f) fclose(f);
+    f = fopen(path.c_str(), "rb");
+    if (!f) return fail(TFBS_E_IO, "Could not open file " + path);
+    cbuf.clear();
+    dbuf.clear();
+    doff = 0;
+    in_eof = done = seen = false;
+    win.clear();
+    last_beg = last_pos = 0;
+    unsigned char m[4] = {0, 0, 0, 0};
+    const size_t got = fread(m, 1, 4, f);
+    fseek(f, 0, SEEK_SET);
+    bgzf = got == 4 && m[0] == 0x1f && m[1] == 0x8b && m[2] == 8 && (m[3] & 4);
+    if (!bgzf) {  // plain gzip members: inflate the whole file at once
+        std::string raw;
+        int rc = read_file(path, raw);
+        if (rc) return rc;
+        if ((rc = bgzf_inflate(raw, dbuf))) return rc;
+        in_eof = true;
+    }
+    while (dbuf.size() < 9 && !in_eof)
+        if (int rc = inflate_more()) return rc;
+    if (dbuf.size() < 9 || memcmp(dbuf.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
     uint32_t l_text;
-    memcpy(&l_text, data.data() + 5, 4);
-    if (9ull + l_text > data.size()) return fail(TFBS_E_PARSE, "truncated BCF header");
-    int gt_key = -1;
-    parse_bcf_header(std::string(data.data() + 9, l_text), samples, contigs, gt_key);
-    per_contig.assign(contigs.size(), {});
-    const unsigned char *p = (const unsigned char *)data.data() + 9 + l_text;
-    const unsigned char *end = (const unsigned char *)data.data() + data.size();
-    while (p + 8 <= end) {
-        BcfRecord r;
-        int32_t chrom;
-        if ((rc = decode_bcf_record(p, end, samples.size(), gt_key, nullptr, r, chrom))) return rc;
-        if (chrom < 0 || (size_t)chrom >= contigs.size()) return fail(TFBS_E_PARSE, "BCF record with unknown contig");
-        per_contig[chrom].push_back(std::move(r));
+    memcpy(&l_text, dbuf.data() + 5, 4);
+    while (dbuf.size() < 9ull + l_text && !in_eof)
+        if (int rc = inflate_more()) return rc;
+    if (9ull + l_text > dbuf.size()) return fail(TFBS_E_PARSE, "truncated BCF header");
+    std::vector<std::string> s, c;
+    parse_bcf_header(std::string(dbuf.data() + 9, l_text), s, c, gt_key);
+    if (samples.empty() && contigs.empty()) {
+        samples = std::move(s);
+        contigs = std::move(c);
     }
-    // overlap queries: per contig the running max of pos + rlen allows a binary search
-    max_end.assign(contigs.size(), {});
-    for (size_t c = 0; c < per_contig.size(); c++) {
-        auto &v = per_contig[c];
-        std::stable_sort(v.begin(), v.end(), [](const BcfRecord &a, const BcfRecord &b) { return a.pos < b.pos; });
-        uint64_t m = 0;
-        for (auto &r : v) {
-            m = std::max(m, r.pos + r.rlen);
-            max_end[c].push_back(m);
+    doff = 9 + l_text;
+    return TFBS_OK;
+}
+
+// Read up to `chunk` compressed bytes, inflate every complete BGZF block in
+// parallel and append the output to dbuf.
+int Bcf::inflate_more() {
+    if (in_eof) return TFBS_OK;
+    if (doff) {
+        dbuf.erase(0, doff);
+        doff = 0;
+    }
+    const size_t have = cbuf.size();
+    cbuf.resize(have + chunk);
+    const size_t got = fread(&cbuf[have], 1, chunk, f);
+    cbuf.resize(have + got);
+    const bool file_end = got < chunk;
+    struct Blk {
+        size_t off, len, out, isize;
+    };
+    std::vector<Blk> blks;
+    size_t o = 0, out = dbuf.size();
+    const unsigned char *c = (const unsigned char *)cbuf.data();
+    while (o + 18 <= cbuf.size()) {
+        if (c[o] != 0x1f || c[o + 1] != 0x8b || c[o + 2] != 8 || !(c[o + 3] & 4))
+            return fail(TFBS_E_PARSE, "corrupt BGZF block header in " + path);
+        const size_t xlen = c[o + 10] | (c[o + 11] << 8);
+        size_t bsize = 0;
+        for (size_t x = o + 12; x + 4 <= o + 12 + xlen && x + 4 <= cbuf.size();) {
+            const size_t slen = c[x + 2] | (c[x + 3] << 8);
+            if (c[x] == 'B' && c[x + 1] == 'C' && slen == 2 && x + 6 <= cbuf.size()) bsize = (c[x + 4] | (c[x + 5] << 8)) + 1;
+            x += 4 + slen;
         }
+        if (!bsize) {
+            if (o + 12 + xlen <= cbuf.size()) return fail(TFBS_E_PARSE, "BGZF block without BSIZE in " + path);
+            break;
+        }
+        if (o + bsize > cbuf.size()) break;
+        if (bsize < 12 + xlen + 8) return fail(TFBS_E_PARSE, "corrupt BGZF block size in " + path);
+        uint32_t isize;
+        memcpy(&isize, c + o + bsize - 4, 4);
+        blks.push_back({o + 12 + xlen, bsize - 12 - xlen - 8, out, isize});
+        out += isize;
+        o += bsize;
     }
+    if (file_end && o < cbuf.size() && blks.empty()) return fail(TFBS_E_PARSE, "truncated BGZF file " + path);
+    dbuf.resize(out);
+    std::vector<int> bad(blks.size(), 0);
+    par_for(blks.size(), blks.size() >= 4 ? threads : 1, [&](size_t i) {
+        const Blk &b = blks[i];
+        if (!b.isize) return;
+        z_stream zs;
+        memset(&zs, 0, sizeof zs);
+        if (inflateInit2(&zs, -15) != Z_OK) {
+            bad[i] = 1;
+            return;
+        }
+        zs.next_in = (Bytef *)(c + b.off);
+        zs.avail_in = (uInt)b.len;
+        zs.next_out = (Bytef *)&dbuf[b.out];
+        zs.avail_out = (uInt)b.isize;
+        const int rc = inflate(&zs, Z_FINISH);
+        bad[i] = rc != Z_STREAM_END || zs.total_out != b.isize;
+        inflateEnd(&zs);
+    });
+    for (int x : bad)
+        if (x) return fail(TFBS_E_IO, "corrupt BGZF data in " + path);
+    cbuf.erase(0, o);
+    if (file_end && cbuf.empty()) in_eof = true;
+    return TFBS_OK;
+}
+
+// Decode the next run of complete records of contig `cur` into the window.
+// Records of other contigs are skipped unread; once the contig's records are
+// over (a later contig follows them) the stream is done.
+int Bcf::fill() {
+    std::vector<size_t> offs;
+    for (;;) {
+        size_t o = doff;
+        const unsigned char *d = (const unsigned char *)dbuf.data();
+        while (o + 8 <= dbuf.size()) {
+            uint32_t ls, li;
+            memcpy(&ls, d + o, 4);
+            memcpy(&li, d + o + 4, 4);
+            const size_t n = 8 + (size_t)ls + li;
+            if (o + n > dbuf.size()) break;
+            if (ls < 24) return fail(TFBS_E_PARSE, "short BCF record");
+            int32_t chrom, pos;
+            memcpy(&chrom, d + o + 8, 4);
+            memcpy(&pos, d + o + 12, 4);
+            if (chrom < 0 || (size_t)chrom >= contigs.size()) return fail(TFBS_E_PARSE, "BCF record with unknown contig");
+            if (chrom == cur) {
+                const uint64_t p = (uint64_t)(int64_t)pos;
+                if (seen && p < last_pos)
+                    return fail(TFBS_E_PARSE, "BCF records are not sorted by position (an indexed BCF is): " + path);
+                seen = true;
+                last_pos = p;
+                offs.push_back(o);
+            } else if (seen) {
+                done = true;
+                break;
+            }
+            o += n;
+        }
+        doff = o;
+        if (done || !offs.empty()) break;
+        if (in_eof) {
+            if (doff + 8 <= dbuf.size()) return fail(TFBS_E_PARSE, "truncated BCF record");
+            done = true;
+            break;
+        }
+        if (int rc = inflate_more()) return rc;
+    }
+    const size_t base = win.size();
+    win.resize(base + offs.size());
+    std::vector<int> rcs(offs.size(), TFBS_OK);
+    const unsigned char *end = (const unsigned char *)dbuf.data() + dbuf.size();
+    const std::vector<size_t> *s = all_samples ? nullptr : &sel;
+    par_for(offs.size(), offs.size() >= 64 ? threads : 1, [&](size_t i) {
+        const unsigned char *p = (const unsigned char *)dbuf.data() + offs[i];
+        int32_t chrom;
+        rcs[i] = decode_bcf_record(p, end, samples.size(), gt_key, s, win[base + i], chrom);
+    });
+    for (size_t i = 0; i < rcs.size(); i++)
+        if (rcs[i]) {  // decode again on this thread for the (thread-local) error message
+            const unsigned char *p = (const unsigned char *)dbuf.data() + offs[i];
+            int32_t chrom;
+            BcfRecord r;
+            return decode_bcf_record(p, end, samples.size(), gt_key, s, r, chrom);
+        }
     return TFBS_OK;
 }
 
@@ -345,15 +529,28 @@ int Bcf::contig_index(const std::string &name) const {
     return -1;
 }
 
-void Bcf::fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out) const {
+int Bcf::fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out) {
     out.clear();
-    if (contig < 0 || (size_t)contig >= per_contig.size()) return;
-    const auto &v = per_contig[contig];
-    const auto &me = max_end[contig];
-    // first record whose running max end exceeds beg
-    size_t lo = (size_t)(std::upper_bound(me.begin(), me.end(), beg) - me.begin());
-    for (size_t i = lo; i < v.size() && v[i].pos < end; i++)
-        if (v[i].pos + v[i].rlen > beg) out.push_back(&v[i]);
+    if (contig < 0 || (size_t)contig >= contigs.size()) return TFBS_OK;
+    if (contig != cur || beg < last_beg) {
+        if (int rc = rewind()) return rc;
+        cur = contig;
+    }
+    last_beg = beg;
+    // drop what no later query (beg' >= beg) can overlap
+    size_t k = 0;
+    while (k < win.size() && win[k].pos + win[k].rlen <= beg) k++;
+    if (k) win.erase(win.begin(), win.begin() + k);
+    if (win.size() > 4096)
+        win.erase(std::remove_if(win.begin(), win.end(), [&](const BcfRecord &r) { return r.pos + r.rlen <= beg; }),
+                  win.end());
+    while (!done && (win.empty() || win.back().pos < end))
+        if (int rc = fill()) return rc;
+    for (const BcfRecord &r : win) {
+        if (r.pos >= end) break;
+        if (r.pos + r.rlen > beg) out.push_back(&r);
+    }
+    return TFBS_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -32,19 +32,47 @@ struct BcfRecord {
     uint32_t rlen = 0;
     uint32_t n_alleles = 0;
     std::string ref, alt;   // alleles[0], alleles[1] (alt empty if a single allele)
-    std::vector<int32_t> gt;  // 2 raw GT ints per sample (all samples), INT32_MIN+1 = vector_end
+    std::vector<int32_t> gt;  // 2 raw GT ints per selected sample, INT32_MIN+1 = vector_end / absent
 };
 
+// Streaming BCF2 reader (f2; replaces rust_htslib's IndexedReader::fetch +
+// records(), haplotype.rs:78-82).  BGZF blocks are inflated chunk by chunk in
+// parallel threads, record boundaries are found serially and records are
+// decoded in parallel, for one contig at a time, keeping GT only for the
+// selected samples.  fetch() keeps a window of the records that can still
+// overlap a later query, so a sweep with nondecreasing `beg` (the run flow's
+// sorted merged regions) reads the file once; a query that goes backwards or
+// to another contig rewinds to the start of the file.  Input must be sorted
+// by position within a contig (an indexed BCF is); unsorted input fails.
 class Bcf {
   public:
-    int open(const std::string &path);
+    int open(const std::string &path, uint32_t threads = 0);
+    // GT columns kept, in this order (default: all samples); rewinds the stream.
+    int select(const std::vector<size_t> &sel);
     int contig_index(const std::string &name) const;
-    void fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out) const;
+    // records with pos < end && pos + rlen > beg, in file order; pointers stay
+    // valid until the next fetch
+    int fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out);
+    ~Bcf();
     std::vector<std::string> samples, contigs;
 
   private:
-    std::vector<std::vector<BcfRecord>> per_contig;
-    std::vector<std::vector<uint64_t>> max_end;
+    int rewind();
+    int inflate_more();
+    int fill();
+    std::string path;
+    FILE *f = nullptr;
+    uint32_t threads = 1;
+    size_t chunk = 8u << 20;            // compressed bytes read per inflate round
+    bool bgzf = true, in_eof = false, done = false, seen = false;
+    std::string cbuf, dbuf;             // compressed tail not yet inflated; inflated bytes from doff on
+    size_t doff = 0;
+    int gt_key = -1;
+    std::vector<size_t> sel;
+    bool all_samples = true;
+    int cur = -1;                       // contig of the window
+    uint64_t last_beg = 0, last_pos = 0;
+    std::vector<BcfRecord> win;         // window of decoded records of contig `cur`, file order
 };
 
 class Fasta {

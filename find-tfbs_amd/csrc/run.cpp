@@ -107,7 +107,7 @@ int tfbs_run(const tfbs_run_args *a) {
 
     // BCF + samples (main.rs:255, 293-314)
     Bcf bcf;
-    rc = bcf.open(a->bcf);
+    rc = bcf.open(a->bcf, std::max(1u, a->threads));
     if (rc) return rc;
     std::vector<size_t> sel;
     if (a->samples_file && *a->samples_file) {
@@ -122,6 +122,7 @@ int tfbs_run(const tfbs_run_args *a) {
     } else {
         for (size_t i = 0; i < bcf.samples.size(); i++) sel.push_back(i);
     }
+    if ((rc = bcf.select(sel))) return rc;  // GT decoded for these samples only
     const int rid = bcf.contig_index(chrom);
     Fasta fasta;
     rc = fasta.open(a->reference);
@@ -147,7 +148,6 @@ int tfbs_run(const tfbs_run_args *a) {
     const uint32_t threads = std::max(1u, a->threads);
     const size_t per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
     uint32_t fake = 1;
-    std::vector<int32_t> gt(2 * sel.size());
     std::vector<const BcfRecord *> recs;
     for (size_t r0 = 0; r0 < merged.size(); r0 += per_batch) {
         tfbs_batch *bb = nullptr;
@@ -182,15 +182,11 @@ int tfbs_run(const tfbs_run_args *a) {
                 }
             // load_diffs (haplotype.rs:78-80): name2rid(chrom).unwrap() panics on an unknown contig
             if (rid < 0) return fail(TFBS_E_ARG, "chromosome " + chrom + " not in the BCF header");
-            bcf.fetch(rid, in.R.es, in.R.ee + 1, recs);
+            if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return rc;
             for (const BcfRecord *br : recs) {
-                for (size_t k = 0; k < sel.size(); k++) {
-                    gt[2 * k] = br->gt[2 * sel[k]];
-                    gt[2 * k + 1] = br->gt[2 * sel[k] + 1];
-                }
                 Record rec;
                 rc = make_record_gt((uint32_t)sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
-                                    br->n_alleles >= 2 ? br->alt.c_str() : nullptr, gt.data(), rec);
+                                    br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->gt.data(), rec);
                 if (rc) return rc;
                 in.recs.push_back(std::move(rec));
             }
@@ -244,6 +240,11 @@ int tfbs_bcf_open(const char *path, tfbs_bcf **out) {
     return TFBS_OK;
 }
 void tfbs_bcf_close(tfbs_bcf *b) { delete b; }
+int tfbs_bcf_select(tfbs_bcf *b, const size_t *idx, size_t n) {
+    if (!b || (n && !idx)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    b->cur.clear();
+    return b->b.select(std::vector<size_t>(idx, idx + n));
+}
 size_t tfbs_bcf_num_samples(const tfbs_bcf *b) { return b ? b->b.samples.size() : 0; }
 const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i) {
     return (b && i < b->b.samples.size()) ? b->b.samples[i].c_str() : nullptr;
@@ -252,7 +253,8 @@ int tfbs_bcf_fetch(tfbs_bcf *b, const char *chrom, uint64_t beg, uint64_t end, s
     if (!b || !chrom || !n) return tfbs::fail(TFBS_E_ARG, "null argument");
     const int rid = b->b.contig_index(chrom);
     if (rid < 0) return tfbs::fail(TFBS_E_ARG, std::string("unknown contig ") + chrom);
-    b->b.fetch(rid, beg, end, b->cur);
+    const int rc = b->b.fetch(rid, beg, end, b->cur);
+    if (rc) return rc;
     *n = b->cur.size();
     return TFBS_OK;
 }

@@ -259,9 +259,14 @@ int tfbs_bcf_open(const char *path, tfbs_bcf **out);
 void tfbs_bcf_close(tfbs_bcf *b);
 size_t tfbs_bcf_num_samples(const tfbs_bcf *b);
 const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i);
-/* Replaces reader.fetch(rid, beg, end) (haplotype.rs:79): records with pos < end && pos + rlen > beg. */
+/* Samples whose GT is decoded, in this order (default: all); main.rs:293-314's sample selection,
+ * applied while decoding.  Rewinds the stream. */
+int tfbs_bcf_select(tfbs_bcf *b, const size_t *idx, size_t n);
+/* Replaces reader.fetch(rid, beg, end) (haplotype.rs:79): records with pos < end && pos + rlen > beg,
+ * in file order.  Streams the file: queries with nondecreasing beg on one contig read it once,
+ * an earlier beg or another contig rewinds to the start. */
 int tfbs_bcf_fetch(tfbs_bcf *b, const char *chrom, uint64_t beg, uint64_t end, size_t *n_records);
-/* Record i of the last fetch: raw GT ints, 2 per BCF sample, INT32_MIN+1 = vector_end; alt NULL
+/* Record i of the last fetch: raw GT ints, 2 per selected sample, INT32_MIN+1 = vector_end; alt NULL
  * for a single-allele record. */
 int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, uint32_t *n_alleles, const char **ref,
                     const char **alt, const int32_t **gt);

@@ -6,6 +6,8 @@ import os
 import random
 import sys
 
+import pytest
+
 import oracle_py as O
 from helpers import GOLD, TD, T
 
@@ -74,3 +76,55 @@ def test_synthetic_bcf_roundtrip(tmp_path):
         assert (g["pos0"], g["rlen"], g["ref"], g["alt"], g["n_alleles"]) == \
             (w["pos0"], w["rlen"], w["alleles"][0], w["alleles"][1], 2)
         assert g["gt"] == w["gt"].astype(int).tolist()
+
+
+def _want(records, beg, end, sel):
+    return [(w["pos0"], w["rlen"], w["alleles"][0], w["alleles"][1], w["gt"][sel].astype(int).tolist())
+            for w in records if w["pos0"] < end and w["pos0"] + w["rlen"] > beg]
+
+
+def test_bcf_stream_sweep_select_and_rewind(tmp_path, monkeypatch):
+    """Streaming reader: 1 KiB read chunks (records and BGZF blocks span chunks),
+    a sample subset in permuted order, a sweep of overlapping windows with
+    nondecreasing beg (the run flow's access pattern), then queries that go
+    backwards (rewind); every answer equals a brute-force filter of the records."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import numpy as np
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path), n_samples=70, n_regions=25, indel_pct=25, seed=9)
+    monkeypatch.setenv("TFBS_BCF_CHUNK_KB", "1")
+    r = T.BcfReader(d["bcf"])
+    sel = [5, 3, 69, 0, 41, 41, 12]
+    r.select(sel)
+    sel = np.asarray(sel)
+    got = lambda b, e: [(g["pos0"], g["rlen"], g["ref"], g["alt"], g["gt"]) for g in r.fetch("chr1", b, e)]
+    n_hit = 0
+    for (s, e) in d["regions"]:
+        for b, z in ((s - 40, e + 40), (s - 5, s + 30), (e - 10, e + 200)):
+            w = _want(d["records"], b, z, sel)
+            n_hit += len(w)
+            assert got(b, z) == w
+    assert n_hit > 0
+    for (s, e) in reversed(d["regions"][:6]):
+        assert got(s - 30, e + 30) == _want(d["records"], s - 30, e + 30, sel)
+    assert got(0, 10 ** 9) == _want(d["records"], 0, 10 ** 9, sel)
+
+
+def test_bcf_stream_rejects_unsorted(tmp_path):
+    """An indexed BCF is position-sorted; the streaming reader fails loudly on
+    records that go backwards instead of silently missing them."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import numpy as np
+    import struct
+    import synth_dataset
+    header = ("##fileformat=VCFv4.2\n##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+              "##contig=<ID=chr1,length=1000>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tA\n").encode() + b"\0"
+    body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+    gt = np.array([[4, 3]], dtype=np.int8)
+    for pos in (100, 50):
+        body += synth_dataset.bcf_record(0, pos, "A", "C", gt)
+    p = str(tmp_path / "unsorted.bcf")
+    open(p, "wb").write(synth_dataset.bgzf_blocks(body))
+    r = T.BcfReader(p)
+    with pytest.raises(Exception, match="not sorted"):
+        r.fetch("chr1", 0, 1000)

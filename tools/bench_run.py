@@ -7,6 +7,7 @@ Usage: python tools/bench_run.py [--samples 1000] [--regions 1000] [--pwms 10]
        [--length-config 2] [--threads 16] [--regions-per-batch 512]
 """
 import argparse
+import ctypes
 import gzip
 import json
 import os
@@ -39,8 +40,11 @@ def main():
     t_gen = time.perf_counter() - t
     out = os.path.join(work, "out.vcf.gz")
     t = time.perf_counter()
-    r = T.BcfReader(d["bcf"])  # native BGZF inflate + BCF2 decode of the whole file (f2)
+    r = T.BcfReader(d["bcf"])  # streaming reader (f2): parallel BGZF inflate + BCF2 decode of the whole contig
+    n = ctypes.c_size_t()
+    T.check(T.lib().tfbs_bcf_fetch(r.h, b"chr1", 0, 1 << 40, ctypes.byref(n)))
     t_bcf = time.perf_counter() - t
+    assert n.value == len(d["records"])
     n_rec = len(d["records"])
     del r
     t = time.perf_counter()
