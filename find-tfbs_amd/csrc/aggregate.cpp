@@ -7,10 +7,13 @@
 // times the multiplicity of the range in that bed list.  counts_as_genotypes
 // (main.rs:439-498) and the row format (main.rs:415-429) follow.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "batch.hpp"
 
@@ -140,45 +143,75 @@ static std::string strip_chr(const std::string &c) {
     return o;
 }
 
-int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out) {
+// Rows of one region, each without its "<chr>\t<POS>\t" prefix (the POS
+// counter is assigned in order afterwards).
+static void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<std::string> &rows) {
+    const uint32_t H = 2 * B.n_samples;
+    std::vector<uint32_t> l(B.n_samples), r(B.n_samples);
+    Membership M(R, H);
+    std::string info, gts;
+    for (const KeyRef &k : region_keys(B, R)) {
+        if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
+        for (uint32_t s = 0; s < B.n_samples; s++) {
+            l[s] = count_of(B, R, M.local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
+            r[s] = count_of(B, R, M.local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
+        }
+        uint32_t maf = 0;
+        info.clear();
+        gts.clear();
+        if (!counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts)) continue;
+        if (maf < min_maf) continue;
+        const uint16_t pid = B.slot_pid[k.slot];
+        auto it = B.pats->names.find(pid);
+        const std::string &pname = it == B.pats->names.end() ? std::string() : it->second;
+        std::string row;
+        row.reserve(B.beds[k.ik->bed].size() + pname.size() + info.size() + gts.size() + 64);
+        row += B.beds[k.ik->bed];
+        row += ',';
+        row += pname;
+        char head[96];
+        snprintf(head, sizeof head, ",%llu-%llu\t.\t.\t.\tPASS\t", (unsigned long long)k.ik->s,
+                 (unsigned long long)k.ik->e);
+        row += head;
+        row += info;
+        row += "\tGT:DS";
+        row += gts;
+        row += '\n';
+        rows.push_back(std::move(row));
+    }
+}
+
+// Pseudo-VCF rows (main.rs:395-432) of every region in batch order, regions
+// formatted in parallel on `threads` threads, POS counter `fake` in row order.
+int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out,
+               uint32_t threads) {
     if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
     const std::string chr = strip_chr(chrom);
-    const uint32_t H = 2 * B.n_samples;
-    std::vector<uint32_t> l(B.n_samples), r(B.n_samples);
-    for (const RegionH &R : B.rh) {
-        if (R.hap_count == 0) continue;
-        Membership M(R, H);
-        for (const KeyRef &k : region_keys(B, R)) {
-            if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
-            for (uint32_t s = 0; s < B.n_samples; s++) {
-                l[s] = count_of(B, R, M.local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
-                r[s] = count_of(B, R, M.local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
-            }
-            uint32_t maf = 0;
-            std::string info, gts;
-            if (!counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts)) continue;
-            if (maf < min_maf) continue;
-            const uint16_t pid = B.slot_pid[k.slot];
-            auto it = B.pats->names.find(pid);
-            const std::string &pname = it == B.pats->names.end() ? std::string() : it->second;
-            char head[96];
-            snprintf(head, sizeof head, "\t%u\t", *fake);
+    const size_t n = B.rh.size();
+    std::vector<std::vector<std::string>> rows(n);
+    std::atomic<size_t> next(0);
+    auto work = [&]() {
+        for (size_t j; (j = next.fetch_add(1)) < n;)
+            if (B.rh[j].hap_count) region_rows(B, B.rh[j], min_maf, rows[j]);
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
+    work();
+    for (auto &t : ts) t.join();
+    size_t bytes = out.size();
+    for (auto &v : rows)
+        for (auto &r : v) bytes += r.size() + chr.size() + 16;
+    out.reserve(bytes);
+    char head[32];
+    for (auto &v : rows)
+        for (auto &r : v) {
+            const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
             out += chr;
-            out += head;
-            out += B.beds[k.ik->bed];
-            out += ',';
-            out += pname;
-            snprintf(head, sizeof head, ",%llu-%llu\t.\t.\t.\tPASS\t", (unsigned long long)k.ik->s,
-                     (unsigned long long)k.ik->e);
-            out += head;
-            out += info;
-            out += "\tGT:DS";
-            out += gts;
-            out += '\n';
+            out.append(head, (size_t)m);
+            out += r;
             (*fake)++;
         }
-    }
     return TFBS_OK;
 }
 
@@ -224,7 +257,7 @@ int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_ma
                     size_t *len) {
     if (!b || !chromosome || !fake || !text || !len) return tfbs::fail(TFBS_E_ARG, "null argument");
     std::string out;
-    int rc = tfbs::batch_rows(b->b, chromosome, min_maf, fake, out);
+    int rc = tfbs::batch_rows(b->b, chromosome, min_maf, fake, out, 1);
     if (rc) return rc;
     char *p = (char *)malloc(out.size() + 1);
     if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");

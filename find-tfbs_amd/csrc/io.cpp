@@ -26,6 +26,21 @@
 
 namespace tfbs {
 
+// run fn(t) for t in [0, n) on up to `threads` threads
+template <class F> static void par_for(size_t n, uint32_t threads, F fn) {
+    const size_t T = std::min<size_t>(std::max<uint32_t>(threads, 1), n);
+    if (T <= 1) {
+        for (size_t i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (size_t t = 0; t < T; t++)
+        ts.emplace_back([&, t] {
+            for (size_t i = t * n / T; i < (t + 1) * n / T; i++) fn(i);
+        });
+    for (auto &x : ts) x.join();
+}
+
 static int read_file(const std::string &path, std::string &out) {
     std::ifstream in(path, std::ios::binary);
     if (!in) return fail(TFBS_E_IO, "Could not open file " + path);
@@ -101,37 +116,55 @@ int bgzf_block(const char *data, size_t n, std::string &out) {
     return TFBS_OK;
 }
 
-int BgzfWriter::open(const std::string &path) {
+int BgzfWriter::open(const std::string &path, uint32_t nthreads) {
     f = fopen(path.c_str(), "wb");
     if (!f) return fail(TFBS_E_IO, "Could not create output file " + path);
+    threads = std::max(1u, nthreads);
     return TFBS_OK;
 }
 int BgzfWriter::write(const char *p, size_t n) {
     while (n) {
-        const size_t take = std::min(n, kBlock - buf.size());
-        buf.append(p, take);
+        const size_t open_at = ends.empty() ? 0 : ends.back();
+        const size_t take = std::min(n, kBlock - (raw.size() - open_at));
+        raw.append(p, take);
         p += take;
         n -= take;
-        if (buf.size() == kBlock) {
-            int rc = emit();
-            if (rc) return rc;
+        if (raw.size() - open_at == kBlock) {
+            ends.push_back(raw.size());
+            if (ends.size() >= 8 * (size_t)threads)
+                if (int rc = drain()) return rc;
         }
     }
     return TFBS_OK;
 }
-int BgzfWriter::emit() {
-    std::string blk;
-    int rc = bgzf_block(buf.data(), buf.size(), blk);
-    if (rc) return rc;
-    if (fwrite(blk.data(), 1, blk.size(), f) != blk.size()) return fail(TFBS_E_IO, "write failed");
-    buf.clear();
+// deflate the queued blocks in parallel, write them in order, keep the open block
+int BgzfWriter::drain() {
+    const size_t nb = ends.size();
+    if (!nb) return TFBS_OK;
+    std::vector<std::string> out(nb);
+    std::vector<int> rcs(nb, TFBS_OK);
+    par_for(nb, threads, [&](size_t i) {
+        const size_t b = i ? ends[i - 1] : 0;
+        rcs[i] = bgzf_block(raw.data() + b, ends[i] - b, out[i]);
+    });
+    for (size_t i = 0; i < nb; i++) {
+        if (rcs[i]) return fail(TFBS_E_IO, "deflate failed");
+        if (fwrite(out[i].data(), 1, out[i].size(), f) != out[i].size()) return fail(TFBS_E_IO, "write failed");
+    }
+    raw.erase(0, ends.back());
+    ends.clear();
     return TFBS_OK;
 }
-int BgzfWriter::flush() { return emit(); }  // like BGzWriter::flush: ends the block (empty block if nothing buffered)
+// like BGzWriter::flush: ends the block (an empty block if nothing is buffered)
+int BgzfWriter::flush() {
+    ends.push_back(raw.size());
+    return ends.size() >= 8 * (size_t)threads ? drain() : TFBS_OK;
+}
 int BgzfWriter::close() {
     if (!f) return TFBS_OK;
     int rc = TFBS_OK;
-    if (!buf.empty()) rc = emit();
+    if (raw.size() > (ends.empty() ? 0 : ends.back())) ends.push_back(raw.size());
+    rc = drain();
     if (!rc && fwrite(kBgzfEof, 1, sizeof kBgzfEof, f) != sizeof kBgzfEof) rc = fail(TFBS_E_IO, "write failed");
     fclose(f);
     f = nullptr;
@@ -311,21 +344,6 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         in.p += sz * vn * ns;
     }
     return TFBS_OK;
-}
-
-// run fn(t) for t in [0, n) on up to `threads` threads
-template <class F> static void par_for(size_t n, uint32_t threads, F fn) {
-    const size_t T = std::min<size_t>(std::max<uint32_t>(threads, 1), n);
-    if (T <= 1) {
-        for (size_t i = 0; i < n; i++) fn(i);
-        return;
-    }
-    std::vector<std::thread> ts;
-    for (size_t t = 0; t < T; t++)
-        ts.emplace_back([&, t] {
-            for (size_t i = t * n / T; i < (t + 1) * n / T; i++) fn(i);
-        });
-    for (auto &x : ts) x.join();
 }
 
 Bcf::~Bcf() {

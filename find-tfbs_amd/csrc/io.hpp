@@ -12,19 +12,25 @@ namespace tfbs {
 int bgzf_inflate(const std::string &in, std::string &out);
 int bgzf_block(const char *data, size_t n, std::string &out);
 
+// BGZF writer with the block boundaries of BGzWriter (main.rs:267-276): a
+// block every kBlock input bytes and at each flush().  Full blocks are queued
+// and deflated in parallel (`threads`), then written in order, so the bytes
+// are those of a one-block-at-a-time writer.
 class BgzfWriter {
   public:
     static constexpr size_t kBlock = 65280;  // htslib/bgzip's BGZF_BLOCK_SIZE of input per block
-    int open(const std::string &path);
+    int open(const std::string &path, uint32_t threads = 1);
     int write(const char *p, size_t n);
     int flush();
     int close();
     ~BgzfWriter();
 
   private:
-    int emit();
+    int drain();
     FILE *f = nullptr;
-    std::string buf;
+    uint32_t threads = 1;
+    std::string raw;                   // queued input: blocks back to back, then the open block
+    std::vector<size_t> ends;          // end offset in raw of each queued (closed) block
 };
 
 struct BcfRecord {

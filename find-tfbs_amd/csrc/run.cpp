@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,7 +29,8 @@
 #include "patterns.hpp"
 
 namespace tfbs {
-int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out);
+int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out,
+               uint32_t threads);
 }
 
 namespace {
@@ -131,7 +133,7 @@ int tfbs_run(const tfbs_run_args *a) {
     // output (main.rs:264-290, 320-324)
     const std::string out = a->output, part = out + ".part";
     BgzfWriter w;
-    rc = w.open(part);
+    rc = w.open(part, std::max(1u, a->threads));
     if (rc) return rc;
     std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
     for (size_t i : sel) header += "\t" + bcf.samples[i];
@@ -148,12 +150,16 @@ int tfbs_run(const tfbs_run_args *a) {
     const uint32_t threads = std::max(1u, a->threads);
     const size_t per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
     uint32_t fake = 1;
+    using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
+    // Host side of one batch (main.rs:147-186 per merged region): FASTA window,
+    // BCF records, inner peaks, distinct haplotypes.  Runs on a helper thread
+    // while the previous batch is on the GPU / being formatted.
     std::vector<const BcfRecord *> recs;
-    for (size_t r0 = 0; r0 < merged.size(); r0 += per_batch) {
+    auto prepare = [&](size_t r0, BatchPtr &out, std::string &err) -> int {
         tfbs_batch *bb = nullptr;
-        rc = tfbs_batch_create(pp, (uint32_t)sel.size(), 1, &bb);
-        if (rc) return rc;
-        std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)> bguard(bb, tfbs_batch_destroy);
+        int rc = tfbs_batch_create(pp, (uint32_t)sel.size(), 1, &bb);
+        if (rc) return err = tfbs_last_error(), rc;
+        out = BatchPtr(bb, tfbs_batch_destroy);
         Batch &B = bb->b;
         for (auto &b : beds) B.beds.push_back(b.first);
         std::vector<RegionInput> ins;
@@ -163,14 +169,17 @@ int tfbs_run(const tfbs_run_args *a) {
             in.R.ms = m.first;
             in.R.me = m.second;
             rc = tfbs_batch_region_ext(bb, m.first, m.second, &in.R.es, &in.R.ee);
-            if (rc) return rc;
+            if (rc) return err = tfbs_last_error(), rc;
             std::string ref;
             rc = fasta.fetch(chrom, in.R.es, in.R.ee + 1, ref);  // main.rs:156-161
-            if (rc) return rc;
+            if (rc) return err = tfbs_last_error(), rc;
             in.ref.resize(ref.size());
             for (size_t i = 0; i < ref.size(); i++) {
                 const int c = to_nuc((uint8_t)ref[i]);
-                if (c < 0) return fail(TFBS_E_BADBASE, "Unknown nucleotide " + std::to_string((int)(uint8_t)ref[i]));
+                if (c < 0) {
+                    err = "Unknown nucleotide " + std::to_string((int)(uint8_t)ref[i]);
+                    return TFBS_E_BADBASE;
+                }
                 in.ref[i] = (uint8_t)c;
             }
             // select_inner_peaks (main.rs:62-72): p.overlaps(merged)
@@ -181,35 +190,92 @@ int tfbs_run(const tfbs_run_args *a) {
                     if (ov) in.inner.push_back({(uint32_t)bi, {p.first, p.second}});
                 }
             // load_diffs (haplotype.rs:78-80): name2rid(chrom).unwrap() panics on an unknown contig
-            if (rid < 0) return fail(TFBS_E_ARG, "chromosome " + chrom + " not in the BCF header");
-            if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return rc;
+            if (rid < 0) {
+                err = "chromosome " + chrom + " not in the BCF header";
+                return TFBS_E_ARG;
+            }
+            if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
             for (const BcfRecord *br : recs) {
                 Record rec;
                 rc = make_record_gt((uint32_t)sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
                                     br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->gt.data(), rec);
-                if (rc) return rc;
+                if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
             ins.push_back(std::move(in));
         }
         rc = add_regions(B, ins, threads);
-        if (rc) return rc;
+        if (rc) return err = tfbs_last_error(), rc;
+        return TFBS_OK;
+    };
+    // per-phase wall time (TFBS_RUN_TIMING=1 prints it to stderr)
+    const bool timing = getenv("TFBS_RUN_TIMING") && atoi(getenv("TFBS_RUN_TIMING"));
+    double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0, t_write = 0;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
+    BatchPtr cur(nullptr, tfbs_batch_destroy);
+    std::string err;
+    if (!merged.empty()) {
+        double t0 = now();
+        if ((rc = prepare(0, cur, err))) return fail(rc, err);
+        t_prep += now() - t0;
+    }
+    for (size_t r0 = 0; r0 < merged.size(); r0 += per_batch) {
+        BatchPtr next(nullptr, tfbs_batch_destroy);
+        std::string nerr;
+        int nrc = TFBS_OK;
+        double nprep = 0;
+        std::thread helper;
+        if (r0 + per_batch < merged.size())
+            helper = std::thread([&, r0] {
+                const double t0 = now();
+                nrc = prepare(r0 + per_batch, next, nerr);
+                nprep = now() - t0;
+            });
+        // join the helper on every exit path
+        struct Joiner {
+            std::thread &t;
+            ~Joiner() {
+                if (t.joinable()) t.join();
+            }
+        } joiner{helper};
+        tfbs_batch *bb = cur.get();
+        Batch &B = bb->b;
+        double t0 = now();
         if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)))
             return rc;
+        double t1 = now();
+        t_gpu += t1 - t0;
         std::string rows;
-        rc = batch_rows(B, chrom, a->min_maf, &fake, rows);
+        rc = batch_rows(B, chrom, a->min_maf, &fake, rows, threads);
         if (rc) return rc;
+        double t2 = now();
+        t_rows += t2 - t1;
         rc = w.write(rows.data(), rows.size());
         if (rc) return rc;
+        t_write += now() - t2;
         if (a->verbose) {
             for (size_t r = 0; r < B.rh.size(); r++)
                 fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", r0 + r + 1, merged.size(),
                         (unsigned long long)B.rh[r].ms, (unsigned long long)B.rh[r].me, B.rh[r].hap_count,
                         B.rh[r].n_variants);
         }
+        t0 = now();
+        if (helper.joinable()) helper.join();
+        t_wait += now() - t0;
+        t_prep += nprep;
+        if (nrc) return fail(nrc, nerr);
+        cur = std::move(next);
     }
     // the reference flushes twice before drop (main.rs:271, 275): two empty blocks
+    double t0 = now();
     if ((rc = w.flush()) || (rc = w.flush()) || (rc = w.close())) return rc;
+    t_write += now() - t0;
+    if (timing)
+        fprintf(stderr,
+                "tfbs_run_timing {\"prep_s\": %.4f, \"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, "
+                "\"write_s\": %.4f, \"loop_s\": %.4f}\n",
+                t_prep, t_wait, t_gpu, t_rows, t_write, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +
                                 part + "'";
