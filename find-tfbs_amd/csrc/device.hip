@@ -78,6 +78,8 @@ struct tfbs_ctx {
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
     uint32_t mfma_lds = 28 * 1024;  // LDS image budget of one MFMA super tile
     uint32_t mfma_hpb = 32;         // haplotypes per MFMA workgroup
+    uint32_t mfma_waves = 4;        // waves per MFMA workgroup (4, 8)
+    uint32_t mfma_roll = 0;         // rolling tile loop (TFBS_MFMA_ROLL)
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
@@ -125,8 +127,9 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
         m.haps_per_block = ctx->mfma_hpb;
+        m.mfma_roll = ctx->mfma_roll;
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
-        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_group_words, n_haps, ctx->stream);
+        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_group_words, n_haps, ctx->mfma_waves, ctx->stream);
         if (n < 0) return n;
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
@@ -203,6 +206,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 28))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32));
+    ctx->mfma_waves = (uint32_t)env_int("TFBS_MFMA_WAVES", 4);
+    ctx->mfma_roll = (uint32_t)env_int("TFBS_MFMA_ROLL", 0);
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;

@@ -34,12 +34,18 @@
 namespace tfbs {
 namespace {
 
+// Bottleneck probes (tools/probe_build.sh, never in the product build):
+// TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live), =2 reads every
+// B fragment from tile 0, =3 skips the hit handling (results wrong; timing only).
+#ifndef TFBS_MFMA_PROBE
+#define TFBS_MFMA_PROBE 0
+#endif
+
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int kMBlock = 256;          // 4 waves, one per SIMD
 constexpr int kMOnehotBytes = 8192;   // LDS: one-hot tables (entries 1 | entries 64), image, words
-constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup with 4 workgroups per CU
+constexpr uint32_t kMStagedPerWave = 10 * 1024;  // LDS per wave at 16 waves per CU (160 KiB)
 
 // The packed words (and N-mask words) a lane needs for its window of the
 // 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
@@ -66,8 +72,8 @@ __device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *w
 
 // A fragments of the 32-window tile at i0: chunk kc = columns 4 kc .. 4 kc + 3
 // of the lane's window, as one-hot bytes with entry 1 (lanes 0-31) or 64
-// (lanes 32-63), read from the LDS table by the 4-mer code.  Bases past the
-// haplotype end or N are zeroed only in the tiles that have them.
+// (lanes 32-63), read from the LDS table by the 4-mer code; N bases zeroed in
+// haplotypes that have them.
 template <int NK>
 __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint32_t lane, const WinWords &ww,
                                              const char *s_onehot, v4i (&a)[NK]) {
@@ -82,11 +88,10 @@ __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint
         const uint32_t code = __builtin_amdgcn_ubfe(kc < 4 ? img_lo : img_hi, 8 * (kc & 3), 8);
         a[kc] = *reinterpret_cast<const v4i *>(tab + code * 16);
     }
-    if ((hm.flags & HAP_HAS_N) || i0 + 2 * kMWindows - 1 > hm.len) {
-        // bases that exist and are not N
-        const int32_t rem = (int32_t)hm.len - (int32_t)i;
-        uint32_t vm = rem >= 32 ? 0xFFFFFFFFu : (rem <= 0 ? 0u : ((1u << rem) - 1u));
-        vm &= ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31);
+    // Bases past the haplotype end need no mask: they only reach windows with
+    // i + L > len (rejected in tile_hits) or columns >= L (zero weights).
+    if (hm.flags & HAP_HAS_N) {  // N scores 0 (pattern.rs:119-135): clear its one-hot
+        const uint32_t vm = ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31);
 #pragma unroll
         for (int kc = 0; kc < NK; kc++)
 #pragma unroll
@@ -103,7 +108,7 @@ struct BFrag {
 template <int NK>
 __device__ __forceinline__ void load_tile(const char *s_img, const DevMSuper &S, uint32_t ti, uint32_t lane,
                                           BFrag<NK> &f) {
-    const char *p = s_img + ti * (NK * kMFragBytes) + lane * 16;
+    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes) + lane * 16;
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
     f.thr = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes)[lane & 31];
@@ -117,24 +122,51 @@ __device__ __forceinline__ v16i tile_scores(const v4i (&a)[NK], const BFrag<NK> 
     return acc;
 }
 
-struct HapCtx {
-    DevHap hm;
-    uint32_t hap, n_inner;
-    const int32_t *inner;
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+
+// haplotype / region descriptors as wave-uniform (SGPR) values
+__device__ __forceinline__ DevHap load_hap(const DevHap *p) {
+    DevHap h = *p;
+    h.word_off = uni(h.word_off);
+    h.len = uni(h.len);
+    h.region = uni(h.region);
+    h.flags = uni(h.flags);
+    h.nmask_off = uni(h.nmask_off);
+    h.pos_off = uni(h.pos_off);
+    h.count_off = ((uint64_t)uni((uint32_t)(h.count_off >> 32)) << 32) | uni((uint32_t)h.count_off);
+    return h;
+}
+
+// Hit-handling context in LDS, so that the out-of-line rare path takes only
+// the scores and a few scalars as arguments (all in registers, no scratch).
+struct KernelHitCtx {
+    uint32_t *counts;
+    const int32_t *posrel;
+    unsigned long long *hits;
+    uint32_t hits_wpp, n_pat;
 };
+struct WaveHitCtx {  // written by the wave at each haplotype
+    const int32_t *inner;
+    uint64_t count_off;
+    uint32_t len, flags, pos_off, hap, n_inner, pad;
+};
+constexpr int kMMaxWaves = 8;
+__shared__ KernelHitCtx s_kctx;
+__shared__ WaveHitCtx s_wctx[kMMaxWaves];
+extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot tables | image | words
 
 // The rare path of check_tile, out of line so that its registers do not
-// constrain the hot loop; everything by value (an address-taken argument would
-// route the caller's haplotype state through scratch).  Registers are tested
-// in groups of four (windows 8 g + 4 h + 0..3): only groups whose max beats a
-// lane's threshold run the per-window validity test (i + L <= len), the
-// inner-range overlap test and the atomic count of the strand's slot.
-__device__ __noinline__ void tile_hits(v16i acc, int32_t thr, const int32_t *meta, uint32_t len, uint32_t flags,
-                                       uint32_t pos_off, uint64_t count_off, uint32_t hap, uint32_t i0, uint32_t lane,
-                                       const int32_t *inner, uint32_t n_inner, uint32_t *counts, const int32_t *posrel,
-                                       unsigned long long *hits, uint32_t hits_wpp, uint32_t n_pat) {
-    const uint32_t n = lane & 31, h = lane >> 5;
+// constrain the hot loop.  Registers are tested in groups of four (windows
+// 8 g + 4 h + 0..3): only groups whose max beats a lane's threshold run the
+// per-window validity test (i + L <= len), the inner-range overlap test and the
+// atomic count of the strand's slot.  meta_off: LDS byte offset of the tile's
+// strand metadata (thr | len | slot | pattern index, 32 each).
+__device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off, uint32_t i0) {
+    const uint32_t lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
+    const WaveHitCtx &W = s_wctx[uni(threadIdx.x >> 6)];
+    const int32_t *meta = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(s_mdyn) + meta_off);
     const uint32_t L = (uint32_t)meta[32 + n];
+    const uint32_t len = W.len;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
         const int32_t gm = max(max(acc[4 * g], acc[4 * g + 1]), max(acc[4 * g + 2], acc[4 * g + 3]));
@@ -144,56 +176,95 @@ __device__ __noinline__ void tile_hits(v16i acc, int32_t thr, const int32_t *met
             const uint32_t i = i0 + q + 8 * g + 4 * h;
             if (!(acc[4 * g + q] > thr && i + L <= len)) continue;
             const uint32_t slot = (uint32_t)meta[64 + n];
-            const int32_t p = (flags & HAP_HAS_POS) ? posrel[pos_off + i] : (int32_t)i;
+            const int32_t p = (W.flags & HAP_HAS_POS) ? s_kctx.posrel[W.pos_off + i] : (int32_t)i;
+            const uint32_t n_inner = W.n_inner;
+            uint32_t *cnt = s_kctx.counts + W.count_off + (uint64_t)slot * n_inner;
             for (uint32_t k = 0; k < n_inner; k++) {
-                const int32_t s = inner[2 * k];
-                const uint32_t span = (uint32_t)(inner[2 * k + 1] - s);
-                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-                    atomicAdd(counts + count_off + (uint64_t)slot * n_inner + k, 1u);
+                const int32_t s = W.inner[2 * k];
+                const uint32_t span = (uint32_t)(W.inner[2 * k + 1] - s);
+                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span) atomicAdd(cnt + k, 1u);
             }
-            if (hits && i / 64 < hits_wpp)
-                atomicOr(hits + ((size_t)hap * n_pat + (uint32_t)meta[96 + n]) * hits_wpp + i / 64, 1ull << (i & 63));
+            unsigned long long *hits = s_kctx.hits;
+            const uint32_t wpp = s_kctx.hits_wpp;
+            if (hits && i / 64 < wpp)
+                atomicOr(hits + ((size_t)W.hap * s_kctx.n_pat + (uint32_t)meta[96 + n]) * wpp + i / 64,
+                         1ull << (i & 63));
         }
     }
 }
 
 // Threshold test of one strand tile: the max of the lane's 16 scores against its
 // strand's min_score, one ballot; hits go to tile_hits.
-__device__ __forceinline__ void check_tile(const ScanArgs &A, const DevMSuper &S, const char *s_img, uint32_t ti,
-                                           const v16i &acc, int32_t thr, const HapCtx &H, uint32_t i0, uint32_t lane) {
+__device__ __forceinline__ void check_tile(const DevMSuper &S, uint32_t ti, const v16i &acc, int32_t thr,
+                                           uint32_t i0) {
+    if (TFBS_MFMA_PROBE == 1) {
+        asm volatile("" ::"v"(acc[0]), "v"(acc[5]), "v"(acc[10]), "v"(acc[15]));
+        return;
+    }
     int32_t m = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])), max(max(acc[4], acc[5]), max(acc[6], acc[7])));
     m = max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
     if (__builtin_expect(__ballot(m > thr) == 0, 1)) return;
-    tile_hits(acc, thr, reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes), H.hm.len, H.hm.flags,
-              H.hm.pos_off, H.hm.count_off, H.hap, i0, lane, H.inner, H.n_inner, A.counts, A.posrel, A.hits,
-              A.hits_wpp, A.n_patterns_total);
+    if (TFBS_MFMA_PROBE == 3) {
+        asm volatile("" ::"v"(m));
+        return;
+    }
+    tile_hits(acc, thr, kMOnehotBytes + S.meta_off + ti * kMMetaBytes, i0);
 }
 
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
 // of this workgroup's haplotypes, biased by their first word, or global memory).
-template <int NK>
+template <int NK, int NW, bool ROLL>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
-    constexpr uint32_t kWaves = kMBlock / 64;
+    constexpr uint32_t kWaves = NW;
     const uint32_t nt = S.tile_count;
     for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
-        HapCtx H;
-        H.hap = hg * A.haps_per_block + hh;
-        if (H.hap >= A.n_haps) break;
-        H.hm = A.haps[H.hap];
-        if (H.hm.len < S.lmin) continue;
-        const DevRegion rg = A.regions[H.hm.region];
-        H.inner = A.inner + 2 * (size_t)rg.inner_off;
-        H.n_inner = rg.n_inner;
-        const uint32_t nwin = H.hm.len - S.lmin + 1;
+        const uint32_t hap = hg * A.haps_per_block + hh;
+        if (hap >= A.n_haps) break;
+        const DevHap hm = load_hap(A.haps + hap);
+        if (hm.len < S.lmin) continue;
+        const DevRegion rg = A.regions[hm.region];
+        {  // every lane stores the same (uniform) values
+            WaveHitCtx &W = s_wctx[wave];
+            W.inner = A.inner + 2 * (size_t)uni(rg.inner_off);
+            W.count_off = hm.count_off;
+            W.len = hm.len;
+            W.flags = hm.flags;
+            W.pos_off = hm.pos_off;
+            W.hap = hap;
+            W.n_inner = uni(rg.n_inner);
+        }
+        const uint32_t nwin = hm.len - S.lmin + 1;
         WinWords ww;
-        load_window(A, words, H.hm, 0, lane, ww);
+        load_window(A, words, hm, 0, lane, ww);
         for (uint32_t i0 = 0; i0 < nwin; i0 += kMWindows) {
             v4i a[NK];
-            build_onehot<NK>(H.hm, i0, lane, ww, s_img - kMOnehotBytes, a);
-            if (i0 + kMWindows < nwin) load_window(A, words, H.hm, i0 + kMWindows, lane, ww);  // next tile's words
+            build_onehot<NK>(hm, i0, lane, ww, s_img - kMOnehotBytes, a);
+            if (i0 + kMWindows < nwin) load_window(A, words, hm, i0 + kMWindows, lane, ww);  // next tile's words
             // the other waves of the SIMD hide the latencies
             uint32_t ti = 0;
+            if (ROLL) {  // tile t's test runs while tile t + 1's MFMAs execute
+                v16i prev;
+                int32_t prev_thr;
+                {
+                    BFrag<NK> f;
+                    load_tile<NK>(s_img, S, 0, lane, f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    prev = tile_scores<NK>(a, f);
+                    prev_thr = f.thr;
+                }
+                for (ti = 1; ti < nt; ti++) {
+                    BFrag<NK> f;
+                    load_tile<NK>(s_img, S, ti, lane, f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const v16i acc = tile_scores<NK>(a, f);
+                    check_tile(S, ti - 1, prev, prev_thr, i0);
+                    prev = acc;
+                    prev_thr = f.thr;
+                }
+                check_tile(S, nt - 1, prev, prev_thr, i0);
+                continue;
+            }
             if (NK <= 4) {  // two tiles at a time: tile 0's test overlaps tile 1's MFMAs
                 for (; ti + 1 < nt; ti += 2) {
                     BFrag<NK> f0, f1;
@@ -202,8 +273,8 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                     __builtin_amdgcn_sched_barrier(0);
                     const v16i acc0 = tile_scores<NK>(a, f0);
                     const v16i acc1 = tile_scores<NK>(a, f1);
-                    check_tile(A, S, s_img, ti, acc0, f0.thr, H, i0, lane);
-                    check_tile(A, S, s_img, ti + 1, acc1, f1.thr, H, i0, lane);
+                    check_tile(S, ti, acc0, f0.thr, i0);
+                    check_tile(S, ti + 1, acc1, f1.thr, i0);
                 }
             }
             for (; ti < nt; ti++) {
@@ -211,7 +282,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                 load_tile<NK>(s_img, S, ti, lane, f);
                 __builtin_amdgcn_sched_barrier(0);  // every B read of the tile issues before its MFMAs
                 const v16i acc = tile_scores<NK>(a, f);
-                check_tile(A, S, s_img, ti, acc, f.thr, H, i0, lane);
+                check_tile(S, ti, acc, f.thr, i0);
             }
         }
     }
@@ -220,9 +291,12 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD.
 // LDS: one-hot tables | super tile image | (STAGED) the packed words of the
 // workgroup's haplotypes, copied once so that every window read is an LDS read.
-template <bool STAGED>
-__global__ __launch_bounds__(kMBlock, 4) void scan_mfma_kernel(ScanArgs A) {
-    extern __shared__ __attribute__((aligned(16))) int32_t smem[];
+template <bool STAGED, int NW>
+__global__ __launch_bounds__(NW * 64, 4) void scan_mfma_kernel(ScanArgs A) {
+    constexpr int kMBlock = NW * 64;
+    static_assert(NW <= kMMaxWaves, "one hit context per wave");
+    int32_t *smem = s_mdyn;
+    if (threadIdx.x == 0) s_kctx = KernelHitCtx{A.counts, A.posrel, A.hits, A.hits_wpp, A.n_patterns_total};
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
     const DevMSuper S = A.msupers[sidx];
@@ -250,21 +324,27 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_kernel(ScanArgs A) {
     }
     __syncthreads();
     const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the wave index is uniform: keep every haplotype-level value in SGPRs
+    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     switch (S.nk) {
-    case 1: scan_super<1>(A, S, s_img, words, hg, lane, wave); break;
-    case 2: scan_super<2>(A, S, s_img, words, hg, lane, wave); break;
-    case 3: scan_super<3>(A, S, s_img, words, hg, lane, wave); break;
-    case 4: scan_super<4>(A, S, s_img, words, hg, lane, wave); break;
-    case 5: scan_super<5>(A, S, s_img, words, hg, lane, wave); break;
-    case 6: scan_super<6>(A, S, s_img, words, hg, lane, wave); break;
-    case 7: scan_super<7>(A, S, s_img, words, hg, lane, wave); break;
-    default: scan_super<8>(A, S, s_img, words, hg, lane, wave); break;
+    case 1: A.mfma_roll ? scan_super<1, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<1, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 2: A.mfma_roll ? scan_super<2, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<2, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 3: A.mfma_roll ? scan_super<3, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<3, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 4: A.mfma_roll ? scan_super<4, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<4, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 5: A.mfma_roll ? scan_super<5, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<5, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 6: A.mfma_roll ? scan_super<6, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<6, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    case 7: A.mfma_roll ? scan_super<7, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<7, NW, false>(A, S, s_img, words, hg, lane, wave); break;
+    default: A.mfma_roll ? scan_super<8, NW, true>(A, S, s_img, words, hg, lane, wave) : scan_super<8, NW, false>(A, S, s_img, words, hg, lane, wave); break;
     }
 }
 
 typedef void (*MfmaKernel)(ScanArgs);
-MfmaKernel mfma_variant(bool staged) { return staged ? scan_mfma_kernel<true> : scan_mfma_kernel<false>; }
+MfmaKernel mfma_variant(bool staged, uint32_t waves) {
+    switch (waves) {
+    case 8: return staged ? scan_mfma_kernel<true, 8> : scan_mfma_kernel<false, 8>;
+    default: return staged ? scan_mfma_kernel<true, 4> : scan_mfma_kernel<false, 4>;
+    }
+}
 
 }  // namespace
 
@@ -279,16 +359,19 @@ uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
 
 size_t mfma_lds_fixed() { return kMOnehotBytes; }
 
-int launch_mfma(const ScanArgs &a0, size_t img_bytes, uint32_t group_words, uint32_t n_haps, hipStream_t stream) {
+int launch_mfma(const ScanArgs &a0, size_t img_bytes, uint32_t group_words, uint32_t n_haps, uint32_t waves,
+                hipStream_t stream) {
+    if (waves != 8) waves = 4;
     if (n_haps == 0 || a0.n_msupers == 0) return 0;
     // stage the group's words in LDS when they fit beside the image at 4 workgroups per CU
     const size_t base = kMOnehotBytes + img_bytes;
     const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
-    const bool staged = staged_bytes <= kMStagedMax;
+    const size_t static_lds = sizeof(KernelHitCtx) + sizeof(s_wctx);  // the hit contexts
+    const bool staged = staged_bytes + static_lds <= kMStagedPerWave * waves;
     const size_t lds = staged ? staged_bytes : base;
     hipError_t e = hipSuccess;
     if (lds > 64 * 1024)
-        e = hipFuncSetAttribute((const void *)mfma_variant(staged), hipFuncAttributeMaxDynamicSharedMemorySize,
+        e = hipFuncSetAttribute((const void *)mfma_variant(staged, waves), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds);
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("MFMA LDS attribute: ") + hipGetErrorString(e));
     const uint32_t hpb = a0.haps_per_block;
@@ -303,7 +386,7 @@ int launch_mfma(const ScanArgs &a0, size_t img_bytes, uint32_t group_words, uint
         a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
         a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
         a.mimg_max = (uint32_t)img_bytes;
-        hipLaunchKernelGGL(mfma_variant(staged), dim3(a0.n_msupers * ng), dim3(kMBlock), lds, stream, a);
+        hipLaunchKernelGGL(mfma_variant(staged, waves), dim3(a0.n_msupers * ng), dim3(64 * waves), lds, stream, a);
         launches++;
     }
     e = hipGetLastError();
