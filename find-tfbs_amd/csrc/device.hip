@@ -63,6 +63,10 @@ struct tfbs_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t evk0 = nullptr, evk1 = nullptr;  // around the dominant kernel (the MFMA launches)
+    // the per-depth MFMA launches run on kSide + 1 streams so that they overlap
+    static constexpr int kSide = 3;
+    hipStream_t side[kSide] = {};
+    hipEvent_t fork = nullptr, join[kSide] = {};
     bool kernel_timed = false;
     float last_kernel_ms = 0.f;
     const Patterns *pats = nullptr;
@@ -78,8 +82,6 @@ struct tfbs_ctx {
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
     uint32_t mfma_lds = 28 * 1024;  // LDS image budget of one MFMA super tile
     uint32_t mfma_hpb = 32;         // haplotypes per MFMA workgroup
-    uint32_t mfma_waves = 4;        // waves per MFMA workgroup (4, 8)
-    uint32_t mfma_roll = 0;         // rolling tile loop (TFBS_MFMA_ROLL)
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
@@ -127,10 +129,20 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
         m.haps_per_block = ctx->mfma_hpb;
-        m.mfma_roll = ctx->mfma_roll;
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
-        const int n = launch_mfma(m, P.max_super_bytes, ctx->mfma_group_words, n_haps, ctx->mfma_waves, ctx->stream);
+        HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+        hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
+        for (int i = 0; i < tfbs_ctx::kSide; i++) {
+            HIP_TRY(hipStreamWaitEvent(ctx->side[i], ctx->fork, 0));
+            streams[i + 1] = ctx->side[i];
+        }
+        const int n = launch_mfma(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words, n_haps,
+                                  streams, tfbs_ctx::kSide + 1);
         if (n < 0) return n;
+        for (int i = 0; i < tfbs_ctx::kSide; i++) {
+            HIP_TRY(hipEventRecord(ctx->join[i], ctx->side[i]));
+            HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->join[i], 0));
+        }
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
@@ -187,6 +199,12 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
     if (ctx->evk1) (void)hipEventDestroy(ctx->evk1);
+    for (int i = 0; i < tfbs_ctx::kSide; i++) {
+        if (ctx->side[i]) (void)hipStreamSynchronize(ctx->side[i]);
+        if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
+        if (ctx->join[i]) (void)hipEventDestroy(ctx->join[i]);
+    }
+    if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -206,12 +224,11 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 28))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32));
-    ctx->mfma_waves = (uint32_t)env_int("TFBS_MFMA_WAVES", 4);
-    ctx->mfma_roll = (uint32_t)env_int("TFBS_MFMA_ROLL", 0);
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
     opt.mfma_lds_bytes = ctx->mfma_lds;
+    if (env_int("TFBS_MFMA_LDS_BY_DEPTH", 0)) mfma_depth_budgets(opt.mfma_lds_by_nk);
     rc = ctx->pats->build_plan(opt, &ctx->plan);
     if (rc) {
         delete ctx;
@@ -227,6 +244,11 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->ev1);
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    for (int i = 0; i < tfbs_ctx::kSide; i++) {
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
         tfbs_ctx_destroy(ctx);
         return tfbs::fail(TFBS_E_HIP, std::string("HIP init: ") + hipGetErrorString(e));

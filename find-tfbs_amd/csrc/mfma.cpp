@@ -36,13 +36,12 @@ bool mfma_eligible(const Pat &p) {
     return true;
 }
 
-void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t lds_bytes, Plan *plan) {
+void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, const PlanOptions &opt, Plan *plan) {
     // strands in slot order (slots are sorted by length, so tiles pack similar lengths)
     std::vector<std::pair<int, uint32_t>> strands;  // (pattern index, slot)
     for (const SlotGroup &g : groups)
         for (int i : g.strands) strands.push_back({i, g.slot});
     if (strands.empty()) return;
-    lds_bytes = std::max<uint32_t>(lds_bytes, kMMaxChunks * kMFragBytes + kMMetaBytes);
 
     struct TileSrc { size_t first, count; uint32_t nk, lmin; };
     std::vector<TileSrc> tiles;
@@ -60,10 +59,11 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
         // a super tile: consecutive tiles of the same K depth within the LDS budget
         const uint32_t nk = tiles[ti].nk;
         const uint32_t per = nk * kMFragBytes + kMMetaBytes;
+        const uint32_t lds_bytes = std::max(per, opt.mfma_lds_by_nk[nk] ? opt.mfma_lds_by_nk[nk] : opt.mfma_lds_bytes);
         // the run of tiles with this depth, split into equal super tiles
         size_t run = ti;
         while (run < tiles.size() && tiles[run].nk == nk) run++;
-        const size_t max_per_super = std::max<size_t>(1, lds_bytes / per);
+        const size_t max_per_super = std::min<size_t>(kMSuperMaxTiles, std::max<size_t>(1, lds_bytes / per));
         const size_t n_super = (run - ti + max_per_super - 1) / max_per_super;
         const size_t tj = ti + (run - ti + n_super - 1) / n_super;
         const uint32_t count = (uint32_t)(tj - ti);

@@ -254,7 +254,7 @@ int Patterns::build_plan(const PlanOptions &opt, Plan *plan) const {
         (m ? mat : lut).push_back(std::move(g));
     }
     build_fast_tiles(*this, lut, opt.tile_blocks, plan);
-    build_mfma_tiles(*this, mat, opt.mfma_lds_bytes, plan);
+    build_mfma_tiles(*this, mat, opt, plan);
     // --- generic (long) strands: one tile per pattern_id group, weights x5
     for (uint32_t gi = 0; gi < groups.size(); gi++) {
         const Group &g = groups[gi];

@@ -45,6 +45,7 @@ struct PlanOptions {
     uint32_t tile_blocks = 20;          // LUT tile: 4 KiB table blocks per workgroup
     bool mfma = false;                  // score eligible strands on the matrix cores
     uint32_t mfma_lds_bytes = 64 * 1024;  // LDS image budget of one MFMA super tile
+    uint32_t mfma_lds_by_nk[9] = {};      // per K depth (chunks 1-8), overrides mfma_lds_bytes when set
 };
 
 struct Patterns {
@@ -63,7 +64,7 @@ void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
 // Strands the int8 one-hot formulation scores exactly (L <= 32, every weight
 // splits as 64 a + b with a, b int8).
 bool mfma_eligible(const Pat &p);
-void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, uint32_t lds_bytes, Plan *plan);
+void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, const PlanOptions &opt, Plan *plan);
 
 int parse_weight(const std::string &s, int32_t *out);
 int parse_threshold_file(const std::string &path, float thr, int32_t *out);

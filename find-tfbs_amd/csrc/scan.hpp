@@ -31,7 +31,6 @@ struct ScanArgs {
     uint32_t n_msupers;
     const int32_t *mimage;
     uint32_t mimg_max;          // LDS bytes reserved for the largest super tile image
-    uint32_t mfma_roll;         // tile loop: 1 = each tile's test overlaps the next tile's MFMAs
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;
     uint32_t n_patterns_total;
@@ -50,10 +49,14 @@ int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
 int fast_kernel_set_lds(const LaunchConfig &cfg);
 // Matrix-core scan (scan_mfma.hip); counts must be zeroed first (atomic adds).
 // group_words: the most packed words any haplotype group of haps_per_block spans.
-// waves per workgroup: 4, 8 or 16 (4 waves per SIMD either way)
-int launch_mfma(const ScanArgs &a, size_t img_bytes, uint32_t group_words, uint32_t n_haps, uint32_t waves,
-                hipStream_t stream);
+// One launch per K depth, spread round-robin over `streams` (deepest first);
+// supers: the host copy of a.msupers (sorted by depth).
+int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
+                const hipStream_t *streams, uint32_t n_streams);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
+// Super tile image budgets per K depth (1-8) that let each depth's kernel reach
+// the waves per SIMD its registers allow.
+void mfma_depth_budgets(uint32_t out[9]);
 size_t mfma_lds_fixed();  // LDS bytes the MFMA kernel needs besides the image and words
 
 }  // namespace tfbs

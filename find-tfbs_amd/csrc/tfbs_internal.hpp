@@ -89,6 +89,7 @@ constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
 constexpr int kMChunkCols = 4;     // columns per K chunk of 32
 constexpr int kMMaxChunks = 8;     // L <= 32
+constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (a 64-bit mask flags the tiles with hits)
 constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
 constexpr int kMMetaBytes = 512;   // per tile: thr[32], len[32], slot[32], orig[32]
 

@@ -5,11 +5,15 @@
 set -e
 cd "$(dirname "$0")/.."
 make -s -j8 find-tfbs_amd/lib/libtfbs_amd.so
-for n in "$@"; do
-  d=find-tfbs_amd/lib/probe$n
+# Each argument: N, or NAME:N:DEFINES (e.g. w1:0:-DTFBS_MFMA_DEEP_WT=1 builds
+# lib/probew1 with probe 0 and the extra define).
+for spec in "$@"; do
+  IFS=: read -r name n extra <<< "$spec"
+  [ -z "$n" ] && n=$name
+  d=find-tfbs_amd/lib/probe$name
   mkdir -p $d
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form \
-    -DTFBS_MFMA_PROBE=$n -x hip -c find-tfbs_amd/csrc/scan_mfma.hip -o $d/scan_mfma.o
+    -DTFBS_MFMA_PROBE=$n $extra -x hip -c find-tfbs_amd/csrc/scan_mfma.hip -o $d/scan_mfma.o
   objs=$(ls find-tfbs_amd/lib/obj/*.o | grep -v scan_mfma.o)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libtfbs_amd.so $objs $d/scan_mfma.o -lz -lpthread
 done
