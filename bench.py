@@ -219,10 +219,13 @@ def main():
         if mms > 0:  # the matrix-core kernel scored every strand of this workload
             mops = MFMA_OPS_PER_CELL * batch.num_cell_ops / (mms / 1e3) / 1e12
             roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS",
-                    "frac": mops / MFMA_I8_PEAK_TOPS, "traffic": traffic, "kernel": "scan_mfma_kernel",
+                    "frac": mops / MFMA_I8_PEAK_TOPS, "traffic": traffic,
+                    "kernel": "scan_mfma_kernel<staged, K depth> (one launch per depth, 4 streams)",
                     "kernel_ms": mms,
                     "note": "achieved = 16 int8 ops per (window, strand, column) of the one-hot x weight-digit "
-                            "GEMM / the kernel's HIP-event time; traffic = HBM bytes per launch from PMC"}
+                            "GEMM / the MFMA phase's HIP-event time (first launch to last, joined on the ctx "
+                            "stream; tools/trace_phase.py gives the same phase from the rocprofv3 trace); "
+                            "traffic = HBM bytes of the phase's dispatches from PMC"}
         else:
             roof = hbm
         path = "mfma" if mms > 0 else "lut"

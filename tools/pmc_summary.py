@@ -10,14 +10,26 @@ out = {}
 root = sys.argv[1]
 for f in glob.glob(os.path.join(root, "*", "pmc_counter_collection.csv")):
     rows = list(csv.DictReader(open(f)))
-    disp = sorted({int(r["Dispatch_Id"]) for r in rows if "scan_" in r["Kernel_Name"]})
-    if not disp:
-        continue
-    d = disp[-1]  # last scan dispatch of the run (warm)
+    # the last scan step: the last run of consecutive scan dispatches (one per
+    # K depth for the MFMA path), counters summed over its dispatches
+    kinds = {}
     for r in rows:
-        if int(r["Dispatch_Id"]) == d and "scan_" in r["Kernel_Name"]:
+        kinds[int(r["Dispatch_Id"])] = "scan_" in r["Kernel_Name"]
+    ids = sorted(kinds)
+    last = []
+    for d in ids:
+        if kinds[d]:
+            last = last + [d] if last and last[-1] == ids[ids.index(d) - 1] else [d]
+    if not last:
+        continue
+    take = set(last)
+    seen = set()
+    for r in rows:
+        d = int(r["Dispatch_Id"])
+        if d in take:
             out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
             out["_kernel"] = r["Kernel_Name"][:60]
+            out["_dispatches"] = len(take)
             out["_grid"] = r["Grid_Size"]
             out["_vgpr"] = r["VGPR_Count"]
             out["_lds"] = r["LDS_Block_Size"]
