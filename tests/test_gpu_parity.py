@@ -364,12 +364,13 @@ def test_many_variant_regions_vs_oracle(tmp_path):
     _compare(ps, n, beds, regions)
 
 
-@pytest.mark.parametrize("indel,per_batch", [(0, 5), (25, 0)])
-def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch):
+@pytest.mark.parametrize("indel,per_batch,subset", [(0, 5, False), (25, 0, False), (10, 3, True)])
+def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset):
     """f2-f4 + the scan at a larger size than test_data: a synthetic BCF/FASTA/BED set
-    (tools/synth_dataset.py) through tfbs_run (native readers, batches of merged
-    regions, device key reduction, BGZF writer) vs the oracle's run() on the same
-    records; decompressed VCF text identical."""
+    (tools/synth_dataset.py) through tfbs_run (streaming BCF reader, batches of
+    merged regions, device key reduction, BGZF writer) vs the oracle's run() on the
+    same records; decompressed VCF text identical.  subset: a samples file naming
+    a shuffled subset plus an unknown name (main.rs:293-314 keeps BCF order)."""
     import gzip
     import sys as _sys
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
@@ -378,11 +379,17 @@ def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch):
                                    length_config=2, seed=7, indel_pct=indel)
     out = tmp_path / "out.vcf.gz"
     samples_file = os.path.join(d["dir"], "samples")
+    wanted = d["samples"]
+    if subset:
+        import random as _random
+        wanted = _random.Random(5).sample(d["samples"], 23)
+        samples_file = str(tmp_path / "wanted.txt")
+        open(samples_file, "w").write("\n".join(wanted + ["NOT_IN_BCF"]) + "\n")
     T.run("chr1", d["bcf"], [d["bed"]], d["fasta"], samples_file, d["pwm_file"], d["thr_dir"], 2e-3, d["names"],
           str(out), threads=4, regions_per_batch=per_batch)
     got = gzip.open(str(out), "rt").read()
     recs = [dict(r, gt=r["gt"].astype(int).tolist()) for r in d["records"]]
-    want = O.run("chr1", recs, [d["bed"]], d["fasta"], d["samples"], d["samples"], d["pwm_file"], d["thr_dir"], 2e-3,
-                 d["names"])
+    want = O.run("chr1", recs, [d["bed"]], d["fasta"], d["samples"], wanted + (["NOT_IN_BCF"] if subset else []),
+                 d["pwm_file"], d["thr_dir"], 2e-3, d["names"])
     assert got == want
     assert got.count("\n") > 1  # some rows
