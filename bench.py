@@ -27,9 +27,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TOPS = 78.64      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
 MFMA_I8_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense BF16 rate (MI355X_MICROARCH.md, MFMA table)
-# int8 ops of the one-hot formulation per (window, strand, column): 4 bases x 2
-# digits = 8 multiply-adds (scan_mfma.hip); padding (K, windows, strands) excluded
-MFMA_OPS_PER_CELL = 16
+# int8 ops of the one-hot formulation per (window, strand, column): 4 bases x 1
+# coarse digit = 4 multiply-adds (scan_mfma.hip); padding (K, windows, strands)
+# and the exact rescoring of the rare candidate tiles excluded
+MFMA_OPS_PER_CELL = 8
 
 
 def parse():
@@ -198,7 +199,7 @@ def main():
         kms = sum(kernel_ms) / len(kernel_ms)
         pattern_bytes = 0
         for p in ps.to_list():
-            pattern_bytes += ((len(p) + 3) // 4) * 1024 + 4 * len(p) + 16
+            pattern_bytes += ((len(p) + 7) // 8) * 1024 + 16 * len(p) + 24
         alg_bytes = batch.input_bytes + batch.output_bytes + pattern_bytes
         achieved = alg_bytes / (kms / 1e3) / 1e9
         traffic = None
@@ -222,7 +223,7 @@ def main():
                     "frac": mops / MFMA_I8_PEAK_TOPS, "traffic": traffic,
                     "kernel": "scan_mfma_kernel<staged, K depth> (one launch per depth, 4 streams)",
                     "kernel_ms": mms,
-                    "note": "achieved = 16 int8 ops per (window, strand, column) of the one-hot x weight-digit "
+                    "note": "achieved = 8 int8 ops per (window, strand, column) of the one-hot x coarse-digit "
                             "GEMM / the MFMA phase's HIP-event time (first launch to last, joined on the ctx "
                             "stream; tools/trace_phase.py gives the same phase from the rocprofv3 trace); "
                             "traffic = HBM bytes of the phase's dispatches from PMC"}

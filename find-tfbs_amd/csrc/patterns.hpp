@@ -45,7 +45,7 @@ struct PlanOptions {
     uint32_t tile_blocks = 20;          // LUT tile: 4 KiB table blocks per workgroup
     bool mfma = false;                  // score eligible strands on the matrix cores
     uint32_t mfma_lds_bytes = 64 * 1024;  // LDS image budget of one MFMA super tile
-    uint32_t mfma_lds_by_nk[9] = {};      // per K depth (chunks 1-8), overrides mfma_lds_bytes when set
+    uint32_t mfma_lds_by_nk[9] = {};      // per K depth (chunks 1-4), overrides mfma_lds_bytes when set
 };
 
 struct Patterns {

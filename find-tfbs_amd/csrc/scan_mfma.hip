@@ -1,29 +1,30 @@
 // Matrix-core scan (gfx950 v_mfma_i32_32x32x32_i8) for strands with L <= 32
-// whose weights split into two int8 digits (mfma.cpp).
+// whose weights stay within 127 x 255 (mfma.cpp).
 //
 // matches (pattern.rs:141-171) scores every window i of a haplotype with
 // sum_j w[j][nuc(i + j)] (N = 0, pattern.rs:119-135).  For 32 consecutive
 // windows x 32 strands that is one int8 GEMM: A[window][k] = one-hot of the
-// window's bases (all zero for N and past the haplotype end), B[k][strand] =
-// the strand's weight digits.  A K chunk of 32 covers 4 columns twice: lanes
-// 0-31 carry the one-hot with entries 1 (against the digit b of w = 64 a + b),
-// lanes 32-63 with entries 64 (against a), so one MFMA per 4 columns adds the
-// exact score into the int32 accumulator.
+// window's bases (all zero for N), B[k][strand] = the strand's weights.  The
+// weights split as w = s q + r (per-strand scale s, int8 q and r): a K chunk
+// of 32 covers 8 columns of the coarse digits q, so one MFMA per 8 columns
+// gives Q; Q > thr_q is necessary for a hit (mfma.cpp), and the rare tiles
+// that pass it are rescored exactly as s Q + one-hot x r.
 //
 //  * A workgroup (4 waves, 4 workgroups per CU) stages one super tile (tiles of
-//    32 strands of equal K depth: B fragments + strand metadata), a one-hot
-//    table and the packed words of its haplotypes in LDS.  Every B fragment is
-//    one conflict-free ds_read_b128 per lane.
+//    32 strands of equal K depth: coarse and residual B fragments + strand
+//    metadata), the one-hot table and the packed words of its haplotypes in
+//    LDS.  Every B fragment is one conflict-free ds_read_b128 per lane.
 //  * Each wave takes haplotypes; per 32-window tile it builds the A fragments
 //    once (one table read per chunk) and reuses them for every strand tile of
-//    the super tile.  Tiles with L <= 16 go two at a time, so one tile's
-//    threshold test overlaps the next tile's MFMAs.
+//    the super tile, two window tiles per B fragment read.
 //  * C layout: lane l holds strand column l & 31 and windows (r & 3) + 8 (r >> 2)
-//    + 4 (l >> 5), r < 16.  A max-reduce of the 16 scores against the lane's
-//    min_score and one ballot gate the (rare, ~1e-4 per window and strand) hit
-//    handling, which applies the inner-range overlap test (range.rs:18-21 as
-//    main.rs:503 uses it) and adds to the count of the strand's pattern_id slot
-//    atomically (counts are zeroed before the scan), so a tile may mix slots.
+//    + 4 (l >> 5), r < 16.  A max-reduce of the 16 coarse sums against the
+//    lane's thr_q and one ballot gate the exact rescore; its max against
+//    min_score and a second ballot gate the (rare, ~1e-4 per window and
+//    strand) hit handling, which applies the inner-range overlap test
+//    (range.rs:18-21 as main.rs:503 uses it) and adds to the count of the
+//    strand's pattern_id slot atomically (counts are zeroed before the scan),
+//    so a tile may mix slots.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -45,23 +46,25 @@ namespace {
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
+// TFBS_MFMA_PIPE=1: software-pipelined strand loop (tests of tile t-1 after the
+// MFMAs of tile t)
+#ifndef TFBS_MFMA_PIPE
+#define TFBS_MFMA_PIPE 0
+#endif
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
 constexpr int kMBlock = 256;          // 4 waves
-constexpr int kMOnehotBytes = 8192;   // LDS: one-hot tables (entries 1 | entries 64), image, words
+constexpr int kMOnehotBytes = 4096;   // LDS: one-hot table, image, words
 constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup at 4 workgroups per CU (160 KiB)
-// per K depth (chunks): window tiles per step and the waves per SIMD the
-// kernel is compiled for (the registers of two A sets + two accumulators)
-#ifndef TFBS_MFMA_DEEP_WT  // window tiles per step for K depths 6-8 (probe builds vary it)
-#define TFBS_MFMA_DEEP_WT 2
-#endif
-constexpr uint32_t kMfmaWindowTiles[9] = {1, 2, 2, 2, 2, 2, TFBS_MFMA_DEEP_WT, TFBS_MFMA_DEEP_WT, TFBS_MFMA_DEEP_WT};
-// waves per SIMD the depth kernels' registers allow (71-154 VGPRs at gfx950's
-// 8-register granule; see mfma_depth_budgets)
-constexpr uint32_t kMfmaRegWaves[9] = {4, 7, 5, 5, 4, 4, 3, 3, 3};
-constexpr int kMfmaMinWaves[9] = {4, 4, 4, 4, 4, 4, 5 - TFBS_MFMA_DEEP_WT, 5 - TFBS_MFMA_DEEP_WT, 5 - TFBS_MFMA_DEEP_WT};
+// per K depth (chunks of 8 columns): window tiles per step and the waves per
+// SIMD the kernel is compiled for (the registers of two A sets + two
+// accumulators)
+constexpr uint32_t kMfmaWindowTiles[kMMaxChunks + 1] = {1, 2, 2, 2, 2};
+// waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
+constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 6, 5, 4, 4};
+constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE};
 
 // The packed words (and N-mask words) a lane needs for its window of the
 // 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
@@ -86,10 +89,9 @@ __device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *w
     }
 }
 
-// A fragments of the 32-window tile at i0: chunk kc = columns 4 kc .. 4 kc + 3
-// of the lane's window, as one-hot bytes with entry 1 (lanes 0-31) or 64
-// (lanes 32-63), read from the LDS table by the 4-mer code; N bases zeroed in
-// haplotypes that have them.
+// A fragments of the 32-window tile at i0: chunk kc, lane half h = lane >> 5:
+// columns 8 kc + 4 h .. + 3 of the lane's window as one-hot bytes, read from
+// the LDS table by the 4-mer code; N bases zeroed in haplotypes that have them.
 template <int NK>
 __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint32_t lane, const WinWords &ww,
                                              const char *s_onehot, v4i (&a)[NK]) {
@@ -98,20 +100,20 @@ __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint
     const uint32_t sh = 2 * (ic & 15);
     const uint32_t img_lo = __builtin_amdgcn_alignbit(ww.w[1], ww.w[0], sh);  // bases i .. i+15
     const uint32_t img_hi = __builtin_amdgcn_alignbit(ww.w[2], ww.w[1], sh);  // bases i+16 .. i+31
-    const char *tab = s_onehot + (lane >> 5) * 4096;
+    const uint32_t hb = 8 * (lane >> 5);
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) {
-        const uint32_t code = __builtin_amdgcn_ubfe(kc < 4 ? img_lo : img_hi, 8 * (kc & 3), 8);
-        a[kc] = *reinterpret_cast<const v4i *>(tab + code * 16);
+        const uint32_t code = __builtin_amdgcn_ubfe(kc < 2 ? img_lo : img_hi, 16 * (kc & 1) + hb, 8);
+        a[kc] = *reinterpret_cast<const v4i *>(s_onehot + code * 16);
     }
     // Bases past the haplotype end need no mask: they only reach windows with
     // i + L > len (rejected in tile_hits) or columns >= L (zero weights).
     if (hm.flags & HAP_HAS_N) {  // N scores 0 (pattern.rs:119-135): clear its one-hot
-        const uint32_t vm = ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31);
+        const uint32_t vm = ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31) >> (hb / 2);
 #pragma unroll
         for (int kc = 0; kc < NK; kc++)
 #pragma unroll
-            for (int t = 0; t < 4; t++) a[kc][t] = ((vm >> (4 * kc + t)) & 1u) ? a[kc][t] : 0;
+            for (int t = 0; t < 4; t++) a[kc][t] = ((vm >> (8 * kc + t)) & 1u) ? a[kc][t] : 0;
     }
 }
 
@@ -136,10 +138,10 @@ __device__ __forceinline__ void load_tile(const char *s_img, const DevMSuper &S,
     f.thr = 1 << 30;
     return;
 #endif
-    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes) + lane * 16;
+    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (2 * NK * kMFragBytes) + lane * 16;
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
-    f.thr = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes)[lane & 31];
+    f.thr = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes)[kMetaThrQ + (lane & 31)];
 }
 
 template <int NK>
@@ -194,7 +196,7 @@ __shared__ uint32_t s_log_n[kMMaxWaves];
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot tables | image | words
 
 #if TFBS_MFMA_PROBE == 4
-__device__ unsigned long long g_probe[4];
+__device__ unsigned long long g_probe[5];
 #endif
 
 // The rare path of check_tile (about one tile in ten), out of line and compact
@@ -204,7 +206,7 @@ __device__ unsigned long long g_probe[4];
 // then walks the set bits: the window validity test (i + L <= len), the
 // inner-range overlap test (range.rs:18-21 as main.rs:503 uses it) and the
 // atomic count of the strand's slot.  meta_off: LDS byte offset of the tile's
-// strand metadata (thr | len | slot | pattern index, 32 each).
+// strand metadata (MMeta fields, 32 each); acc: exact scores, thr: min_score.
 __device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off, uint32_t i0) {
     uint32_t m = 0;
 #pragma unroll
@@ -217,7 +219,7 @@ __device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off,
     const uint32_t lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const WaveHitCtx &W = s_wctx[uni(threadIdx.x >> 6)];
     const int32_t *meta = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(s_mdyn) + meta_off);
-    const uint32_t L = (uint32_t)meta[32 + n];
+    const uint32_t L = (uint32_t)meta[kMetaLen + n];
 #if TFBS_MFMA_PROBE == 4
     if (lane == 0) atomicAdd(&g_probe[0], 1ull);
     for (uint32_t q = m; q; q &= q - 1) {
@@ -229,7 +231,7 @@ __device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off,
     if (m == 0) return;
     const uint32_t len = W.len, flags = W.flags, pos_off = W.pos_off, n_inner = W.n_inner;
     const int32_t il = W.inner_lds;
-    const uint32_t slot = (uint32_t)meta[64 + n];
+    const uint32_t slot = (uint32_t)meta[kMetaSlot + n];
     const uint32_t wave = uni(threadIdx.x >> 6);
     const uint32_t off0 = slot * n_inner;
 #pragma unroll 1
@@ -254,14 +256,22 @@ __device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off,
         unsigned long long *hits = s_kctx.hits;
         const uint32_t wpp = s_kctx.hits_wpp;
         if (hits && i / 64 < wpp)
-            atomicOr(hits + ((size_t)W.hap * s_kctx.n_pat + (uint32_t)meta[96 + n]) * wpp + i / 64, 1ull << (i & 63));
+            atomicOr(hits + ((size_t)W.hap * s_kctx.n_pat + (uint32_t)meta[kMetaOrig + n]) * wpp + i / 64, 1ull << (i & 63));
     } while (m);
 }
 
-// Threshold test of one strand tile: the max of the lane's 16 scores against its
-// strand's min_score, one ballot; hits go to tile_hits.
-__device__ __forceinline__ void check_tile(const DevMSuper &S, uint32_t ti, const v16i &acc, int32_t thr,
-                                           uint32_t i0) {
+__device__ __forceinline__ int32_t max16(const v16i &acc) {
+    int32_t m = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])), max(max(acc[4], acc[5]), max(acc[6], acc[7])));
+    return max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
+}
+
+// Threshold test of one strand tile: the max of the lane's 16 coarse sums
+// against its strand's thr_q, one ballot.  The tiles that pass (about one in
+// eight) are rescored exactly, s Q + one-hot x r with the residual fragments,
+// and their scores above min_score go to tile_hits.
+template <int NK>
+__device__ __forceinline__ void check_tile(const char *s_img, const DevMSuper &S, uint32_t ti, const v16i &acc,
+                                           int32_t thr, const v4i (&a)[NK], uint32_t i0, uint32_t lane) {
     if (TFBS_MFMA_PROBE == 1) {
         asm volatile("" ::"v"(acc[0]), "v"(acc[5]), "v"(acc[10]), "v"(acc[15]));
         return;
@@ -269,14 +279,44 @@ __device__ __forceinline__ void check_tile(const DevMSuper &S, uint32_t ti, cons
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[3], 1ull);
 #endif
-    int32_t m = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])), max(max(acc[4], acc[5]), max(acc[6], acc[7])));
-    m = max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
-    if (__builtin_expect(__ballot(m > thr) == 0, 1)) return;
-    if (TFBS_MFMA_PROBE == 3) {
-        asm volatile("" ::"v"(m));
-        return;
+    if (__builtin_expect(__ballot(max16(acc) > thr) == 0, 1)) return;
+    if (TFBS_MFMA_PROBE == 3) return;
+#if TFBS_MFMA_PROBE == 4
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[4], 1ull);
+#endif
+    const uint32_t meta_off = S.meta_off + ti * kMMetaBytes;
+    const int32_t *meta = reinterpret_cast<const int32_t *>(s_img + meta_off);
+    const int32_t sc = meta[kMetaScale + (lane & 31)], mn = meta[kMetaMin + (lane & 31)];
+    const char *p = s_img + ti * (2 * NK * kMFragBytes) + NK * kMFragBytes + lane * 16;
+    v4i br[NK];
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) br[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
+    v16i ex;
+#pragma unroll
+    for (int r = 0; r < 16; r++) ex[r] = __mul24(acc[r], sc);  // |Q| <= 127 x 32, s <= 255
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) ex = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kc], br[kc], ex, 0, 0, 0);
+    if (__ballot(max16(ex) > mn) == 0) return;
+    tile_hits(ex, mn, kMOnehotBytes + meta_off, i0);
+}
+
+// Coarse sums of strand tile ti for two window tiles (one B fragment read
+// feeds both MFMAs).
+template <int NK>
+__device__ __forceinline__ void pair_scores(const char *s_img, const DevMSuper &S, uint32_t ti, uint32_t lane,
+                                            const v4i (&a0)[NK], const v4i (&a1)[NK], v16i &c0, v16i &c1,
+                                            int32_t &thr) {
+    BFrag<NK> f;
+    load_tile<NK>(s_img, S, ti, lane, f);
+    __builtin_amdgcn_sched_barrier(0);  // every B read of the tile issues before its MFMAs
+    c0 = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    c1 = c0;
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) {
+        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kc], f.b[kc], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[kc], f.b[kc], c1, 0, 0, 0);
     }
-    tile_hits(acc, thr, kMOnehotBytes + S.meta_off + ti * kMMetaBytes, i0);
+    thr = f.thr;
 }
 
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
@@ -323,19 +363,40 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                 load_window(A, words, hm, i0 + kStep + kMWindows, lane, ww1);
             // the other waves of the SIMD hide the latencies
             if (two) {
-                for (uint32_t ti = 0; ti < nt; ti++) {
-                    BFrag<NK> f;
-                    load_tile<NK>(s_img, S, ti, lane, f);
-                    __builtin_amdgcn_sched_barrier(0);  // every B read of the tile issues before its MFMAs
-                    v16i c0 = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, c1 = c0;
-#pragma unroll
-                    for (int kc = 0; kc < NK; kc++) {
-                        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kc], f.b[kc], c0, 0, 0, 0);
-                        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[kc], f.b[kc], c1, 0, 0, 0);
-                    }
-                    check_tile(S, ti, c0, f.thr, i0);
-                    check_tile(S, ti, c1, f.thr, i0 + kMWindows);
+#if TFBS_MFMA_PIPE
+                // software pipeline: tile t's MFMAs issue before tile t-1's
+                // threshold tests, so the tests overlap the matrix pipe
+                v16i c0, c1, d0, d1;
+                int32_t tc, td;
+                pair_scores<NK>(s_img, S, 0, lane, a0, a1, c0, c1, tc);
+                uint32_t ti = 1;
+                for (; ti + 1 < nt; ti += 2) {
+                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, d0, d1, td);
+                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
+                    pair_scores<NK>(s_img, S, ti + 1, lane, a0, a1, c0, c1, tc);
+                    check_tile<NK>(s_img, S, ti, d0, td, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti, d1, td, a1, i0 + kMWindows, lane);
                 }
+                if (ti < nt) {
+                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, d0, d1, td);
+                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
+                    check_tile<NK>(s_img, S, ti, d0, td, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti, d1, td, a1, i0 + kMWindows, lane);
+                } else {
+                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
+                }
+#else
+                for (uint32_t ti = 0; ti < nt; ti++) {
+                    v16i c0, c1;
+                    int32_t tc;
+                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
+                    check_tile<NK>(s_img, S, ti, c0, tc, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti, c1, tc, a1, i0 + kMWindows, lane);
+                }
+#endif
                 continue;
             }
             uint32_t ti = 0;
@@ -347,8 +408,8 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                     __builtin_amdgcn_sched_barrier(0);
                     const v16i acc0 = tile_scores<NK>(a0, f0);
                     const v16i acc1 = tile_scores<NK>(a0, f1);
-                    check_tile(S, ti, acc0, f0.thr, i0);
-                    check_tile(S, ti + 1, acc1, f1.thr, i0);
+                    check_tile<NK>(s_img, S, ti, acc0, f0.thr, a0, i0, lane);
+                    check_tile<NK>(s_img, S, ti + 1, acc1, f1.thr, a0, i0, lane);
                 }
             }
             for (; ti < nt; ti++) {
@@ -356,7 +417,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                 load_tile<NK>(s_img, S, ti, lane, f);
                 __builtin_amdgcn_sched_barrier(0);
                 const v16i acc = tile_scores<NK>(a0, f);
-                check_tile(S, ti, acc, f.thr, i0);
+                check_tile<NK>(s_img, S, ti, acc, f.thr, a0, i0, lane);
             }
         }
         // the haplotype's logged hits: one batch of global atomics
@@ -382,13 +443,11 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
         for (uint32_t i = threadIdx.x; i < S.img_bytes / 16; i += kMBlock) dst[kMOnehotBytes / 16 + i] = src[i];
-        // one-hot tables: 4-mer code -> 4 dwords, base t of the code sets byte
-        // (base value) of dword t to 1 (table 0) or 64 (table 1)
-        for (uint32_t c = threadIdx.x; c < 512; c += kMBlock) {
-            const uint32_t e = c < 256 ? 1u : 64u, k = c & 255;
-            dst[c] = make_uint4(e << (8 * (k & 3)), e << (8 * ((k >> 2) & 3)), e << (8 * ((k >> 4) & 3)),
-                                e << (8 * (k >> 6)));
-        }
+        // one-hot table: 4-mer code -> 4 dwords, base t of the code sets byte
+        // (base value) of dword t to 1
+        for (uint32_t k = threadIdx.x; k < 256; k += kMBlock)
+            dst[k] = make_uint4(1u << (8 * (k & 3)), 1u << (8 * ((k >> 2) & 3)), 1u << (8 * ((k >> 4) & 3)),
+                                1u << (8 * (k >> 6)));
     }
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hl = min(h0 + A.haps_per_block, A.n_haps) - 1;
@@ -423,11 +482,7 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {
     case 1: return mfma_nk<1>(staged);
     case 2: return mfma_nk<2>(staged);
     case 3: return mfma_nk<3>(staged);
-    case 4: return mfma_nk<4>(staged);
-    case 5: return mfma_nk<5>(staged);
-    case 6: return mfma_nk<6>(staged);
-    case 7: return mfma_nk<7>(staged);
-    default: return mfma_nk<8>(staged);
+    default: return mfma_nk<4>(staged);
     }
 }
 
@@ -447,7 +502,7 @@ size_t mfma_lds_fixed() { return kMOnehotBytes; }
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
     const uint32_t reserve = kMOnehotBytes + 4096 + 2048;  // tables, staged words, hit contexts
-    for (int nk = 1; nk <= 8; nk++) out[nk] = (160 * 1024) / waves[nk] - reserve;
+    for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / waves[nk] - reserve;
 }
 
 int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words,
@@ -502,11 +557,12 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan_mfma_kernel launch: ") + hipGetErrorString(e));
 #if TFBS_MFMA_PROBE == 4
-    unsigned long long pr[4] = {0, 0, 0, 0};
+    unsigned long long pr[5] = {0, 0, 0, 0, 0};
     for (uint32_t i = 0; i < n_streams; i++) (void)hipStreamSynchronize(streams[i]);
     (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_probe), sizeof pr);
-    fprintf(stderr, "probe4 tiles %llu entries %llu hits %llu invalid_hits %llu\n", pr[3], pr[0], pr[1], pr[2]);
-    const unsigned long long z[4] = {0, 0, 0, 0};
+    fprintf(stderr, "probe4 tiles %llu rescored %llu entries %llu hits %llu invalid_hits %llu\n", pr[3], pr[4], pr[0],
+            pr[1], pr[2]);
+    const unsigned long long z[5] = {0, 0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof z);
 #endif
     return launches;

@@ -80,22 +80,30 @@ struct DevTile {
     uint32_t pad;
 };
 
-// Matrix-core path (scan_mfma.hip).  A strand's weights split as w = 64 a + b
-// (a, b int8); the score of 32 windows x 32 strands is one-hot(window bases) x
-// [b; a] with the one-hot entries 1 and 64, summed exactly in int32 by
-// v_mfma_i32_32x32x32_i8.  K chunk (32) = 4 columns x 4 bases x 2 digits:
-// k = 16 d + 4 t + c, d = 0 (entry 1, digit b) or 1 (entry 64, digit a).
+// Matrix-core path (scan_mfma.hip).  Each strand's weights split as
+// w = s q + r with a per-strand scale s (1..255), q = round(w / s) in
+// [-127, 127] and |r| <= s / 2.  The coarse sum Q = one-hot(window bases) x q
+// over 32 windows x 32 strands is one v_mfma_i32_32x32x32_i8 per 8 columns; a
+// window can only hit if s Q + E > min_score, E = the largest residual sum, so
+// Q > thr_q = floor((min_score - E) / s) gates the exact rescore s Q + one-hot
+// x r (the same A fragments, the residual B fragments) on the rare tiles that
+// pass it.  K chunk (32) = 8 columns x 4 bases: k = 16 h + 4 t + c <-> column
+// 8 kc + 4 h + t, base c.
 constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
-constexpr int kMChunkCols = 4;     // columns per K chunk of 32
-constexpr int kMMaxChunks = 8;     // L <= 32
-constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (a 64-bit mask flags the tiles with hits)
+constexpr int kMChunkCols = 8;     // columns per K chunk of 32
+constexpr int kMMaxChunks = 4;     // L <= 32
+constexpr int kMMaxScale = 255;    // residual digits stay within int8
+constexpr int kMSuperMaxTiles = 64;  // tiles per super tile
 constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
-constexpr int kMMetaBytes = 512;   // per tile: thr[32], len[32], slot[32], orig[32]
+// per tile metadata, int32 x 32 each: coarse threshold, min_score, scale, len, slot, pattern index
+enum MMeta { kMetaThrQ = 0, kMetaMin = 32, kMetaScale = 64, kMetaLen = 96, kMetaSlot = 128, kMetaOrig = 160 };
+constexpr int kMMetaBytes = 768;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk * 1 KiB ([chunk][lane 64][16
-// bytes]), its metadata at meta_off + t * 512.
+// depth nk; tile t's coarse B fragments at t * 2 nk KiB ([chunk][lane 64][16
+// bytes]) followed by its nk residual fragments, its metadata at meta_off +
+// t * kMMetaBytes.
 struct DevMSuper {
     uint32_t tile_count;
     uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))

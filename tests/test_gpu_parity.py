@@ -155,6 +155,51 @@ def test_octet_boundaries_vs_oracle(monkeypatch, mfma):
         sc.close()
 
 
+def test_mfma_split_edges_vs_oracle(monkeypatch):
+    """The matrix-core path's coarse/residual split (mfma.cpp): scales 1..255 (max |w| up
+    to 127 x 255, and one weight past it going to the LUT path), half-way residuals at
+    even scales, thresholds tied with / one below real window scores (the coarse bound
+    must never drop an exact hit), thresholds below every score (every tile rescored),
+    N bases (one-hot zero, residual zero)."""
+    monkeypatch.setenv("TFBS_MFMA", "1")
+    rnd = random.Random(11)
+    base = "".join(rnd.choice("ACGT") for _ in range(600))
+    seqs = [base, base[:100] + "N" * 3 + base[103:400] + "N" + base[401:], base[:40], ""]
+    pats = []
+
+    def add(w4, ms):
+        pats.append(T.Pattern.PWM([T.Weight(*r) for r in w4], "S%d" % len(pats), len(pats) // 2, ms,
+                                  len(pats) % 2))
+
+    for L in (1, 3, 8, 9, 16, 17, 24, 25, 32):
+        for mx in (1, 2, 127, 128, 254, 1000, 4400, 127 * 254 + 1, 127 * 255):
+            w4 = [[rnd.randint(-mx, mx) for _ in range(4)] for _ in range(L)]
+            w4[rnd.randrange(L)][rnd.randrange(4)] = mx if rnd.random() < 0.5 else -mx
+            if mx % 2 == 0 and L > 1:  # exact halves of an even scale
+                s = (mx + 126) // 127
+                w4[0][1] = s // 2 * (1 if rnd.random() < 0.5 else -1)
+            sc = sorted(_scores(w4, base))
+            top = sc[-1 - rnd.randint(0, 3)] if sc else 0
+            add(w4, top)
+            add(w4, top - 1)
+            if mx in (4400, 127 * 255):
+                add(w4, sc[0] - 1 if sc else -1)  # every window hits
+    w4 = [[127 * 255 + 1, 0, -5, 7]] + [[rnd.randint(-100, 100) for _ in range(4)] for _ in range(7)]
+    pats.append(T.Pattern.PWM([T.Weight(*r) for r in w4], "LUT", 9999, sorted(_scores(w4, base))[-2], 0))
+    st = T.PatternSet.from_patterns(pats).plan_stats(mfma=True)
+    assert st["n_mfma_strands"] == len(pats) - 1, st
+    sc = T.Scanner(pats)
+    try:
+        for trial, seq in enumerate(seqs):
+            hap = _hap(seq, 7000)
+            got = sc.matches_all(hap)
+            for i, p_ in enumerate(pats):
+                w5 = [wt.acgtn for wt in p_.weights]
+                assert got[i] == O.matches(w5, p_.min_score, hap, kind=p_.kind), (trial, i)
+    finally:
+        sc.close()
+
+
 # ------------------------------------------------------------ main.rs:548-568 through the product
 def _c1(bcf_json, beds_files, samples_file=True):
     rec = json.load(open(os.path.join(GOLD, bcf_json)))
