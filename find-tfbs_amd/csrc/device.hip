@@ -77,7 +77,7 @@ struct tfbs_ctx {
     DevBuf<DevUnit> fast_units;
     DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
-    DevBuf<int32_t> lut, wfull, gen_w, m_image;
+    DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights;
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
     uint32_t mfma_lds = 28 * 1024;  // LDS image budget of one MFMA super tile
@@ -128,6 +128,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
+        m.mweights = ctx->m_weights.p;
         m.haps_per_block = ctx->mfma_hpb;
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
@@ -191,7 +192,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
-    ctx->m_image.release(); ctx->m_supers.release();
+    ctx->m_image.release(); ctx->m_weights.release(); ctx->m_supers.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
@@ -223,7 +224,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 28))) * 1024u;
-    ctx->mfma_hpb = (uint32_t)std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32));
+    ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32)));  // 8 bits in a candidate entry
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -271,6 +272,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         (rc = ctx->lut.put(P.lut, ctx->stream)) || (rc = ctx->wfull.put(P.wfull, ctx->stream)) ||
         (rc = ctx->gen_pats.put(P.gen_pats, ctx->stream)) || (rc = ctx->gen_tiles.put(P.gen_tiles, ctx->stream)) ||
         (rc = ctx->gen_w.put(P.gen_w, ctx->stream)) || (rc = ctx->m_image.put(P.m_image, ctx->stream)) ||
+        (rc = ctx->m_weights.put(P.m_weights, ctx->stream)) ||
         (rc = ctx->m_supers.put(P.m_supers, ctx->stream))) {
         tfbs_ctx_destroy(ctx);
         return rc;

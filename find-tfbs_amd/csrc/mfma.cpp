@@ -6,13 +6,12 @@
 // N), that is a dot product of a 0/1 vector with the strand's weights.  Each
 // strand gets a scale s = ceil(max |w| / 127) (1..255) and every weight splits
 // exactly as w = s q + r, q = round(w / s) (halves away from zero) in
-// [-127, 127], |r| <= s / 2 <= 127.  The kernel sums Q = sum q over a window
-// with one MFMA per 8 columns; since score = s Q + R and R <= E = sum over
-// columns of max(0, max_base r), a window can only pass `score > min_score`
-// (pattern.rs:151) when Q > thr_q = floor((min_score - E) / s).  Tiles with
-// such a window are rescored exactly as s Q + one-hot x r (residual
-// fragments, same A), |score| <= 32 * 32512, so nothing wraps and the sum is
-// the reference's i32 sum.
+// [-127, 127], |r| <= s / 2.  The kernel sums Q = sum q over a window with one
+// MFMA per 8 columns; since score = s Q + R and R <= E = sum over columns of
+// max(0, max_base r), a window can only pass `score > min_score`
+// (pattern.rs:151) when Q > thr_q = floor((min_score - E) / s).  Those
+// candidates are rescored exactly (i32 sum of the weights, kept here in
+// m_weights), so the coarse digits only ever select work.
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -27,7 +26,7 @@ namespace {
 
 struct Split {
     int32_t scale = 1, thr_q = INT32_MAX;
-    std::vector<int8_t> q, r;  // len x 4 (A, C, G, T)
+    std::vector<int8_t> q;  // len x 4 (A, C, G, T)
 };
 
 int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
@@ -39,7 +38,6 @@ Split split_weights(const Pat &p) {
         for (int c = 0; c < 4; c++) mx = std::max<int32_t>(mx, std::abs(p.w5[5 * j + c]));
     s.scale = std::max<int32_t>(1, (mx + 126) / 127);
     s.q.resize(4 * p.len);
-    s.r.resize(4 * p.len);
     int64_t e = 0;  // the largest residual a window can add (N adds 0)
     for (uint32_t j = 0; j < p.len; j++) {
         int32_t emax = 0;
@@ -48,13 +46,14 @@ Split split_weights(const Pat &p) {
             const int32_t q = (w < 0 ? -1 : 1) * ((a + s.scale / 2) / s.scale);
             const int32_t r = w - s.scale * q;
             s.q[4 * j + c] = (int8_t)q;
-            s.r[4 * j + c] = (int8_t)r;
             emax = std::max(emax, r);
         }
         e += emax;
     }
+    // |Q| <= 127 x 32, so clamping to +-2^24 changes no outcome and keeps the
+    // kernel's thr_q - Q from wrapping
     const int64_t t = floor_div((int64_t)p.min_score - e, s.scale);
-    s.thr_q = (int32_t)std::max<int64_t>(INT32_MIN, std::min<int64_t>(INT32_MAX, t));
+    s.thr_q = (int32_t)std::max<int64_t>(-(1 << 24), std::min<int64_t>(1 << 24, t));
     return s;
 }
 
@@ -65,7 +64,7 @@ bool mfma_eligible(const Pat &p) {
     for (uint32_t j = 0; j < p.len; j++)
         for (int c = 0; c < 4; c++) {
             const int64_t w = p.w5[5 * j + c];
-            if (w < -127 * kMMaxScale || w > 127 * kMMaxScale) return false;  // s <= 255 keeps r in int8
+            if (w < -127 * kMMaxScale || w > 127 * kMMaxScale) return false;  // s <= 255
         }
     return true;
 }
@@ -77,7 +76,14 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         for (int i : g.strands) strands.push_back({i, g.slot});
     if (strands.empty()) return;
     std::vector<Split> split(strands.size());
-    for (size_t s = 0; s < strands.size(); s++) split[s] = split_weights(P.pats[strands[s].first]);
+    std::vector<uint32_t> woff(strands.size());
+    for (size_t s = 0; s < strands.size(); s++) {
+        const Pat &p = P.pats[strands[s].first];
+        split[s] = split_weights(p);
+        woff[s] = (uint32_t)plan->m_weights.size();
+        for (uint32_t j = 0; j < p.len; j++)
+            for (int c = 0; c < 4; c++) plan->m_weights.push_back(p.w5[5 * j + c]);
+    }
 
     struct TileSrc { size_t first, count; uint32_t nk, lmin; };
     std::vector<TileSrc> tiles;
@@ -94,7 +100,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
     while (ti < tiles.size()) {
         // a super tile: consecutive tiles of the same K depth within the LDS budget
         const uint32_t nk = tiles[ti].nk;
-        const uint32_t per = 2 * nk * kMFragBytes + kMMetaBytes;
+        const uint32_t per = nk * kMFragBytes + kMMetaBytes;
         const uint32_t lds_bytes = std::max(per, opt.mfma_lds_by_nk[nk] ? opt.mfma_lds_by_nk[nk] : opt.mfma_lds_bytes);
         // the run of tiles with this depth, split into equal super tiles
         size_t run = ti;
@@ -108,12 +114,12 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         S.nk = nk;
         S.img_off = (uint32_t)(plan->m_image.size() * 4);
         S.img_bytes = count * per;
-        S.meta_off = count * 2 * nk * kMFragBytes;
+        S.meta_off = count * nk * kMFragBytes;
         S.lmin = UINT32_MAX;
         std::vector<uint8_t> img(S.img_bytes, 0);
         for (uint32_t k = 0; k < count; k++) {
             const TileSrc &t = tiles[ti + k];
-            const uint32_t b_off = k * 2 * nk * kMFragBytes, meta_off = S.meta_off + k * kMMetaBytes;
+            const uint32_t b_off = k * nk * kMFragBytes, meta_off = S.meta_off + k * kMMetaBytes;
             S.lmin = std::min(S.lmin, t.lmin);
             int32_t *meta = reinterpret_cast<int32_t *>(&img[meta_off]);
             for (int n = 0; n < kMStrands; n++) {
@@ -123,23 +129,22 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     const Split &sp = split[t.first + n];
                     meta[kMetaThrQ + n] = sp.thr_q;
                     meta[kMetaMin + n] = p.min_score;
-                    meta[kMetaScale + n] = sp.scale;
+                    meta[kMetaWoff + n] = (int32_t)woff[t.first + n];
                     meta[kMetaLen + n] = (int32_t)p.len;
                     meta[kMetaSlot + n] = (int32_t)st.second;
                     meta[kMetaOrig + n] = st.first;
                     plan->n_mfma_strands++;
                 } else {  // padding column: never a candidate
-                    meta[kMetaThrQ + n] = INT32_MAX;
+                    meta[kMetaThrQ + n] = 1 << 24;
                     meta[kMetaMin + n] = INT32_MAX;
-                    meta[kMetaScale + n] = 1;
+                    meta[kMetaWoff + n] = 0;
                     meta[kMetaLen + n] = 0;
                     meta[kMetaSlot + n] = 0;
                     meta[kMetaOrig + n] = -1;
                 }
             }
             // B fragments: lane l holds column n = l & 31 and k = 16 h + 4 t + c,
-            // h = l >> 5, <-> strand column 8 kc + 4 h + t, base c; coarse digits
-            // in chunks 0 .. nk-1, residual digits in chunks nk .. 2 nk - 1
+            // h = l >> 5, <-> strand column 8 kc + 4 h + t, base c
             for (uint32_t kc = 0; kc < nk; kc++)
                 for (int l = 0; l < 64; l++) {
                     const int n = l & 31, h = l >> 5;
@@ -147,14 +152,10 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     const Pat &p = P.pats[strands[t.first + n].first];
                     const Split &sp = split[t.first + n];
                     int8_t *fq = reinterpret_cast<int8_t *>(&img[b_off + kc * kMFragBytes + l * 16]);
-                    int8_t *fr = reinterpret_cast<int8_t *>(&img[b_off + (nk + kc) * kMFragBytes + l * 16]);
                     for (int tt = 0; tt < 4; tt++) {
                         const uint32_t col = kc * kMChunkCols + 4 * h + tt;
                         if (col >= p.len) continue;
-                        for (int c = 0; c < 4; c++) {
-                            fq[4 * tt + c] = sp.q[4 * col + c];
-                            fr[4 * tt + c] = sp.r[4 * col + c];
-                        }
+                        for (int c = 0; c < 4; c++) fq[4 * tt + c] = sp.q[4 * col + c];
                     }
                 }
         }

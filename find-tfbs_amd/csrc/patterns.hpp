@@ -36,6 +36,7 @@ struct Plan {
     std::vector<DevMSuper> m_supers;
     uint32_t n_mfma_tiles = 0;
     std::vector<int32_t> m_image;    // per super tile: B fragments + strand metadata (LDS image)
+    std::vector<int32_t> m_weights;  // per MFMA strand: exact [A,C,G,T] weights per column (candidate rescoring)
     uint32_t max_super_bytes = 0;
     uint32_t n_mfma_strands = 0;
     bool zero_len_panics = false;

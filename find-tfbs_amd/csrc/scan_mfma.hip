@@ -38,19 +38,14 @@ namespace tfbs {
 namespace {
 
 // Bottleneck probes (tools/probe_build.sh, never in the product build):
-// TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live), =2 reads every
-// B fragment from tile 0, =3 skips the hit handling (results wrong; timing only),
-// =4 counts hit-path entries, hits and invalid-window hits (printed per launch),
-// =5 enters the hit path and returns at once, =6 keeps one B fragment set in
-// registers instead of reading each tile's from LDS.
+// TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live; timing only),
+// =2 reads every B fragment from tile 0 (results wrong; timing only), =4 counts
+// tiles, firing tiles, candidate lanes, exact hits and rejected candidates
+// (printed per launch).
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
-// TFBS_MFMA_PIPE=1: software-pipelined strand loop (tests of tile t-1 after the
-// MFMAs of tile t)
-#ifndef TFBS_MFMA_PIPE
-#define TFBS_MFMA_PIPE 0
-#endif
+
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
@@ -63,8 +58,8 @@ constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup at 4 workgroup
 // accumulators)
 constexpr uint32_t kMfmaWindowTiles[kMMaxChunks + 1] = {1, 2, 2, 2, 2};
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
-constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 6, 5, 4, 4};
-constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE, 4 - TFBS_MFMA_PIPE};
+constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 7, 5, 5, 4};
+constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 
 // The packed words (and N-mask words) a lane needs for its window of the
 // 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
@@ -126,19 +121,7 @@ struct BFrag {
 template <int NK>
 __device__ __forceinline__ void load_tile(const char *s_img, const DevMSuper &S, uint32_t ti, uint32_t lane,
                                           BFrag<NK> &f) {
-#if TFBS_MFMA_PROBE == 6
-    (void)s_img;
-    (void)S;
-    (void)ti;
-#pragma unroll
-    for (int kc = 0; kc < NK; kc++) {
-        f.b[kc] = v4i{(int)lane, (int)kc, 1, 2};
-        asm volatile("" : "+v"(f.b[kc]));
-    }
-    f.thr = 1 << 30;
-    return;
-#endif
-    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (2 * NK * kMFragBytes) + lane * 16;
+    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes) + lane * 16;
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
     f.thr = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes)[kMetaThrQ + (lane & 31)];
@@ -167,97 +150,107 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
     return h;
 }
 
-// Hit-handling context in LDS, so that the out-of-line rare path takes only
-// the scores and a few scalars as arguments (all in registers, no scratch).
-struct KernelHitCtx {
-    uint32_t *counts;
-    const int32_t *posrel;
-    unsigned long long *hits;
-    uint32_t hits_wpp, n_pat;
-};
-struct WaveHitCtx {  // written by the wave at each haplotype
-    const int32_t *inner;  // global inner ranges of the haplotype's region
-    uint64_t count_off;
-    uint32_t len, flags, pos_off, hap, n_inner;
-    int32_t inner_lds;     // the same ranges at s_inner[inner_lds], or -1
-};
-constexpr int kMMaxWaves = 8;
-constexpr uint32_t kMInnerMax = 64;  // inner ranges of a workgroup's regions kept in LDS
-__shared__ KernelHitCtx s_kctx;
-__shared__ WaveHitCtx s_wctx[kMMaxWaves];
-__shared__ int32_t s_inner[2 * kMInnerMax];
-__shared__ uint32_t s_inner_base;    // inner_off of s_inner[0], or UINT32_MAX when not staged
-// Per-wave log of the counts a haplotype's hits add to (offsets from its
-// count_off), flushed as one batch of global atomics after the haplotype, so
-// that the hit path issues no global memory operation.
-constexpr uint32_t kMLog = 64;
-__shared__ uint32_t s_log[kMMaxWaves][kMLog];
-__shared__ uint32_t s_log_n[kMMaxWaves];
-extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot tables | image | words
+// Candidate handling.  A tile whose coarse test fires (about one in nine)
+// appends one entry per lane with a candidate to the wave's queue in LDS.  The
+// strand loop stops before a tile pair whose entries might not fit; the queue
+// (and the wave's last one) is then drained 64 entries at a time, one per
+// lane, by drain_queue, which rescores each candidate window exactly from the
+// strand's weights (pattern.rs:125-135) and counts the hits, and the loop
+// resumes.  Inlined there, where few registers are live, it adds none.  Entry:
+// bits 0-15 the lane's candidate mask (bit 15 - r <-> register r), 16-21 the
+// lane, 22-27 the strand tile, 32-39 the haplotype in the workgroup's group,
+// 40-63 the window tile start / 32.
+constexpr uint32_t kMQueue = 256;  // entries per wave; a tile pair adds at most 128
+__shared__ uint64_t s_queue[kMBlock / 64][kMQueue];
+extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 #if TFBS_MFMA_PROBE == 4
 __device__ unsigned long long g_probe[5];
 #endif
+#if TFBS_MFMA_PROBE == 8
+__device__ unsigned int g_trace_n;
+__device__ uint4 g_trace[8192];  // (kind << 24 | lane, i or m, L or at, score or i0)
+__device__ __forceinline__ void trace(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t k = atomicAdd(&g_trace_n, 1u);
+    if (k < 8192) g_trace[k] = make_uint4(a, b, c, d);
+}
+#endif
 
-// The rare path of check_tile (about one tile in ten), out of line and compact
-// so that neither its registers nor its code crowd the hot loop.  Each lane
-// collects a 16-bit mask of its registers above its strand's threshold (bit
-// 15 - r for register r = window i0 + (r & 3) + 8 (r >> 2) + 4 (lane >> 5)),
-// then walks the set bits: the window validity test (i + L <= len), the
-// inner-range overlap test (range.rs:18-21 as main.rs:503 uses it) and the
-// atomic count of the strand's slot.  meta_off: LDS byte offset of the tile's
-// strand metadata (MMeta fields, 32 each); acc: exact scores, thr: min_score.
-__device__ __noinline__ void tile_hits(v16i acc, int32_t thr, uint32_t meta_off, uint32_t i0) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, (uint32_t)(thr - acc[r]), 31);
-    m &= 0xFFFFu;
-#if TFBS_MFMA_PROBE == 5
-    asm volatile("" ::"v"(m));
-    return;
-#endif
-    const uint32_t lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
-    const WaveHitCtx &W = s_wctx[uni(threadIdx.x >> 6)];
-    const int32_t *meta = reinterpret_cast<const int32_t *>(reinterpret_cast<const char *>(s_mdyn) + meta_off);
-    const uint32_t L = (uint32_t)meta[kMetaLen + n];
-#if TFBS_MFMA_PROBE == 4
-    if (lane == 0) atomicAdd(&g_probe[0], 1ull);
-    for (uint32_t q = m; q; q &= q - 1) {
-        const uint32_t r = 15 - (31 - __builtin_clz(q & -q));
-        const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        atomicAdd(&g_probe[i + L <= W.len ? 1 : 2], 1ull);
+// Exact score of window i of haplotype hp for a strand of length L (i + L <= len)
+__device__ __forceinline__ int32_t exact_score(const ScanArgs &A, const uint32_t *words, const DevHap &hp, uint32_t i,
+                                               uint32_t L, uint32_t woff) {
+    const uint32_t *w = words + hp.word_off + (i >> 4);
+    const uint32_t sh = 2 * (i & 15);
+    const uint32_t img[2] = {__builtin_amdgcn_alignbit(w[1], w[0], sh), __builtin_amdgcn_alignbit(w[2], w[1], sh)};
+    uint32_t live = 0xFFFFFFFFu;  // bit j: base i + j is not N
+    if (hp.flags & HAP_HAS_N) {
+        const uint32_t *m = A.nmask + hp.nmask_off + (i >> 5);
+        live = ~__builtin_amdgcn_alignbit(m[1], m[0], i & 31);
     }
-#endif
-    if (m == 0) return;
-    const uint32_t len = W.len, flags = W.flags, pos_off = W.pos_off, n_inner = W.n_inner;
-    const int32_t il = W.inner_lds;
-    const uint32_t slot = (uint32_t)meta[kMetaSlot + n];
-    const uint32_t wave = uni(threadIdx.x >> 6);
-    const uint32_t off0 = slot * n_inner;
+    const int32_t *wt = A.mweights + woff;
+    int32_t s = 0;
 #pragma unroll 1
-    do {
-        const uint32_t b = 31 - __builtin_clz(m & -m);  // lowest set bit
-        m &= m - 1;
-        const uint32_t r = 15 - b;
-        const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (i + L > len) continue;
-        const int32_t p = (flags & HAP_HAS_POS) ? s_kctx.posrel[pos_off + i] : (int32_t)i;
-#pragma unroll 1
-        for (uint32_t k = 0; k < n_inner; k++) {
-            const int32_t s = il >= 0 ? s_inner[il + 2 * k] : W.inner[2 * k];
-            const int32_t e = il >= 0 ? s_inner[il + 2 * k + 1] : W.inner[2 * k + 1];
-            const uint32_t span = (uint32_t)(e - s);
-            if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span) {
-                const uint32_t at = atomicAdd(&s_log_n[wave], 1u);
-                if (at < kMLog) s_log[wave][at] = off0 + k;
-                else atomicAdd(s_kctx.counts + W.count_off + off0 + k, 1u);  // log full
-            }
+    for (uint32_t j = 0; j < L; j += 4) {  // four independent loads per round, few registers
+        int32_t v[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            const uint32_t jj = j + u, c = (img[jj >> 4] >> (2 * (jj & 15))) & 3u;
+            const int32_t x = wt[4 * min(jj, L - 1) + c];                  // in bounds even past L
+            v[u] = (jj < L && ((live >> jj) & 1u)) ? x : 0;                 // N scores 0
         }
-        unsigned long long *hits = s_kctx.hits;
-        const uint32_t wpp = s_kctx.hits_wpp;
-        if (hits && i / 64 < wpp)
-            atomicOr(hits + ((size_t)W.hap * s_kctx.n_pat + (uint32_t)meta[kMetaOrig + n]) * wpp + i / 64, 1ull << (i & 63));
-    } while (m);
+        s += (v[0] + v[1]) + (v[2] + v[3]);
+    }
+    return s;
+}
+
+// Drains the wave's first n queue entries (all lanes; one entry per lane per
+// round).  h0: the workgroup's first haplotype; meta0: tile 0's metadata.
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+                                            uint32_t h0, uint32_t n, uint32_t wave) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t e = lane; e < n; e += 64) {
+        const uint64_t q = s_queue[wave][e];
+        uint32_t m = (uint32_t)q & 0xFFFFu;
+        const uint32_t src = ((uint32_t)q >> 16) & 63u, ti = ((uint32_t)q >> 22) & 63u;
+        const uint32_t hap = h0 + ((uint32_t)(q >> 32) & 255u), i0 = (uint32_t)(q >> 40) << 5;
+        const uint32_t col = src & 31u, h = src >> 5;
+        const int32_t *meta = meta0 + ti * (kMMetaBytes / 4);
+        const uint32_t L = (uint32_t)meta[kMetaLen + col], woff = (uint32_t)meta[kMetaWoff + col];
+        const int32_t mn = meta[kMetaMin + col];
+        const DevHap hp = A.haps[hap];
+        const DevRegion rg = A.regions[hp.region];
+        const uint32_t off0 = (uint32_t)meta[kMetaSlot + col] * rg.n_inner;
+        const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+        while (m) {
+            const uint32_t b = 31 - __builtin_clz(m & -m);  // lowest set bit
+            m &= m - 1;
+            const uint32_t r = 15 - b;
+            const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (i + L > hp.len) continue;                   // past the end (pattern.rs:147-150)
+            const int32_t sc = exact_score(A, words, hp, i, L, woff);
+#if TFBS_MFMA_PROBE == 7
+            printf("D e %u src %u i %u L %u sc %d mn %d\n", e, src, i, L, sc, mn);
+#endif
+#if TFBS_MFMA_PROBE == 8
+            trace((2u << 24) | src, i, e, (uint32_t)sc);
+#endif
+#if TFBS_MFMA_PROBE == 4
+            atomicAdd(&g_probe[sc > mn ? 1 : 2], 1ull);
+#endif
+            if (!(sc > mn)) continue;                       // strict (pattern.rs:151)
+            const int32_t p = (hp.flags & HAP_HAS_POS) ? A.posrel[hp.pos_off + i] : (int32_t)i;
+            for (uint32_t k = 0; k < rg.n_inner; k++) {     // range.rs:18-21 as main.rs:503 uses it
+                const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+                const uint32_t span = (uint32_t)(en - s);
+                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
+                    atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
+            }
+            if (A.hits && i / 64 < A.hits_wpp)
+                atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kMetaOrig + col]) * A.hits_wpp +
+                             i / 64,
+                         1ull << (i & 63));
+        }
+    }
 }
 
 __device__ __forceinline__ int32_t max16(const v16i &acc) {
@@ -265,39 +258,43 @@ __device__ __forceinline__ int32_t max16(const v16i &acc) {
     return max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
 }
 
-// Threshold test of one strand tile: the max of the lane's 16 coarse sums
-// against its strand's thr_q, one ballot.  The tiles that pass (about one in
-// eight) are rescored exactly, s Q + one-hot x r with the residual fragments,
-// and their scores above min_score go to tile_hits.
-template <int NK>
-__device__ __forceinline__ void check_tile(const char *s_img, const DevMSuper &S, uint32_t ti, const v16i &acc,
-                                           int32_t thr, const v4i (&a)[NK], uint32_t i0, uint32_t lane) {
-    if (TFBS_MFMA_PROBE == 1) {
-        asm volatile("" ::"v"(acc[0]), "v"(acc[5]), "v"(acc[10]), "v"(acc[15]));
-        return;
-    }
+// Coarse test of one strand tile: the max of each lane's 16 coarse sums
+// against its strand's thr_q, one ballot.  Both tiles of a pair are tested
+// before either branches, so every read of the MFMA results sits in the
+// MFMAs' basic block, where the compiler's wait-state accounting holds (a read
+// placed after the branch of the first tile's test got too few wait states
+// and saw stale sums).
+__device__ __forceinline__ uint64_t coarse_test(const v16i &acc, int32_t thr) {
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[3], 1ull);
 #endif
-    if (__builtin_expect(__ballot(max16(acc) > thr) == 0, 1)) return;
-    if (TFBS_MFMA_PROBE == 3) return;
+    if (TFBS_MFMA_PROBE == 1) {
+        asm volatile("" ::"v"(acc[0]), "v"(acc[5]), "v"(acc[10]), "v"(acc[15]));
+        return 0;
+    }
+    return __ballot(max16(acc) > thr);
+}
+
+// A firing tile (fired = its coarse ballot, about one tile in nine): each
+// firing lane queues its candidate mask; qn (wave-uniform) counts the wave's
+// queued entries.
+__device__ __forceinline__ void queue_tile(const v16i &acc, int32_t thr, uint64_t fired, uint32_t ti, uint32_t hh,
+                                           uint32_t i0, uint32_t lane, uint32_t wave, uint32_t &qn) {
+    if (__builtin_expect(fired == 0, 1)) return;
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[4], 1ull);
+    if (fired & (1ull << lane)) atomicAdd(&g_probe[0], 1ull);
 #endif
-    const uint32_t meta_off = S.meta_off + ti * kMMetaBytes;
-    const int32_t *meta = reinterpret_cast<const int32_t *>(s_img + meta_off);
-    const int32_t sc = meta[kMetaScale + (lane & 31)], mn = meta[kMetaMin + (lane & 31)];
-    const char *p = s_img + ti * (2 * NK * kMFragBytes) + NK * kMFragBytes + lane * 16;
-    v4i br[NK];
+    uint32_t m = 0;  // |acc| <= 127 x 32 and |thr| <= 2^24: no wrap
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) br[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
-    v16i ex;
-#pragma unroll
-    for (int r = 0; r < 16; r++) ex[r] = __mul24(acc[r], sc);  // |Q| <= 127 x 32, s <= 255
-#pragma unroll
-    for (int kc = 0; kc < NK; kc++) ex = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kc], br[kc], ex, 0, 0, 0);
-    if (__ballot(max16(ex) > mn) == 0) return;
-    tile_hits(ex, mn, kMOnehotBytes + meta_off, i0);
+    for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, (uint32_t)(thr - acc[r]), 31);
+    const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, 0));
+#if TFBS_MFMA_PROBE == 8
+    if (fired & (1ull << lane)) trace((1u << 24) | lane, m, at, i0);
+#endif
+    if (fired & (1ull << lane))  // every firing lane (m != 0) fills its slot
+        s_queue[wave][at] = (uint64_t)(m | (lane << 16) | (ti << 22)) | ((uint64_t)(hh | ((i0 >> 5) << 8)) << 32);
+    qn += (uint32_t)__popcll(fired);
 }
 
 // Coarse sums of strand tile ti for two window tiles (one B fragment read
@@ -326,24 +323,14 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
     constexpr uint32_t kWaves = kMBlock / 64;
     const uint32_t nt = S.tile_count;
+    const uint32_t h0 = hg * A.haps_per_block;
+    const int32_t *meta0 = reinterpret_cast<const int32_t *>(s_img + S.meta_off);
+    uint32_t qn = 0;
     for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
         const uint32_t hap = hg * A.haps_per_block + hh;
         if (hap >= A.n_haps) break;
         const DevHap hm = load_hap(A.haps + hap);
         if (hm.len < S.lmin) continue;
-        const DevRegion rg = A.regions[hm.region];
-        {  // every lane stores the same (uniform) values
-            WaveHitCtx &W = s_wctx[wave];
-            const uint32_t io = uni(rg.inner_off), ib = s_inner_base;
-            W.inner = A.inner + 2 * (size_t)io;
-            W.inner_lds = ib == UINT32_MAX ? -1 : (int32_t)(2 * (io - ib));
-            W.count_off = hm.count_off;
-            W.len = hm.len;
-            W.flags = hm.flags;
-            W.pos_off = hm.pos_off;
-            W.hap = hap;
-            W.n_inner = uni(rg.n_inner);
-        }
         const uint32_t nwin = hm.len - S.lmin + 1;
         const char *tab = s_img - kMOnehotBytes;
         // window tiles two at a time, so that each B fragment read from LDS
@@ -362,80 +349,53 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             if (kStep > kMWindows && i0 + kStep + kMWindows < nwin)
                 load_window(A, words, hm, i0 + kStep + kMWindows, lane, ww1);
             // the other waves of the SIMD hide the latencies
-            if (two) {
-#if TFBS_MFMA_PIPE
-                // software pipeline: tile t's MFMAs issue before tile t-1's
-                // threshold tests, so the tests overlap the matrix pipe
-                v16i c0, c1, d0, d1;
-                int32_t tc, td;
-                pair_scores<NK>(s_img, S, 0, lane, a0, a1, c0, c1, tc);
-                uint32_t ti = 1;
-                for (; ti + 1 < nt; ti += 2) {
-                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, d0, d1, td);
-                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
-                    pair_scores<NK>(s_img, S, ti + 1, lane, a0, a1, c0, c1, tc);
-                    check_tile<NK>(s_img, S, ti, d0, td, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti, d1, td, a1, i0 + kMWindows, lane);
-                }
-                if (ti < nt) {
-                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, d0, d1, td);
-                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
-                    check_tile<NK>(s_img, S, ti, d0, td, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti, d1, td, a1, i0 + kMWindows, lane);
+            for (uint32_t ti = 0;;) {
+                if (two) {
+                    for (; ti < nt && qn <= kMQueue - 128; ti++) {
+                        v16i c0, c1;
+                        int32_t tc;
+                        pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
+                        const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
+                        queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
+                        queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+                    }
                 } else {
-                    check_tile<NK>(s_img, S, ti - 1, c0, tc, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti - 1, c1, tc, a1, i0 + kMWindows, lane);
+                    // two strand tiles at a time: tile 0's test overlaps tile 1's MFMAs
+                    for (; ti + 1 < nt && qn <= kMQueue - 128; ti += 2) {
+                        BFrag<NK> f0, f1;
+                        load_tile<NK>(s_img, S, ti, lane, f0);
+                        load_tile<NK>(s_img, S, ti + 1, lane, f1);
+                        __builtin_amdgcn_sched_barrier(0);
+                        const v16i acc0 = tile_scores<NK>(a0, f0);
+                        const v16i acc1 = tile_scores<NK>(a0, f1);
+                        const uint64_t g0 = coarse_test(acc0, f0.thr), g1 = coarse_test(acc1, f1.thr);
+                        queue_tile(acc0, f0.thr, g0, ti, hh, i0, lane, wave, qn);
+                        queue_tile(acc1, f1.thr, g1, ti + 1, hh, i0, lane, wave, qn);
+                    }
+                    if (ti + 1 == nt && qn <= kMQueue - 128) {
+                        BFrag<NK> f;
+                        load_tile<NK>(s_img, S, ti, lane, f);
+                        __builtin_amdgcn_sched_barrier(0);
+                        const v16i acc = tile_scores<NK>(a0, f);
+                        queue_tile(acc, f.thr, coarse_test(acc, f.thr), ti, hh, i0, lane, wave, qn);
+                        ti++;
+                    }
                 }
-#else
-                for (uint32_t ti = 0; ti < nt; ti++) {
-                    v16i c0, c1;
-                    int32_t tc;
-                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
-                    check_tile<NK>(s_img, S, ti, c0, tc, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti, c1, tc, a1, i0 + kMWindows, lane);
-                }
-#endif
-                continue;
-            }
-            uint32_t ti = 0;
-            if (NK <= 4) {  // two strand tiles at a time: tile 0's test overlaps tile 1's MFMAs
-                for (; ti + 1 < nt; ti += 2) {
-                    BFrag<NK> f0, f1;
-                    load_tile<NK>(s_img, S, ti, lane, f0);
-                    load_tile<NK>(s_img, S, ti + 1, lane, f1);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const v16i acc0 = tile_scores<NK>(a0, f0);
-                    const v16i acc1 = tile_scores<NK>(a0, f1);
-                    check_tile<NK>(s_img, S, ti, acc0, f0.thr, a0, i0, lane);
-                    check_tile<NK>(s_img, S, ti + 1, acc1, f1.thr, a0, i0, lane);
-                }
-            }
-            for (; ti < nt; ti++) {
-                BFrag<NK> f;
-                load_tile<NK>(s_img, S, ti, lane, f);
-                __builtin_amdgcn_sched_barrier(0);
-                const v16i acc = tile_scores<NK>(a0, f);
-                check_tile<NK>(s_img, S, ti, acc, f.thr, a0, i0, lane);
+                if (ti >= nt) break;
+                drain_queue(A, words, meta0, h0, qn, wave);  // queue nearly full: drain, resume at tile ti
+                qn = 0;
             }
         }
-        // the haplotype's logged hits: one batch of global atomics
-        const uint32_t nl = min(s_log_n[wave], kMLog);
-        for (uint32_t j = lane; j < nl; j += 64) atomicAdd(A.counts + hm.count_off + s_log[wave][j], 1u);
-        s_log_n[wave] = 0;
     }
+    if (qn) drain_queue(A, words, meta0, h0, qn, wave);
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD.
-// LDS: one-hot tables | super tile image | (STAGED) the packed words of the
+// LDS: one-hot table | super tile image | (STAGED) the packed words of the
 // workgroup's haplotypes, copied once so that every window read is an LDS read.
 template <bool STAGED, int NK>
 __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(ScanArgs A) {
-    static_assert(kMBlock / 64 <= kMMaxWaves, "one hit context per wave");
     int32_t *smem = s_mdyn;
-    if (threadIdx.x == 0) s_kctx = KernelHitCtx{A.counts, A.posrel, A.hits, A.hits_wpp, A.n_patterns_total};
-    if (threadIdx.x < kMMaxWaves) s_log_n[threadIdx.x] = 0;
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
     const DevMSuper S = A.msupers[sidx];
@@ -451,13 +411,7 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     }
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hl = min(h0 + A.haps_per_block, A.n_haps) - 1;
-    {  // inner ranges of the group's regions (consecutive in A.inner), for the hit path
-        const DevRegion r0 = A.regions[A.haps[h0].region], r1 = A.regions[A.haps[hl].region];
-        const uint32_t n = r1.inner_off + r1.n_inner - r0.inner_off;
-        if (n <= kMInnerMax)
-            for (uint32_t i = threadIdx.x; i < 2 * n; i += kMBlock) s_inner[i] = A.inner[2 * (size_t)r0.inner_off + i];
-        if (threadIdx.x == 0) s_inner_base = n <= kMInnerMax ? r0.inner_off : UINT32_MAX;
-    }
+    const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     const uint32_t *words = A.words;
     if (STAGED) {
         const uint32_t wbeg = A.haps[h0].word_off;
@@ -467,7 +421,6 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
         words = s_words - wbeg;
     }
     __syncthreads();
-    const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     // the wave index is uniform: keep every haplotype-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
@@ -501,7 +454,7 @@ size_t mfma_lds_fixed() { return kMOnehotBytes; }
 
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
-    const uint32_t reserve = kMOnehotBytes + 4096 + 2048;  // tables, staged words, hit contexts
+    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_queue) + 256;  // table, staged words, queues
     for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / waves[nk] - reserve;
 }
 
@@ -510,8 +463,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     if (n_haps == 0 || n_supers == 0) return 0;
     const uint32_t hpb = a0.haps_per_block;
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds =
-        sizeof(KernelHitCtx) + sizeof(s_wctx) + sizeof(s_inner) + sizeof(s_log) + sizeof(s_log_n) + 16;  // hit contexts
+    const size_t static_lds = sizeof(s_queue) + 16;  // candidate queues
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is
     // compiled for its depth's registers and LDS; the deepest (longest) first
@@ -556,12 +508,27 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan_mfma_kernel launch: ") + hipGetErrorString(e));
+#if TFBS_MFMA_PROBE == 8
+    {
+        for (uint32_t i = 0; i < n_streams; i++) (void)hipStreamSynchronize(streams[i]);
+        unsigned int n = 0;
+        (void)hipMemcpyFromSymbol(&n, HIP_SYMBOL(g_trace_n), sizeof n);
+        std::vector<uint4> t(std::min(n, 8192u));
+        if (!t.empty()) (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_trace), t.size() * sizeof(uint4));
+        for (const uint4 &x : t)
+            fprintf(stderr, "%s lane %u %s %u %s %u %s %d\n", (x.x >> 24) == 1 ? "Q" : "D", x.x & 0xFFFFFF,
+                    (x.x >> 24) == 1 ? "m" : "i", x.y, (x.x >> 24) == 1 ? "at" : "e", x.z,
+                    (x.x >> 24) == 1 ? "i0" : "sc", (int)x.w);
+        n = 0;
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_n), &n, sizeof n);
+    }
+#endif
 #if TFBS_MFMA_PROBE == 4
     unsigned long long pr[5] = {0, 0, 0, 0, 0};
     for (uint32_t i = 0; i < n_streams; i++) (void)hipStreamSynchronize(streams[i]);
     (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_probe), sizeof pr);
-    fprintf(stderr, "probe4 tiles %llu rescored %llu entries %llu hits %llu invalid_hits %llu\n", pr[3], pr[4], pr[0],
-            pr[1], pr[2]);
+    fprintf(stderr, "probe4 tiles %llu fired %llu candidate_lanes %llu hits %llu rejected %llu\n", pr[3], pr[4],
+            pr[0], pr[1], pr[2]);
     const unsigned long long z[5] = {0, 0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof z);
 #endif

@@ -85,25 +85,24 @@ struct DevTile {
 // [-127, 127] and |r| <= s / 2.  The coarse sum Q = one-hot(window bases) x q
 // over 32 windows x 32 strands is one v_mfma_i32_32x32x32_i8 per 8 columns; a
 // window can only hit if s Q + E > min_score, E = the largest residual sum, so
-// Q > thr_q = floor((min_score - E) / s) gates the exact rescore s Q + one-hot
-// x r (the same A fragments, the residual B fragments) on the rare tiles that
-// pass it.  K chunk (32) = 8 columns x 4 bases: k = 16 h + 4 t + c <-> column
-// 8 kc + 4 h + t, base c.
+// Q > thr_q = floor((min_score - E) / s) selects the candidates, which are
+// rescored exactly from the strand's weights.  K chunk (32) = 8 columns x 4
+// bases: k = 16 h + 4 t + c <-> column 8 kc + 4 h + t, base c.
 constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
 constexpr int kMChunkCols = 8;     // columns per K chunk of 32
 constexpr int kMMaxChunks = 4;     // L <= 32
-constexpr int kMMaxScale = 255;    // residual digits stay within int8
-constexpr int kMSuperMaxTiles = 64;  // tiles per super tile
+constexpr int kMMaxScale = 255;    // |w| <= 127 x 255
+constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (6 bits in a candidate entry)
 constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
-// per tile metadata, int32 x 32 each: coarse threshold, min_score, scale, len, slot, pattern index
-enum MMeta { kMetaThrQ = 0, kMetaMin = 32, kMetaScale = 64, kMetaLen = 96, kMetaSlot = 128, kMetaOrig = 160 };
+// per tile metadata, int32 x 32 each: coarse threshold, min_score, offset of
+// the exact weights (4 per column), len, slot, pattern index
+enum MMeta { kMetaThrQ = 0, kMetaMin = 32, kMetaWoff = 64, kMetaLen = 96, kMetaSlot = 128, kMetaOrig = 160 };
 constexpr int kMMetaBytes = 768;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's coarse B fragments at t * 2 nk KiB ([chunk][lane 64][16
-// bytes]) followed by its nk residual fragments, its metadata at meta_off +
-// t * kMMetaBytes.
+// depth nk; tile t's B fragments at t * nk KiB ([chunk][lane 64][16 bytes]),
+// its metadata at meta_off + t * kMMetaBytes.
 struct DevMSuper {
     uint32_t tile_count;
     uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
