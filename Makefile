@@ -25,7 +25,7 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 
 # MFMA results straight into VGPRs (gfx950's unified register file): the
 # threshold test reads every accumulator, so AGPR copies would cost 16 VALU per tile
-$(OBJDIR)/scan_mfma.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+$(OBJDIR)/scan_mfma.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form -ffinite-math-only
 
 $(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)

@@ -26,10 +26,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0       # MI355X spec (MI355X_MICROARCH.md, chip table)
 VALU_PEAK_TOPS = 78.64      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
-MFMA_I8_PEAK_TOPS = 5000.0  # dense int8 MFMA: 2x the ~2.5 PF dense BF16 rate (MI355X_MICROARCH.md, MFMA table)
-# int8 ops of the one-hot formulation per (window, strand, column): 4 bases x 1
-# coarse digit = 4 multiply-adds (scan_mfma.hip); padding (K, windows, strands)
-# and the exact rescoring of the rare candidate tiles excluded
+# dense FP4/FP6 MFMA: 4x the ~2.5 PF dense BF16 rate (MI355X_MICROARCH.md, MFMA table:
+# v_mfma_scale_f32_32x32x64_f8f6f4 with FP4/FP6 operands)
+MFMA_F6_PEAK_TOPS = 10000.0
+# ops of the one-hot formulation per (window, strand, column): 4 bases x 1 FP6
+# digit = 4 multiply-adds (scan_mfma.hip); padding (K, windows, strands) and the
+# exact rescoring of the rare candidate windows excluded
 MFMA_OPS_PER_CELL = 8
 
 
@@ -199,7 +201,7 @@ def main():
         kms = sum(kernel_ms) / len(kernel_ms)
         pattern_bytes = 0
         for p in ps.to_list():
-            pattern_bytes += ((len(p) + 7) // 8) * 1024 + 16 * len(p) + 24
+            pattern_bytes += ((len(p) + 15) // 16) * 1536 + 16 * len(p) + 24
         alg_bytes = batch.input_bytes + batch.output_bytes + pattern_bytes
         achieved = alg_bytes / (kms / 1e3) / 1e9
         traffic = None
@@ -219,11 +221,11 @@ def main():
                        "the scan is compute bound"}
         if mms > 0:  # the matrix-core kernel scored every strand of this workload
             mops = MFMA_OPS_PER_CELL * batch.num_cell_ops / (mms / 1e3) / 1e12
-            roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_I8_PEAK_TOPS, "unit": "TOPS",
-                    "frac": mops / MFMA_I8_PEAK_TOPS, "traffic": traffic,
+            roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TOPS",
+                    "frac": mops / MFMA_F6_PEAK_TOPS, "traffic": traffic,
                     "kernel": "scan_mfma_kernel<staged, K depth> (one launch per depth, 4 streams)",
                     "kernel_ms": mms,
-                    "note": "achieved = 8 int8 ops per (window, strand, column) of the one-hot x coarse-digit "
+                    "note": "achieved = 8 ops per (window, strand, column) of the FP4 one-hot x FP6 bound-digit "
                             "GEMM / the MFMA phase's HIP-event time (first launch to last, joined on the ctx "
                             "stream; tools/trace_phase.py gives the same phase from the rocprofv3 trace); "
                             "traffic = HBM bytes of the phase's dispatches from PMC"}
@@ -241,7 +243,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int8->int32" if path == "mfma" else "int32",
+            "dtype": "fp4xfp6->f32 bound + int32 exact" if path == "mfma" else "int32",
             "data": "synthetic (SURVEY.md 8d generator; no HOCOMOCO/BCF download possible)",
             "config": {
                 "workload": "C3" if (args.samples, args.pwms, args.length_config) == (50000, 600, 3) else "custom",

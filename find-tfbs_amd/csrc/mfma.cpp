@@ -1,17 +1,20 @@
-// Matrix-core plan: pack PWM strands into 32-strand tiles of int8 B fragments
+// Matrix-core plan: pack PWM strands into 32-strand tiles of FP6 B fragments
 // for scan_mfma_kernel (scan_mfma.hip).
 //
 // apply_pwm (pattern.rs:125-135) is score(i) = sum_j w[j][nuc(i + j)], N = 0.
 // With the window's bases one-hot encoded (4 entries per column, all zero for
-// N), that is a dot product of a 0/1 vector with the strand's weights.  Each
-// strand gets a scale s = ceil(max |w| / 127) (1..255) and every weight splits
-// exactly as w = s q + r, q = round(w / s) (halves away from zero) in
-// [-127, 127], |r| <= s / 2.  The kernel sums Q = sum q over a window with one
-// MFMA per 8 columns; since score = s Q + R and R <= E = sum over columns of
-// max(0, max_base r), a window can only pass `score > min_score`
-// (pattern.rs:151) when Q > thr_q = floor((min_score - E) / s).  Those
-// candidates are rescored exactly (i32 sum of the weights, kept here in
-// m_weights), so the coarse digits only ever select work.
+// N), that is a dot product of a 0/1 vector with the strand's weights.  The
+// kernel computes an upper bound of it on the matrix cores at the FP4/FP6
+// rate: per column c_j = max(0, max_base w_j), w' = w - c_j <= 0, and each w'
+// is replaced by s q with q an FP6 (e2m3) value, q >= w' / s (magnitude
+// rounded down onto the FP6 grid), s = ceil(2 max |w'| / 15) so that
+// |w'| / s <= 7.5.  Then score <= C + s Q, C = sum c_j, Q = sum q over the
+// window's non-N columns (an N column adds 0 <= c_j), and Q is an exact f32
+// sum of multiples of 1/8.  A window can hit (score > min_score,
+// pattern.rs:151) only if Q > thr = floor(8 (min_score - C) / s) / 8; those
+// candidates are rescored exactly (i32 sum of the weights, m_weights), so the
+// FP6 digits only ever select work.  Weights whose sum could wrap i32 go to
+// the LUT path (the reference wraps; the bound would not).
 #include <algorithm>
 #include <climits>
 #include <cstring>
@@ -25,48 +28,63 @@ namespace tfbs {
 namespace {
 
 struct Split {
-    int32_t scale = 1, thr_q = INT32_MAX;
-    std::vector<int8_t> q;  // len x 4 (A, C, G, T)
+    float thr = 1e9f;
+    std::vector<uint8_t> code;  // len x 4 (A, C, G, T) FP6 e2m3 codes
 };
 
 int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
 
+// The FP6 e2m3 magnitudes x 8: 0..7 (subnormal), 8..15, 16..30 step 2, 32..60 step 4
+constexpr int kF6Grid8[32] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                              16, 18, 20, 22, 24, 26, 28, 30, 32, 36, 40, 44, 48, 52, 56, 60};
+
 Split split_weights(const Pat &p) {
     Split s;
-    int32_t mx = 0;
-    for (uint32_t j = 0; j < p.len; j++)
-        for (int c = 0; c < 4; c++) mx = std::max<int32_t>(mx, std::abs(p.w5[5 * j + c]));
-    s.scale = std::max<int32_t>(1, (mx + 126) / 127);
-    s.q.resize(4 * p.len);
-    int64_t e = 0;  // the largest residual a window can add (N adds 0)
+    std::vector<int64_t> c(p.len);
+    int64_t mx = 0, cs = 0;
     for (uint32_t j = 0; j < p.len; j++) {
-        int32_t emax = 0;
-        for (int c = 0; c < 4; c++) {
-            const int32_t w = p.w5[5 * j + c], a = std::abs(w);
-            const int32_t q = (w < 0 ? -1 : 1) * ((a + s.scale / 2) / s.scale);
-            const int32_t r = w - s.scale * q;
-            s.q[4 * j + c] = (int8_t)q;
-            emax = std::max(emax, r);
-        }
-        e += emax;
+        int64_t m = 0;  // N weighs 0
+        for (int b = 0; b < 4; b++) m = std::max<int64_t>(m, p.w5[5 * j + b]);
+        c[j] = m;
+        cs += m;
+        for (int b = 0; b < 4; b++) mx = std::max<int64_t>(mx, m - p.w5[5 * j + b]);
     }
-    // |Q| <= 127 x 32, so clamping to +-2^24 changes no outcome and keeps the
-    // kernel's thr_q - Q from wrapping
-    const int64_t t = floor_div((int64_t)p.min_score - e, s.scale);
-    s.thr_q = (int32_t)std::max<int64_t>(-(1 << 24), std::min<int64_t>(1 << 24, t));
+    const int64_t scale = std::max<int64_t>(1, (2 * mx + 14) / 15);
+    s.code.resize(4 * p.len);
+    for (uint32_t j = 0; j < p.len; j++)
+        for (int b = 0; b < 4; b++) {
+            const int64_t mag8 = 8 * (c[j] - p.w5[5 * j + b]);  // 8 |w'|
+            int g = 0;  // the largest grid magnitude with s g <= |w'|
+            while (g + 1 < 32 && kF6Grid8[g + 1] * scale <= mag8) g++;
+            s.code[4 * j + b] = (uint8_t)(g ? 0x20 | g : 0);  // negative: sign bit 5; code g encodes kF6Grid8[g] / 8
+        }
+    // |Q| <= 7.5 x 32, so clamping changes no outcome
+    const int64_t t8 = floor_div(8 * ((int64_t)p.min_score - cs), scale);
+    s.thr = (float)std::max<int64_t>(-(1 << 14), std::min<int64_t>(1 << 14, t8)) / 8.0f;
     return s;
+}
+
+// FP6 bits of element e (column 4 t + base) of a lane's 192-bit B vector
+void put6(uint8_t *frag_lo, uint8_t *frag_hi, int e, uint8_t code) {
+    uint32_t bit = 6 * e;
+    for (int k = 0; k < 6; k++, bit++) {
+        if (!((code >> k) & 1)) continue;
+        uint8_t *byte = bit < 128 ? frag_lo + bit / 8 : frag_hi + (bit - 128) / 8;
+        *byte |= (uint8_t)(1u << (bit % 8));
+    }
 }
 
 }  // namespace
 
 bool mfma_eligible(const Pat &p) {
     if (p.kind != TFBS_KIND_PWM || p.len == 0 || p.len > (uint32_t)(kMMaxChunks * kMChunkCols)) return false;
-    for (uint32_t j = 0; j < p.len; j++)
-        for (int c = 0; c < 4; c++) {
-            const int64_t w = p.w5[5 * j + c];
-            if (w < -127 * kMMaxScale || w > 127 * kMMaxScale) return false;  // s <= 255
-        }
-    return true;
+    int64_t span = 0;  // the largest |sum| any window can reach: below 2^31, no i32 wrap
+    for (uint32_t j = 0; j < p.len; j++) {
+        int64_t m = 0;
+        for (int c = 0; c < 4; c++) m = std::max<int64_t>(m, std::abs((int64_t)p.w5[5 * j + c]));
+        span += m;
+    }
+    return span < INT32_MAX;
 }
 
 void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, const PlanOptions &opt, Plan *plan) {
@@ -127,7 +145,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     const auto &st = strands[t.first + n];
                     const Pat &p = P.pats[st.first];
                     const Split &sp = split[t.first + n];
-                    meta[kMetaThrQ + n] = sp.thr_q;
+                    std::memcpy(&meta[kMetaThrQ + n], &sp.thr, 4);
                     meta[kMetaMin + n] = p.min_score;
                     meta[kMetaWoff + n] = (int32_t)woff[t.first + n];
                     meta[kMetaLen + n] = (int32_t)p.len;
@@ -135,7 +153,8 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     meta[kMetaOrig + n] = st.first;
                     plan->n_mfma_strands++;
                 } else {  // padding column: never a candidate
-                    meta[kMetaThrQ + n] = 1 << 24;
+                    const float never = 1e9f;
+                    std::memcpy(&meta[kMetaThrQ + n], &never, 4);
                     meta[kMetaMin + n] = INT32_MAX;
                     meta[kMetaWoff + n] = 0;
                     meta[kMetaLen + n] = 0;
@@ -143,19 +162,22 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     meta[kMetaOrig + n] = -1;
                 }
             }
-            // B fragments: lane l holds column n = l & 31 and k = 16 h + 4 t + c,
-            // h = l >> 5, <-> strand column 8 kc + 4 h + t, base c
+            // B fragments: lane l holds column n = l & 31 and k = 32 h + 4 t + c,
+            // h = l >> 5, <-> strand column 16 kc + 8 h + t, base c: element e =
+            // 4 t + c at bits 6 e of the lane's 192 bits, dwords 0-3 at lane * 16,
+            // dwords 4-5 at 1024 + lane * 8
             for (uint32_t kc = 0; kc < nk; kc++)
                 for (int l = 0; l < 64; l++) {
                     const int n = l & 31, h = l >> 5;
                     if ((size_t)n >= t.count) continue;
                     const Pat &p = P.pats[strands[t.first + n].first];
                     const Split &sp = split[t.first + n];
-                    int8_t *fq = reinterpret_cast<int8_t *>(&img[b_off + kc * kMFragBytes + l * 16]);
-                    for (int tt = 0; tt < 4; tt++) {
-                        const uint32_t col = kc * kMChunkCols + 4 * h + tt;
+                    uint8_t *lo = &img[b_off + kc * kMFragBytes + l * 16];
+                    uint8_t *hi = &img[b_off + kc * kMFragBytes + 1024 + l * 8];
+                    for (int tt = 0; tt < 8; tt++) {
+                        const uint32_t col = kc * kMChunkCols + 8 * h + tt;
                         if (col >= p.len) continue;
-                        for (int c = 0; c < 4; c++) fq[4 * tt + c] = sp.q[4 * col + c];
+                        for (int c = 0; c < 4; c++) put6(lo, hi, 4 * tt + c, sp.code[4 * col + c]);
                     }
                 }
         }

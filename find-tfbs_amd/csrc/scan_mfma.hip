@@ -1,30 +1,29 @@
-// Matrix-core scan (gfx950 v_mfma_i32_32x32x32_i8) for strands with L <= 32
-// whose weights stay within 127 x 255 (mfma.cpp).
+// Matrix-core scan (gfx950 v_mfma_scale_f32_32x32x64_f8f6f4, FP4 x FP6) for
+// strands with L <= 32 (mfma.cpp).
 //
 // matches (pattern.rs:141-171) scores every window i of a haplotype with
 // sum_j w[j][nuc(i + j)] (N = 0, pattern.rs:119-135).  For 32 consecutive
-// windows x 32 strands that is one int8 GEMM: A[window][k] = one-hot of the
-// window's bases (all zero for N), B[k][strand] = the strand's weights.  The
-// weights split as w = s q + r (per-strand scale s, int8 q and r): a K chunk
-// of 32 covers 8 columns of the coarse digits q, so one MFMA per 8 columns
-// gives Q; Q > thr_q is necessary for a hit (mfma.cpp), and the rare tiles
-// that pass it are rescored exactly as s Q + one-hot x r.
+// windows x 32 strands that is a GEMM: A[window][k] = one-hot of the window's
+// bases (all zero for N), B[k][strand] = the strand's weights.  The kernel
+// runs it on FP6 digits q of an upper bound (score <= C + s Q, mfma.cpp) with
+// the one-hot in FP4, at the matrix cores' FP4/FP6 rate: one MFMA per 16
+// columns, exact f32 sums.  Q > thr is necessary for a hit; those candidate
+// windows are rescored exactly from the strand's integer weights.
 //
-//  * A workgroup (4 waves, 4 workgroups per CU) stages one super tile (tiles of
-//    32 strands of equal K depth: coarse and residual B fragments + strand
-//    metadata), the one-hot table and the packed words of its haplotypes in
-//    LDS.  Every B fragment is one conflict-free ds_read_b128 per lane.
+//  * A workgroup (4 waves) stages one super tile (tiles of 32 strands of equal
+//    K depth: B fragments + strand metadata), the one-hot table and the packed
+//    words of its haplotypes in LDS.  Every B fragment is one conflict-free
+//    ds_read_b128 + ds_read_b64 per lane.
 //  * Each wave takes haplotypes; per 32-window tile it builds the A fragments
-//    once (one table read per chunk) and reuses them for every strand tile of
+//    once (two table reads per chunk) and reuses them for every strand tile of
 //    the super tile, two window tiles per B fragment read.
 //  * C layout: lane l holds strand column l & 31 and windows (r & 3) + 8 (r >> 2)
 //    + 4 (l >> 5), r < 16.  A max-reduce of the 16 coarse sums against the
-//    lane's thr_q and one ballot gate the exact rescore; its max against
-//    min_score and a second ballot gate the (rare, ~1e-4 per window and
-//    strand) hit handling, which applies the inner-range overlap test
+//    lane's thr and one ballot gate the (rare) candidate handling: each firing
+//    lane queues its candidate mask in LDS; drain_queue rescores the queued
+//    windows exactly (pattern.rs:125-151), applies the inner-range overlap test
 //    (range.rs:18-21 as main.rs:503 uses it) and adds to the count of the
-//    strand's pattern_id slot atomically (counts are zeroed before the scan),
-//    so a tile may mix slots.
+//    strand's pattern_id slot atomically (counts are zeroed before the scan).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -48,18 +47,19 @@ namespace {
 
 
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kMBlock = 256;          // 4 waves
-constexpr int kMOnehotBytes = 4096;   // LDS: one-hot table, image, words
+constexpr int kMOnehotBytes = 2048;   // LDS: one-hot table (4-mer -> 4 x 16 bits of FP4), image, words
 constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup at 4 workgroups per CU (160 KiB)
-// per K depth (chunks of 8 columns): window tiles per step and the waves per
+// per K depth (chunks of 16 columns): window tiles per step and the waves per
 // SIMD the kernel is compiled for (the registers of two A sets + two
 // accumulators)
-constexpr uint32_t kMfmaWindowTiles[kMMaxChunks + 1] = {1, 2, 2, 2, 2};
+constexpr uint32_t kMfmaWindowTiles[kMMaxChunks + 1] = {1, 2, 2};
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
-constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 7, 5, 5, 4};
-constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
+constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 6, 5};
+constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4};
 
 // The packed words (and N-mask words) a lane needs for its window of the
 // 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
@@ -85,8 +85,9 @@ __device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *w
 }
 
 // A fragments of the 32-window tile at i0: chunk kc, lane half h = lane >> 5:
-// columns 8 kc + 4 h .. + 3 of the lane's window as one-hot bytes, read from
-// the LDS table by the 4-mer code; N bases zeroed in haplotypes that have them.
+// columns 16 kc + 8 h .. + 7 of the lane's window as FP4 one-hot nibbles (1.0
+// at the base's position, 16 bits per column), two 4-mer table reads; N
+// bases zeroed in haplotypes that have them.
 template <int NK>
 __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint32_t lane, const WinWords &ww,
                                              const char *s_onehot, v4i (&a)[NK]) {
@@ -95,43 +96,63 @@ __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint
     const uint32_t sh = 2 * (ic & 15);
     const uint32_t img_lo = __builtin_amdgcn_alignbit(ww.w[1], ww.w[0], sh);  // bases i .. i+15
     const uint32_t img_hi = __builtin_amdgcn_alignbit(ww.w[2], ww.w[1], sh);  // bases i+16 .. i+31
-    const uint32_t hb = 8 * (lane >> 5);
+    const uint32_t hb = 16 * (lane >> 5);
+    const uint2 *tab = reinterpret_cast<const uint2 *>(s_onehot);
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) {
-        const uint32_t code = __builtin_amdgcn_ubfe(kc < 2 ? img_lo : img_hi, 16 * (kc & 1) + hb, 8);
-        a[kc] = *reinterpret_cast<const v4i *>(s_onehot + code * 16);
+        const uint32_t img = kc == 0 ? img_lo : img_hi;
+        const uint2 x = tab[__builtin_amdgcn_ubfe(img, hb, 8)], y = tab[__builtin_amdgcn_ubfe(img, hb + 8, 8)];
+        a[kc] = v4i{(int)x.x, (int)x.y, (int)y.x, (int)y.y};
     }
     // Bases past the haplotype end need no mask: they only reach windows with
-    // i + L > len (rejected in tile_hits) or columns >= L (zero weights).
+    // i + L > len (rejected when the candidate is rescored) or columns >= L
+    // (zero weights).
     if (hm.flags & HAP_HAS_N) {  // N scores 0 (pattern.rs:119-135): clear its one-hot
         const uint32_t vm = ~__builtin_amdgcn_alignbit(ww.m[1], ww.m[0], ic & 31) >> (hb / 2);
 #pragma unroll
         for (int kc = 0; kc < NK; kc++)
 #pragma unroll
-            for (int t = 0; t < 4; t++) a[kc][t] = ((vm >> (8 * kc + t)) & 1u) ? a[kc][t] : 0;
+            for (int d = 0; d < 4; d++) {
+                const uint32_t keep = ((vm >> (16 * kc + 2 * d)) & 1u ? 0xFFFFu : 0u) |
+                                      ((vm >> (16 * kc + 2 * d + 1)) & 1u ? 0xFFFF0000u : 0u);
+                a[kc][d] &= keep;
+            }
     }
 }
 
+// B fragments of one strand tile: per chunk, the lane's 32 FP6 coarse digits
+// (192 bits) as dwords 0-3 (at lane * 16) and 4-5 (at 1024 + lane * 8).
 template <int NK>
 struct BFrag {
     v4i b[NK];
-    int32_t thr;
+    int2 c[NK];
+    float thr;
 };
 
 template <int NK>
 __device__ __forceinline__ void load_tile(const char *s_img, const DevMSuper &S, uint32_t ti, uint32_t lane,
                                           BFrag<NK> &f) {
-    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes) + lane * 16;
+    const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes);
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes);
-    f.thr = reinterpret_cast<const int32_t *>(s_img + S.meta_off + ti * kMMetaBytes)[kMetaThrQ + (lane & 31)];
+    for (int kc = 0; kc < NK; kc++) {
+        f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes + lane * 16);
+        f.c[kc] = *reinterpret_cast<const int2 *>(p + kc * kMFragBytes + 1024 + lane * 8);
+    }
+    f.thr = reinterpret_cast<const float *>(s_img + S.meta_off + ti * kMMetaBytes)[kMetaThrQ + (lane & 31)];
+}
+
+// One coarse chunk: FP4 one-hot (A) x FP6 digits (B), f32 accumulate, unit scales
+__device__ __forceinline__ v16f mfma_chunk(const v4i &a, const v4i &b, const int2 &c, const v16f &acc) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v8i{a[0], a[1], a[2], a[3], 0, 0, 0, 0},
+                                                           v8i{b[0], b[1], b[2], b[3], c.x, c.y, 0, 0}, acc,
+                                                           4 /* A: FP4 e2m1 */, 2 /* B: FP6 e2m3 */, 0, 127, 0, 127);
 }
 
 template <int NK>
-__device__ __forceinline__ v16i tile_scores(const v4i (&a)[NK], const BFrag<NK> &f) {
-    v16i acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+__device__ __forceinline__ v16f tile_scores(const v4i (&a)[NK], const BFrag<NK> &f) {
+    v16f acc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kc], f.b[kc], acc, 0, 0, 0);
+    for (int kc = 0; kc < NK; kc++) acc = mfma_chunk(a[kc], f.b[kc], f.c[kc], acc);
     return acc;
 }
 
@@ -253,18 +274,19 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
     }
 }
 
-__device__ __forceinline__ int32_t max16(const v16i &acc) {
-    int32_t m = max(max(max(acc[0], acc[1]), max(acc[2], acc[3])), max(max(acc[4], acc[5]), max(acc[6], acc[7])));
-    return max(m, max(max(max(acc[8], acc[9]), max(acc[10], acc[11])), max(max(acc[12], acc[13]), max(acc[14], acc[15]))));
+__device__ __forceinline__ float max16(const v16f &acc) {
+    float m = fmaxf(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])), fmaxf(fmaxf(acc[4], acc[5]), fmaxf(acc[6], acc[7])));
+    return fmaxf(m, fmaxf(fmaxf(fmaxf(acc[8], acc[9]), fmaxf(acc[10], acc[11])),
+                          fmaxf(fmaxf(acc[12], acc[13]), fmaxf(acc[14], acc[15]))));
 }
 
 // Coarse test of one strand tile: the max of each lane's 16 coarse sums
-// against its strand's thr_q, one ballot.  Both tiles of a pair are tested
+// against its strand's thr, one ballot.  Both tiles of a pair are tested
 // before either branches, so every read of the MFMA results sits in the
 // MFMAs' basic block, where the compiler's wait-state accounting holds (a read
 // placed after the branch of the first tile's test got too few wait states
 // and saw stale sums).
-__device__ __forceinline__ uint64_t coarse_test(const v16i &acc, int32_t thr) {
+__device__ __forceinline__ uint64_t coarse_test(const v16f &acc, float thr) {
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[3], 1ull);
 #endif
@@ -278,16 +300,16 @@ __device__ __forceinline__ uint64_t coarse_test(const v16i &acc, int32_t thr) {
 // A firing tile (fired = its coarse ballot, about one tile in nine): each
 // firing lane queues its candidate mask; qn (wave-uniform) counts the wave's
 // queued entries.
-__device__ __forceinline__ void queue_tile(const v16i &acc, int32_t thr, uint64_t fired, uint32_t ti, uint32_t hh,
+__device__ __forceinline__ void queue_tile(const v16f &acc, float thr, uint64_t fired, uint32_t ti, uint32_t hh,
                                            uint32_t i0, uint32_t lane, uint32_t wave, uint32_t &qn) {
     if (__builtin_expect(fired == 0, 1)) return;
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[4], 1ull);
     if (fired & (1ull << lane)) atomicAdd(&g_probe[0], 1ull);
 #endif
-    uint32_t m = 0;  // |acc| <= 127 x 32 and |thr| <= 2^24: no wrap
+    uint32_t m = 0;  // sign of thr - acc (both multiples of 1/8 below 2^12: exact)
 #pragma unroll
-    for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, (uint32_t)(thr - acc[r]), 31);
+    for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, __float_as_uint(thr - acc[r]), 31);
     const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, 0));
 #if TFBS_MFMA_PROBE == 8
     if (fired & (1ull << lane)) trace((1u << 24) | lane, m, at, i0);
@@ -301,17 +323,17 @@ __device__ __forceinline__ void queue_tile(const v16i &acc, int32_t thr, uint64_
 // feeds both MFMAs).
 template <int NK>
 __device__ __forceinline__ void pair_scores(const char *s_img, const DevMSuper &S, uint32_t ti, uint32_t lane,
-                                            const v4i (&a0)[NK], const v4i (&a1)[NK], v16i &c0, v16i &c1,
-                                            int32_t &thr) {
+                                            const v4i (&a0)[NK], const v4i (&a1)[NK], v16f &c0, v16f &c1,
+                                            float &thr) {
     BFrag<NK> f;
     load_tile<NK>(s_img, S, ti, lane, f);
     __builtin_amdgcn_sched_barrier(0);  // every B read of the tile issues before its MFMAs
-    c0 = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    c0 = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     c1 = c0;
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) {
-        c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[kc], f.b[kc], c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[kc], f.b[kc], c1, 0, 0, 0);
+        c0 = mfma_chunk(a0[kc], f.b[kc], f.c[kc], c0);
+        c1 = mfma_chunk(a1[kc], f.b[kc], f.c[kc], c1);
     }
     thr = f.thr;
 }
@@ -352,8 +374,8 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             for (uint32_t ti = 0;;) {
                 if (two) {
                     for (; ti < nt && qn <= kMQueue - 128; ti++) {
-                        v16i c0, c1;
-                        int32_t tc;
+                        v16f c0, c1;
+                        float tc;
                         pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
                         const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
                         queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
@@ -366,8 +388,8 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         load_tile<NK>(s_img, S, ti, lane, f0);
                         load_tile<NK>(s_img, S, ti + 1, lane, f1);
                         __builtin_amdgcn_sched_barrier(0);
-                        const v16i acc0 = tile_scores<NK>(a0, f0);
-                        const v16i acc1 = tile_scores<NK>(a0, f1);
+                        const v16f acc0 = tile_scores<NK>(a0, f0);
+                        const v16f acc1 = tile_scores<NK>(a0, f1);
                         const uint64_t g0 = coarse_test(acc0, f0.thr), g1 = coarse_test(acc1, f1.thr);
                         queue_tile(acc0, f0.thr, g0, ti, hh, i0, lane, wave, qn);
                         queue_tile(acc1, f1.thr, g1, ti + 1, hh, i0, lane, wave, qn);
@@ -376,7 +398,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         BFrag<NK> f;
                         load_tile<NK>(s_img, S, ti, lane, f);
                         __builtin_amdgcn_sched_barrier(0);
-                        const v16i acc = tile_scores<NK>(a0, f);
+                        const v16f acc = tile_scores<NK>(a0, f);
                         queue_tile(acc, f.thr, coarse_test(acc, f.thr), ti, hh, i0, lane, wave, qn);
                         ti++;
                     }
@@ -403,11 +425,14 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
         for (uint32_t i = threadIdx.x; i < S.img_bytes / 16; i += kMBlock) dst[kMOnehotBytes / 16 + i] = src[i];
-        // one-hot table: 4-mer code -> 4 dwords, base t of the code sets byte
-        // (base value) of dword t to 1
-        for (uint32_t k = threadIdx.x; k < 256; k += kMBlock)
-            dst[k] = make_uint4(1u << (8 * (k & 3)), 1u << (8 * ((k >> 2) & 3)), 1u << (8 * ((k >> 4) & 3)),
-                                1u << (8 * (k >> 6)));
+        // one-hot table: 4-mer code -> 64 bits, column t (16 bits) holds FP4
+        // 1.0 (0x2) in the nibble of its base
+        uint2 *tab = reinterpret_cast<uint2 *>(smem);
+        for (uint32_t k = threadIdx.x; k < 256; k += kMBlock) {
+            uint32_t h[4];
+            for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
+            tab[k] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+        }
     }
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hl = min(h0 + A.haps_per_block, A.n_haps) - 1;
@@ -431,12 +456,7 @@ template <int NK> MfmaKernel mfma_nk(bool staged) {
     return staged ? scan_mfma_kernel<true, NK> : scan_mfma_kernel<false, NK>;
 }
 MfmaKernel mfma_variant(bool staged, uint32_t nk) {
-    switch (nk) {
-    case 1: return mfma_nk<1>(staged);
-    case 2: return mfma_nk<2>(staged);
-    case 3: return mfma_nk<3>(staged);
-    default: return mfma_nk<4>(staged);
-    }
+    return nk == 1 ? mfma_nk<1>(staged) : mfma_nk<2>(staged);
 }
 
 }  // namespace

@@ -80,28 +80,26 @@ struct DevTile {
     uint32_t pad;
 };
 
-// Matrix-core path (scan_mfma.hip).  Each strand's weights split as
-// w = s q + r with a per-strand scale s (1..255), q = round(w / s) in
-// [-127, 127] and |r| <= s / 2.  The coarse sum Q = one-hot(window bases) x q
-// over 32 windows x 32 strands is one v_mfma_i32_32x32x32_i8 per 8 columns; a
-// window can only hit if s Q + E > min_score, E = the largest residual sum, so
-// Q > thr_q = floor((min_score - E) / s) selects the candidates, which are
-// rescored exactly from the strand's weights.  K chunk (32) = 8 columns x 4
-// bases: k = 16 h + 4 t + c <-> column 8 kc + 4 h + t, base c.
+// Matrix-core path (scan_mfma.hip).  Each strand's weights are bounded above
+// by C + s q per window (mfma.cpp): q FP6 (e2m3) digits, s a per-strand scale.
+// The coarse sum Q = one-hot(window bases, FP4) x q over 32 windows x 32
+// strands is one v_mfma_scale_f32_32x32x64_f8f6f4 per 16 columns; Q > thr
+// selects the candidate windows, which are rescored exactly from the strand's
+// weights.  K chunk (64) = 16 columns x 4 bases: k = 32 h + 4 t + c <->
+// column 16 kc + 8 h + t, base c.
 constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
-constexpr int kMChunkCols = 8;     // columns per K chunk of 32
-constexpr int kMMaxChunks = 4;     // L <= 32
-constexpr int kMMaxScale = 255;    // |w| <= 127 x 255
+constexpr int kMChunkCols = 16;    // columns per K chunk of 64
+constexpr int kMMaxChunks = 2;     // L <= 32
 constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (6 bits in a candidate entry)
-constexpr int kMFragBytes = 1024;  // one B fragment: 64 lanes x 16 bytes
-// per tile metadata, int32 x 32 each: coarse threshold, min_score, offset of
+constexpr int kMFragBytes = 1536;  // one B fragment: 64 lanes x 24 bytes (dwords 0-3 | dwords 4-5)
+// per tile metadata, 32 x 4 bytes each: coarse threshold (f32), min_score, offset of
 // the exact weights (4 per column), len, slot, pattern index
 enum MMeta { kMetaThrQ = 0, kMetaMin = 32, kMetaWoff = 64, kMetaLen = 96, kMetaSlot = 128, kMetaOrig = 160 };
 constexpr int kMMetaBytes = 768;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk KiB ([chunk][lane 64][16 bytes]),
+// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk),
 // its metadata at meta_off + t * kMMetaBytes.
 struct DevMSuper {
     uint32_t tile_count;

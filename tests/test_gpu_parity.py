@@ -156,11 +156,11 @@ def test_octet_boundaries_vs_oracle(monkeypatch, mfma):
 
 
 def test_mfma_split_edges_vs_oracle(monkeypatch):
-    """The matrix-core path's coarse/residual split (mfma.cpp): scales 1..255 (max |w| up
-    to 127 x 255, and one weight past it going to the LUT path), half-way residuals at
-    even scales, thresholds tied with / one below real window scores (the coarse bound
-    must never drop an exact hit), thresholds below every score (every tile rescored),
-    N bases (one-hot zero, residual zero)."""
+    """The matrix-core path's FP6 upper bound (mfma.cpp): weight spans from 1 to 2^20
+    (scales 1 .. ~10^5, every FP6 grid range), all-negative and all-positive columns,
+    thresholds tied with / one below real window scores (the bound must never drop an
+    exact hit), thresholds below every score (every tile fires), N bases (one-hot zero,
+    bound term c_j >= 0), and a strand whose sum could wrap i32 (LUT path)."""
     monkeypatch.setenv("TFBS_MFMA", "1")
     rnd = random.Random(11)
     base = "".join(rnd.choice("ACGT") for _ in range(600))
@@ -171,20 +171,20 @@ def test_mfma_split_edges_vs_oracle(monkeypatch):
         pats.append(T.Pattern.PWM([T.Weight(*r) for r in w4], "S%d" % len(pats), len(pats) // 2, ms,
                                   len(pats) % 2))
 
-    for L in (1, 3, 8, 9, 16, 17, 24, 25, 32):
-        for mx in (1, 2, 127, 128, 254, 1000, 4400, 127 * 254 + 1, 127 * 255):
-            w4 = [[rnd.randint(-mx, mx) for _ in range(4)] for _ in range(L)]
-            w4[rnd.randrange(L)][rnd.randrange(4)] = mx if rnd.random() < 0.5 else -mx
-            if mx % 2 == 0 and L > 1:  # exact halves of an even scale
-                s = (mx + 126) // 127
-                w4[0][1] = s // 2 * (1 if rnd.random() < 0.5 else -1)
+    for L in (1, 3, 8, 15, 16, 17, 24, 31, 32):
+        for mx in (1, 2, 7, 8, 15, 16, 127, 1000, 4400, 32385, 1 << 20):
+            kind = rnd.randrange(3)  # mixed signs, all negative, all positive
+            lo, hi = (-mx, mx) if kind == 0 else ((-mx, -1) if kind == 1 else (1, mx))
+            if lo > hi:
+                lo, hi = hi, lo
+            w4 = [[rnd.randint(lo, hi) for _ in range(4)] for _ in range(L)]
             sc = sorted(_scores(w4, base))
             top = sc[-1 - rnd.randint(0, 3)] if sc else 0
             add(w4, top)
             add(w4, top - 1)
-            if mx in (4400, 127 * 255):
+            if mx in (4400, 1 << 20):
                 add(w4, sc[0] - 1 if sc else -1)  # every window hits
-    w4 = [[127 * 255 + 1, 0, -5, 7]] + [[rnd.randint(-100, 100) for _ in range(4)] for _ in range(7)]
+    w4 = [[2**30, 0, -5, 7]] * 2 + [[rnd.randint(-100, 100) for _ in range(4)] for _ in range(6)]
     pats.append(T.Pattern.PWM([T.Weight(*r) for r in w4], "LUT", 9999, sorted(_scores(w4, base))[-2], 0))
     st = T.PatternSet.from_patterns(pats).plan_stats(mfma=True)
     assert st["n_mfma_strands"] == len(pats) - 1, st

@@ -12,7 +12,7 @@ for spec in "$@"; do
   [ -z "$n" ] && n=$name
   d=find-tfbs_amd/lib/probe$name
   mkdir -p $d
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form \
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -mllvm -amdgpu-mfma-vgpr-form -ffinite-math-only \
     -DTFBS_MFMA_PROBE=$n $extra -x hip -c find-tfbs_amd/csrc/scan_mfma.hip -o $d/scan_mfma.o
   objs=$(ls find-tfbs_amd/lib/obj/*.o | grep -v scan_mfma.o)
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libtfbs_amd.so $objs $d/scan_mfma.o -lz -lpthread
