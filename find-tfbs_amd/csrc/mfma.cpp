@@ -101,6 +101,8 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         woff[s] = (uint32_t)plan->m_weights.size();
         for (uint32_t j = 0; j < p.len; j++)
             for (int c = 0; c < 4; c++) plan->m_weights.push_back(p.w5[5 * j + c]);
+        // zero columns up to a multiple of 8: the rescoring loop reads whole blocks
+        plan->m_weights.resize(plan->m_weights.size() + 4 * ((8 - p.len % 8) % 8), 0);
     }
 
     struct TileSrc { size_t first, count; uint32_t nk, lmin; };

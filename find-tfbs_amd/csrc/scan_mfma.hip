@@ -40,7 +40,8 @@ namespace {
 // TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live; timing only),
 // =2 reads every B fragment from tile 0 (results wrong; timing only), =4 counts
 // tiles, firing tiles, candidate lanes, exact hits and rejected candidates
-// (printed per launch).
+// (printed per launch), =11 never queues candidates, =12 never drains the
+// queue (11, 12: results wrong; timing only).
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
@@ -197,7 +198,9 @@ __device__ __forceinline__ void trace(uint32_t a, uint32_t b, uint32_t c, uint32
 }
 #endif
 
-// Exact score of window i of haplotype hp for a strand of length L (i + L <= len)
+// Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
+// whole blocks of 8 columns (the weights are zero-padded to them), one load per
+// column, N columns masked out.
 __device__ __forceinline__ int32_t exact_score(const ScanArgs &A, const uint32_t *words, const DevHap &hp, uint32_t i,
                                                uint32_t L, uint32_t woff) {
     const uint32_t *w = words + hp.word_off + (i >> 4);
@@ -211,66 +214,91 @@ __device__ __forceinline__ int32_t exact_score(const ScanArgs &A, const uint32_t
     const int32_t *wt = A.mweights + woff;
     int32_t s = 0;
 #pragma unroll 1
-    for (uint32_t j = 0; j < L; j += 4) {  // four independent loads per round, few registers
-        int32_t v[4];
+    for (uint32_t jb = 0; jb < L; jb += 8) {
+        int32_t v[8];
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-            const uint32_t jj = j + u, c = (img[jj >> 4] >> (2 * (jj & 15))) & 3u;
-            const int32_t x = wt[4 * min(jj, L - 1) + c];                  // in bounds even past L
-            v[u] = (jj < L && ((live >> jj) & 1u)) ? x : 0;                 // N scores 0
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t j = jb + u;
+            v[u] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
         }
-        s += (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) s += v[u] & -(int32_t)((live >> (jb + u)) & 1u);  // N scores 0
     }
     return s;
 }
 
-// Drains the wave's first n queue entries (all lanes; one entry per lane per
-// round).  h0: the workgroup's first haplotype; meta0: tile 0's metadata.
-__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
-                                            uint32_t h0, uint32_t n, uint32_t wave) {
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t e = lane; e < n; e += 64) {
-        const uint64_t q = s_queue[wave][e];
-        uint32_t m = (uint32_t)q & 0xFFFFu;
-        const uint32_t src = ((uint32_t)q >> 16) & 63u, ti = ((uint32_t)q >> 22) & 63u;
-        const uint32_t hap = h0 + ((uint32_t)(q >> 32) & 255u), i0 = (uint32_t)(q >> 40) << 5;
-        const uint32_t col = src & 31u, h = src >> 5;
-        const int32_t *meta = meta0 + ti * (kMMetaBytes / 4);
-        const uint32_t L = (uint32_t)meta[kMetaLen + col], woff = (uint32_t)meta[kMetaWoff + col];
-        const int32_t mn = meta[kMetaMin + col];
-        const DevHap hp = A.haps[hap];
-        const DevRegion rg = A.regions[hp.region];
-        const uint32_t off0 = (uint32_t)meta[kMetaSlot + col] * rg.n_inner;
-        const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-        while (m) {
-            const uint32_t b = 31 - __builtin_clz(m & -m);  // lowest set bit
-            m &= m - 1;
-            const uint32_t r = 15 - b;
-            const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (i + L > hp.len) continue;                   // past the end (pattern.rs:147-150)
-            const int32_t sc = exact_score(A, words, hp, i, L, woff);
-#if TFBS_MFMA_PROBE == 7
-            printf("D e %u src %u i %u L %u sc %d mn %d\n", e, src, i, L, sc, mn);
+// One queue entry: each candidate window of the lane's mask is rescored
+// exactly; hits add to their slot's count for every inner range they overlap.
+__device__ __forceinline__ void drain_entry(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+                                            uint32_t h0, uint64_t q) {
+    uint32_t m = (uint32_t)q & 0xFFFFu;
+    const uint32_t src = ((uint32_t)q >> 16) & 63u, ti = ((uint32_t)q >> 22) & 63u;
+    const uint32_t hap = h0 + ((uint32_t)(q >> 32) & 255u), i0 = (uint32_t)(q >> 40) << 5;
+    const uint32_t col = src & 31u, h = src >> 5;
+    const int32_t *meta = meta0 + ti * (kMMetaBytes / 4);
+    const uint32_t L = (uint32_t)meta[kMetaLen + col], woff = (uint32_t)meta[kMetaWoff + col];
+    const int32_t mn = meta[kMetaMin + col];
+    const DevHap hp = A.haps[hap];
+    const DevRegion rg = A.regions[hp.region];
+    const uint32_t off0 = (uint32_t)meta[kMetaSlot + col] * rg.n_inner;
+    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+    while (m) {
+        const uint32_t b = 31 - __builtin_clz(m & -m);  // lowest set bit
+        m &= m - 1;
+        const uint32_t r = 15 - b;
+        const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (i + L > hp.len) continue;                   // past the end (pattern.rs:147-150)
+        const int32_t sc = exact_score(A, words, hp, i, L, woff);
+#if TFBS_MFMA_PROBE == 4
+        atomicAdd(&g_probe[sc > mn ? 1 : 2], 1ull);
 #endif
 #if TFBS_MFMA_PROBE == 8
-            trace((2u << 24) | src, i, e, (uint32_t)sc);
+        trace((2u << 24) | src, i, 0, (uint32_t)sc);
 #endif
-#if TFBS_MFMA_PROBE == 4
-            atomicAdd(&g_probe[sc > mn ? 1 : 2], 1ull);
-#endif
-            if (!(sc > mn)) continue;                       // strict (pattern.rs:151)
-            const int32_t p = (hp.flags & HAP_HAS_POS) ? A.posrel[hp.pos_off + i] : (int32_t)i;
-            for (uint32_t k = 0; k < rg.n_inner; k++) {     // range.rs:18-21 as main.rs:503 uses it
-                const int32_t s = inner[2 * k], en = inner[2 * k + 1];
-                const uint32_t span = (uint32_t)(en - s);
-                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-                    atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
-            }
-            if (A.hits && i / 64 < A.hits_wpp)
-                atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kMetaOrig + col]) * A.hits_wpp +
-                             i / 64,
-                         1ull << (i & 63));
+        if (!(sc > mn)) continue;                       // strict (pattern.rs:151)
+        const int32_t p = (hp.flags & HAP_HAS_POS) ? A.posrel[hp.pos_off + i] : (int32_t)i;
+        for (uint32_t k = 0; k < rg.n_inner; k++) {     // range.rs:18-21 as main.rs:503 uses it
+            const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+            const uint32_t span = (uint32_t)(en - s);
+            if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
+                atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
         }
+        if (A.hits && i / 64 < A.hits_wpp)
+            atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kMetaOrig + col]) * A.hits_wpp +
+                         i / 64,
+                     1ull << (i & 63));
+    }
+}
+
+// Drains the wave's first n queue entries (one entry per lane per round).
+// h0: the workgroup's first haplotype; meta0: tile 0's metadata.
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+                                            uint32_t h0, uint32_t n, uint32_t wave) {
+#if TFBS_MFMA_PROBE == 12
+    return;  // timing only: queued candidates are dropped
+#endif
+    for (uint32_t e = threadIdx.x & 63; e < n; e += 64) drain_entry(A, words, meta0, h0, s_queue[wave][e]);
+}
+
+__shared__ uint32_t s_qn[kMBlock / 64];
+
+// Drains every wave's queue (entries s_queue[w][0, s_qn[w])) with the whole
+// workgroup, one entry per thread per round.
+__device__ __forceinline__ void drain_pooled(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+                                             uint32_t h0) {
+#if TFBS_MFMA_PROBE == 12
+    return;
+#endif
+    constexpr uint32_t kWaves = kMBlock / 64;
+    uint32_t off[kWaves + 1];
+    off[0] = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kWaves; w++) off[w + 1] = off[w] + s_qn[w];
+    for (uint32_t g = threadIdx.x; g < off[kWaves]; g += kMBlock) {
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t k = 1; k < kWaves; k++) w += g >= off[k];
+        drain_entry(A, words, meta0, h0, s_queue[w][g - off[w]]);
     }
 }
 
@@ -310,6 +338,9 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, float thr, uint64_t 
     uint32_t m = 0;  // sign of thr - acc (both multiples of 1/8 below 2^12: exact)
 #pragma unroll
     for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, __float_as_uint(thr - acc[r]), 31);
+#if TFBS_MFMA_PROBE == 11
+    return;  // timing only: no candidate is queued
+#endif
     const uint32_t at = qn + __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, 0));
 #if TFBS_MFMA_PROBE == 8
     if (fired & (1ull << lane)) trace((1u << 24) | lane, m, at, i0);
@@ -409,7 +440,10 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             }
         }
     }
-    if (qn) drain_queue(A, words, meta0, h0, qn, wave);
+    // the waves' last entries, pooled: every wave drains a share of the sum
+    if (lane == 0) s_qn[wave] = qn;
+    __syncthreads();
+    drain_pooled(A, words, meta0, h0);
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD.
