@@ -8,7 +8,8 @@ import sys
 
 out = {}
 root = sys.argv[1]
-for f in glob.glob(os.path.join(root, "*", "pmc_counter_collection.csv")):
+for f in glob.glob(os.path.join(root, "pmc_counter_collection.csv")) + glob.glob(
+        os.path.join(root, "*", "pmc_counter_collection.csv")):
     rows = list(csv.DictReader(open(f)))
     # the last scan step: the last run of consecutive scan dispatches (one per
     # K depth for the MFMA path), counters summed over its dispatches

@@ -20,12 +20,13 @@ def main():
     root = sys.argv[1]
     regions = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
     path = sys.argv[3] if len(sys.argv) > 3 else "mfma"
-    s = json.load(open(os.path.join(root, "pmc_summary.json")))
+    s = json.load(open(os.path.join(root, "sum_pmc_fetch.json")))
+    s.update(json.load(open(os.path.join(root, "sum_pmc_write.json"))))
     fetch, write = s["FETCH_SIZE"] * 1024, s["WRITE_SIZE"] * 1024
     out = {"workload": "C3", "regions": regions, "scan_path": path, "kernel": s.get("_kernel"),
            "fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
            "fetch_bytes_x2_corrected": 2 * fetch,
-           "source": os.path.join(root, "pmc_summary.json") + " (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
+           "source": os.path.join(root, "sum_pmc_{fetch,write}.json") + " (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
                      "separate passes, last scan dispatch)"}
     dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
     json.dump(out, open(dst, "w"), indent=1)
