@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "patterns.hpp"
@@ -29,6 +30,7 @@ namespace {
 
 struct Split {
     float thr = 1e9f;
+    int64_t t8 = 0;
     std::vector<uint8_t> code;  // len x 4 (A, C, G, T) FP6 e2m3 codes
 };
 
@@ -38,18 +40,10 @@ int64_t floor_div(int64_t a, int64_t b) { return a >= 0 ? a / b : -((-a + b - 1)
 constexpr int kF6Grid8[32] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
                               16, 18, 20, 22, 24, 26, 28, 30, 32, 36, 40, 44, 48, 52, 56, 60};
 
-Split split_weights(const Pat &p) {
+// Digits and threshold of the bound for one scale.  Magnitudes beyond the
+// grid clip to 7.5 (still q >= w' / s: the bound only loosens).
+Split split_at(const Pat &p, const std::vector<int64_t> &c, int64_t cs, int64_t scale) {
     Split s;
-    std::vector<int64_t> c(p.len);
-    int64_t mx = 0, cs = 0;
-    for (uint32_t j = 0; j < p.len; j++) {
-        int64_t m = 0;  // N weighs 0
-        for (int b = 0; b < 4; b++) m = std::max<int64_t>(m, p.w5[5 * j + b]);
-        c[j] = m;
-        cs += m;
-        for (int b = 0; b < 4; b++) mx = std::max<int64_t>(mx, m - p.w5[5 * j + b]);
-    }
-    const int64_t scale = std::max<int64_t>(1, (2 * mx + 14) / 15);
     s.code.resize(4 * p.len);
     for (uint32_t j = 0; j < p.len; j++)
         for (int b = 0; b < 4; b++) {
@@ -60,8 +54,57 @@ Split split_weights(const Pat &p) {
         }
     // |Q| <= 7.5 x 32, so clamping changes no outcome
     const int64_t t8 = floor_div(8 * ((int64_t)p.min_score - cs), scale);
-    s.thr = (float)std::max<int64_t>(-(1 << 14), std::min<int64_t>(1 << 14, t8)) / 8.0f;
+    s.t8 = std::max<int64_t>(-(1 << 14), std::min<int64_t>(1 << 14, t8));
+    s.thr = (float)s.t8 / 8.0f;
     return s;
+}
+
+// P(a window is a candidate) under uniform bases: the distribution of
+// G = -8 Q = sum of the columns' grid magnitudes x 8, by convolution.
+double candidate_rate(const Pat &p, const Split &s) {
+    std::vector<double> d(1, 1.0), e;
+    for (uint32_t j = 0; j < p.len; j++) {
+        e.assign(d.size() + 60, 0.0);
+        for (int b = 0; b < 4; b++) {
+            const int g8 = kF6Grid8[s.code[4 * j + b] & 31];
+            for (size_t x = 0; x < d.size(); x++) e[x + g8] += 0.25 * d[x];
+        }
+        d.swap(e);
+    }
+    // candidate iff Q8 = -G > t8, i.e. G < -t8
+    double r = 0;
+    for (size_t x = 0; x < d.size() && (int64_t)x < -s.t8; x++) r += d[x];
+    return r;
+}
+
+// The bound's scale: s0 = ceil(2 max|w'| / 15) keeps every digit on the grid;
+// smaller scales resolve the small |w'| (the near-best bases that decide the
+// windows near the threshold) more finely and clip the large ones.  The scale
+// with the fewest candidates under uniform bases is kept.
+Split split_weights(const Pat &p) {
+    std::vector<int64_t> c(p.len);
+    int64_t mx = 0, cs = 0;
+    for (uint32_t j = 0; j < p.len; j++) {
+        int64_t m = 0;  // N weighs 0
+        for (int b = 0; b < 4; b++) m = std::max<int64_t>(m, p.w5[5 * j + b]);
+        c[j] = m;
+        cs += m;
+        for (int b = 0; b < 4; b++) mx = std::max<int64_t>(mx, m - p.w5[5 * j + b]);
+    }
+    const int64_t s0 = std::max<int64_t>(1, (2 * mx + 14) / 15);
+    Split best = split_at(p, c, cs, s0);
+    double best_rate = candidate_rate(p, best);
+    for (const double f : {0.85, 0.72, 0.6, 0.5, 0.42, 0.35, 0.3, 0.25}) {
+        const int64_t sc = std::max<int64_t>(1, (int64_t)(s0 * f));
+        if (sc == s0) continue;
+        Split t = split_at(p, c, cs, sc);
+        const double r = candidate_rate(p, t);
+        if (r < best_rate) {
+            best_rate = r;
+            best = std::move(t);
+        }
+    }
+    return best;
 }
 
 // FP6 bits of element e (column 4 t + base) of a lane's 192-bit B vector
@@ -95,9 +138,17 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
     if (strands.empty()) return;
     std::vector<Split> split(strands.size());
     std::vector<uint32_t> woff(strands.size());
+    {  // the scale search convolves score distributions: spread strands over threads
+        const size_t nt = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+        std::vector<std::thread> pool;
+        for (size_t t = 0; t < nt; t++)
+            pool.emplace_back([&, t] {
+                for (size_t s = t; s < strands.size(); s += nt) split[s] = split_weights(P.pats[strands[s].first]);
+            });
+        for (auto &th : pool) th.join();
+    }
     for (size_t s = 0; s < strands.size(); s++) {
         const Pat &p = P.pats[strands[s].first];
-        split[s] = split_weights(p);
         woff[s] = (uint32_t)plan->m_weights.size();
         for (uint32_t j = 0; j < p.len; j++)
             for (int c = 0; c < 4; c++) plan->m_weights.push_back(p.w5[5 * j + c]);
