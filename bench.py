@@ -55,6 +55,13 @@ def parse():
     return ap.parse_args()
 
 
+def workload_name(args):
+    """BASELINE.json configs: C2 = 1 k samples x 10 PWMs (lengths 8-15), C3 = 50 k x 600
+    PWMs per GPU (C4 is C3 sharded over 8 GPUs), C5 = C3 with 30 % indels and PWMs of length 25-30."""
+    key = (args.samples, args.pwms, args.length_config, args.indel_pct)
+    return {(1000, 10, 2, 0): "C2", (50000, 600, 3, 0): "C3", (50000, 600, 5, 30): "C5"}.get(key, "custom")
+
+
 def cpu_baseline(T, ps, args, budget_s):
     """The oracle (C restatement of the reference algorithm) on host threads over a
     bounded sample of the same workload's regions, 50-region chunks per worker as
@@ -246,7 +253,7 @@ def main():
             "dtype": "fp4xfp6->f32 bound + int32 exact" if path == "mfma" else "int32",
             "data": "synthetic (SURVEY.md 8d generator; no HOCOMOCO/BCF download possible)",
             "config": {
-                "workload": "C3" if (args.samples, args.pwms, args.length_config) == (50000, 600, 3) else "custom",
+                "workload": workload_name(args),
                 "samples": args.samples, "haplotypes": 2 * args.samples, "regions_per_gpu": args.regions,
                 "region_bp": 201, "pwms": args.pwms, "patterns": len(ps), "threshold": args.threshold,
                 "indel_pct": args.indel_pct, "distinct_haplotypes_per_gpu": batch.num_haplotypes,
