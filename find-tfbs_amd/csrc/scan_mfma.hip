@@ -50,6 +50,7 @@ namespace {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
+typedef float v2f __attribute__((ext_vector_type(2)));
 
 constexpr int kMBlock = 256;          // 4 waves
 constexpr int kMOnehotBytes = 2048;   // LDS: one-hot table (4-mer -> 4 x 16 bits of FP4), image, words
@@ -302,10 +303,13 @@ __device__ __forceinline__ void drain_pooled(const ScanArgs &A, const uint32_t *
     }
 }
 
-__device__ __forceinline__ float max16(const v16f &acc) {
-    float m = fmaxf(fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])), fmaxf(fmaxf(acc[4], acc[5]), fmaxf(acc[6], acc[7])));
-    return fmaxf(m, fmaxf(fmaxf(fmaxf(acc[8], acc[9]), fmaxf(acc[10], acc[11])),
-                          fmaxf(fmaxf(acc[12], acc[13]), fmaxf(acc[14], acc[15]))));
+// The max of a lane's 16 sums: 7 v_max3 + 1 v_max (a balanced pairwise tree
+// takes 10)
+__device__ __forceinline__ float max16(const v16f &a) {
+    const float t0 = fmaxf(fmaxf(a[0], a[1]), a[2]), t1 = fmaxf(fmaxf(a[3], a[4]), a[5]);
+    const float t2 = fmaxf(fmaxf(a[6], a[7]), a[8]), t3 = fmaxf(fmaxf(a[9], a[10]), a[11]);
+    const float t4 = fmaxf(fmaxf(a[12], a[13]), a[14]);
+    return fmaxf(fmaxf(fmaxf(t0, t1), t2), fmaxf(fmaxf(t3, t4), a[15]));
 }
 
 // Coarse test of one strand tile: the max of each lane's 16 coarse sums
@@ -335,9 +339,14 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, float thr, uint64_t 
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[4], 1ull);
     if (fired & (1ull << lane)) atomicAdd(&g_probe[0], 1ull);
 #endif
-    uint32_t m = 0;  // sign of thr - acc (both multiples of 1/8 below 2^12: exact)
+    uint32_t m = 0;  // sign of thr - acc (both multiples of 1/8 below 2^12: exact), packed subtracts
+    const v2f t2 = {thr, thr};
 #pragma unroll
-    for (int r = 0; r < 16; r++) m = __builtin_amdgcn_alignbit(m, __float_as_uint(thr - acc[r]), 31);
+    for (int r = 0; r < 16; r += 2) {
+        const v2f d = t2 - v2f{acc[r], acc[r + 1]};
+        m = __builtin_amdgcn_alignbit(m, __float_as_uint(d[0]), 31);
+        m = __builtin_amdgcn_alignbit(m, __float_as_uint(d[1]), 31);
+    }
 #if TFBS_MFMA_PROBE == 11
     return;  // timing only: no candidate is queued
 #endif
@@ -366,6 +375,9 @@ __device__ __forceinline__ void pair_scores(const char *s_img, const DevMSuper &
         c0 = mfma_chunk(a0[kc], f.b[kc], f.c[kc], c0);
         c1 = mfma_chunk(a1[kc], f.b[kc], f.c[kc], c1);
     }
+    // both tiles' MFMAs issue before either test reads a result (the first
+    // test then runs under the second tile's MFMA)
+    __builtin_amdgcn_sched_barrier(0);
     thr = f.thr;
 }
 
