@@ -147,6 +147,14 @@ class PatternSet:
     def max_length(self):
         return lib().tfbs_patterns_max_length(self.h)
 
+    def mfma_bound(self, i, window):
+        """The matrix-core bound of pattern i on one window ("ACGTN" string of the pattern's
+        length): dict(eligible, q8, t8, scale, c); bound = c + scale * q8 / 8, candidate iff q8 > t8."""
+        codes = (C.c_uint8 * max(1, len(window)))(*["ACGTN".index(ch) for ch in window])
+        out = _capi.tfbs_mfma_bound()
+        check(lib().tfbs_patterns_mfma_bound(self.h, i, codes, C.byref(out)))
+        return {n: getattr(out, n) for n, _ in out._fields_}
+
     def plan_stats(self, tile_blocks=20, mfma=False):
         """Host-side summary of the device plan (octet/quad/generic/MFMA strands, tiles)."""
         st = _capi.tfbs_plan_stats()

@@ -38,6 +38,11 @@ class tfbs_plan_stats(C.Structure):
         [(n, C.c_uint32) for n in ("n_mfma_strands", "n_mfma_tiles", "n_mfma_supers")]
 
 
+class tfbs_mfma_bound(C.Structure):
+    _fields_ = [("eligible", C.c_int32), ("q8", C.c_int64), ("t8", C.c_int64), ("scale", C.c_int64),
+                ("c", C.c_int64)]
+
+
 class tfbs_run_args(C.Structure):
     _fields_ = [
         ("chromosome", C.c_char_p), ("bcf", C.c_char_p), ("bed_files", C.c_char_p), ("reference", C.c_char_p),
@@ -61,6 +66,7 @@ SIGNATURES = [
     ("tfbs_patterns_max_length", C.c_uint32, [vp]),
     ("tfbs_patterns_destroy", None, [vp]),
     ("tfbs_patterns_plan_stats", C.c_int, [vp, C.c_uint32, C.c_int, C.POINTER(tfbs_plan_stats)]),
+    ("tfbs_patterns_mfma_bound", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_uint8), C.POINTER(tfbs_mfma_bound)]),
     ("tfbs_parse_weight", C.c_int, [C.c_char_p, i32p]),
     ("tfbs_parse_threshold_file", C.c_int, [C.c_char_p, C.c_float, i32p]),
     ("tfbs_device_count", C.c_int, [C.POINTER(C.c_int)]),

@@ -30,7 +30,7 @@ namespace {
 
 struct Split {
     float thr = 1e9f;
-    int64_t t8 = 0;
+    int64_t t8 = 0, scale = 1, c = 0;
     std::vector<uint8_t> code;  // len x 4 (A, C, G, T) FP6 e2m3 codes
 };
 
@@ -56,6 +56,8 @@ Split split_at(const Pat &p, const std::vector<int64_t> &c, int64_t cs, int64_t 
     const int64_t t8 = floor_div(8 * ((int64_t)p.min_score - cs), scale);
     s.t8 = std::max<int64_t>(-(1 << 14), std::min<int64_t>(1 << 14, t8));
     s.thr = (float)s.t8 / 8.0f;
+    s.scale = scale;
+    s.c = cs;
     return s;
 }
 
@@ -118,6 +120,17 @@ void put6(uint8_t *frag_lo, uint8_t *frag_hi, int e, uint8_t code) {
 }
 
 }  // namespace
+
+void mfma_window_bound(const Pat &p, const uint8_t *bases, int64_t *q8, int64_t *t8, int64_t *scale, int64_t *c) {
+    const Split s = split_weights(p);
+    int64_t g = 0;
+    for (uint32_t j = 0; j < p.len; j++)
+        if (bases[j] < 4) g += kF6Grid8[s.code[4 * j + bases[j]] & 31];  // an N column adds 0
+    *q8 = -g;
+    *t8 = s.t8;
+    *scale = s.scale;
+    *c = s.c;
+}
 
 bool mfma_eligible(const Pat &p) {
     if (p.kind != TFBS_KIND_PWM || p.len == 0 || p.len > (uint32_t)(kMMaxChunks * kMChunkCols)) return false;

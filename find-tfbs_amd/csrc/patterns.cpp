@@ -434,6 +434,20 @@ int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, int m
     return TFBS_OK;
 }
 
+int tfbs_patterns_mfma_bound(const tfbs_patterns *p, size_t i, const uint8_t *bases, tfbs_mfma_bound *out) {
+    if (!p || !out || (!bases && i < p->p.pats.size() && p->p.pats[i].len))
+        return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (i >= p->p.pats.size()) return tfbs::fail(TFBS_E_ARG, "pattern index out of range");
+    const tfbs::Pat &pat = p->p.pats[i];
+    *out = tfbs_mfma_bound{};
+    for (uint32_t j = 0; j < pat.len; j++)
+        if (bases[j] > 4) return tfbs::fail(TFBS_E_ARG, "base code above 4");
+    if (!tfbs::mfma_eligible(pat)) return TFBS_OK;
+    out->eligible = 1;
+    tfbs::mfma_window_bound(pat, bases, &out->q8, &out->t8, &out->scale, &out->c);
+    return TFBS_OK;
+}
+
 }  // extern "C"
 
 namespace tfbs {

@@ -65,6 +65,8 @@ void build_fast_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, u
 // Strands the int8 one-hot formulation scores exactly (L <= 32, every weight
 // splits as 64 a + b with a, b int8).
 bool mfma_eligible(const Pat &p);
+// The bound of one window (bases 0-4, 4 = N): 8 Q, t8, scale, C (mfma.cpp)
+void mfma_window_bound(const Pat &p, const uint8_t *bases, int64_t *q8, int64_t *t8, int64_t *scale, int64_t *c);
 void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, const PlanOptions &opt, Plan *plan);
 
 int parse_weight(const std::string &s, int32_t *out);

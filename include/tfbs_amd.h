@@ -94,7 +94,7 @@ void tfbs_patterns_destroy(tfbs_patterns *p);
 /* Host-only diagnostics of the device plan the scan would use with tiles of
  * tile_blocks 4 KiB table blocks (and, if mfma, the matrix-core path): strands
  * on the 16-bit octet path, the 32-bit quad path, the generic (L > 32) kernel
- * and the int8 MFMA path, and their tiles. */
+ * and the FP4 x FP6 MFMA path, and their tiles. */
 typedef struct tfbs_plan_stats {
     uint32_t n_octet_strands, n_quad_strands, n_generic_strands;
     uint32_t n_fast_tiles, n_fast_units, n_generic_tiles, max_tile_blocks;
@@ -102,6 +102,18 @@ typedef struct tfbs_plan_stats {
     uint32_t n_mfma_strands, n_mfma_tiles, n_mfma_supers;
 } tfbs_plan_stats;
 int tfbs_patterns_plan_stats(const tfbs_patterns *p, uint32_t tile_blocks, int mfma, tfbs_plan_stats *out);
+/* Host-only diagnostic of the matrix-core bound (mfma.cpp) for pattern i and
+ * one window of pattern_length bases (0-3 = A,C,G,T, 4 = N): the window's
+ * bound digit sum q8 = 8 Q, the strand's threshold t8, its scale and column
+ * offset c.  The bound is c + scale * q8 / 8 >= apply_pwm (pattern.rs:125-135);
+ * the window is a candidate iff q8 > t8, which every window with
+ * score > min_score (pattern.rs:151) is.  eligible = 0: the pattern is scored
+ * by the LUT kernels instead (the other fields are 0). */
+typedef struct tfbs_mfma_bound {
+    int32_t eligible;
+    int64_t q8, t8, scale, c;
+} tfbs_mfma_bound;
+int tfbs_patterns_mfma_bound(const tfbs_patterns *p, size_t i, const uint8_t *bases, tfbs_mfma_bound *out);
 
 /* pattern.rs:13-16 parse_weight: (f32(s) * 1000f32).round() as i32. */
 int tfbs_parse_weight(const char *s, int32_t *out);

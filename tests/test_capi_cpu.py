@@ -198,3 +198,54 @@ def test_batch_grouping_beyond_64_distinct_diffs(tmp_path):
     for i, (nh, nv, _) in enumerate(stats):
         assert b.region_stats(i) == (nh, nv)
     assert max(s[1] for s in stats) > 64
+
+
+def _window_score(w4, window):
+    """apply_pwm (pattern.rs:125-135): i32 sum, N = 0."""
+    return sum(w4[j]["ACGT".index(ch)] for j, ch in enumerate(window) if ch != "N")
+
+
+def test_mfma_bound_is_sound():
+    """The FP6 bound the matrix-core scan filters with (mfma.cpp): for random patterns
+    (weight spans 1 .. 2^20, mixed / all-negative / all-positive columns, thresholds at,
+    below and above real scores) and random windows with N, 8 * score <= 8 c + scale * q8,
+    and every window with score > min_score (pattern.rs:151) is a candidate (q8 > t8)."""
+    rnd = random.Random(21)
+    checked = hits = 0
+    for trial in range(160):
+        L = rnd.choice([1, 2, 5, 8, 9, 15, 16, 17, 24, 31, 32])
+        mx = rnd.choice([1, 3, 8, 100, 1000, 4400, 32385, 1 << 20])
+        kind = trial % 3
+        lo, hi = (-mx, mx) if kind == 0 else ((-mx, -1) if kind == 1 else (1, mx))
+        if lo > hi:
+            lo, hi = hi, lo
+        w4 = [[rnd.randint(lo, hi) for _ in range(4)] for _ in range(L)]
+        windows = ["".join(rnd.choice("ACGT" if t % 4 else "ACGTN") for _ in range(L)) for t in range(60)]
+        best = "".join("ACGT"[max(range(4), key=lambda b: w4[j][b])] for j in range(L))
+        windows.append(best)
+        scores = sorted(_window_score(w4, x) for x in windows)
+        ms = rnd.choice([scores[-1], scores[-1] - 1, scores[len(scores) // 2], scores[0] - 1, scores[-1] + 5])
+        ps = T.PatternSet.from_patterns([T.Pattern.PWM([T.Weight(*r) for r in w4], "B", 1, ms)])
+        for x in windows:
+            b = ps.mfma_bound(0, x)
+            assert b["eligible"] == 1
+            sc = _window_score(w4, x)
+            assert 8 * sc <= 8 * b["c"] + b["scale"] * b["q8"], (trial, x, sc, b)
+            if sc > ms:
+                hits += 1
+                assert b["q8"] > b["t8"], (trial, x, sc, ms, b)
+            checked += 1
+    assert checked > 9000 and hits > 100
+
+
+def test_mfma_bound_eligibility():
+    """Strands whose window sums could wrap i32 (the reference wraps, pattern.rs:125-135)
+    and strands longer than 32 stay off the matrix-core path."""
+    wrap = [T.Weight(2**30, 0, 0, 0)] * 2
+    ok = [T.Weight(2**29, 0, 0, 0)] * 3
+    long_ = [T.Weight(1, 0, 0, 0)] * 33
+    ps = T.PatternSet.from_patterns([T.Pattern.PWM(wrap, "w", 1, 0), T.Pattern.PWM(ok, "o", 2, 0),
+                                     T.Pattern.PWM(long_, "l", 3, 0)])
+    assert ps.mfma_bound(0, "AA")["eligible"] == 0
+    assert ps.mfma_bound(1, "AAA")["eligible"] == 1
+    assert ps.mfma_bound(2, "A" * 33)["eligible"] == 0
