@@ -312,6 +312,20 @@ def test_synthetic_regions_vs_oracle(tmp_path, monkeypatch, config, indel, n_sam
     assert b.num_haplotypes > n_regions
 
 
+@pytest.mark.parametrize("thr", [0.5, 0.05])
+def test_dense_hits_vs_oracle(tmp_path, monkeypatch, thr):
+    """Loose thresholds (p 0.5 / 0.05: most / many windows hit) through the count path:
+    the matrix-core kernel's candidate queues fill and drain mid-haplotype many times, and
+    the workgroup's pooled final drain carries hundreds of entries per wave."""
+    monkeypatch.setenv("TFBS_MFMA", "1")
+    ps, _ = synth_patterns(tmp_path, 6, 3, 61, thr=thr)
+    n_regions = 4
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
+    regions = make_regions_synth(17, 0, n_regions, 40, ps.max_length, 10)
+    b = _compare(ps, 40, beds, regions)
+    assert b.num_haplotypes > n_regions
+
+
 def test_multi_bed_duplicate_and_nested_inner_peaks(tmp_path):
     """Several bed sources, duplicate ranges (double count), a range that is never selected
     (strictly inside a 3-way merge, bed.rs:77/89), empty ranges, Ns in the reference."""
