@@ -45,6 +45,9 @@ namespace {
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
+#ifndef TFBS_MFMA_QUAD  // 2 strand tiles x 2 window tiles per round at K depth 1 (0: pairs only)
+#define TFBS_MFMA_QUAD 1
+#endif
 
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -183,7 +186,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 // bits 0-15 the lane's candidate mask (bit 15 - r <-> register r), 16-21 the
 // lane, 22-27 the strand tile, 32-39 the haplotype in the workgroup's group,
 // 40-63 the window tile start / 32.
-constexpr uint32_t kMQueue = 256;  // entries per wave; a tile pair adds at most 128
+constexpr uint32_t kMQueue = TFBS_MFMA_QUAD ? 384 : 256;  // entries per wave; a tile pair adds at most 128
 __shared__ uint64_t s_queue[kMBlock / 64][kMQueue];
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
@@ -416,6 +419,39 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             // the other waves of the SIMD hide the latencies
             for (uint32_t ti = 0;;) {
                 if (two) {
+#if TFBS_MFMA_QUAD
+                    // two strand tiles x two window tiles per round: four
+                    // independent MFMAs before the first test (3 % faster than
+                    // pairs at K depth 1; at depth 2 the registers would spill)
+                    for (; NK == 1 && ti + 1 < nt && qn <= kMQueue - 256; ti += 2) {
+                        v16f c0, c1, d0, d1;
+                        float tc, td;
+                        BFrag<NK> f, g;
+                        load_tile<NK>(s_img, S, ti, lane, f);
+                        load_tile<NK>(s_img, S, ti + 1, lane, g);
+                        __builtin_amdgcn_sched_barrier(0);
+                        c0 = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                        c1 = c0;
+                        d0 = c0;
+                        d1 = c0;
+#pragma unroll
+                        for (int kc = 0; kc < NK; kc++) {
+                            c0 = mfma_chunk(a0[kc], f.b[kc], f.c[kc], c0);
+                            c1 = mfma_chunk(a1[kc], f.b[kc], f.c[kc], c1);
+                            d0 = mfma_chunk(a0[kc], g.b[kc], g.c[kc], d0);
+                            d1 = mfma_chunk(a1[kc], g.b[kc], g.c[kc], d1);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        tc = f.thr;
+                        td = g.thr;
+                        const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
+                        const uint64_t g0 = coarse_test(d0, td), g1 = coarse_test(d1, td);
+                        queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
+                        queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+                        queue_tile(d0, td, g0, ti + 1, hh, i0, lane, wave, qn);
+                        queue_tile(d1, td, g1, ti + 1, hh, i0 + kMWindows, lane, wave, qn);
+                    }
+#endif
                     for (; ti < nt && qn <= kMQueue - 128; ti++) {
                         v16f c0, c1;
                         float tc;
