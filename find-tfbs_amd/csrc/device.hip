@@ -77,7 +77,7 @@ struct tfbs_ctx {
     DevBuf<DevUnit> fast_units;
     DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
-    DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights;
+    DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights, m_meta;
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
     uint32_t mfma_lds = 28 * 1024;  // LDS image budget of one MFMA super tile
@@ -129,6 +129,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.n_msupers = (uint32_t)P.m_supers.size();
         m.mimage = ctx->m_image.p;
         m.mweights = ctx->m_weights.p;
+        m.mmeta = ctx->m_meta.p;
         m.haps_per_block = ctx->mfma_hpb;
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
@@ -192,7 +193,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
-    ctx->m_image.release(); ctx->m_weights.release(); ctx->m_supers.release();
+    ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
@@ -272,7 +273,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         (rc = ctx->lut.put(P.lut, ctx->stream)) || (rc = ctx->wfull.put(P.wfull, ctx->stream)) ||
         (rc = ctx->gen_pats.put(P.gen_pats, ctx->stream)) || (rc = ctx->gen_tiles.put(P.gen_tiles, ctx->stream)) ||
         (rc = ctx->gen_w.put(P.gen_w, ctx->stream)) || (rc = ctx->m_image.put(P.m_image, ctx->stream)) ||
-        (rc = ctx->m_weights.put(P.m_weights, ctx->stream)) ||
+        (rc = ctx->m_weights.put(P.m_weights, ctx->stream)) || (rc = ctx->m_meta.put(P.m_meta, ctx->stream)) ||
         (rc = ctx->m_supers.put(P.m_supers, ctx->stream))) {
         tfbs_ctx_destroy(ctx);
         return rc;

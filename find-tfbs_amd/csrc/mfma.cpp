@@ -200,32 +200,31 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         S.img_bytes = count * per;
         S.meta_off = count * nk * kMFragBytes;
         S.lmin = UINT32_MAX;
+        S.tile0 = plan->n_mfma_tiles;
         std::vector<uint8_t> img(S.img_bytes, 0);
         for (uint32_t k = 0; k < count; k++) {
             const TileSrc &t = tiles[ti + k];
             const uint32_t b_off = k * nk * kMFragBytes, meta_off = S.meta_off + k * kMMetaBytes;
             S.lmin = std::min(S.lmin, t.lmin);
-            int32_t *meta = reinterpret_cast<int32_t *>(&img[meta_off]);
+            float *thr = reinterpret_cast<float *>(&img[meta_off]);
+            const size_t g0 = plan->m_meta.size();
+            plan->m_meta.resize(g0 + kGMetaInts, 0);
+            int32_t *gm = &plan->m_meta[g0];
             for (int n = 0; n < kMStrands; n++) {
                 if ((size_t)n < t.count) {
                     const auto &st = strands[t.first + n];
                     const Pat &p = P.pats[st.first];
-                    const Split &sp = split[t.first + n];
-                    std::memcpy(&meta[kMetaThrQ + n], &sp.thr, 4);
-                    meta[kMetaMin + n] = p.min_score;
-                    meta[kMetaWoff + n] = (int32_t)woff[t.first + n];
-                    meta[kMetaLen + n] = (int32_t)p.len;
-                    meta[kMetaSlot + n] = (int32_t)st.second;
-                    meta[kMetaOrig + n] = st.first;
+                    thr[n] = split[t.first + n].thr;
+                    gm[kGMin + n] = p.min_score;
+                    gm[kGWoff + n] = (int32_t)woff[t.first + n];
+                    gm[kGLen + n] = (int32_t)p.len;
+                    gm[kGSlot + n] = (int32_t)st.second;
+                    gm[kGOrig + n] = st.first;
                     plan->n_mfma_strands++;
                 } else {  // padding column: never a candidate
-                    const float never = 1e9f;
-                    std::memcpy(&meta[kMetaThrQ + n], &never, 4);
-                    meta[kMetaMin + n] = INT32_MAX;
-                    meta[kMetaWoff + n] = 0;
-                    meta[kMetaLen + n] = 0;
-                    meta[kMetaSlot + n] = 0;
-                    meta[kMetaOrig + n] = -1;
+                    thr[n] = 1e9f;
+                    gm[kGMin + n] = INT32_MAX;
+                    gm[kGOrig + n] = -1;
                 }
             }
             // B fragments: lane l holds column n = l & 31 and k = 32 h + 4 t + c,

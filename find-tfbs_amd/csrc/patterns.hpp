@@ -37,6 +37,7 @@ struct Plan {
     uint32_t n_mfma_tiles = 0;
     std::vector<int32_t> m_image;    // per super tile: B fragments + strand metadata (LDS image)
     std::vector<int32_t> m_weights;  // per MFMA strand: exact [A,C,G,T] weights per column (candidate rescoring)
+    std::vector<int32_t> m_meta;     // per MFMA tile: kGMetaInts rescoring fields (tfbs_internal.hpp)
     uint32_t max_super_bytes = 0;
     uint32_t n_mfma_strands = 0;
     bool zero_len_panics = false;

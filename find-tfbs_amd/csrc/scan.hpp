@@ -31,6 +31,7 @@ struct ScanArgs {
     uint32_t n_msupers;
     const int32_t *mimage;
     const int32_t *mweights;    // exact weights of the matrix-core strands
+    const int32_t *mmeta;       // their per-tile rescoring fields
     uint32_t mimg_max;          // LDS bytes reserved for the largest super tile image
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;

@@ -140,10 +140,11 @@ __device__ __forceinline__ void load_tile(const char *s_img, const DevMSuper &S,
     const char *p = s_img + (TFBS_MFMA_PROBE == 2 ? 0 : ti) * (NK * kMFragBytes);
 #pragma unroll
     for (int kc = 0; kc < NK; kc++) {
+        if (kc) asm volatile("" ::: "memory");  // no ds_read2 merging across chunks (see the quad loop)
         f.b[kc] = *reinterpret_cast<const v4i *>(p + kc * kMFragBytes + lane * 16);
         f.c[kc] = *reinterpret_cast<const int2 *>(p + kc * kMFragBytes + 1024 + lane * 8);
     }
-    f.thr = reinterpret_cast<const float *>(s_img + S.meta_off + ti * kMMetaBytes)[kMetaThrQ + (lane & 31)];
+    f.thr = reinterpret_cast<const float *>(s_img + S.meta_off + ti * kMMetaBytes)[lane & 31];
 }
 
 // One coarse chunk: FP4 one-hot (A) x FP6 digits (B), f32 accumulate, unit scales
@@ -233,18 +234,18 @@ __device__ __forceinline__ int32_t exact_score(const ScanArgs &A, const uint32_t
 
 // One queue entry: each candidate window of the lane's mask is rescored
 // exactly; hits add to their slot's count for every inner range they overlap.
-__device__ __forceinline__ void drain_entry(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+__device__ __forceinline__ void drain_entry(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                             uint32_t h0, uint64_t q) {
     uint32_t m = (uint32_t)q & 0xFFFFu;
     const uint32_t src = ((uint32_t)q >> 16) & 63u, ti = ((uint32_t)q >> 22) & 63u;
     const uint32_t hap = h0 + ((uint32_t)(q >> 32) & 255u), i0 = (uint32_t)(q >> 40) << 5;
     const uint32_t col = src & 31u, h = src >> 5;
-    const int32_t *meta = meta0 + ti * (kMMetaBytes / 4);
-    const uint32_t L = (uint32_t)meta[kMetaLen + col], woff = (uint32_t)meta[kMetaWoff + col];
-    const int32_t mn = meta[kMetaMin + col];
+    const int32_t *meta = A.mmeta + (size_t)(tile0 + ti) * kGMetaInts;
+    const uint32_t L = (uint32_t)meta[kGLen + col], woff = (uint32_t)meta[kGWoff + col];
+    const int32_t mn = meta[kGMin + col];
     const DevHap hp = A.haps[hap];
     const DevRegion rg = A.regions[hp.region];
-    const uint32_t off0 = (uint32_t)meta[kMetaSlot + col] * rg.n_inner;
+    const uint32_t off0 = (uint32_t)meta[kGSlot + col] * rg.n_inner;
     const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
     while (m) {
         const uint32_t b = 31 - __builtin_clz(m & -m);  // lowest set bit
@@ -268,27 +269,27 @@ __device__ __forceinline__ void drain_entry(const ScanArgs &A, const uint32_t *w
                 atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
         }
         if (A.hits && i / 64 < A.hits_wpp)
-            atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kMetaOrig + col]) * A.hits_wpp +
+            atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + col]) * A.hits_wpp +
                          i / 64,
                      1ull << (i & 63));
     }
 }
 
 // Drains the wave's first n queue entries (one entry per lane per round).
-// h0: the workgroup's first haplotype; meta0: tile 0's metadata.
-__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+// h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                             uint32_t h0, uint32_t n, uint32_t wave) {
 #if TFBS_MFMA_PROBE == 12
     return;  // timing only: queued candidates are dropped
 #endif
-    for (uint32_t e = threadIdx.x & 63; e < n; e += 64) drain_entry(A, words, meta0, h0, s_queue[wave][e]);
+    for (uint32_t e = threadIdx.x & 63; e < n; e += 64) drain_entry(A, words, tile0, h0, s_queue[wave][e]);
 }
 
 __shared__ uint32_t s_qn[kMBlock / 64];
 
 // Drains every wave's queue (entries s_queue[w][0, s_qn[w])) with the whole
 // workgroup, one entry per thread per round.
-__device__ __forceinline__ void drain_pooled(const ScanArgs &A, const uint32_t *words, const int32_t *meta0,
+__device__ __forceinline__ void drain_pooled(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                              uint32_t h0) {
 #if TFBS_MFMA_PROBE == 12
     return;
@@ -302,7 +303,7 @@ __device__ __forceinline__ void drain_pooled(const ScanArgs &A, const uint32_t *
         uint32_t w = 0;
 #pragma unroll
         for (uint32_t k = 1; k < kWaves; k++) w += g >= off[k];
-        drain_entry(A, words, meta0, h0, s_queue[w][g - off[w]]);
+        drain_entry(A, words, tile0, h0, s_queue[w][g - off[w]]);
     }
 }
 
@@ -392,7 +393,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     constexpr uint32_t kWaves = kMBlock / 64;
     const uint32_t nt = S.tile_count;
     const uint32_t h0 = hg * A.haps_per_block;
-    const int32_t *meta0 = reinterpret_cast<const int32_t *>(s_img + S.meta_off);
+    const uint32_t tile0 = S.tile0;
     uint32_t qn = 0;
     for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
         const uint32_t hap = hg * A.haps_per_block + hh;
@@ -428,6 +429,9 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         float tc, td;
                         BFrag<NK> f, g;
                         load_tile<NK>(s_img, S, ti, lane, f);
+                        // keeps the two tiles' dword 4-5 reads apart: merged into one
+                        // ds_read2st64 they need 4 v_mov into the MFMA operand tuples
+                        asm volatile("" ::: "memory");
                         load_tile<NK>(s_img, S, ti + 1, lane, g);
                         __builtin_amdgcn_sched_barrier(0);
                         c0 = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -446,6 +450,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         td = g.thr;
                         const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
                         const uint64_t g0 = coarse_test(d0, td), g1 = coarse_test(d1, td);
+                        if (__builtin_expect((f0 | f1 | g0 | g1) == 0, 1)) continue;  // one branch for four tests
                         queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
                         queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
                         queue_tile(d0, td, g0, ti + 1, hh, i0, lane, wave, qn);
@@ -457,6 +462,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         float tc;
                         pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
                         const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
+                        if (__builtin_expect((f0 | f1) == 0, 1)) continue;
                         queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
                         queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
                     }
@@ -483,7 +489,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                     }
                 }
                 if (ti >= nt) break;
-                drain_queue(A, words, meta0, h0, qn, wave);  // queue nearly full: drain, resume at tile ti
+                drain_queue(A, words, tile0, h0, qn, wave);  // queue nearly full: drain, resume at tile ti
                 qn = 0;
             }
         }
@@ -491,7 +497,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     // the waves' last entries, pooled: every wave drains a share of the sum
     if (lane == 0) s_qn[wave] = qn;
     __syncthreads();
-    drain_pooled(A, words, meta0, h0);
+    drain_pooled(A, words, tile0, h0);
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD.

@@ -93,14 +93,18 @@ constexpr int kMChunkCols = 16;    // columns per K chunk of 64
 constexpr int kMMaxChunks = 2;     // L <= 32
 constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (6 bits in a candidate entry)
 constexpr int kMFragBytes = 1536;  // one B fragment: 64 lanes x 24 bytes (dwords 0-3 | dwords 4-5)
-// per tile metadata, 32 x 4 bytes each: coarse threshold (f32), min_score, offset of
-// the exact weights (4 per column), len, slot, pattern index
-enum MMeta { kMetaThrQ = 0, kMetaMin = 32, kMetaWoff = 64, kMetaLen = 96, kMetaSlot = 128, kMetaOrig = 160 };
-constexpr int kMMetaBytes = 768;
+// Per tile, in the LDS image: the 32 strands' bound thresholds (f32).  The
+// fields only the candidate rescoring reads live in global memory
+// (Plan::m_meta, kGMetaInts per tile): min_score, offset of the exact weights
+// (4 per column), len, slot, pattern index.
+constexpr int kMMetaBytes = 128;
+enum MGMeta { kGMin = 0, kGWoff = 32, kGLen = 64, kGSlot = 96, kGOrig = 128 };
+constexpr int kGMetaInts = 160;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk),
-// its metadata at meta_off + t * kMMetaBytes.
+// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk), its
+// thresholds at meta_off + t * kMMetaBytes; its rescoring fields at
+// Plan::m_meta[(tile0 + t) * kGMetaInts].
 struct DevMSuper {
     uint32_t tile_count;
     uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
@@ -108,7 +112,8 @@ struct DevMSuper {
     uint32_t img_bytes;
     uint32_t meta_off;  // byte offset of tile 0's metadata in the image
     uint32_t lmin;      // shortest strand
-    uint32_t pad0, pad1;
+    uint32_t tile0;     // global index of tile 0 (Plan::m_meta)
+    uint32_t pad1;
 };
 
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };
