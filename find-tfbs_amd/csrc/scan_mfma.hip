@@ -187,7 +187,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 // bits 0-15 the lane's candidate mask (bit 15 - r <-> register r), 16-21 the
 // lane, 22-27 the strand tile, 32-39 the haplotype in the workgroup's group,
 // 40-63 the window tile start / 32.
-constexpr uint32_t kMQueue = TFBS_MFMA_QUAD ? 384 : 256;  // entries per wave; a tile pair adds at most 128
+constexpr uint32_t kMQueue = 384;  // entries per wave (a round of four tile tests adds at most 256)
 __shared__ uint64_t s_queue[kMBlock / 64][kMQueue];
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
@@ -418,79 +418,96 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             if (kStep > kMWindows && i0 + kStep + kMWindows < nwin)
                 load_window(A, words, hm, i0 + kStep + kMWindows, lane, ww1);
             // the other waves of the SIMD hide the latencies
-            for (uint32_t ti = 0;;) {
-                if (two) {
+            // The loops test the queue's room only after a round that queued
+            // something (rare): a round adds at most 64 entries per tile test,
+            // so draining above kMQueue - 256 keeps the next round's entries
+            // in bounds.  Inlined in that cold branch, the drain adds no
+            // registers to the loop.
+            uint32_t ti = 0;
+            if (two) {
 #if TFBS_MFMA_QUAD
-                    // two strand tiles x two window tiles per round: four
-                    // independent MFMAs before the first test (3 % faster than
-                    // pairs at K depth 1; at depth 2 the registers would spill)
-                    for (; NK == 1 && ti + 1 < nt && qn <= kMQueue - 256; ti += 2) {
-                        v16f c0, c1, d0, d1;
-                        float tc, td;
-                        BFrag<NK> f, g;
-                        load_tile<NK>(s_img, S, ti, lane, f);
-                        // keeps the two tiles' dword 4-5 reads apart: merged into one
-                        // ds_read2st64 they need 4 v_mov into the MFMA operand tuples
-                        asm volatile("" ::: "memory");
-                        load_tile<NK>(s_img, S, ti + 1, lane, g);
-                        __builtin_amdgcn_sched_barrier(0);
-                        c0 = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-                        c1 = c0;
-                        d0 = c0;
-                        d1 = c0;
+                // two strand tiles x two window tiles per round: four
+                // independent MFMAs before the first test (3 % faster than
+                // pairs at K depth 1; at depth 2 the registers would spill)
+                for (; NK == 1 && ti + 1 < nt; ti += 2) {
+                    v16f c0, c1, d0, d1;
+                    float tc, td;
+                    BFrag<NK> f, g;
+                    load_tile<NK>(s_img, S, ti, lane, f);
+                    // keeps the two tiles' dword 4-5 reads apart: merged into one
+                    // ds_read2st64 they need 4 v_mov into the MFMA operand tuples
+                    asm volatile("" ::: "memory");
+                    load_tile<NK>(s_img, S, ti + 1, lane, g);
+                    __builtin_amdgcn_sched_barrier(0);
+                    c0 = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+                    c1 = c0;
+                    d0 = c0;
+                    d1 = c0;
 #pragma unroll
-                        for (int kc = 0; kc < NK; kc++) {
-                            c0 = mfma_chunk(a0[kc], f.b[kc], f.c[kc], c0);
-                            c1 = mfma_chunk(a1[kc], f.b[kc], f.c[kc], c1);
-                            d0 = mfma_chunk(a0[kc], g.b[kc], g.c[kc], d0);
-                            d1 = mfma_chunk(a1[kc], g.b[kc], g.c[kc], d1);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                        tc = f.thr;
-                        td = g.thr;
-                        const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
-                        const uint64_t g0 = coarse_test(d0, td), g1 = coarse_test(d1, td);
-                        if (__builtin_expect((f0 | f1 | g0 | g1) == 0, 1)) continue;  // one branch for four tests
-                        queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
-                        queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
-                        queue_tile(d0, td, g0, ti + 1, hh, i0, lane, wave, qn);
-                        queue_tile(d1, td, g1, ti + 1, hh, i0 + kMWindows, lane, wave, qn);
+                    for (int kc = 0; kc < NK; kc++) {
+                        c0 = mfma_chunk(a0[kc], f.b[kc], f.c[kc], c0);
+                        c1 = mfma_chunk(a1[kc], f.b[kc], f.c[kc], c1);
+                        d0 = mfma_chunk(a0[kc], g.b[kc], g.c[kc], d0);
+                        d1 = mfma_chunk(a1[kc], g.b[kc], g.c[kc], d1);
                     }
-#endif
-                    for (; ti < nt && qn <= kMQueue - 128; ti++) {
-                        v16f c0, c1;
-                        float tc;
-                        pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
-                        const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
-                        if (__builtin_expect((f0 | f1) == 0, 1)) continue;
-                        queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
-                        queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
-                    }
-                } else {
-                    // two strand tiles at a time: tile 0's test overlaps tile 1's MFMAs
-                    for (; ti + 1 < nt && qn <= kMQueue - 128; ti += 2) {
-                        BFrag<NK> f0, f1;
-                        load_tile<NK>(s_img, S, ti, lane, f0);
-                        load_tile<NK>(s_img, S, ti + 1, lane, f1);
-                        __builtin_amdgcn_sched_barrier(0);
-                        const v16f acc0 = tile_scores<NK>(a0, f0);
-                        const v16f acc1 = tile_scores<NK>(a0, f1);
-                        const uint64_t g0 = coarse_test(acc0, f0.thr), g1 = coarse_test(acc1, f1.thr);
-                        queue_tile(acc0, f0.thr, g0, ti, hh, i0, lane, wave, qn);
-                        queue_tile(acc1, f1.thr, g1, ti + 1, hh, i0, lane, wave, qn);
-                    }
-                    if (ti + 1 == nt && qn <= kMQueue - 128) {
-                        BFrag<NK> f;
-                        load_tile<NK>(s_img, S, ti, lane, f);
-                        __builtin_amdgcn_sched_barrier(0);
-                        const v16f acc = tile_scores<NK>(a0, f);
-                        queue_tile(acc, f.thr, coarse_test(acc, f.thr), ti, hh, i0, lane, wave, qn);
-                        ti++;
+                    __builtin_amdgcn_sched_barrier(0);
+                    tc = f.thr;
+                    td = g.thr;
+                    const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
+                    const uint64_t g0 = coarse_test(d0, td), g1 = coarse_test(d1, td);
+                    if (__builtin_expect((f0 | f1 | g0 | g1) == 0, 1)) continue;  // one branch for four tests
+                    queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
+                    queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+                    queue_tile(d0, td, g0, ti + 1, hh, i0, lane, wave, qn);
+                    queue_tile(d1, td, g1, ti + 1, hh, i0 + kMWindows, lane, wave, qn);
+                    if (qn > kMQueue - 256) {
+                        drain_queue(A, words, tile0, h0, qn, wave);
+                        qn = 0;
                     }
                 }
-                if (ti >= nt) break;
-                drain_queue(A, words, tile0, h0, qn, wave);  // queue nearly full: drain, resume at tile ti
-                qn = 0;
+#endif
+                for (; ti < nt; ti++) {
+                    v16f c0, c1;
+                    float tc;
+                    pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
+                    const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
+                    if (__builtin_expect((f0 | f1) == 0, 1)) continue;
+                    queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
+                    queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+                    if (qn > kMQueue - 256) {
+                        drain_queue(A, words, tile0, h0, qn, wave);
+                        qn = 0;
+                    }
+                }
+            } else {
+                // two strand tiles at a time: tile 0's test overlaps tile 1's MFMAs
+                for (; ti + 1 < nt; ti += 2) {
+                    BFrag<NK> f0, f1;
+                    load_tile<NK>(s_img, S, ti, lane, f0);
+                    load_tile<NK>(s_img, S, ti + 1, lane, f1);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const v16f acc0 = tile_scores<NK>(a0, f0);
+                    const v16f acc1 = tile_scores<NK>(a0, f1);
+                    const uint64_t g0 = coarse_test(acc0, f0.thr), g1 = coarse_test(acc1, f1.thr);
+                    if (__builtin_expect((g0 | g1) == 0, 1)) continue;
+                    queue_tile(acc0, f0.thr, g0, ti, hh, i0, lane, wave, qn);
+                    queue_tile(acc1, f1.thr, g1, ti + 1, hh, i0, lane, wave, qn);
+                    if (qn > kMQueue - 256) {
+                        drain_queue(A, words, tile0, h0, qn, wave);
+                        qn = 0;
+                    }
+                }
+                if (ti < nt) {
+                    BFrag<NK> f;
+                    load_tile<NK>(s_img, S, ti, lane, f);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const v16f acc = tile_scores<NK>(a0, f);
+                    queue_tile(acc, f.thr, coarse_test(acc, f.thr), ti, hh, i0, lane, wave, qn);
+                    if (qn > kMQueue - 256) {
+                        drain_queue(A, words, tile0, h0, qn, wave);
+                        qn = 0;
+                    }
+                }
             }
         }
     }
