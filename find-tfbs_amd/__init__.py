@@ -386,6 +386,42 @@ class RegionBatch:
             out[(self.beds[bed.value], (s.value, e.value), pid.value)] = (list(l[:ns]), list(r[:ns]))
         return out
 
+    def keys_np(self, region):
+        """keys() with numpy uint32 vectors (large sample counts)."""
+        import numpy as np
+        L = lib()
+        n = C.c_size_t()
+        check(L.tfbs_batch_region_num_keys(self.h, region, C.byref(n)))
+        out = {}
+        ns = self.n_samples
+        for k in range(n.value):
+            bed, s, e, pid = C.c_uint32(), C.c_uint64(), C.c_uint64(), C.c_uint16()
+            l = np.zeros(max(1, ns), dtype=np.uint32)
+            r = np.zeros(max(1, ns), dtype=np.uint32)
+            check(L.tfbs_batch_region_key(self.h, region, k, C.byref(bed), C.byref(s), C.byref(e), C.byref(pid),
+                                          l.ctypes.data_as(_capi.u32p), r.ctypes.data_as(_capi.u32p)))
+            out[(self.beds[bed.value], (s.value, e.value), pid.value)] = (l[:ns], r[:ns])
+        return out
+
+    def region_rows(self, region, chromosome, min_maf=0, fake_position=1):
+        """Rows of one region (main.rs:415-429); returns (text, next fake_position)."""
+        fp = C.c_uint32(fake_position)
+        p = C.c_void_p()
+        n = C.c_size_t()
+        check(lib().tfbs_batch_region_rows(self.h, region, _u(chromosome), min_maf, C.byref(fp), C.byref(p),
+                                           C.byref(n)))
+        try:
+            text = C.string_at(p, n.value).decode()
+        finally:
+            lib().tfbs_free(p)
+        return text, fp.value
+
+    def digest(self, region):
+        """tfbs_batch_region_digest: the region's keys at the distinct-haplotype level."""
+        d = C.c_uint64()
+        check(lib().tfbs_batch_region_digest(self.h, region, C.byref(d)))
+        return d.value
+
     def rows(self, chromosome, min_maf=0, fake_position=1):
         """Rows for every region (main.rs:415-429); returns (text, next fake_position)."""
         fp = C.c_uint32(fake_position)
@@ -453,8 +489,10 @@ def select_inner_peaks(merged, beds):
 
 def run(chromosome, bcf, bed_files, reference_genome_file, wanted_samples, pwm_file, pwm_threshold_directory,
         pwm_threshold, wanted_pwms, output_file, forward_only=False, run_tabix=False, min_maf=0, threads=1,
-        after_position=0, verbose=False, device=0, regions_per_batch=0):
-    """main.rs:234-393 `run` with the reference's argument order; writes the BGZF VCF."""
+        after_position=0, verbose=False, device=0, regions_per_batch=0, devices=None):
+    """main.rs:234-393 `run` with the reference's argument order; writes the BGZF VCF.
+    devices: list of HIP devices, one contiguous block of merged regions each (same text
+    for any list; a device may repeat)."""
     a = _capi.tfbs_run_args()
     keep = [_u(x) if x is not None else None for x in (chromosome, bcf, ",".join(bed_files), reference_genome_file,
                                                         wanted_samples, pwm_file, pwm_threshold_directory,
@@ -470,6 +508,8 @@ def run(chromosome, bcf, bed_files, reference_genome_file, wanted_samples, pwm_f
     a.verbose = 1 if verbose else 0
     a.device = device
     a.regions_per_batch = regions_per_batch
+    dev = _u(",".join(str(int(d)) for d in devices)) if devices else None
+    a.devices = dev
     check(lib().tfbs_run(C.byref(a)))
 
 

@@ -49,7 +49,7 @@ class tfbs_run_args(C.Structure):
         ("samples_file", C.c_char_p), ("pwm_file", C.c_char_p), ("pwm_threshold_dir", C.c_char_p),
         ("pwm_names", C.c_char_p), ("output", C.c_char_p), ("pwm_threshold", C.c_float), ("forward_only", C.c_int),
         ("min_maf", C.c_uint32), ("threads", C.c_uint32), ("after_position", C.c_uint64), ("tabix", C.c_int),
-        ("verbose", C.c_int), ("device", C.c_int), ("regions_per_batch", C.c_uint32),
+        ("verbose", C.c_int), ("device", C.c_int), ("regions_per_batch", C.c_uint32), ("devices", C.c_char_p),
     ]
 
 
@@ -102,6 +102,9 @@ SIGNATURES = [
     ("tfbs_batch_region_num_keys", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("tfbs_batch_region_key", C.c_int, [vp, C.c_size_t, C.c_size_t, u32p, u64p, u64p, u16p, u32p, u32p]),
     ("tfbs_batch_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, u32p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    ("tfbs_batch_region_rows", C.c_int, [vp, C.c_size_t, C.c_char_p, C.c_uint32, u32p, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_size_t)]),
+    ("tfbs_batch_region_digest", C.c_int, [vp, C.c_size_t, u64p]),
     ("tfbs_batch_region_stats", C.c_int, [vp, C.c_size_t, u32p, u32p]),
     ("tfbs_free", None, [C.c_void_p]),
     ("tfbs_counts_as_genotypes", C.c_int, [u32p, u32p, C.c_size_t, u32p, C.c_char_p, C.c_size_t, C.c_char_p,

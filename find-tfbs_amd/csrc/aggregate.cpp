@@ -134,7 +134,7 @@ bool counts_as_genotypes(const uint32_t *v1, const uint32_t *v2, size_t n, uint3
 }
 
 // chromosome.replace("chr", "") (main.rs:402)
-static std::string strip_chr(const std::string &c) {
+std::string strip_chr(const std::string &c) {
     std::string o;
     for (size_t i = 0; i < c.size();) {
         if (c.compare(i, 3, "chr") == 0) i += 3;
@@ -145,7 +145,7 @@ static std::string strip_chr(const std::string &c) {
 
 // Rows of one region, each without its "<chr>\t<POS>\t" prefix (the POS
 // counter is assigned in order afterwards).
-static void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<std::string> &rows) {
+void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<std::string> &rows) {
     const uint32_t H = 2 * B.n_samples;
     std::vector<uint32_t> l(B.n_samples), r(B.n_samples);
     Membership M(R, H);
@@ -181,13 +181,12 @@ static void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std:
     }
 }
 
-// Pseudo-VCF rows (main.rs:395-432) of every region in batch order, regions
-// formatted in parallel on `threads` threads, POS counter `fake` in row order.
-int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out,
-               uint32_t threads) {
+// Row bodies (each row without its "<chr>\t<POS>\t" prefix, '\n'-terminated)
+// of every region in batch order, regions formatted in parallel on `threads`
+// threads (main.rs:395-432).
+int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_t threads) {
     if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
-    const std::string chr = strip_chr(chrom);
     const size_t n = B.rh.size();
     std::vector<std::vector<std::string>> rows(n);
     std::atomic<size_t> next(0);
@@ -201,17 +200,31 @@ int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint3
     for (auto &t : ts) t.join();
     size_t bytes = out.size();
     for (auto &v : rows)
-        for (auto &r : v) bytes += r.size() + chr.size() + 16;
+        for (auto &r : v) bytes += r.size();
     out.reserve(bytes);
-    char head[32];
     for (auto &v : rows)
-        for (auto &r : v) {
-            const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
-            out += chr;
-            out.append(head, (size_t)m);
-            out += r;
-            (*fake)++;
-        }
+        for (auto &r : v) out += r;
+    return TFBS_OK;
+}
+
+// The same rows with the prefix, POS counter `fake` in row order.
+int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out,
+               uint32_t threads) {
+    std::string bodies;
+    if (int rc = batch_row_bodies(B, min_maf, bodies, threads)) return rc;
+    const std::string chr = strip_chr(chrom);
+    char head[32];
+    out.reserve(out.size() + bodies.size() + 64);
+    for (size_t i = 0; i < bodies.size();) {
+        size_t e = bodies.find('\n', i);
+        e = e == std::string::npos ? bodies.size() : e + 1;
+        const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
+        out += chr;
+        out.append(head, (size_t)m);
+        out.append(bodies, i, e - i);
+        (*fake)++;
+        i = e;
+    }
     return TFBS_OK;
 }
 
@@ -250,6 +263,65 @@ int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t
             if (right) right[s] = tfbs::count_of(B, R, M.local[2 * s + 1], q.slot, q.ik->slot) * q.ik->mult;
         }
     }
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chromosome, uint32_t min_maf,
+                           uint32_t *fake, char **text, size_t *len) {
+    if (!b || !chromosome || !fake || !text || !len) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    std::vector<std::string> rows;
+    if (B.rh[region].hap_count) tfbs::region_rows(B, B.rh[region], min_maf, rows);
+    const std::string chr = tfbs::strip_chr(chromosome);
+    std::string out;
+    char head[32];
+    for (auto &r : rows) {
+        const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
+        out += chr;
+        out.append(head, (size_t)m);
+        out += r;
+        (*fake)++;
+    }
+    char *p = (char *)malloc(out.size() + 1);
+    if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");
+    memcpy(p, out.data(), out.size());
+    p[out.size()] = 0;
+    *text = p;
+    *len = out.size();
+    return TFBS_OK;
+}
+
+// A 64-bit digest of a region's keys at the distinct-haplotype level: for every
+// key in row order its (bed, range, pattern_id) and every distinct haplotype's
+// count.  Per-sample vectors follow from these and the membership, so equal
+// digests from the dense download and the device reduction (or from two shards
+// of one workload) mean equal keys.
+int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *digest) {
+    if (!b || !digest) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    const tfbs::RegionH &R = B.rh[region];
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    auto mix = [&h](uint64_t x) {
+        h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+        h *= 0xFF51AFD7ED558CCDull;
+        h ^= h >> 33;
+    };
+    const auto keys = tfbs::region_keys(B, R);
+    mix(keys.size());
+    for (const auto &k : keys) {
+        mix(k.ik->bed);
+        mix(k.ik->s);
+        mix(k.ik->e);
+        mix(k.ik->mult);
+        mix(B.slot_pid[k.slot]);
+        for (uint32_t l = 0; l < R.hap_count; l++) mix(tfbs::count_of(B, R, l, k.slot, k.ik->slot));
+    }
+    *digest = h;
     return TFBS_OK;
 }
 

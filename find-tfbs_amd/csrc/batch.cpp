@@ -303,6 +303,9 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
         dist.push_back(std::move(d));
         carriers.push_back((uint32_t)(H - covered));
     }
+    // the kernels index windows with 29 bits (scan_mfma.hip queue entries)
+    for (const Distinct &d : dist)
+        if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
     if (B.keep_membership) {
         std::sort(member.begin(), member.end());
         R.nonref_id.resize(member.size());

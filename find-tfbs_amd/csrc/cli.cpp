@@ -14,7 +14,9 @@ static void usage() {
             "USAGE: find-tfbs-amd --chromosome CHROM --input IN --output OUT --reference REF --bed BED[,BED..]\n"
             "       --pwm_names N1[,N2..] --pwm_file PWM --pwm_threshold_directory DIR --pwm_threshold T\n"
             "       [--forward_only] [--threads N] [--min_maf N] [--after_position P] [--samples FILE]\n"
-            "       [--tabix] [--verbose] [--device D] [--regions_per_batch N]\n");
+            "       [--tabix] [--verbose] [--device D | --devices D1,D2,.. | --gpus N] [--regions_per_batch N]\n"
+            "  --devices: one contiguous block of merged regions per listed HIP device (a device may repeat);\n"
+            "  --gpus N: devices 0..N-1.  The output is the same for any device list.\n");
 }
 
 int main(int argc, char **argv) {
@@ -22,6 +24,7 @@ int main(int argc, char **argv) {
     memset(&a, 0, sizeof a);
     a.threads = 1;
     bool have_thr = false;
+    std::string gpus;
     for (int i = 1; i < argc; i++) {
         std::string k = argv[i];
         auto val = [&](const char *name) -> const char * {
@@ -56,6 +59,17 @@ int main(int argc, char **argv) {
         else if (k == "--tabix" || k == "-z") a.tabix = 1;
         else if (k == "--verbose" || k == "-v") a.verbose = 1;
         else if (k == "--device") a.device = atoi(val(k.c_str()));
+        else if (k == "--devices") a.devices = val(k.c_str());
+        else if (k == "--gpus") {
+            long n = strtol(val(k.c_str()), nullptr, 10);
+            if (n < 1) {
+                fprintf(stderr, "Wrong number of GPUs\n");
+                return 2;
+            }
+            gpus.clear();
+            for (long d = 0; d < n; d++) gpus += (d ? "," : "") + std::to_string(d);
+            a.devices = gpus.c_str();
+        }
         else if (k == "--regions_per_batch") a.regions_per_batch = (uint32_t)strtoul(val(k.c_str()), nullptr, 10);
         else if (k == "--help" || k == "-h") {
             usage();

@@ -414,7 +414,7 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
 int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t n, uint32_t *counts,
                  uint64_t *out_start, uint64_t *out_end, size_t cap, size_t *n_total) {
     if (!ctx || !n_total || !counts || (n && (!nucs || !pos))) return tfbs::fail(TFBS_E_ARG, "null argument");
-    if (n >= (1u << 30)) return tfbs::fail(TFBS_E_ARG, "haplotype too long");
+    if (n >= kMaxHapLen) return tfbs::fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
     const Patterns &P = *ctx->pats;
     // pack one haplotype; no inner ranges, hit bitmaps only
     std::vector<uint32_t> words((n + 15) / 16 + 3, 0u), nmask;

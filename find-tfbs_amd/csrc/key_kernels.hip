@@ -30,9 +30,15 @@ __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *
                                                                    uint8_t *__restrict__ flags) {
     const DevRegion rg = regions[blockIdx.x];
     const uint32_t K = n_slots * rg.n_inner;
-    if (K == 0 || rg.hap_count == 0) return;
-    const uint64_t base = haps[rg.hap_begin].count_off;
     const uint64_t ko = (uint64_t)rg.inner_off * n_slots;
+    if (rg.hap_count == 0) {  // no samples: no haplotype, no match, no key
+        for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
+            first[ko + j] = 0;
+            flags[ko + j] = 0;
+        }
+        return;
+    }
+    const uint64_t base = haps[rg.hap_begin].count_off;
     for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
         const uint32_t c0 = counts[base + j];
         uint32_t any = c0, diff = 0;

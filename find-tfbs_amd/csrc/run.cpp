@@ -29,8 +29,8 @@
 #include "patterns.hpp"
 
 namespace tfbs {
-int batch_rows(const Batch &B, const std::string &chrom, uint32_t min_maf, uint32_t *fake, std::string &out,
-               uint32_t threads);
+int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_t threads);
+std::string strip_chr(const std::string &c);
 }
 
 namespace {
@@ -62,116 +62,65 @@ bool in_path(const char *prog) {
     return false;
 }
 
-}  // namespace
+// One block of merged regions [r0, r1) on one device: the two-stage pipeline
+// (a helper thread prepares batch k+1 -- FASTA windows, BCF records,
+// load_diffs, distinct haplotypes -- while batch k is scanned, reduced on the
+// device and formatted) with its own readers and ctx.  Row bodies (without
+// the "<chr>\t<POS>\t" prefix) go to `emit` in merged-peak order.
+struct Shard {
+    size_t r0 = 0, r1 = 0;
+    int device = 0;
+    uint32_t threads = 1;
+    int rc = TFBS_OK;
+    std::string err;
+    double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0, t_emit = 0;
+};
 
-extern "C" {
-
-int tfbs_run(const tfbs_run_args *a) {
-    using namespace tfbs;
-    if (!a || !a->chromosome || !a->bcf || !a->bed_files || !a->reference || !a->pwm_file || !a->pwm_threshold_dir ||
-        !a->pwm_names || !a->output)
-        return fail(TFBS_E_ARG, "missing required argument");
-    const std::string chrom = a->chromosome;
-    if (a->tabix && (!in_path("bgzip") || !in_path("tabix")))
-        return fail(TFBS_E_IO, "bgzip/tabix cannot be found in PATH");  // main.rs:220-223
-
-    // patterns (main.rs:237-250)
-    tfbs_patterns *pp = nullptr;
-    int rc = tfbs_patterns_from_files(a->pwm_file, a->pwm_threshold_dir, a->pwm_threshold, a->pwm_names,
-                                      a->forward_only ? 0 : 1, &pp);
-    if (rc) return rc;
-    std::unique_ptr<tfbs_patterns, void (*)(tfbs_patterns *)> pguard(pp, tfbs_patterns_destroy);
-
-    // BED sources (bed.rs:25-47): keyed by path (a repeated path counts once), merged
-    // over all of them, inner peaks keyed by basename (a later file with the same
-    // basename replaces an earlier one).
-    std::vector<std::string> paths;
-    for (auto &b : split(a->bed_files, ','))
-        if (std::find(paths.begin(), paths.end(), b) == paths.end()) paths.push_back(b);
-    std::vector<std::pair<uint64_t, uint64_t>> all;
+struct RunSetup {
+    const tfbs_run_args *a;
+    std::string chrom;
+    tfbs_patterns *pp;
     std::vector<std::pair<std::string, std::vector<std::pair<uint64_t, uint64_t>>>> beds;
-    for (auto &path : paths) {
-        struct stat st;
-        if (stat(path.c_str(), &st) != 0) return fail(TFBS_E_IO, "Bed file " + path + " does not exist");
-        std::vector<std::pair<uint64_t, uint64_t>> peaks, kept;
-        rc = load_bed(path, chrom, peaks);
-        if (rc) return rc;
-        for (auto &p : peaks)
-            if (p.first >= a->after_position) kept.push_back(p);
-        all.insert(all.end(), kept.begin(), kept.end());
-        const std::string bn = basename_of(path);
-        bool replaced = false;
-        for (auto &b : beds)
-            if (b.first == bn) { b.second = kept; replaced = true; }
-        if (!replaced) beds.push_back({bn, kept});
-    }
-    const auto merged = merge_ranges(all);
-
-    // BCF + samples (main.rs:255, 293-314)
-    Bcf bcf;
-    rc = bcf.open(a->bcf, std::max(1u, a->threads));
-    if (rc) return rc;
+    std::vector<std::pair<uint64_t, uint64_t>> merged;
     std::vector<size_t> sel;
-    if (a->samples_file && *a->samples_file) {
-        std::ifstream sf(a->samples_file);
-        if (!sf) return fail(TFBS_E_IO, std::string("Could not open sample file ") + a->samples_file);
-        std::set<std::string> want;
-        std::string l;
-        while (std::getline(sf, l))
-            if (l.size() > 1) want.insert(l);
-        for (size_t i = 0; i < bcf.samples.size(); i++)
-            if (want.count(bcf.samples[i])) sel.push_back(i);
-    } else {
-        for (size_t i = 0; i < bcf.samples.size(); i++) sel.push_back(i);
-    }
-    if ((rc = bcf.select(sel))) return rc;  // GT decoded for these samples only
-    const int rid = bcf.contig_index(chrom);
+    size_t per_batch;
+};
+
+// Row bodies of one shard in merged-peak order; emit(bodies) gets each batch's
+// rows ('\n'-terminated, no chromosome/POS prefix).
+template <class Emit> int run_shard(const RunSetup &S, Shard &sh, Emit &&emit) {
+    using namespace tfbs;
+    const tfbs_run_args *a = S.a;
+    if (sh.r0 >= sh.r1) return TFBS_OK;
+    Bcf bcf;
+    int rc = bcf.open(a->bcf, sh.threads);
+    if (rc) return rc;
+    if ((rc = bcf.select(S.sel))) return rc;  // GT decoded for these samples only
+    const int rid = bcf.contig_index(S.chrom);
     Fasta fasta;
-    rc = fasta.open(a->reference);
-    if (rc) return rc;
-
-    // output (main.rs:264-290, 320-324)
-    const std::string out = a->output, part = out + ".part";
-    BgzfWriter w;
-    rc = w.open(part, std::max(1u, a->threads));
-    if (rc) return rc;
-    std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
-    for (size_t i : sel) header += "\t" + bcf.samples[i];
-    header += "\n";
-    rc = w.write(header.data(), header.size());
-    if (rc) return rc;
-
+    if ((rc = fasta.open(a->reference))) return rc;
     tfbs_ctx *ctx = nullptr;
-    if (!merged.empty()) {
-        rc = tfbs_ctx_create(a->device, pp, &ctx);
-        if (rc) return rc;
-    }
+    if ((rc = tfbs_ctx_create(sh.device, S.pp, &ctx))) return rc;
     std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
-    const uint32_t threads = std::max(1u, a->threads);
-    const size_t per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
-    uint32_t fake = 1;
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
-    // Host side of one batch (main.rs:147-186 per merged region): FASTA window,
-    // BCF records, inner peaks, distinct haplotypes.  Runs on a helper thread
-    // while the previous batch is on the GPU / being formatted.
     std::vector<const BcfRecord *> recs;
-    auto prepare = [&](size_t r0, BatchPtr &out, std::string &err) -> int {
+    auto prepare = [&](size_t b0, BatchPtr &out, std::string &err) -> int {
         tfbs_batch *bb = nullptr;
-        int rc = tfbs_batch_create(pp, (uint32_t)sel.size(), 1, &bb);
+        int rc = tfbs_batch_create(S.pp, (uint32_t)S.sel.size(), 1, &bb);
         if (rc) return err = tfbs_last_error(), rc;
         out = BatchPtr(bb, tfbs_batch_destroy);
         Batch &B = bb->b;
-        for (auto &b : beds) B.beds.push_back(b.first);
+        for (auto &b : S.beds) B.beds.push_back(b.first);
         std::vector<RegionInput> ins;
-        for (size_t r = r0; r < std::min(merged.size(), r0 + per_batch); r++) {
-            const auto &m = merged[r];
+        for (size_t r = b0; r < std::min(sh.r1, b0 + S.per_batch); r++) {
+            const auto &m = S.merged[r];
             RegionInput in;
             in.R.ms = m.first;
             in.R.me = m.second;
             rc = tfbs_batch_region_ext(bb, m.first, m.second, &in.R.es, &in.R.ee);
             if (rc) return err = tfbs_last_error(), rc;
             std::string ref;
-            rc = fasta.fetch(chrom, in.R.es, in.R.ee + 1, ref);  // main.rs:156-161
+            rc = fasta.fetch(S.chrom, in.R.es, in.R.ee + 1, ref);  // main.rs:156-161
             if (rc) return err = tfbs_last_error(), rc;
             in.ref.resize(ref.size());
             for (size_t i = 0; i < ref.size(); i++) {
@@ -183,53 +132,47 @@ int tfbs_run(const tfbs_run_args *a) {
                 in.ref[i] = (uint8_t)c;
             }
             // select_inner_peaks (main.rs:62-72): p.overlaps(merged)
-            for (size_t bi = 0; bi < beds.size(); bi++)
-                for (auto &p : beds[bi].second) {
+            for (size_t bi = 0; bi < S.beds.size(); bi++)
+                for (auto &p : S.beds[bi].second) {
                     const bool ov = (m.first >= p.first && m.first <= p.second) ||
                                     (m.second >= p.first && m.second <= p.second);
                     if (ov) in.inner.push_back({(uint32_t)bi, {p.first, p.second}});
                 }
             // load_diffs (haplotype.rs:78-80): name2rid(chrom).unwrap() panics on an unknown contig
             if (rid < 0) {
-                err = "chromosome " + chrom + " not in the BCF header";
+                err = "chromosome " + S.chrom + " not in the BCF header";
                 return TFBS_E_ARG;
             }
             if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
             for (const BcfRecord *br : recs) {
                 Record rec;
-                rc = make_record_gt((uint32_t)sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
+                rc = make_record_gt((uint32_t)S.sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
                                     br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->gt.data(), rec);
                 if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
             ins.push_back(std::move(in));
         }
-        rc = add_regions(B, ins, threads);
+        rc = add_regions(B, ins, sh.threads);
         if (rc) return err = tfbs_last_error(), rc;
         return TFBS_OK;
     };
-    // per-phase wall time (TFBS_RUN_TIMING=1 prints it to stderr)
-    const bool timing = getenv("TFBS_RUN_TIMING") && atoi(getenv("TFBS_RUN_TIMING"));
-    double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0, t_write = 0;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    const double t_start = now();
     BatchPtr cur(nullptr, tfbs_batch_destroy);
     std::string err;
-    if (!merged.empty()) {
-        double t0 = now();
-        if ((rc = prepare(0, cur, err))) return fail(rc, err);
-        t_prep += now() - t0;
-    }
-    for (size_t r0 = 0; r0 < merged.size(); r0 += per_batch) {
+    double t0 = now();
+    if ((rc = prepare(sh.r0, cur, err))) return fail(rc, err);
+    sh.t_prep += now() - t0;
+    for (size_t b0 = sh.r0; b0 < sh.r1; b0 += S.per_batch) {
         BatchPtr next(nullptr, tfbs_batch_destroy);
         std::string nerr;
         int nrc = TFBS_OK;
         double nprep = 0;
         std::thread helper;
-        if (r0 + per_batch < merged.size())
-            helper = std::thread([&, r0] {
+        if (b0 + S.per_batch < sh.r1)
+            helper = std::thread([&, b0] {
                 const double t0 = now();
-                nrc = prepare(r0 + per_batch, next, nerr);
+                nrc = prepare(b0 + S.per_batch, next, nerr);
                 nprep = now() - t0;
             });
         // join the helper on every exit path
@@ -241,41 +184,230 @@ int tfbs_run(const tfbs_run_args *a) {
         } joiner{helper};
         tfbs_batch *bb = cur.get();
         Batch &B = bb->b;
-        double t0 = now();
+        t0 = now();
         if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)))
             return rc;
         double t1 = now();
-        t_gpu += t1 - t0;
-        std::string rows;
-        rc = batch_rows(B, chrom, a->min_maf, &fake, rows, threads);
-        if (rc) return rc;
+        sh.t_gpu += t1 - t0;
+        std::string bodies;
+        if ((rc = batch_row_bodies(B, a->min_maf, bodies, sh.threads))) return rc;
         double t2 = now();
-        t_rows += t2 - t1;
-        rc = w.write(rows.data(), rows.size());
-        if (rc) return rc;
-        t_write += now() - t2;
+        sh.t_rows += t2 - t1;
+        if ((rc = emit(bodies))) return rc;
+        sh.t_emit += now() - t2;
         if (a->verbose) {
             for (size_t r = 0; r < B.rh.size(); r++)
-                fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", r0 + r + 1, merged.size(),
+                fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", b0 + r + 1, S.merged.size(),
                         (unsigned long long)B.rh[r].ms, (unsigned long long)B.rh[r].me, B.rh[r].hap_count,
                         B.rh[r].n_variants);
         }
         t0 = now();
         if (helper.joinable()) helper.join();
-        t_wait += now() - t0;
-        t_prep += nprep;
+        sh.t_wait += now() - t0;
+        sh.t_prep += nprep;
         if (nrc) return fail(nrc, nerr);
         cur = std::move(next);
     }
+    return TFBS_OK;
+}
+
+// "<chr>\t<POS>\t" before every row body, POS counted by *fake (main.rs:415-429)
+int write_prefixed(tfbs::BgzfWriter &w, const std::string &chr, const char *p, size_t n, uint32_t *fake) {
+    std::string out;
+    out.reserve(n + 64);
+    char head[32];
+    for (size_t i = 0; i < n;) {
+        const char *nl = (const char *)memchr(p + i, '\n', n - i);
+        const size_t e = nl ? (size_t)(nl - p) + 1 : n;
+        const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
+        out += chr;
+        out.append(head, (size_t)m);
+        out.append(p + i, e - i);
+        (*fake)++;
+        i = e;
+        if (out.size() >= (8u << 20)) {
+            if (int rc = w.write(out.data(), out.size())) return rc;
+            out.clear();
+        }
+    }
+    return w.write(out.data(), out.size());
+}
+
+std::vector<int> parse_devices(const tfbs_run_args *a) {
+    std::vector<int> d;
+    if (a->devices && *a->devices)
+        for (auto &x : split(a->devices, ','))
+            if (!x.empty()) d.push_back(atoi(x.c_str()));
+    if (d.empty()) d.push_back(a->device);
+    return d;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfbs_run(const tfbs_run_args *a) {
+    using namespace tfbs;
+    if (!a || !a->chromosome || !a->bcf || !a->bed_files || !a->reference || !a->pwm_file || !a->pwm_threshold_dir ||
+        !a->pwm_names || !a->output)
+        return fail(TFBS_E_ARG, "missing required argument");
+    RunSetup S;
+    S.a = a;
+    S.chrom = a->chromosome;
+    if (a->tabix && (!in_path("bgzip") || !in_path("tabix")))
+        return fail(TFBS_E_IO, "bgzip/tabix cannot be found in PATH");  // main.rs:220-223
+
+    // patterns (main.rs:237-250)
+    int rc = tfbs_patterns_from_files(a->pwm_file, a->pwm_threshold_dir, a->pwm_threshold, a->pwm_names,
+                                      a->forward_only ? 0 : 1, &S.pp);
+    if (rc) return rc;
+    std::unique_ptr<tfbs_patterns, void (*)(tfbs_patterns *)> pguard(S.pp, tfbs_patterns_destroy);
+
+    // BED sources (bed.rs:25-47): keyed by path (a repeated path counts once), merged
+    // over all of them, inner peaks keyed by basename (a later file with the same
+    // basename replaces an earlier one).
+    std::vector<std::string> paths;
+    for (auto &b : split(a->bed_files, ','))
+        if (std::find(paths.begin(), paths.end(), b) == paths.end()) paths.push_back(b);
+    std::vector<std::pair<uint64_t, uint64_t>> all;
+    for (auto &path : paths) {
+        struct stat st;
+        if (stat(path.c_str(), &st) != 0) return fail(TFBS_E_IO, "Bed file " + path + " does not exist");
+        std::vector<std::pair<uint64_t, uint64_t>> peaks, kept;
+        rc = load_bed(path, S.chrom, peaks);
+        if (rc) return rc;
+        for (auto &p : peaks)
+            if (p.first >= a->after_position) kept.push_back(p);
+        all.insert(all.end(), kept.begin(), kept.end());
+        const std::string bn = basename_of(path);
+        bool replaced = false;
+        for (auto &b : S.beds)
+            if (b.first == bn) { b.second = kept; replaced = true; }
+        if (!replaced) S.beds.push_back({bn, kept});
+    }
+    S.merged = merge_ranges(all);
+
+    // BCF header + samples (main.rs:255, 293-314)
+    std::vector<std::string> sample_names;
+    {
+        Bcf hdr;
+        if ((rc = hdr.open(a->bcf, 1))) return rc;
+        sample_names = hdr.samples;
+    }
+    if (a->samples_file && *a->samples_file) {
+        std::ifstream sf(a->samples_file);
+        if (!sf) return fail(TFBS_E_IO, std::string("Could not open sample file ") + a->samples_file);
+        std::set<std::string> want;
+        std::string l;
+        while (std::getline(sf, l))
+            if (l.size() > 1) want.insert(l);
+        for (size_t i = 0; i < sample_names.size(); i++)
+            if (want.count(sample_names[i])) S.sel.push_back(i);
+    } else {
+        for (size_t i = 0; i < sample_names.size(); i++) S.sel.push_back(i);
+    }
+    {
+        Fasta fasta;  // main.rs:259: the reference opens it before any region
+        if ((rc = fasta.open(a->reference))) return rc;
+    }
+
+    // output (main.rs:264-290, 320-324)
+    const std::string out = a->output, part = out + ".part";
+    BgzfWriter w;
+    const uint32_t threads = std::max(1u, a->threads);
+    rc = w.open(part, threads);
+    if (rc) return rc;
+    std::string header = "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT";
+    for (size_t i : S.sel) header += "\t" + sample_names[i];
+    header += "\n";
+    rc = w.write(header.data(), header.size());
+    if (rc) return rc;
+
+    // shards: one contiguous block of merged regions per device
+    S.per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
+    const std::vector<int> devs = parse_devices(a);
+    const size_t n_sh = std::max<size_t>(1, std::min(devs.size(), S.merged.size()));
+    std::vector<Shard> shards(n_sh);
+    for (size_t k = 0; k < n_sh; k++) {
+        shards[k].r0 = k * S.merged.size() / n_sh;
+        shards[k].r1 = (k + 1) * S.merged.size() / n_sh;
+        shards[k].device = devs[k];
+        shards[k].threads = std::max<uint32_t>(1, threads / (uint32_t)n_sh);
+    }
+    const std::string chr = strip_chr(S.chrom);
+    uint32_t fake = 1;
+    const bool timing = getenv("TFBS_RUN_TIMING") && atoi(getenv("TFBS_RUN_TIMING"));
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
+    // shard 0 writes straight through the writer; the others spill their row
+    // bodies to <output>.part.<k> and are appended in order afterwards
+    std::vector<std::string> spill_path(n_sh);
+    std::vector<FILE *> spill(n_sh, nullptr);
+    struct SpillGuard {
+        std::vector<FILE *> &f;
+        std::vector<std::string> &p;
+        ~SpillGuard() {
+            for (size_t k = 0; k < f.size(); k++) {
+                if (f[k]) fclose(f[k]);
+                if (!p[k].empty()) remove(p[k].c_str());
+            }
+        }
+    } spill_guard{spill, spill_path};
+    for (size_t k = 1; k < n_sh; k++) {
+        spill_path[k] = part + "." + std::to_string(k);
+        spill[k] = fopen(spill_path[k].c_str(), "w+b");
+        if (!spill[k]) return fail(TFBS_E_IO, "Could not create " + spill_path[k]);
+    }
+    auto run_one = [&](size_t k) {
+        Shard &sh = shards[k];
+        auto emit = [&](const std::string &bodies) -> int {
+            if (k == 0) return write_prefixed(w, chr, bodies.data(), bodies.size(), &fake);
+            if (!bodies.empty() && fwrite(bodies.data(), 1, bodies.size(), spill[k]) != bodies.size())
+                return fail(TFBS_E_IO, "write failed: " + spill_path[k]);
+            return TFBS_OK;
+        };
+        sh.rc = run_shard(S, sh, emit);
+        if (sh.rc) sh.err = tfbs_last_error();
+    };
+    {
+        std::vector<std::thread> ts;
+        for (size_t k = 1; k < n_sh; k++) ts.emplace_back(run_one, k);
+        run_one(0);
+        for (auto &t : ts) t.join();
+    }
+    for (auto &sh : shards)
+        if (sh.rc) return fail(sh.rc, sh.err);
+    double t_cat = now();
+    {
+        std::vector<char> buf(16u << 20);
+        std::string carry;
+        for (size_t k = 1; k < n_sh; k++) {
+            if (fflush(spill[k]) != 0 || fseek(spill[k], 0, SEEK_SET) != 0)
+                return fail(TFBS_E_IO, "read failed: " + spill_path[k]);
+            carry.clear();
+            for (size_t got; (got = fread(buf.data(), 1, buf.size(), spill[k])) > 0;) {
+                carry.append(buf.data(), got);
+                const size_t cut = carry.rfind('\n');
+                if (cut == std::string::npos) continue;
+                if ((rc = write_prefixed(w, chr, carry.data(), cut + 1, &fake))) return rc;
+                carry.erase(0, cut + 1);
+            }
+            if (!carry.empty() && (rc = write_prefixed(w, chr, carry.data(), carry.size(), &fake))) return rc;
+        }
+    }
+    t_cat = now() - t_cat;
     // the reference flushes twice before drop (main.rs:271, 275): two empty blocks
     double t0 = now();
     if ((rc = w.flush()) || (rc = w.flush()) || (rc = w.close())) return rc;
-    t_write += now() - t0;
+    const double t_close = now() - t0;
     if (timing)
-        fprintf(stderr,
-                "tfbs_run_timing {\"prep_s\": %.4f, \"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, "
-                "\"write_s\": %.4f, \"loop_s\": %.4f}\n",
-                t_prep, t_wait, t_gpu, t_rows, t_write, now() - t_start);
+        for (size_t k = 0; k < n_sh; k++)
+            fprintf(stderr,
+                    "tfbs_run_timing {\"shard\": %zu, \"device\": %d, \"regions\": %zu, \"prep_s\": %.4f, "
+                    "\"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, \"write_s\": %.4f, \"concat_s\": %.4f, "
+                    "\"close_s\": %.4f, \"loop_s\": %.4f}\n",
+                    k, shards[k].device, shards[k].r1 - shards[k].r0, shards[k].t_prep, shards[k].t_wait,
+                    shards[k].t_gpu, shards[k].t_rows, shards[k].t_emit, t_cat, t_close, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +
                                 part + "'";

@@ -36,6 +36,7 @@ constexpr int kUnitMax = 8;        // strands per unit (octet)
 constexpr int kFastMaxLen = 32;    // the LUT path reads a 64-bit (32-base) window per lane
 constexpr int kMaxInnerPass = 8;   // inner ranges handled per pass (accumulators per lane)
 constexpr int kMaxTileSlots = 64;  // pattern_id slots per tile: one lane each
+constexpr uint32_t kMaxHapLen = 1u << 29;  // haplotype bases: window starts fit the kernels' 29-bit fields
 
 enum UnitKind : uint32_t {
     // 8 strands, int16 partial sums biased to <= 0 per block, saturating packed adds:

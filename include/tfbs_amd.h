@@ -230,6 +230,15 @@ int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t
  * tfbs_free); *fake_position is the POS counter, advanced per row. */
 int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t *fake_position,
                     char **text, size_t *len);
+/* The rows of one region (main.rs:415-429 for one process_peak call), same
+ * format and POS handling as tfbs_batch_rows. */
+int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chromosome, uint32_t min_maf,
+                           uint32_t *fake_position, char **text, size_t *len);
+/* 64-bit digest of one region's keys at the distinct-haplotype level (key
+ * identity in row order + every distinct haplotype's count): equal digests
+ * from the dense download and the device reduction, or from a sharded and an
+ * unsharded batch, mean equal count_matches_by_sample maps (main.rs:500-534). */
+int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
 /* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
 int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
 void tfbs_free(void *p);
@@ -259,10 +268,19 @@ typedef struct tfbs_run_args {
     uint64_t after_position;       /* --after_position */
     int tabix;                     /* --tabix */
     int verbose;                   /* --verbose */
-    int device;                    /* HIP device */
+    int device;                    /* HIP device (when devices is NULL/empty) */
     uint32_t regions_per_batch;    /* merged regions per GPU batch (0 = 512) */
+    const char *devices;           /* comma list of HIP devices, one region shard each ("0,1,2,3";
+                                      a device may repeat); NULL/"" = just `device` */
 } tfbs_run_args;
-/* Replaces run() (main.rs:234-393): writes <output>.part, renames it to output. */
+/* Replaces run() (main.rs:234-393): writes <output>.part, renames it to output.
+ * Several devices: the merged regions are cut into one
+ * contiguous block per device (the reference's 50-peak chunks over worker
+ * threads, main.rs:332-381, made static); each block runs its own pipeline
+ * (BCF reader -- CSI-indexed seek when <bcf>.csi exists --, FASTA reader,
+ * host prep thread, ctx on its device, row formatting) and the rows are
+ * concatenated in merged-peak order with POS renumbered, so the output text
+ * is identical for any device list. */
 int tfbs_run(const tfbs_run_args *args);
 
 typedef struct tfbs_bcf tfbs_bcf;

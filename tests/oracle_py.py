@@ -289,6 +289,23 @@ class Job:
             out[(self.bed_names[b.value], (s.value, e.value), pid.value)] = (list(l[:n]), list(r[:n]))
         return out
 
+    def keys_np(self):
+        """keys() with numpy uint32 vectors (large sample counts)."""
+        import numpy as np
+        out = {}
+        n = self.nsamp
+        for i in range(self.L.orc_job_nkeys(self.h)):
+            b, s, e, pid = C.c_int(), C.c_uint64(), C.c_uint64(), C.c_int()
+            l = np.zeros(max(1, n), dtype=np.uint32)
+            r = np.zeros(max(1, n), dtype=np.uint32)
+            self.L.orc_job_key(self.h, i, C.byref(b), C.byref(s), C.byref(e), C.byref(pid),
+                               l.ctypes.data_as(u32p), r.ctypes.data_as(u32p))
+            out[(self.bed_names[b.value], (s.value, e.value), pid.value)] = (l[:n], r[:n])
+        return out
+
+    def clear_rows(self):
+        self.L.orc_job_clear_rows(self.h)
+
     def stats(self):
         a, b, c = C.c_int(), C.c_int(), C.c_uint64()
         self.L.orc_job_stats(self.h, C.byref(a), C.byref(b), C.byref(c))

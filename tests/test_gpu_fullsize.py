@@ -1,0 +1,242 @@
+"""GPU parity at the BASELINE.json sizes.
+
+The batch the bench times is scanned here exactly as bench.py builds it (same
+generator, seeds, PWM sets and thresholds), and checked three ways:
+
+* against the oracle (oracle/tfbs_oracle.c, the C restatement of main.rs:94-154,
+  500-534 and 439-498): every region of C2, and for C3/C5 a deterministic spread
+  of >= 200 regions (first, last, the last haplotype group, evenly spaced ones)
+  key by key -- the per-sample L/R vectors of count_matches_by_sample -- and
+  row by row (POS aside: the oracle numbers rows over its own region subset);
+* device key reduction (the run flow's tfbs_batch_reduce) against the dense
+  count download over the WHOLE batch, region by region, through
+  tfbs_batch_region_digest (keys + every distinct haplotype's count);
+* C4: 100 000 regions scanned as one batch (a 28 GB count matrix: u64 count
+  offsets) and as 8 static region shards of 12 500 (the multi-GPU partition,
+  SURVEY.md 8(e)), run one after the other on this GPU: identical digests for
+  every region, and the oracle on a spread of regions of every shard.
+
+C2/C3 carry no N in the reference (the generator draws ACGT only); the C3
+batch gets extra regions whose reference holds N runs (appended after the
+generator's regions, so they sit in the last haplotype groups).
+"""
+import concurrent.futures as cf
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+from helpers import T, pattern_dicts
+
+pytestmark = pytest.mark.gpu
+
+# workload: (samples, regions, pwms, length_config, indel_pct, seed) -- SURVEY.md 8(d)
+C2 = (1000, 1000, 10, 2, 0, 2)
+C3 = (50000, 10000, 600, 3, 0, 3)
+C4 = (50000, 100000, 600, 3, 0, 4)
+C5 = (50000, 10000, 600, 5, 30, 5)
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if T.device_count() == 0:
+        pytest.fail("gpu test without a visible HIP device")
+
+
+def _patterns(tmp, cfg):
+    n_samples, n_regions, n_pwms, lc, indel, seed = cfg
+    names = T.synth_write_pwms(str(tmp), n_pwms, lc, seed)
+    return T.parse_pwm_files(os.path.join(str(tmp), "pwms.txt"), os.path.join(str(tmp), "thr"), 1e-4, names)
+
+
+def _n_regions(seed, first, count, n_samples, lmax, indel):
+    """Regions after the generator's: its region + N runs in the reference (none over
+    a variant's REF bases, which patch_haplotype checks, haplotype.rs:119-128)."""
+    out = []
+    for j in range(first, first + count):
+        r = T.SynthRegion(seed, j, n_samples, lmax, indel)
+        ref = list(r.ref)
+        busy = set()
+        for pos, rf, _, _ in r.records:
+            busy.update(range(pos - r.ext_start, pos - r.ext_start + len(rf)))
+        k = j - first
+        for a, z in [(3 + 7 * k, 6 + 7 * k), (100 + k, 101 + k), (len(ref) - 9, len(ref) - 5)]:
+            for i in range(a, min(z, len(ref))):
+                if i not in busy:
+                    ref[i] = "N"
+        out.append({"merged": r.merged, "ref": "".join(ref), "records": r.records})
+    return out
+
+
+def _append_regions(b, regions):
+    bed = b.beds.index("synthetic.bed")
+    for reg in regions:
+        s, e = reg["merged"]
+        b.begin(s, e, reg["ref"])
+        b.add_inner(bed, s, e)
+        for pos, ref, alt, car in reg["records"]:
+            b.add_record_carriers(pos, ref, alt, car)
+        b.end()
+
+
+def _strip_pos(rows):
+    out = []
+    for line in rows.splitlines():
+        f = line.split("\t", 2)
+        out.append(f[0] + "\t" + f[2])
+    return out
+
+
+def _oracle_regions(ps, n_samples, seed, indel, jobs):
+    """jobs: [(product region index, merged, ref, records)] -> {index: (keys, rows)} on
+    host threads (ctypes drops the GIL), one oracle Job per thread."""
+    pats = pattern_dicts(ps)
+    ranges = sorted({tuple(j[1]) for j in jobs})
+
+    def work(chunk):
+        job = O.Job(n_samples, "chr1", pats, [("synthetic.bed", ranges)])
+        res = {}
+        try:
+            for idx, merged, ref, recs in chunk:
+                assert job.begin(merged[0], merged[1], ref) == 0
+                for pos, rf, alt, car in recs:
+                    assert job.add_record_carriers(pos, rf, alt, car) == 0
+                assert job.end() == 0
+                res[idx] = (job.keys_np(), _strip_pos(job.rows()))
+                job.clear_rows()
+        finally:
+            job.close()
+        return res
+
+    n = max(1, min(THREADS, len(jobs)))
+    chunks = [jobs[i::n] for i in range(n)]
+    out = {}
+    with cf.ThreadPoolExecutor(n) as ex:
+        for r in ex.map(work, chunks):
+            out.update(r)
+    return out
+
+
+def _synth_jobs(seed, indices, n_samples, lmax, indel):
+    jobs = []
+    for j in indices:
+        r = T.SynthRegion(seed, j, n_samples, lmax, indel)
+        jobs.append((j, r.merged, r.ref, r.records))
+    return jobs
+
+
+def _check_vs_oracle(b, ref, label):
+    """b: scanned batch (counts present); ref: {region: (oracle keys, oracle rows)}."""
+    n_rows = 0
+    for idx in sorted(ref):
+        okeys, orows = ref[idx]
+        pkeys = b.keys_np(idx)
+        assert pkeys.keys() == okeys.keys(), (label, idx)
+        for k in okeys:
+            assert np.array_equal(pkeys[k][0], okeys[k][0]) and np.array_equal(pkeys[k][1], okeys[k][1]), \
+                (label, idx, k)
+        prows = _strip_pos(b.region_rows(idx, "chr1")[0])
+        assert prows == orows, (label, idx)
+        n_rows += len(prows)
+    return n_rows
+
+
+def _spread(n, count):
+    """~count region indices over [0, n): both ends, the last haplotype groups, even spacing."""
+    idx = set(range(0, 8)) | set(range(max(0, n - 12), n))
+    step = max(1, n // max(1, count - len(idx)))
+    idx |= set(range(0, n, step))
+    return sorted(i for i in idx if i < n)
+
+
+def _digests(b):
+    return [b.digest(r) for r in range(b.num_regions)]
+
+
+def _fullsize(tmp_path, cfg, n_check, n_extra_n=0):
+    n_samples, n_regions, _, _, indel, seed = cfg
+    ps = _patterns(tmp_path, cfg)
+    lmax = ps.max_length
+    b = T.RegionBatch(ps, n_samples)
+    b.synth_fill(seed, 0, n_regions, indel)
+    extra = _n_regions(seed, n_regions, n_extra_n, n_samples, lmax, indel) if n_extra_n else []
+    _append_regions(b, extra)
+    assert b.num_regions == n_regions + n_extra_n
+    sc = T.Scanner(ps)
+    try:
+        # the run flow's path: device key reduction
+        b.scan(sc, reduce=True)
+        reduced = _digests(b)
+        check = _spread(n_regions, n_check) if n_check < n_regions else list(range(n_regions))
+        jobs = _synth_jobs(seed, check, n_samples, lmax, indel)
+        jobs += [(n_regions + k, r["merged"], r["ref"], r["records"]) for k, r in enumerate(extra)]
+        ref = _oracle_regions(ps, n_samples, seed, indel, jobs)
+        n_rows = _check_vs_oracle(b, ref, "reduce")
+        # dense download over the same batch, rescanned
+        b.scan(sc, upload=False, download=True)
+        assert _digests(b) == reduced
+        _check_vs_oracle(b, {i: ref[i] for i in list(ref)[:24]}, "dense")
+    finally:
+        sc.close()
+    return b, n_rows, len(ref)
+
+
+def test_c2_full_vs_oracle(tmp_path):
+    """C2 in full: 1 000 samples x 1 000 regions x 10 PWMs, every region vs the oracle."""
+    b, n_rows, n_checked = _fullsize(tmp_path, C2, C2[1])
+    assert n_checked == C2[1] and n_rows > 100
+
+
+def test_c3_full_batch_vs_oracle(tmp_path):
+    """C3 as bench.py times it (50 000 samples, 10 000 regions, 600 PWMs = 1 200 strands,
+    ~1.18 M distinct haplotypes, one batch), plus 6 regions with N runs at its end."""
+    b, n_rows, n_checked = _fullsize(tmp_path, C3, 200, n_extra_n=6)
+    assert n_checked >= 200 and n_rows > 0
+    assert b.num_haplotypes > 1_000_000
+
+
+def test_c5_full_batch_vs_oracle(tmp_path):
+    """C5: C3 with 30 % indels (non-affine positions, variable-length haplotypes) and
+    PWMs of length 25-30 (K depth 2 of the matrix-core kernel)."""
+    b, n_rows, n_checked = _fullsize(tmp_path, C5, 200, n_extra_n=4)
+    assert n_checked >= 200 and n_rows > 0
+
+
+def test_c4_shards_equal_unsharded(tmp_path):
+    """C4: 100 000 regions as one batch vs 8 static shards of 12 500 (the multi-GPU
+    partition, one after the other on this GPU): identical digests region by region;
+    the oracle on a spread of every shard's regions."""
+    n_samples, n_regions, _, _, indel, seed = C4
+    ps = _patterns(tmp_path, C4)
+    lmax = ps.max_length
+    sc = T.Scanner(ps)
+    try:
+        whole = T.RegionBatch(ps, n_samples, keep_membership=False)
+        whole.synth_fill(seed, 0, n_regions, indel)
+        whole.scan(sc, reduce=True)
+        want = _digests(whole)
+        del whole
+        n_shards = 8
+        got, checked = [], 0
+        for k in range(n_shards):
+            r0, r1 = k * n_regions // n_shards, (k + 1) * n_regions // n_shards
+            b = T.RegionBatch(ps, n_samples)
+            b.synth_fill(seed, r0, r1 - r0, indel)
+            b.scan(sc, reduce=True)
+            got += _digests(b)
+            local = [0, (r1 - r0) // 2, r1 - r0 - 1] + list(range(3, r1 - r0, (r1 - r0) // 5))
+            jobs = [(i, m, rf, rc) for (i, m, rf, rc) in _synth_jobs(seed, [r0 + i for i in local], n_samples, lmax,
+                                                                      indel)]
+            jobs = [(i - r0, m, rf, rc) for (i, m, rf, rc) in jobs]
+            ref = _oracle_regions(ps, n_samples, seed, indel, jobs)
+            _check_vs_oracle(b, ref, "shard%d" % k)
+            checked += len(ref)
+            del b
+        assert len(got) == len(want)
+        bad = [i for i in range(n_regions) if got[i] != want[i]]
+        assert not bad, bad[:10]
+        assert checked >= 40
+    finally:
+        sc.close()
