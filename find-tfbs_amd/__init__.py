@@ -523,6 +523,7 @@ class BcfReader:
         n = lib().tfbs_bcf_num_samples(self.h)
         self.samples = [lib().tfbs_bcf_sample_name(self.h, i).decode() for i in range(n)]
         self.selected = list(range(n))
+        self.indexed = bool(lib().tfbs_bcf_indexed(self.h))
 
     def select(self, idx):
         """Decode GT only for these sample indices, in this order."""

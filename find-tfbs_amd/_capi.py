@@ -114,6 +114,7 @@ SIGNATURES = [
     ("tfbs_bcf_close", None, [vp]),
     ("tfbs_bcf_select", C.c_int, [vp, C.POINTER(C.c_size_t), C.c_size_t]),
     ("tfbs_bcf_num_samples", C.c_size_t, [vp]),
+    ("tfbs_bcf_indexed", C.c_int, [vp]),
     ("tfbs_bcf_sample_name", C.c_char_p, [vp, C.c_size_t]),
     ("tfbs_bcf_fetch", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_size_t)]),
     ("tfbs_bcf_record", C.c_int, [vp, C.c_size_t, u64p, u32p, u32p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),

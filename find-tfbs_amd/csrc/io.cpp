@@ -356,6 +356,7 @@ int Bcf::open(const std::string &p, uint32_t nthreads) {
     if (const char *e = getenv("TFBS_BCF_CHUNK_KB")) chunk = std::max<size_t>(1, (size_t)atoll(e)) << 10;
     int rc = rewind();
     if (rc) return rc;
+    if ((rc = load_csi())) return rc;
     sel.resize(samples.size());
     for (size_t i = 0; i < sel.size(); i++) sel[i] = i;
     all_samples = true;
@@ -409,6 +410,93 @@ int Bcf::rewind() {
         contigs = std::move(c);
     }
     doff = 9 + l_text;
+    return TFBS_OK;
+}
+
+// CSI (htslib's coordinate-sorted index, SAM/VCF index spec): BGZF-compressed
+// "CSI\1", min_shift, depth, aux, then per reference its bins (bin, loffset,
+// chunks of [begin, end) virtual offsets).  Only the chunk starts are kept, as
+// (bin end, start) per bin, suffix-minimised over bins sorted by end: every
+// record with pos + rlen > beg sits in a chunk of a bin that ends after beg.
+int Bcf::load_csi() {
+    csi.clear();
+    std::string raw, txt;
+    {
+        std::ifstream in(path + ".csi", std::ios::binary);
+        if (!in || !bgzf) return TFBS_OK;  // no index: sweep from the start
+        std::stringstream ss;
+        ss << in.rdbuf();
+        raw = ss.str();
+    }
+    if (int rc = bgzf_inflate(raw, txt)) return rc;
+    const unsigned char *p = (const unsigned char *)txt.data(), *e = p + txt.size();
+    auto rd = [&](void *dst, size_t n) {
+        if ((size_t)(e - p) < n) return false;
+        memcpy(dst, p, n);
+        p += n;
+        return true;
+    };
+    char magic[4];
+    int32_t min_shift, depth, l_aux, n_ref;
+    if (!rd(magic, 4) || memcmp(magic, "CSI\1", 4) != 0 || !rd(&min_shift, 4) || !rd(&depth, 4) || !rd(&l_aux, 4) ||
+        min_shift < 0 || depth < 0 || min_shift + 3 * depth > 62 || l_aux < 0 || (size_t)(e - p) < (size_t)l_aux)
+        return fail(TFBS_E_PARSE, "bad CSI index " + path + ".csi");
+    p += l_aux;
+    if (!rd(&n_ref, 4) || n_ref < 0) return fail(TFBS_E_PARSE, "bad CSI index " + path + ".csi");
+    const uint64_t n_bins_valid = ((1ull << (3 * (depth + 1))) - 1) / 7;  // bins above are pseudo-bins
+    csi.resize((size_t)n_ref);
+    for (int32_t r = 0; r < n_ref; r++) {
+        int32_t n_bin;
+        if (!rd(&n_bin, 4) || n_bin < 0) return fail(TFBS_E_PARSE, "bad CSI index " + path + ".csi");
+        auto &bins = csi[r];
+        for (int32_t i = 0; i < n_bin; i++) {
+            uint32_t bin;
+            uint64_t loff;
+            int32_t n_chunk;
+            if (!rd(&bin, 4) || !rd(&loff, 8) || !rd(&n_chunk, 4) || n_chunk < 0)
+                return fail(TFBS_E_PARSE, "bad CSI index " + path + ".csi");
+            uint64_t lo = UINT64_MAX;
+            for (int32_t c = 0; c < n_chunk; c++) {
+                uint64_t cb, ce;
+                if (!rd(&cb, 8) || !rd(&ce, 8)) return fail(TFBS_E_PARSE, "bad CSI index " + path + ".csi");
+                lo = std::min(lo, cb);
+            }
+            if (bin >= n_bins_valid || lo == UINT64_MAX) continue;
+            int level = 0;
+            while (level < depth && bin >= ((1ull << (3 * (level + 1))) - 1) / 7) level++;
+            const uint64_t first = ((1ull << (3 * level)) - 1) / 7;
+            const int shift = min_shift + 3 * (depth - level);
+            bins.push_back({(bin - first + 1) << shift, lo});
+        }
+        std::sort(bins.begin(), bins.end());
+        for (size_t i = bins.size(); i-- > 1;) bins[i - 1].second = std::min(bins[i - 1].second, bins[i].second);
+    }
+    if (csi.size() < contigs.size()) csi.resize(contigs.size());
+    return TFBS_OK;
+}
+
+uint64_t Bcf::csi_start(int contig, uint64_t beg) const {
+    if (csi.empty()) return 0;
+    const auto &bins = csi[(size_t)contig];
+    auto it = std::upper_bound(bins.begin(), bins.end(), std::make_pair(beg, UINT64_MAX));
+    return it == bins.end() ? UINT64_MAX : it->second;
+}
+
+// Restart the stream at virtual offset voff (block at voff >> 16, byte voff & 0xFFFF of it).
+int Bcf::seek(int contig, uint64_t voff) {
+    if (fseeko(f, (off_t)(voff >> 16), SEEK_SET) != 0) return fail(TFBS_E_IO, "seek failed in " + path);
+    cbuf.clear();
+    dbuf.clear();
+    doff = 0;
+    in_eof = done = seen = false;
+    win.clear();
+    last_pos = 0;
+    cur = contig;
+    const size_t u = (size_t)(voff & 0xFFFF);
+    while (dbuf.size() < u && !in_eof)
+        if (int rc = inflate_more()) return rc;
+    if (dbuf.size() < u) return fail(TFBS_E_PARSE, "CSI offset past the end of " + path);
+    doff = u;
     return TFBS_OK;
 }
 
@@ -550,7 +638,23 @@ int Bcf::contig_index(const std::string &name) const {
 int Bcf::fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out) {
     out.clear();
     if (contig < 0 || (size_t)contig >= contigs.size()) return TFBS_OK;
-    if (contig != cur || beg < last_beg) {
+    const bool back = contig != cur || beg < last_beg;
+    if (indexed()) {
+        // seek when the sweep would rewind, or when the query's first record lies
+        // past everything read so far (a sparse BED over a large file)
+        const uint64_t v = csi_start(contig, beg);
+        if (v == UINT64_MAX) {  // nothing on this contig ends after beg
+            win.clear();
+            cur = contig;
+            done = true;
+            last_beg = beg;
+            return TFBS_OK;
+        }
+        const off_t fpos = ftello(f);
+        if (back || (fpos >= 0 && (v >> 16) > (uint64_t)fpos)) {
+            if (int rc = seek(contig, v)) return rc;
+        }
+    } else if (back) {
         if (int rc = rewind()) return rc;
         cur = contig;
     }

@@ -50,6 +50,10 @@ struct BcfRecord {
 // sorted merged regions) reads the file once; a query that goes backwards or
 // to another contig rewinds to the start of the file.  Input must be sorted
 // by position within a contig (an indexed BCF is); unsorted input fails.
+// With a CSI index (<path>.csi, as bcftools index writes it) a query that
+// would rewind, or whose first record lies beyond what has been read, seeks
+// to the index's chunk start instead (IndexedReader::fetch's seek); the
+// sweep itself is unchanged.
 class Bcf {
   public:
     int open(const std::string &path, uint32_t threads = 0);
@@ -62,10 +66,20 @@ class Bcf {
     ~Bcf();
     std::vector<std::string> samples, contigs;
 
+    bool indexed() const { return !csi.empty(); }
+
   private:
     int rewind();
     int inflate_more();
     int fill();
+    int load_csi();
+    // virtual offset to start reading for records with pos + rlen > beg on
+    // `contig` (the smallest chunk start of the CSI bins ending after beg);
+    // UINT64_MAX: no such record; 0 with no index.
+    uint64_t csi_start(int contig, uint64_t beg) const;
+    int seek(int contig, uint64_t voff);
+    // per contig: (bin end, smallest chunk start over this and every later entry)
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> csi;
     std::string path;
     FILE *f = nullptr;
     uint32_t threads = 1;

@@ -444,6 +444,7 @@ int tfbs_bcf_select(tfbs_bcf *b, const size_t *idx, size_t n) {
     return b->b.select(std::vector<size_t>(idx, idx + n));
 }
 size_t tfbs_bcf_num_samples(const tfbs_bcf *b) { return b ? b->b.samples.size() : 0; }
+int tfbs_bcf_indexed(const tfbs_bcf *b) { return b && b->b.indexed() ? 1 : 0; }
 const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i) {
     return (b && i < b->b.samples.size()) ? b->b.samples[i].c_str() : nullptr;
 }

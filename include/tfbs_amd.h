@@ -288,6 +288,9 @@ typedef struct tfbs_bcf tfbs_bcf;
 int tfbs_bcf_open(const char *path, tfbs_bcf **out);
 void tfbs_bcf_close(tfbs_bcf *b);
 size_t tfbs_bcf_num_samples(const tfbs_bcf *b);
+/* 1 if <path>.csi was loaded: fetches that would rewind or skip ahead seek to the
+ * index's chunk start (IndexedReader::fetch, haplotype.rs:78-79); 0 = streaming sweep. */
+int tfbs_bcf_indexed(const tfbs_bcf *b);
 const char *tfbs_bcf_sample_name(const tfbs_bcf *b, size_t i);
 /* Samples whose GT is decoded, in this order (default: all); main.rs:293-314's sample selection,
  * applied while decoding.  Rewinds the stream. */

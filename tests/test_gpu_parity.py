@@ -10,7 +10,7 @@ import random
 import pytest
 
 import oracle_py as O
-from helpers import GOLD, TD, T, make_regions_synth, run_oracle, run_product, synth_patterns
+from helpers import GOLD, TD, T, build_batch, make_regions_synth, run_oracle, run_product, synth_patterns
 
 pytestmark = pytest.mark.gpu
 
@@ -423,8 +423,9 @@ def test_many_variant_regions_vs_oracle(tmp_path):
     _compare(ps, n, beds, regions)
 
 
-@pytest.mark.parametrize("indel,per_batch,subset", [(0, 5, False), (25, 0, False), (10, 3, True)])
-def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset):
+@pytest.mark.parametrize("indel,per_batch,subset,index", [(0, 5, False, True), (25, 0, False, False),
+                                                          (10, 3, True, True)])
+def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset, index):
     """f2-f4 + the scan at a larger size than test_data: a synthetic BCF/FASTA/BED set
     (tools/synth_dataset.py) through tfbs_run (streaming BCF reader, batches of
     merged regions, device key reduction, BGZF writer) vs the oracle's run() on the
@@ -435,7 +436,7 @@ def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset)
     _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import synth_dataset
     d = synth_dataset.make_dataset(str(tmp_path / "data"), n_samples=80, n_regions=14, n_pwms=10,
-                                   length_config=2, seed=7, indel_pct=indel)
+                                   length_config=2, seed=7, indel_pct=indel, index=index)
     out = tmp_path / "out.vcf.gz"
     samples_file = os.path.join(d["dir"], "samples")
     wanted = d["samples"]
@@ -452,3 +453,75 @@ def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset)
                  d["pwm_file"], d["thr_dir"], 2e-3, d["names"])
     assert got == want
     assert got.count("\n") > 1  # some rows
+
+
+@pytest.mark.parametrize("index", [True, False])
+def test_run_devices_shards_same_text(tmp_path, index):
+    """Multi-device run flow: the merged regions cut into one block per
+    listed device, each with its own BCF reader (CSI seek to its block, or a sweep from
+    the file start), FASTA reader, prep thread and ctx; rows concatenated in merged-peak
+    order with POS renumbered.  2, 3 and 8 contexts on this one GPU give the text of a
+    single device, which equals the oracle's run()."""
+    import gzip
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path / "data"), n_samples=60, n_regions=37, n_pwms=12,
+                                   length_config=2, seed=8, indel_pct=15, index=index)
+    args = ("chr1", d["bcf"], [d["bed"]], d["fasta"], os.path.join(d["dir"], "samples"), d["pwm_file"],
+            d["thr_dir"], 2e-3, d["names"])
+    texts = []
+    for devs, per_batch in [(None, 4), ([0, 0], 4), ([0, 0, 0], 3), ([0] * 8, 2), ([0] * 16, 1)]:
+        out = tmp_path / ("out%d.vcf.gz" % len(texts))
+        T.run(*args, str(out), threads=4, regions_per_batch=per_batch, devices=devs)
+        texts.append(gzip.open(str(out), "rt").read())
+        assert not [f for f in os.listdir(str(tmp_path)) if ".part" in f]  # spills removed
+    assert all(t == texts[0] for t in texts[1:])
+    recs = [dict(r, gt=r["gt"].astype(int).tolist()) for r in d["records"]]
+    want = O.run("chr1", recs, [d["bed"]], d["fasta"], d["samples"], d["samples"], d["pwm_file"], d["thr_dir"],
+                 2e-3, d["names"])
+    assert texts[0] == want
+    assert want.count("\n") > 10
+
+
+def test_cli_gpus_and_devices(tmp_path):
+    """--gpus N / --devices LIST on the command line: same text as one device."""
+    import gzip
+    import subprocess
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path / "data"), n_samples=30, n_regions=12, n_pwms=6,
+                                   length_config=2, seed=5, indel_pct=10)
+    exe = os.path.join(os.path.dirname(T.__file__), "bin", "find-tfbs-amd")
+    texts = []
+    for extra in ([], ["--gpus", "1"], ["--devices", "0,0,0"]):
+        out = tmp_path / ("cli%d.vcf.gz" % len(texts))
+        r = subprocess.run([exe, "--chromosome", "chr1", "--input", d["bcf"], "--bed", d["bed"], "--reference",
+                            d["fasta"], "--pwm_file", d["pwm_file"], "--pwm_threshold_directory", d["thr_dir"],
+                            "--pwm_threshold", "0.002", "--pwm_names", ",".join(d["names"]), "--output", str(out),
+                            "--threads", "3", "--regions_per_batch", "2"] + extra,
+                           capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stderr
+        texts.append(gzip.open(str(out), "rt").read())
+    assert texts[0] == texts[1] == texts[2]
+    assert texts[0].count("\n") > 1
+
+
+def test_reduce_zero_samples_after_keys(tmp_path):
+    """A batch with no samples has no haplotype and no key (main.rs:500-534 counts
+    nothing), also when its ctx just reduced a batch with keys (reused device buffers)."""
+    ps, _ = synth_patterns(tmp_path, 8, 2, 41, thr=5e-3)
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(3)])]
+    sc = T.Scanner(ps)
+    try:
+        full = build_batch(ps, 30, beds, make_regions_synth(3, 0, 3, 30, ps.max_length))
+        full.scan(sc, reduce=True)
+        assert sum(len(full.keys(r)) for r in range(3)) > 0
+        empty = build_batch(ps, 0, beds, make_regions_synth(3, 0, 3, 0, ps.max_length))
+        empty.scan(sc, reduce=True)
+        for r in range(3):
+            assert empty.keys(r) == {}
+            assert empty.region_rows(r, "chr1")[0] == ""
+    finally:
+        sc.close()

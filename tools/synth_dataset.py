@@ -26,11 +26,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def bgzf_blocks(data):
-    """BGZF framing (SAM spec 4.1): <= 64 KiB-input deflate blocks + the EOF block."""
+BGZF_BLOCK = 65280
+
+
+def bgzf_blocks(data, block_offsets=None):
+    """BGZF framing (SAM spec 4.1): <= 64 KiB-input deflate blocks + the EOF block.
+    block_offsets (a list) receives each block's compressed file offset."""
     out = bytearray()
-    for i in range(0, len(data), 65280):
-        chunk = bytes(data[i:i + 65280])
+    for i in range(0, len(data), BGZF_BLOCK):
+        if block_offsets is not None:
+            block_offsets.append(len(out))
+        chunk = bytes(data[i:i + BGZF_BLOCK])
         co = zlib.compressobj(6, zlib.DEFLATED, -15)
         comp = co.compress(chunk) + co.flush()
         bsize = len(comp) + 25
@@ -39,6 +45,55 @@ def bgzf_blocks(data):
         out += struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
     out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
     return bytes(out)
+
+
+def reg2bin(beg, end, min_shift, depth):
+    """htslib hts_reg2bin: the smallest bin holding [beg, end)."""
+    end -= 1
+    s, t = min_shift, ((1 << (3 * depth)) - 1) // 7
+    for lev in range(depth, 0, -1):
+        if beg >> s == end >> s:
+            return t + (beg >> s)
+        s += 3
+        t -= 1 << (3 * (lev - 1))
+    return 0
+
+
+def csi_index(spans, block_offsets, contig_len, min_shift=14):
+    """A CSI index (htslib's format, as `bcftools index` writes it, without the
+    optional pseudo-bin) for one contig.  spans: per record in file order
+    (pos0, rlen, uncompressed start, uncompressed end) in the BGZF stream."""
+    max_len = contig_len + 256
+    depth, sz = 0, 1 << min_shift
+    while max_len > sz:
+        depth += 1
+        sz <<= 3
+
+    def voff(u):
+        k = u // BGZF_BLOCK
+        if k >= len(block_offsets):  # end of the last block
+            k = len(block_offsets) - 1
+            return (block_offsets[k] << 16) | (u - k * BGZF_BLOCK)
+        return (block_offsets[k] << 16) | (u % BGZF_BLOCK)
+
+    bins = {}
+    for pos0, rlen, u0, u1 in spans:
+        b = reg2bin(pos0, pos0 + max(rlen, 1), min_shift, depth)
+        ch = bins.setdefault(b, [])
+        v0, v1 = voff(u0), voff(u1)
+        if ch and ch[-1][1] == v0:
+            ch[-1][1] = v1
+        else:
+            ch.append([v0, v1])
+    body = b"CSI\1" + struct.pack("<iii", min_shift, depth, 0) + struct.pack("<i", 1)
+    body += struct.pack("<i", len(bins))
+    for b in sorted(bins):
+        ch = bins[b]
+        body += struct.pack("<IQi", b, ch[0][0], len(ch))
+        for v0, v1 in ch:
+            body += struct.pack("<QQ", v0, v1)
+    body += struct.pack("<Q", 0)
+    return bgzf_blocks(body)
 
 
 def typed_str(s):
@@ -58,7 +113,7 @@ def bcf_record(chrom, pos0, ref, alt, gt_pairs):
     return struct.pack("<II", len(shared), len(indiv)) + shared + indiv
 
 
-def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0):
+def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0, index=True):
     import tfbs_pkg
     T = tfbs_pkg.load()
     os.makedirs(out, exist_ok=True)
@@ -107,11 +162,18 @@ def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, se
               "##contig=<ID=chr1,length=%d>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t%s\n"
               % (chrom_len, "\t".join(samples))).encode() + b"\0"
     body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+    spans = []
     for rec in records:
+        u0 = len(body)
         body += bcf_record(0, rec["pos0"], rec["alleles"][0], rec["alleles"][1], rec["gt"])
+        spans.append((rec["pos0"], rec["rlen"], u0, len(body)))
     bcf = os.path.join(out, "genotypes.bcf")
+    offs = []
     with open(bcf, "wb") as f:
-        f.write(bgzf_blocks(body))
+        f.write(bgzf_blocks(body, offs))
+    if index:
+        with open(bcf + ".csi", "wb") as f:
+            f.write(csi_index(spans, offs, chrom_len))
     return {"dir": out, "fasta": fa, "bed": bed, "bcf": bcf, "samples": samples, "names": names,
             "pwm_file": os.path.join(out, "pwms.txt"), "thr_dir": os.path.join(out, "thr"),
             "records": records, "regions": regions}
@@ -126,8 +188,9 @@ def main():
     ap.add_argument("--length-config", type=int, default=2)
     ap.add_argument("--seed", type=int, default=3)
     ap.add_argument("--indel-pct", type=int, default=0)
+    ap.add_argument("--no-index", action="store_true", help="no <bcf>.csi")
     a = ap.parse_args()
-    d = make_dataset(a.out, a.samples, a.regions, a.pwms, a.length_config, a.seed, a.indel_pct)
+    d = make_dataset(a.out, a.samples, a.regions, a.pwms, a.length_config, a.seed, a.indel_pct, not a.no_index)
     print("wrote %s: %d records, %d regions, %d samples" % (d["bcf"], len(d["records"]), len(d["regions"]),
                                                            len(d["samples"])))
 
