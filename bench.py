@@ -1,18 +1,29 @@
 #!/usr/bin/env python3
 """Benchmark: haplotype-windows scored/sec of the MI355X PWM scan (BASELINE.json).
 
-Workload (default, BASELINE.json configs[2] = SURVEY.md section 8d "C3"): per
-GPU, 10 000 merged regions x 201 bp of a synthetic chromosome, 50 000 phased
-samples (100 000 haplotypes), Poisson(20) variant sites per region with
-carrier counts ~ 1/k, 600 synthetic HOCOMOCO-format PWMs (L 8..30) on both
-strands (1 200 patterns), threshold 1e-4.  Regions are reduced to distinct
-haplotypes on the host (untimed, as the reference does before scanning) and
-packed into HBM; one timed step = one tfbs_scan over every distinct haplotype
-x pattern window of the rank's batch.
+Workloads (--workload, default C3 = BASELINE.json configs[2]):
+  C2  1 000 samples x 1 000 regions x 10 PWMs (L 8-15), seed 2
+  C3  50 000 samples x 10 000 regions x 600 PWMs (L 8-30), seed 3     (per GPU)
+  C4  C3's generator with seed 4, 12 500 regions per GPU (100 000 over 8 GPUs)
+  C5  C3 with 30 % indels and PWMs of length 25-30, seed 5
+Regions are 201 bp merged BED rows of a synthetic chromosome with Poisson(20)
+variant sites and carrier counts ~ 1/k; PWMs are synthetic HOCOMOCO-format
+matrices with exact 1e-4 thresholds, both strands.  The host reduces every
+region to its distinct haplotypes and packs them into HBM (untimed, as the
+reference builds them before scanning); one timed step = one tfbs_scan over
+every distinct haplotype x pattern window of the rank's batch.
 
-Multi-GPU (torchrun, one rank per GPU): rank r scans regions
-[r*R, (r+1)*R) of the same synthetic chromosome -- weak scaling, no collective
-on the data path; a barrier + max-over-ranks bracket the timed region.
+Multi-GPU (torchrun, one rank per GPU): rank r scans regions [r R, (r+1) R) --
+the static contiguous region shard tfbs_run --devices uses,
+weak scaling, no collective on the data path; a barrier + max-over-ranks bracket
+the timed region.
+
+Besides the scan-only `value` the line carries an end-to-end leg over the same
+batch (host prep + upload + scan + device key reduction + row formatting), the
+roofline of the dominant kernel (HIP events around its launches on the ctx
+stream; traffic from the rocprofv3 PMC passes of the same bench command,
+tools/profile_round.sh) and the CPU baseline (the oracle, scan-only and
+end-to-end, 1 thread and the box's share of threads).
 """
 import argparse
 import json
@@ -33,6 +44,14 @@ MFMA_F6_PEAK_TOPS = 10000.0
 # digit = 4 multiply-adds (scan_mfma.hip); padding (K, windows, strands) and the
 # exact rescoring of the rare candidate windows excluded
 MFMA_OPS_PER_CELL = 8
+CPU_THREADS_MAX = 16        # the GPU box's CPU share for one GPU (os.cpu_count() shows the whole host)
+
+WORKLOADS = {  # samples, regions per GPU, pwms, length config, indel %, seed
+    "C2": (1000, 1000, 10, 2, 0, 2),
+    "C3": (50000, 10000, 600, 3, 0, 3),
+    "C4": (50000, 12500, 600, 3, 0, 4),
+    "C5": (50000, 10000, 600, 5, 30, 5),
+}
 
 
 def parse():
@@ -40,97 +59,146 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--regions", type=int, default=10000, help="regions per GPU")
-    ap.add_argument("--samples", type=int, default=50000)
-    ap.add_argument("--pwms", type=int, default=600)
-    ap.add_argument("--length-config", type=int, default=3)
-    ap.add_argument("--indel-pct", type=int, default=0)
+    ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
+    ap.add_argument("--regions", type=int, default=None, help="regions per GPU (workload default)")
+    ap.add_argument("--samples", type=int, default=None)
+    ap.add_argument("--pwms", type=int, default=None)
+    ap.add_argument("--length-config", type=int, default=None)
+    ap.add_argument("--indel-pct", type=int, default=None)
+    ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--threshold", type=float, default=1e-4)
-    ap.add_argument("--seed", type=int, default=3)
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget of each CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (profiling passes)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the timing reductions (gloo: rehearse several ranks on one GPU)")
-    ap.add_argument("--pmc-summary", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    w = WORKLOADS[a.workload]
+    for name, v in zip(("samples", "regions", "pwms", "length_config", "indel_pct", "seed"), w):
+        if getattr(a, name) is None:
+            setattr(a, name, v)
+    a.custom = tuple(getattr(a, n) for n in ("samples", "regions", "pwms", "length_config", "indel_pct",
+                                              "seed")) != w
+    return a
 
 
-def workload_name(args):
-    """BASELINE.json configs: C2 = 1 k samples x 10 PWMs (lengths 8-15), C3 = 50 k x 600
-    PWMs per GPU (C4 is C3 sharded over 8 GPUs), C5 = C3 with 30 % indels and PWMs of length 25-30."""
-    key = (args.samples, args.pwms, args.length_config, args.indel_pct)
-    return {(1000, 10, 2, 0): "C2", (50000, 600, 3, 0): "C3", (50000, 600, 5, 30): "C5"}.get(key, "custom")
+def workload_key(args):
+    """What a PMC summary must match to be this run's traffic (profiles/pmc_traffic_<workload>.json)."""
+    return {"workload": args.workload, "samples": args.samples, "regions": args.regions, "pwms": args.pwms,
+            "length_config": args.length_config, "indel_pct": args.indel_pct, "seed": args.seed,
+            "threshold": args.threshold}
+
+
+def pmc_traffic(args, path):
+    """HBM bytes per step of the dominant kernel's launches from the PMC passes of this
+    same bench configuration (tools/pmc_traffic.py), or (None, reason)."""
+    f = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
+    if not os.path.exists(f):
+        return None, "no %s" % os.path.relpath(f, ROOT)
+    try:
+        pm = json.load(open(f))
+    except ValueError:
+        return None, "unreadable %s" % os.path.relpath(f, ROOT)
+    if pm.get("config") != workload_key(args) or pm.get("scan_path") != path:
+        return None, "%s is for another configuration" % os.path.relpath(f, ROOT)
+    return pm["hbm_bytes_per_step"], "%s (%s)" % (os.path.relpath(f, ROOT), pm.get("source", ""))
 
 
 def cpu_baseline(T, ps, args, budget_s):
-    """The oracle (C restatement of the reference algorithm) on host threads over a
-    bounded sample of the same workload's regions, 50-region chunks per worker as
-    main.rs:375-381.  Returns the cpu_baseline object."""
+    """The oracle (oracle/tfbs_oracle.c, the C restatement of the reference algorithm,
+    gcc -O3 -march=x86-64-v3) on host threads over a bounded sample of the workload's
+    regions, 50-region chunks per worker as main.rs:375-381: scan-only (load_diffs +
+    patch + find_all_matches, no count/rows) and end-to-end (+ count_matches_by_sample,
+    counts_as_genotypes, rows), each on 1 thread and on the box's share of threads.
+    Region inputs are generated before the clock starts."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import concurrent.futures as cf
 
+    import numpy as np
     import oracle_py as O
     from helpers import pattern_dicts
 
     pats = pattern_dicts(ps)
-    threads = max(1, min(16, os.cpu_count() or 1))
     lmax = ps.max_length
+    tmax = max(1, min(CPU_THREADS_MAX, os.cpu_count() or 1))
 
-    def run_regions(idx):
-        job = O.Job(args.samples, "chr1", pats, [("synthetic.bed", [])])
-        wall = 0.0
+    def gen(j):
+        r = T.SynthRegion(args.seed, j, args.samples, lmax, args.indel_pct)
+        return (r.merged, r.ref, [(p, rf, a, np.asarray(c, dtype=np.uint32)) for p, rf, a, c in r.records])
+
+    regs = [gen(0)]
+
+    def run_regions(idx, scan_only):
+        job = O.Job(args.samples, "chr1", pats, [("synthetic.bed", [regs[j][0] for j in idx])])
+        job.set_scan_only(scan_only)
         for j in idx:
-            r = T.SynthRegion(args.seed, j, args.samples, lmax, args.indel_pct)
-            t0 = time.perf_counter()
-            rc = job.begin(r.merged[0], r.merged[1], r.ref)
-            for pos, ref, alt, car in r.records:
-                rc |= job.add_record_carriers(pos, ref, alt, car)
+            merged, ref, recs = regs[j]
+            rc = job.begin(merged[0], merged[1], ref)
+            for pos, rf, alt, car in recs:
+                rc |= job.add_record_carriers_np(pos, rf, alt, car)
             rc |= job.end()
-            wall += time.perf_counter() - t0
             assert rc == 0
+            job.clear_rows()
+        ph = job.phase_seconds()
         job.close()
-        return wall
+        return ph
 
-    # calibrate on one region, then size the sample to ~budget_s of wall time
-    t1 = run_regions([0])
-    per_thread = max(1, int(budget_s / max(t1, 1e-3)))
-    n = min(args.regions, threads * per_thread)
-    idx = list(range(n))
-    csize = max(1, min(50, n // threads))  # the reference's 50-peak chunks, split further for small samples
-    chunks = [idx[i:i + csize] for i in range(0, n, csize)]
-    t0 = time.perf_counter()
-    with cf.ThreadPoolExecutor(threads) as ex:
-        list(ex.map(run_regions, chunks))
-    wall = time.perf_counter() - t0
-    b = T.RegionBatch(ps, args.samples, keep_membership=False)
-    b.synth_fill(args.seed, 0, n, args.indel_pct)
-    return {"value": b.num_windows / wall, "unit": "windows/s", "cores": threads, "kind": "port",
-            "sample": "%d of the %d regions (%d distinct haplotypes, %.3g windows), %d samples, %d patterns; "
-                      "oracle/tfbs_oracle.c restating the reference scan + count + genotype path, %d threads, "
-                      "%.1f s wall" % (n, args.regions, b.num_haplotypes, b.num_windows, args.samples, len(ps),
-                                       threads, wall)}
+    t1 = {}
+    for scan_only in (True, False):
+        t0 = time.perf_counter()
+        run_regions([0], scan_only)
+        t1[scan_only] = max(time.perf_counter() - t0, 1e-3)
+    sizes = {(so, th): max(th, min(args.regions, int(th * budget_s / t1[so])))
+             for so in (True, False) for th in (1, tmax)}
+    n_max = max(sizes.values())
+    regs += [gen(j) for j in range(1, n_max)]
+    matrix = {}
+    for (scan_only, threads), n in sizes.items():
+        csize = max(1, min(50, n // threads))  # the reference's 50-peak chunks, split for small samples
+        chunks = [list(range(i, min(n, i + csize))) for i in range(0, n, csize)]
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(threads) as ex:
+            res = list(ex.map(lambda c: run_regions(c, scan_only), chunks))
+        wall = time.perf_counter() - t0
+        b = T.RegionBatch(ps, args.samples, keep_membership=False)
+        b.synth_fill(args.seed, 0, n, args.indel_pct)
+        phases = [sum(p[k] for p in res) for k in range(3)]
+        matrix["%s_t%d" % ("scan" if scan_only else "e2e", threads)] = {
+            "windows_per_s": b.num_windows / wall, "regions_per_s": n / wall, "regions": n, "threads": threads,
+            "wall_s": wall, "windows": b.num_windows,
+            "phase_thread_s": {"load_diffs_patch": phases[0], "find_all_matches": phases[1],
+                               "count_rows": phases[2]}}
+    best = matrix["scan_t%d" % tmax]
+    return {"value": best["windows_per_s"], "unit": "windows/s", "cores": tmax, "kind": "port",
+            "sample": "scan-only leg on %d threads: %d of the %d regions of this workload (%d samples, %d "
+                      "patterns, %.3g windows); oracle/tfbs_oracle.c (C restatement of the reference scan; gcc "
+                      "-O3 -march=x86-64-v3), inputs generated before the clock; matrix: scan-only and "
+                      "end-to-end on 1 and %d threads" % (
+                          tmax, best["regions"], args.regions, args.samples, len(ps), best["windows"], tmax),
+            "matrix": matrix}
 
 
 def shard_batch(T, ps, args, rank):
     """Rank r's share: merged regions [r R, (r+1) R) of the synthetic
-    chromosome, reduced to distinct haplotypes and packed on the host."""
-    batch = T.RegionBatch(ps, args.samples, keep_membership=False)
+    chromosome, reduced to distinct haplotypes and packed on the host (with the
+    haplotype -> distinct membership the rows need)."""
+    batch = T.RegionBatch(ps, args.samples, keep_membership=True)
     batch.synth_fill(args.seed, rank * args.regions, args.regions, args.indel_pct)
     return batch
 
 
-def job_totals(dist, elapsed, windows, regions, eff, device):
+def job_totals(dist, device, elapsed, sums):
     """Max-over-ranks wall time and whole-job sums.  Regions shard with no exchange, so
     the only collectives are these scalar reductions around the timed region."""
     if dist is None:
-        return elapsed, float(windows), float(regions), float(eff)
+        return elapsed, [float(x) for x in sums]
     import torch
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    t = torch.tensor(elapsed if isinstance(elapsed, list) else [elapsed], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    w = torch.tensor([windows, regions, eff], dtype=torch.float64, device=device)
+    w = torch.tensor(sums, dtype=torch.float64, device=device)
     dist.all_reduce(w, op=dist.ReduceOp.SUM)
-    tot = [float(x) for x in w.tolist()]
-    return float(t.item()), tot[0], tot[1], tot[2]
+    tl = [float(x) for x in t.tolist()]
+    return (tl if isinstance(elapsed, list) else tl[0]), [float(x) for x in w.tolist()]
 
 
 def main():
@@ -147,23 +215,41 @@ def main():
             local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dist.init_process_group(args.dist_backend)
+    rdev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     import tfbs_pkg
 
     T = tfbs_pkg.load()
+    threads = max(1, min(CPU_THREADS_MAX, os.cpu_count() or 1))
     work = tempfile.mkdtemp(prefix="tfbs_bench_%d_" % rank)
     names = T.synth_write_pwms(work, args.pwms, args.length_config, args.seed)
     ps = T.parse_pwm_files(os.path.join(work, "pwms.txt"), os.path.join(work, "thr"), args.threshold, names)
     sc = T.Scanner(ps, device=local)
+    L = T.lib()
+
+    # ---- end-to-end leg, once: host prep, upload, scan, device key reduction, rows
     t_prep = time.perf_counter()
     batch = shard_batch(T, ps, args, rank)
     t_prep = time.perf_counter() - t_prep
+    gen_s, build_s, commit_s, fill_s = batch.prep_seconds()
     t_up = time.perf_counter()
-    batch.scan(sc, upload=True, download=False)
-    T.check(T.lib().tfbs_ctx_sync(sc.h))
+    T.check(L.tfbs_batch_upload(sc.h, batch.h))
     t_up = time.perf_counter() - t_up
+    t_scan1 = time.perf_counter()
+    T.check(L.tfbs_scan(sc.h, batch.h))
+    T.check(L.tfbs_ctx_sync(sc.h))
+    t_scan1 = time.perf_counter() - t_scan1
+    t_red = time.perf_counter()
+    T.check(L.tfbs_batch_reduce(sc.h, batch.h))
+    t_red = time.perf_counter() - t_red
+    n_rows = n_row_bytes = 0
+    t_rows = 0.0
+    if not args.no_e2e:
+        t_rows = time.perf_counter()
+        n_rows, n_row_bytes = batch.format_rows("chr1", 0, threads)
+        t_rows = time.perf_counter() - t_rows
 
-    L = T.lib()
+    # ---- timed scan loop
     for _ in range(args.warmup):
         T.check(L.tfbs_scan(sc.h, batch.h))
     T.check(L.tfbs_ctx_sync(sc.h))
@@ -188,57 +274,52 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
 
-    # after the timed region: the two ways the counts leave the GPU
-    t_red = time.perf_counter()
-    T.check(L.tfbs_batch_reduce(sc.h, batch.h))
-    t_red = time.perf_counter() - t_red
+    # the dense download, for reference (the run flow uses the key reduction)
     t_dense = time.perf_counter()
     T.check(L.tfbs_batch_download(sc.h, batch.h))
     t_dense = time.perf_counter() - t_dense
 
-    windows = batch.num_windows
-    regions = batch.num_regions
-    elapsed, tot_windows, tot_regions, tot_eff = job_totals(dist, elapsed, windows, regions,
-                                                             batch.num_effective_windows,
-                                                             "cuda" if args.dist_backend == "nccl" else "cpu")
+    e2e_s = fill_s + t_up + t_scan1 + t_red + t_rows
+    (elapsed, e2e_max), tot = job_totals(dist, rdev, [elapsed, e2e_s],
+                                         [batch.num_windows, batch.num_regions, batch.num_effective_windows,
+                                          n_rows, n_row_bytes])
+    tot_windows, tot_regions, tot_eff, tot_rows, tot_row_bytes = tot
 
     if rank == 0:
         steps = args.steps
         value = tot_windows * steps / elapsed
         kms = sum(kernel_ms) / len(kernel_ms)
+        mms = sum(mfma_ms) / len(mfma_ms)
+        path = "mfma" if mms > 0 else "lut"
+        traffic, traffic_src = pmc_traffic(args, path)
         pattern_bytes = 0
         for p in ps.to_list():
             pattern_bytes += ((len(p) + 15) // 16) * 1536 + 16 * len(p) + 24
         alg_bytes = batch.input_bytes + batch.output_bytes + pattern_bytes
-        achieved = alg_bytes / (kms / 1e3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_summary):
-            try:
-                pm = json.load(open(args.pmc_summary))
-                if (pm.get("workload") == "C3" and pm.get("regions") == args.regions
-                        and pm.get("scan_path") == ("mfma" if min(mfma_ms) > 0 else "lut")):
-                    traffic = pm.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
         cell_tops = batch.num_cell_ops / (kms / 1e3) / 1e12
-        mms = sum(mfma_ms) / len(mfma_ms)
-        hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-               "note": "algorithmic bytes/launch = packed haplotypes + metadata + pattern tables + u32 counts; "
-                       "the scan is compute bound"}
         if mms > 0:  # the matrix-core kernel scored every strand of this workload
             mops = MFMA_OPS_PER_CELL * batch.num_cell_ops / (mms / 1e3) / 1e12
-            roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TOPS",
+            roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TFLOP/s",
                     "frac": mops / MFMA_F6_PEAK_TOPS, "traffic": traffic,
-                    "kernel": "scan_mfma_kernel<staged, K depth> (one launch per depth, 4 streams)",
+                    "kernel": "scan_mfma_kernel<staged, K depth> (one launch per K depth, 4 streams)",
                     "kernel_ms": mms,
-                    "note": "achieved = 8 ops per (window, strand, column) of the FP4 one-hot x FP6 bound-digit "
-                            "GEMM / the MFMA phase's HIP-event time (first launch to last, joined on the ctx "
-                            "stream; tools/trace_phase.py gives the same phase from the rocprofv3 trace); "
-                            "traffic = HBM bytes of the phase's dispatches from PMC"}
+                    "note": "achieved = 8 ops per (window, strand, column) cell of the FP4 one-hot x FP6 "
+                            "bound-digit GEMM x %.4g cells / the MFMA phase's HIP-event time (first launch to "
+                            "last, joined on the ctx stream; tools/trace_phase.py reads the same phase from "
+                            "the rocprofv3 trace); traffic = HBM bytes of the phase's dispatches per step, "
+                            "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, from %s" % (batch.num_cell_ops, traffic_src)}
+            hbm_ms = mms
         else:
+            roof = None
+            hbm_ms = kms
+        achieved = alg_bytes / (hbm_ms / 1e3) / 1e9
+        hbm = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+               "note": "algorithmic bytes/step = packed haplotypes + metadata (%d B) + pattern tables (%d B) + "
+                       "u32 counts (%d B); the scan is compute bound" % (
+                           batch.input_bytes, pattern_bytes, batch.output_bytes)}
+        if roof is None:
             roof = hbm
-        path = "mfma" if mms > 0 else "lut"
         out = {
             "metric": "haplotype-windows scored/sec",
             "value": value,
@@ -253,19 +334,30 @@ def main():
             "dtype": "fp4xfp6->f32 bound + int32 exact" if path == "mfma" else "int32",
             "data": "synthetic (SURVEY.md 8d generator; no HOCOMOCO/BCF download possible)",
             "config": {
-                "workload": workload_name(args),
+                "workload": args.workload + ("-custom" if args.custom else ""),
                 "samples": args.samples, "haplotypes": 2 * args.samples, "regions_per_gpu": args.regions,
                 "region_bp": 201, "pwms": args.pwms, "patterns": len(ps), "threshold": args.threshold,
-                "indel_pct": args.indel_pct, "distinct_haplotypes_per_gpu": batch.num_haplotypes,
+                "indel_pct": args.indel_pct, "seed": args.seed,
+                "distinct_haplotypes_per_gpu": batch.num_haplotypes,
                 "windows_per_step": int(tot_windows), "parallelism": "region shard x%d" % world,
                 "scan_path": path,
             },
-            "regions_per_s": tot_regions * steps / elapsed,
+            "scan_regions_per_s": tot_regions * steps / elapsed,
             "effective_windows_per_s": tot_eff * steps / elapsed,
+            "end_to_end": {
+                "regions_per_s": tot_regions / e2e_max,
+                "windows_per_s": tot_windows / e2e_max,
+                "seconds": e2e_max,
+                "note": "one pass over the rank's batch: host prep (synthetic generation + load_diffs/"
+                        "patch/dedup/pack on %d threads) + upload + scan + device key reduction + row "
+                        "formatting (%d rows, %.3g bytes); the BGZF write is not included" % (
+                            threads, tot_rows, tot_row_bytes),
+                "rank0_phases_s": {"host_prep_wall": fill_s, "synthetic_generation_thread_s": gen_s,
+                                   "build_region_thread_s": build_s, "commit_wall": commit_s,
+                                   "upload": t_up, "scan": t_scan1, "key_reduce": t_red, "rows": t_rows},
+                "rows": int(tot_rows),
+            },
             "kernel_ms_avg": kms,
-            "host_prep_s": t_prep,
-            "upload_s": t_up,
-            "key_reduce_s": t_red,
             "dense_download_s": t_dense,
             "roofline": roof,
             "hbm_roofline": hbm,

@@ -422,6 +422,18 @@ class RegionBatch:
         check(lib().tfbs_batch_region_digest(self.h, region, C.byref(d)))
         return d.value
 
+    def format_rows(self, chromosome, min_maf=0, threads=1):
+        """Format every region's rows on host threads and discard them: (rows, bytes)."""
+        r, n = C.c_uint64(), C.c_uint64()
+        check(lib().tfbs_batch_format_rows(self.h, _u(chromosome), min_maf, threads, C.byref(r), C.byref(n)))
+        return r.value, n.value
+
+    def prep_seconds(self):
+        """(generation CPU-s, build_region CPU-s, commit wall-s, fill wall-s) of synth_fill."""
+        out = (C.c_double * 4)()
+        check(lib().tfbs_batch_prep_seconds(self.h, out))
+        return tuple(out)
+
     def rows(self, chromosome, min_maf=0, fake_position=1):
         """Rows for every region (main.rs:415-429); returns (text, next fake_position)."""
         fp = C.c_uint32(fake_position)

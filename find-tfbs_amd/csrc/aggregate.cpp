@@ -340,6 +340,43 @@ int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_ma
     return TFBS_OK;
 }
 
+int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t threads,
+                           uint64_t *n_rows, uint64_t *n_bytes) {
+    if (!b || !chromosome || !n_rows || !n_bytes) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    const size_t n = B.rh.size();
+    const size_t prefix = tfbs::strip_chr(chromosome).size() + 2;
+    std::atomic<size_t> next(0);
+    std::atomic<uint64_t> rows(0), bytes(0);
+    auto work = [&]() {
+        std::vector<std::string> rr;
+        uint64_t r = 0, by = 0;
+        for (size_t j; (j = next.fetch_add(1)) < n;) {
+            rr.clear();
+            if (B.rh[j].hap_count) tfbs::region_rows(B, B.rh[j], min_maf, rr);
+            for (auto &x : rr) by += x.size() + prefix;
+            r += rr.size();
+        }
+        rows += r;
+        bytes += by;
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
+    work();
+    for (auto &t : ts) t.join();
+    *n_rows = rows;
+    *n_bytes = bytes;  // + the POS digits, which depend on the run's counter
+    return TFBS_OK;
+}
+
+int tfbs_batch_prep_seconds(const tfbs_batch *b, double *out) {
+    if (!b || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    memcpy(out, b->b.prep_s, sizeof b->b.prep_s);
+    return TFBS_OK;
+}
+
 void tfbs_free(void *p) { free(p); }
 
 int tfbs_counts_as_genotypes(const uint32_t *left, const uint32_t *right, size_t n, uint32_t *maf, char *info,

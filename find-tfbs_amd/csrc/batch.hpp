@@ -70,6 +70,9 @@ struct Batch {
 
     std::vector<RegionH> rh;
     uint64_t windows = 0, eff_windows = 0, cell_ops = 0;
+    // host prep seconds (tfbs_batch_prep_seconds): synthetic generation (thread
+    // CPU-seconds), build_region (thread CPU-seconds), serial commit (wall), whole fill (wall)
+    double prep_s[4] = {0, 0, 0, 0};
 
     // region under construction
     bool open = false;

@@ -10,6 +10,8 @@
 #include <cstring>
 #include <string>
 #include <sys/stat.h>
+#include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -321,16 +323,21 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
     T = std::max(1u, std::min(16u, T));
     B.counts_valid = false;
     const uint64_t chunk = 64ull * T;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_fill = now();
     for (uint64_t c0 = first; c0 < first + count; c0 += chunk) {
         const uint64_t n = std::min<uint64_t>(chunk, first + count - c0);
         std::vector<tfbs::RegionBuilt> built(n);
         std::vector<int> rcs(n, TFBS_OK);
         std::atomic<uint64_t> next(0);
+        std::mutex mu;
         auto work = [&]() {
             tfbs::SynthRegion R;
+            double t_gen = 0, t_build = 0;
             for (;;) {
                 const uint64_t j = next.fetch_add(1);
                 if (j >= n) break;
+                const double t0 = now();
                 tfbs::synth_region(seed, c0 + j, B.n_samples, lmax, indel_pct, R);
                 tfbs::RegionInput in;
                 in.R.ms = R.ms;
@@ -348,18 +355,27 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
                     in.recs.push_back(std::move(r));
                 }
                 in.inner.push_back({(uint32_t)bed, {R.ms, R.me}});
+                const double t1 = now();
                 rcs[j] = tfbs::build_region(B, std::move(in), built[j]);
+                t_gen += t1 - t0;
+                t_build += now() - t1;
             }
+            std::lock_guard<std::mutex> g(mu);
+            B.prep_s[0] += t_gen;
+            B.prep_s[1] += t_build;
         };
         std::vector<std::thread> ts;
         for (uint32_t t = 0; t + 1 < T && t + 1 < n; t++) ts.emplace_back(work);
         work();
         for (auto &t : ts) t.join();
+        const double t_commit = now();
         for (uint64_t j = 0; j < n; j++) {
             if (rcs[j]) return rcs[j];
             tfbs::commit_region(B, std::move(built[j]));
         }
+        B.prep_s[2] += now() - t_commit;
     }
+    B.prep_s[3] += now() - t_fill;
     return TFBS_OK;
 }
 

@@ -241,6 +241,15 @@ int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chrom
 int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
 /* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
 int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
+/* Formats every region's rows (main.rs:415-429) on `threads` host threads and
+ * discards them: the row count and bytes (without POS digits).  The bench's
+ * end-to-end leg times it; tfbs_run writes the same rows. */
+int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t threads,
+                           uint64_t *n_rows, uint64_t *n_bytes);
+/* Host prep seconds of the batch's synthetic fills (out[4]): generation and
+ * build_region (thread CPU-seconds, summed), the serial commit and the whole
+ * fill (wall). */
+int tfbs_batch_prep_seconds(const tfbs_batch *b, double *out);
 void tfbs_free(void *p);
 
 /* counts_as_genotypes alone (main.rs:439-498): 1 = row (strings written), 0 = no variation. */

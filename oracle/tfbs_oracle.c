@@ -751,6 +751,11 @@ typedef struct orc_job {
     int last_haplotypes;         /* number_of_haplotypes (main.rs:97-130) */
     int last_variants;           /* variant_count (haplotype.rs:25) */
     uint64_t last_matches;       /* sum of haplotype ids over matches (main.rs:431) */
+    /* baseline timing (bench.py cpu_baseline): scan_only skips count_matches_by_sample and
+     * the rows (matches are still found and counted); phase wall seconds summed over regions:
+     * [0] load_diffs + group + patch, [1] find_all_matches, [2] keys + rows */
+    int scan_only;
+    double phase_s[3];
 } orc_job;
 
 orc_job *orc_job_new(int nsamp, const char *chrom, uint32_t min_maf) {
@@ -936,8 +941,18 @@ typedef struct {
 static void scan_cb(void *ctx, uint64_t s, uint64_t e) {
     scan_ctx *c = (scan_ctx *)ctx;
     c->nmatch_ids += (uint64_t)c->nids;
+    if (c->j->scan_only) return;
     count_one_match(&c->j->keys, 0, c->ib, c->is, c->ie, c->ninner, s, e, c->pid, c->ids, c->nids);
 }
+
+#include <time.h>
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+void orc_job_set_scan_only(orc_job *j, int on) { j->scan_only = on; }
+void orc_job_phase_seconds(const orc_job *j, double *out) { memcpy(out, j->phase_s, sizeof j->phase_s); }
 
 
 /* Finish the region: find_all_matches + count_matches_by_sample +
@@ -947,6 +962,7 @@ int orc_region_end(orc_job *j) {
     keymap_free(&j->keys);
     j->keys.nsamp = j->nsamp;
     int H = 2 * j->nsamp;
+    double t_phase = now_s();
 
     /* load_diffs: HashMap<HaplotypeId, Vec<Diff>> built in record order. */
     orc_diff *diffs = (orc_diff *)malloc(sizeof(orc_diff) * (j->nrec ? j->nrec : 1));
@@ -1038,6 +1054,7 @@ int orc_region_end(orc_job *j) {
         }
     }
     /* find_all_matches (main.rs:94-154) */
+    { double t = now_s(); j->phase_s[0] += t - t_phase; t_phase = t; }
     uint64_t nmatch_ids = 0;
     int nhap = 0;
     if (rc == ORC_OK) {
@@ -1068,6 +1085,7 @@ int orc_region_end(orc_job *j) {
         free(in_ref);
     }
     /* rows (main.rs:415-429), D2 order */
+    { double t = now_s(); j->phase_s[1] += t - t_phase; t_phase = t; }
     if (rc == ORC_OK) {
         qsort(j->keys.k, j->keys.n, sizeof(orc_key), cmp_key);
         /* chromosome.replace("chr", "") */
@@ -1100,6 +1118,7 @@ int orc_region_end(orc_job *j) {
         }
         free(chr.p);
     }
+    j->phase_s[2] += now_s() - t_phase;
     j->last_haplotypes = nhap;
     j->last_variants = variants;
     j->last_matches = nmatch_ids;

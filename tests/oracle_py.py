@@ -79,6 +79,8 @@ def lib():
         L.orc_job_nkeys.argtypes = [C.c_void_p]
         L.orc_job_key.argtypes = [C.c_void_p, C.c_int, intp, u64p, u64p, intp, u32p, u32p]
         L.orc_job_stats.argtypes = [C.c_void_p, intp, intp, u64p]
+        L.orc_job_set_scan_only.argtypes = [C.c_void_p, C.c_int]
+        L.orc_job_phase_seconds.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         _lib = L
     return _lib
 
@@ -272,6 +274,11 @@ class Job:
         return self.L.orc_region_add_record_carriers(self.h, pos, ref.encode(), alt.encode(),
                                                      arr(C.c_uint32, hap_ids), len(hap_ids))
 
+    def add_record_carriers_np(self, pos, ref, alt, hap_ids):
+        """hap_ids: a contiguous numpy uint32 array (no per-id conversion)."""
+        return self.L.orc_region_add_record_carriers(self.h, pos, ref.encode(), alt.encode(),
+                                                     hap_ids.ctypes.data_as(u32p), len(hap_ids))
+
     def end(self):
         return self.L.orc_region_end(self.h)
 
@@ -302,6 +309,16 @@ class Job:
                                l.ctypes.data_as(u32p), r.ctypes.data_as(u32p))
             out[(self.bed_names[b.value], (s.value, e.value), pid.value)] = (l[:n], r[:n])
         return out
+
+    def set_scan_only(self, on=True):
+        """Skip count_matches_by_sample and the rows (the bench's scan-only CPU baseline)."""
+        self.L.orc_job_set_scan_only(self.h, 1 if on else 0)
+
+    def phase_seconds(self):
+        """Wall seconds summed over regions: (load_diffs+patch, find_all_matches, keys+rows)."""
+        out = (C.c_double * 3)()
+        self.L.orc_job_phase_seconds(self.h, out)
+        return tuple(out)
 
     def clear_rows(self):
         self.L.orc_job_clear_rows(self.h)

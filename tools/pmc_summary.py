@@ -1,38 +1,58 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 --pmc CSVs for the scan kernels: per-dispatch counter sums."""
+"""Summarise a rocprofv3 --pmc pass over bench.py: counters summed over the
+dispatches of the last scan step's MFMA phase (every scan_mfma_kernel dispatch
+after the last non-MFMA dispatch that precedes them -- one per K depth and hap
+group chunk), plus the dispatches' kernel names.
+
+Usage: python tools/pmc_summary.py PMC_DIR  -> PMC_DIR/pmc_summary.json
+"""
 import csv
 import glob
 import json
 import os
+import re
 import sys
 
-out = {}
-root = sys.argv[1]
-for f in glob.glob(os.path.join(root, "pmc_counter_collection.csv")) + glob.glob(
-        os.path.join(root, "*", "pmc_counter_collection.csv")):
-    rows = list(csv.DictReader(open(f)))
-    # the last scan step: the last run of consecutive scan dispatches (one per
-    # K depth for the MFMA path), counters summed over its dispatches
-    kinds = {}
+
+def last_phase(rows):
+    """Dispatch ids of the last run of consecutive scan_mfma_kernel dispatches."""
+    names = {}
     for r in rows:
-        kinds[int(r["Dispatch_Id"])] = "scan_" in r["Kernel_Name"]
-    ids = sorted(kinds)
-    last = []
-    for d in ids:
-        if kinds[d]:
-            last = last + [d] if last and last[-1] == ids[ids.index(d) - 1] else [d]
-    if not last:
-        continue
-    take = set(last)
-    seen = set()
-    for r in rows:
-        d = int(r["Dispatch_Id"])
-        if d in take:
-            out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-            out["_kernel"] = r["Kernel_Name"][:60]
-            out["_dispatches"] = len(take)
-            out["_grid"] = r["Grid_Size"]
-            out["_vgpr"] = r["VGPR_Count"]
-            out["_lds"] = r["LDS_Block_Size"]
-json.dump(out, open(os.path.join(root, "pmc_summary.json"), "w"), indent=1)
-print(json.dumps(out, indent=1))
+        names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
+    run, best = [], []
+    for d in sorted(names):
+        if "scan_mfma_kernel" in names[d]:
+            run.append(d)
+        else:
+            if run:
+                best = run
+            run = []
+    return set(run or best), names
+
+
+def main():
+    root = sys.argv[1]
+    files = glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)
+    out = {"_files": files}
+    for f in files:
+        rows = list(csv.DictReader(open(f)))
+        take, names = last_phase(rows)
+        if not take:
+            continue
+        kern = {}
+        for r in rows:
+            d = int(r["Dispatch_Id"])
+            if d in take:
+                out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        for d in sorted(take):
+            m = re.search(r"scan_mfma_kernel<[^>]*>", names[d])
+            k = m.group(0) if m else names[d][:80]
+            kern[k] = kern.get(k, 0) + 1
+        out["_dispatches"] = len(take)
+        out["_kernels"] = kern
+    json.dump(out, open(os.path.join(root, "pmc_summary.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()

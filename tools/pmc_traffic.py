@@ -1,34 +1,39 @@
 #!/usr/bin/env python3
-"""Write profiles/pmc_traffic.json (roofline.traffic for bench.py) from the
-FETCH_SIZE / WRITE_SIZE passes of tools/gpu_round.sh.
+"""profiles/pmc_traffic_<workload>.json: HBM bytes per scan step of the MFMA
+phase (bench.py's roofline.traffic) from the FETCH_SIZE and WRITE_SIZE passes
+tools/profile_round.sh ran over the same bench.py arguments.
 
-Usage: python tools/pmc_traffic.py gpurun_out/TAG [regions] [scan_path]
-FETCH_SIZE and WRITE_SIZE are KiB per dispatch (rocprofv3); the dominant scan
-kernel's last dispatch is used.  The gfx950 x2 correction of FETCH_SIZE applies
-to 16-B-per-lane streaming reads only (MI355X_MICROARCH.md, HBM); the scan's
-memory-side reads are the staging copies of the tables and the haplotype words
-(16-B and 4-B per lane), so both the raw and the corrected figures are kept and
-the raw one is reported."""
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch (rocprofv3), summed over the last
+step's scan_mfma_kernel dispatches (tools/pmc_summary.py).  On gfx950
+FETCH_SIZE reports half the bytes of wide streaming reads
+(MI355X_MICROARCH.md, HBM section): it is doubled; WRITE_SIZE is taken as is.
+
+Usage: python tools/pmc_traffic.py OUT_DIR [bench.py args...]
+"""
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def main():
     root = sys.argv[1]
-    regions = int(sys.argv[2]) if len(sys.argv) > 2 else 10000
-    path = sys.argv[3] if len(sys.argv) > 3 else "mfma"
-    s = json.load(open(os.path.join(root, "sum_pmc_fetch.json")))
-    s.update(json.load(open(os.path.join(root, "sum_pmc_write.json"))))
-    fetch, write = s["FETCH_SIZE"] * 1024, s["WRITE_SIZE"] * 1024
-    out = {"workload": "C3", "regions": regions, "scan_path": path, "kernel": s.get("_kernel"),
-           "fetch_bytes": fetch, "write_bytes": write, "hbm_bytes_per_launch": fetch + write,
-           "fetch_bytes_x2_corrected": 2 * fetch,
-           "source": os.path.join(root, "sum_pmc_{fetch,write}.json") + " (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, "
-                     "separate passes, last scan dispatch)"}
-    dst = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+    sys.argv = ["bench.py"] + sys.argv[2:]
+    import bench
+    args = bench.parse()
+    f = json.load(open(os.path.join(root, "pmc_fetch", "pmc_summary.json")))
+    w = json.load(open(os.path.join(root, "pmc_write", "pmc_summary.json")))
+    fetch, write = f["FETCH_SIZE"] * 1024, w["WRITE_SIZE"] * 1024
+    out = {"config": bench.workload_key(args), "scan_path": "mfma",
+           "kernels": f.get("_kernels"), "dispatches": f.get("_dispatches"),
+           "fetch_size_bytes": fetch, "fetch_bytes_x2": 2 * fetch, "write_bytes": write,
+           "hbm_bytes_per_step": 2 * fetch + write,
+           "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes over `bench.py %s "
+                     "--steps 2 --warmup 0 --no-cpu --no-e2e`, the last step's scan_mfma_kernel dispatches "
+                     "summed, FETCH_SIZE x2" % " ".join(sys.argv[1:])}
+    dst = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
