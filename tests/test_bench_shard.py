@@ -34,10 +34,14 @@ def _rank(rank, world, port, out):
     T = tfbs_pkg.load()
     ps = _patterns(T, tempfile.mkdtemp())
     b = bench.shard_batch(T, ps, Args, rank)
-    elapsed = 1.0 + rank  # max over ranks must win
-    tot = bench.job_totals(dist, elapsed, b.num_windows, b.num_regions, b.num_effective_windows, "cpu")
+    elapsed = [1.0 + rank, 5.0 - rank]  # max over ranks must win, per entry
+    tot = bench.job_totals(dist, "cpu", elapsed, [b.num_windows, b.num_regions, b.num_effective_windows])
+    # the shards' regions, in rank order, as the whole job sees them
+    mine = [b.region_stats(r) for r in range(b.num_regions)]
+    every = [None] * world
+    dist.all_gather_object(every, mine)
     if rank == 0:
-        out.put(tot)
+        out.put((tot, [x for part in every for x in part]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -60,7 +64,7 @@ def test_two_rank_shards_tile_the_workload():
     procs = [ctx.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    tot = q.get(timeout=300)
+    tot, stats = q.get(timeout=300)
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
@@ -70,8 +74,9 @@ def test_two_rank_shards_tile_the_workload():
         regions = 2 * Args.regions
 
     whole = bench.shard_batch(T, ps, Both, 0)
-    elapsed, windows, regions, eff = tot
-    assert elapsed == 2.0
+    elapsed, (windows, regions, eff) = tot
+    assert elapsed == [2.0, 5.0]
+    assert stats == [whole.region_stats(r) for r in range(whole.num_regions)]
     assert regions == whole.num_regions == 2 * Args.regions
     assert windows == whole.num_windows
     assert eff == whole.num_effective_windows
