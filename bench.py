@@ -243,11 +243,18 @@ def main():
     T.check(L.tfbs_batch_reduce(sc.h, batch.h))
     t_red = time.perf_counter() - t_red
     n_rows = n_row_bytes = 0
-    t_rows = 0.0
-    if not args.no_e2e:
-        t_rows = time.perf_counter()
-        n_rows, n_row_bytes = batch.format_rows("chr1", 0, threads)
-        t_rows = time.perf_counter() - t_rows
+    t_rows = t_enc = 0.0
+    if not args.no_e2e:  # device per-sample encoding + row formatting, 512 regions at a time (the run flow's batch)
+        for r0 in range(0, batch.num_regions, 512):
+            r1 = min(batch.num_regions, r0 + 512)
+            t = time.perf_counter()
+            batch.encode(sc, r0, r1)
+            t_enc += time.perf_counter() - t
+            t = time.perf_counter()
+            nr, nb = batch.format_rows("chr1", 0, threads, r0, r1)
+            t_rows += time.perf_counter() - t
+            n_rows += nr
+            n_row_bytes += nb
 
     # ---- timed scan loop
     for _ in range(args.warmup):
@@ -279,7 +286,7 @@ def main():
     T.check(L.tfbs_batch_download(sc.h, batch.h))
     t_dense = time.perf_counter() - t_dense
 
-    e2e_s = fill_s + t_up + t_scan1 + t_red + t_rows
+    e2e_s = fill_s + t_up + t_scan1 + t_red + t_enc + t_rows
     (elapsed, e2e_max), tot = job_totals(dist, rdev, [elapsed, e2e_s],
                                          [batch.num_windows, batch.num_regions, batch.num_effective_windows,
                                           n_rows, n_row_bytes])
@@ -349,12 +356,14 @@ def main():
                 "windows_per_s": tot_windows / e2e_max,
                 "seconds": e2e_max,
                 "note": "one pass over the rank's batch: host prep (synthetic generation + load_diffs/"
-                        "patch/dedup/pack on %d threads) + upload + scan + device key reduction + row "
-                        "formatting (%d rows, %.3g bytes); the BGZF write is not included" % (
+                        "patch/dedup/pack on %d threads) + upload + scan + device key reduction + device "
+                        "per-sample encoding + row formatting from the codes (%d rows, %.3g bytes); the BGZF "
+                        "write is not included" % (
                             threads, tot_rows, tot_row_bytes),
                 "rank0_phases_s": {"host_prep_wall": fill_s, "synthetic_generation_thread_s": gen_s,
                                    "build_region_thread_s": build_s, "commit_wall": commit_s,
-                                   "upload": t_up, "scan": t_scan1, "key_reduce": t_red, "rows": t_rows},
+                                   "upload": t_up, "scan": t_scan1, "key_reduce": t_red,
+                                   "device_encode": t_enc, "rows": t_rows},
                 "rows": int(tot_rows),
             },
             "kernel_ms_avg": kms,

@@ -359,16 +359,24 @@ class RegionBatch:
         check(lib().tfbs_batch_region_stats(self.h, r, C.byref(a), C.byref(b)))
         return a.value, b.value
 
-    def scan(self, scanner, upload=True, download=True, reduce=False):
+    def scan(self, scanner, upload=True, download=True, reduce=False, encode=False):
         """tfbs_scan; then either download the dense counts or (reduce=True) classify the
-        keys on the GPU and fetch only what row emission needs (tfbs_batch_reduce)."""
+        keys on the GPU and fetch only what row emission needs (tfbs_batch_reduce), and
+        (encode=True) encode every varying key's per-sample totals on the GPU
+        (tfbs_batch_encode) so rows format from codes."""
         if upload:
             check(lib().tfbs_batch_upload(scanner.h, self.h))
         check(lib().tfbs_scan(scanner.h, self.h))
-        if reduce:
+        if reduce or encode:
             check(lib().tfbs_batch_reduce(scanner.h, self.h))
+            if encode:
+                self.encode(scanner)
         elif download:
             check(lib().tfbs_batch_download(scanner.h, self.h))
+
+    def encode(self, scanner, r0=0, r1=None):
+        """tfbs_batch_encode for regions [r0, r1) (after a reduced scan)."""
+        check(lib().tfbs_batch_encode(scanner.h, self.h, r0, self.num_regions if r1 is None else r1))
 
     def keys(self, region):
         """count_matches_by_sample for one region: {(bed, (s, e), pattern_id): (L, R)}."""
@@ -422,10 +430,11 @@ class RegionBatch:
         check(lib().tfbs_batch_region_digest(self.h, region, C.byref(d)))
         return d.value
 
-    def format_rows(self, chromosome, min_maf=0, threads=1):
-        """Format every region's rows on host threads and discard them: (rows, bytes)."""
+    def format_rows(self, chromosome, min_maf=0, threads=1, r0=0, r1=None):
+        """Format the rows of regions [r0, r1) on host threads and discard them: (rows, bytes)."""
         r, n = C.c_uint64(), C.c_uint64()
-        check(lib().tfbs_batch_format_rows(self.h, _u(chromosome), min_maf, threads, C.byref(r), C.byref(n)))
+        check(lib().tfbs_batch_format_rows(self.h, _u(chromosome), min_maf, threads, r0,
+                                           self.num_regions if r1 is None else r1, C.byref(r), C.byref(n)))
         return r.value, n.value
 
     def prep_seconds(self):

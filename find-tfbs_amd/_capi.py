@@ -99,6 +99,7 @@ SIGNATURES = [
     ("tfbs_scan", C.c_int, [vp, vp]),
     ("tfbs_batch_download", C.c_int, [vp, vp]),
     ("tfbs_batch_reduce", C.c_int, [vp, vp]),
+    ("tfbs_batch_encode", C.c_int, [vp, vp, C.c_size_t, C.c_size_t]),
     ("tfbs_batch_region_num_keys", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("tfbs_batch_region_key", C.c_int, [vp, C.c_size_t, C.c_size_t, u32p, u64p, u64p, u16p, u32p, u32p]),
     ("tfbs_batch_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, u32p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
@@ -106,7 +107,8 @@ SIGNATURES = [
                                          C.POINTER(C.c_size_t)]),
     ("tfbs_batch_region_digest", C.c_int, [vp, C.c_size_t, u64p]),
     ("tfbs_batch_region_stats", C.c_int, [vp, C.c_size_t, u32p, u32p]),
-    ("tfbs_batch_format_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32, u64p, u64p]),
+    ("tfbs_batch_format_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, u64p,
+                                         u64p]),
     ("tfbs_batch_prep_seconds", C.c_int, [vp, C.POINTER(C.c_double)]),
     ("tfbs_free", None, [C.c_void_p]),
     ("tfbs_counts_as_genotypes", C.c_int, [u32p, u32p, C.c_size_t, u32p, C.c_char_p, C.c_size_t, C.c_char_p,

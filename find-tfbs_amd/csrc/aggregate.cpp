@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -143,23 +144,111 @@ std::string strip_chr(const std::string &c) {
     return o;
 }
 
+// The device encoding of a key (tfbs_batch_encode) usable for region r, or UINT32_MAX.
+static uint32_t encoded_key(const Batch &B, size_t r, uint64_t key) {
+    if (!B.reduced || B.counts_valid || r < B.enc_r0 || r >= B.enc_r1) return UINT32_MAX;
+    const uint32_t vi = B.var_idx[key];
+    if (vi == UINT32_MAX) return UINT32_MAX;
+    const uint32_t e = B.enc_idx[vi];
+    return (e != UINT32_MAX && B.enc_hdr[e].status == 0) ? e : UINT32_MAX;
+}
+
+// counts_as_genotypes (main.rs:439-498) from a device encoding: the text of
+// each distinct total is built once (with the range multiplicity applied,
+// u32 arithmetic as counts_as_genotypes), a sample's text is the table entry
+// of its code.  Returns 1 (row), 0 (the totals do not vary) or -1 (the
+// multiplicity would wrap the totals: use the host path).
+static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t *maf, std::string &info,
+                             std::string &gts) {
+    const EncHdr &h = B.enc_hdr[e];
+    if ((uint64_t)h.hi * mult > UINT32_MAX) return -1;
+    if (h.n_vals < 2) return 0;
+    const uint32_t *vals = B.enc_vals.data() + (size_t)e * (kEncMaxVals + 1);
+    const uint32_t *hist = B.enc_hist.data() + (size_t)e * (kEncMaxVals + 1);
+    const uint32_t nv = h.n_vals, lo = vals[0] * mult, hi = vals[nv - 1] * mult;
+    const uint32_t i1 = (lo * 1000u * 3u + hi * 1000u) / 4u;  // u32, wrapping as --release
+    const uint32_t i3 = (lo * 1000u + hi * 1000u * 3u) / 4u;
+    const float lof = (float)lo;
+    const float spread = (float)hi - lof;
+    char tab[kEncMaxVals + 1][16];
+    uint8_t len[kEncMaxVals + 1];
+    uint64_t cls[3] = {0, 0, 0}, total = 0;
+    for (uint32_t k = 0; k < nv; k++) {
+        const uint32_t x = vals[k] * mult;
+        int c;
+        memset(tab[k], 0, 16);
+        if (x == lo) { memcpy(tab[k], "\t0|0:0.0", 8); len[k] = 8; c = 0; }
+        else if (x == hi) { memcpy(tab[k], "\t1|1:2.0", 8); len[k] = 8; c = 2; }
+        else {
+            const uint32_t x1000 = x * 1000u;
+            c = x1000 < i1 ? 0 : (x1000 < i3 ? 1 : 2);
+            const float ds = (((float)x - lof) * 2.0f) / spread;  // f32 throughout
+            char buf[32];
+            const int m = snprintf(buf, sizeof buf, "%s:%.4f", c == 0 ? "\t0|0" : (c == 1 ? "\t0|1" : "\t1|1"),
+                                   (double)ds);
+            memcpy(tab[k], buf, 16);
+            len[k] = (uint8_t)m;
+        }
+        cls[c] += hist[k];
+        total += (uint64_t)hist[k] * len[k];
+    }
+    const uint32_t zero = (uint32_t)cls[0], one = (uint32_t)cls[1], two = (uint32_t)cls[2];
+    if (zero >= one && zero >= two) *maf = one + two;
+    else if (two >= zero && two >= one) *maf = zero + one;
+    else *maf = zero + two;
+    char buf[48];
+    info += "COUNTS=";
+    for (uint32_t k = 0; k < nv; k++) {
+        const int m = snprintf(buf, sizeof buf, k ? ",%u" : "%u", vals[k] * mult);
+        info.append(buf, (size_t)m);
+    }
+    const int m = snprintf(buf, sizeof buf, ";freqs=%u/%u/%u", zero, one, two);
+    info.append(buf, (size_t)m);
+    const size_t at = gts.size();
+    gts.resize(at + total + 16);
+    char *dst = &gts[at];
+    const uint8_t *codes = B.enc_codes.data() + (size_t)e * B.n_samples;
+    for (uint32_t s = 0; s < B.n_samples; s++) {
+        const uint8_t c = codes[s];
+        memcpy(dst, tab[c], 16);
+        dst += len[c];
+    }
+    gts.resize(at + total);
+    return 1;
+}
+
 // Rows of one region, each without its "<chr>\t<POS>\t" prefix (the POS
-// counter is assigned in order afterwards).
+// counter is assigned in order afterwards).  Keys the device encoded
+// (tfbs_batch_encode) are formatted from their value tables and codes; the
+// others from the per-haplotype counts through the membership.
 void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<std::string> &rows) {
     const uint32_t H = 2 * B.n_samples;
-    std::vector<uint32_t> l(B.n_samples), r(B.n_samples);
-    Membership M(R, H);
+    const size_t ri = (size_t)(&R - B.rh.data());
+    std::vector<uint32_t> l, r;
+    std::unique_ptr<Membership> M;
     std::string info, gts;
     for (const KeyRef &k : region_keys(B, R)) {
         if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
-        for (uint32_t s = 0; s < B.n_samples; s++) {
-            l[s] = count_of(B, R, M.local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
-            r[s] = count_of(B, R, M.local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
-        }
         uint32_t maf = 0;
         info.clear();
         gts.clear();
-        if (!counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts)) continue;
+        const uint32_t e = encoded_key(B, ri, key_of(B, R, k.slot, k.ik->slot));
+        int made = e == UINT32_MAX ? -1 : encoded_genotypes(B, e, k.ik->mult, &maf, info, gts);
+        if (made < 0) {
+            info.clear();
+            gts.clear();
+            if (!M) {
+                M.reset(new Membership(R, H));
+                l.resize(B.n_samples);
+                r.resize(B.n_samples);
+            }
+            for (uint32_t s = 0; s < B.n_samples; s++) {
+                l[s] = count_of(B, R, M->local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
+                r[s] = count_of(B, R, M->local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
+            }
+            made = counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts) ? 1 : 0;
+        }
+        if (!made) continue;
         if (maf < min_maf) continue;
         const uint16_t pid = B.slot_pid[k.slot];
         auto it = B.pats->names.find(pid);
@@ -341,14 +430,14 @@ int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_ma
 }
 
 int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t threads,
-                           uint64_t *n_rows, uint64_t *n_bytes) {
+                           size_t r0, size_t r1, uint64_t *n_rows, uint64_t *n_bytes) {
     if (!b || !chromosome || !n_rows || !n_bytes) return tfbs::fail(TFBS_E_ARG, "null argument");
     const Batch &B = b->b;
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
-    const size_t n = B.rh.size();
+    const size_t n = std::min(r1, B.rh.size());
     const size_t prefix = tfbs::strip_chr(chromosome).size() + 2;
-    std::atomic<size_t> next(0);
+    std::atomic<size_t> next(std::min(r0, n));
     std::atomic<uint64_t> rows(0), bytes(0);
     auto work = [&]() {
         std::vector<std::string> rr;

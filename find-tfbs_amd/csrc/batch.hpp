@@ -66,7 +66,18 @@ struct Batch {
     std::vector<uint8_t> key_flags;
     std::vector<uint32_t> var_off;        // UINT32_MAX unless the key varies
     std::vector<uint32_t> var_counts;
+    std::vector<DevVarKey> var_keys;      // the varying keys in reduction order
+    std::vector<uint32_t> var_idx;        // key -> index in var_keys, UINT32_MAX unless it varies
     bool reduced = false;
+    // device-side per-sample encoding of the varying keys of regions
+    // [enc_r0, enc_r1) (tfbs_batch_encode): per encoded key (index in enc_key
+    // order) its header, value table, per-value sample counts and codes;
+    // enc_idx[var key index] = encoded key or UINT32_MAX
+    uint32_t enc_r0 = 0, enc_r1 = 0;
+    std::vector<uint32_t> enc_idx;
+    std::vector<EncHdr> enc_hdr;
+    std::vector<uint32_t> enc_vals, enc_hist;  // (kEncMaxVals + 1) per encoded key
+    std::vector<uint8_t> enc_codes;            // n_samples per encoded key
 
     std::vector<RegionH> rh;
     uint64_t windows = 0, eff_windows = 0, cell_ops = 0;

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -92,7 +94,11 @@ struct tfbs_ctx {
     // key reduction (tfbs_batch_reduce)
     DevBuf<uint32_t> key_first, var_counts;
     DevBuf<uint8_t> key_flags;
-    DevBuf<DevVarKey> var_keys;
+    DevBuf<DevVarKey> var_keys, enc_keys;
+    // per-sample encoding (tfbs_batch_encode)
+    DevBuf<uint8_t> enc_memb, enc_codes;
+    DevBuf<EncHdr> enc_hdr;
+    DevBuf<uint32_t> enc_vals, enc_hist;
     const tfbs_batch *resident = nullptr;
     float last_ms = 0.f;
     int last_launches = 0;
@@ -197,6 +203,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
+    ctx->enc_keys.release(); ctx->enc_memb.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
+    ctx->enc_vals.release(); ctx->enc_hist.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
@@ -348,6 +356,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->last_launches = n;
     ctx->timing_pending = true;
     b->b.counts_valid = b->b.reduced = false;
+    b->b.enc_r0 = b->b.enc_r1 = 0;
     return TFBS_OK;
 }
 
@@ -385,6 +394,7 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     // columns of the varying keys, one count per distinct haplotype
     std::vector<DevVarKey> vk;
     B.var_off.assign(n_keys, UINT32_MAX);
+    B.var_idx.assign(n_keys, UINT32_MAX);
     uint64_t total = 0;
     for (uint32_t r = 0; r < B.regions.size(); r++) {
         const DevRegion &rg = B.regions[r];
@@ -394,11 +404,15 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
             if (B.key_flags[ko + j] & KEY_VARIES) {
                 if (total + rg.hap_count >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
                 B.var_off[ko + j] = (uint32_t)total;
+                B.var_idx[ko + j] = (uint32_t)vk.size();
                 vk.push_back(DevVarKey{r, j, total});
                 total += rg.hap_count;
             }
     }
     B.var_counts.resize(total);
+    B.var_keys = vk;
+    B.enc_r0 = B.enc_r1 = 0;
+    B.enc_idx.clear();
     if (!vk.empty()) {
         if ((rc = ctx->var_keys.put(vk, ctx->stream)) || (rc = ctx->var_counts.ensure(total))) return rc;
         if ((rc = launch_key_gather(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->var_keys.p,
@@ -408,6 +422,88 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.reduced = true;
+    return TFBS_OK;
+}
+
+int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    Batch &B = b->b;
+    if (!B.reduced) return tfbs::fail(TFBS_E_STATE, "keys not reduced (tfbs_batch_reduce)");
+    if (!B.keep_membership) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    r1 = std::min(r1, B.rh.size());
+    r0 = std::min(r0, r1);
+    HIP_TRY(hipSetDevice(ctx->device));
+    B.enc_r0 = B.enc_r1 = 0;
+    B.enc_idx.assign(B.var_keys.size(), UINT32_MAX);
+    B.enc_hdr.clear();
+    B.enc_vals.clear();
+    B.enc_hist.clear();
+    B.enc_codes.clear();
+    const uint32_t N = B.n_samples, H = 2 * N;
+    if (N == 0 || r0 == r1) {
+        B.enc_r0 = (uint32_t)r0;
+        B.enc_r1 = (uint32_t)r1;
+        return TFBS_OK;
+    }
+    // the keys to encode: varying keys of [r0, r1) whose region has <= 255 distinct haplotypes
+    std::vector<DevVarKey> ek;
+    std::vector<uint32_t> ek_var;
+    for (uint32_t i = 0; i < B.var_keys.size(); i++) {
+        const DevVarKey &k = B.var_keys[i];
+        if (k.region < r0 || k.region >= r1 || B.regions[k.region].hap_count > kEncMaxHaps) continue;
+        B.enc_idx[i] = (uint32_t)ek.size();
+        ek.push_back(k);
+        ek_var.push_back(i);
+    }
+    const size_t nk = ek.size();
+    // membership rows: haplotype id -> distinct index (u8), 2 N bytes per region of [r0, r1)
+    std::vector<uint8_t> memb((r1 - r0) * (size_t)H);
+    {
+        const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::atomic<size_t> next(r0);
+        auto work = [&]() {
+            for (size_t r; (r = next.fetch_add(1)) < r1;) {
+                const RegionH &R = B.rh[r];
+                if (R.hap_count > kEncMaxHaps) continue;
+                uint8_t *row = memb.data() + (r - r0) * (size_t)H;
+                memset(row, R.ref_local < 0 ? 0 : R.ref_local, H);
+                for (size_t i = 0; i < R.nonref_id.size(); i++) row[R.nonref_id[i]] = (uint8_t)R.nonref_local[i];
+            }
+        };
+        std::vector<std::thread> ts;
+        for (uint32_t t = 1; t < T; t++) ts.emplace_back(work);
+        work();
+        for (auto &t : ts) t.join();
+    }
+    int rc;
+    if ((rc = ctx->enc_memb.put(memb, ctx->stream)) || (rc = ctx->enc_keys.put(ek, ctx->stream)) ||
+        (rc = ctx->enc_hdr.ensure(std::max<size_t>(nk, 1))) ||
+        (rc = ctx->enc_vals.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
+        (rc = ctx->enc_hist.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
+        (rc = ctx->enc_codes.ensure(std::max<size_t>(nk, 1) * N)))
+        return rc;
+    if ((rc = launch_key_encode(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->enc_keys.p, (uint32_t)nk,
+                                ctx->enc_memb.p, (uint32_t)r0, N, ctx->enc_hdr.p, ctx->enc_vals.p, ctx->enc_hist.p,
+                                ctx->enc_codes.p, ctx->stream)))
+        return rc;
+    B.enc_hdr.resize(nk);
+    B.enc_vals.resize(nk * (kEncMaxVals + 1));
+    B.enc_hist.resize(nk * (kEncMaxVals + 1));
+    B.enc_codes.resize(nk * (size_t)N);
+    if (nk) {
+        HIP_TRY(hipMemcpyAsync(B.enc_hdr.data(), ctx->enc_hdr.p, nk * sizeof(EncHdr), hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipMemcpyAsync(B.enc_vals.data(), ctx->enc_vals.p, B.enc_vals.size() * 4, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipMemcpyAsync(B.enc_hist.data(), ctx->enc_hist.p, B.enc_hist.size() * 4, hipMemcpyDeviceToHost,
+                               ctx->stream));
+        HIP_TRY(hipMemcpyAsync(B.enc_codes.data(), ctx->enc_codes.p, B.enc_codes.size(), hipMemcpyDeviceToHost,
+                               ctx->stream));
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    B.enc_r0 = (uint32_t)r0;
+    B.enc_r1 = (uint32_t)r1;
     return TFBS_OK;
 }
 

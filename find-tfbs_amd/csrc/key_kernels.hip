@@ -67,7 +67,128 @@ __global__ __launch_bounds__(256) void key_gather_kernel(const DevHap *__restric
     for (uint32_t l = threadIdx.x & 63; l < rg.hap_count; l += 64) out[vk.out_off + l] = counts[base + (uint64_t)l * K + vk.j];
 }
 
+// counts_as_genotypes' per-sample half (main.rs:439-498) for one varying key:
+// the sample totals, their min / max, the distinct values (a bitmap of
+// hi - lo + 1 bits in LDS, ranks from per-word prefix counts) and one code per
+// sample.  Three passes over the region's membership row (L2-resident: every
+// key of the region reads it); the key's column of distinct-haplotype counts
+// sits in LDS.  The range multiplicity and the text stay on the host, which
+// formats a row from the value table and the codes (aggregate.cpp).
+constexpr int kEncBlock = 256;
+constexpr uint32_t kEncWords = kEncMaxRange / 32;
+
+__global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__restrict__ haps,
+                                                                 const DevRegion *__restrict__ regions,
+                                                                 const uint32_t *__restrict__ counts, uint32_t n_slots,
+                                                                 const DevVarKey *__restrict__ keys,
+                                                                 const uint8_t *__restrict__ memb, uint32_t region0,
+                                                                 uint32_t n_samples, EncHdr *__restrict__ hdr,
+                                                                 uint32_t *__restrict__ vals,
+                                                                 uint32_t *__restrict__ hist,
+                                                                 uint8_t *__restrict__ codes) {
+    __shared__ uint32_t s_c[kEncMaxHaps + 1];
+    __shared__ uint32_t s_bits[kEncWords];
+    __shared__ uint16_t s_rank[kEncWords];  // distinct values in the words before
+    __shared__ uint32_t s_hist[kEncMaxVals + 1];
+    __shared__ uint32_t s_red[2 * kEncBlock / 64];
+    __shared__ uint32_t s_nv;
+    const uint32_t k = blockIdx.x;
+    const DevVarKey vk = keys[k];
+    const DevRegion rg = regions[vk.region];
+    const uint32_t K = n_slots * rg.n_inner;
+    const uint64_t base = haps[rg.hap_begin].count_off;
+    for (uint32_t l = threadIdx.x; l < rg.hap_count; l += kEncBlock) s_c[l] = counts[base + (uint64_t)l * K + vk.j];
+    __syncthreads();
+    const uint16_t *m = reinterpret_cast<const uint16_t *>(memb + (size_t)(vk.region - region0) * 2 * n_samples);
+    auto total = [&](uint32_t s) {
+        const uint32_t pr = m[s];
+        return s_c[pr & 0xFF] + s_c[pr >> 8];  // u32 wrapping, as the reference's additions
+    };
+    // pass 1: min / max
+    uint32_t lo = UINT32_MAX, hi = 0;
+    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
+        const uint32_t v = total(s);
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+    for (int o = 32; o; o >>= 1) {
+        lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+        hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+    }
+    const uint32_t wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_red[wave] = lo;
+        s_red[kEncBlock / 64 + wave] = hi;
+    }
+    __syncthreads();
+    lo = s_red[0];
+    hi = s_red[kEncBlock / 64];
+    for (int w = 1; w < kEncBlock / 64; w++) {
+        lo = min(lo, s_red[w]);
+        hi = max(hi, s_red[kEncBlock / 64 + w]);
+    }
+    if (hi - lo >= kEncMaxRange) {
+        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, 0, 1};
+        return;
+    }
+    // pass 2: which values occur
+    const uint32_t nw = (hi - lo) / 32 + 1;
+    for (uint32_t w = threadIdx.x; w < nw; w += kEncBlock) s_bits[w] = 0;
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
+        const uint32_t d = total(s) - lo;
+        atomicOr(&s_bits[d >> 5], 1u << (d & 31));
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // ranks: a serial prefix over <= 2048 words
+        uint32_t r = 0;
+        for (uint32_t w = 0; w < nw; w++) {
+            s_rank[w] = (uint16_t)min(r, 0xFFFFu);
+            r += __popc(s_bits[w]);
+        }
+        s_nv = r;
+    }
+    for (uint32_t i = threadIdx.x; i <= kEncMaxVals; i += kEncBlock) s_hist[i] = 0;
+    __syncthreads();
+    const uint32_t nv = s_nv;
+    if (nv > kEncMaxVals) {
+        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 1};
+        return;
+    }
+    for (uint32_t w = threadIdx.x; w < nw; w += kEncBlock) {  // the sorted value table
+        uint32_t b = s_bits[w], r = s_rank[w];
+        while (b) {
+            const uint32_t t = __ffs(b) - 1;
+            b &= b - 1;
+            vals[(size_t)k * (kEncMaxVals + 1) + r++] = lo + 32 * w + t;
+        }
+    }
+    // pass 3: codes and per-value sample counts
+    uint8_t *out = codes + (size_t)k * n_samples;
+    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
+        const uint32_t d = total(s) - lo, w = d >> 5;
+        const uint32_t c = s_rank[w] + __popc(s_bits[w] & ((1u << (d & 31)) - 1u));
+        out[s] = (uint8_t)c;
+        atomicAdd(&s_hist[c], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nv; i += kEncBlock) hist[(size_t)k * (kEncMaxVals + 1) + i] = s_hist[i];
+    if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 0};
+}
+
 }  // namespace
+
+int launch_key_encode(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
+                      const DevVarKey *keys, uint32_t n_keys, const uint8_t *memb, uint32_t region0,
+                      uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
+                      hipStream_t stream) {
+    if (n_keys == 0) return TFBS_OK;
+    hipLaunchKernelGGL(key_encode_kernel, dim3(n_keys), dim3(kEncBlock), 0, stream, haps, regions, counts, n_slots,
+                       keys, memb, region0, n_samples, hdr, vals, hist, codes);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_encode_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
 
 int launch_key_reduce(const DevHap *haps, const DevRegion *regions, uint32_t n_regions, const uint32_t *counts,
                       uint32_t n_slots, uint32_t *first, uint8_t *flags, hipStream_t stream) {

@@ -185,7 +185,8 @@ template <class Emit> int run_shard(const RunSetup &S, Shard &sh, Emit &&emit) {
         tfbs_batch *bb = cur.get();
         Batch &B = bb->b;
         t0 = now();
-        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)))
+        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)) ||
+            (rc = tfbs_batch_encode(ctx, bb, 0, B.rh.size())))
             return rc;
         double t1 = now();
         sh.t_gpu += t1 - t0;

@@ -48,6 +48,12 @@ namespace {
 #ifndef TFBS_MFMA_QUAD  // 2 strand tiles x 2 window tiles per round at K depth 1 (0: pairs only)
 #define TFBS_MFMA_QUAD 1
 #endif
+#ifndef TFBS_MFMA_W4  // 1 strand tile x 4 window tiles per round (steps of 128 windows): bit d-1 = K depth d
+#define TFBS_MFMA_W4 0
+#endif
+#ifndef TFBS_MFMA_W4_PF  // ... with the next round's B fragment read ahead: bit d-1 = K depth d
+#define TFBS_MFMA_W4_PF 1
+#endif
 
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -64,7 +70,10 @@ constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup at 4 workgroup
 constexpr uint32_t kMfmaWindowTiles[kMMaxChunks + 1] = {1, 2, 2};
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
 constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 6, 5};
-constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4};
+#ifndef TFBS_MFMA_D2_WAVES
+#define TFBS_MFMA_D2_WAVES 4
+#endif
+constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, TFBS_MFMA_D2_WAVES};
 
 // The packed words (and N-mask words) a lane needs for its window of the
 // 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
@@ -191,6 +200,9 @@ constexpr uint32_t kMQueue = 384;  // entries per wave (a round of four tile tes
 __shared__ uint64_t s_queue[kMBlock / 64][kMQueue];
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
+#if TFBS_MFMA_PROBE == 13
+__device__ unsigned long long g_sink;  // probe 13: the fired-lane count, so the tests stay live
+#endif
 #if TFBS_MFMA_PROBE == 4
 __device__ unsigned long long g_probe[5];
 #endif
@@ -279,7 +291,7 @@ __device__ __forceinline__ void drain_entry(const ScanArgs &A, const uint32_t *w
 // h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
 __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                             uint32_t h0, uint32_t n, uint32_t wave) {
-#if TFBS_MFMA_PROBE == 12
+#if TFBS_MFMA_PROBE == 12 || TFBS_MFMA_PROBE == 13
     return;  // timing only: queued candidates are dropped
 #endif
     for (uint32_t e = threadIdx.x & 63; e < n; e += 64) drain_entry(A, words, tile0, h0, s_queue[wave][e]);
@@ -339,6 +351,10 @@ __device__ __forceinline__ uint64_t coarse_test(const v16f &acc, float thr) {
 __device__ __forceinline__ void queue_tile(const v16f &acc, float thr, uint64_t fired, uint32_t ti, uint32_t hh,
                                            uint32_t i0, uint32_t lane, uint32_t wave, uint32_t &qn) {
     if (__builtin_expect(fired == 0, 1)) return;
+#if TFBS_MFMA_PROBE == 13
+    qn += (uint32_t)__popcll(fired) & 1u;  // timing only: the tests' cost without the candidate handling
+    return;
+#endif
 #if TFBS_MFMA_PROBE == 4
     if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[4], 1ull);
     if (fired & (1ull << lane)) atomicAdd(&g_probe[0], 1ull);
@@ -385,6 +401,63 @@ __device__ __forceinline__ void pair_scores(const char *s_img, const DevMSuper &
     thr = f.thr;
 }
 
+// Four window tiles x one strand tile per round (TFBS_MFMA_W4): one B fragment
+// read (prefetched a round ahead) feeds four MFMA chains, whose tests share the
+// strand tile's thresholds.  Steps of 128 windows while at least three of their
+// window tiles hold windows; returns the first window the pair loop still has
+// to score.
+template <int NK>
+__device__ __forceinline__ uint32_t scan_hap_w4(const ScanArgs &A, const DevMSuper &S, const char *s_img,
+                                                const uint32_t *words, const DevHap &hm, uint32_t nwin, uint32_t hh,
+                                                uint32_t lane, uint32_t wave, uint32_t tile0, uint32_t h0,
+                                                uint32_t &qn) {
+    const uint32_t nt = S.tile_count;
+    const char *tab = s_img - kMOnehotBytes;
+    uint32_t i0 = 0;
+    for (; i0 + 2 * kMWindows < nwin; i0 += 4 * kMWindows) {
+        v4i a[4][NK];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            WinWords ww;
+            load_window(A, words, hm, i0 + t * kMWindows, lane, ww);
+            build_onehot<NK>(hm, i0 + t * kMWindows, lane, ww, tab, a[t]);
+        }
+        BFrag<NK> f;
+        load_tile<NK>(s_img, S, 0, lane, f);
+        constexpr bool kPf = (TFBS_MFMA_W4_PF >> (NK - 1)) & 1;
+        for (uint32_t ti = 0; ti < nt; ti++) {
+            BFrag<NK> g;
+            if (!kPf) {
+                if (ti) load_tile<NK>(s_img, S, ti, lane, f);
+            } else if (ti + 1 < nt) {
+                load_tile<NK>(s_img, S, ti + 1, lane, g);  // next round's fragment
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            v16f c[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) c[t] = v16f{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int kc = 0; kc < NK; kc++)
+#pragma unroll
+                for (int t = 0; t < 4; t++) c[t] = mfma_chunk(a[t][kc], f.b[kc], f.c[kc], c[t]);
+            __builtin_amdgcn_sched_barrier(0);
+            const float thr = f.thr;
+            uint64_t q[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++) q[t] = coarse_test(c[t], thr);
+            if (kPf) f = g;
+            if (__builtin_expect((q[0] | q[1] | q[2] | q[3]) == 0, 1)) continue;  // one branch for four tests
+#pragma unroll
+            for (int t = 0; t < 4; t++) queue_tile(c[t], thr, q[t], ti, hh, i0 + t * kMWindows, lane, wave, qn);
+            if (qn > kMQueue - 256) {
+                drain_queue(A, words, tile0, h0, qn, wave);
+                qn = 0;
+            }
+        }
+    }
+    return i0;
+}
+
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
 // of this workgroup's haplotypes, biased by their first word, or global memory).
 template <int NK>
@@ -406,10 +479,13 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         // feeds two MFMAs (the LDS read rate, not the matrix core, bounds one
         // read per MFMA)
         constexpr uint32_t kStep = kMfmaWindowTiles[NK] * kMWindows;
+        const uint32_t ibeg = ((TFBS_MFMA_W4 >> (NK - 1)) & 1) ? scan_hap_w4<NK>(A, S, s_img, words, hm, nwin, hh, lane, wave, tile0, h0, qn)
+                                           : 0;
+        if (ibeg >= nwin) continue;
         WinWords ww0, ww1;
-        load_window(A, words, hm, 0, lane, ww0);
-        if (kStep > kMWindows && kMWindows < nwin) load_window(A, words, hm, kMWindows, lane, ww1);
-        for (uint32_t i0 = 0; i0 < nwin; i0 += kStep) {
+        load_window(A, words, hm, ibeg, lane, ww0);
+        if (kStep > kMWindows && ibeg + kMWindows < nwin) load_window(A, words, hm, ibeg + kMWindows, lane, ww1);
+        for (uint32_t i0 = ibeg; i0 < nwin; i0 += kStep) {
             const bool two = kStep > kMWindows && i0 + kMWindows < nwin;
             v4i a0[NK], a1[NK];
             build_onehot<NK>(hm, i0, lane, ww0, tab, a0);
@@ -512,6 +588,10 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         }
     }
     // the waves' last entries, pooled: every wave drains a share of the sum
+#if TFBS_MFMA_PROBE == 13
+    if (lane == 0) atomicAdd(&g_sink, (unsigned long long)qn);
+    return;
+#endif
     if (lane == 0) s_qn[wave] = qn;
     __syncthreads();
     drain_pooled(A, words, tile0, h0);

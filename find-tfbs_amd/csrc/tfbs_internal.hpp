@@ -136,6 +136,19 @@ struct DevRegion {
     uint32_t hap_count;
 };
 
+// Per-sample encoding of one varying key (tfbs_batch_encode, key_encode_kernel):
+// v[s] = C[hap(2s)] + C[hap(2s+1)] over the samples (counts before the inner
+// range's multiplicity), its min / max, the sorted distinct values (COUNTS=,
+// main.rs:466-470) with their sample counts, and one u8 code per sample = the
+// rank of v[s] among them.  status != 0: too many distinct values or too wide a
+// range for the encoding -- the rows take the host path for that key.
+struct EncHdr {
+    uint32_t lo, hi, n_vals, status;
+};
+constexpr uint32_t kEncMaxVals = 255;       // u8 codes
+constexpr uint32_t kEncMaxRange = 1u << 16;  // value bitmap of hi - lo + 1 bits in LDS
+constexpr uint32_t kEncMaxHaps = 255;       // u8 membership: distinct haplotypes per region
+
 // One key (region, slot * n_inner + range) whose distinct-haplotype counts differ;
 // the gather copies its hap_count counts to out_off (tfbs_batch_reduce).
 struct DevVarKey {

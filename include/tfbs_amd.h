@@ -219,6 +219,14 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
  * flags, one count per key and the per-haplotype counts of the disagreeing
  * keys.  The key / row functions below then work as after a download. */
 int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
+/* counts_as_genotypes' per-sample half on the device (main.rs:439-534, SURVEY.md
+ * 8(f) f1) for the varying keys of regions [r0, r1) after tfbs_batch_reduce:
+ * per key v[s] = C[hap(2s)] + C[hap(2s+1)] over the samples, min / max, the
+ * sorted distinct values with their sample counts, and one u8 code per sample;
+ * rows of these regions are then formatted from the codes (no per-sample
+ * count gather on the host).  Keys whose region has > 255 distinct haplotypes,
+ * > 255 distinct totals or a total range >= 65536 keep the host path. */
+int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1);
 
 /* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
  * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */
@@ -241,11 +249,11 @@ int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chrom
 int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
 /* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
 int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
-/* Formats every region's rows (main.rs:415-429) on `threads` host threads and
+/* Formats the rows of regions [r0, r1) (main.rs:415-429) on `threads` host threads and
  * discards them: the row count and bytes (without POS digits).  The bench's
  * end-to-end leg times it; tfbs_run writes the same rows. */
 int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t threads,
-                           uint64_t *n_rows, uint64_t *n_bytes);
+                           size_t r0, size_t r1, uint64_t *n_rows, uint64_t *n_bytes);
 /* Host prep seconds of the batch's synthetic fills (out[4]): generation and
  * build_region (thread CPU-seconds, summed), the serial commit and the whole
  * fill (wall). */

@@ -71,9 +71,9 @@ def build_batch(pset, n_samples, beds, regions):
     return b
 
 
-def run_product(scanner, pset, n_samples, beds, regions, chrom="chr1", min_maf=0, reduce=False):
+def run_product(scanner, pset, n_samples, beds, regions, chrom="chr1", min_maf=0, reduce=False, encode=False):
     b = build_batch(pset, n_samples, beds, regions)
-    b.scan(scanner, reduce=reduce)
+    b.scan(scanner, reduce=reduce, encode=encode)
     keys = [b.keys(i) for i in range(b.num_regions)]
     rows, _ = b.rows(chrom, min_maf)
     return keys, rows, b

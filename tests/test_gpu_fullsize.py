@@ -8,6 +8,8 @@ generator, seeds, PWM sets and thresholds), and checked three ways:
   of >= 200 regions (first, last, the last haplotype group, evenly spaced ones)
   key by key -- the per-sample L/R vectors of count_matches_by_sample -- and
   row by row (POS aside: the oracle numbers rows over its own region subset);
+* the device per-sample encoding (tfbs_batch_encode: the rows formatted from
+  per-sample codes) against the oracle on the same regions;
 * device key reduction (the run flow's tfbs_batch_reduce) against the dense
   count download over the WHOLE batch, region by region, through
   tfbs_batch_region_digest (keys + every distinct haplotype's count);
@@ -174,6 +176,14 @@ def _fullsize(tmp_path, cfg, n_check, n_extra_n=0):
         jobs += [(n_regions + k, r["merged"], r["ref"], r["records"]) for k, r in enumerate(extra)]
         ref = _oracle_regions(ps, n_samples, seed, indel, jobs)
         n_rows = _check_vs_oracle(b, ref, "reduce")
+        # the device per-sample encoding (f1) the run flow formats rows from, 2 000
+        # regions at a time (codes: one byte per sample per varying key)
+        n_enc = 0
+        for r0 in range(0, b.num_regions, 2000):
+            r1 = min(b.num_regions, r0 + 2000)
+            b.encode(sc, r0, r1)
+            n_enc += _check_vs_oracle(b, {i: ref[i] for i in ref if r0 <= i < r1}, "encode")
+        assert n_enc == n_rows
         # dense download over the same batch, rescanned
         b.scan(sc, upload=False, download=True)
         assert _digests(b) == reduced

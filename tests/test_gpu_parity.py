@@ -286,15 +286,17 @@ def _compare(ps, n_samples, beds, regions, min_maf=0):
     okeys, orows, _ = run_oracle(ps, n_samples, beds, regions, min_maf=min_maf)
     sc = T.Scanner(ps)
     try:
-        # dense download, and the device key reduction (f1) the run flow uses
-        for reduce in (False, True):
-            pkeys, prows, b = run_product(sc, ps, n_samples, beds, regions, min_maf=min_maf, reduce=reduce)
+        # dense download, the device key reduction and the device per-sample encoding
+        # (f1) the run flow uses
+        for reduce, encode in ((False, False), (True, False), (True, True)):
+            pkeys, prows, b = run_product(sc, ps, n_samples, beds, regions, min_maf=min_maf, reduce=reduce,
+                                          encode=encode)
             assert len(okeys) == len(pkeys)
             for i, (a, z) in enumerate(zip(okeys, pkeys)):
                 assert a.keys() == z.keys(), (reduce, i)
                 for k in a:
                     assert a[k] == z[k], (reduce, i, k)
-            assert prows == orows, reduce
+            assert prows == orows, (reduce, encode)
     finally:
         sc.close()
     return b
@@ -412,12 +414,14 @@ def test_large_scan_counts_are_invariant_to_tiling(tmp_path, monkeypatch):
     assert rows_dense.count("\n") > 0
 
 
-def test_many_variant_regions_vs_oracle(tmp_path):
+@pytest.mark.parametrize("n", [120, 300])
+def test_many_variant_regions_vs_oracle(tmp_path, n):
     """Regions with 64 and ~90 distinct diffs: both haplotype-grouping paths of the
-    host (64-bit diff masks / sorted diff lists) through the GPU scan vs the oracle."""
+    host (64-bit diff masks / sorted diff lists) through the GPU scan vs the oracle;
+    at 300 samples the regions have > 255 distinct haplotypes, beyond the device
+    encoding's u8 membership (those keys take the host path)."""
     from helpers import many_variant_regions
     ps, _ = synth_patterns(tmp_path, 10, 2, 31, thr=2e-3)
-    n = 120
     regions = many_variant_regions(n, ps.max_length)
     beds = [("synthetic.bed", [tuple(r["merged"]) for r in regions])]
     _compare(ps, n, beds, regions)
