@@ -207,11 +207,15 @@ static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t
     const size_t at = gts.size();
     gts.resize(at + total + 16);
     char *dst = &gts[at];
-    const uint8_t *codes = B.enc_codes.data() + (size_t)e * B.n_samples;
-    for (uint32_t s = 0; s < B.n_samples; s++) {
-        const uint8_t c = codes[s];
-        memcpy(dst, tab[c], 16);
-        dst += len[c];
+    const uint8_t *codes = B.enc_codes.data() + B.enc_code_off[e];
+    const uint32_t width = h.width, per = 8 / width, mask = (1u << width) - 1u;
+    for (uint32_t s = 0; s < B.n_samples; s += per) {
+        uint32_t byte = codes[s / per];
+        for (uint32_t q = 0; q < per && s + q < B.n_samples; q++, byte >>= width) {
+            const uint32_t c = byte & mask;
+            memcpy(dst, tab[c], 16);
+            dst += len[c];
+        }
     }
     gts.resize(at + total);
     return 1;

@@ -319,75 +319,150 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     return TFBS_OK;
 }
 
-// Appends a built region to the batch: packs its haplotypes for the GPU.
-void commit_region(Batch &B, RegionBuilt &&built) {
-    RegionH &R = built.R;
-    const std::vector<Distinct> &dist = built.dist;
-    const std::vector<uint32_t> &carriers = built.carriers;
-    // ---- pack
-    const uint32_t region_index = (uint32_t)B.rh.size();
-    R.hap_begin = (uint32_t)B.haps.size();
-    R.hap_count = (uint32_t)dist.size();
-    DevRegion dr{};
-    dr.inner_off = (uint32_t)(B.inner.size() / 2);
-    dr.n_inner = (uint32_t)R.ranges.size();
-    dr.hap_begin = R.hap_begin;
-    dr.hap_count = R.hap_count;
-    R.key_off = (uint64_t)dr.inner_off * B.n_slots;
-    for (auto &r : R.ranges) {
-        // positions relative to ext_start, clamped: only containment of small
-        // non-negative positions is ever tested, which clamping preserves.
-        auto rel = [&](uint64_t x) -> int32_t {
-            if (x < R.es) { uint64_t d = R.es - x; return d > (1u << 30) ? -(1 << 30) : -(int32_t)d; }
-            uint64_t d = x - R.es;
-            return d > (1u << 30) ? (1 << 30) : (int32_t)d;
+// Appends built regions to the batch in order: packs their haplotypes for the
+// GPU.  Offsets are laid out serially (prefix sums over the regions'
+// haplotypes), the packing of bases, N masks and positions runs on `threads`
+// threads.
+void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads) {
+    const size_t nr = built.size();
+    if (!nr) return;
+    // per haplotype: length, has N, affine positions (parallel scan of the sequences)
+    struct HapInfo {
+        uint32_t n;
+        bool has_n, affine;
+    };
+    std::vector<std::vector<HapInfo>> info(nr);
+    auto par = [&](auto fn) {
+        std::atomic<size_t> next(0);
+        auto work = [&]() {
+            for (size_t j; (j = next.fetch_add(1)) < nr;) fn(j);
         };
-        B.inner.push_back(rel(r.first));
-        B.inner.push_back(rel(r.second));
+        std::vector<std::thread> ts;
+        for (uint32_t t = 1; t < threads && t < nr; t++) ts.emplace_back(work);
+        work();
+        for (auto &t : ts) t.join();
+    };
+    par([&](size_t j) {
+        const RegionBuilt &rb = built[j];
+        info[j].resize(rb.dist.size());
+        for (size_t i = 0; i < rb.dist.size(); i++) {
+            const Distinct &d = rb.dist[i];
+            HapInfo &h = info[j][i];
+            h.n = (uint32_t)d.nuc.size();
+            h.has_n = std::find(d.nuc.begin(), d.nuc.end(), (uint8_t)4) != d.nuc.end();
+            h.affine = true;
+            for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
+        }
+    });
+    // serial layout: region / haplotype / word / mask / position offsets
+    struct Off {
+        size_t hap, inner;
+        uint64_t word, nmask, pos, count;
+    };
+    std::vector<Off> off(nr);
+    Off cur{B.haps.size(), B.inner.size(), B.words.size(), B.nmask.size(), B.posrel.size(), B.n_counts};
+    for (size_t j = 0; j < nr; j++) {
+        off[j] = cur;
+        const uint32_t n_inner = (uint32_t)built[j].R.ranges.size();
+        cur.hap += built[j].dist.size();
+        cur.inner += 2 * n_inner;
+        for (const HapInfo &h : info[j]) {
+            cur.word += (h.n + 15) / 16 + 3;
+            if (h.has_n) cur.nmask += (h.n + 31) / 32 + 2;
+            if (!h.affine) cur.pos += h.n;
+            cur.count += (uint64_t)B.n_slots * n_inner;
+        }
     }
-    B.regions.push_back(dr);
-    for (uint32_t i = 0; i < dist.size(); i++) {
-        const Distinct &d = dist[i];
-        const uint32_t n = (uint32_t)d.nuc.size();
-        DevHap hm{};
-        hm.word_off = (uint32_t)B.words.size();
-        hm.len = n;
-        hm.region = region_index;
-        size_t nw = (n + 15) / 16 + 3;
-        B.words.resize(B.words.size() + nw, 0u);
-        bool has_n = false, affine = true;
-        for (uint32_t p = 0; p < n; p++) {
-            uint8_t c = d.nuc[p];
-            if (c == 4) { has_n = true; c = 0; }  // N packs as A; the kernel subtracts w[j][A]
-            B.words[hm.word_off + p / 16] |= (uint32_t)c << (2 * (p % 16));
-            if (d.pos[p] != R.es + p) affine = false;
+    const uint32_t region0 = (uint32_t)B.rh.size();
+    B.haps.resize(cur.hap);
+    B.hap_carriers.resize(cur.hap);
+    B.inner.resize(cur.inner);
+    B.words.resize(cur.word, 0u);
+    B.nmask.resize(cur.nmask, 0u);
+    B.posrel.resize(cur.pos);
+    B.regions.resize(region0 + nr);
+    B.n_counts = cur.count;
+    std::vector<uint64_t> win(nr, 0), eff(nr, 0), cells(nr, 0);
+    par([&](size_t j) {
+        RegionBuilt &rb = built[j];
+        RegionH &R = rb.R;
+        const Off &o = off[j];
+        R.hap_begin = (uint32_t)o.hap;
+        R.hap_count = (uint32_t)rb.dist.size();
+        DevRegion dr{};
+        dr.inner_off = (uint32_t)(o.inner / 2);
+        dr.n_inner = (uint32_t)R.ranges.size();
+        dr.hap_begin = R.hap_begin;
+        dr.hap_count = R.hap_count;
+        R.key_off = (uint64_t)dr.inner_off * B.n_slots;
+        size_t ii = o.inner;
+        for (auto &r : R.ranges) {
+            // positions relative to ext_start, clamped: only containment of small
+            // non-negative positions is ever tested, which clamping preserves.
+            auto rel = [&](uint64_t x) -> int32_t {
+                if (x < R.es) { uint64_t d = R.es - x; return d > (1u << 30) ? -(1 << 30) : -(int32_t)d; }
+                uint64_t d = x - R.es;
+                return d > (1u << 30) ? (1 << 30) : (int32_t)d;
+            };
+            B.inner[ii++] = rel(r.first);
+            B.inner[ii++] = rel(r.second);
         }
-        if (has_n) {
-            hm.flags |= HAP_HAS_N;
-            hm.nmask_off = (uint32_t)B.nmask.size();
-            B.nmask.resize(B.nmask.size() + (n + 31) / 32 + 2, 0u);
-            for (uint32_t p = 0; p < n; p++)
-                if (d.nuc[p] == 4) B.nmask[hm.nmask_off + p / 32] |= 1u << (p % 32);
-        }
-        if (!affine) {
-            hm.flags |= HAP_HAS_POS;
-            hm.pos_off = (uint32_t)B.posrel.size();
-            for (uint32_t p = 0; p < n; p++) B.posrel.push_back((int32_t)(d.pos[p] - R.es));
-        }
-        hm.count_off = B.n_counts;
-        B.n_counts += (uint64_t)B.n_slots * dr.n_inner;
-        B.haps.push_back(hm);
-        B.hap_carriers.push_back(carriers[i]);
-        uint64_t w = 0;
-        for (const auto &lc : B.pwm_len_hist)
-            if (n >= lc.first) {
-                w += (uint64_t)(n - lc.first + 1) * lc.second;
-                B.cell_ops += (uint64_t)(n - lc.first + 1) * lc.first * lc.second;
+        B.regions[region0 + j] = dr;
+        uint64_t word = o.word, nmask = o.nmask, pos = o.pos, count = o.count;
+        for (uint32_t i = 0; i < rb.dist.size(); i++) {
+            const Distinct &d = rb.dist[i];
+            const HapInfo &h = info[j][i];
+            const uint32_t n = h.n;
+            DevHap hm{};
+            hm.word_off = (uint32_t)word;
+            hm.len = n;
+            hm.region = region0 + (uint32_t)j;
+            uint32_t *w = B.words.data() + word;
+            for (uint32_t p = 0; p < n; p++) {
+                const uint32_t c = d.nuc[p] == 4 ? 0u : d.nuc[p];  // N packs as A (masked by the N bits)
+                w[p / 16] |= c << (2 * (p % 16));
             }
-        B.windows += w;
-        B.eff_windows += w * carriers[i];
+            word += (n + 15) / 16 + 3;
+            if (h.has_n) {
+                hm.flags |= HAP_HAS_N;
+                hm.nmask_off = (uint32_t)nmask;
+                uint32_t *m = B.nmask.data() + nmask;
+                for (uint32_t p = 0; p < n; p++)
+                    if (d.nuc[p] == 4) m[p / 32] |= 1u << (p % 32);
+                nmask += (n + 31) / 32 + 2;
+            }
+            if (!h.affine) {
+                hm.flags |= HAP_HAS_POS;
+                hm.pos_off = (uint32_t)pos;
+                for (uint32_t p = 0; p < n; p++) B.posrel[pos + p] = (int32_t)(d.pos[p] - R.es);
+                pos += n;
+            }
+            hm.count_off = count;
+            count += (uint64_t)B.n_slots * dr.n_inner;
+            B.haps[o.hap + i] = hm;
+            B.hap_carriers[o.hap + i] = rb.carriers[i];
+            uint64_t wn = 0;
+            for (const auto &lc : B.pwm_len_hist)
+                if (n >= lc.first) {
+                    wn += (uint64_t)(n - lc.first + 1) * lc.second;
+                    cells[j] += (uint64_t)(n - lc.first + 1) * lc.first * lc.second;
+                }
+            win[j] += wn;
+            eff[j] += wn * rb.carriers[i];
+        }
+    });
+    for (size_t j = 0; j < nr; j++) {
+        B.windows += win[j];
+        B.eff_windows += eff[j];
+        B.cell_ops += cells[j];
+        B.rh.push_back(std::move(built[j].R));
     }
-    B.rh.push_back(std::move(R));
+}
+
+void commit_region(Batch &B, RegionBuilt &&built) {
+    std::vector<RegionBuilt> one(1);
+    one[0] = std::move(built);
+    commit_regions(B, one, 1);
 }
 
 }  // namespace tfbs
@@ -530,10 +605,9 @@ int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads) {
     work();
     for (auto &t : ts) t.join();
     B.counts_valid = B.reduced = false;
-    for (size_t j = 0; j < n; j++) {
+    for (size_t j = 0; j < n; j++)
         if (rcs[j]) return rcs[j];
-        commit_region(B, std::move(built[j]));
-    }
+    commit_regions(B, built, threads);
     return TFBS_OK;
 }
 }  // namespace tfbs

@@ -37,6 +37,18 @@ struct RegionH {
     std::vector<uint32_t> nonref_id, nonref_local;
 };
 
+// Page-locked host bytes (hipHostMalloc): device downloads land at full PCIe rate.
+struct PinnedBytes {
+    uint8_t *p = nullptr;
+    size_t cap = 0;
+    int reserve(size_t n);  // keeps nothing; TFBS_E_HIP on failure
+    const uint8_t *data() const { return p; }
+    ~PinnedBytes();
+    PinnedBytes() = default;
+    PinnedBytes(const PinnedBytes &) = delete;
+    PinnedBytes &operator=(const PinnedBytes &) = delete;
+};
+
 struct Batch {
     const Patterns *pats = nullptr;
     uint32_t n_samples = 0;
@@ -77,7 +89,8 @@ struct Batch {
     std::vector<uint32_t> enc_idx;
     std::vector<EncHdr> enc_hdr;
     std::vector<uint32_t> enc_vals, enc_hist;  // (kEncMaxVals + 1) per encoded key
-    std::vector<uint8_t> enc_codes;            // n_samples per encoded key
+    PinnedBytes enc_codes;                     // packed codes of every encoded key, back to back
+    std::vector<uint64_t> enc_code_off;        // per encoded key, + the end
 
     std::vector<RegionH> rh;
     uint64_t windows = 0, eff_windows = 0, cell_ops = 0;
@@ -119,6 +132,7 @@ struct RegionBuilt {
 
 int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);
 void commit_region(Batch &B, RegionBuilt &&built);
+void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads);
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads);
 int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
                    const int32_t *gt, Record &r);

@@ -96,7 +96,8 @@ struct tfbs_ctx {
     DevBuf<uint8_t> key_flags;
     DevBuf<DevVarKey> var_keys, enc_keys;
     // per-sample encoding (tfbs_batch_encode)
-    DevBuf<uint8_t> enc_memb, enc_codes;
+    DevBuf<uint8_t> enc_memb, enc_codes, enc_packed;
+    DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
     DevBuf<uint32_t> enc_vals, enc_hist;
     const tfbs_batch *resident = nullptr;
@@ -104,6 +105,26 @@ struct tfbs_ctx {
     int last_launches = 0;
     bool timing_pending = false;
 };
+
+namespace tfbs {
+int PinnedBytes::reserve(size_t n) {
+    if (n <= cap) return TFBS_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const hipError_t e = hipHostMalloc((void **)&p, std::max<size_t>(n, 1 << 20), hipHostMallocDefault);
+    if (e != hipSuccess) {
+        p = nullptr;
+        return tfbs::fail(TFBS_E_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    }
+    cap = std::max<size_t>(n, 1 << 20);
+    return TFBS_OK;
+}
+PinnedBytes::~PinnedBytes() {
+    if (p) (void)hipHostFree(p);
+}
+
+}  // namespace tfbs
 
 static int env_int(const char *name, int dflt) {
     const char *v = getenv(name);
@@ -204,7 +225,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_memb.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
-    ctx->enc_vals.release(); ctx->enc_hist.release();
+    ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
@@ -439,7 +460,7 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
     B.enc_hdr.clear();
     B.enc_vals.clear();
     B.enc_hist.clear();
-    B.enc_codes.clear();
+    B.enc_code_off.assign(1, 0);
     const uint32_t N = B.n_samples, H = 2 * N;
     if (N == 0 || r0 == r1) {
         B.enc_r0 = (uint32_t)r0;
@@ -490,7 +511,6 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
     B.enc_hdr.resize(nk);
     B.enc_vals.resize(nk * (kEncMaxVals + 1));
     B.enc_hist.resize(nk * (kEncMaxVals + 1));
-    B.enc_codes.resize(nk * (size_t)N);
     if (nk) {
         HIP_TRY(hipMemcpyAsync(B.enc_hdr.data(), ctx->enc_hdr.p, nk * sizeof(EncHdr), hipMemcpyDeviceToHost,
                                ctx->stream));
@@ -498,8 +518,23 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
                                ctx->stream));
         HIP_TRY(hipMemcpyAsync(B.enc_hist.data(), ctx->enc_hist.p, B.enc_hist.size() * 4, hipMemcpyDeviceToHost,
                                ctx->stream));
-        HIP_TRY(hipMemcpyAsync(B.enc_codes.data(), ctx->enc_codes.p, B.enc_codes.size(), hipMemcpyDeviceToHost,
-                               ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        // the packed codes back to back (a key's width is known only now), one download
+        B.enc_code_off.resize(nk + 1);
+        for (size_t k = 0; k < nk; k++) {
+            const EncHdr &h = B.enc_hdr[k];
+            const uint64_t bytes = h.status ? 0 : ((uint64_t)N * h.width + 7) / 8;
+            B.enc_code_off[k + 1] = B.enc_code_off[k] + bytes;
+        }
+        const uint64_t total = B.enc_code_off[nk];
+        if ((rc = ctx->enc_off.put(B.enc_code_off, ctx->stream)) ||
+            (rc = ctx->enc_packed.ensure(std::max<uint64_t>(total, 1))) || (rc = B.enc_codes.reserve(total)))
+            return rc;
+        if ((rc = launch_code_compact(ctx->enc_codes.p, (uint32_t)nk, N, ctx->enc_off.p, ctx->enc_packed.p,
+                                      ctx->stream)))
+            return rc;
+        if (total)
+            HIP_TRY(hipMemcpyAsync(B.enc_codes.p, ctx->enc_packed.p, total, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.enc_r0 = (uint32_t)r0;

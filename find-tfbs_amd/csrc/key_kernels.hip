@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__r
         hi = max(hi, s_red[kEncBlock / 64 + w]);
     }
     if (hi - lo >= kEncMaxRange) {
-        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, 0, 1};
+        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, 0, 1, 0};
         return;
     }
     // pass 2: which values occur
@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__r
     __syncthreads();
     const uint32_t nv = s_nv;
     if (nv > kEncMaxVals) {
-        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 1};
+        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 1, 0};
         return;
     }
     for (uint32_t w = threadIdx.x; w < nw; w += kEncBlock) {  // the sorted value table
@@ -163,17 +163,34 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__r
             vals[(size_t)k * (kEncMaxVals + 1) + r++] = lo + 32 * w + t;
         }
     }
-    // pass 3: codes and per-value sample counts
+    // pass 3: codes (packed: each thread writes whole bytes) and per-value sample counts
+    const uint32_t width = nv <= 4 ? 2 : (nv <= 16 ? 4 : 8), per = 8 / width;
     uint8_t *out = codes + (size_t)k * n_samples;
-    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
-        const uint32_t d = total(s) - lo, w = d >> 5;
-        const uint32_t c = s_rank[w] + __popc(s_bits[w] & ((1u << (d & 31)) - 1u));
-        out[s] = (uint8_t)c;
-        atomicAdd(&s_hist[c], 1u);
+    const uint32_t nbytes = (n_samples + per - 1) / per;
+    for (uint32_t byte = threadIdx.x; byte < nbytes; byte += kEncBlock) {
+        uint32_t packed = 0;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t s = byte * per + q;
+            if (s >= n_samples) break;
+            const uint32_t d = total(s) - lo, w = d >> 5;
+            const uint32_t c = s_rank[w] + __popc(s_bits[w] & ((1u << (d & 31)) - 1u));
+            packed |= c << (q * width);
+            atomicAdd(&s_hist[c], 1u);
+        }
+        out[byte] = (uint8_t)packed;
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nv; i += kEncBlock) hist[(size_t)k * (kEncMaxVals + 1) + i] = s_hist[i];
-    if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 0};
+    if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 0, width};
+}
+
+// Copies each key's packed codes (at k * n_samples) to off[k] of a contiguous buffer.
+__global__ __launch_bounds__(256) void code_compact_kernel(const uint8_t *__restrict__ codes, uint32_t n_samples,
+                                                           const uint64_t *__restrict__ off, uint8_t *__restrict__ dst) {
+    const uint32_t k = blockIdx.x;
+    const uint64_t o = off[k], n = off[k + 1] - o;
+    const uint8_t *src = codes + (size_t)k * n_samples;
+    for (uint64_t i = threadIdx.x; i < n; i += 256) dst[o + i] = src[i];
 }
 
 }  // namespace
@@ -187,6 +204,15 @@ int launch_key_encode(const DevHap *haps, const DevRegion *regions, const uint32
                        keys, memb, region0, n_samples, hdr, vals, hist, codes);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_encode_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_samples, const uint64_t *off, uint8_t *dst,
+                        hipStream_t stream) {
+    if (n_keys == 0) return TFBS_OK;
+    hipLaunchKernelGGL(code_compact_kernel, dim3(n_keys), dim3(256), 0, stream, codes, n_samples, off, dst);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("code_compact_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 

@@ -20,6 +20,8 @@ int launch_key_encode(const DevHap *haps, const DevRegion *regions, const uint32
                       const DevVarKey *keys, uint32_t n_keys, const uint8_t *memb, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream);
+int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_samples, const uint64_t *off, uint8_t *dst,
+                        hipStream_t stream);
 int launch_key_gather(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
                       const DevVarKey *keys, uint32_t n_keys, uint32_t *out, hipStream_t stream);
 

@@ -369,10 +369,9 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
         work();
         for (auto &t : ts) t.join();
         const double t_commit = now();
-        for (uint64_t j = 0; j < n; j++) {
+        for (uint64_t j = 0; j < n; j++)
             if (rcs[j]) return rcs[j];
-            tfbs::commit_region(B, std::move(built[j]));
-        }
+        tfbs::commit_regions(B, built, T);
         B.prep_s[2] += now() - t_commit;
     }
     B.prep_s[3] += now() - t_fill;

@@ -140,10 +140,12 @@ struct DevRegion {
 // v[s] = C[hap(2s)] + C[hap(2s+1)] over the samples (counts before the inner
 // range's multiplicity), its min / max, the sorted distinct values (COUNTS=,
 // main.rs:466-470) with their sample counts, and one u8 code per sample = the
-// rank of v[s] among them.  status != 0: too many distinct values or too wide a
+// rank of v[s] among them, packed at 2, 4 or 8 bits.  status != 0: too many
+// distinct values or too wide a
 // range for the encoding -- the rows take the host path for that key.
 struct EncHdr {
     uint32_t lo, hi, n_vals, status;
+    uint32_t width;  // bits per code (2, 4 or 8): codes packed LSB first, n_samples * width / 8 bytes
 };
 constexpr uint32_t kEncMaxVals = 255;       // u8 codes
 constexpr uint32_t kEncMaxRange = 1u << 16;  // value bitmap of hi - lo + 1 bits in LDS
