@@ -546,10 +546,19 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                     v16f c0, c1;
                     float tc;
                     pair_scores<NK>(s_img, S, ti, lane, a0, a1, c0, c1, tc);
+#if TFBS_MFMA_PROBE == 20
+                    // round 1's failing placement, for the ISA lint (tools/isa_lint.py):
+                    // the second tile's test reads its MFMA results after the first tile's branch
+                    const uint64_t f0 = coarse_test(c0, tc);
+                    queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
+                    const uint64_t f1 = coarse_test(c1, tc);
+                    queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+#else
                     const uint64_t f0 = coarse_test(c0, tc), f1 = coarse_test(c1, tc);
                     if (__builtin_expect((f0 | f1) == 0, 1)) continue;
                     queue_tile(c0, tc, f0, ti, hh, i0, lane, wave, qn);
                     queue_tile(c1, tc, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
+#endif
                     if (qn > kMQueue - 256) {
                         drain_queue(A, words, tile0, h0, qn, wave);
                         qn = 0;
