@@ -82,39 +82,45 @@ struct DevTile {
 };
 
 // Matrix-core path (scan_mfma.hip).  Each strand's weights are bounded above
-// by C + s q per window (mfma.cpp): q FP6 (e2m3) digits, s a per-strand scale.
-// The coarse sum Q = one-hot(window bases, FP4) x q over 32 windows x 32
-// strands is one v_mfma_scale_f32_32x32x64_f8f6f4 per 16 columns; Q > thr
-// selects the candidate windows, which are rescored exactly from the strand's
-// weights.  K chunk (64) = 16 columns x 4 bases: k = 32 h + 4 t + c <->
-// column 16 kc + 8 h + t, base c.
-constexpr int kMStrands = 32;      // strands per MFMA tile (the N dimension)
+// by C + s q per window (mfma.cpp): q <= 0 FP6 (e2m3) digits, s a per-strand
+// scale, U = 8 Q an integer.  Two strands share one column of the
+// v_mfma_scale_f32_32x32x64_f8f6f4 GEMM: the first's digits in K block 0, the
+// second's in K block 1, whose A scale is 2^11, and the accumulator starts at
+// 2^23 + (1023 - T0) (1 + 2^11).  Every output is then an integer in
+// [2^23, 2^24) whose mantissa holds two 11-bit fields V = U + 1023 - T0, one
+// per strand; a window is a candidate (U > T0, T0 the super tile's common
+// threshold) iff its field's bit 10 is set, so one OR tree tests two strands
+// per element.  Candidates are rescored exactly from the strand's weights.
+// K chunk (64) = 2 strands x 8 columns x 4 bases: k = 32 h + 4 t + c <->
+// strand 2 n + h, column 8 kc + t, base c.
+constexpr int kMStrands = 64;      // strands per MFMA tile (32 columns of strand pairs)
 constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
-constexpr int kMChunkCols = 16;    // columns per K chunk of 64
-constexpr int kMMaxChunks = 2;     // L <= 32
+constexpr int kMChunkCols = 8;     // columns per strand per K chunk
+constexpr int kMMaxChunks = 4;     // L <= 32
 constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (6 bits in a candidate entry)
 constexpr int kMFragBytes = 1536;  // one B fragment: 64 lanes x 24 bytes (dwords 0-3 | dwords 4-5)
-// Per tile, in the LDS image: the 32 strands' bound thresholds (f32).  The
-// fields only the candidate rescoring reads live in global memory
-// (Plan::m_meta, kGMetaInts per tile): min_score, offset of the exact weights
-// (4 per column), len, slot, pattern index.
-constexpr int kMMetaBytes = 128;
-enum MGMeta { kGMin = 0, kGWoff = 32, kGLen = 64, kGSlot = 96, kGOrig = 128 };
-constexpr int kGMetaInts = 160;
+constexpr int kMFieldBits = 11;    // bits per strand field of an output
+constexpr int kMFieldBias = 1023;  // V = U + kMFieldBias - T0: candidate iff V >= 1024
+// The fields only the candidate rescoring reads live in global memory
+// (Plan::m_meta, kGMetaInts per tile, indexed by the strand 2 n + h): min_score,
+// offset of the exact weights (4 per column), len, slot, pattern index.
+enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256 };
+constexpr int kGMetaInts = 320;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk), its
-// thresholds at meta_off + t * kMMetaBytes; its rescoring fields at
-// Plan::m_meta[(tile0 + t) * kGMetaInts].
+// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk); its
+// rescoring fields at Plan::m_meta[(tile0 + t) * kGMetaInts].  t0: the common
+// candidate threshold of its strands' bounds (U > t0), acc0 the accumulator's
+// start value 2^23 + (1023 - t0) (1 + 2^11) as f32 bits.
 struct DevMSuper {
     uint32_t tile_count;
     uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
     uint32_t img_off;   // byte offset of the LDS image in Plan::m_image
     uint32_t img_bytes;
-    uint32_t meta_off;  // byte offset of tile 0's metadata in the image
+    int32_t t0;
     uint32_t lmin;      // shortest strand
     uint32_t tile0;     // global index of tile 0 (Plan::m_meta)
-    uint32_t pad1;
+    uint32_t acc0;
 };
 
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };

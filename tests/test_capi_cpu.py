@@ -209,7 +209,8 @@ def test_mfma_bound_is_sound():
     """The FP6 bound the matrix-core scan filters with (mfma.cpp): for random patterns
     (weight spans 1 .. 2^20, mixed / all-negative / all-positive columns, thresholds at,
     below and above real scores) and random windows with N, 8 * score <= 8 c + scale * q8,
-    and every window with score > min_score (pattern.rs:151) is a candidate (q8 > t8)."""
+    every window with score > min_score (pattern.rs:151) is a candidate (q8 > t8), and the
+    window's 11-bit field q8 + 1023 - t8 neither borrows nor carries."""
     rnd = random.Random(21)
     checked = hits = 0
     for trial in range(160):
@@ -231,6 +232,8 @@ def test_mfma_bound_is_sound():
             assert b["eligible"] == 1
             sc = _window_score(w4, x)
             assert 8 * sc <= 8 * b["c"] + b["scale"] * b["q8"], (trial, x, sc, b)
+            # the packed two-strand fields (scan_mfma.hip): V = q8 + 1023 - t8 in [0, 2048)
+            assert -1024 < b["t8"] <= 0 and 0 <= b["q8"] + 1023 - b["t8"] < 2048, (trial, x, b)
             if sc > ms:
                 hits += 1
                 assert b["q8"] > b["t8"], (trial, x, sc, ms, b)

@@ -1,0 +1,111 @@
+// Probe: per-lane block scales and a non-zero C of
+// v_mfma_scale_f32_32x32x64_f8f6f4 (FP4 A x FP6 B), the two facts the packed
+// two-strand bound rests on (scan_mfma.hip):
+//  (1) lane l's scale_a applies to A row l & 31, K block l >> 5 (32 entries),
+//      lane l's scale_b to B column l & 31, K block l >> 5;
+//  (2) with C = 2^23 + small integers and integer products, every output in
+//      [2^23, 2^24) is exact (D = A x B + C bit for bit).
+// Build: hipcc --offload-arch=gfx950 -O2 f4f6_scale.hip -o f4f6_scale
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <random>
+#include <vector>
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+__global__ void k(const uint32_t *a, const uint32_t *b, const int *sa, const int *sb, const float *cin, float *out) {
+    const int l = threadIdx.x;
+    v8i va = {0, 0, 0, 0, 0, 0, 0, 0}, vb = va;
+    for (int i = 0; i < 4; i++) va[i] = a[l * 4 + i];
+    for (int i = 0; i < 6; i++) vb[i] = b[l * 6 + i];
+    v16f c;
+    for (int r = 0; r < 16; r++) c[r] = cin[l * 16 + r];
+    const v16f d = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(va, vb, c, 4, 2, 0, sa[l], 0, sb[l]);
+    for (int r = 0; r < 16; r++) out[l * 16 + r] = d[r];
+}
+
+static double fp4(uint32_t x) {
+    const double mag[8] = {0, 0.5, 1, 1.5, 2, 3, 4, 6};
+    return (x & 8 ? -1.0 : 1.0) * mag[x & 7];
+}
+static double fp6(uint32_t x) {  // e2m3, bias 1
+    const uint32_t e = (x >> 3) & 3, m = x & 7;
+    const double v = e == 0 ? m / 8.0 : (1 + m / 8.0) * std::ldexp(1.0, (int)e - 1);
+    return (x & 32 ? -1.0 : 1.0) * v;
+}
+static uint32_t bits(const uint32_t *w, int pos, int n) {
+    uint64_t x = w[pos / 32] | ((uint64_t)w[pos / 32 + 1] << 32);
+    return (uint32_t)(x >> (pos % 32)) & ((1u << n) - 1);
+}
+
+int main() {
+    std::mt19937 rng(7);
+    uint32_t *da, *db;
+    int *dsa, *dsb;
+    float *dc, *dout;
+    hipMalloc(&da, (64 * 4 + 1) * 4);
+    hipMalloc(&db, (64 * 6 + 1) * 4);
+    hipMalloc(&dsa, 64 * 4);
+    hipMalloc(&dsb, 64 * 4);
+    hipMalloc(&dc, 64 * 16 * 4);
+    hipMalloc(&dout, 64 * 16 * 4);
+    int fails = 0;
+    for (int trial = 0; trial < 4; trial++) {
+        std::vector<uint32_t> a(64 * 4 + 1, 0), b(64 * 6 + 1, 0);
+        std::vector<int> sa(64), sb(64);
+        std::vector<float> cin(64 * 16);
+        // A: one-hot style FP4 (0 or 1.0 = code 2), B: FP6 digits <= 0
+        for (int l = 0; l < 64; l++)
+            for (int e = 0; e < 32; e++) {
+                if (rng() % 4 == 0) a[l * 4 + e / 8] |= 2u << (4 * (e % 8));
+                const uint32_t code = (rng() % 3 == 0) ? 0 : (0x20 | (rng() % 32));
+                const int pos = 6 * e;
+                for (int q = 0; q < 6; q++)
+                    if ((code >> q) & 1) b[l * 6 + (pos + q) / 32] |= 1u << ((pos + q) % 32);
+            }
+        for (int l = 0; l < 64; l++) {
+            if (trial == 0) {
+                sa[l] = l < 32 ? 127 : 138;  // the packed layout: block 1 scaled by 2^11
+                sb[l] = 130;                 // digits x 8: integer units
+            } else {
+                sa[l] = 124 + rng() % 16;  // which lane's scale lands where
+                sb[l] = 125 + rng() % 8;
+            }
+        }
+        for (int l = 0; l < 64; l++)
+            for (int r = 0; r < 16; r++)
+                cin[l * 16 + r] = trial == 0 ? (float)(8388608 + (rng() % 2000) + 2048 * (rng() % 2000)) : 0.0f;
+        hipMemcpy(da, a.data(), a.size() * 4, hipMemcpyHostToDevice);
+        hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice);
+        hipMemcpy(dsa, sa.data(), 64 * 4, hipMemcpyHostToDevice);
+        hipMemcpy(dsb, sb.data(), 64 * 4, hipMemcpyHostToDevice);
+        hipMemcpy(dc, cin.data(), cin.size() * 4, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, da, db, dsa, dsb, dc, dout);
+        std::vector<float> out(64 * 16);
+        hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost);
+        int ok = 0;
+        for (int l = 0; l < 64; l++)
+            for (int r = 0; r < 16; r++) {
+                const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
+                double c = cin[l * 16 + r];
+                for (int kk = 0; kk < 64; kk++) {
+                    const int la = i + 32 * (kk >> 5), lb = j + 32 * (kk >> 5);  // hypothesis (1)
+                    const double av = fp4(bits(&a[la * 4], 4 * (kk & 31), 4)) * std::ldexp(1.0, sa[la] - 127);
+                    const double bv = fp6(bits(&b[lb * 6], 6 * (kk & 31), 6)) * std::ldexp(1.0, sb[lb] - 127);
+                    c += av * bv;
+                }
+                const double tol = trial == 0 ? 0.0 : 1e-5 * std::max(1.0, std::fabs(c));  // trial 0 must be exact
+                if (std::fabs((double)out[l * 16 + r] - c) <= tol) ok++;
+                else if (fails++ < 8)
+                    printf("trial %d lane %d r %d: got %.3f want %.3f\n", trial, l, r, out[l * 16 + r], c);
+            }
+        printf("trial %d (%s): %d/1024 outputs exact\n", trial, trial == 0 ? "packed scales" : "random scales", ok);
+    }
+    printf(fails ? "FAIL\n" : "PASS\n");
+    return fails ? 1 : 0;
+}
