@@ -80,12 +80,12 @@ struct tfbs_ctx {
     DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
     DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights, m_meta;
-    DevBuf<uint32_t> cands, cand_count;  // matrix-core candidate lists (scan.hpp)
-    uint32_t cand_cap = 0;               // per stripe
+    DevBuf<uint32_t> cands;              // matrix-core candidate lists (scan.hpp)
+    uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
-    uint32_t mfma_lds = 19 * 1024;  // LDS image budget of one MFMA super tile
-    uint32_t mfma_hpb = 32;         // haplotypes per MFMA workgroup
+    uint32_t mfma_lds = 40 * 1024;  // LDS image budget of one MFMA super tile
+    uint32_t mfma_hpb = 64;         // haplotypes per MFMA workgroup
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
     DevBuf<uint32_t> words, nmask, counts;
@@ -134,14 +134,6 @@ static int env_int(const char *name, int dflt) {
     return atoi(v);
 }
 
-// Candidate list capacity per stripe for haplotypes of `bases` bases in total:
-// about 1 window x strand pair in 4 000 (C3 bounds pass ~1.5e-4 of them), at
-// least 64 Ki entries; a full stripe falls back to rescoring inside the scan.
-static void size_candidates(tfbs_ctx *ctx, uint64_t bases) {
-    const uint64_t want = bases * std::max<uint32_t>(1, ctx->plan.n_mfma_strands) / 4000 / kCandStripes;
-    ctx->cand_cap = (uint32_t)std::min<uint64_t>(1u << 26, std::max<uint64_t>(1u << 16, want));
-}
-
 static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits, uint32_t hits_wpp) {
     const Plan &P = ctx->plan;
     if (n_haps == 0) return 0;
@@ -168,13 +160,12 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.mweights = ctx->m_weights.p;
         m.mmeta = ctx->m_meta.p;
         m.haps_per_block = ctx->mfma_hpb;
+        // one candidate region per scan workgroup (super tile x haplotype group)
+        const uint64_t n_regions = (uint64_t)P.m_supers.size() * ((n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb);
         int rc;
-        if ((rc = ctx->cand_count.ensure(kCandStripes)) || (rc = ctx->cands.ensure((size_t)ctx->cand_cap * 3 * kCandStripes)))
-            return rc;
+        if ((rc = ctx->cands.ensure(n_regions * ctx->cand_cap * 3))) return rc;
         m.cands = ctx->cands.p;
-        m.cand_count = ctx->cand_count.p;
         m.cand_cap = ctx->cand_cap;
-        HIP_TRY(hipMemsetAsync(ctx->cand_count.p, 0, kCandStripes * 4, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
@@ -192,9 +183,6 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
-        const int r = launch_rescore(m, ctx->stream);
-        if (r < 0) return r;
-        launches += r;
     }
     if (!P.fast_tiles.empty()) {
         ScanArgs f = a;
@@ -241,7 +229,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
-    ctx->cands.release(); ctx->cand_count.release();
+    ctx->cands.release();
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
@@ -274,8 +262,9 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 128));
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
-    ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 19))) * 1024u;
-    ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 32)));  // 8 bits in a candidate entry
+    ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 40))) * 1024u;
+    ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
+    ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -383,9 +372,6 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->resident = b;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
-    uint64_t bases = 0;
-    for (const DevHap &h : B.haps) bases += h.len;
-    size_candidates(ctx, bases);
     return TFBS_OK;
 }
 
@@ -604,7 +590,6 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
         return rc;
     ctx->resident = nullptr;
     ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->mfma_hpb);
-    size_candidates(ctx, n);
     const size_t nh = (size_t)P.pats.size() * wpp;
     if ((rc = ctx->hits.ensure(std::max<size_t>(nh, 1)))) return rc;
     if (nh) HIP_TRY(hipMemsetAsync(ctx->hits.p, 0, nh * 8, ctx->stream));

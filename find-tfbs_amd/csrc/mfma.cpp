@@ -218,7 +218,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
     while (ti < tiles.size()) {
         // a super tile: consecutive tiles of the same K depth within the LDS budget
         const uint32_t nk = tiles[ti].nk;
-        const uint32_t per = nk * kMFragBytes;
+        const uint32_t per = mfma_tile_bytes(nk);
         const uint32_t lds_bytes = std::max(per, opt.mfma_lds_by_nk[nk] ? opt.mfma_lds_by_nk[nk] : opt.mfma_lds_bytes);
         // the run of tiles with this depth, split into equal super tiles
         size_t run = ti;
@@ -254,7 +254,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         std::vector<uint8_t> img(S.img_bytes, 0);
         for (uint32_t k = 0; k < count; k++) {
             const TileSrc &t = tiles[ti + k];
-            const uint32_t b_off = k * nk * kMFragBytes;
+            const uint32_t b_off = k * per;
             S.lmin = std::min(S.lmin, t.lmin);
             const size_t g0 = plan->m_meta.size();
             plan->m_meta.resize(g0 + kGMetaInts, 0);
@@ -280,14 +280,15 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
             // B fragments: lane l holds column n = l & 31 (strands 2n, 2n+1) and
             // k = 32 h + 4 t + c, h = l >> 5, <-> strand 2 n + h, column
             // 8 kc + t, base c: element e = 4 t + c at bits 6 e of the lane's 192
-            // bits, dwords 0-3 at lane * 16, dwords 4-5 at 1024 + lane * 8
+            // bits, dwords 0-3 at kc * 1536 + lane * 16, dwords 4-5 at kc * 1536 +
+            // 1024 + lane * 8 (mfma_tile_bytes)
             for (uint32_t kc = 0; kc < nk; kc++)
                 for (int l = 0; l < 64; l++) {
                     const int sn = 2 * (l & 31) + (l >> 5);
                     const Split &sp = split[sn];
                     const uint32_t len = (size_t)sn < t.count ? P.pats[strands[t.first + sn].first].len : 0;
-                    uint8_t *lo = &img[b_off + kc * kMFragBytes + l * 16];
-                    uint8_t *hi = &img[b_off + kc * kMFragBytes + 1024 + l * 8];
+                    uint8_t *lo = &img[b_off + kc * 1536 + l * 16];
+                    uint8_t *hi = &img[b_off + kc * 1536 + 1024 + l * 8];
                     for (int tt = 0; tt < kMChunkCols; tt++) {
                         const uint32_t col = kc * kMChunkCols + tt;
                         for (int c = 0; c < 4; c++) {

@@ -36,15 +36,14 @@ struct ScanArgs {
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;
     uint32_t n_patterns_total;
-    // matrix-core candidates (scan_mfma.hip): kCandStripes lists of cand_cap
-    // (haplotype, strand, window) triples, appended by the scan, rescored by
-    // rescore_kernel; hap_base: this launch's first haplotype in the batch
+    // matrix-core candidates (scan_mfma.hip): one region of cand_cap (haplotype,
+    // strand, window) triples per scan workgroup (region region_base +
+    // blockIdx.x), filled through an LDS counter and rescored by the workgroup
+    // at its end
     uint32_t *cands;
-    uint32_t *cand_count;
     uint32_t cand_cap;
-    uint32_t hap_base;
+    uint32_t region_base;
 };
-constexpr uint32_t kCandStripes = 8;
 
 struct LaunchConfig {
     int minw = 2;               // __launch_bounds__ min waves per SIMD of the fast kernel
@@ -63,9 +62,6 @@ int fast_kernel_set_lds(const LaunchConfig &cfg);
 // supers: the host copy of a.msupers (sorted by depth).
 int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
                 const hipStream_t *streams, uint32_t n_streams);
-// Exact rescoring of the candidates the launches above appended (a: the batch's
-// base pointers, as for launch_mfma); enqueued on `stream` after them.
-int launch_rescore(const ScanArgs &a, hipStream_t stream);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach
 // the waves per SIMD its registers allow.

@@ -19,15 +19,16 @@
 //    2n + 1 in bits 11-21, each in [0, 2048) (mfma.cpp clips the digits so);
 //    U > T0 iff the field's top bit (10 or 21) is set.  One OR tree over a
 //    lane's 16 outputs (v_or3 + v_bitop3) tests 32 (window, strand) pairs.
-//  * A workgroup (4 waves) stages one super tile (tiles of 64 strands of equal
+//  * A workgroup (8 waves) stages one super tile (tiles of 64 strands of equal
 //    K depth), the one-hot table and the packed words of its haplotypes in
 //    LDS.  Every B fragment is one conflict-free ds_read_b128 + ds_read_b64 per
 //    lane and feeds two window tiles.
 //  * C layout: lane l holds column l & 31 (strands 2 (l & 31), + 1) and windows
 //    (r & 3) + 8 (r >> 2) + 4 (l >> 5), r < 16.  A firing lane (rare) appends
 //    the fields' top bits of its 16 outputs (16 bytes) to the wave's LDS queue;
-//    drain_queue decodes them into (haplotype, strand, window) candidates in a
-//    global list, and rescore_kernel rescores those exactly (pattern.rs:125-151),
+//    drain_queue decodes them into (haplotype, strand, window) candidates in the
+//    workgroup's region of a global (L2-resident) list, and at its end the
+//    workgroup rescores those exactly, one per thread (pattern.rs:125-151),
 //    applies the inner-range overlap test (range.rs:18-21 as main.rs:503 uses
 //    it) and adds to the count of the strand's pattern_id slot atomically
 //    (counts are zeroed before the scan).
@@ -56,9 +57,9 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-constexpr int kMBlock = 256;          // 4 waves
+constexpr int kMBlock = 512;          // 8 waves (two per SIMD) share one super tile image
 constexpr int kMOnehotBytes = 2048;   // LDS: one-hot table (4-mer -> 4 x 16 bits of FP4), image, words
-constexpr uint32_t kMStagedMax = 40 * 1024;  // LDS per workgroup at 4 workgroups per CU (160 KiB)
+constexpr uint32_t kMStagedMax = 80 * 1024;  // LDS per workgroup at 2 workgroups per CU (160 KiB)
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
 constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
@@ -124,19 +125,25 @@ __device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint
     }
 }
 
-// B fragment of one strand tile and K chunk: the lane's 32 FP6 digits (192
-// bits) as dwords 0-3 (at lane * 16) and 4-5 (at 1024 + lane * 8).
+// B fragments of one strand tile: chunk kc's 32 FP6 digits per lane (192
+// bits) as dwords 0-3 (at kc * 1536 + lane * 16) and dwords 4-5 (at kc * 1536 +
+// 1024 + lane * 8), mfma_tile_bytes per tile: conflict-free reads.
 struct BFrag {
     v4i b;
     int2 c;
 };
 
-__device__ __forceinline__ BFrag load_frag(const char *s_img, uint32_t ti, uint32_t nk, uint32_t kc, uint32_t lane) {
-    const char *p = s_img + (ti * nk + kc) * kMFragBytes;
-    BFrag f;
-    f.b = *reinterpret_cast<const v4i *>(p + lane * 16);
-    f.c = *reinterpret_cast<const int2 *>(p + 1024 + lane * 8);
-    return f;
+template <int NK>
+__device__ __forceinline__ void load_frags(const char *s_img, uint32_t ti, uint32_t lane, BFrag (&f)[NK]) {
+    const char *p = s_img + ti * mfma_tile_bytes(NK);
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) {
+        // no ds_read2 merging across chunks: merged pairs need v_mov copies
+        // into the MFMA operand tuples
+        if (kc) asm volatile("" ::: "memory");
+        f[kc].b = *reinterpret_cast<const v4i *>(p + kc * 1536 + lane * 16);
+        f[kc].c = *reinterpret_cast<const int2 *>(p + kc * 1536 + 1024 + lane * 8);
+    }
 }
 
 // One chunk: FP4 one-hot (A) x FP6 digits (B), f32 accumulate; sa: the lane's
@@ -173,6 +180,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 constexpr uint32_t kMQueue = 96;  // entries per wave (>= one tile's 64)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue][2];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
+__shared__ uint32_t s_cn;  // candidates the workgroup appended
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 #if TFBS_MFMA_PROBE == 4
@@ -240,17 +248,17 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
 
 // Drains the wave's first n queue entries, one entry per lane per round: the
 // candidate bits of both strands of the entry's column are decoded and each
-// candidate (haplotype, strand, window) is appended to the launch's stripe of
-// the candidate list for rescore_kernel, one candidate per lane per pass.  A
-// full stripe (pathological thresholds) rescores here instead.
+// candidate (haplotype, strand, window) is appended to the workgroup's region
+// of the candidate list (slots from an LDS counter), one candidate per lane per
+// pass.  A full region (pathological thresholds)
+// rescores here instead.
 // h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
 __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                             uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane) {
 #if TFBS_MFMA_PROBE == 12
     return;  // timing only: queued candidates are dropped
 #endif
-    const uint32_t stripe = blockIdx.x % kCandStripes;
-    uint32_t *list = A.cands + (size_t)stripe * A.cand_cap * 3;
+    uint32_t *list = A.cands + (size_t)(A.region_base + blockIdx.x) * A.cand_cap * 3;
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
         const uint32_t e = e0 + lane;
         uint32_t m0 = 0, m1 = 0, src = 0, ti = 0, hl = 0, i0 = 0;
@@ -285,7 +293,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
             }
             const uint32_t first = (uint32_t)__builtin_ctzll(act);
             uint32_t base = 0;
-            if (lane == first) base = atomicAdd(A.cand_count + stripe, (uint32_t)__popcll(act));
+            if (lane == first) base = atomicAdd(&s_cn, (uint32_t)__popcll(act));
             base = __builtin_amdgcn_readlane(base, first);
             if (has) {
                 const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
@@ -293,7 +301,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
                 const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * (src >> 5);
                 const uint32_t g = (tile0 + ti) * kMStrands + sn;
                 if (slot < A.cand_cap) {
-                    list[3 * (size_t)slot] = A.hap_base + h0 + hl;
+                    list[3 * (size_t)slot] = h0 + hl;
                     list[3 * (size_t)slot + 1] = g;
                     list[3 * (size_t)slot + 2] = i;
                 } else {
@@ -349,6 +357,32 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t
     qn += (uint32_t)__popcll(fired);
 }
 
+// The accumulators of one round: strand tile ti x the window tiles a0, a1 (one
+// B fragment read feeds both MFMAs), starting from the field biases cb.
+template <int NK>
+__device__ __forceinline__ void round_scores(const char *s_img, uint32_t ti, uint32_t lane, const v4i (&a0)[NK],
+                                             const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
+    BFrag f[NK];
+    load_frags<NK>(s_img, ti, lane, f);
+    c0 = cb;
+    c1 = cb;
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) {
+        c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+        c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+    }
+}
+
+template <int NK>
+__device__ __forceinline__ void tile_scores(const char *s_img, uint32_t ti, uint32_t lane, const v4i (&a0)[NK],
+                                            const v16f &cb, int sa, v16f &c0) {
+    BFrag f[NK];
+    load_frags<NK>(s_img, ti, lane, f);
+    c0 = cb;
+#pragma unroll
+    for (int kc = 0; kc < NK; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+}
+
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
 // of this workgroup's haplotypes, biased by their first word, or global memory).
 template <int NK>
@@ -386,29 +420,22 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             // a tile whose entries do not fit drains the queue and its round is
             // scored again (skip0: the first tile's entries are already queued)
             if (two) {
-                bool skip0 = false;
-                for (uint32_t ti = 0; ti < nt;) {
-                    v16f c0 = cb, c1 = cb;
-#pragma unroll
-                    for (int kc = 0; kc < NK; kc++) {
-                        // no ds_read2 merging across chunks: the merged pair needs
-                        // v_mov copies into the MFMA operand tuples
-                        if (kc) asm volatile("" ::: "memory");
-                        const BFrag f = load_frag(s_img, ti, NK, kc, lane);
-                        c0 = mfma_chunk(a0[kc], f, c0, sa);
-                        c1 = mfma_chunk(a1[kc], f, c1, sa);
-                    }
-                    const uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
+                for (uint32_t ti = 0; ti < nt; ti++) {
+                    v16f c0, c1;
+                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                    uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
                     const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-                    if (__builtin_expect((f0 | f1) == 0, 1)) {  // one branch for both tests
-                        ti++;
-                        continue;
-                    }
-                    if (f0 && !skip0) {
+                    if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
+                    // cold: queue the firing tiles; a tile whose entries do not fit
+                    // drains the queue first and its round is scored again (no
+                    // accumulator is live across a drain)
+                    if (f0) {
                         if (qn + (uint32_t)__popcll(f0) > kMQueue) {
                             drain_queue(A, words, tile0, h0, qn, wave, lane);
                             qn = 0;
-                            continue;
+                            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                            x0 = coarse_test(c0);
+                            x1 = coarse_test(c1);
                         }
                         queue_tile(c0, x0, f0, ti, hh, i0, lane, wave, qn);
                     }
@@ -416,30 +443,26 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                         if (qn + (uint32_t)__popcll(f1) > kMQueue) {
                             drain_queue(A, words, tile0, h0, qn, wave, lane);
                             qn = 0;
-                            skip0 = true;
-                            continue;
+                            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                            x1 = coarse_test(c1);
                         }
                         queue_tile(c1, x1, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
                     }
-                    skip0 = false;
-                    ti++;
                 }
             } else {
-                for (uint32_t ti = 0; ti < nt;) {
-                    v16f c0 = cb;
-#pragma unroll
-                    for (int kc = 0; kc < NK; kc++) c0 = mfma_chunk(a0[kc], load_frag(s_img, ti, NK, kc, lane), c0, sa);
-                    const uint32_t x0 = coarse_test(c0);
+                for (uint32_t ti = 0; ti < nt; ti++) {
+                    v16f c0;
+                    tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+                    uint32_t x0 = coarse_test(c0);
                     const uint64_t f0 = __ballot(x0 != 0);
-                    if (f0) {
-                        if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                            drain_queue(A, words, tile0, h0, qn, wave, lane);
-                            qn = 0;
-                            continue;
-                        }
-                        queue_tile(c0, x0, f0, ti, hh, i0, lane, wave, qn);
+                    if (__builtin_expect(f0 == 0, 1)) continue;
+                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                        drain_queue(A, words, tile0, h0, qn, wave, lane);
+                        qn = 0;
+                        tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+                        x0 = coarse_test(c0);
                     }
-                    ti++;
+                    queue_tile(c0, x0, f0, ti, hh, i0, lane, wave, qn);
                 }
             }
         }
@@ -447,7 +470,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     drain_queue(A, words, tile0, h0, qn, wave, lane);  // the wave's last entries
 }
 
-// Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD.
+// Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD (two workgroups per CU).
 // LDS: one-hot table | super tile image | (STAGED) the packed words of the
 // workgroup's haplotypes, copied once so that every window read is an LDS read.
 template <bool STAGED, int NK>
@@ -463,6 +486,7 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
         // one-hot table: 4-mer code -> 64 bits, column t (16 bits) holds FP4
         // 1.0 (0x2) in the nibble of its base
         uint2 *tab = reinterpret_cast<uint2 *>(smem);
+        if (threadIdx.x == 0) s_cn = 0;
         for (uint32_t k = threadIdx.x; k < 256; k += kMBlock) {
             uint32_t h[4];
             for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
@@ -484,21 +508,14 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     // the wave index is uniform: keep every haplotype-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
-}
-
-// The candidates of every stripe, one per thread (grid-stride): exact score of
-// the window from the strand's integer weights and the counting, as the
-// reference's matches + count_matches_by_sample (pattern.rs:141-171,
-// main.rs:500-534) for the windows the bound let through.
-__global__ __launch_bounds__(256) void rescore_kernel(ScanArgs A) {
-    const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t s = 0; s < kCandStripes; s++) {
-        const uint32_t n = min(A.cand_count[s], A.cand_cap);
-        const uint32_t *list = A.cands + (size_t)s * A.cand_cap * 3;
-        for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-            const uint32_t hap = list[3 * (size_t)k], g = list[3 * (size_t)k + 1], i = list[3 * (size_t)k + 2];
-            score_candidate(A, A.words, A.haps[hap], hap, g, i);
-        }
+    // the workgroup's candidates, one per thread: they overlap the MFMA work of
+    // the other workgroups on the CU
+    __syncthreads();
+    const uint32_t n = min(s_cn, A.cand_cap);
+    const uint32_t *list = A.cands + (size_t)(A.region_base + blockIdx.x) * A.cand_cap * 3;
+    for (uint32_t k = threadIdx.x; k < n; k += kMBlock) {
+        const uint32_t hap = list[3 * (size_t)k], g = list[3 * (size_t)k + 1], i = list[3 * (size_t)k + 2];
+        score_candidate(A, words, A.haps[hap], hap, g, i);
     }
 }
 
@@ -517,13 +534,6 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {
 
 }  // namespace
 
-int launch_rescore(const ScanArgs &a, hipStream_t stream) {
-    hipLaunchKernelGGL(rescore_kernel, dim3(4096), dim3(256), 0, stream, a);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("rescore_kernel launch: ") + hipGetErrorString(e));
-    return 1;
-}
-
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
     uint32_t mx = 0;
     for (uint32_t h0 = 0; h0 < n_haps; h0 += hpb) {
@@ -538,7 +548,8 @@ size_t mfma_lds_fixed() { return kMOnehotBytes; }
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
     const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + 256;  // table, staged words, queues
-    for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / waves[nk] - reserve;
+    // workgroups per CU = 4 SIMDs x waves per SIMD / waves per workgroup
+    for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / (4 * waves[nk] / (kMBlock / 64)) - reserve;
 }
 
 int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words,
@@ -546,7 +557,8 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     if (n_haps == 0 || n_supers == 0) return 0;
     const uint32_t hpb = a0.haps_per_block;
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta);  // candidate queues
+    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_cn);  // candidate queues
+    uint32_t region = 0;
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is
     // compiled for its depth's registers and LDS; the deepest (longest) first
@@ -567,7 +579,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
         // stage the group's words in LDS when they fit beside the image at 4 workgroups per CU
         const size_t base = kMOnehotBytes + img_bytes;
         const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
-        const bool staged = staged_bytes + static_lds <= std::max<size_t>(kMStagedMax, (160 * 1024) / kMfmaRegWaves[nk]);
+        const bool staged = staged_bytes + static_lds <= kMStagedMax;
         const size_t lds = staged ? staged_bytes : base;
         const MfmaKernel kern = mfma_variant(staged, nk);
         hipError_t e = hipSuccess;
@@ -584,7 +596,8 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.haps = a0.haps + h0;
             a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
             a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
-            a.hap_base = h0;
+            a.region_base = region;
+            region += ns * ng;
             a.mimg_max = (uint32_t)img_bytes;
             hipLaunchKernelGGL(kern, dim3(ns * ng), dim3(kMBlock), lds, stream, a);
             launches++;

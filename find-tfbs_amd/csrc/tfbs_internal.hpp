@@ -98,7 +98,9 @@ constexpr int kMWindows = 32;      // windows per MFMA tile (the M dimension)
 constexpr int kMChunkCols = 8;     // columns per strand per K chunk
 constexpr int kMMaxChunks = 4;     // L <= 32
 constexpr int kMSuperMaxTiles = 64;  // tiles per super tile (6 bits in a candidate entry)
-constexpr int kMFragBytes = 1536;  // one B fragment: 64 lanes x 24 bytes (dwords 0-3 | dwords 4-5)
+// one strand tile of nk chunks in LDS: per chunk 64 lanes x 16 bytes (B dwords
+// 0-3) and 64 lanes x 8 bytes (dwords 4-5)
+constexpr inline uint32_t mfma_tile_bytes(uint32_t nk) { return nk * 1536; }
 constexpr int kMFieldBits = 11;    // bits per strand field of an output
 constexpr int kMFieldBias = 1023;  // V = U + kMFieldBias - T0: candidate iff V >= 1024
 // The fields only the candidate rescoring reads live in global memory
@@ -108,7 +110,7 @@ enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256 };
 constexpr int kGMetaInts = 320;
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * nk * kMFragBytes (per chunk); its
+// depth nk; tile t's B fragments at t * mfma_tile_bytes(nk); its
 // rescoring fields at Plan::m_meta[(tile0 + t) * kGMetaInts].  t0: the common
 // candidate threshold of its strands' bounds (U > t0), acc0 the accumulator's
 // start value 2^23 + (1023 - t0) (1 + 2^11) as f32 bits.
