@@ -347,6 +347,16 @@ class RegionBatch:
         return lib().tfbs_batch_num_effective_windows(self.h)
 
     @property
+    def num_scan_windows(self):
+        """Windows the scan executes (reference-window reuse skips SNV-only haplotypes'
+        windows equal to the reference's)."""
+        return lib().tfbs_batch_num_scan_windows(self.h)
+
+    @property
+    def num_scan_cell_ops(self):
+        return lib().tfbs_batch_num_scan_cell_ops(self.h)
+
+    @property
     def input_bytes(self):
         return lib().tfbs_batch_input_bytes(self.h)
 

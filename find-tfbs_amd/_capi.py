@@ -93,6 +93,8 @@ SIGNATURES = [
     ("tfbs_batch_num_windows", C.c_uint64, [vp]),
     ("tfbs_batch_num_effective_windows", C.c_uint64, [vp]),
     ("tfbs_batch_num_cell_ops", C.c_uint64, [vp]),
+    ("tfbs_batch_num_scan_windows", C.c_uint64, [vp]),
+    ("tfbs_batch_num_scan_cell_ops", C.c_uint64, [vp]),
     ("tfbs_batch_input_bytes", C.c_uint64, [vp]),
     ("tfbs_batch_output_bytes", C.c_uint64, [vp]),
     ("tfbs_batch_upload", C.c_int, [vp, vp]),

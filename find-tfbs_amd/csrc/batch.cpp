@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <map>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <thread>
@@ -303,6 +304,20 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
         dist.push_back(std::move(d));
         carriers.push_back((uint32_t)(H - covered));
     }
+    // reference-window reuse needs the reference's windows: without a reference
+    // group, a helper copy is scanned after the distinct haplotypes (no carriers,
+    // no keys)
+    out.helper = false;
+    if (B.dedup && R.ref_local < 0 && !dist.empty()) {
+        Distinct d;
+        d.nuc = I.ref;
+        d.pos.resize(I.ref.size());
+        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.group = -2;
+        dist.push_back(std::move(d));
+        carriers.push_back(0);
+        out.helper = true;
+    }
     // the kernels index windows with 29 bits (scan_mfma.hip queue entries)
     for (const Distinct &d : dist)
         if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
@@ -329,7 +344,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     // per haplotype: length, has N, affine positions (parallel scan of the sequences)
     struct HapInfo {
         uint32_t n;
-        bool has_n, affine;
+        bool has_n, affine, dedup = false;
+        uint32_t dirty[4] = {0, 0, 0, 0};
     };
     std::vector<std::vector<HapInfo>> info(nr);
     auto par = [&](auto fn) {
@@ -352,6 +368,29 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             h.has_n = std::find(d.nuc.begin(), d.nuc.end(), (uint8_t)4) != d.nuc.end();
             h.affine = true;
             for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
+        }
+        // reference-window reuse: SNV-only haplotypes of the reference's length
+        // and N positions mark the window tiles whose windows (of up to 8 nk
+        // columns) hold a differing base
+        const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.dist.size() - 1 : -1);
+        if (!B.dedup || ref < 0) return;
+        const std::vector<uint8_t> &rn = rb.dist[ref].nuc;
+        for (size_t i = 0; i < rb.dist.size(); i++) {
+            HapInfo &h = info[j][i];
+            if ((int32_t)i == ref || !h.affine || h.n != rn.size() || (h.n + kMWindows - 1) / kMWindows > kDedupMaxTiles)
+                continue;
+            const std::vector<uint8_t> &dn = rb.dist[i].nuc;
+            bool ok = true;
+            for (uint32_t p = 0; p < h.n && ok; p++) ok = (dn[p] == 4) == (rn[p] == 4);
+            if (!ok) continue;
+            h.dedup = true;
+            for (uint32_t p = 0; p < h.n; p++) {
+                if (dn[p] == rn[p]) continue;
+                for (uint32_t d = 0; d < 4; d++) {  // windows p - 8 (d + 1) + 1 .. p
+                    const uint32_t w0 = p + 1 >= 8 * (d + 1) ? p + 1 - 8 * (d + 1) : 0;
+                    for (uint32_t t = w0 / kMWindows; t <= p / kMWindows; t++) h.dirty[d] |= 1u << t;
+                }
+            }
         }
     });
     // serial layout: region / haplotype / word / mask / position offsets
@@ -382,18 +421,20 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     B.posrel.resize(cur.pos);
     B.regions.resize(region0 + nr);
     B.n_counts = cur.count;
-    std::vector<uint64_t> win(nr, 0), eff(nr, 0), cells(nr, 0);
+    std::vector<uint64_t> win(nr, 0), eff(nr, 0), cells(nr, 0), swin(nr, 0), scells(nr, 0);
     par([&](size_t j) {
         RegionBuilt &rb = built[j];
         RegionH &R = rb.R;
         const Off &o = off[j];
         R.hap_begin = (uint32_t)o.hap;
-        R.hap_count = (uint32_t)rb.dist.size();
+        R.hap_count = (uint32_t)rb.dist.size() - (rb.helper ? 1 : 0);
+        const int32_t ref = R.ref_local >= 0 ? R.ref_local : (rb.helper ? (int32_t)R.hap_count : -1);
         DevRegion dr{};
         dr.inner_off = (uint32_t)(o.inner / 2);
         dr.n_inner = (uint32_t)R.ranges.size();
         dr.hap_begin = R.hap_begin;
         dr.hap_count = R.hap_count;
+        dr.ref_hap = ref >= 0 && B.dedup ? R.hap_begin + (uint32_t)ref : UINT32_MAX;
         R.key_off = (uint64_t)dr.inner_off * B.n_slots;
         size_t ii = o.inner;
         for (auto &r : R.ranges) {
@@ -439,13 +480,30 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             }
             hm.count_off = count;
             count += (uint64_t)B.n_slots * dr.n_inner;
+            if (dr.ref_hap == o.hap + i) hm.flags |= HAP_REF;
+            if (h.dedup) {
+                hm.flags |= HAP_DEDUP;
+                for (int d = 0; d < 4; d++) hm.dirty[d] = h.dirty[d];
+            }
             B.haps[o.hap + i] = hm;
             B.hap_carriers[o.hap + i] = rb.carriers[i];
+            const bool helper = rb.helper && i + 1 == rb.dist.size();
             uint64_t wn = 0;
             for (const auto &lc : B.pwm_len_hist)
                 if (n >= lc.first) {
-                    wn += (uint64_t)(n - lc.first + 1) * lc.second;
-                    cells[j] += (uint64_t)(n - lc.first + 1) * lc.first * lc.second;
+                    const uint64_t nw = n - lc.first + 1;
+                    uint64_t sw = nw;  // windows the scan reads
+                    if (h.dedup && lc.first <= (uint32_t)(kMMaxChunks * kMChunkCols)) {
+                        const uint32_t m = h.dirty[(lc.first + kMChunkCols - 1) / kMChunkCols - 1];
+                        sw = 0;
+                        for (uint32_t t = 0; t < kDedupMaxTiles; t++)
+                            if ((m >> t) & 1u) sw += std::min<uint64_t>(kMWindows, nw > t * kMWindows ? nw - t * kMWindows : 0);
+                    }
+                    swin[j] += sw * lc.second;
+                    scells[j] += sw * lc.first * lc.second;
+                    if (helper) continue;
+                    wn += nw * lc.second;
+                    cells[j] += nw * lc.first * lc.second;
                 }
             win[j] += wn;
             eff[j] += wn * rb.carriers[i];
@@ -455,6 +513,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         B.windows += win[j];
         B.eff_windows += eff[j];
         B.cell_ops += cells[j];
+        B.scan_windows += swin[j];
+        B.scan_cell_ops += scells[j];
         B.rh.push_back(std::move(built[j].R));
     }
 }
@@ -488,6 +548,10 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     B.pats = &P;
     B.n_samples = n_samples;
     B.keep_membership = keep_membership != 0;
+    {
+        const char *v = getenv("TFBS_DEDUP");
+        B.dedup = !(v && *v && atoi(v) == 0);
+    }
     B.slot_pid = plan.slot_pid;
     B.slots_by_pid.resize(B.slot_pid.size());
     std::iota(B.slots_by_pid.begin(), B.slots_by_pid.end(), 0u);
@@ -667,6 +731,8 @@ size_t tfbs_batch_num_haplotypes(const tfbs_batch *b) { return b ? b->b.haps.siz
 uint64_t tfbs_batch_num_windows(const tfbs_batch *b) { return b ? b->b.windows : 0; }
 uint64_t tfbs_batch_num_effective_windows(const tfbs_batch *b) { return b ? b->b.eff_windows : 0; }
 uint64_t tfbs_batch_num_cell_ops(const tfbs_batch *b) { return b ? b->b.cell_ops : 0; }
+uint64_t tfbs_batch_num_scan_windows(const tfbs_batch *b) { return b ? b->b.scan_windows : 0; }
+uint64_t tfbs_batch_num_scan_cell_ops(const tfbs_batch *b) { return b ? b->b.scan_cell_ops : 0; }
 uint64_t tfbs_batch_input_bytes(const tfbs_batch *b) { return b ? b->b.device_bytes() : 0; }
 uint64_t tfbs_batch_output_bytes(const tfbs_batch *b) { return b ? b->b.n_counts * 4ull : 0; }
 

@@ -94,6 +94,10 @@ struct Batch {
 
     std::vector<RegionH> rh;
     uint64_t windows = 0, eff_windows = 0, cell_ops = 0;
+    // reference-window reuse (HAP_DEDUP, TFBS_DEDUP=0 turns it off): windows and
+    // column lookups the scan executes (helper reference haplotypes included)
+    bool dedup = true;
+    uint64_t scan_windows = 0, scan_cell_ops = 0;
     // host prep seconds (tfbs_batch_prep_seconds): synthetic generation (thread
     // CPU-seconds), build_region (thread CPU-seconds), serial commit (wall), whole fill (wall)
     double prep_s[4] = {0, 0, 0, 0};
@@ -128,6 +132,7 @@ struct RegionBuilt {
     RegionH R;
     std::vector<Distinct> dist;
     std::vector<uint32_t> carriers;
+    bool helper = false;  // dist.back() is a helper reference haplotype (no carriers, no keys)
 };
 
 int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);

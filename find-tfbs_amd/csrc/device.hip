@@ -81,6 +81,10 @@ struct tfbs_ctx {
     DevBuf<DevTile> fast_tiles, gen_tiles;
     DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights, m_meta;
     DevBuf<uint32_t> cands;              // matrix-core candidate lists (scan.hpp)
+    DevBuf<uint32_t> ref_hits, ref_count, ref_over, ref_over_count;  // reference-window reuse (scan.hpp)
+    uint32_t ref_over_cap = 1u << 16;
+    uint32_t n_regions = 0;                // of the resident batch
+    uint32_t *ref_count_host = nullptr;    // pinned: the overflow list's count
     uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
@@ -166,6 +170,19 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         if ((rc = ctx->cands.ensure(n_regions * ctx->cand_cap * 3))) return rc;
         m.cands = ctx->cands.p;
         m.cand_cap = ctx->cand_cap;
+        const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
+        if ((rc = ctx->ref_count.ensure(nr)) || (rc = ctx->ref_hits.ensure((size_t)nr * kRefPerRegion * 2)) ||
+            (rc = ctx->ref_over_count.ensure(1)) || (rc = ctx->ref_over.ensure((size_t)ctx->ref_over_cap * 3)))
+            return rc;
+        m.dedup = 1;
+        m.n_regions = ctx->n_regions;
+        m.ref_hits = ctx->ref_hits.p;
+        m.ref_count = ctx->ref_count.p;
+        m.ref_over = ctx->ref_over.p;
+        m.ref_over_count = ctx->ref_over_count.p;
+        m.ref_over_cap = ctx->ref_over_cap;
+        HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
+        HIP_TRY(hipMemsetAsync(ctx->ref_over_count.p, 0, 4, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
@@ -183,6 +200,9 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
+        const int f = launch_ref_fixup(m, ctx->stream);
+        if (f < 0) return f;
+        launches += f;
     }
     if (!P.fast_tiles.empty()) {
         ScanArgs f = a;
@@ -229,7 +249,9 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
-    ctx->cands.release();
+    ctx->cands.release(); ctx->ref_hits.release(); ctx->ref_count.release(); ctx->ref_over.release();
+    ctx->ref_over_count.release();
+    if (ctx->ref_count_host) (void)hipHostFree(ctx->ref_count_host);
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
@@ -372,6 +394,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->resident = b;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
+    ctx->n_regions = (uint32_t)B.regions.size();
     return TFBS_OK;
 }
 
@@ -383,6 +406,18 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->kernel_timed = false;
     int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
+    if (!ctx->plan.m_supers.empty()) {
+        // the reference-hit overflow list must have held every hit: otherwise grow it and scan again
+        if (!ctx->ref_count_host) HIP_TRY(hipHostMalloc((void **)&ctx->ref_count_host, 4, hipHostMallocDefault));
+        HIP_TRY(hipMemcpyAsync(ctx->ref_count_host, ctx->ref_over_count.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (*ctx->ref_count_host > ctx->ref_over_cap) {
+            ctx->ref_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)*ctx->ref_count_host * 5 / 4 + 1024);
+            ctx->kernel_timed = false;
+            n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
+            if (n < 0) return n;
+        }
+    }
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
     ctx->timing_pending = true;
@@ -578,7 +613,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
             if (nucs[i] == 4) nmask[i / 32] |= 1u << (i % 32);
     }
     std::vector<DevHap> haps{hm};
-    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1}};
+    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, {0, 0, 0}}};
     std::vector<int32_t> inner{0, 0}, posrel{0};
     const uint32_t wpp = (uint32_t)((n + 255) / 256 * 4);
     HIP_TRY(hipSetDevice(ctx->device));
@@ -590,6 +625,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
         return rc;
     ctx->resident = nullptr;
     ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->mfma_hpb);
+    ctx->n_regions = 1;
     const size_t nh = (size_t)P.pats.size() * wpp;
     if ((rc = ctx->hits.ensure(std::max<size_t>(nh, 1)))) return rc;
     if (nh) HIP_TRY(hipMemsetAsync(ctx->hits.p, 0, nh * 8, ctx->stream));

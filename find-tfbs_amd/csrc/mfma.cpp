@@ -259,6 +259,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
             const size_t g0 = plan->m_meta.size();
             plan->m_meta.resize(g0 + kGMetaInts, 0);
             int32_t *gm = &plan->m_meta[g0];
+            gm[kGDepth] = (int32_t)nk;
             std::vector<Split> split(kMStrands);
             for (int n = 0; n < kMStrands; n++) {
                 if ((size_t)n < t.count) {

@@ -43,7 +43,21 @@ struct ScanArgs {
     uint32_t *cands;
     uint32_t cand_cap;
     uint32_t region_base;
+    // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
+    // != 0 scans only their dirty window tiles; the HAP_REF haplotypes' hits
+    // (strand, window) are listed per region (ref_count[r] of kRefPerRegion at
+    // ref_hits + 2 kRefPerRegion r), the excess in an overflow list of
+    // (region, strand, window) (*ref_over_count of ref_over_cap), for the
+    // fix-up kernels
+    uint32_t dedup;
+    uint32_t n_regions;
+    uint32_t *ref_hits;
+    uint32_t *ref_count;
+    uint32_t *ref_over;
+    uint32_t *ref_over_count;
+    uint32_t ref_over_cap;
 };
+constexpr uint32_t kRefPerRegion = 64;
 
 struct LaunchConfig {
     int minw = 2;               // __launch_bounds__ min waves per SIMD of the fast kernel
@@ -62,6 +76,9 @@ int fast_kernel_set_lds(const LaunchConfig &cfg);
 // supers: the host copy of a.msupers (sorted by depth).
 int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
                 const hipStream_t *streams, uint32_t n_streams);
+// Adds to every HAP_DEDUP haplotype the reference's hits in the windows it did
+// not scan (after launch_mfma on the same stream; a: as for launch_mfma).
+int launch_ref_fixup(const ScanArgs &a, hipStream_t stream);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach
 // the waves per SIMD its registers allow.

@@ -167,6 +167,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
     h.nmask_off = uni(h.nmask_off);
     h.pos_off = uni(h.pos_off);
     h.count_off = ((uint64_t)uni((uint32_t)(h.count_off >> 32)) << 32) | uni((uint32_t)h.count_off);
+    for (int d = 0; d < 4; d++) h.dirty[d] = uni(h.dirty[d]);
     return h;
 }
 
@@ -244,6 +245,20 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
     if (A.hits && i / 64 < A.hits_wpp)
         atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + sn]) * A.hits_wpp + i / 64,
                  1ull << (i & 63));
+    if ((hp.flags & HAP_REF) && A.dedup) {  // for the HAP_DEDUP haplotypes' unscanned windows
+        const uint32_t at = atomicAdd(A.ref_count + hp.region, 1u);
+        if (at < kRefPerRegion) {
+            A.ref_hits[2 * ((size_t)hp.region * kRefPerRegion + at)] = g;
+            A.ref_hits[2 * ((size_t)hp.region * kRefPerRegion + at) + 1] = i;
+        } else {
+            const uint32_t o = atomicAdd(A.ref_over_count, 1u);
+            if (o < A.ref_over_cap) {
+                A.ref_over[3 * (size_t)o] = hp.region;
+                A.ref_over[3 * (size_t)o + 1] = g;
+                A.ref_over[3 * (size_t)o + 2] = i;
+            }
+        }
+    }
 }
 
 // Drains the wave's first n queue entries, one entry per lane per round: the
@@ -383,6 +398,61 @@ __device__ __forceinline__ void tile_scores(const char *s_img, uint32_t ti, uint
     for (int kc = 0; kc < NK; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
 }
 
+// One step: window tiles at i0a (A fragments a0) and, if two, i0b (a1) x every
+// strand tile of the super tile.
+template <int NK>
+__device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, const uint32_t *words, uint32_t tile0,
+                                          uint32_t h0, uint32_t nt, uint32_t lane, uint32_t wave, uint32_t hh,
+                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t i0a,
+                                          uint32_t i0b, const v16f &cb, int sa, uint32_t &qn) {
+    if (two) {
+        for (uint32_t ti = 0; ti < nt; ti++) {
+            v16f c0, c1;
+            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
+            const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
+            if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
+            // cold: queue the firing tiles; a tile whose entries do not fit
+            // drains the queue first and its round is scored again (no
+            // accumulator is live across a drain)
+            if (f0) {
+                if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                    drain_queue(A, words, tile0, h0, qn, wave, lane);
+                    qn = 0;
+                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                    x0 = coarse_test(c0);
+                    x1 = coarse_test(c1);
+                }
+                queue_tile(c0, x0, f0, ti, hh, i0a, lane, wave, qn);
+            }
+            if (f1) {
+                if (qn + (uint32_t)__popcll(f1) > kMQueue) {
+                    drain_queue(A, words, tile0, h0, qn, wave, lane);
+                    qn = 0;
+                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                    x1 = coarse_test(c1);
+                }
+                queue_tile(c1, x1, f1, ti, hh, i0b, lane, wave, qn);
+            }
+        }
+    } else {
+        for (uint32_t ti = 0; ti < nt; ti++) {
+            v16f c0;
+            tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+            uint32_t x0 = coarse_test(c0);
+            const uint64_t f0 = __ballot(x0 != 0);
+            if (__builtin_expect(f0 == 0, 1)) continue;
+            if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                drain_queue(A, words, tile0, h0, qn, wave, lane);
+                qn = 0;
+                tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+                x0 = coarse_test(c0);
+            }
+            queue_tile(c0, x0, f0, ti, hh, i0a, lane, wave, qn);
+        }
+    }
+}
+
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
 // of this workgroup's haplotypes, biased by their first word, or global memory).
 template <int NK>
@@ -404,6 +474,27 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         const DevHap hm = load_hap(A.haps + hap);
         if (hm.len < S.lmin) continue;
         const uint32_t nwin = hm.len - S.lmin + 1;
+        if ((hm.flags & HAP_DEDUP) && A.dedup) {
+            // only the window tiles holding a base that differs from the
+            // reference (the others are ref_fixup_kernel's), two at a time
+            const uint32_t ntiles = (nwin + kMWindows - 1) / kMWindows;
+            uint32_t m = hm.dirty[NK - 1] & (ntiles >= 32 ? ~0u : (1u << ntiles) - 1);
+            while (m) {
+                const uint32_t i0a = kMWindows * __builtin_ctz(m);
+                m &= m - 1;
+                const bool two = m != 0;
+                const uint32_t i0b = two ? kMWindows * __builtin_ctz(m) : i0a;
+                if (two) m &= m - 1;
+                WinWords wa, wb;
+                v4i a0[NK], a1[NK];
+                load_window(A, words, hm, i0a, lane, wa);
+                if (two) load_window(A, words, hm, i0b, lane, wb);
+                build_onehot<NK>(hm, i0a, lane, wa, tab, a0);
+                if (two) build_onehot<NK>(hm, i0b, lane, wb, tab, a1);
+                scan_step<NK>(A, s_img, words, tile0, h0, nt, lane, wave, hh, a0, a1, two, i0a, i0b, cb, sa, qn);
+            }
+            continue;
+        }
         // window tiles two at a time, so that each B fragment read from LDS
         // feeds two MFMAs
         WinWords ww0, ww1;
@@ -417,54 +508,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             if (i0 + 2 * kMWindows < nwin) load_window(A, words, hm, i0 + 2 * kMWindows, lane, ww0);  // next step's words
             if (i0 + 3 * kMWindows < nwin) load_window(A, words, hm, i0 + 3 * kMWindows, lane, ww1);
             // the other waves of the SIMD hide the latencies
-            // a tile whose entries do not fit drains the queue and its round is
-            // scored again (skip0: the first tile's entries are already queued)
-            if (two) {
-                for (uint32_t ti = 0; ti < nt; ti++) {
-                    v16f c0, c1;
-                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
-                    uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
-                    const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-                    if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
-                    // cold: queue the firing tiles; a tile whose entries do not fit
-                    // drains the queue first and its round is scored again (no
-                    // accumulator is live across a drain)
-                    if (f0) {
-                        if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                            drain_queue(A, words, tile0, h0, qn, wave, lane);
-                            qn = 0;
-                            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
-                            x0 = coarse_test(c0);
-                            x1 = coarse_test(c1);
-                        }
-                        queue_tile(c0, x0, f0, ti, hh, i0, lane, wave, qn);
-                    }
-                    if (f1) {
-                        if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                            drain_queue(A, words, tile0, h0, qn, wave, lane);
-                            qn = 0;
-                            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
-                            x1 = coarse_test(c1);
-                        }
-                        queue_tile(c1, x1, f1, ti, hh, i0 + kMWindows, lane, wave, qn);
-                    }
-                }
-            } else {
-                for (uint32_t ti = 0; ti < nt; ti++) {
-                    v16f c0;
-                    tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
-                    uint32_t x0 = coarse_test(c0);
-                    const uint64_t f0 = __ballot(x0 != 0);
-                    if (__builtin_expect(f0 == 0, 1)) continue;
-                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                        drain_queue(A, words, tile0, h0, qn, wave, lane);
-                        qn = 0;
-                        tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
-                        x0 = coarse_test(c0);
-                    }
-                    queue_tile(c0, x0, f0, ti, hh, i0, lane, wave, qn);
-                }
-            }
+            scan_step<NK>(A, s_img, words, tile0, h0, nt, lane, wave, hh, a0, a1, two, i0, i0 + kMWindows, cb, sa, qn);
         }
     }
     drain_queue(A, words, tile0, h0, qn, wave, lane);  // the wave's last entries
@@ -519,6 +563,109 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     }
 }
 
+// Reference-window reuse.  A HAP_DEDUP haplotype whose window tile of a
+// reference hit (strand g, window i) was not scanned (the tile holds no base
+// differing from the reference) has the same bases and positions there, so it
+// has the hit too: its counts get the hit's inner-range overlaps (range.rs:18-21
+// as main.rs:503 uses it).
+__device__ __forceinline__ uint32_t ref_hit_overlaps(const ScanArgs &A, const DevRegion &rg, uint32_t g, uint32_t i,
+                                                     uint32_t &nk, uint32_t &off0) {
+    const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
+    const uint32_t sn = g & 63u, L = (uint32_t)meta[kGLen + sn];
+    nk = (uint32_t)meta[kGDepth];
+    off0 = (uint32_t)meta[kGSlot + sn] * rg.n_inner;
+    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+    const int32_t p = (int32_t)i;  // the reference's positions are affine
+    uint32_t mask = 0;             // bit k: the match overlaps inner range k (k < 32)
+    for (uint32_t k = 0; k < rg.n_inner && k < 32; k++) {
+        const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+        const uint32_t span = (uint32_t)(en - s);
+        if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span) mask |= 1u << k;
+    }
+    return mask;
+}
+
+// One workgroup per region: its listed reference hits in LDS, one thread per
+// distinct haplotype.
+constexpr uint32_t kFixBlock = 128;
+__global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
+    __shared__ uint32_t s_g[kRefPerRegion], s_i[kRefPerRegion], s_nk[kRefPerRegion], s_off[kRefPerRegion],
+        s_mask[kRefPerRegion];
+    const uint32_t region = blockIdx.x;
+    const DevRegion rg = A.regions[region];
+    if (rg.ref_hap == UINT32_MAX || rg.n_inner == 0) return;
+    const uint32_t n = min(A.ref_count[region], kRefPerRegion);
+    if (n == 0) return;
+    for (uint32_t t = threadIdx.x; t < n; t += kFixBlock) {
+        const uint32_t g = A.ref_hits[2 * ((size_t)region * kRefPerRegion + t)];
+        const uint32_t i = A.ref_hits[2 * ((size_t)region * kRefPerRegion + t) + 1];
+        uint32_t nk, off0;
+        s_mask[t] = ref_hit_overlaps(A, rg, g, i, nk, off0);
+        s_g[t] = g;
+        s_i[t] = i;
+        s_nk[t] = nk;
+        s_off[t] = off0;
+    }
+    __syncthreads();
+    for (uint32_t h = rg.hap_begin + threadIdx.x; h < rg.hap_begin + rg.hap_count; h += kFixBlock) {
+        const DevHap hp = A.haps[h];
+        if (!(hp.flags & HAP_DEDUP)) continue;
+        for (uint32_t t = 0; t < n; t++) {
+            if ((hp.dirty[s_nk[t] - 1] >> (s_i[t] / kMWindows)) & 1u) continue;  // scanned
+            // no-return atomics: issued back to back (a plain add would wait on
+            // every load, as the adds may alias)
+            for (uint32_t m = s_mask[t]; m; m &= m - 1) atomicAdd(A.counts + hp.count_off + s_off[t] + __builtin_ctz(m), 1u);
+        }
+    }
+    // inner ranges past 32 (rare): atomics, as the overflow list
+    if (rg.n_inner > 32) {
+        __syncthreads();
+        for (uint32_t t = 0; t < n; t++) {
+            const uint32_t g = s_g[t], i = s_i[t];
+            const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
+            const uint32_t L = (uint32_t)meta[kGLen + (g & 63u)];
+            const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+            for (uint32_t h = rg.hap_begin + threadIdx.x; h < rg.hap_begin + rg.hap_count; h += kFixBlock) {
+                const DevHap hp = A.haps[h];
+                if (!(hp.flags & HAP_DEDUP) || ((hp.dirty[s_nk[t] - 1] >> (i / kMWindows)) & 1u)) continue;
+                for (uint32_t k = 32; k < rg.n_inner; k++) {
+                    const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+                    const uint32_t span = (uint32_t)(en - s);
+                    if ((uint32_t)((int32_t)i - s) <= span || (uint32_t)((int32_t)(i + L) - 1 - s) <= span)
+                        atomicAdd(A.counts + hp.count_off + s_off[t] + k, 1u);
+                }
+            }
+        }
+    }
+}
+
+// The overflow list (regions with more than kRefPerRegion reference hits): one
+// wave per hit, atomics (runs after ref_fixup_kernel).
+__global__ __launch_bounds__(256) void ref_fixup_over_kernel(ScanArgs A) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t n = min(*A.ref_over_count, A.ref_over_cap);
+    for (uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += gridDim.x * 4) {
+        const uint32_t region = A.ref_over[3 * (size_t)r], g = A.ref_over[3 * (size_t)r + 1];
+        const uint32_t i = A.ref_over[3 * (size_t)r + 2];
+        const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
+        const uint32_t sn = g & 63u, L = (uint32_t)meta[kGLen + sn], nk = (uint32_t)meta[kGDepth];
+        const DevRegion rg = A.regions[region];
+        const uint32_t off0 = (uint32_t)meta[kGSlot + sn] * rg.n_inner;
+        const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+        const int32_t p = (int32_t)i;
+        for (uint32_t h = rg.hap_begin + lane; h < rg.hap_begin + rg.hap_count; h += 64) {
+            const DevHap hp = A.haps[h];
+            if (!(hp.flags & HAP_DEDUP) || ((hp.dirty[nk - 1] >> (i / kMWindows)) & 1u)) continue;
+            for (uint32_t k = 0; k < rg.n_inner; k++) {
+                const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+                const uint32_t span = (uint32_t)(en - s);
+                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
+                    atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
+            }
+        }
+    }
+}
+
 typedef void (*MfmaKernel)(ScanArgs);
 template <int NK> MfmaKernel mfma_nk(bool staged) {
     return staged ? scan_mfma_kernel<true, NK> : scan_mfma_kernel<false, NK>;
@@ -533,6 +680,15 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {
 }
 
 }  // namespace
+
+int launch_ref_fixup(const ScanArgs &a, hipStream_t stream) {
+    if (a.n_regions == 0) return 0;
+    hipLaunchKernelGGL(ref_fixup_kernel, dim3(a.n_regions), dim3(kFixBlock), 0, stream, a);
+    hipLaunchKernelGGL(ref_fixup_over_kernel, dim3(1024), dim3(256), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("ref_fixup_kernel launch: ") + hipGetErrorString(e));
+    return 2;
+}
 
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
     uint32_t mx = 0;

@@ -106,8 +106,8 @@ constexpr int kMFieldBias = 1023;  // V = U + kMFieldBias - T0: candidate iff V 
 // The fields only the candidate rescoring reads live in global memory
 // (Plan::m_meta, kGMetaInts per tile, indexed by the strand 2 n + h): min_score,
 // offset of the exact weights (4 per column), len, slot, pattern index.
-enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256 };
-constexpr int kGMetaInts = 320;
+enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256, kGDepth = 320 };
+constexpr int kGMetaInts = 384;  // [kGDepth]: the tile's K depth (one int)
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
 // depth nk; tile t's B fragments at t * mfma_tile_bytes(nk); its
@@ -125,7 +125,16 @@ struct DevMSuper {
     uint32_t acc0;
 };
 
-enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u };
+// HAP_REF: the region's reference haplotype (the reference group's, or a
+// helper with no carriers after the region's distinct haplotypes); its
+// matrix-core hits are listed for the reference-window fix-up.  HAP_DEDUP: an
+// SNV-only haplotype of the reference's length and N positions: the matrix-core
+// scan reads only its window tiles that contain a base differing from the
+// reference (dirty[nk - 1], for strands of up to 8 nk columns); every other
+// window has the reference window's bases and positions, so its hits are the
+// reference's, added by ref_fixup_kernel.
+enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
+constexpr uint32_t kDedupMaxTiles = 32;  // window tiles a dirty mask covers
 
 struct DevHap {
     uint32_t word_off;   // packed 2-bit bases, 16 per u32, LSB first
@@ -135,13 +144,16 @@ struct DevHap {
     uint32_t nmask_off;  // u32 words of the N mask (bit i = base i is N), if HAP_HAS_N
     uint32_t pos_off;    // int32 positions relative to ext_start, if HAP_HAS_POS
     uint64_t count_off;  // counts[count_off + slot * n_inner + k]
+    uint32_t dirty[4];   // HAP_DEDUP: per K depth, bit t = window tile t (windows 32 t ..) holds a differing base
 };
 
 struct DevRegion {
     uint32_t inner_off;  // into the inner (s_rel, e_rel) pair array
     uint32_t n_inner;    // distinct inner ranges
     uint32_t hap_begin;  // first distinct haplotype (their count blocks are consecutive)
-    uint32_t hap_count;
+    uint32_t hap_count;  // distinct haplotypes (a helper reference haplotype follows them)
+    uint32_t ref_hap;    // the HAP_REF haplotype, UINT32_MAX if none
+    uint32_t pad[3];
 };
 
 // Per-sample encoding of one varying key (tfbs_batch_encode, key_encode_kernel):

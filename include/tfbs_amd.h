@@ -198,6 +198,12 @@ uint64_t tfbs_batch_num_windows(const tfbs_batch *b);
 uint64_t tfbs_batch_num_cell_ops(const tfbs_batch *b);
 /* Per-sample-weighted windows (each distinct haplotype times its carrier count). */
 uint64_t tfbs_batch_num_effective_windows(const tfbs_batch *b);
+/* Windows and column lookups the scan executes: a window of an SNV-only haplotype
+   whose bases and positions equal the region's reference window takes the
+   reference window's result (reference-window reuse, TFBS_DEDUP=0 disables it);
+   helper reference haplotypes of regions without a reference group count here. */
+uint64_t tfbs_batch_num_scan_windows(const tfbs_batch *b);
+uint64_t tfbs_batch_num_scan_cell_ops(const tfbs_batch *b);
 /* Packed bytes the scan reads from HBM per launch (sequence + masks + positions + metadata). */
 uint64_t tfbs_batch_input_bytes(const tfbs_batch *b);
 /* Bytes of hit counts the scan writes. */
