@@ -328,6 +328,47 @@ def test_dense_hits_vs_oracle(tmp_path, monkeypatch, thr):
     assert b.num_haplotypes > n_regions
 
 
+@pytest.mark.parametrize("thr", [1e-3, 0.05])
+def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
+    """Reference-window reuse (HAP_DEDUP, ref_fixup_kernel) on its edge cases, against
+    the oracle: an SNV every haplotype carries (no reference group: the helper copy of
+    the reference supplies the hits), N runs in the reference, haplotypes with indels
+    (scanned whole), 40 nested inner ranges (the fix-up's path past 32 ranges) and
+    p = 0.05 thresholds (over 64 reference hits per region: the overflow list)."""
+    monkeypatch.setenv("TFBS_MFMA", "1")
+    ps, _ = synth_patterns(tmp_path, 10, 3, 71, thr=thr)
+    n_samples, n_regions = 60, 6
+    H = 2 * n_samples
+    rnd = random.Random(5)
+    regions, ranges = [], []
+    for j in range(n_regions):
+        r = T.SynthRegion(31, j, n_samples, ps.max_length, 20 if j == 3 else 0)
+        s, e = r.merged
+        es = s - ps.max_length + 1
+        ref = list(r.ref)
+        if j == 2:  # N runs away from the variant sites
+            for q in range(10, 18):
+                ref[q] = "N"
+        ref = "".join(ref)
+        recs = [("car", pos, rf, alt, car) for pos, rf, alt, car in r.records
+                if j != 2 or not any(10 <= pos - es + t < 18 for t in range(len(rf)))]
+        if j in (0, 4):  # every haplotype carries one SNV: no reference group
+            q = len(ref) // 2
+            while ref[q] == "N" or any(rec[1] == es + q for rec in recs):
+                q += 1
+            recs.append(("car", es + q, ref[q], "ACGT"[("ACGT".index(ref[q]) + 1) % 4], list(range(H))))
+        regions.append({"merged": (s, e), "ref": ref, "records": recs})
+        ranges.append((s, e))
+        if j == 5:  # 40 nested inner ranges sharing the merged start
+            ranges.extend((s, s + 1 + k) for k in range(39))
+    beds = [("synthetic.bed", ranges)]
+    b = _compare(ps, n_samples, beds, regions)
+    assert b.num_scan_windows < b.num_windows
+    monkeypatch.setenv("TFBS_DEDUP", "0")  # the same job scanning every window
+    b0 = _compare(ps, n_samples, beds, regions)
+    assert b0.num_scan_windows > b.num_scan_windows
+
+
 def test_multi_bed_duplicate_and_nested_inner_peaks(tmp_path):
     """Several bed sources, duplicate ranges (double count), a range that is never selected
     (strictly inside a 3-way merge, bed.rs:77/89), empty ranges, Ns in the reference."""
