@@ -289,8 +289,8 @@ def main():
     e2e_s = fill_s + t_up + t_scan1 + t_red + t_enc + t_rows
     (elapsed, e2e_max), tot = job_totals(dist, rdev, [elapsed, e2e_s],
                                          [batch.num_windows, batch.num_regions, batch.num_effective_windows,
-                                          n_rows, n_row_bytes])
-    tot_windows, tot_regions, tot_eff, tot_rows, tot_row_bytes = tot
+                                          n_rows, n_row_bytes, batch.num_scan_windows])
+    tot_windows, tot_regions, tot_eff, tot_rows, tot_row_bytes, tot_scan = tot
 
     if rank == 0:
         steps = args.steps
@@ -303,18 +303,22 @@ def main():
         for p in ps.to_list():
             pattern_bytes += ((len(p) + 15) // 16) * 1536 + 16 * len(p) + 24
         alg_bytes = batch.input_bytes + batch.output_bytes + pattern_bytes
-        cell_tops = batch.num_cell_ops / (kms / 1e3) / 1e12
+        # executed work: the cells of the windows the scan reads (reference-window
+        # reuse leaves the others to the reference's result)
+        scan_cells = batch.num_scan_cell_ops
+        cell_tops = scan_cells / (kms / 1e3) / 1e12
         if mms > 0:  # the matrix-core kernel scored every strand of this workload
-            mops = MFMA_OPS_PER_CELL * batch.num_cell_ops / (mms / 1e3) / 1e12
+            mops = MFMA_OPS_PER_CELL * scan_cells / (mms / 1e3) / 1e12
             roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TFLOP/s",
                     "frac": mops / MFMA_F6_PEAK_TOPS, "traffic": traffic,
                     "kernel": "scan_mfma_kernel<staged, K depth> (one launch per K depth, 4 streams)",
                     "kernel_ms": mms,
                     "note": "achieved = 8 ops per (window, strand, column) cell of the FP4 one-hot x FP6 "
-                            "bound-digit GEMM x %.4g cells / the MFMA phase's HIP-event time (first launch to "
-                            "last, joined on the ctx stream; tools/trace_phase.py reads the same phase from "
-                            "the rocprofv3 trace); traffic = HBM bytes of the phase's dispatches per step, "
-                            "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, from %s" % (batch.num_cell_ops, traffic_src)}
+                            "bound-digit GEMM x %.4g cells the scan reads (of %.4g: reference-window reuse) / "
+                            "the MFMA phase's HIP-event time (first launch to last, joined on the ctx stream; "
+                            "tools/trace_phase.py reads the same phase from the rocprofv3 trace); traffic = HBM "
+                            "bytes of the phase's dispatches per step, FETCH_SIZE x2 (gfx950) + WRITE_SIZE, "
+                            "from %s" % (scan_cells, batch.num_cell_ops, traffic_src)}
             hbm_ms = mms
         else:
             roof = None
@@ -348,7 +352,14 @@ def main():
                 "distinct_haplotypes_per_gpu": batch.num_haplotypes,
                 "windows_per_step": int(tot_windows), "parallelism": "region shard x%d" % world,
                 "scan_path": path,
+                "scanned_windows_per_step": int(tot_scan),
             },
+            "value_note": "windows of every distinct haplotype resolved per second (the reference scores each "
+                          "of them); an SNV-only haplotype's windows whose bases and positions equal the "
+                          "region's reference window take the reference window's result (reference-window "
+                          "reuse, exact; TFBS_DEDUP=0 scans them all), scanned_windows_per_s counts the "
+                          "windows the kernels read",
+            "scanned_windows_per_s": tot_scan * steps / elapsed,
             "scan_regions_per_s": tot_regions * steps / elapsed,
             "effective_windows_per_s": tot_eff * steps / elapsed,
             "end_to_end": {

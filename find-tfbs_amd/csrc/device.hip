@@ -88,7 +88,7 @@ struct tfbs_ctx {
     uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
-    uint32_t mfma_lds = 40 * 1024;  // LDS image budget of one MFMA super tile
+    uint32_t mfma_lds = 44 * 1024;  // LDS image budget of one MFMA super tile
     uint32_t mfma_hpb = 64;         // haplotypes per MFMA workgroup
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
@@ -284,7 +284,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->haps_per_block = (uint32_t)std::max(8, env_int("TFBS_HAPS_PER_BLOCK", 128));
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
-    ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 40))) * 1024u;
+    ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 44))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     PlanOptions opt;

@@ -216,16 +216,19 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
     }
     size_t ti = 0;
     while (ti < tiles.size()) {
-        // a super tile: consecutive tiles of the same K depth within the LDS budget
-        const uint32_t nk = tiles[ti].nk;
-        const uint32_t per = mfma_tile_bytes(nk);
-        const uint32_t lds_bytes = std::max(per, opt.mfma_lds_by_nk[nk] ? opt.mfma_lds_by_nk[nk] : opt.mfma_lds_bytes);
-        // the run of tiles with this depth, split into equal super tiles
+        // a super tile: consecutive tiles of one depth class within the LDS budget
+        const uint32_t nk = mfma_depth_class(tiles[ti].nk);
+        const uint32_t lds_bytes = opt.mfma_lds_by_nk[nk] ? opt.mfma_lds_by_nk[nk] : opt.mfma_lds_bytes;
+        // the run of tiles of this class, split into equal-sized super tiles
         size_t run = ti;
-        while (run < tiles.size() && tiles[run].nk == nk) run++;
-        const size_t max_per_super = std::min<size_t>(kMSuperMaxTiles, std::max<size_t>(1, lds_bytes / per));
-        const size_t n_super = (run - ti + max_per_super - 1) / max_per_super;
-        const size_t tj = ti + (run - ti + n_super - 1) / n_super;
+        uint64_t run_bytes = 0;
+        while (run < tiles.size() && mfma_depth_class(tiles[run].nk) == nk) run_bytes += mfma_tile_bytes(tiles[run++].nk);
+        const size_t n_super = std::max<size_t>((run - ti + kMSuperMaxTiles - 1) / kMSuperMaxTiles,
+                                                (run_bytes + lds_bytes - 1) / std::max<uint32_t>(1, lds_bytes));
+        const size_t per_super = (run - ti + n_super - 1) / n_super;
+        size_t tj = ti;
+        uint32_t img_bytes = 0;
+        while (tj < run && tj - ti < per_super) img_bytes += mfma_tile_bytes(tiles[tj++].nk);
         const uint32_t count = (uint32_t)(tj - ti);
         // the common threshold with the fewest candidates over the super tile's strands
         size_t bk = 0;
@@ -243,7 +246,12 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         S.tile_count = count;
         S.nk = nk;
         S.img_off = (uint32_t)(plan->m_image.size() * 4);
-        S.img_bytes = count * per;
+        S.img_bytes = img_bytes;
+        for (uint32_t d = 1; d <= 4; d++) {  // tiles are sorted by depth (strands by length)
+            uint32_t e = 0;
+            while (e < count && tiles[ti + e].nk <= d) e++;
+            S.seg |= e << (8 * (d - 1));
+        }
         S.t0 = (int32_t)t0;
         S.acc0 = f32_bits((float)((1 << 23) + (kMFieldBias - t0) * (1 + (1 << kMFieldBits))));
         S.lmin = UINT32_MAX;
@@ -252,9 +260,9 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         // the first columns, so U <= t0 for windows without N there
         const uint32_t pad_cols = (uint32_t)((-t0) / 60 + 1);
         std::vector<uint8_t> img(S.img_bytes, 0);
-        for (uint32_t k = 0; k < count; k++) {
+        uint32_t b_off = 0;
+        for (uint32_t k = 0; k < count; b_off += mfma_tile_bytes(tiles[ti + k].nk), k++) {
             const TileSrc &t = tiles[ti + k];
-            const uint32_t b_off = k * per;
             S.lmin = std::min(S.lmin, t.lmin);
             const size_t g0 = plan->m_meta.size();
             plan->m_meta.resize(g0 + kGMetaInts, 0);
@@ -283,7 +291,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
             // 8 kc + t, base c: element e = 4 t + c at bits 6 e of the lane's 192
             // bits, dwords 0-3 at kc * 1536 + lane * 16, dwords 4-5 at kc * 1536 +
             // 1024 + lane * 8 (mfma_tile_bytes)
-            for (uint32_t kc = 0; kc < nk; kc++)
+            for (uint32_t kc = 0; kc < t.nk; kc++)
                 for (int l = 0; l < 64; l++) {
                     const int sn = 2 * (l & 31) + (l >> 5);
                     const Split &sp = split[sn];

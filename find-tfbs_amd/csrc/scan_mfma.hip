@@ -133,16 +133,15 @@ struct BFrag {
     int2 c;
 };
 
-template <int NK>
-__device__ __forceinline__ void load_frags(const char *s_img, uint32_t ti, uint32_t lane, BFrag (&f)[NK]) {
-    const char *p = s_img + ti * mfma_tile_bytes(NK);
+template <int D>
+__device__ __forceinline__ void load_frags(const char *tile, uint32_t lane, BFrag (&f)[D]) {
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) {
+    for (int kc = 0; kc < D; kc++) {
         // no ds_read2 merging across chunks: merged pairs need v_mov copies
         // into the MFMA operand tuples
         if (kc) asm volatile("" ::: "memory");
-        f[kc].b = *reinterpret_cast<const v4i *>(p + kc * 1536 + lane * 16);
-        f[kc].c = *reinterpret_cast<const int2 *>(p + kc * 1536 + 1024 + lane * 8);
+        f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
+        f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
     }
 }
 
@@ -178,7 +177,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 // workgroup's group, 32-63 the window tile start / 32).  A tile whose entries do
 // not fit drains the queue (drain_queue) and its round is scored again, so no
 // accumulator is live across a drain.
-constexpr uint32_t kMQueue = 96;  // entries per wave (>= one tile's 64)
+constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue][2];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint32_t s_cn;  // candidates the workgroup appended
@@ -372,43 +371,47 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t
     qn += (uint32_t)__popcll(fired);
 }
 
-// The accumulators of one round: strand tile ti x the window tiles a0, a1 (one
-// B fragment read feeds both MFMAs), starting from the field biases cb.
-template <int NK>
-__device__ __forceinline__ void round_scores(const char *s_img, uint32_t ti, uint32_t lane, const v4i (&a0)[NK],
-                                             const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
-    BFrag f[NK];
-    load_frags<NK>(s_img, ti, lane, f);
+// The accumulators of one round: a strand tile of depth D (its image at
+// `tile`) x the window tiles a0, a1 (one B fragment read feeds both MFMAs),
+// starting from the field biases cb.
+template <int D, int NK>
+__device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v4i (&a1)[NK],
+                                             const v16f &cb, int sa, v16f &c0, v16f &c1) {
+    BFrag f[D];
+    load_frags<D>(tile, lane, f);
     c0 = cb;
     c1 = cb;
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) {
+    for (int kc = 0; kc < D; kc++) {
         c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
         c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
     }
 }
 
-template <int NK>
-__device__ __forceinline__ void tile_scores(const char *s_img, uint32_t ti, uint32_t lane, const v4i (&a0)[NK],
-                                            const v16f &cb, int sa, v16f &c0) {
-    BFrag f[NK];
-    load_frags<NK>(s_img, ti, lane, f);
+template <int D, int NK>
+__device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v16f &cb,
+                                            int sa, v16f &c0) {
+    BFrag f[D];
+    load_frags<D>(tile, lane, f);
     c0 = cb;
 #pragma unroll
-    for (int kc = 0; kc < NK; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+    for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
 }
 
-// One step: window tiles at i0a (A fragments a0) and, if two, i0b (a1) x every
-// strand tile of the super tile.
-template <int NK>
-__device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, const uint32_t *words, uint32_t tile0,
-                                          uint32_t h0, uint32_t nt, uint32_t lane, uint32_t wave, uint32_t hh,
-                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t i0a,
-                                          uint32_t i0b, const v16f &cb, int sa, uint32_t &qn) {
+// The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
+// at i0a (A fragments a0) and, if two, i0b (a1).
+template <int D, int NK>
+__device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
+                                             const uint32_t *words, uint32_t tile0, uint32_t h0, uint32_t lane,
+                                             uint32_t wave, uint32_t hh, const v4i (&a0)[NK], const v4i (&a1)[NK],
+                                             bool two, uint32_t i0a, uint32_t i0b, const v16f &cb, int sa,
+                                             uint32_t &qn) {
+    constexpr uint32_t kTB = mfma_tile_bytes(D);
     if (two) {
-        for (uint32_t ti = 0; ti < nt; ti++) {
+        for (uint32_t ti = tb; ti < te; ti++) {
+            const char *tile = img + (ti - tb) * kTB;
             v16f c0, c1;
-            round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+            round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
             uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
             const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
             if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
@@ -419,7 +422,7 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
                 if (qn + (uint32_t)__popcll(f0) > kMQueue) {
                     drain_queue(A, words, tile0, h0, qn, wave, lane);
                     qn = 0;
-                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                    round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x0 = coarse_test(c0);
                     x1 = coarse_test(c1);
                 }
@@ -429,28 +432,54 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
                 if (qn + (uint32_t)__popcll(f1) > kMQueue) {
                     drain_queue(A, words, tile0, h0, qn, wave, lane);
                     qn = 0;
-                    round_scores<NK>(s_img, ti, lane, a0, a1, cb, sa, c0, c1);
+                    round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x1 = coarse_test(c1);
                 }
                 queue_tile(c1, x1, f1, ti, hh, i0b, lane, wave, qn);
             }
         }
     } else {
-        for (uint32_t ti = 0; ti < nt; ti++) {
+        for (uint32_t ti = tb; ti < te; ti++) {
+            const char *tile = img + (ti - tb) * kTB;
             v16f c0;
-            tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+            tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
             uint32_t x0 = coarse_test(c0);
             const uint64_t f0 = __ballot(x0 != 0);
             if (__builtin_expect(f0 == 0, 1)) continue;
             if (qn + (uint32_t)__popcll(f0) > kMQueue) {
                 drain_queue(A, words, tile0, h0, qn, wave, lane);
                 qn = 0;
-                tile_scores<NK>(s_img, ti, lane, a0, cb, sa, c0);
+                tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
                 x0 = coarse_test(c0);
             }
             queue_tile(c0, x0, f0, ti, hh, i0a, lane, wave, qn);
         }
     }
+}
+
+// One step: every strand tile of the super tile (depth segments 1..NK, byte
+// d - 1 of seg = the end of depth d) x the window tiles at i0a / i0b.
+template <int NK>
+__device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const uint32_t *words,
+                                          uint32_t tile0, uint32_t h0, uint32_t lane, uint32_t wave, uint32_t hh,
+                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t i0a,
+                                          uint32_t i0b, const v16f &cb, int sa, uint32_t &qn) {
+    uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
+    const char *img = s_img;
+#define TFBS_SEGMENT(D)                                                                                          \
+    if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
+        const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \
+        if (te > tb)                                                                                             \
+            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, words, tile0, h0, lane, wave, hh, a0, a1, two, \
+                                                 i0a, i0b, cb, sa, qn);                                          \
+        img += (te - tb) * mfma_tile_bytes(D);                                                                   \
+        tb = te;                                                                                                 \
+    }
+    TFBS_SEGMENT(1)
+    TFBS_SEGMENT(2)
+    TFBS_SEGMENT(3)
+    TFBS_SEGMENT(4)
+#undef TFBS_SEGMENT
 }
 
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
@@ -459,7 +488,6 @@ template <int NK>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
     constexpr uint32_t kWaves = kMBlock / 64;
-    const uint32_t nt = S.tile_count;
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t tile0 = S.tile0;
     const float a0f = __uint_as_float(S.acc0);
@@ -474,16 +502,21 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         const DevHap hm = load_hap(A.haps + hap);
         if (hm.len < S.lmin) continue;
         const uint32_t nwin = hm.len - S.lmin + 1;
-        if ((hm.flags & HAP_DEDUP) && A.dedup) {
-            // only the window tiles holding a base that differs from the
-            // reference (the others are ref_fixup_kernel's), two at a time
-            const uint32_t ntiles = (nwin + kMWindows - 1) / kMWindows;
-            uint32_t m = hm.dirty[NK - 1] & (ntiles >= 32 ? ~0u : (1u << ntiles) - 1);
+        // window tiles two at a time (each B fragment read from LDS feeds two
+        // MFMAs), 32 tiles per mask; a HAP_DEDUP haplotype only the tiles holding
+        // a base that differs from the reference (the others are
+        // ref_fixup_kernel's)
+        const uint32_t ntiles = (nwin + kMWindows - 1) / kMWindows;
+        const bool dedup = (hm.flags & HAP_DEDUP) && A.dedup;  // then ntiles <= 32
+        for (uint32_t base = 0; base < ntiles; base += 32) {
+            const uint32_t nb = min(32u, ntiles - base);
+            uint32_t m = nb >= 32 ? ~0u : (1u << nb) - 1;
+            if (dedup) m &= hm.dirty[NK - 1];
             while (m) {
-                const uint32_t i0a = kMWindows * __builtin_ctz(m);
+                const uint32_t i0a = kMWindows * (base + __builtin_ctz(m));
                 m &= m - 1;
                 const bool two = m != 0;
-                const uint32_t i0b = two ? kMWindows * __builtin_ctz(m) : i0a;
+                const uint32_t i0b = two ? kMWindows * (base + __builtin_ctz(m)) : i0a;
                 if (two) m &= m - 1;
                 WinWords wa, wb;
                 v4i a0[NK], a1[NK];
@@ -491,24 +524,9 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
                 if (two) load_window(A, words, hm, i0b, lane, wb);
                 build_onehot<NK>(hm, i0a, lane, wa, tab, a0);
                 if (two) build_onehot<NK>(hm, i0b, lane, wb, tab, a1);
-                scan_step<NK>(A, s_img, words, tile0, h0, nt, lane, wave, hh, a0, a1, two, i0a, i0b, cb, sa, qn);
+                // the other waves of the SIMD hide the latencies
+                scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, hh, a0, a1, two, i0a, i0b, cb, sa, qn);
             }
-            continue;
-        }
-        // window tiles two at a time, so that each B fragment read from LDS
-        // feeds two MFMAs
-        WinWords ww0, ww1;
-        load_window(A, words, hm, 0, lane, ww0);
-        if (kMWindows < nwin) load_window(A, words, hm, kMWindows, lane, ww1);
-        for (uint32_t i0 = 0; i0 < nwin; i0 += 2 * kMWindows) {
-            const bool two = i0 + kMWindows < nwin;
-            v4i a0[NK], a1[NK];
-            build_onehot<NK>(hm, i0, lane, ww0, tab, a0);
-            if (two) build_onehot<NK>(hm, i0 + kMWindows, lane, ww1, tab, a1);
-            if (i0 + 2 * kMWindows < nwin) load_window(A, words, hm, i0 + 2 * kMWindows, lane, ww0);  // next step's words
-            if (i0 + 3 * kMWindows < nwin) load_window(A, words, hm, i0 + 3 * kMWindows, lane, ww1);
-            // the other waves of the SIMD hide the latencies
-            scan_step<NK>(A, s_img, words, tile0, h0, nt, lane, wave, hh, a0, a1, two, i0, i0 + kMWindows, cb, sa, qn);
         }
     }
     drain_queue(A, words, tile0, h0, qn, wave, lane);  // the wave's last entries
@@ -670,13 +688,8 @@ typedef void (*MfmaKernel)(ScanArgs);
 template <int NK> MfmaKernel mfma_nk(bool staged) {
     return staged ? scan_mfma_kernel<true, NK> : scan_mfma_kernel<false, NK>;
 }
-MfmaKernel mfma_variant(bool staged, uint32_t nk) {
-    switch (nk) {
-    case 1: return mfma_nk<1>(staged);
-    case 2: return mfma_nk<2>(staged);
-    case 3: return mfma_nk<3>(staged);
-    default: return mfma_nk<4>(staged);
-    }
+MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_depth_class)
+    return nk <= 2 ? mfma_nk<2>(staged) : mfma_nk<4>(staged);
 }
 
 }  // namespace

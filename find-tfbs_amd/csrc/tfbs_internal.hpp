@@ -109,21 +109,27 @@ constexpr int kMFieldBias = 1023;  // V = U + kMFieldBias - T0: candidate iff V 
 enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256, kGDepth = 320 };
 constexpr int kGMetaInts = 384;  // [kGDepth]: the tile's K depth (one int)
 
-// The strand tiles one workgroup stages in LDS: tile_count tiles of equal K
-// depth nk; tile t's B fragments at t * mfma_tile_bytes(nk); its
-// rescoring fields at Plan::m_meta[(tile0 + t) * kGMetaInts].  t0: the common
-// candidate threshold of its strands' bounds (U > t0), acc0 the accumulator's
-// start value 2^23 + (1023 - t0) (1 + 2^11) as f32 bits.
+// The strand tiles one workgroup stages in LDS: tile_count tiles of K depth
+// 1..nk (nk = 2 for tiles of depth 1-2, 4 for 3-4: one kernel, one A fragment
+// build per window tile for each class), sorted by depth: byte seg d - 1 of
+// `seg` = the first tile deeper than d; the tiles lie back to back, each
+// mfma_tile_bytes(its depth); tile t's rescoring fields at
+// Plan::m_meta[(tile0 + t) * kGMetaInts].  t0: the common candidate threshold
+// of its strands' bounds (U > t0), acc0 the accumulator's start value
+// 2^23 + (1023 - t0) (1 + 2^11) as f32 bits.
 struct DevMSuper {
     uint32_t tile_count;
-    uint32_t nk;        // K chunks of every tile (ceil(longest strand / 8))
+    uint32_t nk;        // the depth class: K chunks of the A fragments (2 or 4)
     uint32_t img_off;   // byte offset of the LDS image in Plan::m_image
     uint32_t img_bytes;
     int32_t t0;
     uint32_t lmin;      // shortest strand
     uint32_t tile0;     // global index of tile 0 (Plan::m_meta)
     uint32_t acc0;
+    uint32_t seg;       // depth segment ends, one byte per depth
+    uint32_t pad[3];
 };
+constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 4u; }
 
 // HAP_REF: the region's reference haplotype (the reference group's, or a
 // helper with no carriers after the region's distinct haplotypes); its
