@@ -46,7 +46,7 @@ inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint3
     if (B.counts_valid) {
         const DevHap &h = B.haps[R.hap_begin + local];
         const uint32_t n_inner = (uint32_t)R.ranges.size();
-        return B.counts[h.count_off + (uint64_t)slot * n_inner + (uint32_t)range_slot];
+        return B.counts[h.count_off + ((uint64_t)slot * n_inner + (uint32_t)range_slot) * B.regions[h.region].count_stride];
     }
     const uint64_t k = key_of(B, R, slot, range_slot);
     const uint32_t off = B.var_off[k];

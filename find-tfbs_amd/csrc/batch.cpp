@@ -435,6 +435,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         dr.hap_begin = R.hap_begin;
         dr.hap_count = R.hap_count;
         dr.ref_hap = ref >= 0 && B.dedup ? R.hap_begin + (uint32_t)ref : UINT32_MAX;
+        dr.count_stride = (uint32_t)rb.dist.size();
         R.key_off = (uint64_t)dr.inner_off * B.n_slots;
         size_t ii = o.inner;
         for (auto &r : R.ranges) {
@@ -478,8 +479,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 for (uint32_t p = 0; p < n; p++) B.posrel[pos + p] = (int32_t)(d.pos[p] - R.es);
                 pos += n;
             }
-            hm.count_off = count;
-            count += (uint64_t)B.n_slots * dr.n_inner;
+            hm.count_off = count + i;  // key-major: [key][haplotype]
             if (dr.ref_hap == o.hap + i) hm.flags |= HAP_REF;
             if (h.dedup) {
                 hm.flags |= HAP_DEDUP;

@@ -613,7 +613,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
             if (nucs[i] == 4) nmask[i / 32] |= 1u << (i % 32);
     }
     std::vector<DevHap> haps{hm};
-    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, {0, 0, 0}}};
+    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, 1, {0, 0}}};
     std::vector<int32_t> inner{0, 0}, posrel{0};
     const uint32_t wpp = (uint32_t)((n + 255) / 256 * 4);
     HIP_TRY(hipSetDevice(ctx->device));

@@ -3,7 +3,8 @@
 // count_matches_by_sample (main.rs:500-534) builds, per key (bed, inner range,
 // pattern_id), the per-sample L/R vectors; counts_as_genotypes (main.rs:439-498)
 // emits a row only when the per-sample totals differ.  The scan leaves, per
-// region, a [distinct haplotype][slot * n_inner + range] count matrix in HBM.
+// region, a [slot * n_inner + range][distinct haplotype] count matrix in HBM
+// (key-major: a key's counts are adjacent, DevRegion::count_stride apart).
 // Every sample's total is a sum of two of its rows, so a key can only produce a
 // row if its column is not constant.  key_reduce_kernel classifies every column
 // (any count != 0 -> the key exists in the reference's HashMap; counts differ ->
@@ -21,8 +22,9 @@ namespace {
 
 constexpr int kReduceBlock = 256;
 
-// One workgroup per region; threads stride over the region's key columns and
-// walk the distinct-haplotype rows (coalesced across the columns).
+// One workgroup per region, one wave per key column at a time: the key's
+// counts of every distinct haplotype are adjacent (key-major layout, DevRegion),
+// lanes read them coalesced and the wave reduces "any" and "differs".
 __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *__restrict__ haps,
                                                                    const DevRegion *__restrict__ regions,
                                                                    const uint32_t *__restrict__ counts,
@@ -31,6 +33,7 @@ __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *
     const DevRegion rg = regions[blockIdx.x];
     const uint32_t K = n_slots * rg.n_inner;
     const uint64_t ko = (uint64_t)rg.inner_off * n_slots;
+    const uint32_t lane = threadIdx.x & 63;
     if (rg.hap_count == 0) {  // no samples: no haplotype, no match, no key
         for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
             first[ko + j] = 0;
@@ -39,16 +42,20 @@ __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *
         return;
     }
     const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
-        const uint32_t c0 = counts[base + j];
-        uint32_t any = c0, diff = 0;
-        for (uint32_t l = 1; l < rg.hap_count; l++) {
-            const uint32_t c = counts[base + (uint64_t)l * K + j];
+    for (uint32_t j = threadIdx.x >> 6; j < K; j += kReduceBlock / 64) {
+        const uint32_t *col = counts + base + (uint64_t)j * rg.count_stride;
+        const uint32_t c0 = col[0];
+        uint32_t any = 0, diff = 0;
+        for (uint32_t l = lane; l < rg.hap_count; l += 64) {
+            const uint32_t c = col[l];
             any |= c;
             diff |= c ^ c0;
         }
-        first[ko + j] = c0;
-        flags[ko + j] = (uint8_t)((any ? KEY_ANY : 0) | (diff ? KEY_VARIES : 0));
+        const bool a = __ballot(any != 0) != 0, d = __ballot(diff != 0) != 0;
+        if (lane == 0) {
+            first[ko + j] = c0;
+            flags[ko + j] = (uint8_t)((a ? KEY_ANY : 0) | (d ? KEY_VARIES : 0));
+        }
     }
 }
 
@@ -62,9 +69,9 @@ __global__ __launch_bounds__(256) void key_gather_kernel(const DevHap *__restric
     if (k >= n_keys) return;
     const DevVarKey vk = keys[k];
     const DevRegion rg = regions[vk.region];
-    const uint32_t K = n_slots * rg.n_inner;
     const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t l = threadIdx.x & 63; l < rg.hap_count; l += 64) out[vk.out_off + l] = counts[base + (uint64_t)l * K + vk.j];
+    const uint32_t *col = counts + base + (uint64_t)vk.j * rg.count_stride;
+    for (uint32_t l = threadIdx.x & 63; l < rg.hap_count; l += 64) out[vk.out_off + l] = col[l];
 }
 
 // counts_as_genotypes' per-sample half (main.rs:439-498) for one varying key:
@@ -95,9 +102,9 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__r
     const uint32_t k = blockIdx.x;
     const DevVarKey vk = keys[k];
     const DevRegion rg = regions[vk.region];
-    const uint32_t K = n_slots * rg.n_inner;
     const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t l = threadIdx.x; l < rg.hap_count; l += kEncBlock) s_c[l] = counts[base + (uint64_t)l * K + vk.j];
+    for (uint32_t l = threadIdx.x; l < rg.hap_count; l += kEncBlock)
+        s_c[l] = counts[base + (uint64_t)vk.j * rg.count_stride + l];
     __syncthreads();
     const uint16_t *m = reinterpret_cast<const uint16_t *>(memb + (size_t)(vk.region - region0) * 2 * n_samples);
     auto total = [&](uint32_t s) {

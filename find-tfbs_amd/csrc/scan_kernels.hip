@@ -278,10 +278,11 @@ __global__ __launch_bounds__(512, MINW) void scan_fast_kernel(ScanArgs A) {
                     scan_chunks<1>(A, t, s_lut, s_units, hm, h, cg, inner, n_pass, write_hits, lane, acc);
             }
             if (n_pass && lane < t.nslots) {
-                uint32_t *out = A.counts + hm.count_off + (size_t)(t.slot_begin + lane) * n_inner + k0;
+                const size_t st = rg.count_stride;
+                uint32_t *out = A.counts + hm.count_off + ((size_t)(t.slot_begin + lane) * n_inner + k0) * st;
 #pragma unroll
                 for (int kk = 0; kk < kMaxInnerPass; kk++)
-                    if ((uint32_t)kk < n_pass) out[kk] = acc[kk];
+                    if ((uint32_t)kk < n_pass) out[kk * st] = acc[kk];
             }
         }
     }
@@ -354,9 +355,10 @@ __global__ __launch_bounds__(kGenBlock) void scan_generic_kernel(ScanArgs A) {
                 }
             }
             if (n_pass && lane == 0) {
-                uint32_t *out = A.counts + hm.count_off + (size_t)t.slot_begin * n_inner + k0;
+                const size_t st = rg.count_stride;
+                uint32_t *out = A.counts + hm.count_off + ((size_t)t.slot_begin * n_inner + k0) * st;
                 for (int kk = 0; kk < kMaxInnerPass; kk++)
-                    if ((uint32_t)kk < n_pass) out[kk] = acc[kk];
+                    if ((uint32_t)kk < n_pass) out[kk * st] = acc[kk];
             }
         }
     }

@@ -239,7 +239,7 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
         const int32_t s = inner[2 * k], en = inner[2 * k + 1];
         const uint32_t span = (uint32_t)(en - s);
         if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-            atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
+            atomicAdd(A.counts + hp.count_off + (size_t)(off0 + k) * rg.count_stride, 1u);
     }
     if (A.hits && i / 64 < A.hits_wpp)
         atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + sn]) * A.hits_wpp + i / 64,
@@ -632,7 +632,9 @@ __global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
             if ((hp.dirty[s_nk[t] - 1] >> (s_i[t] / kMWindows)) & 1u) continue;  // scanned
             // no-return atomics: issued back to back (a plain add would wait on
             // every load, as the adds may alias)
-            for (uint32_t m = s_mask[t]; m; m &= m - 1) atomicAdd(A.counts + hp.count_off + s_off[t] + __builtin_ctz(m), 1u);
+            // lanes are consecutive haplotypes: one key's counts are adjacent
+            for (uint32_t m = s_mask[t]; m; m &= m - 1)
+                atomicAdd(A.counts + hp.count_off + (size_t)(s_off[t] + __builtin_ctz(m)) * rg.count_stride, 1u);
         }
     }
     // inner ranges past 32 (rare): atomics, as the overflow list
@@ -650,7 +652,7 @@ __global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
                     const int32_t s = inner[2 * k], en = inner[2 * k + 1];
                     const uint32_t span = (uint32_t)(en - s);
                     if ((uint32_t)((int32_t)i - s) <= span || (uint32_t)((int32_t)(i + L) - 1 - s) <= span)
-                        atomicAdd(A.counts + hp.count_off + s_off[t] + k, 1u);
+                        atomicAdd(A.counts + hp.count_off + (size_t)(s_off[t] + k) * rg.count_stride, 1u);
                 }
             }
         }
@@ -678,7 +680,7 @@ __global__ __launch_bounds__(256) void ref_fixup_over_kernel(ScanArgs A) {
                 const int32_t s = inner[2 * k], en = inner[2 * k + 1];
                 const uint32_t span = (uint32_t)(en - s);
                 if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-                    atomicAdd(A.counts + hp.count_off + off0 + k, 1u);
+                    atomicAdd(A.counts + hp.count_off + (size_t)(off0 + k) * rg.count_stride, 1u);
             }
         }
     }

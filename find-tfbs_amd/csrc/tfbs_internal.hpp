@@ -149,7 +149,7 @@ struct DevHap {
     uint32_t flags;      // HapFlags
     uint32_t nmask_off;  // u32 words of the N mask (bit i = base i is N), if HAP_HAS_N
     uint32_t pos_off;    // int32 positions relative to ext_start, if HAP_HAS_POS
-    uint64_t count_off;  // counts[count_off + slot * n_inner + k]
+    uint64_t count_off;  // counts[count_off + (slot * n_inner + k) * DevRegion::count_stride]
     uint32_t dirty[4];   // HAP_DEDUP: per K depth, bit t = window tile t (windows 32 t ..) holds a differing base
 };
 
@@ -159,7 +159,11 @@ struct DevRegion {
     uint32_t hap_begin;  // first distinct haplotype (their count blocks are consecutive)
     uint32_t hap_count;  // distinct haplotypes (a helper reference haplotype follows them)
     uint32_t ref_hap;    // the HAP_REF haplotype, UINT32_MAX if none
-    uint32_t pad[3];
+    // the region's counts are [key = slot * n_inner + range][haplotype]: a key's
+    // counts for every haplotype of the region (the helper's included) are
+    // consecutive, count_stride apart from the next key's
+    uint32_t count_stride;
+    uint32_t pad[2];
 };
 
 // Per-sample encoding of one varying key (tfbs_batch_encode, key_encode_kernel):
