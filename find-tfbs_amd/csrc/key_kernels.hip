@@ -22,9 +22,10 @@ namespace {
 
 constexpr int kReduceBlock = 256;
 
-// One workgroup per region, one wave per key column at a time: the key's
-// counts of every distinct haplotype are adjacent (key-major layout, DevRegion),
-// lanes read them coalesced and the wave reduces "any" and "differs".
+// One workgroup per region, one thread per key: the key's counts of every
+// distinct haplotype are adjacent (key-major layout, DevRegion), read in order
+// (unrolled: several loads in flight per lane; each cache line serves 32
+// iterations).
 __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *__restrict__ haps,
                                                                    const DevRegion *__restrict__ regions,
                                                                    const uint32_t *__restrict__ counts,
@@ -33,7 +34,6 @@ __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *
     const DevRegion rg = regions[blockIdx.x];
     const uint32_t K = n_slots * rg.n_inner;
     const uint64_t ko = (uint64_t)rg.inner_off * n_slots;
-    const uint32_t lane = threadIdx.x & 63;
     if (rg.hap_count == 0) {  // no samples: no haplotype, no match, no key
         for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
             first[ko + j] = 0;
@@ -42,20 +42,18 @@ __global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *
         return;
     }
     const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t j = threadIdx.x >> 6; j < K; j += kReduceBlock / 64) {
+    for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
         const uint32_t *col = counts + base + (uint64_t)j * rg.count_stride;
         const uint32_t c0 = col[0];
-        uint32_t any = 0, diff = 0;
-        for (uint32_t l = lane; l < rg.hap_count; l += 64) {
+        uint32_t any = c0, diff = 0;
+#pragma unroll 8
+        for (uint32_t l = 1; l < rg.hap_count; l++) {
             const uint32_t c = col[l];
             any |= c;
             diff |= c ^ c0;
         }
-        const bool a = __ballot(any != 0) != 0, d = __ballot(diff != 0) != 0;
-        if (lane == 0) {
-            first[ko + j] = c0;
-            flags[ko + j] = (uint8_t)((a ? KEY_ANY : 0) | (d ? KEY_VARIES : 0));
-        }
+        first[ko + j] = c0;
+        flags[ko + j] = (uint8_t)((any ? KEY_ANY : 0) | (diff ? KEY_VARIES : 0));
     }
 }
 
