@@ -451,6 +451,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         }
         B.regions[region0 + j] = dr;
         uint64_t word = o.word, nmask = o.nmask, pos = o.pos, count = o.count;
+        // per-region sums in registers (the arrays are shared by the threads)
+        uint64_t r_win = 0, r_eff = 0, r_cells = 0, r_swin = 0, r_scells = 0;
         for (uint32_t i = 0; i < rb.dist.size(); i++) {
             const Distinct &d = rb.dist[i];
             const HapInfo &h = info[j][i];
@@ -495,19 +497,24 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                     uint64_t sw = nw;  // windows the scan reads
                     if (h.dedup && lc.first <= (uint32_t)(kMMaxChunks * kMChunkCols)) {
                         const uint32_t m = h.dirty[(lc.first + kMChunkCols - 1) / kMChunkCols - 1];
-                        sw = 0;
-                        for (uint32_t t = 0; t < kDedupMaxTiles; t++)
-                            if ((m >> t) & 1u) sw += std::min<uint64_t>(kMWindows, nw > t * kMWindows ? nw - t * kMWindows : 0);
+                        const uint64_t full = nw / kMWindows, rem = nw % kMWindows;  // whole tiles, then a partial one
+                        const uint32_t fm = full >= 32 ? ~0u : (1u << full) - 1;
+                        sw = (uint64_t)kMWindows * __builtin_popcount(m & fm) + (full < 32 && ((m >> full) & 1u) ? rem : 0);
                     }
-                    swin[j] += sw * lc.second;
-                    scells[j] += sw * lc.first * lc.second;
+                    r_swin += sw * lc.second;
+                    r_scells += sw * lc.first * lc.second;
                     if (helper) continue;
                     wn += nw * lc.second;
-                    cells[j] += nw * lc.first * lc.second;
+                    r_cells += nw * lc.first * lc.second;
                 }
-            win[j] += wn;
-            eff[j] += wn * rb.carriers[i];
+            r_win += wn;
+            r_eff += wn * rb.carriers[i];
         }
+        win[j] = r_win;
+        eff[j] = r_eff;
+        cells[j] = r_cells;
+        swin[j] = r_swin;
+        scells[j] = r_scells;
     });
     for (size_t j = 0; j < nr; j++) {
         B.windows += win[j];
