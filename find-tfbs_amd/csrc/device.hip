@@ -167,7 +167,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         // one candidate region per scan workgroup (super tile x haplotype group)
         const uint64_t n_regions = (uint64_t)P.m_supers.size() * ((n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb);
         int rc;
-        if ((rc = ctx->cands.ensure(n_regions * ctx->cand_cap * 3))) return rc;
+        if ((rc = ctx->cands.ensure(n_regions * ctx->cand_cap * kCandWords))) return rc;
         m.cands = ctx->cands.p;
         m.cand_cap = ctx->cand_cap;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);

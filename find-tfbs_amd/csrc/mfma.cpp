@@ -202,6 +202,9 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         // zero columns up to a multiple of 8: the rescoring loop reads whole blocks
         plan->m_weights.resize(plan->m_weights.size() + 4 * ((8 - p.len % 8) % 8), 0);
     }
+    // the rescoring loads every block of 8 columns up to 32 (masked): the last
+    // strand's reads stay in the buffer
+    plan->m_weights.resize(plan->m_weights.size() + 4 * 32, 0);
 
     struct TileSrc { size_t first, count; uint32_t nk, lmin; };
     std::vector<TileSrc> tiles;
@@ -274,15 +277,15 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
                     const auto &st = strands[t.first + n];
                     const Pat &p = P.pats[st.first];
                     split[n] = split_for(p, t0);
-                    gm[kGMin + n] = p.min_score;
-                    gm[kGWoff + n] = (int32_t)woff[t.first + n];
-                    gm[kGLen + n] = (int32_t)p.len;
-                    gm[kGSlot + n] = (int32_t)st.second;
+                    gm[kGStrandInts * n + kGMin] = p.min_score;
+                    gm[kGStrandInts * n + kGWoff] = (int32_t)woff[t.first + n];
+                    gm[kGStrandInts * n + kGLen] = (int32_t)p.len;
+                    gm[kGStrandInts * n + kGSlot] = (int32_t)st.second;
                     gm[kGOrig + n] = st.first;
                     plan->n_mfma_strands++;
                 } else {  // padding strand: never a hit (L = 0 scores 0, not > INT32_MAX)
                     split[n].never = true;
-                    gm[kGMin + n] = INT32_MAX;
+                    gm[kGStrandInts * n + kGMin] = INT32_MAX;
                     gm[kGOrig + n] = -1;
                 }
             }

@@ -36,11 +36,11 @@ struct ScanArgs {
     unsigned long long *hits;   // debug (tfbs_matches): per (hap, pattern, 64-window chunk) hit masks
     uint32_t hits_wpp;
     uint32_t n_patterns_total;
-    // matrix-core candidates (scan_mfma.hip): one region of cand_cap (haplotype,
-    // strand, window) triples per scan workgroup (region region_base +
-    // blockIdx.x), filled through an LDS counter and rescored by the workgroup
-    // at its end
-    uint32_t *cands;
+    // matrix-core candidates (scan_mfma.hip): one region of cand_cap (strand |
+    // haplotype in the group << 24, window) pairs per scan workgroup (region
+    // region_base + blockIdx.x), an equal share per wave, each wave's filled and
+    // rescored by the wave
+    uint32_t *cands;  // kCandWords per entry
     uint32_t cand_cap;
     uint32_t region_base;
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
@@ -58,6 +58,7 @@ struct ScanArgs {
     uint32_t ref_over_cap;
 };
 constexpr uint32_t kRefPerRegion = 64;
+constexpr uint32_t kCandWords = 2;  // candidate list entry: strand | haplotype in the group << 24, window
 
 struct LaunchConfig {
     int minw = 2;               // __launch_bounds__ min waves per SIMD of the fast kernel

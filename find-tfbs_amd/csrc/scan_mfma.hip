@@ -47,8 +47,8 @@ namespace {
 // Bottleneck probes (tools/probe_build.sh, never in the product build):
 // TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live; timing only),
 // =4 counts tile tests, firing tiles, queued lanes, exact hits and rejected
-// candidates (printed per launch), =12 never drains the queue (results wrong;
-// timing only).
+// candidates (printed per launch), =12 never drains the queue, =13 drains it
+// but never rescores (results wrong; timing only).
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
@@ -180,7 +180,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue][2];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
-__shared__ uint32_t s_cn;  // candidates the workgroup appended
+__shared__ uint32_t s_hnext;  // the workgroup's next haplotype (scan_super)
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 #if TFBS_MFMA_PROBE == 4
@@ -188,54 +188,80 @@ __device__ unsigned long long g_probe[5];
 #endif
 
 // Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
-// whole blocks of 8 columns (the weights are zero-padded to them), one load per
-// column, N columns masked out.
-__device__ __forceinline__ int32_t exact_score(const ScanArgs &A, const uint32_t *words, const DevHap &hp, uint32_t i,
-                                               uint32_t L, uint32_t woff) {
+// one load per column, N columns masked out.  ALL: every block of 8 columns up
+// to 32 issued before the first is summed (the weights are zero-padded to whole
+// blocks, the buffer's tail pad keeps the masked blocks' reads inside it; used
+// where no accumulator is live), else block by block (fewer registers).
+template <bool ALL>
+__device__ __forceinline__ int32_t exact_score(const uint32_t *words, const DevHap &hp, uint32_t i, uint32_t L,
+                                               const int32_t *wt, uint32_t live) {
     const uint32_t *w = words + hp.word_off + (i >> 4);
     const uint32_t sh = 2 * (i & 15);
     const uint32_t img[2] = {__builtin_amdgcn_alignbit(w[1], w[0], sh), __builtin_amdgcn_alignbit(w[2], w[1], sh)};
-    uint32_t live = 0xFFFFFFFFu;  // bit j: base i + j is not N
-    if (hp.flags & HAP_HAS_N) {
-        const uint32_t *m = A.nmask + hp.nmask_off + (i >> 5);
-        live = ~__builtin_amdgcn_alignbit(m[1], m[0], i & 31);
-    }
-    const int32_t *wt = A.mweights + woff;
+    const uint32_t keep = live & (L >= 32 ? ~0u : (1u << L) - 1);  // columns < L that are not N
     int32_t s = 0;
+    if (ALL) {
+        int32_t v[32];
+#pragma unroll
+        for (uint32_t j = 0; j < 32; j++) v[j] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
+#pragma unroll
+        for (uint32_t j = 0; j < 32; j++) s += v[j] & -(int32_t)((keep >> j) & 1u);  // N scores 0
+    } else {
 #pragma unroll 1
-    for (uint32_t jb = 0; jb < L; jb += 8) {
-        int32_t v[8];
+        for (uint32_t jb = 0; jb < L; jb += 8) {
+            int32_t v[8];
 #pragma unroll
-        for (uint32_t u = 0; u < 8; u++) {
-            const uint32_t j = jb + u;
-            v[u] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = jb + u;
+                v[u] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) s += v[u] & -(int32_t)((keep >> (jb + u)) & 1u);
         }
-#pragma unroll
-        for (uint32_t u = 0; u < 8; u++) s += v[u] & -(int32_t)((live >> (jb + u)) & 1u);  // N scores 0
     }
     return s;
 }
 
 // Exact rescoring of one candidate: window i of haplotype hp (hits index hap)
 // for the strand g = global tile * 64 + strand in tile; a hit adds to its
-// slot's count for every inner range it overlaps.
+// slot's count for every inner range it overlaps.  The loads are issued in
+// three dependent rounds (strand fields | weights, region, position, N mask |
+// inner ranges) before the atomics.
+template <bool ALL = true>
 __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_t *words, const DevHap &hp,
                                                 uint32_t hap, uint32_t g, uint32_t i) {
     const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
     const uint32_t sn = g & 63u;
-    const uint32_t L = (uint32_t)meta[kGLen + sn];
-    if (i + L > hp.len) return;                         // past the end (pattern.rs:147-150)
-    const int32_t sc = exact_score(A, words, hp, i, L, (uint32_t)meta[kGWoff + sn]);
-    const int32_t mn = meta[kGMin + sn];
-#if TFBS_MFMA_PROBE == 4
-    atomicAdd(&g_probe[sc > mn ? 1 : 2], 1ull);
-#endif
-    if (!(sc > mn)) return;                             // strict (pattern.rs:151)
+    const int4 sf = *reinterpret_cast<const int4 *>(meta + kGStrandInts * sn);  // min, woff, len, slot
     const DevRegion rg = A.regions[hp.region];
-    const uint32_t off0 = (uint32_t)meta[kGSlot + sn] * rg.n_inner;
+    const uint32_t ic = min(i, hp.len - 1);  // i + L > len: no hit (below), reads stay in range
+    const int32_t p = (hp.flags & HAP_HAS_POS) ? A.posrel[hp.pos_off + ic] : (int32_t)i;
+    uint32_t live = 0xFFFFFFFFu;  // bit j: base i + j is not N
+    if (hp.flags & HAP_HAS_N) {
+        const uint32_t *m = A.nmask + hp.nmask_off + (ic >> 5);
+        live = ~__builtin_amdgcn_alignbit(m[1], m[0], ic & 31);
+    }
+    const uint32_t L = (uint32_t)sf.z;
+    if (i + L > hp.len) return;                         // past the end (pattern.rs:147-150)
+    const int32_t sc = exact_score<ALL>(words, hp, i, L, A.mweights + sf.y, live);
+#if TFBS_MFMA_PROBE == 4
+    atomicAdd(&g_probe[sc > sf.x ? 1 : 2], 1ull);
+#endif
+    if (!(sc > sf.x)) return;                           // strict (pattern.rs:151)
+    const uint32_t off0 = (uint32_t)sf.w * rg.n_inner;
     const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-    const int32_t p = (hp.flags & HAP_HAS_POS) ? A.posrel[hp.pos_off + i] : (int32_t)i;
-    for (uint32_t k = 0; k < rg.n_inner; k++) {         // range.rs:18-21 as main.rs:503 uses it
+    // range.rs:18-21 as main.rs:503 uses it: every range's bounds loaded before
+    // the first atomic (which the loads could alias)
+    uint32_t mask = 0;
+    const uint32_t nk = min(rg.n_inner, 32u);
+    for (uint32_t k = 0; k < nk; k++) {
+        const int2 r = *reinterpret_cast<const int2 *>(inner + 2 * k);
+        const uint32_t span = (uint32_t)(r.y - r.x);
+        if ((uint32_t)(p - r.x) <= span || (uint32_t)(p + (int32_t)L - 1 - r.x) <= span) mask |= 1u << k;
+    }
+    for (; mask; mask &= mask - 1)
+        atomicAdd(A.counts + hp.count_off + (size_t)(off0 + __builtin_ctz(mask)) * rg.count_stride, 1u);
+    for (uint32_t k = 32; k < rg.n_inner; k++) {        // ranges past 32 (rare)
         const int32_t s = inner[2 * k], en = inner[2 * k + 1];
         const uint32_t span = (uint32_t)(en - s);
         if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
@@ -260,69 +286,79 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
     }
 }
 
-// Drains the wave's first n queue entries, one entry per lane per round: the
-// candidate bits of both strands of the entry's column are decoded and each
-// candidate (haplotype, strand, window) is appended to the workgroup's region
-// of the candidate list (slots from an LDS counter), one candidate per lane per
-// pass.  A full region (pathological thresholds)
-// rescores here instead.
+// Drains the wave's first n queue entries, one entry per lane per pass: the
+// candidate bits of both strands of the entry's column are gathered into one
+// mask and each candidate (haplotype, strand, window) is appended to the
+// wave's region of the candidate list (2 dwords: global strand | haplotype in
+// the group << 24, window), one candidate per lane per round; the wave rescores
+// its list when it has scanned (rescore_list).  A full region (pathological
+// thresholds) rescores here instead.
 // h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
+__device__ __forceinline__ uint32_t wave_cand_cap(const ScanArgs &A) { return A.cand_cap / (kMBlock / 64); }
+__device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
+    return reinterpret_cast<uint2 *>(A.cands) + (size_t)(A.region_base + blockIdx.x) * A.cand_cap +
+           (size_t)wave * wave_cand_cap(A);
+}
+
 __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
-                                            uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane) {
+                                            uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane, uint32_t &cn) {
 #if TFBS_MFMA_PROBE == 12
     return;  // timing only: queued candidates are dropped
 #endif
-    uint32_t *list = A.cands + (size_t)(A.region_base + blockIdx.x) * A.cand_cap * 3;
+    uint2 *list = cand_list(A, wave);
+    const uint32_t cap = wave_cand_cap(A);
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
         const uint32_t e = e0 + lane;
-        uint32_t m0 = 0, m1 = 0, src = 0, ti = 0, hl = 0, i0 = 0;
+        uint32_t m = 0, g0 = 0, i0 = 0, hl = 0;
         if (e < n) {
             const uint4 d0 = s_qdata[wave][e][0], d1 = s_qdata[wave][e][1];
             const uint64_t q = s_qmeta[wave][e];
-            src = (uint32_t)q & 63u;
-            ti = ((uint32_t)q >> 6) & 63u;
+            const uint32_t src = (uint32_t)q & 63u, ti = ((uint32_t)q >> 6) & 63u;
             hl = ((uint32_t)q >> 12) & 255u;
-            i0 = (uint32_t)(q >> 32) << 5;
-            // dword k: outputs 2k, 2k+1: the first field's top bit at 2, 10, the
-            // second's at 21, 29 (queue_tile)
+            i0 = ((uint32_t)(q >> 32) << 5) + 4 * (src >> 5);
+            g0 = (tile0 + ti) * kMStrands + 2 * (src & 31u);
+            // dword k (queue_tile): outputs 2k, 2k+1, the first strand's top bits
+            // at 2, 10, the second's at 21, 29.  lo collects bits 2 + k, 10 + k,
+            // hi 5 + k, 13 + k; m bit b: strand b >> 4, output 2 (b & 7) + (b >> 3 & 1)
             const uint32_t dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+            uint32_t lo = 0, hi = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
-                m0 |= ((dd[k] >> 2) & 1u) << (2 * k) | ((dd[k] >> 10) & 1u) << (2 * k + 1);
-                m1 |= ((dd[k] >> 21) & 1u) << (2 * k) | ((dd[k] >> 29) & 1u) << (2 * k + 1);
+                lo |= (dd[k] << k) & (0x0404u << k);
+                hi |= (dd[k] >> (16 - k)) & (0x2020u << k);
             }
+            m = (lo >> 2) | (hi << 11);
         }
-        for (;;) {
-            const bool has = (m0 | m1) != 0;
-            const uint64_t act = __ballot(has);
-            if (act == 0) break;
-            uint32_t r = 0, sn = 2 * (src & 31u);
-            if (m0) {
-                r = __builtin_ctz(m0);
-                m0 &= m0 - 1;
-            } else if (m1) {
-                r = __builtin_ctz(m1);
-                m1 &= m1 - 1;
-                sn += 1;
+        uint64_t act;
+        while ((act = __ballot(m != 0)) != 0) {
+            if (m) {
+                const uint32_t b = __builtin_ctz(m);
+                m &= m - 1;
+                const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
+                const uint32_t r = 2 * (b & 7u) + ((b >> 3) & 1u);
+                const uint32_t i = i0 + (r & 3) + 8 * (r >> 2), g = g0 + (b >> 4);
+                if (slot < cap) list[slot] = make_uint2(g | (hl << 24), i);
+                else score_candidate<false>(A, words, A.haps[h0 + hl], h0 + hl, g, i);
             }
-            const uint32_t first = (uint32_t)__builtin_ctzll(act);
-            uint32_t base = 0;
-            if (lane == first) base = atomicAdd(&s_cn, (uint32_t)__popcll(act));
-            base = __builtin_amdgcn_readlane(base, first);
-            if (has) {
-                const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-                const uint32_t i = i0 + (r & 3) + 8 * (r >> 2) + 4 * (src >> 5);
-                const uint32_t g = (tile0 + ti) * kMStrands + sn;
-                if (slot < A.cand_cap) {
-                    list[3 * (size_t)slot] = h0 + hl;
-                    list[3 * (size_t)slot + 1] = g;
-                    list[3 * (size_t)slot + 2] = i;
-                } else {
-                    score_candidate(A, words, A.haps[h0 + hl], h0 + hl, g, i);
-                }
-            }
+            cn += (uint32_t)__popcll(act);
         }
+    }
+}
+
+// The wave's listed candidates, one per lane (after its scan: no accumulator
+// is live, and the other waves keep the matrix cores busy).
+__device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *words, uint32_t h0, uint32_t wave,
+                                             uint32_t lane, uint32_t cn) {
+#if TFBS_MFMA_PROBE == 13
+    return;  // timing only: listed candidates are dropped
+#endif
+    const uint32_t n = min(cn, wave_cand_cap(A));
+    const uint2 *list = cand_list(A, wave);
+    for (uint32_t k = lane; k < n; k += 64) {
+        const uint2 c = list[k];
+        const uint32_t hap = h0 + (c.x >> 24);
+        score_candidate(A, words, A.haps[hap], hap, c.x & 0xFFFFFFu, c.y);
     }
 }
 
@@ -403,9 +439,9 @@ __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, con
 template <int D, int NK>
 __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
                                              const uint32_t *words, uint32_t tile0, uint32_t h0, uint32_t lane,
-                                             uint32_t wave, uint32_t hh, const v4i (&a0)[NK], const v4i (&a1)[NK],
-                                             bool two, uint32_t i0a, uint32_t i0b, const v16f &cb, int sa,
-                                             uint32_t &qn) {
+                                             uint32_t wave, const v4i (&a0)[NK], const v4i (&a1)[NK], bool two,
+                                             uint32_t ha, uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb,
+                                             int sa, uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
     if (two) {
         for (uint32_t ti = tb; ti < te; ti++) {
@@ -420,22 +456,22 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             // accumulator is live across a drain)
             if (f0) {
                 if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                    drain_queue(A, words, tile0, h0, qn, wave, lane);
+                    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x0 = coarse_test(c0);
                     x1 = coarse_test(c1);
                 }
-                queue_tile(c0, x0, f0, ti, hh, i0a, lane, wave, qn);
+                queue_tile(c0, x0, f0, ti, ha, i0a, lane, wave, qn);
             }
             if (f1) {
                 if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                    drain_queue(A, words, tile0, h0, qn, wave, lane);
+                    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x1 = coarse_test(c1);
                 }
-                queue_tile(c1, x1, f1, ti, hh, i0b, lane, wave, qn);
+                queue_tile(c1, x1, f1, ti, hb, i0b, lane, wave, qn);
             }
         }
     } else {
@@ -447,31 +483,33 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             const uint64_t f0 = __ballot(x0 != 0);
             if (__builtin_expect(f0 == 0, 1)) continue;
             if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                drain_queue(A, words, tile0, h0, qn, wave, lane);
+                drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
                 qn = 0;
                 tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
                 x0 = coarse_test(c0);
             }
-            queue_tile(c0, x0, f0, ti, hh, i0a, lane, wave, qn);
+            queue_tile(c0, x0, f0, ti, ha, i0a, lane, wave, qn);
         }
     }
 }
 
 // One step: every strand tile of the super tile (depth segments 1..NK, byte
-// d - 1 of seg = the end of depth d) x the window tiles at i0a / i0b.
+// d - 1 of seg = the end of depth d) x the window tiles at i0a of haplotype
+// ha (in the workgroup's group) and, if two, at i0b of hb.
 template <int NK>
 __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const uint32_t *words,
-                                          uint32_t tile0, uint32_t h0, uint32_t lane, uint32_t wave, uint32_t hh,
-                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t i0a,
-                                          uint32_t i0b, const v16f &cb, int sa, uint32_t &qn) {
+                                          uint32_t tile0, uint32_t h0, uint32_t lane, uint32_t wave,
+                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t ha,
+                                          uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb, int sa,
+                                          uint32_t &qn, uint32_t &cn) {
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
 #define TFBS_SEGMENT(D)                                                                                          \
     if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
         const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \
         if (te > tb)                                                                                             \
-            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, words, tile0, h0, lane, wave, hh, a0, a1, two, \
-                                                 i0a, i0b, cb, sa, qn);                                          \
+            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, words, tile0, h0, lane, wave, a0, a1, two, ha, \
+                                                 i0a, hb, i0b, cb, sa, qn, cn);                                  \
         img += (te - tb) * mfma_tile_bytes(D);                                                                   \
         tb = te;                                                                                                 \
     }
@@ -487,7 +525,6 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
 template <int NK>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
-    constexpr uint32_t kWaves = kMBlock / 64;
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t tile0 = S.tile0;
     const float a0f = __uint_as_float(S.acc0);
@@ -495,17 +532,26 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
     const int sa = lane < 32 ? kScaleA0 : kScaleA1;
     const char *tab = s_img - kMOnehotBytes;
-    uint32_t qn = 0;
-    for (uint32_t hh = wave; hh < A.haps_per_block; hh += kWaves) {
+    uint32_t qn = 0, cn = 0;  // the wave's queued entries, listed candidates
+    // window tiles two at a time (each B fragment read from LDS feeds two
+    // MFMAs), pairs formed across the wave's haplotypes: a tile waits in a0
+    // (haplotype pa, window pi0) for the next one
+    v4i a0[NK], a1[NK];
+    bool pending = false;
+    uint32_t pa = 0, pi0 = 0;
+    // haplotypes taken one at a time from the workgroup's counter: the waves
+    // finish together however the dirty tiles of reused haplotypes fall
+    for (;;) {
+        uint32_t hh = 0;
+        if (lane == 0) hh = atomicAdd(&s_hnext, 1u);
+        hh = __builtin_amdgcn_readfirstlane(hh);
         const uint32_t hap = h0 + hh;
-        if (hap >= A.n_haps) break;
+        if (hh >= A.haps_per_block || hap >= A.n_haps) break;
         const DevHap hm = load_hap(A.haps + hap);
         if (hm.len < S.lmin) continue;
         const uint32_t nwin = hm.len - S.lmin + 1;
-        // window tiles two at a time (each B fragment read from LDS feeds two
-        // MFMAs), 32 tiles per mask; a HAP_DEDUP haplotype only the tiles holding
-        // a base that differs from the reference (the others are
-        // ref_fixup_kernel's)
+        // 32 tiles per mask; a HAP_DEDUP haplotype only the tiles holding a
+        // base that differs from the reference (the others are ref_fixup_kernel's)
         const uint32_t ntiles = (nwin + kMWindows - 1) / kMWindows;
         const bool dedup = (hm.flags & HAP_DEDUP) && A.dedup;  // then ntiles <= 32
         for (uint32_t base = 0; base < ntiles; base += 32) {
@@ -513,23 +559,27 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
             uint32_t m = nb >= 32 ? ~0u : (1u << nb) - 1;
             if (dedup) m &= hm.dirty[NK - 1];
             while (m) {
-                const uint32_t i0a = kMWindows * (base + __builtin_ctz(m));
+                const uint32_t i0 = kMWindows * (base + __builtin_ctz(m));
                 m &= m - 1;
-                const bool two = m != 0;
-                const uint32_t i0b = two ? kMWindows * (base + __builtin_ctz(m)) : i0a;
-                if (two) m &= m - 1;
-                WinWords wa, wb;
-                v4i a0[NK], a1[NK];
-                load_window(A, words, hm, i0a, lane, wa);
-                if (two) load_window(A, words, hm, i0b, lane, wb);
-                build_onehot<NK>(hm, i0a, lane, wa, tab, a0);
-                if (two) build_onehot<NK>(hm, i0b, lane, wb, tab, a1);
+                WinWords ww;
+                load_window(A, words, hm, i0, lane, ww);
+                if (!pending) {
+                    build_onehot<NK>(hm, i0, lane, ww, tab, a0);
+                    pa = hh;
+                    pi0 = i0;
+                    pending = true;
+                    continue;
+                }
+                build_onehot<NK>(hm, i0, lane, ww, tab, a1);
                 // the other waves of the SIMD hide the latencies
-                scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, hh, a0, a1, two, i0a, i0b, cb, sa, qn);
+                scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, a0, a1, true, pa, pi0, hh, i0, cb, sa, qn, cn);
+                pending = false;
             }
         }
     }
-    drain_queue(A, words, tile0, h0, qn, wave, lane);  // the wave's last entries
+    if (pending) scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, a0, a1, false, pa, pi0, pa, pi0, cb, sa, qn, cn);
+    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);  // the wave's last entries
+    rescore_list(A, words, h0, wave, lane, cn);
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD (two workgroups per CU).
@@ -548,7 +598,7 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
         // one-hot table: 4-mer code -> 64 bits, column t (16 bits) holds FP4
         // 1.0 (0x2) in the nibble of its base
         uint2 *tab = reinterpret_cast<uint2 *>(smem);
-        if (threadIdx.x == 0) s_cn = 0;
+        if (threadIdx.x == 0) s_hnext = 0;
         for (uint32_t k = threadIdx.x; k < 256; k += kMBlock) {
             uint32_t h[4];
             for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
@@ -570,15 +620,6 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     // the wave index is uniform: keep every haplotype-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
-    // the workgroup's candidates, one per thread: they overlap the MFMA work of
-    // the other workgroups on the CU
-    __syncthreads();
-    const uint32_t n = min(s_cn, A.cand_cap);
-    const uint32_t *list = A.cands + (size_t)(A.region_base + blockIdx.x) * A.cand_cap * 3;
-    for (uint32_t k = threadIdx.x; k < n; k += kMBlock) {
-        const uint32_t hap = list[3 * (size_t)k], g = list[3 * (size_t)k + 1], i = list[3 * (size_t)k + 2];
-        score_candidate(A, words, A.haps[hap], hap, g, i);
-    }
 }
 
 // Reference-window reuse.  A HAP_DEDUP haplotype whose window tile of a
@@ -589,9 +630,9 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
 __device__ __forceinline__ uint32_t ref_hit_overlaps(const ScanArgs &A, const DevRegion &rg, uint32_t g, uint32_t i,
                                                      uint32_t &nk, uint32_t &off0) {
     const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-    const uint32_t sn = g & 63u, L = (uint32_t)meta[kGLen + sn];
+    const uint32_t sn = g & 63u, L = (uint32_t)meta[kGStrandInts * sn + kGLen];
     nk = (uint32_t)meta[kGDepth];
-    off0 = (uint32_t)meta[kGSlot + sn] * rg.n_inner;
+    off0 = (uint32_t)meta[kGStrandInts * sn + kGSlot] * rg.n_inner;
     const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
     const int32_t p = (int32_t)i;  // the reference's positions are affine
     uint32_t mask = 0;             // bit k: the match overlaps inner range k (k < 32)
@@ -643,7 +684,7 @@ __global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
         for (uint32_t t = 0; t < n; t++) {
             const uint32_t g = s_g[t], i = s_i[t];
             const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-            const uint32_t L = (uint32_t)meta[kGLen + (g & 63u)];
+            const uint32_t L = (uint32_t)meta[kGStrandInts * (g & 63u) + kGLen];
             const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
             for (uint32_t h = rg.hap_begin + threadIdx.x; h < rg.hap_begin + rg.hap_count; h += kFixBlock) {
                 const DevHap hp = A.haps[h];
@@ -668,9 +709,9 @@ __global__ __launch_bounds__(256) void ref_fixup_over_kernel(ScanArgs A) {
         const uint32_t region = A.ref_over[3 * (size_t)r], g = A.ref_over[3 * (size_t)r + 1];
         const uint32_t i = A.ref_over[3 * (size_t)r + 2];
         const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-        const uint32_t sn = g & 63u, L = (uint32_t)meta[kGLen + sn], nk = (uint32_t)meta[kGDepth];
+        const uint32_t sn = g & 63u, L = (uint32_t)meta[kGStrandInts * sn + kGLen], nk = (uint32_t)meta[kGDepth];
         const DevRegion rg = A.regions[region];
-        const uint32_t off0 = (uint32_t)meta[kGSlot + sn] * rg.n_inner;
+        const uint32_t off0 = (uint32_t)meta[kGStrandInts * sn + kGSlot] * rg.n_inner;
         const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
         const int32_t p = (int32_t)i;
         for (uint32_t h = rg.hap_begin + lane; h < rg.hap_begin + rg.hap_count; h += 64) {
@@ -727,8 +768,12 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
                 uint32_t n_haps, const hipStream_t *streams, uint32_t n_streams) {
     if (n_haps == 0 || n_supers == 0) return 0;
     const uint32_t hpb = a0.haps_per_block;
+    // candidate list entries: global strand < 2^24, haplotype in the group < 2^8
+    const DevMSuper &last = supers[n_supers - 1];
+    if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > 256)
+        return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 256 haplotypes per workgroup");
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_cn);  // candidate queues
+    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext);  // candidate queues
     uint32_t region = 0;
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is

@@ -104,9 +104,10 @@ constexpr inline uint32_t mfma_tile_bytes(uint32_t nk) { return nk * 1536; }
 constexpr int kMFieldBits = 11;    // bits per strand field of an output
 constexpr int kMFieldBias = 1023;  // V = U + kMFieldBias - T0: candidate iff V >= 1024
 // The fields only the candidate rescoring reads live in global memory
-// (Plan::m_meta, kGMetaInts per tile, indexed by the strand 2 n + h): min_score,
-// offset of the exact weights (4 per column), len, slot, pattern index.
-enum MGMeta { kGMin = 0, kGWoff = 64, kGLen = 128, kGSlot = 192, kGOrig = 256, kGDepth = 320 };
+// (Plan::m_meta, kGMetaInts per tile, strand sn = 2 n + h): min_score, offset of
+// the exact weights (4 per column), len and slot at kGStrandInts * sn + field
+// (one 16-byte load), the pattern index at kGOrig + sn.
+enum MGMeta { kGMin = 0, kGWoff = 1, kGLen = 2, kGSlot = 3, kGStrandInts = 4, kGOrig = 256, kGDepth = 320 };
 constexpr int kGMetaInts = 384;  // [kGDepth]: the tile's K depth (one int)
 
 // The strand tiles one workgroup stages in LDS: tile_count tiles of K depth
