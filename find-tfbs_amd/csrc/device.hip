@@ -69,6 +69,12 @@ struct tfbs_ctx {
     static constexpr int kSide = 3;
     hipStream_t side[kSide] = {};
     hipEvent_t fork = nullptr, join[kSide] = {};
+    // the matrix-core scan adds into zeroed counts: the idle buffer of a pair is
+    // zeroed on zero_stream beside each scan, for the next one (TFBS_PREZERO)
+    hipStream_t zero_stream = nullptr;
+    hipEvent_t zero_fork = nullptr, zero_ev = nullptr;
+    size_t alt_zero_n = 0;  // counts_alt's elements zeroed (0: none pending)
+    bool prezero = true;
     bool kernel_timed = false;
     float last_kernel_ms = 0.f;
     const Patterns *pats = nullptr;
@@ -83,8 +89,10 @@ struct tfbs_ctx {
     DevBuf<uint32_t> cands;              // matrix-core candidate lists (scan.hpp)
     DevBuf<uint32_t> ref_hits, ref_count, ref_over, ref_over_count;  // reference-window reuse (scan.hpp)
     uint32_t ref_over_cap = 1u << 16;
+    DevBuf<uint32_t> cand_over;  // candidates past the waves' list regions (scan.hpp)
+    uint32_t cand_over_cap = 1u << 16;
     uint32_t n_regions = 0;                // of the resident batch
-    uint32_t *ref_count_host = nullptr;    // pinned: the overflow list's count
+    uint32_t *ref_count_host = nullptr;    // pinned: the overflow lists' counts (reference hits, candidates)
     uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
@@ -92,7 +100,7 @@ struct tfbs_ctx {
     uint32_t mfma_hpb = 64;         // haplotypes per MFMA workgroup
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
-    DevBuf<uint32_t> words, nmask, counts;
+    DevBuf<uint32_t> words, nmask, counts, counts_alt;
     DevBuf<int32_t> posrel, inner;
     DevBuf<DevHap> haps;
     DevBuf<DevRegion> regions;
@@ -156,7 +164,27 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
     a.n_patterns_total = (uint32_t)ctx->pats->pats.size();
     int launches = 0;
     if (!P.m_supers.empty()) {  // atomic adds: zero its slots first (the other kernels store theirs)
-        if (ctx->counts.n) HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, ctx->counts.n * 4, ctx->stream));
+        if (ctx->counts.n) {
+            const size_t need = ctx->counts.n;
+            if (ctx->alt_zero_n >= need) {  // zeroed beside the previous scan
+                std::swap(ctx->counts, ctx->counts_alt);
+                ctx->counts.n = need;
+                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev, 0));
+            } else {
+                HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, need * 4, ctx->stream));
+            }
+            ctx->alt_zero_n = 0;
+            a.counts = ctx->counts.p;
+            if (ctx->prezero) {  // the other buffer for the next scan (its last reader is already queued)
+                int rc;
+                if ((rc = ctx->counts_alt.ensure(need))) return rc;
+                HIP_TRY(hipEventRecord(ctx->zero_fork, ctx->stream));
+                HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_fork, 0));
+                HIP_TRY(hipMemsetAsync(ctx->counts_alt.p, 0, need * 4, ctx->zero_stream));
+                HIP_TRY(hipEventRecord(ctx->zero_ev, ctx->zero_stream));
+                ctx->alt_zero_n = need;
+            }
+        }
         ScanArgs m = a;
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
@@ -172,7 +200,8 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.cand_cap = ctx->cand_cap;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
         if ((rc = ctx->ref_count.ensure(nr)) || (rc = ctx->ref_hits.ensure((size_t)nr * kRefPerRegion * 2)) ||
-            (rc = ctx->ref_over_count.ensure(1)) || (rc = ctx->ref_over.ensure((size_t)ctx->ref_over_cap * 3)))
+            (rc = ctx->ref_over_count.ensure(2)) || (rc = ctx->ref_over.ensure((size_t)ctx->ref_over_cap * 3)) ||
+            (rc = ctx->cand_over.ensure((size_t)ctx->cand_over_cap * 3)))
             return rc;
         m.dedup = 1;
         m.n_regions = ctx->n_regions;
@@ -181,8 +210,10 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.ref_over = ctx->ref_over.p;
         m.ref_over_count = ctx->ref_over_count.p;
         m.ref_over_cap = ctx->ref_over_cap;
+        m.cand_over = ctx->cand_over.p;
+        m.cand_over_cap = ctx->cand_over_cap;
         HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
-        HIP_TRY(hipMemsetAsync(ctx->ref_over_count.p, 0, 4, ctx->stream));
+        HIP_TRY(hipMemsetAsync(ctx->ref_over_count.p, 0, 8, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
@@ -249,10 +280,10 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
-    ctx->cands.release(); ctx->ref_hits.release(); ctx->ref_count.release(); ctx->ref_over.release();
+    ctx->cands.release(); ctx->cand_over.release(); ctx->ref_hits.release(); ctx->ref_count.release(); ctx->ref_over.release();
     ctx->ref_over_count.release();
     if (ctx->ref_count_host) (void)hipHostFree(ctx->ref_count_host);
-    ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
+    ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->counts_alt.release(); ctx->posrel.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_memb.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
@@ -267,6 +298,9 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
         if (ctx->join[i]) (void)hipEventDestroy(ctx->join[i]);
     }
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->zero_fork) (void)hipEventDestroy(ctx->zero_fork);
+    if (ctx->zero_ev) (void)hipEventDestroy(ctx->zero_ev);
+    if (ctx->zero_stream) (void)hipStreamDestroy(ctx->zero_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -287,6 +321,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 44))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
+    ctx->prezero = env_int("TFBS_PREZERO", 1) != 0;
+    ctx->cand_over_cap = (uint32_t)std::max(1, env_int("TFBS_CAND_OVER_CAP", 1 << 16));  // grows on demand (tfbs_scan)
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -308,6 +344,9 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->zero_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->zero_ev, hipEventDisableTiming);
     for (int i = 0; i < tfbs_ctx::kSide; i++) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
@@ -407,12 +446,17 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
     if (!ctx->plan.m_supers.empty()) {
-        // the reference-hit overflow list must have held every hit: otherwise grow it and scan again
-        if (!ctx->ref_count_host) HIP_TRY(hipHostMalloc((void **)&ctx->ref_count_host, 4, hipHostMallocDefault));
-        HIP_TRY(hipMemcpyAsync(ctx->ref_count_host, ctx->ref_over_count.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+        // the overflow lists (reference hits, candidates) must have held every
+        // entry: otherwise grow them and scan again
+        if (!ctx->ref_count_host) HIP_TRY(hipHostMalloc((void **)&ctx->ref_count_host, 8, hipHostMallocDefault));
+        HIP_TRY(hipMemcpyAsync(ctx->ref_count_host, ctx->ref_over_count.p, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        if (*ctx->ref_count_host > ctx->ref_over_cap) {
-            ctx->ref_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)*ctx->ref_count_host * 5 / 4 + 1024);
+        const uint32_t nref = ctx->ref_count_host[0], ncand = ctx->ref_count_host[1];
+        if (nref > ctx->ref_over_cap || ncand > ctx->cand_over_cap) {
+            if (nref > ctx->ref_over_cap)
+                ctx->ref_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)nref * 5 / 4 + 1024);
+            if (ncand > ctx->cand_over_cap)
+                ctx->cand_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)ncand * 5 / 4 + 1024);
             ctx->kernel_timed = false;
             n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
             if (n < 0) return n;

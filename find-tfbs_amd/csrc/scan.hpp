@@ -54,8 +54,12 @@ struct ScanArgs {
     uint32_t *ref_hits;
     uint32_t *ref_count;
     uint32_t *ref_over;
-    uint32_t *ref_over_count;
+    uint32_t *ref_over_count;  // [0] reference hits, [1] candidates past a wave's list
     uint32_t ref_over_cap;
+    // candidates past a wave's list region: (haplotype, strand, window) triples,
+    // rescored by a kernel after the scan (launch_ref_fixup)
+    uint32_t *cand_over;
+    uint32_t cand_over_cap;
 };
 constexpr uint32_t kRefPerRegion = 64;
 constexpr uint32_t kCandWords = 2;  // candidate list entry: strand | haplotype in the group << 24, window

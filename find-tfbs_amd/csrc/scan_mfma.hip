@@ -48,7 +48,9 @@ namespace {
 // TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live; timing only),
 // =4 counts tile tests, firing tiles, queued lanes, exact hits and rejected
 // candidates (printed per launch), =12 never drains the queue, =13 drains it
-// but never rescores (results wrong; timing only).
+// but never rescores, =14 skips the rounds, =16 never queues, =17 decodes the
+// queue but lists nothing, =18 writes the queue but decodes nothing (results
+// wrong; timing only).
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
@@ -154,19 +156,18 @@ __device__ __forceinline__ v16f mfma_chunk(const v4i &a, const BFrag &f, const v
                                                            kScaleB);
 }
 
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-
-// haplotype / region descriptors as wave-uniform (SGPR) values
+// haplotype descriptors as wave-uniform (SGPR) values: through the constant
+// address space (the descriptors are read-only during a launch), so they are
+// scalar loads, counted apart from the vector memory operations in flight
+typedef const __attribute__((address_space(4))) uint32_t ConstU32;
 __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
-    DevHap h = *p;
-    h.word_off = uni(h.word_off);
-    h.len = uni(h.len);
-    h.region = uni(h.region);
-    h.flags = uni(h.flags);
-    h.nmask_off = uni(h.nmask_off);
-    h.pos_off = uni(h.pos_off);
-    h.count_off = ((uint64_t)uni((uint32_t)(h.count_off >> 32)) << 32) | uni((uint32_t)h.count_off);
-    for (int d = 0; d < 4; d++) h.dirty[d] = uni(h.dirty[d]);
+    static_assert(sizeof(DevHap) == 48, "DevHap: 12 dwords");
+    ConstU32 *q = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(p));
+    uint32_t w[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) w[k] = q[k];
+    DevHap h;
+    __builtin_memcpy(&h, w, sizeof(h));
     return h;
 }
 
@@ -178,47 +179,43 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 // not fit drains the queue (drain_queue) and its round is scored again, so no
 // accumulator is live across a drain.
 constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
+#ifndef TFBS_MFMA_RESCORE_AT
+#define TFBS_MFMA_RESCORE_AT 16
+#endif
+constexpr uint32_t kRescoreAt = TFBS_MFMA_RESCORE_AT;  // queued / listed entries rescored between haplotypes
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue][2];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint32_t s_hnext;  // the workgroup's next haplotype (scan_super)
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 #if TFBS_MFMA_PROBE == 4
-__device__ unsigned long long g_probe[5];
+__device__ unsigned long long g_probe[8];
 #endif
 
 // Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
-// one load per column, N columns masked out.  ALL: every block of 8 columns up
-// to 32 issued before the first is summed (the weights are zero-padded to whole
-// blocks, the buffer's tail pad keeps the masked blocks' reads inside it; used
-// where no accumulator is live), else block by block (fewer registers).
-template <bool ALL>
+// one load per column of the strand's blocks of 8 (zero-padded), all issued
+// before the first is summed (the rescoring runs where no accumulator is
+// live), N columns masked out.
 __device__ __forceinline__ int32_t exact_score(const uint32_t *words, const DevHap &hp, uint32_t i, uint32_t L,
                                                const int32_t *wt, uint32_t live) {
     const uint32_t *w = words + hp.word_off + (i >> 4);
     const uint32_t sh = 2 * (i & 15);
     const uint32_t img[2] = {__builtin_amdgcn_alignbit(w[1], w[0], sh), __builtin_amdgcn_alignbit(w[2], w[1], sh)};
     const uint32_t keep = live & (L >= 32 ? ~0u : (1u << L) - 1);  // columns < L that are not N
-    int32_t s = 0;
-    if (ALL) {
-        int32_t v[32];
+    int32_t v[32];
 #pragma unroll
-        for (uint32_t j = 0; j < 32; j++) v[j] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
+    for (uint32_t jb = 0; jb < 32; jb += 8) {
+        if (jb < L) {  // a lane loads only its strand's blocks
 #pragma unroll
-        for (uint32_t j = 0; j < 32; j++) s += v[j] & -(int32_t)((keep >> j) & 1u);  // N scores 0
-    } else {
-#pragma unroll 1
-        for (uint32_t jb = 0; jb < L; jb += 8) {
-            int32_t v[8];
+            for (uint32_t j = jb; j < jb + 8; j++) v[j] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
+        } else {
 #pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = jb + u;
-                v[u] = wt[4 * j + ((img[j >> 4] >> (2 * (j & 15))) & 3u)];
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < 8; u++) s += v[u] & -(int32_t)((keep >> (jb + u)) & 1u);
+            for (uint32_t j = jb; j < jb + 8; j++) v[j] = 0;
         }
     }
+    int32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 32; j++) s += v[j] & -(int32_t)((keep >> j) & 1u);  // N scores 0
     return s;
 }
 
@@ -227,7 +224,6 @@ __device__ __forceinline__ int32_t exact_score(const uint32_t *words, const DevH
 // slot's count for every inner range it overlaps.  The loads are issued in
 // three dependent rounds (strand fields | weights, region, position, N mask |
 // inner ranges) before the atomics.
-template <bool ALL = true>
 __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_t *words, const DevHap &hp,
                                                 uint32_t hap, uint32_t g, uint32_t i) {
     const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
@@ -243,7 +239,7 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
     }
     const uint32_t L = (uint32_t)sf.z;
     if (i + L > hp.len) return;                         // past the end (pattern.rs:147-150)
-    const int32_t sc = exact_score<ALL>(words, hp, i, L, A.mweights + sf.y, live);
+    const int32_t sc = exact_score(words, hp, i, L, A.mweights + sf.y, live);
 #if TFBS_MFMA_PROBE == 4
     atomicAdd(&g_probe[sc > sf.x ? 1 : 2], 1ull);
 #endif
@@ -291,8 +287,8 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
 // mask and each candidate (haplotype, strand, window) is appended to the
 // wave's region of the candidate list (2 dwords: global strand | haplotype in
 // the group << 24, window), one candidate per lane per round; the wave rescores
-// its list when it has scanned (rescore_list).  A full region (pathological
-// thresholds) rescores here instead.
+// its list when it has scanned (rescore_list).  A full region (dense hits)
+// spills to A.cand_over (cand_over_kernel).
 // h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
 __device__ __forceinline__ uint32_t wave_cand_cap(const ScanArgs &A) { return A.cand_cap / (kMBlock / 64); }
 __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
@@ -305,9 +301,19 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
 #if TFBS_MFMA_PROBE == 12
     return;  // timing only: queued candidates are dropped
 #endif
+#if TFBS_MFMA_PROBE == 18
+    if (lane < n) asm volatile("" ::"v"(s_qdata[wave][lane][0].x), "v"(s_qmeta[wave][lane]));
+    return;  // timing only: the queue is written and read, nothing decoded
+#endif
     uint2 *list = cand_list(A, wave);
     const uint32_t cap = wave_cand_cap(A);
+#if TFBS_MFMA_PROBE == 4
+    if (lane == 0) atomicAdd(&g_probe[5], 1ull);
+#endif
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
+#if TFBS_MFMA_PROBE == 4
+        if (lane == 0) atomicAdd(&g_probe[6], 1ull);
+#endif
         const uint32_t e = e0 + lane;
         uint32_t m = 0, g0 = 0, i0 = 0, hl = 0;
         if (e < n) {
@@ -331,6 +337,9 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
         }
         uint64_t act;
         while ((act = __ballot(m != 0)) != 0) {
+#if TFBS_MFMA_PROBE == 4
+            if (lane == 0) atomicAdd(&g_probe[7], 1ull);
+#endif
             if (m) {
                 const uint32_t b = __builtin_ctz(m);
                 m &= m - 1;
@@ -338,8 +347,19 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
                 const uint32_t r = 2 * (b & 7u) + ((b >> 3) & 1u);
                 const uint32_t i = i0 + (r & 3) + 8 * (r >> 2), g = g0 + (b >> 4);
-                if (slot < cap) list[slot] = make_uint2(g | (hl << 24), i);
-                else score_candidate<false>(A, words, A.haps[h0 + hl], h0 + hl, g, i);
+                if (TFBS_MFMA_PROBE == 17) {
+                    asm volatile("" ::"v"(g), "v"(i), "v"(slot));
+                } else if (slot < cap) {
+                    list[slot] = make_uint2(g | (hl << 24), i);
+                } else {  // rescored after the scan (no rescoring code, whose loads would stay
+                          // pending, in the scan loop)
+                    const uint32_t o = atomicAdd(A.ref_over_count + 1, 1u);
+                    if (o < A.cand_over_cap) {
+                        A.cand_over[3 * (size_t)o] = h0 + hl;
+                        A.cand_over[3 * (size_t)o + 1] = g;
+                        A.cand_over[3 * (size_t)o + 2] = i;
+                    }
+                }
             }
             cn += (uint32_t)__popcll(act);
         }
@@ -392,6 +412,10 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t
         atomicAdd(&g_probe[4], 1ull);
         atomicAdd(&g_probe[0], (unsigned long long)__popcll(fired));
     }
+#endif
+#if TFBS_MFMA_PROBE == 16
+    asm volatile("" ::"v"(x));
+    return;  // timing only: firing tiles are not queued
 #endif
     const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, qn));
     if (x) {
@@ -502,6 +526,10 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
                                           const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t ha,
                                           uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb, int sa,
                                           uint32_t &qn, uint32_t &cn) {
+#if TFBS_MFMA_PROBE == 14
+    asm volatile("" ::"v"(a0[0]), "v"(a1[0]), "v"(a0[NK - 1]), "v"(a1[NK - 1]));
+    return;  // timing only: the haplotype loop and A fragments without the rounds
+#endif
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
 #define TFBS_SEGMENT(D)                                                                                          \
@@ -532,6 +560,9 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
     const int sa = lane < 32 ? kScaleA0 : kScaleA1;
     const char *tab = s_img - kMOnehotBytes;
+#ifdef TFBS_MFMA_PRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
     uint32_t qn = 0, cn = 0;  // the wave's queued entries, listed candidates
     // window tiles two at a time (each B fragment read from LDS feeds two
     // MFMAs), pairs formed across the wave's haplotypes: a tile waits in a0
@@ -542,6 +573,17 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     // haplotypes taken one at a time from the workgroup's counter: the waves
     // finish together however the dirty tiles of reused haplotypes fall
     for (;;) {
+        // between haplotypes (no accumulator live): drain and rescore once enough
+        // candidates wait, so the rescoring latency falls while the workgroup's
+        // other waves still scan (not all at its end)
+        if (qn >= kRescoreAt) {
+            drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
+            qn = 0;
+        }
+        if (cn >= kRescoreAt) {
+            rescore_list(A, words, h0, wave, lane, cn);
+            cn = 0;
+        }
         uint32_t hh = 0;
         if (lane == 0) hh = atomicAdd(&s_hnext, 1u);
         hh = __builtin_amdgcn_readfirstlane(hh);
@@ -700,6 +742,16 @@ __global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
     }
 }
 
+// Candidates past the waves' list regions (drain_queue), one per thread; before
+// ref_fixup_kernel (a reference haplotype's hits are listed for it).
+__global__ __launch_bounds__(256) void cand_over_kernel(ScanArgs A) {
+    const uint32_t n = min(A.ref_over_count[1], A.cand_over_cap);
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const uint32_t hap = A.cand_over[3 * (size_t)k], g = A.cand_over[3 * (size_t)k + 1];
+        score_candidate(A, A.words, A.haps[hap], hap, g, A.cand_over[3 * (size_t)k + 2]);
+    }
+}
+
 // The overflow list (regions with more than kRefPerRegion reference hits): one
 // wave per hit, atomics (runs after ref_fixup_kernel).
 __global__ __launch_bounds__(256) void ref_fixup_over_kernel(ScanArgs A) {
@@ -738,12 +790,13 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_dept
 }  // namespace
 
 int launch_ref_fixup(const ScanArgs &a, hipStream_t stream) {
-    if (a.n_regions == 0) return 0;
+    hipLaunchKernelGGL(cand_over_kernel, dim3(256), dim3(256), 0, stream, a);
+    if (a.n_regions == 0) return 1;
     hipLaunchKernelGGL(ref_fixup_kernel, dim3(a.n_regions), dim3(kFixBlock), 0, stream, a);
     hipLaunchKernelGGL(ref_fixup_over_kernel, dim3(1024), dim3(256), 0, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("ref_fixup_kernel launch: ") + hipGetErrorString(e));
-    return 2;
+    return 3;
 }
 
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
@@ -822,12 +875,14 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan_mfma_kernel launch: ") + hipGetErrorString(e));
 #if TFBS_MFMA_PROBE == 4
-    unsigned long long pr[5] = {0, 0, 0, 0, 0};
+    unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (uint32_t i = 0; i < n_streams; i++) (void)hipStreamSynchronize(streams[i]);
     (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_probe), sizeof pr);
-    fprintf(stderr, "probe4 tile_tests %llu fired %llu queued_lanes %llu hits %llu rejected %llu\n", pr[3], pr[4],
-            pr[0], pr[1], pr[2]);
-    const unsigned long long z[5] = {0, 0, 0, 0, 0};
+    fprintf(stderr,
+            "probe4 tile_tests %llu fired %llu queued_lanes %llu hits %llu rejected %llu drains %llu passes %llu "
+            "rounds %llu\n",
+            pr[3], pr[4], pr[0], pr[1], pr[2], pr[5], pr[6], pr[7]);
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof z);
 #endif
     return launches;

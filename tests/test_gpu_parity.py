@@ -334,7 +334,8 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
     the oracle: an SNV every haplotype carries (no reference group: the helper copy of
     the reference supplies the hits), N runs in the reference, haplotypes with indels
     (scanned whole), 40 nested inner ranges (the fix-up's path past 32 ranges) and
-    p = 0.05 thresholds (over 64 reference hits per region: the overflow list)."""
+    p = 0.05 thresholds (over 64 reference hits per region: the overflow list; with
+    small candidate lists, the candidate overflow list and its regrowth)."""
     monkeypatch.setenv("TFBS_MFMA", "1")
     ps, _ = synth_patterns(tmp_path, 10, 3, 71, thr=thr)
     n_samples, n_regions = 60, 6
@@ -367,6 +368,13 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
     monkeypatch.setenv("TFBS_DEDUP", "0")  # the same job scanning every window
     b0 = _compare(ps, n_samples, beds, regions)
     assert b0.num_scan_windows > b.num_scan_windows
+    if thr > 0.01:
+        # 8 list entries per wave: candidates spill to the overflow list, which
+        # itself overflows (16 entries): the scan grows it and runs again
+        monkeypatch.setenv("TFBS_DEDUP", "1")
+        monkeypatch.setenv("TFBS_CAND_CAP", "64")
+        monkeypatch.setenv("TFBS_CAND_OVER_CAP", "16")
+        _compare(ps, n_samples, beds, regions)
 
 
 def test_multi_bed_duplicate_and_nested_inner_peaks(tmp_path):
