@@ -49,8 +49,8 @@ namespace {
 // =4 counts tile tests, firing tiles, queued lanes, exact hits and rejected
 // candidates (printed per launch), =12 never drains the queue, =13 drains it
 // but never rescores, =14 skips the rounds, =16 never queues, =17 decodes the
-// queue but lists nothing, =18 writes the queue but decodes nothing (results
-// wrong; timing only).
+// queue but lists nothing, =18 writes the queue but decodes nothing, =19
+// rescores without the count atomics (results wrong; timing only).
 #ifndef TFBS_MFMA_PROBE
 #define TFBS_MFMA_PROBE 0
 #endif
@@ -66,6 +66,7 @@ constexpr uint32_t kMStagedMax = 80 * 1024;  // LDS per workgroup at 2 workgroup
 constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 constexpr uint32_t kTestMask = (1u << (kMFieldBits - 1)) | (1u << (2 * kMFieldBits - 1));  // the fields' top bits
+constexpr uint32_t kQueueBits = 0x20200404u;  // those bits after queue_tile's byte permute (outputs 2j, 2j + 1)
 constexpr int kScaleA0 = 127, kScaleA1 = 127 + kMFieldBits, kScaleB = 130;  // e8m0: 1, 2^11, 2^3
 
 // The packed words (and N-mask words) a lane needs for its window of the
@@ -179,11 +180,7 @@ __device__ __forceinline__ DevHap load_hap(const DevHap *p) {
 // not fit drains the queue (drain_queue) and its round is scored again, so no
 // accumulator is live across a drain.
 constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
-#ifndef TFBS_MFMA_RESCORE_AT
-#define TFBS_MFMA_RESCORE_AT 16
-#endif
-constexpr uint32_t kRescoreAt = TFBS_MFMA_RESCORE_AT;  // queued / listed entries rescored between haplotypes
-__shared__ uint4 s_qdata[kMBlock / 64][kMQueue][2];
+__shared__ uint4 s_qdata[kMBlock / 64][kMQueue];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint32_t s_hnext;  // the workgroup's next haplotype (scan_super)
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
@@ -255,6 +252,10 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
         const uint32_t span = (uint32_t)(r.y - r.x);
         if ((uint32_t)(p - r.x) <= span || (uint32_t)(p + (int32_t)L - 1 - r.x) <= span) mask |= 1u << k;
     }
+#if TFBS_MFMA_PROBE == 19
+    asm volatile("" ::"v"(mask), "v"(off0));
+    return;  // timing only: no count atomics
+#endif
     for (; mask; mask &= mask - 1)
         atomicAdd(A.counts + hp.count_off + (size_t)(off0 + __builtin_ctz(mask)) * rg.count_stride, 1u);
     for (uint32_t k = 32; k < rg.n_inner; k++) {        // ranges past 32 (rare)
@@ -302,7 +303,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
     return;  // timing only: queued candidates are dropped
 #endif
 #if TFBS_MFMA_PROBE == 18
-    if (lane < n) asm volatile("" ::"v"(s_qdata[wave][lane][0].x), "v"(s_qmeta[wave][lane]));
+    if (lane < n) asm volatile("" ::"v"(s_qdata[wave][lane].x), "v"(s_qmeta[wave][lane]));
     return;  // timing only: the queue is written and read, nothing decoded
 #endif
     uint2 *list = cand_list(A, wave);
@@ -317,23 +318,23 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
         const uint32_t e = e0 + lane;
         uint32_t m = 0, g0 = 0, i0 = 0, hl = 0;
         if (e < n) {
-            const uint4 d0 = s_qdata[wave][e][0], d1 = s_qdata[wave][e][1];
+            const uint4 d = s_qdata[wave][e];
             const uint64_t q = s_qmeta[wave][e];
             const uint32_t src = (uint32_t)q & 63u, ti = ((uint32_t)q >> 6) & 63u;
             hl = ((uint32_t)q >> 12) & 255u;
             i0 = ((uint32_t)(q >> 32) << 5) + 4 * (src >> 5);
             g0 = (tile0 + ti) * kMStrands + 2 * (src & 31u);
-            // dword k (queue_tile): outputs 2k, 2k+1, the first strand's top bits
-            // at 2, 10, the second's at 21, 29.  lo collects bits 2 + k, 10 + k,
-            // hi 5 + k, 13 + k; m bit b: strand b >> 4, output 2 (b & 7) + (b >> 3 & 1)
-            const uint32_t dd[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
-            uint32_t lo = 0, hi = 0;
+            // dword k (queue_tile): the first strand's top bits of outputs 4k, 4k+1,
+            // 4k+2, 4k+3 at 2, 10, 3, 11, the second's at 21, 29, 22, 30.  m bit
+            // b: strand b >> 4, output 4 (b >> 1 & 3) + 2 (b & 1) + (b >> 3 & 1)
+            const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
+            uint32_t lo = (dd[0] >> 2) & 0x303u, hi = (dd[0] >> 21) & 0x303u;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                lo |= (dd[k] << k) & (0x0404u << k);
-                hi |= (dd[k] >> (16 - k)) & (0x2020u << k);
+            for (int k = 1; k < 4; k++) {
+                lo |= (dd[k] << (2 * k - 2)) & (0x303u << (2 * k));
+                hi |= (dd[k] >> (21 - 2 * k)) & (0x303u << (2 * k));
             }
-            m = (lo >> 2) | (hi << 11);
+            m = lo | (hi << 16);
         }
         uint64_t act;
         while ((act = __ballot(m != 0)) != 0) {
@@ -345,7 +346,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
                 m &= m - 1;
                 const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-                const uint32_t r = 2 * (b & 7u) + ((b >> 3) & 1u);
+                const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
                 const uint32_t i = i0 + (r & 3) + 8 * (r >> 2), g = g0 + (b >> 4);
                 if (TFBS_MFMA_PROBE == 17) {
                     asm volatile("" ::"v"(g), "v"(i), "v"(slot));
@@ -419,13 +420,16 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t
 #endif
     const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, qn));
     if (x) {
-        // bytes 1, 1', 2, 2' of outputs 2k, 2k + 1: top bits at 2, 10, 21, 29
+        // bytes 1, 1', 2, 2' of outputs 2j, 2j + 1: top bits at 2, 10, 21, 29;
+        // dword k keeps those of j = 2k and, one bit up, of j = 2k + 1
         uint32_t d[8];
 #pragma unroll
-        for (int k = 0; k < 8; k++)
-            d[k] = __builtin_amdgcn_perm(__float_as_uint(acc[2 * k + 1]), __float_as_uint(acc[2 * k]), 0x06020501u);
-        s_qdata[wave][at][0] = uint4{d[0], d[1], d[2], d[3]};
-        s_qdata[wave][at][1] = uint4{d[4], d[5], d[6], d[7]};
+        for (int j = 0; j < 8; j++)
+            d[j] = __builtin_amdgcn_perm(__float_as_uint(acc[2 * j + 1]), __float_as_uint(acc[2 * j]), 0x06020501u);
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = __builtin_amdgcn_bitop3_b32(d[2 * k], d[2 * k + 1] << 1, kQueueBits, 0xe4);  // M ? d[2k] : d[2k+1] << 1
+        s_qdata[wave][at] = uint4{x[0], x[1], x[2], x[3]};
         s_qmeta[wave][at] = (uint64_t)(lane | (ti << 6) | (hh << 12)) | ((uint64_t)(i0 >> 5) << 32);
     }
     qn += (uint32_t)__popcll(fired);
@@ -573,17 +577,6 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     // haplotypes taken one at a time from the workgroup's counter: the waves
     // finish together however the dirty tiles of reused haplotypes fall
     for (;;) {
-        // between haplotypes (no accumulator live): drain and rescore once enough
-        // candidates wait, so the rescoring latency falls while the workgroup's
-        // other waves still scan (not all at its end)
-        if (qn >= kRescoreAt) {
-            drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
-            qn = 0;
-        }
-        if (cn >= kRescoreAt) {
-            rescore_list(A, words, h0, wave, lane, cn);
-            cn = 0;
-        }
         uint32_t hh = 0;
         if (lane == 0) hh = atomicAdd(&s_hnext, 1u);
         hh = __builtin_amdgcn_readfirstlane(hh);
