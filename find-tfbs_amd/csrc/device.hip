@@ -90,7 +90,8 @@ struct tfbs_ctx {
     DevBuf<uint32_t> ref_hits, ref_count, ref_over, ref_over_count;  // reference-window reuse (scan.hpp)
     uint32_t ref_over_cap = 1u << 16;
     DevBuf<uint32_t> cand_over;  // candidates past the waves' list regions (scan.hpp)
-    uint32_t cand_over_cap = 1u << 16;
+    uint32_t cand_over_cap = 1u << 20;
+    bool debug_over = false;  // TFBS_DEBUG_OVER: print the overflow lists' fill after each scan
     uint32_t n_regions = 0;                // of the resident batch
     uint32_t *ref_count_host = nullptr;    // pinned: the overflow lists' counts (reference hits, candidates)
     uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
@@ -322,7 +323,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     ctx->prezero = env_int("TFBS_PREZERO", 1) != 0;
-    ctx->cand_over_cap = (uint32_t)std::max(1, env_int("TFBS_CAND_OVER_CAP", 1 << 16));  // grows on demand (tfbs_scan)
+    ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
+    ctx->cand_over_cap = (uint32_t)std::max(1, env_int("TFBS_CAND_OVER_CAP", 1 << 20));  // grows on demand (tfbs_scan)
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
     opt.mfma = ctx->mfma;
@@ -445,22 +447,27 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->kernel_timed = false;
     int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
-    if (!ctx->plan.m_supers.empty()) {
-        // the overflow lists (reference hits, candidates) must have held every
-        // entry: otherwise grow them and scan again
+    // the overflow lists (reference hits, candidates) must have held every entry:
+    // otherwise grow them and scan again
+    for (int round = 0; !ctx->plan.m_supers.empty(); round++) {
         if (!ctx->ref_count_host) HIP_TRY(hipHostMalloc((void **)&ctx->ref_count_host, 8, hipHostMallocDefault));
         HIP_TRY(hipMemcpyAsync(ctx->ref_count_host, ctx->ref_over_count.p, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         const uint32_t nref = ctx->ref_count_host[0], ncand = ctx->ref_count_host[1];
-        if (nref > ctx->ref_over_cap || ncand > ctx->cand_over_cap) {
-            if (nref > ctx->ref_over_cap)
-                ctx->ref_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)nref * 5 / 4 + 1024);
-            if (ncand > ctx->cand_over_cap)
-                ctx->cand_over_cap = (uint32_t)std::min<uint64_t>(UINT32_MAX / 4, (uint64_t)ncand * 5 / 4 + 1024);
-            ctx->kernel_timed = false;
-            n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
-            if (n < 0) return n;
-        }
+        if (ctx->debug_over)
+            fprintf(stderr, "tfbs_scan overflow lists: reference hits %u/%u candidates %u/%u\n", nref,
+                    ctx->ref_over_cap, ncand, ctx->cand_over_cap);
+        if (nref <= ctx->ref_over_cap && ncand <= ctx->cand_over_cap) break;
+        // a dropped candidate may have been a reference hit: the next scan is checked too
+        if (round == 8) return tfbs::fail(TFBS_E_NOMEM, "scan overflow lists still full after 8 rescans");
+        auto grow = [](uint32_t &cap, uint32_t need, uint64_t lim) {
+            if (need > cap) cap = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need * 5 / 4 + 1024);
+        };
+        grow(ctx->ref_over_cap, ncand > ctx->cand_over_cap ? 2 * std::max(nref, 1024u) : nref, UINT32_MAX / 4);
+        grow(ctx->cand_over_cap, ncand, UINT32_MAX / 4);
+        ctx->kernel_timed = false;
+        n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
+        if (n < 0) return n;
     }
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
