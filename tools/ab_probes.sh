@@ -1,4 +1,5 @@
-# same-box timing of the in-tree build and probe builds on tools/tune.py (C3 lengths)
+# Same-box timing of the in-tree build and tools/probe_build.sh builds on tools/tune.py (C3 lengths).
+# Usage: bash tools/ab_probes.sh TAG NAME...   (NAME: find-tfbs_amd/lib/probe<NAME>)
 OUT=gpurun_out/${1:-xp}; shift; mkdir -p $OUT
 for rep in 1 2; do for lib in base "$@"; do
   if [ $lib = base ]; then unset TFBS_LIB; else export TFBS_LIB=find-tfbs_amd/lib/probe$lib/libtfbs_amd.so; fi

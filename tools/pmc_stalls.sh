@@ -1,4 +1,5 @@
-# PMC: stall breakdown of the in-tree build on the tune.py workload (two SQ passes)
+# PMC stall breakdown (two SQ passes) of the in-tree build on the tools/tune.py workload.
+# Usage: bash tools/pmc_stalls.sh TAG
 OUT=gpurun_out/${1:-pw}; mkdir -p $OUT
 export TMPDIR=/tmp TFBS_MFMA=1
 p1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC"
