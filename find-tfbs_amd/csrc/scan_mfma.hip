@@ -27,11 +27,12 @@
 //    (r & 3) + 8 (r >> 2) + 4 (l >> 5), r < 16.  A firing lane (rare) appends
 //    the fields' top bits of its 16 outputs (16 bytes) to the wave's LDS queue;
 //    drain_queue decodes them into (haplotype, strand, window) candidates in the
-//    workgroup's region of a global (L2-resident) list, and at its end the
-//    workgroup rescores those exactly, one per thread (pattern.rs:125-151),
+//    wave's region of a global (L2-resident) list, and when the wave has
+//    scanned it rescores those exactly, one per lane (pattern.rs:125-151),
 //    applies the inner-range overlap test (range.rs:18-21 as main.rs:503 uses
 //    it) and adds to the count of the strand's pattern_id slot atomically
-//    (counts are zeroed before the scan).
+//    (counts are zeroed before the scan); a full wave list spills to a
+//    launch-wide list rescored by cand_over_kernel after the scan.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
