@@ -355,7 +355,7 @@ def main():
                 "scanned_windows_per_step": int(tot_scan),
             },
             "value_note": "windows of every distinct haplotype resolved per second (the reference scores each "
-                          "of them); an SNV-only haplotype's windows whose bases and positions equal the "
+                          "of them); a haplotype's windows whose bases and positions equal the "
                           "region's reference window take the reference window's result (reference-window "
                           "reuse, exact; TFBS_DEDUP=0 scans them all), scanned_windows_per_s counts the "
                           "windows the kernels read",

@@ -369,28 +369,32 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             h.affine = true;
             for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
         }
-        // reference-window reuse: SNV-only haplotypes of the reference's length
-        // and N positions mark the window tiles whose windows (of up to 8 nk
-        // columns) hold a differing base
+        // reference-window reuse: a window whose bases and positions are the
+        // reference window's has its hits.  Per haplotype, the window tiles whose
+        // windows (of up to 8 nk columns) reach a column that differs from the
+        // reference -- another base, another position (past an indel), or past
+        // the end of either sequence -- are marked; the others are reused
+        // (haplotypes of up to kDedupMaxTiles tiles, the reference's too).
         const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.dist.size() - 1 : -1);
         if (!B.dedup || ref < 0) return;
         const std::vector<uint8_t> &rn = rb.dist[ref].nuc;
+        if ((rn.size() + kMWindows - 1) / kMWindows > kDedupMaxTiles) return;
         for (size_t i = 0; i < rb.dist.size(); i++) {
             HapInfo &h = info[j][i];
-            if ((int32_t)i == ref || !h.affine || h.n != rn.size() || (h.n + kMWindows - 1) / kMWindows > kDedupMaxTiles)
-                continue;
-            const std::vector<uint8_t> &dn = rb.dist[i].nuc;
-            bool ok = true;
-            for (uint32_t p = 0; p < h.n && ok; p++) ok = (dn[p] == 4) == (rn[p] == 4);
-            if (!ok) continue;
-            h.dedup = true;
-            for (uint32_t p = 0; p < h.n; p++) {
-                if (dn[p] == rn[p]) continue;
-                for (uint32_t d = 0; d < 4; d++) {  // windows p - 8 (d + 1) + 1 .. p
-                    const uint32_t w0 = p + 1 >= 8 * (d + 1) ? p + 1 - 8 * (d + 1) : 0;
-                    for (uint32_t t = w0 / kMWindows; t <= p / kMWindows; t++) h.dirty[d] |= 1u << t;
+            if ((int32_t)i == ref || (h.n + kMWindows - 1) / kMWindows > kDedupMaxTiles) continue;
+            const Distinct &d = rb.dist[i];
+            const uint32_t nmin = std::min<uint32_t>(h.n, (uint32_t)rn.size());
+            auto mark = [&](uint32_t p, bool to_end) {  // windows p - 8 (d + 1) + 1 .. p (.. the last tile)
+                for (uint32_t dd = 0; dd < 4; dd++) {
+                    const uint32_t w0 = p + 1 >= 8 * (dd + 1) ? p + 1 - 8 * (dd + 1) : 0;
+                    const uint32_t t1 = to_end ? kDedupMaxTiles - 1 : std::min(p / kMWindows, kDedupMaxTiles - 1);
+                    for (uint32_t t = w0 / kMWindows; t <= t1; t++) h.dirty[dd] |= 1u << t;
                 }
-            }
+            };
+            h.dedup = true;
+            for (uint32_t p = 0; p < nmin; p++)
+                if (d.nuc[p] != rn[p] || d.pos[p] != rb.R.es + p) mark(p, false);
+            if (h.n != rn.size()) mark(nmin, true);  // columns past the shorter sequence differ
         }
     });
     // serial layout: region / haplotype / word / mask / position offsets

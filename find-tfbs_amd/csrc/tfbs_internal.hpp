@@ -134,11 +134,12 @@ constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 
 
 // HAP_REF: the region's reference haplotype (the reference group's, or a
 // helper with no carriers after the region's distinct haplotypes); its
-// matrix-core hits are listed for the reference-window fix-up.  HAP_DEDUP: an
-// SNV-only haplotype of the reference's length and N positions: the matrix-core
-// scan reads only its window tiles that contain a base differing from the
-// reference (dirty[nk - 1], for strands of up to 8 nk columns); every other
-// window has the reference window's bases and positions, so its hits are the
+// matrix-core hits are listed for the reference-window fix-up.  HAP_DEDUP: a
+// haplotype of at most kDedupMaxTiles window tiles: the matrix-core scan reads
+// only its tiles with a window (of up to 8 nk columns, dirty[nk - 1]) that
+// reaches a column differing from the reference's -- another base or N, another
+// position (past an indel), past the end of either sequence; every other window
+// has the reference window's bases and positions, so its hits are the
 // reference's, added by ref_fixup_kernel.
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
 constexpr uint32_t kDedupMaxTiles = 32;  // window tiles a dirty mask covers

@@ -333,7 +333,7 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
     """Reference-window reuse (HAP_DEDUP, ref_fixup_kernel) on its edge cases, against
     the oracle: an SNV every haplotype carries (no reference group: the helper copy of
     the reference supplies the hits), N runs in the reference, haplotypes with indels
-    (scanned whole), 40 nested inner ranges (the fix-up's path past 32 ranges) and
+    (reused before the first indel, scanned after it), 40 nested inner ranges (the fix-up's path past 32 ranges) and
     p = 0.05 thresholds (over 64 reference hits per region: the overflow list; with
     small candidate lists, the candidate overflow list and its regrowth)."""
     monkeypatch.setenv("TFBS_MFMA", "1")
