@@ -36,11 +36,12 @@ struct RefWindow {
     // haplotype.rs:90-92 get(): bases with pos in [s, e]
     void get(uint64_t s, uint64_t e, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) const {
         if (n == 0 || e < s) return;
-        uint64_t lo = std::max(s, start), hi = std::min(e, start + n - 1);
-        for (uint64_t p = lo; p <= hi && p >= lo; p++) {
-            nucs.push_back(nuc[p - start]);
-            pos.push_back(p);
-        }
+        const uint64_t lo = std::max(s, start), hi = std::min(e, start + n - 1);
+        if (hi < lo) return;
+        nucs.insert(nucs.end(), nuc + (lo - start), nuc + (hi - start) + 1);
+        const size_t k = pos.size();
+        pos.resize(k + (hi - lo + 1));
+        for (uint64_t p = lo; p <= hi; p++) pos[k + (p - lo)] = p;
     }
     // haplotype.rs:119-125: the base at pos, N if absent
     uint8_t at(uint64_t p) const { return (p >= start && p - start < n) ? nuc[p - start] : 4; }
@@ -143,8 +144,12 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // Result of load_diffs + group_by_diffs: hap_ids ascending, each haplotype's
     // diff ranks ascending in hd[span_b[k], span_e[k]), and the groups as runs of
     // `order` (indices into hap_ids), in ascending Vec<Diff> order.
+    // (The mask path keeps no spans: a group's diffs are its mask's bits, gmask.)
     std::vector<std::pair<uint32_t, uint32_t>> hd;  // (hap, rank)
-    std::vector<uint32_t> hap_ids, span_b, span_e, order;
+    std::vector<uint32_t> span_b, span_e, order;
+    thread_local std::vector<uint32_t> hap_ids;  // reused: no page faults per region
+    hap_ids.clear();
+    std::vector<uint64_t> gmask;  // mask path: each group's diff mask
     struct Group { uint32_t first, last; };  // run in `order`
     std::vector<Group> groups;
     bool masks_ok = uniq.size() <= 64;
@@ -174,25 +179,48 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
         }
     }
     if (masks_ok) {
-        std::unordered_map<uint64_t, uint32_t> gid;  // mask -> distinct mask index
+        // mask -> distinct mask index in an open-addressed table (masks are
+        // non-zero, 0 marks a free slot); each haplotype's index in gk, then the
+        // members scattered per mask in ascending haplotype order (counting sort)
+        thread_local std::vector<uint64_t> tkey;
+        thread_local std::vector<uint32_t> tval;
+        size_t cap = 1024;
+        tkey.assign(cap, 0);
+        tval.resize(cap);
         std::vector<uint64_t> masks;
-        std::vector<std::vector<uint32_t>> members;  // indices into hap_ids, ascending
+        std::vector<uint32_t> gcount;
+        thread_local std::vector<uint32_t> gk;
+        gk.clear();
+        auto slot_of = [&](uint64_t m) {
+            size_t s = (size_t)((m * 0x9E3779B97F4A7C15ull) >> 40) & (cap - 1);
+            while (tkey[s] != 0 && tkey[s] != m) s = (s + 1) & (cap - 1);
+            return s;
+        };
         for (uint32_t h = 0; h < H; h++) {
             const uint64_t m = sig[h];
             if (!m) continue;
             sig[h] = 0;
-            const uint32_t k = (uint32_t)hap_ids.size();
             hap_ids.push_back(h);
-            span_b.push_back((uint32_t)hd.size());
-            for (uint64_t x = m; x; x &= x - 1) hd.push_back({h, (uint32_t)__builtin_ctzll(x)});
-            span_e.push_back((uint32_t)hd.size());
-            auto it = gid.find(m);
-            if (it == gid.end()) {
-                it = gid.emplace(m, (uint32_t)masks.size()).first;
+            size_t s = slot_of(m);
+            if (tkey[s] == 0) {
+                if (2 * (masks.size() + 1) > cap) {  // grow to keep the load under 1/2
+                    cap *= 2;
+                    tkey.assign(cap, 0);
+                    tval.resize(cap);
+                    for (uint32_t q = 0; q < masks.size(); q++) {
+                        const size_t t = slot_of(masks[q]);
+                        tkey[t] = masks[q];
+                        tval[t] = q;
+                    }
+                    s = slot_of(m);
+                }
+                tkey[s] = m;
+                tval[s] = (uint32_t)masks.size();
                 masks.push_back(m);
-                members.emplace_back();
+                gcount.push_back(0);
             }
-            members[it->second].push_back(k);
+            gk.push_back(tval[s]);
+            gcount[tval[s]]++;
         }
         // Vec<Diff> order of the masks' ascending rank lists
         auto lex_less = [](uint64_t a, uint64_t b) {
@@ -205,10 +233,16 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
         std::vector<uint32_t> gs(masks.size());
         std::iota(gs.begin(), gs.end(), 0u);
         std::sort(gs.begin(), gs.end(), [&](uint32_t x, uint32_t y) { return lex_less(masks[x], masks[y]); });
+        std::vector<uint32_t> start(masks.size());
+        uint32_t at = 0;
         for (uint32_t g : gs) {
-            groups.push_back({(uint32_t)order.size(), (uint32_t)(order.size() + members[g].size())});
-            order.insert(order.end(), members[g].begin(), members[g].end());
+            start[g] = at;
+            groups.push_back({at, at + gcount[g]});
+            gmask.push_back(masks[g]);
+            at += gcount[g];
         }
+        order.resize(at);
+        for (uint32_t k = 0; k < (uint32_t)gk.size(); k++) order[start[gk[k]]++] = k;
     } else {
         for (auto &r : I.recs) {
             if (r.n_alleles != 2 || r.carriers.empty()) continue;
@@ -257,8 +291,13 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     for (uint32_t g = 0; g < groups.size(); g++) {
         uint32_t rep = order[groups[g].first];
         std::vector<const Record *> diffs;
-        for (uint32_t t = span_b[rep]; t < span_e[rep]; t++) diffs.push_back(uniq[hd[t].second]);
+        if (masks_ok)
+            for (uint64_t x = gmask[g]; x; x &= x - 1) diffs.push_back(uniq[__builtin_ctzll(x)]);
+        else
+            for (uint32_t t = span_b[rep]; t < span_e[rep]; t++) diffs.push_back(uniq[hd[t].second]);
         Distinct d;
+        d.nuc.reserve(R.ee - R.es + 16);
+        d.pos.reserve(R.ee - R.es + 16);
         int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos);
         if (rc) return rc;
         d.group = (int32_t)g;
@@ -284,14 +323,17 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // membership and carrier counts
     std::vector<uint32_t> &carriers = out.carriers;
     carriers.assign(dist.size(), 0);
-    std::vector<std::pair<uint32_t, uint32_t>> member;  // (hap id, local)
+    // local distinct index per entry of hap_ids (ascending haplotype ids; each
+    // in at most one group, a losing group's members in none)
+    std::vector<uint32_t> local_of;
+    if (B.keep_membership) local_of.assign(hap_ids.size(), UINT32_MAX);
     uint64_t covered = 0;
     for (uint32_t i = 0; i < dist.size(); i++) {
         const Group &G = groups[dist[i].group];
         carriers[i] = G.last - G.first;
         covered += carriers[i];
         if (B.keep_membership)
-            for (uint32_t t = G.first; t < G.last; t++) member.push_back({hap_ids[order[t]], i});
+            for (uint32_t t = G.first; t < G.last; t++) local_of[order[t]] = i;
     }
     R.ref_local = -1;
     if (covered < H) {  // haplotypes_with_reference_genome is non-empty (main.rs:129)
@@ -321,14 +363,14 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // the kernels index windows with 29 bits (scan_mfma.hip queue entries)
     for (const Distinct &d : dist)
         if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
-    if (B.keep_membership) {
-        std::sort(member.begin(), member.end());
-        R.nonref_id.resize(member.size());
-        R.nonref_local.resize(member.size());
-        for (size_t i = 0; i < member.size(); i++) {
-            R.nonref_id[i] = member[i].first;
-            R.nonref_local[i] = member[i].second;
-        }
+    if (B.keep_membership) {  // (hap id, local) in ascending hap id: hap_ids' order
+        R.nonref_id.clear();
+        R.nonref_local.clear();
+        for (size_t k = 0; k < hap_ids.size(); k++)
+            if (local_of[k] != UINT32_MAX) {
+                R.nonref_id.push_back(hap_ids[k]);
+                R.nonref_local.push_back(local_of[k]);
+            }
     }
 
     return TFBS_OK;
