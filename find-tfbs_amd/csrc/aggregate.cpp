@@ -153,13 +153,21 @@ static uint32_t encoded_key(const Batch &B, size_t r, uint64_t key) {
     return (e != UINT32_MAX && B.enc_hdr[e].status == 0) ? e : UINT32_MAX;
 }
 
+// A key's per-value sample texts (16-byte slots, len bytes used) and the
+// length of its genotype text.
+struct EncText {
+    char tab[kEncMaxVals + 1][16];
+    uint8_t len[kEncMaxVals + 1];
+    uint64_t total;
+};
+
 // counts_as_genotypes (main.rs:439-498) from a device encoding: the text of
 // each distinct total is built once (with the range multiplicity applied,
 // u32 arithmetic as counts_as_genotypes), a sample's text is the table entry
-// of its code.  Returns 1 (row), 0 (the totals do not vary) or -1 (the
-// multiplicity would wrap the totals: use the host path).
+// of its code (encoded_write).  Returns 1 (row), 0 (the totals do not vary) or
+// -1 (the multiplicity would wrap the totals: use the host path).
 static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t *maf, std::string &info,
-                             std::string &gts) {
+                             EncText &t) {
     const EncHdr &h = B.enc_hdr[e];
     if ((uint64_t)h.hi * mult > UINT32_MAX) return -1;
     if (h.n_vals < 2) return 0;
@@ -170,8 +178,8 @@ static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t
     const uint32_t i3 = (lo * 1000u + hi * 1000u * 3u) / 4u;
     const float lof = (float)lo;
     const float spread = (float)hi - lof;
-    char tab[kEncMaxVals + 1][16];
-    uint8_t len[kEncMaxVals + 1];
+    char(&tab)[kEncMaxVals + 1][16] = t.tab;
+    uint8_t(&len)[kEncMaxVals + 1] = t.len;
     uint64_t cls[3] = {0, 0, 0}, total = 0;
     for (uint32_t k = 0; k < nv; k++) {
         const uint32_t x = vals[k] * mult;
@@ -204,40 +212,87 @@ static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t
     }
     const int m = snprintf(buf, sizeof buf, ";freqs=%u/%u/%u", zero, one, two);
     info.append(buf, (size_t)m);
-    const size_t at = gts.size();
-    gts.resize(at + total + 16);
-    char *dst = &gts[at];
-    const uint8_t *codes = B.enc_codes.data() + B.enc_code_off[e];
-    const uint32_t width = h.width, per = 8 / width, mask = (1u << width) - 1u;
-    for (uint32_t s = 0; s < B.n_samples; s += per) {
-        uint32_t byte = codes[s / per];
-        for (uint32_t q = 0; q < per && s + q < B.n_samples; q++, byte >>= width) {
-            const uint32_t c = byte & mask;
-            memcpy(dst, tab[c], 16);
-            dst += len[c];
-        }
-    }
-    gts.resize(at + total);
+    t.total = total;
     return 1;
 }
 
-// Rows of one region, each without its "<chr>\t<POS>\t" prefix (the POS
-// counter is assigned in order afterwards).  Keys the device encoded
-// (tfbs_batch_encode) are formatted from their value tables and codes; the
-// others from the per-haplotype counts through the membership.
-void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<std::string> &rows) {
+// The genotype text of key e into dst (t.total bytes; up to kEncPad written
+// past it).  Codes of 2 or 4 bits go a whole byte at a time through a table of
+// the byte's concatenated sample texts (16 bytes per sample slot).
+constexpr size_t kEncPad = 64;
+static void encoded_write(const Batch &B, uint32_t e, const EncText &t, char *dst) {
+    const EncHdr &h = B.enc_hdr[e];
+    const uint8_t *codes = B.enc_codes.data() + B.enc_code_off[e];
+    const uint32_t width = h.width, per = 8 / width, mask = (1u << width) - 1u;
+    uint32_t s = 0;
+    if (per > 1) {
+        const uint32_t slot = 16 * per;  // 64 or 32 bytes
+        thread_local char bt[256 * 64];
+        uint8_t bl[256];
+        for (uint32_t v = 0; v < 256; v++) {
+            char *q = bt + v * slot;
+            uint32_t n = 0;
+            for (uint32_t k = 0, x = v; k < per; k++, x >>= width) {
+                const uint32_t c = x & mask;
+                if (c >= h.n_vals) {  // a byte the codes never hold
+                    n = 0;
+                    break;
+                }
+                memcpy(q + n, t.tab[c], t.len[c]);
+                n += t.len[c];
+            }
+            bl[v] = (uint8_t)n;
+        }
+        const uint32_t full = B.n_samples / per;
+        if (slot == 64) {
+            for (uint32_t i = 0; i < full; i++) {
+                const uint32_t v = codes[i];
+                memcpy(dst, bt + v * 64, 64);
+                dst += bl[v];
+            }
+        } else {
+            for (uint32_t i = 0; i < full; i++) {
+                const uint32_t v = codes[i];
+                memcpy(dst, bt + v * 32, 32);
+                dst += bl[v];
+            }
+        }
+        s = full * per;
+    }
+    for (; s < B.n_samples; s += per) {
+        uint32_t byte = codes[s / per];
+        for (uint32_t q = 0; q < per && s + q < B.n_samples; q++, byte >>= width) {
+            const uint32_t c = byte & mask;
+            memcpy(dst, t.tab[c], 16);
+            dst += t.len[c];
+        }
+    }
+}
+
+// Rows of one region appended to out, each without its "<chr>\t<POS>\t" prefix
+// (the POS counter is assigned in order afterwards) and '\n'-terminated; returns
+// the number of rows.  Keys the device encoded (tfbs_batch_encode) are
+// formatted from their value tables and codes straight into out; the others
+// from the per-haplotype counts through the membership.  With `per_row`, each
+// row is handed to it as soon as it is complete and out is cleared (a streaming
+// consumer keeps one row's text, cache-resident, instead of the region's).
+template <class PerRow>
+size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out, PerRow &&per_row) {
     const uint32_t H = 2 * B.n_samples;
     const size_t ri = (size_t)(&R - B.rh.data());
     std::vector<uint32_t> l, r;
     std::unique_ptr<Membership> M;
     std::string info, gts;
+    EncText et;
+    size_t n_rows = 0;
     for (const KeyRef &k : region_keys(B, R)) {
         if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
         uint32_t maf = 0;
         info.clear();
         gts.clear();
         const uint32_t e = encoded_key(B, ri, key_of(B, R, k.slot, k.ik->slot));
-        int made = e == UINT32_MAX ? -1 : encoded_genotypes(B, e, k.ik->mult, &maf, info, gts);
+        int made = e == UINT32_MAX ? -1 : encoded_genotypes(B, e, k.ik->mult, &maf, info, et);
+        const bool direct = made > 0;
         if (made < 0) {
             info.clear();
             gts.clear();
@@ -257,21 +312,35 @@ void region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector
         const uint16_t pid = B.slot_pid[k.slot];
         auto it = B.pats->names.find(pid);
         const std::string &pname = it == B.pats->names.end() ? std::string() : it->second;
-        std::string row;
-        row.reserve(B.beds[k.ik->bed].size() + pname.size() + info.size() + gts.size() + 64);
-        row += B.beds[k.ik->bed];
-        row += ',';
-        row += pname;
+        const uint64_t body = direct ? et.total : gts.size();
+        if (out.capacity() < out.size() + body + 4096)
+            out.reserve(std::max<size_t>(2 * out.capacity(), out.size() + body + 4096));
+        out += B.beds[k.ik->bed];
+        out += ',';
+        out += pname;
         char head[96];
         snprintf(head, sizeof head, ",%llu-%llu\t.\t.\t.\tPASS\t", (unsigned long long)k.ik->s,
                  (unsigned long long)k.ik->e);
-        row += head;
-        row += info;
-        row += "\tGT:DS";
-        row += gts;
-        row += '\n';
-        rows.push_back(std::move(row));
+        out += head;
+        out += info;
+        out += "\tGT:DS";
+        if (direct) {
+            const size_t at = out.size();
+            out.resize(at + body + kEncPad);
+            encoded_write(B, e, et, &out[at]);
+            out.resize(at + body);
+        } else {
+            out += gts;
+        }
+        out += '\n';
+        n_rows++;
+        per_row(out);
     }
+    return n_rows;
+}
+
+size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out) {
+    return region_rows_each(B, R, min_maf, out, [](std::string &) {});
 }
 
 // Row bodies (each row without its "<chr>\t<POS>\t" prefix, '\n'-terminated)
@@ -281,7 +350,7 @@ int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_
     if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
     const size_t n = B.rh.size();
-    std::vector<std::vector<std::string>> rows(n);
+    std::vector<std::string> rows(n);  // each region's rows
     std::atomic<size_t> next(0);
     auto work = [&]() {
         for (size_t j; (j = next.fetch_add(1)) < n;)
@@ -292,11 +361,12 @@ int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_
     work();
     for (auto &t : ts) t.join();
     size_t bytes = out.size();
-    for (auto &v : rows)
-        for (auto &r : v) bytes += r.size();
+    for (auto &v : rows) bytes += v.size();
     out.reserve(bytes);
-    for (auto &v : rows)
-        for (auto &r : v) out += r;
+    for (auto &v : rows) {
+        out += v;
+        std::string().swap(v);
+    }
     return TFBS_OK;
 }
 
@@ -366,17 +436,20 @@ int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chrom
     if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
-    std::vector<std::string> rows;
-    if (B.rh[region].hap_count) tfbs::region_rows(B, B.rh[region], min_maf, rows);
+    std::string bodies;
+    if (B.rh[region].hap_count) tfbs::region_rows(B, B.rh[region], min_maf, bodies);
     const std::string chr = tfbs::strip_chr(chromosome);
     std::string out;
     char head[32];
-    for (auto &r : rows) {
+    for (size_t i = 0; i < bodies.size();) {
+        size_t e = bodies.find('\n', i);
+        e = e == std::string::npos ? bodies.size() : e + 1;
         const int m = snprintf(head, sizeof head, "\t%u\t", *fake);
         out += chr;
         out.append(head, (size_t)m);
-        out += r;
+        out.append(bodies, i, e - i);
         (*fake)++;
+        i = e;
     }
     char *p = (char *)malloc(out.size() + 1);
     if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");
@@ -444,14 +517,14 @@ int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t
     std::atomic<size_t> next(std::min(r0, n));
     std::atomic<uint64_t> rows(0), bytes(0);
     auto work = [&]() {
-        std::vector<std::string> rr;
+        std::string rr;  // reused: one row's text at a time
         uint64_t r = 0, by = 0;
-        for (size_t j; (j = next.fetch_add(1)) < n;) {
-            rr.clear();
-            if (B.rh[j].hap_count) tfbs::region_rows(B, B.rh[j], min_maf, rr);
-            for (auto &x : rr) by += x.size() + prefix;
-            r += rr.size();
-        }
+        auto take = [&](std::string &row) {
+            by += row.size() + prefix;
+            row.clear();
+        };
+        for (size_t j; (j = next.fetch_add(1)) < n;)
+            if (B.rh[j].hap_count) r += tfbs::region_rows_each(B, B.rh[j], min_maf, rr, take);
         rows += r;
         bytes += by;
     };
