@@ -112,6 +112,7 @@ struct tfbs_ctx {
     DevBuf<DevVarKey> var_keys, enc_keys;
     // per-sample encoding (tfbs_batch_encode)
     DevBuf<uint8_t> enc_memb, enc_codes, enc_packed;
+    tfbs::PinnedBytes enc_memb_host;  // membership rows staged for upload (reused; no zero fill)
     DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
     DevBuf<uint32_t> enc_vals, enc_hist;
@@ -574,8 +575,13 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
         ek_var.push_back(i);
     }
     const size_t nk = ek.size();
-    // membership rows: haplotype id -> distinct index (u8), 2 N bytes per region of [r0, r1)
-    std::vector<uint8_t> memb((r1 - r0) * (size_t)H);
+    // membership rows: haplotype id -> distinct index (u8), 2 N bytes per region of
+    // [r0, r1), written by the host threads into the ctx's pinned staging buffer
+    // (rows of regions with no encoded keys are left unwritten: never read)
+    const size_t mbytes = (r1 - r0) * (size_t)H;
+    int rc;
+    if ((rc = ctx->enc_memb_host.reserve(mbytes))) return rc;
+    uint8_t *const memb = ctx->enc_memb_host.p;
     {
         const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::atomic<size_t> next(r0);
@@ -583,7 +589,7 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
             for (size_t r; (r = next.fetch_add(1)) < r1;) {
                 const RegionH &R = B.rh[r];
                 if (R.hap_count > kEncMaxHaps) continue;
-                uint8_t *row = memb.data() + (r - r0) * (size_t)H;
+                uint8_t *row = memb + (r - r0) * (size_t)H;
                 memset(row, R.ref_local < 0 ? 0 : R.ref_local, H);
                 for (size_t i = 0; i < R.nonref_id.size(); i++) row[R.nonref_id[i]] = (uint8_t)R.nonref_local[i];
             }
@@ -593,8 +599,10 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
         work();
         for (auto &t : ts) t.join();
     }
-    int rc;
-    if ((rc = ctx->enc_memb.put(memb, ctx->stream)) || (rc = ctx->enc_keys.put(ek, ctx->stream)) ||
+    if ((rc = ctx->enc_memb.ensure(mbytes)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->enc_memb.p, memb, mbytes, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = ctx->enc_keys.put(ek, ctx->stream)) ||
         (rc = ctx->enc_hdr.ensure(std::max<size_t>(nk, 1))) ||
         (rc = ctx->enc_vals.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
         (rc = ctx->enc_hist.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||

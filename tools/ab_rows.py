@@ -30,6 +30,13 @@ T.check(L.tfbs_batch_upload(sc.h, b.h))
 T.check(L.tfbs_scan(sc.h, b.h))
 T.check(L.tfbs_ctx_sync(sc.h))
 T.check(L.tfbs_batch_reduce(sc.h, b.h))
+te = []
+for _ in range(a.rounds):  # the bench's device encoding: 512 regions per call
+    t = time.perf_counter()
+    for r0 in range(0, b.num_regions, 512):
+        b.encode(sc, r0, min(b.num_regions, r0 + 512))
+    te.append(time.perf_counter() - t)
+print("encode (512 regions per call) median %.4f s min %.4f s" % (statistics.median(te), min(te)))
 b.encode(sc, 0, b.num_regions)
 ts = []
 for _ in range(a.rounds):
