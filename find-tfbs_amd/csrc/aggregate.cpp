@@ -273,10 +273,12 @@ static void encoded_write(const Batch &B, uint32_t e, const EncText &t, char *ds
 // (the POS counter is assigned in order afterwards) and '\n'-terminated; returns
 // the number of rows.  Keys the device encoded (tfbs_batch_encode) are
 // formatted from their value tables and codes straight into out; the others
-// from the per-haplotype counts through the membership.  With `per_row`, each
-// row is handed to it as soon as it is complete and out is cleared (a streaming
-// consumer keeps one row's text, cache-resident, instead of the region's).
-template <class PerRow>
+// from the per-haplotype counts through the membership.  kStream: each row goes
+// to per_row(head, gts, n) as soon as it is complete, the row being head + the
+// n bytes at gts + '\n'; the genotype text of an encoded key is then written
+// into a reused raw buffer (cache-resident, never zero-filled) and head is the
+// consumer's to clear.
+template <bool kStream, class PerRow>
 size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out, PerRow &&per_row) {
     const uint32_t H = 2 * B.n_samples;
     const size_t ri = (size_t)(&R - B.rh.data());
@@ -324,6 +326,22 @@ size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std:
         out += head;
         out += info;
         out += "\tGT:DS";
+        if (kStream) {
+            thread_local std::unique_ptr<char[]> gbuf;
+            thread_local size_t gcap = 0;
+            const char *tail = gts.data();
+            if (direct) {
+                if (gcap < body + kEncPad) {
+                    gcap = body + kEncPad;
+                    gbuf.reset(new char[gcap]);
+                }
+                encoded_write(B, e, et, gbuf.get());
+                tail = gbuf.get();
+            }
+            n_rows++;
+            per_row(out, tail, (size_t)body);
+            continue;
+        }
         if (direct) {
             const size_t at = out.size();
             out.resize(at + body + kEncPad);
@@ -334,13 +352,12 @@ size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std:
         }
         out += '\n';
         n_rows++;
-        per_row(out);
     }
     return n_rows;
 }
 
 size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out) {
-    return region_rows_each(B, R, min_maf, out, [](std::string &) {});
+    return region_rows_each<false>(B, R, min_maf, out, [](std::string &, const char *, size_t) {});
 }
 
 // Row bodies (each row without its "<chr>\t<POS>\t" prefix, '\n'-terminated)
@@ -519,12 +536,12 @@ int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t
     auto work = [&]() {
         std::string rr;  // reused: one row's text at a time
         uint64_t r = 0, by = 0;
-        auto take = [&](std::string &row) {
-            by += row.size() + prefix;
-            row.clear();
+        auto take = [&](std::string &head, const char *, size_t n) {
+            by += head.size() + n + 1 + prefix;
+            head.clear();
         };
         for (size_t j; (j = next.fetch_add(1)) < n;)
-            if (B.rh[j].hap_count) r += tfbs::region_rows_each(B, B.rh[j], min_maf, rr, take);
+            if (B.rh[j].hap_count) r += tfbs::region_rows_each<true>(B, B.rh[j], min_maf, rr, take);
         rows += r;
         bytes += by;
     };
