@@ -50,7 +50,7 @@ inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint3
     }
     const uint64_t k = key_of(B, R, slot, range_slot);
     const uint32_t off = B.var_off[k];
-    return off == UINT32_MAX ? B.key_first[k] : B.var_counts[off + local];
+    return off == UINT32_MAX ? B.key_first[k] : reinterpret_cast<const uint32_t *>(B.var_counts.data())[off + local];
 }
 
 // Some distinct haplotype matched (the key exists in the reference's HashMap).

@@ -77,7 +77,7 @@ struct Batch {
     std::vector<uint32_t> key_first;
     std::vector<uint8_t> key_flags;
     std::vector<uint32_t> var_off;        // UINT32_MAX unless the key varies
-    std::vector<uint32_t> var_counts;
+    PinnedBytes var_counts;  // u32 counts, downloaded into pinned memory
     std::vector<DevVarKey> var_keys;      // the varying keys in reduction order
     std::vector<uint32_t> var_idx;        // key -> index in var_keys, UINT32_MAX unless it varies
     bool reduced = false;

@@ -527,7 +527,7 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
                 total += rg.hap_count;
             }
     }
-    B.var_counts.resize(total);
+    if ((rc = B.var_counts.reserve(total * 4))) return rc;
     B.var_keys = vk;
     B.enc_r0 = B.enc_r1 = 0;
     B.enc_idx.clear();
@@ -536,7 +536,7 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         if ((rc = launch_key_gather(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->var_keys.p,
                                     (uint32_t)vk.size(), ctx->var_counts.p, ctx->stream)))
             return rc;
-        HIP_TRY(hipMemcpyAsync(B.var_counts.data(), ctx->var_counts.p, total * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(B.var_counts.p, ctx->var_counts.p, total * 4, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.reduced = true;
