@@ -13,10 +13,20 @@ region to its distinct haplotypes and packs them into HBM (untimed, as the
 reference builds them before scanning); one timed step = one tfbs_scan over
 every distinct haplotype x pattern window of the rank's batch.
 
-Multi-GPU (torchrun, one rank per GPU): rank r scans regions [r R, (r+1) R) --
-the static contiguous region shard tfbs_run --devices uses,
-weak scaling, no collective on the data path; a barrier + max-over-ranks bracket
-the timed region.
+Multi-GPU (one rank per GPU; `--gpus N` without WORLD_SIZE starts torchrun with
+N ranks itself, before anything touches a GPU): weak scaling, no collective on
+the data path; a barrier + max-over-ranks bracket the timed region.
+  --shard regions         rank r scans regions [r R, (r+1) R) -- the static
+                          contiguous region shard tfbs_run --devices uses
+                          (SURVEY.md 8(e)); R = regions per GPU
+  --shard regions_x_pwms  the 2-D region x PWM split (BASELINE config C4): P
+                          pattern shards (--pwm-shards, pattern_id % P, both
+                          strands of a PWM on one rank) x N / P region blocks
+                          of P R regions; rank r = block r // P, pattern shard
+                          r % P; every rank keeps the whole set's windows
+                          (tfbs_batch_set_window_lmax), so the per-key counts
+                          of the P shards of a block are the unsharded run's
+                          (the host merges disjoint pattern_id keys)
 
 Besides the scan-only `value` the line carries an end-to-end leg over the same
 batch (host prep + upload + scan + device key reduction + row formatting), the
@@ -72,6 +82,9 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (profiling passes)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the timing reductions (gloo: rehearse several ranks on one GPU)")
+    ap.add_argument("--shard", default="regions", choices=["regions", "regions_x_pwms"])
+    ap.add_argument("--pwm-shards", type=int, default=None,
+                    help="pattern shards of --shard regions_x_pwms (default 2 on an even rank count, else 1)")
     a = ap.parse_args()
     w = WORKLOADS[a.workload]
     for name, v in zip(("samples", "regions", "pwms", "length_config", "indel_pct", "seed"), w):
@@ -150,6 +163,9 @@ def cpu_baseline(T, ps, args, budget_s):
         t1[scan_only] = max(time.perf_counter() - t0, 1e-3)
     sizes = {(so, th): max(th, min(args.regions, int(th * budget_s / t1[so])))
              for so in (True, False) for th in (1, tmax)}
+    ncpu = os.cpu_count() or 1
+    if ncpu > tmax:  # every host CPU the box shows (its share is tmax): the scan-only leg's sample, ncpu threads
+        sizes[(True, ncpu)] = max(ncpu, sizes[(True, tmax)])
     n_max = max(sizes.values())
     regs += [gen(j) for j in range(1, n_max)]
     matrix = {}
@@ -169,7 +185,15 @@ def cpu_baseline(T, ps, args, budget_s):
             "phase_thread_s": {"load_diffs_patch": phases[0], "find_all_matches": phases[1],
                                "count_rows": phases[2]}}
     best = matrix["scan_t%d" % tmax]
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = ncpu
     return {"value": best["windows_per_s"], "unit": "windows/s", "cores": tmax, "kind": "port",
+            "host_cpus": {"os_cpu_count": ncpu, "sched_affinity": affinity, "share_used": tmax,
+                          "note": "the GPU box shows every host CPU but grants one GPU's job a share of %d; "
+                                  "scan_t%d runs the scan-only sample on all %d" % (tmax, ncpu, ncpu)
+                          if ncpu > tmax else "all host CPUs used"},
             "sample": "scan-only leg on %d threads: %d of the %d regions of this workload (%d samples, %d "
                       "patterns, %.3g windows); oracle/tfbs_oracle.c (C restatement of the reference scan; gcc "
                       "-O3 -march=x86-64-v3), inputs generated before the clock; matrix: scan-only and "
@@ -178,12 +202,32 @@ def cpu_baseline(T, ps, args, budget_s):
             "matrix": matrix}
 
 
-def shard_batch(T, ps, args, rank):
-    """Rank r's share: merged regions [r R, (r+1) R) of the synthetic
-    chromosome, reduced to distinct haplotypes and packed on the host (with the
-    haplotype -> distinct membership the rows need)."""
-    batch = T.RegionBatch(ps, args.samples, keep_membership=True)
-    batch.synth_fill(args.seed, rank * args.regions, args.regions, args.indel_pct)
+def shard_plan(args, rank, world):
+    """(first region, regions, pattern shard index, pattern shards) of rank r (SURVEY.md
+    8(e)): the 1-D region shard, or the 2-D region x PWM split (module docstring)."""
+    if getattr(args, "shard", "regions") == "regions_x_pwms":
+        p = args.pwm_shards or (2 if world % 2 == 0 else 1)
+        if p < 1 or world % p:
+            raise SystemExit("--shard regions_x_pwms: %d ranks are not a multiple of --pwm-shards %d" % (world, p))
+        block = rank // p
+        return block * p * args.regions, p * args.regions, rank % p, p
+    return rank * args.regions, args.regions, 0, 1
+
+
+def shard_patterns(T, ps, part, parts):
+    """The rank's pattern shard: pattern_id % parts == part (both strands of a PWM
+    share their id, pattern.rs:73-77)."""
+    return ps if parts == 1 else ps.subset(lambda pid: pid % parts == part)
+
+
+def shard_batch(T, ps, args, rank, world=1, window_lmax=None):
+    """Rank r's share: its merged regions of the synthetic chromosome
+    (shard_plan), reduced to distinct haplotypes and packed on the host (with the
+    haplotype -> distinct membership the rows need); ps is the rank's pattern shard,
+    window_lmax the whole pattern set's L_max when it is a shard."""
+    first, count, _, _ = shard_plan(args, rank, world)
+    batch = T.RegionBatch(ps, args.samples, keep_membership=True, window_lmax=window_lmax)
+    batch.synth_fill(args.seed, first, count, args.indel_pct)
     return batch
 
 
@@ -201,11 +245,32 @@ def job_totals(dist, device, elapsed, sums):
     return (tl if isinstance(elapsed, list) else tl[0]), [float(x) for x in w.tolist()]
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start the same command under
+    torch.distributed.run with N ranks on this node as a child process -- nothing here
+    has touched a GPU -- and exit with its status."""
+    import socket
+    import subprocess
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     dist = None
     if world > 1:
         import torch
@@ -223,13 +288,15 @@ def main():
     threads = max(1, min(CPU_THREADS_MAX, os.cpu_count() or 1))
     work = tempfile.mkdtemp(prefix="tfbs_bench_%d_" % rank)
     names = T.synth_write_pwms(work, args.pwms, args.length_config, args.seed)
-    ps = T.parse_pwm_files(os.path.join(work, "pwms.txt"), os.path.join(work, "thr"), args.threshold, names)
+    ps_all = T.parse_pwm_files(os.path.join(work, "pwms.txt"), os.path.join(work, "thr"), args.threshold, names)
+    first, count, part, parts = shard_plan(args, rank, world)
+    ps = shard_patterns(T, ps_all, part, parts)
     sc = T.Scanner(ps, device=local)
     L = T.lib()
 
     # ---- end-to-end leg, once: host prep, upload, scan, device key reduction, rows
     t_prep = time.perf_counter()
-    batch = shard_batch(T, ps, args, rank)
+    batch = shard_batch(T, ps, args, rank, world, window_lmax=ps_all.max_length if parts > 1 else None)
     t_prep = time.perf_counter() - t_prep
     gen_s, build_s, commit_s, fill_s = batch.prep_seconds()
     t_up = time.perf_counter()
@@ -287,6 +354,12 @@ def main():
     t_dense = time.perf_counter() - t_dense
 
     e2e_s = fill_s + t_up + t_scan1 + t_red + t_enc + t_rows
+    per_rank_ms = [elapsed * 1e3 / args.steps]
+    if dist is not None:  # every rank's ms per step, as the collective saw them
+        import torch
+        g = [torch.zeros(1, dtype=torch.float64, device=rdev) for _ in range(world)]
+        dist.all_gather(g, torch.tensor(per_rank_ms, dtype=torch.float64, device=rdev))
+        per_rank_ms = [float(x.item()) for x in g]
     (elapsed, e2e_max), tot = job_totals(dist, rdev, [elapsed, e2e_s],
                                          [batch.num_windows, batch.num_regions, batch.num_effective_windows,
                                           n_rows, n_row_bytes, batch.num_scan_windows])
@@ -347,10 +420,13 @@ def main():
             "config": {
                 "workload": args.workload + ("-custom" if args.custom else ""),
                 "samples": args.samples, "haplotypes": 2 * args.samples, "regions_per_gpu": args.regions,
+                "regions_per_rank_batch": count,
                 "region_bp": 201, "pwms": args.pwms, "patterns": len(ps), "threshold": args.threshold,
                 "indel_pct": args.indel_pct, "seed": args.seed,
                 "distinct_haplotypes_per_gpu": batch.num_haplotypes,
-                "windows_per_step": int(tot_windows), "parallelism": "region shard x%d" % world,
+                "windows_per_step": int(tot_windows),
+                "parallelism": ("region shard x%d" % world if parts == 1 else
+                                "region x PWM shard: %d region blocks x %d pattern shards" % (world // parts, parts)),
                 "scan_path": path,
                 "scanned_windows_per_step": int(tot_scan),
             },
@@ -359,6 +435,8 @@ def main():
                           "region's reference window take the reference window's result (reference-window "
                           "reuse, exact; TFBS_DEDUP=0 scans them all), scanned_windows_per_s counts the "
                           "windows the kernels read",
+            "ranks": {"world_size": world, "backend": args.dist_backend if dist is not None else None,
+                      "ms_per_step": per_rank_ms},
             "scanned_windows_per_s": tot_scan * steps / elapsed,
             "scan_regions_per_s": tot_regions * steps / elapsed,
             "effective_windows_per_s": tot_eff * steps / elapsed,

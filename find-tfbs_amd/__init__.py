@@ -155,6 +155,13 @@ class PatternSet:
         check(lib().tfbs_patterns_mfma_bound(self.h, i, codes, C.byref(out)))
         return {n: getattr(out, n) for n, _ in out._fields_}
 
+    def subset(self, keep_pattern_id):
+        """A new PatternSet of the patterns whose pattern_id passes keep_pattern_id (both
+        strands of a PWM share an id, so they stay together): a pattern shard of SURVEY.md
+        8(e)'s region x PWM split.  Batches scanning it pass the whole set's max_length to
+        RegionBatch(window_lmax=...) so their windows are the unsharded run's."""
+        return PatternSet.from_patterns([p for p in self.to_list() if keep_pattern_id(p.pattern_id)])
+
     def plan_stats(self, tile_blocks=20, mfma=False):
         """Host-side summary of the device plan (octet/quad/generic/MFMA strands, tiles)."""
         st = _capi.tfbs_plan_stats()
@@ -280,12 +287,14 @@ class RegionBatch:
 
     VECTOR_END = -2147483647
 
-    def __init__(self, patterns, n_samples, keep_membership=True):
+    def __init__(self, patterns, n_samples, keep_membership=True, window_lmax=None):
         self.patterns = patterns
         self.n_samples = n_samples
         self.h = C.c_void_p()
         check(lib().tfbs_batch_create(patterns.h, n_samples, 1 if keep_membership else 0, C.byref(self.h)))
         self.beds = []
+        if window_lmax is not None:  # a pattern shard: the whole set's windows (tfbs_batch_set_window_lmax)
+            check(lib().tfbs_batch_set_window_lmax(self.h, window_lmax))
 
     def __del__(self):
         if getattr(self, "h", None):
@@ -438,6 +447,18 @@ class RegionBatch:
         """tfbs_batch_region_digest: the region's keys at the distinct-haplotype level."""
         d = C.c_uint64()
         check(lib().tfbs_batch_region_digest(self.h, region, C.byref(d)))
+        return d.value
+
+    def key_digest_sum(self, region):
+        """tfbs_batch_region_key_digest_sum: order-free; pattern shards add up to the whole."""
+        d = C.c_uint64()
+        check(lib().tfbs_batch_region_key_digest_sum(self.h, region, C.byref(d)))
+        return d.value
+
+    def input_digest(self, region):
+        """tfbs_batch_region_input_digest: what the host prep packed for the region."""
+        d = C.c_uint64()
+        check(lib().tfbs_batch_region_input_digest(self.h, region, C.byref(d)))
         return d.value
 
     def format_rows(self, chromosome, min_maf=0, threads=1, r0=0, r1=None):

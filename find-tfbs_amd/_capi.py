@@ -82,6 +82,7 @@ SIGNATURES = [
     ("tfbs_batch_create", C.c_int, [vp, C.c_uint32, C.c_int, C.POINTER(vp)]),
     ("tfbs_batch_destroy", None, [vp]),
     ("tfbs_batch_add_bed", C.c_int, [vp, C.c_char_p]),
+    ("tfbs_batch_set_window_lmax", C.c_int, [vp, C.c_uint32]),
     ("tfbs_batch_region_ext", C.c_int, [vp, C.c_uint64, C.c_uint64, u64p, u64p]),
     ("tfbs_batch_region_begin", C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_char_p, C.c_size_t]),
     ("tfbs_batch_region_add_inner", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64]),
@@ -108,6 +109,8 @@ SIGNATURES = [
     ("tfbs_batch_region_rows", C.c_int, [vp, C.c_size_t, C.c_char_p, C.c_uint32, u32p, C.POINTER(C.c_void_p),
                                          C.POINTER(C.c_size_t)]),
     ("tfbs_batch_region_digest", C.c_int, [vp, C.c_size_t, u64p]),
+    ("tfbs_batch_region_key_digest_sum", C.c_int, [vp, C.c_size_t, u64p]),
+    ("tfbs_batch_region_input_digest", C.c_int, [vp, C.c_size_t, u64p]),
     ("tfbs_batch_region_stats", C.c_int, [vp, C.c_size_t, u32p, u32p]),
     ("tfbs_batch_format_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, u64p,
                                          u64p]),

@@ -509,6 +509,70 @@ int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *diges
     return TFBS_OK;
 }
 
+namespace {
+uint64_t mix64(uint64_t h, uint64_t x) {
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
+}
+}  // namespace
+
+int tfbs_batch_region_key_digest_sum(const tfbs_batch *b, size_t region, uint64_t *digest) {
+    if (!b || !digest) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    const tfbs::RegionH &R = B.rh[region];
+    uint64_t sum = 0;
+    for (const auto &k : tfbs::region_keys(B, R)) {  // one hash per key, added: order-free
+        uint64_t h = 0x2545F4914F6CDD1Dull;
+        h = mix64(h, k.ik->bed);
+        h = mix64(h, k.ik->s);
+        h = mix64(h, k.ik->e);
+        h = mix64(h, k.ik->mult);
+        h = mix64(h, B.slot_pid[k.slot]);
+        for (uint32_t l = 0; l < R.hap_count; l++) h = mix64(h, tfbs::count_of(B, R, l, k.slot, k.ik->slot));
+        sum += h;
+    }
+    *digest = sum;
+    return TFBS_OK;
+}
+
+int tfbs_batch_region_input_digest(const tfbs_batch *b, size_t region, uint64_t *digest) {
+    if (!b || !digest) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
+    const tfbs::RegionH &R = B.rh[region];
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    for (uint64_t x : {R.ms, R.me, R.es, R.ee, (uint64_t)R.hap_count, (uint64_t)(int64_t)R.ref_local,
+                       (uint64_t)R.n_variants})
+        h = mix64(h, x);
+    for (const auto &k : R.keys) {
+        h = mix64(h, k.bed);
+        h = mix64(h, k.s);
+        h = mix64(h, k.e);
+        h = mix64(h, k.mult);
+    }
+    for (size_t i = 0; i < R.nonref_id.size(); i++) h = mix64(h, ((uint64_t)R.nonref_id[i] << 32) | R.nonref_local[i]);
+    for (uint32_t l = 0; l < R.hap_count; l++) {  // the packed bases, N masks and positions of each distinct haplotype
+        const tfbs::DevHap &d = B.haps[R.hap_begin + l];
+        h = mix64(h, d.len);
+        h = mix64(h, d.flags & (tfbs::HAP_HAS_N | tfbs::HAP_HAS_POS));
+        h = mix64(h, B.hap_carriers[R.hap_begin + l]);
+        for (uint32_t w = 0; w < (d.len + 15) / 16; w++) {
+            uint32_t x = B.words[d.word_off + w];
+            if (16 * w + 16 > d.len) x &= (1u << (2 * (d.len - 16 * w))) - 1;  // bits past the end are padding
+            h = mix64(h, x);
+        }
+        if (d.flags & tfbs::HAP_HAS_N)
+            for (uint32_t w = 0; w < (d.len + 31) / 32; w++) h = mix64(h, B.nmask[d.nmask_off + w]);
+        if (d.flags & tfbs::HAP_HAS_POS)
+            for (uint32_t i = 0; i < d.len; i++) h = mix64(h, (uint32_t)B.posrel[d.pos_off + i]);
+    }
+    *digest = h;
+    return TFBS_OK;
+}
+
 int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t *fake, char **text,
                     size_t *len) {
     if (!b || !chromosome || !fake || !text || !len) return tfbs::fail(TFBS_E_ARG, "null argument");

@@ -627,9 +627,17 @@ int tfbs_batch_add_bed(tfbs_batch *b, const char *basename) {
     return (int)b->b.beds.size() - 1;
 }
 
+int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax) {
+    if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (lmax < b->b.pats->max_length()) return tfbs::fail(TFBS_E_ARG, "window L_max below the longest pattern");
+    if (!b->b.rh.empty() || b->b.open) return tfbs::fail(TFBS_E_STATE, "regions already added");
+    b->b.window_lmax = lmax;
+    return TFBS_OK;
+}
+
 int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t ms, uint64_t me, uint64_t *es, uint64_t *ee) {
     if (!b || !es || !ee) return tfbs::fail(TFBS_E_ARG, "null argument");
-    uint64_t L = b->b.pats->max_length();
+    uint64_t L = b->b.lmax();
     if (ms + 1 < L) return tfbs::fail(TFBS_E_RANGE, "region start closer than the PWM length to 0 (main.rs:407)");
     *es = ms + 1 - L;  // u64 wrapping as in --release (L = 0 gives [s+1, e-1])
     *ee = me + L - 1;

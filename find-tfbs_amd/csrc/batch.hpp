@@ -110,6 +110,13 @@ struct Batch {
     std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> cur_inner;
     int status = TFBS_OK;
 
+    // L_max of the halo-extended window (main.rs:404-407): the pattern set's
+    // longest strand unless set wider (tfbs_batch_set_window_lmax: a shard of
+    // the patterns keeps the whole set's windows, so its counts are the whole
+    // run's for its pattern_ids)
+    uint32_t window_lmax = 0;
+    uint32_t lmax() const { return window_lmax ? window_lmax : pats->max_length(); }
+
     uint64_t device_bytes() const;
 };
 

@@ -317,7 +317,7 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
     for (size_t i = 0; i < B.beds.size(); i++)
         if (B.beds[i] == "synthetic.bed") bed = (int)i;
     if (bed < 0) bed = tfbs_batch_add_bed(b, "synthetic.bed");
-    const uint32_t lmax = B.pats->max_length();
+    const uint32_t lmax = B.lmax();
     const char *env = getenv("TFBS_HOST_THREADS");
     uint32_t T = env && *env ? (uint32_t)atoi(env) : std::thread::hardware_concurrency();
     T = std::max(1u, std::min(16u, T));

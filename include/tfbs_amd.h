@@ -170,6 +170,11 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
 void tfbs_batch_destroy(tfbs_batch *b);
 /* Registers a BED source by basename (bed.rs:49-60); returns its index >= 0. */
 int tfbs_batch_add_bed(tfbs_batch *b, const char *basename);
+/* main.rs:404: L_max of the halo-extended windows, if wider than the pattern set's
+ * longest strand (>= it; before the first region).  A batch scanning a shard of the
+ * pattern_ids passes the whole set's L_max so that its windows, distinct haplotypes
+ * and counts are those of the unsharded run (SURVEY.md 8(e) region x PWM shard). */
+int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax);
 /* main.rs:404-407: the halo-extended window of a merged region. */
 int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t merged_start, uint64_t merged_end, uint64_t *ext_start,
                           uint64_t *ext_end);
@@ -253,6 +258,15 @@ int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chrom
  * from the dense download and the device reduction, or from a sharded and an
  * unsharded batch, mean equal count_matches_by_sample maps (main.rs:500-534). */
 int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
+/* Order-free digest: the sum over the region's keys of a hash of the key (bed,
+ * range, multiplicity, pattern_id) and its distinct haplotypes' counts.  Batches
+ * over disjoint pattern_id shards of one pattern set (same windows: see
+ * tfbs_batch_set_window_lmax) sum to the unsharded batch's digest. */
+int tfbs_batch_region_key_digest_sum(const tfbs_batch *b, size_t region, uint64_t *digest);
+/* Digest of what the host prep packed for a region (window, inner keys, distinct
+ * haplotypes' bases / N masks / positions, carriers, membership): equal for the
+ * same region built in any batch or shard. */
+int tfbs_batch_region_input_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
 /* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
 int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
 /* Formats the rows of regions [r0, r1) (main.rs:415-429) on `threads` host threads and

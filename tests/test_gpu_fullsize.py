@@ -250,3 +250,47 @@ def test_c4_shards_equal_unsharded(tmp_path):
         assert checked >= 40
     finally:
         sc.close()
+
+
+def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
+    """C4's 2-D split (bench.py --shard regions_x_pwms): one region block of the C4
+    generator scanned with all 600 PWMs and as 2 pattern_id shards (both strands of a
+    PWM together, the whole set's window L_max): per region the shards' order-free key
+    digests add up to the unsharded digest, and their rows together are its rows."""
+    import bench
+
+    n_samples, _, _, _, indel, seed = C4
+    n_regions = 3000
+    ps = _patterns(tmp_path, C4)
+    whole = T.RegionBatch(ps, n_samples)
+    whole.synth_fill(seed, 0, n_regions, indel)
+    sc = T.Scanner(ps)
+    try:
+        whole.scan(sc, reduce=True)
+        want = [whole.key_digest_sum(r) for r in range(n_regions)]
+        want_rows = [sorted(_strip_pos(whole.region_rows(r, "chr1")[0])) for r in range(n_regions)]
+    finally:
+        sc.close()
+    del whole
+    got = [0] * n_regions
+    got_rows = [[] for _ in range(n_regions)]
+    pids = []
+    for part in range(2):
+        sub = bench.shard_patterns(T, ps, part, 2)
+        pids.append({p.pattern_id for p in sub.to_list()})
+        b = T.RegionBatch(sub, n_samples, window_lmax=ps.max_length)
+        b.synth_fill(seed, 0, n_regions, indel)
+        sc = T.Scanner(sub)
+        try:
+            b.scan(sc, reduce=True)
+            for r in range(n_regions):
+                got[r] = (got[r] + b.key_digest_sum(r)) % (1 << 64)
+                got_rows[r] += _strip_pos(b.region_rows(r, "chr1")[0])
+        finally:
+            sc.close()
+        del b
+    assert not pids[0] & pids[1] and len(pids[0] | pids[1]) == 600
+    bad = [r for r in range(n_regions) if got[r] != want[r]]
+    assert not bad, bad[:10]
+    assert [sorted(x) for x in got_rows] == want_rows
+    assert sum(len(x) for x in want_rows) > 1000
