@@ -269,6 +269,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if rank != 0:  # one JSON line on stdout: the other ranks' output (library chatter included) to stderr
+        sys.stdout.flush()
+        os.dup2(2, 1)
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     dist = None

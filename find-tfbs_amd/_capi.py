@@ -73,6 +73,7 @@ SIGNATURES = [
     ("tfbs_ctx_create", C.c_int, [C.c_int, vp, C.POINTER(vp)]),
     ("tfbs_ctx_destroy", None, [vp]),
     ("tfbs_ctx_sync", C.c_int, [vp]),
+    ("tfbs_ctx_set_host_threads", C.c_int, [vp, C.c_uint32]),
     ("tfbs_ctx_last_scan_ms", C.c_float, [vp]),
     ("tfbs_ctx_last_scan_launches", C.c_int, [vp]),
     ("tfbs_ctx_last_mfma_ms", C.c_float, [vp]),

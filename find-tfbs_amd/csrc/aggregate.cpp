@@ -220,7 +220,7 @@ static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t
 // past it).  Codes of 2 or 4 bits go a whole byte at a time through a table of
 // the byte's concatenated sample texts (16 bytes per sample slot).
 constexpr size_t kEncPad = 64;
-__attribute__((target("avx2"))) static void encoded_write(const Batch &B, uint32_t e, const EncText &t, char *dst) {
+__attribute__((target_clones("avx2", "default"))) static void encoded_write(const Batch &B, uint32_t e, const EncText &t, char *dst) {
     const EncHdr &h = B.enc_hdr[e];
     const uint8_t *codes = B.enc_codes.data() + B.enc_code_off[e];
     const uint32_t width = h.width, per = 8 / width, mask = (1u << width) - 1u;

@@ -349,8 +349,13 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // reference-window reuse needs the reference's windows: without a reference
     // group, a helper copy is scanned after the distinct haplotypes (no carriers,
     // no keys)
+    // (only when the reference's windows can be reused: it and some distinct
+    // haplotype fit kDedupMaxTiles window tiles)
     out.helper = false;
-    if (B.dedup && R.ref_local < 0 && !dist.empty()) {
+    auto fits = [](size_t n) { return (n + kMWindows - 1) / kMWindows <= kDedupMaxTiles; };
+    bool reusable = false;
+    for (const Distinct &d : dist) reusable = reusable || fits(d.nuc.size());
+    if (B.dedup && R.ref_local < 0 && reusable && fits(I.ref.size())) {
         Distinct d;
         d.nuc = I.ref;
         d.pos.resize(I.ref.size());
@@ -788,7 +793,12 @@ int tfbs_batch_region_end(tfbs_batch *b) {
 }
 
 size_t tfbs_batch_num_regions(const tfbs_batch *b) { return b ? b->b.rh.size() : 0; }
-size_t tfbs_batch_num_haplotypes(const tfbs_batch *b) { return b ? b->b.haps.size() : 0; }
+size_t tfbs_batch_num_haplotypes(const tfbs_batch *b) {  // helper reference copies excluded
+    if (!b) return 0;
+    size_t n = 0;
+    for (const auto &R : b->b.rh) n += R.hap_count;
+    return n;
+}
 uint64_t tfbs_batch_num_windows(const tfbs_batch *b) { return b ? b->b.windows : 0; }
 uint64_t tfbs_batch_num_effective_windows(const tfbs_batch *b) { return b ? b->b.eff_windows : 0; }
 uint64_t tfbs_batch_num_cell_ops(const tfbs_batch *b) { return b ? b->b.cell_ops : 0; }

@@ -41,7 +41,9 @@ struct RegionH {
 struct PinnedBytes {
     uint8_t *p = nullptr;
     size_t cap = 0;
-    int reserve(size_t n);  // keeps nothing; TFBS_E_HIP on failure
+    bool pinned = false;    // hipHostMalloc'd (else malloc'd: page-locked memory ran out)
+    int reserve(size_t n);  // keeps nothing; TFBS_E_NOMEM on failure
+    void release();
     const uint8_t *data() const { return p; }
     ~PinnedBytes();
     PinnedBytes() = default;

@@ -69,12 +69,6 @@ struct tfbs_ctx {
     static constexpr int kSide = 3;
     hipStream_t side[kSide] = {};
     hipEvent_t fork = nullptr, join[kSide] = {};
-    // the matrix-core scan adds into zeroed counts: the idle buffer of a pair is
-    // zeroed on zero_stream beside each scan, for the next one (TFBS_PREZERO)
-    hipStream_t zero_stream = nullptr;
-    hipEvent_t zero_fork = nullptr, zero_ev = nullptr;
-    size_t alt_zero_n = 0;  // counts_alt's elements zeroed (0: none pending)
-    bool prezero = true;
     bool kernel_timed = false;
     float last_kernel_ms = 0.f;
     const Patterns *pats = nullptr;
@@ -86,14 +80,27 @@ struct tfbs_ctx {
     DevBuf<DevPattern> gen_pats;
     DevBuf<DevTile> fast_tiles, gen_tiles;
     DevBuf<int32_t> lut, wfull, gen_w, m_image, m_weights, m_meta;
+    DevBuf<uint8_t> slot_mfma;           // Plan::slot_mfma
     DevBuf<uint32_t> cands;              // matrix-core candidate lists (scan.hpp)
-    DevBuf<uint32_t> ref_hits, ref_count, ref_over, ref_over_count;  // reference-window reuse (scan.hpp)
-    uint32_t ref_over_cap = 1u << 16;
+    DevBuf<uint32_t> hitl, hitn;         // matrix-core hit lists (scan.hpp)
+    DevBuf<uint32_t> ref_hits, ref_count;  // reference-window reuse (scan.hpp)
+    DevBuf<uint32_t> spill, over;        // spill records, [0] their count, [1] candidates past the wave lists
+    uint32_t spill_cap = 1u << 16;
+    DevBuf<uint32_t> spill_sorted, spill_bcnt, spill_boff;  // the spill records in region order
     DevBuf<uint32_t> cand_over;  // candidates past the waves' list regions (scan.hpp)
     uint32_t cand_over_cap = 1u << 20;
-    bool debug_over = false;  // TFBS_DEBUG_OVER: print the overflow lists' fill after each scan
+    // the last scan's overflow counters, copied back asynchronously (checked,
+    // and the scan redone with larger lists, before its results are read)
+    uint32_t *over_host = nullptr;       // pinned [spill records, candidates past the lists]
+    hipEvent_t over_ev = nullptr;
+    bool over_pending = false;
+    uint32_t n_spill = 0;                // spill records of the last checked scan
+    HitSrc srcs_host[kMaxHitSrcs] = {};
+    ScanArgs last_margs{};               // the last matrix-core scan's arguments (launch_post_scan)
+    uint32_t n_srcs = 0;
+    DevBuf<HitSrc> srcs;
+    bool debug_over = false;  // TFBS_DEBUG_OVER: print the overflow lists' fill after each check
     uint32_t n_regions = 0;                // of the resident batch
-    uint32_t *ref_count_host = nullptr;    // pinned: the overflow lists' counts (reference hits, candidates)
     uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
@@ -101,22 +108,31 @@ struct tfbs_ctx {
     uint32_t mfma_hpb = 64;         // haplotypes per MFMA workgroup
     uint32_t mfma_group_words = 0;  // packed words of the largest haplotype group (LDS staging)
     // batch image
-    DevBuf<uint32_t> words, nmask, counts, counts_alt;
+    DevBuf<uint32_t> words, nmask, counts;  // counts: dense, for the LUT/generic slots (and tfbs_batch_download)
+    bool counts_live = false;             // counts allocated for the resident batch
     DevBuf<int32_t> posrel, inner;
     DevBuf<DevHap> haps;
     DevBuf<DevRegion> regions;
     DevBuf<unsigned long long> hits;
+    DevBuf<uint32_t> asm_scratch;         // key assembly counters of regions with many distinct haplotypes
     // key reduction (tfbs_batch_reduce)
-    DevBuf<uint32_t> key_first, var_counts;
+    DevBuf<uint32_t> key_first, var_counts, var_tot;
     DevBuf<uint8_t> key_flags;
     DevBuf<DevVarKey> var_keys, enc_keys;
+    uint32_t var_keys_cap = 1u << 16;
+    uint64_t var_cap = 1u << 24;
+    uint32_t *var_tot_host = nullptr;    // pinned
     // per-sample encoding (tfbs_batch_encode)
-    DevBuf<uint8_t> enc_memb, enc_codes, enc_packed;
-    tfbs::PinnedBytes enc_memb_host;  // membership rows staged for upload (reused; no zero fill)
+    DevBuf<uint8_t> enc_codes, enc_packed;
+    DevBuf<uint16_t> enc_pidx, enc_pab;   // per sample its haplotype pair; per pair its distinct indices
+    DevBuf<uint32_t> enc_pcnt, enc_pair_off;
+    tfbs::PinnedBytes enc_memb_host;  // the samples' pair indices staged for upload (reused)
+    uint32_t host_threads = 16;      // host threads of tfbs_batch_encode (tfbs_ctx_set_host_threads)
     DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
     DevBuf<uint32_t> enc_vals, enc_hist;
     const tfbs_batch *resident = nullptr;
+    bool scanned = false;                 // the resident batch has been scanned (its lists exist)
     float last_ms = 0.f;
     int last_launches = 0;
     bool timing_pending = false;
@@ -125,20 +141,28 @@ struct tfbs_ctx {
 namespace tfbs {
 int PinnedBytes::reserve(size_t n) {
     if (n <= cap) return TFBS_OK;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    const hipError_t e = hipHostMalloc((void **)&p, std::max<size_t>(n, 1 << 20), hipHostMallocDefault);
-    if (e != hipSuccess) {
-        p = nullptr;
-        return tfbs::fail(TFBS_E_HIP, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    release();
+    const size_t want = std::max<size_t>(n, 1 << 20);
+    if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) == hipSuccess) {
+        pinned = true;
+    } else {  // page-locked memory exhausted: pageable memory (slower copies, same results)
+        (void)hipGetLastError();
+        p = static_cast<uint8_t *>(malloc(want));
+        pinned = false;
+        if (!p) return tfbs::fail(TFBS_E_NOMEM, "host staging buffer");
     }
-    cap = std::max<size_t>(n, 1 << 20);
+    cap = want;
     return TFBS_OK;
 }
-PinnedBytes::~PinnedBytes() {
-    if (p) (void)hipHostFree(p);
+void PinnedBytes::release() {
+    if (p) {
+        if (pinned) (void)hipHostFree(p);
+        else free(p);
+    }
+    p = nullptr;
+    cap = 0;
 }
+PinnedBytes::~PinnedBytes() { release(); }
 
 }  // namespace tfbs
 
@@ -154,39 +178,20 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
     ScanArgs a{};
     a.haps = ctx->haps.p;
     a.n_haps = n_haps;
+    a.hap_base = 0;
     a.regions = ctx->regions.p;
     a.inner = ctx->inner.p;
     a.words = ctx->words.p;
     a.nmask = ctx->nmask.p;
     a.posrel = ctx->posrel.p;
-    a.counts = ctx->counts.p;
+    a.counts = ctx->counts_live ? ctx->counts.p : nullptr;
     a.haps_per_block = ctx->haps_per_block;
     a.hits = hits;
     a.hits_wpp = hits_wpp;
     a.n_patterns_total = (uint32_t)ctx->pats->pats.size();
     int launches = 0;
-    if (!P.m_supers.empty()) {  // atomic adds: zero its slots first (the other kernels store theirs)
-        if (ctx->counts.n) {
-            const size_t need = ctx->counts.n;
-            if (ctx->alt_zero_n >= need) {  // zeroed beside the previous scan
-                std::swap(ctx->counts, ctx->counts_alt);
-                ctx->counts.n = need;
-                HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->zero_ev, 0));
-            } else {
-                HIP_TRY(hipMemsetAsync(ctx->counts.p, 0, need * 4, ctx->stream));
-            }
-            ctx->alt_zero_n = 0;
-            a.counts = ctx->counts.p;
-            if (ctx->prezero) {  // the other buffer for the next scan (its last reader is already queued)
-                int rc;
-                if ((rc = ctx->counts_alt.ensure(need))) return rc;
-                HIP_TRY(hipEventRecord(ctx->zero_fork, ctx->stream));
-                HIP_TRY(hipStreamWaitEvent(ctx->zero_stream, ctx->zero_fork, 0));
-                HIP_TRY(hipMemsetAsync(ctx->counts_alt.p, 0, need * 4, ctx->zero_stream));
-                HIP_TRY(hipEventRecord(ctx->zero_ev, ctx->zero_stream));
-                ctx->alt_zero_n = need;
-            }
-        }
+    ctx->n_srcs = 0;
+    if (!P.m_supers.empty()) {  // sparse hits: no count matrix to zero
         ScanArgs m = a;
         m.msupers = ctx->m_supers.p;
         m.n_msupers = (uint32_t)P.m_supers.size();
@@ -194,28 +199,34 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.mweights = ctx->m_weights.p;
         m.mmeta = ctx->m_meta.p;
         m.haps_per_block = ctx->mfma_hpb;
-        // one candidate region per scan workgroup (super tile x haplotype group)
-        const uint64_t n_regions = (uint64_t)P.m_supers.size() * ((n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb);
+        // one candidate list and one hit list per scan workgroup (super tile x haplotype group)
+        const uint64_t n_wg = (uint64_t)P.m_supers.size() * ((n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb);
         int rc;
-        if ((rc = ctx->cands.ensure(n_regions * ctx->cand_cap * kCandWords))) return rc;
+        if ((rc = ctx->cands.ensure(n_wg * ctx->cand_cap * kCandWords)) ||
+            (rc = ctx->hitl.ensure(n_wg * ctx->cand_cap * 2)) || (rc = ctx->hitn.ensure(n_wg * (kMBlockWaves))))
+            return rc;
         m.cands = ctx->cands.p;
         m.cand_cap = ctx->cand_cap;
+        m.hitl = ctx->hitl.p;
+        m.hitn = ctx->hitn.p;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
         if ((rc = ctx->ref_count.ensure(nr)) || (rc = ctx->ref_hits.ensure((size_t)nr * kRefPerRegion * 2)) ||
-            (rc = ctx->ref_over_count.ensure(2)) || (rc = ctx->ref_over.ensure((size_t)ctx->ref_over_cap * 3)) ||
-            (rc = ctx->cand_over.ensure((size_t)ctx->cand_over_cap * 3)))
+            (rc = ctx->over.ensure(2)) || (rc = ctx->spill.ensure((size_t)ctx->spill_cap * 3)) ||
+            (rc = ctx->cand_over.ensure((size_t)ctx->cand_over_cap * 3)) ||
+            (rc = ctx->spill_sorted.ensure((size_t)ctx->spill_cap * 3)) || (rc = ctx->spill_bcnt.ensure(nr + 1)) ||
+            (rc = ctx->spill_boff.ensure(nr + 1)))
             return rc;
         m.dedup = 1;
         m.n_regions = ctx->n_regions;
         m.ref_hits = ctx->ref_hits.p;
         m.ref_count = ctx->ref_count.p;
-        m.ref_over = ctx->ref_over.p;
-        m.ref_over_count = ctx->ref_over_count.p;
-        m.ref_over_cap = ctx->ref_over_cap;
+        m.spill = ctx->spill.p;
+        m.over = ctx->over.p;
+        m.spill_cap = ctx->spill_cap;
         m.cand_over = ctx->cand_over.p;
         m.cand_over_cap = ctx->cand_over_cap;
         HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
-        HIP_TRY(hipMemsetAsync(ctx->ref_over_count.p, 0, 8, ctx->stream));
+        HIP_TRY(hipMemsetAsync(ctx->over.p, 0, 8, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
@@ -224,7 +235,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             streams[i + 1] = ctx->side[i];
         }
         const int n = launch_mfma(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words, n_haps,
-                                  streams, tfbs_ctx::kSide + 1);
+                                  streams, tfbs_ctx::kSide + 1, ctx->srcs_host, &ctx->n_srcs);
         if (n < 0) return n;
         for (int i = 0; i < tfbs_ctx::kSide; i++) {
             HIP_TRY(hipEventRecord(ctx->join[i], ctx->side[i]));
@@ -233,9 +244,15 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
-        const int f = launch_ref_fixup(m, ctx->stream);
-        if (f < 0) return f;
-        launches += f;
+        ctx->last_margs = m;  // the overflow candidates are rescored when the results are read (check_overflow)
+        if ((rc = ctx->srcs.ensure(kMaxHitSrcs))) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->srcs.p, ctx->srcs_host, sizeof(ctx->srcs_host), hipMemcpyHostToDevice,
+                               ctx->stream));
+        // the overflow counters, for the check before the results are read
+        if (!ctx->over_host) HIP_TRY(hipHostMalloc((void **)&ctx->over_host, 8, hipHostMallocDefault));
+        HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipEventRecord(ctx->over_ev, ctx->stream));
+        ctx->over_pending = true;
     }
     if (!P.fast_tiles.empty()) {
         ScanArgs f = a;
@@ -261,6 +278,82 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
     return launches;
 }
 
+// The last scan's overflow lists must have held every entry (a dropped
+// candidate may hide a hit, a dropped spill record is a lost count): read the
+// counters copied back after it and, if one overflowed, grow the lists and scan
+// again.  Runs before anything reads the scan's results.
+// The last scan's overflow lists must have held every entry (a dropped
+// candidate may hide a hit, a dropped spill record is a lost count): read the
+// counters copied back after it and, if one overflowed, grow the lists and scan
+// again.  Then the candidates past the waves' lists are rescored (their hits
+// join the spill list) and the spill records bucketed by region -- work only
+// when there is any.  Runs before anything reads the scan's results.
+static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits = nullptr, uint32_t wpp = 0) {
+    auto grow = [](uint32_t &cap, uint32_t need, uint64_t lim) {
+        if (need > cap) cap = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need * 5 / 4 + 1024);
+    };
+    for (int round = 0; ctx->over_pending; round++) {
+        if (round == 8) return tfbs::fail(TFBS_E_NOMEM, "scan overflow lists still full after 8 rescans");
+        HIP_TRY(hipEventSynchronize(ctx->over_ev));
+        uint32_t nspill = ctx->over_host[0];
+        const uint32_t ncand = ctx->over_host[1];
+        if (ncand > 0 && ncand <= ctx->cand_over_cap) {  // rescore them: their hits add spill records
+            const int f = launch_post_scan(ctx->last_margs, ctx->stream);
+            if (f < 0) return f;
+            HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            nspill = ctx->over_host[0];
+        }
+        if (ctx->debug_over)
+            fprintf(stderr, "tfbs_scan overflow lists: spill %u/%u candidates %u/%u\n", nspill, ctx->spill_cap, ncand,
+                    ctx->cand_over_cap);
+        if (nspill <= ctx->spill_cap && ncand <= ctx->cand_over_cap) {
+            ctx->over_pending = false;
+            ctx->n_spill = nspill;
+            if (nspill) {
+                const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
+                const int rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, nr, ctx->spill_bcnt.p,
+                                                    ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream);
+                if (rc) return rc;
+            }
+            return TFBS_OK;
+        }
+        grow(ctx->spill_cap, ncand > ctx->cand_over_cap ? 2 * std::max(nspill, 1024u) : nspill, UINT32_MAX / 4);
+        grow(ctx->cand_over_cap, ncand, UINT32_MAX / 4);
+        const int n = launch_scan(ctx, n_haps, hits, wpp);
+        if (n < 0) return n;
+    }
+    return TFBS_OK;
+}
+
+static AsmArgs asm_args(tfbs_ctx *ctx, const Batch &B, int mode) {
+    AsmArgs a{};
+    a.haps = ctx->haps.p;
+    a.regions = ctx->regions.p;
+    a.inner = ctx->inner.p;
+    a.mmeta = ctx->m_meta.p;
+    a.slot_mfma = ctx->slot_mfma.p;
+    a.any_dense = (!ctx->plan.fast_tiles.empty() || !ctx->plan.gen_tiles.empty()) ? 1 : 0;
+    a.n_slots = B.n_slots;
+    a.hpb = ctx->mfma_hpb;
+    a.hitl = ctx->hitl.p;
+    a.hitn = ctx->hitn.p;
+    a.cand_cap = ctx->cand_cap;
+    a.srcs = ctx->srcs.p;
+    a.mfma = ctx->plan.m_supers.empty() ? 0 : 1;
+    a.n_srcs = a.mfma ? ctx->n_srcs : 0;
+    a.ref_hits = ctx->ref_hits.p;
+    a.ref_count = ctx->ref_count.p;
+    a.spill_sorted = ctx->spill_sorted.p;
+    a.spill_off = ctx->spill_boff.p;
+    a.n_spill = ctx->plan.m_supers.empty() ? 0 : ctx->n_spill;
+    a.counts = ctx->counts_live ? ctx->counts.p : nullptr;
+    a.dense_base = ctx->counts_live ? 1 : 0;
+    a.scratch = ctx->asm_scratch.p;
+    a.mode = mode;
+    return a;
+}
+
 extern "C" {
 
 int tfbs_device_count(int *n) {
@@ -280,29 +373,31 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
-    ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release();
+    ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release(); ctx->slot_mfma.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
-    ctx->cands.release(); ctx->cand_over.release(); ctx->ref_hits.release(); ctx->ref_count.release(); ctx->ref_over.release();
-    ctx->ref_over_count.release();
-    if (ctx->ref_count_host) (void)hipHostFree(ctx->ref_count_host);
-    ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->counts_alt.release(); ctx->posrel.release();
-    ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release();
-    ctx->key_first.release(); ctx->var_counts.release(); ctx->key_flags.release(); ctx->var_keys.release();
-    ctx->enc_keys.release(); ctx->enc_memb.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
+    ctx->cands.release(); ctx->hitl.release(); ctx->hitn.release(); ctx->cand_over.release(); ctx->ref_hits.release();
+    ctx->ref_count.release(); ctx->spill.release(); ctx->over.release(); ctx->spill_sorted.release();
+    ctx->spill_bcnt.release(); ctx->spill_boff.release(); ctx->srcs.release();
+    if (ctx->over_host) (void)hipHostFree(ctx->over_host);
+    if (ctx->var_tot_host) (void)hipHostFree(ctx->var_tot_host);
+    ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
+    ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
+    ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
+    ctx->var_keys.release();
+    ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
+    ctx->enc_pair_off.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
     if (ctx->evk1) (void)hipEventDestroy(ctx->evk1);
+    if (ctx->over_ev) (void)hipEventDestroy(ctx->over_ev);
     for (int i = 0; i < tfbs_ctx::kSide; i++) {
         if (ctx->side[i]) (void)hipStreamSynchronize(ctx->side[i]);
         if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
         if (ctx->join[i]) (void)hipEventDestroy(ctx->join[i]);
     }
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
-    if (ctx->zero_fork) (void)hipEventDestroy(ctx->zero_fork);
-    if (ctx->zero_ev) (void)hipEventDestroy(ctx->zero_ev);
-    if (ctx->zero_stream) (void)hipStreamDestroy(ctx->zero_stream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -323,8 +418,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 44))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
-    ctx->prezero = env_int("TFBS_PREZERO", 1) != 0;
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
+    ctx->host_threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     ctx->cand_over_cap = (uint32_t)std::max(1, env_int("TFBS_CAND_OVER_CAP", 1 << 20));  // grows on demand (tfbs_scan)
     PlanOptions opt;
     opt.tile_blocks = ctx->tile_blocks;
@@ -347,9 +442,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->zero_stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->zero_fork, hipEventDisableTiming);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->zero_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->over_ev, hipEventDisableTiming);
     for (int i = 0; i < tfbs_ctx::kSide; i++) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
@@ -377,7 +470,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         (rc = ctx->gen_pats.put(P.gen_pats, ctx->stream)) || (rc = ctx->gen_tiles.put(P.gen_tiles, ctx->stream)) ||
         (rc = ctx->gen_w.put(P.gen_w, ctx->stream)) || (rc = ctx->m_image.put(P.m_image, ctx->stream)) ||
         (rc = ctx->m_weights.put(P.m_weights, ctx->stream)) || (rc = ctx->m_meta.put(P.m_meta, ctx->stream)) ||
-        (rc = ctx->m_supers.put(P.m_supers, ctx->stream))) {
+        (rc = ctx->m_supers.put(P.m_supers, ctx->stream)) || (rc = ctx->slot_mfma.put(P.slot_mfma, ctx->stream))) {
         tfbs_ctx_destroy(ctx);
         return rc;
     }
@@ -387,6 +480,12 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
         return tfbs::fail(TFBS_E_HIP, std::string("upload: ") + hipGetErrorString(e));
     }
     *out = ctx;
+    return TFBS_OK;
+}
+
+int tfbs_ctx_set_host_threads(tfbs_ctx *ctx, uint32_t threads) {
+    if (!ctx || threads == 0) return tfbs::fail(TFBS_E_ARG, "null ctx or zero threads");
+    ctx->host_threads = threads;
     return TFBS_OK;
 }
 
@@ -427,16 +526,29 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     if (B.open) return tfbs::fail(TFBS_E_STATE, "region still open");
     if (B.slot_pid != ctx->plan.slot_pid) return tfbs::fail(TFBS_E_STATE, "batch slot order differs from the ctx plan");
     HIP_TRY(hipSetDevice(ctx->device));
+    // key assembly scratch for regions of more distinct haplotypes than its LDS block holds
+    uint64_t big = 0;
+    for (DevRegion &rg : B.regions) {
+        rg.big_off = big;
+        if (rg.hap_count > key_asm_lds_counters()) big += rg.hap_count;
+    }
+    // dense counts only for the LUT / generic kernels' slots (they store theirs)
+    const bool dense = !ctx->plan.fast_tiles.empty() || !ctx->plan.gen_tiles.empty();
     int rc;
     if ((rc = ctx->words.put(B.words, ctx->stream)) || (rc = ctx->nmask.put(B.nmask, ctx->stream)) ||
         (rc = ctx->posrel.put(B.posrel, ctx->stream)) || (rc = ctx->haps.put(B.haps, ctx->stream)) ||
         (rc = ctx->regions.put(B.regions, ctx->stream)) || (rc = ctx->inner.put(B.inner, ctx->stream)) ||
-        (rc = ctx->counts.ensure(B.n_counts)))
+        (rc = ctx->asm_scratch.ensure(std::max<uint64_t>(big, 1))) ||
+        (dense && (rc = ctx->counts.ensure(std::max<uint64_t>(B.n_counts, 1)))))
         return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->counts_live = dense;
     ctx->resident = b;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     ctx->n_regions = (uint32_t)B.regions.size();
+    ctx->over_pending = false;
+    ctx->n_spill = 0;
+    ctx->scanned = false;
     return TFBS_OK;
 }
 
@@ -446,30 +558,11 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipSetDevice(ctx->device));
     HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     ctx->kernel_timed = false;
-    int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
+    // asynchronous: the overflow lists are checked (and the scan redone if one
+    // overflowed) when its results are read (tfbs_batch_reduce / download)
+    const int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
-    // the overflow lists (reference hits, candidates) must have held every entry:
-    // otherwise grow them and scan again
-    for (int round = 0; !ctx->plan.m_supers.empty(); round++) {
-        if (!ctx->ref_count_host) HIP_TRY(hipHostMalloc((void **)&ctx->ref_count_host, 8, hipHostMallocDefault));
-        HIP_TRY(hipMemcpyAsync(ctx->ref_count_host, ctx->ref_over_count.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        const uint32_t nref = ctx->ref_count_host[0], ncand = ctx->ref_count_host[1];
-        if (ctx->debug_over)
-            fprintf(stderr, "tfbs_scan overflow lists: reference hits %u/%u candidates %u/%u\n", nref,
-                    ctx->ref_over_cap, ncand, ctx->cand_over_cap);
-        if (nref <= ctx->ref_over_cap && ncand <= ctx->cand_over_cap) break;
-        // a dropped candidate may have been a reference hit: the next scan is checked too
-        if (round == 8) return tfbs::fail(TFBS_E_NOMEM, "scan overflow lists still full after 8 rescans");
-        auto grow = [](uint32_t &cap, uint32_t need, uint64_t lim) {
-            if (need > cap) cap = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need * 5 / 4 + 1024);
-        };
-        grow(ctx->ref_over_cap, ncand > ctx->cand_over_cap ? 2 * std::max(nref, 1024u) : nref, UINT32_MAX / 4);
-        grow(ctx->cand_over_cap, ncand, UINT32_MAX / 4);
-        ctx->kernel_timed = false;
-        n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
-        if (n < 0) return n;
-    }
+    ctx->scanned = true;
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
     ctx->timing_pending = true;
@@ -481,8 +574,18 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
 int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
     if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    if (!ctx->scanned) return tfbs::fail(TFBS_E_STATE, "batch not scanned (tfbs_scan)");
     HIP_TRY(hipSetDevice(ctx->device));
     Batch &B = b->b;
+    int rc;
+    if ((rc = check_overflow(ctx, (uint32_t)B.haps.size()))) return rc;
+    if (!ctx->counts_live) {  // no LUT/generic slots: the matrix is the assembly's alone
+        if ((rc = ctx->counts.ensure(std::max<uint64_t>(B.n_counts, 1)))) return rc;
+    }
+    AsmArgs a = asm_args(ctx, B, 1);
+    a.counts = ctx->counts.p;
+    a.dense_base = 1;
+    if ((rc = launch_key_asm(a, (uint32_t)B.regions.size(), ctx->stream))) return rc;
     B.counts.resize(B.n_counts);
     if (B.n_counts)
         HIP_TRY(hipMemcpyAsync(B.counts.data(), ctx->counts.p, B.n_counts * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -494,51 +597,64 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    if (!ctx->scanned) return tfbs::fail(TFBS_E_STATE, "batch not scanned (tfbs_scan)");
     HIP_TRY(hipSetDevice(ctx->device));
     Batch &B = b->b;
-    const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
     int rc;
-    if ((rc = ctx->key_first.ensure(n_keys)) || (rc = ctx->key_flags.ensure(n_keys))) return rc;
-    if ((rc = launch_key_reduce(ctx->haps.p, ctx->regions.p, (uint32_t)B.regions.size(), ctx->counts.p, B.n_slots,
-                                ctx->key_first.p, ctx->key_flags.p, ctx->stream)))
+    if ((rc = check_overflow(ctx, (uint32_t)B.haps.size()))) return rc;
+    const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
+    if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
+        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->var_tot.ensure(2)))
         return rc;
+    if (!ctx->var_tot_host) HIP_TRY(hipHostMalloc((void **)&ctx->var_tot_host, 8, hipHostMallocDefault));
+    // per region: the keys' flags and first counts, and the varying keys' counts
+    // appended to a compact list (grown and redone if it was too small)
+    for (int round = 0;; round++) {
+        if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
+        AsmArgs a = asm_args(ctx, B, 0);
+        a.key_first = ctx->key_first.p;
+        a.key_flags = ctx->key_flags.p;
+        a.var_keys = ctx->var_keys.p;
+        a.var_keys_cap = ctx->var_keys_cap;
+        a.var_counts = ctx->var_counts.p;
+        a.var_cap = ctx->var_cap;
+        a.var_tot = ctx->var_tot.p;
+        HIP_TRY(hipMemsetAsync(ctx->var_tot.p, 0, 8, ctx->stream));
+        if ((rc = launch_key_asm(a, (uint32_t)B.regions.size(), ctx->stream))) return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->var_tot_host, ctx->var_tot.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        const uint32_t nk = ctx->var_tot_host[0], nc = ctx->var_tot_host[1];
+        if (nk <= ctx->var_keys_cap && nc <= ctx->var_cap) break;
+        if (round == 2 || (uint64_t)nc >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
+        ctx->var_keys_cap = std::max<uint32_t>(ctx->var_keys_cap, nk + nk / 4 + 1024);
+        ctx->var_cap = std::max<uint64_t>(ctx->var_cap, (uint64_t)nc + nc / 4 + 4096);
+    }
+    const uint32_t nk = ctx->var_tot_host[0], nc = ctx->var_tot_host[1];
     B.key_first.resize(n_keys);
     B.key_flags.resize(n_keys);
+    std::vector<DevVarKey> vk(nk);
+    if ((rc = B.var_counts.reserve((size_t)nc * 4))) return rc;
     if (n_keys) {
         HIP_TRY(hipMemcpyAsync(B.key_first.data(), ctx->key_first.p, n_keys * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(B.key_flags.data(), ctx->key_flags.p, n_keys, hipMemcpyDeviceToHost, ctx->stream));
     }
+    if (nk) HIP_TRY(hipMemcpyAsync(vk.data(), ctx->var_keys.p, nk * sizeof(DevVarKey), hipMemcpyDeviceToHost, ctx->stream));
+    if (nc) HIP_TRY(hipMemcpyAsync(B.var_counts.p, ctx->var_counts.p, (size_t)nc * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    // columns of the varying keys, one count per distinct haplotype
-    std::vector<DevVarKey> vk;
+    // the varying keys in (region, key) order; their counts stay where the device put them
+    std::sort(vk.begin(), vk.end(), [](const DevVarKey &x, const DevVarKey &y) {
+        return x.region != y.region ? x.region < y.region : x.j < y.j;
+    });
     B.var_off.assign(n_keys, UINT32_MAX);
     B.var_idx.assign(n_keys, UINT32_MAX);
-    uint64_t total = 0;
-    for (uint32_t r = 0; r < B.regions.size(); r++) {
-        const DevRegion &rg = B.regions[r];
-        const uint64_t ko = (uint64_t)rg.inner_off * B.n_slots;
-        const uint32_t K = B.n_slots * rg.n_inner;
-        for (uint32_t j = 0; j < K; j++)
-            if (B.key_flags[ko + j] & KEY_VARIES) {
-                if (total + rg.hap_count >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
-                B.var_off[ko + j] = (uint32_t)total;
-                B.var_idx[ko + j] = (uint32_t)vk.size();
-                vk.push_back(DevVarKey{r, j, total});
-                total += rg.hap_count;
-            }
+    for (uint32_t i = 0; i < nk; i++) {
+        const uint64_t k = (uint64_t)B.regions[vk[i].region].inner_off * B.n_slots + vk[i].j;
+        B.var_off[k] = (uint32_t)vk[i].out_off;
+        B.var_idx[k] = i;
     }
-    if ((rc = B.var_counts.reserve(total * 4))) return rc;
-    B.var_keys = vk;
+    B.var_keys = std::move(vk);
     B.enc_r0 = B.enc_r1 = 0;
     B.enc_idx.clear();
-    if (!vk.empty()) {
-        if ((rc = ctx->var_keys.put(vk, ctx->stream)) || (rc = ctx->var_counts.ensure(total))) return rc;
-        if ((rc = launch_key_gather(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->var_keys.p,
-                                    (uint32_t)vk.size(), ctx->var_counts.p, ctx->stream)))
-            return rc;
-        HIP_TRY(hipMemcpyAsync(B.var_counts.p, ctx->var_counts.p, total * 4, hipMemcpyDeviceToHost, ctx->stream));
-    }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.reduced = true;
     return TFBS_OK;
 }
@@ -564,34 +680,55 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
         B.enc_r1 = (uint32_t)r1;
         return TFBS_OK;
     }
-    // the keys to encode: varying keys of [r0, r1) whose region has <= 255 distinct haplotypes
-    std::vector<DevVarKey> ek;
-    std::vector<uint32_t> ek_var;
-    for (uint32_t i = 0; i < B.var_keys.size(); i++) {
-        const DevVarKey &k = B.var_keys[i];
-        if (k.region < r0 || k.region >= r1 || B.regions[k.region].hap_count > kEncMaxHaps) continue;
-        B.enc_idx[i] = (uint32_t)ek.size();
-        ek.push_back(k);
-        ek_var.push_back(i);
-    }
-    const size_t nk = ek.size();
-    // membership rows: haplotype id -> distinct index (u8), 2 N bytes per region of
-    // [r0, r1), written by the host threads into the ctx's pinned staging buffer
-    // (rows of regions with no encoded keys are left unwritten: never read)
-    const size_t mbytes = (r1 - r0) * (size_t)H;
+    // per region of [r0, r1) with <= 255 distinct haplotypes: its distinct (left,
+    // right) haplotype pairs with their sample counts and each sample's pair (u16,
+    // written by the host threads into the ctx's pinned staging buffer).  Most
+    // samples carry the reference group on both sides: the rows start as that
+    // pair, and only samples with a haplotype outside the group are looked up.
+    const size_t nr = r1 - r0;
+    const size_t pbytes = nr * (size_t)N * 2;
     int rc;
-    if ((rc = ctx->enc_memb_host.reserve(mbytes))) return rc;
-    uint8_t *const memb = ctx->enc_memb_host.p;
+    if ((rc = ctx->enc_memb_host.reserve(pbytes))) return rc;
+    uint16_t *const pidx = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p);
+    std::vector<std::vector<uint16_t>> pab(nr);
+    std::vector<std::vector<uint32_t>> pcnt(nr);
     {
-        const uint32_t T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        const uint32_t T = std::max(1u, std::min(ctx->host_threads, (uint32_t)nr));
         std::atomic<size_t> next(r0);
         auto work = [&]() {
+            std::vector<uint8_t> memb(H);
+            std::vector<uint16_t> slot(1u << 16, 0);  // pair -> index + 1 (reset after each region)
+            std::vector<uint32_t> seen((N + 31) / 32, 0);
             for (size_t r; (r = next.fetch_add(1)) < r1;) {
                 const RegionH &R = B.rh[r];
                 if (R.hap_count > kEncMaxHaps) continue;
-                uint8_t *row = memb + (r - r0) * (size_t)H;
-                memset(row, R.ref_local < 0 ? 0 : R.ref_local, H);
-                for (size_t i = 0; i < R.nonref_id.size(); i++) row[R.nonref_id[i]] = (uint8_t)R.nonref_local[i];
+                const uint8_t d = (uint8_t)(R.ref_local < 0 ? 0 : R.ref_local);
+                memset(memb.data(), d, H);
+                for (size_t i = 0; i < R.nonref_id.size(); i++) memb[R.nonref_id[i]] = (uint8_t)R.nonref_local[i];
+                std::vector<uint16_t> &ab = pab[r - r0];
+                std::vector<uint32_t> &cn = pcnt[r - r0];
+                ab.assign(1, (uint16_t)(d | (d << 8)));
+                cn.assign(1, N);
+                slot[ab[0]] = 1;
+                uint16_t *row = pidx + (r - r0) * (size_t)N;
+                std::fill(row, row + N, (uint16_t)0);
+                for (size_t i = 0; i < R.nonref_id.size() && ab.size() <= kEncMaxPairs; i++) {
+                    const uint32_t smp = R.nonref_id[i] >> 1;
+                    if (seen[smp >> 5] >> (smp & 31) & 1u) continue;
+                    seen[smp >> 5] |= 1u << (smp & 31);
+                    const uint16_t key = (uint16_t)(memb[2 * smp] | (memb[2 * smp + 1] << 8));
+                    uint16_t &sl = slot[key];
+                    if (!sl) {
+                        ab.push_back(key);
+                        cn.push_back(0);
+                        sl = (uint16_t)ab.size();
+                    }
+                    cn[0]--;
+                    cn[sl - 1]++;
+                    row[smp] = (uint16_t)(sl - 1);
+                }
+                for (uint16_t k : ab) slot[k] = 0;
+                for (size_t i = 0; i < R.nonref_id.size(); i++) seen[R.nonref_id[i] >> 6] = 0;
             }
         };
         std::vector<std::thread> ts;
@@ -599,18 +736,38 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
         work();
         for (auto &t : ts) t.join();
     }
-    if ((rc = ctx->enc_memb.ensure(mbytes)))
-        return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->enc_memb.p, memb, mbytes, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = ctx->enc_keys.put(ek, ctx->stream)) ||
+    std::vector<uint32_t> pair_off(nr + 1, 0);
+    for (size_t i = 0; i < nr; i++) pair_off[i + 1] = pair_off[i] + (uint32_t)pab[i].size();
+    std::vector<uint16_t> pab_all(std::max<uint32_t>(pair_off[nr], 1));
+    std::vector<uint32_t> pcnt_all(pab_all.size());
+    for (size_t i = 0; i < nr; i++) {
+        std::copy(pab[i].begin(), pab[i].end(), pab_all.begin() + pair_off[i]);
+        std::copy(pcnt[i].begin(), pcnt[i].end(), pcnt_all.begin() + pair_off[i]);
+    }
+    // the keys to encode: varying keys of [r0, r1) whose region has <= 255 distinct
+    // haplotypes and <= kEncMaxPairs haplotype pairs (the others keep the host path)
+    std::vector<DevVarKey> ek;
+    for (uint32_t i = 0; i < B.var_keys.size(); i++) {
+        const DevVarKey &k = B.var_keys[i];
+        if (k.region < r0 || k.region >= r1 || B.regions[k.region].hap_count > kEncMaxHaps ||
+            pab[k.region - r0].size() > kEncMaxPairs)
+            continue;
+        B.enc_idx[i] = (uint32_t)ek.size();
+        ek.push_back(k);
+    }
+    const size_t nk = ek.size();
+    if ((rc = ctx->enc_pidx.ensure(std::max<size_t>(nr * (size_t)N, 1)))) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->enc_pidx.p, pidx, pbytes, hipMemcpyHostToDevice, ctx->stream));
+    if ((rc = ctx->enc_keys.put(ek, ctx->stream)) || (rc = ctx->enc_pab.put(pab_all, ctx->stream)) ||
+        (rc = ctx->enc_pcnt.put(pcnt_all, ctx->stream)) || (rc = ctx->enc_pair_off.put(pair_off, ctx->stream)) ||
         (rc = ctx->enc_hdr.ensure(std::max<size_t>(nk, 1))) ||
         (rc = ctx->enc_vals.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
         (rc = ctx->enc_hist.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
         (rc = ctx->enc_codes.ensure(std::max<size_t>(nk, 1) * N)))
         return rc;
-    if ((rc = launch_key_encode(ctx->haps.p, ctx->regions.p, ctx->counts.p, B.n_slots, ctx->enc_keys.p, (uint32_t)nk,
-                                ctx->enc_memb.p, (uint32_t)r0, N, ctx->enc_hdr.p, ctx->enc_vals.p, ctx->enc_hist.p,
-                                ctx->enc_codes.p, ctx->stream)))
+    if ((rc = launch_key_encode(ctx->var_counts.p, ctx->enc_keys.p, (uint32_t)nk, ctx->enc_pab.p, ctx->enc_pcnt.p,
+                                ctx->enc_pair_off.p, ctx->enc_pidx.p, (uint32_t)r0, N, ctx->enc_hdr.p, ctx->enc_vals.p,
+                                ctx->enc_hist.p, ctx->enc_codes.p, ctx->stream)))
         return rc;
     B.enc_hdr.resize(nk);
     B.enc_vals.resize(nk * (kEncMaxVals + 1));
@@ -672,7 +829,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
             if (nucs[i] == 4) nmask[i / 32] |= 1u << (i % 32);
     }
     std::vector<DevHap> haps{hm};
-    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, 1, {0, 0}}};
+    std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, 1, 0}};
     std::vector<int32_t> inner{0, 0}, posrel{0};
     const uint32_t wpp = (uint32_t)((n + 255) / 256 * 4);
     HIP_TRY(hipSetDevice(ctx->device));
@@ -680,9 +837,11 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
     if ((rc = ctx->words.put(words, ctx->stream)) || (rc = ctx->nmask.put(nmask, ctx->stream)) ||
         (rc = ctx->posrel.put(posrel, ctx->stream)) || (rc = ctx->haps.put(haps, ctx->stream)) ||
         (rc = ctx->regions.put(regions, ctx->stream)) || (rc = ctx->inner.put(inner, ctx->stream)) ||
-        (rc = ctx->counts.ensure(1)))
+        (rc = ctx->counts.ensure(std::max<uint64_t>(P.pats.size(), 1))))
         return rc;
+    ctx->counts_live = true;
     ctx->resident = nullptr;
+    ctx->scanned = false;
     ctx->mfma_group_words = mfma_group_words(haps.data(), 1, ctx->mfma_hpb);
     ctx->n_regions = 1;
     const size_t nh = (size_t)P.pats.size() * wpp;
@@ -690,6 +849,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
     if (nh) HIP_TRY(hipMemsetAsync(ctx->hits.p, 0, nh * 8, ctx->stream));
     int l = launch_scan(ctx, 1, ctx->hits.p, wpp);
     if (l < 0) return l;
+    if ((rc = check_overflow(ctx, 1, ctx->hits.p, wpp))) return rc;  // a rescan (larger lists) sets the same bits again
     std::vector<unsigned long long> h(nh);
     if (nh) HIP_TRY(hipMemcpyAsync(h.data(), ctx->hits.p, nh * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));

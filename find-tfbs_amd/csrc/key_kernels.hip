@@ -1,16 +1,22 @@
-// Count gather on the device.
+// Per-region key assembly on the device.
 //
 // count_matches_by_sample (main.rs:500-534) builds, per key (bed, inner range,
 // pattern_id), the per-sample L/R vectors; counts_as_genotypes (main.rs:439-498)
-// emits a row only when the per-sample totals differ.  The scan leaves, per
-// region, a [slot * n_inner + range][distinct haplotype] count matrix in HBM
-// (key-major: a key's counts are adjacent, DevRegion::count_stride apart).
-// Every sample's total is a sum of two of its rows, so a key can only produce a
-// row if its column is not constant.  key_reduce_kernel classifies every column
-// (any count != 0 -> the key exists in the reference's HashMap; counts differ ->
-// the key may emit a row) in one pass over the matrix, and
-// key_gather_kernel compacts the columns of the varying keys, so the host
-// downloads flags + first values + a few columns instead of the dense matrix.
+// emits a row only when the per-sample totals differ.  Every sample's total is
+// a sum of two distinct haplotypes' counts, so a key can only produce a row if
+// its counts over the region's distinct haplotypes are not constant.
+//
+// The matrix-core scan leaves no count matrix: per hit one (haplotype, key =
+// slot * n_inner + range) pair in its workgroup's hit list (or the spill list),
+// plus the region's reference hits (strand, window) that every HAP_DEDUP
+// haplotype inherits in the window tiles it did not scan.  key_asm_kernel (one
+// workgroup per region) counts them into a [key][distinct haplotype] block in
+// LDS, a chunk of keys at a time -- the LUT/generic kernels' slots are copied
+// from their dense counts -- and then either classifies every key (any count
+// != 0 -> the key exists in the reference's HashMap; counts differ -> it may
+// emit a row) and appends the varying keys' counts to a compact list (the run
+// flow's reduction), or stores the block into the dense matrix (the debug
+// download).
 #include <hip/hip_runtime.h>
 
 #include <string>
@@ -20,111 +26,444 @@
 namespace tfbs {
 namespace {
 
-constexpr int kReduceBlock = 256;
+constexpr int kAsmBlock = 256;
+constexpr uint32_t kAsmWaves = kAsmBlock / 64;
+constexpr uint32_t kAsmCounters = 6144;  // u32 counters of the LDS block (24 KiB)
+constexpr uint32_t kAsmHaps = 1024;      // haplotypes whose dirty masks sit in LDS (else read from L2)
+constexpr uint32_t kAsmHits = 2048;      // own hits staged in LDS (else re-read from the lists per pass)
+constexpr uint32_t kAsmRefs = 256;       // reference hits staged in LDS (else re-read)
+constexpr uint32_t kAsmKeyWords = 2048;  // touched-key bitmap: keys handled per key window
+constexpr uint32_t kAsmKeyWin = 32 * kAsmKeyWords;
 
-// One workgroup per region, one thread per key: the key's counts of every
-// distinct haplotype are adjacent (key-major layout, DevRegion), read in order
-// (unrolled: several loads in flight per lane; each cache line serves 32
-// iterations).
-__global__ __launch_bounds__(kReduceBlock) void key_reduce_kernel(const DevHap *__restrict__ haps,
-                                                                   const DevRegion *__restrict__ regions,
-                                                                   const uint32_t *__restrict__ counts,
-                                                                   uint32_t n_slots, uint32_t *__restrict__ first,
-                                                                   uint8_t *__restrict__ flags) {
-    const DevRegion rg = regions[blockIdx.x];
-    const uint32_t K = n_slots * rg.n_inner;
-    const uint64_t ko = (uint64_t)rg.inner_off * n_slots;
-    if (rg.hap_count == 0) {  // no samples: no haplotype, no match, no key
-        for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
-            first[ko + j] = 0;
-            flags[ko + j] = 0;
+// Region r's spill records (bucketed: [spill_off[r], spill_off[r + 1]) of spill_sorted).
+__device__ __forceinline__ uint2 spill_range(const AsmArgs &A, uint32_t r) {
+    return A.n_spill ? make_uint2(A.spill_off[r], A.spill_off[r + 1]) : make_uint2(0, 0);
+}
+
+// The inner ranges [k0, k0 + nk) a reference hit (window i of a strand of length L)
+// overlaps (range.rs:18-21 as main.rs:503 uses it; the reference's positions are
+// affine): bit k - k0.
+__device__ __forceinline__ uint32_t ref_overlaps(const AsmArgs &A, const DevRegion &rg, uint32_t L, uint32_t i,
+                                                 uint32_t k0, uint32_t nk) {
+    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+    uint32_t mask = 0;
+    for (uint32_t k = k0; k < k0 + nk; k++) {
+        const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+        const uint32_t span = (uint32_t)(en - s);
+        if ((uint32_t)((int32_t)i - s) <= span || (uint32_t)((int32_t)(i + L) - 1 - s) <= span) mask |= 1u << (k - k0);
+    }
+    return mask;
+}
+
+// A reference hit (strand g, window i) as the assembly uses it: {first key
+// (slot * n_inner), window, L | (K depth - 1) << 16, inner ranges < 32 it overlaps}.
+__device__ __forceinline__ uint4 make_ref(const AsmArgs &A, const DevRegion &rg, uint32_t g, uint32_t i) {
+    const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
+    const uint32_t sn = g & 63u, L = (uint32_t)meta[kGStrandInts * sn + kGLen];
+    const uint32_t dk = (uint32_t)meta[kGDepth] - 1;
+    const uint32_t key0 = (uint32_t)meta[kGStrandInts * sn + kGSlot] * rg.n_inner;
+    return make_uint4(key0, i, L | (dk << 16), ref_overlaps(A, rg, L, i, 0, min(rg.n_inner, 32u)));
+}
+
+// Every own hit (local haplotype l < U, key) of region r: the workgroup lists of the
+// matrix-core launches (one wave per list), then the region's spill records.
+template <class F>
+__device__ __forceinline__ void visit_hits(const AsmArgs &A, uint32_t r, uint32_t hb, uint32_t U, F &&f) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t g_lo = hb / A.hpb, g_hi = (hb + U - 1) / A.hpb;
+    for (uint32_t si = 0; si < A.n_srcs; si++) {
+        const HitSrc src = A.srcs[si];
+        const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
+        if (ga >= gb) continue;
+        const uint32_t per_g = src.ns * kMBlockWaves, n_l = (gb - ga) * per_g;
+        for (uint32_t li = wave; li < n_l; li += kAsmWaves) {
+            const uint32_t g = ga + li / per_g, rem = li % per_g;
+            const uint32_t wg = src.wg_base + (g - src.g0) * src.ns + rem / kMBlockWaves, w = rem % kMBlockWaves;
+            const uint32_t n = A.hitn[(size_t)wg * kMBlockWaves + w];
+            const uint2 *lst = reinterpret_cast<const uint2 *>(A.hitl) + (size_t)wg * A.cand_cap +
+                               (size_t)w * (A.cand_cap / kMBlockWaves);
+            for (uint32_t e = lane; e < n; e += 64) {
+                const uint2 h = lst[e];
+                if (h.x - hb < U) f(h.x - hb, h.y);
+            }
         }
+    }
+    const uint2 sp = spill_range(A, r);
+    for (uint32_t e = sp.x + threadIdx.x; e < sp.y; e += kAsmBlock) {
+        const uint32_t *q = A.spill_sorted + 3 * (size_t)e;
+        if (!(q[0] >> 31) && q[1] - hb < U) f(q[1] - hb, q[2]);
+    }
+}
+
+// Every reference hit of region r (its list, then its spill records).
+template <class F>
+__device__ __forceinline__ void visit_refs(const AsmArgs &A, uint32_t r, const DevRegion &rg, F &&f) {
+    const uint32_t nl = min(A.ref_count[r], kRefPerRegion);
+    for (uint32_t t = threadIdx.x; t < nl; t += kAsmBlock)
+        f(make_ref(A, rg, A.ref_hits[2 * ((size_t)r * kRefPerRegion + t)],
+                   A.ref_hits[2 * ((size_t)r * kRefPerRegion + t) + 1]));
+    const uint2 sp = spill_range(A, r);
+    for (uint32_t e = sp.x + threadIdx.x; e < sp.y; e += kAsmBlock) {
+        const uint32_t *q = A.spill_sorted + 3 * (size_t)e;
+        if (q[0] >> 31) f(make_ref(A, rg, q[1], q[2]));
+    }
+}
+
+__global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
+    __shared__ uint32_t s_cnt[kAsmCounters];
+    __shared__ uint32_t s_d[4][kAsmHaps];  // dirty window-tile masks per K depth (all set: not HAP_DEDUP)
+    __shared__ uint2 s_hit[kAsmHits];      // (local haplotype, key)
+    __shared__ uint4 s_ref[kAsmRefs];      // make_ref
+    __shared__ uint32_t s_bits[kAsmKeyWords], s_rbase[kAsmKeyWords];  // touched keys of the window, rows before each word
+    __shared__ uint32_t s_scan[kAsmBlock];
+    __shared__ uint32_t s_nhit, s_nref, s_nvar, s_vbase, s_obase;
+    const uint32_t r = blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const DevRegion rg = A.regions[r];
+    const uint32_t U = rg.hap_count, n_inner = rg.n_inner;
+    const uint32_t K = A.n_slots * n_inner;
+    const uint64_t ko = (uint64_t)rg.inner_off * A.n_slots;
+    if (U == 0 || K == 0) {  // no samples: no haplotype, no match, no key
+        if (A.mode == 0)
+            for (uint32_t j = tid; j < K; j += kAsmBlock) {
+                A.key_first[ko + j] = 0;
+                A.key_flags[ko + j] = 0;
+            }
         return;
     }
-    const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t j = threadIdx.x; j < K; j += kReduceBlock) {
-        const uint32_t *col = counts + base + (uint64_t)j * rg.count_stride;
-        const uint32_t c0 = col[0];
-        uint32_t any = c0, diff = 0;
-#pragma unroll 8
-        for (uint32_t l = 1; l < rg.hap_count; l++) {
-            const uint32_t c = col[l];
-            any |= c;
-            diff |= c ^ c0;
+    const uint32_t hb = rg.hap_begin;
+    const bool lds_haps = U <= kAsmHaps;
+    if (lds_haps)
+        for (uint32_t l = tid; l < U; l += kAsmBlock) {
+            const DevHap h = A.haps[hb + l];
+            const bool dd = (h.flags & HAP_DEDUP) != 0;
+            for (int d = 0; d < 4; d++) s_d[d][l] = dd ? h.dirty[d] : 0xFFFFFFFFu;  // not HAP_DEDUP: all scanned
         }
-        first[ko + j] = c0;
-        flags[ko + j] = (uint8_t)((any ? KEY_ANY : 0) | (diff ? KEY_VARIES : 0));
+    const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
+    // stage the region's own hits and reference hits in LDS (the lists are read once)
+    if (tid == 0) s_nhit = s_nref = 0;
+    __syncthreads();
+    if (A.mfma) {
+        visit_hits(A, r, hb, U, [&](uint32_t l, uint32_t key) {
+            const uint32_t at = atomicAdd(&s_nhit, 1u);
+            if (at < kAsmHits) s_hit[at] = make_uint2(l, key);
+        });
+        if (refs_on)
+            visit_refs(A, r, rg, [&](const uint4 &q) {
+                const uint32_t at = atomicAdd(&s_nref, 1u);
+                if (at < kAsmRefs) s_ref[at] = q;
+            });
+    }
+    __syncthreads();
+    const uint32_t nhit = s_nhit, nref = s_nref;
+    const bool hits_lds = nhit <= kAsmHits, refs_lds = nref <= kAsmRefs;
+    auto each_hit = [&](auto &&f) {
+        if (!A.mfma) return;
+        if (hits_lds) {
+            for (uint32_t e = tid; e < nhit; e += kAsmBlock) f(s_hit[e].x, s_hit[e].y);
+        } else {
+            visit_hits(A, r, hb, U, f);
+        }
+    };
+    auto each_ref = [&](auto &&f) {  // thread-parallel over the reference hits
+        if (!refs_on) return;
+        if (refs_lds) {
+            for (uint32_t t = tid; t < nref; t += kAsmBlock) f(s_ref[t]);
+        } else {
+            visit_refs(A, r, rg, f);
+        }
+    };
+    // the keys a reference hit adds to: its ranges past 32 recomputed, the others in q.w
+    auto ref_keys = [&](const uint4 &q, auto &&f) {
+        const uint32_t L = q.z & 0xFFFFu;
+        for (uint32_t kb = 0; kb < n_inner; kb += 32)
+            for (uint32_t m = kb ? ref_overlaps(A, rg, L, q.y, kb, min(32u, n_inner - kb)) : q.w; m; m &= m - 1)
+                f(q.x + kb + __builtin_ctz(m));
+    };
+    const uint64_t dense_base = A.dense_base ? A.haps[hb].count_off : 0;
+    const bool lds_cnt = U <= kAsmCounters;
+    const uint32_t rows_per = lds_cnt ? kAsmCounters / U : 1;
+    uint32_t *cnt = lds_cnt ? s_cnt : A.scratch + rg.big_off;
+    for (uint32_t kw0 = 0; kw0 < K; kw0 += kAsmKeyWin) {  // key windows (one unless 65536 keys)
+        const uint32_t kwn = min(kAsmKeyWin, K - kw0), nw = (kwn + 31) / 32;
+        __syncthreads();
+        for (uint32_t w = tid; w < nw; w += kAsmBlock) s_bits[w] = 0;
+        __syncthreads();
+        // touched keys: own hits, reference hits, every key of a LUT/generic slot
+        each_hit([&](uint32_t, uint32_t key) {
+            const uint32_t j = key - kw0;
+            if (j < kwn) atomicOr(&s_bits[j >> 5], 1u << (j & 31));
+        });
+        each_ref([&](const uint4 &q) {
+            ref_keys(q, [&](uint32_t key) {
+                const uint32_t j = key - kw0;
+                if (j < kwn) atomicOr(&s_bits[j >> 5], 1u << (j & 31));
+            });
+        });
+        if (A.any_dense)
+            for (uint32_t j = tid; j < kwn; j += kAsmBlock)
+                if (!A.slot_mfma[(kw0 + j) / n_inner]) atomicOr(&s_bits[j >> 5], 1u << (j & 31));
+        __syncthreads();
+        // rows: touched keys in key order (block scan of the words' popcounts)
+        constexpr uint32_t per = kAsmKeyWords / kAsmBlock;
+        uint32_t mine = 0;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t w = tid * per + q;
+            if (w < nw) mine += __popc(s_bits[w]);
+        }
+        s_scan[tid] = mine;
+        __syncthreads();
+        for (uint32_t o = 1; o < kAsmBlock; o <<= 1) {
+            const uint32_t t = tid >= o ? s_scan[tid - o] : 0;
+            __syncthreads();
+            s_scan[tid] += t;
+            __syncthreads();
+        }
+        {
+            uint32_t run = s_scan[tid] - mine;
+            for (uint32_t q = 0; q < per; q++) {
+                const uint32_t w = tid * per + q;
+                if (w < nw) {
+                    s_rbase[w] = run;
+                    run += __popc(s_bits[w]);
+                }
+            }
+        }
+        const uint32_t T = s_scan[kAsmBlock - 1];
+        __syncthreads();
+        auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
+        auto key_of_row = [&](uint32_t t) {  // the word whose rows start at or before t, then its bit
+            uint32_t lo = 0, hi = nw - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (s_rbase[mid] <= t) lo = mid;
+                else hi = mid - 1;
+            }
+            uint32_t b = s_bits[lo];
+            for (uint32_t k = t - s_rbase[lo]; k; k--) b &= b - 1;
+            return 32 * lo + __builtin_ctz(b);
+        };
+        // untouched keys: no match -- no key in the reference's HashMap (zeros in the dense matrix)
+        for (uint32_t j = tid; j < kwn; j += kAsmBlock) {
+            if ((s_bits[j >> 5] >> (j & 31)) & 1u) continue;
+            if (A.mode == 0) {
+                A.key_first[ko + kw0 + j] = 0;
+                A.key_flags[ko + kw0 + j] = 0;
+            } else {
+                for (uint32_t l = 0; l < U; l++) A.counts[dense_base + (uint64_t)(kw0 + j) * rg.count_stride + l] = 0;
+            }
+        }
+        for (uint32_t t0 = 0; t0 < T; t0 += rows_per) {
+            const uint32_t nrow = min(rows_per, T - t0);
+            __syncthreads();  // the previous chunk's readers are done
+            for (uint32_t rr = wave; rr < nrow; rr += kAsmWaves) {  // a LUT/generic key: its dense counts
+                const uint32_t j = kw0 + key_of_row(t0 + rr);
+                const bool dense = A.any_dense && !A.slot_mfma[j / n_inner];
+                for (uint32_t l = lane; l < U; l += 64)
+                    cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l] : 0u;
+            }
+            __syncthreads();
+            each_hit([&](uint32_t l, uint32_t key) {
+                const uint32_t j = key - kw0;
+                if (j >= kwn) return;
+                const uint32_t t = row_of(j) - t0;
+                if (t < nrow) atomicAdd(&cnt[t * U + l], 1u);
+            });
+            // reference hits: +1 to every HAP_DEDUP haplotype whose tile of the hit's
+            // window it did not scan (same bases and positions as the reference there)
+            auto dirty_of = [&](uint32_t l, uint32_t dk) {
+                return lds_haps ? s_d[dk][l]
+                                : ((A.haps[hb + l].flags & HAP_DEDUP) ? A.haps[hb + l].dirty[dk] : 0xFFFFFFFFu);
+            };
+            if (refs_on && refs_lds) {
+                for (uint32_t q0 = 0; q0 < nref; q0++) {  // workgroup-uniform; threads over the haplotypes
+                    const uint4 q = s_ref[q0];
+                    const uint32_t dk = q.z >> 16, tile = q.y / kMWindows;
+                    ref_keys(q, [&](uint32_t key) {
+                        const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
+                        if (t >= nrow) return;
+                        for (uint32_t l = tid; l < U; l += kAsmBlock)
+                            if (!((dirty_of(l, dk) >> tile) & 1u)) atomicAdd(&cnt[t * U + l], 1u);
+                    });
+                }
+            } else if (refs_on) {  // too many for LDS (rare): each thread walks its hits' haplotypes
+                visit_refs(A, r, rg, [&](const uint4 &q) {
+                    const uint32_t dk = q.z >> 16, tile = q.y / kMWindows;
+                    ref_keys(q, [&](uint32_t key) {
+                        const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
+                        if (t >= nrow) return;
+                        for (uint32_t l = 0; l < U; l++)
+                            if (!((dirty_of(l, dk) >> tile) & 1u)) atomicAdd(&cnt[t * U + l], 1u);
+                    });
+                });
+            }
+            __syncthreads();
+            if (A.mode == 1) {  // dense: the matrix-core slots' counts into the count matrix
+                for (uint32_t rr = wave; rr < nrow; rr += kAsmWaves) {
+                    const uint32_t j = kw0 + key_of_row(t0 + rr);
+                    if (!A.slot_mfma[j / n_inner]) continue;
+                    for (uint32_t l = lane; l < U; l += 64)
+                        A.counts[dense_base + (uint64_t)j * rg.count_stride + l] = cnt[rr * U + l];
+                }
+                continue;
+            }
+            // classify: one wave per row
+            if (tid == 0) s_nvar = 0;
+            __syncthreads();
+            for (uint32_t rr = wave; rr < nrow; rr += kAsmWaves) {
+                const uint32_t j = kw0 + key_of_row(t0 + rr);
+                const uint32_t *col = cnt + rr * U;
+                const uint32_t c0 = col[0];
+                uint32_t any = 0, diff = 0;
+                for (uint32_t l = lane; l < U; l += 64) {
+                    const uint32_t c = col[l];
+                    any |= c;
+                    diff |= c ^ c0;
+                }
+                const bool a = __ballot(any != 0) != 0, v = __ballot(diff != 0) != 0;
+                if (lane == 0) {
+                    A.key_first[ko + j] = c0;
+                    A.key_flags[ko + j] = (uint8_t)((a ? KEY_ANY : 0) | (v ? KEY_VARIES : 0));
+                    if (v) atomicAdd(&s_nvar, 1u);
+                }
+            }
+            __syncthreads();
+            const uint32_t nvar = s_nvar;
+            if (nvar == 0) continue;
+            if (tid == 0) {  // the chunk's share of the compact lists
+                s_vbase = atomicAdd(A.var_tot, nvar);
+                s_obase = atomicAdd(A.var_tot + 1, nvar * U);
+                s_nvar = 0;
+            }
+            __syncthreads();
+            for (uint32_t rr = wave; rr < nrow; rr += kAsmWaves) {
+                const uint32_t *col = cnt + rr * U;
+                const uint32_t c0 = col[0];
+                uint32_t diff = 0;
+                for (uint32_t l = lane; l < U; l += 64) diff |= col[l] ^ c0;
+                if (__ballot(diff != 0) == 0) continue;
+                const uint32_t j = kw0 + key_of_row(t0 + rr);
+                uint32_t at = 0;
+                if (lane == 0) at = atomicAdd(&s_nvar, 1u);
+                at = __shfl(at, 0);
+                const uint32_t vi = s_vbase + at;
+                const uint64_t off = (uint64_t)s_obase + (uint64_t)at * U;
+                if (vi < A.var_keys_cap && off + U <= A.var_cap) {
+                    if (lane == 0) A.var_keys[vi] = DevVarKey{r, j, off};
+                    for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = col[l];
+                }
+            }
+        }
     }
 }
 
-// One wave per varying key: copy its column (one count per distinct haplotype).
-__global__ __launch_bounds__(256) void key_gather_kernel(const DevHap *__restrict__ haps,
-                                                         const DevRegion *__restrict__ regions,
-                                                         const uint32_t *__restrict__ counts, uint32_t n_slots,
-                                                         const DevVarKey *__restrict__ keys, uint32_t n_keys,
-                                                         uint32_t *__restrict__ out) {
-    const uint32_t k = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (k >= n_keys) return;
-    const DevVarKey vk = keys[k];
-    const DevRegion rg = regions[vk.region];
-    const uint64_t base = haps[rg.hap_begin].count_off;
-    const uint32_t *col = counts + base + (uint64_t)vk.j * rg.count_stride;
-    for (uint32_t l = threadIdx.x & 63; l < rg.hap_count; l += 64) out[vk.out_off + l] = col[l];
+// Spill bucketing: per-region record counts, their exclusive scan (one
+// workgroup), and the scatter into region order.
+__global__ __launch_bounds__(256) void spill_hist_kernel(const uint32_t *__restrict__ over, uint32_t cap,
+                                                          const uint32_t *__restrict__ spill, uint32_t *__restrict__ bcnt) {
+    const uint32_t n = min(over[0], cap);
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256)
+        atomicAdd(&bcnt[spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
 }
 
-// counts_as_genotypes' per-sample half (main.rs:439-498) for one varying key:
-// the sample totals, their min / max, the distinct values (a bitmap of
-// hi - lo + 1 bits in LDS, ranks from per-word prefix counts) and one code per
-// sample.  Three passes over the region's membership row (L2-resident: every
-// key of the region reads it); the key's column of distinct-haplotype counts
-// sits in LDS.  The range multiplicity and the text stay on the host, which
-// formats a row from the value table and the codes (aggregate.cpp).
+__global__ __launch_bounds__(1024) void spill_scan_kernel(uint32_t *__restrict__ bcnt, uint32_t n,
+                                                          uint32_t *__restrict__ boff) {
+    __shared__ uint32_t s[1024];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += 1024) {
+        const uint32_t i = b0 + threadIdx.x;
+        const uint32_t v = i < n ? bcnt[i] : 0;
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+            const uint32_t t = threadIdx.x >= o ? s[threadIdx.x - o] : 0;
+            __syncthreads();
+            s[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < n) {
+            boff[i] = carry + s[threadIdx.x] - v;
+            bcnt[i] = 0;  // the scatter's fill counters
+        }
+        carry += s[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) boff[n] = carry;
+}
+
+__global__ __launch_bounds__(256) void spill_scatter_kernel(const uint32_t *__restrict__ over, uint32_t cap,
+                                                            const uint32_t *__restrict__ spill,
+                                                            const uint32_t *__restrict__ boff,
+                                                            uint32_t *__restrict__ bfill, uint32_t *__restrict__ out) {
+    const uint32_t n = min(over[0], cap);
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
+        const uint32_t r = spill[3 * (size_t)e] & 0x7FFFFFFFu;
+        const uint32_t at = boff[r] + atomicAdd(&bfill[r], 1u);
+        out[3 * (size_t)at] = spill[3 * (size_t)e];
+        out[3 * (size_t)at + 1] = spill[3 * (size_t)e + 1];
+        out[3 * (size_t)at + 2] = spill[3 * (size_t)e + 2];
+    }
+}
+
+// counts_as_genotypes' per-sample half (main.rs:439-498) for one varying key.
+// A sample's total is C[a] + C[b] for its two haplotypes' distinct indices (a,
+// b); the host lists each region's distinct (a, b) pairs with their sample
+// counts and gives every sample its pair index (tfbs_batch_encode), so the key's
+// totals, min / max, distinct values (a bitmap of hi - lo + 1 bits), their
+// ranks and sample counts are computed over the P pairs, not the N samples (no
+// per-sample atomics); the one per-sample pass packs code[pair[s]].  The range
+// multiplicity and the text stay on the host, which formats a row from the
+// value table and the codes (aggregate.cpp).
 constexpr int kEncBlock = 256;
 constexpr uint32_t kEncWords = kEncMaxRange / 32;
+constexpr uint32_t kEncWordsPerThread = kEncWords / kEncBlock;  // the rank scan's share of the bitmap
 
-__global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__restrict__ haps,
-                                                                 const DevRegion *__restrict__ regions,
-                                                                 const uint32_t *__restrict__ counts, uint32_t n_slots,
+__global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const uint32_t *__restrict__ var_counts,
                                                                  const DevVarKey *__restrict__ keys,
-                                                                 const uint8_t *__restrict__ memb, uint32_t region0,
+                                                                 const uint16_t *__restrict__ pab,
+                                                                 const uint32_t *__restrict__ pcnt,
+                                                                 const uint32_t *__restrict__ pair_off,
+                                                                 const uint16_t *__restrict__ pidx, uint32_t region0,
                                                                  uint32_t n_samples, EncHdr *__restrict__ hdr,
                                                                  uint32_t *__restrict__ vals,
                                                                  uint32_t *__restrict__ hist,
                                                                  uint8_t *__restrict__ codes) {
-    __shared__ uint32_t s_c[kEncMaxHaps + 1];
+    __shared__ uint32_t s_v[kEncMaxPairs];   // the pairs' totals, then their codes
     __shared__ uint32_t s_bits[kEncWords];
-    __shared__ uint16_t s_rank[kEncWords];  // distinct values in the words before
+    __shared__ uint16_t s_rank[kEncWords];   // distinct values in the words before
     __shared__ uint32_t s_hist[kEncMaxVals + 1];
     __shared__ uint32_t s_red[2 * kEncBlock / 64];
-    __shared__ uint32_t s_nv;
-    const uint32_t k = blockIdx.x;
+    __shared__ uint32_t s_tsum[kEncBlock];
+    const uint32_t k = blockIdx.x, tid = threadIdx.x;
     const DevVarKey vk = keys[k];
-    const DevRegion rg = regions[vk.region];
-    const uint64_t base = haps[rg.hap_begin].count_off;
-    for (uint32_t l = threadIdx.x; l < rg.hap_count; l += kEncBlock)
-        s_c[l] = counts[base + (uint64_t)vk.j * rg.count_stride + l];
-    __syncthreads();
-    const uint16_t *m = reinterpret_cast<const uint16_t *>(memb + (size_t)(vk.region - region0) * 2 * n_samples);
-    auto total = [&](uint32_t s) {
-        const uint32_t pr = m[s];
-        return s_c[pr & 0xFF] + s_c[pr >> 8];  // u32 wrapping, as the reference's additions
-    };
-    // pass 1: min / max
+    const uint32_t r = vk.region - region0;
+    const uint32_t p0 = pair_off[r], P = pair_off[r + 1] - p0;
+    // each pair's total (u32 wrapping, as the reference's additions) from the key's
+    // distinct-haplotype counts (a region's U counts, cache-resident); the host
+    // sends only regions of <= 255 distinct haplotypes and <= kEncMaxPairs pairs
+    const uint32_t *cnt = var_counts + vk.out_off;
     uint32_t lo = UINT32_MAX, hi = 0;
-    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
-        const uint32_t v = total(s);
-        lo = min(lo, v);
-        hi = max(hi, v);
+    {
+        for (uint32_t p = tid; p < P; p += kEncBlock) {
+            const uint32_t ab = pab[p0 + p];
+            const uint32_t v = cnt[ab & 0xFF] + cnt[ab >> 8];
+            s_v[p] = v;
+            if (pcnt[p0 + p] == 0) continue;  // the reference group's pair when every sample carries a variant
+            lo = min(lo, v);
+            hi = max(hi, v);
+        }
     }
     for (int o = 32; o; o >>= 1) {
         lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
         hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
     }
-    const uint32_t wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
+    const uint32_t wave = tid >> 6;
+    if ((tid & 63) == 0) {
         s_red[wave] = lo;
         s_red[kEncBlock / 64 + wave] = hi;
     }
+    for (uint32_t w = tid; w < kEncWords; w += kEncBlock) s_bits[w] = 0;
+    for (uint32_t i = tid; i <= kEncMaxVals; i += kEncBlock) s_hist[i] = 0;
     __syncthreads();
     lo = s_red[0];
     hi = s_red[kEncBlock / 64];
@@ -133,60 +472,84 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const DevHap *__r
         hi = max(hi, s_red[kEncBlock / 64 + w]);
     }
     if (hi - lo >= kEncMaxRange) {
-        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, 0, 1, 0};
+        if (tid == 0) hdr[k] = EncHdr{lo, hi, 0, 1, 0};
         return;
     }
-    // pass 2: which values occur
-    const uint32_t nw = (hi - lo) / 32 + 1;
-    for (uint32_t w = threadIdx.x; w < nw; w += kEncBlock) s_bits[w] = 0;
-    __syncthreads();
-    for (uint32_t s = threadIdx.x; s < n_samples; s += kEncBlock) {
-        const uint32_t d = total(s) - lo;
+    // which totals occur: one bit per pair (P LDS ORs, not N)
+    for (uint32_t p = tid; p < P; p += kEncBlock) {
+        if (pcnt[p0 + p] == 0) continue;
+        const uint32_t d = s_v[p] - lo;
         atomicOr(&s_bits[d >> 5], 1u << (d & 31));
     }
     __syncthreads();
-    if (threadIdx.x == 0) {  // ranks: a serial prefix over <= 2048 words
-        uint32_t r = 0;
-        for (uint32_t w = 0; w < nw; w++) {
-            s_rank[w] = (uint16_t)min(r, 0xFFFFu);
-            r += __popc(s_bits[w]);
-        }
-        s_nv = r;
+    // ranks: each thread's words summed, a block scan of the sums, the words' prefixes
+    const uint32_t nw = (hi - lo) / 32 + 1;
+    uint32_t mine = 0;
+    for (uint32_t q = 0; q < kEncWordsPerThread; q++) {
+        const uint32_t w = tid * kEncWordsPerThread + q;
+        if (w < nw) mine += __popc(s_bits[w]);
     }
-    for (uint32_t i = threadIdx.x; i <= kEncMaxVals; i += kEncBlock) s_hist[i] = 0;
+    s_tsum[tid] = mine;
     __syncthreads();
-    const uint32_t nv = s_nv;
+    for (uint32_t o = 1; o < kEncBlock; o <<= 1) {
+        const uint32_t t = tid >= o ? s_tsum[tid - o] : 0;
+        __syncthreads();
+        s_tsum[tid] += t;
+        __syncthreads();
+    }
+    {
+        uint32_t run = s_tsum[tid] - mine;
+        for (uint32_t q = 0; q < kEncWordsPerThread; q++) {
+            const uint32_t w = tid * kEncWordsPerThread + q;
+            if (w < nw) {
+                s_rank[w] = (uint16_t)min(run, 0xFFFFu);
+                run += __popc(s_bits[w]);
+            }
+        }
+    }
+    const uint32_t nv = s_tsum[kEncBlock - 1];
+    __syncthreads();
     if (nv > kEncMaxVals) {
-        if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 1, 0};
+        if (tid == 0) hdr[k] = EncHdr{lo, hi, nv, 1, 0};
         return;
     }
-    for (uint32_t w = threadIdx.x; w < nw; w += kEncBlock) {  // the sorted value table
-        uint32_t b = s_bits[w], r = s_rank[w];
+    for (uint32_t w = tid; w < nw; w += kEncBlock) {  // the sorted value table
+        uint32_t b = s_bits[w], rk = s_rank[w];
         while (b) {
             const uint32_t t = __ffs(b) - 1;
             b &= b - 1;
-            vals[(size_t)k * (kEncMaxVals + 1) + r++] = lo + 32 * w + t;
+            vals[(size_t)k * (kEncMaxVals + 1) + rk++] = lo + 32 * w + t;
         }
     }
-    // pass 3: codes (packed: each thread writes whole bytes) and per-value sample counts
+    // each pair's code and its samples into the histogram (P LDS adds)
+    for (uint32_t p = tid; p < P; p += kEncBlock) {
+        const uint32_t n = pcnt[p0 + p];
+        if (n == 0) {  // no sample has this pair: no code (its total may lie outside [lo, hi])
+            s_v[p] = 0;
+            continue;
+        }
+        const uint32_t d = s_v[p] - lo, w = d >> 5;
+        const uint32_t c = s_rank[w] + __popc(s_bits[w] & ((1u << (d & 31)) - 1u));
+        s_v[p] = c;
+        atomicAdd(&s_hist[c], n);
+    }
+    __syncthreads();
+    // the per-sample pass: code[pair[s]] packed (each thread writes whole bytes)
     const uint32_t width = nv <= 4 ? 2 : (nv <= 16 ? 4 : 8), per = 8 / width;
     uint8_t *out = codes + (size_t)k * n_samples;
+    const uint16_t *pi = pidx + (size_t)r * n_samples;
     const uint32_t nbytes = (n_samples + per - 1) / per;
-    for (uint32_t byte = threadIdx.x; byte < nbytes; byte += kEncBlock) {
+    for (uint32_t byte = tid; byte < nbytes; byte += kEncBlock) {
         uint32_t packed = 0;
         for (uint32_t q = 0; q < per; q++) {
-            const uint32_t s = byte * per + q;
-            if (s >= n_samples) break;
-            const uint32_t d = total(s) - lo, w = d >> 5;
-            const uint32_t c = s_rank[w] + __popc(s_bits[w] & ((1u << (d & 31)) - 1u));
-            packed |= c << (q * width);
-            atomicAdd(&s_hist[c], 1u);
+            const uint32_t smp = byte * per + q;
+            if (smp >= n_samples) break;
+            packed |= s_v[pi[smp]] << (q * width);
         }
         out[byte] = (uint8_t)packed;
     }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < nv; i += kEncBlock) hist[(size_t)k * (kEncMaxVals + 1) + i] = s_hist[i];
-    if (threadIdx.x == 0) hdr[k] = EncHdr{lo, hi, nv, 0, width};
+    for (uint32_t i = tid; i < nv; i += kEncBlock) hist[(size_t)k * (kEncMaxVals + 1) + i] = s_hist[i];
+    if (tid == 0) hdr[k] = EncHdr{lo, hi, nv, 0, width};
 }
 
 // Copies each key's packed codes (at k * n_samples) to off[k] of a contiguous buffer.
@@ -200,13 +563,13 @@ __global__ __launch_bounds__(256) void code_compact_kernel(const uint8_t *__rest
 
 }  // namespace
 
-int launch_key_encode(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
-                      const DevVarKey *keys, uint32_t n_keys, const uint8_t *memb, uint32_t region0,
+int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint16_t *pab,
+                      const uint32_t *pcnt, const uint32_t *pair_off, const uint16_t *pidx, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream) {
     if (n_keys == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_encode_kernel, dim3(n_keys), dim3(kEncBlock), 0, stream, haps, regions, counts, n_slots,
-                       keys, memb, region0, n_samples, hdr, vals, hist, codes);
+    hipLaunchKernelGGL(key_encode_kernel, dim3(n_keys), dim3(kEncBlock), 0, stream, var_counts, keys, pab, pcnt,
+                       pair_off, pidx, region0, n_samples, hdr, vals, hist, codes);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_encode_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
@@ -221,24 +584,26 @@ int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_sample
     return TFBS_OK;
 }
 
-int launch_key_reduce(const DevHap *haps, const DevRegion *regions, uint32_t n_regions, const uint32_t *counts,
-                      uint32_t n_slots, uint32_t *first, uint8_t *flags, hipStream_t stream) {
-    if (n_regions == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_reduce_kernel, dim3(n_regions), dim3(kReduceBlock), 0, stream, haps, regions, counts,
-                       n_slots, first, flags);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_reduce_kernel: ") + hipGetErrorString(e));
+int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spill, uint32_t n_regions, uint32_t *bcnt,
+                         uint32_t *boff, uint32_t *sorted, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(bcnt, 0, (size_t)(n_regions + 1) * 4, stream);
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("spill bucket memset: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(spill_hist_kernel, dim3(64), dim3(256), 0, stream, over, cap, spill, bcnt);
+    hipLaunchKernelGGL(spill_scan_kernel, dim3(1), dim3(1024), 0, stream, bcnt, n_regions, boff);
+    hipLaunchKernelGGL(spill_scatter_kernel, dim3(64), dim3(256), 0, stream, over, cap, spill, boff, bcnt, sorted);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("spill bucket kernels: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 
-int launch_key_gather(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
-                      const DevVarKey *keys, uint32_t n_keys, uint32_t *out, hipStream_t stream) {
-    if (n_keys == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_gather_kernel, dim3((n_keys + 3) / 4), dim3(256), 0, stream, haps, regions, counts, n_slots,
-                       keys, n_keys, out);
+int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
+    if (n_regions == 0) return TFBS_OK;
+    hipLaunchKernelGGL(key_asm_kernel, dim3(n_regions), dim3(kAsmBlock), 0, stream, a);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_gather_kernel: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_asm_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
+
+uint32_t key_asm_lds_counters() { return kAsmCounters; }
 
 }  // namespace tfbs

@@ -1,4 +1,4 @@
-// Launch interface of the count-gather kernels (key_kernels.hip), used by device.hip.
+// Launch interface of the key kernels (key_kernels.hip), used by device.hip.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -6,23 +6,64 @@
 #include <cstdint>
 
 #include "batch.hpp"
+#include "scan.hpp"
 
 namespace tfbs {
 
-int launch_key_reduce(const DevHap *haps, const DevRegion *regions, uint32_t n_regions, const uint32_t *counts,
-                      uint32_t n_slots, uint32_t *first, uint8_t *flags, hipStream_t stream);
-// One workgroup per key: v[s] = C[memb[2s]] + C[memb[2s+1]] for s < n_samples,
-// where memb (u8, one row of 2 n_samples per region of the chunk, at
-// memb_row[key's region - region0]) maps haplotype ids to distinct indices.
-// Writes hdr[k], vals[k * 256 ..] (sorted distinct values), hist[k * 256 ..]
-// (samples per value) and codes[k * n_samples ..].
-int launch_key_encode(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
-                      const DevVarKey *keys, uint32_t n_keys, const uint8_t *memb, uint32_t region0,
+// Everything key_asm_kernel reads and writes (device pointers; see key_kernels.hip).
+struct AsmArgs {
+    const DevHap *haps;
+    const DevRegion *regions;
+    const int32_t *inner;
+    const int32_t *mmeta;       // matrix-core tiles' rescoring fields (strand length, slot, depth)
+    const uint8_t *slot_mfma;   // per slot: 1 = matrix-core hits, 0 = the LUT/generic kernels' dense counts
+    uint32_t any_dense;         // some slot is not on the matrix cores
+    uint32_t n_slots;
+    uint32_t hpb;               // haplotypes per matrix-core workgroup
+    // the matrix-core launches' hit lists (ScanArgs::hitl / hitn)
+    const uint32_t *hitl, *hitn;
+    uint32_t cand_cap;
+    const HitSrc *srcs;
+    uint32_t n_srcs;
+    uint32_t mfma;              // 0: the matrix-core kernel did not run (no hit lists, no reference hits)
+    // reference hits per region, and the spill records bucketed by region
+    const uint32_t *ref_hits, *ref_count;
+    const uint32_t *spill_sorted, *spill_off;
+    uint32_t n_spill;           // 0: no spill records (spill_off unused)
+    uint32_t *counts;           // dense counts: read (LUT/generic slots) / written (mode 1)
+    uint32_t dense_base;        // != 0: counts exist (haps' count_off are valid)
+    uint32_t *scratch;          // counters of regions with more haplotypes than the LDS block holds
+    int mode;                   // 0: classify + compact varying keys, 1: dense counts
+    // mode 0 outputs: per key (region inner_off * n_slots + j) the first
+    // haplotype's count and KeyFlags; the varying keys (var_tot[0] of
+    // var_keys_cap) with their counts (var_tot[1] of var_cap u32)
+    uint32_t *key_first;
+    uint8_t *key_flags;
+    DevVarKey *var_keys;
+    uint32_t var_keys_cap;
+    uint32_t *var_counts;
+    uint64_t var_cap;
+    uint32_t *var_tot;
+};
+
+int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
+uint32_t key_asm_lds_counters();  // regions with more distinct haplotypes use AsmArgs::scratch
+// Buckets the spill records (ScanArgs::spill, *over of cap) by region: boff[r]
+// .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters).
+int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spill, uint32_t n_regions, uint32_t *bcnt,
+                         uint32_t *boff, uint32_t *sorted, hipStream_t stream);
+// One workgroup per key: counts_as_genotypes' per-sample half over the
+// region's distinct haplotype pairs: pab[pair_off[r] + p] = a | b << 8 (the
+// distinct indices of a sample's two haplotypes), pcnt[..] the samples with that
+// pair, pidx (u16, one row of n_samples per region of the chunk, region -
+// region0) each sample's pair.  Writes hdr[k], vals[k *
+// 256 ..] (sorted distinct totals), hist[k * 256 ..] (samples per value) and
+// codes[k * n_samples ..].
+int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint16_t *pab,
+                      const uint32_t *pcnt, const uint32_t *pair_off, const uint16_t *pidx, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream);
 int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_samples, const uint64_t *off, uint8_t *dst,
                         hipStream_t stream);
-int launch_key_gather(const DevHap *haps, const DevRegion *regions, const uint32_t *counts, uint32_t n_slots,
-                      const DevVarKey *keys, uint32_t n_keys, uint32_t *out, hipStream_t stream);
 
 }  // namespace tfbs

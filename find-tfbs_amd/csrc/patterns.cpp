@@ -253,6 +253,8 @@ int Patterns::build_plan(const PlanOptions &opt, Plan *plan) const {
         for (int i : g.strands) m = m && mfma_eligible(pats[i]);
         (m ? mat : lut).push_back(std::move(g));
     }
+    plan->slot_mfma.assign(groups.size(), 0);
+    for (const SlotGroup &g : mat) plan->slot_mfma[g.slot] = 1;
     build_fast_tiles(*this, lut, opt.tile_blocks, plan);
     build_mfma_tiles(*this, mat, opt, plan);
     // --- generic (long) strands: one tile per pattern_id group, weights x5

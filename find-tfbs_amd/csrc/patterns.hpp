@@ -22,6 +22,7 @@ struct Pat {  // Pattern (types.rs:86-90)
 
 struct Plan {
     std::vector<uint16_t> slot_pid;  // slot -> pattern_id
+    std::vector<uint8_t> slot_mfma;  // slot -> 1 if the matrix-core kernel scores it (sparse hits), 0: LUT/generic
     std::vector<DevUnit> fast_units;
     std::vector<DevTile> fast_tiles;
     std::vector<int32_t> lut;        // blocks x 256 codes x 16 bytes (8 x int16 or 4 x int32)

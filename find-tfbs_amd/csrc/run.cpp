@@ -101,6 +101,10 @@ template <class Emit> int run_shard(const RunSetup &S, Shard &sh, Emit &&emit) {
     if ((rc = fasta.open(a->reference))) return rc;
     tfbs_ctx *ctx = nullptr;
     if ((rc = tfbs_ctx_create(sh.device, S.pp, &ctx))) return rc;
+    if ((rc = tfbs_ctx_set_host_threads(ctx, sh.threads))) {
+        tfbs_ctx_destroy(ctx);
+        return rc;
+    }
     std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
     std::vector<const BcfRecord *> recs;

@@ -20,11 +20,14 @@ struct ScanArgs {
     const int32_t *gw;          // generic path: 5 weights per column
     const DevHap *haps;
     uint32_t n_haps;
+    uint32_t hap_base;          // batch index of haps[0] (a launch over a later part of the batch)
     const DevRegion *regions;
     const int32_t *inner;
     const uint32_t *words;
     const uint32_t *nmask;
     const int32_t *posrel;
+    // dense counts [count_off + key * count_stride] of the slots the LUT and generic
+    // kernels score (stores); nullptr when every slot is on the matrix cores
     uint32_t *counts;
     uint32_t haps_per_block;
     const DevMSuper *msupers;   // matrix-core path
@@ -43,25 +46,35 @@ struct ScanArgs {
     uint32_t *cands;  // kCandWords per entry
     uint32_t cand_cap;
     uint32_t region_base;
+    // matrix-core hits, sparse (no count matrix, no atomics): the wave that
+    // rescores its candidates appends one (haplotype, key = slot * n_inner +
+    // range) pair per hit and overlapped inner range to its part of the
+    // workgroup's hit list (hitl + 2 (wg cand_cap + wave cand_cap / 8), the same
+    // geometry as the candidate list) and stores their number at hitn[8 wg +
+    // wave]; the excess goes to the spill list
+    uint32_t *hitl;
+    uint32_t *hitn;
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
     // != 0 scans only their dirty window tiles; the HAP_REF haplotypes' hits
     // (strand, window) are listed per region (ref_count[r] of kRefPerRegion at
-    // ref_hits + 2 kRefPerRegion r), the excess in an overflow list of
-    // (region, strand, window) (*ref_over_count of ref_over_cap), for the
-    // fix-up kernels
+    // ref_hits + 2 kRefPerRegion r), the excess in the spill list
     uint32_t dedup;
     uint32_t n_regions;
     uint32_t *ref_hits;
     uint32_t *ref_count;
-    uint32_t *ref_over;
-    uint32_t *ref_over_count;  // [0] reference hits, [1] candidates past a wave's list
-    uint32_t ref_over_cap;
+    // spill list: (region | kind << 31, x, y) records -- kind 0 a hit (haplotype,
+    // key), kind 1 a reference hit (strand, window) -- counted at over[0] (of
+    // spill_cap), bucketed by region after the scan (launch_spill_buckets)
+    uint32_t *spill;
+    uint32_t *over;  // [0] spill records, [1] candidates past a wave's list
+    uint32_t spill_cap;
     // candidates past a wave's list region: (haplotype, strand, window) triples,
-    // rescored by a kernel after the scan (launch_ref_fixup)
+    // rescored by a kernel after the scan (launch_post_scan)
     uint32_t *cand_over;
     uint32_t cand_over_cap;
 };
 constexpr uint32_t kRefPerRegion = 64;
+constexpr uint32_t kMBlockWaves = 8;  // waves per matrix-core workgroup (hit list parts per workgroup)
 constexpr uint32_t kCandWords = 2;  // candidate list entry: strand | haplotype in the group << 24, window
 
 struct LaunchConfig {
@@ -75,15 +88,22 @@ int launch_fast(const ScanArgs &a, const LaunchConfig &cfg, uint32_t n_haps, hip
 int launch_generic(const ScanArgs &a, uint32_t n_haps, hipStream_t stream);
 // Opts the fast kernel into more than 64 KiB of dynamic LDS.
 int fast_kernel_set_lds(const LaunchConfig &cfg);
-// Matrix-core scan (scan_mfma.hip); counts must be zeroed first (atomic adds).
+// The workgroups of one matrix-core launch: hap groups [g0, g0 + ng) x ns super
+// tiles, workgroup wg_base + (g - g0) ns + super; their hit lists are read back
+// per region by the key assembly (key_kernels.hip).
+struct HitSrc {
+    uint32_t wg_base, ns, g0, ng;
+};
+constexpr int kMaxHitSrcs = 64;
+// Matrix-core scan (scan_mfma.hip): sparse hits (hitl / hitn / spill), no counts.
 // group_words: the most packed words any haplotype group of haps_per_block spans.
 // One launch per K depth, spread round-robin over `streams` (deepest first);
-// supers: the host copy of a.msupers (sorted by depth).
+// supers: the host copy of a.msupers (sorted by depth); srcs receives one
+// HitSrc per launch (*n_srcs of kMaxHitSrcs).
 int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
-                const hipStream_t *streams, uint32_t n_streams);
-// Adds to every HAP_DEDUP haplotype the reference's hits in the windows it did
-// not scan (after launch_mfma on the same stream; a: as for launch_mfma).
-int launch_ref_fixup(const ScanArgs &a, hipStream_t stream);
+                const hipStream_t *streams, uint32_t n_streams, HitSrc *srcs, uint32_t *n_srcs);
+// Rescores the candidates past the waves' lists (after launch_mfma on the same stream).
+int launch_post_scan(const ScanArgs &a, hipStream_t stream);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach
 // the waves per SIMD its registers allow.

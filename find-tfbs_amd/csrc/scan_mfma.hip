@@ -30,9 +30,10 @@
 //    wave's region of a global (L2-resident) list, and when the wave has
 //    scanned it rescores those exactly, one per lane (pattern.rs:125-151),
 //    applies the inner-range overlap test (range.rs:18-21 as main.rs:503 uses
-//    it) and adds to the count of the strand's pattern_id slot atomically
-//    (counts are zeroed before the scan); a full wave list spills to a
-//    launch-wide list rescored by cand_over_kernel after the scan.
+//    it) and appends one (haplotype, key) pair per hit and overlapped range to
+//    its part of the workgroup's hit list (no count matrix, no atomics: the
+//    key assembly, key_kernels.hip, counts them per region); a full wave list
+//    spills to a launch-wide list rescored by cand_over_kernel after the scan.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -61,6 +62,7 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kMBlock = 512;          // 8 waves (two per SIMD) share one super tile image
+static_assert(kMBlock / 64 == kMBlockWaves, "hit list parts per workgroup");
 constexpr int kMOnehotBytes = 2048;   // LDS: one-hot table (4-mer -> 4 x 16 bits of FP4), image, words
 constexpr uint32_t kMStagedMax = 80 * 1024;  // LDS per workgroup at 2 workgroups per CU (160 KiB)
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
@@ -217,13 +219,28 @@ __device__ __forceinline__ int32_t exact_score(const uint32_t *words, const DevH
     return s;
 }
 
+// Appends a record to the spill list (rare: hits past a wave's list, reference
+// hits past a region's list, inner ranges past 32).
+__device__ __forceinline__ void spill_record(const ScanArgs &A, uint32_t head, uint32_t x, uint32_t y) {
+    const uint32_t o = atomicAdd(A.over, 1u);
+    if (o < A.spill_cap) {
+        A.spill[3 * (size_t)o] = head;
+        A.spill[3 * (size_t)o + 1] = x;
+        A.spill[3 * (size_t)o + 2] = y;
+    }
+}
+
 // Exact rescoring of one candidate: window i of haplotype hp (hits index hap)
-// for the strand g = global tile * 64 + strand in tile; a hit adds to its
-// slot's count for every inner range it overlaps.  The loads are issued in
-// three dependent rounds (strand fields | weights, region, position, N mask |
-// inner ranges) before the atomics.
-__device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_t *words, const DevHap &hp,
-                                                uint32_t hap, uint32_t g, uint32_t i) {
+// for the strand g = global tile * 64 + strand in tile.  Returns the hit's
+// inner ranges k < 32 (bit k; key = *key0 + k) to be listed by the caller;
+// ranges past 32 go to the spill list here.  A hit of the region's reference
+// haplotype is also listed for the reuse of its window by the HAP_DEDUP
+// haplotypes; a helper reference haplotype (past the region's distinct
+// haplotypes) has no counts of its own.  The loads are issued in three
+// dependent rounds (strand fields | weights, region, position, N mask | inner
+// ranges).
+__device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uint32_t *words, const DevHap &hp,
+                                                    uint32_t hap, uint32_t g, uint32_t i, uint32_t *key0) {
     const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
     const uint32_t sn = g & 63u;
     const int4 sf = *reinterpret_cast<const int4 *>(meta + kGStrandInts * sn);  // min, woff, len, slot
@@ -236,35 +253,12 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
         live = ~__builtin_amdgcn_alignbit(m[1], m[0], ic & 31);
     }
     const uint32_t L = (uint32_t)sf.z;
-    if (i + L > hp.len) return;                         // past the end (pattern.rs:147-150)
+    if (i + L > hp.len) return 0;                       // past the end (pattern.rs:147-150)
     const int32_t sc = exact_score(words, hp, i, L, A.mweights + sf.y, live);
 #if TFBS_MFMA_PROBE == 4
     atomicAdd(&g_probe[sc > sf.x ? 1 : 2], 1ull);
 #endif
-    if (!(sc > sf.x)) return;                           // strict (pattern.rs:151)
-    const uint32_t off0 = (uint32_t)sf.w * rg.n_inner;
-    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-    // range.rs:18-21 as main.rs:503 uses it: every range's bounds loaded before
-    // the first atomic (which the loads could alias)
-    uint32_t mask = 0;
-    const uint32_t nk = min(rg.n_inner, 32u);
-    for (uint32_t k = 0; k < nk; k++) {
-        const int2 r = *reinterpret_cast<const int2 *>(inner + 2 * k);
-        const uint32_t span = (uint32_t)(r.y - r.x);
-        if ((uint32_t)(p - r.x) <= span || (uint32_t)(p + (int32_t)L - 1 - r.x) <= span) mask |= 1u << k;
-    }
-#if TFBS_MFMA_PROBE == 19
-    asm volatile("" ::"v"(mask), "v"(off0));
-    return;  // timing only: no count atomics
-#endif
-    for (; mask; mask &= mask - 1)
-        atomicAdd(A.counts + hp.count_off + (size_t)(off0 + __builtin_ctz(mask)) * rg.count_stride, 1u);
-    for (uint32_t k = 32; k < rg.n_inner; k++) {        // ranges past 32 (rare)
-        const int32_t s = inner[2 * k], en = inner[2 * k + 1];
-        const uint32_t span = (uint32_t)(en - s);
-        if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-            atomicAdd(A.counts + hp.count_off + (size_t)(off0 + k) * rg.count_stride, 1u);
-    }
+    if (!(sc > sf.x)) return 0;                         // strict (pattern.rs:151)
     if (A.hits && i / 64 < A.hits_wpp)
         atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + sn]) * A.hits_wpp + i / 64,
                  1ull << (i & 63));
@@ -274,14 +268,28 @@ __device__ __forceinline__ void score_candidate(const ScanArgs &A, const uint32_
             A.ref_hits[2 * ((size_t)hp.region * kRefPerRegion + at)] = g;
             A.ref_hits[2 * ((size_t)hp.region * kRefPerRegion + at) + 1] = i;
         } else {
-            const uint32_t o = atomicAdd(A.ref_over_count, 1u);
-            if (o < A.ref_over_cap) {
-                A.ref_over[3 * (size_t)o] = hp.region;
-                A.ref_over[3 * (size_t)o + 1] = g;
-                A.ref_over[3 * (size_t)o + 2] = i;
-            }
+            spill_record(A, hp.region | 0x80000000u, g, i);
         }
     }
+    if (hap >= rg.hap_begin + rg.hap_count) return 0;  // a helper reference haplotype: no keys
+    const uint32_t off0 = (uint32_t)sf.w * rg.n_inner;
+    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
+    // range.rs:18-21 as main.rs:503 uses it
+    uint32_t mask = 0;
+    const uint32_t nk = min(rg.n_inner, 32u);
+    for (uint32_t k = 0; k < nk; k++) {
+        const int2 r = *reinterpret_cast<const int2 *>(inner + 2 * k);
+        const uint32_t span = (uint32_t)(r.y - r.x);
+        if ((uint32_t)(p - r.x) <= span || (uint32_t)(p + (int32_t)L - 1 - r.x) <= span) mask |= 1u << k;
+    }
+    for (uint32_t k = 32; k < rg.n_inner; k++) {        // ranges past 32 (rare)
+        const int32_t s = inner[2 * k], en = inner[2 * k + 1];
+        const uint32_t span = (uint32_t)(en - s);
+        if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
+            spill_record(A, hp.region, A.hap_base + hap, off0 + k);
+    }
+    *key0 = off0;
+    return mask;
 }
 
 // Drains the wave's first n queue entries, one entry per lane per pass: the
@@ -355,9 +363,9 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
                     list[slot] = make_uint2(g | (hl << 24), i);
                 } else {  // rescored after the scan (no rescoring code, whose loads would stay
                           // pending, in the scan loop)
-                    const uint32_t o = atomicAdd(A.ref_over_count + 1, 1u);
+                    const uint32_t o = atomicAdd(A.over + 1, 1u);
                     if (o < A.cand_over_cap) {
-                        A.cand_over[3 * (size_t)o] = h0 + hl;
+                        A.cand_over[3 * (size_t)o] = A.hap_base + h0 + hl;  // batch index
                         A.cand_over[3 * (size_t)o + 1] = g;
                         A.cand_over[3 * (size_t)o + 2] = i;
                     }
@@ -369,19 +377,41 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
 }
 
 // The wave's listed candidates, one per lane (after its scan: no accumulator
-// is live, and the other waves keep the matrix cores busy).
+// is live, and the other waves keep the matrix cores busy); each hit's
+// (haplotype, key) pairs are appended to the wave's part of the workgroup's hit
+// list in lane order (ballot prefix: no atomics), the excess spilled.
 __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *words, uint32_t h0, uint32_t wave,
                                              uint32_t lane, uint32_t cn) {
-#if TFBS_MFMA_PROBE == 13
-    return;  // timing only: listed candidates are dropped
-#endif
-    const uint32_t n = min(cn, wave_cand_cap(A));
+    const uint32_t cap = wave_cand_cap(A);
+    const size_t part = (size_t)(A.region_base + blockIdx.x) * A.cand_cap + (size_t)wave * cap;
+    uint2 *out = reinterpret_cast<uint2 *>(A.hitl) + part;
+    uint32_t hn = 0;  // wave-uniform
+#if TFBS_MFMA_PROBE != 13  // 13: listed candidates are dropped (timing only)
+    const uint32_t n = min(cn, cap);
     const uint2 *list = cand_list(A, wave);
-    for (uint32_t k = lane; k < n; k += 64) {
-        const uint2 c = list[k];
-        const uint32_t hap = h0 + (c.x >> 24);
-        score_candidate(A, words, A.haps[hap], hap, c.x & 0xFFFFFFu, c.y);
+    for (uint32_t k0 = 0; k0 < n; k0 += 64) {
+        const uint32_t k = k0 + lane;
+        uint32_t mask = 0, key0 = 0, hap = 0;
+        if (k < n) {
+            const uint2 c = list[k];
+            hap = h0 + (c.x >> 24);
+            mask = score_candidate(A, words, A.haps[hap], hap, c.x & 0xFFFFFFu, c.y, &key0);
+        }
+        uint64_t act;
+        while ((act = __ballot(mask != 0)) != 0) {
+            if (mask) {
+                const uint32_t at = hn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
+                const uint32_t key = key0 + __builtin_ctz(mask);
+                mask &= mask - 1;
+                if (at < cap) out[at] = make_uint2(A.hap_base + hap, key);
+                else spill_record(A, A.haps[hap].region, A.hap_base + hap, key);
+            }
+            hn += (uint32_t)__popcll(act);
+        }
     }
+#endif
+    if (lane == 0) A.hitn[(size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave] = min(hn, cap);
 }
 
 // Coarse test of one tile: OR of the lane's 16 outputs, the fields' top bits
@@ -453,6 +483,32 @@ __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, co
     }
 }
 
+// round_scores and both tests with the second tile's MFMAs interleaved with the
+// first tile's test (a wave's own VALU issues in its MFMA gaps; TFBS_MFMA_ILV).
+#ifndef TFBS_MFMA_ILV
+#define TFBS_MFMA_ILV 0
+#endif
+template <int D, int NK>
+__device__ __forceinline__ void round_tested(const char *tile, uint32_t lane, const v4i (&a0)[NK],
+                                             const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1,
+                                             uint32_t &x0, uint32_t &x1) {
+    BFrag f[D];
+    load_frags<D>(tile, lane, f);
+    c0 = cb;
+#pragma unroll
+    for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+    c1 = mfma_chunk(a1[0], f[0], cb, sa);
+    // the first tile's test sits between the second tile's first and later MFMAs
+    // (after the last one for D = 1): scheduling barriers keep that order
+    __builtin_amdgcn_sched_barrier(0);
+    x0 = coarse_test(c0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kc = 1; kc < D; kc++) c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+    __builtin_amdgcn_sched_barrier(0);
+    x1 = coarse_test(c1);
+}
+
 template <int D, int NK>
 __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v16f &cb,
                                             int sa, v16f &c0) {
@@ -476,8 +532,14 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
         for (uint32_t ti = tb; ti < te; ti++) {
             const char *tile = img + (ti - tb) * kTB;
             v16f c0, c1;
-            round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
+            uint32_t x0, x1;
+            if (TFBS_MFMA_ILV) {
+                round_tested<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1, x0, x1);
+            } else {
+                round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                x0 = coarse_test(c0);
+                x1 = coarse_test(c1);
+            }
             const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
             if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
             // cold: queue the firing tiles; a tile whose entries do not fit
@@ -658,118 +720,17 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
 }
 
-// Reference-window reuse.  A HAP_DEDUP haplotype whose window tile of a
-// reference hit (strand g, window i) was not scanned (the tile holds no base
-// differing from the reference) has the same bases and positions there, so it
-// has the hit too: its counts get the hit's inner-range overlaps (range.rs:18-21
-// as main.rs:503 uses it).
-__device__ __forceinline__ uint32_t ref_hit_overlaps(const ScanArgs &A, const DevRegion &rg, uint32_t g, uint32_t i,
-                                                     uint32_t &nk, uint32_t &off0) {
-    const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-    const uint32_t sn = g & 63u, L = (uint32_t)meta[kGStrandInts * sn + kGLen];
-    nk = (uint32_t)meta[kGDepth];
-    off0 = (uint32_t)meta[kGStrandInts * sn + kGSlot] * rg.n_inner;
-    const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-    const int32_t p = (int32_t)i;  // the reference's positions are affine
-    uint32_t mask = 0;             // bit k: the match overlaps inner range k (k < 32)
-    for (uint32_t k = 0; k < rg.n_inner && k < 32; k++) {
-        const int32_t s = inner[2 * k], en = inner[2 * k + 1];
-        const uint32_t span = (uint32_t)(en - s);
-        if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span) mask |= 1u << k;
-    }
-    return mask;
-}
-
-// One workgroup per region: its listed reference hits in LDS, one thread per
-// distinct haplotype.
-constexpr uint32_t kFixBlock = 128;
-__global__ __launch_bounds__(kFixBlock) void ref_fixup_kernel(ScanArgs A) {
-    __shared__ uint32_t s_g[kRefPerRegion], s_i[kRefPerRegion], s_nk[kRefPerRegion], s_off[kRefPerRegion],
-        s_mask[kRefPerRegion];
-    const uint32_t region = blockIdx.x;
-    const DevRegion rg = A.regions[region];
-    if (rg.ref_hap == UINT32_MAX || rg.n_inner == 0) return;
-    const uint32_t n = min(A.ref_count[region], kRefPerRegion);
-    if (n == 0) return;
-    for (uint32_t t = threadIdx.x; t < n; t += kFixBlock) {
-        const uint32_t g = A.ref_hits[2 * ((size_t)region * kRefPerRegion + t)];
-        const uint32_t i = A.ref_hits[2 * ((size_t)region * kRefPerRegion + t) + 1];
-        uint32_t nk, off0;
-        s_mask[t] = ref_hit_overlaps(A, rg, g, i, nk, off0);
-        s_g[t] = g;
-        s_i[t] = i;
-        s_nk[t] = nk;
-        s_off[t] = off0;
-    }
-    __syncthreads();
-    for (uint32_t h = rg.hap_begin + threadIdx.x; h < rg.hap_begin + rg.hap_count; h += kFixBlock) {
-        const DevHap hp = A.haps[h];
-        if (!(hp.flags & HAP_DEDUP)) continue;
-        for (uint32_t t = 0; t < n; t++) {
-            if ((hp.dirty[s_nk[t] - 1] >> (s_i[t] / kMWindows)) & 1u) continue;  // scanned
-            // no-return atomics: issued back to back (a plain add would wait on
-            // every load, as the adds may alias)
-            // lanes are consecutive haplotypes: one key's counts are adjacent
-            for (uint32_t m = s_mask[t]; m; m &= m - 1)
-                atomicAdd(A.counts + hp.count_off + (size_t)(s_off[t] + __builtin_ctz(m)) * rg.count_stride, 1u);
-        }
-    }
-    // inner ranges past 32 (rare): atomics, as the overflow list
-    if (rg.n_inner > 32) {
-        __syncthreads();
-        for (uint32_t t = 0; t < n; t++) {
-            const uint32_t g = s_g[t], i = s_i[t];
-            const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-            const uint32_t L = (uint32_t)meta[kGStrandInts * (g & 63u) + kGLen];
-            const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-            for (uint32_t h = rg.hap_begin + threadIdx.x; h < rg.hap_begin + rg.hap_count; h += kFixBlock) {
-                const DevHap hp = A.haps[h];
-                if (!(hp.flags & HAP_DEDUP) || ((hp.dirty[s_nk[t] - 1] >> (i / kMWindows)) & 1u)) continue;
-                for (uint32_t k = 32; k < rg.n_inner; k++) {
-                    const int32_t s = inner[2 * k], en = inner[2 * k + 1];
-                    const uint32_t span = (uint32_t)(en - s);
-                    if ((uint32_t)((int32_t)i - s) <= span || (uint32_t)((int32_t)(i + L) - 1 - s) <= span)
-                        atomicAdd(A.counts + hp.count_off + (size_t)(s_off[t] + k) * rg.count_stride, 1u);
-                }
-            }
-        }
-    }
-}
-
-// Candidates past the waves' list regions (drain_queue), one per thread; before
-// ref_fixup_kernel (a reference haplotype's hits are listed for it).
+// Candidates past the waves' list regions (drain_queue), one per thread; their
+// hits go to the spill list.
 __global__ __launch_bounds__(256) void cand_over_kernel(ScanArgs A) {
-    const uint32_t n = min(A.ref_over_count[1], A.cand_over_cap);
+    const uint32_t n = min(A.over[1], A.cand_over_cap);
     for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
         const uint32_t hap = A.cand_over[3 * (size_t)k], g = A.cand_over[3 * (size_t)k + 1];
-        score_candidate(A, A.words, A.haps[hap], hap, g, A.cand_over[3 * (size_t)k + 2]);
-    }
-}
-
-// The overflow list (regions with more than kRefPerRegion reference hits): one
-// wave per hit, atomics (runs after ref_fixup_kernel).
-__global__ __launch_bounds__(256) void ref_fixup_over_kernel(ScanArgs A) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t n = min(*A.ref_over_count, A.ref_over_cap);
-    for (uint32_t r = blockIdx.x * 4 + (threadIdx.x >> 6); r < n; r += gridDim.x * 4) {
-        const uint32_t region = A.ref_over[3 * (size_t)r], g = A.ref_over[3 * (size_t)r + 1];
-        const uint32_t i = A.ref_over[3 * (size_t)r + 2];
-        const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
-        const uint32_t sn = g & 63u, L = (uint32_t)meta[kGStrandInts * sn + kGLen], nk = (uint32_t)meta[kGDepth];
-        const DevRegion rg = A.regions[region];
-        const uint32_t off0 = (uint32_t)meta[kGStrandInts * sn + kGSlot] * rg.n_inner;
-        const int32_t *inner = A.inner + 2 * (size_t)rg.inner_off;
-        const int32_t p = (int32_t)i;
-        for (uint32_t h = rg.hap_begin + lane; h < rg.hap_begin + rg.hap_count; h += 64) {
-            const DevHap hp = A.haps[h];
-            if (!(hp.flags & HAP_DEDUP) || ((hp.dirty[nk - 1] >> (i / kMWindows)) & 1u)) continue;
-            for (uint32_t k = 0; k < rg.n_inner; k++) {
-                const int32_t s = inner[2 * k], en = inner[2 * k + 1];
-                const uint32_t span = (uint32_t)(en - s);
-                if ((uint32_t)(p - s) <= span || (uint32_t)(p + (int32_t)L - 1 - s) <= span)
-                    atomicAdd(A.counts + hp.count_off + (size_t)(off0 + k) * rg.count_stride, 1u);
-            }
-        }
+        const DevHap hp = A.haps[hap];
+        uint32_t key0 = 0;
+        for (uint32_t m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0); m;
+             m &= m - 1)
+            spill_record(A, hp.region, hap, key0 + __builtin_ctz(m));
     }
 }
 
@@ -783,14 +744,11 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_dept
 
 }  // namespace
 
-int launch_ref_fixup(const ScanArgs &a, hipStream_t stream) {
+int launch_post_scan(const ScanArgs &a, hipStream_t stream) {
     hipLaunchKernelGGL(cand_over_kernel, dim3(256), dim3(256), 0, stream, a);
-    if (a.n_regions == 0) return 1;
-    hipLaunchKernelGGL(ref_fixup_kernel, dim3(a.n_regions), dim3(kFixBlock), 0, stream, a);
-    hipLaunchKernelGGL(ref_fixup_over_kernel, dim3(1024), dim3(256), 0, stream, a);
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("ref_fixup_kernel launch: ") + hipGetErrorString(e));
-    return 3;
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("cand_over_kernel launch: ") + hipGetErrorString(e));
+    return 1;
 }
 
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
@@ -812,7 +770,8 @@ void mfma_depth_budgets(uint32_t out[9]) {
 }
 
 int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words,
-                uint32_t n_haps, const hipStream_t *streams, uint32_t n_streams) {
+                uint32_t n_haps, const hipStream_t *streams, uint32_t n_streams, HitSrc *srcs, uint32_t *n_srcs) {
+    *n_srcs = 0;
     if (n_haps == 0 || n_supers == 0) return 0;
     const uint32_t hpb = a0.haps_per_block;
     // candidate list entries: global strand < 2^24, haplotype in the group < 2^8
@@ -857,9 +816,12 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.msupers = a0.msupers + s0;
             a.n_msupers = ns;
             a.haps = a0.haps + h0;
+            a.hap_base = a0.hap_base + h0;
             a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
             a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
             a.region_base = region;
+            if (*n_srcs >= (uint32_t)kMaxHitSrcs) return fail(TFBS_E_ARG, "matrix-core scan: too many launches");
+            srcs[(*n_srcs)++] = HitSrc{region, ns, (uint32_t)g0, ng};
             region += ns * ng;
             a.mimg_max = (uint32_t)img_bytes;
             hipLaunchKernelGGL(kern, dim3(ns * ng), dim3(kMBlock), lds, stream, a);

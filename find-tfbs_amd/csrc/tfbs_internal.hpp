@@ -165,7 +165,9 @@ struct DevRegion {
     // counts for every haplotype of the region (the helper's included) are
     // consecutive, count_stride apart from the next key's
     uint32_t count_stride;
-    uint32_t pad[2];
+    // key assembly scratch (u32 counters) of a region with more distinct
+    // haplotypes than the assembly's LDS block holds (key_kernels.hip)
+    uint64_t big_off;
 };
 
 // Per-sample encoding of one varying key (tfbs_batch_encode, key_encode_kernel):
@@ -182,6 +184,7 @@ struct EncHdr {
 constexpr uint32_t kEncMaxVals = 255;       // u8 codes
 constexpr uint32_t kEncMaxRange = 1u << 16;  // value bitmap of hi - lo + 1 bits in LDS
 constexpr uint32_t kEncMaxHaps = 255;       // u8 membership: distinct haplotypes per region
+constexpr uint32_t kEncMaxPairs = 8192;     // distinct (left, right) haplotype pairs per region (LDS)
 
 // One key (region, slot * n_inner + range) whose distinct-haplotype counts differ;
 // the gather copies its hap_count counts to out_off (tfbs_batch_reduce).

@@ -130,6 +130,9 @@ int tfbs_device_count(int *n);
 int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out);
 void tfbs_ctx_destroy(tfbs_ctx *ctx);
 int tfbs_ctx_sync(tfbs_ctx *ctx);
+/* Host threads the ctx's host-side work may use (tfbs_batch_encode's staging;
+ * default min(16, hardware threads)): a run with one ctx per device passes its share. */
+int tfbs_ctx_set_host_threads(tfbs_ctx *ctx, uint32_t threads);
 /* Device time (HIP events on the ctx stream) of the last tfbs_scan, ms. */
 float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx);
 /* Number of scan-kernel launches issued by the last tfbs_scan. */
@@ -196,7 +199,7 @@ int tfbs_batch_region_add_record_carriers(tfbs_batch *b, uint64_t pos, const cha
 int tfbs_batch_region_end(tfbs_batch *b);
 
 size_t tfbs_batch_num_regions(const tfbs_batch *b);
-size_t tfbs_batch_num_haplotypes(const tfbs_batch *b); /* distinct haplotypes to scan */
+size_t tfbs_batch_num_haplotypes(const tfbs_batch *b); /* distinct haplotypes (number_of_haplotypes, main.rs:97-130) */
 /* Windows the scan scores: sum over distinct haplotypes and PWM patterns of max(0, len - L + 1). */
 uint64_t tfbs_batch_num_windows(const tfbs_batch *b);
 /* Column lookups the scan performs: sum over windows of the pattern length L. */

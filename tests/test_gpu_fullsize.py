@@ -261,6 +261,7 @@ def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
 
     n_samples, _, _, _, indel, seed = C4
     n_regions = 3000
+    rows_at = _spread(n_regions, 60)  # rows of 50 000 samples are 0.4 MB each: text on a spread
     ps = _patterns(tmp_path, C4)
     whole = T.RegionBatch(ps, n_samples)
     whole.synth_fill(seed, 0, n_regions, indel)
@@ -268,12 +269,12 @@ def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
     try:
         whole.scan(sc, reduce=True)
         want = [whole.key_digest_sum(r) for r in range(n_regions)]
-        want_rows = [sorted(_strip_pos(whole.region_rows(r, "chr1")[0])) for r in range(n_regions)]
+        want_rows = [sorted(_strip_pos(whole.region_rows(r, "chr1")[0])) for r in rows_at]
     finally:
         sc.close()
     del whole
     got = [0] * n_regions
-    got_rows = [[] for _ in range(n_regions)]
+    got_rows = [[] for _ in rows_at]
     pids = []
     for part in range(2):
         sub = bench.shard_patterns(T, ps, part, 2)
@@ -285,7 +286,8 @@ def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
             b.scan(sc, reduce=True)
             for r in range(n_regions):
                 got[r] = (got[r] + b.key_digest_sum(r)) % (1 << 64)
-                got_rows[r] += _strip_pos(b.region_rows(r, "chr1")[0])
+            for q, r in enumerate(rows_at):
+                got_rows[q] += _strip_pos(b.region_rows(r, "chr1")[0])
         finally:
             sc.close()
         del b
@@ -293,4 +295,4 @@ def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
     bad = [r for r in range(n_regions) if got[r] != want[r]]
     assert not bad, bad[:10]
     assert [sorted(x) for x in got_rows] == want_rows
-    assert sum(len(x) for x in want_rows) > 1000
+    assert sum(len(x) for x in want_rows) > 200
