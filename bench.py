@@ -202,6 +202,22 @@ def cpu_baseline(T, ps, args, budget_s):
             "matrix": matrix}
 
 
+def host_bgzf_sample(T, batch, sc, threads, n_regions=8):
+    """The host writer (zlib level 6 deflate, the run flow's TFBS_GPU_BGZF=0 and
+    multi-device path) on the rows of the first regions: its single-thread rate and
+    the time the batch's text would take on `threads` threads at that rate."""
+    L = T.lib()
+    import ctypes as C
+    batch.encode(sc, 0, min(n_regions, batch.num_regions))
+    text = b"".join(batch.region_rows(i, "chr1")[0].encode() for i in range(min(n_regions, batch.num_regions)))
+    if not text:
+        return None
+    t = time.perf_counter()
+    T.check(L.tfbs_bgzf_write_file(os.devnull.encode(), C.c_char_p(text), len(text), 0))
+    dt = time.perf_counter() - t
+    return {"sample_bytes": len(text), "seconds_1_thread": dt, "mb_per_s_1_thread": len(text) / dt / 1e6}
+
+
 def shard_plan(args, rank, world):
     """(first region, regions, pattern shard index, pattern shards) of rank r (SURVEY.md
     8(e)): the 1-D region shard, or the 2-D region x PWM split (module docstring)."""
@@ -301,7 +317,7 @@ def main():
     t_prep = time.perf_counter()
     batch = shard_batch(T, ps, args, rank, world, window_lmax=ps_all.max_length if parts > 1 else None)
     t_prep = time.perf_counter() - t_prep
-    gen_s, build_s, commit_s, fill_s = batch.prep_seconds()
+    gen_s, build_s, prep_wall, fill_s = batch.prep_seconds()  # prep_wall: build_region + commit, no generation
     t_up = time.perf_counter()
     T.check(L.tfbs_batch_upload(sc.h, batch.h))
     t_up = time.perf_counter() - t_up
@@ -312,19 +328,28 @@ def main():
     t_red = time.perf_counter()
     T.check(L.tfbs_batch_reduce(sc.h, batch.h))
     t_red = time.perf_counter() - t_red
-    n_rows = n_row_bytes = 0
+    n_rows = n_row_bytes = n_bgzf = 0
     t_rows = t_enc = 0.0
-    if not args.no_e2e:  # device per-sample encoding + row formatting, 512 regions at a time (the run flow's batch)
+    host_bgzf = None
+    if not args.no_e2e:
+        # device per-sample encoding, then the rows as BGZF blocks made on the device
+        # (tfbs_batch_rows_bgzf: heads on the host, genotype text + deflate + CRC32 on the
+        # GPU), 512 regions at a time (the run flow's batch); the blocks reach host memory
+        # (the file write is not timed)
+        fake = 1
         for r0 in range(0, batch.num_regions, 512):
             r1 = min(batch.num_regions, r0 + 512)
             t = time.perf_counter()
-            batch.encode(sc, r0, r1)
+            batch.encode(sc, r0, r1, device_codes=True)
             t_enc += time.perf_counter() - t
             t = time.perf_counter()
-            nr, nb = batch.format_rows("chr1", 0, threads, r0, r1)
+            data, fake, nr, nb = batch.rows_bgzf(sc, "chr1", 0, fake, r0, r1)
             t_rows += time.perf_counter() - t
             n_rows += nr
             n_row_bytes += nb
+            n_bgzf += len(data)
+            del data
+        host_bgzf = host_bgzf_sample(T, batch, sc, threads)
 
     # ---- timed scan loop
     for _ in range(args.warmup):
@@ -356,7 +381,9 @@ def main():
     T.check(L.tfbs_batch_download(sc.h, batch.h))
     t_dense = time.perf_counter() - t_dense
 
-    e2e_s = fill_s + t_up + t_scan1 + t_red + t_enc + t_rows
+    e2e_s = prep_wall + t_up + t_scan1 + t_red + t_enc + t_rows
+    if host_bgzf:
+        host_bgzf["estimate_s_%d_threads" % threads] = n_row_bytes / (host_bgzf["mb_per_s_1_thread"] * 1e6 * threads)
     per_rank_ms = [elapsed * 1e3 / args.steps]
     if dist is not None:  # every rank's ms per step, as the collective saw them
         import torch
@@ -365,8 +392,8 @@ def main():
         per_rank_ms = [float(x.item()) for x in g]
     (elapsed, e2e_max), tot = job_totals(dist, rdev, [elapsed, e2e_s],
                                          [batch.num_windows, batch.num_regions, batch.num_effective_windows,
-                                          n_rows, n_row_bytes, batch.num_scan_windows])
-    tot_windows, tot_regions, tot_eff, tot_rows, tot_row_bytes, tot_scan = tot
+                                          n_rows, n_row_bytes, batch.num_scan_windows, n_bgzf])
+    tot_windows, tot_regions, tot_eff, tot_rows, tot_row_bytes, tot_scan, tot_bgzf = tot
 
     if rank == 0:
         steps = args.steps
@@ -447,15 +474,18 @@ def main():
                 "regions_per_s": tot_regions / e2e_max,
                 "windows_per_s": tot_windows / e2e_max,
                 "seconds": e2e_max,
-                "note": "one pass over the rank's batch: host prep (synthetic generation + load_diffs/"
-                        "patch/dedup/pack on %d threads) + upload + scan + device key reduction + device "
-                        "per-sample encoding + row formatting from the codes (%d rows, %.3g bytes); the BGZF "
-                        "write is not included" % (
-                            threads, tot_rows, tot_row_bytes),
-                "rank0_phases_s": {"host_prep_wall": fill_s, "synthetic_generation_thread_s": gen_s,
-                                   "build_region_thread_s": build_s, "commit_wall": commit_s,
+                "note": "one pass over the rank's batch: host prep (load_diffs/group/patch/dedup/pack on %d "
+                        "threads; the synthetic records are generated before, as for the CPU baseline) + upload "
+                        "+ scan + device key reduction + device "
+                        "per-sample encoding + the VCF rows as BGZF blocks made on the GPU (%d rows, %.3g bytes "
+                        "of text deflated to %.3g bytes, in host memory; the file write not timed)" % (
+                            threads, tot_rows, tot_row_bytes, tot_bgzf),
+                "bgzf_bytes": int(tot_bgzf),
+                "host_bgzf_writer": host_bgzf,
+                "rank0_phases_s": {"host_prep_wall": prep_wall, "synthetic_generation_wall": fill_s - prep_wall,
+                                   "synthetic_generation_thread_s": gen_s, "build_region_thread_s": build_s,
                                    "upload": t_up, "scan": t_scan1, "key_reduce": t_red,
-                                   "device_encode": t_enc, "rows": t_rows},
+                                   "device_encode": t_enc, "rows_bgzf": t_rows},
                 "rows": int(tot_rows),
             },
             "kernel_ms_avg": kms,

@@ -393,9 +393,11 @@ class RegionBatch:
         elif download:
             check(lib().tfbs_batch_download(scanner.h, self.h))
 
-    def encode(self, scanner, r0=0, r1=None):
-        """tfbs_batch_encode for regions [r0, r1) (after a reduced scan)."""
-        check(lib().tfbs_batch_encode(scanner.h, self.h, r0, self.num_regions if r1 is None else r1))
+    def encode(self, scanner, r0=0, r1=None, device_codes=False):
+        """tfbs_batch_encode for regions [r0, r1) (after a reduced scan); device_codes: keep the
+        per-sample codes on the GPU (for rows_bgzf)."""
+        check(lib().tfbs_batch_encode_flags(scanner.h, self.h, r0, self.num_regions if r1 is None else r1,
+                                            1 if device_codes else 0))
 
     def keys(self, region):
         """count_matches_by_sample for one region: {(bed, (s, e), pattern_id): (L, R)}."""
@@ -469,10 +471,26 @@ class RegionBatch:
         return r.value, n.value
 
     def prep_seconds(self):
-        """(generation CPU-s, build_region CPU-s, commit wall-s, fill wall-s) of synth_fill."""
+        """(generation CPU-s, build_region CPU-s, build + commit wall-s, fill wall-s) of synth_fill."""
         out = (C.c_double * 4)()
         check(lib().tfbs_batch_prep_seconds(self.h, out))
         return tuple(out)
+
+    def rows_bgzf(self, scanner, chromosome, min_maf=0, fake_position=1, r0=0, r1=None):
+        """tfbs_batch_rows_bgzf: the rows of regions [r0, r1) as BGZF blocks built on the
+        GPU (after encode over them); returns (bytes, next fake_position, rows, text bytes)."""
+        fp = C.c_uint32(fake_position)
+        p = C.c_void_p()
+        n = C.c_size_t()
+        nr, nb = C.c_uint64(), C.c_uint64()
+        check(lib().tfbs_batch_rows_bgzf(scanner.h, self.h, r0, self.num_regions if r1 is None else r1,
+                                         _u(chromosome), min_maf, C.byref(fp), C.byref(p), C.byref(n), C.byref(nr),
+                                         C.byref(nb)))
+        try:
+            data = C.string_at(p, n.value)
+        finally:
+            lib().tfbs_free(p)
+        return data, fp.value, nr.value, nb.value
 
     def rows(self, chromosome, min_maf=0, fake_position=1):
         """Rows for every region (main.rs:415-429); returns (text, next fake_position)."""

@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "batch.hpp"
+#include "rows.hpp"
 
 namespace tfbs {
 
@@ -144,9 +145,11 @@ std::string strip_chr(const std::string &c) {
     return o;
 }
 
-// The device encoding of a key (tfbs_batch_encode) usable for region r, or UINT32_MAX.
-static uint32_t encoded_key(const Batch &B, size_t r, uint64_t key) {
+// The device encoding of a key (tfbs_batch_encode) of region r, or UINT32_MAX;
+// host_codes: the caller formats from the codes on the host (they were downloaded).
+static uint32_t encoded_key(const Batch &B, size_t r, uint64_t key, bool host_codes = true) {
     if (!B.reduced || B.counts_valid || r < B.enc_r0 || r >= B.enc_r1) return UINT32_MAX;
+    if (host_codes && !B.enc_codes_host) return UINT32_MAX;
     const uint32_t vi = B.var_idx[key];
     if (vi == UINT32_MAX) return UINT32_MAX;
     const uint32_t e = B.enc_idx[vi];
@@ -355,6 +358,129 @@ size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std:
         n_rows++;
     }
     return n_rows;
+}
+
+// One row of build_row_plan before its POS: the head after "<chr>\t<POS>\t"
+// (the whole row text but its '\n' when the device did not encode the key), and
+// for an encoded key its index, value texts and genotype text length.
+struct RowPart {
+    std::string head;
+    uint32_t e = UINT32_MAX;
+    uint32_t nv = 0;
+    uint64_t total = 0;
+    std::vector<char> tok;     // kRowTokBytes per value
+    std::vector<uint8_t> len;
+};
+
+// region_rows_each's rows of one region as RowParts (no genotype text for the
+// keys the device encoded).
+static void region_row_parts(const Batch &B, const RegionH &R, uint32_t min_maf, std::vector<RowPart> &parts) {
+    const uint32_t H = 2 * B.n_samples;
+    const size_t ri = (size_t)(&R - B.rh.data());
+    std::vector<uint32_t> l, r;
+    std::unique_ptr<Membership> M;
+    std::string info, gts;
+    EncText et;
+    for (const KeyRef &k : region_keys(B, R)) {
+        if (!key_varies(B, R, k.slot, k.ik->slot)) continue;
+        uint32_t maf = 0;
+        info.clear();
+        gts.clear();
+        const uint32_t e = encoded_key(B, ri, key_of(B, R, k.slot, k.ik->slot), false);
+        int made = e == UINT32_MAX ? -1 : encoded_genotypes(B, e, k.ik->mult, &maf, info, et);
+        const bool direct = made > 0;
+        if (made < 0) {
+            info.clear();
+            gts.clear();
+            if (!M) {
+                M.reset(new Membership(R, H));
+                l.resize(B.n_samples);
+                r.resize(B.n_samples);
+            }
+            for (uint32_t s = 0; s < B.n_samples; s++) {
+                l[s] = count_of(B, R, M->local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
+                r[s] = count_of(B, R, M->local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
+            }
+            made = counts_as_genotypes(l.data(), r.data(), B.n_samples, &maf, info, gts) ? 1 : 0;
+        }
+        if (!made) continue;
+        if (maf < min_maf) continue;
+        const uint16_t pid = B.slot_pid[k.slot];
+        auto it = B.pats->names.find(pid);
+        const std::string &pname = it == B.pats->names.end() ? std::string() : it->second;
+        parts.emplace_back();
+        RowPart &p = parts.back();
+        p.head += B.beds[k.ik->bed];
+        p.head += ',';
+        p.head += pname;
+        char head[96];
+        snprintf(head, sizeof head, ",%llu-%llu\t.\t.\t.\tPASS\t", (unsigned long long)k.ik->s,
+                 (unsigned long long)k.ik->e);
+        p.head += head;
+        p.head += info;
+        p.head += "\tGT:DS";
+        if (direct) {
+            p.e = e;
+            p.nv = B.enc_hdr[e].n_vals;
+            p.total = et.total;
+            p.tok.assign((size_t)p.nv * kRowTokBytes, 0);
+            p.len.assign(et.len, et.len + p.nv);
+            for (uint32_t v = 0; v < p.nv; v++) memcpy(&p.tok[(size_t)v * kRowTokBytes], et.tab[v], kRowTokBytes);
+        } else {
+            p.head += gts;
+        }
+    }
+}
+
+int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chrom, uint32_t min_maf,
+                   uint32_t *fake, uint32_t threads, RowPlan &plan) {
+    if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
+    if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
+    r1 = std::min(r1, B.rh.size());
+    r0 = std::min(r0, r1);
+    const size_t n = r1 - r0;
+    std::vector<std::vector<RowPart>> parts(n);
+    std::atomic<size_t> next(0);
+    auto work = [&]() {
+        for (size_t j; (j = next.fetch_add(1)) < n;)
+            if (B.rh[r0 + j].hap_count) region_row_parts(B, B.rh[r0 + j], min_maf, parts[j]);
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
+    work();
+    for (auto &t : ts) t.join();
+    // serially: POS, offsets in the stream, token slots
+    plan = RowPlan();
+    const std::string chr = strip_chr(chrom);
+    uint64_t at = 0;
+    char pos[32];
+    for (auto &v : parts)
+        for (RowPart &p : v) {
+            DevRow d{};
+            d.head_off = (uint32_t)plan.heads.size();
+            const int m = snprintf(pos, sizeof pos, "\t%u\t", *fake);
+            (*fake)++;
+            plan.heads += chr;
+            plan.heads.append(pos, (size_t)m);
+            plan.heads += p.head;
+            if (plan.heads.size() >= UINT32_MAX) return fail(TFBS_E_NOMEM, "row heads past 4 GiB in one call");
+            d.head_len = (uint32_t)(plan.heads.size() - d.head_off);
+            d.text_off = at;
+            if (p.e != UINT32_MAX) {
+                d.geno_len = p.total;
+                d.code_off = B.enc_code_off[p.e];
+                d.width = B.enc_hdr[p.e].width;
+                d.tok = (uint32_t)plan.tok_len.size();
+                plan.tok_len.insert(plan.tok_len.end(), p.len.begin(), p.len.end());
+                plan.tok_text.insert(plan.tok_text.end(), p.tok.begin(), p.tok.end());
+            }
+            at += d.head_len + d.geno_len + 1;
+            plan.rows.push_back(d);
+            std::string().swap(p.head);
+        }
+    plan.text_bytes = at;
+    plan.n_rows = plan.rows.size();
+    return TFBS_OK;
 }
 
 size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out) {

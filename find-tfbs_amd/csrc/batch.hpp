@@ -92,6 +92,7 @@ struct Batch {
     std::vector<EncHdr> enc_hdr;
     std::vector<uint32_t> enc_vals, enc_hist;  // (kEncMaxVals + 1) per encoded key
     PinnedBytes enc_codes;                     // packed codes of every encoded key, back to back
+    bool enc_codes_host = true;                // enc_codes downloaded (not with TFBS_ENC_DEVICE_CODES)
     std::vector<uint64_t> enc_code_off;        // per encoded key, + the end
 
     std::vector<RegionH> rh;

@@ -1,0 +1,402 @@
+// The VCF rows of device-encoded keys as BGZF blocks, built on the GPU
+// (the writer of main.rs:258-290).
+//
+// A row's text is its head (formatted on the host: "<chr>\t<POS>\t<id>\t.\t.\t.
+// \tPASS\t<COUNTS/freqs>\tGT:DS"), then one sample text per sample -- the
+// key's value text of the sample's code (tfbs_batch_encode) -- then '\n'.  At
+// 50 000 samples that is ~0.4 MB per row, most of it runs of one text, so the
+// text is never materialised: every BGZF block (65 280 bytes of the stream, one
+// workgroup) generates its bytes from the codes and deflates them with the
+// fixed Huffman code (RFC 1951 3.2.6) and matches the text's structure gives
+// for free, no search: a sample text equal to the one before continues a run
+// (distance = its length, one match per up to 258 bytes), otherwise it refers
+// to the same text among the 8 samples before it (one match), else it is
+// literals.  Each thread encodes 255 bytes of the block (bit counts, a block
+// scan, then the bits at their offsets); the block's CRC32 is the XOR of the
+// threads' CRCs shifted by x^(8 n) operators (powers of two precomputed).  A
+// block that would not shrink is stored (BTYPE 00).
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "bgzf_gpu.hpp"
+
+namespace tfbs {
+namespace {
+
+constexpr int kBgBlock = 256;
+constexpr uint32_t kBgPer = (kBgzfRaw + kBgBlock - 1) / kBgBlock;  // bytes per thread
+constexpr uint32_t kBgWords = (kBgzfMax - 26) / 4;                  // deflate data words a block can hold
+constexpr uint32_t kLookback = 8;                                   // sample texts searched for a match
+
+__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
+                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
+__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
+__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
+                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
+__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
+
+__device__ __forceinline__ uint32_t rev(uint32_t code, uint32_t n) { return __builtin_bitreverse32(code) >> (32 - n); }
+
+// The bit stream of one thread: counts bits (write = false) or ORs them into the
+// block's LDS buffer at their offset (neighbouring threads share edge words).
+struct BitOut {
+    uint32_t *buf;
+    uint32_t off;
+    bool write;
+    __device__ void put(uint32_t v, uint32_t n) {
+        if (write && n) {
+            const uint32_t w = off >> 5, sh = off & 31;
+            atomicOr(&buf[w], v << sh);
+            if (sh + n > 32) atomicOr(&buf[w + 1], v >> (32 - sh));
+        }
+        off += n;
+    }
+    __device__ void lit(uint32_t b) {  // literal/length codes 0-143: 8 bits, 144-255: 9 bits
+        if (b < 144) put(rev(0x30 + b, 8), 8);
+        else put(rev(0x190 + b - 144, 9), 9);
+    }
+    __device__ void match(uint32_t len, uint32_t dist) {  // 3 <= len <= 258, dist <= 32768
+        uint32_t i = 0;
+        while (i < 28 && c_len_base[i + 1] <= len) i++;
+        const uint32_t sym = 257 + i;
+        if (sym < 280) put(rev(sym - 256, 7), 7);
+        else put(rev(0xC0 + sym - 280, 8), 8);
+        put(len - c_len_base[i], c_len_extra[i]);
+        uint32_t d = 0;
+        while (d < 29 && c_dist_base[d + 1] <= dist) d++;
+        put(rev(d, 5), 5);
+        put(dist - c_dist_base[d], c_dist_extra[d]);
+    }
+};
+
+struct Ctx {
+    const BgArgs &A;
+    uint64_t b0;  // block start in the stream
+    __device__ uint32_t find_row(uint64_t p) const {  // the last row starting at or before p
+        uint32_t lo = 0, hi = A.n_rows - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (A.rows[mid].text_off <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    }
+    __device__ uint32_t code(const DevRow &R, uint32_t s) const {
+        const uint32_t bit = s * R.width;
+        return (A.codes[R.code_off + (bit >> 3)] >> (bit & 7)) & ((1u << R.width) - 1u);
+    }
+    __device__ uint32_t tlen(const DevRow &R, uint32_t c) const { return A.tok_len[R.tok + c]; }
+    __device__ uint8_t tbyte(const DevRow &R, uint32_t c, uint32_t o) const {
+        return (uint8_t)A.tok_text[(size_t)(R.tok + c) * kRowTokBytes + o];
+    }
+    // sample s and offset o of byte g of the row's genotype text
+    __device__ void locate(const DevRow &R, uint64_t g, uint32_t &s, uint32_t &o) const {
+        const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
+        const uint32_t *cum = A.cum + R.cum_off;
+        uint32_t lo = 0, hi = ng - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (cum[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        uint64_t pos = cum[lo];
+        s = lo * kCumGroup;
+        for (; s + 1 < A.n_samples; s++) {  // bounded: g lies inside the row's genotype text
+            const uint32_t t = tlen(R, code(R, s));
+            if (g < pos + t) break;
+            pos += t;
+        }
+        o = (uint32_t)(g - pos);
+    }
+    // every byte of [p, e), in order
+    template <class F>
+    __device__ void bytes(uint64_t p, uint64_t e, F &&f) const {
+        if (p >= e) return;
+        uint32_t r = find_row(p);
+        while (p < e) {
+            while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
+            const DevRow R = A.rows[r];
+            const uint64_t local = p - R.text_off;
+            if (local < R.head_len) {
+                const uint64_t n = min((uint64_t)R.head_len - local, e - p);
+                for (uint64_t i = 0; i < n; i++) f((uint8_t)A.heads[R.head_off + local + i]);
+                p += n;
+                continue;
+            }
+            uint64_t g = local - R.head_len;
+            if (g >= R.geno_len) {
+                f((uint8_t)'\n');
+                p++;
+                continue;
+            }
+            uint32_t s, o;
+            locate(R, g, s, o);
+            while (p < e && g < R.geno_len) {
+                const uint32_t c = code(R, s), t = tlen(R, c);
+                const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
+                for (uint32_t i = 0; i < n; i++) f(tbyte(R, c, o + i));
+                p += n;
+                g += n;
+                o += n;
+                if (o == t) {
+                    s++;
+                    o = 0;
+                }
+            }
+        }
+    }
+    // the deflate symbols of [p, e) into out
+    __device__ void encode(uint64_t p, uint64_t e, BitOut &out) const {
+        if (p >= e) return;
+        uint32_t r = find_row(p);
+        while (p < e) {
+            while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
+            const DevRow R = A.rows[r];
+            const uint64_t local = p - R.text_off;
+            if (local < R.head_len) {
+                const uint64_t n = min((uint64_t)R.head_len - local, e - p);
+                for (uint64_t i = 0; i < n; i++) out.lit((uint8_t)A.heads[R.head_off + local + i]);
+                p += n;
+                continue;
+            }
+            uint64_t g = local - R.head_len;
+            if (g >= R.geno_len) {
+                out.lit('\n');
+                p++;
+                continue;
+            }
+            uint32_t s, o;
+            locate(R, g, s, o);
+            while (p < e && g < R.geno_len) {
+                const uint32_t c = code(R, s), t = tlen(R, c);
+                const uint64_t tok0 = p - o;  // this sample text's first byte
+                if (s > 0 && code(R, s - 1) == c && tok0 >= b0 + t) {
+                    // a run: every byte equals the one t before it, to the run's end
+                    uint64_t end = tok0 + t;
+                    uint32_t s2 = s + 1;
+                    while (end < e && s2 < A.n_samples && code(R, s2) == c) {
+                        end += t;
+                        s2++;
+                    }
+                    end = min(end, e);
+                    uint32_t left = (uint32_t)(end - p), oo = o;
+                    while (left) {
+                        if (left < 3) {  // too short for a match: literals
+                            out.lit(tbyte(R, c, oo));
+                            oo = (oo + 1) % t;
+                            left--;
+                            continue;
+                        }
+                        const uint32_t m = left > 258 ? (left - 258 < 3 ? left - 3 : 258) : left;
+                        out.match(m, t);
+                        oo = (uint32_t)((oo + m) % t);
+                        left -= m;
+                    }
+                    const uint64_t adv = end - p;
+                    g += adv;
+                    p = end;
+                    const uint64_t q = o + adv;
+                    s += (uint32_t)(q / t);
+                    o = (uint32_t)(q % t);
+                    continue;
+                }
+                const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
+                uint32_t dist = 0, acc = 0;
+                for (uint32_t k = 1; k <= kLookback && k <= s; k++) {  // the same text among the samples before
+                    const uint32_t cc = code(R, s - k);
+                    acc += tlen(R, cc);
+                    if (tok0 < b0 + acc) break;
+                    if (cc == c) {
+                        dist = acc;
+                        break;
+                    }
+                }
+                if (dist && n >= 3) {
+                    out.match(n, dist);
+                } else {
+                    for (uint32_t i = 0; i < n; i++) out.lit(tbyte(R, c, o + i));
+                }
+                p += n;
+                g += n;
+                o += n;
+                if (o == t) {
+                    s++;
+                    o = 0;
+                }
+            }
+        }
+    }
+};
+
+// x^(8 n) applied to a CRC register: the operators of 2^k bytes, k < 32
+__device__ __forceinline__ uint32_t crc_shift(const uint32_t *ops, uint32_t v, uint64_t n) {
+    for (uint32_t k = 0; n; k++, n >>= 1) {
+        if (!(n & 1)) continue;
+        const uint32_t *M = ops + 32 * k;
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < 32; i++)
+            if ((v >> i) & 1u) r ^= M[i];
+        v = r;
+    }
+    return v;
+}
+
+// Row r's genotype text offsets of samples 0, 64, 128, ... (and its end).
+__global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
+    __shared__ uint32_t s_scan[256];
+    const uint32_t r = blockIdx.x;
+    const DevRow R = A.rows[r];
+    if (!R.width) return;
+    const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
+    uint32_t *cum = A.cum + R.cum_off;
+    Ctx C{A, 0};
+    uint32_t carry = 0;
+    for (uint32_t q0 = 0; q0 < ng; q0 += 256) {
+        const uint32_t q = q0 + threadIdx.x;
+        uint32_t sum = 0;
+        if (q < ng)
+            for (uint32_t s = q * kCumGroup; s < min(A.n_samples, (q + 1) * kCumGroup); s++) sum += C.tlen(R, C.code(R, s));
+        s_scan[threadIdx.x] = sum;
+        __syncthreads();
+        for (uint32_t o = 1; o < 256; o <<= 1) {
+            const uint32_t t = threadIdx.x >= o ? s_scan[threadIdx.x - o] : 0;
+            __syncthreads();
+            s_scan[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (q < ng) cum[q] = carry + s_scan[threadIdx.x] - sum;
+        carry += s_scan[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) cum[ng] = carry;
+}
+
+__global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
+    __shared__ uint32_t s_bits[kBgWords + 1];
+    __shared__ uint32_t s_crc_tab[256];
+    __shared__ uint32_t s_scan[kBgBlock];
+    __shared__ uint32_t s_crc[kBgBlock];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t blk = A.block0 + blockIdx.x;
+    const uint64_t b0 = blk * kBgzfRaw;
+    const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
+    for (uint32_t i = tid; i < 256; i += kBgBlock) s_crc_tab[i] = A.crc_tab[i];
+    for (uint32_t i = tid; i <= kBgWords; i += kBgBlock) s_bits[i] = 0;
+    __syncthreads();
+    const Ctx C{A, b0};
+    const uint64_t p = b0 + min(n, tid * kBgPer), e = b0 + min(n, (tid + 1) * kBgPer);
+    // CRC32 (reflected 0xEDB88320, zero start) of the thread's bytes, shifted to the block end
+    uint32_t crc = 0;
+    C.bytes(p, e, [&](uint8_t b) { crc = s_crc_tab[(crc ^ b) & 0xFFu] ^ (crc >> 8); });
+    s_crc[tid] = crc_shift(A.crc_ops, crc, b0 + n - e);
+    // pass 1: the thread's bits
+    BitOut cnt{s_bits, 0, false};
+    C.encode(p, e, cnt);
+    s_scan[tid] = cnt.off;
+    __syncthreads();
+    for (uint32_t o = 1; o < kBgBlock; o <<= 1) {
+        const uint32_t t = tid >= o ? s_scan[tid - o] : 0;
+        __syncthreads();
+        s_scan[tid] += t;
+        __syncthreads();
+    }
+    const uint32_t total_bits = 3 + s_scan[kBgBlock - 1] + 7;  // BFINAL + BTYPE, symbols, end of block
+    const uint32_t dbytes = (total_bits + 7) / 8;
+    const bool stored = dbytes > 4 * kBgWords;
+    if (!stored) {  // pass 2: the bits at their offsets
+        if (tid == 0) s_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
+        __syncthreads();
+        BitOut w{s_bits, 3 + s_scan[tid] - cnt.off, true};
+        C.encode(p, e, w);
+    }
+    if (tid == 0) {  // the block's CRC: XOR of the shifted parts, then the start value and final XOR
+        uint32_t x = 0;
+        for (uint32_t t = 0; t < kBgBlock; t++) x ^= s_crc[t];
+        s_crc[0] = x ^ crc_shift(A.crc_ops, 0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint8_t *out = A.out + (size_t)blockIdx.x * kBgzfMax;
+    const uint32_t clen = stored ? 5 + n : dbytes;
+    const uint32_t bsize = 18 + clen + 8;
+    if (stored) {  // BFINAL = 1, BTYPE = 00, LEN, NLEN, the bytes
+        uint32_t k = 0;
+        C.bytes(p, e, [&](uint8_t b) { out[18 + 5 + (p - b0) + k++] = b; });
+        if (tid == 0) {
+            out[18] = 1;
+            out[19] = (uint8_t)n;
+            out[20] = (uint8_t)(n >> 8);
+            out[21] = (uint8_t)~n;
+            out[22] = (uint8_t)(~n >> 8);
+        }
+    } else {
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(s_bits);
+        for (uint32_t i = tid; i < dbytes; i += kBgBlock) out[18 + i] = src[i];
+    }
+    if (tid == 0) {
+        const uint8_t hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0,
+                                 (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+        for (int i = 0; i < 18; i++) out[i] = hdr[i];
+        const uint32_t crc32 = s_crc[0];
+        for (int i = 0; i < 4; i++) out[18 + clen + i] = (uint8_t)(crc32 >> (8 * i));
+        for (int i = 0; i < 4; i++) out[18 + clen + 4 + i] = (uint8_t)(n >> (8 * i));
+        A.out_len[blockIdx.x] = bsize;
+    }
+}
+
+// Copies each block to its offset of one contiguous buffer.
+__global__ __launch_bounds__(256) void bgzf_compact_kernel(const uint8_t *__restrict__ in,
+                                                           const uint64_t *__restrict__ off,
+                                                           uint8_t *__restrict__ out) {
+    const uint64_t o = off[blockIdx.x], n = off[blockIdx.x + 1] - o;
+    const uint8_t *src = in + (size_t)blockIdx.x * kBgzfMax;
+    for (uint64_t i = threadIdx.x; i < n; i += 256) out[o + i] = src[i];
+}
+
+}  // namespace
+
+void bgzf_crc_tables(uint32_t *tab, uint32_t *ops) {
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+        tab[i] = c;
+    }
+    // one zero byte: v -> tab[v & 0xff] ^ (v >> 8); 2^(k+1) bytes = 2^k bytes twice
+    for (uint32_t i = 0; i < 32; i++) {
+        const uint32_t v = 1u << i;
+        ops[i] = tab[v & 0xFF] ^ (v >> 8);
+    }
+    for (uint32_t k = 1; k < kBgzfOps; k++)
+        for (uint32_t i = 0; i < 32; i++) {
+            uint32_t v = ops[32 * (k - 1) + i], r = 0;
+            for (uint32_t j = 0; j < 32; j++)
+                if ((v >> j) & 1u) r ^= ops[32 * (k - 1) + j];
+            ops[32 * k + i] = r;
+        }
+}
+
+int launch_row_cum(const BgArgs &a, hipStream_t stream) {
+    if (a.n_rows == 0) return TFBS_OK;
+    hipLaunchKernelGGL(row_cum_kernel, dim3(a.n_rows), dim3(256), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("row_cum_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream) {
+    if (n_blocks == 0) return TFBS_OK;
+    hipLaunchKernelGGL(bgzf_block_kernel, dim3(n_blocks), dim3(kBgBlock), 0, stream, a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_block_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_bgzf_compact(const uint8_t *in, const uint64_t *off, uint32_t n_blocks, uint8_t *out, hipStream_t stream) {
+    if (n_blocks == 0) return TFBS_OK;
+    hipLaunchKernelGGL(bgzf_compact_kernel, dim3(n_blocks), dim3(256), 0, stream, in, off, out);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_compact_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+}  // namespace tfbs

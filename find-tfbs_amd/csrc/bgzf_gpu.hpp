@@ -1,0 +1,41 @@
+// Launch interface of the device BGZF row writer (bgzf_gpu.hip), used by device.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "rows.hpp"
+
+namespace tfbs {
+
+constexpr uint32_t kCumGroup = 64;  // samples per entry of a row's genotype text offsets
+constexpr uint32_t kBgzfOps = 32;   // CRC32 shift operators of 2^k zero bytes, k < 32
+
+struct BgArgs {
+    const DevRow *rows;
+    uint32_t n_rows;
+    const char *heads;
+    const char *tok_text;       // kRowTokBytes per token slot
+    const uint8_t *tok_len;
+    const uint8_t *codes;       // the encoded keys' packed codes (tfbs_batch_encode's compact buffer)
+    uint32_t *cum;              // per row (DevRow::cum_off): (n_samples + 63) / 64 + 1 genotype text offsets
+    uint32_t n_samples;
+    uint64_t text_bytes;        // of the rows' stream
+    uint64_t block0;            // first block of the launch
+    uint8_t *out;               // kBgzfMax bytes per block of the launch
+    uint32_t *out_len;          // the blocks' sizes
+    const uint32_t *crc_tab;    // CRC32 byte table
+    const uint32_t *crc_ops;    // kBgzfOps x 32 columns
+};
+
+// CRC32 table and the x^(8 * 2^k) operators (host side, uploaded once).
+void bgzf_crc_tables(uint32_t *tab, uint32_t *ops);
+// Per row: its genotype text offsets every 64 samples.
+int launch_row_cum(const BgArgs &a, hipStream_t stream);
+// Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each.
+int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream);
+// The blocks back to back: block i's out_len bytes at off[i] (off[n_blocks] = total).
+int launch_bgzf_compact(const uint8_t *in, const uint64_t *off, uint32_t n_blocks, uint8_t *out, hipStream_t stream);
+
+}  // namespace tfbs

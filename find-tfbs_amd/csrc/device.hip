@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "batch.hpp"
+#include "bgzf_gpu.hpp"
 #include "patterns.hpp"
 #include "keys.hpp"
 #include "scan.hpp"
@@ -131,6 +132,13 @@ struct tfbs_ctx {
     DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
     DevBuf<uint32_t> enc_vals, enc_hist;
+    // device BGZF rows (tfbs_batch_rows_bgzf)
+    DevBuf<DevRow> bg_rows;
+    DevBuf<char> bg_heads, bg_tok_text;
+    DevBuf<uint8_t> bg_tok_len, bg_out, bg_packed;
+    DevBuf<uint32_t> bg_cum, bg_out_len, bg_crc;  // bg_crc: byte table | shift operators
+    DevBuf<uint64_t> bg_off;
+    tfbs::PinnedBytes bg_host;       // compressed blocks staged for the host
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
     float last_ms = 0.f;
@@ -387,6 +395,9 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
     ctx->enc_pair_off.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
+    ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
+    ctx->bg_out.release(); ctx->bg_packed.release(); ctx->bg_cum.release(); ctx->bg_out_len.release();
+    ctx->bg_crc.release(); ctx->bg_off.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
@@ -660,6 +671,10 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
 }
 
 int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
+    return tfbs_batch_encode_flags(ctx, b, r0, r1, 0);
+}
+
+int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, int flags) {
     if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
     Batch &B = b->b;
@@ -794,12 +809,93 @@ int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1) {
         if ((rc = launch_code_compact(ctx->enc_codes.p, (uint32_t)nk, N, ctx->enc_off.p, ctx->enc_packed.p,
                                       ctx->stream)))
             return rc;
-        if (total)
+        if (total && !(flags & TFBS_ENC_DEVICE_CODES))
             HIP_TRY(hipMemcpyAsync(B.enc_codes.p, ctx->enc_packed.p, total, hipMemcpyDeviceToHost, ctx->stream));
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     B.enc_r0 = (uint32_t)r0;
     B.enc_r1 = (uint32_t)r1;
+    B.enc_codes_host = !(flags & TFBS_ENC_DEVICE_CODES);
+    return TFBS_OK;
+}
+
+int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
+                         uint32_t min_maf, uint32_t *fake_position, unsigned char **out, size_t *len,
+                         uint64_t *n_rows, uint64_t *text_bytes) {
+    if (!ctx || !b || !chromosome || !fake_position || !out || !len) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    Batch &B = b->b;
+    r1 = std::min(r1, B.rh.size());
+    r0 = std::min(r0, r1);
+    if (!B.reduced || B.enc_r0 > r0 || B.enc_r1 < r1)
+        return tfbs::fail(TFBS_E_STATE, "regions not encoded on this ctx (tfbs_batch_encode)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    tfbs::RowPlan plan;
+    int rc;
+    if ((rc = tfbs::build_row_plan(B, r0, r1, chromosome, min_maf, fake_position, ctx->host_threads, plan))) return rc;
+    const uint32_t N = B.n_samples, ng = (N + kCumGroup - 1) / kCumGroup;
+    const uint64_t n_blocks = (plan.text_bytes + kBgzfRaw - 1) / kBgzfRaw;
+    if ((uint64_t)plan.rows.size() * (ng + 1) >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many rows in one call");
+    for (size_t i = 0; i < plan.rows.size(); i++) plan.rows[i].cum_off = (uint32_t)(i * (ng + 1));
+    if (n_rows) *n_rows = plan.n_rows;
+    if (text_bytes) *text_bytes = plan.text_bytes;
+    std::vector<unsigned char> host;
+    if (n_blocks) {
+        if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
+            std::vector<uint32_t> t(256 + 32 * kBgzfOps);
+            tfbs::bgzf_crc_tables(t.data(), t.data() + 256);
+            if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
+        }
+        std::vector<char> heads(plan.heads.begin(), plan.heads.end());
+        if ((rc = ctx->bg_rows.put(plan.rows, ctx->stream)) || (rc = ctx->bg_heads.put(heads, ctx->stream)) ||
+            (rc = ctx->bg_tok_text.put(plan.tok_text, ctx->stream)) ||
+            (rc = ctx->bg_tok_len.put(plan.tok_len, ctx->stream)) ||
+            (rc = ctx->bg_cum.ensure(std::max<size_t>(plan.rows.size() * (ng + 1), 1))))
+            return rc;
+        tfbs::BgArgs a{};
+        a.rows = ctx->bg_rows.p;
+        a.n_rows = (uint32_t)plan.rows.size();
+        a.heads = ctx->bg_heads.p;
+        a.tok_text = ctx->bg_tok_text.p;
+        a.tok_len = ctx->bg_tok_len.p;
+        a.codes = ctx->enc_packed.p;
+        a.cum = ctx->bg_cum.p;
+        a.n_samples = N;
+        a.text_bytes = plan.text_bytes;
+        a.crc_tab = ctx->bg_crc.p;
+        a.crc_ops = ctx->bg_crc.p + 256;
+        if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
+        constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
+        std::vector<uint32_t> blen;
+        std::vector<uint64_t> off;
+        for (uint64_t b0 = 0; b0 < n_blocks; b0 += kBatchBlocks) {
+            const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
+            if ((rc = ctx->bg_out.ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len.ensure(nb))) return rc;
+            a.block0 = b0;
+            a.out = ctx->bg_out.p;
+            a.out_len = ctx->bg_out_len.p;
+            if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream))) return rc;
+            blen.resize(nb);
+            HIP_TRY(hipMemcpyAsync(blen.data(), ctx->bg_out_len.p, (size_t)nb * 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            off.assign(nb + 1, 0);
+            for (uint32_t i = 0; i < nb; i++) off[i + 1] = off[i] + blen[i];
+            const uint64_t total = off[nb];
+            if ((rc = ctx->bg_off.put(off, ctx->stream)) || (rc = ctx->bg_packed.ensure(total)) ||
+                (rc = ctx->bg_host.reserve(total)))
+                return rc;
+            if ((rc = tfbs::launch_bgzf_compact(ctx->bg_out.p, ctx->bg_off.p, nb, ctx->bg_packed.p, ctx->stream)))
+                return rc;
+            HIP_TRY(hipMemcpyAsync(ctx->bg_host.p, ctx->bg_packed.p, total, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            host.insert(host.end(), ctx->bg_host.p, ctx->bg_host.p + total);
+        }
+    }
+    unsigned char *p = (unsigned char *)malloc(std::max<size_t>(host.size(), 1));
+    if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");
+    if (!host.empty()) memcpy(p, host.data(), host.size());
+    *out = p;
+    *len = host.size();
     return TFBS_OK;
 }
 

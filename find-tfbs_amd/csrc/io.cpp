@@ -155,6 +155,12 @@ int BgzfWriter::drain() {
     ends.clear();
     return TFBS_OK;
 }
+int BgzfWriter::write_blocks(const unsigned char *p, size_t n) {
+    if (raw.size() > (ends.empty() ? 0 : ends.back())) ends.push_back(raw.size());
+    if (int rc = drain()) return rc;
+    if (n && fwrite(p, 1, n, f) != n) return fail(TFBS_E_IO, "write failed");
+    return TFBS_OK;
+}
 // like BGzWriter::flush: ends the block (an empty block if nothing is buffered)
 int BgzfWriter::flush() {
     ends.push_back(raw.size());

@@ -88,7 +88,11 @@ struct RunSetup {
 
 // Row bodies of one shard in merged-peak order; emit(bodies) gets each batch's
 // rows ('\n'-terminated, no chromosome/POS prefix).
-template <class Emit> int run_shard(const RunSetup &S, Shard &sh, Emit &&emit) {
+// emit(bodies): row bodies formatted on the host; blocks(data, n) (non-null for
+// the single shard of a one-device run): the rows as device-made BGZF blocks,
+// POS from *fake.
+template <class Emit, class Blocks>
+int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_t *fake) {
     using namespace tfbs;
     const tfbs_run_args *a = S.a;
     if (sh.r0 >= sh.r1) return TFBS_OK;
@@ -190,16 +194,29 @@ template <class Emit> int run_shard(const RunSetup &S, Shard &sh, Emit &&emit) {
         Batch &B = bb->b;
         t0 = now();
         if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)) ||
-            (rc = tfbs_batch_encode(ctx, bb, 0, B.rh.size())))
+            (rc = tfbs_batch_encode_flags(ctx, bb, 0, B.rh.size(), blocks ? TFBS_ENC_DEVICE_CODES : 0)))
             return rc;
         double t1 = now();
         sh.t_gpu += t1 - t0;
-        std::string bodies;
-        if ((rc = batch_row_bodies(B, a->min_maf, bodies, sh.threads))) return rc;
-        double t2 = now();
-        sh.t_rows += t2 - t1;
-        if ((rc = emit(bodies))) return rc;
-        sh.t_emit += now() - t2;
+        if (blocks) {  // rows formatted and deflated on the device (the only shard: POS is known here)
+            unsigned char *data = nullptr;
+            size_t len = 0;
+            if ((rc = tfbs_batch_rows_bgzf(ctx, bb, 0, B.rh.size(), S.chrom.c_str(), a->min_maf, fake, &data, &len,
+                                           nullptr, nullptr)))
+                return rc;
+            std::unique_ptr<unsigned char, void (*)(void *)> dguard(data, free);
+            double t2 = now();
+            sh.t_rows += t2 - t1;
+            if ((rc = (*blocks)(data, len))) return rc;
+            sh.t_emit += now() - t2;
+        } else {
+            std::string bodies;
+            if ((rc = batch_row_bodies(B, a->min_maf, bodies, sh.threads))) return rc;
+            double t2 = now();
+            sh.t_rows += t2 - t1;
+            if ((rc = emit(bodies))) return rc;
+            sh.t_emit += now() - t2;
+        }
         if (a->verbose) {
             for (size_t r = 0; r < B.rh.size(); r++)
                 fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", b0 + r + 1, S.merged.size(),
@@ -342,6 +359,9 @@ int tfbs_run(const tfbs_run_args *a) {
     const std::string chr = strip_chr(S.chrom);
     uint32_t fake = 1;
     const bool timing = getenv("TFBS_RUN_TIMING") && atoi(getenv("TFBS_RUN_TIMING"));
+    // TFBS_GPU_BGZF=0: rows formatted and deflated on the host threads, as a
+    // multi-device run does (its shards' POS are known only when they are joined)
+    const bool gpu_bgzf = !(getenv("TFBS_GPU_BGZF") && atoi(getenv("TFBS_GPU_BGZF")) == 0);
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
     // shard 0 writes straight through the writer; the others spill their row
@@ -371,7 +391,9 @@ int tfbs_run(const tfbs_run_args *a) {
                 return fail(TFBS_E_IO, "write failed: " + spill_path[k]);
             return TFBS_OK;
         };
-        sh.rc = run_shard(S, sh, emit);
+        auto put_blocks = [&](const unsigned char *p, size_t n) { return w.write_blocks(p, n); };
+        sh.rc = n_sh == 1 && gpu_bgzf ? run_shard(S, sh, emit, &put_blocks, &fake)
+                                      : run_shard(S, sh, emit, (decltype(put_blocks) *)nullptr, &fake);
         if (sh.rc) sh.err = tfbs_last_error();
     };
     {

@@ -46,16 +46,6 @@
 namespace tfbs {
 namespace {
 
-// Bottleneck probes (tools/probe_build.sh, never in the product build):
-// TFBS_MFMA_PROBE=1 skips the threshold test (scores kept live; timing only),
-// =4 counts tile tests, firing tiles, queued lanes, exact hits and rejected
-// candidates (printed per launch), =12 never drains the queue, =13 drains it
-// but never rescores, =14 skips the rounds, =16 never queues, =17 decodes the
-// queue but lists nothing, =18 writes the queue but decodes nothing, =19
-// rescores without the count atomics (results wrong; timing only).
-#ifndef TFBS_MFMA_PROBE
-#define TFBS_MFMA_PROBE 0
-#endif
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v8i __attribute__((ext_vector_type(8)));
@@ -188,9 +178,6 @@ __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint32_t s_hnext;  // the workgroup's next haplotype (scan_super)
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
-#if TFBS_MFMA_PROBE == 4
-__device__ unsigned long long g_probe[8];
-#endif
 
 // Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
 // one load per column of the strand's blocks of 8 (zero-padded), all issued
@@ -255,9 +242,6 @@ __device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uin
     const uint32_t L = (uint32_t)sf.z;
     if (i + L > hp.len) return 0;                       // past the end (pattern.rs:147-150)
     const int32_t sc = exact_score(words, hp, i, L, A.mweights + sf.y, live);
-#if TFBS_MFMA_PROBE == 4
-    atomicAdd(&g_probe[sc > sf.x ? 1 : 2], 1ull);
-#endif
     if (!(sc > sf.x)) return 0;                         // strict (pattern.rs:151)
     if (A.hits && i / 64 < A.hits_wpp)
         atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + sn]) * A.hits_wpp + i / 64,
@@ -308,22 +292,9 @@ __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
 
 __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
                                             uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane, uint32_t &cn) {
-#if TFBS_MFMA_PROBE == 12
-    return;  // timing only: queued candidates are dropped
-#endif
-#if TFBS_MFMA_PROBE == 18
-    if (lane < n) asm volatile("" ::"v"(s_qdata[wave][lane].x), "v"(s_qmeta[wave][lane]));
-    return;  // timing only: the queue is written and read, nothing decoded
-#endif
     uint2 *list = cand_list(A, wave);
     const uint32_t cap = wave_cand_cap(A);
-#if TFBS_MFMA_PROBE == 4
-    if (lane == 0) atomicAdd(&g_probe[5], 1ull);
-#endif
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-#if TFBS_MFMA_PROBE == 4
-        if (lane == 0) atomicAdd(&g_probe[6], 1ull);
-#endif
         const uint32_t e = e0 + lane;
         uint32_t m = 0, g0 = 0, i0 = 0, hl = 0;
         if (e < n) {
@@ -347,9 +318,6 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
         }
         uint64_t act;
         while ((act = __ballot(m != 0)) != 0) {
-#if TFBS_MFMA_PROBE == 4
-            if (lane == 0) atomicAdd(&g_probe[7], 1ull);
-#endif
             if (m) {
                 const uint32_t b = __builtin_ctz(m);
                 m &= m - 1;
@@ -357,9 +325,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
                 const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
                 const uint32_t i = i0 + (r & 3) + 8 * (r >> 2), g = g0 + (b >> 4);
-                if (TFBS_MFMA_PROBE == 17) {
-                    asm volatile("" ::"v"(g), "v"(i), "v"(slot));
-                } else if (slot < cap) {
+                if (slot < cap) {
                     list[slot] = make_uint2(g | (hl << 24), i);
                 } else {  // rescored after the scan (no rescoring code, whose loads would stay
                           // pending, in the scan loop)
@@ -386,7 +352,6 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
     const size_t part = (size_t)(A.region_base + blockIdx.x) * A.cand_cap + (size_t)wave * cap;
     uint2 *out = reinterpret_cast<uint2 *>(A.hitl) + part;
     uint32_t hn = 0;  // wave-uniform
-#if TFBS_MFMA_PROBE != 13  // 13: listed candidates are dropped (timing only)
     const uint32_t n = min(cn, cap);
     const uint2 *list = cand_list(A, wave);
     for (uint32_t k0 = 0; k0 < n; k0 += 64) {
@@ -410,7 +375,6 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
             hn += (uint32_t)__popcll(act);
         }
     }
-#endif
     if (lane == 0) A.hitn[(size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave] = min(hn, cap);
 }
 
@@ -419,13 +383,6 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
 // pair are tested in the MFMAs' basic block (tools/isa_lint.py checks the wait
 // states).
 __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
-#if TFBS_MFMA_PROBE == 4
-    if ((threadIdx.x & 63) == 0) atomicAdd(&g_probe[3], 1ull);
-#endif
-    if (TFBS_MFMA_PROBE == 1) {
-        asm volatile("" ::"v"(acc[0]), "v"(acc[5]), "v"(acc[10]), "v"(acc[15]));
-        return 0;
-    }
     uint32_t u[16];
 #pragma unroll
     for (int r = 0; r < 16; r++) u[r] = __float_as_uint(acc[r]);
@@ -439,16 +396,6 @@ __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
 // bits); qn (wave-uniform) counts the wave's queued entries.
 __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t fired, uint32_t ti, uint32_t hh,
                                            uint32_t i0, uint32_t lane, uint32_t wave, uint32_t &qn) {
-#if TFBS_MFMA_PROBE == 4
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&g_probe[4], 1ull);
-        atomicAdd(&g_probe[0], (unsigned long long)__popcll(fired));
-    }
-#endif
-#if TFBS_MFMA_PROBE == 16
-    asm volatile("" ::"v"(x));
-    return;  // timing only: firing tiles are not queued
-#endif
     const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, qn));
     if (x) {
         // bytes 1, 1', 2, 2' of outputs 2j, 2j + 1: top bits at 2, 10, 21, 29;
@@ -483,32 +430,6 @@ __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, co
     }
 }
 
-// round_scores and both tests with the second tile's MFMAs interleaved with the
-// first tile's test (a wave's own VALU issues in its MFMA gaps; TFBS_MFMA_ILV).
-#ifndef TFBS_MFMA_ILV
-#define TFBS_MFMA_ILV 0
-#endif
-template <int D, int NK>
-__device__ __forceinline__ void round_tested(const char *tile, uint32_t lane, const v4i (&a0)[NK],
-                                             const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1,
-                                             uint32_t &x0, uint32_t &x1) {
-    BFrag f[D];
-    load_frags<D>(tile, lane, f);
-    c0 = cb;
-#pragma unroll
-    for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
-    c1 = mfma_chunk(a1[0], f[0], cb, sa);
-    // the first tile's test sits between the second tile's first and later MFMAs
-    // (after the last one for D = 1): scheduling barriers keep that order
-    __builtin_amdgcn_sched_barrier(0);
-    x0 = coarse_test(c0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kc = 1; kc < D; kc++) c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
-    __builtin_amdgcn_sched_barrier(0);
-    x1 = coarse_test(c1);
-}
-
 template <int D, int NK>
 __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v16f &cb,
                                             int sa, v16f &c0) {
@@ -532,14 +453,8 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
         for (uint32_t ti = tb; ti < te; ti++) {
             const char *tile = img + (ti - tb) * kTB;
             v16f c0, c1;
-            uint32_t x0, x1;
-            if (TFBS_MFMA_ILV) {
-                round_tested<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1, x0, x1);
-            } else {
-                round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                x0 = coarse_test(c0);
-                x1 = coarse_test(c1);
-            }
+            round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
             const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
             if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
             // cold: queue the firing tiles; a tile whose entries do not fit
@@ -593,10 +508,6 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
                                           const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t ha,
                                           uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb, int sa,
                                           uint32_t &qn, uint32_t &cn) {
-#if TFBS_MFMA_PROBE == 14
-    asm volatile("" ::"v"(a0[0]), "v"(a1[0]), "v"(a0[NK - 1]), "v"(a1[NK - 1]));
-    return;  // timing only: the haplotype loop and A fragments without the rounds
-#endif
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
 #define TFBS_SEGMENT(D)                                                                                          \
@@ -627,9 +538,6 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
     const int sa = lane < 32 ? kScaleA0 : kScaleA1;
     const char *tab = s_img - kMOnehotBytes;
-#ifdef TFBS_MFMA_PRIO
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
     uint32_t qn = 0, cn = 0;  // the wave's queued entries, listed candidates
     // window tiles two at a time (each B fragment read from LDS feeds two
     // MFMAs), pairs formed across the wave's haplotypes: a tile waits in a0
@@ -830,17 +738,6 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan_mfma_kernel launch: ") + hipGetErrorString(e));
-#if TFBS_MFMA_PROBE == 4
-    unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = 0; i < n_streams; i++) (void)hipStreamSynchronize(streams[i]);
-    (void)hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_probe), sizeof pr);
-    fprintf(stderr,
-            "probe4 tile_tests %llu fired %llu queued_lanes %llu hits %llu rejected %llu drains %llu passes %llu "
-            "rounds %llu\n",
-            pr[3], pr[4], pr[0], pr[1], pr[2], pr[5], pr[6], pr[7]);
-    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof z);
-#endif
     return launches;
 }
 

@@ -327,19 +327,19 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
     const double t_fill = now();
     for (uint64_t c0 = first; c0 < first + count; c0 += chunk) {
         const uint64_t n = std::min<uint64_t>(chunk, first + count - c0);
-        std::vector<tfbs::RegionBuilt> built(n);
-        std::vector<int> rcs(n, TFBS_OK);
+        // phase 1: the synthetic inputs (what a BCF / FASTA reader would hand over)
+        std::vector<tfbs::RegionInput> ins(n);
         std::atomic<uint64_t> next(0);
         std::mutex mu;
-        auto work = [&]() {
+        auto gen = [&]() {
             tfbs::SynthRegion R;
-            double t_gen = 0, t_build = 0;
+            double t_gen = 0;
             for (;;) {
                 const uint64_t j = next.fetch_add(1);
                 if (j >= n) break;
                 const double t0 = now();
                 tfbs::synth_region(seed, c0 + j, B.n_samples, lmax, indel_pct, R);
-                tfbs::RegionInput in;
+                tfbs::RegionInput &in = ins[j];
                 in.R.ms = R.ms;
                 in.R.me = R.me;
                 in.R.es = R.es;
@@ -355,24 +355,44 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
                     in.recs.push_back(std::move(r));
                 }
                 in.inner.push_back({(uint32_t)bed, {R.ms, R.me}});
-                const double t1 = now();
-                rcs[j] = tfbs::build_region(B, std::move(in), built[j]);
-                t_gen += t1 - t0;
-                t_build += now() - t1;
+                t_gen += now() - t0;
             }
             std::lock_guard<std::mutex> g(mu);
             B.prep_s[0] += t_gen;
-            B.prep_s[1] += t_build;
         };
-        std::vector<std::thread> ts;
-        for (uint32_t t = 0; t + 1 < T && t + 1 < n; t++) ts.emplace_back(work);
-        work();
-        for (auto &t : ts) t.join();
-        const double t_commit = now();
+        {
+            std::vector<std::thread> ts;
+            for (uint32_t t = 0; t + 1 < T && t + 1 < n; t++) ts.emplace_back(gen);
+            gen();
+            for (auto &t : ts) t.join();
+        }
+        // phase 2: load_diffs / group / patch / dedup / pack (build_region), then the commit
+        const double t_build = now();
+        std::vector<tfbs::RegionBuilt> built(n);
+        std::vector<int> rcs(n, TFBS_OK);
+        next = 0;
+        auto work = [&]() {
+            double t_b = 0;
+            for (;;) {
+                const uint64_t j = next.fetch_add(1);
+                if (j >= n) break;
+                const double t1 = now();
+                rcs[j] = tfbs::build_region(B, std::move(ins[j]), built[j]);
+                t_b += now() - t1;
+            }
+            std::lock_guard<std::mutex> g(mu);
+            B.prep_s[1] += t_b;
+        };
+        {
+            std::vector<std::thread> ts;
+            for (uint32_t t = 0; t + 1 < T && t + 1 < n; t++) ts.emplace_back(work);
+            work();
+            for (auto &t : ts) t.join();
+        }
         for (uint64_t j = 0; j < n; j++)
             if (rcs[j]) return rcs[j];
         tfbs::commit_regions(B, built, T);
-        B.prep_s[2] += now() - t_commit;
+        B.prep_s[2] += now() - t_build;
     }
     B.prep_s[3] += now() - t_fill;
     return TFBS_OK;

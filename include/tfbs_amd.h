@@ -241,6 +241,23 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
  * count gather on the host).  Keys whose region has > 255 distinct haplotypes,
  * > 255 distinct totals or a total range >= 65536 keep the host path. */
 int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1);
+/* tfbs_batch_encode with flags: TFBS_ENC_DEVICE_CODES keeps the per-sample codes on
+ * the device only (for tfbs_batch_rows_bgzf; host row functions then take their
+ * slower path for these keys). */
+#define TFBS_ENC_DEVICE_CODES 1
+int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, int flags);
+
+/* The rows of regions [r0, r1) (main.rs:415-429, same text as tfbs_batch_rows) as
+ * BGZF blocks (main.rs:258-290's BGzWriter) built on the GPU
+ * after tfbs_batch_encode over them: row heads formatted on the host, the
+ * per-sample genotype text generated from the device codes and deflated there
+ * (fixed-Huffman deflate, CRC32), so the text never crosses PCIe.  *out
+ * (malloc'd; tfbs_free) receives whole blocks -- the last one shorter -- to be
+ * written after the header's blocks; *fake_position is the POS counter, advanced
+ * per row; *n_rows / *text_bytes (optional) the rows and their uncompressed bytes. */
+int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
+                         uint32_t min_maf, uint32_t *fake_position, unsigned char **out, size_t *len,
+                         uint64_t *n_rows, uint64_t *text_bytes);
 
 /* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
  * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */
@@ -278,8 +295,9 @@ int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_hapl
 int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t threads,
                            size_t r0, size_t r1, uint64_t *n_rows, uint64_t *n_bytes);
 /* Host prep seconds of the batch's synthetic fills (out[4]): generation and
- * build_region (thread CPU-seconds, summed), the serial commit and the whole
- * fill (wall). */
+ * build_region (thread CPU-seconds, summed), build_region + the serial commit
+ * (wall: the prep a BCF reader's records go through) and the whole fill (wall,
+ * generation included). */
 int tfbs_batch_prep_seconds(const tfbs_batch *b, double *out);
 void tfbs_free(void *p);
 

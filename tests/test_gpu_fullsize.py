@@ -4,10 +4,13 @@ The batch the bench times is scanned here exactly as bench.py builds it (same
 generator, seeds, PWM sets and thresholds), and checked three ways:
 
 * against the oracle (oracle/tfbs_oracle.c, the C restatement of main.rs:94-154,
-  500-534 and 439-498): every region of C2, and for C3/C5 a deterministic spread
-  of >= 200 regions (first, last, the last haplotype group, evenly spaced ones)
-  key by key -- the per-sample L/R vectors of count_matches_by_sample -- and
-  row by row (POS aside: the oracle numbers rows over its own region subset);
+  500-534 and 439-498): every region of C2, and for C3/C5 >= 1 000 regions (a
+  deterministic spread: first, last, the last haplotype group, evenly spaced
+  ones; the 50 with the most distinct haplotypes and the 50 with the most
+  variant records -- C5's indel-dense ones --; every region with N runs) key
+  by key -- the per-sample L/R vectors of count_matches_by_sample -- and row by
+  row (POS aside: the oracle numbers rows over its own region subset), in full
+  on 100 of them and through xxh3 digests of the same on the rest;
 * the device per-sample encoding (tfbs_batch_encode: the rows formatted from
   per-sample codes) against the oracle on the same regions;
 * device key reduction (the run flow's tfbs_batch_reduce) against the dense
@@ -27,6 +30,7 @@ import os
 
 import numpy as np
 import pytest
+import xxhash
 
 import oracle_py as O
 from helpers import T, pattern_dicts
@@ -91,9 +95,28 @@ def _strip_pos(rows):
     return out
 
 
-def _oracle_regions(ps, n_samples, seed, indel, jobs):
+def _keys_digest(keys):
+    """xxh3 over a region's count_matches_by_sample map: key identity + both vectors."""
+    h = xxhash.xxh3_64()
+    for k in sorted(keys):
+        h.update(repr(k).encode())
+        h.update(np.ascontiguousarray(keys[k][0], dtype=np.uint32).tobytes())
+        h.update(np.ascontiguousarray(keys[k][1], dtype=np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def _rows_digest(rows):
+    h = xxhash.xxh3_64()
+    for r in rows:
+        h.update(r.encode())
+        h.update(b"\n")
+    return h.hexdigest()
+
+
+def _oracle_regions(ps, n_samples, seed, indel, jobs, digest=False):
     """jobs: [(product region index, merged, ref, records)] -> {index: (keys, rows)} on
-    host threads (ctypes drops the GIL), one oracle Job per thread."""
+    host threads (ctypes drops the GIL), one oracle Job per thread; digest=True keeps
+    only sha1 digests of both (wide spreads at 50 000 samples)."""
     pats = pattern_dicts(ps)
     ranges = sorted({tuple(j[1]) for j in jobs})
 
@@ -106,7 +129,8 @@ def _oracle_regions(ps, n_samples, seed, indel, jobs):
                 for pos, rf, alt, car in recs:
                     assert job.add_record_carriers(pos, rf, alt, car) == 0
                 assert job.end() == 0
-                res[idx] = (job.keys_np(), _strip_pos(job.rows()))
+                keys, rows = job.keys_np(), _strip_pos(job.rows())
+                res[idx] = (_keys_digest(keys), _rows_digest(rows)) if digest else (keys, rows)
                 job.clear_rows()
         finally:
             job.close()
@@ -129,19 +153,25 @@ def _synth_jobs(seed, indices, n_samples, lmax, indel):
     return jobs
 
 
-def _check_vs_oracle(b, ref, label):
-    """b: scanned batch (counts present); ref: {region: (oracle keys, oracle rows)}."""
+def _check_vs_oracle(b, ref, label, digest=False, keys=True, rows=True):
+    """b: scanned batch (counts present); ref: {region: (oracle keys, oracle rows)}, or
+    their _keys_digest / _rows_digest (digest=True); keys / rows: which to compare."""
     n_rows = 0
     for idx in sorted(ref):
         okeys, orows = ref[idx]
-        pkeys = b.keys_np(idx)
-        assert pkeys.keys() == okeys.keys(), (label, idx)
-        for k in okeys:
-            assert np.array_equal(pkeys[k][0], okeys[k][0]) and np.array_equal(pkeys[k][1], okeys[k][1]), \
-                (label, idx, k)
-        prows = _strip_pos(b.region_rows(idx, "chr1")[0])
-        assert prows == orows, (label, idx)
-        n_rows += len(prows)
+        if keys:
+            pkeys = b.keys_np(idx)
+            if digest:
+                assert _keys_digest(pkeys) == okeys, (label, idx)
+            else:
+                assert pkeys.keys() == okeys.keys(), (label, idx)
+                for k in okeys:
+                    assert np.array_equal(pkeys[k][0], okeys[k][0]) and np.array_equal(pkeys[k][1], okeys[k][1]), \
+                        (label, idx, k)
+        if rows:
+            prows = _strip_pos(b.region_rows(idx, "chr1")[0])
+            assert (_rows_digest(prows) if digest else prows) == orows, (label, idx)
+            n_rows += len(prows)
     return n_rows
 
 
@@ -157,7 +187,13 @@ def _digests(b):
     return [b.digest(r) for r in range(b.num_regions)]
 
 
-def _fullsize(tmp_path, cfg, n_check, n_extra_n=0):
+def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0):
+    """n_check regions spread over the batch (all of them if n_check >= its size), the
+    n_top regions with the most distinct haplotypes and the n_top with the most
+    variant records, and the n_extra_n regions with N runs, against the oracle:
+    key by key and row by row on a 100-region subset, by xxh3 digests of the same
+    (count_matches_by_sample vectors of every key after the key reduction, row
+    text after the device encoding) on all of them."""
     n_samples, n_regions, _, _, indel, seed = cfg
     ps = _patterns(tmp_path, cfg)
     lmax = ps.max_length
@@ -171,26 +207,38 @@ def _fullsize(tmp_path, cfg, n_check, n_extra_n=0):
         # the run flow's path: device key reduction
         b.scan(sc, reduce=True)
         reduced = _digests(b)
-        check = _spread(n_regions, n_check) if n_check < n_regions else list(range(n_regions))
+        check = set(_spread(n_regions, n_check) if n_check < n_regions else range(n_regions))
+        if n_top:
+            st = [b.region_stats(i) for i in range(n_regions)]
+            check |= set(sorted(range(n_regions), key=lambda i: -st[i][0])[:n_top])
+            check |= set(sorted(range(n_regions), key=lambda i: -st[i][1])[:n_top])
+        check = sorted(check)
+        full = set(check) if len(check) <= 100 else {check[i] for i in _spread(len(check), 100)}
         jobs = _synth_jobs(seed, check, n_samples, lmax, indel)
         jobs += [(n_regions + k, r["merged"], r["ref"], r["records"]) for k, r in enumerate(extra)]
-        ref = _oracle_regions(ps, n_samples, seed, indel, jobs)
-        n_rows = _check_vs_oracle(b, ref, "reduce")
+        full |= {n_regions + k for k in range(len(extra))}
+        ref = _oracle_regions(ps, n_samples, seed, indel, [j for j in jobs if j[0] in full])
+        dig = _oracle_regions(ps, n_samples, seed, indel, [j for j in jobs if j[0] not in full], digest=True)
+        # the device key reduction: every checked region's keys (rows in full on the subset)
+        n_full = _check_vs_oracle(b, ref, "reduce")
+        _check_vs_oracle(b, dig, "reduce", digest=True, rows=False)
         # the device per-sample encoding (f1) the run flow formats rows from, 2 000
-        # regions at a time (codes: one byte per sample per varying key)
-        n_enc = 0
+        # regions at a time: every checked region's rows
+        n_enc = n_rows = 0
         for r0 in range(0, b.num_regions, 2000):
             r1 = min(b.num_regions, r0 + 2000)
             b.encode(sc, r0, r1)
-            n_enc += _check_vs_oracle(b, {i: ref[i] for i in ref if r0 <= i < r1}, "encode")
-        assert n_enc == n_rows
+            n_enc += _check_vs_oracle(b, {i: ref[i] for i in ref if r0 <= i < r1}, "encode", keys=False)
+            n_rows += _check_vs_oracle(b, {i: dig[i] for i in dig if r0 <= i < r1}, "encode", digest=True, keys=False)
+        assert n_enc == n_full
+        n_rows += n_enc
         # dense download over the same batch, rescanned
         b.scan(sc, upload=False, download=True)
         assert _digests(b) == reduced
         _check_vs_oracle(b, {i: ref[i] for i in list(ref)[:24]}, "dense")
     finally:
         sc.close()
-    return b, n_rows, len(ref)
+    return b, n_rows, len(ref) + len(dig)
 
 
 def test_c2_full_vs_oracle(tmp_path):
@@ -202,16 +250,16 @@ def test_c2_full_vs_oracle(tmp_path):
 def test_c3_full_batch_vs_oracle(tmp_path):
     """C3 as bench.py times it (50 000 samples, 10 000 regions, 600 PWMs = 1 200 strands,
     ~1.18 M distinct haplotypes, one batch), plus 6 regions with N runs at its end."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C3, 200, n_extra_n=6)
-    assert n_checked >= 200 and n_rows > 0
+    b, n_rows, n_checked = _fullsize(tmp_path, C3, 1000, n_extra_n=6, n_top=50)
+    assert n_checked >= 1000 and n_rows > 0
     assert b.num_haplotypes > 1_000_000
 
 
 def test_c5_full_batch_vs_oracle(tmp_path):
     """C5: C3 with 30 % indels (non-affine positions, variable-length haplotypes) and
     PWMs of length 25-30 (K depth 2 of the matrix-core kernel)."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C5, 200, n_extra_n=4)
-    assert n_checked >= 200 and n_rows > 0
+    b, n_rows, n_checked = _fullsize(tmp_path, C5, 1000, n_extra_n=4, n_top=50)
+    assert n_checked >= 1000 and n_rows > 0
 
 
 def test_c4_shards_equal_unsharded(tmp_path):
