@@ -476,21 +476,33 @@ class RegionBatch:
         check(lib().tfbs_batch_prep_seconds(self.h, out))
         return tuple(out)
 
-    def rows_bgzf(self, scanner, chromosome, min_maf=0, fake_position=1, r0=0, r1=None):
+    def rows_bgzf(self, scanner, chromosome, min_maf=0, fake_position=1, r0=0, r1=None, fd=None):
         """tfbs_batch_rows_bgzf: the rows of regions [r0, r1) as BGZF blocks built on the
-        GPU (after encode over them); returns (bytes, next fake_position, rows, text bytes)."""
+        GPU (after encode over them), written to file descriptor fd; without fd they are
+        returned.  Returns (bytes or bytes written, next fake_position, rows, text bytes)."""
+        import os
+        import tempfile
         fp = C.c_uint32(fake_position)
-        p = C.c_void_p()
-        n = C.c_size_t()
-        nr, nb = C.c_uint64(), C.c_uint64()
-        check(lib().tfbs_batch_rows_bgzf(scanner.h, self.h, r0, self.num_regions if r1 is None else r1,
-                                         _u(chromosome), min_maf, C.byref(fp), C.byref(p), C.byref(n), C.byref(nr),
-                                         C.byref(nb)))
+        nw, nr, nb = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        tmp = None
+        if fd is None:
+            tmp = tempfile.TemporaryFile()
+            fd_ = tmp.fileno()
+        else:
+            fd_ = fd
         try:
-            data = C.string_at(p, n.value)
+            check(lib().tfbs_batch_rows_bgzf(scanner.h, self.h, r0, self.num_regions if r1 is None else r1,
+                                             _u(chromosome), min_maf, C.byref(fp), fd_, C.byref(nw), C.byref(nr),
+                                             C.byref(nb)))
+            if tmp is not None:
+                tmp.seek(0)
+                out = tmp.read()
+            else:
+                out = nw.value
         finally:
-            lib().tfbs_free(p)
-        return data, fp.value, nr.value, nb.value
+            if tmp is not None:
+                tmp.close()
+        return out, fp.value, nr.value, nb.value
 
     def rows(self, chromosome, min_maf=0, fake_position=1):
         """Rows for every region (main.rs:415-429); returns (text, next fake_position)."""

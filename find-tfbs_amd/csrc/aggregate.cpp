@@ -471,6 +471,7 @@ int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chro
                 d.code_off = B.enc_code_off[p.e];
                 d.width = B.enc_hdr[p.e].width;
                 d.tok = (uint32_t)plan.tok_len.size();
+                d.nv = p.nv;
                 plan.tok_len.insert(plan.tok_len.end(), p.len.begin(), p.len.end());
                 plan.tok_text.insert(plan.tok_text.end(), p.tok.begin(), p.tok.end());
             }

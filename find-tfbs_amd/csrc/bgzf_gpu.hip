@@ -242,21 +242,39 @@ __device__ __forceinline__ uint32_t crc_shift(const uint32_t *ops, uint32_t v, u
     return v;
 }
 
-// Row r's genotype text offsets of samples 0, 64, 128, ... (and its end).
+// Row r's genotype text offsets of samples 0, 64, 128, ... (and its end): the
+// packed codes a byte at a time through a table of the byte's summed text lengths.
 __global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
     __shared__ uint32_t s_scan[256];
+    __shared__ uint16_t s_blen[256];  // code byte -> bytes of text of its samples
     const uint32_t r = blockIdx.x;
     const DevRow R = A.rows[r];
     if (!R.width) return;
     const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
     uint32_t *cum = A.cum + R.cum_off;
     Ctx C{A, 0};
+    const uint32_t per = 8 / R.width, mask = (1u << R.width) - 1u;
+    {
+        const uint32_t v = threadIdx.x;
+        uint32_t n = 0;
+        for (uint32_t k = 0; k < per; k++) {
+            const uint32_t c = (v >> (k * R.width)) & mask;
+            if (c < R.nv) n += C.tlen(R, c);  // (other codes never occur)
+        }
+        s_blen[v] = (uint16_t)n;
+    }
+    __syncthreads();
+    const uint32_t gbytes = kCumGroup / per;  // whole bytes per group of 64 samples
     uint32_t carry = 0;
     for (uint32_t q0 = 0; q0 < ng; q0 += 256) {
         const uint32_t q = q0 + threadIdx.x;
         uint32_t sum = 0;
-        if (q < ng)
-            for (uint32_t s = q * kCumGroup; s < min(A.n_samples, (q + 1) * kCumGroup); s++) sum += C.tlen(R, C.code(R, s));
+        if (q + 1 < ng || (q + 1 == ng && A.n_samples % kCumGroup == 0)) {  // a full group
+            const uint8_t *b = A.codes + R.code_off + (size_t)q * gbytes;
+            for (uint32_t i = 0; i < gbytes; i++) sum += s_blen[b[i]];
+        } else if (q < ng) {  // the last, partial group: sample by sample
+            for (uint32_t s = q * kCumGroup; s < A.n_samples; s++) sum += C.tlen(R, C.code(R, s));
+        }
         s_scan[threadIdx.x] = sum;
         __syncthreads();
         for (uint32_t o = 1; o < 256; o <<= 1) {

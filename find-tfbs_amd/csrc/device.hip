@@ -3,8 +3,11 @@
 // scan_kernels.hip; this file owns device memory, the stream and timing.
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <cerrno>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -820,9 +823,9 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
 }
 
 int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
-                         uint32_t min_maf, uint32_t *fake_position, unsigned char **out, size_t *len,
-                         uint64_t *n_rows, uint64_t *text_bytes) {
-    if (!ctx || !b || !chromosome || !fake_position || !out || !len) return tfbs::fail(TFBS_E_ARG, "null argument");
+                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                         uint64_t *text_bytes) {
+    if (!ctx || !b || !chromosome || !fake_position || fd < 0) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
     Batch &B = b->b;
     r1 = std::min(r1, B.rh.size());
@@ -839,7 +842,7 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
     for (size_t i = 0; i < plan.rows.size(); i++) plan.rows[i].cum_off = (uint32_t)(i * (ng + 1));
     if (n_rows) *n_rows = plan.n_rows;
     if (text_bytes) *text_bytes = plan.text_bytes;
-    std::vector<unsigned char> host;
+    uint64_t written = 0;
     if (n_blocks) {
         if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
             std::vector<uint32_t> t(256 + 32 * kBgzfOps);
@@ -888,14 +891,18 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
                 return rc;
             HIP_TRY(hipMemcpyAsync(ctx->bg_host.p, ctx->bg_packed.p, total, hipMemcpyDeviceToHost, ctx->stream));
             HIP_TRY(hipStreamSynchronize(ctx->stream));
-            host.insert(host.end(), ctx->bg_host.p, ctx->bg_host.p + total);
+            for (uint64_t at = 0; at < total;) {  // the blocks to the file as they are
+                const ssize_t w = ::write(fd, ctx->bg_host.p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
+                if (w < 0) {
+                    if (errno == EINTR) continue;
+                    return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
+                }
+                at += (uint64_t)w;
+            }
+            written += total;
         }
     }
-    unsigned char *p = (unsigned char *)malloc(std::max<size_t>(host.size(), 1));
-    if (!p) return tfbs::fail(TFBS_E_NOMEM, "malloc");
-    if (!host.empty()) memcpy(p, host.data(), host.size());
-    *out = p;
-    *len = host.size();
+    if (bytes) *bytes = written;
     return TFBS_OK;
 }
 

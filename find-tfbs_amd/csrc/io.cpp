@@ -155,11 +155,11 @@ int BgzfWriter::drain() {
     ends.clear();
     return TFBS_OK;
 }
-int BgzfWriter::write_blocks(const unsigned char *p, size_t n) {
+int BgzfWriter::raw_fd() {
     if (raw.size() > (ends.empty() ? 0 : ends.back())) ends.push_back(raw.size());
     if (int rc = drain()) return rc;
-    if (n && fwrite(p, 1, n, f) != n) return fail(TFBS_E_IO, "write failed");
-    return TFBS_OK;
+    if (fflush(f) != 0) return fail(TFBS_E_IO, "write failed");
+    return fileno(f);
 }
 // like BGzWriter::flush: ends the block (an empty block if nothing is buffered)
 int BgzfWriter::flush() {

@@ -21,9 +21,10 @@ class BgzfWriter {
     static constexpr size_t kBlock = 65280;  // htslib/bgzip's BGZF_BLOCK_SIZE of input per block
     int open(const std::string &path, uint32_t threads = 1);
     int write(const char *p, size_t n);
-    // Whole BGZF blocks made elsewhere (tfbs_batch_rows_bgzf): the open block, if
-    // it holds anything, is ended and written first, then these bytes.
-    int write_blocks(const unsigned char *p, size_t n);
+    // For whole BGZF blocks made elsewhere (tfbs_batch_rows_bgzf): the open block,
+    // if it holds anything, is ended and written, the stream flushed; returns the
+    // file descriptor to append the blocks to (or < 0 with the error set).
+    int raw_fd();
     int flush();
     int close();
     ~BgzfWriter();

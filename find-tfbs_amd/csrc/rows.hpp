@@ -30,7 +30,7 @@ struct DevRow {
     uint32_t tok;        // first token slot (RowPlan::tok_text / tok_len)
     uint32_t width;      // bits per code (2, 4, 8); 0: no genotype part on the device
     uint32_t cum_off;    // its per-64-sample byte offsets (bgzf_gpu.hip)
-    uint32_t pad;
+    uint32_t nv;         // token slots (distinct totals) of the key
 };
 
 struct RowPlan {

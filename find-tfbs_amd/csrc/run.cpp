@@ -88,9 +88,9 @@ struct RunSetup {
 
 // Row bodies of one shard in merged-peak order; emit(bodies) gets each batch's
 // rows ('\n'-terminated, no chromosome/POS prefix).
-// emit(bodies): row bodies formatted on the host; blocks(data, n) (non-null for
-// the single shard of a one-device run): the rows as device-made BGZF blocks,
-// POS from *fake.
+// emit(bodies): row bodies formatted on the host; blocks() (non-null for the
+// single shard of a one-device run): the output's file descriptor, the writer's
+// open block written, for the rows as device-made BGZF blocks (POS from *fake).
 template <class Emit, class Blocks>
 int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_t *fake) {
     using namespace tfbs;
@@ -199,16 +199,12 @@ int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_
         double t1 = now();
         sh.t_gpu += t1 - t0;
         if (blocks) {  // rows formatted and deflated on the device (the only shard: POS is known here)
-            unsigned char *data = nullptr;
-            size_t len = 0;
-            if ((rc = tfbs_batch_rows_bgzf(ctx, bb, 0, B.rh.size(), S.chrom.c_str(), a->min_maf, fake, &data, &len,
+            const int fd = (*blocks)();
+            if (fd < 0) return fd;
+            if ((rc = tfbs_batch_rows_bgzf(ctx, bb, 0, B.rh.size(), S.chrom.c_str(), a->min_maf, fake, fd, nullptr,
                                            nullptr, nullptr)))
                 return rc;
-            std::unique_ptr<unsigned char, void (*)(void *)> dguard(data, free);
-            double t2 = now();
-            sh.t_rows += t2 - t1;
-            if ((rc = (*blocks)(data, len))) return rc;
-            sh.t_emit += now() - t2;
+            sh.t_rows += now() - t1;
         } else {
             std::string bodies;
             if ((rc = batch_row_bodies(B, a->min_maf, bodies, sh.threads))) return rc;
@@ -391,7 +387,7 @@ int tfbs_run(const tfbs_run_args *a) {
                 return fail(TFBS_E_IO, "write failed: " + spill_path[k]);
             return TFBS_OK;
         };
-        auto put_blocks = [&](const unsigned char *p, size_t n) { return w.write_blocks(p, n); };
+        auto put_blocks = [&]() { return w.raw_fd(); };
         sh.rc = n_sh == 1 && gpu_bgzf ? run_shard(S, sh, emit, &put_blocks, &fake)
                                       : run_shard(S, sh, emit, (decltype(put_blocks) *)nullptr, &fake);
         if (sh.rc) sh.err = tfbs_last_error();

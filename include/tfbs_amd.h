@@ -251,13 +251,14 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
  * BGZF blocks (main.rs:258-290's BGzWriter) built on the GPU
  * after tfbs_batch_encode over them: row heads formatted on the host, the
  * per-sample genotype text generated from the device codes and deflated there
- * (fixed-Huffman deflate, CRC32), so the text never crosses PCIe.  *out
- * (malloc'd; tfbs_free) receives whole blocks -- the last one shorter -- to be
- * written after the header's blocks; *fake_position is the POS counter, advanced
- * per row; *n_rows / *text_bytes (optional) the rows and their uncompressed bytes. */
+ * (deflate, CRC32), so the text never crosses PCIe.  Whole blocks -- the last one
+ * shorter -- are written to file descriptor fd (after the header's blocks);
+ * *fake_position is the POS counter, advanced per row; *bytes / *n_rows /
+ * *text_bytes (optional) receive the bytes written, the rows and their
+ * uncompressed bytes. */
 int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
-                         uint32_t min_maf, uint32_t *fake_position, unsigned char **out, size_t *len,
-                         uint64_t *n_rows, uint64_t *text_bytes);
+                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                         uint64_t *text_bytes);
 
 /* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
  * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */
