@@ -287,7 +287,7 @@ class RegionBatch:
 
     VECTOR_END = -2147483647
 
-    def __init__(self, patterns, n_samples, keep_membership=True, window_lmax=None):
+    def __init__(self, patterns, n_samples, keep_membership=True, window_lmax=None, build_device=None):
         self.patterns = patterns
         self.n_samples = n_samples
         self.h = C.c_void_p()
@@ -295,6 +295,14 @@ class RegionBatch:
         self.beds = []
         if window_lmax is not None:  # a pattern shard: the whole set's windows (tfbs_batch_set_window_lmax)
             check(lib().tfbs_batch_set_window_lmax(self.h, window_lmax))
+        if build_device is not None:  # haplotype grouping on a device (tfbs_batch_set_build_device)
+            check(lib().tfbs_batch_set_build_device(self.h, build_device))
+
+    def build_stats(self):
+        """(regions grouped on the device, regions built on the host)."""
+        d, h = C.c_uint64(), C.c_uint64()
+        check(lib().tfbs_batch_build_stats(self.h, C.byref(d), C.byref(h)))
+        return d.value, h.value
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -28,11 +28,22 @@ struct KeyRef {
     uint32_t slot;  // pattern_id slot
 };
 
-// hap id -> local distinct index for region R
+// hap id -> local distinct index for region R (a device-grouped region's row is
+// fetched from the device; a failed copy there is fatal)
 struct Membership {
     const RegionH &R;
     std::vector<uint32_t> local;  // dense, built once per region
-    Membership(const RegionH &r, uint32_t H) : R(r), local(H, r.ref_local < 0 ? 0u : (uint32_t)r.ref_local) {
+    Membership(const Batch &B, const RegionH &r, uint32_t H)
+        : R(r), local(H, r.ref_local < 0 ? 0u : (uint32_t)r.ref_local) {
+        if (!r.memb_host) {
+            std::vector<uint8_t> row(H);
+            if (!B.grouper || B.grouper->fetch(r.memb_dev, H, row.data())) {
+                fprintf(stderr, "tfbs: membership fetch from the device failed: %s\n", tfbs_last_error());
+                abort();
+            }
+            for (uint32_t h = 0; h < H; h++) local[h] = row[h];
+            return;
+        }
         for (size_t i = 0; i < r.nonref_id.size(); i++) local[r.nonref_id[i]] = r.nonref_local[i];
     }
 };
@@ -303,7 +314,7 @@ size_t region_rows_each(const Batch &B, const RegionH &R, uint32_t min_maf, std:
             info.clear();
             gts.clear();
             if (!M) {
-                M.reset(new Membership(R, H));
+                M.reset(new Membership(B, R, H));
                 l.resize(B.n_samples);
                 r.resize(B.n_samples);
             }
@@ -393,7 +404,7 @@ static void region_row_parts(const Batch &B, const RegionH &R, uint32_t min_maf,
             info.clear();
             gts.clear();
             if (!M) {
-                M.reset(new Membership(R, H));
+                M.reset(new Membership(B, R, H));
                 l.resize(B.n_samples);
                 r.resize(B.n_samples);
             }
@@ -565,7 +576,8 @@ int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t
     if (end) *end = q.ik->e;
     if (pid) *pid = B.slot_pid[q.slot];
     if (left || right) {
-        tfbs::Membership M(R, 2 * B.n_samples);
+        if (int rc = tfbs::region_membership(B, R)) return rc;
+        tfbs::Membership M(B, R, 2 * B.n_samples);
         for (uint32_t s = 0; s < B.n_samples; s++) {
             if (left) left[s] = tfbs::count_of(B, R, M.local[2 * s], q.slot, q.ik->slot) * q.ik->mult;
             if (right) right[s] = tfbs::count_of(B, R, M.local[2 * s + 1], q.slot, q.ik->slot) * q.ik->mult;
@@ -680,6 +692,7 @@ int tfbs_batch_region_input_digest(const tfbs_batch *b, size_t region, uint64_t 
         h = mix64(h, k.e);
         h = mix64(h, k.mult);
     }
+    if (int rc = tfbs::region_membership(B, R)) return rc;
     for (size_t i = 0; i < R.nonref_id.size(); i++) h = mix64(h, ((uint64_t)R.nonref_id[i] << 32) | R.nonref_local[i]);
     for (uint32_t l = 0; l < R.hap_count; l++) {  // the packed bases, N masks and positions of each distinct haplotype
         const tfbs::DevHap &d = B.haps[R.hap_begin + l];

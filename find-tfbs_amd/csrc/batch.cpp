@@ -6,8 +6,10 @@
 // the same sequence the later one wins (HashMap::insert, haplotype.rs:84); the
 // loser's haplotype ids stay with the reference group (main.rs:103-105, 129-137).
 #include <algorithm>
-#include <map>
 #include <atomic>
+#include <chrono>
+#include <map>
+#include <mutex>
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
@@ -105,32 +107,34 @@ uint64_t Batch::device_bytes() const {
 // ---------------------------------------------------------------------------
 // Builds one region's distinct haplotypes from its inputs; touches no batch
 // state, so regions can be built on several host threads (commit is serial).
+// inner keys: unique (bed, s, e) with multiplicity; distinct non-empty ranges
+static void inner_keys(std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> in, RegionH &R) {
+    R.keys.clear();
+    R.ranges.clear();
+    std::sort(in.begin(), in.end(), [](const auto &a, const auto &b) {
+        if (a.second != b.second) return a.second < b.second;
+        return a.first < b.first;
+    });
+    for (size_t i = 0; i < in.size();) {
+        size_t j = i;
+        while (j < in.size() && in[j] == in[i]) j++;
+        InnerKey k{in[i].first, in[i].second.first, in[i].second.second, (uint32_t)(j - i), -1};
+        if (k.e >= k.s) {
+            auto r = std::make_pair(k.s, k.e);
+            if (R.ranges.empty() || R.ranges.back() != r) R.ranges.push_back(r);
+            k.slot = (int32_t)R.ranges.size() - 1;
+        }
+        R.keys.push_back(k);
+        i = j;
+    }
+}
+
 int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     out.R = std::move(I.R);
     RegionH &R = out.R;
     const uint32_t H = 2 * B.n_samples;
     R.n_variants = (uint32_t)I.recs.size();  // variant_count counts every fetched record (haplotype.rs:25)
-
-    // ---- inner keys: unique (bed, s, e) with multiplicity; distinct non-empty ranges
-    {
-        std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> in = std::move(I.inner);
-        std::sort(in.begin(), in.end(), [](const auto &a, const auto &b) {
-            if (a.second != b.second) return a.second < b.second;
-            return a.first < b.first;
-        });
-        for (size_t i = 0; i < in.size();) {
-            size_t j = i;
-            while (j < in.size() && in[j] == in[i]) j++;
-            InnerKey k{in[i].first, in[i].second.first, in[i].second.second, (uint32_t)(j - i), -1};
-            if (k.e >= k.s) {
-                auto r = std::make_pair(k.s, k.e);
-                if (R.ranges.empty() || R.ranges.back() != r) R.ranges.push_back(r);
-                k.slot = (int32_t)R.ranges.size() - 1;
-            }
-            R.keys.push_back(k);
-            i = j;
-        }
-    }
+    inner_keys(std::move(I.inner), R);
 
     // ---- load_diffs: (haplotype id, canonical diff rank) in record order
     std::vector<const Record *> uniq;
@@ -381,6 +385,204 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     return TFBS_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Device grouping (tfbs_batch_set_build_device).  A region qualifies when
+// load_haplotypes reduces to substitutions into the reference window: every
+// applied record (bi-allelic, with carriers) is an SNV inside the window whose
+// REF base is the window's and whose ALT is another of A/C/G/T; at most 64 of
+// them, no two at one position; every carrier list strictly ascending below 2 *
+// n_samples; no N in the window.  Then no diff list repeats a diff, no two
+// lists patch to one sequence (so HashMap::insert never replaces, haplotype.rs:84)
+// and no patch truncates (haplotype.rs:140-152): the distinct haplotypes are
+// the distinct diff masks in Vec<Diff> order plus the reference group, exactly
+// what build_region finds.  The device computes the masks, the groups and the
+// membership (build_gpu.hip); the host takes the rest from the masks.  Anything
+// else -- and a region of more than kGrpMax masks -- is built by build_region.
+static bool snv_prepare(const Batch &B, const RegionInput &I, RegionBuilt &out, std::vector<const Record *> &uniq) {
+    const uint32_t H = 2 * B.n_samples;
+    const uint64_t n = I.ref.size();
+    if (n == 0 || I.R.ee < I.R.es || n != I.R.ee - I.R.es + 1) return false;
+    for (uint8_t c : I.ref)
+        if (c > 3) return false;
+    uniq.clear();
+    for (const Record &r : I.recs) {
+        if (r.n_alleles != 2 || r.carriers.empty()) continue;  // not applied (haplotype.rs:28-31)
+        if (r.ref.size() != 1 || r.alt.size() != 1 || r.alt[0] > 3 || r.pos < I.R.es || r.pos > I.R.ee) return false;
+        if (I.ref[r.pos - I.R.es] != r.ref[0] || r.alt[0] == r.ref[0]) return false;
+        if (r.carriers.back() >= H) return false;
+        for (size_t i = 1; i < r.carriers.size(); i++)
+            if (r.carriers[i] <= r.carriers[i - 1]) return false;
+        uniq.push_back(&r);
+    }
+    if (uniq.size() > 64) return false;
+    std::sort(uniq.begin(), uniq.end(), diff_less);
+    for (size_t i = 1; i < uniq.size(); i++)
+        if (uniq[i]->pos == uniq[i - 1]->pos) return false;
+    out = RegionBuilt();
+    out.R = I.R;
+    out.R.n_variants = (uint32_t)I.recs.size();
+    inner_keys(I.inner, out.R);
+    out.dev = true;
+    for (const Record *r : uniq) {
+        out.snv_rel.push_back((uint32_t)(r->pos - I.R.es));
+        out.snv_alt.push_back(r->alt[0]);
+    }
+    out.ref = I.ref;
+    return true;
+}
+
+// The device's groups of a qualifying region: G masks with their carrier counts,
+// then the reference group (ids in no group) and the helper as build_region adds them.
+static int snv_finish(const Batch &B, RegionBuilt &b, const uint64_t *masks, const uint32_t *counts, uint32_t G,
+                      uint64_t memb) {
+    const uint32_t H = 2 * B.n_samples;
+    RegionH &R = b.R;
+    b.masks.assign(masks, masks + G);
+    b.carriers.assign(counts, counts + G);
+    uint64_t covered = 0;
+    for (uint32_t i = 0; i < G; i++) covered += counts[i];
+    R.ref_local = -1;
+    if (covered < H) {
+        R.ref_local = (int32_t)G;
+        b.masks.push_back(0);
+        b.carriers.push_back((uint32_t)(H - covered));
+    }
+    const size_t n = b.ref.size();
+    const bool fits = (n + kMWindows - 1) / kMWindows <= kDedupMaxTiles;
+    b.helper = false;
+    if (B.dedup && R.ref_local < 0 && !b.masks.empty() && fits) {
+        b.masks.push_back(0);
+        b.carriers.push_back(0);
+        b.helper = true;
+    }
+    if (n >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
+    R.memb_dev = memb;
+    R.memb_host = false;
+    R.nonref_id.clear();
+    R.nonref_local.clear();
+    return TFBS_OK;
+}
+
+int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std::vector<RegionBuilt> &built,
+                  double *build_s) {
+    const size_t n = ins.size();
+    built.clear();
+    built.resize(n);
+    std::vector<int> rcs(n, TFBS_OK);
+    std::vector<std::vector<const Record *>> uniq(n);
+    std::vector<uint8_t> where(n, 0);  // 1: device grouping, 2: device overflow (host build)
+    const bool dev = B.grouper && B.n_samples > 0;
+    std::mutex mu;
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    auto par = [&](size_t count, auto fn) {
+        std::atomic<size_t> next(0);
+        auto work = [&]() {
+            const double t0 = now();
+            for (size_t j; (j = next.fetch_add(1)) < count;) fn(j);
+            if (build_s) {
+                std::lock_guard<std::mutex> g(mu);
+                *build_s += now() - t0;
+            }
+        };
+        std::vector<std::thread> ts;
+        for (uint32_t t = 1; t < threads && t < count; t++) ts.emplace_back(work);
+        work();
+        for (auto &t : ts) t.join();
+    };
+    par(n, [&](size_t j) {
+        if (dev && snv_prepare(B, ins[j], built[j], uniq[j])) {
+            where[j] = 1;
+            return;
+        }
+        rcs[j] = build_region(B, std::move(ins[j]), built[j]);
+    });
+    if (dev) {
+        std::vector<size_t> dj;
+        for (size_t j = 0; j < n; j++)
+            if (where[j] == 1) dj.push_back(j);
+        const uint32_t H = 2 * B.n_samples;
+        // chunks: the masks scratch (8 bytes per haplotype id and region) within 1 GiB
+        const size_t max_regions = std::max<size_t>(1, std::min<size_t>(1024, (1ull << 30) / (8ull * H)));
+        for (size_t c0 = 0; c0 < dj.size();) {
+            size_t c1 = c0;
+            uint64_t ncar = 0;
+            while (c1 < dj.size() && c1 - c0 < max_regions) {
+                uint64_t m = 0;
+                for (const Record *r : uniq[dj[c1]]) m += r->carriers.size();
+                if (c1 > c0 && ncar + m > (1ull << 30)) break;
+                ncar += m;
+                c1++;
+            }
+            std::vector<GrpRecord> recs;
+            std::vector<GrpRegion> regs;
+            std::vector<uint32_t> rec0(c1 - c0);
+            uint32_t off = 0;
+            for (size_t k = c0; k < c1; k++) {
+                const auto &u = uniq[dj[k]];
+                rec0[k - c0] = (uint32_t)recs.size();
+                regs.push_back({(uint32_t)recs.size(), (uint32_t)u.size()});
+                for (uint32_t q = 0; q < u.size(); q++) {
+                    recs.push_back({off, (uint32_t)u[q]->carriers.size(), q, (uint32_t)(k - c0)});
+                    off += (uint32_t)u[q]->carriers.size();
+                }
+            }
+            uint32_t *car = B.grouper->carriers(ncar);
+            if (!car) return fail(TFBS_E_NOMEM, "device grouping staging");
+            par(c1 - c0, [&](size_t k) {
+                const auto &u = uniq[dj[c0 + k]];
+                for (uint32_t q = 0; q < u.size(); q++) {
+                    const GrpRecord &g = recs[rec0[k] + q];
+                    memcpy(car + g.off, u[q]->carriers.data(), (size_t)g.n * 4);
+                }
+            });
+            GroupOut go;
+            if (int rc = B.grouper->group(ncar, recs, regs, H, go)) return rc;
+            for (size_t k = c0; k < c1; k++) {
+                const size_t j = dj[k], c = k - c0;
+                if (go.n_groups[c] == UINT32_MAX) {
+                    where[j] = 2;
+                    continue;
+                }
+                rcs[j] = snv_finish(B, built[j], go.masks.data() + c * kGrpMax, go.counts.data() + c * kGrpMax,
+                                    go.n_groups[c], go.memb[c]);
+            }
+            c0 = c1;
+        }
+        std::vector<size_t> hj;
+        for (size_t j = 0; j < n; j++)
+            if (where[j] == 2) hj.push_back(j);
+        par(hj.size(), [&](size_t k) {
+            const size_t j = hj[k];
+            built[j] = RegionBuilt();
+            rcs[j] = build_region(B, std::move(ins[j]), built[j]);
+        });
+    }
+    for (size_t j = 0; j < n; j++) {
+        if (rcs[j]) return rcs[j];
+        if (built[j].dev) B.dev_regions++;
+        else B.host_regions++;
+    }
+    return TFBS_OK;
+}
+
+int region_membership(const Batch &B, const RegionH &R) {
+    if (R.memb_host) return TFBS_OK;
+    if (!B.grouper) return fail(TFBS_E_STATE, "membership on a device without its grouper");
+    const uint32_t H = 2 * B.n_samples;
+    std::vector<uint8_t> row(H);
+    if (int rc = B.grouper->fetch(R.memb_dev, H, row.data())) return rc;
+    R.nonref_id.clear();
+    R.nonref_local.clear();
+    const uint8_t ref = (uint8_t)(R.ref_local < 0 ? 0xFF : R.ref_local);
+    for (uint32_t h = 0; h < H; h++)
+        if (row[h] != ref) {
+            R.nonref_id.push_back(h);
+            R.nonref_local.push_back(row[h]);
+        }
+    R.memb_host = true;
+    return TFBS_OK;
+}
+
 // Appends built regions to the batch in order: packs their haplotypes for the
 // GPU.  Offsets are laid out serially (prefix sums over the regions'
 // haplotypes), the packing of bases, N masks and positions runs on `threads`
@@ -407,7 +609,14 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     };
     par([&](size_t j) {
         const RegionBuilt &rb = built[j];
-        info[j].resize(rb.dist.size());
+        info[j].resize(rb.n_haps());
+        if (rb.dev) {  // the reference window with SNVs: its length, no N, affine positions
+            for (HapInfo &h : info[j]) {
+                h.n = (uint32_t)rb.ref.size();
+                h.has_n = false;
+                h.affine = true;
+            }
+        }
         for (size_t i = 0; i < rb.dist.size(); i++) {
             const Distinct &d = rb.dist[i];
             HapInfo &h = info[j][i];
@@ -422,8 +631,25 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         // reference -- another base, another position (past an indel), or past
         // the end of either sequence -- are marked; the others are reused
         // (haplotypes of up to kDedupMaxTiles tiles, the reference's too).
-        const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.dist.size() - 1 : -1);
+        const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.n_haps() - 1 : -1);
         if (!B.dedup || ref < 0) return;
+        auto mark_at = [](HapInfo &h, uint32_t p, bool to_end) {  // windows p - 8 (d + 1) + 1 .. p (.. the last tile)
+            for (uint32_t dd = 0; dd < 4; dd++) {
+                const uint32_t w0 = p + 1 >= 8 * (dd + 1) ? p + 1 - 8 * (dd + 1) : 0;
+                const uint32_t t1 = to_end ? kDedupMaxTiles - 1 : std::min(p / kMWindows, kDedupMaxTiles - 1);
+                for (uint32_t t = w0 / kMWindows; t <= t1; t++) h.dirty[dd] |= 1u << t;
+            }
+        };
+        if (rb.dev) {  // every haplotype has the reference's length: its SNV columns differ
+            if ((rb.ref.size() + kMWindows - 1) / kMWindows > kDedupMaxTiles) return;
+            for (size_t i = 0; i < rb.masks.size(); i++) {
+                if ((int32_t)i == ref) continue;
+                HapInfo &h = info[j][i];
+                h.dedup = true;
+                for (uint64_t x = rb.masks[i]; x; x &= x - 1) mark_at(h, rb.snv_rel[__builtin_ctzll(x)], false);
+            }
+            return;
+        }
         const std::vector<uint8_t> &rn = rb.dist[ref].nuc;
         if ((rn.size() + kMWindows - 1) / kMWindows > kDedupMaxTiles) return;
         for (size_t i = 0; i < rb.dist.size(); i++) {
@@ -431,13 +657,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if ((int32_t)i == ref || (h.n + kMWindows - 1) / kMWindows > kDedupMaxTiles) continue;
             const Distinct &d = rb.dist[i];
             const uint32_t nmin = std::min<uint32_t>(h.n, (uint32_t)rn.size());
-            auto mark = [&](uint32_t p, bool to_end) {  // windows p - 8 (d + 1) + 1 .. p (.. the last tile)
-                for (uint32_t dd = 0; dd < 4; dd++) {
-                    const uint32_t w0 = p + 1 >= 8 * (dd + 1) ? p + 1 - 8 * (dd + 1) : 0;
-                    const uint32_t t1 = to_end ? kDedupMaxTiles - 1 : std::min(p / kMWindows, kDedupMaxTiles - 1);
-                    for (uint32_t t = w0 / kMWindows; t <= t1; t++) h.dirty[dd] |= 1u << t;
-                }
-            };
+            auto mark = [&](uint32_t p, bool to_end) { mark_at(h, p, to_end); };
             h.dedup = true;
             for (uint32_t p = 0; p < nmin; p++)
                 if (d.nuc[p] != rn[p] || d.pos[p] != rb.R.es + p) mark(p, false);
@@ -454,7 +674,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     for (size_t j = 0; j < nr; j++) {
         off[j] = cur;
         const uint32_t n_inner = (uint32_t)built[j].R.ranges.size();
-        cur.hap += built[j].dist.size();
+        cur.hap += built[j].n_haps();
         cur.inner += 2 * n_inner;
         for (const HapInfo &h : info[j]) {
             cur.word += (h.n + 15) / 16 + 3;
@@ -478,7 +698,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         RegionH &R = rb.R;
         const Off &o = off[j];
         R.hap_begin = (uint32_t)o.hap;
-        R.hap_count = (uint32_t)rb.dist.size() - (rb.helper ? 1 : 0);
+        R.hap_count = (uint32_t)rb.n_haps() - (rb.helper ? 1 : 0);
         const int32_t ref = R.ref_local >= 0 ? R.ref_local : (rb.helper ? (int32_t)R.hap_count : -1);
         DevRegion dr{};
         dr.inner_off = (uint32_t)(o.inner / 2);
@@ -486,7 +706,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         dr.hap_begin = R.hap_begin;
         dr.hap_count = R.hap_count;
         dr.ref_hap = ref >= 0 && B.dedup ? R.hap_begin + (uint32_t)ref : UINT32_MAX;
-        dr.count_stride = (uint32_t)rb.dist.size();
+        dr.count_stride = (uint32_t)rb.n_haps();
         R.key_off = (uint64_t)dr.inner_off * B.n_slots;
         size_t ii = o.inner;
         for (auto &r : R.ranges) {
@@ -504,8 +724,12 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         uint64_t word = o.word, nmask = o.nmask, pos = o.pos, count = o.count;
         // per-region sums in registers (the arrays are shared by the threads)
         uint64_t r_win = 0, r_eff = 0, r_cells = 0, r_swin = 0, r_scells = 0;
-        for (uint32_t i = 0; i < rb.dist.size(); i++) {
-            const Distinct &d = rb.dist[i];
+        std::vector<uint32_t> refw;  // device-grouped: the reference window packed once
+        if (rb.dev) {
+            refw.assign((rb.ref.size() + 15) / 16, 0u);
+            for (size_t p = 0; p < rb.ref.size(); p++) refw[p / 16] |= (uint32_t)rb.ref[p] << (2 * (p % 16));
+        }
+        for (uint32_t i = 0; i < rb.n_haps(); i++) {
             const HapInfo &h = info[j][i];
             const uint32_t n = h.n;
             DevHap hm{};
@@ -513,12 +737,22 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             hm.len = n;
             hm.region = region0 + (uint32_t)j;
             uint32_t *w = B.words.data() + word;
-            for (uint32_t p = 0; p < n; p++) {
-                const uint32_t c = d.nuc[p] == 4 ? 0u : d.nuc[p];  // N packs as A (masked by the N bits)
-                w[p / 16] |= c << (2 * (p % 16));
+            if (rb.dev) {  // the reference's words, the SNVs' bases written over
+                std::copy(refw.begin(), refw.end(), w);
+                for (uint64_t x = rb.masks[i]; x; x &= x - 1) {
+                    const uint32_t k = __builtin_ctzll(x), p = rb.snv_rel[k];
+                    w[p / 16] = (w[p / 16] & ~(3u << (2 * (p % 16)))) | ((uint32_t)rb.snv_alt[k] << (2 * (p % 16)));
+                }
+            } else {
+                const Distinct &d = rb.dist[i];
+                for (uint32_t p = 0; p < n; p++) {
+                    const uint32_t c = d.nuc[p] == 4 ? 0u : d.nuc[p];  // N packs as A (masked by the N bits)
+                    w[p / 16] |= c << (2 * (p % 16));
+                }
             }
             word += (n + 15) / 16 + 3;
             if (h.has_n) {
+                const Distinct &d = rb.dist[i];
                 hm.flags |= HAP_HAS_N;
                 hm.nmask_off = (uint32_t)nmask;
                 uint32_t *m = B.nmask.data() + nmask;
@@ -527,6 +761,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 nmask += (n + 31) / 32 + 2;
             }
             if (!h.affine) {
+                const Distinct &d = rb.dist[i];
                 hm.flags |= HAP_HAS_POS;
                 hm.pos_off = (uint32_t)pos;
                 for (uint32_t p = 0; p < n; p++) B.posrel[pos + p] = (int32_t)(d.pos[p] - R.es);
@@ -540,7 +775,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             }
             B.haps[o.hap + i] = hm;
             B.hap_carriers[o.hap + i] = rb.carriers[i];
-            const bool helper = rb.helper && i + 1 == rb.dist.size();
+            const bool helper = rb.helper && i + 1 == rb.n_haps();
             uint64_t wn = 0;
             for (const auto &lc : B.pwm_len_hist)
                 if (n >= lc.first) {
@@ -640,6 +875,25 @@ int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax) {
     return TFBS_OK;
 }
 
+int tfbs_batch_set_build_device(tfbs_batch *b, int device) {
+    if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    Batch &B = b->b;
+    if (!B.rh.empty() || B.open) return tfbs::fail(TFBS_E_STATE, "regions already added");
+    B.grouper.reset();
+    if (device < 0) return TFBS_OK;
+    tfbs::DevGrouper *g = tfbs::make_gpu_grouper(device);
+    if (!g) return TFBS_E_NODEVICE;
+    B.grouper.reset(g);
+    return TFBS_OK;
+}
+
+int tfbs_batch_build_stats(const tfbs_batch *b, uint64_t *dev_regions, uint64_t *host_regions) {
+    if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (dev_regions) *dev_regions = b->b.dev_regions;
+    if (host_regions) *host_regions = b->b.host_regions;
+    return TFBS_OK;
+}
+
 int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t ms, uint64_t me, uint64_t *es, uint64_t *ee) {
     if (!b || !es || !ee) return tfbs::fail(TFBS_E_ARG, "null argument");
     uint64_t L = b->b.lmax();
@@ -719,24 +973,9 @@ int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const c
 
 // Builds regions on up to `threads` host threads, commits them in order.
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads) {
-    const size_t n = ins.size();
-    std::vector<RegionBuilt> built(n);
-    std::vector<int> rcs(n, TFBS_OK);
-    std::atomic<size_t> next(0);
-    auto work = [&]() {
-        for (;;) {
-            const size_t j = next.fetch_add(1);
-            if (j >= n) break;
-            rcs[j] = build_region(B, std::move(ins[j]), built[j]);
-        }
-    };
-    std::vector<std::thread> ts;
-    for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
-    work();
-    for (auto &t : ts) t.join();
+    std::vector<RegionBuilt> built;
     B.counts_valid = B.reduced = false;
-    for (size_t j = 0; j < n; j++)
-        if (rcs[j]) return rcs[j];
+    if (int rc = build_regions(B, ins, threads, built, nullptr)) return rc;
     commit_regions(B, built, threads);
     return TFBS_OK;
 }
@@ -785,11 +1024,9 @@ int tfbs_batch_region_end(tfbs_batch *b) {
     in.inner = std::move(B.cur_inner);
     B.cur_rec.clear();
     B.cur_inner.clear();
-    tfbs::RegionBuilt built;
-    int rc = tfbs::build_region(B, std::move(in), built);
-    if (rc) return rc;
-    tfbs::commit_region(B, std::move(built));
-    return TFBS_OK;
+    std::vector<tfbs::RegionInput> ins(1);
+    ins[0] = std::move(in);
+    return tfbs::add_regions(B, ins, 1);
 }
 
 size_t tfbs_batch_num_regions(const tfbs_batch *b) { return b ? b->b.rh.size() : 0; }

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -33,8 +34,13 @@ struct RegionH {
     uint64_t key_off = 0;                   // first key (slot * n_inner + range) in the reduced arrays
     std::vector<InnerKey> keys;             // sorted by (s, e, bed)
     std::vector<std::pair<uint64_t, uint64_t>> ranges;  // distinct non-empty inner ranges
-    // membership: haplotype id -> local distinct index; ids not listed use ref_local
-    std::vector<uint32_t> nonref_id, nonref_local;
+    // membership: haplotype id -> local distinct index; ids not listed use ref_local.
+    // A region grouped on the device (memb_dev != 0) keeps its membership there, one
+    // byte per haplotype id; the lists are filled from it when a host path asks
+    // (region_membership).
+    mutable std::vector<uint32_t> nonref_id, nonref_local;
+    uint64_t memb_dev = 0;          // device address of the membership row, 0 if host-built
+    mutable bool memb_host = true;  // nonref_id / nonref_local are valid
 };
 
 // Page-locked host bytes (hipHostMalloc): device downloads land at full PCIe rate.
@@ -50,6 +56,37 @@ struct PinnedBytes {
     PinnedBytes(const PinnedBytes &) = delete;
     PinnedBytes &operator=(const PinnedBytes &) = delete;
 };
+
+// Device grouping (haplotype.rs:16-88 on the GPU): regions whose
+// applied diffs are all SNVs get their haplotypes' diff masks, distinct groups and
+// membership computed on a device (build_gpu.hip).  One chunk of regions:
+// carrier ids back to back (each record's list), the records and the regions.
+struct GrpRecord {
+    uint32_t off, n;     // carriers [off, off + n) of the chunk's carrier array
+    uint32_t rank;       // the diff's rank in Vec<Diff> order (its bit in the masks)
+    uint32_t region;     // chunk region index
+};
+struct GrpRegion {
+    uint32_t rec_off, n_rec;  // records [rec_off, rec_off + n_rec) of the chunk
+};
+constexpr uint32_t kGrpMax = 254;  // distinct diff masks of a device-grouped region (u8 membership)
+struct GroupOut {                 // per chunk region
+    std::vector<uint32_t> n_groups;  // distinct non-empty masks, UINT32_MAX: more than kGrpMax (host build)
+    std::vector<uint64_t> masks;     // kGrpMax per region, ascending Vec<Diff> order
+    std::vector<uint32_t> counts;    // carriers per mask
+    std::vector<uint64_t> memb;      // device address of each region's membership row
+};
+struct DevGrouper {
+    virtual ~DevGrouper() {}
+    virtual int device() const = 0;
+    // staging for n carrier ids (page-locked, valid until the next group call)
+    virtual uint32_t *carriers(size_t n) = 0;
+    virtual int group(size_t n_car, const std::vector<GrpRecord> &recs, const std::vector<GrpRegion> &regs,
+                      uint32_t H, GroupOut &out) = 0;
+    // one membership row (H bytes) to the host
+    virtual int fetch(uint64_t memb, uint32_t H, uint8_t *out) = 0;
+};
+DevGrouper *make_gpu_grouper(int device);  // build_gpu.hip
 
 struct Batch {
     const Patterns *pats = nullptr;
@@ -120,6 +157,11 @@ struct Batch {
     uint32_t window_lmax = 0;
     uint32_t lmax() const { return window_lmax ? window_lmax : pats->max_length(); }
 
+    // device grouping of SNV-only regions (tfbs_batch_set_build_device); it owns
+    // their membership rows, so it lives as long as the batch
+    std::unique_ptr<DevGrouper> grouper;
+    uint64_t dev_regions = 0, host_regions = 0;  // regions grouped on the device / built on the host
+
     uint64_t device_bytes() const;
 };
 
@@ -143,9 +185,24 @@ struct RegionBuilt {
     std::vector<Distinct> dist;
     std::vector<uint32_t> carriers;
     bool helper = false;  // dist.back() is a helper reference haplotype (no carriers, no keys)
+    // grouped on the device: distinct haplotype i is the reference window with the
+    // SNVs of masks[i] (bit k = snv_rel[k] / snv_alt[k]; 0 = the reference group or
+    // the helper); dist stays empty
+    bool dev = false;
+    std::vector<uint64_t> masks;
+    std::vector<uint32_t> snv_rel;
+    std::vector<uint8_t> snv_alt;
+    std::vector<uint8_t> ref;
+    size_t n_haps() const { return dev ? masks.size() : dist.size(); }
 };
 
 int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);
+// Builds regions (on the device grouper where they qualify, see batch.cpp),
+// `threads` host threads; *build_s (optional) += the host threads' seconds.
+int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std::vector<RegionBuilt> &built,
+                  double *build_s);
+// The region's nonref_id / nonref_local (fetched from the device if grouped there).
+int region_membership(const Batch &B, const RegionH &R);
 void commit_region(Batch &B, RegionBuilt &&built);
 void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads);
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads);

@@ -706,6 +706,8 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     const size_t nr = r1 - r0;
     const size_t pbytes = nr * (size_t)N * 2;
     int rc;
+    for (size_t r = r0; r < r1; r++)
+        if ((rc = region_membership(B, B.rh[r]))) return rc;
     if ((rc = ctx->enc_memb_host.reserve(pbytes))) return rc;
     uint16_t *const pidx = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p);
     std::vector<std::vector<uint16_t>> pab(nr);

@@ -366,31 +366,11 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
             gen();
             for (auto &t : ts) t.join();
         }
-        // phase 2: load_diffs / group / patch / dedup / pack (build_region), then the commit
+        // phase 2: load_diffs / group / patch / dedup / pack (build_regions: on the
+        // device grouper where the region qualifies), then the commit
         const double t_build = now();
-        std::vector<tfbs::RegionBuilt> built(n);
-        std::vector<int> rcs(n, TFBS_OK);
-        next = 0;
-        auto work = [&]() {
-            double t_b = 0;
-            for (;;) {
-                const uint64_t j = next.fetch_add(1);
-                if (j >= n) break;
-                const double t1 = now();
-                rcs[j] = tfbs::build_region(B, std::move(ins[j]), built[j]);
-                t_b += now() - t1;
-            }
-            std::lock_guard<std::mutex> g(mu);
-            B.prep_s[1] += t_b;
-        };
-        {
-            std::vector<std::thread> ts;
-            for (uint32_t t = 0; t + 1 < T && t + 1 < n; t++) ts.emplace_back(work);
-            work();
-            for (auto &t : ts) t.join();
-        }
-        for (uint64_t j = 0; j < n; j++)
-            if (rcs[j]) return rcs[j];
+        std::vector<tfbs::RegionBuilt> built;
+        if (int rc = tfbs::build_regions(B, ins, T, built, &B.prep_s[1])) return rc;
         tfbs::commit_regions(B, built, T);
         B.prep_s[2] += now() - t_build;
     }

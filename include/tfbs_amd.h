@@ -178,6 +178,18 @@ int tfbs_batch_add_bed(tfbs_batch *b, const char *basename);
  * pattern_ids passes the whole set's L_max so that its windows, distinct haplotypes
  * and counts are those of the unsharded run (SURVEY.md 8(e) region x PWM shard). */
 int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax);
+/* load_diffs / group_by_diffs / load_haplotypes (haplotype.rs:16-88) on a device
+ * (before the first region; device < 0: host only): a region whose applied
+ * records are all SNVs inside its window (REF = the window's base, ALT another of
+ * A/C/G/T, at most 64, one per position, carrier ids ascending) and whose window
+ * has no N gets its haplotypes' diff masks, distinct groups and membership
+ * computed there (the membership stays on the device, one byte per haplotype id,
+ * fetched only when a host path needs it); every other region, and one of more
+ * than 254 distinct groups, is built on the host.  The batch is the same either
+ * way (tfbs_batch_region_input_digest). */
+int tfbs_batch_set_build_device(tfbs_batch *b, int device);
+/* Regions grouped on the device / built on the host so far. */
+int tfbs_batch_build_stats(const tfbs_batch *b, uint64_t *dev_regions, uint64_t *host_regions);
 /* main.rs:404-407: the halo-extended window of a merged region. */
 int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t merged_start, uint64_t merged_end, uint64_t *ext_start,
                           uint64_t *ext_end);
