@@ -36,7 +36,7 @@ struct Membership {
     Membership(const Batch &B, const RegionH &r, uint32_t H)
         : R(r), local(H, r.ref_local < 0 ? 0u : (uint32_t)r.ref_local) {
         if (!r.memb_host) {
-            std::vector<uint8_t> row(H);
+            std::vector<uint16_t> row(H);
             if (!B.grouper || B.grouper->fetch(r.memb_dev, H, row.data())) {
                 fprintf(stderr, "tfbs: membership fetch from the device failed: %s\n", tfbs_last_error());
                 abort();

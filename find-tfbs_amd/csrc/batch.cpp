@@ -391,7 +391,8 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
 // applied record (bi-allelic, with carriers) is an SNV inside the window whose
 // REF base is the window's and whose ALT is another of A/C/G/T; at most 64 of
 // them, no two at one position; every carrier list strictly ascending below 2 *
-// n_samples; no N in the window.  Then no diff list repeats a diff, no two
+// n_samples; no N in the window.  (A region of more than kGrpMax distinct masks
+// is built on the host too.)  Then no diff list repeats a diff, no two
 // lists patch to one sequence (so HashMap::insert never replaces, haplotype.rs:84)
 // and no patch truncates (haplotype.rs:140-152): the distinct haplotypes are
 // the distinct diff masks in Vec<Diff> order plus the reference group, exactly
@@ -543,7 +544,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
                     where[j] = 2;
                     continue;
                 }
-                rcs[j] = snv_finish(B, built[j], go.masks.data() + c * kGrpMax, go.counts.data() + c * kGrpMax,
+                rcs[j] = snv_finish(B, built[j], go.masks.data() + go.first[c], go.counts.data() + go.first[c],
                                     go.n_groups[c], go.memb[c]);
             }
             c0 = c1;
@@ -569,11 +570,11 @@ int region_membership(const Batch &B, const RegionH &R) {
     if (R.memb_host) return TFBS_OK;
     if (!B.grouper) return fail(TFBS_E_STATE, "membership on a device without its grouper");
     const uint32_t H = 2 * B.n_samples;
-    std::vector<uint8_t> row(H);
+    std::vector<uint16_t> row(H);
     if (int rc = B.grouper->fetch(R.memb_dev, H, row.data())) return rc;
     R.nonref_id.clear();
     R.nonref_local.clear();
-    const uint8_t ref = (uint8_t)(R.ref_local < 0 ? 0xFF : R.ref_local);
+    const uint32_t ref = R.ref_local < 0 ? UINT32_MAX : (uint32_t)R.ref_local;
     for (uint32_t h = 0; h < H; h++)
         if (row[h] != ref) {
             R.nonref_id.push_back(h);

@@ -36,7 +36,7 @@ struct RegionH {
     std::vector<std::pair<uint64_t, uint64_t>> ranges;  // distinct non-empty inner ranges
     // membership: haplotype id -> local distinct index; ids not listed use ref_local.
     // A region grouped on the device (memb_dev != 0) keeps its membership there, one
-    // byte per haplotype id; the lists are filled from it when a host path asks
+    // u16 per haplotype id; the lists are filled from it when a host path asks
     // (region_membership).
     mutable std::vector<uint32_t> nonref_id, nonref_local;
     uint64_t memb_dev = 0;          // device address of the membership row, 0 if host-built
@@ -69,10 +69,11 @@ struct GrpRecord {
 struct GrpRegion {
     uint32_t rec_off, n_rec;  // records [rec_off, rec_off + n_rec) of the chunk
 };
-constexpr uint32_t kGrpMax = 254;  // distinct diff masks of a device-grouped region (u8 membership)
+constexpr uint32_t kGrpMax = 2047;  // distinct diff masks of a device-grouped region (the LDS table)
 struct GroupOut {                 // per chunk region
     std::vector<uint32_t> n_groups;  // distinct non-empty masks, UINT32_MAX: more than kGrpMax (host build)
-    std::vector<uint64_t> masks;     // kGrpMax per region, ascending Vec<Diff> order
+    std::vector<uint32_t> first;     // the region's first mask in masks / counts
+    std::vector<uint64_t> masks;     // per region n_groups masks, ascending Vec<Diff> order
     std::vector<uint32_t> counts;    // carriers per mask
     std::vector<uint64_t> memb;      // device address of each region's membership row
 };
@@ -83,8 +84,8 @@ struct DevGrouper {
     virtual uint32_t *carriers(size_t n) = 0;
     virtual int group(size_t n_car, const std::vector<GrpRecord> &recs, const std::vector<GrpRegion> &regs,
                       uint32_t H, GroupOut &out) = 0;
-    // one membership row (H bytes) to the host
-    virtual int fetch(uint64_t memb, uint32_t H, uint8_t *out) = 0;
+    // one membership row (H u16) to the host
+    virtual int fetch(uint64_t memb, uint32_t H, uint16_t *out) = 0;
 };
 DevGrouper *make_gpu_grouper(int device);  // build_gpu.hip
 

@@ -1,8 +1,8 @@
 // Device grouping of SNV-only regions (haplotype.rs:16-88 for the regions
 // batch.cpp's snv_prepare admits): every haplotype id's diff mask, the
-// distinct masks in Vec<Diff> order with their carrier counts, and one
-// membership byte per haplotype id (its distinct index; the reference group's
-// index for ids carrying no diff).
+// distinct masks in Vec<Diff> order with their carrier counts, and one u16 of
+// membership per haplotype id (its distinct index; the reference group's index
+// for ids carrying no diff).
 //
 //   mask_scatter_kernel  one workgroup per record: each carrier id ORs the
 //                        record's rank bit into its mask (a chunk-wide scratch of
@@ -35,10 +35,10 @@ namespace tfbs {
 namespace {
 
 constexpr int kGrpBlock = 512;
-constexpr uint32_t kGrpSlots = 2048;  // LDS hash slots: kGrpMax masks + one claim per thread stay below half
+constexpr uint32_t kGrpSlots = 8192;  // LDS hash slots: kGrpMax masks + one claim per thread stay below half
 
 __device__ __forceinline__ uint32_t mask_slot(uint64_t m) {
-    return (uint32_t)((m * 0x9E3779B97F4A7C15ull) >> 53) & (kGrpSlots - 1);
+    return (uint32_t)((m * 0x9E3779B97F4A7C15ull) >> 51) & (kGrpSlots - 1);
 }
 
 // Vec<Diff> order of two masks' ascending rank lists (batch.cpp's lex_less)
@@ -63,16 +63,17 @@ __global__ __launch_bounds__(kGrpBlock) void mask_group_kernel(const GrpRegion *
                                                                const GrpRecord *__restrict__ recs,
                                                                const uint32_t *__restrict__ car,
                                                                unsigned long long *__restrict__ sig, uint32_t H,
-                                                               uint8_t *__restrict__ memb, size_t memb_stride,
+                                                               uint16_t *__restrict__ memb, size_t memb_stride,
                                                                uint32_t *__restrict__ n_groups,
+                                                               uint32_t *__restrict__ first, uint32_t *__restrict__ total,
                                                                unsigned long long *__restrict__ masks,
                                                                uint32_t *__restrict__ counts) {
     __shared__ unsigned long long s_key[kGrpSlots];
     __shared__ uint32_t s_cnt[kGrpSlots];
-    __shared__ uint8_t s_idx[kGrpSlots];
+    __shared__ uint16_t s_idx[kGrpSlots];
     __shared__ unsigned long long s_m[kGrpMax];
     __shared__ uint32_t s_c[kGrpMax], s_slot[kGrpMax];
-    __shared__ uint32_t s_n, s_over, s_pos;
+    __shared__ uint32_t s_n, s_over, s_pos, s_first;
     const uint32_t j = blockIdx.x, tid = threadIdx.x;
     const GrpRegion R = regs[j];
     unsigned long long *row = sig + (size_t)j * H;
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(kGrpBlock) void mask_group_kernel(const GrpRegion *
     const bool over = s_over != 0;
     const uint32_t G = s_n;
     if (!over) {
+        if (tid == 0) s_first = atomicAdd(total, G);  // the region's masks at [first, first + G)
         for (uint32_t t = tid; t < kGrpSlots; t += kGrpBlock)
             if (s_key[t]) {
                 const uint32_t at = atomicAdd(&s_pos, 1u);
@@ -127,15 +129,15 @@ __global__ __launch_bounds__(kGrpBlock) void mask_group_kernel(const GrpRegion *
             const unsigned long long m = s_m[t];
             uint32_t rk = 0;
             for (uint32_t u = 0; u < G; u++) rk += lex_less(s_m[u], m) ? 1u : 0u;
-            masks[(size_t)j * kGrpMax + rk] = m;
-            counts[(size_t)j * kGrpMax + rk] = s_c[t];
-            s_idx[s_slot[t]] = (uint8_t)rk;
+            masks[s_first + rk] = m;
+            counts[s_first + rk] = s_c[t];
+            s_idx[s_slot[t]] = (uint16_t)rk;
         }
         // the membership row: the reference group's index (G) for every id ...
-        uint8_t *mrow = memb + (size_t)j * memb_stride;
-        const uint32_t fill = G * 0x01010101u;
+        uint16_t *mrow = memb + (size_t)j * memb_stride;
+        const uint32_t fill = G * 0x00010001u;
         const uint4 f4 = make_uint4(fill, fill, fill, fill);
-        for (uint32_t i = tid; i < (uint32_t)(memb_stride / 16); i += kGrpBlock)
+        for (uint32_t i = tid; i < (uint32_t)(memb_stride / 8); i += kGrpBlock)
             reinterpret_cast<uint4 *>(mrow)[i] = f4;
     }
     __syncthreads();
@@ -159,7 +161,10 @@ __global__ __launch_bounds__(kGrpBlock) void mask_group_kernel(const GrpRegion *
         const GrpRecord r = recs[R.rec_off + q];
         for (uint32_t i = tid; i < r.n; i += kGrpBlock) row[car[r.off + i]] = 0ull;
     }
-    if (tid == 0) n_groups[j] = over ? UINT32_MAX : G;
+    if (tid == 0) {
+        n_groups[j] = over ? UINT32_MAX : G;
+        first[j] = over ? 0 : s_first;
+    }
 }
 
 template <typename T>
@@ -188,12 +193,13 @@ struct GpuGrouper final : DevGrouper {
     hipStream_t stream = nullptr;
     Buf<unsigned long long> sig;  // zero between chunks
     bool sig_zero = false;        // sig holds zeros up to its capacity
-    Buf<uint32_t> car, n_groups, counts;
+    Buf<uint32_t> car, n_groups, first, counts;
+    uint32_t *total_host = nullptr;  // pinned: the chunk's masks
     Buf<unsigned long long> masks;
     Buf<GrpRecord> recs;
     Buf<GrpRegion> regs;
     PinnedBytes car_host;
-    std::vector<uint8_t *> memb;  // one allocation per chunk, for the batch's lifetime
+    std::vector<uint16_t *> memb;  // one allocation per chunk, for the batch's lifetime
 
     ~GpuGrouper() override {
         (void)hipSetDevice(dev);
@@ -201,11 +207,13 @@ struct GpuGrouper final : DevGrouper {
         sig.release();
         car.release();
         n_groups.release();
+        first.release();
         counts.release();
+        if (total_host) (void)hipHostFree(total_host);
         masks.release();
         recs.release();
         regs.release();
-        for (uint8_t *p : memb) (void)hipFree(p);
+        for (uint16_t *p : memb) (void)hipFree(p);
         if (stream) (void)hipStreamDestroy(stream);
     }
     int device() const override { return dev; }
@@ -218,21 +226,23 @@ struct GpuGrouper final : DevGrouper {
         HIP_OK(hipSetDevice(dev));
         const size_t nr = rg.size();
         out.n_groups.assign(nr, 0);
-        out.masks.assign(nr * kGrpMax, 0);
-        out.counts.assign(nr * kGrpMax, 0);
+        out.first.assign(nr, 0);
         out.memb.assign(nr, 0);
         if (!nr) return TFBS_OK;
-        const size_t stride = ((size_t)H + 15) / 16 * 16;
-        uint8_t *mb = nullptr;
-        HIP_OK(hipMalloc(&mb, std::max<size_t>(nr * stride, 16)));
+        const size_t stride = ((size_t)H + 7) / 8 * 8;  // u16 per id, rows 16-byte aligned
+        uint16_t *mb = nullptr;
+        HIP_OK(hipMalloc(&mb, std::max<size_t>(nr * stride * 2, 16)));
         memb.push_back(mb);
         int rc;
         const size_t sig_n = nr * (size_t)H;
         if (sig_n > sig.cap) sig_zero = false;
         if ((rc = sig.ensure(sig_n)) || (rc = car.ensure(std::max<size_t>(n_car, 1))) ||
             (rc = recs.ensure(std::max<size_t>(rv.size(), 1))) || (rc = regs.ensure(nr)) ||
-            (rc = n_groups.ensure(nr)) || (rc = masks.ensure(nr * kGrpMax)) || (rc = counts.ensure(nr * kGrpMax)))
+            (rc = n_groups.ensure(nr + 1)) || (rc = first.ensure(nr)) || (rc = masks.ensure(nr * kGrpMax)) ||
+            (rc = counts.ensure(nr * kGrpMax)))
             return rc;
+        if (!total_host) HIP_OK(hipHostMalloc((void **)&total_host, 4, hipHostMallocDefault));
+        HIP_OK(hipMemsetAsync(n_groups.p + nr, 0, 4, stream));  // the masks' counter
         if (!sig_zero) {
             HIP_OK(hipMemsetAsync(sig.p, 0, sig.cap * sizeof(unsigned long long), stream));
             sig_zero = true;
@@ -245,12 +255,23 @@ struct GpuGrouper final : DevGrouper {
             hipLaunchKernelGGL(mask_scatter_kernel, dim3((uint32_t)rv.size()), dim3(256), 0, stream, recs.p, car.p,
                                sig.p, H);
         hipLaunchKernelGGL(mask_group_kernel, dim3((uint32_t)nr), dim3(kGrpBlock), 0, stream, regs.p, recs.p, car.p,
-                           sig.p, H, mb, stride, n_groups.p, masks.p, counts.p);
+                           sig.p, H, mb, stride, n_groups.p, first.p, n_groups.p + nr, masks.p, counts.p);
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(out.n_groups.data(), n_groups.p, nr * 4, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipMemcpyAsync(out.masks.data(), masks.p, nr * kGrpMax * 8, hipMemcpyDeviceToHost, stream));
-        HIP_OK(hipMemcpyAsync(out.counts.data(), counts.p, nr * kGrpMax * 4, hipMemcpyDeviceToHost, stream));
-        const hipError_t e = hipStreamSynchronize(stream);
+        HIP_OK(hipMemcpyAsync(out.first.data(), first.p, nr * 4, hipMemcpyDeviceToHost, stream));
+        HIP_OK(hipMemcpyAsync(total_host, n_groups.p + nr, 4, hipMemcpyDeviceToHost, stream));
+        hipError_t e = hipStreamSynchronize(stream);
+        if (e == hipSuccess) {
+            const uint32_t tot = *total_host;
+            out.masks.resize(tot);
+            out.counts.resize(tot);
+            if (tot) {
+                e = hipMemcpyAsync(out.masks.data(), masks.p, (size_t)tot * 8, hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(out.counts.data(), counts.p, (size_t)tot * 4, hipMemcpyDeviceToHost, stream);
+                if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            }
+        }
         if (e != hipSuccess) {
             sig_zero = false;
             return fail(TFBS_E_HIP, std::string("device grouping: ") + hipGetErrorString(e));
@@ -258,9 +279,9 @@ struct GpuGrouper final : DevGrouper {
         for (size_t j = 0; j < nr; j++) out.memb[j] = (uint64_t)(uintptr_t)(mb + j * stride);
         return TFBS_OK;
     }
-    int fetch(uint64_t m, uint32_t H, uint8_t *out) override {
+    int fetch(uint64_t m, uint32_t H, uint16_t *out) override {
         HIP_OK(hipSetDevice(dev));
-        HIP_OK(hipMemcpy(out, (const void *)(uintptr_t)m, H, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(out, (const void *)(uintptr_t)m, (size_t)H * 2, hipMemcpyDeviceToHost));
         return TFBS_OK;
     }
 };

@@ -128,9 +128,11 @@ struct tfbs_ctx {
     uint32_t *var_tot_host = nullptr;    // pinned
     // per-sample encoding (tfbs_batch_encode)
     DevBuf<uint8_t> enc_codes, enc_packed;
-    DevBuf<uint16_t> enc_pidx, enc_pab;   // per sample its haplotype pair; per pair its distinct indices
-    DevBuf<uint32_t> enc_pcnt, enc_pair_off;
-    tfbs::PinnedBytes enc_memb_host;  // the samples' pair indices staged for upload (reused)
+    DevBuf<uint16_t> enc_pidx;            // per sample its haplotype pair
+    DevBuf<uint32_t> enc_pab, enc_pcnt, enc_pair_n;  // per pair its distinct indices a | b << 16, its samples
+    DevBuf<uint16_t> enc_memb;            // membership rows of host-built regions (u16 per haplotype id)
+    DevBuf<uint64_t> enc_rows;            // per region the device address of its membership row
+    tfbs::PinnedBytes enc_memb_host;  // host-built regions' membership rows staged for upload (reused)
     uint32_t host_threads = 16;      // host threads of tfbs_batch_encode (tfbs_ctx_set_host_threads)
     DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
@@ -396,7 +398,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
     ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
-    ctx->enc_pair_off.release(); ctx->enc_codes.release(); ctx->enc_hdr.release();
+    ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_rows.release(); ctx->enc_codes.release();
+    ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
     ctx->bg_out.release(); ctx->bg_packed.release(); ctx->bg_cum.release(); ctx->bg_out_len.release();
@@ -698,57 +701,36 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
         B.enc_r1 = (uint32_t)r1;
         return TFBS_OK;
     }
-    // per region of [r0, r1) with <= 255 distinct haplotypes: its distinct (left,
-    // right) haplotype pairs with their sample counts and each sample's pair (u16,
-    // written by the host threads into the ctx's pinned staging buffer).  Most
-    // samples carry the reference group on both sides: the rows start as that
-    // pair, and only samples with a haplotype outside the group are looked up.
+    // every region's u16 membership row on this device -- a device-grouped region's
+    // own, the others' made by the host threads in the ctx's pinned staging and
+    // uploaded -- then its distinct (left, right) haplotype pairs and each sample's
+    // pair on the device (launch_pair_table)
     const size_t nr = r1 - r0;
-    const size_t pbytes = nr * (size_t)N * 2;
     int rc;
-    for (size_t r = r0; r < r1; r++)
+    std::vector<uint64_t> rows(nr, 0);
+    std::vector<size_t> hostr;
+    for (size_t r = r0; r < r1; r++) {
+        const RegionH &R = B.rh[r];
+        if (R.hap_count > kEncMaxHaps) continue;
+        if (!R.memb_host && B.grouper && B.grouper->device() == ctx->device) rows[r - r0] = R.memb_dev;
+        else hostr.push_back(r);
+    }
+    for (size_t r : hostr)
         if ((rc = region_membership(B, B.rh[r]))) return rc;
-    if ((rc = ctx->enc_memb_host.reserve(pbytes))) return rc;
-    uint16_t *const pidx = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p);
-    std::vector<std::vector<uint16_t>> pab(nr);
-    std::vector<std::vector<uint32_t>> pcnt(nr);
+    const size_t Hp = ((size_t)H + 7) / 8 * 8;
+    if ((rc = ctx->enc_memb_host.reserve(std::max<size_t>(hostr.size(), 1) * Hp * 2)) ||
+        (rc = ctx->enc_memb.ensure(std::max<size_t>(hostr.size(), 1) * Hp)))
+        return rc;
     {
-        const uint32_t T = std::max(1u, std::min(ctx->host_threads, (uint32_t)nr));
-        std::atomic<size_t> next(r0);
+        uint16_t *const stage = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p);
+        const uint32_t T = std::max(1u, std::min(ctx->host_threads, (uint32_t)std::max<size_t>(hostr.size(), 1)));
+        std::atomic<size_t> next(0);
         auto work = [&]() {
-            std::vector<uint8_t> memb(H);
-            std::vector<uint16_t> slot(1u << 16, 0);  // pair -> index + 1 (reset after each region)
-            std::vector<uint32_t> seen((N + 31) / 32, 0);
-            for (size_t r; (r = next.fetch_add(1)) < r1;) {
-                const RegionH &R = B.rh[r];
-                if (R.hap_count > kEncMaxHaps) continue;
-                const uint8_t d = (uint8_t)(R.ref_local < 0 ? 0 : R.ref_local);
-                memset(memb.data(), d, H);
-                for (size_t i = 0; i < R.nonref_id.size(); i++) memb[R.nonref_id[i]] = (uint8_t)R.nonref_local[i];
-                std::vector<uint16_t> &ab = pab[r - r0];
-                std::vector<uint32_t> &cn = pcnt[r - r0];
-                ab.assign(1, (uint16_t)(d | (d << 8)));
-                cn.assign(1, N);
-                slot[ab[0]] = 1;
-                uint16_t *row = pidx + (r - r0) * (size_t)N;
-                std::fill(row, row + N, (uint16_t)0);
-                for (size_t i = 0; i < R.nonref_id.size() && ab.size() <= kEncMaxPairs; i++) {
-                    const uint32_t smp = R.nonref_id[i] >> 1;
-                    if (seen[smp >> 5] >> (smp & 31) & 1u) continue;
-                    seen[smp >> 5] |= 1u << (smp & 31);
-                    const uint16_t key = (uint16_t)(memb[2 * smp] | (memb[2 * smp + 1] << 8));
-                    uint16_t &sl = slot[key];
-                    if (!sl) {
-                        ab.push_back(key);
-                        cn.push_back(0);
-                        sl = (uint16_t)ab.size();
-                    }
-                    cn[0]--;
-                    cn[sl - 1]++;
-                    row[smp] = (uint16_t)(sl - 1);
-                }
-                for (uint16_t k : ab) slot[k] = 0;
-                for (size_t i = 0; i < R.nonref_id.size(); i++) seen[R.nonref_id[i] >> 6] = 0;
+            for (size_t k; (k = next.fetch_add(1)) < hostr.size();) {
+                const RegionH &R = B.rh[hostr[k]];
+                uint16_t *row = stage + k * Hp;
+                std::fill(row, row + H, (uint16_t)(R.ref_local < 0 ? 0 : R.ref_local));
+                for (size_t i = 0; i < R.nonref_id.size(); i++) row[R.nonref_id[i]] = (uint16_t)R.nonref_local[i];
             }
         };
         std::vector<std::thread> ts;
@@ -756,37 +738,37 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
         work();
         for (auto &t : ts) t.join();
     }
-    std::vector<uint32_t> pair_off(nr + 1, 0);
-    for (size_t i = 0; i < nr; i++) pair_off[i + 1] = pair_off[i] + (uint32_t)pab[i].size();
-    std::vector<uint16_t> pab_all(std::max<uint32_t>(pair_off[nr], 1));
-    std::vector<uint32_t> pcnt_all(pab_all.size());
-    for (size_t i = 0; i < nr; i++) {
-        std::copy(pab[i].begin(), pab[i].end(), pab_all.begin() + pair_off[i]);
-        std::copy(pcnt[i].begin(), pcnt[i].end(), pcnt_all.begin() + pair_off[i]);
-    }
-    // the keys to encode: varying keys of [r0, r1) whose region has <= 255 distinct
-    // haplotypes and <= kEncMaxPairs haplotype pairs (the others keep the host path)
+    if (!hostr.empty())
+        HIP_TRY(hipMemcpyAsync(ctx->enc_memb.p, ctx->enc_memb_host.p, hostr.size() * Hp * 2, hipMemcpyHostToDevice,
+                               ctx->stream));
+    for (size_t k = 0; k < hostr.size(); k++) rows[hostr[k] - r0] = (uint64_t)(uintptr_t)(ctx->enc_memb.p + k * Hp);
+    std::vector<uint32_t> pair_n(nr);
+    if ((rc = ctx->enc_rows.put(rows, ctx->stream)) || (rc = ctx->enc_pab.ensure(nr * kEncMaxPairs)) ||
+        (rc = ctx->enc_pcnt.ensure(nr * kEncMaxPairs)) || (rc = ctx->enc_pair_n.ensure(nr)) ||
+        (rc = ctx->enc_pidx.ensure(std::max<size_t>(nr * (size_t)N, 1))))
+        return rc;
+    if ((rc = launch_pair_table(ctx->enc_rows.p, (uint32_t)nr, N, ctx->enc_pab.p, ctx->enc_pcnt.p,
+                                ctx->enc_pair_n.p, ctx->enc_pidx.p, ctx->stream)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(pair_n.data(), ctx->enc_pair_n.p, nr * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    // the keys to encode: varying keys of [r0, r1) whose region's pairs were listed
+    // (<= kEncMaxHaps distinct haplotypes, <= kEncMaxPairs pairs; the others keep the host path)
     std::vector<DevVarKey> ek;
     for (uint32_t i = 0; i < B.var_keys.size(); i++) {
         const DevVarKey &k = B.var_keys[i];
-        if (k.region < r0 || k.region >= r1 || B.regions[k.region].hap_count > kEncMaxHaps ||
-            pab[k.region - r0].size() > kEncMaxPairs)
-            continue;
+        if (k.region < r0 || k.region >= r1 || pair_n[k.region - r0] == UINT32_MAX) continue;
         B.enc_idx[i] = (uint32_t)ek.size();
         ek.push_back(k);
     }
     const size_t nk = ek.size();
-    if ((rc = ctx->enc_pidx.ensure(std::max<size_t>(nr * (size_t)N, 1)))) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->enc_pidx.p, pidx, pbytes, hipMemcpyHostToDevice, ctx->stream));
-    if ((rc = ctx->enc_keys.put(ek, ctx->stream)) || (rc = ctx->enc_pab.put(pab_all, ctx->stream)) ||
-        (rc = ctx->enc_pcnt.put(pcnt_all, ctx->stream)) || (rc = ctx->enc_pair_off.put(pair_off, ctx->stream)) ||
-        (rc = ctx->enc_hdr.ensure(std::max<size_t>(nk, 1))) ||
+    if ((rc = ctx->enc_keys.put(ek, ctx->stream)) || (rc = ctx->enc_hdr.ensure(std::max<size_t>(nk, 1))) ||
         (rc = ctx->enc_vals.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
         (rc = ctx->enc_hist.ensure(std::max<size_t>(nk, 1) * (kEncMaxVals + 1))) ||
         (rc = ctx->enc_codes.ensure(std::max<size_t>(nk, 1) * N)))
         return rc;
     if ((rc = launch_key_encode(ctx->var_counts.p, ctx->enc_keys.p, (uint32_t)nk, ctx->enc_pab.p, ctx->enc_pcnt.p,
-                                ctx->enc_pair_off.p, ctx->enc_pidx.p, (uint32_t)r0, N, ctx->enc_hdr.p, ctx->enc_vals.p,
+                                ctx->enc_pair_n.p, ctx->enc_pidx.p, (uint32_t)r0, N, ctx->enc_hdr.p, ctx->enc_vals.p,
                                 ctx->enc_hist.p, ctx->enc_codes.p, ctx->stream)))
         return rc;
     B.enc_hdr.resize(nk);

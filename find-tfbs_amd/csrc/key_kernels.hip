@@ -405,13 +405,98 @@ __global__ __launch_bounds__(256) void spill_scatter_kernel(const uint32_t *__re
     }
 }
 
+// A region's distinct (left, right) haplotype pairs: sample s carries distinct
+// haplotypes (a, b) = (memb[2 s], memb[2 s + 1]) of its u16 membership row.  The
+// pairs (key a | b << 16) go into an LDS hash table with their sample counts
+// (one insert per wave for the lanes sharing lane 0's pair, which is most of
+// them: the reference group on both sides), are listed at r * kEncMaxPairs of
+// pab / pcnt in table order, and each sample gets its pair's index in pidx.
+// More than kEncMaxPairs pairs: pair_n[r] = UINT32_MAX (the host path).
+constexpr int kPairBlock = 512;
+constexpr uint32_t kPairSlots = 2 * kEncMaxPairs;
+constexpr uint32_t kPairEmpty = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t pair_slot(uint32_t key) { return (key * 0x9E3779B1u) >> (32 - 14); }
+static_assert(kPairSlots == 1u << 14, "pair_slot hashes into 2^14 slots");
+
+__global__ __launch_bounds__(kPairBlock) void pair_table_kernel(const uint64_t *__restrict__ rows, uint32_t n_samples,
+                                                                uint32_t *__restrict__ pab, uint32_t *__restrict__ pcnt,
+                                                                uint32_t *__restrict__ pair_n,
+                                                                uint16_t *__restrict__ pidx) {
+    __shared__ uint32_t s_key[kPairSlots];
+    __shared__ uint32_t s_val[kPairSlots];  // sample counts, then the pairs' indices
+    __shared__ uint32_t s_n, s_over, s_pos;
+    const uint32_t r = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const uint16_t *m = reinterpret_cast<const uint16_t *>(rows[r]);
+    if (!m) {
+        if (tid == 0) pair_n[r] = kPairEmpty;
+        return;
+    }
+    for (uint32_t t = tid; t < kPairSlots; t += kPairBlock) {
+        s_key[t] = kPairEmpty;
+        s_val[t] = 0;
+    }
+    if (tid == 0) {
+        s_n = 0;
+        s_over = 0;
+        s_pos = 0;
+    }
+    __syncthreads();
+    auto insert = [&](uint32_t key, uint32_t add) {
+        uint32_t sl = pair_slot(key);
+        while (!*(volatile uint32_t *)&s_over) {
+            const uint32_t old = atomicCAS(&s_key[sl], kPairEmpty, key);
+            if (old == kPairEmpty && atomicAdd(&s_n, 1u) >= kEncMaxPairs) atomicOr(&s_over, 1u);
+            if (old == kPairEmpty || old == key) {
+                atomicAdd(&s_val[sl], add);
+                return;
+            }
+            sl = (sl + 1) & (kPairSlots - 1);
+        }
+    };
+    for (uint32_t s0 = 0; s0 < n_samples; s0 += kPairBlock) {
+        const uint32_t s = s0 + tid;
+        const bool valid = s < n_samples;
+        const uint32_t key = valid ? (uint32_t)m[2 * s] | ((uint32_t)m[2 * s + 1] << 16) : kPairEmpty;
+        const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)key);
+        const unsigned long long same = __ballot(valid && key == k0);
+        if (valid && key == k0) {
+            if (lane == (uint32_t)__builtin_ctzll(same)) insert(k0, (uint32_t)__popcll(same));
+        } else if (valid) {
+            insert(key, 1u);
+        }
+    }
+    __syncthreads();
+    if (s_over) {
+        if (tid == 0) pair_n[r] = kPairEmpty;
+        return;
+    }
+    const size_t p0 = (size_t)r * kEncMaxPairs;
+    for (uint32_t t = tid; t < kPairSlots; t += kPairBlock)
+        if (s_key[t] != kPairEmpty) {
+            const uint32_t i = atomicAdd(&s_pos, 1u);
+            pab[p0 + i] = s_key[t];
+            pcnt[p0 + i] = s_val[t];
+            s_val[t] = i;
+        }
+    __syncthreads();
+    uint16_t *out = pidx + (size_t)r * n_samples;
+    for (uint32_t s = tid; s < n_samples; s += kPairBlock) {
+        const uint32_t key = (uint32_t)m[2 * s] | ((uint32_t)m[2 * s + 1] << 16);
+        uint32_t sl = pair_slot(key);
+        while (s_key[sl] != key) sl = (sl + 1) & (kPairSlots - 1);
+        out[s] = (uint16_t)s_val[sl];
+    }
+    if (tid == 0) pair_n[r] = s_n;
+}
+
 // counts_as_genotypes' per-sample half (main.rs:439-498) for one varying key.
 // A sample's total is C[a] + C[b] for its two haplotypes' distinct indices (a,
-// b); the host lists each region's distinct (a, b) pairs with their sample
-// counts and gives every sample its pair index (tfbs_batch_encode), so the key's
-// totals, min / max, distinct values (a bitmap of hi - lo + 1 bits), their
-// ranks and sample counts are computed over the P pairs, not the N samples (no
-// per-sample atomics); the one per-sample pass packs code[pair[s]].  The range
+// b); pair_table_kernel lists each region's distinct (a, b) pairs with their
+// sample counts and gives every sample its pair index, so the key's totals, min
+// / max, distinct values (a bitmap of hi - lo + 1 bits), their ranks and sample
+// counts are computed over the P pairs, not the N samples (no per-sample
+// atomics); the one per-sample pass packs code[pair[s]].  The range
 // multiplicity and the text stay on the host, which formats a row from the
 // value table and the codes (aggregate.cpp).
 constexpr int kEncBlock = 256;
@@ -420,9 +505,9 @@ constexpr uint32_t kEncWordsPerThread = kEncWords / kEncBlock;  // the rank scan
 
 __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const uint32_t *__restrict__ var_counts,
                                                                  const DevVarKey *__restrict__ keys,
-                                                                 const uint16_t *__restrict__ pab,
+                                                                 const uint32_t *__restrict__ pab,
                                                                  const uint32_t *__restrict__ pcnt,
-                                                                 const uint32_t *__restrict__ pair_off,
+                                                                 const uint32_t *__restrict__ pair_n,
                                                                  const uint16_t *__restrict__ pidx, uint32_t region0,
                                                                  uint32_t n_samples, EncHdr *__restrict__ hdr,
                                                                  uint32_t *__restrict__ vals,
@@ -437,16 +522,17 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const uint32_t *_
     const uint32_t k = blockIdx.x, tid = threadIdx.x;
     const DevVarKey vk = keys[k];
     const uint32_t r = vk.region - region0;
-    const uint32_t p0 = pair_off[r], P = pair_off[r + 1] - p0;
+    const size_t p0 = (size_t)r * kEncMaxPairs;
+    const uint32_t P = pair_n[r];
     // each pair's total (u32 wrapping, as the reference's additions) from the key's
     // distinct-haplotype counts (a region's U counts, cache-resident); the host
-    // sends only regions of <= 255 distinct haplotypes and <= kEncMaxPairs pairs
+    // sends only keys of regions with <= kEncMaxPairs pairs
     const uint32_t *cnt = var_counts + vk.out_off;
     uint32_t lo = UINT32_MAX, hi = 0;
     {
         for (uint32_t p = tid; p < P; p += kEncBlock) {
             const uint32_t ab = pab[p0 + p];
-            const uint32_t v = cnt[ab & 0xFF] + cnt[ab >> 8];
+            const uint32_t v = cnt[ab & 0xFFFFu] + cnt[ab >> 16];
             s_v[p] = v;
             if (pcnt[p0 + p] == 0) continue;  // the reference group's pair when every sample carries a variant
             lo = min(lo, v);
@@ -563,13 +649,23 @@ __global__ __launch_bounds__(256) void code_compact_kernel(const uint8_t *__rest
 
 }  // namespace
 
-int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint16_t *pab,
-                      const uint32_t *pcnt, const uint32_t *pair_off, const uint16_t *pidx, uint32_t region0,
+int launch_pair_table(const uint64_t *rows, uint32_t n_regions, uint32_t n_samples, uint32_t *pab, uint32_t *pcnt,
+                      uint32_t *pair_n, uint16_t *pidx, hipStream_t stream) {
+    if (n_regions == 0) return TFBS_OK;
+    hipLaunchKernelGGL(pair_table_kernel, dim3(n_regions), dim3(kPairBlock), 0, stream, rows, n_samples, pab, pcnt,
+                       pair_n, pidx);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("pair_table_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint32_t *pab,
+                      const uint32_t *pcnt, const uint32_t *pair_n, const uint16_t *pidx, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream) {
     if (n_keys == 0) return TFBS_OK;
     hipLaunchKernelGGL(key_encode_kernel, dim3(n_keys), dim3(kEncBlock), 0, stream, var_counts, keys, pab, pcnt,
-                       pair_off, pidx, region0, n_samples, hdr, vals, hist, codes);
+                       pair_n, pidx, region0, n_samples, hdr, vals, hist, codes);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_encode_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;

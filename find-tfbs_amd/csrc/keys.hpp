@@ -52,15 +52,19 @@ uint32_t key_asm_lds_counters();  // regions with more distinct haplotypes use A
 // .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters).
 int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spill, uint32_t n_regions, uint32_t *bcnt,
                          uint32_t *boff, uint32_t *sorted, hipStream_t stream);
+// A region's distinct haplotype pairs and each sample's pair (rows[r]: the device
+// address of region r's u16 membership row, 0 to skip it): pab / pcnt at
+// r * kEncMaxPairs, pair_n[r] (UINT32_MAX: skipped or too many pairs), pidx at r * n_samples.
+int launch_pair_table(const uint64_t *rows, uint32_t n_regions, uint32_t n_samples, uint32_t *pab, uint32_t *pcnt,
+                      uint32_t *pair_n, uint16_t *pidx, hipStream_t stream);
 // One workgroup per key: counts_as_genotypes' per-sample half over the
-// region's distinct haplotype pairs: pab[pair_off[r] + p] = a | b << 8 (the
-// distinct indices of a sample's two haplotypes), pcnt[..] the samples with that
-// pair, pidx (u16, one row of n_samples per region of the chunk, region -
-// region0) each sample's pair.  Writes hdr[k], vals[k *
+// region's distinct haplotype pairs (launch_pair_table's, region - region0):
+// pab = a | b << 16 (the distinct indices of a sample's two haplotypes), pcnt
+// the samples with that pair, pidx each sample's pair.  Writes hdr[k], vals[k *
 // 256 ..] (sorted distinct totals), hist[k * 256 ..] (samples per value) and
 // codes[k * n_samples ..].
-int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint16_t *pab,
-                      const uint32_t *pcnt, const uint32_t *pair_off, const uint16_t *pidx, uint32_t region0,
+int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_t n_keys, const uint32_t *pab,
+                      const uint32_t *pcnt, const uint32_t *pair_n, const uint16_t *pidx, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream);
 int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_samples, const uint64_t *off, uint8_t *dst,

@@ -183,7 +183,7 @@ struct EncHdr {
 };
 constexpr uint32_t kEncMaxVals = 255;       // u8 codes
 constexpr uint32_t kEncMaxRange = 1u << 16;  // value bitmap of hi - lo + 1 bits in LDS
-constexpr uint32_t kEncMaxHaps = 255;       // u8 membership: distinct haplotypes per region
+constexpr uint32_t kEncMaxHaps = 65535;     // u16 membership: distinct haplotypes per region
 constexpr uint32_t kEncMaxPairs = 8192;     // distinct (left, right) haplotype pairs per region (LDS)
 
 // One key (region, slot * n_inner + range) whose distinct-haplotype counts differ;

