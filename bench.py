@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="budget of each CPU baseline leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end leg (profiling passes)")
+    ap.add_argument("--host-build", action="store_true",
+                    help="reduce haplotypes to distinct ones on the host only (no device grouping)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for the timing reductions (gloo: rehearse several ranks on one GPU)")
     ap.add_argument("--shard", default="regions", choices=["regions", "regions_x_pwms"])
@@ -236,13 +238,15 @@ def shard_patterns(T, ps, part, parts):
     return ps if parts == 1 else ps.subset(lambda pid: pid % parts == part)
 
 
-def shard_batch(T, ps, args, rank, world=1, window_lmax=None):
+def shard_batch(T, ps, args, rank, world=1, window_lmax=None, build_device=None):
     """Rank r's share: its merged regions of the synthetic chromosome
-    (shard_plan), reduced to distinct haplotypes and packed on the host (with the
-    haplotype -> distinct membership the rows need); ps is the rank's pattern shard,
-    window_lmax the whole pattern set's L_max when it is a shard."""
+    (shard_plan), reduced to distinct haplotypes (grouped on build_device where the
+    region is SNV-only, else on the host) and packed (with the haplotype -> distinct
+    membership the rows need); ps is the rank's pattern shard, window_lmax the whole
+    pattern set's L_max when it is a shard."""
     first, count, _, _ = shard_plan(args, rank, world)
-    batch = T.RegionBatch(ps, args.samples, keep_membership=True, window_lmax=window_lmax)
+    batch = T.RegionBatch(ps, args.samples, keep_membership=True, window_lmax=window_lmax,
+                          build_device=build_device)
     batch.synth_fill(args.seed, first, count, args.indel_pct)
     return batch
 
@@ -315,7 +319,9 @@ def main():
 
     # ---- end-to-end leg, once: host prep, upload, scan, device key reduction, rows
     t_prep = time.perf_counter()
-    batch = shard_batch(T, ps, args, rank, world, window_lmax=ps_all.max_length if parts > 1 else None)
+    batch = shard_batch(T, ps, args, rank, world, window_lmax=ps_all.max_length if parts > 1 else None,
+                        build_device=None if args.host_build else local)
+    dev_regions, host_regions = batch.build_stats()
     t_prep = time.perf_counter() - t_prep
     gen_s, build_s, prep_wall, fill_s = batch.prep_seconds()  # prep_wall: build_region + commit, no generation
     t_up = time.perf_counter()
@@ -475,8 +481,9 @@ def main():
                 "regions_per_s": tot_regions / e2e_max,
                 "windows_per_s": tot_windows / e2e_max,
                 "seconds": e2e_max,
-                "note": "one pass over the rank's batch: host prep (load_diffs/group/patch/dedup/pack on %d "
-                        "threads; the synthetic records are generated before, as for the CPU baseline) + upload "
+                "note": "one pass over the rank's batch: haplotype reconstruction (load_diffs/group on the GPU "
+                        "for SNV-only regions, else on the host; patch/dedup/pack on %d host threads; the "
+                        "synthetic records are generated before, as for the CPU baseline) + upload "
                         "+ scan + device key reduction + device "
                         "per-sample encoding + the VCF rows as BGZF blocks made on the GPU and written out (%d rows, "
                         "%.3g bytes of text deflated to %.3g bytes, to /dev/null)" % (
@@ -488,6 +495,8 @@ def main():
                                    "upload": t_up, "scan": t_scan1, "key_reduce": t_red,
                                    "device_encode": t_enc, "rows_bgzf": t_rows},
                 "rows": int(tot_rows),
+                "regions_grouped_on_device": int(dev_regions),
+                "regions_built_on_host": int(host_regions),
             },
             "kernel_ms_avg": kms,
             "dense_download_s": t_dense,

@@ -27,6 +27,9 @@ namespace {
 constexpr int kBgBlock = 256;
 constexpr uint32_t kBgPer = (kBgzfRaw + kBgBlock - 1) / kBgBlock;  // bytes per thread
 constexpr uint32_t kBgWords = (kBgzfMax - 26) / 4;                  // deflate data words a block can hold
+// the LDS bit buffer: blocks that compress to at most half are deflated (32 KiB,
+// two workgroups per CU), the others stored
+constexpr uint32_t kBitWords = kBgWords / 2;
 constexpr uint32_t kLookback = 8;                                   // sample texts searched for a match
 
 __constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
@@ -70,9 +73,39 @@ struct BitOut {
     }
 };
 
+// What a block stages in LDS (bgzf_block_kernel's setup): for up to kStRows
+// rows with genotype text in the block, the token lengths and texts, the group
+// offsets (cum) of the 64-sample groups the block touches and the packed codes
+// of their samples.  Everything else (more rows: rows of a few samples) is read
+// from global memory.
+constexpr uint32_t kStRows = 8;
+constexpr uint32_t kStCodes = 16896;  // >= the codes of 65280 bytes of 4-byte sample texts + 2 groups per row
+constexpr uint32_t kStTok = 512;      // token slots (kRowTokBytes of text each)
+constexpr uint32_t kStCum = 512;
+
+struct StRow {
+    uint32_t row;          // row index
+    uint32_t s_lo, s_hi;   // samples whose codes are staged
+    uint32_t cfirst;       // the row's code byte of sample s_lo (s_lo * width / 8)
+    uint32_t code_at;      // its place in Stage::codes
+    uint32_t tok_at;       // Stage::tlen / text slot of token 0
+    uint32_t g_lo, ncum;   // cum entries [g_lo, g_lo + ncum) at cum_at
+    uint32_t cum_at;
+};
+
+struct Stage {
+    uint32_t n;
+    StRow r[kStRows];
+    uint8_t codes[kStCodes];
+    uint8_t tlen[kStTok];
+    uint8_t text[kStTok * kRowTokBytes];
+    uint32_t cum[kStCum];
+};
+
 struct Ctx {
     const BgArgs &A;
-    uint64_t b0;  // block start in the stream
+    uint64_t b0;
+    const Stage &S;
     __device__ uint32_t find_row(uint64_t p) const {  // the last row starting at or before p
         uint32_t lo = 0, hi = A.n_rows - 1;
         while (lo < hi) {
@@ -82,29 +115,54 @@ struct Ctx {
         }
         return lo;
     }
-    __device__ uint32_t code(const DevRow &R, uint32_t s) const {
-        const uint32_t bit = s * R.width;
-        return (A.codes[R.code_off + (bit >> 3)] >> (bit & 7)) & ((1u << R.width) - 1u);
+    __device__ int slot(uint32_t r) const {
+        for (uint32_t k = 0; k < S.n; k++)
+            if (S.r[k].row == r) return (int)k;
+        return -1;
     }
-    __device__ uint32_t tlen(const DevRow &R, uint32_t c) const { return A.tok_len[R.tok + c]; }
-    __device__ uint8_t tbyte(const DevRow &R, uint32_t c, uint32_t o) const {
-        return (uint8_t)A.tok_text[(size_t)(R.tok + c) * kRowTokBytes + o];
+    __device__ uint32_t code(const DevRow &R, int k, uint32_t s) const {
+        const uint32_t bit = s * R.width;
+        uint32_t b;
+        if (k >= 0 && s >= S.r[k].s_lo && s < S.r[k].s_hi) b = S.codes[S.r[k].code_at + (bit >> 3) - S.r[k].cfirst];
+        else b = A.codes[R.code_off + (bit >> 3)];
+        return (b >> (bit & 7)) & ((1u << R.width) - 1u);
+    }
+    __device__ uint32_t tlen(const DevRow &R, int k, uint32_t c) const {
+        return k >= 0 ? S.tlen[S.r[k].tok_at + c] : A.tok_len[R.tok + c];
+    }
+    __device__ uint8_t tbyte(const DevRow &R, int k, uint32_t c, uint32_t o) const {
+        return k >= 0 ? S.text[(S.r[k].tok_at + c) * kRowTokBytes + o]
+                      : (uint8_t)A.tok_text[(size_t)(R.tok + c) * kRowTokBytes + o];
     }
     // sample s and offset o of byte g of the row's genotype text
-    __device__ void locate(const DevRow &R, uint64_t g, uint32_t &s, uint32_t &o) const {
+    __device__ void locate(const DevRow &R, int k, uint64_t g, uint32_t &s, uint32_t &o) const {
+        uint32_t q, pos;
         const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
-        const uint32_t *cum = A.cum + R.cum_off;
-        uint32_t lo = 0, hi = ng - 1;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) / 2;
-            if (cum[mid] <= g) lo = mid;
-            else hi = mid - 1;
+        if (k >= 0 && g >= S.cum[S.r[k].cum_at] && g < S.cum[S.r[k].cum_at + S.r[k].ncum - 1]) {
+            const uint32_t *cum = S.cum + S.r[k].cum_at;  // staged groups
+            uint32_t lo = 0, hi = S.r[k].ncum - 2;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (cum[mid] <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            q = S.r[k].g_lo + lo;
+            pos = cum[lo];
+        } else {
+            const uint32_t *cum = A.cum + R.cum_off;
+            uint32_t lo = 0, hi = ng - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (cum[mid] <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            q = lo;
+            pos = cum[lo];
         }
-        uint64_t pos = cum[lo];
-        s = lo * kCumGroup;
+        s = q * kCumGroup;
         for (; s + 1 < A.n_samples; s++) {  // bounded: g lies inside the row's genotype text
-            const uint32_t t = tlen(R, code(R, s));
-            if (g < pos + t) break;
+            const uint32_t t = tlen(R, k, code(R, k, s));
+            if (g < (uint64_t)pos + t) break;
             pos += t;
         }
         o = (uint32_t)(g - pos);
@@ -117,6 +175,7 @@ struct Ctx {
         while (p < e) {
             while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
             const DevRow R = A.rows[r];
+            const int k = slot(r);
             const uint64_t local = p - R.text_off;
             if (local < R.head_len) {
                 const uint64_t n = min((uint64_t)R.head_len - local, e - p);
@@ -131,11 +190,11 @@ struct Ctx {
                 continue;
             }
             uint32_t s, o;
-            locate(R, g, s, o);
+            locate(R, k, g, s, o);
             while (p < e && g < R.geno_len) {
-                const uint32_t c = code(R, s), t = tlen(R, c);
+                const uint32_t c = code(R, k, s), t = tlen(R, k, c);
                 const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
-                for (uint32_t i = 0; i < n; i++) f(tbyte(R, c, o + i));
+                for (uint32_t i = 0; i < n; i++) f(tbyte(R, k, c, o + i));
                 p += n;
                 g += n;
                 o += n;
@@ -153,6 +212,7 @@ struct Ctx {
         while (p < e) {
             while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
             const DevRow R = A.rows[r];
+            const int k = slot(r);
             const uint64_t local = p - R.text_off;
             if (local < R.head_len) {
                 const uint64_t n = min((uint64_t)R.head_len - local, e - p);
@@ -167,15 +227,15 @@ struct Ctx {
                 continue;
             }
             uint32_t s, o;
-            locate(R, g, s, o);
+            locate(R, k, g, s, o);
             while (p < e && g < R.geno_len) {
-                const uint32_t c = code(R, s), t = tlen(R, c);
+                const uint32_t c = code(R, k, s), t = tlen(R, k, c);
                 const uint64_t tok0 = p - o;  // this sample text's first byte
-                if (s > 0 && code(R, s - 1) == c && tok0 >= b0 + t) {
+                if (s > 0 && code(R, k, s - 1) == c && tok0 >= b0 + t) {
                     // a run: every byte equals the one t before it, to the run's end
                     uint64_t end = tok0 + t;
                     uint32_t s2 = s + 1;
-                    while (end < e && s2 < A.n_samples && code(R, s2) == c) {
+                    while (end < e && s2 < A.n_samples && code(R, k, s2) == c) {
                         end += t;
                         s2++;
                     }
@@ -183,7 +243,7 @@ struct Ctx {
                     uint32_t left = (uint32_t)(end - p), oo = o;
                     while (left) {
                         if (left < 3) {  // too short for a match: literals
-                            out.lit(tbyte(R, c, oo));
+                            out.lit(tbyte(R, k, c, oo));
                             oo = (oo + 1) % t;
                             left--;
                             continue;
@@ -203,9 +263,9 @@ struct Ctx {
                 }
                 const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
                 uint32_t dist = 0, acc = 0;
-                for (uint32_t k = 1; k <= kLookback && k <= s; k++) {  // the same text among the samples before
-                    const uint32_t cc = code(R, s - k);
-                    acc += tlen(R, cc);
+                for (uint32_t kk = 1; kk <= kLookback && kk <= s; kk++) {  // the same text among the samples before
+                    const uint32_t cc = code(R, k, s - kk);
+                    acc += tlen(R, k, cc);
                     if (tok0 < b0 + acc) break;
                     if (cc == c) {
                         dist = acc;
@@ -215,7 +275,7 @@ struct Ctx {
                 if (dist && n >= 3) {
                     out.match(n, dist);
                 } else {
-                    for (uint32_t i = 0; i < n; i++) out.lit(tbyte(R, c, o + i));
+                    for (uint32_t i = 0; i < n; i++) out.lit(tbyte(R, k, c, o + i));
                 }
                 p += n;
                 g += n;
@@ -228,6 +288,58 @@ struct Ctx {
         }
     }
 };
+
+// The block's setup: which rows to stage and where (one thread), then the copies.
+__device__ void stage_block(const BgArgs &A, uint64_t b0, uint64_t e, Stage &S) {
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        const Ctx C{A, b0, S};
+        const uint32_t r_first = C.find_row(b0), r_last = C.find_row(e - 1);
+        const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
+        uint32_t n = 0, code_used = 0, tok_used = 0, cum_used = 0;
+        auto group_of = [&](const DevRow &R, uint64_t g) {  // the group holding genotype byte g
+            const uint32_t *cum = A.cum + R.cum_off;
+            uint32_t lo = 0, hi = ng - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (cum[mid] <= g) lo = mid;
+                else hi = mid - 1;
+            }
+            return lo;
+        };
+        for (uint32_t r = r_first; r <= r_last && n < kStRows; r++) {
+            const DevRow R = A.rows[r];
+            if (!R.width) continue;
+            const uint64_t gs = R.text_off + R.head_len, ge = gs + R.geno_len;
+            const uint64_t lo = max(b0, gs), hi = min(e, ge);
+            if (lo >= hi) continue;
+            const uint32_t g_lo = lo == gs ? 0 : group_of(R, lo - gs);
+            const uint32_t g_hi = hi == ge ? ng - 1 : group_of(R, hi - 1 - gs);
+            const uint32_t s_lo = g_lo * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
+            const uint32_t cb0 = s_lo * R.width / 8, cb1 = (s_hi * R.width + 7) / 8;
+            const uint32_t ncum = g_hi - g_lo + 2;
+            if (code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok || cum_used + ncum > kStCum) break;
+            S.r[n] = StRow{r, s_lo, s_hi, cb0, code_used, tok_used, g_lo, ncum, cum_used};
+            code_used += cb1 - cb0;
+            tok_used += R.nv;
+            cum_used += ncum;
+            n++;
+        }
+        S.n = n;
+    }
+    __syncthreads();
+    for (uint32_t k = 0; k < S.n; k++) {
+        const StRow &T = S.r[k];
+        const DevRow R = A.rows[T.row];
+        const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
+        for (uint32_t i = tid; i < nb; i += blockDim.x) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
+        for (uint32_t i = tid; i < R.nv; i += blockDim.x) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
+        for (uint32_t i = tid; i < R.nv * kRowTokBytes; i += blockDim.x)
+            S.text[T.tok_at * kRowTokBytes + i] = (uint8_t)A.tok_text[(size_t)R.tok * kRowTokBytes + i];
+        for (uint32_t i = tid; i < T.ncum; i += blockDim.x) S.cum[T.cum_at + i] = A.cum[R.cum_off + T.g_lo + i];
+    }
+    __syncthreads();
+}
 
 // x^(8 n) applied to a CRC register: the operators of 2^k bytes, k < 32
 __device__ __forceinline__ uint32_t crc_shift(const uint32_t *ops, uint32_t v, uint64_t n) {
@@ -252,14 +364,18 @@ __global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
     if (!R.width) return;
     const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
     uint32_t *cum = A.cum + R.cum_off;
-    Ctx C{A, 0};
     const uint32_t per = 8 / R.width, mask = (1u << R.width) - 1u;
+    auto tlen = [&](uint32_t c) { return (uint32_t)A.tok_len[R.tok + c]; };
+    auto code = [&](uint32_t s) {
+        const uint32_t bit = s * R.width;
+        return (A.codes[R.code_off + (bit >> 3)] >> (bit & 7)) & mask;
+    };
     {
         const uint32_t v = threadIdx.x;
         uint32_t n = 0;
         for (uint32_t k = 0; k < per; k++) {
             const uint32_t c = (v >> (k * R.width)) & mask;
-            if (c < R.nv) n += C.tlen(R, c);  // (other codes never occur)
+            if (c < R.nv) n += tlen(c);  // (other codes never occur)
         }
         s_blen[v] = (uint16_t)n;
     }
@@ -273,7 +389,7 @@ __global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
             const uint8_t *b = A.codes + R.code_off + (size_t)q * gbytes;
             for (uint32_t i = 0; i < gbytes; i++) sum += s_blen[b[i]];
         } else if (q < ng) {  // the last, partial group: sample by sample
-            for (uint32_t s = q * kCumGroup; s < A.n_samples; s++) sum += C.tlen(R, C.code(R, s));
+            for (uint32_t s = q * kCumGroup; s < A.n_samples; s++) sum += tlen(code(s));
         }
         s_scan[threadIdx.x] = sum;
         __syncthreads();
@@ -291,18 +407,19 @@ __global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
 }
 
 __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
-    __shared__ uint32_t s_bits[kBgWords + 1];
+    __shared__ uint32_t s_bits[kBitWords + 1];
     __shared__ uint32_t s_crc_tab[256];
     __shared__ uint32_t s_scan[kBgBlock];
     __shared__ uint32_t s_crc[kBgBlock];
+    __shared__ Stage S;
     const uint32_t tid = threadIdx.x;
     const uint64_t blk = A.block0 + blockIdx.x;
     const uint64_t b0 = blk * kBgzfRaw;
     const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
     for (uint32_t i = tid; i < 256; i += kBgBlock) s_crc_tab[i] = A.crc_tab[i];
-    for (uint32_t i = tid; i <= kBgWords; i += kBgBlock) s_bits[i] = 0;
-    __syncthreads();
-    const Ctx C{A, b0};
+    for (uint32_t i = tid; i <= kBitWords; i += kBgBlock) s_bits[i] = 0;
+    stage_block(A, b0, b0 + n, S);
+    const Ctx C{A, b0, S};
     const uint64_t p = b0 + min(n, tid * kBgPer), e = b0 + min(n, (tid + 1) * kBgPer);
     // CRC32 (reflected 0xEDB88320, zero start) of the thread's bytes, shifted to the block end
     uint32_t crc = 0;
@@ -321,7 +438,7 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     }
     const uint32_t total_bits = 3 + s_scan[kBgBlock - 1] + 7;  // BFINAL + BTYPE, symbols, end of block
     const uint32_t dbytes = (total_bits + 7) / 8;
-    const bool stored = dbytes > 4 * kBgWords;
+    const bool stored = dbytes > 4 * kBitWords;  // (also when deflate would not fit the BGZF block)
     if (!stored) {  // pass 2: the bits at their offsets
         if (tid == 0) s_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
         __syncthreads();
