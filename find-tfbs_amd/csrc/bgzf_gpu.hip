@@ -73,15 +73,18 @@ struct BitOut {
     }
 };
 
-// What a block stages in LDS (bgzf_block_kernel's setup): for up to kStRows
-// rows with genotype text in the block, the token lengths and texts, the group
-// offsets (cum) of the 64-sample groups the block touches and the packed codes
-// of their samples.  Everything else (more rows: rows of a few samples) is read
-// from global memory.
+// What a block stages in LDS: the descriptors of its first kStRowDesc rows,
+// and for up to kStRows rows with genotype text in the block their token
+// lengths and texts, the group offsets (cum) of the 64-sample groups the block
+// touches and those samples' packed codes.  bgzf_plan_kernel chooses them (one
+// thread per block, so the binary searches of many blocks overlap); anything
+// else (rows of a few samples) is read from global memory.
 constexpr uint32_t kStRows = 8;
+constexpr uint32_t kStRowDesc = 96;
 constexpr uint32_t kStCodes = 16896;  // >= the codes of 65280 bytes of 4-byte sample texts + 2 groups per row
 constexpr uint32_t kStTok = 512;      // token slots (kRowTokBytes of text each)
 constexpr uint32_t kStCum = 512;
+constexpr uint32_t kCrcOps = 16;      // shift operators of 2^k bytes, k < 16 (shifts below 64 KiB)
 
 struct StRow {
     uint32_t row;          // row index
@@ -93,60 +96,96 @@ struct StRow {
     uint32_t cum_at;
 };
 
+struct BlockPlan {
+    uint32_t r_first, n_rows;  // the rows overlapping the block
+    uint32_t n_st, pad;
+    StRow st[kStRows];
+};
+
 struct Stage {
-    uint32_t n;
-    StRow r[kStRows];
+    BlockPlan P;
+    DevRow rows[kStRowDesc];  // rows r_first ..
     uint8_t codes[kStCodes];
     uint8_t tlen[kStTok];
     uint8_t text[kStTok * kRowTokBytes];
     uint32_t cum[kStCum];
+    uint32_t crc_tab[256];
+    uint32_t crc_ops[kCrcOps * 32];
 };
+
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t *tab, uint32_t crc, uint32_t b) {
+    return tab[(crc ^ b) & 0xFFu] ^ (crc >> 8);
+}
+
+// x^(8 n) applied to a CRC register (n < 2^kCrcOps)
+__device__ __forceinline__ uint32_t crc_shift_lds(const uint32_t *ops, uint32_t v, uint32_t n) {
+    for (uint32_t k = 0; n; k++, n >>= 1) {
+        if (!(n & 1)) continue;
+        const uint32_t *M = ops + 32 * k;
+        uint32_t r = 0;
+        for (uint32_t i = 0; i < 32; i++) r ^= ((v >> i) & 1u) ? M[i] : 0u;
+        v = r;
+    }
+    return v;
+}
 
 struct Ctx {
     const BgArgs &A;
     uint64_t b0;
     const Stage &S;
-    __device__ uint32_t find_row(uint64_t p) const {  // the last row starting at or before p
-        uint32_t lo = 0, hi = A.n_rows - 1;
+    __device__ DevRow row(uint32_t r) const {
+        const uint32_t d = r - S.P.r_first;
+        return d < min(S.P.n_rows, kStRowDesc) ? S.rows[d] : A.rows[r];
+    }
+    __device__ uint64_t row_off(uint32_t r) const {
+        const uint32_t d = r - S.P.r_first;
+        return d < min(S.P.n_rows, kStRowDesc) ? S.rows[d].text_off : A.rows[r].text_off;
+    }
+    // the last row starting at or before p (p inside the block)
+    __device__ uint32_t find_row(uint64_t p) const {
+        uint32_t lo = S.P.r_first, hi = S.P.r_first + S.P.n_rows - 1;
         while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) / 2;
-            if (A.rows[mid].text_off <= p) lo = mid;
+            if (row_off(mid) <= p) lo = mid;
             else hi = mid - 1;
         }
         return lo;
     }
     __device__ int slot(uint32_t r) const {
-        for (uint32_t k = 0; k < S.n; k++)
-            if (S.r[k].row == r) return (int)k;
+        for (uint32_t k = 0; k < S.P.n_st; k++)
+            if (S.P.st[k].row == r) return (int)k;
         return -1;
     }
     __device__ uint32_t code(const DevRow &R, int k, uint32_t s) const {
         const uint32_t bit = s * R.width;
         uint32_t b;
-        if (k >= 0 && s >= S.r[k].s_lo && s < S.r[k].s_hi) b = S.codes[S.r[k].code_at + (bit >> 3) - S.r[k].cfirst];
-        else b = A.codes[R.code_off + (bit >> 3)];
+        if (k >= 0 && s >= S.P.st[k].s_lo && s < S.P.st[k].s_hi)
+            b = S.codes[S.P.st[k].code_at + (bit >> 3) - S.P.st[k].cfirst];
+        else
+            b = A.codes[R.code_off + (bit >> 3)];
         return (b >> (bit & 7)) & ((1u << R.width) - 1u);
     }
     __device__ uint32_t tlen(const DevRow &R, int k, uint32_t c) const {
-        return k >= 0 ? S.tlen[S.r[k].tok_at + c] : A.tok_len[R.tok + c];
+        return k >= 0 ? S.tlen[S.P.st[k].tok_at + c] : A.tok_len[R.tok + c];
     }
     __device__ uint8_t tbyte(const DevRow &R, int k, uint32_t c, uint32_t o) const {
-        return k >= 0 ? S.text[(S.r[k].tok_at + c) * kRowTokBytes + o]
+        return k >= 0 ? S.text[(S.P.st[k].tok_at + c) * kRowTokBytes + o]
                       : (uint8_t)A.tok_text[(size_t)(R.tok + c) * kRowTokBytes + o];
     }
     // sample s and offset o of byte g of the row's genotype text
     __device__ void locate(const DevRow &R, int k, uint64_t g, uint32_t &s, uint32_t &o) const {
         uint32_t q, pos;
         const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
-        if (k >= 0 && g >= S.cum[S.r[k].cum_at] && g < S.cum[S.r[k].cum_at + S.r[k].ncum - 1]) {
-            const uint32_t *cum = S.cum + S.r[k].cum_at;  // staged groups
-            uint32_t lo = 0, hi = S.r[k].ncum - 2;
+        const StRow *T = k >= 0 ? &S.P.st[k] : nullptr;
+        if (T && g >= S.cum[T->cum_at] && g < S.cum[T->cum_at + T->ncum - 1]) {
+            const uint32_t *cum = S.cum + T->cum_at;  // the staged groups
+            uint32_t lo = 0, hi = T->ncum - 2;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) / 2;
                 if (cum[mid] <= g) lo = mid;
                 else hi = mid - 1;
             }
-            q = S.r[k].g_lo + lo;
+            q = T->g_lo + lo;
             pos = cum[lo];
         } else {
             const uint32_t *cum = A.cum + R.cum_off;
@@ -173,8 +212,8 @@ struct Ctx {
         if (p >= e) return;
         uint32_t r = find_row(p);
         while (p < e) {
-            while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
-            const DevRow R = A.rows[r];
+            while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
+            const DevRow R = row(r);
             const int k = slot(r);
             const uint64_t local = p - R.text_off;
             if (local < R.head_len) {
@@ -205,24 +244,30 @@ struct Ctx {
             }
         }
     }
-    // the deflate symbols of [p, e) into out
-    __device__ void encode(uint64_t p, uint64_t e, BitOut &out) const {
+    // the deflate symbols of [p, e) into out; with crc, every byte into *crc too
+    template <bool kCrc>
+    __device__ void encode(uint64_t p, uint64_t e, BitOut &out, uint32_t *crc) const {
         if (p >= e) return;
         uint32_t r = find_row(p);
         while (p < e) {
-            while (r + 1 < A.n_rows && A.rows[r + 1].text_off <= p) r++;
-            const DevRow R = A.rows[r];
+            while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
+            const DevRow R = row(r);
             const int k = slot(r);
             const uint64_t local = p - R.text_off;
             if (local < R.head_len) {
                 const uint64_t n = min((uint64_t)R.head_len - local, e - p);
-                for (uint64_t i = 0; i < n; i++) out.lit((uint8_t)A.heads[R.head_off + local + i]);
+                for (uint64_t i = 0; i < n; i++) {
+                    const uint32_t b = (uint8_t)A.heads[R.head_off + local + i];
+                    out.lit(b);
+                    if (kCrc) *crc = crc_byte(S.crc_tab, *crc, b);
+                }
                 p += n;
                 continue;
             }
             uint64_t g = local - R.head_len;
             if (g >= R.geno_len) {
                 out.lit('\n');
+                if (kCrc) *crc = crc_byte(S.crc_tab, *crc, '\n');
                 p++;
                 continue;
             }
@@ -241,6 +286,14 @@ struct Ctx {
                     }
                     end = min(end, e);
                     uint32_t left = (uint32_t)(end - p), oo = o;
+                    if (kCrc) {
+                        uint32_t x = *crc;
+                        for (uint32_t i = 0, q = o; i < left; i++) {
+                            x = crc_byte(S.crc_tab, x, tbyte(R, k, c, q));
+                            q = q + 1 == t ? 0 : q + 1;
+                        }
+                        *crc = x;
+                    }
                     while (left) {
                         if (left < 3) {  // too short for a match: literals
                             out.lit(tbyte(R, k, c, oo));
@@ -274,8 +327,14 @@ struct Ctx {
                 }
                 if (dist && n >= 3) {
                     out.match(n, dist);
+                    if (kCrc)
+                        for (uint32_t i = 0; i < n; i++) *crc = crc_byte(S.crc_tab, *crc, tbyte(R, k, c, o + i));
                 } else {
-                    for (uint32_t i = 0; i < n; i++) out.lit(tbyte(R, k, c, o + i));
+                    for (uint32_t i = 0; i < n; i++) {
+                        const uint32_t b = tbyte(R, k, c, o + i);
+                        out.lit(b);
+                        if (kCrc) *crc = crc_byte(S.crc_tab, *crc, b);
+                    }
                 }
                 p += n;
                 g += n;
@@ -288,71 +347,6 @@ struct Ctx {
         }
     }
 };
-
-// The block's setup: which rows to stage and where (one thread), then the copies.
-__device__ void stage_block(const BgArgs &A, uint64_t b0, uint64_t e, Stage &S) {
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) {
-        const Ctx C{A, b0, S};
-        const uint32_t r_first = C.find_row(b0), r_last = C.find_row(e - 1);
-        const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
-        uint32_t n = 0, code_used = 0, tok_used = 0, cum_used = 0;
-        auto group_of = [&](const DevRow &R, uint64_t g) {  // the group holding genotype byte g
-            const uint32_t *cum = A.cum + R.cum_off;
-            uint32_t lo = 0, hi = ng - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) / 2;
-                if (cum[mid] <= g) lo = mid;
-                else hi = mid - 1;
-            }
-            return lo;
-        };
-        for (uint32_t r = r_first; r <= r_last && n < kStRows; r++) {
-            const DevRow R = A.rows[r];
-            if (!R.width) continue;
-            const uint64_t gs = R.text_off + R.head_len, ge = gs + R.geno_len;
-            const uint64_t lo = max(b0, gs), hi = min(e, ge);
-            if (lo >= hi) continue;
-            const uint32_t g_lo = lo == gs ? 0 : group_of(R, lo - gs);
-            const uint32_t g_hi = hi == ge ? ng - 1 : group_of(R, hi - 1 - gs);
-            const uint32_t s_lo = g_lo * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
-            const uint32_t cb0 = s_lo * R.width / 8, cb1 = (s_hi * R.width + 7) / 8;
-            const uint32_t ncum = g_hi - g_lo + 2;
-            if (code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok || cum_used + ncum > kStCum) break;
-            S.r[n] = StRow{r, s_lo, s_hi, cb0, code_used, tok_used, g_lo, ncum, cum_used};
-            code_used += cb1 - cb0;
-            tok_used += R.nv;
-            cum_used += ncum;
-            n++;
-        }
-        S.n = n;
-    }
-    __syncthreads();
-    for (uint32_t k = 0; k < S.n; k++) {
-        const StRow &T = S.r[k];
-        const DevRow R = A.rows[T.row];
-        const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
-        for (uint32_t i = tid; i < nb; i += blockDim.x) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
-        for (uint32_t i = tid; i < R.nv; i += blockDim.x) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
-        for (uint32_t i = tid; i < R.nv * kRowTokBytes; i += blockDim.x)
-            S.text[T.tok_at * kRowTokBytes + i] = (uint8_t)A.tok_text[(size_t)R.tok * kRowTokBytes + i];
-        for (uint32_t i = tid; i < T.ncum; i += blockDim.x) S.cum[T.cum_at + i] = A.cum[R.cum_off + T.g_lo + i];
-    }
-    __syncthreads();
-}
-
-// x^(8 n) applied to a CRC register: the operators of 2^k bytes, k < 32
-__device__ __forceinline__ uint32_t crc_shift(const uint32_t *ops, uint32_t v, uint64_t n) {
-    for (uint32_t k = 0; n; k++, n >>= 1) {
-        if (!(n & 1)) continue;
-        const uint32_t *M = ops + 32 * k;
-        uint32_t r = 0;
-        for (uint32_t i = 0; i < 32; i++)
-            if ((v >> i) & 1u) r ^= M[i];
-        v = r;
-    }
-    return v;
-}
 
 // Row r's genotype text offsets of samples 0, 64, 128, ... (and its end): the
 // packed codes a byte at a time through a table of the byte's summed text lengths.
@@ -406,9 +400,62 @@ __global__ __launch_bounds__(256) void row_cum_kernel(BgArgs A) {
     if (threadIdx.x == 0) cum[ng] = carry;
 }
 
+// One thread per block of a launch: the rows overlapping it and which of their
+// token tables, group offsets and codes it stages (Stage).
+__global__ __launch_bounds__(256) void bgzf_plan_kernel(BgArgs A, uint32_t n_blocks) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n_blocks) return;
+    const uint64_t b0 = (A.block0 + i) * kBgzfRaw;
+    const uint64_t e = b0 + min((uint64_t)kBgzfRaw, A.text_bytes - b0);
+    auto find_row = [&](uint64_t p) {
+        uint32_t lo = 0, hi = A.n_rows - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (A.rows[mid].text_off <= p) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    BlockPlan P{};
+    P.r_first = find_row(b0);
+    const uint32_t r_last = find_row(e - 1);
+    P.n_rows = r_last - P.r_first + 1;
+    const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
+    auto group_of = [&](const DevRow &R, uint64_t g) {  // the group holding genotype byte g
+        const uint32_t *cum = A.cum + R.cum_off;
+        uint32_t lo = 0, hi = ng - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) / 2;
+            if (cum[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        return lo;
+    };
+    uint32_t n = 0, code_used = 0, tok_used = 0, cum_used = 0;
+    for (uint32_t r = P.r_first; r <= r_last && n < kStRows; r++) {
+        const DevRow R = A.rows[r];
+        if (!R.width) continue;
+        const uint64_t gs = R.text_off + R.head_len, ge = gs + R.geno_len;
+        const uint64_t lo = max(b0, gs), hi = min(e, ge);
+        if (lo >= hi) continue;
+        const uint32_t g_lo = lo == gs ? 0 : group_of(R, lo - gs);
+        const uint32_t g_hi = hi == ge ? ng - 1 : group_of(R, hi - 1 - gs);
+        const uint32_t s_lo = g_lo * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
+        const uint32_t cb0 = s_lo * R.width / 8, cb1 = (s_hi * R.width + 7) / 8;
+        const uint32_t ncum = g_hi - g_lo + 2;
+        if (code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok || cum_used + ncum > kStCum) break;
+        P.st[n] = StRow{r, s_lo, s_hi, cb0, code_used, tok_used, g_lo, ncum, cum_used};
+        code_used += cb1 - cb0;
+        tok_used += R.nv;
+        cum_used += ncum;
+        n++;
+    }
+    P.n_st = n;
+    reinterpret_cast<BlockPlan *>(A.plans)[i] = P;
+}
+
 __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     __shared__ uint32_t s_bits[kBitWords + 1];
-    __shared__ uint32_t s_crc_tab[256];
     __shared__ uint32_t s_scan[kBgBlock];
     __shared__ uint32_t s_crc[kBgBlock];
     __shared__ Stage S;
@@ -416,18 +463,39 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     const uint64_t blk = A.block0 + blockIdx.x;
     const uint64_t b0 = blk * kBgzfRaw;
     const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
-    for (uint32_t i = tid; i < 256; i += kBgBlock) s_crc_tab[i] = A.crc_tab[i];
-    for (uint32_t i = tid; i <= kBitWords; i += kBgBlock) s_bits[i] = 0;
-    stage_block(A, b0, b0 + n, S);
+    // the block's plan, rows, token tables, group offsets and codes into LDS
+    {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const BlockPlan *>(A.plans) + blockIdx.x);
+        for (uint32_t i = tid; i < sizeof(BlockPlan) / 4; i += kBgBlock) reinterpret_cast<uint32_t *>(&S.P)[i] = src[i];
+        for (uint32_t i = tid; i < 256; i += kBgBlock) S.crc_tab[i] = A.crc_tab[i];
+        for (uint32_t i = tid; i < kCrcOps * 32; i += kBgBlock) S.crc_ops[i] = A.crc_ops[i];
+        for (uint32_t i = tid; i <= kBitWords; i += kBgBlock) s_bits[i] = 0;
+    }
+    __syncthreads();
+    {
+        const uint32_t nd = min(S.P.n_rows, kStRowDesc) * (uint32_t)(sizeof(DevRow) / 4);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
+        for (uint32_t i = tid; i < nd; i += kBgBlock) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
+        for (uint32_t k = 0; k < S.P.n_st; k++) {
+            const StRow T = S.P.st[k];
+            const DevRow R = A.rows[T.row];
+            const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
+            for (uint32_t i = tid; i < nb; i += kBgBlock) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
+            for (uint32_t i = tid; i < R.nv; i += kBgBlock) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
+            for (uint32_t i = tid; i < R.nv * kRowTokBytes; i += kBgBlock)
+                S.text[T.tok_at * kRowTokBytes + i] = (uint8_t)A.tok_text[(size_t)R.tok * kRowTokBytes + i];
+            for (uint32_t i = tid; i < T.ncum; i += kBgBlock) S.cum[T.cum_at + i] = A.cum[R.cum_off + T.g_lo + i];
+        }
+    }
+    __syncthreads();
     const Ctx C{A, b0, S};
     const uint64_t p = b0 + min(n, tid * kBgPer), e = b0 + min(n, (tid + 1) * kBgPer);
-    // CRC32 (reflected 0xEDB88320, zero start) of the thread's bytes, shifted to the block end
-    uint32_t crc = 0;
-    C.bytes(p, e, [&](uint8_t b) { crc = s_crc_tab[(crc ^ b) & 0xFFu] ^ (crc >> 8); });
-    s_crc[tid] = crc_shift(A.crc_ops, crc, b0 + n - e);
-    // pass 1: the thread's bits
+    // pass 1: the thread's bits, and the CRC32 (reflected 0xEDB88320, zero start) of
+    // its bytes shifted to the block end
     BitOut cnt{s_bits, 0, false};
-    C.encode(p, e, cnt);
+    uint32_t crc = 0;
+    C.encode<true>(p, e, cnt, &crc);
+    s_crc[tid] = crc_shift_lds(S.crc_ops, crc, (uint32_t)(b0 + n - e));
     s_scan[tid] = cnt.off;
     __syncthreads();
     for (uint32_t o = 1; o < kBgBlock; o <<= 1) {
@@ -443,13 +511,14 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
         if (tid == 0) s_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
         __syncthreads();
         BitOut w{s_bits, 3 + s_scan[tid] - cnt.off, true};
-        C.encode(p, e, w);
+        C.encode<false>(p, e, w, nullptr);
     }
-    if (tid == 0) {  // the block's CRC: XOR of the shifted parts, then the start value and final XOR
-        uint32_t x = 0;
-        for (uint32_t t = 0; t < kBgBlock; t++) x ^= s_crc[t];
-        s_crc[0] = x ^ crc_shift(A.crc_ops, 0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+    // the block's CRC: XOR of the shifted parts, then the start value and final XOR
+    for (uint32_t o = kBgBlock / 2; o; o >>= 1) {
+        __syncthreads();
+        if (tid < o) s_crc[tid] ^= s_crc[tid + o];
     }
+    if (tid == 0) s_crc[0] ^= crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
     __syncthreads();
     uint8_t *out = A.out + (size_t)blockIdx.x * kBgzfMax;
     const uint32_t clen = stored ? 5 + n : dbytes;
@@ -518,8 +587,11 @@ int launch_row_cum(const BgArgs &a, hipStream_t stream) {
     return TFBS_OK;
 }
 
+size_t bgzf_plan_bytes() { return sizeof(BlockPlan); }
+
 int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream) {
     if (n_blocks == 0) return TFBS_OK;
+    hipLaunchKernelGGL(bgzf_plan_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, stream, a, n_blocks);
     hipLaunchKernelGGL(bgzf_block_kernel, dim3(n_blocks), dim3(kBgBlock), 0, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_block_kernel: ") + hipGetErrorString(e));

@@ -27,13 +27,16 @@ struct BgArgs {
     uint32_t *out_len;          // the blocks' sizes
     const uint32_t *crc_tab;    // CRC32 byte table
     const uint32_t *crc_ops;    // kBgzfOps x 32 columns
+    void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
 };
+size_t bgzf_plan_bytes();
 
 // CRC32 table and the x^(8 * 2^k) operators (host side, uploaded once).
 void bgzf_crc_tables(uint32_t *tab, uint32_t *ops);
 // Per row: its genotype text offsets every 64 samples.
 int launch_row_cum(const BgArgs &a, hipStream_t stream);
-// Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each.
+// Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a
+// planning kernel, one thread per block).
 int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream);
 // The blocks back to back: block i's out_len bytes at off[i] (off[n_blocks] = total).
 int launch_bgzf_compact(const uint8_t *in, const uint64_t *off, uint32_t n_blocks, uint8_t *out, hipStream_t stream);

@@ -140,7 +140,7 @@ struct tfbs_ctx {
     // device BGZF rows (tfbs_batch_rows_bgzf)
     DevBuf<DevRow> bg_rows;
     DevBuf<char> bg_heads, bg_tok_text;
-    DevBuf<uint8_t> bg_tok_len, bg_out, bg_packed;
+    DevBuf<uint8_t> bg_tok_len, bg_out, bg_packed, bg_plans;
     DevBuf<uint32_t> bg_cum, bg_out_len, bg_crc;  // bg_crc: byte table | shift operators
     DevBuf<uint64_t> bg_off;
     tfbs::PinnedBytes bg_host;       // compressed blocks staged for the host
@@ -403,7 +403,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
     ctx->bg_out.release(); ctx->bg_packed.release(); ctx->bg_cum.release(); ctx->bg_out_len.release();
-    ctx->bg_crc.release(); ctx->bg_off.release();
+    ctx->bg_crc.release(); ctx->bg_off.release(); ctx->bg_plans.release();
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
@@ -857,7 +857,10 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         std::vector<uint64_t> off;
         for (uint64_t b0 = 0; b0 < n_blocks; b0 += kBatchBlocks) {
             const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
-            if ((rc = ctx->bg_out.ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len.ensure(nb))) return rc;
+            if ((rc = ctx->bg_out.ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len.ensure(nb)) ||
+                (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
+                return rc;
+            a.plans = ctx->bg_plans.p;
             a.block0 = b0;
             a.out = ctx->bg_out.p;
             a.out_len = ctx->bg_out_len.p;
