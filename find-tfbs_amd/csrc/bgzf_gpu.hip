@@ -548,6 +548,30 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     }
 }
 
+// off[i] = the sizes of blocks before i, off[nb] = their total (one workgroup).
+__global__ __launch_bounds__(1024) void bgzf_offsets_kernel(const uint32_t *__restrict__ len, uint32_t nb,
+                                                            uint64_t *__restrict__ off) {
+    __shared__ uint64_t s_sum[1024];
+    const uint32_t tid = threadIdx.x, per = (nb + 1023) / 1024;
+    const uint32_t i0 = min(nb, tid * per), i1 = min(nb, i0 + per);
+    uint64_t mine = 0;
+    for (uint32_t i = i0; i < i1; i++) mine += len[i];
+    s_sum[tid] = mine;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint64_t t = tid >= o ? s_sum[tid - o] : 0;
+        __syncthreads();
+        s_sum[tid] += t;
+        __syncthreads();
+    }
+    uint64_t at = s_sum[tid] - mine;
+    for (uint32_t i = i0; i < i1; i++) {
+        off[i] = at;
+        at += len[i];
+    }
+    if (tid == 1023) off[nb] = s_sum[1023];
+}
+
 // Copies each block to its offset of one contiguous buffer.
 __global__ __launch_bounds__(256) void bgzf_compact_kernel(const uint8_t *__restrict__ in,
                                                            const uint64_t *__restrict__ off,
@@ -598,8 +622,10 @@ int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream) {
     return TFBS_OK;
 }
 
-int launch_bgzf_compact(const uint8_t *in, const uint64_t *off, uint32_t n_blocks, uint8_t *out, hipStream_t stream) {
+int launch_bgzf_compact(const uint8_t *in, const uint32_t *len, uint64_t *off, uint32_t n_blocks, uint8_t *out,
+                        hipStream_t stream) {
     if (n_blocks == 0) return TFBS_OK;
+    hipLaunchKernelGGL(bgzf_offsets_kernel, dim3(1), dim3(1024), 0, stream, len, n_blocks, off);
     hipLaunchKernelGGL(bgzf_compact_kernel, dim3(n_blocks), dim3(256), 0, stream, in, off, out);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_compact_kernel: ") + hipGetErrorString(e));

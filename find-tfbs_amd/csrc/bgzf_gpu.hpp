@@ -38,7 +38,9 @@ int launch_row_cum(const BgArgs &a, hipStream_t stream);
 // Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a
 // planning kernel, one thread per block).
 int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream);
-// The blocks back to back: block i's out_len bytes at off[i] (off[n_blocks] = total).
-int launch_bgzf_compact(const uint8_t *in, const uint64_t *off, uint32_t n_blocks, uint8_t *out, hipStream_t stream);
+// The blocks back to back: off[i] = the sizes len[] of the blocks before i (off[n_blocks] =
+// their total), block i's bytes at off[i] of out.
+int launch_bgzf_compact(const uint8_t *in, const uint32_t *len, uint64_t *off, uint32_t n_blocks, uint8_t *out,
+                        hipStream_t stream);
 
 }  // namespace tfbs

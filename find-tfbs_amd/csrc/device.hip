@@ -140,10 +140,16 @@ struct tfbs_ctx {
     // device BGZF rows (tfbs_batch_rows_bgzf)
     DevBuf<DevRow> bg_rows;
     DevBuf<char> bg_heads, bg_tok_text;
-    DevBuf<uint8_t> bg_tok_len, bg_out, bg_packed, bg_plans;
-    DevBuf<uint32_t> bg_cum, bg_out_len, bg_crc;  // bg_crc: byte table | shift operators
-    DevBuf<uint64_t> bg_off;
-    tfbs::PinnedBytes bg_host;       // compressed blocks staged for the host
+    DevBuf<uint8_t> bg_tok_len, bg_plans;
+    DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
+    // two slots of block batches (one being made, one copied back and written)
+    DevBuf<uint8_t> bg_out[2], bg_packed[2];
+    DevBuf<uint32_t> bg_out_len[2];
+    DevBuf<uint64_t> bg_off[2];
+    tfbs::PinnedBytes bg_host[2];     // compressed blocks staged for the host
+    uint64_t *bg_total_host = nullptr;  // pinned: each slot's packed bytes
+    hipEvent_t bg_done[2] = {}, bg_copied[2] = {};
+    hipStream_t copy_stream = nullptr;
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
     float last_ms = 0.f;
@@ -402,8 +408,18 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
-    ctx->bg_out.release(); ctx->bg_packed.release(); ctx->bg_cum.release(); ctx->bg_out_len.release();
-    ctx->bg_crc.release(); ctx->bg_off.release(); ctx->bg_plans.release();
+    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release();
+    for (int k = 0; k < 2; k++) {
+        ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
+        ctx->bg_host[k].release();
+        if (ctx->bg_done[k]) (void)hipEventDestroy(ctx->bg_done[k]);
+        if (ctx->bg_copied[k]) (void)hipEventDestroy(ctx->bg_copied[k]);
+    }
+    if (ctx->bg_total_host) (void)hipHostFree(ctx->bg_total_host);
+    if (ctx->copy_stream) {
+        (void)hipStreamSynchronize(ctx->copy_stream);
+        (void)hipStreamDestroy(ctx->copy_stream);
+    }
     if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
     if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
     if (ctx->evk0) (void)hipEventDestroy(ctx->evk0);
@@ -852,34 +868,29 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         a.crc_tab = ctx->bg_crc.p;
         a.crc_ops = ctx->bg_crc.p + 256;
         if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
+        // batches of blocks in two slots: while the device makes batch i, the host copies
+        // batch i - 1's packed blocks back (copy stream) and writes them to fd
         constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
-        std::vector<uint32_t> blen;
-        std::vector<uint64_t> off;
-        for (uint64_t b0 = 0; b0 < n_blocks; b0 += kBatchBlocks) {
-            const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
-            if ((rc = ctx->bg_out.ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len.ensure(nb)) ||
-                (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
-                return rc;
-            a.plans = ctx->bg_plans.p;
-            a.block0 = b0;
-            a.out = ctx->bg_out.p;
-            a.out_len = ctx->bg_out_len.p;
-            if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream))) return rc;
-            blen.resize(nb);
-            HIP_TRY(hipMemcpyAsync(blen.data(), ctx->bg_out_len.p, (size_t)nb * 4, hipMemcpyDeviceToHost, ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
-            off.assign(nb + 1, 0);
-            for (uint32_t i = 0; i < nb; i++) off[i + 1] = off[i] + blen[i];
-            const uint64_t total = off[nb];
-            if ((rc = ctx->bg_off.put(off, ctx->stream)) || (rc = ctx->bg_packed.ensure(total)) ||
-                (rc = ctx->bg_host.reserve(total)))
-                return rc;
-            if ((rc = tfbs::launch_bgzf_compact(ctx->bg_out.p, ctx->bg_off.p, nb, ctx->bg_packed.p, ctx->stream)))
-                return rc;
-            HIP_TRY(hipMemcpyAsync(ctx->bg_host.p, ctx->bg_packed.p, total, hipMemcpyDeviceToHost, ctx->stream));
-            HIP_TRY(hipStreamSynchronize(ctx->stream));
+        const uint64_t n_batches = (n_blocks + kBatchBlocks - 1) / kBatchBlocks;
+        if (!ctx->bg_total_host) HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 16, hipHostMallocDefault));
+        for (int k = 0; k < 2; k++) {
+            if (!ctx->bg_done[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_done[k], hipEventDisableTiming));
+            if (!ctx->bg_copied[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_copied[k], hipEventDisableTiming));
+        }
+        if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+        auto drain = [&](uint64_t i) -> int {  // batch i's blocks to fd
+            const int k = (int)(i & 1);
+            HIP_TRY(hipEventSynchronize(ctx->bg_done[k]));
+            const uint64_t total = ctx->bg_total_host[k];
+            int r;
+            if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
+            if (total)
+                HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost,
+                                       ctx->copy_stream));
+            HIP_TRY(hipEventRecord(ctx->bg_copied[k], ctx->copy_stream));
+            HIP_TRY(hipEventSynchronize(ctx->bg_copied[k]));
             for (uint64_t at = 0; at < total;) {  // the blocks to the file as they are
-                const ssize_t w = ::write(fd, ctx->bg_host.p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
+                const ssize_t w = ::write(fd, ctx->bg_host[k].p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
                 if (w < 0) {
                     if (errno == EINTR) continue;
                     return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
@@ -887,7 +898,32 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
                 at += (uint64_t)w;
             }
             written += total;
+            return TFBS_OK;
+        };
+        for (uint64_t i = 0; i < n_batches; i++) {
+            const int k = (int)(i & 1);
+            const uint64_t b0 = i * kBatchBlocks;
+            const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
+            if ((rc = ctx->bg_out[k].ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len[k].ensure(nb)) ||
+                (rc = ctx->bg_off[k].ensure(nb + 1)) || (rc = ctx->bg_packed[k].ensure((size_t)nb * kBgzfMax)) ||
+                (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
+                return rc;
+            // slot k's packed blocks were copied back (batch i - 2) before they are overwritten
+            if (i >= 2) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+            a.plans = ctx->bg_plans.p;
+            a.block0 = b0;
+            a.out = ctx->bg_out[k].p;
+            a.out_len = ctx->bg_out_len[k].p;
+            if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) ||
+                (rc = tfbs::launch_bgzf_compact(ctx->bg_out[k].p, ctx->bg_out_len[k].p, ctx->bg_off[k].p, nb,
+                                                ctx->bg_packed[k].p, ctx->stream)))
+                return rc;
+            HIP_TRY(hipMemcpyAsync(ctx->bg_total_host + k, ctx->bg_off[k].p + nb, 8, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+            HIP_TRY(hipEventRecord(ctx->bg_done[k], ctx->stream));
+            if (i >= 1 && (rc = drain(i - 1))) return rc;
         }
+        if ((rc = drain(n_batches - 1))) return rc;
     }
     if (bytes) *bytes = written;
     return TFBS_OK;
