@@ -32,13 +32,6 @@ constexpr uint32_t kBgWords = (kBgzfMax - 26) / 4;                  // deflate d
 constexpr uint32_t kBitWords = kBgWords / 2;
 constexpr uint32_t kLookback = 8;                                   // sample texts searched for a match
 
-__constant__ uint16_t c_len_base[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
-                                        31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
-__constant__ uint8_t c_len_extra[29] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 0};
-__constant__ uint16_t c_dist_base[30] = {1,   2,   3,   4,   5,   7,    9,    13,   17,   25,   33,   49,   65,    97,    129,
-                                         193, 257, 385, 513, 769, 1025, 1537, 2049, 3073, 4097, 6145, 8193, 12289, 16385, 24577};
-__constant__ uint8_t c_dist_extra[30] = {0, 0, 0, 0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13};
-
 __device__ __forceinline__ uint32_t rev(uint32_t code, uint32_t n) { return __builtin_bitreverse32(code) >> (32 - n); }
 
 // The bit stream of one thread: counts bits (write = false) or ORs them into the
@@ -59,17 +52,35 @@ struct BitOut {
         if (b < 144) put(rev(0x30 + b, 8), 8);
         else put(rev(0x190 + b - 144, 9), 9);
     }
+    // RFC 1951 3.2.5's length and distance codes, from the values' bit lengths:
+    // lengths 3-10 and distances 1-4 have codes of their own, then each code covers
+    // 2^extra values, four length codes (two distance codes) per extra bit count
     __device__ void match(uint32_t len, uint32_t dist) {  // 3 <= len <= 258, dist <= 32768
-        uint32_t i = 0;
-        while (i < 28 && c_len_base[i + 1] <= len) i++;
-        const uint32_t sym = 257 + i;
+        uint32_t sym, xb = 0, xv = 0;
+        if (len == 258) {
+            sym = 285;
+        } else if (len <= 10) {
+            sym = 254 + len;
+        } else {
+            const uint32_t x = len - 3, nb = 31 - __builtin_clz(x);  // nb >= 3
+            sym = 257 + 4 * (nb - 1) + ((x >> (nb - 2)) & 3u);
+            xb = nb - 2;
+            xv = x & ((1u << xb) - 1u);
+        }
         if (sym < 280) put(rev(sym - 256, 7), 7);
         else put(rev(0xC0 + sym - 280, 8), 8);
-        put(len - c_len_base[i], c_len_extra[i]);
-        uint32_t d = 0;
-        while (d < 29 && c_dist_base[d + 1] <= dist) d++;
-        put(rev(d, 5), 5);
-        put(dist - c_dist_base[d], c_dist_extra[d]);
+        put(xv, xb);
+        uint32_t dc, db = 0, dv = 0;
+        if (dist <= 4) {
+            dc = dist - 1;
+        } else {
+            const uint32_t x = dist - 1, nb = 31 - __builtin_clz(x);  // nb >= 2
+            dc = 2 * nb + ((x >> (nb - 1)) & 1u);
+            db = nb - 1;
+            dv = x & ((1u << db) - 1u);
+        }
+        put(rev(dc, 5), 5);
+        put(dv, db);
     }
 };
 
