@@ -118,7 +118,7 @@ struct Stage {
     DevRow rows[kStRowDesc];  // rows r_first ..
     uint8_t codes[kStCodes];
     uint8_t tlen[kStTok];
-    uint8_t text[kStTok * kRowTokBytes];
+    alignas(16) uint8_t text[kStTok * kRowTokBytes];
     uint32_t cum[kStCum];
     uint32_t crc_tab[256];
     uint32_t crc_ops[kCrcOps * 32];
@@ -140,14 +140,21 @@ __device__ __forceinline__ uint32_t crc_shift_lds(const uint32_t *ops, uint32_t 
     return v;
 }
 
+// One row as a thread reads it: where its codes, token lengths and texts are
+// (LDS when the block staged them), held in registers while the thread is in it.
+struct RowView {
+    DevRow R;
+    bool st;                  // staged
+    uint32_t s_lo, s_hi;      // staged samples
+    int32_t cbase;            // Stage::codes index of the row's code byte 0 (may be negative)
+    uint32_t tok_at, cum_at, g_lo, ncum;
+    uint32_t mask;
+};
+
 struct Ctx {
     const BgArgs &A;
     uint64_t b0;
     const Stage &S;
-    __device__ DevRow row(uint32_t r) const {
-        const uint32_t d = r - S.P.r_first;
-        return d < min(S.P.n_rows, kStRowDesc) ? S.rows[d] : A.rows[r];
-    }
     __device__ uint64_t row_off(uint32_t r) const {
         const uint32_t d = r - S.P.r_first;
         return d < min(S.P.n_rows, kStRowDesc) ? S.rows[d].text_off : A.rows[r].text_off;
@@ -162,44 +169,59 @@ struct Ctx {
         }
         return lo;
     }
-    __device__ int slot(uint32_t r) const {
+    __device__ RowView view(uint32_t r) const {
+        RowView v;
+        const uint32_t d = r - S.P.r_first;
+        v.R = d < min(S.P.n_rows, kStRowDesc) ? S.rows[d] : A.rows[r];
+        v.st = false;
+        v.mask = (1u << v.R.width) - 1u;
         for (uint32_t k = 0; k < S.P.n_st; k++)
-            if (S.P.st[k].row == r) return (int)k;
-        return -1;
+            if (S.P.st[k].row == r) {
+                const StRow T = S.P.st[k];
+                v.st = true;
+                v.s_lo = T.s_lo;
+                v.s_hi = T.s_hi;
+                v.cbase = (int32_t)T.code_at - (int32_t)T.cfirst;
+                v.tok_at = T.tok_at;
+                v.cum_at = T.cum_at;
+                v.g_lo = T.g_lo;
+                v.ncum = T.ncum;
+            }
+        return v;
     }
-    __device__ uint32_t code(const DevRow &R, int k, uint32_t s) const {
-        const uint32_t bit = s * R.width;
-        uint32_t b;
-        if (k >= 0 && s >= S.P.st[k].s_lo && s < S.P.st[k].s_hi)
-            b = S.codes[S.P.st[k].code_at + (bit >> 3) - S.P.st[k].cfirst];
-        else
-            b = A.codes[R.code_off + (bit >> 3)];
-        return (b >> (bit & 7)) & ((1u << R.width) - 1u);
+    __device__ uint32_t code(const RowView &v, uint32_t s) const {
+        const uint32_t bit = s * v.R.width;
+        const uint32_t b = (v.st && s >= v.s_lo && s < v.s_hi) ? S.codes[v.cbase + (int32_t)(bit >> 3)]
+                                                               : A.codes[v.R.code_off + (bit >> 3)];
+        return (b >> (bit & 7)) & v.mask;
     }
-    __device__ uint32_t tlen(const DevRow &R, int k, uint32_t c) const {
-        return k >= 0 ? S.tlen[S.P.st[k].tok_at + c] : A.tok_len[R.tok + c];
+    __device__ uint32_t tlen(const RowView &v, uint32_t c) const {
+        return v.st ? S.tlen[v.tok_at + c] : A.tok_len[v.R.tok + c];
     }
-    __device__ uint8_t tbyte(const DevRow &R, int k, uint32_t c, uint32_t o) const {
-        return k >= 0 ? S.text[(S.P.st[k].tok_at + c) * kRowTokBytes + o]
-                      : (uint8_t)A.tok_text[(size_t)(R.tok + c) * kRowTokBytes + o];
+    __device__ uint4 ttext(const RowView &v, uint32_t c) const {  // the token's 16 bytes
+        return v.st ? reinterpret_cast<const uint4 *>(S.text)[v.tok_at + c]
+                    : reinterpret_cast<const uint4 *>(A.tok_text)[v.R.tok + c];
+    }
+    static __device__ __forceinline__ uint32_t byte_of(const uint4 &t, uint32_t o) {
+        const uint32_t w = o < 8 ? (o < 4 ? t.x : t.y) : (o < 12 ? t.z : t.w);
+        return (w >> (8 * (o & 3))) & 0xFFu;
     }
     // sample s and offset o of byte g of the row's genotype text
-    __device__ void locate(const DevRow &R, int k, uint64_t g, uint32_t &s, uint32_t &o) const {
+    __device__ void locate(const RowView &v, uint64_t g, uint32_t &s, uint32_t &o) const {
         uint32_t q, pos;
         const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
-        const StRow *T = k >= 0 ? &S.P.st[k] : nullptr;
-        if (T && g >= S.cum[T->cum_at] && g < S.cum[T->cum_at + T->ncum - 1]) {
-            const uint32_t *cum = S.cum + T->cum_at;  // the staged groups
-            uint32_t lo = 0, hi = T->ncum - 2;
+        if (v.st && g >= S.cum[v.cum_at] && g < S.cum[v.cum_at + v.ncum - 1]) {
+            const uint32_t *cum = S.cum + v.cum_at;  // the staged groups
+            uint32_t lo = 0, hi = v.ncum - 2;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) / 2;
                 if (cum[mid] <= g) lo = mid;
                 else hi = mid - 1;
             }
-            q = T->g_lo + lo;
+            q = v.g_lo + lo;
             pos = cum[lo];
         } else {
-            const uint32_t *cum = A.cum + R.cum_off;
+            const uint32_t *cum = A.cum + v.R.cum_off;
             uint32_t lo = 0, hi = ng - 1;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) / 2;
@@ -211,7 +233,7 @@ struct Ctx {
         }
         s = q * kCumGroup;
         for (; s + 1 < A.n_samples; s++) {  // bounded: g lies inside the row's genotype text
-            const uint32_t t = tlen(R, k, code(R, k, s));
+            const uint32_t t = tlen(v, code(v, s));
             if (g < (uint64_t)pos + t) break;
             pos += t;
         }
@@ -224,27 +246,27 @@ struct Ctx {
         uint32_t r = find_row(p);
         while (p < e) {
             while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
-            const DevRow R = row(r);
-            const int k = slot(r);
-            const uint64_t local = p - R.text_off;
-            if (local < R.head_len) {
-                const uint64_t n = min((uint64_t)R.head_len - local, e - p);
-                for (uint64_t i = 0; i < n; i++) f((uint8_t)A.heads[R.head_off + local + i]);
+            const RowView v = view(r);
+            const uint64_t local = p - v.R.text_off;
+            if (local < v.R.head_len) {
+                const uint64_t n = min((uint64_t)v.R.head_len - local, e - p);
+                for (uint64_t i = 0; i < n; i++) f((uint8_t)A.heads[v.R.head_off + local + i]);
                 p += n;
                 continue;
             }
-            uint64_t g = local - R.head_len;
-            if (g >= R.geno_len) {
+            uint64_t g = local - v.R.head_len;
+            if (g >= v.R.geno_len) {
                 f((uint8_t)'\n');
                 p++;
                 continue;
             }
             uint32_t s, o;
-            locate(R, k, g, s, o);
-            while (p < e && g < R.geno_len) {
-                const uint32_t c = code(R, k, s), t = tlen(R, k, c);
+            locate(v, g, s, o);
+            while (p < e && g < v.R.geno_len) {
+                const uint32_t c = code(v, s), t = tlen(v, c);
+                const uint4 tx = ttext(v, c);
                 const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
-                for (uint32_t i = 0; i < n; i++) f(tbyte(R, k, c, o + i));
+                for (uint32_t i = 0; i < n; i++) f((uint8_t)byte_of(tx, o + i));
                 p += n;
                 g += n;
                 o += n;
@@ -260,76 +282,76 @@ struct Ctx {
     __device__ void encode(uint64_t p, uint64_t e, BitOut &out, uint32_t *crc) const {
         if (p >= e) return;
         uint32_t r = find_row(p);
+        uint32_t x = kCrc ? *crc : 0u;
         while (p < e) {
             while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
-            const DevRow R = row(r);
-            const int k = slot(r);
-            const uint64_t local = p - R.text_off;
-            if (local < R.head_len) {
-                const uint64_t n = min((uint64_t)R.head_len - local, e - p);
+            const RowView v = view(r);
+            const uint64_t local = p - v.R.text_off;
+            if (local < v.R.head_len) {
+                const uint64_t n = min((uint64_t)v.R.head_len - local, e - p);
                 for (uint64_t i = 0; i < n; i++) {
-                    const uint32_t b = (uint8_t)A.heads[R.head_off + local + i];
+                    const uint32_t b = (uint8_t)A.heads[v.R.head_off + local + i];
                     out.lit(b);
-                    if (kCrc) *crc = crc_byte(S.crc_tab, *crc, b);
+                    if (kCrc) x = crc_byte(S.crc_tab, x, b);
                 }
                 p += n;
                 continue;
             }
-            uint64_t g = local - R.head_len;
-            if (g >= R.geno_len) {
+            uint64_t g = local - v.R.head_len;
+            if (g >= v.R.geno_len) {
                 out.lit('\n');
-                if (kCrc) *crc = crc_byte(S.crc_tab, *crc, '\n');
+                if (kCrc) x = crc_byte(S.crc_tab, x, '\n');
                 p++;
                 continue;
             }
             uint32_t s, o;
-            locate(R, k, g, s, o);
-            while (p < e && g < R.geno_len) {
-                const uint32_t c = code(R, k, s), t = tlen(R, k, c);
+            locate(v, g, s, o);
+            uint32_t prev = s > 0 ? code(v, s - 1) : UINT32_MAX;
+            while (p < e && g < v.R.geno_len) {
+                const uint32_t c = code(v, s), t = tlen(v, c);
+                const uint4 tx = ttext(v, c);
                 const uint64_t tok0 = p - o;  // this sample text's first byte
-                if (s > 0 && code(R, k, s - 1) == c && tok0 >= b0 + t) {
+                if (prev == c && tok0 >= b0 + t) {
                     // a run: every byte equals the one t before it, to the run's end
                     uint64_t end = tok0 + t;
                     uint32_t s2 = s + 1;
-                    while (end < e && s2 < A.n_samples && code(R, k, s2) == c) {
+                    while (end < e && s2 < A.n_samples && code(v, s2) == c) {
                         end += t;
                         s2++;
                     }
                     end = min(end, e);
                     uint32_t left = (uint32_t)(end - p), oo = o;
-                    if (kCrc) {
-                        uint32_t x = *crc;
+                    if (kCrc)
                         for (uint32_t i = 0, q = o; i < left; i++) {
-                            x = crc_byte(S.crc_tab, x, tbyte(R, k, c, q));
+                            x = crc_byte(S.crc_tab, x, byte_of(tx, q));
                             q = q + 1 == t ? 0 : q + 1;
                         }
-                        *crc = x;
-                    }
                     while (left) {
                         if (left < 3) {  // too short for a match: literals
-                            out.lit(tbyte(R, k, c, oo));
-                            oo = (oo + 1) % t;
+                            out.lit(byte_of(tx, oo));
+                            oo = oo + 1 == t ? 0 : oo + 1;
                             left--;
                             continue;
                         }
                         const uint32_t m = left > 258 ? (left - 258 < 3 ? left - 3 : 258) : left;
                         out.match(m, t);
-                        oo = (uint32_t)((oo + m) % t);
+                        oo = (oo + m) % t;
                         left -= m;
                     }
-                    const uint64_t adv = end - p;
+                    const uint32_t adv = (uint32_t)(end - p);
                     g += adv;
                     p = end;
-                    const uint64_t q = o + adv;
-                    s += (uint32_t)(q / t);
-                    o = (uint32_t)(q % t);
+                    const uint32_t q = o + adv;
+                    s += q / t;
+                    o = q % t;
+                    prev = c;
                     continue;
                 }
                 const uint32_t n = (uint32_t)min((uint64_t)(t - o), e - p);
                 uint32_t dist = 0, acc = 0;
                 for (uint32_t kk = 1; kk <= kLookback && kk <= s; kk++) {  // the same text among the samples before
-                    const uint32_t cc = code(R, k, s - kk);
-                    acc += tlen(R, k, cc);
+                    const uint32_t cc = kk == 1 ? prev : code(v, s - kk);
+                    acc += tlen(v, cc);
                     if (tok0 < b0 + acc) break;
                     if (cc == c) {
                         dist = acc;
@@ -339,12 +361,12 @@ struct Ctx {
                 if (dist && n >= 3) {
                     out.match(n, dist);
                     if (kCrc)
-                        for (uint32_t i = 0; i < n; i++) *crc = crc_byte(S.crc_tab, *crc, tbyte(R, k, c, o + i));
+                        for (uint32_t i = 0; i < n; i++) x = crc_byte(S.crc_tab, x, byte_of(tx, o + i));
                 } else {
                     for (uint32_t i = 0; i < n; i++) {
-                        const uint32_t b = tbyte(R, k, c, o + i);
+                        const uint32_t b = byte_of(tx, o + i);
                         out.lit(b);
-                        if (kCrc) *crc = crc_byte(S.crc_tab, *crc, b);
+                        if (kCrc) x = crc_byte(S.crc_tab, x, b);
                     }
                 }
                 p += n;
@@ -353,9 +375,11 @@ struct Ctx {
                 if (o == t) {
                     s++;
                     o = 0;
+                    prev = c;
                 }
             }
         }
+        if (kCrc) *crc = x;
     }
 };
 
