@@ -84,22 +84,23 @@ struct BitOut {
     }
 };
 
-// What a block stages in LDS: the descriptors of its first kStRowDesc rows,
-// and for up to kStRows rows with genotype text in the block their token
-// lengths and texts, the group offsets (cum) of the 64-sample groups the block
-// touches and those samples' packed codes.  bgzf_plan_kernel chooses them (one
-// thread per block, so the binary searches of many blocks overlap); anything
-// else (rows of a few samples) is read from global memory.
+// What a block stages in LDS: the descriptors of its rows (up to kStRowDesc),
+// and for each of its (up to kStRows) rows with genotype text in the block the
+// token lengths and texts, the group offsets (cum) of the 64-sample groups the
+// block touches and those samples' packed codes (one group more before, for the
+// look-backs).  bgzf_plan_kernel decides (one thread per block, so the binary
+// searches of many blocks overlap); a block whose rows do not all fit (rows of a
+// few samples) reads everything from global memory instead.
 constexpr uint32_t kStRows = 8;
 constexpr uint32_t kStRowDesc = 96;
-constexpr uint32_t kStCodes = 16896;  // >= the codes of 65280 bytes of 4-byte sample texts + 2 groups per row
+constexpr uint32_t kStCodes = 18432;  // >= the codes of 65280 bytes of 4-byte sample texts + 3 groups per row
 constexpr uint32_t kStTok = 512;      // token slots (kRowTokBytes of text each)
 constexpr uint32_t kStCum = 512;
 constexpr uint32_t kCrcOps = 16;      // shift operators of 2^k bytes, k < 16 (shifts below 64 KiB)
 
 struct StRow {
     uint32_t row;          // row index
-    uint32_t s_lo, s_hi;   // samples whose codes are staged
+    uint32_t s_lo, s_hi;   // samples whose codes are staged (a group before the block's first, for look-backs)
     uint32_t cfirst;       // the row's code byte of sample s_lo (s_lo * width / 8)
     uint32_t code_at;      // its place in Stage::codes
     uint32_t tok_at;       // Stage::tlen / text slot of token 0
@@ -109,7 +110,8 @@ struct StRow {
 
 struct BlockPlan {
     uint32_t r_first, n_rows;  // the rows overlapping the block
-    uint32_t n_st, pad;
+    uint32_t n_st;
+    uint32_t all;              // every row's descriptor and genotype data are staged
     StRow st[kStRows];
 };
 
@@ -123,6 +125,11 @@ struct Stage {
     uint32_t crc_tab[256];
     uint32_t crc_ops[kCrcOps * 32];
 };
+
+// the block kernel's stage, at file scope so that every access compiles to LDS
+// instructions (through a generic reference the selects between staged and global
+// data become flat loads that wait on both counters)
+__shared__ Stage g_st;
 
 __device__ __forceinline__ uint32_t crc_byte(const uint32_t *tab, uint32_t crc, uint32_t b) {
     return tab[(crc ^ b) & 0xFFu] ^ (crc >> 8);
@@ -140,28 +147,28 @@ __device__ __forceinline__ uint32_t crc_shift_lds(const uint32_t *ops, uint32_t 
     return v;
 }
 
-// One row as a thread reads it: where its codes, token lengths and texts are
-// (LDS when the block staged them), held in registers while the thread is in it.
+// One row as a thread reads it.  kSt: the block staged everything (the plan's
+// `all`), so every access is an LDS access; otherwise every access goes to global
+// memory (blocks of many short rows).  The two never mix in one load: a select
+// between LDS and global data compiles to a flat load that waits on both counters.
 struct RowView {
     DevRow R;
-    bool st;                  // staged
-    uint32_t s_lo, s_hi;      // staged samples
-    int32_t cbase;            // Stage::codes index of the row's code byte 0 (may be negative)
+    int32_t cbase;            // kSt: Stage::codes index of the row's code byte 0 (may be negative)
     uint32_t tok_at, cum_at, g_lo, ncum;
     uint32_t mask;
 };
 
+template <bool kSt>
 struct Ctx {
     const BgArgs &A;
     uint64_t b0;
-    const Stage &S;
     __device__ uint64_t row_off(uint32_t r) const {
-        const uint32_t d = r - S.P.r_first;
-        return d < min(S.P.n_rows, kStRowDesc) ? S.rows[d].text_off : A.rows[r].text_off;
+        if constexpr (kSt) return g_st.rows[r - g_st.P.r_first].text_off;
+        else return A.rows[r].text_off;
     }
     // the last row starting at or before p (p inside the block)
     __device__ uint32_t find_row(uint64_t p) const {
-        uint32_t lo = S.P.r_first, hi = S.P.r_first + S.P.n_rows - 1;
+        uint32_t lo = g_st.P.r_first, hi = g_st.P.r_first + g_st.P.n_rows - 1;
         while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) / 2;
             if (row_off(mid) <= p) lo = mid;
@@ -170,48 +177,48 @@ struct Ctx {
         return lo;
     }
     __device__ RowView view(uint32_t r) const {
-        RowView v;
-        const uint32_t d = r - S.P.r_first;
-        v.R = d < min(S.P.n_rows, kStRowDesc) ? S.rows[d] : A.rows[r];
-        v.st = false;
+        RowView v{};
+        if constexpr (kSt) {
+            v.R = g_st.rows[r - g_st.P.r_first];
+            for (uint32_t k = 0; k < g_st.P.n_st; k++)
+                if (g_st.P.st[k].row == r) {
+                    const StRow T = g_st.P.st[k];
+                    v.cbase = (int32_t)T.code_at - (int32_t)T.cfirst;
+                    v.tok_at = T.tok_at;
+                    v.cum_at = T.cum_at;
+                    v.g_lo = T.g_lo;
+                    v.ncum = T.ncum;
+                }
+        } else {
+            v.R = A.rows[r];
+        }
         v.mask = (1u << v.R.width) - 1u;
-        for (uint32_t k = 0; k < S.P.n_st; k++)
-            if (S.P.st[k].row == r) {
-                const StRow T = S.P.st[k];
-                v.st = true;
-                v.s_lo = T.s_lo;
-                v.s_hi = T.s_hi;
-                v.cbase = (int32_t)T.code_at - (int32_t)T.cfirst;
-                v.tok_at = T.tok_at;
-                v.cum_at = T.cum_at;
-                v.g_lo = T.g_lo;
-                v.ncum = T.ncum;
-            }
         return v;
     }
     __device__ uint32_t code(const RowView &v, uint32_t s) const {
         const uint32_t bit = s * v.R.width;
-        const uint32_t b = (v.st && s >= v.s_lo && s < v.s_hi) ? S.codes[v.cbase + (int32_t)(bit >> 3)]
-                                                               : A.codes[v.R.code_off + (bit >> 3)];
+        uint32_t b;
+        if constexpr (kSt) b = g_st.codes[v.cbase + (int32_t)(bit >> 3)];
+        else b = A.codes[v.R.code_off + (bit >> 3)];
         return (b >> (bit & 7)) & v.mask;
     }
     __device__ uint32_t tlen(const RowView &v, uint32_t c) const {
-        return v.st ? S.tlen[v.tok_at + c] : A.tok_len[v.R.tok + c];
+        if constexpr (kSt) return g_st.tlen[v.tok_at + c];
+        else return A.tok_len[v.R.tok + c];
     }
     __device__ uint4 ttext(const RowView &v, uint32_t c) const {  // the token's 16 bytes
-        return v.st ? reinterpret_cast<const uint4 *>(S.text)[v.tok_at + c]
-                    : reinterpret_cast<const uint4 *>(A.tok_text)[v.R.tok + c];
+        if constexpr (kSt) return reinterpret_cast<const uint4 *>(g_st.text)[v.tok_at + c];
+        else return reinterpret_cast<const uint4 *>(A.tok_text)[v.R.tok + c];
     }
     static __device__ __forceinline__ uint32_t byte_of(const uint4 &t, uint32_t o) {
-        const uint32_t w = o < 8 ? (o < 4 ? t.x : t.y) : (o < 12 ? t.z : t.w);
-        return (w >> (8 * (o & 3))) & 0xFFu;
+        const uint64_t lo = (uint64_t)t.x | ((uint64_t)t.y << 32), hi = (uint64_t)t.z | ((uint64_t)t.w << 32);
+        return (uint32_t)((o < 8 ? lo : hi) >> (8 * (o & 7))) & 0xFFu;
     }
     // sample s and offset o of byte g of the row's genotype text
     __device__ void locate(const RowView &v, uint64_t g, uint32_t &s, uint32_t &o) const {
         uint32_t q, pos;
-        const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
-        if (v.st && g >= S.cum[v.cum_at] && g < S.cum[v.cum_at + v.ncum - 1]) {
-            const uint32_t *cum = S.cum + v.cum_at;  // the staged groups
+        if constexpr (kSt) {
+            const uint32_t *cum = g_st.cum + v.cum_at;  // the staged groups
             uint32_t lo = 0, hi = v.ncum - 2;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi + 1) / 2;
@@ -221,6 +228,7 @@ struct Ctx {
             q = v.g_lo + lo;
             pos = cum[lo];
         } else {
+            const uint32_t ng = (A.n_samples + kCumGroup - 1) / kCumGroup;
             const uint32_t *cum = A.cum + v.R.cum_off;
             uint32_t lo = 0, hi = ng - 1;
             while (lo < hi) {
@@ -292,7 +300,7 @@ struct Ctx {
                 for (uint64_t i = 0; i < n; i++) {
                     const uint32_t b = (uint8_t)A.heads[v.R.head_off + local + i];
                     out.lit(b);
-                    if (kCrc) x = crc_byte(S.crc_tab, x, b);
+                    if (kCrc) x = crc_byte(g_st.crc_tab, x, b);
                 }
                 p += n;
                 continue;
@@ -300,7 +308,7 @@ struct Ctx {
             uint64_t g = local - v.R.head_len;
             if (g >= v.R.geno_len) {
                 out.lit('\n');
-                if (kCrc) x = crc_byte(S.crc_tab, x, '\n');
+                if (kCrc) x = crc_byte(g_st.crc_tab, x, '\n');
                 p++;
                 continue;
             }
@@ -323,7 +331,7 @@ struct Ctx {
                     uint32_t left = (uint32_t)(end - p), oo = o;
                     if (kCrc)
                         for (uint32_t i = 0, q = o; i < left; i++) {
-                            x = crc_byte(S.crc_tab, x, byte_of(tx, q));
+                            x = crc_byte(g_st.crc_tab, x, byte_of(tx, q));
                             q = q + 1 == t ? 0 : q + 1;
                         }
                     while (left) {
@@ -361,12 +369,12 @@ struct Ctx {
                 if (dist && n >= 3) {
                     out.match(n, dist);
                     if (kCrc)
-                        for (uint32_t i = 0; i < n; i++) x = crc_byte(S.crc_tab, x, byte_of(tx, o + i));
+                        for (uint32_t i = 0; i < n; i++) x = crc_byte(g_st.crc_tab, x, byte_of(tx, o + i));
                 } else {
                     for (uint32_t i = 0; i < n; i++) {
                         const uint32_t b = byte_of(tx, o + i);
                         out.lit(b);
-                        if (kCrc) x = crc_byte(S.crc_tab, x, b);
+                        if (kCrc) x = crc_byte(g_st.crc_tab, x, b);
                     }
                 }
                 p += n;
@@ -467,7 +475,8 @@ __global__ __launch_bounds__(256) void bgzf_plan_kernel(BgArgs A, uint32_t n_blo
         return lo;
     };
     uint32_t n = 0, code_used = 0, tok_used = 0, cum_used = 0;
-    for (uint32_t r = P.r_first; r <= r_last && n < kStRows; r++) {
+    bool all = P.n_rows <= kStRowDesc;
+    for (uint32_t r = P.r_first; r <= r_last && all; r++) {
         const DevRow R = A.rows[r];
         if (!R.width) continue;
         const uint64_t gs = R.text_off + R.head_len, ge = gs + R.geno_len;
@@ -475,10 +484,14 @@ __global__ __launch_bounds__(256) void bgzf_plan_kernel(BgArgs A, uint32_t n_blo
         if (lo >= hi) continue;
         const uint32_t g_lo = lo == gs ? 0 : group_of(R, lo - gs);
         const uint32_t g_hi = hi == ge ? ng - 1 : group_of(R, hi - 1 - gs);
-        const uint32_t s_lo = g_lo * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
+        const uint32_t s_lo = (g_lo ? g_lo - 1 : 0) * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
         const uint32_t cb0 = s_lo * R.width / 8, cb1 = (s_hi * R.width + 7) / 8;
         const uint32_t ncum = g_hi - g_lo + 2;
-        if (code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok || cum_used + ncum > kStCum) break;
+        if (n == kStRows || code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok ||
+            cum_used + ncum > kStCum) {
+            all = false;
+            break;
+        }
         P.st[n] = StRow{r, s_lo, s_hi, cb0, code_used, tok_used, g_lo, ncum, cum_used};
         code_used += cb1 - cb0;
         tok_used += R.nv;
@@ -486,6 +499,7 @@ __global__ __launch_bounds__(256) void bgzf_plan_kernel(BgArgs A, uint32_t n_blo
         n++;
     }
     P.n_st = n;
+    P.all = all ? 1u : 0u;
     reinterpret_cast<BlockPlan *>(A.plans)[i] = P;
 }
 
@@ -493,7 +507,7 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     __shared__ uint32_t s_bits[kBitWords + 1];
     __shared__ uint32_t s_scan[kBgBlock];
     __shared__ uint32_t s_crc[kBgBlock];
-    __shared__ Stage S;
+    Stage &S = g_st;
     const uint32_t tid = threadIdx.x;
     const uint64_t blk = A.block0 + blockIdx.x;
     const uint64_t b0 = blk * kBgzfRaw;
@@ -507,8 +521,8 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
         for (uint32_t i = tid; i <= kBitWords; i += kBgBlock) s_bits[i] = 0;
     }
     __syncthreads();
-    {
-        const uint32_t nd = min(S.P.n_rows, kStRowDesc) * (uint32_t)(sizeof(DevRow) / 4);
+    if (S.P.all) {  // (uniform: the whole block stages or none of it)
+        const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
         for (uint32_t i = tid; i < nd; i += kBgBlock) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
         for (uint32_t k = 0; k < S.P.n_st; k++) {
@@ -523,13 +537,16 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
         }
     }
     __syncthreads();
-    const Ctx C{A, b0, S};
+    const bool all = S.P.all != 0;
+    const Ctx<true> CS{A, b0};
+    const Ctx<false> CG{A, b0};
     const uint64_t p = b0 + min(n, tid * kBgPer), e = b0 + min(n, (tid + 1) * kBgPer);
     // pass 1: the thread's bits, and the CRC32 (reflected 0xEDB88320, zero start) of
     // its bytes shifted to the block end
     BitOut cnt{s_bits, 0, false};
     uint32_t crc = 0;
-    C.encode<true>(p, e, cnt, &crc);
+    if (all) CS.template encode<true>(p, e, cnt, &crc);
+    else CG.template encode<true>(p, e, cnt, &crc);
     s_crc[tid] = crc_shift_lds(S.crc_ops, crc, (uint32_t)(b0 + n - e));
     s_scan[tid] = cnt.off;
     __syncthreads();
@@ -546,7 +563,8 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
         if (tid == 0) s_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
         __syncthreads();
         BitOut w{s_bits, 3 + s_scan[tid] - cnt.off, true};
-        C.encode<false>(p, e, w, nullptr);
+        if (all) CS.template encode<false>(p, e, w, nullptr);
+        else CG.template encode<false>(p, e, w, nullptr);
     }
     // the block's CRC: XOR of the shifted parts, then the start value and final XOR
     for (uint32_t o = kBgBlock / 2; o; o >>= 1) {
@@ -560,7 +578,7 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     const uint32_t bsize = 18 + clen + 8;
     if (stored) {  // BFINAL = 1, BTYPE = 00, LEN, NLEN, the bytes
         uint32_t k = 0;
-        C.bytes(p, e, [&](uint8_t b) { out[18 + 5 + (p - b0) + k++] = b; });
+        CG.bytes(p, e, [&](uint8_t b) { out[18 + 5 + (p - b0) + k++] = b; });
         if (tid == 0) {
             out[18] = 1;
             out[19] = (uint8_t)n;
