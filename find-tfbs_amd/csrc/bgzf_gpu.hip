@@ -253,7 +253,7 @@ struct Ctx {
         if (p >= e) return;
         uint32_t r = find_row(p);
         while (p < e) {
-            while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
+            while (r + 1 < g_st.P.r_first + g_st.P.n_rows && row_off(r + 1) <= p) r++;  // (the block's rows)
             const RowView v = view(r);
             const uint64_t local = p - v.R.text_off;
             if (local < v.R.head_len) {
@@ -292,7 +292,7 @@ struct Ctx {
         uint32_t r = find_row(p);
         uint32_t x = kCrc ? *crc : 0u;
         while (p < e) {
-            while (r + 1 < A.n_rows && row_off(r + 1) <= p) r++;
+            while (r + 1 < g_st.P.r_first + g_st.P.n_rows && row_off(r + 1) <= p) r++;  // (the block's rows)
             const RowView v = view(r);
             const uint64_t local = p - v.R.text_off;
             if (local < v.R.head_len) {
