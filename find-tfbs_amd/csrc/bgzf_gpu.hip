@@ -521,6 +521,7 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
         for (uint32_t i = tid; i <= kBitWords; i += kBgBlock) s_bits[i] = 0;
     }
     __syncthreads();
+    if (S.P.all) return;  // (uniform) bgzf_wave_kernel's block
     if (S.P.all) {  // (uniform: the whole block stages or none of it)
         const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
@@ -601,6 +602,337 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The wave-parallel encoder of blocks whose rows are all staged (BlockPlan::all):
+// one wave per 64-sample group of a row -- lane = sample -- so that every lane
+// does the same work (bgzf_block_kernel's thread-serial loop diverges per byte).
+// A group's sample texts get their offsets from a wave prefix sum of their
+// lengths; a text equal to the one before it (inside the block) belongs to a
+// run, the wave's runs are cut into matches of up to 258 bytes at distance =
+// the text's length (a run continuing into the next group starts a new match
+// there: one more symbol per 64 texts); another text is a match against the same
+// text among the 8 before it, or literals; texts cut by the block's edges are
+// literals.  Heads and newlines are literals.  Pass 1 counts each group's bits
+// and writes the block's bytes to LDS (for the CRC), a block scan gives every
+// group its bit offset, pass 2 writes the bits.
+constexpr int kWv = 1024;             // threads
+constexpr uint32_t kWvItems = 1024;   // heads, groups, newlines of a block (<= 2 kStRowDesc + kStCum)
+enum : uint32_t { IT_HEAD = 0u, IT_GROUP = 1u, IT_NL = 2u };
+
+__shared__ uint32_t g_bits[kBitWords + 1];
+__shared__ uint8_t g_text[kBgzfRaw];
+__shared__ uint32_t g_item[kWvItems];
+__shared__ uint32_t g_ioff[kWvItems + 1];
+__shared__ uint32_t g_red[kWv / 64];
+
+__device__ __forceinline__ void wv_put(uint32_t &off, uint32_t v, uint32_t n) {
+    if (n) {
+        const uint32_t w = off >> 5, sh = off & 31;
+        atomicOr(&g_bits[w], v << sh);
+        if (sh + n > 32) atomicOr(&g_bits[w + 1], v >> (32 - sh));
+    }
+    off += n;
+}
+__device__ __forceinline__ uint32_t lit_bits(uint32_t b) { return b < 144 ? 8u : 9u; }
+__device__ __forceinline__ void wv_lit(uint32_t &off, uint32_t b) {
+    if (b < 144) wv_put(off, rev(0x30 + b, 8), 8);
+    else wv_put(off, rev(0x190 + b - 144, 9), 9);
+}
+// RFC 1951 3.2.5 codes of a match: bits, and (kWrite) the symbols
+template <bool kWrite>
+__device__ __forceinline__ uint32_t wv_match(uint32_t &off, uint32_t len, uint32_t dist) {
+    uint32_t sym, xb = 0, xv = 0;
+    if (len == 258) {
+        sym = 285;
+    } else if (len <= 10) {
+        sym = 254 + len;
+    } else {
+        const uint32_t x = len - 3, nb = 31 - __builtin_clz(x);
+        sym = 257 + 4 * (nb - 1) + ((x >> (nb - 2)) & 3u);
+        xb = nb - 2;
+        xv = x & ((1u << xb) - 1u);
+    }
+    uint32_t dc, db = 0, dv = 0;
+    if (dist <= 4) {
+        dc = dist - 1;
+    } else {
+        const uint32_t x = dist - 1, nb = 31 - __builtin_clz(x);
+        dc = 2 * nb + ((x >> (nb - 1)) & 1u);
+        db = nb - 1;
+        dv = x & ((1u << db) - 1u);
+    }
+    const uint32_t sn = sym < 280 ? 7u : 8u;
+    if (kWrite) {
+        if (sym < 280) wv_put(off, rev(sym - 256, 7), 7);
+        else wv_put(off, rev(0xC0 + sym - 280, 8), 8);
+        wv_put(off, xv, xb);
+        wv_put(off, rev(dc, 5), 5);
+        wv_put(off, dv, db);
+    }
+    return sn + xb + 5 + db;
+}
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane) {
+    uint32_t x = v;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+        if (lane >= d) x += y;
+    }
+    return x - v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+    for (int d = 32; d; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d);
+    return v;
+}
+
+// One item of the block (all lanes of a wave together): its bits; kWrite: the
+// symbols at base + the lanes' prefix; !kWrite: its bytes into g_text.
+template <bool kWrite>
+__device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t item,
+                            uint32_t base, uint32_t lane) {
+    const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
+    const RowView v = C.view(g_st.P.r_first + d);
+    if (kind == IT_NL) {
+        if (lane == 0) {
+            if (kWrite) wv_lit(base, '\n');
+            else g_text[v.R.text_off + v.R.head_len + v.R.geno_len - b0] = '\n';
+        }
+        return 8;
+    }
+    if (kind == IT_HEAD) {
+        const uint64_t hs = max(b0, v.R.text_off), he = min(e, v.R.text_off + v.R.head_len);
+        uint32_t total = 0;
+        for (uint64_t q0 = hs; q0 < he; q0 += 64) {
+            const uint64_t q = q0 + lane;
+            const bool in = q < he;
+            const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
+            const uint32_t nb = in ? lit_bits(b) : 0u;
+            if (kWrite) {
+                uint32_t off = base + total + wave_excl_sum(nb, lane);
+                if (in) wv_lit(off, b);
+            } else if (in) {
+                g_text[q - b0] = (uint8_t)b;
+            }
+            total += wave_sum(nb);
+        }
+        return total;
+    }
+    // a 64-sample group
+    const uint32_t g = item & 0x7FFFFFu, N = A.n_samples;
+    const uint32_t s = g * kCumGroup + lane;
+    const bool valid = s < N;
+    uint32_t c = 0, t = 0;
+    if (valid) {
+        c = C.code(v, s);
+        t = C.tlen(v, c);
+    }
+    const uint4 tx = C.ttext(v, c);
+    // the text's first byte relative to the block start (may be negative at its edge)
+    const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + g_st.cum[v.cum_at + g - v.g_lo]) -
+                                  (int64_t)b0) + (int32_t)wave_excl_sum(t, lane);
+    const int32_t n = (int32_t)(e - b0);
+    const int32_t lo = max(rel, 0), hi = min(rel + (int32_t)t, n);
+    const bool in = valid && hi > lo;
+    const bool full = in && rel >= 0 && rel + (int32_t)t <= n;
+    uint32_t prevc = (uint32_t)__shfl_up((int)c, 1);
+    if (lane == 0) prevc = s > 0 ? C.code(v, s - 1) : 0xFFFFFFFFu;
+    const bool run = full && prevc == c && rel >= (int32_t)t && t >= 1;
+    // the wave's runs: a run's first and last texts
+    const uint64_t rm = __ballot(run);
+    const uint64_t starts = rm & ~(rm << 1), ends = rm & ~(rm >> 1);
+    const uint64_t below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t sb = starts & below, ea = ends & ~((1ull << lane) - 1ull);
+    const uint32_t sl = sb ? 63u - (uint32_t)__builtin_clzll(sb) : lane;
+    const uint32_t el = ea ? (uint32_t)__builtin_ctzll(ea) : lane;
+    const int32_t S0 = __shfl(rel, sl), S1 = __shfl(rel + (int32_t)t, el);
+    uint32_t dist = 0;
+    if (full && !run && t >= 3) {  // the same text among the 8 before it, inside the block
+        uint32_t acc = 0;
+        for (uint32_t kk = 1; kk <= kLookback && kk <= s; kk++) {
+            const uint32_t cc = C.code(v, s - kk);
+            acc += C.tlen(v, cc);
+            if (rel < (int32_t)acc) break;
+            if (cc == c) {
+                dist = acc;
+                break;
+            }
+        }
+    }
+    // the run's matches that start in this text: 258 bytes each from the run's first
+    // byte; a remainder of 1-2 bytes moves 3 - r bytes of the last whole match into a
+    // final 3-byte match
+    uint32_t m1 = 0, m2 = 0;
+    const bool runm = run && S1 - S0 >= 3;  // (texts are >= 4 bytes: every run is)
+    if (runm) {
+        const uint32_t a = (uint32_t)(rel - S0), b = a + t, Lr = (uint32_t)(S1 - S0);
+        const uint32_t nfull = Lr / 258, r = Lr % 258;
+        const uint32_t j = (a + 257) / 258;
+        if (258 * j < b) {
+            if (r == 0 || r >= 3) m1 = j < nfull ? 258u : (j == nfull ? r : 0u);
+            else m1 = j + 1 < nfull ? 258u : (j + 1 == nfull ? 255u + r : 0u);
+        }
+        if ((r == 1 || r == 2) && Lr >= 3 && a <= Lr - 3 && Lr - 3 < b) m2 = 3;
+    }
+    uint32_t nb = 0, dummy = 0;
+    if (runm) {
+        if (m1) nb += wv_match<false>(dummy, m1, t);
+        if (m2) nb += wv_match<false>(dummy, m2, t);
+    } else if (dist) {
+        nb = wv_match<false>(dummy, t, dist);
+    } else if (in) {
+        for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+    }
+    if (kWrite) {
+        uint32_t off = base + wave_excl_sum(nb, lane);
+        if (runm) {
+            if (m1) wv_match<true>(off, m1, t);
+            if (m2) wv_match<true>(off, m2, t);
+        } else if (dist) {
+            wv_match<true>(off, t, dist);
+        } else if (in) {
+            for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        }
+    } else if (in) {
+        for (int32_t q = lo; q < hi; q++) g_text[q] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
+    }
+    return wave_sum(nb);
+}
+
+__global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
+    Stage &S = g_st;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t b0 = (A.block0 + blockIdx.x) * kBgzfRaw;
+    const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
+    const uint64_t e = b0 + n;
+    {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const BlockPlan *>(A.plans) + blockIdx.x);
+        for (uint32_t i = tid; i < sizeof(BlockPlan) / 4; i += kWv) reinterpret_cast<uint32_t *>(&S.P)[i] = src[i];
+    }
+    __syncthreads();
+    if (!S.P.all) return;  // (uniform) bgzf_block_kernel's block
+    {
+        for (uint32_t i = tid; i < 256; i += kWv) S.crc_tab[i] = A.crc_tab[i];
+        for (uint32_t i = tid; i < kCrcOps * 32; i += kWv) S.crc_ops[i] = A.crc_ops[i];
+        for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = 0;
+        const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
+        for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
+        for (uint32_t k = 0; k < S.P.n_st; k++) {
+            const StRow T = S.P.st[k];
+            const DevRow R = A.rows[T.row];
+            const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
+            for (uint32_t i = tid; i < nb; i += kWv) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
+            for (uint32_t i = tid; i < R.nv; i += kWv) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
+            for (uint32_t i = tid; i < R.nv * kRowTokBytes; i += kWv)
+                S.text[T.tok_at * kRowTokBytes + i] = (uint8_t)A.tok_text[(size_t)R.tok * kRowTokBytes + i];
+            for (uint32_t i = tid; i < T.ncum; i += kWv) S.cum[T.cum_at + i] = A.cum[R.cum_off + T.g_lo + i];
+        }
+    }
+    __syncthreads();
+    // the block's items in stream order: per row its head, its groups, its newline
+    const Ctx<true> C{A, b0};
+    uint32_t my_items = 0;
+    if (tid < S.P.n_rows) {
+        const DevRow R = S.rows[tid];
+        const bool head = R.head_len && R.text_off < e && R.text_off + R.head_len > b0;
+        const uint64_t nl = R.text_off + R.head_len + R.geno_len;
+        uint32_t groups = 0;
+        for (uint32_t k = 0; k < S.P.n_st; k++)
+            if (S.P.st[k].row == S.P.r_first + tid) groups = S.P.st[k].ncum - 1;
+        my_items = (head ? 1u : 0u) + groups + ((nl >= b0 && nl < e) ? 1u : 0u);
+        g_ioff[tid] = my_items;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t at = 0;
+        for (uint32_t i = 0; i < S.P.n_rows; i++) {
+            const uint32_t c = g_ioff[i];
+            g_ioff[i] = at;
+            at += c;
+        }
+        g_ioff[kWvItems] = at;
+    }
+    __syncthreads();
+    if (tid < S.P.n_rows) {
+        const DevRow R = S.rows[tid];
+        uint32_t at = g_ioff[tid];
+        if (R.head_len && R.text_off < e && R.text_off + R.head_len > b0) g_item[at++] = (IT_HEAD << 30) | (tid << 23);
+        for (uint32_t k = 0; k < S.P.n_st; k++)
+            if (S.P.st[k].row == S.P.r_first + tid)
+                for (uint32_t q = 0; q + 1 < S.P.st[k].ncum; q++)
+                    g_item[at++] = (IT_GROUP << 30) | (tid << 23) | (S.P.st[k].g_lo + q);
+        const uint64_t nl = R.text_off + R.head_len + R.geno_len;
+        if (nl >= b0 && nl < e) g_item[at++] = (IT_NL << 30) | (tid << 23);
+    }
+    __syncthreads();
+    const uint32_t n_items = g_ioff[kWvItems];
+    // pass 1: each item's bits; the block's bytes into g_text
+    for (uint32_t i = wave; i < n_items; i += kWv / 64) {
+        const uint32_t nb = wv_item<false>(A, C, b0, e, g_item[i], 0, lane);
+        if (lane == 0) g_ioff[i] = nb;
+    }
+    __syncthreads();
+    // exclusive scan of the items' bits (n_items <= kWv)
+    {
+        const uint32_t v = tid < n_items ? g_ioff[tid] : 0u;
+        const uint32_t x = wave_excl_sum(v, lane);
+        if (lane == 63) g_red[wave] = x + v;
+        __syncthreads();
+        uint32_t carry = 0;
+        for (uint32_t w = 0; w < wave; w++) carry += g_red[w];
+        __syncthreads();
+        if (tid < n_items) g_ioff[tid] = carry + x;
+        if (tid == kWv - 1) g_ioff[kWvItems] = carry + x + v;
+    }
+    __syncthreads();
+    const uint32_t total_bits = 3 + g_ioff[kWvItems] + 7;  // BFINAL + BTYPE, symbols, end of block
+    const uint32_t dbytes = (total_bits + 7) / 8;
+    const bool stored = dbytes > 4 * kBitWords;
+    if (!stored) {  // pass 2: the bits at their offsets
+        if (tid == 0) g_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
+        __syncthreads();
+        for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item<true>(A, C, b0, e, g_item[i], 3 + g_ioff[i], lane);
+    }
+    // the CRC32 of the block's bytes: 64 per thread, shifted to the block end, XORed
+    {
+        const uint32_t q0 = min(n, tid * 64u), q1 = min(n, q0 + 64u);
+        uint32_t crc = 0;
+        for (uint32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[q]);
+        crc = crc_shift_lds(S.crc_ops, crc, n - q1);
+        for (int dd = 32; dd; dd >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, dd);
+        __syncthreads();
+        if (lane == 0) g_red[wave] = crc;
+        __syncthreads();
+    }
+    uint8_t *out = A.out + (size_t)blockIdx.x * kBgzfMax;
+    const uint32_t clen = stored ? 5 + n : dbytes;
+    const uint32_t bsize = 18 + clen + 8;
+    if (stored) {  // BFINAL = 1, BTYPE = 00, LEN, NLEN, the bytes
+        for (uint32_t i = tid; i < n; i += kWv) out[23 + i] = g_text[i];
+        if (tid == 0) {
+            out[18] = 1;
+            out[19] = (uint8_t)n;
+            out[20] = (uint8_t)(n >> 8);
+            out[21] = (uint8_t)~n;
+            out[22] = (uint8_t)(~n >> 8);
+        }
+    } else {
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(g_bits);
+        for (uint32_t i = tid; i < dbytes; i += kWv) out[18 + i] = src[i];
+    }
+    if (tid == 0) {
+        uint32_t x = 0;
+        for (uint32_t w = 0; w < kWv / 64; w++) x ^= g_red[w];
+        const uint32_t crc32 = x ^ crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
+        const uint8_t hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0,
+                                 (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+        for (int i = 0; i < 18; i++) out[i] = hdr[i];
+        for (int i = 0; i < 4; i++) out[18 + clen + i] = (uint8_t)(crc32 >> (8 * i));
+        for (int i = 0; i < 4; i++) out[18 + clen + 4 + i] = (uint8_t)(n >> (8 * i));
+        A.out_len[blockIdx.x] = bsize;
+    }
+}
+
 // off[i] = the sizes of blocks before i, off[nb] = their total (one workgroup).
 __global__ __launch_bounds__(1024) void bgzf_offsets_kernel(const uint32_t *__restrict__ len, uint32_t nb,
                                                             uint64_t *__restrict__ off) {
@@ -669,6 +1001,7 @@ size_t bgzf_plan_bytes() { return sizeof(BlockPlan); }
 int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream) {
     if (n_blocks == 0) return TFBS_OK;
     hipLaunchKernelGGL(bgzf_plan_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, stream, a, n_blocks);
+    hipLaunchKernelGGL(bgzf_wave_kernel, dim3(n_blocks), dim3(kWv), 0, stream, a);
     hipLaunchKernelGGL(bgzf_block_kernel, dim3(n_blocks), dim3(kBgBlock), 0, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_block_kernel: ") + hipGetErrorString(e));
