@@ -672,17 +672,20 @@ __device__ __forceinline__ uint32_t wv_match(uint32_t &off, uint32_t len, uint32
     return sn + xb + 5 + db;
 }
 
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane) {
-    uint32_t x = v;
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-        if (lane >= d) x += y;
-    }
-    return x - v;
+// wave64 inclusive prefix sum with DPP (GFX9 row shifts within 16 lanes, then the
+// row_bcast:15 / row_bcast:31 carries across rows): no LDS permutes
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
 }
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t) { return wave_incl_sum(v) - v; }
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-    for (int d = 32; d; d >>= 1) v += (uint32_t)__shfl_xor((int)v, d);
-    return v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
 }
 
 // One item of the block (all lanes of a wave together): its bits; kWrite: the
@@ -893,12 +896,19 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         __syncthreads();
         for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item<true>(A, C, b0, e, g_item[i], 3 + g_ioff[i], lane);
     }
-    // the CRC32 of the block's bytes: 64 per thread, shifted to the block end, XORed
+    // the CRC32 of the block's bytes: 64 per thread counted from the block's end (so
+    // that thread t's CRC shifts by 64 (kWv - 1 - t) bytes: one operator of the
+    // table), XORed
     {
-        const uint32_t q0 = min(n, tid * 64u), q1 = min(n, q0 + 64u);
+        const int32_t q1 = (int32_t)n - 64 * (kWv - 1 - (int32_t)tid), q0 = max(0, q1 - 64);
         uint32_t crc = 0;
-        for (uint32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[q]);
-        crc = crc_shift_lds(S.crc_ops, crc, n - q1);
+        for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[q]);
+        {
+            const uint32_t *M = A.crc_ops64 + 32 * (kWv - 1 - tid);
+            uint32_t r = 0;
+            for (uint32_t i = 0; i < 32; i++) r ^= ((crc >> i) & 1u) ? M[i] : 0u;
+            crc = r;
+        }
         for (int dd = 32; dd; dd >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, dd);
         __syncthreads();
         if (lane == 0) g_red[wave] = crc;
@@ -968,7 +978,7 @@ __global__ __launch_bounds__(256) void bgzf_compact_kernel(const uint8_t *__rest
 
 }  // namespace
 
-void bgzf_crc_tables(uint32_t *tab, uint32_t *ops) {
+void bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *ops64) {
     for (uint32_t i = 0; i < 256; i++) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
@@ -986,7 +996,19 @@ void bgzf_crc_tables(uint32_t *tab, uint32_t *ops) {
                 if ((v >> j) & 1u) r ^= ops[32 * (k - 1) + j];
             ops[32 * k + i] = r;
         }
+    // shifts by 64 k bytes, k < kWv: identity, then each the one before composed with 64 bytes
+    for (uint32_t i = 0; i < 32; i++) ops64[i] = 1u << i;
+    const uint32_t *M64 = ops + 32 * 6;
+    for (uint32_t k = 1; k < (uint32_t)kWv; k++)
+        for (uint32_t i = 0; i < 32; i++) {
+            uint32_t v = ops64[32 * (k - 1) + i], r = 0;
+            for (uint32_t j = 0; j < 32; j++)
+                if ((v >> j) & 1u) r ^= M64[j];
+            ops64[32 * k + i] = r;
+        }
 }
+
+uint32_t bgzf_crc_ops64_count() { return (uint32_t)kWv; }
 
 int launch_row_cum(const BgArgs &a, hipStream_t stream) {
     if (a.n_rows == 0) return TFBS_OK;

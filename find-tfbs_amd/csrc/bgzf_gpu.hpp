@@ -27,12 +27,14 @@ struct BgArgs {
     uint32_t *out_len;          // the blocks' sizes
     const uint32_t *crc_tab;    // CRC32 byte table
     const uint32_t *crc_ops;    // kBgzfOps x 32 columns
+    const uint32_t *crc_ops64;  // bgzf_crc_ops64_count() x 32 columns: shifts by 64 k bytes
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
 };
 size_t bgzf_plan_bytes();
 
 // CRC32 table and the x^(8 * 2^k) operators (host side, uploaded once).
-void bgzf_crc_tables(uint32_t *tab, uint32_t *ops);
+uint32_t bgzf_crc_ops64_count();
+void bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *ops64);
 // Per row: its genotype text offsets every 64 samples.
 int launch_row_cum(const BgArgs &a, hipStream_t stream);
 // Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a

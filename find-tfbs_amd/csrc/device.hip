@@ -845,8 +845,8 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
     uint64_t written = 0;
     if (n_blocks) {
         if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
-            std::vector<uint32_t> t(256 + 32 * kBgzfOps);
-            tfbs::bgzf_crc_tables(t.data(), t.data() + 256);
+            std::vector<uint32_t> t(256 + 32 * kBgzfOps + 32 * tfbs::bgzf_crc_ops64_count());
+            tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
             if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
         }
         std::vector<char> heads(plan.heads.begin(), plan.heads.end());
@@ -867,6 +867,7 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         a.text_bytes = plan.text_bytes;
         a.crc_tab = ctx->bg_crc.p;
         a.crc_ops = ctx->bg_crc.p + 256;
+        a.crc_ops64 = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
         if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
         // batches of blocks in two slots: while the device makes batch i, the host copies
         // batch i - 1's packed blocks back (copy stream) and writes them to fd
