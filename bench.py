@@ -36,6 +36,7 @@ tools/profile_round.sh) and the CPU baseline (the oracle, scan-only and
 end-to-end, 1 thread and the box's share of threads).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -356,6 +357,8 @@ def main():
             n_row_bytes += nb
             n_bgzf += nw
         os.close(devnull)
+        rows_split = (ctypes.c_double * 2)()
+        T.check(L.tfbs_ctx_rows_bgzf_seconds(sc.h, rows_split))
         host_bgzf = host_bgzf_sample(T, batch, sc, threads)
 
     # ---- timed scan loop
@@ -493,7 +496,9 @@ def main():
                 "rank0_phases_s": {"host_prep_wall": prep_wall, "synthetic_generation_wall": fill_s - prep_wall,
                                    "synthetic_generation_thread_s": gen_s, "build_region_thread_s": build_s,
                                    "upload": t_up, "scan": t_scan1, "key_reduce": t_red,
-                                   "device_encode": t_enc, "rows_bgzf": t_rows},
+                                   "device_encode": t_enc, "rows_bgzf": t_rows,
+                                   "rows_bgzf_host_plan": rows_split[0] if not args.no_e2e else 0.0,
+                                   "rows_bgzf_device_and_write": rows_split[1] if not args.no_e2e else 0.0},
                 "rows": int(tot_rows),
                 "regions_grouped_on_device": int(dev_regions),
                 "regions_built_on_host": int(host_regions),

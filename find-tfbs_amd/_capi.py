@@ -107,6 +107,7 @@ SIGNATURES = [
     ("tfbs_batch_reduce", C.c_int, [vp, vp]),
     ("tfbs_batch_encode", C.c_int, [vp, vp, C.c_size_t, C.c_size_t]),
     ("tfbs_batch_encode_flags", C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_int]),
+    ("tfbs_ctx_rows_bgzf_seconds", C.c_int, [vp, C.POINTER(C.c_double)]),
     ("tfbs_batch_rows_bgzf", C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_char_p, C.c_uint32, u32p, C.c_int,
                                        u64p, u64p, u64p]),
     ("tfbs_batch_region_num_keys", C.c_int, [vp, C.c_size_t, C.POINTER(C.c_size_t)]),

@@ -185,8 +185,8 @@ static int encoded_genotypes(const Batch &B, uint32_t e, uint32_t mult, uint32_t
     const EncHdr &h = B.enc_hdr[e];
     if ((uint64_t)h.hi * mult > UINT32_MAX) return -1;
     if (h.n_vals < 2) return 0;
-    const uint32_t *vals = B.enc_vals.data() + (size_t)e * (kEncMaxVals + 1);
-    const uint32_t *hist = B.enc_hist.data() + (size_t)e * (kEncMaxVals + 1);
+    const uint32_t *vals = B.enc_vals.data() + B.enc_val_off[e];
+    const uint32_t *hist = B.enc_hist.data() + B.enc_val_off[e];
     const uint32_t nv = h.n_vals, lo = vals[0] * mult, hi = vals[nv - 1] * mult;
     const uint32_t i1 = (lo * 1000u * 3u + hi * 1000u) / 4u;  // u32, wrapping as --release
     const uint32_t i3 = (lo * 1000u + hi * 1000u * 3u) / 4u;

@@ -128,7 +128,8 @@ struct Batch {
     uint32_t enc_r0 = 0, enc_r1 = 0;
     std::vector<uint32_t> enc_idx;
     std::vector<EncHdr> enc_hdr;
-    std::vector<uint32_t> enc_vals, enc_hist;  // (kEncMaxVals + 1) per encoded key
+    std::vector<uint32_t> enc_vals, enc_hist;  // per encoded key its n_vals entries at enc_val_off[key]
+    std::vector<uint32_t> enc_val_off;         // per encoded key, + the end
     PinnedBytes enc_codes;                     // packed codes of every encoded key, back to back
     bool enc_codes_host = true;                // enc_codes downloaded (not with TFBS_ENC_DEVICE_CODES)
     std::vector<uint64_t> enc_code_off;        // per encoded key, + the end

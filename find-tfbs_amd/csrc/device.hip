@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cerrno>
+#include <chrono>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -136,7 +137,8 @@ struct tfbs_ctx {
     uint32_t host_threads = 16;      // host threads of tfbs_batch_encode (tfbs_ctx_set_host_threads)
     DevBuf<uint64_t> enc_off;
     DevBuf<EncHdr> enc_hdr;
-    DevBuf<uint32_t> enc_vals, enc_hist;
+    DevBuf<uint32_t> enc_vals, enc_hist;  // kEncMaxVals + 1 per key
+    DevBuf<uint32_t> enc_vals_c, enc_hist_c, enc_val_off;  // compacted for the download
     // device BGZF rows (tfbs_batch_rows_bgzf)
     DevBuf<DevRow> bg_rows;
     DevBuf<char> bg_heads, bg_tok_text;
@@ -150,6 +152,7 @@ struct tfbs_ctx {
     uint64_t *bg_total_host = nullptr;  // pinned: each slot's packed bytes
     hipEvent_t bg_done[2] = {}, bg_copied[2] = {};
     hipStream_t copy_stream = nullptr;
+    double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
     float last_ms = 0.f;
@@ -407,6 +410,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_rows.release(); ctx->enc_codes.release();
     ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
+    ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
     ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release();
     for (int k = 0; k < 2; k++) {
@@ -545,6 +549,13 @@ float tfbs_ctx_last_scan_ms(const tfbs_ctx *ctx) {
 }
 
 int tfbs_ctx_last_scan_launches(const tfbs_ctx *ctx) { return ctx ? ctx->last_launches : 0; }
+
+int tfbs_ctx_rows_bgzf_seconds(const tfbs_ctx *ctx, double *out) {
+    if (!ctx || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    out[0] = ctx->rows_s[0];
+    out[1] = ctx->rows_s[1];
+    return TFBS_OK;
+}
 
 float tfbs_ctx_last_mfma_ms(const tfbs_ctx *ctx) {
     if (!ctx) return -1.f;
@@ -710,6 +721,7 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     B.enc_hdr.clear();
     B.enc_vals.clear();
     B.enc_hist.clear();
+    B.enc_val_off.assign(1, 0);
     B.enc_code_off.assign(1, 0);
     const uint32_t N = B.n_samples, H = 2 * N;
     if (N == 0 || r0 == r1) {
@@ -788,22 +800,35 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
                                 ctx->enc_hist.p, ctx->enc_codes.p, ctx->stream)))
         return rc;
     B.enc_hdr.resize(nk);
-    B.enc_vals.resize(nk * (kEncMaxVals + 1));
-    B.enc_hist.resize(nk * (kEncMaxVals + 1));
+    B.enc_val_off.assign(nk + 1, 0);
     if (nk) {
         HIP_TRY(hipMemcpyAsync(B.enc_hdr.data(), ctx->enc_hdr.p, nk * sizeof(EncHdr), hipMemcpyDeviceToHost,
                                ctx->stream));
-        HIP_TRY(hipMemcpyAsync(B.enc_vals.data(), ctx->enc_vals.p, B.enc_vals.size() * 4, hipMemcpyDeviceToHost,
-                               ctx->stream));
-        HIP_TRY(hipMemcpyAsync(B.enc_hist.data(), ctx->enc_hist.p, B.enc_hist.size() * 4, hipMemcpyDeviceToHost,
-                               ctx->stream));
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        // the packed codes back to back (a key's width is known only now), one download
+        // the value tables and histograms, and the packed codes, back to back (a key's
+        // number of values and code width are known only now)
         B.enc_code_off.resize(nk + 1);
         for (size_t k = 0; k < nk; k++) {
             const EncHdr &h = B.enc_hdr[k];
             const uint64_t bytes = h.status ? 0 : ((uint64_t)N * h.width + 7) / 8;
             B.enc_code_off[k + 1] = B.enc_code_off[k] + bytes;
+            B.enc_val_off[k + 1] = B.enc_val_off[k] + (h.status ? 0u : h.n_vals);
+        }
+        const uint32_t nv_tot = B.enc_val_off[nk];
+        if ((rc = ctx->enc_val_off.put(B.enc_val_off, ctx->stream)) ||
+            (rc = ctx->enc_vals_c.ensure(std::max<uint32_t>(nv_tot, 1))) ||
+            (rc = ctx->enc_hist_c.ensure(std::max<uint32_t>(nv_tot, 1))))
+            return rc;
+        if ((rc = launch_val_compact(ctx->enc_vals.p, ctx->enc_hist.p, (uint32_t)nk, ctx->enc_val_off.p,
+                                     ctx->enc_vals_c.p, ctx->enc_hist_c.p, ctx->stream)))
+            return rc;
+        B.enc_vals.resize(nv_tot);
+        B.enc_hist.resize(nv_tot);
+        if (nv_tot) {
+            HIP_TRY(hipMemcpyAsync(B.enc_vals.data(), ctx->enc_vals_c.p, (size_t)nv_tot * 4, hipMemcpyDeviceToHost,
+                                   ctx->stream));
+            HIP_TRY(hipMemcpyAsync(B.enc_hist.data(), ctx->enc_hist_c.p, (size_t)nv_tot * 4, hipMemcpyDeviceToHost,
+                                   ctx->stream));
         }
         const uint64_t total = B.enc_code_off[nk];
         if ((rc = ctx->enc_off.put(B.enc_code_off, ctx->stream)) ||
@@ -833,9 +858,19 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
     if (!B.reduced || B.enc_r0 > r0 || B.enc_r1 < r1)
         return tfbs::fail(TFBS_E_STATE, "regions not encoded on this ctx (tfbs_batch_encode)");
     HIP_TRY(hipSetDevice(ctx->device));
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = now();
     tfbs::RowPlan plan;
     int rc;
     if ((rc = tfbs::build_row_plan(B, r0, r1, chromosome, min_maf, fake_position, ctx->host_threads, plan))) return rc;
+    const double t1 = now();
+    ctx->rows_s[0] += t1 - t0;
+    struct Done {  // the device part's seconds, on every exit
+        tfbs_ctx *c;
+        double t;
+        double (*f)();
+        ~Done() { c->rows_s[1] += f() - t; }
+    } done{ctx, t1, +[] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }};
     const uint32_t N = B.n_samples, ng = (N + kCumGroup - 1) / kCumGroup;
     const uint64_t n_blocks = (plan.text_bytes + kBgzfRaw - 1) / kBgzfRaw;
     if ((uint64_t)plan.rows.size() * (ng + 1) >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many rows in one call");

@@ -647,7 +647,29 @@ __global__ __launch_bounds__(256) void code_compact_kernel(const uint8_t *__rest
     for (uint64_t i = threadIdx.x; i < n; i += 256) dst[o + i] = src[i];
 }
 
+// Each key's n_vals value-table entries and histogram counts (of kEncMaxVals + 1
+// slots) back to back at off[k].
+__global__ __launch_bounds__(64) void val_compact_kernel(const uint32_t *__restrict__ vals,
+                                                         const uint32_t *__restrict__ hist,
+                                                         const uint32_t *__restrict__ off, uint32_t *__restrict__ ov,
+                                                         uint32_t *__restrict__ oh) {
+    const uint32_t k = blockIdx.x, o = off[k], n = off[k + 1] - o;
+    for (uint32_t i = threadIdx.x; i < n; i += 64) {
+        ov[o + i] = vals[(size_t)k * (kEncMaxVals + 1) + i];
+        oh[o + i] = hist[(size_t)k * (kEncMaxVals + 1) + i];
+    }
+}
+
 }  // namespace
+
+int launch_val_compact(const uint32_t *vals, const uint32_t *hist, uint32_t n_keys, const uint32_t *off, uint32_t *ov,
+                       uint32_t *oh, hipStream_t stream) {
+    if (n_keys == 0) return TFBS_OK;
+    hipLaunchKernelGGL(val_compact_kernel, dim3(n_keys), dim3(64), 0, stream, vals, hist, off, ov, oh);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("val_compact_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
 
 int launch_pair_table(const uint64_t *rows, uint32_t n_regions, uint32_t n_samples, uint32_t *pab, uint32_t *pcnt,
                       uint32_t *pair_n, uint16_t *pidx, hipStream_t stream) {

@@ -67,6 +67,9 @@ int launch_key_encode(const uint32_t *var_counts, const DevVarKey *keys, uint32_
                       const uint32_t *pcnt, const uint32_t *pair_n, const uint16_t *pidx, uint32_t region0,
                       uint32_t n_samples, EncHdr *hdr, uint32_t *vals, uint32_t *hist, uint8_t *codes,
                       hipStream_t stream);
+// Key k's first (off[k + 1] - off[k]) value-table and histogram entries to off[k] of ov / oh.
+int launch_val_compact(const uint32_t *vals, const uint32_t *hist, uint32_t n_keys, const uint32_t *off, uint32_t *ov,
+                       uint32_t *oh, hipStream_t stream);
 int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_samples, const uint64_t *off, uint8_t *dst,
                         hipStream_t stream);
 

@@ -271,6 +271,9 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
 int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
                          uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
                          uint64_t *text_bytes);
+/* Seconds spent in tfbs_batch_rows_bgzf on this ctx so far: out[0] the row plan on
+ * the host (heads, token tables), out[1] the rest (uploads, kernels, copy-back, write). */
+int tfbs_ctx_rows_bgzf_seconds(const tfbs_ctx *ctx, double *out);
 
 /* After download: count_matches_by_sample (main.rs:500-534), keys ordered by
  * (inner.start, inner.end, bed basename, pattern_id).  keys are per region. */
