@@ -620,27 +620,53 @@ constexpr uint32_t kWvItems = 1024;   // heads, groups, newlines of a block (<= 
 enum : uint32_t { IT_HEAD = 0u, IT_GROUP = 1u, IT_NL = 2u };
 
 __shared__ uint32_t g_bits[kBitWords + 1];
-__shared__ uint8_t g_text[kBgzfRaw];
+// the block's bytes, 4 bytes of padding after every 64 (so that the CRC's 64-byte
+// slices, one per lane, start in different banks): byte q at txt_at(q)
+alignas(16) __shared__ uint8_t g_text[kBgzfRaw + kBgzfRaw / 16 + 16];
+__device__ __forceinline__ uint32_t txt_at(uint32_t q) { return q + ((q >> 6) << 2); }
 __shared__ uint32_t g_item[kWvItems];
 __shared__ uint32_t g_ioff[kWvItems + 1];
 __shared__ uint32_t g_red[kWv / 64];
 
-__device__ __forceinline__ void wv_put(uint32_t &off, uint32_t v, uint32_t n) {
-    if (n) {
+// A lane's bit stream: symbols gathered in a register, ORed into g_bits 32 bits at
+// a time (two LDS atomics at most per 32 bits, not per symbol)
+struct LaneBits {
+    uint64_t acc;
+    uint32_t n, off;  // bits held; the stream offset of the first
+    __device__ void out(uint32_t v, uint32_t nb) {
         const uint32_t w = off >> 5, sh = off & 31;
         atomicOr(&g_bits[w], v << sh);
-        if (sh + n > 32) atomicOr(&g_bits[w + 1], v >> (32 - sh));
+        if (sh + nb > 32) atomicOr(&g_bits[w + 1], v >> (32 - sh));
     }
-    off += n;
+    __device__ void put(uint32_t v, uint32_t nb) {  // nb <= 16
+        acc |= (uint64_t)v << n;
+        n += nb;
+        if (n >= 32) {
+            out((uint32_t)acc, 32);
+            off += 32;
+            acc >>= 32;
+            n -= 32;
+        }
+    }
+    __device__ void finish() {
+        if (n) out((uint32_t)acc & (n == 32 ? ~0u : ((1u << n) - 1u)), n);
+        off += n;
+        acc = 0;
+        n = 0;
+    }
+};
+
+__device__ __forceinline__ void wv_put(LaneBits &o, uint32_t v, uint32_t n) {
+    if (n) o.put(v, n);
 }
 __device__ __forceinline__ uint32_t lit_bits(uint32_t b) { return b < 144 ? 8u : 9u; }
-__device__ __forceinline__ void wv_lit(uint32_t &off, uint32_t b) {
-    if (b < 144) wv_put(off, rev(0x30 + b, 8), 8);
-    else wv_put(off, rev(0x190 + b - 144, 9), 9);
+__device__ __forceinline__ void wv_lit(LaneBits &o, uint32_t b) {
+    if (b < 144) wv_put(o, rev(0x30 + b, 8), 8);
+    else wv_put(o, rev(0x190 + b - 144, 9), 9);
 }
 // RFC 1951 3.2.5 codes of a match: bits, and (kWrite) the symbols
 template <bool kWrite>
-__device__ __forceinline__ uint32_t wv_match(uint32_t &off, uint32_t len, uint32_t dist) {
+__device__ __forceinline__ uint32_t wv_match(LaneBits &off, uint32_t len, uint32_t dist) {
     uint32_t sym, xb = 0, xv = 0;
     if (len == 258) {
         sym = 285;
@@ -697,8 +723,12 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
     const RowView v = C.view(g_st.P.r_first + d);
     if (kind == IT_NL) {
         if (lane == 0) {
-            if (kWrite) wv_lit(base, '\n');
-            else g_text[v.R.text_off + v.R.head_len + v.R.geno_len - b0] = '\n';
+            if (kWrite) {
+                LaneBits o{0, 0, base};
+                wv_lit(o, '\n');
+                o.finish();
+            }
+            else g_text[txt_at((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0))] = '\n';
         }
         return 8;
     }
@@ -711,10 +741,11 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
             const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
             const uint32_t nb = in ? lit_bits(b) : 0u;
             if (kWrite) {
-                uint32_t off = base + total + wave_excl_sum(nb, lane);
-                if (in) wv_lit(off, b);
+                LaneBits o{0, 0, base + total + wave_excl_sum(nb, lane)};
+                if (in) wv_lit(o, b);
+                o.finish();
             } else if (in) {
-                g_text[q - b0] = (uint8_t)b;
+                g_text[txt_at((uint32_t)(q - b0))] = (uint8_t)b;
             }
             total += wave_sum(nb);
         }
@@ -776,7 +807,8 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         }
         if ((r == 1 || r == 2) && Lr >= 3 && a <= Lr - 3 && Lr - 3 < b) m2 = 3;
     }
-    uint32_t nb = 0, dummy = 0;
+    uint32_t nb = 0;
+    LaneBits dummy{0, 0, 0};
     if (runm) {
         if (m1) nb += wv_match<false>(dummy, m1, t);
         if (m2) nb += wv_match<false>(dummy, m2, t);
@@ -786,7 +818,7 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
     if (kWrite) {
-        uint32_t off = base + wave_excl_sum(nb, lane);
+        LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
         if (runm) {
             if (m1) wv_match<true>(off, m1, t);
             if (m2) wv_match<true>(off, m2, t);
@@ -795,8 +827,9 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         } else if (in) {
             for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
         }
+        off.finish();
     } else if (in) {
-        for (int32_t q = lo; q < hi; q++) g_text[q] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
+        for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
     }
     return wave_sum(nb);
 }
@@ -902,7 +935,18 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     {
         const int32_t q1 = (int32_t)n - 64 * (kWv - 1 - (int32_t)tid), q0 = max(0, q1 - 64);
         uint32_t crc = 0;
-        for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[q]);
+        if (q1 - q0 == 64 && (q0 & 63) == 0) {  // a whole padded slice: dword reads, no bank conflicts
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(g_text) + (txt_at((uint32_t)q0) >> 2);
+            for (uint32_t i = 0; i < 16; i++) {
+                const uint32_t x = w[i];
+                crc = crc_byte(S.crc_tab, crc, x & 0xFFu);
+                crc = crc_byte(S.crc_tab, crc, (x >> 8) & 0xFFu);
+                crc = crc_byte(S.crc_tab, crc, (x >> 16) & 0xFFu);
+                crc = crc_byte(S.crc_tab, crc, x >> 24);
+            }
+        } else {
+            for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[txt_at((uint32_t)q)]);
+        }
         {
             const uint32_t *M = A.crc_ops64 + 32 * (kWv - 1 - tid);
             uint32_t r = 0;
@@ -918,7 +962,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     const uint32_t clen = stored ? 5 + n : dbytes;
     const uint32_t bsize = 18 + clen + 8;
     if (stored) {  // BFINAL = 1, BTYPE = 00, LEN, NLEN, the bytes
-        for (uint32_t i = tid; i < n; i += kWv) out[23 + i] = g_text[i];
+        for (uint32_t i = tid; i < n; i += kWv) out[23 + i] = g_text[txt_at(i)];
         if (tid == 0) {
             out[18] = 1;
             out[19] = (uint8_t)n;
