@@ -290,9 +290,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if rank != 0:  # one JSON line on stdout: the other ranks' output (library chatter included) to stderr
-        sys.stdout.flush()
-        os.dup2(2, 1)
+    # one JSON line on stdout, from rank 0: every rank's other output (library chatter
+    # such as gloo's connection messages included) goes to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w") if rank == 0 else None
+    os.dup2(2, 1)
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE %d" % (args.gpus, world))
     dist = None
@@ -513,7 +515,7 @@ def main():
         }
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = cpu_baseline(T, ps, args, args.cpu_seconds)
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     sc.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -706,7 +706,10 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         dr.n_inner = (uint32_t)R.ranges.size();
         dr.hap_begin = R.hap_begin;
         dr.hap_count = R.hap_count;
-        dr.ref_hap = ref >= 0 && B.dedup ? R.hap_begin + (uint32_t)ref : UINT32_MAX;
+        // the reference's hits are listed only when some haplotype reuses them
+        bool reused = false;
+        for (const HapInfo &h : info[j]) reused = reused || h.dedup;
+        dr.ref_hap = ref >= 0 && B.dedup && reused ? R.hap_begin + (uint32_t)ref : UINT32_MAX;
         dr.count_stride = (uint32_t)rb.n_haps();
         R.key_off = (uint64_t)dr.inner_off * B.n_slots;
         size_t ii = o.inner;
