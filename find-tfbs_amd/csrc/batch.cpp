@@ -100,8 +100,8 @@ int patch(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const uin
 }
 
 uint64_t Batch::device_bytes() const {
-    return words.size() * 4ull + nmask.size() * 4ull + posrel.size() * 4ull + haps.size() * sizeof(DevHap) +
-           regions.size() * sizeof(DevRegion) + inner.size() * 4ull;
+    return words.size() * 4ull + nmask.size() * 4ull + posrel.size() * 4ull + druns.size() * 4ull +
+           haps.size() * sizeof(DevHap) + regions.size() * sizeof(DevRegion) + inner.size() * 4ull;
 }
 
 // ---------------------------------------------------------------------------
@@ -354,9 +354,9 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // group, a helper copy is scanned after the distinct haplotypes (no carriers,
     // no keys)
     // (only when the reference's windows can be reused: it and some distinct
-    // haplotype fit kDedupMaxTiles window tiles)
+    // haplotype have at most kDedupMaxWindows bases)
     out.helper = false;
-    auto fits = [](size_t n) { return (n + kMWindows - 1) / kMWindows <= kDedupMaxTiles; };
+    auto fits = [](size_t n) { return n <= kDedupMaxWindows; };
     bool reusable = false;
     for (const Distinct &d : dist) reusable = reusable || fits(d.nuc.size());
     if (B.dedup && R.ref_local < 0 && reusable && fits(I.ref.size())) {
@@ -371,7 +371,7 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     }
     // the kernels index windows with 29 bits (scan_mfma.hip queue entries)
     for (const Distinct &d : dist)
-        if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
+        if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^26 - 1 bases");
     if (B.keep_membership) {  // (hap id, local) in ascending hap id: hap_ids' order
         R.nonref_id.clear();
         R.nonref_local.clear();
@@ -449,14 +449,14 @@ static int snv_finish(const Batch &B, RegionBuilt &b, const uint64_t *masks, con
         b.carriers.push_back((uint32_t)(H - covered));
     }
     const size_t n = b.ref.size();
-    const bool fits = (n + kMWindows - 1) / kMWindows <= kDedupMaxTiles;
+    const bool fits = n <= kDedupMaxWindows;
     b.helper = false;
     if (B.dedup && R.ref_local < 0 && !b.masks.empty() && fits) {
         b.masks.push_back(0);
         b.carriers.push_back(0);
         b.helper = true;
     }
-    if (n >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
+    if (n >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^26 - 1 bases");
     R.memb_dev = memb;
     R.memb_host = false;
     R.nonref_id.clear();
@@ -588,6 +588,21 @@ int region_membership(const Batch &B, const RegionH &R) {
 // GPU.  Offsets are laid out serially (prefix sums over the regions'
 // haplotypes), the packing of bases, N masks and positions runs on `threads`
 // threads.
+// The windows [0, nw) of a HAP_DEDUP haplotype with diff runs `runs` that a depth
+// class of span S reads: those meeting a run (tfbs_internal.hpp run_meets).
+static uint64_t dirty_windows(const uint32_t *runs, size_t nruns, uint32_t S, uint32_t nw) {
+    uint64_t n = 0, next = 0;  // windows below `next` are counted
+    for (size_t k = 0; k < nruns; k += 2) {
+        const uint64_t lo = std::max<uint64_t>(next, runs[k] >= S - 1 ? runs[k] - (S - 1) : 0);
+        const uint64_t hi = std::min<uint64_t>(runs[k + 1], nw - 1);  // inclusive
+        if (hi + 1 > lo) {
+            n += hi + 1 - lo;
+            next = hi + 1;
+        }
+    }
+    return n;
+}
+
 void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads) {
     const size_t nr = built.size();
     if (!nr) return;
@@ -595,9 +610,10 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     struct HapInfo {
         uint32_t n;
         bool has_n, affine, dedup = false;
-        uint32_t dirty[4] = {0, 0, 0, 0};
+        uint32_t r0 = 0, rn = 0;  // HAP_DEDUP: its diff runs (a, b), ascending, merged: rruns[j][r0 .. r0 + rn)
     };
     std::vector<std::vector<HapInfo>> info(nr);
+    std::vector<std::vector<uint32_t>> rruns(nr);  // per region, its haplotypes' diff runs
     auto par = [&](auto fn) {
         std::atomic<size_t> next(0);
         auto work = [&]() {
@@ -627,51 +643,67 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
         }
         // reference-window reuse: a window whose bases and positions are the
-        // reference window's has its hits.  Per haplotype, the window tiles whose
-        // windows (of up to 8 nk columns) reach a column that differs from the
-        // reference -- another base, another position (past an indel), or past
-        // the end of either sequence -- are marked; the others are reused
-        // (haplotypes of up to kDedupMaxTiles tiles, the reference's too).
+        // reference window's has its hits.  Per haplotype, the runs of columns that
+        // differ from the reference -- another base, another position (past an
+        // indel), or past the end of either sequence -- are recorded; the scan reads
+        // only the windows that meet one (haplotypes and reference of up to
+        // kDedupMaxWindows bases, at most kMaxDiffRuns runs).
         const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.n_haps() - 1 : -1);
         if (!B.dedup || ref < 0) return;
-        auto mark_at = [](HapInfo &h, uint32_t p, bool to_end) {  // windows p - 8 (d + 1) + 1 .. p (.. the last tile)
-            for (uint32_t dd = 0; dd < 4; dd++) {
-                const uint32_t w0 = p + 1 >= 8 * (dd + 1) ? p + 1 - 8 * (dd + 1) : 0;
-                const uint32_t t1 = to_end ? kDedupMaxTiles - 1 : std::min(p / kMWindows, kDedupMaxTiles - 1);
-                for (uint32_t t = w0 / kMWindows; t <= t1; t++) h.dirty[dd] |= 1u << t;
+        std::vector<uint32_t> &rv = rruns[j];
+        auto start = [&](HapInfo &h) { h.r0 = (uint32_t)rv.size(); };
+        auto add = [&](HapInfo &h, uint32_t p, uint32_t e) {  // columns p .. e, appended in ascending order
+            if (rv.size() > h.r0 && (rv.back() == kRunToEnd || rv.back() + 1 >= p)) {
+                rv.back() = std::max(rv.back(), e);
+            } else {
+                rv.push_back(p);
+                rv.push_back(e);
+            }
+        };
+        auto finish = [&](HapInfo &h) {
+            h.rn = (uint32_t)rv.size() - h.r0;
+            h.dedup = h.rn / 2 <= kMaxDiffRuns;
+            if (!h.dedup) {
+                rv.resize(h.r0);
+                h.rn = 0;
             }
         };
         if (rb.dev) {  // every haplotype has the reference's length: its SNV columns differ
-            if ((rb.ref.size() + kMWindows - 1) / kMWindows > kDedupMaxTiles) return;
+            if (rb.ref.size() > kDedupMaxWindows) return;
             for (size_t i = 0; i < rb.masks.size(); i++) {
                 if ((int32_t)i == ref) continue;
                 HapInfo &h = info[j][i];
-                h.dedup = true;
-                for (uint64_t x = rb.masks[i]; x; x &= x - 1) mark_at(h, rb.snv_rel[__builtin_ctzll(x)], false);
+                start(h);
+                for (uint64_t x = rb.masks[i]; x; x &= x - 1) {
+                    const uint32_t p = rb.snv_rel[__builtin_ctzll(x)];
+                    add(h, p, p);
+                }
+                finish(h);
             }
             return;
         }
         const std::vector<uint8_t> &rn = rb.dist[ref].nuc;
-        if ((rn.size() + kMWindows - 1) / kMWindows > kDedupMaxTiles) return;
+        if (rn.size() > kDedupMaxWindows) return;
         for (size_t i = 0; i < rb.dist.size(); i++) {
             HapInfo &h = info[j][i];
-            if ((int32_t)i == ref || (h.n + kMWindows - 1) / kMWindows > kDedupMaxTiles) continue;
+            if ((int32_t)i == ref || h.n > kDedupMaxWindows) continue;
             const Distinct &d = rb.dist[i];
+            start(h);
             const uint32_t nmin = std::min<uint32_t>(h.n, (uint32_t)rn.size());
-            auto mark = [&](uint32_t p, bool to_end) { mark_at(h, p, to_end); };
-            h.dedup = true;
             for (uint32_t p = 0; p < nmin; p++)
-                if (d.nuc[p] != rn[p] || d.pos[p] != rb.R.es + p) mark(p, false);
-            if (h.n != rn.size()) mark(nmin, true);  // columns past the shorter sequence differ
+                if (d.nuc[p] != rn[p] || d.pos[p] != rb.R.es + p) add(h, p, p);
+            if (h.n != rn.size()) add(h, nmin, kRunToEnd);  // columns past the shorter sequence differ
+            finish(h);
         }
     });
     // serial layout: region / haplotype / word / mask / position offsets
     struct Off {
         size_t hap, inner;
-        uint64_t word, nmask, pos, count;
+        uint64_t word, nmask, pos, count, runs;
     };
     std::vector<Off> off(nr);
-    Off cur{B.haps.size(), B.inner.size(), B.words.size(), B.nmask.size(), B.posrel.size(), B.n_counts};
+    Off cur{B.haps.size(), B.inner.size(), B.words.size(), B.nmask.size(), B.posrel.size(), B.n_counts,
+            B.druns.size()};
     for (size_t j = 0; j < nr; j++) {
         off[j] = cur;
         const uint32_t n_inner = (uint32_t)built[j].R.ranges.size();
@@ -682,6 +714,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if (h.has_n) cur.nmask += (h.n + 31) / 32 + 2;
             if (!h.affine) cur.pos += h.n;
             cur.count += (uint64_t)B.n_slots * n_inner;
+            cur.runs += h.rn;
         }
     }
     const uint32_t region0 = (uint32_t)B.rh.size();
@@ -691,6 +724,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     B.words.resize(cur.word, 0u);
     B.nmask.resize(cur.nmask, 0u);
     B.posrel.resize(cur.pos);
+    B.druns.resize(cur.runs);
     B.regions.resize(region0 + nr);
     B.n_counts = cur.count;
     std::vector<uint64_t> win(nr, 0), eff(nr, 0), cells(nr, 0), swin(nr, 0), scells(nr, 0);
@@ -725,7 +759,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             B.inner[ii++] = rel(r.second);
         }
         B.regions[region0 + j] = dr;
-        uint64_t word = o.word, nmask = o.nmask, pos = o.pos, count = o.count;
+        uint64_t word = o.word, nmask = o.nmask, pos = o.pos, count = o.count, runs = o.runs;
         // per-region sums in registers (the arrays are shared by the threads)
         uint64_t r_win = 0, r_eff = 0, r_cells = 0, r_swin = 0, r_scells = 0;
         std::vector<uint32_t> refw;  // device-grouped: the reference window packed once
@@ -775,7 +809,10 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if (dr.ref_hap == o.hap + i) hm.flags |= HAP_REF;
             if (h.dedup) {
                 hm.flags |= HAP_DEDUP;
-                for (int d = 0; d < 4; d++) hm.dirty[d] = h.dirty[d];
+                hm.drun_off = (uint32_t)(runs / 2);
+                hm.n_druns = h.rn / 2;
+                std::copy(rruns[j].begin() + h.r0, rruns[j].begin() + h.r0 + h.rn, B.druns.begin() + runs);
+                runs += h.rn;
             }
             B.haps[o.hap + i] = hm;
             B.hap_carriers[o.hap + i] = rb.carriers[i];
@@ -786,10 +823,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                     const uint64_t nw = n - lc.first + 1;
                     uint64_t sw = nw;  // windows the scan reads
                     if (h.dedup && lc.first <= (uint32_t)(kMMaxChunks * kMChunkCols)) {
-                        const uint32_t m = h.dirty[(lc.first + kMChunkCols - 1) / kMChunkCols - 1];
-                        const uint64_t full = nw / kMWindows, rem = nw % kMWindows;  // whole tiles, then a partial one
-                        const uint32_t fm = full >= 32 ? ~0u : (1u << full) - 1;
-                        sw = (uint64_t)kMWindows * __builtin_popcount(m & fm) + (full < 32 && ((m >> full) & 1u) ? rem : 0);
+                        const uint32_t span = kMChunkCols * mfma_depth_class((lc.first + kMChunkCols - 1) / kMChunkCols);
+                        sw = dirty_windows(rruns[j].data() + h.r0, h.rn, span, (uint32_t)nw);
                     }
                     r_swin += sw * lc.second;
                     r_scells += sw * lc.first * lc.second;

@@ -103,6 +103,7 @@ struct Batch {
     std::vector<uint32_t> words;          // 2-bit bases, 16 per word, LSB first, +3 pad words per hap
     std::vector<uint32_t> nmask;          // N masks (+2 pad words per hap)
     std::vector<int32_t> posrel;          // positions relative to ext_start (non-affine haps only)
+    std::vector<uint32_t> druns;          // HAP_DEDUP haplotypes' diff runs, (a, b) pairs (tfbs_internal.hpp)
     std::vector<DevHap> haps;
     std::vector<DevRegion> regions;
     std::vector<int32_t> inner;           // (s_rel, e_rel) pairs

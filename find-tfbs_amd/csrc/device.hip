@@ -117,6 +117,12 @@ struct tfbs_ctx {
     bool counts_live = false;             // counts allocated for the resident batch
     DevBuf<int32_t> posrel, inner;
     DevBuf<DevHap> haps;
+    DevBuf<uint32_t> druns;               // HAP_DEDUP haplotypes' diff runs
+    // matrix-core window lists per depth class (ScanArgs::wlist), built at upload
+    DevBuf<uint64_t> wl_off[2], wl_tmp;
+    DevBuf<uint32_t> wl[2];
+    uint64_t wl_entries[2] = {0, 0};
+    double wl_seconds = 0;                // the last build's wall time
     DevBuf<DevRegion> regions;
     DevBuf<unsigned long long> hits;
     DevBuf<uint32_t> asm_scratch;         // key assembly counters of regions with many distinct haplotypes
@@ -194,6 +200,45 @@ static int env_int(const char *name, int dflt) {
     return atoi(v);
 }
 
+// The matrix-core window lists of the haplotypes just put on the device (one
+// per depth class the plan has; scan.hpp build_window_lists).
+static int build_lists(tfbs_ctx *ctx, uint32_t n_haps) {
+    const Plan &P = ctx->plan;
+    if (P.m_supers.empty()) return TFBS_OK;
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t lmin[2] = {0, 0};
+    for (const DevMSuper &S : P.m_supers) {
+        uint32_t &l = lmin[S.nk > 2 ? 1 : 0];
+        l = l ? std::min(l, S.lmin) : S.lmin;
+    }
+    int rc;
+    for (int c = 0; c < 2; c++)
+        if (lmin[c] && (rc = ctx->wl_off[c].ensure((size_t)n_haps + 1))) return rc;
+    if ((rc = ctx->wl_tmp.ensure(scan_tmp_words((size_t)n_haps + 1))) ||
+        (rc = ctx->druns.ensure(std::max<size_t>(ctx->druns.n, 1))))
+        return rc;
+    WindowListBufs bufs{};
+    for (int c = 0; c < 2; c++) {
+        bufs.off[c] = lmin[c] ? ctx->wl_off[c].p : nullptr;
+        bufs.list[c] = nullptr;
+    }
+    bufs.scan_tmp = ctx->wl_tmp.p;
+    auto ensure = [](void *x, int c, uint64_t n, uint32_t **p) {
+        tfbs_ctx *cx = static_cast<tfbs_ctx *>(x);
+        if (int e = cx->wl[c].ensure(n)) return e;
+        *p = cx->wl[c].p;
+        return TFBS_OK;
+    };
+    if ((rc = build_window_lists(ctx->haps.p, n_haps, ctx->druns.p, lmin, ctx->mfma_hpb, 1, bufs, ctx->wl_entries,
+                                 ctx->stream, ensure, ctx)))
+        return rc;
+    for (int c = 0; c < 2; c++)
+        if (!lmin[c]) ctx->wl_off[c].release(), ctx->wl[c].release();
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    ctx->wl_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return TFBS_OK;
+}
+
 static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits, uint32_t hits_wpp) {
     const Plan &P = ctx->plan;
     if (n_haps == 0) return 0;
@@ -247,6 +292,10 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.spill_cap = ctx->spill_cap;
         m.cand_over = ctx->cand_over.p;
         m.cand_over_cap = ctx->cand_over_cap;
+        for (int c = 0; c < 2; c++) {
+            m.wlist[c] = ctx->wl[c].p;
+            m.wlist_off[c] = ctx->wl_off[c].p;
+        }
         HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
         HIP_TRY(hipMemsetAsync(ctx->over.p, 0, 8, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
@@ -351,6 +400,7 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
 static AsmArgs asm_args(tfbs_ctx *ctx, const Batch &B, int mode) {
     AsmArgs a{};
     a.haps = ctx->haps.p;
+    a.druns = ctx->druns.p;
     a.regions = ctx->regions.p;
     a.inner = ctx->inner.p;
     a.mmeta = ctx->m_meta.p;
@@ -403,6 +453,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->over_host) (void)hipHostFree(ctx->over_host);
     if (ctx->var_tot_host) (void)hipHostFree(ctx->var_tot_host);
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
+    ctx->druns.release(); ctx->wl_tmp.release();
+    for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
     ctx->var_keys.release();
@@ -453,7 +505,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->cfg.minw = env_int("TFBS_FAST_MINW", 2) == 4 ? 4 : 2;
     ctx->mfma = env_int("TFBS_MFMA", 1) != 0;
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 44))) * 1024u;
-    ctx->mfma_hpb = (uint32_t)std::min(256, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 8 bits in a candidate entry
+    ctx->mfma_hpb = (uint32_t)std::min((int)kMMaxHapsPerBlock, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 6 bits in a window list entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
     ctx->host_threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -581,10 +633,12 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     int rc;
     if ((rc = ctx->words.put(B.words, ctx->stream)) || (rc = ctx->nmask.put(B.nmask, ctx->stream)) ||
         (rc = ctx->posrel.put(B.posrel, ctx->stream)) || (rc = ctx->haps.put(B.haps, ctx->stream)) ||
+        (rc = ctx->druns.put(B.druns, ctx->stream)) ||
         (rc = ctx->regions.put(B.regions, ctx->stream)) || (rc = ctx->inner.put(B.inner, ctx->stream)) ||
         (rc = ctx->asm_scratch.ensure(std::max<uint64_t>(big, 1))) ||
         (dense && (rc = ctx->counts.ensure(std::max<uint64_t>(B.n_counts, 1)))))
         return rc;
+    if ((rc = build_lists(ctx, (uint32_t)B.haps.size()))) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->counts_live = dense;
     ctx->resident = b;
@@ -968,7 +1022,7 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
 int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t n, uint32_t *counts,
                  uint64_t *out_start, uint64_t *out_end, size_t cap, size_t *n_total) {
     if (!ctx || !n_total || !counts || (n && (!nucs || !pos))) return tfbs::fail(TFBS_E_ARG, "null argument");
-    if (n >= kMaxHapLen) return tfbs::fail(TFBS_E_ARG, "haplotype longer than 2^29 - 1 bases");
+    if (n >= kMaxHapLen) return tfbs::fail(TFBS_E_ARG, "haplotype longer than 2^26 - 1 bases");
     const Patterns &P = *ctx->pats;
     // pack one haplotype; no inner ranges, hit bitmaps only
     std::vector<uint32_t> words((n + 15) / 16 + 3, 0u), nmask;
@@ -999,7 +1053,8 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
     if ((rc = ctx->words.put(words, ctx->stream)) || (rc = ctx->nmask.put(nmask, ctx->stream)) ||
         (rc = ctx->posrel.put(posrel, ctx->stream)) || (rc = ctx->haps.put(haps, ctx->stream)) ||
         (rc = ctx->regions.put(regions, ctx->stream)) || (rc = ctx->inner.put(inner, ctx->stream)) ||
-        (rc = ctx->counts.ensure(std::max<uint64_t>(P.pats.size(), 1))))
+        (rc = ctx->counts.ensure(std::max<uint64_t>(P.pats.size(), 1))) || (rc = ctx->druns.ensure(1)) ||
+        (rc = build_lists(ctx, 1)))
         return rc;
     ctx->counts_live = true;
     ctx->resident = nullptr;

@@ -29,7 +29,9 @@ namespace {
 constexpr int kAsmBlock = 256;
 constexpr uint32_t kAsmWaves = kAsmBlock / 64;
 constexpr uint32_t kAsmCounters = 6144;  // u32 counters of the LDS block (24 KiB)
-constexpr uint32_t kAsmHaps = 1024;      // haplotypes whose dirty masks sit in LDS (else read from L2)
+constexpr uint32_t kAsmHaps = 1024;      // haplotypes whose diff runs sit in LDS (else read from L2)
+
+constexpr uint32_t kAsmRuns = 2048;      // diff runs staged in LDS
 constexpr uint32_t kAsmHits = 2048;      // own hits staged in LDS (else re-read from the lists per pass)
 constexpr uint32_t kAsmRefs = 256;       // reference hits staged in LDS (else re-read)
 constexpr uint32_t kAsmKeyWords = 2048;  // touched-key bitmap: keys handled per key window
@@ -111,7 +113,8 @@ __device__ __forceinline__ void visit_refs(const AsmArgs &A, uint32_t r, const D
 
 __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
     __shared__ uint32_t s_cnt[kAsmCounters];
-    __shared__ uint32_t s_d[4][kAsmHaps];  // dirty window-tile masks per K depth (all set: not HAP_DEDUP)
+    __shared__ uint32_t s_rh[kAsmHaps];    // per haplotype: first staged run | runs << 16 (0xFFFFFFFF: not HAP_DEDUP)
+    __shared__ uint2 s_run[kAsmRuns];      // the region's diff runs
     __shared__ uint2 s_hit[kAsmHits];      // (local haplotype, key)
     __shared__ uint4 s_ref[kAsmRefs];      // make_ref
     __shared__ uint32_t s_bits[kAsmKeyWords], s_rbase[kAsmKeyWords];  // touched keys of the window, rows before each word
@@ -132,13 +135,28 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
         return;
     }
     const uint32_t hb = rg.hap_begin;
-    const bool lds_haps = U <= kAsmHaps;
-    if (lds_haps)
+    // the diff runs of the region's HAP_DEDUP haplotypes (consecutive in the batch's
+    // run array) in LDS when they fit
+    uint32_t run0 = 0, run1 = 0;
+    for (uint32_t l = 0; l < U; l++)  // uniform: the first and last HAP_DEDUP haplotype's runs
+        if (A.haps[hb + l].flags & HAP_DEDUP) {
+            run0 = A.haps[hb + l].drun_off;
+            break;
+        }
+    for (uint32_t l = U; l-- > 0;)
+        if (A.haps[hb + l].flags & HAP_DEDUP) {
+            run1 = A.haps[hb + l].drun_off + A.haps[hb + l].n_druns;
+            break;
+        }
+    const bool lds_haps = U <= kAsmHaps && run1 - run0 <= kAsmRuns;
+    if (lds_haps) {
         for (uint32_t l = tid; l < U; l += kAsmBlock) {
             const DevHap h = A.haps[hb + l];
-            const bool dd = (h.flags & HAP_DEDUP) != 0;
-            for (int d = 0; d < 4; d++) s_d[d][l] = dd ? h.dirty[d] : 0xFFFFFFFFu;  // not HAP_DEDUP: all scanned
+            s_rh[l] = (h.flags & HAP_DEDUP) ? (h.drun_off - run0) | (h.n_druns << 16) : 0xFFFFFFFFu;
         }
+        for (uint32_t k = tid; k < run1 - run0; k += kAsmBlock)
+            s_run[k] = make_uint2(A.druns[2 * (run0 + k)], A.druns[2 * (run0 + k) + 1]);
+    }
     const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
     // stage the region's own hits and reference hits in LDS (the lists are read once)
     if (tid == 0) s_nhit = s_nref = 0;
@@ -269,31 +287,47 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 const uint32_t t = row_of(j) - t0;
                 if (t < nrow) atomicAdd(&cnt[t * U + l], 1u);
             });
-            // reference hits: +1 to every HAP_DEDUP haplotype whose tile of the hit's
-            // window it did not scan (same bases and positions as the reference there)
-            auto dirty_of = [&](uint32_t l, uint32_t dk) {
-                return lds_haps ? s_d[dk][l]
-                                : ((A.haps[hb + l].flags & HAP_DEDUP) ? A.haps[hb + l].dirty[dk] : 0xFFFFFFFFu);
+            // reference hits: +1 to every HAP_DEDUP haplotype for which the hit's
+            // window is not dirty (the scan did not read it: same bases and positions
+            // as the reference's; tfbs_internal.hpp run_meets, span 8 x the class)
+            auto dirty = [&](uint32_t l, uint32_t dk, uint32_t w) {
+                const uint32_t S = kMChunkCols * (dk + 1);
+                if (lds_haps) {
+                    const uint32_t x = s_rh[l];
+                    if (x == 0xFFFFFFFFu) return true;
+                    for (uint32_t k = x & 0xFFFFu, e = k + (x >> 16); k < e; k++)
+                        if (run_meets(s_run[k].x, s_run[k].y, w, S)) return true;
+                    return false;
+                }
+                const DevHap &h = A.haps[hb + l];
+                if (!(h.flags & HAP_DEDUP)) return true;
+                for (uint32_t k = h.drun_off; k < h.drun_off + h.n_druns; k++)
+                    if (run_meets(A.druns[2 * k], A.druns[2 * k + 1], w, S)) return true;
+                return false;
             };
-            if (refs_on && refs_lds) {
+            if (refs_on && refs_lds && U <= 32 * kAsmBlock) {
                 for (uint32_t q0 = 0; q0 < nref; q0++) {  // workgroup-uniform; threads over the haplotypes
                     const uint4 q = s_ref[q0];
-                    const uint32_t dk = q.z >> 16, tile = q.y / kMWindows;
+                    const uint32_t dk = q.z >> 16;
+                    uint32_t keep = 0;  // bit j: haplotype tid + j kAsmBlock inherits the hit (U <= kAsmHaps)
+                    for (uint32_t l = tid, j = 0; l < U; l += kAsmBlock, j++)
+                        if (!dirty(l, dk, q.y)) keep |= 1u << j;
+                    if (__syncthreads_or(keep) == 0) continue;
                     ref_keys(q, [&](uint32_t key) {
                         const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
                         if (t >= nrow) return;
-                        for (uint32_t l = tid; l < U; l += kAsmBlock)
-                            if (!((dirty_of(l, dk) >> tile) & 1u)) atomicAdd(&cnt[t * U + l], 1u);
+                        for (uint32_t m = keep; m; m &= m - 1)
+                            atomicAdd(&cnt[t * U + tid + kAsmBlock * __builtin_ctz(m)], 1u);
                     });
                 }
             } else if (refs_on) {  // too many for LDS (rare): each thread walks its hits' haplotypes
                 visit_refs(A, r, rg, [&](const uint4 &q) {
-                    const uint32_t dk = q.z >> 16, tile = q.y / kMWindows;
+                    const uint32_t dk = q.z >> 16;
                     ref_keys(q, [&](uint32_t key) {
                         const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
                         if (t >= nrow) return;
                         for (uint32_t l = 0; l < U; l++)
-                            if (!((dirty_of(l, dk) >> tile) & 1u)) atomicAdd(&cnt[t * U + l], 1u);
+                            if (!dirty(l, dk, q.y)) atomicAdd(&cnt[t * U + l], 1u);
                     });
                 });
             }

@@ -13,6 +13,7 @@ namespace tfbs {
 // Everything key_asm_kernel reads and writes (device pointers; see key_kernels.hip).
 struct AsmArgs {
     const DevHap *haps;
+    const uint32_t *druns;  // HAP_DEDUP haplotypes' diff runs (tfbs_internal.hpp)
     const DevRegion *regions;
     const int32_t *inner;
     const int32_t *mmeta;       // matrix-core tiles' rescoring fields (strand length, slot, depth)

@@ -54,8 +54,14 @@ struct ScanArgs {
     // wave]; the excess goes to the spill list
     uint32_t *hitl;
     uint32_t *hitn;
+    // matrix-core window lists (build_window_lists), per depth class (2, 4): the
+    // windows the scan reads, haplotype-major, entry = window << 6 | the haplotype's
+    // index in its group of haps_per_block (<= 64); haplotype h's entries start at
+    // wlist_off[c][h] (n_haps + 1 offsets, relative to this launch's haps)
+    const uint32_t *wlist[2];
+    const uint64_t *wlist_off[2];
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
-    // != 0 scans only their dirty window tiles; the HAP_REF haplotypes' hits
+    // != 0 scans only their dirty windows (the lists); the HAP_REF haplotypes' hits
     // (strand, window) are listed per region (ref_count[r] of kRefPerRegion at
     // ref_hits + 2 kRefPerRegion r), the excess in the spill list
     uint32_t dedup;
@@ -105,6 +111,22 @@ int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, u
 // Rescores the candidates past the waves' lists (after launch_mfma on the same stream).
 int launch_post_scan(const ScanArgs &a, hipStream_t stream);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
+constexpr uint32_t kMMaxHapsPerBlock = 64;  // 6 bits of a window list entry
+// Builds the window lists of every haplotype of the batch for the depth classes
+// c (0: class 2, 1: class 4) with lmin[c] != 0 (the class's shortest strand):
+// all windows [0, len - lmin + 1) of a haplotype, only the dirty ones of a
+// HAP_DEDUP haplotype when dedup (tfbs_internal.hpp); off[c] gets n_haps + 1
+// offsets, list[c] (grown with ensure_list) the entries.  Synchronises `stream`.
+struct WindowListBufs {
+    uint64_t *off[2];      // n_haps + 1 each
+    uint64_t *scan_tmp;    // >= scan_tmp_words(n_haps + 1)
+    uint32_t *list[2];
+    uint64_t list_cap[2];  // entries
+};
+size_t scan_tmp_words(size_t n);
+int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
+                       uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
+                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p), void *ensure_ctx);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach
 // the waves per SIMD its registers allow.
 void mfma_depth_budgets(uint32_t out[9]);

@@ -62,16 +62,20 @@ constexpr uint32_t kTestMask = (1u << (kMFieldBits - 1)) | (1u << (2 * kMFieldBi
 constexpr uint32_t kQueueBits = 0x20200404u;  // those bits after queue_tile's byte permute (outputs 2j, 2j + 1)
 constexpr int kScaleA0 = 127, kScaleA1 = 127 + kMFieldBits, kScaleB = 130;  // e8m0: 1, 2^11, 2^3
 
-// The packed words (and N-mask words) a lane needs for its window of the
-// 32-window tile at i0 (lane l covers window i0 + (l & 31)), read one tile
-// ahead of use.
+// A lane's haplotype (the group's descriptors are staged in LDS, s_hd).
+struct LaneHap {
+    uint32_t word_off, len, flags, nmask_off;
+};
+
+// The packed words (and N-mask words) a lane needs for its window i (read one
+// pair of tiles ahead of use).
 struct WinWords {
     uint32_t w[3], m[2];
 };
 
-__device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *words, const DevHap &hm, uint32_t i0,
-                                            uint32_t lane, WinWords &ww) {
-    const uint32_t ic = min(i0 + (lane & 31), hm.len);  // reads stay inside the +3 word pad
+__device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *words, const LaneHap &hm, uint32_t i,
+                                            WinWords &ww) {
+    const uint32_t ic = min(i, hm.len);  // reads stay inside the +3 word pad
     const uint32_t *w = words + hm.word_off + (ic >> 4);
     ww.w[0] = w[0];
     ww.w[1] = w[1];
@@ -85,14 +89,13 @@ __device__ __forceinline__ void load_window(const ScanArgs &A, const uint32_t *w
     }
 }
 
-// A fragments of the 32-window tile at i0: chunk kc = columns 8 kc .. + 7 of
-// the lane's window as FP4 one-hot nibbles (1.0 at the base's position, 16
-// bits per column; the same in both lane halves, which the A scales tell
-// apart), two 4-mer table reads; N bases zeroed in haplotypes that have them.
+// A fragments of the lane's window i: chunk kc = columns 8 kc .. + 7 as FP4
+// one-hot nibbles (1.0 at the base's position, 16 bits per column; the same in
+// both lane halves, which the A scales tell apart), two 4-mer table reads; N
+// bases zeroed in haplotypes that have them.
 template <int NK>
-__device__ __forceinline__ void build_onehot(const DevHap &hm, uint32_t i0, uint32_t lane, const WinWords &ww,
-                                             const char *s_onehot, v4i (&a)[NK]) {
-    const uint32_t i = i0 + (lane & 31);
+__device__ __forceinline__ void build_onehot(const LaneHap &hm, uint32_t i, const WinWords &ww, const char *s_onehot,
+                                             v4i (&a)[NK]) {
     const uint32_t ic = min(i, hm.len);
     const uint32_t sh = 2 * (ic & 15);
     const uint32_t img_lo = __builtin_amdgcn_alignbit(ww.w[1], ww.w[0], sh);  // bases i .. i+15
@@ -150,32 +153,18 @@ __device__ __forceinline__ v16f mfma_chunk(const v4i &a, const BFrag &f, const v
                                                            kScaleB);
 }
 
-// haplotype descriptors as wave-uniform (SGPR) values: through the constant
-// address space (the descriptors are read-only during a launch), so they are
-// scalar loads, counted apart from the vector memory operations in flight
-typedef const __attribute__((address_space(4))) uint32_t ConstU32;
-__device__ __forceinline__ DevHap load_hap(const DevHap *p) {
-    static_assert(sizeof(DevHap) == 48, "DevHap: 12 dwords");
-    ConstU32 *q = reinterpret_cast<ConstU32 *>(reinterpret_cast<uintptr_t>(p));
-    uint32_t w[12];
-#pragma unroll
-    for (int k = 0; k < 12; k++) w[k] = q[k];
-    DevHap h;
-    __builtin_memcpy(&h, w, sizeof(h));
-    return h;
-}
-
 // Candidate handling.  A tile test that fires (about one in four) appends one
 // entry per firing lane to the wave's queue in LDS: bytes 1-2 of its 16 outputs
 // (the fields' top bits; 8 v_perm, 32 bytes; see drain_queue) and a descriptor
-// (bits 0-5 the lane, 6-11 the strand tile, 12-19 the haplotype in the
-// workgroup's group, 32-63 the window tile start / 32).  A tile whose entries do
-// not fit drains the queue (drain_queue) and its round is scored again, so no
-// accumulator is live across a drain.
+// (bits 0-5 the lane, 6-11 the strand tile, 32-63 the window tile: its index
+// in the group's window list).  A tile whose entries do not fit drains the
+// queue (drain_queue) and its round is scored again, so no accumulator is live
+// across a drain.
 constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
-__shared__ uint32_t s_hnext;  // the workgroup's next haplotype (scan_super)
+__shared__ uint32_t s_hnext;  // the workgroup's next pair of window tiles (scan_super)
+__shared__ uint4 s_hd[kMMaxHapsPerBlock];  // the group's haplotypes: LaneHap
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 
@@ -278,7 +267,8 @@ __device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uin
 
 // Drains the wave's first n queue entries, one entry per lane per pass: the
 // candidate bits of both strands of the entry's column are gathered into one
-// mask and each candidate (haplotype, strand, window) is appended to the
+// mask and each candidate (window row of a tile of the group's window list wl,
+// nw entries; rows past nw are the last tile's padding) is appended to the
 // wave's region of the candidate list (2 dwords: global strand | haplotype in
 // the group << 24, window), one candidate per lane per round; the wave rescores
 // its list when it has scanned (rescore_list).  A full region (dense hits)
@@ -290,19 +280,18 @@ __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
            (size_t)wave * wave_cand_cap(A);
 }
 
-__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *words, uint32_t tile0,
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *wl, uint32_t nw, uint32_t tile0,
                                             uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane, uint32_t &cn) {
     uint2 *list = cand_list(A, wave);
     const uint32_t cap = wave_cand_cap(A);
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
         const uint32_t e = e0 + lane;
-        uint32_t m = 0, g0 = 0, i0 = 0, hl = 0;
+        uint32_t m = 0, g0 = 0, q0 = 0;
         if (e < n) {
             const uint4 d = s_qdata[wave][e];
             const uint64_t q = s_qmeta[wave][e];
             const uint32_t src = (uint32_t)q & 63u, ti = ((uint32_t)q >> 6) & 63u;
-            hl = ((uint32_t)q >> 12) & 255u;
-            i0 = ((uint32_t)(q >> 32) << 5) + 4 * (src >> 5);
+            q0 = ((uint32_t)(q >> 32) << 5) + 4 * (src >> 5);  // the list position of the lane's row 0
             g0 = (tile0 + ti) * kMStrands + 2 * (src & 31u);
             // dword k (queue_tile): the first strand's top bits of outputs 4k, 4k+1,
             // 4k+2, 4k+3 at 2, 10, 3, 11, the second's at 21, 29, 22, 30.  m bit
@@ -316,15 +305,21 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
             }
             m = lo | (hi << 16);
         }
-        uint64_t act;
-        while ((act = __ballot(m != 0)) != 0) {
-            if (m) {
-                const uint32_t b = __builtin_ctz(m);
+        while (__ballot(m != 0) != 0) {
+            bool have = m != 0;
+            uint32_t b = 0, q = 0;
+            if (have) {
+                b = __builtin_ctz(m);
                 m &= m - 1;
+                const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
+                q = q0 + (r & 3) + 8 * (r >> 2);
+                have = q < nw;  // the last tile's padding rows repeat an earlier window
+            }
+            const uint64_t act = __ballot(have);
+            if (have) {
                 const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-                const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
-                const uint32_t i = i0 + (r & 3) + 8 * (r >> 2), g = g0 + (b >> 4);
+                const uint32_t we = wl[q], hl = we & (kMMaxHapsPerBlock - 1), i = we >> 6, g = g0 + (b >> 4);
                 if (slot < cap) {
                     list[slot] = make_uint2(g | (hl << 24), i);
                 } else {  // rescored after the scan (no rescoring code, whose loads would stay
@@ -392,10 +387,11 @@ __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
 }
 
 // A firing tile (x: the lane's coarse test, fired = its ballot; the queue has
-// room): each firing lane queues bytes 1-2 of its outputs (the fields' top
-// bits); qn (wave-uniform) counts the wave's queued entries.
-__device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t fired, uint32_t ti, uint32_t hh,
-                                           uint32_t i0, uint32_t lane, uint32_t wave, uint32_t &qn) {
+// room; t: its index in the group's window list): each firing lane queues bytes
+// 1-2 of its outputs (the fields' top bits); qn (wave-uniform) counts the wave's
+// queued entries.
+__device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t fired, uint32_t ti, uint32_t t,
+                                           uint32_t lane, uint32_t wave, uint32_t &qn) {
     const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, qn));
     if (x) {
         // bytes 1, 1', 2, 2' of outputs 2j, 2j + 1: top bits at 2, 10, 21, 29;
@@ -408,7 +404,7 @@ __device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t
 #pragma unroll
         for (int k = 0; k < 4; k++) x[k] = __builtin_amdgcn_bitop3_b32(d[2 * k], d[2 * k + 1] << 1, kQueueBits, 0xe4);  // M ? d[2k] : d[2k+1] << 1
         s_qdata[wave][at] = uint4{x[0], x[1], x[2], x[3]};
-        s_qmeta[wave][at] = (uint64_t)(lane | (ti << 6) | (hh << 12)) | ((uint64_t)(i0 >> 5) << 32);
+        s_qmeta[wave][at] = (uint64_t)(lane | (ti << 6)) | ((uint64_t)t << 32);
     }
     qn += (uint32_t)__popcll(fired);
 }
@@ -440,14 +436,20 @@ __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, con
     for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
 }
 
+// What the firing path of a round needs: the group's window list (wl, nw
+// entries) for the drain, the first global tile and haplotype of the workgroup.
+struct GroupCtx {
+    const uint32_t *wl;
+    uint32_t nw, tile0, h0;
+};
+
 // The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
-// at i0a (A fragments a0) and, if two, i0b (a1).
+// ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
 template <int D, int NK>
 __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
-                                             const uint32_t *words, uint32_t tile0, uint32_t h0, uint32_t lane,
-                                             uint32_t wave, const v4i (&a0)[NK], const v4i (&a1)[NK], bool two,
-                                             uint32_t ha, uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb,
-                                             int sa, uint32_t &qn, uint32_t &cn) {
+                                             const GroupCtx &G, uint32_t lane, uint32_t wave, const v4i (&a0)[NK],
+                                             const v4i (&a1)[NK], bool two, uint32_t ta, const v16f &cb, int sa,
+                                             uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
     if (two) {
         for (uint32_t ti = tb; ti < te; ti++) {
@@ -462,22 +464,22 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             // accumulator is live across a drain)
             if (f0) {
                 if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
+                    drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x0 = coarse_test(c0);
                     x1 = coarse_test(c1);
                 }
-                queue_tile(c0, x0, f0, ti, ha, i0a, lane, wave, qn);
+                queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
             }
             if (f1) {
                 if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
+                    drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x1 = coarse_test(c1);
                 }
-                queue_tile(c1, x1, f1, ti, hb, i0b, lane, wave, qn);
+                queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
             }
         }
     } else {
@@ -489,33 +491,29 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             const uint64_t f0 = __ballot(x0 != 0);
             if (__builtin_expect(f0 == 0, 1)) continue;
             if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                drain_queue(A, words, tile0, h0, qn, wave, lane, cn);
+                drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
                 qn = 0;
                 tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
                 x0 = coarse_test(c0);
             }
-            queue_tile(c0, x0, f0, ti, ha, i0a, lane, wave, qn);
+            queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
         }
     }
 }
 
 // One step: every strand tile of the super tile (depth segments 1..NK, byte
-// d - 1 of seg = the end of depth d) x the window tiles at i0a of haplotype
-// ha (in the workgroup's group) and, if two, at i0b of hb.
+// d - 1 of seg = the end of depth d) x the window tiles ta and, if two, ta + 1.
 template <int NK>
-__device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const uint32_t *words,
-                                          uint32_t tile0, uint32_t h0, uint32_t lane, uint32_t wave,
-                                          const v4i (&a0)[NK], const v4i (&a1)[NK], bool two, uint32_t ha,
-                                          uint32_t i0a, uint32_t hb, uint32_t i0b, const v16f &cb, int sa,
-                                          uint32_t &qn, uint32_t &cn) {
+__device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const GroupCtx &G,
+                                          uint32_t lane, uint32_t wave, const v4i (&a0)[NK], const v4i (&a1)[NK],
+                                          bool two, uint32_t ta, const v16f &cb, int sa, uint32_t &qn, uint32_t &cn) {
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
 #define TFBS_SEGMENT(D)                                                                                          \
     if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
         const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \
         if (te > tb)                                                                                             \
-            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, words, tile0, h0, lane, wave, a0, a1, two, ha, \
-                                                 i0a, hb, i0b, cb, sa, qn, cn);                                  \
+            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, G, lane, wave, a0, a1, two, ta, cb, sa, qn, cn); \
         img += (te - tb) * mfma_tile_bytes(D);                                                                   \
         tb = te;                                                                                                 \
     }
@@ -526,65 +524,68 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
 #undef TFBS_SEGMENT
 }
 
+// The A fragments of list entry we (window << 6 | haplotype in the group): the
+// lane's haplotype from the LDS descriptors, its window's words, the one-hot.
+template <int NK>
+__device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *words, uint32_t we, const char *tab,
+                                             v4i (&a)[NK]) {
+    const uint4 d = s_hd[we & (kMMaxHapsPerBlock - 1)];
+    const LaneHap hm{d.x, d.y, d.z, d.w};
+    const uint32_t i = we >> 6;
+    WinWords ww;
+    load_window(A, words, hm, i, ww);
+    build_onehot<NK>(hm, i, ww, tab, a);
+}
+
 // words: the packed haplotype words, indexed by DevHap::word_off (an LDS copy
 // of this workgroup's haplotypes, biased by their first word, or global memory).
+// The group's window list (the windows of its haplotypes the class reads) is
+// cut into tiles of 32 windows (the last one padded with its last window),
+// handed to the waves two at a time from an LDS counter -- the waves finish
+// together however the windows fall -- and the next pair's list entries are
+// loaded while the current pair is scored.
 template <int NK>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
     const uint32_t h0 = hg * A.haps_per_block;
-    const uint32_t tile0 = S.tile0;
+    const uint32_t h1 = min(h0 + A.haps_per_block, A.n_haps);
+    const uint64_t e0 = A.wlist_off[NK > 2][h0];
+    GroupCtx G;
+    G.wl = A.wlist[NK > 2] + e0;
+    G.nw = (uint32_t)(A.wlist_off[NK > 2][h1] - e0);
+    G.tile0 = S.tile0;
+    G.h0 = h0;
+    const uint32_t ntile = (G.nw + kMWindows - 1) / kMWindows, npair = (ntile + 1) / 2;
     const float a0f = __uint_as_float(S.acc0);
     v16f cb = {a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f};
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
     const int sa = lane < 32 ? kScaleA0 : kScaleA1;
     const char *tab = s_img - kMOnehotBytes;
     uint32_t qn = 0, cn = 0;  // the wave's queued entries, listed candidates
-    // window tiles two at a time (each B fragment read from LDS feeds two
-    // MFMAs), pairs formed across the wave's haplotypes: a tile waits in a0
-    // (haplotype pa, window pi0) for the next one
-    v4i a0[NK], a1[NK];
-    bool pending = false;
-    uint32_t pa = 0, pi0 = 0;
-    // haplotypes taken one at a time from the workgroup's counter: the waves
-    // finish together however the dirty tiles of reused haplotypes fall
-    for (;;) {
-        uint32_t hh = 0;
-        if (lane == 0) hh = atomicAdd(&s_hnext, 1u);
-        hh = __builtin_amdgcn_readfirstlane(hh);
-        const uint32_t hap = h0 + hh;
-        if (hh >= A.haps_per_block || hap >= A.n_haps) break;
-        const DevHap hm = load_hap(A.haps + hap);
-        if (hm.len < S.lmin) continue;
-        const uint32_t nwin = hm.len - S.lmin + 1;
-        // 32 tiles per mask; a HAP_DEDUP haplotype only the tiles holding a
-        // base that differs from the reference (the others are ref_fixup_kernel's)
-        const uint32_t ntiles = (nwin + kMWindows - 1) / kMWindows;
-        const bool dedup = (hm.flags & HAP_DEDUP) && A.dedup;  // then ntiles <= 32
-        for (uint32_t base = 0; base < ntiles; base += 32) {
-            const uint32_t nb = min(32u, ntiles - base);
-            uint32_t m = nb >= 32 ? ~0u : (1u << nb) - 1;
-            if (dedup) m &= hm.dirty[NK - 1];
-            while (m) {
-                const uint32_t i0 = kMWindows * (base + __builtin_ctz(m));
-                m &= m - 1;
-                WinWords ww;
-                load_window(A, words, hm, i0, lane, ww);
-                if (!pending) {
-                    build_onehot<NK>(hm, i0, lane, ww, tab, a0);
-                    pa = hh;
-                    pi0 = i0;
-                    pending = true;
-                    continue;
-                }
-                build_onehot<NK>(hm, i0, lane, ww, tab, a1);
-                // the other waves of the SIMD hide the latencies
-                scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, a0, a1, true, pa, pi0, hh, i0, cb, sa, qn, cn);
-                pending = false;
-            }
-        }
+    auto next_pair = [&]() {
+        uint32_t p = 0;
+        if (lane == 0) p = atomicAdd(&s_hnext, 1u);
+        return (uint32_t)__builtin_amdgcn_readfirstlane(p);
+    };
+    // lane l scores window row l & 31 of each tile
+    auto entries = [&](uint32_t p, uint32_t &ea, uint32_t &eb) {
+        const uint32_t q = kMWindows * 2 * p + (lane & 31);
+        ea = G.wl[min(q, G.nw - 1)];
+        eb = G.wl[min(q + kMWindows, G.nw - 1)];
+    };
+    uint32_t p = next_pair(), ea = 0, eb = 0;
+    if (p < npair) entries(p, ea, eb);
+    while (p < npair) {
+        const uint32_t pn = next_pair();
+        const bool two = 2 * p + 1 < ntile;
+        v4i a0[NK], a1[NK];
+        entry_onehot<NK>(A, words, ea, tab, a0);
+        entry_onehot<NK>(A, words, eb, tab, a1);  // (a copy of the last window when !two: unused)
+        if (pn < npair) entries(pn, ea, eb);      // in flight while this pair is scored
+        scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
+        p = pn;
     }
-    if (pending) scan_step<NK>(A, s_img, S.seg, words, tile0, h0, lane, wave, a0, a1, false, pa, pi0, pa, pi0, cb, sa, qn, cn);
-    drain_queue(A, words, tile0, h0, qn, wave, lane, cn);  // the wave's last entries
+    drain_queue(A, G.wl, G.nw, G.tile0, h0, qn, wave, lane, cn);  // the wave's last entries
     rescore_list(A, words, h0, wave, lane, cn);
 }
 
@@ -598,6 +599,8 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     const uint32_t hg = blockIdx.x / A.n_msupers;
     const DevMSuper S = A.msupers[sidx];
     uint4 *dst = reinterpret_cast<uint4 *>(smem);
+    const uint32_t h0 = hg * A.haps_per_block;
+    const uint32_t hn = min(h0 + A.haps_per_block, A.n_haps) - h0;
     {
         const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
         for (uint32_t i = threadIdx.x; i < S.img_bytes / 16; i += kMBlock) dst[kMOnehotBytes / 16 + i] = src[i];
@@ -610,12 +613,15 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
             for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
             tab[k] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
         }
+        if (threadIdx.x < hn) {
+            const DevHap &h = A.haps[h0 + threadIdx.x];
+            s_hd[threadIdx.x] = make_uint4(h.word_off, h.len, h.flags, h.nmask_off);
+        }
     }
-    const uint32_t h0 = hg * A.haps_per_block;
-    const uint32_t hl = min(h0 + A.haps_per_block, A.n_haps) - 1;
     const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     const uint32_t *words = A.words;
     if (STAGED) {
+        const uint32_t hl = h0 + hn - 1;
         const uint32_t wbeg = A.haps[h0].word_off;
         const uint32_t wend = A.haps[hl].word_off + (A.haps[hl].len + 15) / 16 + 3;
         uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max) / 4;
@@ -623,7 +629,7 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
         words = s_words - wbeg;
     }
     __syncthreads();
-    // the wave index is uniform: keep every haplotype-level value in SGPRs
+    // the wave index is uniform: keep every group-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
 }
@@ -640,6 +646,105 @@ __global__ __launch_bounds__(256) void cand_over_kernel(ScanArgs A) {
              m &= m - 1)
             spill_record(A, hp.region, hap, key0 + __builtin_ctz(m));
     }
+}
+
+// ---------------------------------------------------------------------------
+// Window lists (ScanArgs::wlist): per depth class of span S, the windows [0, len
+// - lmin + 1) of every haplotype, only those meeting a diff run for a HAP_DEDUP
+// haplotype (tfbs_internal.hpp): f(lo, hi) gets them as ascending intervals.
+template <class F>
+__device__ __forceinline__ uint32_t for_windows(const DevHap &hm, const uint32_t *druns, uint32_t lmin, uint32_t S,
+                                                uint32_t dedup, F &&f) {
+    if (hm.len < lmin) return 0;
+    const uint32_t nw = hm.len - lmin + 1;
+    if (!dedup || !(hm.flags & HAP_DEDUP)) {
+        f(0u, nw);
+        return nw;
+    }
+    uint32_t n = 0, next = 0;  // windows below next are listed
+    for (uint32_t k = 0; k < hm.n_druns; k++) {
+        const uint32_t a = druns[2 * (hm.drun_off + k)], b = druns[2 * (hm.drun_off + k) + 1];
+        const uint32_t lo = max(next, a >= S - 1 ? a - (S - 1) : 0u), hi = min(b, nw - 1) + 1;
+        if (hi > lo) {
+            f(lo, hi);
+            n += hi - lo;
+            next = hi;
+        }
+    }
+    return n;
+}
+
+__global__ __launch_bounds__(256) void wl_count_kernel(const DevHap *__restrict__ haps, uint32_t n,
+                                                       const uint32_t *__restrict__ druns, uint32_t lmin, uint32_t S,
+                                                       uint32_t dedup, uint64_t *__restrict__ cnt) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h > n) return;
+    cnt[h] = h < n ? for_windows(haps[h], druns, lmin, S, dedup, [](uint32_t, uint32_t) {}) : 0u;
+}
+
+// one wave per haplotype: its entries written 64 at a time
+__global__ __launch_bounds__(256) void wl_fill_kernel(const DevHap *__restrict__ haps, uint32_t n,
+                                                      const uint32_t *__restrict__ druns, uint32_t lmin, uint32_t S,
+                                                      uint32_t dedup, uint32_t hpb, const uint64_t *__restrict__ off,
+                                                      uint32_t *__restrict__ list) {
+    const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (h >= n) return;
+    uint64_t at = off[h];
+    const uint32_t hl = h % hpb;
+    for_windows(haps[h], druns, lmin, S, dedup, [&](uint32_t lo, uint32_t hi) {
+        for (uint32_t w = lo + lane; w < hi; w += 64) list[at + (w - lo)] = (w << 6) | hl;
+        at += hi - lo;
+    });
+}
+
+// In-place exclusive scan of u64 values, 4096 per workgroup; sums[b] = tile b's total.
+constexpr uint32_t kScanThreads = 1024, kScanTile = 4 * kScanThreads;
+__global__ __launch_bounds__(kScanThreads) void scan_tile_kernel(uint64_t *__restrict__ x, uint64_t n,
+                                                                 uint64_t *__restrict__ sums) {
+    __shared__ uint64_t s[2][kScanThreads];
+    const uint32_t t = threadIdx.x;
+    const uint64_t base = (uint64_t)blockIdx.x * kScanTile + 4 * t;
+    uint64_t v[4], tot = 0;
+    for (int k = 0; k < 4; k++) {
+        v[k] = base + k < n ? x[base + k] : 0;
+        tot += v[k];
+    }
+    int cur = 0;
+    s[0][t] = tot;
+    __syncthreads();
+    for (uint32_t o = 1; o < kScanThreads; o <<= 1) {
+        s[cur ^ 1][t] = s[cur][t] + (t >= o ? s[cur][t - o] : 0);
+        cur ^= 1;
+        __syncthreads();
+    }
+    uint64_t run = s[cur][t] - tot;
+    for (int k = 0; k < 4; k++) {
+        if (base + k < n) x[base + k] = run;
+        run += v[k];
+    }
+    if (t == kScanThreads - 1) sums[blockIdx.x] = s[cur][t];
+}
+
+__global__ __launch_bounds__(256) void scan_add_kernel(uint64_t *__restrict__ x, uint64_t n,
+                                                       const uint64_t *__restrict__ sums) {
+    const uint64_t add = sums[blockIdx.x];
+    for (uint32_t k = threadIdx.x; k < kScanTile; k += 256) {
+        const uint64_t i = (uint64_t)blockIdx.x * kScanTile + k;
+        if (i < n) x[i] += add;
+    }
+}
+
+int exclusive_scan(uint64_t *x, uint64_t n, uint64_t *tmp, hipStream_t stream) {
+    const uint64_t nt = (n + kScanTile - 1) / kScanTile;
+    if (nt == 0) return TFBS_OK;
+    hipLaunchKernelGGL(scan_tile_kernel, dim3((uint32_t)nt), dim3(kScanThreads), 0, stream, x, n, tmp);
+    if (nt > 1) {
+        if (int rc = exclusive_scan(tmp, nt, tmp + nt, stream)) return rc;
+        hipLaunchKernelGGL(scan_add_kernel, dim3((uint32_t)nt), dim3(256), 0, stream, x, n, tmp);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan kernels: ") + hipGetErrorString(e));
+    return TFBS_OK;
 }
 
 typedef void (*MfmaKernel)(ScanArgs);
@@ -668,11 +773,40 @@ uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb) {
     return mx;
 }
 
+size_t scan_tmp_words(size_t n) {
+    size_t w = 0;
+    for (size_t nt = (n + kScanTile - 1) / kScanTile; nt > 0; nt = nt > 1 ? (nt + kScanTile - 1) / kScanTile : 0) w += nt;
+    return w + 1;
+}
+
+int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
+                       uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
+                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p), void *ensure_ctx) {
+    for (int c = 0; c < 2; c++) {
+        total[c] = 0;
+        if (!lmin[c]) continue;
+        const uint32_t S = kMChunkCols * (c ? 4 : 2);
+        hipLaunchKernelGGL(wl_count_kernel, dim3(n_haps / 256 + 1), dim3(256), 0, stream, haps, n_haps, druns, lmin[c],
+                           S, dedup, bufs.off[c]);
+        if (int rc = exclusive_scan(bufs.off[c], (uint64_t)n_haps + 1, bufs.scan_tmp, stream)) return rc;
+        hipError_t e = hipMemcpyAsync(&total[c], bufs.off[c] + n_haps, 8, hipMemcpyDeviceToHost, stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(stream);
+        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("window list size: ") + hipGetErrorString(e));
+        if (int rc = ensure_list(ensure_ctx, c, std::max<uint64_t>(total[c], 1), &bufs.list[c])) return rc;
+        if (n_haps)
+            hipLaunchKernelGGL(wl_fill_kernel, dim3((n_haps + 3) / 4), dim3(256), 0, stream, haps, n_haps, druns,
+                               lmin[c], S, dedup, hpb, bufs.off[c], bufs.list[c]);
+        e = hipGetLastError();
+        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("wl_fill_kernel: ") + hipGetErrorString(e));
+    }
+    return TFBS_OK;
+}
+
 size_t mfma_lds_fixed() { return kMOnehotBytes; }
 
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
-    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + 256;  // table, staged words, queues
+    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hd) + 256;  // table, staged words, queues
     // workgroups per CU = 4 SIMDs x waves per SIMD / waves per workgroup
     for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / (4 * waves[nk] / (kMBlock / 64)) - reserve;
 }
@@ -684,10 +818,10 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     const uint32_t hpb = a0.haps_per_block;
     // candidate list entries: global strand < 2^24, haplotype in the group < 2^8
     const DevMSuper &last = supers[n_supers - 1];
-    if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > 256)
-        return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 256 haplotypes per workgroup");
+    if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > kMMaxHapsPerBlock)
+        return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 64 haplotypes per workgroup");
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext);  // candidate queues
+    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd);  // queues, descriptors
     uint32_t region = 0;
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is
@@ -725,6 +859,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.n_msupers = ns;
             a.haps = a0.haps + h0;
             a.hap_base = a0.hap_base + h0;
+            for (int c = 0; c < 2; c++) a.wlist_off[c] = a0.wlist_off[c] ? a0.wlist_off[c] + h0 : nullptr;
             a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
             a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
             a.region_base = region;

@@ -36,7 +36,7 @@ constexpr int kUnitMax = 8;        // strands per unit (octet)
 constexpr int kFastMaxLen = 32;    // the LUT path reads a 64-bit (32-base) window per lane
 constexpr int kMaxInnerPass = 8;   // inner ranges handled per pass (accumulators per lane)
 constexpr int kMaxTileSlots = 64;  // pattern_id slots per tile: one lane each
-constexpr uint32_t kMaxHapLen = 1u << 29;  // haplotype bases: window starts fit the kernels' 29-bit fields
+constexpr uint32_t kMaxHapLen = 1u << 26;  // haplotype bases: window starts fit the window lists' 26-bit fields
 
 enum UnitKind : uint32_t {
     // 8 strands, int16 partial sums biased to <= 0 per block, saturating packed adds:
@@ -134,15 +134,20 @@ constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 
 
 // HAP_REF: the region's reference haplotype (the reference group's, or a
 // helper with no carriers after the region's distinct haplotypes); its
-// matrix-core hits are listed for the reference-window fix-up.  HAP_DEDUP: a
-// haplotype of at most kDedupMaxTiles window tiles: the matrix-core scan reads
-// only its tiles with a window (of up to 8 nk columns, dirty[nk - 1]) that
-// reaches a column differing from the reference's -- another base or N, another
-// position (past an indel), past the end of either sequence; every other window
-// has the reference window's bases and positions, so its hits are the
-// reference's, added by ref_fixup_kernel.
+// matrix-core hits are listed for the reference-window reuse.  HAP_DEDUP: a
+// haplotype of at most kDedupMaxWindows bases whose columns differing from the
+// reference's -- another base or N, another position (past an indel), past the
+// end of either sequence -- form at most kMaxDiffRuns runs (diff runs [a, b],
+// inclusive, ascending, at DevHap::drun_off of the batch's run array).  For a
+// depth class of span S = 8 nk columns, window i is *dirty* iff some run meets
+// [i, i + S - 1]; the matrix-core scan reads only the dirty windows of a
+// HAP_DEDUP haplotype (its window list, scan_mfma.hip), every other window has
+// the reference window's bases and positions, so its hits are the reference's,
+// which the key assembly adds (key_kernels.hip, same predicate).
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
-constexpr uint32_t kDedupMaxTiles = 32;  // window tiles a dirty mask covers
+constexpr uint32_t kDedupMaxWindows = 1024;  // longest HAP_DEDUP haplotype (and reference)
+constexpr uint32_t kMaxDiffRuns = 16;        // diff runs of a HAP_DEDUP haplotype
+constexpr uint32_t kRunToEnd = 0xFFFFFFFFu;  // a run's end past either sequence's end
 
 struct DevHap {
     uint32_t word_off;   // packed 2-bit bases, 16 per u32, LSB first
@@ -152,8 +157,14 @@ struct DevHap {
     uint32_t nmask_off;  // u32 words of the N mask (bit i = base i is N), if HAP_HAS_N
     uint32_t pos_off;    // int32 positions relative to ext_start, if HAP_HAS_POS
     uint64_t count_off;  // counts[count_off + (slot * n_inner + k) * DevRegion::count_stride]
-    uint32_t dirty[4];   // HAP_DEDUP: per K depth, bit t = window tile t (windows 32 t ..) holds a differing base
+    uint32_t drun_off;   // HAP_DEDUP: its diff runs, (a, b) u32 pairs at druns + 2 drun_off
+    uint32_t n_druns;
+    uint32_t pad[2];
 };
+
+// Window w of a class of span S is dirty for a haplotype with diff runs r
+// (HAP_DEDUP): some run meets the window's columns [w, w + S - 1].
+inline constexpr bool run_meets(uint32_t a, uint32_t b, uint32_t w, uint32_t S) { return a <= w + S - 1 && b >= w; }
 
 struct DevRegion {
     uint32_t inner_off;  // into the inner (s_rel, e_rel) pair array
