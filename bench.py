@@ -330,6 +330,8 @@ def main():
     t_up = time.perf_counter()
     T.check(L.tfbs_batch_upload(sc.h, batch.h))
     t_up = time.perf_counter() - t_up
+    wl_entries, wl_s = (ctypes.c_uint64 * 2)(), ctypes.c_double()
+    T.check(L.tfbs_ctx_window_lists(sc.h, wl_entries, ctypes.byref(wl_s)))
     t_scan1 = time.perf_counter()
     T.check(L.tfbs_scan(sc.h, batch.h))
     T.check(L.tfbs_ctx_sync(sc.h))
@@ -471,6 +473,7 @@ def main():
                                 "region x PWM shard: %d region blocks x %d pattern shards" % (world // parts, parts)),
                 "scan_path": path,
                 "scanned_windows_per_step": int(tot_scan),
+                "window_list_entries": [int(wl_entries[0]), int(wl_entries[1])],
             },
             "value_note": "windows of every distinct haplotype resolved per second (the reference scores each "
                           "of them); a haplotype's windows whose bases and positions equal the "
@@ -497,7 +500,8 @@ def main():
                 "host_bgzf_writer": host_bgzf,
                 "rank0_phases_s": {"host_prep_wall": prep_wall, "synthetic_generation_wall": fill_s - prep_wall,
                                    "synthetic_generation_thread_s": gen_s, "build_region_thread_s": build_s,
-                                   "upload": t_up, "scan": t_scan1, "key_reduce": t_red,
+                                   "upload": t_up, "upload_window_lists": wl_s.value, "scan": t_scan1,
+                                   "key_reduce": t_red,
                                    "device_encode": t_enc, "rows_bgzf": t_rows,
                                    "rows_bgzf_host_plan": rows_split[0] if not args.no_e2e else 0.0,
                                    "rows_bgzf_device_and_write": rows_split[1] if not args.no_e2e else 0.0},

@@ -375,9 +375,18 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
             HIP_TRY(hipStreamSynchronize(ctx->stream));
             nspill = ctx->over_host[0];
         }
-        if (ctx->debug_over)
+        if (ctx->debug_over) {
             fprintf(stderr, "tfbs_scan overflow lists: spill %u/%u candidates %u/%u\n", nspill, ctx->spill_cap, ncand,
                     ctx->cand_over_cap);
+            // the hits of the scan workgroups' lists
+            const size_t nw = ctx->hitn.n;
+            std::vector<uint32_t> hn(nw);
+            HIP_TRY(hipMemcpy(hn.data(), ctx->hitn.p, nw * 4, hipMemcpyDeviceToHost));
+            uint64_t sh = 0, mh = 0;
+            for (size_t i = 0; i < nw; i++) sh += hn[i], mh = std::max<uint64_t>(mh, hn[i]);
+            fprintf(stderr, "tfbs_scan hit pairs %llu (max per wave %llu) over %zu waves\n", (unsigned long long)sh,
+                    (unsigned long long)mh, nw);
+        }
         if (nspill <= ctx->spill_cap && ncand <= ctx->cand_over_cap) {
             ctx->over_pending = false;
             ctx->n_spill = nspill;
@@ -606,6 +615,14 @@ int tfbs_ctx_rows_bgzf_seconds(const tfbs_ctx *ctx, double *out) {
     if (!ctx || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
     out[0] = ctx->rows_s[0];
     out[1] = ctx->rows_s[1];
+    return TFBS_OK;
+}
+
+int tfbs_ctx_window_lists(const tfbs_ctx *ctx, uint64_t entries[2], double *seconds) {
+    if (!ctx || !entries || !seconds) return tfbs::fail(TFBS_E_ARG, "null argument");
+    entries[0] = ctx->wl_entries[0];
+    entries[1] = ctx->wl_entries[1];
+    *seconds = ctx->wl_seconds;
     return TFBS_OK;
 }
 

@@ -309,10 +309,14 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 for (uint32_t q0 = 0; q0 < nref; q0++) {  // workgroup-uniform; threads over the haplotypes
                     const uint4 q = s_ref[q0];
                     const uint32_t dk = q.z >> 16;
-                    uint32_t keep = 0;  // bit j: haplotype tid + j kAsmBlock inherits the hit (U <= kAsmHaps)
+                    bool here = false;  // uniform: a key of the hit is in this chunk
+                    ref_keys(q, [&](uint32_t key) {
+                        here = here || (key - kw0 < kwn && row_of(key - kw0) - t0 < nrow);
+                    });
+                    if (!here) continue;
+                    uint32_t keep = 0;  // bit j: haplotype tid + j kAsmBlock inherits the hit
                     for (uint32_t l = tid, j = 0; l < U; l += kAsmBlock, j++)
                         if (!dirty(l, dk, q.y)) keep |= 1u << j;
-                    if (__syncthreads_or(keep) == 0) continue;
                     ref_keys(q, [&](uint32_t key) {
                         const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
                         if (t >= nrow) return;

@@ -20,13 +20,17 @@
 //    U > T0 iff the field's top bit (10 or 21) is set.  One OR tree over a
 //    lane's 16 outputs (v_or3 + v_bitop3) tests 32 (window, strand) pairs.
 //  * A workgroup (8 waves) stages one super tile (tiles of 64 strands of equal
-//    K depth), the one-hot table and the packed words of its haplotypes in
-//    LDS.  Every B fragment is one conflict-free ds_read_b128 + ds_read_b64 per
-//    lane and feeds two window tiles.
+//    K depth), the one-hot table, its group's haplotype descriptors and packed
+//    words in LDS.  Every B fragment is one conflict-free ds_read_b128 +
+//    ds_read_b64 per lane and feeds two window tiles.
+//  * Window tiles come from the group's window list (build_window_lists): 32
+//    listed windows of any of the group's haplotypes per tile, lane l & 31 its
+//    own (haplotype, window), so reference-window reuse leaves no holes.
 //  * C layout: lane l holds column l & 31 (strands 2 (l & 31), + 1) and windows
 //    (r & 3) + 8 (r >> 2) + 4 (l >> 5), r < 16.  A firing lane (rare) appends
 //    the fields' top bits of its 16 outputs (16 bytes) to the wave's LDS queue;
-//    drain_queue decodes them into (haplotype, strand, window) candidates in the
+//    drain_queue decodes them (through the window list) into (haplotype,
+//    strand, window) candidates in the
 //    wave's region of a global (L2-resident) list, and when the wave has
 //    scanned it rescores those exactly, one per lane (pattern.rs:125-151),
 //    applies the inner-range overlap test (range.rs:18-21 as main.rs:503 uses

@@ -140,6 +140,10 @@ int tfbs_ctx_last_scan_launches(const tfbs_ctx *ctx);
 /* Device time (ms) of the last tfbs_scan's matrix-core kernel launches alone
  * (HIP events on the ctx stream), or -1 if the scan ran no MFMA tile. */
 float tfbs_ctx_last_mfma_ms(const tfbs_ctx *ctx);
+/* The matrix-core window lists of the uploaded batch (built by tfbs_batch_upload):
+ * entries[c] = windows depth class c (0: strands of 1-2 K chunks, 1: 3-4) reads,
+ * *seconds = the build's wall time.  Zeros before an upload or without MFMA strands. */
+int tfbs_ctx_window_lists(const tfbs_ctx *ctx, uint64_t entries[2], double *seconds);
 
 /* Replaces matches() (pattern.rs:141-171) for ONE haplotype against every
  * pattern, on the GPU.  nucs are codes 0..4, pos the NucleotidePos.pos values.
