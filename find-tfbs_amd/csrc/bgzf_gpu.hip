@@ -625,6 +625,12 @@ __shared__ uint32_t g_bits[kBitWords + 1];
 alignas(16) __shared__ uint8_t g_text[kBgzfRaw + kBgzfRaw / 16 + 16];
 __device__ __forceinline__ uint32_t txt_at(uint32_t q) { return q + ((q >> 6) << 2); }
 __shared__ uint32_t g_item[kWvItems];
+// per staged token slot: the fixed-Huffman literal codes of its text, LSB first,
+// and their bit count (kNoTokLit: more than 128 bits, the per-byte path), so that
+// a whole text of literals is a few 32-bit puts, not one per byte
+__shared__ uint4 g_tlit[kStTok];
+__shared__ uint8_t g_tlitn[kStTok];
+constexpr uint32_t kNoTokLit = 255;
 __shared__ uint32_t g_ioff[kWvItems + 1];
 __shared__ uint32_t g_red[kWv / 64];
 
@@ -638,7 +644,7 @@ struct LaneBits {
         atomicOr(&g_bits[w], v << sh);
         if (sh + nb > 32) atomicOr(&g_bits[w + 1], v >> (32 - sh));
     }
-    __device__ void put(uint32_t v, uint32_t nb) {  // nb <= 16
+    __device__ void put(uint32_t v, uint32_t nb) {  // nb <= 32, v < 2^nb
         acc |= (uint64_t)v << n;
         n += nb;
         if (n >= 32) {
@@ -815,7 +821,9 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
     } else if (dist) {
         nb = wv_match<false>(dummy, t, dist);
     } else if (in) {
-        for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        const uint32_t tn = g_tlitn[v.tok_at + c];
+        if (full && tn != kNoTokLit) nb = tn;
+        else for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
     if (kWrite) {
         LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
@@ -825,9 +833,28 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         } else if (dist) {
             wv_match<true>(off, t, dist);
         } else if (in) {
-            for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+            const uint32_t tn = g_tlitn[v.tok_at + c];
+            if (full && tn != kNoTokLit) {
+                const uint4 L = g_tlit[v.tok_at + c];
+                const uint32_t lw[4] = {L.x, L.y, L.z, L.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (tn > 32u * j) off.put(lw[j], min(tn - 32u * j, 32u));
+            } else {
+                for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+            }
         }
         off.finish();
+    } else if (full) {  // the text's dwords, ORed (neighbouring texts share edge dwords)
+        const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
+        const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
+        uint32_t prev = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) {
+            const uint32_t d = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
+            prev = T[j];
+            if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), d);
+        }
     } else if (in) {
         for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
     }
@@ -853,6 +880,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
         for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
+        for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
         for (uint32_t k = 0; k < S.P.n_st; k++) {
             const StRow T = S.P.st[k];
             const DevRow R = A.rows[T.row];
@@ -865,6 +893,38 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         }
     }
     __syncthreads();
+    // the staged tokens' literal codes (bytes past a text's length zeroed: the text's
+    // dwords are ORed into g_text whole)
+    {
+        uint32_t tok_end = 0;
+        for (uint32_t k = 0; k < S.P.n_st; k++) tok_end = max(tok_end, S.P.st[k].tok_at + S.rows[S.P.st[k].row - S.P.r_first].nv);
+        for (uint32_t k = tid; k < tok_end; k += kWv) {
+            uint4 &tx = reinterpret_cast<uint4 *>(S.text)[k];
+            const uint32_t t = S.tlen[k];
+            uint32_t w[4] = {tx.x, tx.y, tx.z, tx.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int32_t keep = (int32_t)t - 4 * j;  // bytes of dword j inside the text
+                w[j] &= keep >= 4 ? ~0u : (keep <= 0 ? 0u : (1u << (8 * keep)) - 1u);
+            }
+            tx = uint4{w[0], w[1], w[2], w[3]};
+            uint64_t lo = 0, hi = 0;
+            uint32_t nb = 0;
+            for (uint32_t i = 0; i < t && nb <= 128; i++) {
+                const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                const uint32_t code = b < 144 ? rev(0x30 + b, 8) : rev(0x190 + b - 144, 9), n = b < 144 ? 8u : 9u;
+                if (nb < 64) {
+                    lo |= (uint64_t)code << nb;
+                    if (nb + n > 64) hi |= (uint64_t)code >> (64 - nb);
+                } else {
+                    hi |= (uint64_t)code << (nb - 64);
+                }
+                nb += n;
+            }
+            g_tlit[k] = uint4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+            g_tlitn[k] = (uint8_t)(nb <= 128 ? nb : kNoTokLit);
+        }
+    }
     // the block's items in stream order: per row its head, its groups, its newline
     const Ctx<true> C{A, b0};
     uint32_t my_items = 0;
