@@ -633,16 +633,17 @@ __shared__ uint8_t g_tlitn[kStTok];
 constexpr uint32_t kNoTokLit = 255;
 __shared__ uint32_t g_ioff[kWvItems + 1];
 __shared__ uint32_t g_red[kWv / 64];
+__shared__ uint32_t g_pub[kWvItems];  // item i's end bit + 1 (0: not yet known; wv_chain)
 
 // A lane's bit stream: symbols gathered in a register, ORed into g_bits 32 bits at
 // a time (two LDS atomics at most per 32 bits, not per symbol)
 struct LaneBits {
     uint64_t acc;
     uint32_t n, off;  // bits held; the stream offset of the first
-    __device__ void out(uint32_t v, uint32_t nb) {
+    __device__ void out(uint32_t v, uint32_t nb) {  // (bits past the buffer: the block is stored)
         const uint32_t w = off >> 5, sh = off & 31;
-        atomicOr(&g_bits[w], v << sh);
-        if (sh + nb > 32) atomicOr(&g_bits[w + 1], v >> (32 - sh));
+        if (w <= kBitWords) atomicOr(&g_bits[w], v << sh);
+        if (sh + nb > 32 && w < kBitWords) atomicOr(&g_bits[w + 1], v >> (32 - sh));
     }
     __device__ void put(uint32_t v, uint32_t nb) {  // nb <= 32, v < 2^nb
         acc |= (uint64_t)v << n;
@@ -720,23 +721,36 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
 }
 
-// One item of the block (all lanes of a wave together): its bits; kWrite: the
-// symbols at base + the lanes' prefix; !kWrite: its bytes into g_text.
-template <bool kWrite>
-__device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t item,
-                            uint32_t base, uint32_t lane) {
+// Item i's first bit: the end of item i - 1, published by the wave that wrote it
+// (items go to the waves round-robin and each wave takes its items in order, so
+// the chain always advances); then item i's end is published.
+__device__ __forceinline__ uint32_t wv_chain(uint32_t i, uint32_t total, uint32_t lane) {
+    uint32_t base = 3;  // BFINAL + BTYPE
+    if (i) {
+        uint32_t p;
+        while ((p = __hip_atomic_load(&g_pub[i - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+            __builtin_amdgcn_s_sleep(1);
+        base = p - 1;
+    }
+    if (lane == 0) __hip_atomic_store(&g_pub[i], base + total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return base;
+}
+
+// Item i of the block (all lanes of a wave together), in one pass: its bytes into
+// g_text, its bit count, its first bit from the chain (wv_chain), its symbols.
+__device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane) {
+    const uint32_t item = g_item[i];
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
     const RowView v = C.view(g_st.P.r_first + d);
     if (kind == IT_NL) {
+        const uint32_t base = wv_chain(i, 8, lane);
         if (lane == 0) {
-            if (kWrite) {
-                LaneBits o{0, 0, base};
-                wv_lit(o, '\n');
-                o.finish();
-            }
-            else g_text[txt_at((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0))] = '\n';
+            g_text[txt_at((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0))] = '\n';
+            LaneBits o{0, 0, base};
+            wv_lit(o, '\n');
+            o.finish();
         }
-        return 8;
+        return;
     }
     if (kind == IT_HEAD) {
         const uint64_t hs = max(b0, v.R.text_off), he = min(e, v.R.text_off + v.R.head_len);
@@ -745,17 +759,21 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
             const uint64_t q = q0 + lane;
             const bool in = q < he;
             const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
-            const uint32_t nb = in ? lit_bits(b) : 0u;
-            if (kWrite) {
-                LaneBits o{0, 0, base + total + wave_excl_sum(nb, lane)};
-                if (in) wv_lit(o, b);
-                o.finish();
-            } else if (in) {
-                g_text[txt_at((uint32_t)(q - b0))] = (uint8_t)b;
-            }
-            total += wave_sum(nb);
+            if (in) g_text[txt_at((uint32_t)(q - b0))] = (uint8_t)b;
+            total += wave_sum(in ? lit_bits(b) : 0u);
         }
-        return total;
+        uint32_t at = wv_chain(i, total, lane);
+        for (uint64_t q0 = hs; q0 < he; q0 += 64) {
+            const uint64_t q = q0 + lane;
+            const bool in = q < he;
+            const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
+            const uint32_t nb = in ? lit_bits(b) : 0u;
+            LaneBits o{0, 0, at + wave_excl_sum(nb, lane)};
+            if (in) wv_lit(o, b);
+            o.finish();
+            at += wave_sum(nb);
+        }
+        return;
     }
     // a 64-sample group
     const uint32_t g = item & 0x7FFFFFu, N = A.n_samples;
@@ -813,6 +831,23 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         }
         if ((r == 1 || r == 2) && Lr >= 3 && a <= Lr - 3 && Lr - 3 < b) m2 = 3;
     }
+    // the text's bytes (for the CRC)
+    if (full) {  // its dwords, ORed (neighbouring texts share edge dwords)
+        const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
+        const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
+        uint32_t prev = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 5; j++) {
+            const uint32_t dw = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
+            prev = T[j];
+            if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), dw);
+        }
+    } else if (in) {
+        for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
+    }
+    // its bits, its place in the block's stream, its symbols
+    const uint32_t tn = in ? g_tlitn[v.tok_at + c] : 0u;
+    const bool whole_lit = full && tn != kNoTokLit;
     uint32_t nb = 0;
     LaneBits dummy{0, 0, 0};
     if (runm) {
@@ -820,45 +855,28 @@ __device__ uint32_t wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, ui
         if (m2) nb += wv_match<false>(dummy, m2, t);
     } else if (dist) {
         nb = wv_match<false>(dummy, t, dist);
+    } else if (whole_lit) {
+        nb = tn;
     } else if (in) {
-        const uint32_t tn = g_tlitn[v.tok_at + c];
-        if (full && tn != kNoTokLit) nb = tn;
-        else for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
-    if (kWrite) {
-        LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
-        if (runm) {
-            if (m1) wv_match<true>(off, m1, t);
-            if (m2) wv_match<true>(off, m2, t);
-        } else if (dist) {
-            wv_match<true>(off, t, dist);
-        } else if (in) {
-            const uint32_t tn = g_tlitn[v.tok_at + c];
-            if (full && tn != kNoTokLit) {
-                const uint4 L = g_tlit[v.tok_at + c];
-                const uint32_t lw[4] = {L.x, L.y, L.z, L.w};
+    const uint32_t base = wv_chain(i, wave_sum(nb), lane);
+    LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
+    if (runm) {
+        if (m1) wv_match<true>(off, m1, t);
+        if (m2) wv_match<true>(off, m2, t);
+    } else if (dist) {
+        wv_match<true>(off, t, dist);
+    } else if (whole_lit) {
+        const uint4 L = g_tlit[v.tok_at + c];
+        const uint32_t lw[4] = {L.x, L.y, L.z, L.w};
 #pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (tn > 32u * j) off.put(lw[j], min(tn - 32u * j, 32u));
-            } else {
-                for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
-            }
-        }
-        off.finish();
-    } else if (full) {  // the text's dwords, ORed (neighbouring texts share edge dwords)
-        const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
-        const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
-        uint32_t prev = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 5; j++) {
-            const uint32_t d = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
-            prev = T[j];
-            if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), d);
-        }
+        for (int j = 0; j < 4; j++)
+            if (tn > 32u * j) off.put(lw[j], min(tn - 32u * j, 32u));
     } else if (in) {
-        for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
+        for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
-    return wave_sum(nb);
+    off.finish();
 }
 
 __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
@@ -876,7 +894,8 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     {
         for (uint32_t i = tid; i < 256; i += kWv) S.crc_tab[i] = A.crc_tab[i];
         for (uint32_t i = tid; i < kCrcOps * 32; i += kWv) S.crc_ops[i] = A.crc_ops[i];
-        for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = 0;
+        for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
+        for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = 0;
         const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
         for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
@@ -962,33 +981,13 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     }
     __syncthreads();
     const uint32_t n_items = g_ioff[kWvItems];
-    // pass 1: each item's bits; the block's bytes into g_text
-    for (uint32_t i = wave; i < n_items; i += kWv / 64) {
-        const uint32_t nb = wv_item<false>(A, C, b0, e, g_item[i], 0, lane);
-        if (lane == 0) g_ioff[i] = nb;
-    }
+    // the items in one pass (wv_item: the bytes, the bit count, the chained offset, the
+    // bits); a block that does not shrink to the bit buffer is stored instead
+    for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item(A, C, b0, e, i, lane);
     __syncthreads();
-    // exclusive scan of the items' bits (n_items <= kWv)
-    {
-        const uint32_t v = tid < n_items ? g_ioff[tid] : 0u;
-        const uint32_t x = wave_excl_sum(v, lane);
-        if (lane == 63) g_red[wave] = x + v;
-        __syncthreads();
-        uint32_t carry = 0;
-        for (uint32_t w = 0; w < wave; w++) carry += g_red[w];
-        __syncthreads();
-        if (tid < n_items) g_ioff[tid] = carry + x;
-        if (tid == kWv - 1) g_ioff[kWvItems] = carry + x + v;
-    }
-    __syncthreads();
-    const uint32_t total_bits = 3 + g_ioff[kWvItems] + 7;  // BFINAL + BTYPE, symbols, end of block
+    const uint32_t total_bits = g_pub[n_items - 1] - 1 + 7;  // BFINAL + BTYPE, symbols, end of block
     const uint32_t dbytes = (total_bits + 7) / 8;
     const bool stored = dbytes > 4 * kBitWords;
-    if (!stored) {  // pass 2: the bits at their offsets
-        if (tid == 0) g_bits[0] = 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-        __syncthreads();
-        for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item<true>(A, C, b0, e, g_item[i], 3 + g_ioff[i], lane);
-    }
     // the CRC32 of the block's bytes: 64 per thread counted from the block's end (so
     // that thread t's CRC shifts by 64 (kWv - 1 - t) bytes: one operator of the
     // table), XORed
