@@ -918,37 +918,23 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     return TFBS_OK;
 }
 
-int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
-                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
-                         uint64_t *text_bytes) {
-    if (!ctx || !b || !chromosome || !fake_position || fd < 0) return tfbs::fail(TFBS_E_ARG, "null argument");
-    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
-    Batch &B = b->b;
-    r1 = std::min(r1, B.rh.size());
-    r0 = std::min(r0, r1);
-    if (!B.reduced || B.enc_r0 > r0 || B.enc_r1 < r1)
-        return tfbs::fail(TFBS_E_STATE, "regions not encoded on this ctx (tfbs_batch_encode)");
-    HIP_TRY(hipSetDevice(ctx->device));
+namespace {
+
+// The device half of tfbs_batch_rows_bgzf: one row plan's BGZF blocks made on the
+// GPU and written to fd (written += their bytes).
+int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, int fd, uint64_t &written) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    const double t0 = now();
-    tfbs::RowPlan plan;
     int rc;
-    if ((rc = tfbs::build_row_plan(B, r0, r1, chromosome, min_maf, fake_position, ctx->host_threads, plan))) return rc;
-    const double t1 = now();
-    ctx->rows_s[0] += t1 - t0;
     struct Done {  // the device part's seconds, on every exit
         tfbs_ctx *c;
         double t;
         double (*f)();
         ~Done() { c->rows_s[1] += f() - t; }
-    } done{ctx, t1, +[] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }};
+    } done{ctx, now(), +[] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); }};
     const uint32_t N = B.n_samples, ng = (N + kCumGroup - 1) / kCumGroup;
     const uint64_t n_blocks = (plan.text_bytes + kBgzfRaw - 1) / kBgzfRaw;
     if ((uint64_t)plan.rows.size() * (ng + 1) >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many rows in one call");
     for (size_t i = 0; i < plan.rows.size(); i++) plan.rows[i].cum_off = (uint32_t)(i * (ng + 1));
-    if (n_rows) *n_rows = plan.n_rows;
-    if (text_bytes) *text_bytes = plan.text_bytes;
-    uint64_t written = 0;
     if (n_blocks) {
         if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
             std::vector<uint32_t> t(256 + 32 * kBgzfOps + 32 * tfbs::bgzf_crc_ops64_count());
@@ -1032,6 +1018,55 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         }
         if ((rc = drain(n_batches - 1))) return rc;
     }
+    return TFBS_OK;
+}
+
+}  // namespace
+
+int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
+                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                         uint64_t *text_bytes) {
+    if (!ctx || !b || !chromosome || !fake_position || fd < 0) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    Batch &B = b->b;
+    r1 = std::min(r1, B.rh.size());
+    r0 = std::min(r0, r1);
+    if (!B.reduced || B.enc_r0 > r0 || B.enc_r1 < r1)
+        return tfbs::fail(TFBS_E_STATE, "regions not encoded on this ctx (tfbs_batch_encode)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    // the regions in up to 4 pieces: a helper thread formats piece j + 1's rows (the
+    // host row plan: heads, POS, token tables) while the GPU makes piece j's blocks;
+    // every piece starts a new BGZF block (the decompressed stream is the same)
+    const size_t n = r1 - r0;
+    const size_t pieces = n >= 256 ? 4 : (n >= 64 ? 2 : 1);
+    auto cut = [&](size_t j) { return r0 + n * j / pieces; };
+    const std::string chrom(chromosome);
+    tfbs::RowPlan plans[2];
+    auto build = [&](size_t j) {
+        const double t0 = now();
+        const int r = tfbs::build_row_plan(B, cut(j), cut(j + 1), chrom, min_maf, fake_position, ctx->host_threads,
+                                           plans[j & 1]);
+        ctx->rows_s[0] += now() - t0;
+        return r;
+    };
+    int rc = build(0);
+    if (rc) return rc;
+    uint64_t written = 0, rows = 0, text = 0;
+    for (size_t j = 0; j < pieces; j++) {
+        int next_rc = TFBS_OK;
+        std::thread helper;
+        if (j + 1 < pieces) helper = std::thread([&, j] { next_rc = build(j + 1); });
+        tfbs::RowPlan &plan = plans[j & 1];
+        rows += plan.n_rows;
+        text += plan.text_bytes;
+        rc = rows_bgzf_device(ctx, B, plan, fd, written);
+        if (helper.joinable()) helper.join();
+        if (rc) return rc;
+        if (next_rc) return next_rc;
+    }
+    if (n_rows) *n_rows = rows;
+    if (text_bytes) *text_bytes = text;
     if (bytes) *bytes = written;
     return TFBS_OK;
 }
