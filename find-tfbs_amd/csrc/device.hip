@@ -41,11 +41,18 @@ struct DevBuf {
     int ensure(size_t want) {
         n = want;
         if (want <= cap) return TFBS_OK;
+        // geometric growth (hipFree waits for the device: a buffer regrown per call
+        // would serialise the pipelined callers), the exact size if that fails
+        size_t c = std::max<size_t>({want, cap + cap / 2, 16});
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t c = std::max<size_t>(want, 16);
         hipError_t e = hipMalloc(&p, c * sizeof(T));
+        if (e != hipSuccess && c > want) {
+            (void)hipGetLastError();
+            c = want;
+            e = hipMalloc(&p, c * sizeof(T));
+        }
         if (e != hipSuccess) return tfbs::fail(TFBS_E_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
         cap = c;
         return TFBS_OK;
@@ -170,7 +177,7 @@ namespace tfbs {
 int PinnedBytes::reserve(size_t n) {
     if (n <= cap) return TFBS_OK;
     release();
-    const size_t want = std::max<size_t>(n, 1 << 20);
+    const size_t want = std::max<size_t>({n, cap + cap / 2, (size_t)1 << 20});  // geometric: page-locking is slow
     if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) == hipSuccess) {
         pinned = true;
     } else {  // page-locked memory exhausted: pageable memory (slower copies, same results)
@@ -756,10 +763,22 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     if (nk) HIP_TRY(hipMemcpyAsync(vk.data(), ctx->var_keys.p, nk * sizeof(DevVarKey), hipMemcpyDeviceToHost, ctx->stream));
     if (nc) HIP_TRY(hipMemcpyAsync(B.var_counts.p, ctx->var_counts.p, (size_t)nc * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    // the varying keys in (region, key) order; their counts stay where the device put them
-    std::sort(vk.begin(), vk.end(), [](const DevVarKey &x, const DevVarKey &y) {
-        return x.region != y.region ? x.region < y.region : x.j < y.j;
-    });
+    // the varying keys in (region, key) order -- a counting sort by region, then each
+    // region's few keys by key; their counts stay where the device put them
+    {
+        std::vector<uint32_t> at(B.regions.size() + 1, 0);
+        for (const DevVarKey &k : vk) at[k.region + 1]++;
+        for (size_t r = 0; r < B.regions.size(); r++) at[r + 1] += at[r];
+        std::vector<DevVarKey> by(nk);
+        {
+            std::vector<uint32_t> put(at.begin(), at.end() - 1);
+            for (const DevVarKey &k : vk) by[put[k.region]++] = k;
+        }
+        for (size_t r = 0; r < B.regions.size(); r++)
+            std::sort(by.begin() + at[r], by.begin() + at[r + 1],
+                      [](const DevVarKey &x, const DevVarKey &y) { return x.j < y.j; });
+        vk.swap(by);
+    }
     B.var_off.assign(n_keys, UINT32_MAX);
     B.var_idx.assign(n_keys, UINT32_MAX);
     for (uint32_t i = 0; i < nk; i++) {
@@ -854,9 +873,15 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     // the keys to encode: varying keys of [r0, r1) whose region's pairs were listed
     // (<= kEncMaxHaps distinct haplotypes, <= kEncMaxPairs pairs; the others keep the host path)
     std::vector<DevVarKey> ek;
-    for (uint32_t i = 0; i < B.var_keys.size(); i++) {
+    // (B.var_keys is in region order: tfbs_batch_reduce)
+    auto region_lb = [&](size_t r) {
+        return (uint32_t)(std::lower_bound(B.var_keys.begin(), B.var_keys.end(), r,
+                                           [](const DevVarKey &k, size_t x) { return k.region < x; }) -
+                          B.var_keys.begin());
+    };
+    for (uint32_t i = region_lb(r0), i1 = region_lb(r1); i < i1; i++) {
         const DevVarKey &k = B.var_keys[i];
-        if (k.region < r0 || k.region >= r1 || pair_n[k.region - r0] == UINT32_MAX) continue;
+        if (pair_n[k.region - r0] == UINT32_MAX) continue;
         B.enc_idx[i] = (uint32_t)ek.size();
         ek.push_back(k);
     }
@@ -903,7 +928,8 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
         }
         const uint64_t total = B.enc_code_off[nk];
         if ((rc = ctx->enc_off.put(B.enc_code_off, ctx->stream)) ||
-            (rc = ctx->enc_packed.ensure(std::max<uint64_t>(total, 1))) || (rc = B.enc_codes.reserve(total)))
+            (rc = ctx->enc_packed.ensure(std::max<uint64_t>(total, 1))) ||
+            (!(flags & TFBS_ENC_DEVICE_CODES) && (rc = B.enc_codes.reserve(total))))
             return rc;
         if ((rc = launch_code_compact(ctx->enc_codes.p, (uint32_t)nk, N, ctx->enc_off.p, ctx->enc_packed.p,
                                       ctx->stream)))
