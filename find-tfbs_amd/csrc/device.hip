@@ -946,9 +946,43 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
 
 namespace {
 
-// The device half of tfbs_batch_rows_bgzf: one row plan's BGZF blocks made on the
-// GPU and written to fd (written += their bytes).
-int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, int fd, uint64_t &written) {
+// The BGZF batches of one tfbs_batch_rows_bgzf call, across its pieces: batch i uses
+// slot i & 1; a launched batch is written out after the next one is launched (also
+// the next piece's first), so the GPU never waits for a copy back or a file write.
+struct BgPipe {
+    uint64_t next = 0;  // the call's next batch
+    int pending = -1;   // the slot of the launched batch not yet written (-1: none)
+    uint64_t written = 0;
+};
+
+// The launched batch in slot k: its packed blocks back (copy stream) and to fd.
+int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
+    HIP_TRY(hipEventSynchronize(ctx->bg_done[k]));
+    const uint64_t total = ctx->bg_total_host[k];
+    int r;
+    if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
+    if (total)
+        HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost, ctx->copy_stream));
+    HIP_TRY(hipEventRecord(ctx->bg_copied[k], ctx->copy_stream));
+    HIP_TRY(hipEventSynchronize(ctx->bg_copied[k]));
+    for (uint64_t at = 0; at < total;) {  // the blocks to the file as they are
+        const ssize_t w = ::write(fd, ctx->bg_host[k].p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
+        }
+        at += (uint64_t)w;
+    }
+    written += total;
+    return TFBS_OK;
+}
+
+// The device half of tfbs_batch_rows_bgzf: one row plan's BGZF blocks launched on the
+// GPU (the previous batch written out after each launch: BgPipe).  plan and heads
+// (its heads as uploaded) must stay untouched until this piece's first batch has
+// been written, i.e. until the next piece's device half has launched.
+int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::vector<char> &heads, int fd,
+                     BgPipe &pp) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     int rc;
     struct Done {  // the device part's seconds, on every exit
@@ -961,88 +995,66 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, int fd,
     const uint64_t n_blocks = (plan.text_bytes + kBgzfRaw - 1) / kBgzfRaw;
     if ((uint64_t)plan.rows.size() * (ng + 1) >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many rows in one call");
     for (size_t i = 0; i < plan.rows.size(); i++) plan.rows[i].cum_off = (uint32_t)(i * (ng + 1));
-    if (n_blocks) {
-        if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
-            std::vector<uint32_t> t(256 + 32 * kBgzfOps + 32 * tfbs::bgzf_crc_ops64_count());
-            tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
-            if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
-        }
-        std::vector<char> heads(plan.heads.begin(), plan.heads.end());
-        if ((rc = ctx->bg_rows.put(plan.rows, ctx->stream)) || (rc = ctx->bg_heads.put(heads, ctx->stream)) ||
-            (rc = ctx->bg_tok_text.put(plan.tok_text, ctx->stream)) ||
-            (rc = ctx->bg_tok_len.put(plan.tok_len, ctx->stream)) ||
-            (rc = ctx->bg_cum.ensure(std::max<size_t>(plan.rows.size() * (ng + 1), 1))))
+    if (!n_blocks) {  // nothing launched: the pending batch goes out now (its piece's host data is released)
+        if (pp.pending >= 0 && (rc = bgzf_drain(ctx, pp.pending, fd, pp.written))) return rc;
+        pp.pending = -1;
+        return TFBS_OK;
+    }
+    if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
+        std::vector<uint32_t> t(256 + 32 * kBgzfOps + 32 * tfbs::bgzf_crc_ops64_count());
+        tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
+        if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
+    }
+    heads.assign(plan.heads.begin(), plan.heads.end());
+    if ((rc = ctx->bg_rows.put(plan.rows, ctx->stream)) || (rc = ctx->bg_heads.put(heads, ctx->stream)) ||
+        (rc = ctx->bg_tok_text.put(plan.tok_text, ctx->stream)) ||
+        (rc = ctx->bg_tok_len.put(plan.tok_len, ctx->stream)) ||
+        (rc = ctx->bg_cum.ensure(std::max<size_t>(plan.rows.size() * (ng + 1), 1))))
+        return rc;
+    tfbs::BgArgs a{};
+    a.rows = ctx->bg_rows.p;
+    a.n_rows = (uint32_t)plan.rows.size();
+    a.heads = ctx->bg_heads.p;
+    a.tok_text = ctx->bg_tok_text.p;
+    a.tok_len = ctx->bg_tok_len.p;
+    a.codes = ctx->enc_packed.p;
+    a.cum = ctx->bg_cum.p;
+    a.n_samples = N;
+    a.text_bytes = plan.text_bytes;
+    a.crc_tab = ctx->bg_crc.p;
+    a.crc_ops = ctx->bg_crc.p + 256;
+    a.crc_ops64 = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
+    if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
+    constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
+    const uint64_t n_batches = (n_blocks + kBatchBlocks - 1) / kBatchBlocks;
+    if (!ctx->bg_total_host) HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 16, hipHostMallocDefault));
+    for (int k = 0; k < 2; k++) {
+        if (!ctx->bg_done[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_done[k], hipEventDisableTiming));
+        if (!ctx->bg_copied[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_copied[k], hipEventDisableTiming));
+    }
+    if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    for (uint64_t i = 0; i < n_batches; i++, pp.next++) {
+        const int k = (int)(pp.next & 1);
+        const uint64_t b0 = i * kBatchBlocks;
+        const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
+        if ((rc = ctx->bg_out[k].ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len[k].ensure(nb)) ||
+            (rc = ctx->bg_off[k].ensure(nb + 1)) || (rc = ctx->bg_packed[k].ensure((size_t)nb * kBgzfMax)) ||
+            (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
             return rc;
-        tfbs::BgArgs a{};
-        a.rows = ctx->bg_rows.p;
-        a.n_rows = (uint32_t)plan.rows.size();
-        a.heads = ctx->bg_heads.p;
-        a.tok_text = ctx->bg_tok_text.p;
-        a.tok_len = ctx->bg_tok_len.p;
-        a.codes = ctx->enc_packed.p;
-        a.cum = ctx->bg_cum.p;
-        a.n_samples = N;
-        a.text_bytes = plan.text_bytes;
-        a.crc_tab = ctx->bg_crc.p;
-        a.crc_ops = ctx->bg_crc.p + 256;
-        a.crc_ops64 = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
-        if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
-        // batches of blocks in two slots: while the device makes batch i, the host copies
-        // batch i - 1's packed blocks back (copy stream) and writes them to fd
-        constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
-        const uint64_t n_batches = (n_blocks + kBatchBlocks - 1) / kBatchBlocks;
-        if (!ctx->bg_total_host) HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 16, hipHostMallocDefault));
-        for (int k = 0; k < 2; k++) {
-            if (!ctx->bg_done[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_done[k], hipEventDisableTiming));
-            if (!ctx->bg_copied[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_copied[k], hipEventDisableTiming));
-        }
-        if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
-        auto drain = [&](uint64_t i) -> int {  // batch i's blocks to fd
-            const int k = (int)(i & 1);
-            HIP_TRY(hipEventSynchronize(ctx->bg_done[k]));
-            const uint64_t total = ctx->bg_total_host[k];
-            int r;
-            if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
-            if (total)
-                HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost,
-                                       ctx->copy_stream));
-            HIP_TRY(hipEventRecord(ctx->bg_copied[k], ctx->copy_stream));
-            HIP_TRY(hipEventSynchronize(ctx->bg_copied[k]));
-            for (uint64_t at = 0; at < total;) {  // the blocks to the file as they are
-                const ssize_t w = ::write(fd, ctx->bg_host[k].p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
-                if (w < 0) {
-                    if (errno == EINTR) continue;
-                    return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
-                }
-                at += (uint64_t)w;
-            }
-            written += total;
-            return TFBS_OK;
-        };
-        for (uint64_t i = 0; i < n_batches; i++) {
-            const int k = (int)(i & 1);
-            const uint64_t b0 = i * kBatchBlocks;
-            const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
-            if ((rc = ctx->bg_out[k].ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len[k].ensure(nb)) ||
-                (rc = ctx->bg_off[k].ensure(nb + 1)) || (rc = ctx->bg_packed[k].ensure((size_t)nb * kBgzfMax)) ||
-                (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
-                return rc;
-            // slot k's packed blocks were copied back (batch i - 2) before they are overwritten
-            if (i >= 2) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
-            a.plans = ctx->bg_plans.p;
-            a.block0 = b0;
-            a.out = ctx->bg_out[k].p;
-            a.out_len = ctx->bg_out_len[k].p;
-            if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) ||
-                (rc = tfbs::launch_bgzf_compact(ctx->bg_out[k].p, ctx->bg_out_len[k].p, ctx->bg_off[k].p, nb,
-                                                ctx->bg_packed[k].p, ctx->stream)))
-                return rc;
-            HIP_TRY(hipMemcpyAsync(ctx->bg_total_host + k, ctx->bg_off[k].p + nb, 8, hipMemcpyDeviceToHost,
-                                   ctx->stream));
-            HIP_TRY(hipEventRecord(ctx->bg_done[k], ctx->stream));
-            if (i >= 1 && (rc = drain(i - 1))) return rc;
-        }
-        if ((rc = drain(n_batches - 1))) return rc;
+        // slot k's packed blocks were copied back (two batches ago) before they are overwritten
+        if (pp.next >= 2) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+        a.plans = ctx->bg_plans.p;
+        a.block0 = b0;
+        a.out = ctx->bg_out[k].p;
+        a.out_len = ctx->bg_out_len[k].p;
+        if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) ||
+            (rc = tfbs::launch_bgzf_compact(ctx->bg_out[k].p, ctx->bg_out_len[k].p, ctx->bg_off[k].p, nb,
+                                            ctx->bg_packed[k].p, ctx->stream)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(ctx->bg_total_host + k, ctx->bg_off[k].p + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipEventRecord(ctx->bg_done[k], ctx->stream));
+        if (pp.pending >= 0 && (rc = bgzf_drain(ctx, pp.pending, fd, pp.written))) return rc;
+        pp.pending = k;
     }
     return TFBS_OK;
 }
@@ -1061,39 +1073,49 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         return tfbs::fail(TFBS_E_STATE, "regions not encoded on this ctx (tfbs_batch_encode)");
     HIP_TRY(hipSetDevice(ctx->device));
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    // the regions in up to 4 pieces: a helper thread formats piece j + 1's rows (the
-    // host row plan: heads, POS, token tables) while the GPU makes piece j's blocks;
-    // every piece starts a new BGZF block (the decompressed stream is the same)
+    // the regions in pieces of >= 64 (at most 8): a helper thread formats piece j + 1's
+    // rows (the host row plan: heads, POS, token tables) while the GPU makes piece j's
+    // blocks; every piece starts a new BGZF block (the decompressed stream is the same).
+    // Three plan slots: piece j's host data stays put until piece j + 1 has launched
+    // (rows_bgzf_device), while piece j + 2's is being built.
     const size_t n = r1 - r0;
-    const size_t pieces = n >= 256 ? 4 : (n >= 64 ? 2 : 1);
+    const size_t pieces = std::max<size_t>(1, std::min<size_t>(8, n / 64));
     auto cut = [&](size_t j) { return r0 + n * j / pieces; };
     const std::string chrom(chromosome);
-    tfbs::RowPlan plans[2];
+    tfbs::RowPlan plans[3];
+    std::vector<char> heads[3];
     auto build = [&](size_t j) {
         const double t0 = now();
         const int r = tfbs::build_row_plan(B, cut(j), cut(j + 1), chrom, min_maf, fake_position, ctx->host_threads,
-                                           plans[j & 1]);
+                                           plans[j % 3]);
         ctx->rows_s[0] += now() - t0;
         return r;
     };
     int rc = build(0);
     if (rc) return rc;
-    uint64_t written = 0, rows = 0, text = 0;
+    BgPipe pp;
+    uint64_t rows = 0, text = 0;
     for (size_t j = 0; j < pieces; j++) {
         int next_rc = TFBS_OK;
         std::thread helper;
         if (j + 1 < pieces) helper = std::thread([&, j] { next_rc = build(j + 1); });
-        tfbs::RowPlan &plan = plans[j & 1];
+        tfbs::RowPlan &plan = plans[j % 3];
         rows += plan.n_rows;
         text += plan.text_bytes;
-        rc = rows_bgzf_device(ctx, B, plan, fd, written);
+        rc = rows_bgzf_device(ctx, B, plan, heads[j % 3], fd, pp);
         if (helper.joinable()) helper.join();
         if (rc) return rc;
         if (next_rc) return next_rc;
     }
+    if (pp.pending >= 0) {
+        const double t0 = now();
+        rc = bgzf_drain(ctx, pp.pending, fd, pp.written);
+        ctx->rows_s[1] += now() - t0;
+        if (rc) return rc;
+    }
     if (n_rows) *n_rows = rows;
     if (text_bytes) *text_bytes = text;
-    if (bytes) *bytes = written;
+    if (bytes) *bytes = pp.written;
     return TFBS_OK;
 }
 
