@@ -741,7 +741,34 @@ __device__ __forceinline__ uint32_t wv_chain(uint32_t i, uint32_t total, uint32_
 __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane) {
     const uint32_t item = g_item[i];
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
-    const RowView v = C.view(g_st.P.r_first + d);
+    // the item's row as wave-uniform values (SGPRs: its arithmetic is scalar)
+    RowView v;
+    {
+        const DevRow &R = g_st.rows[d];
+        auto u32 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
+        auto u64 = [&](uint64_t x) { return (uint64_t)u32((uint32_t)x) | ((uint64_t)u32((uint32_t)(x >> 32)) << 32); };
+        v.R.text_off = u64(R.text_off);
+        v.R.geno_len = u64(R.geno_len);
+        v.R.code_off = u64(R.code_off);
+        v.R.head_off = u32(R.head_off);
+        v.R.head_len = u32(R.head_len);
+        v.R.tok = u32(R.tok);
+        v.R.width = u32(R.width);
+        v.R.cum_off = u32(R.cum_off);
+        v.R.nv = u32(R.nv);
+        v.mask = (1u << v.R.width) - 1u;
+        if (kind == IT_GROUP) {  // its staged codes, tokens and group offsets (item bits 20-22)
+            const StRow &T = g_st.P.st[(item >> 20) & 7u];
+            v.cbase = (int32_t)u32(T.code_at) - (int32_t)u32(T.cfirst);
+            v.tok_at = u32(T.tok_at);
+            v.cum_at = u32(T.cum_at);
+            v.g_lo = u32(T.g_lo);
+            v.ncum = u32(T.ncum);
+        } else {
+            v.cbase = 0;
+            v.tok_at = v.cum_at = v.g_lo = v.ncum = 0;
+        }
+    }
     if (kind == IT_NL) {
         const uint32_t base = wv_chain(i, 8, lane);
         if (lane == 0) {
@@ -776,7 +803,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         return;
     }
     // a 64-sample group
-    const uint32_t g = item & 0x7FFFFFu, N = A.n_samples;
+    const uint32_t g = item & 0xFFFFFu, N = A.n_samples;
     const uint32_t s = g * kCumGroup + lane;
     const bool valid = s < N;
     uint32_t c = 0, t = 0;
@@ -786,8 +813,9 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     }
     const uint4 tx = C.ttext(v, c);
     // the text's first byte relative to the block start (may be negative at its edge)
-    const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + g_st.cum[v.cum_at + g - v.g_lo]) -
-                                  (int64_t)b0) + (int32_t)wave_excl_sum(t, lane);
+    const uint32_t cum_g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_st.cum[v.cum_at + g - v.g_lo]);
+    const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0) +
+                        (int32_t)wave_excl_sum(t, lane);
     const int32_t n = (int32_t)(e - b0);
     const int32_t lo = max(rel, 0), hi = min(rel + (int32_t)t, n);
     const bool in = valid && hi > lo;
@@ -975,7 +1003,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         for (uint32_t k = 0; k < S.P.n_st; k++)
             if (S.P.st[k].row == S.P.r_first + tid)
                 for (uint32_t q = 0; q + 1 < S.P.st[k].ncum; q++)
-                    g_item[at++] = (IT_GROUP << 30) | (tid << 23) | (S.P.st[k].g_lo + q);
+                    g_item[at++] = (IT_GROUP << 30) | (tid << 23) | (k << 20) | (S.P.st[k].g_lo + q);
         const uint64_t nl = R.text_off + R.head_len + R.geno_len;
         if (nl >= b0 && nl < e) g_item[at++] = (IT_NL << 30) | (tid << 23);
     }
