@@ -139,6 +139,7 @@ struct tfbs_ctx {
     DevBuf<DevVarKey> var_keys, enc_keys;
     uint32_t var_keys_cap = 1u << 16;
     uint64_t var_cap = 1u << 24;
+    bool var_cap_forced = false;     // TFBS_VAR_CAP applied (tfbs_batch_reduce)
     uint32_t *var_tot_host = nullptr;    // pinned
     // per-sample encoding (tfbs_batch_encode)
     DevBuf<uint8_t> enc_codes, enc_packed;
@@ -730,7 +731,20 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         return rc;
     if (!ctx->var_tot_host) HIP_TRY(hipHostMalloc((void **)&ctx->var_tot_host, 8, hipHostMallocDefault));
     // per region: the keys' flags and first counts, and the varying keys' counts
-    // appended to a compact list (grown and redone if it was too small)
+    // appended to a compact list (grown and redone if it was too small); a first
+    // guess of 1/16 of the keys and of the dense counts avoids the rerun at C3 shapes
+    // (TFBS_VAR_CAP=n: lists of n keys and 4 n counts at first, no guess -- the
+    // regrow path's test)
+    if (const int vc = env_int("TFBS_VAR_CAP", 0); vc > 0) {
+        if (!ctx->var_cap_forced) {
+            ctx->var_keys_cap = (uint32_t)vc;
+            ctx->var_cap = 4ull * (uint32_t)vc;
+            ctx->var_cap_forced = true;
+        }
+    } else {
+        ctx->var_keys_cap = std::max<uint32_t>(ctx->var_keys_cap, (uint32_t)std::min<uint64_t>(n_keys / 16, 1u << 26));
+        ctx->var_cap = std::max<uint64_t>(ctx->var_cap, std::min<uint64_t>(B.n_counts / 16, 1ull << 28));
+    }
     for (int round = 0;; round++) {
         if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
         AsmArgs a = asm_args(ctx, B, 0);

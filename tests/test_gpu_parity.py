@@ -374,6 +374,8 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
         monkeypatch.setenv("TFBS_DEDUP", "1")
         monkeypatch.setenv("TFBS_CAND_CAP", "64")
         monkeypatch.setenv("TFBS_CAND_OVER_CAP", "16")
+        # and varying-key lists of 8 keys / 32 counts: the key reduction grows them and reruns
+        monkeypatch.setenv("TFBS_VAR_CAP", "8")
         _compare(ps, n_samples, beds, regions)
 
 
