@@ -159,12 +159,13 @@ struct tfbs_ctx {
     DevBuf<uint8_t> bg_tok_len, bg_plans;
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
     // two slots of block batches (one being made, one copied back and written)
-    DevBuf<uint8_t> bg_out[2], bg_packed[2];
-    DevBuf<uint32_t> bg_out_len[2];
-    DevBuf<uint64_t> bg_off[2];
-    tfbs::PinnedBytes bg_host[2];     // compressed blocks staged for the host
+    static constexpr int kBgSlots = 3;  // batches of blocks in flight: two queued while one is written out
+    DevBuf<uint8_t> bg_out[kBgSlots], bg_packed[kBgSlots];
+    DevBuf<uint32_t> bg_out_len[kBgSlots];
+    DevBuf<uint64_t> bg_off[kBgSlots];
+    tfbs::PinnedBytes bg_host[kBgSlots];  // compressed blocks staged for the host
     uint64_t *bg_total_host = nullptr;  // pinned: each slot's packed bytes
-    hipEvent_t bg_done[2] = {}, bg_copied[2] = {};
+    hipEvent_t bg_done[kBgSlots] = {}, bg_copied[kBgSlots] = {};
     hipStream_t copy_stream = nullptr;
     double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
     const tfbs_batch *resident = nullptr;
@@ -482,7 +483,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
     ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release();
-    for (int k = 0; k < 2; k++) {
+    for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
         ctx->bg_host[k].release();
         if (ctx->bg_done[k]) (void)hipEventDestroy(ctx->bg_done[k]);
@@ -961,12 +962,20 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
 namespace {
 
 // The BGZF batches of one tfbs_batch_rows_bgzf call, across its pieces: batch i uses
-// slot i & 1; a launched batch is written out after the next one is launched (also
-// the next piece's first), so the GPU never waits for a copy back or a file write.
+// slot i % kBgSlots; a launched batch is written out once two more are queued behind
+// it (also across pieces), so the GPU never waits for a copy back or a file write.
+int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written);
 struct BgPipe {
-    uint64_t next = 0;  // the call's next batch
-    int pending = -1;   // the slot of the launched batch not yet written (-1: none)
+    uint64_t next = 0;                      // the call's next batch
+    int pending[tfbs_ctx::kBgSlots] = {};   // launched batches not yet written (their slots, oldest first)
+    int n_pending = 0;
     uint64_t written = 0;
+    int drain_oldest(tfbs_ctx *ctx, int fd) {
+        const int rc = bgzf_drain(ctx, pending[0], fd, written);
+        for (int i = 1; i < n_pending; i++) pending[i - 1] = pending[i];
+        n_pending--;
+        return rc;
+    }
 };
 
 // The launched batch in slot k: its packed blocks back (copy stream) and to fd.
@@ -992,9 +1001,9 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
 }
 
 // The device half of tfbs_batch_rows_bgzf: one row plan's BGZF blocks launched on the
-// GPU (the previous batch written out after each launch: BgPipe).  plan and heads
-// (its heads as uploaded) must stay untouched until this piece's first batch has
-// been written, i.e. until the next piece's device half has launched.
+// GPU (older batches written out as newer ones queue: BgPipe).  plan and heads (its
+// heads as uploaded) must stay untouched until one of this piece's batches has been
+// written out.
 int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::vector<char> &heads, int fd,
                      BgPipe &pp) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1009,9 +1018,9 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     const uint64_t n_blocks = (plan.text_bytes + kBgzfRaw - 1) / kBgzfRaw;
     if ((uint64_t)plan.rows.size() * (ng + 1) >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many rows in one call");
     for (size_t i = 0; i < plan.rows.size(); i++) plan.rows[i].cum_off = (uint32_t)(i * (ng + 1));
-    if (!n_blocks) {  // nothing launched: the pending batch goes out now (its piece's host data is released)
-        if (pp.pending >= 0 && (rc = bgzf_drain(ctx, pp.pending, fd, pp.written))) return rc;
-        pp.pending = -1;
+    if (!n_blocks) {  // nothing launched: the pending batches go out now (their pieces' host data is released)
+        while (pp.n_pending)
+            if ((rc = pp.drain_oldest(ctx, fd))) return rc;
         return TFBS_OK;
     }
     if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
@@ -1041,22 +1050,23 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
     constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
     const uint64_t n_batches = (n_blocks + kBatchBlocks - 1) / kBatchBlocks;
-    if (!ctx->bg_total_host) HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 16, hipHostMallocDefault));
-    for (int k = 0; k < 2; k++) {
+    if (!ctx->bg_total_host)
+        HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 8 * tfbs_ctx::kBgSlots, hipHostMallocDefault));
+    for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         if (!ctx->bg_done[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_done[k], hipEventDisableTiming));
         if (!ctx->bg_copied[k]) HIP_TRY(hipEventCreateWithFlags(&ctx->bg_copied[k], hipEventDisableTiming));
     }
     if (!ctx->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
     for (uint64_t i = 0; i < n_batches; i++, pp.next++) {
-        const int k = (int)(pp.next & 1);
+        const int k = (int)(pp.next % tfbs_ctx::kBgSlots);
         const uint64_t b0 = i * kBatchBlocks;
         const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
         if ((rc = ctx->bg_out[k].ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len[k].ensure(nb)) ||
             (rc = ctx->bg_off[k].ensure(nb + 1)) || (rc = ctx->bg_packed[k].ensure((size_t)nb * kBgzfMax)) ||
             (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
             return rc;
-        // slot k's packed blocks were copied back (two batches ago) before they are overwritten
-        if (pp.next >= 2) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+        // slot k's packed blocks were copied back (kBgSlots batches ago) before they are overwritten
+        if (pp.next >= (uint64_t)tfbs_ctx::kBgSlots) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
         a.plans = ctx->bg_plans.p;
         a.block0 = b0;
         a.out = ctx->bg_out[k].p;
@@ -1067,8 +1077,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
             return rc;
         HIP_TRY(hipMemcpyAsync(ctx->bg_total_host + k, ctx->bg_off[k].p + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->bg_done[k], ctx->stream));
-        if (pp.pending >= 0 && (rc = bgzf_drain(ctx, pp.pending, fd, pp.written))) return rc;
-        pp.pending = k;
+        pp.pending[pp.n_pending++] = k;
+        if (pp.n_pending == tfbs_ctx::kBgSlots && (rc = pp.drain_oldest(ctx, fd))) return rc;
     }
     return TFBS_OK;
 }
@@ -1090,18 +1100,21 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
     // the regions in pieces of >= 64 (at most 8): a helper thread formats piece j + 1's
     // rows (the host row plan: heads, POS, token tables) while the GPU makes piece j's
     // blocks; every piece starts a new BGZF block (the decompressed stream is the same).
-    // Three plan slots: piece j's host data stays put until piece j + 1 has launched
-    // (rows_bgzf_device), while piece j + 2's is being built.
+    // kBgSlots + 1 plan slots: piece j's host data (uploaded by its device half) stays
+    // put until one of its batches has been written out -- by then the host has waited
+    // for an event after its uploads -- which BgPipe's lag guarantees before the helper
+    // builds piece j + kBgSlots + 1 into the same slot.
     const size_t n = r1 - r0;
     const size_t pieces = std::max<size_t>(1, std::min<size_t>(8, n / 64));
     auto cut = [&](size_t j) { return r0 + n * j / pieces; };
     const std::string chrom(chromosome);
-    tfbs::RowPlan plans[3];
-    std::vector<char> heads[3];
+    constexpr size_t kPlanSlots = tfbs_ctx::kBgSlots + 1;
+    tfbs::RowPlan plans[kPlanSlots];
+    std::vector<char> heads[kPlanSlots];
     auto build = [&](size_t j) {
         const double t0 = now();
         const int r = tfbs::build_row_plan(B, cut(j), cut(j + 1), chrom, min_maf, fake_position, ctx->host_threads,
-                                           plans[j % 3]);
+                                           plans[j % kPlanSlots]);
         ctx->rows_s[0] += now() - t0;
         return r;
     };
@@ -1113,17 +1126,17 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         int next_rc = TFBS_OK;
         std::thread helper;
         if (j + 1 < pieces) helper = std::thread([&, j] { next_rc = build(j + 1); });
-        tfbs::RowPlan &plan = plans[j % 3];
+        tfbs::RowPlan &plan = plans[j % kPlanSlots];
         rows += plan.n_rows;
         text += plan.text_bytes;
-        rc = rows_bgzf_device(ctx, B, plan, heads[j % 3], fd, pp);
+        rc = rows_bgzf_device(ctx, B, plan, heads[j % kPlanSlots], fd, pp);
         if (helper.joinable()) helper.join();
         if (rc) return rc;
         if (next_rc) return next_rc;
     }
-    if (pp.pending >= 0) {
+    {
         const double t0 = now();
-        rc = bgzf_drain(ctx, pp.pending, fd, pp.written);
+        while (pp.n_pending && !rc) rc = pp.drain_oldest(ctx, fd);
         ctx->rows_s[1] += now() - t0;
         if (rc) return rc;
     }
