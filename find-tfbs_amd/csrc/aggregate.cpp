@@ -52,6 +52,10 @@ inline uint64_t key_of(const Batch &B, const RegionH &R, uint32_t slot, int32_t 
     return R.key_off + (uint64_t)slot * R.ranges.size() + (uint32_t)range_slot;
 }
 
+// Readers of the varying counts (count_of) on the host: the device key reduction's
+// counts are downloaded on first use (ensure_host_var_counts).
+inline int host_counts(const Batch &B) { return B.counts_valid ? 0 : ensure_host_var_counts(B); }
+
 // Count of distinct haplotype `local` for a key, from the dense download or
 // from the device key reduction (tfbs_batch_reduce).
 inline uint32_t count_of(const Batch &B, const RegionH &R, uint32_t local, uint32_t slot, int32_t range_slot) {
@@ -408,6 +412,7 @@ static void region_row_parts(const Batch &B, const RegionH &R, uint32_t min_maf,
                 l.resize(B.n_samples);
                 r.resize(B.n_samples);
             }
+            if (host_counts(B)) return;  // (build_row_plan returns the error)
             for (uint32_t s = 0; s < B.n_samples; s++) {
                 l[s] = count_of(B, R, M->local[2 * s], k.slot, k.ik->slot) * k.ik->mult;
                 r[s] = count_of(B, R, M->local[2 * s + 1], k.slot, k.ik->slot) * k.ik->mult;
@@ -460,6 +465,7 @@ int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chro
     for (uint32_t t = 1; t < threads && t < n; t++) ts.emplace_back(work);
     work();
     for (auto &t : ts) t.join();
+    if (!B.counts_valid && B.var_host && B.var_err) return B.var_err;  // a lazy count download failed
     // serially: POS, offsets in the stream, token slots
     plan = RowPlan();
     const std::string chr = strip_chr(chrom);
@@ -504,6 +510,7 @@ size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::stri
 // threads (main.rs:395-432).
 int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_t threads) {
     if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = host_counts(B)) return rc;  // the varying counts on the host
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
     const size_t n = B.rh.size();
     std::vector<std::string> rows(n);  // each region's rows
@@ -565,6 +572,7 @@ int tfbs_batch_region_key(const tfbs_batch *b, size_t region, size_t k, uint32_t
     if (!b || region >= b->b.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     const Batch &B = b->b;
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
     if (!B.keep_membership && B.n_samples && (left || right))
         return tfbs::fail(TFBS_E_STATE, "batch created without membership");
     const tfbs::RegionH &R = B.rh[region];
@@ -592,6 +600,7 @@ int tfbs_batch_region_rows(const tfbs_batch *b, size_t region, const char *chrom
     const Batch &B = b->b;
     if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
     if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
     std::string bodies;
     if (B.rh[region].hap_count) tfbs::region_rows(B, B.rh[region], min_maf, bodies);
@@ -627,6 +636,7 @@ int tfbs_batch_region_digest(const tfbs_batch *b, size_t region, uint64_t *diges
     const Batch &B = b->b;
     if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
     const tfbs::RegionH &R = B.rh[region];
     uint64_t h = 0x9E3779B97F4A7C15ull;
     auto mix = [&h](uint64_t x) {
@@ -661,6 +671,7 @@ int tfbs_batch_region_key_digest_sum(const tfbs_batch *b, size_t region, uint64_
     const Batch &B = b->b;
     if (region >= B.rh.size()) return tfbs::fail(TFBS_E_ARG, "bad region");
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
     const tfbs::RegionH &R = B.rh[region];
     uint64_t sum = 0;
     for (const auto &k : tfbs::region_keys(B, R)) {  // one hash per key, added: order-free
@@ -733,6 +744,7 @@ int tfbs_batch_format_rows(const tfbs_batch *b, const char *chromosome, uint32_t
     if (!b || !chromosome || !n_rows || !n_bytes) return tfbs::fail(TFBS_E_ARG, "null argument");
     const Batch &B = b->b;
     if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
     if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
     const size_t n = std::min(r1, B.rh.size());
     const size_t prefix = tfbs::strip_chr(chromosome).size() + 2;

@@ -898,7 +898,10 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     return TFBS_OK;
 }
 
-void tfbs_batch_destroy(tfbs_batch *b) { delete b; }
+void tfbs_batch_destroy(tfbs_batch *b) {
+    if (b) tfbs::forget_var_counts(b->b);
+    delete b;
+}
 
 int tfbs_batch_add_bed(tfbs_batch *b, const char *basename) {
     if (!b || !basename) return tfbs::fail(TFBS_E_ARG, "null argument");

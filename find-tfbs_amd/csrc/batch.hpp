@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -118,7 +119,18 @@ struct Batch {
     std::vector<uint32_t> key_first;
     std::vector<uint8_t> key_flags;
     std::vector<uint32_t> var_off;        // UINT32_MAX unless the key varies
-    PinnedBytes var_counts;  // u32 counts, downloaded into pinned memory
+    PinnedBytes var_counts;  // u32 counts, host copy (made on first use: ensure_host_var_counts)
+    // tfbs_batch_reduce leaves the varying counts on the device (the device encode
+    // and BGZF rows need no host copy); var_dev / var_n / var_device locate them
+    // while var_ctx holds them (its next reduction of another batch, or its
+    // destruction, makes the host copy first)
+    mutable std::mutex var_mu;
+    const void *var_dev = nullptr;
+    size_t var_n = 0;
+    int var_device = -1;
+    struct ::tfbs_ctx *var_ctx = nullptr;
+    bool var_host = true;   // var_counts holds the counts
+    int var_err = 0;        // the host copy's failure, if any
     std::vector<DevVarKey> var_keys;      // the varying keys in reduction order
     std::vector<uint32_t> var_idx;        // key -> index in var_keys, UINT32_MAX unless it varies
     bool reduced = false;
@@ -208,6 +220,11 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
 int region_membership(const Batch &B, const RegionH &R);
 void commit_region(Batch &B, RegionBuilt &&built);
 void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads);
+// The varying keys' counts of the last tfbs_batch_reduce on the host (downloaded on
+// first use; thread-safe, idempotent); every host reader of var_counts calls it.
+int ensure_host_var_counts(const Batch &B);
+// A batch going away: its ctx forgets it as the holder of its device counts.
+void forget_var_counts(Batch &B);
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads);
 int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
                    const int32_t *gt, Record &r);

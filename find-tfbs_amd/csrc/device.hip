@@ -140,6 +140,7 @@ struct tfbs_ctx {
     uint32_t var_keys_cap = 1u << 16;
     uint64_t var_cap = 1u << 24;
     bool var_cap_forced = false;     // TFBS_VAR_CAP applied (tfbs_batch_reduce)
+    Batch *var_owner = nullptr;      // the batch whose varying counts are only in var_counts (device)
     uint32_t *var_tot_host = nullptr;    // pinned
     // per-sample encoding (tfbs_batch_encode)
     DevBuf<uint8_t> enc_codes, enc_packed;
@@ -462,6 +463,11 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->var_owner) {  // its varying counts to the host before var_counts goes
+        (void)tfbs::ensure_host_var_counts(*ctx->var_owner);
+        ctx->var_owner->var_ctx = nullptr;
+        ctx->var_owner = nullptr;
+    }
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release(); ctx->slot_mfma.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
@@ -726,6 +732,11 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     Batch &B = b->b;
     int rc;
     if ((rc = check_overflow(ctx, (uint32_t)B.haps.size()))) return rc;
+    if (ctx->var_owner && ctx->var_owner != &B) {  // another batch's counts: to its host copy first
+        if ((rc = tfbs::ensure_host_var_counts(*ctx->var_owner))) return rc;
+        ctx->var_owner->var_ctx = nullptr;
+        ctx->var_owner = nullptr;
+    }
     const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
     if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
         (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->var_tot.ensure(2)))
@@ -770,13 +781,11 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
     B.key_first.resize(n_keys);
     B.key_flags.resize(n_keys);
     std::vector<DevVarKey> vk(nk);
-    if ((rc = B.var_counts.reserve((size_t)nc * 4))) return rc;
     if (n_keys) {
         HIP_TRY(hipMemcpyAsync(B.key_first.data(), ctx->key_first.p, n_keys * 4, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipMemcpyAsync(B.key_flags.data(), ctx->key_flags.p, n_keys, hipMemcpyDeviceToHost, ctx->stream));
     }
     if (nk) HIP_TRY(hipMemcpyAsync(vk.data(), ctx->var_keys.p, nk * sizeof(DevVarKey), hipMemcpyDeviceToHost, ctx->stream));
-    if (nc) HIP_TRY(hipMemcpyAsync(B.var_counts.p, ctx->var_counts.p, (size_t)nc * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     // the varying keys in (region, key) order -- a counting sort by region, then each
     // region's few keys by key; their counts stay where the device put them
@@ -802,6 +811,16 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         B.var_idx[k] = i;
     }
     B.var_keys = std::move(vk);
+    {  // the varying counts stay on the device until a host reader needs them
+        std::lock_guard<std::mutex> g(B.var_mu);
+        B.var_dev = ctx->var_counts.p;
+        B.var_n = nc;
+        B.var_device = ctx->device;
+        B.var_ctx = ctx;
+        B.var_host = false;
+        B.var_err = 0;
+    }
+    ctx->var_owner = &B;
     B.enc_r0 = B.enc_r1 = 0;
     B.enc_idx.clear();
     B.reduced = true;
@@ -1223,3 +1242,31 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
 }
 
 }  // extern "C"
+
+namespace tfbs {
+
+int ensure_host_var_counts(const Batch &B) {
+    std::lock_guard<std::mutex> g(B.var_mu);
+    if (B.var_host) return B.var_err;
+    Batch &M = const_cast<Batch &>(B);
+    int rc = M.var_counts.reserve(std::max<size_t>(B.var_n * 4, 1));
+    if (!rc && B.var_n) {
+        int dev = -1;
+        (void)hipGetDevice(&dev);
+        const hipError_t e = hipSetDevice(B.var_device);
+        const hipError_t c = e == hipSuccess ? hipMemcpy(M.var_counts.p, B.var_dev, B.var_n * 4, hipMemcpyDeviceToHost) : e;
+        if (dev >= 0) (void)hipSetDevice(dev);
+        if (c != hipSuccess) rc = fail(TFBS_E_HIP, std::string("varying counts download: ") + hipGetErrorString(c));
+    }
+    M.var_host = true;
+    M.var_err = rc;
+    M.var_dev = nullptr;
+    return rc;
+}
+
+void forget_var_counts(Batch &B) {
+    if (B.var_ctx && B.var_ctx->var_owner == &B) B.var_ctx->var_owner = nullptr;
+    B.var_ctx = nullptr;
+}
+
+}  // namespace tfbs
