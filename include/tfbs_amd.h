@@ -246,8 +246,11 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
  * count_matches_by_sample, main.rs:500-534, moved to the device): classifies
  * every (region, pattern_id, inner range) key on the GPU (some distinct
  * haplotype matched / distinct haplotypes disagree) and downloads only the
- * flags, one count per key and the per-haplotype counts of the disagreeing
- * keys.  The key / row functions below then work as after a download. */
+ * flags and one count per key; the per-haplotype counts of the disagreeing keys
+ * stay on the device (tfbs_batch_encode / tfbs_batch_rows_bgzf read them there)
+ * and are downloaded when a host key / row function first needs them -- the ctx
+ * makes that copy itself before it reduces another batch or is destroyed.  The
+ * key / row functions below then work as after a download. */
 int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
 /* counts_as_genotypes' per-sample half on the device (main.rs:439-534, SURVEY.md
  * 8(f) f1) for the varying keys of regions [r0, r1) after tfbs_batch_reduce:
