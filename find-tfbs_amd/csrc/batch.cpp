@@ -851,6 +851,22 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     }
 }
 
+void reserve_batch(Batch &B, double factor) {
+    auto grow = [factor](auto &v) {
+        const size_t want = (size_t)((double)v.size() * factor) + 16;
+        if (want > v.capacity()) v.reserve(want);
+    };
+    grow(B.words);
+    grow(B.nmask);
+    grow(B.posrel);
+    grow(B.druns);
+    grow(B.haps);
+    grow(B.hap_carriers);
+    grow(B.regions);
+    grow(B.inner);
+    grow(B.rh);
+}
+
 void commit_region(Batch &B, RegionBuilt &&built) {
     std::vector<RegionBuilt> one(1);
     one[0] = std::move(built);

@@ -220,6 +220,9 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
 int region_membership(const Batch &B, const RegionH &R);
 void commit_region(Batch &B, RegionBuilt &&built);
 void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads);
+// Capacity for `factor` times the batch's current contents (a caller that knows how
+// many more regions follow: no regrowth copies of the packed arrays).
+void reserve_batch(Batch &B, double factor);
 // The varying keys' counts of the last tfbs_batch_reduce on the host (downloaded on
 // first use; thread-safe, idempotent); every host reader of var_counts calls it.
 int ensure_host_var_counts(const Batch &B);

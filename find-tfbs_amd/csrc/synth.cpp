@@ -372,6 +372,8 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
         std::vector<tfbs::RegionBuilt> built;
         if (int rc = tfbs::build_regions(B, ins, T, built, &B.prep_s[1])) return rc;
         tfbs::commit_regions(B, built, T);
+        if (c0 == first && n < count)  // the rest of the regions will look alike: room for them now
+            tfbs::reserve_batch(B, 1.15 * (double)(B.rh.size() + count - n) / (double)std::max<size_t>(B.rh.size(), 1));
         B.prep_s[2] += now() - t_build;
     }
     B.prep_s[3] += now() - t_fill;
