@@ -811,6 +811,8 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         B.var_idx[k] = i;
     }
     B.var_keys = std::move(vk);
+    // (a batch reduced before on another ctx: that ctx no longer holds its counts)
+    if (B.var_ctx && B.var_ctx != ctx && B.var_ctx->var_owner == &B) B.var_ctx->var_owner = nullptr;
     {  // the varying counts stay on the device until a host reader needs them
         std::lock_guard<std::mutex> g(B.var_mu);
         B.var_dev = ctx->var_counts.p;
