@@ -147,6 +147,8 @@ struct tfbs_ctx {
     DevBuf<uint16_t> enc_pidx;            // per sample its haplotype pair
     DevBuf<uint32_t> enc_pab, enc_pcnt, enc_pair_n;  // per pair its distinct indices a | b << 16, its samples
     DevBuf<uint16_t> enc_memb;            // membership rows of host-built regions (u16 per haplotype id)
+    DevBuf<uint32_t> enc_nr_ids, enc_nr_meta;  // host-built regions' non-reference ids, per row (offset, reference)
+    DevBuf<uint16_t> enc_nr_loc;               // and their distinct indices (launch_memb_fill)
     DevBuf<uint64_t> enc_rows;            // per region the device address of its membership row
     tfbs::PinnedBytes enc_memb_host;  // host-built regions' membership rows staged for upload (reused)
     uint32_t host_threads = 16;      // host threads of tfbs_batch_encode (tfbs_ctx_set_host_threads)
@@ -483,7 +485,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
     ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
-    ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_rows.release(); ctx->enc_codes.release();
+    ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_nr_ids.release(); ctx->enc_nr_meta.release();
+    ctx->enc_nr_loc.release(); ctx->enc_rows.release(); ctx->enc_codes.release();
     ctx->enc_hdr.release();
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
@@ -872,29 +875,49 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     for (size_t r : hostr)
         if ((rc = region_membership(B, B.rh[r]))) return rc;
     const size_t Hp = ((size_t)H + 7) / 8 * 8;
-    if ((rc = ctx->enc_memb_host.reserve(std::max<size_t>(hostr.size(), 1) * Hp * 2)) ||
-        (rc = ctx->enc_memb.ensure(std::max<size_t>(hostr.size(), 1) * Hp)))
-        return rc;
-    {
-        uint16_t *const stage = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p);
-        const uint32_t T = std::max(1u, std::min(ctx->host_threads, (uint32_t)std::max<size_t>(hostr.size(), 1)));
+    if (!hostr.empty()) {
+        // their non-reference lists (haplotype id, distinct index) go up, the rows are
+        // filled on the device (launch_memb_fill): a few MB instead of Hp u16 per region
+        std::vector<uint32_t> meta(2 * (hostr.size() + 1), 0);
+        uint64_t tot = 0;
+        for (size_t k = 0; k < hostr.size(); k++) {
+            const RegionH &R = B.rh[hostr[k]];
+            meta[2 * k] = (uint32_t)tot;
+            meta[2 * k + 1] = (uint32_t)(R.ref_local < 0 ? 0 : R.ref_local);
+            tot += R.nonref_id.size();
+        }
+        if (tot >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many non-reference haplotypes in one call");
+        meta[2 * hostr.size()] = (uint32_t)tot;
+        if ((rc = ctx->enc_memb_host.reserve(std::max<uint64_t>(tot, 1) * 6)) ||
+            (rc = ctx->enc_memb.ensure(hostr.size() * Hp)) || (rc = ctx->enc_nr_ids.ensure(std::max<uint64_t>(tot, 1))) ||
+            (rc = ctx->enc_nr_loc.ensure(std::max<uint64_t>(tot, 1))) || (rc = ctx->enc_nr_meta.put(meta, ctx->stream)))
+            return rc;
+        uint32_t *const ids = reinterpret_cast<uint32_t *>(ctx->enc_memb_host.p);
+        uint16_t *const loc = reinterpret_cast<uint16_t *>(ctx->enc_memb_host.p + 4 * std::max<uint64_t>(tot, 1));
+        const uint32_t T = std::max(1u, std::min(ctx->host_threads, (uint32_t)hostr.size()));
         std::atomic<size_t> next(0);
         auto work = [&]() {
             for (size_t k; (k = next.fetch_add(1)) < hostr.size();) {
                 const RegionH &R = B.rh[hostr[k]];
-                uint16_t *row = stage + k * Hp;
-                std::fill(row, row + H, (uint16_t)(R.ref_local < 0 ? 0 : R.ref_local));
-                for (size_t i = 0; i < R.nonref_id.size(); i++) row[R.nonref_id[i]] = (uint16_t)R.nonref_local[i];
+                const size_t o = meta[2 * k];
+                for (size_t i = 0; i < R.nonref_id.size(); i++) {
+                    ids[o + i] = R.nonref_id[i];
+                    loc[o + i] = (uint16_t)R.nonref_local[i];
+                }
             }
         };
         std::vector<std::thread> ts;
         for (uint32_t t = 1; t < T; t++) ts.emplace_back(work);
         work();
         for (auto &t : ts) t.join();
+        if (tot) {
+            HIP_TRY(hipMemcpyAsync(ctx->enc_nr_ids.p, ids, tot * 4, hipMemcpyHostToDevice, ctx->stream));
+            HIP_TRY(hipMemcpyAsync(ctx->enc_nr_loc.p, loc, tot * 2, hipMemcpyHostToDevice, ctx->stream));
+        }
+        if ((rc = launch_memb_fill(ctx->enc_nr_meta.p, ctx->enc_nr_ids.p, ctx->enc_nr_loc.p, (uint32_t)hostr.size(),
+                                   (uint32_t)Hp, ctx->enc_memb.p, ctx->stream)))
+            return rc;
     }
-    if (!hostr.empty())
-        HIP_TRY(hipMemcpyAsync(ctx->enc_memb.p, ctx->enc_memb_host.p, hostr.size() * Hp * 2, hipMemcpyHostToDevice,
-                               ctx->stream));
     for (size_t k = 0; k < hostr.size(); k++) rows[hostr[k] - r0] = (uint64_t)(uintptr_t)(ctx->enc_memb.p + k * Hp);
     std::vector<uint32_t> pair_n(nr);
     if ((rc = ctx->enc_rows.put(rows, ctx->stream)) || (rc = ctx->enc_pab.ensure(nr * kEncMaxPairs)) ||

@@ -676,6 +676,21 @@ __global__ __launch_bounds__(kEncBlock) void key_encode_kernel(const uint32_t *_
     if (tid == 0) hdr[k] = EncHdr{lo, hi, nv, 0, width};
 }
 
+// Membership rows of host-built regions from their non-reference lists: row k
+// (Hp u16 at k * Hp) is the region's reference group everywhere (meta[2k + 1]),
+// then its entries [meta[2k], meta[2k + 2]) of ids / loc scattered over it.
+__global__ __launch_bounds__(256) void memb_fill_kernel(const uint32_t *__restrict__ meta, const uint32_t *__restrict__ ids,
+                                                        const uint16_t *__restrict__ loc, uint32_t Hp,
+                                                        uint16_t *__restrict__ memb) {
+    const uint32_t k = blockIdx.x;
+    const uint32_t o0 = meta[2 * k], o1 = meta[2 * k + 2], ref = meta[2 * k + 1] & 0xFFFFu;
+    uint16_t *row = memb + (size_t)k * Hp;
+    const uint32_t v = ref | (ref << 16);
+    for (uint32_t i = threadIdx.x; i < Hp / 8; i += 256) reinterpret_cast<uint4 *>(row)[i] = uint4{v, v, v, v};
+    __syncthreads();
+    for (uint32_t i = o0 + threadIdx.x; i < o1; i += 256) row[ids[i]] = loc[i];
+}
+
 // Copies each key's packed codes (at k * n_samples) to off[k] of a contiguous buffer.
 __global__ __launch_bounds__(256) void code_compact_kernel(const uint8_t *__restrict__ codes, uint32_t n_samples,
                                                            const uint64_t *__restrict__ off, uint8_t *__restrict__ dst) {
@@ -706,6 +721,15 @@ int launch_val_compact(const uint32_t *vals, const uint32_t *hist, uint32_t n_ke
     hipLaunchKernelGGL(val_compact_kernel, dim3(n_keys), dim3(64), 0, stream, vals, hist, off, ov, oh);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("val_compact_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_memb_fill(const uint32_t *meta, const uint32_t *ids, const uint16_t *loc, uint32_t n_rows, uint32_t Hp,
+                     uint16_t *memb, hipStream_t stream) {
+    if (n_rows == 0) return TFBS_OK;
+    hipLaunchKernelGGL(memb_fill_kernel, dim3(n_rows), dim3(256), 0, stream, meta, ids, loc, Hp, memb);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("memb_fill_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 

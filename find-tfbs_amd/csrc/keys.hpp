@@ -58,6 +58,11 @@ int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spi
 // r * kEncMaxPairs, pair_n[r] (UINT32_MAX: skipped or too many pairs), pidx at r * n_samples.
 int launch_pair_table(const uint64_t *rows, uint32_t n_regions, uint32_t n_samples, uint32_t *pab, uint32_t *pcnt,
                       uint32_t *pair_n, uint16_t *pidx, hipStream_t stream);
+// Host-built regions' u16 membership rows made on the device (Hp, a multiple of 8,
+// u16 per row): row k = the reference group (meta[2k + 1]) with the entries
+// [meta[2k], meta[2k + 2]) of (ids, loc) -- haplotype id, distinct index -- over it.
+int launch_memb_fill(const uint32_t *meta, const uint32_t *ids, const uint16_t *loc, uint32_t n_rows, uint32_t Hp,
+                     uint16_t *memb, hipStream_t stream);
 // One workgroup per key: counts_as_genotypes' per-sample half over the
 // region's distinct haplotype pairs (launch_pair_table's, region - region0):
 // pab = a | b << 16 (the distinct indices of a sample's two haplotypes), pcnt
