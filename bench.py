@@ -365,9 +365,19 @@ def main():
         T.check(L.tfbs_ctx_rows_bgzf_seconds(sc.h, rows_split))
         host_bgzf = host_bgzf_sample(T, batch, sc, threads)
 
-    # ---- timed scan loop
-    for _ in range(args.warmup):
+    # ---- timed loop: one step = the scan and the key assembly of the rank's batch
+    # (tfbs_scan: the matrix-core / LUT kernels' hit lists and the reference hits;
+    # tfbs_batch_assemble: overflow candidates rescored, spill records bucketed, every
+    # region's keys assembled -- reference-window reuse resolved per haplotype --,
+    # classified and the varying keys' counts compacted; tfbs_batch_assemble_wait:
+    # the host waits and checks every list, rescanning if one overflowed)
+    def step():
         T.check(L.tfbs_scan(sc.h, batch.h))
+        T.check(L.tfbs_batch_assemble(sc.h, batch.h))
+        T.check(L.tfbs_batch_assemble_wait(sc.h, batch.h))
+
+    for _ in range(args.warmup):
+        step()
     T.check(L.tfbs_ctx_sync(sc.h))
 
     def barrier():
@@ -377,12 +387,13 @@ def main():
             dist.barrier()
 
     barrier()
-    kernel_ms, mfma_ms = [], []
+    kernel_ms, mfma_ms, asm_ms = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        T.check(L.tfbs_scan(sc.h, batch.h))
-        kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # waits for this step's end event
+        step()
+        kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # the scan's launches (HIP events)
         mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
+        asm_ms.append(L.tfbs_ctx_last_assemble_ms(sc.h))  # the assembly's launches
     T.check(L.tfbs_ctx_sync(sc.h))
     if dist is not None:
         import torch
@@ -414,6 +425,7 @@ def main():
         value = tot_windows * steps / elapsed
         kms = sum(kernel_ms) / len(kernel_ms)
         mms = sum(mfma_ms) / len(mfma_ms)
+        ams = sum(asm_ms) / len(asm_ms)
         path = "mfma" if mms > 0 else "lut"
         traffic, traffic_src = pmc_traffic(args, path)
         pattern_bytes = 0
@@ -479,17 +491,26 @@ def main():
                 "scanned_windows_per_step": int(tot_scan),
                 "window_list_entries": [int(wl_entries[0]), int(wl_entries[1])],
             },
-            "value_note": "windows of every distinct haplotype resolved per second (the reference scores each "
-                          "of them); a haplotype's windows whose bases and positions equal the "
-                          "region's reference window take the reference window's result (reference-window "
-                          "reuse, exact; TFBS_DEDUP=0 scans them all), scanned_windows_per_s counts the "
+            "value_note": "windows of every distinct haplotype resolved per second, scan AND key assembly in "
+                          "the timed step (the reference scores each window and counts its hits per key, "
+                          "main.rs:94-154, 500-534); a haplotype's windows whose bases and positions equal the "
+                          "region's reference window take the reference window's hits in the assembly (reference-"
+                          "window reuse, exact; TFBS_DEDUP=0 scans them all); scanned_windows_per_s counts the "
                           "windows the kernels read",
+            "step": "tfbs_scan + tfbs_batch_assemble + tfbs_batch_assemble_wait (host sync and list check "
+                    "every step): scan kernels, overflow rescoring, spill bucketing, key assembly + "
+                    "classification + varying-count compaction of every region of the batch",
+            "step_device_ms": {"scan": kms, "mfma_phase": mms, "assemble": ams},
             "ranks": {"world_size": world, "backend": args.dist_backend if dist is not None else None,
                       "ms_per_step": per_rank_ms},
             "scanned_windows_per_s": tot_scan * steps / elapsed,
             "scan_regions_per_s": tot_regions * steps / elapsed,
             "effective_windows_per_s": tot_eff * steps / elapsed,
             "end_to_end": {
+                # definition v3 (round 3 on): host prep wall (build_region + commit; the synthetic
+                # generation excluded) + upload + scan + key reduction + device encode + device BGZF
+                # rows written to /dev/null.  v2 (round 2) summed the whole synthetic fill and host rows.
+                "definition": "v3",
                 "regions_per_s": tot_regions / e2e_max,
                 "windows_per_s": tot_windows / e2e_max,
                 "seconds": e2e_max,

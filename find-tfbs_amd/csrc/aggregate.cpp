@@ -448,14 +448,22 @@ static void region_row_parts(const Batch &B, const RegionH &R, uint32_t min_maf,
     }
 }
 
-int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chrom, uint32_t min_maf,
-                   uint32_t *fake, uint32_t threads, RowPlan &plan) {
+struct RowParts {
+    size_t r0 = 0;
+    std::vector<std::vector<RowPart>> parts;  // per region of [r0, r0 + parts.size())
+};
+
+int build_row_parts(const Batch &B, size_t r0, size_t r1, uint32_t min_maf, uint32_t threads,
+                    std::shared_ptr<RowParts> &out, uint64_t *n_rows) {
     if (!have_counts(B)) return fail(TFBS_E_STATE, "counts not downloaded");
     if (!B.keep_membership && B.n_samples) return fail(TFBS_E_STATE, "batch created without membership");
     r1 = std::min(r1, B.rh.size());
     r0 = std::min(r0, r1);
     const size_t n = r1 - r0;
-    std::vector<std::vector<RowPart>> parts(n);
+    out = std::make_shared<RowParts>();
+    out->r0 = r0;
+    std::vector<std::vector<RowPart>> &parts = out->parts;
+    parts.resize(n);
     std::atomic<size_t> next(0);
     auto work = [&]() {
         for (size_t j; (j = next.fetch_add(1)) < n;)
@@ -466,13 +474,21 @@ int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chro
     work();
     for (auto &t : ts) t.join();
     if (!B.counts_valid && B.var_host && B.var_err) return B.var_err;  // a lazy count download failed
+    uint64_t rows = 0;
+    for (auto &v : parts) rows += v.size();
+    if (n_rows) *n_rows = rows;
+    return TFBS_OK;
+}
+
+int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std::string &chrom, uint32_t *fake,
+                    RowPlan &plan) {
     // serially: POS, offsets in the stream, token slots
     plan = RowPlan();
     const std::string chr = strip_chr(chrom);
     uint64_t at = 0;
     char pos[32];
-    for (auto &v : parts)
-        for (RowPart &p : v) {
+    for (size_t r = std::max(r0, P.r0); r < std::min(r1, P.r0 + P.parts.size()); r++)
+        for (RowPart &p : P.parts[r - P.r0]) {
             DevRow d{};
             d.head_off = (uint32_t)plan.heads.size();
             const int m = snprintf(pos, sizeof pos, "\t%u\t", *fake);
@@ -499,6 +515,13 @@ int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chro
     plan.text_bytes = at;
     plan.n_rows = plan.rows.size();
     return TFBS_OK;
+}
+
+int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chrom, uint32_t min_maf,
+                   uint32_t *fake, uint32_t threads, RowPlan &plan) {
+    std::shared_ptr<RowParts> P;
+    if (int rc = build_row_parts(B, r0, r1, min_maf, threads, P, nullptr)) return rc;
+    return plan_from_parts(B, *P, r0, r1, chrom, fake, plan);
 }
 
 size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out) {

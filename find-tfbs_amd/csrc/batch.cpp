@@ -538,6 +538,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
             });
             GroupOut go;
             if (int rc = B.grouper->group(ncar, recs, regs, H, go)) return rc;
+            if (go.memb_alloc) B.memb_allocs.push_back(go.memb_alloc);
             for (size_t k = c0; k < c1; k++) {
                 const size_t j = dj[k], c = k - c0;
                 if (go.n_groups[c] == UINT32_MAX) {

@@ -77,6 +77,7 @@ struct GroupOut {                 // per chunk region
     std::vector<uint64_t> masks;     // per region n_groups masks, ascending Vec<Diff> order
     std::vector<uint32_t> counts;    // carriers per mask
     std::vector<uint64_t> memb;      // device address of each region's membership row
+    void *memb_alloc = nullptr;      // the chunk's rows' allocation (the batch hands it back: recycle)
 };
 struct DevGrouper {
     virtual ~DevGrouper() {}
@@ -87,6 +88,9 @@ struct DevGrouper {
                       uint32_t H, GroupOut &out) = 0;
     // one membership row (H u16) to the host
     virtual int fetch(uint64_t memb, uint32_t H, uint16_t *out) = 0;
+    // membership allocations of a batch going away, kept for later chunks (a grouper
+    // shared by a run's batches allocates once; thread-safe)
+    virtual void recycle(std::vector<void *> &allocs) = 0;
 };
 DevGrouper *make_gpu_grouper(int device);  // build_gpu.hip
 
@@ -172,9 +176,14 @@ struct Batch {
     uint32_t window_lmax = 0;
     uint32_t lmax() const { return window_lmax ? window_lmax : pats->max_length(); }
 
-    // device grouping of SNV-only regions (tfbs_batch_set_build_device); it owns
-    // their membership rows, so it lives as long as the batch
-    std::unique_ptr<DevGrouper> grouper;
+    // device grouping of SNV-only regions (tfbs_batch_set_build_device, or one
+    // grouper shared by a run's batches on a device); the batch's membership rows
+    // (memb_allocs) go back to it when the batch goes
+    std::shared_ptr<DevGrouper> grouper;
+    std::vector<void *> memb_allocs;
+    ~Batch() {
+        if (grouper) grouper->recycle(memb_allocs);
+    }
     uint64_t dev_regions = 0, host_regions = 0;  // regions grouped on the device / built on the host
 
     uint64_t device_bytes() const;

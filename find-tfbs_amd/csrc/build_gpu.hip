@@ -18,6 +18,8 @@
 // 100 000 haplotype ids (build_region's loop over every id).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 #include <cstring>
 #include <string>
@@ -199,7 +201,11 @@ struct GpuGrouper final : DevGrouper {
     Buf<GrpRecord> recs;
     Buf<GrpRegion> regs;
     PinnedBytes car_host;
-    std::vector<uint16_t *> memb;  // one allocation per chunk, for the batch's lifetime
+    // membership rows: one allocation per chunk, held by its batch until it goes
+    // (recycle), then reused by a later chunk that fits
+    std::mutex memb_mu;
+    std::vector<std::pair<uint16_t *, size_t>> memb_all;   // every allocation (bytes)
+    std::vector<std::pair<uint16_t *, size_t>> memb_free;  // returned ones
 
     ~GpuGrouper() override {
         (void)hipSetDevice(dev);
@@ -213,8 +219,34 @@ struct GpuGrouper final : DevGrouper {
         masks.release();
         recs.release();
         regs.release();
-        for (uint16_t *p : memb) (void)hipFree(p);
+        for (auto &m : memb_all) (void)hipFree(m.first);
         if (stream) (void)hipStreamDestroy(stream);
+    }
+    void recycle(std::vector<void *> &allocs) override {
+        std::lock_guard<std::mutex> g(memb_mu);
+        for (void *p : allocs)
+            for (auto &m : memb_all)
+                if (m.first == p) memb_free.push_back(m);
+        allocs.clear();
+    }
+    uint16_t *memb_alloc(size_t bytes) {  // the smallest returned allocation that fits, else a new one
+        {
+            std::lock_guard<std::mutex> g(memb_mu);
+            size_t best = memb_free.size();
+            for (size_t i = 0; i < memb_free.size(); i++)
+                if (memb_free[i].second >= bytes && (best == memb_free.size() || memb_free[i].second < memb_free[best].second))
+                    best = i;
+            if (best < memb_free.size()) {
+                uint16_t *p = memb_free[best].first;
+                memb_free.erase(memb_free.begin() + best);
+                return p;
+            }
+        }
+        uint16_t *p = nullptr;
+        if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+        std::lock_guard<std::mutex> g(memb_mu);
+        memb_all.push_back({p, bytes});
+        return p;
     }
     int device() const override { return dev; }
     uint32_t *carriers(size_t n) override {
@@ -230,9 +262,9 @@ struct GpuGrouper final : DevGrouper {
         out.memb.assign(nr, 0);
         if (!nr) return TFBS_OK;
         const size_t stride = ((size_t)H + 7) / 8 * 8;  // u16 per id, rows 16-byte aligned
-        uint16_t *mb = nullptr;
-        HIP_OK(hipMalloc(&mb, std::max<size_t>(nr * stride * 2, 16)));
-        memb.push_back(mb);
+        uint16_t *mb = memb_alloc(std::max<size_t>(nr * stride * 2, 16));
+        if (!mb) return fail(TFBS_E_HIP, "device grouping: membership rows");
+        out.memb_alloc = mb;
         int rc;
         const size_t sig_n = nr * (size_t)H;
         if (sig_n > sig.cap) sig_zero = false;

@@ -13,6 +13,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -20,6 +22,7 @@
 #include "bgzf_gpu.hpp"
 #include "patterns.hpp"
 #include "keys.hpp"
+#include "rows.hpp"
 #include "scan.hpp"
 #include "tfbs_internal.hpp"
 
@@ -106,7 +109,7 @@ struct tfbs_ctx {
     uint32_t *over_host = nullptr;       // pinned [spill records, candidates past the lists]
     hipEvent_t over_ev = nullptr;
     bool over_pending = false;
-    uint32_t n_spill = 0;                // spill records of the last checked scan
+    bool post_done = false;              // the last scan's overflow candidates were rescored (launch_post_scan)
     HitSrc srcs_host[kMaxHitSrcs] = {};
     ScanArgs last_margs{};               // the last matrix-core scan's arguments (launch_post_scan)
     uint32_t n_srcs = 0;
@@ -134,14 +137,27 @@ struct tfbs_ctx {
     DevBuf<unsigned long long> hits;
     DevBuf<uint32_t> asm_scratch;         // key assembly counters of regions with many distinct haplotypes
     // key reduction (tfbs_batch_reduce)
-    DevBuf<uint32_t> key_first, var_counts, var_tot;
+    DevBuf<uint32_t> key_first, var_counts, asm_redo;   // asm_redo: n_regions + 1 list entries, then the arena's fill
+    DevBuf<uint32_t> cor_arena;                          // key_fast_kernel's corrections past its LDS list
+    uint32_t cor_cap = 1u << 22;
+    DevBuf<unsigned long long> var_tot;
     DevBuf<uint8_t> key_flags;
     DevBuf<DevVarKey> var_keys, enc_keys;
     uint32_t var_keys_cap = 1u << 16;
+    uint32_t key_fast_max_u = 1u << 30;  // TFBS_KEY_FAST_MAXU (0: every region through key_asm_kernel)
+    uint32_t key_cor_lds = 1u << 30;     // TFBS_KEY_COR_LDS (0: every region's corrections in the arena)
     uint64_t var_cap = 1u << 24;
     bool var_cap_forced = false;     // TFBS_VAR_CAP applied (tfbs_batch_reduce)
     Batch *var_owner = nullptr;      // the batch whose varying counts are only in var_counts (device)
-    uint32_t *var_tot_host = nullptr;    // pinned
+    // the assembly's counters, copied back after it (pinned): [0] spill records,
+    // [1] candidates past the wave lists, [2] regions left to key_asm_kernel, [3]
+    // the correction arena's fill; at byte 16 the varying keys and counts (u64)
+    uint32_t *asm_host = nullptr;
+    hipEvent_t asm_ev = nullptr, asm_t0 = nullptr, asm_t1 = nullptr;
+    const Batch *asm_batch = nullptr;    // the batch the enqueued assembly is for
+    int asm_state = 0;                   // 0 none, 1 enqueued, 2 complete (checked)
+    bool asm_timed = false;
+    float last_asm_ms = 0.f;
     // per-sample encoding (tfbs_batch_encode)
     DevBuf<uint8_t> enc_codes, enc_packed;
     DevBuf<uint16_t> enc_pidx;            // per sample its haplotype pair
@@ -171,6 +187,7 @@ struct tfbs_ctx {
     hipEvent_t bg_done[kBgSlots] = {}, bg_copied[kBgSlots] = {};
     hipStream_t copy_stream = nullptr;
     double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
+    uint64_t rows_text_last = 0;          // the last call's uncompressed row bytes
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
     float last_ms = 0.f;
@@ -296,6 +313,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             (rc = ctx->spill_boff.ensure(nr + 1)))
             return rc;
         m.dedup = 1;
+        m.druns = ctx->druns.p;
         m.n_regions = ctx->n_regions;
         m.ref_hits = ctx->ref_hits.p;
         m.ref_count = ctx->ref_count.p;
@@ -328,6 +346,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         ctx->kernel_timed = true;
         launches += n;
         ctx->last_margs = m;  // the overflow candidates are rescored when the results are read (check_overflow)
+        ctx->post_done = false;
         if ((rc = ctx->srcs.ensure(kMaxHitSrcs))) return rc;
         HIP_TRY(hipMemcpyAsync(ctx->srcs.p, ctx->srcs_host, sizeof(ctx->srcs_host), hipMemcpyHostToDevice,
                                ctx->stream));
@@ -380,7 +399,7 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
         HIP_TRY(hipEventSynchronize(ctx->over_ev));
         uint32_t nspill = ctx->over_host[0];
         const uint32_t ncand = ctx->over_host[1];
-        if (ncand > 0 && ncand <= ctx->cand_over_cap) {  // rescore them: their hits add spill records
+        if (ncand > 0 && ncand <= ctx->cand_over_cap && !ctx->post_done) {  // rescore them: their hits add spill records
             const int f = launch_post_scan(ctx->last_margs, ctx->stream);
             if (f < 0) return f;
             HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -401,7 +420,7 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
         }
         if (nspill <= ctx->spill_cap && ncand <= ctx->cand_over_cap) {
             ctx->over_pending = false;
-            ctx->n_spill = nspill;
+            ctx->post_done = true;
             if (nspill) {
                 const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
                 const int rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, nr, ctx->spill_bcnt.p,
@@ -417,6 +436,8 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
     }
     return TFBS_OK;
 }
+
+static int assembly_wait(tfbs_ctx *ctx, Batch &B);
 
 static AsmArgs asm_args(tfbs_ctx *ctx, const Batch &B, int mode) {
     AsmArgs a{};
@@ -439,7 +460,8 @@ static AsmArgs asm_args(tfbs_ctx *ctx, const Batch &B, int mode) {
     a.ref_count = ctx->ref_count.p;
     a.spill_sorted = ctx->spill_sorted.p;
     a.spill_off = ctx->spill_boff.p;
-    a.n_spill = ctx->plan.m_supers.empty() ? 0 : ctx->n_spill;
+    a.spill_count = ctx->plan.m_supers.empty() ? nullptr : ctx->over.p;
+    a.spill_cap = ctx->spill_cap;
     a.counts = ctx->counts_live ? ctx->counts.p : nullptr;
     a.dense_base = ctx->counts_live ? 1 : 0;
     a.scratch = ctx->asm_scratch.p;
@@ -467,7 +489,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->var_owner) {  // its varying counts to the host before var_counts goes
         (void)tfbs::ensure_host_var_counts(*ctx->var_owner);
-        ctx->var_owner->var_ctx = nullptr;
+        std::lock_guard<std::mutex> g(ctx->var_owner->var_mu);
+        if (ctx->var_owner->var_ctx == ctx) ctx->var_owner->var_ctx = nullptr;
         ctx->var_owner = nullptr;
     }
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
@@ -477,12 +500,16 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->ref_count.release(); ctx->spill.release(); ctx->over.release(); ctx->spill_sorted.release();
     ctx->spill_bcnt.release(); ctx->spill_boff.release(); ctx->srcs.release();
     if (ctx->over_host) (void)hipHostFree(ctx->over_host);
-    if (ctx->var_tot_host) (void)hipHostFree(ctx->var_tot_host);
+    if (ctx->asm_host) (void)hipHostFree(ctx->asm_host);
+    if (ctx->asm_ev) (void)hipEventDestroy(ctx->asm_ev);
+    if (ctx->asm_t0) (void)hipEventDestroy(ctx->asm_t0);
+    if (ctx->asm_t1) (void)hipEventDestroy(ctx->asm_t1);
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->druns.release(); ctx->wl_tmp.release();
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
+    ctx->asm_redo.release(); ctx->cor_arena.release();
     ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
     ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_nr_ids.release(); ctx->enc_nr_meta.release();
@@ -535,6 +562,9 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_hpb = (uint32_t)std::min((int)kMMaxHapsPerBlock, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 6 bits in a window list entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
+    ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
+    ctx->key_cor_lds = (uint32_t)std::max(0, env_int("TFBS_KEY_COR_LDS", 1 << 30));
+    ctx->cor_cap = (uint32_t)std::max(1, env_int("TFBS_KEY_COR_CAP", 1 << 22));
     ctx->host_threads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     ctx->cand_over_cap = (uint32_t)std::max(1, env_int("TFBS_CAND_OVER_CAP", 1 << 20));  // grows on demand (tfbs_scan)
     PlanOptions opt;
@@ -559,6 +589,9 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->over_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->asm_ev, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->asm_t0);
+    if (e == hipSuccess) e = hipEventCreate(&ctx->asm_t1);
     for (int i = 0; i < tfbs_ctx::kSide; i++) {
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->side[i], hipStreamNonBlocking);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->join[i], hipEventDisableTiming);
@@ -680,8 +713,8 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     ctx->n_regions = (uint32_t)B.regions.size();
     ctx->over_pending = false;
-    ctx->n_spill = 0;
     ctx->scanned = false;
+    ctx->asm_state = 0;
     return TFBS_OK;
 }
 
@@ -696,6 +729,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     const int n = launch_scan(ctx, (uint32_t)b->b.haps.size(), nullptr, 0);
     if (n < 0) return n;
     ctx->scanned = true;
+    ctx->asm_state = 0;
     HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
     ctx->timing_pending = true;
@@ -711,6 +745,7 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipSetDevice(ctx->device));
     Batch &B = b->b;
     int rc;
+    if (ctx->asm_state == 1 && ctx->asm_batch == &B && (rc = assembly_wait(ctx, B))) return rc;
     if ((rc = check_overflow(ctx, (uint32_t)B.haps.size()))) return rc;
     if (!ctx->counts_live) {  // no LUT/generic slots: the matrix is the assembly's alone
         if ((rc = ctx->counts.ensure(std::max<uint64_t>(B.n_counts, 1)))) return rc;
@@ -727,29 +762,24 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
     return TFBS_OK;
 }
 
-int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
-    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
-    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
-    if (!ctx->scanned) return tfbs::fail(TFBS_E_STATE, "batch not scanned (tfbs_scan)");
-    HIP_TRY(hipSetDevice(ctx->device));
-    Batch &B = b->b;
+}  // extern "C"
+
+// The device half of the key reduction, enqueued on the ctx stream behind the scan
+// with no host wait: the candidates past the waves' lists rescored and the spill
+// records bucketed by region (post: once per scan -- the rescoring appends spill
+// records), then the key assembly (launch_key_fast); the overflow and list
+// counters are copied back for assembly_wait.  Buffers are sized from the batch
+// (1/16 of its keys and dense counts for the varying lists: no regrowth at C3
+// shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
+static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     int rc;
-    if ((rc = check_overflow(ctx, (uint32_t)B.haps.size()))) return rc;
-    if (ctx->var_owner && ctx->var_owner != &B) {  // another batch's counts: to its host copy first
-        if ((rc = tfbs::ensure_host_var_counts(*ctx->var_owner))) return rc;
-        ctx->var_owner->var_ctx = nullptr;
-        ctx->var_owner = nullptr;
-    }
     const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
+    const uint32_t nr = (uint32_t)B.regions.size();
     if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
-        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->var_tot.ensure(2)))
+        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->var_tot.ensure(2)) ||
+        (rc = ctx->asm_redo.ensure((size_t)nr + 2)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
         return rc;
-    if (!ctx->var_tot_host) HIP_TRY(hipHostMalloc((void **)&ctx->var_tot_host, 8, hipHostMallocDefault));
-    // per region: the keys' flags and first counts, and the varying keys' counts
-    // appended to a compact list (grown and redone if it was too small); a first
-    // guess of 1/16 of the keys and of the dense counts avoids the rerun at C3 shapes
-    // (TFBS_VAR_CAP=n: lists of n keys and 4 n counts at first, no guess -- the
-    // regrow path's test)
+    if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 32, hipHostMallocDefault));
     if (const int vc = env_int("TFBS_VAR_CAP", 0); vc > 0) {
         if (!ctx->var_cap_forced) {
             ctx->var_keys_cap = (uint32_t)vc;
@@ -760,27 +790,141 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         ctx->var_keys_cap = std::max<uint32_t>(ctx->var_keys_cap, (uint32_t)std::min<uint64_t>(n_keys / 16, 1u << 26));
         ctx->var_cap = std::max<uint64_t>(ctx->var_cap, std::min<uint64_t>(B.n_counts / 16, 1ull << 28));
     }
-    for (int round = 0;; round++) {
-        if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
-        AsmArgs a = asm_args(ctx, B, 0);
-        a.key_first = ctx->key_first.p;
-        a.key_flags = ctx->key_flags.p;
-        a.var_keys = ctx->var_keys.p;
-        a.var_keys_cap = ctx->var_keys_cap;
-        a.var_counts = ctx->var_counts.p;
-        a.var_cap = ctx->var_cap;
-        a.var_tot = ctx->var_tot.p;
-        HIP_TRY(hipMemsetAsync(ctx->var_tot.p, 0, 8, ctx->stream));
-        if ((rc = launch_key_asm(a, (uint32_t)B.regions.size(), ctx->stream))) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->var_tot_host, ctx->var_tot.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        const uint32_t nk = ctx->var_tot_host[0], nc = ctx->var_tot_host[1];
-        if (nk <= ctx->var_keys_cap && nc <= ctx->var_cap) break;
-        if (round == 2 || (uint64_t)nc >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
-        ctx->var_keys_cap = std::max<uint32_t>(ctx->var_keys_cap, nk + nk / 4 + 1024);
-        ctx->var_cap = std::max<uint64_t>(ctx->var_cap, (uint64_t)nc + nc / 4 + 4096);
+    if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
+    HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
+    const bool mfma = !ctx->plan.m_supers.empty();
+    if (mfma && post) {
+        if (!ctx->post_done) {  // (once per scan: the rescoring appends spill records)
+            const int f = launch_post_scan(ctx->last_margs, ctx->stream);
+            if (f < 0) return f;
+            ctx->post_done = true;
+        }
+        if ((rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, std::max<uint32_t>(1, nr),
+                                       ctx->spill_bcnt.p, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream)))
+            return rc;
     }
-    const uint32_t nk = ctx->var_tot_host[0], nc = ctx->var_tot_host[1];
+    AsmArgs a = asm_args(ctx, B, 0);
+    a.key_first = ctx->key_first.p;
+    a.key_flags = ctx->key_flags.p;
+    a.var_keys = ctx->var_keys.p;
+    a.var_keys_cap = ctx->var_keys_cap;
+    a.var_counts = ctx->var_counts.p;
+    a.var_cap = ctx->var_cap;
+    a.var_tot = ctx->var_tot.p;
+    a.redo = ctx->asm_redo.p;
+    a.fast_max_u = ctx->key_fast_max_u;
+    a.cor_arena = ctx->cor_arena.p;
+    a.cor_cap = ctx->cor_cap;
+    a.cor_used = ctx->asm_redo.p + nr + 1;
+    a.cor_lds = ctx->key_cor_lds;
+    HIP_TRY(hipMemsetAsync(ctx->var_tot.p, 0, 16, ctx->stream));
+    if ((rc = launch_key_fast(a, nr, ctx->stream))) return rc;
+    HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
+    if (mfma) HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+    else ctx->asm_host[0] = ctx->asm_host[1] = 0;
+    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 2, ctx->asm_redo.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 3, ctx->asm_redo.p + nr + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 4, ctx->var_tot.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
+    ctx->over_pending = false;  // the assembly's check covers this scan's overflow lists
+    ctx->asm_batch = &B;
+    ctx->asm_state = 1;
+    ctx->asm_timed = true;
+    return TFBS_OK;
+}
+
+// Waits for the enqueued assembly and checks its lists: a scan overflow list that
+// dropped entries means a rescan with larger lists (and a new assembly), a full
+// varying-key list a new assembly with larger ones.
+static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
+    auto grow = [](uint32_t &cap, uint32_t need, uint64_t lim) {
+        if (need > cap) cap = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need * 5 / 4 + 1024);
+    };
+    for (int round = 0; ctx->asm_state == 1; round++) {
+        if (round == 8) return tfbs::fail(TFBS_E_NOMEM, "scan / key lists still full after 8 reruns");
+        HIP_TRY(hipEventSynchronize(ctx->asm_ev));
+        const uint32_t nspill = ctx->asm_host[0], ncand = ctx->asm_host[1];
+        const uint64_t *vt = reinterpret_cast<const uint64_t *>(ctx->asm_host + 4);
+        const uint64_t nk = vt[0], nc = vt[1];
+        if (ctx->debug_over)
+            fprintf(stderr, "tfbs assembly: spill %u/%u candidates %u/%u left to key_asm %u arena %u/%u varying keys "
+                            "%llu/%u counts %llu/%llu\n", nspill, ctx->spill_cap, ncand, ctx->cand_over_cap,
+                    ctx->asm_host[2], ctx->asm_host[3], ctx->cor_cap,
+                    (unsigned long long)nk, ctx->var_keys_cap, (unsigned long long)nc,
+                    (unsigned long long)ctx->var_cap);
+        int rc;
+        if (ctx->asm_host[3] > ctx->cor_cap)  // regions that found the arena full went to key_asm_kernel: larger next time
+            ctx->cor_cap = (uint32_t)std::min<uint64_t>((uint64_t)ctx->asm_host[3] * 5 / 4, 1u << 30);
+        if (nspill > ctx->spill_cap || ncand > ctx->cand_over_cap) {
+            grow(ctx->spill_cap, ncand > ctx->cand_over_cap ? 2 * std::max(nspill, 1024u) : nspill, UINT32_MAX / 4);
+            grow(ctx->cand_over_cap, ncand, UINT32_MAX / 4);
+            const int n = launch_scan(ctx, (uint32_t)B.haps.size(), nullptr, 0);
+            if (n < 0) return n;
+            if ((rc = enqueue_assembly(ctx, B, true))) return rc;
+            continue;
+        }
+        if (nk > ctx->var_keys_cap || nc > ctx->var_cap) {
+            if (nk >= (1ull << 32) || nc >= (1ull << 40)) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts");
+            ctx->var_keys_cap = (uint32_t)std::max<uint64_t>(ctx->var_keys_cap, std::min<uint64_t>(nk + nk / 4 + 1024, UINT32_MAX));
+            ctx->var_cap = std::max<uint64_t>(ctx->var_cap, nc + nc / 4 + 4096);
+            if ((rc = enqueue_assembly(ctx, B, false))) return rc;
+            continue;
+        }
+        ctx->asm_state = 2;
+    }
+    return TFBS_OK;
+}
+
+extern "C" {
+
+int tfbs_batch_assemble(tfbs_ctx *ctx, tfbs_batch *b) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    if (!ctx->scanned) return tfbs::fail(TFBS_E_STATE, "batch not scanned (tfbs_scan)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    Batch &B = b->b;
+    if (ctx->asm_state != 0 && ctx->asm_batch == &B) return TFBS_OK;  // this scan's assembly is on its way
+    // another batch's varying counts live in var_counts: to its host copy first
+    if (ctx->var_owner && ctx->var_owner != &B) {
+        int rc;
+        if ((rc = tfbs::ensure_host_var_counts(*ctx->var_owner))) return rc;
+        std::lock_guard<std::mutex> g(ctx->var_owner->var_mu);
+        if (ctx->var_owner->var_ctx == ctx) ctx->var_owner->var_ctx = nullptr;
+        ctx->var_owner = nullptr;
+    }
+    return enqueue_assembly(ctx, B, true);
+}
+
+int tfbs_batch_assemble_wait(tfbs_ctx *ctx, tfbs_batch *b) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b || ctx->asm_state == 0 || ctx->asm_batch != &b->b)
+        return tfbs::fail(TFBS_E_STATE, "no assembly of this batch on this ctx (tfbs_batch_assemble)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    return assembly_wait(ctx, b->b);
+}
+
+float tfbs_ctx_last_assemble_ms(const tfbs_ctx *ctx) {
+    if (!ctx || !ctx->asm_timed) return -1.f;
+    auto *c = const_cast<tfbs_ctx *>(ctx);
+    float ms = -1.f;
+    if (hipEventSynchronize(c->asm_t1) == hipSuccess && hipEventElapsedTime(&ms, c->asm_t0, c->asm_t1) == hipSuccess)
+        c->last_asm_ms = ms;
+    return c->last_asm_ms;
+}
+
+int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
+    if (!ctx->scanned) return tfbs::fail(TFBS_E_STATE, "batch not scanned (tfbs_scan)");
+    HIP_TRY(hipSetDevice(ctx->device));
+    Batch &B = b->b;
+    int rc;
+    if ((rc = tfbs_batch_assemble(ctx, b)) || (rc = assembly_wait(ctx, B))) return rc;
+    const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
+    const uint64_t *vt = reinterpret_cast<const uint64_t *>(ctx->asm_host + 4);
+    const uint32_t nk = (uint32_t)vt[0];
+    const uint64_t nc = vt[1];
+    if (nc >= UINT32_MAX) return tfbs::fail(TFBS_E_NOMEM, "too many varying counts (u32 offsets)");
     B.key_first.resize(n_keys);
     B.key_flags.resize(n_keys);
     std::vector<DevVarKey> vk(nk);
@@ -814,8 +958,8 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b) {
         B.var_idx[k] = i;
     }
     B.var_keys = std::move(vk);
-    // (a batch reduced before on another ctx: that ctx no longer holds its counts)
-    if (B.var_ctx && B.var_ctx != ctx && B.var_ctx->var_owner == &B) B.var_ctx->var_owner = nullptr;
+    // (a batch reduced before on another ctx: B.var_ctx moves here; that ctx drops B
+    // as its owner when it next looks -- it checks B.var_ctx under B.var_mu)
     {  // the varying counts stay on the device until a host reader needs them
         std::lock_guard<std::mutex> g(B.var_mu);
         B.var_dev = ctx->var_counts.p;
@@ -842,6 +986,10 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
     Batch &B = b->b;
     if (!B.reduced) return tfbs::fail(TFBS_E_STATE, "keys not reduced (tfbs_batch_reduce)");
     if (!B.keep_membership) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    {  // the varying counts the encode reads are this ctx's (var_counts, at the offsets of its reduction)
+        std::lock_guard<std::mutex> g(B.var_mu);
+        if (B.var_ctx != ctx) return tfbs::fail(TFBS_E_STATE, "batch last reduced on another ctx (tfbs_batch_reduce here)");
+    }
     r1 = std::min(r1, B.rh.size());
     r0 = std::min(r0, r1);
     HIP_TRY(hipSetDevice(ctx->device));
@@ -1129,9 +1277,15 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
 
 }  // namespace
 
-int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
-                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
-                         uint64_t *text_bytes) {
+}  // extern "C"
+
+namespace tfbs {
+
+// tfbs_batch_rows_bgzf; pos_base (optional): the POS base is asked for once the
+// call's rows are counted (every piece's row parts built first).
+int rows_bgzf_chained(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome, uint32_t min_maf,
+                      uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                      const std::function<int(uint64_t, uint32_t *)> &pos_base) {
     if (!ctx || !b || !chromosome || !fake_position || fd < 0) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not resident on this ctx");
     Batch &B = b->b;
@@ -1155,10 +1309,19 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
     constexpr size_t kPlanSlots = tfbs_ctx::kBgSlots + 1;
     tfbs::RowPlan plans[kPlanSlots];
     std::vector<char> heads[kPlanSlots];
+    std::shared_ptr<RowParts> parts;  // pos_base: every piece's rows before the first POS
+    if (pos_base) {
+        const double t0 = now();
+        uint64_t nr = 0;
+        int rc = build_row_parts(B, r0, r1, min_maf, ctx->host_threads, parts, &nr);
+        ctx->rows_s[0] += now() - t0;
+        if (rc || (rc = pos_base(nr, fake_position))) return rc;
+    }
     auto build = [&](size_t j) {
         const double t0 = now();
-        const int r = tfbs::build_row_plan(B, cut(j), cut(j + 1), chrom, min_maf, fake_position, ctx->host_threads,
-                                           plans[j % kPlanSlots]);
+        const int r = parts ? plan_from_parts(B, *parts, cut(j), cut(j + 1), chrom, fake_position, plans[j % kPlanSlots])
+                            : tfbs::build_row_plan(B, cut(j), cut(j + 1), chrom, min_maf, fake_position,
+                                                   ctx->host_threads, plans[j % kPlanSlots]);
         ctx->rows_s[0] += now() - t0;
         return r;
     };
@@ -1185,9 +1348,21 @@ int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, con
         if (rc) return rc;
     }
     if (n_rows) *n_rows = rows;
-    if (text_bytes) *text_bytes = text;
     if (bytes) *bytes = pp.written;
+    ctx->rows_text_last = text;
     return TFBS_OK;
+}
+
+}  // namespace tfbs
+
+extern "C" {
+
+int tfbs_batch_rows_bgzf(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
+                         uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                         uint64_t *text_bytes) {
+    const int rc = tfbs::rows_bgzf_chained(ctx, b, r0, r1, chromosome, min_maf, fake_position, fd, bytes, n_rows, {});
+    if (!rc && text_bytes) *text_bytes = ctx->rows_text_last;
+    return rc;
 }
 
 int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t n, uint32_t *counts,

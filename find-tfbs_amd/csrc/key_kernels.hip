@@ -19,6 +19,7 @@
 // download).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <string>
 
 #include "keys.hpp"
@@ -39,7 +40,7 @@ constexpr uint32_t kAsmKeyWin = 32 * kAsmKeyWords;
 
 // Region r's spill records (bucketed: [spill_off[r], spill_off[r + 1]) of spill_sorted).
 __device__ __forceinline__ uint2 spill_range(const AsmArgs &A, uint32_t r) {
-    return A.n_spill ? make_uint2(A.spill_off[r], A.spill_off[r + 1]) : make_uint2(0, 0);
+    return (A.spill_count && *A.spill_count) ? make_uint2(A.spill_off[r], A.spill_off[r + 1]) : make_uint2(0, 0);
 }
 
 // The inner ranges [k0, k0 + nk) a reference hit (window i of a strand of length L)
@@ -111,7 +112,9 @@ __device__ __forceinline__ void visit_refs(const AsmArgs &A, uint32_t r, const D
     }
 }
 
-__global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
+// One region per iteration: every region (list == nullptr, grid = regions) or the
+// list[0] regions at list + 1 over a fixed grid.
+__global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uint32_t *list) {
     __shared__ uint32_t s_cnt[kAsmCounters];
     __shared__ uint32_t s_rh[kAsmHaps];    // per haplotype: first staged run | runs << 16 (0xFFFFFFFF: not HAP_DEDUP)
     __shared__ uint2 s_run[kAsmRuns];      // the region's diff runs
@@ -119,9 +122,14 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
     __shared__ uint4 s_ref[kAsmRefs];      // make_ref
     __shared__ uint32_t s_bits[kAsmKeyWords], s_rbase[kAsmKeyWords];  // touched keys of the window, rows before each word
     __shared__ uint32_t s_scan[kAsmBlock];
-    __shared__ uint32_t s_nhit, s_nref, s_nvar, s_vbase, s_obase;
-    const uint32_t r = blockIdx.x;
+    __shared__ uint32_t s_nhit, s_nref, s_nvar, s_nput;
+    __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n_it = list ? list[0] : gridDim.x;
+    for (uint32_t it = blockIdx.x; it < n_it; it += gridDim.x) {
+    const uint32_t r = list ? list[1 + it] : it;
+    __syncthreads();  // the previous region's LDS readers are done
+    [&]() {
     const DevRegion rg = A.regions[r];
     const uint32_t U = rg.hap_count, n_inner = rg.n_inner;
     const uint32_t K = A.n_slots * n_inner;
@@ -288,10 +296,10 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 if (t < nrow) atomicAdd(&cnt[t * U + l], 1u);
             });
             // reference hits: +1 to every HAP_DEDUP haplotype for which the hit's
-            // window is not dirty (the scan did not read it: same bases and positions
-            // as the reference's; tfbs_internal.hpp run_meets, span 8 x the class)
-            auto dirty = [&](uint32_t l, uint32_t dk, uint32_t w) {
-                const uint32_t S = kMChunkCols * (dk + 1);
+            // window is not dirty (its strand columns have the reference's bases and
+            // positions: the scan lists no hit there; tfbs_internal.hpp run_meets, span L)
+            auto dirty = [&](uint32_t l, uint32_t L, uint32_t w) {
+                const uint32_t S = L;
                 if (lds_haps) {
                     const uint32_t x = s_rh[l];
                     if (x == 0xFFFFFFFFu) return true;
@@ -308,7 +316,7 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
             if (refs_on && refs_lds && U <= 32 * kAsmBlock) {
                 for (uint32_t q0 = 0; q0 < nref; q0++) {  // workgroup-uniform; threads over the haplotypes
                     const uint4 q = s_ref[q0];
-                    const uint32_t dk = q.z >> 16;
+                    const uint32_t L = q.z & 0xFFFFu;
                     bool here = false;  // uniform: a key of the hit is in this chunk
                     ref_keys(q, [&](uint32_t key) {
                         here = here || (key - kw0 < kwn && row_of(key - kw0) - t0 < nrow);
@@ -316,7 +324,7 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                     if (!here) continue;
                     uint32_t keep = 0;  // bit j: haplotype tid + j kAsmBlock inherits the hit
                     for (uint32_t l = tid, j = 0; l < U; l += kAsmBlock, j++)
-                        if (!dirty(l, dk, q.y)) keep |= 1u << j;
+                        if (!dirty(l, L, q.y)) keep |= 1u << j;
                     ref_keys(q, [&](uint32_t key) {
                         const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
                         if (t >= nrow) return;
@@ -326,12 +334,12 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 }
             } else if (refs_on) {  // too many for LDS (rare): each thread walks its hits' haplotypes
                 visit_refs(A, r, rg, [&](const uint4 &q) {
-                    const uint32_t dk = q.z >> 16;
+                    const uint32_t L = q.z & 0xFFFFu;
                     ref_keys(q, [&](uint32_t key) {
                         const uint32_t t = key - kw0 < kwn ? row_of(key - kw0) - t0 : UINT32_MAX;
                         if (t >= nrow) return;
                         for (uint32_t l = 0; l < U; l++)
-                            if (!dirty(l, dk, q.y)) atomicAdd(&cnt[t * U + l], 1u);
+                            if (!dirty(l, L, q.y)) atomicAdd(&cnt[t * U + l], 1u);
                     });
                 });
             }
@@ -366,12 +374,12 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 }
             }
             __syncthreads();
-            const uint32_t nvar = s_nvar;
+            const uint32_t nvar = s_nvar;  // (reset only after the next chunk's first barrier)
             if (nvar == 0) continue;
             if (tid == 0) {  // the chunk's share of the compact lists
-                s_vbase = atomicAdd(A.var_tot, nvar);
-                s_obase = atomicAdd(A.var_tot + 1, nvar * U);
-                s_nvar = 0;
+                s_vbase = atomicAdd(A.var_tot, (unsigned long long)nvar);
+                s_obase = atomicAdd(A.var_tot + 1, (unsigned long long)nvar * U);
+                s_nput = 0;
             }
             __syncthreads();
             for (uint32_t rr = wave; rr < nrow; rr += kAsmWaves) {
@@ -382,15 +390,418 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A) {
                 if (__ballot(diff != 0) == 0) continue;
                 const uint32_t j = kw0 + key_of_row(t0 + rr);
                 uint32_t at = 0;
-                if (lane == 0) at = atomicAdd(&s_nvar, 1u);
+                if (lane == 0) at = atomicAdd(&s_nput, 1u);
                 at = __shfl(at, 0);
-                const uint32_t vi = s_vbase + at;
-                const uint64_t off = (uint64_t)s_obase + (uint64_t)at * U;
+                const uint64_t vi = s_vbase + at;
+                const uint64_t off = s_obase + (uint64_t)at * U;
                 if (vi < A.var_keys_cap && off + U <= A.var_cap) {
                     if (lane == 0) A.var_keys[vi] = DevVarKey{r, j, off};
                     for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = col[l];
                 }
             }
+        }
+    }
+    }();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// key_fast_kernel: the reduction (mode 0) of one region per workgroup with
+// every list in LDS.  A distinct haplotype l's count on key j is
+//     own(l, j) + [HAP_DEDUP l] * (R(j) - D(l, j))
+// (own: its hits, all in windows the scan read; R: the reference hits on j;
+// D: those whose window is dirty for l -- the scan read that window of l, so
+// its own hits already cover it).  So the region's work is its own hits plus,
+// per HAP_DEDUP haplotype, the reference hits inside its few dirty windows
+// (found by walking its diff runs over the reference hits sorted by window):
+// one "correction" list of (key, l, +1 | -1) entries (in LDS, or for a region
+// with many haplotypes a share of a launch-wide arena in global memory), then
+// per chunk of touched keys a [key][haplotype] block in LDS that starts at the
+// base (R(j) or 0, or the dense count of a LUT/generic slot) and takes the
+// corrections with LDS atomics.  A region past the kernel's limits (haplotypes,
+// keys, hit lists, reference hits, diff runs, arena) is appended to A.redo and
+// left to key_asm_kernel.
+constexpr int kFBlock = 256;
+constexpr uint32_t kFWaves = kFBlock / 64;
+constexpr uint32_t kFMaxU = 1024;     // distinct haplotypes (10 bits of a correction)
+constexpr uint32_t kFCor = 3072;      // corrections: own hits and dirty reference hits
+constexpr uint32_t kFRefs = 256;      // reference hits
+constexpr uint32_t kFRuns = 512;      // diff runs of the region's HAP_DEDUP haplotypes
+constexpr uint32_t kFCnt = 4096;      // u32 counters of a chunk: rows x U
+constexpr uint32_t kFRows = 512;      // rows (touched keys) per chunk
+constexpr uint32_t kFKeyWords = 512;  // touched-key bitmap: keys <= 16384
+constexpr uint32_t kFLists = 256;     // scan hit lists over the region's haplotypes
+constexpr uint32_t kFNone = 0xFFFFFFFFu;
+static_assert(kFMaxU % kFBlock == 0 && kFKeyWords % kFBlock == 0 && kFLists <= kFBlock && kFRefs <= kFBlock,
+              "key_fast_kernel's per-thread shares");
+
+// correction: key << 11 | (-1) << 10 | local haplotype
+__device__ __forceinline__ uint32_t cor_entry(uint32_t key, uint32_t l, uint32_t neg) {
+    return (key << 11) | (neg << 10) | l;
+}
+
+// Appends v from the wave's lanes with want set, in lane order (one LDS atomic
+// per wave); *n counts every attempt (> cap: overflow).
+__device__ __forceinline__ void wave_push(uint32_t *list, uint32_t *n, uint32_t cap, bool want, uint32_t v) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63, leader = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(n, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    if (want) {
+        const uint32_t at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        if (at < cap) list[at] = v;
+    }
+}
+
+// Exclusive prefix of v over the workgroup (wave scans + the waves' totals in s_w).
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_w[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kFWaves; w++) {
+        const uint32_t t = s_w[w];
+        pre += w < wave ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
+    __shared__ uint32_t s_cor[kFCor];
+    __shared__ uint4 s_ref[kFRefs];          // make_ref, sorted by window
+    __shared__ uint2 s_run[kFRuns];
+    __shared__ uint32_t s_hap[kFMaxU];       // HAP_DEDUP: its first run in s_run | runs << 16; else kFNone
+    __shared__ uint32_t s_cnt[kFCnt];
+    __shared__ uint32_t s_bits[kFKeyWords], s_rbase[kFKeyWords];
+    __shared__ uint32_t s_rkey[kFRows], s_rr[kFRows];  // per row of a chunk: its key; R(key), then its varying slot
+    __shared__ uint32_t s_loff[kFLists + 1], s_lidx[kFLists];
+    __shared__ uint32_t s_w[kFWaves];
+    __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena;
+    __shared__ unsigned long long s_vbase, s_obase;
+    const uint32_t r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const DevRegion rg = A.regions[r];
+    const uint32_t U = rg.hap_count, n_inner = rg.n_inner, K = A.n_slots * n_inner;
+    const uint64_t ko = (uint64_t)rg.inner_off * A.n_slots;
+    if (U == 0 || K == 0) {  // no samples: no haplotype, no match, no key
+        for (uint32_t j = tid; j < K; j += kFBlock) {
+            A.key_first[ko + j] = 0;
+            A.key_flags[ko + j] = 0;
+        }
+        return;
+    }
+    auto give_up = [&]() {  // workgroup-uniform, before any output
+        if (tid == 0) A.redo[1 + atomicAdd(A.redo, 1u)] = r;
+    };
+    if (U > min(kFMaxU, A.fast_max_u) || K > 32 * kFKeyWords || n_inner > 32) return give_up();
+    const uint32_t hb = rg.hap_begin;
+    const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
+    if (tid == 0) {
+        s_ncor = s_nref = s_run1 = 0;
+        s_run0 = kFNone;
+    }
+    __syncthreads();
+    // descriptors: which haplotypes reuse the reference's windows, and their runs
+    constexpr uint32_t kPer = kFMaxU / kFBlock;
+    uint32_t roff[kPer], rn[kPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; q++) {
+        const uint32_t l = tid + q * kFBlock;
+        roff[q] = kFNone;
+        rn[q] = 0;
+        if (l < U) {
+            const DevHap &h = A.haps[hb + l];
+            if (h.flags & HAP_DEDUP) {
+                roff[q] = h.drun_off;
+                rn[q] = h.n_druns;
+                atomicMin(&s_run0, h.drun_off);
+                atomicMax(&s_run1, h.drun_off + h.n_druns);
+            }
+        }
+    }
+    // own hits: the scan workgroups' lists over the region's haplotype groups (one
+    // hitn load per thread), their entries read flat over the workgroup below
+    uint32_t nl = 0;
+    const uint32_t g_lo = hb / A.hpb, g_hi = (hb + U - 1) / A.hpb;
+    if (A.mfma)
+        for (uint32_t si = 0; si < A.n_srcs; si++) {
+            const HitSrc src = A.srcs[si];
+            const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
+            if (ga < gb) nl += (gb - ga) * src.ns * kMBlockWaves;
+        }
+    if (nl > kFLists) return give_up();
+    uint32_t lcnt = 0;
+    if (tid < nl) {
+        uint32_t t = tid;
+        for (uint32_t si = 0; si < A.n_srcs; si++) {
+            const HitSrc src = A.srcs[si];
+            const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
+            if (ga >= gb) continue;
+            const uint32_t per_g = src.ns * kMBlockWaves;
+            if (t < (gb - ga) * per_g) {
+                const uint32_t g = ga + t / per_g, rem = t % per_g;
+                const uint32_t wg = src.wg_base + (g - src.g0) * src.ns + rem / kMBlockWaves;
+                const uint32_t idx = wg * kMBlockWaves + rem % kMBlockWaves;
+                lcnt = A.hitn[idx];
+                s_lidx[tid] = idx;
+                break;
+            }
+            t -= (gb - ga) * per_g;
+        }
+    }
+    uint32_t n_ent = 0;
+    const uint32_t loff = block_excl_scan(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    if (tid < nl) s_loff[tid] = loff;
+    if (tid == 0) s_loff[nl] = n_ent;
+    const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
+    if (nruns > kFRuns) return give_up();
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; q++) {
+        const uint32_t l = tid + q * kFBlock;
+        if (l < U) s_hap[l] = roff[q] == kFNone ? kFNone : (roff[q] - run0) | (rn[q] << 16);
+    }
+    for (uint32_t k = tid; k < nruns; k += kFBlock)
+        s_run[k] = make_uint2(A.druns[2 * (run0 + k)], A.druns[2 * (run0 + k) + 1]);
+    // reference hits: the region's list, then its spill records of kind 1
+    const uint2 sp = spill_range(A, r);
+    if (refs_on) {
+        const uint32_t n = min(A.ref_count[r], kRefPerRegion);
+        if (tid < n) {
+            const size_t o = 2 * ((size_t)r * kRefPerRegion + tid);
+            const uint32_t at = atomicAdd(&s_nref, 1u);
+            if (at < kFRefs) s_ref[at] = make_ref(A, rg, A.ref_hits[o], A.ref_hits[o + 1]);
+        }
+        for (uint32_t e = sp.x + tid; e < sp.y; e += kFBlock) {
+            const uint32_t *q = A.spill_sorted + 3 * (size_t)e;
+            if (q[0] >> 31) {
+                const uint32_t at = atomicAdd(&s_nref, 1u);
+                if (at < kFRefs) s_ref[at] = make_ref(A, rg, q[1], q[2]);
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nref = s_nref;
+    if (nref > kFRefs) return give_up();
+    {  // the reference hits by window (rank sort; ties by list position)
+        uint4 mine = make_uint4(0, 0, 0, 0);
+        uint32_t rank = 0;
+        if (tid < nref) {
+            mine = s_ref[tid];
+            for (uint32_t j = 0; j < nref; j++) {
+                const uint32_t w = s_ref[j].y;
+                rank += (w < mine.y || (w == mine.y && j < tid)) ? 1u : 0u;
+            }
+        }
+        __syncthreads();
+        if (tid < nref) s_ref[rank] = mine;
+        __syncthreads();
+    }
+    // D: per HAP_DEDUP haplotype the reference hits in its dirty windows (a run
+    // [a, b] meets the columns [w, w + L - 1] of windows w in [a - L + 1, b]; the
+    // hits in [a - 31, b] are tested with their strand's L <= 32, each once: runs
+    // ascend and the cursor only moves forward).  f(l, ref hit) per dirty pair.
+    auto each_dirty = [&](auto &&f) {
+        if (!nref) return;
+        for (uint32_t l = tid; l < U; l += kFBlock) {
+            const uint32_t x = s_hap[l];
+            if (x == kFNone) continue;
+            const uint32_t k0 = x & 0xFFFFu, k1 = k0 + (x >> 16);
+            uint32_t p = 0;
+            for (uint32_t k = k0; k < k1 && p < nref; k++) {
+                const uint32_t a = s_run[k].x, b = s_run[k].y;
+                const uint32_t lo = a >= kMChunkCols * kMMaxChunks - 1 ? a - (kMChunkCols * kMMaxChunks - 1) : 0u;
+                while (p < nref && s_ref[p].y < lo) p++;
+                for (; p < nref && s_ref[p].y <= b; p++) {
+                    const uint4 q = s_ref[p];
+                    bool dirty = false;
+                    for (uint32_t k2 = k0; k2 < k1 && !dirty; k2++)
+                        dirty = run_meets(s_run[k2].x, s_run[k2].y, q.y, q.z & 0xFFFFu);
+                    if (dirty) f(l, q);
+                }
+            }
+        }
+    };
+    uint32_t nd = 0;
+    each_dirty([&](uint32_t, const uint4 &q) { nd += __popc(q.w); });
+    uint32_t nD = 0;
+    (void)block_excl_scan(nd, s_w, nD);
+    // the corrections' list: LDS when they fit, else a share of the launch's arena
+    const uint32_t need = n_ent + (sp.y - sp.x) + nD;  // (an upper bound: entries of other regions' haplotypes)
+    const bool in_lds = need <= min(kFCor, A.cor_lds);
+    if (tid == 0) {
+        s_arena = kFNone;
+        if (!in_lds) {
+            const uint32_t at = atomicAdd(A.cor_used, need);
+            if (at <= A.cor_cap && need <= A.cor_cap - at) s_arena = at;
+        }
+    }
+    __syncthreads();
+    if (!in_lds && s_arena == kFNone) return give_up();  // the host grows the arena for the next call
+    uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
+    const uint2 *hitl = reinterpret_cast<const uint2 *>(A.hitl);
+    for (uint32_t e0 = 0; e0 < n_ent; e0 += kFBlock) {
+        const uint32_t e = e0 + tid;
+        bool want = false;
+        uint32_t v = 0;
+        if (e < n_ent) {
+            uint32_t lo = 0, hi = nl - 1;  // the list holding entry e: the last with s_loff <= e
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (s_loff[mid] <= e) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint32_t idx = s_lidx[lo];
+            const uint2 h = hitl[(size_t)(idx / kMBlockWaves) * A.cand_cap +
+                                 (size_t)(idx % kMBlockWaves) * (A.cand_cap / kMBlockWaves) + (e - s_loff[lo])];
+            want = h.x - hb < U;
+            v = cor_entry(h.y, h.x - hb, 0);
+        }
+        wave_push(cor, &s_ncor, need, want, v);
+    }
+    for (uint32_t e0 = sp.x; e0 < sp.y; e0 += kFBlock) {  // own hits of the spill list (kind 0)
+        const uint32_t e = e0 + tid;
+        bool want = false;
+        uint32_t v = 0;
+        if (e < sp.y) {
+            const uint32_t *q = A.spill_sorted + 3 * (size_t)e;
+            want = !(q[0] >> 31) && q[1] - hb < U;
+            v = cor_entry(q[2], q[1] - hb, 0);
+        }
+        wave_push(cor, &s_ncor, need, want, v);
+    }
+    each_dirty([&](uint32_t l, const uint4 &q) {
+        for (uint32_t m = q.w; m; m &= m - 1) {
+            const uint32_t at = atomicAdd(&s_ncor, 1u);
+            if (at < need) cor[at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
+        }
+    });
+    const uint32_t nw = (K + 31) / 32;
+    for (uint32_t w = tid; w < nw; w += kFBlock) s_bits[w] = 0;
+    __syncthreads();
+    const uint32_t ncor = s_ncor;  // <= need
+    // touched keys: own hits (the dirty reference hits' keys are reference keys),
+    // reference hits, every key of a LUT/generic slot; rows in key order
+    for (uint32_t e = tid; e < ncor; e += kFBlock) {
+        const uint32_t c = cor[e];
+        if (!((c >> 10) & 1u)) atomicOr(&s_bits[c >> 16], 1u << ((c >> 11) & 31u));
+    }
+    if (tid < nref)
+        for (uint32_t m = s_ref[tid].w; m; m &= m - 1) {
+            const uint32_t key = s_ref[tid].x + __builtin_ctz(m);
+            atomicOr(&s_bits[key >> 5], 1u << (key & 31u));
+        }
+    if (A.any_dense)
+        for (uint32_t j = tid; j < K; j += kFBlock)
+            if (!A.slot_mfma[j / n_inner]) atomicOr(&s_bits[j >> 5], 1u << (j & 31u));
+    __syncthreads();
+    uint32_t T = 0;
+    {
+        constexpr uint32_t per = kFKeyWords / kFBlock;
+        uint32_t mine = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t w = tid * per + q;
+            if (w < nw) mine += __popc(s_bits[w]);
+        }
+        uint32_t run = block_excl_scan(mine, s_w, T);
+#pragma unroll
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t w = tid * per + q;
+            if (w < nw) {
+                s_rbase[w] = run;
+                run += __popc(s_bits[w]);
+            }
+        }
+    }
+    auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
+    // untouched keys: no match -- no key in the reference's HashMap
+    for (uint32_t j = tid; j < K; j += kFBlock)
+        if (!((s_bits[j >> 5] >> (j & 31)) & 1u)) {
+            A.key_first[ko + j] = 0;
+            A.key_flags[ko + j] = 0;
+        }
+    const uint32_t rows_per = min(kFCnt / U, kFRows);
+    const uint64_t dense_base = A.dense_base ? A.haps[hb].count_off : 0;
+    for (uint32_t t0 = 0; t0 < T; t0 += rows_per) {
+        const uint32_t nrow = min(rows_per, T - t0);
+        __syncthreads();  // s_rbase written / the previous chunk's readers done
+        if (tid == 0) s_nvar = 0;
+        for (uint32_t rr = tid; rr < nrow; rr += kFBlock) {  // the row's key: the word whose rows start at or before it
+            const uint32_t t = t0 + rr;
+            uint32_t lo = 0, hi = nw - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (s_rbase[mid] <= t) lo = mid;
+                else hi = mid - 1;
+            }
+            uint32_t b = s_bits[lo];
+            for (uint32_t k = t - s_rbase[lo]; k; k--) b &= b - 1;
+            s_rkey[rr] = 32 * lo + __builtin_ctz(b);
+            s_rr[rr] = 0;
+        }
+        __syncthreads();
+        if (tid < nref)  // R: reference hits per key
+            for (uint32_t m = s_ref[tid].w; m; m &= m - 1) {
+                const uint32_t t = row_of(s_ref[tid].x + __builtin_ctz(m)) - t0;
+                if (t < nrow) atomicAdd(&s_rr[t], 1u);
+            }
+        __syncthreads();
+        for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {  // the base of every haplotype
+            const uint32_t j = s_rkey[rr], R = s_rr[rr];
+            const bool dense = A.any_dense && !A.slot_mfma[j / n_inner];
+            for (uint32_t l = lane; l < U; l += 64)
+                s_cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
+                                          : (s_hap[l] != kFNone ? R : 0u);
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < ncor; e += kFBlock) {
+            const uint32_t c = cor[e];
+            const uint32_t t = row_of(c >> 11) - t0;
+            if (t < nrow) atomicAdd(&s_cnt[t * U + (c & 1023u)], ((c >> 10) & 1u) ? 0xFFFFFFFFu : 1u);
+        }
+        __syncthreads();
+        // classify: one wave per row
+        for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {
+            const uint32_t *col = s_cnt + rr * U;
+            const uint32_t c0 = col[0];
+            uint32_t any = 0, diff = 0;
+            for (uint32_t l = lane; l < U; l += 64) {
+                const uint32_t c = col[l];
+                any |= c;
+                diff |= c ^ c0;
+            }
+            const bool a = __ballot(any != 0) != 0, v = __ballot(diff != 0) != 0;
+            if (lane == 0) {
+                const uint32_t j = s_rkey[rr];
+                A.key_first[ko + j] = c0;
+                A.key_flags[ko + j] = (uint8_t)((a ? KEY_ANY : 0) | (v ? KEY_VARIES : 0));
+                s_rr[rr] = v ? atomicAdd(&s_nvar, 1u) : kFNone;
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && s_nvar) {  // the chunk's share of the compact lists
+            s_vbase = atomicAdd(A.var_tot, (unsigned long long)s_nvar);
+            s_obase = atomicAdd(A.var_tot + 1, (unsigned long long)s_nvar * U);
+        }
+        __syncthreads();
+        for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {
+            const uint32_t slot = s_rr[rr];
+            if (slot == kFNone) continue;
+            const uint64_t vi = s_vbase + slot, off = s_obase + (uint64_t)slot * U;
+            if (vi >= A.var_keys_cap || off + U > A.var_cap) continue;  // the host grows the lists and reruns
+            if (lane == 0) A.var_keys[vi] = DevVarKey{r, s_rkey[rr], off};
+            for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = s_cnt[rr * U + l];
         }
     }
 }
@@ -404,9 +815,10 @@ __global__ __launch_bounds__(256) void spill_hist_kernel(const uint32_t *__restr
         atomicAdd(&bcnt[spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
 }
 
-__global__ __launch_bounds__(1024) void spill_scan_kernel(uint32_t *__restrict__ bcnt, uint32_t n,
-                                                          uint32_t *__restrict__ boff) {
+__global__ __launch_bounds__(1024) void spill_scan_kernel(const uint32_t *__restrict__ over, uint32_t *__restrict__ bcnt,
+                                                          uint32_t n, uint32_t *__restrict__ boff) {
     __shared__ uint32_t s[1024];
+    if (over[0] == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 < n; b0 += 1024) {
         const uint32_t i = b0 + threadIdx.x;
@@ -769,7 +1181,7 @@ int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spi
     hipError_t e = hipMemsetAsync(bcnt, 0, (size_t)(n_regions + 1) * 4, stream);
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("spill bucket memset: ") + hipGetErrorString(e));
     hipLaunchKernelGGL(spill_hist_kernel, dim3(64), dim3(256), 0, stream, over, cap, spill, bcnt);
-    hipLaunchKernelGGL(spill_scan_kernel, dim3(1), dim3(1024), 0, stream, bcnt, n_regions, boff);
+    hipLaunchKernelGGL(spill_scan_kernel, dim3(1), dim3(1024), 0, stream, over, bcnt, n_regions, boff);
     hipLaunchKernelGGL(spill_scatter_kernel, dim3(64), dim3(256), 0, stream, over, cap, spill, boff, bcnt, sorted);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("spill bucket kernels: ") + hipGetErrorString(e));
@@ -778,9 +1190,23 @@ int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spi
 
 int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
     if (n_regions == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_asm_kernel, dim3(n_regions), dim3(kAsmBlock), 0, stream, a);
+    hipLaunchKernelGGL(key_asm_kernel, dim3(n_regions), dim3(kAsmBlock), 0, stream, a, (const uint32_t *)nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_asm_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
+    if (n_regions == 0) return TFBS_OK;
+    hipError_t e = hipMemsetAsync(a.redo, 0, 4, stream);
+    if (e == hipSuccess) e = hipMemsetAsync(a.cor_used, 0, 4, stream);
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast memset: ") + hipGetErrorString(e));
+    hipLaunchKernelGGL(key_fast_kernel, dim3(n_regions), dim3(kFBlock), 0, stream, a);
+    // the regions it left: a fixed grid over the list (no host round trip)
+    hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
+                       (const uint32_t *)a.redo);
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 

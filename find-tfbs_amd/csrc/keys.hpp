@@ -30,7 +30,10 @@ struct AsmArgs {
     // reference hits per region, and the spill records bucketed by region
     const uint32_t *ref_hits, *ref_count;
     const uint32_t *spill_sorted, *spill_off;
-    uint32_t n_spill;           // 0: no spill records (spill_off unused)
+    // the scan's spill record count (device, ScanArgs::over[0]; 0: spill_off is not
+    // read), bucketed up to spill_cap records
+    const uint32_t *spill_count;
+    uint32_t spill_cap;
     uint32_t *counts;           // dense counts: read (LUT/generic slots) / written (mode 1)
     uint32_t dense_base;        // != 0: counts exist (haps' count_off are valid)
     uint32_t *scratch;          // counters of regions with more haplotypes than the LDS block holds
@@ -44,10 +47,27 @@ struct AsmArgs {
     uint32_t var_keys_cap;
     uint32_t *var_counts;
     uint64_t var_cap;
-    uint32_t *var_tot;
+    unsigned long long *var_tot;
+    // regions key_fast_kernel leaves to key_asm_kernel (redo[0] of them at redo + 1):
+    // written by key_fast_kernel, worked through by key_asm_kernel's list pass
+    uint32_t *redo;
+    uint32_t fast_max_u;  // key_fast_kernel takes regions of at most this many haplotypes (TFBS_KEY_FAST_MAXU)
+    // key_fast_kernel's corrections of regions past its LDS list: shares of cor_arena
+    // (cor_cap u32) taken from *cor_used (zeroed by launch_key_fast; read back by the host)
+    uint32_t *cor_arena;
+    uint32_t cor_cap;
+    uint32_t *cor_used;
+    uint32_t cor_lds;  // corrections kept in LDS at most (TFBS_KEY_COR_LDS, tests: the arena path)
 };
 
+// key_asm_kernel over every region (mode 0 or 1).
 int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
+// The reduction (mode 0) in two launches, no host round trip: key_fast_kernel
+// takes every region whose haplotypes, keys, hits and reference hits fit its LDS
+// lists (all of them at BASELINE shapes) and appends the others to a.redo, which
+// key_asm_kernel then works through (a fixed grid looping over the list).
+// a.redo[0] must be zero (launch_key_fast clears it on the stream).
+int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 uint32_t key_asm_lds_counters();  // regions with more distinct haplotypes use AsmArgs::scratch
 // Buckets the spill records (ScanArgs::spill, *over of cap) by region: boff[r]
 // .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters).

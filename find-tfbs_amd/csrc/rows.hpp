@@ -6,6 +6,8 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -47,5 +49,19 @@ struct RowPlan {
 // metadata, regions formatted on `threads` host threads.
 int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chrom, uint32_t min_maf,
                    uint32_t *fake, uint32_t threads, RowPlan &plan);
+// build_row_plan in two steps: the rows of [r0, r1) without their POS (parallel;
+// *n_rows of them), then the plan of a sub-range [r0, r1) of them with POS from
+// *fake (serial, cheap) -- a caller that must know a call's row count before its
+// POS base (the multi-device run flow's POS chain) builds the parts first.
+struct RowParts;
+int build_row_parts(const Batch &B, size_t r0, size_t r1, uint32_t min_maf, uint32_t threads,
+                    std::shared_ptr<RowParts> &out, uint64_t *n_rows);
+int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std::string &chrom, uint32_t *fake,
+                    RowPlan &plan);
+// tfbs_batch_rows_bgzf (device.hip) whose POS base is asked for once the call's rows
+// are counted: pos_base(n_rows, &base) -- it may block -- sets *fake_position.
+int rows_bgzf_chained(::tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
+                      uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
+                      const std::function<int(uint64_t, uint32_t *)> &pos_base);
 
 }  // namespace tfbs

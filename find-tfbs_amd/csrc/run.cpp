@@ -8,8 +8,14 @@
 // (the reference spreads 50-peak chunks over threads and emits rows in thread
 // interleaving / HashMap order); rows within a region are sorted (D2); the
 // POS counter is therefore deterministic.
+#include <sys/mman.h>
+#include <sys/sendfile.h>
 #include <sys/stat.h>
 #include <unistd.h>
+
+#include <cerrno>
+#include <condition_variable>
+#include <mutex>
 
 #include <algorithm>
 #include <chrono>
@@ -27,6 +33,7 @@
 #include "batch.hpp"
 #include "io.hpp"
 #include "patterns.hpp"
+#include "rows.hpp"
 
 namespace tfbs {
 int batch_row_bodies(const Batch &B, uint32_t min_maf, std::string &out, uint32_t threads);
@@ -62,18 +69,20 @@ bool in_path(const char *prog) {
     return false;
 }
 
-// One block of merged regions [r0, r1) on one device: the two-stage pipeline
-// (a helper thread prepares batch k+1 -- FASTA windows, BCF records,
-// load_diffs, distinct haplotypes -- while batch k is scanned, reduced on the
-// device and formatted) with its own readers and ctx.  Row bodies (without
-// the "<chr>\t<POS>\t" prefix) go to `emit` in merged-peak order.
+// One device's share of the run: batches of merged regions (global batch g =
+// regions [g per_batch, (g + 1) per_batch)), processed in the two-stage pipeline
+// (a helper thread prepares the next batch -- FASTA windows, BCF records,
+// load_diffs, distinct haplotypes, grouped on the device where the region is
+// SNV-only -- while this one is scanned, reduced and encoded on the device) with
+// its own readers and ctx; out(g, ctx, batch) emits each batch's rows.
 struct Shard {
-    size_t r0 = 0, r1 = 0;
+    std::vector<size_t> batches;  // global batch indices, ascending
     int device = 0;
     uint32_t threads = 1;
     int rc = TFBS_OK;
     std::string err;
-    double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0, t_emit = 0;
+    size_t regions = 0;
+    double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0;
 };
 
 struct RunSetup {
@@ -86,16 +95,11 @@ struct RunSetup {
     size_t per_batch;
 };
 
-// Row bodies of one shard in merged-peak order; emit(bodies) gets each batch's
-// rows ('\n'-terminated, no chromosome/POS prefix).
-// emit(bodies): row bodies formatted on the host; blocks() (non-null for the
-// single shard of a one-device run): the output's file descriptor, the writer's
-// open block written, for the rows as device-made BGZF blocks (POS from *fake).
-template <class Emit, class Blocks>
-int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_t *fake) {
+template <class Out>
+int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     using namespace tfbs;
     const tfbs_run_args *a = S.a;
-    if (sh.r0 >= sh.r1) return TFBS_OK;
+    if (sh.batches.empty()) return TFBS_OK;
     Bcf bcf;
     int rc = bcf.open(a->bcf, sh.threads);
     if (rc) return rc;
@@ -110,17 +114,27 @@ int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_
         return rc;
     }
     std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
+    // SNV-only regions grouped on this device (haplotype.rs:16-88 on the GPU), one
+    // grouper for the shard's batches (its membership rows recycled batch to batch);
+    // TFBS_RUN_BUILD_DEVICE=0: every region on the host
+    std::shared_ptr<DevGrouper> grouper;
+    if (!(getenv("TFBS_RUN_BUILD_DEVICE") && atoi(getenv("TFBS_RUN_BUILD_DEVICE")) == 0)) {
+        grouper.reset(make_gpu_grouper(sh.device));
+        if (!grouper) return TFBS_E_NODEVICE;
+    }
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
     std::vector<const BcfRecord *> recs;
-    auto prepare = [&](size_t b0, BatchPtr &out, std::string &err) -> int {
+    auto prepare = [&](size_t g, BatchPtr &bp, std::string &err) -> int {
+        const size_t b0 = g * S.per_batch, b1 = std::min(S.merged.size(), b0 + S.per_batch);
         tfbs_batch *bb = nullptr;
         int rc = tfbs_batch_create(S.pp, (uint32_t)S.sel.size(), 1, &bb);
         if (rc) return err = tfbs_last_error(), rc;
-        out = BatchPtr(bb, tfbs_batch_destroy);
+        bp = BatchPtr(bb, tfbs_batch_destroy);
         Batch &B = bb->b;
+        B.grouper = grouper;
         for (auto &b : S.beds) B.beds.push_back(b.first);
         std::vector<RegionInput> ins;
-        for (size_t r = b0; r < std::min(sh.r1, b0 + S.per_batch); r++) {
+        for (size_t r = b0; r < b1; r++) {
             const auto &m = S.merged[r];
             RegionInput in;
             in.R.ms = m.first;
@@ -169,18 +183,19 @@ int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_
     BatchPtr cur(nullptr, tfbs_batch_destroy);
     std::string err;
     double t0 = now();
-    if ((rc = prepare(sh.r0, cur, err))) return fail(rc, err);
+    if ((rc = prepare(sh.batches[0], cur, err))) return fail(rc, err);
     sh.t_prep += now() - t0;
-    for (size_t b0 = sh.r0; b0 < sh.r1; b0 += S.per_batch) {
+    for (size_t bi = 0; bi < sh.batches.size(); bi++) {
+        const size_t g = sh.batches[bi];
         BatchPtr next(nullptr, tfbs_batch_destroy);
         std::string nerr;
         int nrc = TFBS_OK;
         double nprep = 0;
         std::thread helper;
-        if (b0 + S.per_batch < sh.r1)
-            helper = std::thread([&, b0] {
+        if (bi + 1 < sh.batches.size())
+            helper = std::thread([&, bi] {
                 const double t0 = now();
-                nrc = prepare(b0 + S.per_batch, next, nerr);
+                nrc = prepare(sh.batches[bi + 1], next, nerr);
                 nprep = now() - t0;
             });
         // join the helper on every exit path
@@ -193,31 +208,20 @@ int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_
         tfbs_batch *bb = cur.get();
         Batch &B = bb->b;
         t0 = now();
-        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_reduce(ctx, bb)) ||
-            (rc = tfbs_batch_encode_flags(ctx, bb, 0, B.rh.size(), blocks ? TFBS_ENC_DEVICE_CODES : 0)))
+        if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_assemble(ctx, bb)) ||
+            (rc = tfbs_batch_reduce(ctx, bb)) ||
+            (rc = tfbs_batch_encode_flags(ctx, bb, 0, B.rh.size(), out.device_rows ? TFBS_ENC_DEVICE_CODES : 0)))
             return rc;
         double t1 = now();
         sh.t_gpu += t1 - t0;
-        if (blocks) {  // rows formatted and deflated on the device (the only shard: POS is known here)
-            const int fd = (*blocks)();
-            if (fd < 0) return fd;
-            if ((rc = tfbs_batch_rows_bgzf(ctx, bb, 0, B.rh.size(), S.chrom.c_str(), a->min_maf, fake, fd, nullptr,
-                                           nullptr, nullptr)))
-                return rc;
-            sh.t_rows += now() - t1;
-        } else {
-            std::string bodies;
-            if ((rc = batch_row_bodies(B, a->min_maf, bodies, sh.threads))) return rc;
-            double t2 = now();
-            sh.t_rows += t2 - t1;
-            if ((rc = emit(bodies))) return rc;
-            sh.t_emit += now() - t2;
-        }
+        sh.regions += B.rh.size();
+        if ((rc = out(g, ctx, bb))) return rc;
+        sh.t_rows += now() - t1;
         if (a->verbose) {
             for (size_t r = 0; r < B.rh.size(); r++)
-                fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", b0 + r + 1, S.merged.size(),
-                        (unsigned long long)B.rh[r].ms, (unsigned long long)B.rh[r].me, B.rh[r].hap_count,
-                        B.rh[r].n_variants);
+                fprintf(stdout, "Peak %zu/%zu\t%llu\t%llu\t%u haplotypes\t%u variants\n", g * S.per_batch + r + 1,
+                        S.merged.size(), (unsigned long long)B.rh[r].ms, (unsigned long long)B.rh[r].me,
+                        B.rh[r].hap_count, B.rh[r].n_variants);
         }
         t0 = now();
         if (helper.joinable()) helper.join();
@@ -225,6 +229,72 @@ int run_shard(const RunSetup &S, Shard &sh, Emit &&emit, Blocks *blocks, uint32_
         sh.t_prep += nprep;
         if (nrc) return fail(nrc, nerr);
         cur = std::move(next);
+    }
+    return TFBS_OK;
+}
+
+// The batches' output in batch order across the devices' threads: the POS chain
+// (batch g's first POS = batch g - 1's + its rows, published as soon as g - 1 has
+// counted them, before it deflates) and the ordered writer (each batch's BGZF
+// blocks -- in a memory file -- or row bodies, written out in order).
+struct Ordered {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int64_t> base;  // POS of batch g's first row, -1 unknown
+    struct Item {
+        bool ready = false;
+        int fd = -1;           // BGZF blocks (memory file), or
+        std::string bodies;    // row bodies (host rows)
+    };
+    std::vector<Item> items;
+    bool failed = false;
+    int first_rc = TFBS_OK;  // the failure that stopped the others
+    std::string first_err;
+    explicit Ordered(size_t n) : base(n + 1, -1), items(n) { base[0] = 1; }
+    int chain(size_t g, uint64_t n_rows, uint32_t *fake) {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return failed || base[g] >= 0; });
+        if (failed) return tfbs::fail(TFBS_E_STATE, "another device's shard failed");
+        *fake = (uint32_t)base[g];
+        base[g + 1] = base[g] + (int64_t)n_rows;
+        cv.notify_all();
+        return TFBS_OK;
+    }
+    void submit(size_t g, Item &&it) {
+        std::lock_guard<std::mutex> l(mu);
+        items[g] = std::move(it);
+        items[g].ready = true;
+        cv.notify_all();
+    }
+    void abort(int rc, const std::string &err) {
+        std::lock_guard<std::mutex> l(mu);
+        if (!failed) {
+            first_rc = rc;
+            first_err = err;
+        }
+        failed = true;
+        cv.notify_all();
+    }
+    bool take(size_t g, Item &it) {  // waits for batch g; false if a shard failed
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return failed || items[g].ready; });
+        if (failed) return false;
+        it = std::move(items[g]);
+        return true;
+    }
+};
+
+int copy_fd(int src, int dst) {  // a memory file's bytes to dst
+    off_t off = 0;
+    const off_t n = lseek(src, 0, SEEK_END);
+    if (n < 0) return tfbs::fail(TFBS_E_IO, std::string("lseek: ") + strerror(errno));
+    while (off < n) {
+        const ssize_t w = sendfile(dst, src, &off, (size_t)std::min<off_t>(n - off, 1 << 30));
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
+        }
+        if (w == 0) return tfbs::fail(TFBS_E_IO, "write: short copy");
     }
     return TFBS_OK;
 }
@@ -341,84 +411,124 @@ int tfbs_run(const tfbs_run_args *a) {
     rc = w.write(header.data(), header.size());
     if (rc) return rc;
 
-    // shards: one contiguous block of merged regions per device
+    // shards: batch g of merged regions on device g % n (one device:
+    // every batch); rows in merged-peak order, POS counted across the devices
     S.per_batch = a->regions_per_batch ? a->regions_per_batch : 512;
     const std::vector<int> devs = parse_devices(a);
-    const size_t n_sh = std::max<size_t>(1, std::min(devs.size(), S.merged.size()));
+    const size_t n_batches = (S.merged.size() + S.per_batch - 1) / S.per_batch;
+    const size_t n_sh = std::max<size_t>(1, std::min(devs.size(), n_batches));
     std::vector<Shard> shards(n_sh);
     for (size_t k = 0; k < n_sh; k++) {
-        shards[k].r0 = k * S.merged.size() / n_sh;
-        shards[k].r1 = (k + 1) * S.merged.size() / n_sh;
         shards[k].device = devs[k];
         shards[k].threads = std::max<uint32_t>(1, threads / (uint32_t)n_sh);
     }
+    for (size_t g = 0; g < n_batches; g++) shards[g % n_sh].batches.push_back(g);
     const std::string chr = strip_chr(S.chrom);
     uint32_t fake = 1;
     const bool timing = getenv("TFBS_RUN_TIMING") && atoi(getenv("TFBS_RUN_TIMING"));
-    // TFBS_GPU_BGZF=0: rows formatted and deflated on the host threads, as a
-    // multi-device run does (its shards' POS are known only when they are joined)
+    // TFBS_GPU_BGZF=0: rows formatted on the host and deflated by the writer's host
+    // threads (zlib); default: BGZF blocks made on each device (bgzf_gpu.hip)
     const bool gpu_bgzf = !(getenv("TFBS_GPU_BGZF") && atoi(getenv("TFBS_GPU_BGZF")) == 0);
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
-    // shard 0 writes straight through the writer; the others spill their row
-    // bodies to <output>.part.<k> and are appended in order afterwards
-    std::vector<std::string> spill_path(n_sh);
-    std::vector<FILE *> spill(n_sh, nullptr);
-    struct SpillGuard {
-        std::vector<FILE *> &f;
-        std::vector<std::string> &p;
-        ~SpillGuard() {
-            for (size_t k = 0; k < f.size(); k++) {
-                if (f[k]) fclose(f[k]);
-                if (!p[k].empty()) remove(p[k].c_str());
+    double t_write = 0;
+    if (n_sh == 1) {  // one device: its batches in order, straight to the output
+        struct One {
+            bool device_rows;
+            const RunSetup &S;
+            tfbs::BgzfWriter &w;
+            const std::string &chr;
+            uint32_t &fake;
+            double &t_write;
+            int operator()(size_t, tfbs_ctx *ctx, tfbs_batch *bb) {
+                const size_t n = bb->b.rh.size();
+                if (device_rows) {
+                    const int fd = w.raw_fd();
+                    if (fd < 0) return fd;
+                    return tfbs_batch_rows_bgzf(ctx, bb, 0, n, S.chrom.c_str(), S.a->min_maf, &fake, fd, nullptr,
+                                                nullptr, nullptr);
+                }
+                std::string bodies;
+                if (int rc = tfbs::batch_row_bodies(bb->b, S.a->min_maf, bodies, std::max(1u, S.a->threads))) return rc;
+                return write_prefixed(w, chr, bodies.data(), bodies.size(), &fake);
             }
-        }
-    } spill_guard{spill, spill_path};
-    for (size_t k = 1; k < n_sh; k++) {
-        spill_path[k] = part + "." + std::to_string(k);
-        spill[k] = fopen(spill_path[k].c_str(), "w+b");
-        if (!spill[k]) return fail(TFBS_E_IO, "Could not create " + spill_path[k]);
-    }
-    auto run_one = [&](size_t k) {
-        Shard &sh = shards[k];
-        auto emit = [&](const std::string &bodies) -> int {
-            if (k == 0) return write_prefixed(w, chr, bodies.data(), bodies.size(), &fake);
-            if (!bodies.empty() && fwrite(bodies.data(), 1, bodies.size(), spill[k]) != bodies.size())
-                return fail(TFBS_E_IO, "write failed: " + spill_path[k]);
-            return TFBS_OK;
+        } one{gpu_bgzf, S, w, chr, fake, t_write};
+        shards[0].rc = run_shard(S, shards[0], one);
+        if (shards[0].rc) shards[0].err = tfbs_last_error();
+    } else {  // several: each batch's output to the ordered writer
+        Ordered ord(n_batches);
+        struct Many {
+            bool device_rows;
+            const RunSetup &S;
+            Ordered &ord;
+            uint32_t threads;
+            int operator()(size_t g, tfbs_ctx *ctx, tfbs_batch *bb) {
+                const size_t n = bb->b.rh.size();
+                Ordered::Item it;
+                if (device_rows) {  // BGZF blocks into a memory file; the POS base from the chain
+                    it.fd = memfd_create("tfbs_rows", MFD_CLOEXEC);
+                    if (it.fd < 0) return tfbs::fail(TFBS_E_IO, std::string("memfd_create: ") + strerror(errno));
+                    uint32_t fk = 0;
+                    const int rc = tfbs::rows_bgzf_chained(
+                        ctx, bb, 0, n, S.chrom.c_str(), S.a->min_maf, &fk, it.fd, nullptr, nullptr,
+                        [&](uint64_t rows, uint32_t *base) { return ord.chain(g, rows, base); });
+                    if (rc) {
+                        close(it.fd);
+                        return rc;
+                    }
+                } else if (int rc = tfbs::batch_row_bodies(bb->b, S.a->min_maf, it.bodies, threads)) {
+                    return rc;
+                }
+                ord.submit(g, std::move(it));
+                return TFBS_OK;
+            }
         };
-        auto put_blocks = [&]() { return w.raw_fd(); };
-        sh.rc = n_sh == 1 && gpu_bgzf ? run_shard(S, sh, emit, &put_blocks, &fake)
-                                      : run_shard(S, sh, emit, (decltype(put_blocks) *)nullptr, &fake);
-        if (sh.rc) sh.err = tfbs_last_error();
-    };
-    {
+        std::thread writer([&] {  // batches in order: blocks copied, bodies prefixed with POS and deflated
+            const int out_fd = gpu_bgzf ? w.raw_fd() : 0;
+            if (out_fd < 0) {
+                ord.abort(out_fd, tfbs_last_error());
+                return;
+            }
+            for (size_t g = 0; g < n_batches; g++) {
+                Ordered::Item it;
+                if (!ord.take(g, it)) return;
+                const double t0 = now();
+                int rc;
+                if (it.fd >= 0) {
+                    rc = copy_fd(it.fd, out_fd);
+                    close(it.fd);
+                } else {
+                    rc = write_prefixed(w, chr, it.bodies.data(), it.bodies.size(), &fake);
+                }
+                t_write += now() - t0;
+                if (rc) {
+                    ord.abort(rc, tfbs_last_error());
+                    return;
+                }
+            }
+        });
+        auto run_one = [&](size_t k) {
+            Many m{gpu_bgzf, S, ord, shards[k].threads};
+            shards[k].rc = run_shard(S, shards[k], m);
+            if (shards[k].rc) {
+                shards[k].err = tfbs_last_error();
+                ord.abort(shards[k].rc, shards[k].err);
+            }
+        };
         std::vector<std::thread> ts;
         for (size_t k = 1; k < n_sh; k++) ts.emplace_back(run_one, k);
         run_one(0);
         for (auto &t : ts) t.join();
+        writer.join();
+        {  // memory files a failed run left behind
+            std::lock_guard<std::mutex> l(ord.mu);
+            for (auto &it : ord.items)
+                if (it.fd >= 0) close(it.fd);
+        }
+        if (ord.failed) return fail(ord.first_rc, ord.first_err);
     }
     for (auto &sh : shards)
         if (sh.rc) return fail(sh.rc, sh.err);
-    double t_cat = now();
-    {
-        std::vector<char> buf(16u << 20);
-        std::string carry;
-        for (size_t k = 1; k < n_sh; k++) {
-            if (fflush(spill[k]) != 0 || fseek(spill[k], 0, SEEK_SET) != 0)
-                return fail(TFBS_E_IO, "read failed: " + spill_path[k]);
-            carry.clear();
-            for (size_t got; (got = fread(buf.data(), 1, buf.size(), spill[k])) > 0;) {
-                carry.append(buf.data(), got);
-                const size_t cut = carry.rfind('\n');
-                if (cut == std::string::npos) continue;
-                if ((rc = write_prefixed(w, chr, carry.data(), cut + 1, &fake))) return rc;
-                carry.erase(0, cut + 1);
-            }
-            if (!carry.empty() && (rc = write_prefixed(w, chr, carry.data(), carry.size(), &fake))) return rc;
-        }
-    }
-    t_cat = now() - t_cat;
     // the reference flushes twice before drop (main.rs:271, 275): two empty blocks
     double t0 = now();
     if ((rc = w.flush()) || (rc = w.flush()) || (rc = w.close())) return rc;
@@ -426,11 +536,11 @@ int tfbs_run(const tfbs_run_args *a) {
     if (timing)
         for (size_t k = 0; k < n_sh; k++)
             fprintf(stderr,
-                    "tfbs_run_timing {\"shard\": %zu, \"device\": %d, \"regions\": %zu, \"prep_s\": %.4f, "
-                    "\"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, \"write_s\": %.4f, \"concat_s\": %.4f, "
-                    "\"close_s\": %.4f, \"loop_s\": %.4f}\n",
-                    k, shards[k].device, shards[k].r1 - shards[k].r0, shards[k].t_prep, shards[k].t_wait,
-                    shards[k].t_gpu, shards[k].t_rows, shards[k].t_emit, t_cat, t_close, now() - t_start);
+                    "tfbs_run_timing {\"shard\": %zu, \"device\": %d, \"regions\": %zu, \"batches\": %zu, "
+                    "\"prep_s\": %.4f, \"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, "
+                    "\"ordered_write_s\": %.4f, \"close_s\": %.4f, \"loop_s\": %.4f}\n",
+                    k, shards[k].device, shards[k].regions, shards[k].batches.size(), shards[k].t_prep,
+                    shards[k].t_wait, shards[k].t_gpu, shards[k].t_rows, t_write, t_close, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +
                                 part + "'";

@@ -65,6 +65,10 @@ struct ScanArgs {
     // (strand, window) are listed per region (ref_count[r] of kRefPerRegion at
     // ref_hits + 2 kRefPerRegion r), the excess in the spill list
     uint32_t dedup;
+    // HAP_DEDUP haplotypes' diff runs: a hit of one in a window whose strand columns
+    // [i, i + L - 1] meet no run is the reference's (the key assembly adds it), so
+    // the rescoring does not list it
+    const uint32_t *druns;
     uint32_t n_regions;
     uint32_t *ref_hits;
     uint32_t *ref_count;

@@ -211,7 +211,10 @@ __device__ __forceinline__ void spill_record(const ScanArgs &A, uint32_t head, u
 }
 
 // Exact rescoring of one candidate: window i of haplotype hp (hits index hap)
-// for the strand g = global tile * 64 + strand in tile.  Returns the hit's
+// for the strand g = global tile * 64 + strand in tile.  A HAP_DEDUP haplotype's
+// window read because it meets a diff run within the class span, but whose strand
+// columns [i, i + L) meet none, is the reference's window for that strand: not
+// listed (the key assembly adds the reference's hit, tfbs_internal.hpp).  Returns the hit's
 // inner ranges k < 32 (bit k; key = *key0 + k) to be listed by the caller;
 // ranges past 32 go to the spill list here.  A hit of the region's reference
 // haplotype is also listed for the reuse of its window by the HAP_DEDUP
@@ -236,6 +239,12 @@ __device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uin
     if (i + L > hp.len) return 0;                       // past the end (pattern.rs:147-150)
     const int32_t sc = exact_score(words, hp, i, L, A.mweights + sf.y, live);
     if (!(sc > sf.x)) return 0;                         // strict (pattern.rs:151)
+    if ((hp.flags & HAP_DEDUP) && A.dedup) {  // columns [i, i + L) the reference's: its hit (key assembly)
+        bool dirty = false;
+        for (uint32_t k = hp.drun_off; k < hp.drun_off + hp.n_druns && !dirty; k++)
+            dirty = run_meets(A.druns[2 * k], A.druns[2 * k + 1], i, L);
+        if (!dirty) return 0;
+    }
     if (A.hits && i / 64 < A.hits_wpp)
         atomicOr(A.hits + ((size_t)hap * A.n_patterns_total + (uint32_t)meta[kGOrig + sn]) * A.hits_wpp + i / 64,
                  1ull << (i & 63));

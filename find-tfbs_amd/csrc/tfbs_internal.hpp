@@ -138,12 +138,13 @@ constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 
 // haplotype of at most kDedupMaxWindows bases whose columns differing from the
 // reference's -- another base or N, another position (past an indel), past the
 // end of either sequence -- form at most kMaxDiffRuns runs (diff runs [a, b],
-// inclusive, ascending, at DevHap::drun_off of the batch's run array).  For a
-// depth class of span S = 8 nk columns, window i is *dirty* iff some run meets
-// [i, i + S - 1]; the matrix-core scan reads only the dirty windows of a
-// HAP_DEDUP haplotype (its window list, scan_mfma.hip), every other window has
-// the reference window's bases and positions, so its hits are the reference's,
-// which the key assembly adds (key_kernels.hip, same predicate).
+// inclusive, ascending, at DevHap::drun_off of the batch's run array).  Window i
+// of a strand of length L is *dirty* iff some run meets its columns [i, i + L -
+// 1]; every other window has the reference window's bases and positions, so its
+// hit (or none) is the reference's, which the key assembly adds
+// (key_kernels.hip).  The matrix-core scan reads the windows dirty for the span
+// S = 8 nk of their depth class (S >= L: a superset; the window list,
+// scan_mfma.hip) and lists only the hits of windows dirty for the strand's L.
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
 constexpr uint32_t kDedupMaxWindows = 1024;  // longest HAP_DEDUP haplotype (and reference)
 constexpr uint32_t kMaxDiffRuns = 16;        // diff runs of a HAP_DEDUP haplotype
@@ -162,8 +163,8 @@ struct DevHap {
     uint32_t pad[2];
 };
 
-// Window w of a class of span S is dirty for a haplotype with diff runs r
-// (HAP_DEDUP): some run meets the window's columns [w, w + S - 1].
+// Window w of span S (a strand's L, or a depth class's 8 nk) is dirty for a
+// haplotype with diff runs r (HAP_DEDUP): some run meets its columns [w, w + S - 1].
 inline constexpr bool run_meets(uint32_t a, uint32_t b, uint32_t w, uint32_t S) { return a <= w + S - 1 && b >= w; }
 
 struct DevRegion {

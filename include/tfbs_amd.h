@@ -252,6 +252,21 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
  * makes that copy itself before it reduces another batch or is destroyed.  The
  * key / row functions below then work as after a download. */
 int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
+/* The device half of tfbs_batch_reduce, enqueued behind tfbs_scan with no host
+ * wait (main.rs:94-154's per-region result + count_matches_by_sample's key
+ * vectors, main.rs:500-534): candidates past the scan's lists rescored, spill
+ * records bucketed, every region's keys assembled from its hit lists -- each
+ * HAP_DEDUP haplotype's count is the reference haplotype's plus its own hits
+ * minus the reference hits inside its dirty windows -- classified, and the
+ * varying keys' counts compacted on the device.  tfbs_batch_assemble_wait
+ * waits for it and checks every list (a scan list that overflowed is rescanned
+ * larger, a full varying-key list reassembled); tfbs_batch_reduce then only
+ * downloads.  One step of scan + assembly = tfbs_scan, tfbs_batch_assemble,
+ * tfbs_batch_assemble_wait. */
+int tfbs_batch_assemble(tfbs_ctx *ctx, tfbs_batch *b);
+int tfbs_batch_assemble_wait(tfbs_ctx *ctx, tfbs_batch *b);
+/* Device time (ms, HIP events on the ctx stream) of the last assembly, -1 if none ran. */
+float tfbs_ctx_last_assemble_ms(const tfbs_ctx *ctx);
 /* counts_as_genotypes' per-sample half on the device (main.rs:439-534, SURVEY.md
  * 8(f) f1) for the varying keys of regions [r0, r1) after tfbs_batch_reduce:
  * per key v[s] = C[hap(2s)] + C[hap(2s+1)] over the samples, min / max, the

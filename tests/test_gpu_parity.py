@@ -328,15 +328,28 @@ def test_dense_hits_vs_oracle(tmp_path, monkeypatch, thr):
     assert b.num_haplotypes > n_regions
 
 
-@pytest.mark.parametrize("thr", [1e-3, 0.05])
-def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr):
+@pytest.mark.parametrize("thr,fast_max_u,cor", [(1e-3, None, None), (0.05, None, None), (1e-3, "0", None),
+                                                (0.05, "40", None), (0.05, None, ("0", None)),
+                                                (1e-3, None, ("16", "200"))])
+def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr, fast_max_u, cor):
     """Reference-window reuse (HAP_DEDUP, ref_fixup_kernel) on its edge cases, against
     the oracle: an SNV every haplotype carries (no reference group: the helper copy of
     the reference supplies the hits), N runs in the reference, haplotypes with indels
     (reused before the first indel, scanned after it), 40 nested inner ranges (the fix-up's path past 32 ranges) and
     p = 0.05 thresholds (over 64 reference hits per region: the overflow list; with
-    small candidate lists, the candidate overflow list and its regrowth)."""
+    small candidate lists, the candidate overflow list and its regrowth).  fast_max_u:
+    regions of more distinct haplotypes than that leave key_fast_kernel for the list
+    pass of key_asm_kernel (0: every region; 40: some -- both kernels in one reduction);
+    the region with 40 inner ranges always takes that pass.  cor: key_fast_kernel's
+    corrections in its global arena instead of LDS (every region, or past 16 entries
+    with an arena of 200 that fills: those regions go to key_asm_kernel)."""
     monkeypatch.setenv("TFBS_MFMA", "1")
+    if fast_max_u is not None:
+        monkeypatch.setenv("TFBS_KEY_FAST_MAXU", fast_max_u)
+    if cor is not None:
+        monkeypatch.setenv("TFBS_KEY_COR_LDS", cor[0])
+        if cor[1] is not None:
+            monkeypatch.setenv("TFBS_KEY_COR_CAP", cor[1])
     ps, _ = synth_patterns(tmp_path, 10, 3, 71, thr=thr)
     n_samples, n_regions = 60, 6
     H = 2 * n_samples
