@@ -581,8 +581,8 @@ def run(chromosome, bcf, bed_files, reference_genome_file, wanted_samples, pwm_f
         pwm_threshold, wanted_pwms, output_file, forward_only=False, run_tabix=False, min_maf=0, threads=1,
         after_position=0, verbose=False, device=0, regions_per_batch=0, devices=None):
     """main.rs:234-393 `run` with the reference's argument order; writes the BGZF VCF.
-    devices: list of HIP devices, one contiguous block of merged regions each (same text
-    for any list; a device may repeat)."""
+    devices: list of HIP devices; batch g of merged regions runs on devices[g % n] (same
+    text for any list; a device may repeat)."""
     a = _capi.tfbs_run_args()
     keep = [_u(x) if x is not None else None for x in (chromosome, bcf, ",".join(bed_files), reference_genome_file,
                                                         wanted_samples, pwm_file, pwm_threshold_directory,

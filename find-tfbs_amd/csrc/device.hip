@@ -846,6 +846,22 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
         const uint32_t nspill = ctx->asm_host[0], ncand = ctx->asm_host[1];
         const uint64_t *vt = reinterpret_cast<const uint64_t *>(ctx->asm_host + 4);
         const uint64_t nk = vt[0], nc = vt[1];
+        if (ctx->debug_over && ctx->asm_host[2]) {  // the regions left to key_asm_kernel: their shapes
+            std::vector<uint32_t> redo(ctx->asm_host[2]);
+            HIP_TRY(hipMemcpy(redo.data(), ctx->asm_redo.p + 1, redo.size() * 4, hipMemcpyDeviceToHost));
+            uint64_t su = 0, sr = 0;
+            uint32_t mu = 0, mi = 0;
+            for (uint32_t r : redo) {
+                const DevRegion &rg = B.regions[r];
+                su += rg.hap_count;
+                mu = std::max(mu, rg.hap_count);
+                mi = std::max(mi, rg.n_inner);
+                for (uint32_t l = 0; l < rg.hap_count; l++) sr += B.haps[rg.hap_begin + l].n_druns;
+            }
+            fprintf(stderr, "tfbs assembly: %zu regions left to key_asm: mean haplotypes %.1f (max %u), max inner %u, "
+                            "mean diff runs %.1f\n", redo.size(), (double)su / redo.size(), mu, mi,
+                    (double)sr / redo.size());
+        }
         if (ctx->debug_over)
             fprintf(stderr, "tfbs assembly: spill %u/%u candidates %u/%u left to key_asm %u arena %u/%u varying keys "
                             "%llu/%u counts %llu/%llu\n", nspill, ctx->spill_cap, ncand, ctx->cand_over_cap,
@@ -1240,7 +1256,9 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.crc_ops = ctx->bg_crc.p + 256;
     a.crc_ops64 = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
     if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
-    constexpr uint64_t kBatchBlocks = 8192;  // 512 MiB of block slots per launch
+    // blocks per launch (512 MiB of block slots); TFBS_BGZF_BATCH_BLOCKS=n: smaller
+    // launches, so one call cycles the kBgSlots slots (the tests' path)
+    const uint64_t kBatchBlocks = (uint64_t)std::max(1, env_int("TFBS_BGZF_BATCH_BLOCKS", 8192));
     const uint64_t n_batches = (n_blocks + kBatchBlocks - 1) / kBatchBlocks;
     if (!ctx->bg_total_host)
         HIP_TRY(hipHostMalloc((void **)&ctx->bg_total_host, 8 * tfbs_ctx::kBgSlots, hipHostMallocDefault));

@@ -423,22 +423,27 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
 // left to key_asm_kernel.
 constexpr int kFBlock = 256;
 constexpr uint32_t kFWaves = kFBlock / 64;
-constexpr uint32_t kFMaxU = 1024;     // distinct haplotypes (10 bits of a correction)
-constexpr uint32_t kFCor = 3072;      // corrections: own hits and dirty reference hits
+constexpr uint32_t kFMaxU = 2048;     // distinct haplotypes (11 bits of a correction)
+constexpr uint32_t kFHapLds = 1024;   // haplotypes whose reuse descriptor sits in LDS (the others: read again)
+constexpr uint32_t kFCor = 4096;      // corrections in LDS: own hits and dirty reference hits
 constexpr uint32_t kFRefs = 256;      // reference hits
-constexpr uint32_t kFRuns = 512;      // diff runs of the region's HAP_DEDUP haplotypes
 constexpr uint32_t kFCnt = 4096;      // u32 counters of a chunk: rows x U
+constexpr uint32_t kFRuns = kFCnt / 2;  // diff runs of the region's HAP_DEDUP haplotypes staged (over the counters)
 constexpr uint32_t kFRows = 512;      // rows (touched keys) per chunk
 constexpr uint32_t kFKeyWords = 512;  // touched-key bitmap: keys <= 16384
 constexpr uint32_t kFLists = 256;     // scan hit lists over the region's haplotypes
 constexpr uint32_t kFNone = 0xFFFFFFFFu;
-static_assert(kFMaxU % kFBlock == 0 && kFKeyWords % kFBlock == 0 && kFLists <= kFBlock && kFRefs <= kFBlock,
+static_assert(kFMaxU % kFBlock == 0 && kFHapLds % kFBlock == 0 && kFKeyWords % kFBlock == 0 && kFLists <= kFBlock &&
+                  kFRefs <= kFBlock,
               "key_fast_kernel's per-thread shares");
 
-// correction: key << 11 | (-1) << 10 | local haplotype
+// correction: key << 12 | (-1) << 11 | local haplotype (key < 2^20)
 __device__ __forceinline__ uint32_t cor_entry(uint32_t key, uint32_t l, uint32_t neg) {
-    return (key << 11) | (neg << 10) | l;
+    return (key << 12) | (neg << 11) | l;
 }
+__device__ __forceinline__ uint32_t cor_key(uint32_t c) { return c >> 12; }
+__device__ __forceinline__ bool cor_neg(uint32_t c) { return (c >> 11) & 1u; }
+__device__ __forceinline__ uint32_t cor_hap(uint32_t c) { return c & 2047u; }
 
 // Appends v from the wave's lanes with want set, in lane order (one LDS atomic
 // per wave); *n counts every attempt (> cap: overflow).
@@ -481,9 +486,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     __shared__ uint32_t s_cor[kFCor];
     __shared__ uint4 s_ref[kFRefs];          // make_ref, sorted by window
-    __shared__ uint2 s_run[kFRuns];
-    __shared__ uint32_t s_hap[kFMaxU];       // HAP_DEDUP: its first run in s_run | runs << 16; else kFNone
-    __shared__ uint32_t s_cnt[kFCnt];
+    __shared__ uint32_t s_hap[kFHapLds];     // HAP_DEDUP: its first run (from the region's first) | runs << 16; else kFNone
+    __shared__ uint32_t s_cnt[kFCnt];        // the counters; before them the diff runs (s_run)
+    uint2 *const s_run = reinterpret_cast<uint2 *>(s_cnt);
     __shared__ uint32_t s_bits[kFKeyWords], s_rbase[kFKeyWords];
     __shared__ uint32_t s_rkey[kFRows], s_rr[kFRows];  // per row of a chunk: its key; R(key), then its varying slot
     __shared__ uint32_t s_loff[kFLists + 1], s_lidx[kFLists];
@@ -565,14 +570,22 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     if (tid < nl) s_loff[tid] = loff;
     if (tid == 0) s_loff[nl] = n_ent;
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
-    if (nruns > kFRuns) return give_up();
+    if (nruns >= 65536) return give_up();
 #pragma unroll
-    for (uint32_t q = 0; q < kPer; q++) {
+    for (uint32_t q = 0; q < kFHapLds / kFBlock; q++) {
         const uint32_t l = tid + q * kFBlock;
         if (l < U) s_hap[l] = roff[q] == kFNone ? kFNone : (roff[q] - run0) | (rn[q] << 16);
     }
-    for (uint32_t k = tid; k < nruns; k += kFBlock)
-        s_run[k] = make_uint2(A.druns[2 * (run0 + k)], A.druns[2 * (run0 + k) + 1]);
+    auto hap_info = [&](uint32_t l) -> uint32_t {  // s_hap's entry of any haplotype
+        if (l < kFHapLds) return s_hap[l];
+        const DevHap &h = A.haps[hb + l];
+        return (h.flags & HAP_DEDUP) ? (h.drun_off - run0) | (h.n_druns << 16) : kFNone;
+    };
+    // the runs in LDS when they fit, else read from global memory (L2)
+    const uint2 *const runs = nruns <= kFRuns ? s_run : reinterpret_cast<const uint2 *>(A.druns) + run0;
+    if (nruns <= kFRuns)
+        for (uint32_t k = tid; k < nruns; k += kFBlock)
+            s_run[k] = make_uint2(A.druns[2 * (run0 + k)], A.druns[2 * (run0 + k) + 1]);
     // reference hits: the region's list, then its spill records of kind 1
     const uint2 sp = spill_range(A, r);
     if (refs_on) {
@@ -614,19 +627,19 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     auto each_dirty = [&](auto &&f) {
         if (!nref) return;
         for (uint32_t l = tid; l < U; l += kFBlock) {
-            const uint32_t x = s_hap[l];
+            const uint32_t x = hap_info(l);
             if (x == kFNone) continue;
             const uint32_t k0 = x & 0xFFFFu, k1 = k0 + (x >> 16);
             uint32_t p = 0;
             for (uint32_t k = k0; k < k1 && p < nref; k++) {
-                const uint32_t a = s_run[k].x, b = s_run[k].y;
+                const uint32_t a = runs[k].x, b = runs[k].y;
                 const uint32_t lo = a >= kMChunkCols * kMMaxChunks - 1 ? a - (kMChunkCols * kMMaxChunks - 1) : 0u;
                 while (p < nref && s_ref[p].y < lo) p++;
                 for (; p < nref && s_ref[p].y <= b; p++) {
                     const uint4 q = s_ref[p];
                     bool dirty = false;
                     for (uint32_t k2 = k0; k2 < k1 && !dirty; k2++)
-                        dirty = run_meets(s_run[k2].x, s_run[k2].y, q.y, q.z & 0xFFFFu);
+                        dirty = run_meets(runs[k2].x, runs[k2].y, q.y, q.z & 0xFFFFu);
                     if (dirty) f(l, q);
                 }
             }
@@ -694,7 +707,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     // reference hits, every key of a LUT/generic slot; rows in key order
     for (uint32_t e = tid; e < ncor; e += kFBlock) {
         const uint32_t c = cor[e];
-        if (!((c >> 10) & 1u)) atomicOr(&s_bits[c >> 16], 1u << ((c >> 11) & 31u));
+        if (!cor_neg(c)) atomicOr(&s_bits[cor_key(c) >> 5], 1u << (cor_key(c) & 31u));
     }
     if (tid < nref)
         for (uint32_t m = s_ref[tid].w; m; m &= m - 1) {
@@ -725,13 +738,28 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         }
     }
     auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
+    // the counter block: LDS chunks of rows x U, or -- when that would take more than
+    // 4 chunks (many haplotypes and keys), each re-reading every correction --
+    // chunks of kFRows rows in a share of the arena (global atomics)
+    uint32_t rows_per = min(kFCnt / U, kFRows);
+    uint32_t *cnt = s_cnt;
+    if ((T + rows_per - 1) / rows_per > 4 || A.cor_lds == 0) {  // (cor_lds 0: the tests' all-global path)
+        rows_per = min(T, kFRows);
+        if (tid == 0) {
+            s_arena = kFNone;
+            const uint32_t want = rows_per * U, at = atomicAdd(A.cor_used, want);
+            if (at <= A.cor_cap && want <= A.cor_cap - at) s_arena = at;
+        }
+        __syncthreads();
+        if (s_arena == kFNone) return give_up();  // the host grows the arena for the next call
+        cnt = A.cor_arena + s_arena;
+    }
     // untouched keys: no match -- no key in the reference's HashMap
     for (uint32_t j = tid; j < K; j += kFBlock)
         if (!((s_bits[j >> 5] >> (j & 31)) & 1u)) {
             A.key_first[ko + j] = 0;
             A.key_flags[ko + j] = 0;
         }
-    const uint32_t rows_per = min(kFCnt / U, kFRows);
     const uint64_t dense_base = A.dense_base ? A.haps[hb].count_off : 0;
     for (uint32_t t0 = 0; t0 < T; t0 += rows_per) {
         const uint32_t nrow = min(rows_per, T - t0);
@@ -761,19 +789,19 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             const uint32_t j = s_rkey[rr], R = s_rr[rr];
             const bool dense = A.any_dense && !A.slot_mfma[j / n_inner];
             for (uint32_t l = lane; l < U; l += 64)
-                s_cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
-                                          : (s_hap[l] != kFNone ? R : 0u);
+                cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
+                                        : (hap_info(l) != kFNone ? R : 0u);
         }
         __syncthreads();
         for (uint32_t e = tid; e < ncor; e += kFBlock) {
             const uint32_t c = cor[e];
-            const uint32_t t = row_of(c >> 11) - t0;
-            if (t < nrow) atomicAdd(&s_cnt[t * U + (c & 1023u)], ((c >> 10) & 1u) ? 0xFFFFFFFFu : 1u);
+            const uint32_t t = row_of(cor_key(c)) - t0;
+            if (t < nrow) atomicAdd(&cnt[t * U + cor_hap(c)], cor_neg(c) ? 0xFFFFFFFFu : 1u);
         }
         __syncthreads();
         // classify: one wave per row
         for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {
-            const uint32_t *col = s_cnt + rr * U;
+            const uint32_t *col = cnt + rr * U;
             const uint32_t c0 = col[0];
             uint32_t any = 0, diff = 0;
             for (uint32_t l = lane; l < U; l += 64) {
@@ -801,7 +829,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             const uint64_t vi = s_vbase + slot, off = s_obase + (uint64_t)slot * U;
             if (vi >= A.var_keys_cap || off + U > A.var_cap) continue;  // the host grows the lists and reruns
             if (lane == 0) A.var_keys[vi] = DevVarKey{r, s_rkey[rr], off};
-            for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = s_cnt[rr * U + l];
+            for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = cnt[rr * U + l];
         }
     }
 }

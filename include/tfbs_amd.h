@@ -187,10 +187,10 @@ int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax);
  * records are all SNVs inside its window (REF = the window's base, ALT another of
  * A/C/G/T, at most 64, one per position, carrier ids ascending) and whose window
  * has no N gets its haplotypes' diff masks, distinct groups and membership
- * computed there (the membership stays on the device, one byte per haplotype id,
- * fetched only when a host path needs it); every other region, and one of more
- * than 254 distinct groups, is built on the host.  The batch is the same either
- * way (tfbs_batch_region_input_digest). */
+ * computed there (the membership stays on the device, a u16 distinct index per
+ * haplotype id, fetched only when a host path needs it); every other region, and
+ * one of more than 2 047 distinct diff masks, is built on the host.  The batch is
+ * the same either way (tfbs_batch_region_input_digest). */
 int tfbs_batch_set_build_device(tfbs_batch *b, int device);
 /* Regions grouped on the device / built on the host so far. */
 int tfbs_batch_build_stats(const tfbs_batch *b, uint64_t *dev_regions, uint64_t *host_regions);
@@ -235,10 +235,14 @@ uint64_t tfbs_batch_output_bytes(const tfbs_batch *b);
 
 /* Copies the packed batch into ctx device memory (H2D). */
 int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b);
-/* Scans the uploaded batch on the GPU: per (distinct haplotype, pattern_id,
- * inner range) hit counts, strands summed (the work of matches() over every
- * distinct haplotype, main.rs:101-147, plus the overlap test of main.rs:503).
- * Asynchronous on the ctx stream; tfbs_batch_download waits. */
+/* Scans the uploaded batch on the GPU (the work of matches() over every distinct
+ * haplotype, main.rs:101-147, plus the overlap test of main.rs:503): sparse hit
+ * lists -- one (distinct haplotype, pattern_id slot x inner range) entry per hit
+ * and overlapped range from the matrix-core kernel, the region's reference
+ * haplotype's hits listed for reference-window reuse -- and, for strands the
+ * LUT / generic kernels score, dense counts.  Asynchronous on the ctx stream;
+ * tfbs_batch_assemble / tfbs_batch_reduce / tfbs_batch_download turn the lists
+ * into per-key counts. */
 int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b);
 /* D2H copy of the counts into the batch. */
 int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b);
@@ -370,13 +374,15 @@ typedef struct tfbs_run_args {
                                       a device may repeat); NULL/"" = just `device` */
 } tfbs_run_args;
 /* Replaces run() (main.rs:234-393): writes <output>.part, renames it to output.
- * Several devices: the merged regions are cut into one
- * contiguous block per device (the reference's 50-peak chunks over worker
- * threads, main.rs:332-381, made static); each block runs its own pipeline
- * (BCF reader -- CSI-indexed seek when <bcf>.csi exists --, FASTA reader,
- * host prep thread, ctx on its device, row formatting) and the rows are
- * concatenated in merged-peak order with POS renumbered, so the output text
- * is identical for any device list. */
+ * The merged regions go in batches of regions_per_batch (the reference's 50-peak
+ * chunks over worker threads, main.rs:332-381); each batch is built (BCF records,
+ * load_diffs; SNV-only regions grouped on the GPU), scanned, reduced, encoded and
+ * its rows made as BGZF blocks on the device.  Several devices:
+ * batch g runs on device g % n, each device with its own pipeline (BCF reader --
+ * CSI-indexed seek when <bcf>.csi exists --, FASTA reader, host prep thread,
+ * ctx); batch g's first POS is batch g - 1's plus its row count (published before
+ * either deflates) and the batches' blocks are written in order, so the output
+ * text is identical for any device list. */
 int tfbs_run(const tfbs_run_args *args);
 
 typedef struct tfbs_bcf tfbs_bcf;

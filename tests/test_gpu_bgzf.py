@@ -116,3 +116,22 @@ def test_bgzf_c3_regions_vs_host_rows(tmp_path):
         sc.close()
     assert got == want
     assert len(data) * 8 < len(want)
+
+
+@pytest.mark.parametrize("batch_blocks", [None, "2"])
+def test_bgzf_many_pieces_one_call(tmp_path, monkeypatch, batch_blocks):
+    """One call over 640 regions (the run flow's batches are 512): 8 pieces, the host
+    row plan of piece j + 1 built on the helper thread into kBgSlots + 1 plan slots
+    while the GPU deflates piece j; with 2 blocks per launch the call launches many
+    batches, cycling the 3 block slots (each reused after its copy back,
+    hipStreamWaitEvent on bg_copied).  Inflated == the host rows."""
+    if batch_blocks:
+        monkeypatch.setenv("TFBS_BGZF_BATCH_BLOCKS", batch_blocks)
+    ps, _ = synth_patterns(tmp_path, 40, 2, 105, thr=2e-3)
+    n_regions, n_samples = 640, 600
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
+    regions = make_regions_synth(15, 0, n_regions, n_samples, ps.max_length, 10)
+    want, data = _compare(ps, n_samples, beds, regions)
+    blocks = _members(data)
+    assert len(blocks) > 3 * 2 * 3  # several launches per slot when batch_blocks is 2
+    assert want.count("\n") > 500

@@ -187,18 +187,24 @@ def _digests(b):
     return [b.digest(r) for r in range(b.num_regions)]
 
 
-def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0):
+def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0, build_device=None):
     """n_check regions spread over the batch (all of them if n_check >= its size), the
     n_top regions with the most distinct haplotypes and the n_top with the most
     variant records, and the n_extra_n regions with N runs, against the oracle:
     key by key and row by row on a 100-region subset, by xxh3 digests of the same
     (count_matches_by_sample vectors of every key after the key reduction, row
-    text after the device encoding) on all of them."""
+    text after the device encoding) on all of them.  build_device: the batch is
+    grouped there as bench.py builds it (SNV-only regions' haplotypes grouped on
+    the GPU); the 100-region subset's rows are then also made as BGZF blocks on
+    the device (tfbs_batch_rows_bgzf), inflated and compared with the oracle's."""
     n_samples, n_regions, _, _, indel, seed = cfg
     ps = _patterns(tmp_path, cfg)
     lmax = ps.max_length
-    b = T.RegionBatch(ps, n_samples)
+    b = T.RegionBatch(ps, n_samples, build_device=build_device)
     b.synth_fill(seed, 0, n_regions, indel)
+    if build_device is not None:
+        dev_regions, _ = b.build_stats()
+        assert dev_regions > n_regions // 2, dev_regions
     extra = _n_regions(seed, n_regions, n_extra_n, n_samples, lmax, indel) if n_extra_n else []
     _append_regions(b, extra)
     assert b.num_regions == n_regions + n_extra_n
@@ -224,13 +230,22 @@ def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0):
         _check_vs_oracle(b, dig, "reduce", digest=True, rows=False)
         # the device per-sample encoding (f1) the run flow formats rows from, 2 000
         # regions at a time: every checked region's rows
-        n_enc = n_rows = 0
+        n_enc = n_rows = n_bgzf = 0
         for r0 in range(0, b.num_regions, 2000):
             r1 = min(b.num_regions, r0 + 2000)
             b.encode(sc, r0, r1)
             n_enc += _check_vs_oracle(b, {i: ref[i] for i in ref if r0 <= i < r1}, "encode", keys=False)
             n_rows += _check_vs_oracle(b, {i: dig[i] for i in dig if r0 <= i < r1}, "encode", digest=True, keys=False)
+            if build_device is not None:  # the device BGZF writer's rows of the subset vs the oracle's
+                import gzip
+                for i in sorted(x for x in ref if r0 <= x < r1):
+                    data, _, nr, _ = b.rows_bgzf(sc, "chr1", 0, 1, i, i + 1)
+                    got = _strip_pos(gzip.decompress(data).decode()) if data else []
+                    assert got == ref[i][1], ("bgzf", i)
+                    n_bgzf += nr
         assert n_enc == n_full
+        if build_device is not None:
+            assert n_bgzf == n_full
         n_rows += n_enc
         # dense download over the same batch, rescanned
         b.scan(sc, upload=False, download=True)
@@ -249,8 +264,10 @@ def test_c2_full_vs_oracle(tmp_path):
 
 def test_c3_full_batch_vs_oracle(tmp_path):
     """C3 as bench.py times it (50 000 samples, 10 000 regions, 600 PWMs = 1 200 strands,
-    ~1.18 M distinct haplotypes, one batch), plus 6 regions with N runs at its end."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C3, 1000, n_extra_n=6, n_top=50)
+    ~1.18 M distinct haplotypes, one batch, SNV-only regions grouped on the GPU), plus
+    6 regions with N runs at its end (built on the host); the device BGZF rows of the
+    100-region subset against the oracle's."""
+    b, n_rows, n_checked = _fullsize(tmp_path, C3, 1000, n_extra_n=6, n_top=50, build_device=0)
     assert n_checked >= 1000 and n_rows > 0
     assert b.num_haplotypes > 1_000_000
 
@@ -258,7 +275,7 @@ def test_c3_full_batch_vs_oracle(tmp_path):
 def test_c5_full_batch_vs_oracle(tmp_path):
     """C5: C3 with 30 % indels (non-affine positions, variable-length haplotypes) and
     PWMs of length 25-30 (K depth 2 of the matrix-core kernel)."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C5, 1000, n_extra_n=4, n_top=50)
+    b, n_rows, n_checked = _fullsize(tmp_path, C5, 1000, n_extra_n=4, n_top=50, build_device=0)
     assert n_checked >= 1000 and n_rows > 0
 
 

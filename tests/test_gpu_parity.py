@@ -341,8 +341,9 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr, fast_max_u
     regions of more distinct haplotypes than that leave key_fast_kernel for the list
     pass of key_asm_kernel (0: every region; 40: some -- both kernels in one reduction);
     the region with 40 inner ranges always takes that pass.  cor: key_fast_kernel's
-    corrections in its global arena instead of LDS (every region, or past 16 entries
-    with an arena of 200 that fills: those regions go to key_asm_kernel)."""
+    corrections in its global arena instead of LDS (every region -- its counter
+    chunks too --, or past 16 entries with an arena of 200 that fills: those regions
+    go to key_asm_kernel)."""
     monkeypatch.setenv("TFBS_MFMA", "1")
     if fast_max_u is not None:
         monkeypatch.setenv("TFBS_KEY_FAST_MAXU", fast_max_u)
