@@ -464,6 +464,135 @@ static int snv_finish(const Batch &B, RegionBuilt &b, const uint64_t *masks, con
     return TFBS_OK;
 }
 
+// Device grouping for the other regions whose diff lists are masks (at most 64
+// applied records, all distinct diffs, carrier lists strictly ascending below 2 *
+// n_samples): the device finds the distinct masks in Vec<Diff> order, their
+// carrier counts and the membership (build_gpu.hip) -- load_diffs and
+// group_by_diffs over every haplotype id, the region's O(H x records) part -- and
+// the host patches only the distinct groups (haplotype.rs:77-88; mask_finish),
+// exactly as build_region's mask path does after its grouping.
+static bool mask_prepare(const Batch &B, const RegionInput &I, std::vector<const Record *> &uniq) {
+    const uint32_t H = 2 * B.n_samples;
+    uniq.clear();
+    for (const Record &r : I.recs) {
+        if (r.n_alleles != 2 || r.carriers.empty()) continue;  // not applied (haplotype.rs:28-31)
+        if (r.carriers.back() >= H) return false;
+        for (size_t i = 1; i < r.carriers.size(); i++)
+            if (r.carriers[i] <= r.carriers[i - 1]) return false;
+        uniq.push_back(&r);
+    }
+    if (uniq.size() > 64) return false;
+    std::stable_sort(uniq.begin(), uniq.end(), diff_less);
+    for (size_t i = 1; i < uniq.size(); i++)
+        if (diff_equal(uniq[i], uniq[i - 1])) return false;  // [d, d] lists: build_region's list path
+    return true;
+}
+
+// The device's groups of a mask_prepare region, patched (build_region's
+// load_haplotypes part: dedup by (nucs, pos), the later group wins, the loser's ids
+// join the reference group), then the reference group and the helper.  The
+// device's membership row (group rank per id, G for ids without a diff) is the
+// distinct index as it stands unless a group lost; then the row is fetched and
+// remapped here.
+static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const std::vector<const Record *> &uniq,
+                       const uint64_t *masks, const uint32_t *counts, uint32_t G, uint64_t memb) {
+    const uint32_t H = 2 * B.n_samples;
+    out = RegionBuilt();
+    out.R = I.R;
+    RegionH &R = out.R;
+    R.n_variants = (uint32_t)I.recs.size();
+    inner_keys(I.inner, R);
+    out.dev_grouped = true;
+    std::vector<Distinct> &dist = out.dist;
+    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    RefWindow ref{I.ref.data(), R.es, I.ref.size()};
+    std::vector<const Record *> diffs;
+    for (uint32_t g = 0; g < G; g++) {
+        diffs.clear();
+        for (uint64_t x = masks[g]; x; x &= x - 1) diffs.push_back(uniq[__builtin_ctzll(x)]);
+        Distinct d;
+        d.nuc.reserve(R.ee - R.es + 16);
+        d.pos.reserve(R.ee - R.es + 16);
+        if (int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos)) return rc;
+        d.group = (int32_t)g;
+        uint64_t h = 1469598103934665603ull;
+        for (size_t i = 0; i < d.nuc.size(); i++) {
+            h = (h ^ d.nuc[i]) * 1099511628211ull;
+            h = (h ^ (d.pos[i] - R.es)) * 1099511628211ull;
+        }
+        auto &bucket = by_hash[h];
+        bool replaced = false;
+        for (uint32_t idx : bucket)
+            if (dist[idx].nuc == d.nuc && dist[idx].pos == d.pos) {
+                dist[idx].group = (int32_t)g;  // HashMap::insert replaces the value
+                replaced = true;
+                break;
+            }
+        if (!replaced) {
+            bucket.push_back((uint32_t)dist.size());
+            dist.push_back(std::move(d));
+        }
+    }
+    std::vector<uint32_t> &carriers = out.carriers;
+    carriers.assign(dist.size(), 0);
+    uint64_t covered = 0;
+    for (uint32_t i = 0; i < dist.size(); i++) {
+        carriers[i] = counts[dist[i].group];
+        covered += carriers[i];
+    }
+    const bool lost = dist.size() != G;  // a group's sequence taken by a later group
+    R.ref_local = -1;
+    if (covered < H) {
+        Distinct d;
+        d.nuc = I.ref;
+        d.pos.resize(I.ref.size());
+        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.group = -1;
+        R.ref_local = (int32_t)dist.size();
+        dist.push_back(std::move(d));
+        carriers.push_back((uint32_t)(H - covered));
+    }
+    out.helper = false;
+    auto fits = [](size_t n) { return n <= kDedupMaxWindows; };
+    bool reusable = false;
+    for (const Distinct &d : dist) reusable = reusable || fits(d.nuc.size());
+    if (B.dedup && R.ref_local < 0 && reusable && fits(I.ref.size())) {
+        Distinct d;
+        d.nuc = I.ref;
+        d.pos.resize(I.ref.size());
+        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.group = -2;
+        dist.push_back(std::move(d));
+        carriers.push_back(0);
+        out.helper = true;
+    }
+    for (const Distinct &d : dist)
+        if (d.nuc.size() >= kMaxHapLen) return fail(TFBS_E_ARG, "haplotype longer than 2^26 - 1 bases");
+    R.nonref_id.clear();
+    R.nonref_local.clear();
+    if (!lost) {  // the device row holds the distinct indices (G = ref_local for ids without a diff)
+        R.memb_dev = memb;
+        R.memb_host = false;
+        return TFBS_OK;
+    }
+    R.memb_dev = 0;
+    R.memb_host = true;
+    if (!B.keep_membership) return TFBS_OK;
+    std::vector<uint32_t> local(G + 1, (uint32_t)R.ref_local);  // group rank -> distinct index
+    for (uint32_t i = 0; i < dist.size(); i++)
+        if (dist[i].group >= 0) local[dist[i].group] = i;
+    std::vector<uint16_t> row(H);
+    if (int rc = B.grouper->fetch(memb, H, row.data())) return rc;
+    for (uint32_t h = 0; h < H; h++) {
+        const uint32_t v = row[h] < G ? local[row[h]] : (uint32_t)R.ref_local;
+        if (v != (uint32_t)R.ref_local) {
+            R.nonref_id.push_back(h);
+            R.nonref_local.push_back(v);
+        }
+    }
+    return TFBS_OK;
+}
+
 int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std::vector<RegionBuilt> &built,
                   double *build_s) {
     const size_t n = ins.size();
@@ -490,9 +619,15 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
         work();
         for (auto &t : ts) t.join();
     };
+    // 1: SNV-only, grouped and patched from the masks; 3: grouped on the device,
+    // patched on the host (mask_finish); 2: device overflow -> build_region
     par(n, [&](size_t j) {
         if (dev && snv_prepare(B, ins[j], built[j], uniq[j])) {
             where[j] = 1;
+            return;
+        }
+        if (dev && B.dev_patch && mask_prepare(B, ins[j], uniq[j])) {
+            where[j] = 3;
             return;
         }
         rcs[j] = build_region(B, std::move(ins[j]), built[j]);
@@ -500,7 +635,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
     if (dev) {
         std::vector<size_t> dj;
         for (size_t j = 0; j < n; j++)
-            if (where[j] == 1) dj.push_back(j);
+            if (where[j] == 1 || where[j] == 3) dj.push_back(j);
         const uint32_t H = 2 * B.n_samples;
         // chunks: the masks scratch (8 bytes per haplotype id and region) within 1 GiB
         const size_t max_regions = std::max<size_t>(1, std::min<size_t>(1024, (1ull << 30) / (8ull * H)));
@@ -539,15 +674,19 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
             GroupOut go;
             if (int rc = B.grouper->group(ncar, recs, regs, H, go)) return rc;
             if (go.memb_alloc) B.memb_allocs.push_back(go.memb_alloc);
-            for (size_t k = c0; k < c1; k++) {
-                const size_t j = dj[k], c = k - c0;
+            par(c1 - c0, [&](size_t c) {
+                const size_t j = dj[c0 + c];
                 if (go.n_groups[c] == UINT32_MAX) {
                     where[j] = 2;
-                    continue;
+                    return;
                 }
-                rcs[j] = snv_finish(B, built[j], go.masks.data() + go.first[c], go.counts.data() + go.first[c],
-                                    go.n_groups[c], go.memb[c]);
-            }
+                if (where[j] == 1)
+                    rcs[j] = snv_finish(B, built[j], go.masks.data() + go.first[c], go.counts.data() + go.first[c],
+                                        go.n_groups[c], go.memb[c]);
+                else
+                    rcs[j] = mask_finish(B, ins[j], built[j], uniq[j], go.masks.data() + go.first[c],
+                                         go.counts.data() + go.first[c], go.n_groups[c], go.memb[c]);
+            });
             c0 = c1;
         }
         std::vector<size_t> hj;
@@ -561,7 +700,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
     }
     for (size_t j = 0; j < n; j++) {
         if (rcs[j]) return rcs[j];
-        if (built[j].dev) B.dev_regions++;
+        if (built[j].dev || built[j].dev_grouped) B.dev_regions++;
         else B.host_regions++;
     }
     return TFBS_OK;
@@ -900,6 +1039,8 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     {
         const char *v = getenv("TFBS_DEDUP");
         B.dedup = !(v && *v && atoi(v) == 0);
+        const char *w = getenv("TFBS_DEV_PATCH");  // 0: only SNV-only regions are grouped on the device
+        B.dev_patch = !(w && *w && atoi(w) == 0);
     }
     B.slot_pid = plan.slot_pid;
     B.slots_by_pid.resize(B.slot_pid.size());

@@ -156,6 +156,7 @@ struct Batch {
     // reference-window reuse (HAP_DEDUP, TFBS_DEDUP=0 turns it off): windows and
     // column lookups the scan executes (helper reference haplotypes included)
     bool dedup = true;
+    bool dev_patch = true;   // device grouping + host patching of indel regions (TFBS_DEV_PATCH=0: off)
     uint64_t scan_windows = 0, scan_cell_ops = 0;
     // host prep seconds (tfbs_batch_prep_seconds): synthetic generation (thread
     // CPU-seconds), build_region (thread CPU-seconds), serial commit (wall), whole fill (wall)
@@ -213,6 +214,10 @@ struct RegionBuilt {
     // SNVs of masks[i] (bit k = snv_rel[k] / snv_alt[k]; 0 = the reference group or
     // the helper); dist stays empty
     bool dev = false;
+    // grouped on the device, patched on the host (regions with indels, N or diffs
+    // outside the window): dist holds the patched groups, the membership row stays
+    // on the device unless two groups patched to one sequence
+    bool dev_grouped = false;
     std::vector<uint64_t> masks;
     std::vector<uint32_t> snv_rel;
     std::vector<uint8_t> snv_alt;

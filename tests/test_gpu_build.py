@@ -1,12 +1,15 @@
 """Device haplotype grouping (tfbs_batch_set_build_device; haplotype.rs:16-88 on the
-GPU for SNV-only regions, build_gpu.hip): a batch whose regions were grouped on the
-device must be the batch the host builds -- per region the same distinct
+GPU, build_gpu.hip): SNV-only regions are grouped and patched from the device's
+masks; regions with indels, N in the window, diffs outside it or two records at
+one position are grouped on the device and only their distinct groups patched on
+the host (batch.cpp mask_finish, with HashMap::insert's collision rule).  A batch
+built so must be the batch the host builds -- per region the same distinct
 haplotypes in the same order, packed bases, carrier counts, reference group,
 keys and membership (tfbs_batch_region_input_digest), the same scan statistics
 (reference-window reuse masks included) -- and scan to the same keys and rows.
-Regions the device does not take (indels, N in the window, two records at one
-position, unsorted carriers, more than 2047 distinct diff masks) are built on the
-host in the same batch."""
+Regions the device does not take (unsorted carriers, a repeated diff, more than 64
+applied records or 2047 distinct diff masks) are built on the host in the same
+batch."""
 import os
 import random
 
@@ -73,16 +76,22 @@ def test_device_grouping_c3_batch(tmp_path):
         sc.close()
 
 
-def test_device_grouping_indels_mixed(tmp_path):
-    """C5-like regions (3 % indels: about half the regions have one): the SNV-only ones on
-    the device, the rest on the host."""
+@pytest.mark.parametrize("dev_patch", ["1", "0"])
+def test_device_grouping_indels_mixed(tmp_path, monkeypatch, dev_patch):
+    """C5-like regions (3 % indels: about half the regions have one): every region grouped
+    on the device, the indel ones patched on the host; with TFBS_DEV_PATCH=0 the SNV-only
+    ones on the device and the rest built on the host."""
+    monkeypatch.setenv("TFBS_DEV_PATCH", dev_patch)
     ps, _ = synth_patterns(tmp_path, 12, 5, 105, thr=1e-3)
     host = T.RegionBatch(ps, 2000)
     host.synth_fill(5, 0, 120, 3)
     dev = T.RegionBatch(ps, 2000, build_device=0)
     dev.synth_fill(5, 0, 120, 3)
     nd, nh = dev.build_stats()
-    assert nd > 0 and nh > 0, (nd, nh)
+    if dev_patch == "1":
+        assert (nd, nh) == (120, 0), (nd, nh)
+    else:
+        assert nd > 0 and nh > 0, (nd, nh)
     _same_batches(host, dev)
     sc = T.Scanner(ps)
     try:
@@ -154,6 +163,19 @@ def _edge_regions(n_samples, lmax):
         regs.append({"merged": m, "ref": ref,
                      "records": [snv(ref, es, p, sorted(rnd.sample(range(H), 2)))
                                  for p in sorted(rnd.sample(range(len(ref)), ns))]})
+    # 11: a collision (device grouping, host patch): a deletion starting before the
+    # window (patch_haplotype drops it, haplotype.rs:95) on haplotypes {0, 1}, an SNV on
+    # {0, 2}: the groups [del, snv] and [snv] patch to one sequence, [snv] (later in
+    # Vec<Diff> order) wins and haplotype 0 joins the reference group
+    ref, m, es = base(11)
+    regs.append({"merged": m, "ref": ref, "records": [("car", es - 2, "AC", "A", [0, 1]),
+                                                      snv(ref, es, 40, [0, 2])]})
+    # 12: an insertion and a deletion on one haplotype, a deletion over the window's end
+    ref, m, es = base(12)
+    n = len(ref)
+    regs.append({"merged": m, "ref": ref, "records": [("car", es + 9, ref[9], ref[9] + "GT", [3, 4, 5]),
+                                                      ("car", es + 30, ref[30:33], ref[30], [4, 6]),
+                                                      ("car", es + n - 2, ref[n - 2:], ref[n - 2], [7])]})
     return regs
 
 
@@ -178,7 +200,7 @@ def test_device_grouping_edge_cases(tmp_path):
                 dev.add_record_gt(rec[1], rec[2], rec[3], rec[4], rec[5])
         dev.end()
     nd, nh = dev.build_stats()
-    assert (nd, nh) == (5, 6), (nd, nh)  # regions 0, 1, 2, 8, 9 on the device
+    assert (nd, nh) == (10, 3), (nd, nh)  # on the host: 4 (unsorted carriers), 6 (masks), 10 (65 records)
     _same_batches(host, dev)
     sc = T.Scanner(ps)
     try:

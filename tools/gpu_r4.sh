@@ -11,3 +11,4 @@ rc=$?
 tail -25 $O/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
 bash tools/profile_round.sh ${T}_c3 --no-cpu || exit 1
+bash tools/pmc_scan_stalls.sh ${T}_stall || exit 1
