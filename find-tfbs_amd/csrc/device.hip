@@ -138,6 +138,7 @@ struct tfbs_ctx {
     DevBuf<uint32_t> asm_scratch;         // key assembly counters of regions with many distinct haplotypes
     // key reduction (tfbs_batch_reduce)
     DevBuf<uint32_t> key_first, var_counts, asm_redo;   // asm_redo: n_regions + 1 list entries, then the arena's fill
+    DevBuf<uint32_t> asm_why;                            // TFBS_DEBUG_OVER: key_fast_kernel's give-up reasons
     DevBuf<uint32_t> cor_arena;                          // key_fast_kernel's corrections past its LDS list
     uint32_t cor_cap = 1u << 22;
     DevBuf<unsigned long long> var_tot;
@@ -509,7 +510,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
-    ctx->asm_redo.release(); ctx->cor_arena.release();
+    ctx->asm_redo.release(); ctx->cor_arena.release(); ctx->asm_why.release();
     ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
     ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_nr_ids.release(); ctx->enc_nr_meta.release();
@@ -817,6 +818,12 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.cor_cap = ctx->cor_cap;
     a.cor_used = ctx->asm_redo.p + nr + 1;
     a.cor_lds = ctx->key_cor_lds;
+    a.why = nullptr;
+    if (ctx->debug_over) {
+        if ((rc = ctx->asm_why.ensure(8))) return rc;
+        HIP_TRY(hipMemsetAsync(ctx->asm_why.p, 0, 32, ctx->stream));
+        a.why = ctx->asm_why.p;
+    }
     HIP_TRY(hipMemsetAsync(ctx->var_tot.p, 0, 16, ctx->stream));
     if ((rc = launch_key_fast(a, nr, ctx->stream))) return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
@@ -858,9 +865,12 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
                 mi = std::max(mi, rg.n_inner);
                 for (uint32_t l = 0; l < rg.hap_count; l++) sr += B.haps[rg.hap_begin + l].n_druns;
             }
+            uint32_t why[8];
+            HIP_TRY(hipMemcpy(why, ctx->asm_why.p, 32, hipMemcpyDeviceToHost));
             fprintf(stderr, "tfbs assembly: %zu regions left to key_asm: mean haplotypes %.1f (max %u), max inner %u, "
-                            "mean diff runs %.1f\n", redo.size(), (double)su / redo.size(), mu, mi,
-                    (double)sr / redo.size());
+                            "mean diff runs %.1f; reasons: shape %u lists %u runs %u refs %u arena(cor) %u arena(cnt) %u\n",
+                    redo.size(), (double)su / redo.size(), mu, mi, (double)sr / redo.size(), why[0], why[1], why[2],
+                    why[3], why[4], why[5]);
         }
         if (ctx->debug_over)
             fprintf(stderr, "tfbs assembly: spill %u/%u candidates %u/%u left to key_asm %u arena %u/%u varying keys "

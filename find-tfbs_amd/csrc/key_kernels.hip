@@ -506,10 +506,13 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         }
         return;
     }
-    auto give_up = [&]() {  // workgroup-uniform, before any output
-        if (tid == 0) A.redo[1 + atomicAdd(A.redo, 1u)] = r;
+    auto give_up = [&](uint32_t why) {  // workgroup-uniform, before any output
+        if (tid == 0) {
+            A.redo[1 + atomicAdd(A.redo, 1u)] = r;
+            if (A.why) atomicAdd(A.why + why, 1u);  // (TFBS_DEBUG_OVER: the reasons)
+        }
     };
-    if (U > min(kFMaxU, A.fast_max_u) || K > 32 * kFKeyWords || n_inner > 32) return give_up();
+    if (U > min(kFMaxU, A.fast_max_u) || K > 32 * kFKeyWords || n_inner > 32) return give_up(0);
     const uint32_t hb = rg.hap_begin;
     const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
     if (tid == 0) {
@@ -545,7 +548,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
             if (ga < gb) nl += (gb - ga) * src.ns * kMBlockWaves;
         }
-    if (nl > kFLists) return give_up();
+    if (nl > kFLists) return give_up(1);
     uint32_t lcnt = 0;
     if (tid < nl) {
         uint32_t t = tid;
@@ -570,7 +573,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     if (tid < nl) s_loff[tid] = loff;
     if (tid == 0) s_loff[nl] = n_ent;
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
-    if (nruns >= 65536) return give_up();
+    if (nruns >= 65536) return give_up(2);
 #pragma unroll
     for (uint32_t q = 0; q < kFHapLds / kFBlock; q++) {
         const uint32_t l = tid + q * kFBlock;
@@ -605,7 +608,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     }
     __syncthreads();
     const uint32_t nref = s_nref;
-    if (nref > kFRefs) return give_up();
+    if (nref > kFRefs) return give_up(3);
     {  // the reference hits by window (rank sort; ties by list position)
         uint4 mine = make_uint4(0, 0, 0, 0);
         uint32_t rank = 0;
@@ -660,7 +663,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         }
     }
     __syncthreads();
-    if (!in_lds && s_arena == kFNone) return give_up();  // the host grows the arena for the next call
+    if (!in_lds && s_arena == kFNone) return give_up(4);  // the host grows the arena for the next call
     uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
     const uint2 *hitl = reinterpret_cast<const uint2 *>(A.hitl);
     for (uint32_t e0 = 0; e0 < n_ent; e0 += kFBlock) {
@@ -739,11 +742,12 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     }
     auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
     // the counter block: LDS chunks of rows x U, or -- when that would take more than
-    // 4 chunks (many haplotypes and keys), each re-reading every correction --
-    // chunks of kFRows rows in a share of the arena (global atomics)
+    // 32 chunks (hundreds of haplotypes and keys: each chunk re-reads every
+    // correction and costs a few barriers) -- chunks of kFRows rows in a share of
+    // the arena (global atomics)
     uint32_t rows_per = min(kFCnt / U, kFRows);
     uint32_t *cnt = s_cnt;
-    if ((T + rows_per - 1) / rows_per > 4 || A.cor_lds == 0) {  // (cor_lds 0: the tests' all-global path)
+    if ((T + rows_per - 1) / rows_per > 32 || A.cor_lds == 0) {  // (cor_lds 0: the tests' all-global path)
         rows_per = min(T, kFRows);
         if (tid == 0) {
             s_arena = kFNone;
@@ -751,7 +755,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             if (at <= A.cor_cap && want <= A.cor_cap - at) s_arena = at;
         }
         __syncthreads();
-        if (s_arena == kFNone) return give_up();  // the host grows the arena for the next call
+        if (s_arena == kFNone) return give_up(5);  // the host grows the arena for the next call
         cnt = A.cor_arena + s_arena;
     }
     // untouched keys: no match -- no key in the reference's HashMap

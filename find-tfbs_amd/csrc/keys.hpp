@@ -58,6 +58,7 @@ struct AsmArgs {
     uint32_t cor_cap;
     uint32_t *cor_used;
     uint32_t cor_lds;  // corrections kept in LDS at most (TFBS_KEY_COR_LDS, tests: the arena path)
+    uint32_t *why;     // debug (TFBS_DEBUG_OVER): key_fast_kernel's give-ups per reason (8 counters), or null
 };
 
 // key_asm_kernel over every region (mode 0 or 1).

@@ -439,6 +439,35 @@ __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, co
     }
 }
 
+#ifndef TFBS_BPREFETCH
+#define TFBS_BPREFETCH 1
+#endif
+// The same with chunk 0's B fragment already loaded (f0: read during the round
+// before, so the round's first MFMAs do not wait for LDS); chunks 1.. are read
+// before the first MFMA is issued.
+template <int D, int NK>
+__device__ __forceinline__ void round_scores_pf(const char *tile, uint32_t lane, const BFrag &f0, const v4i (&a0)[NK],
+                                                const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
+    BFrag f[D];
+    f[0] = f0;
+#pragma unroll
+    for (int kc = 1; kc < D; kc++) {
+        f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
+        f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
+    }
+    c0 = cb;
+    c1 = cb;
+#pragma unroll
+    for (int kc = 0; kc < D; kc++) {
+        c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+        c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+    }
+}
+__device__ __forceinline__ void load_frag0(const char *tile, uint32_t lane, BFrag &f) {
+    f.b = *reinterpret_cast<const v4i *>(tile + lane * 16);
+    f.c = *reinterpret_cast<const int2 *>(tile + 1024 + lane * 8);
+}
+
 template <int D, int NK>
 __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v16f &cb,
                                             int sa, v16f &c0) {
@@ -465,10 +494,19 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
                                              uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
     if (two) {
+#if TFBS_BPREFETCH
+        BFrag pf;  // the next round's chunk-0 B fragment, read while this round's MFMAs run
+        load_frag0(img, lane, pf);
+#endif
         for (uint32_t ti = tb; ti < te; ti++) {
             const char *tile = img + (ti - tb) * kTB;
             v16f c0, c1;
+#if TFBS_BPREFETCH
+            round_scores_pf<D, NK>(tile, lane, pf, a0, a1, cb, sa, c0, c1);
+            load_frag0(ti + 1 < te ? tile + kTB : tile, lane, pf);
+#else
             round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+#endif
             uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
             const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
             if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
