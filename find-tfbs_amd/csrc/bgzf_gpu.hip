@@ -616,7 +616,8 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
 // and writes the block's bytes to LDS (for the CRC), a block scan gives every
 // group its bit offset, pass 2 writes the bits.
 constexpr int kWv = 1024;             // threads
-constexpr uint32_t kWvItems = 1024;   // heads, groups, newlines of a block (<= 2 kStRowDesc + kStCum)
+constexpr uint32_t kWvItems = 768;    // heads, groups, newlines of a block (<= 2 kStRowDesc + kStCum)
+static_assert(kWvItems >= 2 * kStRowDesc + kStCum, "a block's items");
 enum : uint32_t { IT_HEAD = 0u, IT_GROUP = 1u, IT_NL = 2u };
 
 __shared__ uint32_t g_bits[kBitWords + 1];
@@ -633,7 +634,8 @@ __shared__ uint8_t g_tlitn[kStTok];
 constexpr uint32_t kNoTokLit = 255;
 __shared__ uint32_t g_ioff[kWvItems + 1];
 __shared__ uint32_t g_red[kWv / 64];
-__shared__ uint32_t g_pub[kWvItems];  // item i's end bit + 1 (0: not yet known; wv_chain)
+__shared__ uint32_t g_pub[kWvItems];  // item i's end bit + 1 (0: not yet known; wv_place)
+__shared__ uint32_t g_agg[kWvItems];  // item i's bit count + 1 (0: not yet known; wv_place)
 
 // A lane's bit stream: symbols gathered in a register, ORed into g_bits 32 bits at
 // a time (two LDS atomics at most per 32 bits, not per symbol)
@@ -721,23 +723,44 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_sum(v), 63);
 }
 
-// Item i's first bit: the end of item i - 1, published by the wave that wrote it
-// (items go to the waves round-robin and each wave takes its items in order, so
-// the chain always advances); then item i's end is published.
-__device__ __forceinline__ uint32_t wv_chain(uint32_t i, uint32_t total, uint32_t lane) {
-    uint32_t base = 3;  // BFINAL + BTYPE
-    if (i) {
-        uint32_t p;
-        while ((p = __hip_atomic_load(&g_pub[i - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0)
+// Item i's first bit by decoupled look-back (no chain through the waves): the
+// item's bit count is published first (g_agg); then the wave's lanes read the
+// 64 items before it at once -- lane k item i - 1 - k -- and the first bit is
+// the end of the nearest one whose end is known (g_pub) plus the bit counts of
+// the items between (a wave sum), further windows of 64 while none is known.
+// Every item publishes its count before it looks back and waits only on lower
+// items, so all counts arrive (items go to the waves round-robin, in order).
+// Then item i's end is published.
+__device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_t lane) {
+    if (lane == 0) __hip_atomic_store(&g_agg[i], total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    uint32_t acc = 3;  // BFINAL + BTYPE before item 0
+    for (int32_t hi = (int32_t)i; hi > 0;) {
+        const int32_t j = hi - 1 - (int32_t)lane;
+        uint32_t inc = 0, agg = 1;
+        if (j >= 0) {
+            inc = __hip_atomic_load(&g_pub[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            agg = __hip_atomic_load(&g_agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        const uint64_t have = __ballot(j >= 0 && inc != 0);
+        const uint32_t ks = have ? (uint32_t)__builtin_ctzll(have) : 64u;  // nearest known end
+        const bool need = j >= 0 && lane < ks;
+        if (__ballot(need && agg == 0)) {  // a count between not published yet: look again
             __builtin_amdgcn_s_sleep(1);
-        base = p - 1;
+            continue;
+        }
+        acc += wave_sum(need ? agg - 1 : 0u);
+        if (have) {
+            acc += (uint32_t)__builtin_amdgcn_readlane((int)inc, (int)ks) - 1 - 3;  // (its end includes the 3)
+            break;
+        }
+        hi -= 64;
     }
-    if (lane == 0) __hip_atomic_store(&g_pub[i], base + total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return base;
+    if (lane == 0) __hip_atomic_store(&g_pub[i], acc + total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return acc;
 }
 
 // Item i of the block (all lanes of a wave together), in one pass: its bytes into
-// g_text, its bit count, its first bit from the chain (wv_chain), its symbols.
+// g_text, its bit count, its first bit (wv_place), its symbols.
 __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane) {
     const uint32_t item = g_item[i];
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
@@ -770,7 +793,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         }
     }
     if (kind == IT_NL) {
-        const uint32_t base = wv_chain(i, 8, lane);
+        const uint32_t base = wv_place(i, 8, lane);
         if (lane == 0) {
             g_text[txt_at((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0))] = '\n';
             LaneBits o{0, 0, base};
@@ -789,7 +812,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
             if (in) g_text[txt_at((uint32_t)(q - b0))] = (uint8_t)b;
             total += wave_sum(in ? lit_bits(b) : 0u);
         }
-        uint32_t at = wv_chain(i, total, lane);
+        uint32_t at = wv_place(i, total, lane);
         for (uint64_t q0 = hs; q0 < he; q0 += 64) {
             const uint64_t q = q0 + lane;
             const bool in = q < he;
@@ -888,7 +911,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     } else if (in) {
         for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
-    const uint32_t base = wv_chain(i, wave_sum(nb), lane);
+    const uint32_t base = wv_place(i, wave_sum(nb), lane);
     LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
     if (runm) {
         if (m1) wv_match<true>(off, m1, t);
@@ -923,7 +946,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         for (uint32_t i = tid; i < 256; i += kWv) S.crc_tab[i] = A.crc_tab[i];
         for (uint32_t i = tid; i < kCrcOps * 32; i += kWv) S.crc_ops[i] = A.crc_ops[i];
         for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-        for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = 0;
+        for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
         const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
         for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
