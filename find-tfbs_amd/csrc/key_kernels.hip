@@ -421,17 +421,21 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
 // corrections with LDS atomics.  A region past the kernel's limits (haplotypes,
 // keys, hit lists, reference hits, diff runs, arena) is appended to A.redo and
 // left to key_asm_kernel.
-constexpr int kFBlock = 256;
+#ifndef TFBS_KF_BLOCK
+#define TFBS_KF_BLOCK 256
+#endif
+constexpr int kFBlock = TFBS_KF_BLOCK;  // threads per region (the lists below scale with it)
 constexpr uint32_t kFWaves = kFBlock / 64;
 constexpr uint32_t kFMaxU = 2048;     // distinct haplotypes (11 bits of a correction)
-constexpr uint32_t kFHapLds = 1024;   // haplotypes whose reuse descriptor sits in LDS (the others: read again)
-constexpr uint32_t kFCor = 4096;      // corrections in LDS: own hits and dirty reference hits
-constexpr uint32_t kFRefs = 256;      // reference hits
-constexpr uint32_t kFCnt = 4096;      // u32 counters of a chunk: rows x U
+constexpr uint32_t kFHapLds = 4 * kFBlock;  // haplotypes whose reuse descriptor sits in LDS (the others: read again)
+constexpr uint32_t kFCor = 16 * kFBlock;    // corrections in LDS: own hits and dirty reference hits
+constexpr uint32_t kFRefs = kFBlock;        // reference hits
+constexpr uint32_t kFCnt = 16 * kFBlock;    // u32 counters of a chunk: rows x U
 constexpr uint32_t kFRuns = kFCnt / 2;  // diff runs of the region's HAP_DEDUP haplotypes staged (over the counters)
-constexpr uint32_t kFRows = 512;      // rows (touched keys) per chunk
+constexpr uint32_t kFRows = 2 * kFBlock;    // rows (touched keys) per chunk
 constexpr uint32_t kFKeyWords = 512;  // touched-key bitmap: keys <= 16384
-constexpr uint32_t kFLists = 256;     // scan hit lists over the region's haplotypes
+constexpr uint32_t kFLists = kFBlock;       // scan hit lists over the region's haplotypes
+constexpr uint32_t kFBatch = 8;       // hit-list entries each thread has in flight
 constexpr uint32_t kFNone = 0xFFFFFFFFu;
 static_assert(kFMaxU % kFBlock == 0 && kFHapLds % kFBlock == 0 && kFKeyWords % kFBlock == 0 && kFLists <= kFBlock &&
                   kFRefs <= kFBlock,
@@ -548,10 +552,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
             if (ga < gb) nl += (gb - ga) * src.ns * kMBlockWaves;
         }
-    if (nl > kFLists) return give_up(1);
-    uint32_t lcnt = 0;
-    if (tid < nl) {
-        uint32_t t = tid;
+    auto list_idx = [&](uint32_t t) -> uint32_t {  // list t of the region's: its wave list (wg x 8 + wave)
         for (uint32_t si = 0; si < A.n_srcs; si++) {
             const HitSrc src = A.srcs[si];
             const uint32_t ga = max(g_lo, src.g0), gb = min(g_hi + 1, src.g0 + src.ng);
@@ -560,18 +561,16 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             if (t < (gb - ga) * per_g) {
                 const uint32_t g = ga + t / per_g, rem = t % per_g;
                 const uint32_t wg = src.wg_base + (g - src.g0) * src.ns + rem / kMBlockWaves;
-                const uint32_t idx = wg * kMBlockWaves + rem % kMBlockWaves;
-                lcnt = A.hitn[idx];
-                s_lidx[tid] = idx;
-                break;
+                return wg * kMBlockWaves + rem % kMBlockWaves;
             }
             t -= (gb - ga) * per_g;
         }
-    }
+        return 0;
+    };
+    uint32_t lcnt = 0;  // the region's entries (an upper bound of its hits: groups are shared)
+    for (uint32_t t = tid; t < nl; t += kFBlock) lcnt += A.hitn[list_idx(t)];
     uint32_t n_ent = 0;
-    const uint32_t loff = block_excl_scan(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
-    if (tid < nl) s_loff[tid] = loff;
-    if (tid == 0) s_loff[nl] = n_ent;
+    (void)block_excl_scan(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
     if (nruns >= 65536) return give_up(2);
 #pragma unroll
@@ -666,24 +665,42 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     if (!in_lds && s_arena == kFNone) return give_up(4);  // the host grows the arena for the next call
     uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
     const uint2 *hitl = reinterpret_cast<const uint2 *>(A.hitl);
-    for (uint32_t e0 = 0; e0 < n_ent; e0 += kFBlock) {
-        const uint32_t e = e0 + tid;
-        bool want = false;
-        uint32_t v = 0;
-        if (e < n_ent) {
-            uint32_t lo = 0, hi = nl - 1;  // the list holding entry e: the last with s_loff <= e
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) / 2;
-                if (s_loff[mid] <= e) lo = mid;
-                else hi = mid - 1;
-            }
-            const uint32_t idx = s_lidx[lo];
-            const uint2 h = hitl[(size_t)(idx / kMBlockWaves) * A.cand_cap +
-                                 (size_t)(idx % kMBlockWaves) * (A.cand_cap / kMBlockWaves) + (e - s_loff[lo])];
-            want = h.x - hb < U;
-            v = cor_entry(h.y, h.x - hb, 0);
+    for (uint32_t l0 = 0; l0 < nl; l0 += kFLists) {  // kFLists lists at a time: their offsets in LDS
+        const uint32_t nlc = min(kFLists, nl - l0);
+        uint32_t lc = 0;
+        if (tid < nlc) {
+            const uint32_t idx = list_idx(l0 + tid);
+            lc = A.hitn[idx];
+            s_lidx[tid] = idx;
         }
-        wave_push(cor, &s_ncor, need, want, v);
+        uint32_t tot = 0;
+        const uint32_t off = block_excl_scan(lc, s_w, tot);
+        if (tid < nlc) s_loff[tid] = off;
+        if (tid == 0) s_loff[nlc] = tot;
+        __syncthreads();
+        for (uint32_t e0 = 0; e0 < tot; e0 += kFBlock * kFBatch) {  // kFBatch loads in flight per thread
+            uint2 h[kFBatch];
+#pragma unroll
+            for (uint32_t q = 0; q < kFBatch; q++) {
+                const uint32_t e = e0 + q * kFBlock + tid;
+                h[q] = make_uint2(hb + U, 0);  // (no entry: not the region's)
+                if (e < tot) {
+                    uint32_t lo = 0, hi = nlc - 1;  // the list holding entry e: the last with s_loff <= e
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi + 1) / 2;
+                        if (s_loff[mid] <= e) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    const uint32_t idx = s_lidx[lo];
+                    h[q] = hitl[(size_t)(idx / kMBlockWaves) * A.cand_cap +
+                                (size_t)(idx % kMBlockWaves) * (A.cand_cap / kMBlockWaves) + (e - s_loff[lo])];
+                }
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < kFBatch; q++)
+                wave_push(cor, &s_ncor, need, h[q].x - hb < U, cor_entry(h[q].y, h[q].x - hb, 0));
+        }
+        __syncthreads();  // s_loff / s_lidx reused by the next lists
     }
     for (uint32_t e0 = sp.x; e0 < sp.y; e0 += kFBlock) {  // own hits of the spill list (kind 0)
         const uint32_t e = e0 + tid;

@@ -1,18 +1,16 @@
-# Round-4 A/B: the BGZF tests, key assembly diagnostics, then the in-tree scan (B
-# prefetch) against the probe builds named on the command line (tools/exp_libs.sh,
-# C3 mix), and the device BGZF writer (look-back placement) against probechain.
+# Round-4 A/B: the key-assembly GPU tests, assembly diagnostics, then the bench step
+# of the in-tree build against the probe builds named on the command line.
 set -o pipefail
 T=${1:-ab}; shift
 mkdir -p gpurun_out/$T
-timeout -k 10 300 python -u -m pytest tests/test_gpu_bgzf.py -x -q --timeout 200 --timeout-method thread > gpurun_out/$T/bgzf_tests.log 2>&1 || { tail -20 gpurun_out/$T/bgzf_tests.log; exit 1; }
-tail -1 gpurun_out/$T/bgzf_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "reuse or synthetic_regions or c3_full or many_variant or reduce" > gpurun_out/$T/tests.log 2>&1 || { tail -20 gpurun_out/$T/tests.log; exit 1; }
+tail -1 gpurun_out/$T/tests.log
 TFBS_DEBUG_OVER=1 timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu --no-e2e > gpurun_out/$T/diag.json 2> gpurun_out/$T/diag.err || { tail -5 gpurun_out/$T/diag.err; exit 1; }
 grep "regions left\|assembly: spill" gpurun_out/$T/diag.err | tail -3
 for rep in 1 2; do
-  for lib in base chain; do
+  for lib in base "$@"; do
     if [ $lib = base ]; then unset TFBS_LIB; else export TFBS_LIB=find-tfbs_amd/lib/probe$lib/libtfbs_amd.so; fi
-    echo "bgzf $lib: $(timeout -k 10 200 python3 tools/bgzf_only.py 1000 2>&1 | tail -1)"
+    timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e > gpurun_out/$T/step_$lib.json 2>/dev/null || { echo "bench $lib failed"; exit 1; }
+    echo "step $lib: $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$T/step_$lib.json | head -1) $(grep -o '"step_device_ms": {[^}]*}' gpurun_out/$T/step_$lib.json)"
   done
 done
-unset TFBS_LIB
-bash tools/exp_libs.sh ${T}_x 3 "$@"
