@@ -111,6 +111,8 @@ struct tfbs_ctx {
     bool over_pending = false;
     bool post_done = false;              // the last scan's overflow candidates were rescored (launch_post_scan)
     HitSrc srcs_host[kMaxHitSrcs] = {};
+    HitSrc srcs_dev[kMaxHitSrcs] = {};   // what srcs holds (copied from here: stable while the copy runs)
+    bool srcs_on_dev = false;
     ScanArgs last_margs{};               // the last matrix-core scan's arguments (launch_post_scan)
     uint32_t n_srcs = 0;
     DevBuf<HitSrc> srcs;
@@ -137,11 +139,13 @@ struct tfbs_ctx {
     DevBuf<unsigned long long> hits;
     DevBuf<uint32_t> asm_scratch;         // key assembly counters of regions with many distinct haplotypes
     // key reduction (tfbs_batch_reduce)
-    DevBuf<uint32_t> key_first, var_counts, asm_redo;   // asm_redo: n_regions + 1 list entries, then the arena's fill
-    DevBuf<uint32_t> asm_why;                            // TFBS_DEBUG_OVER: key_fast_kernel's give-up reasons
+    DevBuf<uint32_t> key_first, var_counts, asm_redo;   // asm_redo: the regions left to key_asm_kernel
+    // the assembly's counters (one memset, one copy back): [0..1] the scan's spill /
+    // candidate overflow counts (asm_report_kernel), [2] regions left, [3] the arena's
+    // fill, [4..7] the varying keys and counts (u64), [8..15] give-up reasons (debug)
+    DevBuf<uint32_t> asm_ctr;
     DevBuf<uint32_t> cor_arena;                          // key_fast_kernel's corrections past its LDS list
     uint32_t cor_cap = 1u << 22;
-    DevBuf<unsigned long long> var_tot;
     DevBuf<uint8_t> key_flags;
     DevBuf<DevVarKey> var_keys, enc_keys;
     uint32_t var_keys_cap = 1u << 16;
@@ -150,10 +154,7 @@ struct tfbs_ctx {
     uint64_t var_cap = 1u << 24;
     bool var_cap_forced = false;     // TFBS_VAR_CAP applied (tfbs_batch_reduce)
     Batch *var_owner = nullptr;      // the batch whose varying counts are only in var_counts (device)
-    // the assembly's counters, copied back after it (pinned): [0] spill records,
-    // [1] candidates past the wave lists, [2] regions left to key_asm_kernel, [3]
-    // the correction arena's fill; at byte 16 the varying keys and counts (u64)
-    uint32_t *asm_host = nullptr;
+    uint32_t *asm_host = nullptr;  // asm_ctr copied back (pinned)
     hipEvent_t asm_ev = nullptr, asm_t0 = nullptr, asm_t1 = nullptr;
     const Batch *asm_batch = nullptr;    // the batch the enqueued assembly is for
     int asm_state = 0;                   // 0 none, 1 enqueued, 2 complete (checked)
@@ -349,8 +350,13 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         ctx->last_margs = m;  // the overflow candidates are rescored when the results are read (check_overflow)
         ctx->post_done = false;
         if ((rc = ctx->srcs.ensure(kMaxHitSrcs))) return rc;
-        HIP_TRY(hipMemcpyAsync(ctx->srcs.p, ctx->srcs_host, sizeof(ctx->srcs_host), hipMemcpyHostToDevice,
-                               ctx->stream));
+        if (!ctx->srcs_on_dev || memcmp(ctx->srcs_dev, ctx->srcs_host, sizeof(ctx->srcs_host)) != 0) {
+            // (a rescan of the same batch launches the same workgroups: no copy)
+            memcpy(ctx->srcs_dev, ctx->srcs_host, sizeof(ctx->srcs_host));
+            HIP_TRY(hipMemcpyAsync(ctx->srcs.p, ctx->srcs_dev, sizeof(ctx->srcs_dev), hipMemcpyHostToDevice,
+                                   ctx->stream));
+            ctx->srcs_on_dev = true;
+        }
         // the overflow counters, for the check before the results are read
         if (!ctx->over_host) HIP_TRY(hipHostMalloc((void **)&ctx->over_host, 8, hipHostMallocDefault));
         HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -509,8 +515,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->druns.release(); ctx->wl_tmp.release();
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
-    ctx->key_first.release(); ctx->var_counts.release(); ctx->var_tot.release(); ctx->key_flags.release();
-    ctx->asm_redo.release(); ctx->cor_arena.release(); ctx->asm_why.release();
+    ctx->key_first.release(); ctx->var_counts.release(); ctx->asm_ctr.release(); ctx->key_flags.release();
+    ctx->asm_redo.release(); ctx->cor_arena.release();
     ctx->var_keys.release();
     ctx->enc_keys.release(); ctx->enc_pidx.release(); ctx->enc_pab.release(); ctx->enc_pcnt.release();
     ctx->enc_pair_n.release(); ctx->enc_memb.release(); ctx->enc_nr_ids.release(); ctx->enc_nr_meta.release();
@@ -777,10 +783,10 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
     const uint32_t nr = (uint32_t)B.regions.size();
     if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
-        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->var_tot.ensure(2)) ||
-        (rc = ctx->asm_redo.ensure((size_t)nr + 2)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
+        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(16)) ||
+        (rc = ctx->asm_redo.ensure((size_t)nr + 1)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
         return rc;
-    if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 32, hipHostMallocDefault));
+    if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 64, hipHostMallocDefault));
     if (const int vc = env_int("TFBS_VAR_CAP", 0); vc > 0) {
         if (!ctx->var_cap_forced) {
             ctx->var_keys_cap = (uint32_t)vc;
@@ -811,27 +817,21 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.var_keys_cap = ctx->var_keys_cap;
     a.var_counts = ctx->var_counts.p;
     a.var_cap = ctx->var_cap;
-    a.var_tot = ctx->var_tot.p;
+    a.var_tot = reinterpret_cast<unsigned long long *>(ctx->asm_ctr.p + 4);
     a.redo = ctx->asm_redo.p;
+    a.redo_n = ctx->asm_ctr.p + 2;
     a.fast_max_u = ctx->key_fast_max_u;
     a.cor_arena = ctx->cor_arena.p;
     a.cor_cap = ctx->cor_cap;
-    a.cor_used = ctx->asm_redo.p + nr + 1;
+    a.cor_used = ctx->asm_ctr.p + 3;
     a.cor_lds = ctx->key_cor_lds;
-    a.why = nullptr;
-    if (ctx->debug_over) {
-        if ((rc = ctx->asm_why.ensure(8))) return rc;
-        HIP_TRY(hipMemsetAsync(ctx->asm_why.p, 0, 32, ctx->stream));
-        a.why = ctx->asm_why.p;
-    }
-    HIP_TRY(hipMemsetAsync(ctx->var_tot.p, 0, 16, ctx->stream));
-    if ((rc = launch_key_fast(a, nr, ctx->stream))) return rc;
+    a.why = ctx->debug_over ? ctx->asm_ctr.p + 8 : nullptr;
+    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0, 64, ctx->stream));
+    if ((rc = launch_key_fast(a, nr, ctx->stream)) ||
+        (rc = launch_asm_report(mfma ? ctx->over.p : nullptr, ctx->asm_ctr.p, ctx->stream)))
+        return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
-    if (mfma) HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-    else ctx->asm_host[0] = ctx->asm_host[1] = 0;
-    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 2, ctx->asm_redo.p, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 3, ctx->asm_redo.p + nr + 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->asm_host + 4, ctx->var_tot.p, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->asm_ctr.p, 64, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
     ctx->over_pending = false;  // the assembly's check covers this scan's overflow lists
     ctx->asm_batch = &B;
@@ -855,7 +855,7 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
         const uint64_t nk = vt[0], nc = vt[1];
         if (ctx->debug_over && ctx->asm_host[2]) {  // the regions left to key_asm_kernel: their shapes
             std::vector<uint32_t> redo(ctx->asm_host[2]);
-            HIP_TRY(hipMemcpy(redo.data(), ctx->asm_redo.p + 1, redo.size() * 4, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(redo.data(), ctx->asm_redo.p, redo.size() * 4, hipMemcpyDeviceToHost));
             uint64_t su = 0, sr = 0;
             uint32_t mu = 0, mi = 0;
             for (uint32_t r : redo) {
@@ -865,8 +865,7 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
                 mi = std::max(mi, rg.n_inner);
                 for (uint32_t l = 0; l < rg.hap_count; l++) sr += B.haps[rg.hap_begin + l].n_druns;
             }
-            uint32_t why[8];
-            HIP_TRY(hipMemcpy(why, ctx->asm_why.p, 32, hipMemcpyDeviceToHost));
+            const uint32_t *why = ctx->asm_host + 8;
             fprintf(stderr, "tfbs assembly: %zu regions left to key_asm: mean haplotypes %.1f (max %u), max inner %u, "
                             "mean diff runs %.1f; reasons: shape %u lists %u runs %u refs %u arena(cor) %u arena(cnt) %u\n",
                     redo.size(), (double)su / redo.size(), mu, mi, (double)sr / redo.size(), why[0], why[1], why[2],

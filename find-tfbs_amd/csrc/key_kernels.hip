@@ -113,8 +113,8 @@ __device__ __forceinline__ void visit_refs(const AsmArgs &A, uint32_t r, const D
 }
 
 // One region per iteration: every region (list == nullptr, grid = regions) or the
-// list[0] regions at list + 1 over a fixed grid.
-__global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uint32_t *list) {
+// *list_n regions at list over a fixed grid.
+__global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uint32_t *list, const uint32_t *list_n) {
     __shared__ uint32_t s_cnt[kAsmCounters];
     __shared__ uint32_t s_rh[kAsmHaps];    // per haplotype: first staged run | runs << 16 (0xFFFFFFFF: not HAP_DEDUP)
     __shared__ uint2 s_run[kAsmRuns];      // the region's diff runs
@@ -125,9 +125,9 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
     __shared__ uint32_t s_nhit, s_nref, s_nvar, s_nput;
     __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t n_it = list ? list[0] : gridDim.x;
+    const uint32_t n_it = list ? *list_n : gridDim.x;
     for (uint32_t it = blockIdx.x; it < n_it; it += gridDim.x) {
-    const uint32_t r = list ? list[1 + it] : it;
+    const uint32_t r = list ? list[it] : it;
     __syncthreads();  // the previous region's LDS readers are done
     [&]() {
     const DevRegion rg = A.regions[r];
@@ -512,7 +512,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     }
     auto give_up = [&](uint32_t why) {  // workgroup-uniform, before any output
         if (tid == 0) {
-            A.redo[1 + atomicAdd(A.redo, 1u)] = r;
+            A.redo[atomicAdd(A.redo_n, 1u)] = r;
             if (A.why) atomicAdd(A.why + why, 1u);  // (TFBS_DEBUG_OVER: the reasons)
         }
     };
@@ -1239,7 +1239,8 @@ int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spi
 
 int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
     if (n_regions == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_asm_kernel, dim3(n_regions), dim3(kAsmBlock), 0, stream, a, (const uint32_t *)nullptr);
+    hipLaunchKernelGGL(key_asm_kernel, dim3(n_regions), dim3(kAsmBlock), 0, stream, a, (const uint32_t *)nullptr,
+                       (const uint32_t *)nullptr);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_asm_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
@@ -1247,15 +1248,23 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
 
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
     if (n_regions == 0) return TFBS_OK;
-    hipError_t e = hipMemsetAsync(a.redo, 0, 4, stream);
-    if (e == hipSuccess) e = hipMemsetAsync(a.cor_used, 0, 4, stream);
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast memset: ") + hipGetErrorString(e));
     hipLaunchKernelGGL(key_fast_kernel, dim3(n_regions), dim3(kFBlock), 0, stream, a);
     // the regions it left: a fixed grid over the list (no host round trip)
     hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
-                       (const uint32_t *)a.redo);
-    e = hipGetLastError();
+                       (const uint32_t *)a.redo, (const uint32_t *)a.redo_n);
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
+__global__ void asm_report_kernel(const uint32_t *__restrict__ over, uint32_t *__restrict__ ctr) {
+    if (threadIdx.x < 2) ctr[threadIdx.x] = over ? over[threadIdx.x] : 0u;
+}
+
+int launch_asm_report(const uint32_t *over, uint32_t *ctr, hipStream_t stream) {
+    hipLaunchKernelGGL(asm_report_kernel, dim3(1), dim3(64), 0, stream, over, ctr);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("asm_report_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 

@@ -48,9 +48,9 @@ struct AsmArgs {
     uint32_t *var_counts;
     uint64_t var_cap;
     unsigned long long *var_tot;
-    // regions key_fast_kernel leaves to key_asm_kernel (redo[0] of them at redo + 1):
+    // regions key_fast_kernel leaves to key_asm_kernel (*redo_n of them at redo):
     // written by key_fast_kernel, worked through by key_asm_kernel's list pass
-    uint32_t *redo;
+    uint32_t *redo, *redo_n;
     uint32_t fast_max_u;  // key_fast_kernel takes regions of at most this many haplotypes (TFBS_KEY_FAST_MAXU)
     // key_fast_kernel's corrections of regions past its LDS list: shares of cor_arena
     // (cor_cap u32) taken from *cor_used (zeroed by launch_key_fast; read back by the host)
@@ -64,11 +64,13 @@ struct AsmArgs {
 // key_asm_kernel over every region (mode 0 or 1).
 int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 // The reduction (mode 0) in two launches, no host round trip: key_fast_kernel
-// takes every region whose haplotypes, keys, hits and reference hits fit its LDS
-// lists (all of them at BASELINE shapes) and appends the others to a.redo, which
-// key_asm_kernel then works through (a fixed grid looping over the list).
-// a.redo[0] must be zero (launch_key_fast clears it on the stream).
+// takes every region within its limits (all of them at BASELINE shapes) and
+// appends the others to a.redo, which key_asm_kernel then works through (a fixed
+// grid looping over the list).  *a.redo_n, *a.cor_used and a.var_tot must be zero.
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
+// ctr[0], ctr[1] = over[0], over[1] (the scan's overflow counters next to the
+// assembly's, for one copy back).
+int launch_asm_report(const uint32_t *over, uint32_t *ctr, hipStream_t stream);
 uint32_t key_asm_lds_counters();  // regions with more distinct haplotypes use AsmArgs::scratch
 // Buckets the spill records (ScanArgs::spill, *over of cap) by region: boff[r]
 // .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters).
