@@ -636,6 +636,9 @@ __shared__ uint32_t g_ioff[kWvItems + 1];
 __shared__ uint32_t g_red[kWv / 64];
 __shared__ uint32_t g_pub[kWvItems];  // item i's end bit + 1 (0: not yet known; wv_place)
 __shared__ uint32_t g_agg[kWvItems];  // item i's bit count + 1 (0: not yet known; wv_place)
+// TFBS_BGZF_PROF counts: wv_place's waits; items all-run, with look-back matches,
+// with whole-token literals, with byte literals; heads; newlines
+__shared__ uint32_t g_pstat[8];
 
 // A lane's bit stream: symbols gathered in a register, ORed into g_bits 32 bits at
 // a time (two LDS atomics at most per 32 bits, not per symbol)
@@ -745,6 +748,7 @@ __device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_
         const uint32_t ks = have ? (uint32_t)__builtin_ctzll(have) : 64u;  // nearest known end
         const bool need = j >= 0 && lane < ks;
         if (__ballot(need && agg == 0)) {  // a count between not published yet: look again
+            if (lane == 0) atomicAdd(&g_pstat[0], 1u);
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
@@ -792,6 +796,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
             v.tok_at = v.cum_at = v.g_lo = v.ncum = 0;
         }
     }
+    if (A.prof && lane == 0) atomicAdd(&g_pstat[kind == IT_NL ? 6 : 5], kind != IT_GROUP ? 1u : 0u);
     if (kind == IT_NL) {
         const uint32_t base = wv_place(i, 8, lane);
         if (lane == 0) {
@@ -911,6 +916,16 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     } else if (in) {
         for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
+    if (A.prof) {
+        const bool all_run = __ballot(run) == ~0ull, lb = __ballot(dist != 0) != 0, wl = __ballot(!runm && !dist && whole_lit) != 0,
+                   bl = __ballot(!runm && !dist && !whole_lit && in) != 0;
+        if (lane == 0) {
+            if (all_run) atomicAdd(&g_pstat[1], 1u);
+            if (lb) atomicAdd(&g_pstat[2], 1u);
+            if (wl) atomicAdd(&g_pstat[3], 1u);
+            if (bl) atomicAdd(&g_pstat[4], 1u);
+        }
+    }
     const uint32_t base = wv_place(i, wave_sum(nb), lane);
     LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
     if (runm) {
@@ -936,6 +951,13 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     const uint64_t b0 = (A.block0 + blockIdx.x) * kBgzfRaw;
     const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
     const uint64_t e = b0 + n;
+    // phase clocks (TFBS_BGZF_PROF): start, staged, items listed, items done, CRC, end
+    uint64_t *const pf = A.prof ? A.prof + 16 * (size_t)blockIdx.x : nullptr;
+    auto stamp = [&](int k) {
+        if (pf && tid == 0) pf[k] = clock64();
+    };
+    stamp(0);
+    if (tid < 8) g_pstat[tid] = 0;
     {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const BlockPlan *>(A.plans) + blockIdx.x);
         for (uint32_t i = tid; i < sizeof(BlockPlan) / 4; i += kWv) reinterpret_cast<uint32_t *>(&S.P)[i] = src[i];
@@ -963,6 +985,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         }
     }
     __syncthreads();
+    stamp(1);
     // the staged tokens' literal codes (bytes past a text's length zeroed: the text's
     // dwords are ORed into g_text whole)
     {
@@ -1032,10 +1055,12 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     }
     __syncthreads();
     const uint32_t n_items = g_ioff[kWvItems];
+    stamp(2);
     // the items in one pass (wv_item: the bytes, the bit count, the chained offset, the
     // bits); a block that does not shrink to the bit buffer is stored instead
     for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item(A, C, b0, e, i, lane);
     __syncthreads();
+    stamp(3);
     const uint32_t total_bits = g_pub[n_items - 1] - 1 + 7;  // BFINAL + BTYPE, symbols, end of block
     const uint32_t dbytes = (total_bits + 7) / 8;
     const bool stored = dbytes > 4 * kBitWords;
@@ -1068,6 +1093,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         if (lane == 0) g_red[wave] = crc;
         __syncthreads();
     }
+    stamp(4);
     uint8_t *out = A.out + (size_t)blockIdx.x * kBgzfMax;
     const uint32_t clen = stored ? 5 + n : dbytes;
     const uint32_t bsize = 18 + clen + 8;
@@ -1094,6 +1120,11 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         for (int i = 0; i < 4; i++) out[18 + clen + i] = (uint8_t)(crc32 >> (8 * i));
         for (int i = 0; i < 4; i++) out[18 + clen + 4 + i] = (uint8_t)(n >> (8 * i));
         A.out_len[blockIdx.x] = bsize;
+    }
+    stamp(5);
+    if (pf && tid == 0) {
+        pf[6] = n_items;
+        for (int k = 0; k < 8; k++) pf[8 + k] = g_pstat[k];
     }
 }
 

@@ -29,6 +29,7 @@ struct BgArgs {
     const uint32_t *crc_ops;    // kBgzfOps x 32 columns
     const uint32_t *crc_ops64;  // bgzf_crc_ops64_count() x 32 columns: shifts by 64 k bytes
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
+    uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 16 words of phase clocks and counts
 };
 size_t bgzf_plan_bytes();
 

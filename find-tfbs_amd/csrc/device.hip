@@ -179,6 +179,7 @@ struct tfbs_ctx {
     DevBuf<char> bg_heads, bg_tok_text;
     DevBuf<uint8_t> bg_tok_len, bg_plans;
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
+    DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
     // two slots of block batches (one being made, one copied back and written)
     static constexpr int kBgSlots = 3;  // batches of blocks in flight: two queued while one is written out
     DevBuf<uint8_t> bg_out[kBgSlots], bg_packed[kBgSlots];
@@ -525,7 +526,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
-    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release();
+    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release();
     for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
         ctx->bg_host[k].release();
@@ -1221,6 +1222,31 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
 // GPU (older batches written out as newer ones queue: BgPipe).  plan and heads (its
 // heads as uploaded) must stay untouched until one of this piece's batches has been
 // written out.
+
+// TFBS_BGZF_PROF: the launch's bgzf_wave_kernel phase clocks (debug; synchronises).
+static int bgzf_prof_report(tfbs_ctx *ctx, uint32_t nb) {
+    std::vector<uint64_t> h((size_t)nb * 16);
+    HIP_TRY(hipMemcpyAsync(h.data(), ctx->bg_prof.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    double ph[5] = {0, 0, 0, 0, 0}, items = 0, st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t nw = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint64_t *p = &h[(size_t)b * 16];
+        if (!p[5]) continue;  // a bgzf_block_kernel block
+        nw++;
+        for (int k = 0; k < 5; k++) ph[k] += (double)(p[k + 1] - p[k]);
+        items += (double)p[6];
+        for (int k = 0; k < 8; k++) st[k] += (double)p[8 + k];
+    }
+    const double d = nw ? nw : 1;
+    fprintf(stderr,
+            "[bgzf prof] blocks %u wave %u cycles/block: stage %.0f list %.0f items %.0f crc %.0f out %.0f; per block: "
+            "items %.1f spins %.1f all-run %.1f look-back %.1f token-lit %.1f byte-lit %.1f heads %.1f newlines %.1f\n",
+            nb, nw, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, items / d, st[0] / d, st[1] / d, st[2] / d,
+            st[3] / d, st[4] / d, st[5] / d, st[6] / d);
+    return TFBS_OK;
+}
+
 int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::vector<char> &heads, int fd,
                      BgPipe &pp) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -1290,7 +1316,13 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
         a.block0 = b0;
         a.out = ctx->bg_out[k].p;
         a.out_len = ctx->bg_out_len[k].p;
-        if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) ||
+        static const bool prof = env_int("TFBS_BGZF_PROF", 0) != 0;
+        if (prof) {
+            if ((rc = ctx->bg_prof.ensure((size_t)nb * 16))) return rc;
+            HIP_TRY(hipMemsetAsync(ctx->bg_prof.p, 0, (size_t)nb * 128, ctx->stream));
+            a.prof = ctx->bg_prof.p;
+        }
+        if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) || (prof && (rc = bgzf_prof_report(ctx, nb))) ||
             (rc = tfbs::launch_bgzf_compact(ctx->bg_out[k].p, ctx->bg_out_len[k].p, ctx->bg_off[k].p, nb,
                                             ctx->bg_packed[k].p, ctx->stream)))
             return rc;

@@ -14,3 +14,10 @@ for rep in 1 2; do
     echo "step $lib: $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/$T/step_$lib.json | head -1) $(grep -o '"step_device_ms": {[^}]*}' gpurun_out/$T/step_$lib.json)"
   done
 done
+unset TFBS_LIB
+for thr in 1e-4 1e-5 1e-6; do
+  timeout -k 10 300 python3 bench.py --threshold $thr --steps 5 --warmup 2 --no-cpu --no-e2e > gpurun_out/$T/thr_$thr.json 2>/dev/null || { echo "bench thr $thr failed"; exit 1; }
+  echo "threshold $thr: $(grep -o '"step_device_ms": {[^}]*}' gpurun_out/$T/thr_$thr.json)"
+done
+TFBS_BGZF_PROF=1 timeout -k 10 300 python3 tools/bgzf_only.py 1000 > gpurun_out/$T/bgzf_prof.txt 2>&1 || { tail -5 gpurun_out/$T/bgzf_prof.txt; exit 1; }
+grep "bgzf prof" gpurun_out/$T/bgzf_prof.txt | head -3; tail -1 gpurun_out/$T/bgzf_prof.txt
