@@ -118,7 +118,7 @@ struct BlockPlan {
 struct Stage {
     BlockPlan P;
     DevRow rows[kStRowDesc];  // rows r_first ..
-    uint8_t codes[kStCodes];
+    alignas(16) uint8_t codes[kStCodes];  // (dword reads: wv_item's look-back)
     uint8_t tlen[kStTok];
     alignas(16) uint8_t text[kStTok * kRowTokBytes];
     uint32_t cum[kStCum];
@@ -676,10 +676,10 @@ __device__ __forceinline__ void wv_lit(LaneBits &o, uint32_t b) {
     if (b < 144) wv_put(o, rev(0x30 + b, 8), 8);
     else wv_put(o, rev(0x190 + b - 144, 9), 9);
 }
-// RFC 1951 3.2.5 codes of a match: bits, and (kWrite) the symbols
-template <bool kWrite>
-__device__ __forceinline__ uint32_t wv_match(LaneBits &off, uint32_t len, uint32_t dist) {
-    uint32_t sym, xb = 0, xv = 0;
+// RFC 1951 3.2.5: a match's codes as they go into the stream (LSB first) and
+// their bit count (<= 8 + 5 + 5 + 13 = 31), one put
+__device__ __forceinline__ uint2 match_code(uint32_t len, uint32_t dist) {
+    uint32_t sym, xv = 0, xb = 0;
     if (len == 258) {
         sym = 285;
     } else if (len <= 10) {
@@ -690,7 +690,7 @@ __device__ __forceinline__ uint32_t wv_match(LaneBits &off, uint32_t len, uint32
         xb = nb - 2;
         xv = x & ((1u << xb) - 1u);
     }
-    uint32_t dc, db = 0, dv = 0;
+    uint32_t dc, dv = 0, db = 0;
     if (dist <= 4) {
         dc = dist - 1;
     } else {
@@ -699,15 +699,20 @@ __device__ __forceinline__ uint32_t wv_match(LaneBits &off, uint32_t len, uint32
         db = nb - 1;
         dv = x & ((1u << db) - 1u);
     }
-    const uint32_t sn = sym < 280 ? 7u : 8u;
-    if (kWrite) {
-        if (sym < 280) wv_put(off, rev(sym - 256, 7), 7);
-        else wv_put(off, rev(0xC0 + sym - 280, 8), 8);
-        wv_put(off, xv, xb);
-        wv_put(off, rev(dc, 5), 5);
-        wv_put(off, dv, db);
+    uint32_t v, at;
+    if (sym < 280) {
+        v = rev(sym - 256, 7);
+        at = 7;
+    } else {
+        v = rev(0xC0 + sym - 280, 8);
+        at = 8;
     }
-    return sn + xb + 5 + db;
+    v |= xv << at;
+    at += xb;
+    v |= rev(dc, 5) << at;
+    at += 5;
+    v |= dv << at;
+    return uint2{v, at + db};
 }
 
 // wave64 inclusive prefix sum with DPP (GFX9 row shifts within 16 lanes, then the
@@ -859,11 +864,38 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const uint32_t sl = sb ? 63u - (uint32_t)__builtin_clzll(sb) : lane;
     const uint32_t el = ea ? (uint32_t)__builtin_ctzll(ea) : lane;
     const int32_t S0 = __shfl(rel, sl), S1 = __shfl(rel + (int32_t)t, el);
+    // the same text among the 8 before it, inside the block: the nearest, from the
+    // 8 packed codes before the sample (a zero-field test of codes ^ c), its distance
+    // from the texts' offsets (a lane of this item, or the token lengths between);
+    // 8-bit codes and a row's first 8 samples: sample by sample
     uint32_t dist = 0;
-    if (full && !run && t >= 3) {  // the same text among the 8 before it, inside the block
+    const bool want = full && !run && t >= 3;
+    const bool packed = want && v.R.width <= 4 && s >= kLookback;
+    uint32_t kk = 0, P = 0;
+    if (packed) {
+        const uint32_t w = v.R.width, bit0 = (s - kLookback) * w, a = (uint32_t)(v.cbase + (int32_t)(bit0 >> 3));
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(g_st.codes) + (a >> 2);
+        const uint64_t x = (uint64_t)dw[0] | ((uint64_t)dw[1] << 32);
+        P = (uint32_t)(x >> (8 * (a & 3u) + (bit0 & 7u)));  // field k: sample s - 8 + k
+        const uint32_t R = w == 2 ? 0x5555u : 0x11111111u, H = R << (w - 1), M = H - R;
+        if (w == 2) P &= 0xFFFFu;
+        const uint32_t X = P ^ (c * R), Z = ~(((X & M) + M) | X | M) & H;
+        if (Z) kk = kLookback - ((31u - __builtin_clz(Z)) >> (w == 2 ? 1 : 2));
+    }
+    const int32_t rsrc = __shfl(rel, (int)(lane - min(kk, lane)));
+    if (kk) {
+        uint32_t acc;
+        if (kk <= lane) {
+            acc = (uint32_t)(rel - rsrc);
+        } else {  // sample s - kk is in the group before
+            acc = 0;
+            for (uint32_t k = 1; k <= kk; k++) acc += C.tlen(v, (P >> ((kLookback - k) * v.R.width)) & v.mask);
+        }
+        if (rel >= (int32_t)acc) dist = acc;
+    } else if (want && !packed) {
         uint32_t acc = 0;
-        for (uint32_t kk = 1; kk <= kLookback && kk <= s; kk++) {
-            const uint32_t cc = C.code(v, s - kk);
+        for (uint32_t k = 1; k <= kLookback && k <= s; k++) {
+            const uint32_t cc = C.code(v, s - k);
             acc += C.tlen(v, cc);
             if (rel < (int32_t)acc) break;
             if (cc == c) {
@@ -905,12 +937,14 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const uint32_t tn = in ? g_tlitn[v.tok_at + c] : 0u;
     const bool whole_lit = full && tn != kNoTokLit;
     uint32_t nb = 0;
-    LaneBits dummy{0, 0, 0};
+    uint2 mc0{0, 0}, mc1{0, 0};  // the text's match codes
     if (runm) {
-        if (m1) nb += wv_match<false>(dummy, m1, t);
-        if (m2) nb += wv_match<false>(dummy, m2, t);
+        if (m1) mc0 = match_code(m1, t);
+        if (m2) mc1 = match_code(m2, t);
+        nb = mc0.y + mc1.y;
     } else if (dist) {
-        nb = wv_match<false>(dummy, t, dist);
+        mc0 = match_code(t, dist);
+        nb = mc0.y;
     } else if (whole_lit) {
         nb = tn;
     } else if (in) {
@@ -928,11 +962,9 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     }
     const uint32_t base = wv_place(i, wave_sum(nb), lane);
     LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
-    if (runm) {
-        if (m1) wv_match<true>(off, m1, t);
-        if (m2) wv_match<true>(off, m2, t);
-    } else if (dist) {
-        wv_match<true>(off, t, dist);
+    if (runm || dist) {
+        wv_put(off, mc0.x, mc0.y);
+        wv_put(off, mc1.x, mc1.y);
     } else if (whole_lit) {
         const uint4 L = g_tlit[v.tok_at + c];
         const uint32_t lw[4] = {L.x, L.y, L.z, L.w};

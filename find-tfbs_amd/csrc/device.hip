@@ -332,16 +332,23 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
         HIP_TRY(hipMemsetAsync(ctx->over.p, 0, 8, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
-        HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+        // one stream per depth launch (launch_mfma: one per K depth), side streams
+        // forked and joined only when there is more than one (small batches: no
+        // cross-stream waits)
+        int n_depths = 0;
+        for (size_t k = 0; k < P.m_supers.size(); k++)
+            n_depths += (k == 0 || P.m_supers[k].nk != P.m_supers[k - 1].nk) ? 1 : 0;
+        const int n_side = std::min(n_depths - 1, (int)tfbs_ctx::kSide);
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
-        for (int i = 0; i < tfbs_ctx::kSide; i++) {
+        if (n_side > 0) HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
+        for (int i = 0; i < n_side; i++) {
             HIP_TRY(hipStreamWaitEvent(ctx->side[i], ctx->fork, 0));
             streams[i + 1] = ctx->side[i];
         }
         const int n = launch_mfma(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words, n_haps,
-                                  streams, tfbs_ctx::kSide + 1, ctx->srcs_host, &ctx->n_srcs);
+                                  streams, (uint32_t)n_side + 1, ctx->srcs_host, &ctx->n_srcs);
         if (n < 0) return n;
-        for (int i = 0; i < tfbs_ctx::kSide; i++) {
+        for (int i = 0; i < n_side; i++) {
             HIP_TRY(hipEventRecord(ctx->join[i], ctx->side[i]));
             HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->join[i], 0));
         }
@@ -388,10 +395,6 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
     return launches;
 }
 
-// The last scan's overflow lists must have held every entry (a dropped
-// candidate may hide a hit, a dropped spill record is a lost count): read the
-// counters copied back after it and, if one overflowed, grow the lists and scan
-// again.  Runs before anything reads the scan's results.
 // The last scan's overflow lists must have held every entry (a dropped
 // candidate may hide a hit, a dropped spill record is a lost count): read the
 // counters copied back after it and, if one overflowed, grow the lists and scan
@@ -784,7 +787,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
     const uint32_t nr = (uint32_t)B.regions.size();
     if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
-        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(16)) ||
+        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(16 + (size_t)std::max<uint32_t>(1, nr) + 1)) ||
         (rc = ctx->asm_redo.ensure((size_t)nr + 1)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
         return rc;
     if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 64, hipHostMallocDefault));
@@ -801,6 +804,9 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
     const bool mfma = !ctx->plan.m_supers.empty();
+    // the assembly's counters and the spill buckets' (at asm_ctr + 16): one memset
+    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0, (16 + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4,
+                           ctx->stream));
     if (mfma && post) {
         if (!ctx->post_done) {  // (once per scan: the rescoring appends spill records)
             const int f = launch_post_scan(ctx->last_margs, ctx->stream);
@@ -808,7 +814,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
             ctx->post_done = true;
         }
         if ((rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, std::max<uint32_t>(1, nr),
-                                       ctx->spill_bcnt.p, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream)))
+                                       ctx->asm_ctr.p + 16, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream, true)))
             return rc;
     }
     AsmArgs a = asm_args(ctx, B, 0);
@@ -827,9 +833,10 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.cor_used = ctx->asm_ctr.p + 3;
     a.cor_lds = ctx->key_cor_lds;
     a.why = ctx->debug_over ? ctx->asm_ctr.p + 8 : nullptr;
-    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0, 64, ctx->stream));
+    a.report_src = mfma ? ctx->over.p : nullptr;  // (copied by the list pass: no report launch)
+    a.report = ctx->asm_ctr.p;
     if ((rc = launch_key_fast(a, nr, ctx->stream)) ||
-        (rc = launch_asm_report(mfma ? ctx->over.p : nullptr, ctx->asm_ctr.p, ctx->stream)))
+        (nr == 0 && (rc = launch_asm_report(a.report_src, ctx->asm_ctr.p, ctx->stream))))
         return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->asm_ctr.p, 64, hipMemcpyDeviceToHost, ctx->stream));

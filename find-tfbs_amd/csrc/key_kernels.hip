@@ -125,6 +125,7 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
     __shared__ uint32_t s_nhit, s_nref, s_nvar, s_nput;
     __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (list && A.report && blockIdx.x == 0 && tid < 2) A.report[tid] = A.report_src ? A.report_src[tid] : 0u;
     const uint32_t n_it = list ? *list_n : gridDim.x;
     for (uint32_t it = blockIdx.x; it < n_it; it += gridDim.x) {
     const uint32_t r = list ? list[it] : it;
@@ -1226,8 +1227,8 @@ int launch_code_compact(const uint8_t *codes, uint32_t n_keys, uint32_t n_sample
 }
 
 int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spill, uint32_t n_regions, uint32_t *bcnt,
-                         uint32_t *boff, uint32_t *sorted, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(bcnt, 0, (size_t)(n_regions + 1) * 4, stream);
+                         uint32_t *boff, uint32_t *sorted, hipStream_t stream, bool bcnt_zeroed) {
+    hipError_t e = bcnt_zeroed ? hipSuccess : hipMemsetAsync(bcnt, 0, (size_t)(n_regions + 1) * 4, stream);
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("spill bucket memset: ") + hipGetErrorString(e));
     hipLaunchKernelGGL(spill_hist_kernel, dim3(64), dim3(256), 0, stream, over, cap, spill, bcnt);
     hipLaunchKernelGGL(spill_scan_kernel, dim3(1), dim3(1024), 0, stream, over, bcnt, n_regions, boff);

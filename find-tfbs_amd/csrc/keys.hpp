@@ -59,6 +59,10 @@ struct AsmArgs {
     uint32_t *cor_used;
     uint32_t cor_lds;  // corrections kept in LDS at most (TFBS_KEY_COR_LDS, tests: the arena path)
     uint32_t *why;     // debug (TFBS_DEBUG_OVER): key_fast_kernel's give-ups per reason (8 counters), or null
+    // launch_key_fast's list pass also copies report_src[0..1] (the scan's overflow
+    // counters; null: zeros) to report[0..1] (null: not)
+    const uint32_t *report_src;
+    uint32_t *report;
 };
 
 // key_asm_kernel over every region (mode 0 or 1).
@@ -73,9 +77,10 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 int launch_asm_report(const uint32_t *over, uint32_t *ctr, hipStream_t stream);
 uint32_t key_asm_lds_counters();  // regions with more distinct haplotypes use AsmArgs::scratch
 // Buckets the spill records (ScanArgs::spill, *over of cap) by region: boff[r]
-// .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters).
+// .. boff[r + 1] of sorted (bcnt: n_regions + 1 scratch counters, zeroed here
+// unless bcnt_zeroed).
 int launch_spill_buckets(const uint32_t *over, uint32_t cap, const uint32_t *spill, uint32_t n_regions, uint32_t *bcnt,
-                         uint32_t *boff, uint32_t *sorted, hipStream_t stream);
+                         uint32_t *boff, uint32_t *sorted, hipStream_t stream, bool bcnt_zeroed = false);
 // A region's distinct haplotype pairs and each sample's pair (rows[r]: the device
 // address of region r's u16 membership row, 0 to skip it): pab / pcnt at
 // r * kEncMaxPairs, pair_n[r] (UINT32_MAX: skipped or too many pairs), pidx at r * n_samples.
