@@ -853,8 +853,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const int32_t lo = max(rel, 0), hi = min(rel + (int32_t)t, n);
     const bool in = valid && hi > lo;
     const bool full = in && rel >= 0 && rel + (int32_t)t <= n;
-    uint32_t prevc = (uint32_t)__shfl_up((int)c, 1);
-    if (lane == 0) prevc = s > 0 ? C.code(v, s - 1) : 0xFFFFFFFFu;
+    const uint32_t prevc = valid && s > 0 ? C.code(v, s - 1) : 0xFFFFFFFFu;
     const bool run = full && prevc == c && rel >= (int32_t)t && t >= 1;
     // the wave's runs: a run's first and last texts
     const uint64_t rm = __ballot(run);
@@ -933,48 +932,59 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     } else if (in) {
         for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
     }
-    // its bits, its place in the block's stream, its symbols
+    // its bits, its place in the block's stream, its symbols: a match or two, or a
+    // whole token's literal codes, as up to 4 words (LSB first) that go into the
+    // stream with at most two LDS ORs each; texts cut by the block's edges and tokens
+    // of more than 128 bits of literals go byte by byte (rare)
     const uint32_t tn = in ? g_tlitn[v.tok_at + c] : 0u;
     const bool whole_lit = full && tn != kNoTokLit;
-    uint32_t nb = 0;
-    uint2 mc0{0, 0}, mc1{0, 0};  // the text's match codes
-    if (runm) {
-        if (m1) mc0 = match_code(m1, t);
-        if (m2) mc1 = match_code(m2, t);
-        nb = mc0.y + mc1.y;
-    } else if (dist) {
-        mc0 = match_code(t, dist);
-        nb = mc0.y;
+    const bool by_byte = in && !runm && !dist && !whole_lit;
+    uint32_t bw[4] = {0, 0, 0, 0}, bn = 0;
+    if (runm || dist) {
+        const uint2 a = runm ? (m1 ? match_code(m1, t) : uint2{0, 0}) : match_code(t, dist);
+        const uint2 b = runm && m2 ? match_code(m2, t) : uint2{0, 0};
+        const uint64_t x = (uint64_t)a.x | ((uint64_t)b.x << a.y);
+        bw[0] = (uint32_t)x;
+        bw[1] = (uint32_t)(x >> 32);
+        bn = a.y + b.y;
     } else if (whole_lit) {
-        nb = tn;
-    } else if (in) {
-        for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        const uint4 L = g_tlit[v.tok_at + c];
+        bw[0] = L.x;
+        bw[1] = L.y;
+        bw[2] = L.z;
+        bw[3] = L.w;
+        bn = tn;
     }
+    uint32_t nb = bn;
+    const bool any_bytes = __ballot(by_byte) != 0;
+    if (any_bytes && by_byte)
+        for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     if (A.prof) {
-        const bool all_run = __ballot(run) == ~0ull, lb = __ballot(dist != 0) != 0, wl = __ballot(!runm && !dist && whole_lit) != 0,
-                   bl = __ballot(!runm && !dist && !whole_lit && in) != 0;
+        const bool all_run = __ballot(run) == ~0ull, lb = __ballot(dist != 0) != 0,
+                   wl = __ballot(!runm && !dist && whole_lit) != 0;
         if (lane == 0) {
             if (all_run) atomicAdd(&g_pstat[1], 1u);
             if (lb) atomicAdd(&g_pstat[2], 1u);
             if (wl) atomicAdd(&g_pstat[3], 1u);
-            if (bl) atomicAdd(&g_pstat[4], 1u);
+            if (any_bytes) atomicAdd(&g_pstat[4], 1u);
         }
     }
     const uint32_t base = wv_place(i, wave_sum(nb), lane);
-    LaneBits off{0, 0, base + wave_excl_sum(nb, lane)};
-    if (runm || dist) {
-        wv_put(off, mc0.x, mc0.y);
-        wv_put(off, mc1.x, mc1.y);
-    } else if (whole_lit) {
-        const uint4 L = g_tlit[v.tok_at + c];
-        const uint32_t lw[4] = {L.x, L.y, L.z, L.w};
+    const uint32_t off = base + wave_excl_sum(nb, lane);
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-            if (tn > 32u * j) off.put(lw[j], min(tn - 32u * j, 32u));
-    } else if (in) {
-        for (int32_t q = lo; q < hi; q++) wv_lit(off, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+    for (uint32_t k = 0; k < 4; k++) {
+        if (!__ballot(bn > 32 * k)) break;
+        if (bn > 32 * k) {
+            const uint32_t o = off + 32 * k, w = o >> 5, sh = o & 31, nk = min(bn - 32 * k, 32u);
+            if (w <= kBitWords) atomicOr(&g_bits[w], bw[k] << sh);
+            if (sh + nk > 32 && w < kBitWords) atomicOr(&g_bits[w + 1], bw[k] >> (32 - sh));
+        }
     }
-    off.finish();
+    if (any_bytes && by_byte) {
+        LaneBits o{0, 0, off};
+        for (int32_t q = lo; q < hi; q++) wv_lit(o, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        o.finish();
+    }
 }
 
 __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
