@@ -770,12 +770,15 @@ __device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_
 
 // Item i of the block (all lanes of a wave together), in one pass: its bytes into
 // g_text, its bit count, its first bit (wv_place), its symbols.
-__device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane) {
-    const uint32_t item = g_item[i];
+// v / vkey: the wave's last item's row view and its key (item bits 20-31), kept
+// across the wave's items (consecutive ones are mostly groups of one row).
+__device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane,
+                        RowView &v, uint32_t &vkey) {
+    const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_item[i]);
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
     // the item's row as wave-uniform values (SGPRs: its arithmetic is scalar)
-    RowView v;
-    {
+    if ((item >> 20) != vkey) {
+        vkey = item >> 20;
         const DevRow &R = g_st.rows[d];
         auto u32 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
         auto u64 = [&](uint64_t x) { return (uint64_t)u32((uint32_t)x) | ((uint64_t)u32((uint32_t)(x >> 32)) << 32); };
@@ -1100,7 +1103,11 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     stamp(2);
     // the items in one pass (wv_item: the bytes, the bit count, the chained offset, the
     // bits); a block that does not shrink to the bit buffer is stored instead
-    for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item(A, C, b0, e, i, lane);
+    {
+        RowView v{};
+        uint32_t vkey = ~0u;
+        for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item(A, C, b0, e, i, lane, v, vkey);
+    }
     __syncthreads();
     stamp(3);
     const uint32_t total_bits = g_pub[n_items - 1] - 1 + 7;  // BFINAL + BTYPE, symbols, end of block
