@@ -325,6 +325,7 @@ def main():
     batch = shard_batch(T, ps, args, rank, world, window_lmax=ps_all.max_length if parts > 1 else None,
                         build_device=None if args.host_build else local)
     dev_regions, host_regions = batch.build_stats()
+    patched_regions = batch.patch_stats()
     t_prep = time.perf_counter() - t_prep
     gen_s, build_s, prep_wall, fill_s = batch.prep_seconds()  # prep_wall: build_region + commit, no generation
     t_up = time.perf_counter()
@@ -533,6 +534,7 @@ def main():
                 "rows": int(tot_rows),
                 "regions_grouped_on_device": int(dev_regions),
                 "regions_built_on_host": int(host_regions),
+                "regions_grouped_on_device_patched_on_host": int(patched_regions),
             },
             "kernel_ms_avg": kms,
             "dense_download_s": t_dense,

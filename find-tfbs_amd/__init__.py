@@ -304,6 +304,12 @@ class RegionBatch:
         check(lib().tfbs_batch_build_stats(self.h, C.byref(d), C.byref(h)))
         return d.value, h.value
 
+    def patch_stats(self):
+        """Regions grouped on the device whose distinct groups the host patched."""
+        p = C.c_uint64()
+        check(lib().tfbs_batch_patch_stats(self.h, C.byref(p)))
+        return p.value
+
     def __del__(self):
         if getattr(self, "h", None):
             lib().tfbs_batch_destroy(self.h)

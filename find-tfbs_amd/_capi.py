@@ -87,6 +87,7 @@ SIGNATURES = [
     ("tfbs_batch_set_window_lmax", C.c_int, [vp, C.c_uint32]),
     ("tfbs_batch_set_build_device", C.c_int, [vp, C.c_int]),
     ("tfbs_batch_build_stats", C.c_int, [vp, u64p, u64p]),
+    ("tfbs_batch_patch_stats", C.c_int, [vp, u64p]),
     ("tfbs_batch_region_ext", C.c_int, [vp, C.c_uint64, C.c_uint64, u64p, u64p]),
     ("tfbs_batch_region_begin", C.c_int, [vp, C.c_uint64, C.c_uint64, C.c_char_p, C.c_size_t]),
     ("tfbs_batch_region_add_inner", C.c_int, [vp, C.c_uint32, C.c_uint64, C.c_uint64]),

@@ -702,6 +702,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
         if (rcs[j]) return rcs[j];
         if (built[j].dev || built[j].dev_grouped) B.dev_regions++;
         else B.host_regions++;
+        if (built[j].dev_grouped) B.patched_regions++;
     }
     return TFBS_OK;
 }
@@ -1091,6 +1092,12 @@ int tfbs_batch_build_stats(const tfbs_batch *b, uint64_t *dev_regions, uint64_t 
     if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (dev_regions) *dev_regions = b->b.dev_regions;
     if (host_regions) *host_regions = b->b.host_regions;
+    return TFBS_OK;
+}
+
+int tfbs_batch_patch_stats(const tfbs_batch *b, uint64_t *patched_regions) {
+    if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (patched_regions) *patched_regions = b->b.patched_regions;
     return TFBS_OK;
 }
 

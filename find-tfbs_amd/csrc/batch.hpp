@@ -186,6 +186,7 @@ struct Batch {
         if (grouper) grouper->recycle(memb_allocs);
     }
     uint64_t dev_regions = 0, host_regions = 0;  // regions grouped on the device / built on the host
+    uint64_t patched_regions = 0;                // of dev_regions: distinct groups patched on the host
 
     uint64_t device_bytes() const;
 };

@@ -186,14 +186,21 @@ int tfbs_batch_set_window_lmax(tfbs_batch *b, uint32_t lmax);
  * (before the first region; device < 0: host only): a region whose applied
  * records are all SNVs inside its window (REF = the window's base, ALT another of
  * A/C/G/T, at most 64, one per position, carrier ids ascending) and whose window
- * has no N gets its haplotypes' diff masks, distinct groups and membership
- * computed there (the membership stays on the device, a u16 distinct index per
- * haplotype id, fetched only when a host path needs it); every other region, and
- * one of more than 2 047 distinct diff masks, is built on the host.  The batch is
- * the same either way (tfbs_batch_region_input_digest). */
+ * has no N gets its haplotypes' diff masks, distinct groups, patched and packed
+ * haplotypes and membership computed there (the membership stays on the device, a
+ * u16 distinct index per haplotype id, fetched only when a host path needs it).  A
+ * region with indels or N whose applied records are at most 64 distinct diffs with
+ * ascending carriers is grouped there (distinct masks, carrier counts, membership:
+ * the O(haplotypes x records) part) and the host patches only its distinct groups
+ * (TFBS_DEV_PATCH=0: built on the host).  Every other region, and one of more than
+ * 2 047 distinct diff masks, is built on the host.  The batch is the same either
+ * way (tfbs_batch_region_input_digest). */
 int tfbs_batch_set_build_device(tfbs_batch *b, int device);
 /* Regions grouped on the device / built on the host so far. */
 int tfbs_batch_build_stats(const tfbs_batch *b, uint64_t *dev_regions, uint64_t *host_regions);
+/* Of the regions grouped on the device, those whose distinct groups the host
+ * patched (indels / N). */
+int tfbs_batch_patch_stats(const tfbs_batch *b, uint64_t *patched_regions);
 /* main.rs:404-407: the halo-extended window of a merged region. */
 int tfbs_batch_region_ext(const tfbs_batch *b, uint64_t merged_start, uint64_t merged_end, uint64_t *ext_start,
                           uint64_t *ext_end);
