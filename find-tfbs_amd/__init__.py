@@ -628,6 +628,11 @@ class BcfReader:
         check(lib().tfbs_bcf_select(self.h, arr, len(idx)))
         self.selected = idx
 
+    def set_carriers_mode(self, on=True):
+        """Records keep load_diffs' carrier ids (and the ploidy check) instead of raw GT."""
+        check(lib().tfbs_bcf_set_carriers_mode(self.h, 1 if on else 0))
+        self.carriers_mode = bool(on)
+
     def __del__(self):
         if getattr(self, "h", None):
             lib().tfbs_bcf_close(self.h)
@@ -644,9 +649,16 @@ class BcfReader:
             gt = _capi.i32p()
             check(lib().tfbs_bcf_record(self.h, i, C.byref(pos), C.byref(rlen), C.byref(na), C.byref(ref),
                                         C.byref(alt), C.byref(gt)))
-            out.append({"pos0": pos.value, "rlen": rlen.value, "n_alleles": na.value, "ref": ref.value.decode(),
-                        "alt": alt.value.decode() if alt.value is not None else None,
-                        "gt": [[gt[2 * s], gt[2 * s + 1]] for s in range(ns)]})
+            rec = {"pos0": pos.value, "rlen": rlen.value, "n_alleles": na.value, "ref": ref.value.decode(),
+                   "alt": alt.value.decode() if alt.value is not None else None}
+            if getattr(self, "carriers_mode", False):
+                ids, nc, st = _capi.u32p(), C.c_size_t(), C.c_int()
+                check(lib().tfbs_bcf_record_carriers(self.h, i, C.byref(ids), C.byref(nc), C.byref(st)))
+                rec["carriers"] = [ids[k] for k in range(nc.value)]
+                rec["gt_status"] = st.value
+            else:
+                rec["gt"] = [[gt[2 * s], gt[2 * s + 1]] for s in range(ns)]
+            out.append(rec)
         return out
 
 

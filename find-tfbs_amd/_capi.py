@@ -138,6 +138,8 @@ SIGNATURES = [
     ("tfbs_bcf_indexed", C.c_int, [vp]),
     ("tfbs_bcf_sample_name", C.c_char_p, [vp, C.c_size_t]),
     ("tfbs_bcf_fetch", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_size_t)]),
+    ("tfbs_bcf_set_carriers_mode", C.c_int, [vp, C.c_int]),
+    ("tfbs_bcf_record_carriers", C.c_int, [vp, C.c_size_t, C.POINTER(u32p), C.POINTER(C.c_size_t), C.POINTER(C.c_int)]),
     ("tfbs_bcf_record", C.c_int, [vp, C.c_size_t, u64p, u32p, u32p, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p),
                                   C.POINTER(i32p)]),
     ("tfbs_fasta_fetch", C.c_int, [C.c_char_p, C.c_char_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_void_p),

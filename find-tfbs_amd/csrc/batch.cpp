@@ -1178,6 +1178,23 @@ int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const c
     return TFBS_OK;
 }
 
+int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                    const std::vector<uint32_t> &carriers, int gt_status, Record &r) {
+    if (n_alleles < 2 || !alt) return fail(TFBS_E_ALLELES, "record with one allele (haplotype.rs:22)");
+    if (!ref) return fail(TFBS_E_ARG, "null argument");
+    r = Record();
+    r.pos = pos;
+    r.n_alleles = n_alleles;
+    int rc = to_codes(ref, r.ref);
+    if (!rc) rc = to_codes(alt, r.alt);
+    if (rc) return rc;
+    if (n_alleles == 2) {
+        if (gt_status) return fail(gt_status, "Inconsistent number of alleles");
+        r.carriers = carriers;
+    }
+    return TFBS_OK;
+}
+
 // Builds regions on up to `threads` host threads, commits them in order.
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads) {
     std::vector<RegionBuilt> built;

@@ -246,6 +246,11 @@ void forget_var_counts(Batch &B);
 int add_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads);
 int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
                    const int32_t *gt, Record &r);
+// The same from a record whose carriers the BCF reader found while decoding it
+// (Bcf::set_carriers_mode): gt_status is its ploidy check, raised here as
+// make_record_gt would (after the allele count and the REF / ALT bases).
+int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                    const std::vector<uint32_t> &carriers, int gt_status, Record &r);
 
 // haplotype.rs:94-156 over a reference window given as codes for positions
 // [ref_start, ref_start + n_ref).  Diffs are pointers to records.

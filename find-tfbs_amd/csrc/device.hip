@@ -180,6 +180,8 @@ struct tfbs_ctx {
     DevBuf<uint8_t> bg_tok_len, bg_plans;
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
+    DevBuf<uint64_t> kf_prof;         // TFBS_KF_PROF: key_fast_kernel phase clocks and sizes per region
+    bool kf_prof_on = false;
     // two slots of block batches (one being made, one copied back and written)
     static constexpr int kBgSlots = 3;  // batches of blocks in flight: two queued while one is written out
     DevBuf<uint8_t> bg_out[kBgSlots], bg_packed[kBgSlots];
@@ -529,7 +531,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
-    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release();
+    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release(); ctx->kf_prof.release();
     for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
         ctx->bg_host[k].release();
@@ -573,6 +575,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_hpb = (uint32_t)std::min((int)kMMaxHapsPerBlock, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 6 bits in a window list entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
+    ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
     ctx->key_cor_lds = (uint32_t)std::max(0, env_int("TFBS_KEY_COR_LDS", 1 << 30));
     ctx->cor_cap = (uint32_t)std::max(1, env_int("TFBS_KEY_COR_CAP", 1 << 22));
@@ -835,6 +838,11 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.why = ctx->debug_over ? ctx->asm_ctr.p + 8 : nullptr;
     a.report_src = mfma ? ctx->over.p : nullptr;  // (copied by the list pass: no report launch)
     a.report = ctx->asm_ctr.p;
+    if (ctx->kf_prof_on && nr) {
+        if ((rc = ctx->kf_prof.ensure((size_t)nr * 16))) return rc;
+        HIP_TRY(hipMemsetAsync(ctx->kf_prof.p, 0, (size_t)nr * 128, ctx->stream));
+        a.prof = ctx->kf_prof.p;
+    }
     if ((rc = launch_key_fast(a, nr, ctx->stream)) ||
         (nr == 0 && (rc = launch_asm_report(a.report_src, ctx->asm_ctr.p, ctx->stream))))
         return rc;
@@ -851,6 +859,31 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
 // Waits for the enqueued assembly and checks its lists: a scan overflow list that
 // dropped entries means a rescan with larger lists (and a new assembly), a full
 // varying-key list a new assembly with larger ones.
+// TFBS_KF_PROF: key_fast_kernel's mean phase cycles and sizes over the regions it
+// finished (debug; synchronises).
+static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
+    std::vector<uint64_t> h((size_t)nr * 16);
+    HIP_TRY(hipMemcpy(h.data(), ctx->kf_prof.p, h.size() * 8, hipMemcpyDeviceToHost));
+    double ph[6] = {0, 0, 0, 0, 0, 0}, sz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mx = 0;
+    uint32_t n = 0;
+    for (uint32_t r = 0; r < nr; r++) {
+        const uint64_t *p = &h[(size_t)r * 16];
+        if (!p[6]) continue;  // empty, or left to key_asm_kernel
+        n++;
+        for (int k = 0; k < 6; k++) ph[k] += (double)(p[k + 1] - p[k]);
+        mx = std::max(mx, (double)(p[6] - p[0]));
+        for (int k = 0; k < 8; k++) sz[k] += (double)p[8 + k];
+    }
+    const double d = n ? n : 1;
+    fprintf(stderr,
+            "[kf prof] regions %u of %u cycles/region: descr+hitn %.0f refs %.0f dirty %.0f lists %.0f keys %.0f "
+            "chunks %.0f (max total %.0f); per region: U %.1f entries %.1f dirty-refs %.1f corrections %.1f rows "
+            "%.1f chunks %.2f in-LDS %.2f refs %.1f\n",
+            n, nr, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, ph[5] / d, mx, sz[0] / d, sz[1] / d,
+            sz[2] / d, sz[3] / d, sz[4] / d, sz[5] / d, sz[6] / d, sz[7] / d);
+    return TFBS_OK;
+}
+
 static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
     auto grow = [](uint32_t &cap, uint32_t need, uint64_t lim) {
         if (need > cap) cap = (uint32_t)std::min<uint64_t>(lim, (uint64_t)need * 5 / 4 + 1024);
@@ -904,6 +937,7 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
             continue;
         }
         ctx->asm_state = 2;
+        if (ctx->kf_prof_on && (rc = kf_prof_report(ctx, (uint32_t)B.regions.size()))) return rc;
     }
     return TFBS_OK;
 }

@@ -275,8 +275,38 @@ static void parse_bcf_header(const std::string &text, std::vector<std::string> &
 // One BCF2 record (l_shared, l_indiv, shared, indiv) at p.  GT is kept raw for
 // the samples in sel (all samples if sel is null): 2 ints each, vector_end and
 // absent values as INT32_MIN + 1.
+// Carriers of a bi-allelic record from its int8 diploid GT bytes g (2 per sample of
+// the file): byte j of sample k's pair carries id 2 k + side when it is Unphased(1)
+// (4) in slot 0 or Phased(1) (5) in slot 1 (haplotype.rs:27-36); a vector_end byte
+// (-127) in either slot is a ploidy error (haplotype.rs:24-26).  Without a sample
+// selection the bytes are swept 8 at a time (SWAR: most are 0|0 and skipped whole).
+static void gt8_carriers(const int8_t *g, size_t ns, const std::vector<size_t> *sel, std::vector<uint32_t> &car,
+                         int &status) {
+    car.clear();
+    auto one = [&](size_t k, int8_t a, int8_t b) {
+        if (a == -127 || b == -127) status = TFBS_E_PLOIDY;
+        if (a == 4) car.push_back((uint32_t)(2 * k));
+        if (b == 5) car.push_back((uint32_t)(2 * k + 1));
+    };
+    if (sel) {
+        for (size_t k = 0; k < sel->size(); k++) one(k, g[2 * (*sel)[k]], g[2 * (*sel)[k] + 1]);
+        return;
+    }
+    const uint64_t P = 0x0504050405040504ull, V = 0x8181818181818181ull, L = 0x0101010101010101ull,
+                   H = 0x8080808080808080ull;
+    size_t j = 0;
+    for (; j + 8 <= 2 * ns; j += 8) {
+        uint64_t x;
+        memcpy(&x, g + j, 8);
+        const uint64_t a = x ^ P, b = x ^ V;  // zero bytes: a carrier allele / a vector_end
+        if ((((a - L) & ~a) | ((b - L) & ~b)) & H)
+            for (size_t q = j; q < j + 8; q += 2) one(q / 2, g[q], g[q + 1]);
+    }
+    for (; j < 2 * ns; j += 2) one(j / 2, g[j], g[j + 1]);
+}
+
 static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, size_t ns, int gt_key,
-                             const std::vector<size_t> *sel, BcfRecord &r, int32_t &chrom) {
+                             const std::vector<size_t> *sel, bool carriers, BcfRecord &r, int32_t &chrom) {
     uint32_t l_shared, l_indiv;
     memcpy(&l_shared, p, 4);
     memcpy(&l_indiv, p + 4, 4);
@@ -314,7 +344,14 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         else if (a == 1) r.alt = al;
     }
     const size_t nk = sel ? sel->size() : ns;
-    r.gt.assign(2 * nk, INT32_MIN + 1);
+    r.carriers.clear();
+    r.gt_status = TFBS_OK;
+    if (carriers) {  // load_diffs' view of the record only (bi-allelic: carriers, ploidy)
+        r.gt.clear();
+        if (n_allele == 2 && nk) r.gt_status = TFBS_E_PLOIDY;  // (no GT field: every GT is empty)
+    } else {
+        r.gt.assign(2 * nk, INT32_MIN + 1);
+    }
     for (uint32_t f = 0; f < n_fmt; f++) {
         int kt;
         uint32_t kn;
@@ -325,7 +362,26 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
         const size_t sz = type_size(vt);
         if (!in.need(sz * vn * ns)) return fail(TFBS_E_PARSE, "truncated FORMAT data");
-        if (key == gt_key && vt == 1 && vn == 2) {  // the common diploid int8 layout
+        if (carriers) {
+            if (key == gt_key && n_allele == 2 && nk && vt >= 1 && vt <= 3) {
+                r.gt_status = vn >= 2 ? TFBS_OK : TFBS_E_PLOIDY;  // one value per sample: glen 1
+                if (vt == 1 && vn == 2) {
+                    gt8_carriers((const int8_t *)in.p, ns, sel, r.carriers, r.gt_status);
+                } else if (vn >= 2) {  // wider ints: the first two values of every sample
+                    const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
+                    for (size_t k = 0; k < nk; k++) {
+                        const size_t s = sel ? (*sel)[k] : k;
+                        Cur c{in.p + sz * vn * s, in.p + sz * vn * (s + 1)};
+                        int64_t a = 0, b = 0;
+                        read_int(c, vt, a);
+                        read_int(c, vt, b);
+                        if (a == ve || b == ve) r.gt_status = TFBS_E_PLOIDY;
+                        if (a == 4) r.carriers.push_back((uint32_t)(2 * k));
+                        if (b == 5) r.carriers.push_back((uint32_t)(2 * k + 1));
+                    }
+                }
+            }
+        } else if (key == gt_key && vt == 1 && vn == 2) {  // the common diploid int8 layout
             const int8_t *g = (const int8_t *)in.p;
             int32_t *o = r.gt.data();
             for (size_t k = 0; k < nk; k++) {
@@ -367,6 +423,12 @@ int Bcf::open(const std::string &p, uint32_t nthreads) {
     for (size_t i = 0; i < sel.size(); i++) sel[i] = i;
     all_samples = true;
     return TFBS_OK;
+}
+
+int Bcf::set_carriers_mode(bool on) {
+    carriers_mode = on;
+    cur = -1;  // the decoded records change: drop the window
+    return rewind();
 }
 
 int Bcf::select(const std::vector<size_t> &s) {
@@ -623,14 +685,14 @@ int Bcf::fill() {
     par_for(offs.size(), offs.size() >= 64 ? threads : 1, [&](size_t i) {
         const unsigned char *p = (const unsigned char *)dbuf.data() + offs[i];
         int32_t chrom;
-        rcs[i] = decode_bcf_record(p, end, samples.size(), gt_key, s, win[base + i], chrom);
+        rcs[i] = decode_bcf_record(p, end, samples.size(), gt_key, s, carriers_mode, win[base + i], chrom);
     });
     for (size_t i = 0; i < rcs.size(); i++)
         if (rcs[i]) {  // decode again on this thread for the (thread-local) error message
             const unsigned char *p = (const unsigned char *)dbuf.data() + offs[i];
             int32_t chrom;
             BcfRecord r;
-            return decode_bcf_record(p, end, samples.size(), gt_key, s, r, chrom);
+            return decode_bcf_record(p, end, samples.size(), gt_key, s, carriers_mode, r, chrom);
         }
     return TFBS_OK;
 }

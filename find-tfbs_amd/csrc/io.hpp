@@ -43,6 +43,13 @@ struct BcfRecord {
     uint32_t n_alleles = 0;
     std::string ref, alt;   // alleles[0], alleles[1] (alt empty if a single allele)
     std::vector<int32_t> gt;  // 2 raw GT ints per selected sample, INT32_MIN+1 = vector_end / absent
+    // carriers mode (Bcf::set_carriers_mode; raw gt left empty): load_diffs' carriers of
+    // a bi-allelic record (haplotype.rs:16-41: 2 k + 0 iff GT[0] = Unphased(1), 2 k + 1
+    // iff GT[1] = Phased(1), k the selected sample), found while the record is decoded
+    // on the reader's threads; gt_status TFBS_E_PLOIDY if some selected sample's GT
+    // does not have 2 alleles (raised when a region uses the record)
+    std::vector<uint32_t> carriers;
+    int gt_status = 0;
 };
 
 // Streaming BCF2 reader (f2; replaces rust_htslib's IndexedReader::fetch +
@@ -63,6 +70,8 @@ class Bcf {
     int open(const std::string &path, uint32_t threads = 0);
     // GT columns kept, in this order (default: all samples); rewinds the stream.
     int select(const std::vector<size_t> &sel);
+    // records keep their carriers instead of raw GT (the run flow; rewinds the stream)
+    int set_carriers_mode(bool on);
     int contig_index(const std::string &name) const;
     // records with pos < end && pos + rlen > beg, in file order; pointers stay
     // valid until the next fetch
@@ -94,6 +103,7 @@ class Bcf {
     int gt_key = -1;
     std::vector<size_t> sel;
     bool all_samples = true;
+    bool carriers_mode = false;
     int cur = -1;                       // contig of the window
     uint64_t last_beg = 0, last_pos = 0;
     std::vector<BcfRecord> win;         // window of decoded records of contig `cur`, file order

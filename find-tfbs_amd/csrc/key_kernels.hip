@@ -501,6 +501,11 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena;
     __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // TFBS_KF_PROF: phase clocks 0-7, then sizes (U, entries, dirty reference hits, rows, chunks)
+    auto stamp = [&](uint32_t k, uint64_t v) {
+        if (A.prof && tid == 0) A.prof[16 * (size_t)r + k] = v;
+    };
+    stamp(0, clock64());
     const DevRegion rg = A.regions[r];
     const uint32_t U = rg.hap_count, n_inner = rg.n_inner, K = A.n_slots * n_inner;
     const uint64_t ko = (uint64_t)rg.inner_off * A.n_slots;
@@ -572,6 +577,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     for (uint32_t t = tid; t < nl; t += kFBlock) lcnt += A.hitn[list_idx(t)];
     uint32_t n_ent = 0;
     (void)block_excl_scan(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    stamp(1, clock64());
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
     if (nruns >= 65536) return give_up(2);
 #pragma unroll
@@ -623,6 +629,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         if (tid < nref) s_ref[rank] = mine;
         __syncthreads();
     }
+    stamp(2, clock64());
     // D: per HAP_DEDUP haplotype the reference hits in its dirty windows (a run
     // [a, b] meets the columns [w, w + L - 1] of windows w in [a - L + 1, b]; the
     // hits in [a - 31, b] are tested with their strand's L <= 32, each once: runs
@@ -664,6 +671,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     }
     __syncthreads();
     if (!in_lds && s_arena == kFNone) return give_up(4);  // the host grows the arena for the next call
+    stamp(3, clock64());
     uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
     const uint2 *hitl = reinterpret_cast<const uint2 *>(A.hitl);
     for (uint32_t l0 = 0; l0 < nl; l0 += kFLists) {  // kFLists lists at a time: their offsets in LDS
@@ -723,6 +731,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     const uint32_t nw = (K + 31) / 32;
     for (uint32_t w = tid; w < nw; w += kFBlock) s_bits[w] = 0;
     __syncthreads();
+    stamp(4, clock64());
     const uint32_t ncor = s_ncor;  // <= need
     // touched keys: own hits (the dirty reference hits' keys are reference keys),
     // reference hits, every key of a LUT/generic slot; rows in key order
@@ -758,6 +767,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             }
         }
     }
+    stamp(5, clock64());
     auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
     // the counter block: LDS chunks of rows x U, or -- when that would take more than
     // 32 chunks (hundreds of haplotypes and keys: each chunk re-reads every
@@ -854,6 +864,15 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = cnt[rr * U + l];
         }
     }
+    stamp(6, clock64());
+    stamp(8, U);
+    stamp(9, n_ent);
+    stamp(10, nD);
+    stamp(11, ncor);
+    stamp(12, T);
+    stamp(13, (T + rows_per - 1) / rows_per);
+    stamp(14, in_lds);
+    stamp(15, nref);
 }
 
 // Spill bucketing: per-region record counts, their exclusive scan (one

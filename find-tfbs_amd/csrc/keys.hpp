@@ -63,6 +63,7 @@ struct AsmArgs {
     // counters; null: zeros) to report[0..1] (null: not)
     const uint32_t *report_src;
     uint32_t *report;
+    uint64_t *prof;  // debug (TFBS_KF_PROF): key_fast_kernel's phase clocks and sizes, 16 per region, or null
 };
 
 // key_asm_kernel over every region (mode 0 or 1).

@@ -104,6 +104,7 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     int rc = bcf.open(a->bcf, sh.threads);
     if (rc) return rc;
     if ((rc = bcf.select(S.sel))) return rc;  // GT decoded for these samples only
+    if ((rc = bcf.set_carriers_mode(true))) return rc;  // load_diffs' carriers found while decoding
     const int rid = bcf.contig_index(S.chrom);
     Fasta fasta;
     if ((rc = fasta.open(a->reference))) return rc;
@@ -168,8 +169,8 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
             if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
             for (const BcfRecord *br : recs) {
                 Record rec;
-                rc = make_record_gt((uint32_t)S.sel.size(), br->pos, br->n_alleles, br->ref.c_str(),
-                                    br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->gt.data(), rec);
+                rc = make_record_ids(br->pos, br->n_alleles, br->ref.c_str(),
+                                     br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->carriers, br->gt_status, rec);
                 if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
@@ -599,7 +600,21 @@ int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, 
     if (n_alleles) *n_alleles = r->n_alleles;
     if (ref) *ref = r->ref.c_str();
     if (alt) *alt = r->n_alleles >= 2 ? r->alt.c_str() : nullptr;
-    if (gt) *gt = r->gt.data();
+    if (gt) *gt = r->gt.empty() ? nullptr : r->gt.data();
+    return TFBS_OK;
+}
+
+int tfbs_bcf_set_carriers_mode(tfbs_bcf *b, int on) {
+    if (!b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    b->cur.clear();
+    return b->b.set_carriers_mode(on != 0);
+}
+int tfbs_bcf_record_carriers(const tfbs_bcf *b, size_t i, const uint32_t **ids, size_t *n, int *gt_status) {
+    if (!b || i >= b->cur.size()) return tfbs::fail(TFBS_E_ARG, "bad record index");
+    const tfbs::BcfRecord *r = b->cur[i];
+    if (ids) *ids = r->carriers.data();
+    if (n) *n = r->carriers.size();
+    if (gt_status) *gt_status = r->gt_status;
     return TFBS_OK;
 }
 

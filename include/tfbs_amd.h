@@ -412,6 +412,15 @@ int tfbs_bcf_fetch(tfbs_bcf *b, const char *chrom, uint64_t beg, uint64_t end, s
  * for a single-allele record. */
 int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, uint32_t *n_alleles, const char **ref,
                     const char **alt, const int32_t **gt);
+/* Carriers mode (on != 0; rewinds the stream): records keep load_diffs' carrier ids of a bi-allelic
+ * record (haplotype.rs:16-41: 2 k iff GT[0] = Unphased(1), 2 k + 1 iff GT[1] = Phased(1), k the
+ * selected sample), found on the reader's threads while decoding, instead of raw GT (tfbs_bcf_record
+ * then returns gt NULL).  tfbs_run reads its BCF this way. */
+int tfbs_bcf_set_carriers_mode(tfbs_bcf *b, int on);
+/* Record i of the last fetch in carriers mode: ascending carrier ids and the ploidy check
+ * (TFBS_OK, or TFBS_E_PLOIDY when a selected sample's GT does not hold 2 alleles,
+ * haplotype.rs:24-26); 0 ids for a record that is not bi-allelic. */
+int tfbs_bcf_record_carriers(const tfbs_bcf *b, size_t i, const uint32_t **ids, size_t *n, int *gt_status);
 /* Replaces bio fasta IndexedReader fetch(chrom, start, stop) + read (main.rs:156-161). */
 int tfbs_fasta_fetch(const char *fasta, const char *chrom, uint64_t start, uint64_t stop, char **out, size_t *n);
 /* BGZF writer as BGzWriter (main.rs:267-276): data blocks, `flushes` empty blocks, EOF block. */

@@ -180,3 +180,74 @@ def test_bcf_stream_rejects_unsorted(tmp_path):
     r = T.BcfReader(p)
     with pytest.raises(Exception, match="not sorted"):
         r.fetch("chr1", 0, 1000)
+
+
+def _carriers_from_gt(gt):
+    """load_diffs (haplotype.rs:16-41) on raw GT pairs: 2 k iff GT[0] = Unphased(1) (4),
+    2 k + 1 iff GT[1] = Phased(1) (5); a vector_end (INT32_MIN + 1) in either slot
+    makes glen != 2: the ploidy error."""
+    ve = -2 ** 31 + 1
+    ids, bad = [], False
+    for k, (a, b) in enumerate(gt):
+        bad |= a == ve or b == ve
+        if a == 4:
+            ids.append(2 * k)
+        if b == 5:
+            ids.append(2 * k + 1)
+    return ids, bad
+
+
+@pytest.mark.parametrize("sel", [None, [5, 3, 69, 0, 41, 41, 12]])
+def test_bcf_carriers_mode_matches_raw_gt(tmp_path, sel):
+    """The run flow's reader mode: carrier ids found while decoding (8 GT bytes at a
+    time without a selection) equal load_diffs on the raw GT of the same records --
+    carriers at every byte of a word, in the tail, both phasings, haploid / missing
+    samples (ploidy status) -- with and without a sample selection."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import struct
+
+    import numpy as np
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path / "s"), n_samples=70, n_regions=12, indel_pct=25, seed=6)
+    # hand-made records: 70 samples (140 GT bytes: 17 words + a 4-byte tail)
+    ns = 70
+    header = ("##fileformat=VCFv4.2\n##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+              "##contig=<ID=chr1,length=100000>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
+              "\t".join("S%d" % i for i in range(ns)) + "\n").encode() + b"\0"
+    body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+    rnd = np.random.default_rng(1)
+    gts = []
+    for pos in range(100, 1300, 100):
+        g = np.full((ns, 2), [2, 3], dtype=np.int8)           # 0|0
+        k = rnd.choice(ns, size=rnd.integers(0, 12), replace=False)
+        g[k, 0] = rnd.choice([4, 5, 2, 3], size=len(k))       # 1/., 1|., 0/., 0|.
+        g[k, 1] = rnd.choice([4, 5, 2, 3], size=len(k))
+        if pos == 300:
+            g[ns - 1, 1] = 5                                  # the last byte of the tail
+        if pos == 500:
+            g[:4] = [[4, 5]] * 4                              # a whole word of carriers
+        if pos == 700:
+            g[33, 1] = -127                                   # haploid sample: ploidy error
+        if pos == 900:
+            g[0, 0] = -127                                    # empty GT
+        gts.append(g)
+        body += synth_dataset.bcf_record(0, pos, "A", "C", g)
+    hand = str(tmp_path / "hand.bcf")
+    open(hand, "wb").write(synth_dataset.bgzf_blocks(body))
+    n_bad = n_car = 0
+    for path in (d["bcf"], hand):
+        raw, car = T.BcfReader(path), T.BcfReader(path)
+        if sel is not None:
+            raw.select(sel)
+            car.select(sel)
+        car.set_carriers_mode(True)
+        for b, e in ((0, 500), (400, 900), (850, 10 ** 9)):
+            rr, cc = raw.fetch("chr1", b, e), car.fetch("chr1", b, e)
+            assert [(r["pos0"], r["ref"], r["alt"]) for r in rr] == [(c["pos0"], c["ref"], c["alt"]) for c in cc]
+            for r, c in zip(rr, cc):
+                ids, bad = _carriers_from_gt(r["gt"])
+                assert c["carriers"] == ids, (path, r["pos0"])
+                assert (c["gt_status"] != 0) == bad, (path, r["pos0"])
+                n_bad += bad
+                n_car += len(ids)
+    assert n_car > 50 and (n_bad > 0 or sel is not None)
