@@ -84,6 +84,7 @@ struct tfbs_ctx {
     static constexpr int kSide = 3;
     hipStream_t side[kSide] = {};
     hipEvent_t fork = nullptr, join[kSide] = {};
+    hipEvent_t kf_fork = nullptr, kf_join = nullptr;  // the big-region key assembly on side[0]
     bool kernel_timed = false;
     float last_kernel_ms = 0.f;
     const Patterns *pats = nullptr;
@@ -181,6 +182,9 @@ struct tfbs_ctx {
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
     DevBuf<uint64_t> kf_prof;         // TFBS_KF_PROF: key_fast_kernel phase clocks and sizes per region
+    DevBuf<uint32_t> asm_order;       // the resident batch's regions by distinct haplotypes, most first
+    uint32_t asm_order_n = 0;         // regions asm_order holds (0: none)
+    uint32_t asm_order_big = 0;       // the first of them with more than key_fast_big_u() haplotypes
     bool kf_prof_on = false;
     // two slots of block batches (one being made, one copied back and written)
     static constexpr int kBgSlots = 3;  // batches of blocks in flight: two queued while one is written out
@@ -531,7 +535,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
-    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release(); ctx->kf_prof.release();
+    ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release(); ctx->kf_prof.release(); ctx->asm_order.release();
     for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
         ctx->bg_host[k].release();
@@ -554,6 +558,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
         if (ctx->join[i]) (void)hipEventDestroy(ctx->join[i]);
     }
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
+    if (ctx->kf_fork) (void)hipEventDestroy(ctx->kf_fork);
+    if (ctx->kf_join) (void)hipEventDestroy(ctx->kf_join);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -602,6 +608,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk0);
     if (e == hipSuccess) e = hipEventCreate(&ctx->evk1);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->kf_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->kf_join, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->over_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->asm_ev, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreate(&ctx->asm_t0);
@@ -720,6 +728,18 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
         (rc = ctx->asm_scratch.ensure(std::max<uint64_t>(big, 1))) ||
         (dense && (rc = ctx->counts.ensure(std::max<uint64_t>(B.n_counts, 1)))))
         return rc;
+    std::vector<uint32_t> order(B.regions.size());  // (alive until the stream sync below)
+    {  // key_fast_kernel's region order: most distinct haplotypes first (their workgroups run longest)
+        for (uint32_t i = 0; i < order.size(); i++) order[i] = i;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) {
+            return B.regions[x].hap_count > B.regions[y].hap_count;
+        });
+        if ((rc = ctx->asm_order.put(order, ctx->stream))) return rc;
+        ctx->asm_order_n = (uint32_t)order.size();
+        ctx->asm_order_big = 0;
+        while (ctx->asm_order_big < order.size() && B.regions[order[ctx->asm_order_big]].hap_count > key_fast_big_u())
+            ctx->asm_order_big++;
+    }
     if ((rc = build_lists(ctx, (uint32_t)B.haps.size()))) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->counts_live = dense;
@@ -838,12 +858,14 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.why = ctx->debug_over ? ctx->asm_ctr.p + 8 : nullptr;
     a.report_src = mfma ? ctx->over.p : nullptr;  // (copied by the list pass: no report launch)
     a.report = ctx->asm_ctr.p;
+    a.order = ctx->asm_order_n == nr ? ctx->asm_order.p : nullptr;
     if (ctx->kf_prof_on && nr) {
         if ((rc = ctx->kf_prof.ensure((size_t)nr * 16))) return rc;
         HIP_TRY(hipMemsetAsync(ctx->kf_prof.p, 0, (size_t)nr * 128, ctx->stream));
         a.prof = ctx->kf_prof.p;
     }
-    if ((rc = launch_key_fast(a, nr, ctx->stream)) ||
+    if ((rc = launch_key_fast(a, nr, a.order ? ctx->asm_order_big : 0, ctx->stream, ctx->side[0], ctx->kf_fork,
+                              ctx->kf_join)) ||
         (nr == 0 && (rc = launch_asm_report(a.report_src, ctx->asm_ctr.p, ctx->stream))))
         return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
@@ -873,6 +895,22 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
         for (int k = 0; k < 6; k++) ph[k] += (double)(p[k + 1] - p[k]);
         mx = std::max(mx, (double)(p[6] - p[0]));
         for (int k = 0; k < 8; k++) sz[k] += (double)p[8 + k];
+    }
+    std::vector<std::pair<double, uint32_t>> tot;  // (cycles, region)
+    for (uint32_t r = 0; r < nr; r++)
+        if (h[(size_t)r * 16 + 6]) tot.push_back({(double)(h[(size_t)r * 16 + 6] - h[(size_t)r * 16]), r});
+    std::sort(tot.begin(), tot.end());
+    if (!tot.empty()) {
+        auto pct = [&](double f) { return tot[std::min(tot.size() - 1, (size_t)(f * tot.size()))].first; };
+        fprintf(stderr, "[kf prof] total cycles p50 %.0f p90 %.0f p99 %.0f max %.0f; slowest regions (cycles U rows chunks "
+                        "corrections refs):", pct(0.5), pct(0.9), pct(0.99), tot.back().first);
+        for (size_t i = tot.size(); i-- > 0 && i + 6 > tot.size();) {
+            const uint64_t *p = &h[(size_t)tot[i].second * 16];
+            fprintf(stderr, " [%.0f %llu %llu %llu %llu %llu]", tot[i].first, (unsigned long long)p[8],
+                    (unsigned long long)p[12], (unsigned long long)p[13], (unsigned long long)p[11],
+                    (unsigned long long)p[15]);
+        }
+        fprintf(stderr, "\n");
     }
     const double d = n ? n : 1;
     fprintf(stderr,
@@ -1493,6 +1531,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
     std::vector<DevHap> haps{hm};
     std::vector<DevRegion> regions{DevRegion{0, 0, 0, 1, UINT32_MAX, 1, 0}};
     std::vector<int32_t> inner{0, 0}, posrel{0};
+    ctx->asm_order_n = 0;  // (this one-haplotype upload replaces the resident batch)
     const uint32_t wpp = (uint32_t)((n + 255) / 256 * 4);
     HIP_TRY(hipSetDevice(ctx->device));
     int rc;

@@ -425,22 +425,30 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
 #ifndef TFBS_KF_BLOCK
 #define TFBS_KF_BLOCK 256
 #endif
-constexpr int kFBlock = TFBS_KF_BLOCK;  // threads per region (the lists below scale with it)
-constexpr uint32_t kFWaves = kFBlock / 64;
 constexpr uint32_t kFMaxU = 2048;     // distinct haplotypes (11 bits of a correction)
-constexpr uint32_t kFHapLds = 4 * kFBlock;  // haplotypes whose reuse descriptor sits in LDS (the others: read again)
-constexpr uint32_t kFCor = 16 * kFBlock;    // corrections in LDS: own hits and dirty reference hits
-constexpr uint32_t kFRefs = kFBlock;        // reference hits
-constexpr uint32_t kFCnt = 16 * kFBlock;    // u32 counters of a chunk: rows x U
-constexpr uint32_t kFRuns = kFCnt / 2;  // diff runs of the region's HAP_DEDUP haplotypes staged (over the counters)
-constexpr uint32_t kFRows = 2 * kFBlock;    // rows (touched keys) per chunk
 constexpr uint32_t kFKeyWords = 512;  // touched-key bitmap: keys <= 16384
-constexpr uint32_t kFLists = kFBlock;       // scan hit lists over the region's haplotypes
 constexpr uint32_t kFBatch = 8;       // hit-list entries each thread has in flight
 constexpr uint32_t kFNone = 0xFFFFFFFFu;
-static_assert(kFMaxU % kFBlock == 0 && kFHapLds % kFBlock == 0 && kFKeyWords % kFBlock == 0 && kFLists <= kFBlock &&
-                  kFRefs <= kFBlock,
-              "key_fast_kernel's per-thread shares");
+// Two shapes of the kernel: the common one (TFBS_KF_BLOCK threads, ~51 KB of LDS,
+// three regions per CU) and one for regions of many distinct haplotypes (1 024
+// threads and ~154 KB of LDS: a whole CU, counter chunks of 24 Ki u32 -- 17 rows of
+// 1 400 haplotypes instead of 2, which sent such a region's counters to the
+// global arena).  HAP_LDS: haplotypes whose reuse descriptor sits in LDS (the
+// others: read again); COR: corrections in LDS; REFS: reference hits; CNT: u32
+// counters of a chunk (rows x U); ROWS: rows (touched keys) per chunk; LISTS: scan
+// hit lists staged at a time.
+template <int BLOCK, uint32_t HAP_LDS, uint32_t COR, uint32_t REFS, uint32_t CNT, uint32_t ROWS, uint32_t LISTS>
+struct KfShape {
+    static constexpr int kBlock = BLOCK;
+    static constexpr uint32_t kWaves = BLOCK / 64, kHapLds = HAP_LDS, kCor = COR, kRefs = REFS, kCnt = CNT,
+                              kRuns = CNT / 2, kRows = ROWS, kLists = LISTS;
+    static_assert(kFMaxU % BLOCK == 0 && HAP_LDS % BLOCK == 0 && LISTS <= BLOCK && REFS <= BLOCK,
+                  "key_fast_kernel's per-thread shares");
+};
+constexpr int kFB = TFBS_KF_BLOCK;
+using KfSmall = KfShape<kFB, 4 * kFB, 16 * kFB, kFB, 16 * kFB, 2 * kFB, kFB>;
+using KfBig = KfShape<1024, 2048, 8192, 256, 24576, 1024, 256>;
+constexpr uint32_t kFBigU = 384;  // regions of more distinct haplotypes take KfBig
 
 // correction: key << 12 | (-1) << 11 | local haplotype (key < 2^20)
 __device__ __forceinline__ uint32_t cor_entry(uint32_t key, uint32_t l, uint32_t neg) {
@@ -466,6 +474,7 @@ __device__ __forceinline__ void wave_push(uint32_t *list, uint32_t *n, uint32_t 
 }
 
 // Exclusive prefix of v over the workgroup (wave scans + the waves' totals in s_w).
+template <uint32_t kFWaves>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, uint32_t &total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = v;
@@ -488,7 +497,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
     return pre + x - v;
 }
 
-__global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
+template <class C>
+__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first) {
+    constexpr int kFBlock = C::kBlock;
+    constexpr uint32_t kFWaves = C::kWaves, kFHapLds = C::kHapLds, kFCor = C::kCor, kFRefs = C::kRefs,
+                       kFCnt = C::kCnt, kFRuns = C::kRuns, kFRows = C::kRows, kFLists = C::kLists;
+    constexpr uint32_t kPerW = kFKeyWords >= (uint32_t)kFBlock ? kFKeyWords / kFBlock : 1u;  // key words per thread
     __shared__ uint32_t s_cor[kFCor];
     __shared__ uint4 s_ref[kFRefs];          // make_ref, sorted by window
     __shared__ uint32_t s_hap[kFHapLds];     // HAP_DEDUP: its first run (from the region's first) | runs << 16; else kFNone
@@ -500,7 +514,8 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     __shared__ uint32_t s_w[kFWaves];
     __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena;
     __shared__ unsigned long long s_vbase, s_obase;
-    const uint32_t r = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t r = A.order ? A.order[first + blockIdx.x] : first + blockIdx.x, tid = threadIdx.x, lane = tid & 63,
+                   wave = tid >> 6;
     // TFBS_KF_PROF: phase clocks 0-7, then sizes (U, entries, dirty reference hits, rows, chunks)
     auto stamp = [&](uint32_t k, uint64_t v) {
         if (A.prof && tid == 0) A.prof[16 * (size_t)r + k] = v;
@@ -576,7 +591,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     uint32_t lcnt = 0;  // the region's entries (an upper bound of its hits: groups are shared)
     for (uint32_t t = tid; t < nl; t += kFBlock) lcnt += A.hitn[list_idx(t)];
     uint32_t n_ent = 0;
-    (void)block_excl_scan(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    (void)block_excl_scan<kFWaves>(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
     stamp(1, clock64());
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
     if (nruns >= 65536) return give_up(2);
@@ -615,7 +630,17 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     __syncthreads();
     const uint32_t nref = s_nref;
     if (nref > kFRefs) return give_up(3);
-    {  // the reference hits by window (rank sort; ties by list position)
+    // D: per HAP_DEDUP haplotype the reference hits in its dirty windows (a run
+    // [a, b] meets the columns [w, w + L - 1] of window w).  Up to 64 Ki (haplotype,
+    // reference hit) pairs are tested pairwise -- a wave's lanes are hpw haplotypes x
+    // rpl hits, every run of the lane's haplotype tried (<= 16) -- so the waves share
+    // the work and no lane walks a chain of LDS reads; past that the hits are sorted
+    // by window and each haplotype walks its runs over them (a hit in [a - 31, b] of
+    // run [a, b] tested once: runs ascend, the cursor only moves forward).
+    // f(l, ref hit, dirty): in pairwise mode called by every lane of the wave together
+    // (uniform = true), else only for dirty pairs.
+    const bool pairwise = (uint64_t)U * nref <= 65536;
+    if (!pairwise) {  // the reference hits by window (rank sort; ties by list position)
         uint4 mine = make_uint4(0, 0, 0, 0);
         uint32_t rank = 0;
         if (tid < nref) {
@@ -630,12 +655,31 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         __syncthreads();
     }
     stamp(2, clock64());
-    // D: per HAP_DEDUP haplotype the reference hits in its dirty windows (a run
-    // [a, b] meets the columns [w, w + L - 1] of windows w in [a - L + 1, b]; the
-    // hits in [a - 31, b] are tested with their strand's L <= 32, each once: runs
-    // ascend and the cursor only moves forward).  f(l, ref hit) per dirty pair.
+    const uint32_t rpl = nref <= 1 ? 1u : nref >= 64 ? 64u : 1u << (32 - __clz(nref - 1));  // hits per lane group
+    const uint32_t hpw = 64 / rpl;                                                         // haplotypes per wave
     auto each_dirty = [&](auto &&f) {
         if (!nref) return;
+        if (pairwise) {
+            for (uint32_t l0 = wave * hpw; l0 < U; l0 += kFWaves * hpw) {
+                const uint32_t l = l0 + lane / rpl;
+                for (uint32_t p0 = 0; p0 < nref; p0 += rpl) {
+                    const uint32_t p = p0 + lane % rpl;
+                    uint4 q = make_uint4(0, 0, 0, 0);
+                    bool dirty = false;
+                    if (l < U && p < nref) {
+                        const uint32_t x = hap_info(l);
+                        if (x != kFNone) {
+                            q = s_ref[p];
+                            const uint32_t k0 = x & 0xFFFFu, k1 = k0 + (x >> 16);
+                            for (uint32_t k = k0; k < k1 && !dirty; k++)
+                                dirty = run_meets(runs[k].x, runs[k].y, q.y, q.z & 0xFFFFu);
+                        }
+                    }
+                    f(l, q, dirty, true);
+                }
+            }
+            return;
+        }
         for (uint32_t l = tid; l < U; l += kFBlock) {
             const uint32_t x = hap_info(l);
             if (x == kFNone) continue;
@@ -650,15 +694,15 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
                     bool dirty = false;
                     for (uint32_t k2 = k0; k2 < k1 && !dirty; k2++)
                         dirty = run_meets(runs[k2].x, runs[k2].y, q.y, q.z & 0xFFFFu);
-                    if (dirty) f(l, q);
+                    if (dirty) f(l, q, true, false);
                 }
             }
         }
     };
     uint32_t nd = 0;
-    each_dirty([&](uint32_t, const uint4 &q) { nd += __popc(q.w); });
+    each_dirty([&](uint32_t, const uint4 &q, bool dirty, bool) { nd += dirty ? __popc(q.w) : 0u; });
     uint32_t nD = 0;
-    (void)block_excl_scan(nd, s_w, nD);
+    (void)block_excl_scan<kFWaves>(nd, s_w, nD);
     // the corrections' list: LDS when they fit, else a share of the launch's arena
     const uint32_t need = n_ent + (sp.y - sp.x) + nD;  // (an upper bound: entries of other regions' haplotypes)
     const bool in_lds = need <= min(kFCor, A.cor_lds);
@@ -683,7 +727,7 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             s_lidx[tid] = idx;
         }
         uint32_t tot = 0;
-        const uint32_t off = block_excl_scan(lc, s_w, tot);
+        const uint32_t off = block_excl_scan<kFWaves>(lc, s_w, tot);
         if (tid < nlc) s_loff[tid] = off;
         if (tid == 0) s_loff[nlc] = tot;
         __syncthreads();
@@ -722,11 +766,25 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         }
         wave_push(cor, &s_ncor, need, want, v);
     }
-    each_dirty([&](uint32_t l, const uint4 &q) {
-        for (uint32_t m = q.w; m; m &= m - 1) {
-            const uint32_t at = atomicAdd(&s_ncor, 1u);
-            if (at < need) cor[at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
+    each_dirty([&](uint32_t l, const uint4 &q, bool dirty, bool uniform) {
+        const uint32_t c = dirty ? __popc(q.w) : 0u;
+        uint32_t at;
+        if (uniform) {  // one LDS atomic per wave: an inclusive scan of the lanes' entries
+            uint32_t x = c;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+                if (lane >= (uint32_t)o) x += y;
+            }
+            const uint32_t tot = (uint32_t)__shfl((int)x, 63);
+            uint32_t base = 0;
+            if (lane == 0 && tot) base = atomicAdd(&s_ncor, tot);
+            at = (uint32_t)__shfl((int)base, 0) + x - c;
+        } else {
+            at = atomicAdd(&s_ncor, c);
         }
+        for (uint32_t m = q.w; c && m; m &= m - 1, at++)
+            if (at < need) cor[at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
     });
     const uint32_t nw = (K + 31) / 32;
     for (uint32_t w = tid; w < nw; w += kFBlock) s_bits[w] = 0;
@@ -750,14 +808,14 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
     __syncthreads();
     uint32_t T = 0;
     {
-        constexpr uint32_t per = kFKeyWords / kFBlock;
+        constexpr uint32_t per = kPerW;
         uint32_t mine = 0;
 #pragma unroll
         for (uint32_t q = 0; q < per; q++) {
             const uint32_t w = tid * per + q;
             if (w < nw) mine += __popc(s_bits[w]);
         }
-        uint32_t run = block_excl_scan(mine, s_w, T);
+        uint32_t run = block_excl_scan<kFWaves>(mine, s_w, T);
 #pragma unroll
         for (uint32_t q = 0; q < per; q++) {
             const uint32_t w = tid * per + q;
@@ -793,23 +851,31 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
             A.key_flags[ko + j] = 0;
         }
     const uint64_t dense_base = A.dense_base ? A.haps[hb].count_off : 0;
+    // the corrections by row (key << 12 becomes row << 12: no row_of per chunk)
+    for (uint32_t e = tid; e < ncor; e += kFBlock) {
+        const uint32_t c = cor[e];
+        cor[e] = (row_of(cor_key(c)) << 12) | (c & 4095u);
+    }
+    uint32_t dedup_bits = 0;  // bit i: haplotype lane + 64 i takes the reference's counts as its base
+    for (uint32_t i = 0, l = lane; l < U; i++, l += 64)
+        if (hap_info(l) != kFNone) dedup_bits |= 1u << i;
     for (uint32_t t0 = 0; t0 < T; t0 += rows_per) {
         const uint32_t nrow = min(rows_per, T - t0);
-        __syncthreads();  // s_rbase written / the previous chunk's readers done
+        __syncthreads();  // s_rbase / cor rows written, the previous chunk's readers done
         if (tid == 0) s_nvar = 0;
-        for (uint32_t rr = tid; rr < nrow; rr += kFBlock) {  // the row's key: the word whose rows start at or before it
-            const uint32_t t = t0 + rr;
-            uint32_t lo = 0, hi = nw - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) / 2;
-                if (s_rbase[mid] <= t) lo = mid;
-                else hi = mid - 1;
+        {  // each row's key, from the key words this thread scanned (rows [s_rbase[w], ..))
+            constexpr uint32_t per = kPerW;
+#pragma unroll
+            for (uint32_t q = 0; q < per; q++) {
+                const uint32_t w = tid * per + q;
+                if (w >= nw) continue;
+                uint32_t t = s_rbase[w], b = s_bits[w];
+                if (t >= t0 + nrow || t + __popc(b) <= t0) continue;
+                for (; b; b &= b - 1, t++)
+                    if (t - t0 < nrow) s_rkey[t - t0] = 32 * w + __builtin_ctz(b);
             }
-            uint32_t b = s_bits[lo];
-            for (uint32_t k = t - s_rbase[lo]; k; k--) b &= b - 1;
-            s_rkey[rr] = 32 * lo + __builtin_ctz(b);
-            s_rr[rr] = 0;
         }
+        for (uint32_t rr = tid; rr < nrow; rr += kFBlock) s_rr[rr] = 0;
         __syncthreads();
         if (tid < nref)  // R: reference hits per key
             for (uint32_t m = s_ref[tid].w; m; m &= m - 1) {
@@ -820,14 +886,14 @@ __global__ __launch_bounds__(kFBlock) void key_fast_kernel(AsmArgs A) {
         for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {  // the base of every haplotype
             const uint32_t j = s_rkey[rr], R = s_rr[rr];
             const bool dense = A.any_dense && !A.slot_mfma[j / n_inner];
-            for (uint32_t l = lane; l < U; l += 64)
+            for (uint32_t i = 0, l = lane; l < U; i++, l += 64)
                 cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
-                                        : (hap_info(l) != kFNone ? R : 0u);
+                                        : ((dedup_bits >> i) & 1u ? R : 0u);
         }
         __syncthreads();
         for (uint32_t e = tid; e < ncor; e += kFBlock) {
             const uint32_t c = cor[e];
-            const uint32_t t = row_of(cor_key(c)) - t0;
+            const uint32_t t = cor_key(c) - t0;  // (its row)
             if (t < nrow) atomicAdd(&cnt[t * U + cor_hap(c)], cor_neg(c) ? 0xFFFFFFFFu : 1u);
         }
         __syncthreads();
@@ -1266,13 +1332,29 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
     return TFBS_OK;
 }
 
-int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
+int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
+                    hipEvent_t fork, hipEvent_t join) {
     if (n_regions == 0) return TFBS_OK;
-    hipLaunchKernelGGL(key_fast_kernel, dim3(n_regions), dim3(kFBlock), 0, stream, a);
+    if (!a.order || !side) n_big = 0;
+    n_big = std::min(n_big, n_regions);
+    hipError_t e = hipSuccess;
+    if (n_big) {  // the regions of many haplotypes (order[0, n_big)) beside the others, on a side stream
+        if ((e = hipEventRecord(fork, stream)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(n_big), dim3(KfBig::kBlock), 0, side, a, 0u);
+            e = hipEventRecord(join, side);
+        }
+        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel (big): ") + hipGetErrorString(e));
+    }
+    if (n_regions > n_big)
+        hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(n_regions - n_big), dim3(KfSmall::kBlock), 0, stream, a,
+                           n_big);
+    if (n_big && (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess)
+        return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
     // the regions it left: a fixed grid over the list (no host round trip)
     hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
                        (const uint32_t *)a.redo, (const uint32_t *)a.redo_n);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
@@ -1289,5 +1371,6 @@ int launch_asm_report(const uint32_t *over, uint32_t *ctr, hipStream_t stream) {
 }
 
 uint32_t key_asm_lds_counters() { return kAsmCounters; }
+uint32_t key_fast_big_u() { return kFBigU; }
 
 }  // namespace tfbs

@@ -63,6 +63,9 @@ struct AsmArgs {
     // counters; null: zeros) to report[0..1] (null: not)
     const uint32_t *report_src;
     uint32_t *report;
+    // key_fast_kernel: workgroup b takes region order[b] (regions by distinct haplotypes,
+    // most first: the longest regions start first and do not trail the launch), or b
+    const uint32_t *order;
     uint64_t *prof;  // debug (TFBS_KF_PROF): key_fast_kernel's phase clocks and sizes, 16 per region, or null
 };
 
@@ -72,7 +75,12 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 // takes every region within its limits (all of them at BASELINE shapes) and
 // appends the others to a.redo, which key_asm_kernel then works through (a fixed
 // grid looping over the list).  *a.redo_n, *a.cor_used and a.var_tot must be zero.
-int launch_key_fast(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
+// a.order lists the regions with the n_big of more than key_fast_big_u() distinct
+// haplotypes first: those take the 1 024-thread kernel on `side` (forked from and
+// joined back into `stream` with the two events) beside the others.
+int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
+                    hipEvent_t fork, hipEvent_t join);
+uint32_t key_fast_big_u();
 // ctr[0], ctr[1] = over[0], over[1] (the scan's overflow counters next to the
 // assembly's, for one copy back).
 int launch_asm_report(const uint32_t *over, uint32_t *ctr, hipStream_t stream);
