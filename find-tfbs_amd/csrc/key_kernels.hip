@@ -446,7 +446,11 @@ struct KfShape {
                   "key_fast_kernel's per-thread shares");
 };
 constexpr int kFB = TFBS_KF_BLOCK;
+#ifdef TFBS_KF_LDS4  // (A/B: ~39 KB, four regions per CU)
+using KfSmall = KfShape<kFB, 2 * kFB, 13 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
+#else
 using KfSmall = KfShape<kFB, 4 * kFB, 16 * kFB, kFB, 16 * kFB, 2 * kFB, kFB>;
+#endif
 using KfBig = KfShape<1024, 2048, 8192, 256, 24576, 1024, 256>;
 constexpr uint32_t kFBigU = 384;  // regions of more distinct haplotypes take KfBig
 
@@ -512,7 +516,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     __shared__ uint32_t s_rkey[kFRows], s_rr[kFRows];  // per row of a chunk: its key; R(key), then its varying slot
     __shared__ uint32_t s_loff[kFLists + 1], s_lidx[kFLists];
     __shared__ uint32_t s_w[kFWaves];
-    __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena;
+    __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena, s_ndirty;
     __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t r = A.order ? A.order[first + blockIdx.x] : first + blockIdx.x, tid = threadIdx.x, lane = tid & 63,
                    wave = tid >> 6;
@@ -541,7 +545,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     const uint32_t hb = rg.hap_begin;
     const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
     if (tid == 0) {
-        s_ncor = s_nref = s_run1 = 0;
+        s_ncor = s_nref = s_run1 = s_ndirty = 0;
         s_run0 = kFNone;
     }
     __syncthreads();
@@ -588,10 +592,20 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         }
         return 0;
     };
-    uint32_t lcnt = 0;  // the region's entries (an upper bound of its hits: groups are shared)
-    for (uint32_t t = tid; t < nl; t += kFBlock) lcnt += A.hitn[list_idx(t)];
+    uint32_t lcnt = 0, lidx = 0;  // the region's entries (an upper bound of its hits: groups are shared)
+    for (uint32_t t = tid; t < nl; t += kFBlock) {
+        const uint32_t i = list_idx(t);
+        if (t == tid) lidx = i;
+        lcnt += A.hitn[i];
+    }
     uint32_t n_ent = 0;
-    (void)block_excl_scan<kFWaves>(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    const uint32_t loff = block_excl_scan<kFWaves>(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    const bool lists_staged = nl <= kFLists;  // one list per thread: its offset and index kept for the list pass
+    if (lists_staged && tid < nl) {
+        s_lidx[tid] = lidx;
+        s_loff[tid] = loff;
+    }
+    if (lists_staged && tid == 0) s_loff[nl] = n_ent;
     stamp(1, clock64());
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
     if (nruns >= 65536) return give_up(2);
@@ -699,11 +713,37 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
             }
         }
     };
+    // the slot of a lane's first of c entries: one counter atomic per wave (an
+    // inclusive scan of the lanes' counts) when the wave calls together, else per lane
+    auto slots = [&](uint32_t c, bool uniform, uint32_t *ctr) -> uint32_t {
+        if (!uniform) return atomicAdd(ctr, c);
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        const uint32_t tot = (uint32_t)__shfl((int)x, 63);
+        uint32_t base = 0;
+        if (lane == 0 && tot) base = atomicAdd(ctr, tot);
+        return (uint32_t)__shfl((int)base, 0) + x - c;
+    };
+    // pairwise mode lists the dirty corrections while counting them, at the top of
+    // s_cor downwards (the first kFCor); the walk lists them in a second pass
     uint32_t nd = 0;
-    each_dirty([&](uint32_t, const uint4 &q, bool dirty, bool) { nd += dirty ? __popc(q.w) : 0u; });
+    each_dirty([&](uint32_t l, const uint4 &q, bool dirty, bool uniform) {
+        const uint32_t c = dirty ? __popc(q.w) : 0u;
+        nd += c;
+        if (!uniform) return;
+        uint32_t at = slots(c, true, &s_ndirty);
+        for (uint32_t m = q.w; c && m; m &= m - 1, at++)
+            if (at < kFCor) s_cor[kFCor - 1 - at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
+    });
     uint32_t nD = 0;
     (void)block_excl_scan<kFWaves>(nd, s_w, nD);
-    // the corrections' list: LDS when they fit, else a share of the launch's arena
+    const bool dirty_listed = pairwise && nD <= kFCor;
+    // the corrections' list: LDS when they fit (own hits from the bottom, the dirty
+    // ones at the top), else a share of the launch's arena (the dirty ones first)
     const uint32_t need = n_ent + (sp.y - sp.x) + nD;  // (an upper bound: entries of other regions' haplotypes)
     const bool in_lds = need <= min(kFCor, A.cor_lds);
     if (tid == 0) {
@@ -711,26 +751,31 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         if (!in_lds) {
             const uint32_t at = atomicAdd(A.cor_used, need);
             if (at <= A.cor_cap && need <= A.cor_cap - at) s_arena = at;
+            if (dirty_listed) s_ncor = nD;
         }
     }
     __syncthreads();
     if (!in_lds && s_arena == kFNone) return give_up(4);  // the host grows the arena for the next call
     stamp(3, clock64());
     uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
+    if (!in_lds && dirty_listed)
+        for (uint32_t e = tid; e < nD; e += kFBlock) cor[e] = s_cor[kFCor - 1 - e];
     const uint2 *hitl = reinterpret_cast<const uint2 *>(A.hitl);
     for (uint32_t l0 = 0; l0 < nl; l0 += kFLists) {  // kFLists lists at a time: their offsets in LDS
         const uint32_t nlc = min(kFLists, nl - l0);
-        uint32_t lc = 0;
-        if (tid < nlc) {
-            const uint32_t idx = list_idx(l0 + tid);
-            lc = A.hitn[idx];
-            s_lidx[tid] = idx;
+        uint32_t tot = n_ent;
+        if (!lists_staged) {
+            uint32_t lc = 0;
+            if (tid < nlc) {
+                const uint32_t idx = list_idx(l0 + tid);
+                lc = A.hitn[idx];
+                s_lidx[tid] = idx;
+            }
+            const uint32_t off = block_excl_scan<kFWaves>(lc, s_w, tot);
+            if (tid < nlc) s_loff[tid] = off;
+            if (tid == 0) s_loff[nlc] = tot;
+            __syncthreads();
         }
-        uint32_t tot = 0;
-        const uint32_t off = block_excl_scan<kFWaves>(lc, s_w, tot);
-        if (tid < nlc) s_loff[tid] = off;
-        if (tid == 0) s_loff[nlc] = tot;
-        __syncthreads();
         for (uint32_t e0 = 0; e0 < tot; e0 += kFBlock * kFBatch) {  // kFBatch loads in flight per thread
             uint2 h[kFBatch];
 #pragma unroll
@@ -766,34 +811,23 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         }
         wave_push(cor, &s_ncor, need, want, v);
     }
-    each_dirty([&](uint32_t l, const uint4 &q, bool dirty, bool uniform) {
-        const uint32_t c = dirty ? __popc(q.w) : 0u;
-        uint32_t at;
-        if (uniform) {  // one LDS atomic per wave: an inclusive scan of the lanes' entries
-            uint32_t x = c;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = (uint32_t)__shfl_up((int)x, o);
-                if (lane >= (uint32_t)o) x += y;
-            }
-            const uint32_t tot = (uint32_t)__shfl((int)x, 63);
-            uint32_t base = 0;
-            if (lane == 0 && tot) base = atomicAdd(&s_ncor, tot);
-            at = (uint32_t)__shfl((int)base, 0) + x - c;
-        } else {
-            at = atomicAdd(&s_ncor, c);
-        }
-        for (uint32_t m = q.w; c && m; m &= m - 1, at++)
-            if (at < need) cor[at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
-    });
+    if (!dirty_listed)
+        each_dirty([&](uint32_t l, const uint4 &q, bool dirty, bool uniform) {
+            const uint32_t c = dirty ? __popc(q.w) : 0u;
+            uint32_t at = slots(c, uniform, &s_ncor);
+            for (uint32_t m = q.w; c && m; m &= m - 1, at++)
+                if (at < need) cor[at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
+        });
     const uint32_t nw = (K + 31) / 32;
     for (uint32_t w = tid; w < nw; w += kFBlock) s_bits[w] = 0;
     __syncthreads();
     stamp(4, clock64());
-    const uint32_t ncor = s_ncor;  // <= need
+    // the corrections: [0, nA) and, listed at the top of s_cor, [kFCor - nB, kFCor)
+    const uint32_t nA = s_ncor, nB = in_lds && dirty_listed ? nD : 0u, ncor = nA + nB;  // (nA <= need)
+    auto cor_at = [&](uint32_t e) -> uint32_t & { return e < nA ? cor[e] : s_cor[kFCor - nB + (e - nA)]; };
     // touched keys: own hits (the dirty reference hits' keys are reference keys),
     // reference hits, every key of a LUT/generic slot; rows in key order
-    for (uint32_t e = tid; e < ncor; e += kFBlock) {
+    for (uint32_t e = tid; e < nA; e += kFBlock) {
         const uint32_t c = cor[e];
         if (!cor_neg(c)) atomicOr(&s_bits[cor_key(c) >> 5], 1u << (cor_key(c) & 31u));
     }
@@ -853,8 +887,8 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     const uint64_t dense_base = A.dense_base ? A.haps[hb].count_off : 0;
     // the corrections by row (key << 12 becomes row << 12: no row_of per chunk)
     for (uint32_t e = tid; e < ncor; e += kFBlock) {
-        const uint32_t c = cor[e];
-        cor[e] = (row_of(cor_key(c)) << 12) | (c & 4095u);
+        uint32_t &c = cor_at(e);
+        c = (row_of(cor_key(c)) << 12) | (c & 4095u);
     }
     uint32_t dedup_bits = 0;  // bit i: haplotype lane + 64 i takes the reference's counts as its base
     for (uint32_t i = 0, l = lane; l < U; i++, l += 64)
@@ -892,7 +926,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         }
         __syncthreads();
         for (uint32_t e = tid; e < ncor; e += kFBlock) {
-            const uint32_t c = cor[e];
+            const uint32_t c = cor_at(e);
             const uint32_t t = cor_key(c) - t0;  // (its row)
             if (t < nrow) atomicAdd(&cnt[t * U + cor_hap(c)], cor_neg(c) ? 0xFFFFFFFFu : 1u);
         }
