@@ -186,6 +186,7 @@ struct tfbs_ctx {
     uint32_t asm_order_n = 0;         // regions asm_order holds (0: none)
     uint32_t asm_order_big = 0;       // the first of them with more than key_fast_big_u() haplotypes
     bool kf_prof_on = false;
+    bool kf_persistent = true;        // TFBS_KF_PERSIST=0: one workgroup per region
     // two slots of block batches (one being made, one copied back and written)
     static constexpr int kBgSlots = 3;  // batches of blocks in flight: two queued while one is written out
     DevBuf<uint8_t> bg_out[kBgSlots], bg_packed[kBgSlots];
@@ -582,6 +583,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
+    ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
     ctx->key_cor_lds = (uint32_t)std::max(0, env_int("TFBS_KEY_COR_LDS", 1 << 30));
     ctx->cor_cap = (uint32_t)std::max(1, env_int("TFBS_KEY_COR_CAP", 1 << 22));
@@ -805,12 +807,17 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // counters are copied back for assembly_wait.  Buffers are sized from the batch
 // (1/16 of its keys and dense counts for the varying lists: no regrowth at C3
 // shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
+// asm_ctr: [0, 2) the scan's overflow counters (copied), 2 regions left to key_asm,
+// 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
+// give-up reasons, 16 / 17 key_fast_kernel's region counters; the spill buckets after.
+constexpr size_t kAsmCtrWords = 24;
+
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     int rc;
     const uint64_t n_keys = (uint64_t)(B.inner.size() / 2) * B.n_slots;
     const uint32_t nr = (uint32_t)B.regions.size();
     if ((rc = ctx->key_first.ensure(std::max<uint64_t>(n_keys, 1))) ||
-        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(16 + (size_t)std::max<uint32_t>(1, nr) + 1)) ||
+        (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(kAsmCtrWords + (size_t)std::max<uint32_t>(1, nr) + 1)) ||
         (rc = ctx->asm_redo.ensure((size_t)nr + 1)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
         return rc;
     if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 64, hipHostMallocDefault));
@@ -827,9 +834,9 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
     const bool mfma = !ctx->plan.m_supers.empty();
-    // the assembly's counters and the spill buckets' (at asm_ctr + 16): one memset
-    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0, (16 + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4,
-                           ctx->stream));
+    // the assembly's counters and the spill buckets' (at asm_ctr + kAsmCtrWords): one memset
+    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0,
+                           (kAsmCtrWords + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4, ctx->stream));
     if (mfma && post) {
         if (!ctx->post_done) {  // (once per scan: the rescoring appends spill records)
             const int f = launch_post_scan(ctx->last_margs, ctx->stream);
@@ -837,7 +844,8 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
             ctx->post_done = true;
         }
         if ((rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, std::max<uint32_t>(1, nr),
-                                       ctx->asm_ctr.p + 16, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream, true)))
+                                       ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream,
+                                       true)))
             return rc;
     }
     AsmArgs a = asm_args(ctx, B, 0);
@@ -859,6 +867,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.report_src = mfma ? ctx->over.p : nullptr;  // (copied by the list pass: no report launch)
     a.report = ctx->asm_ctr.p;
     a.order = ctx->asm_order_n == nr ? ctx->asm_order.p : nullptr;
+    a.next = ctx->kf_persistent ? ctx->asm_ctr.p + 16 : nullptr;
     if (ctx->kf_prof_on && nr) {
         if ((rc = ctx->kf_prof.ensure((size_t)nr * 16))) return rc;
         HIP_TRY(hipMemsetAsync(ctx->kf_prof.p, 0, (size_t)nr * 128, ctx->stream));

@@ -502,7 +502,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 }
 
 template <class C>
-__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first) {
+__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count, uint32_t which) {
     constexpr int kFBlock = C::kBlock;
     constexpr uint32_t kFWaves = C::kWaves, kFHapLds = C::kHapLds, kFCor = C::kCor, kFRefs = C::kRefs,
                        kFCnt = C::kCnt, kFRuns = C::kRuns, kFRows = C::kRows, kFLists = C::kLists;
@@ -518,8 +518,9 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     __shared__ uint32_t s_w[kFWaves];
     __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena, s_ndirty;
     __shared__ unsigned long long s_vbase, s_obase;
-    const uint32_t r = A.order ? A.order[first + blockIdx.x] : first + blockIdx.x, tid = threadIdx.x, lane = tid & 63,
-                   wave = tid >> 6;
+    __shared__ uint32_t s_idx;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    auto process = [&](const uint32_t r) {  // one region (every exit is workgroup-uniform)
     // TFBS_KF_PROF: phase clocks 0-7, then sizes (U, entries, dirty reference hits, rows, chunks)
     auto stamp = [&](uint32_t k, uint64_t v) {
         if (A.prof && tid == 0) A.prof[16 * (size_t)r + k] = v;
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
             if (A.why) atomicAdd(A.why + why, 1u);  // (TFBS_DEBUG_OVER: the reasons)
         }
     };
-    if (U > min(kFMaxU, A.fast_max_u) || K > 32 * kFKeyWords || n_inner > 32) return give_up(0);
+    if (U > (kFMaxU < A.fast_max_u ? kFMaxU : A.fast_max_u) || K > 32 * kFKeyWords || n_inner > 32) return give_up(0);
     const uint32_t hb = rg.hap_begin;
     const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
     if (tid == 0) {
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     // the corrections' list: LDS when they fit (own hits from the bottom, the dirty
     // ones at the top), else a share of the launch's arena (the dirty ones first)
     const uint32_t need = n_ent + (sp.y - sp.x) + nD;  // (an upper bound: entries of other regions' haplotypes)
-    const bool in_lds = need <= min(kFCor, A.cor_lds);
+    const bool in_lds = need <= (kFCor < A.cor_lds ? kFCor : A.cor_lds);
     if (tid == 0) {
         s_arena = kFNone;
         if (!in_lds) {
@@ -973,6 +974,21 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     stamp(13, (T + rows_per - 1) / rows_per);
     stamp(14, in_lds);
     stamp(15, nref);
+    };
+    // regions [first, first + count) in A.order's order: taken from the counter
+    // A.next[which] by a grid of a few workgroups per CU (no workgroup launch per
+    // region, the last ones free as soon as the counter runs out), or one per workgroup
+    for (uint32_t it = blockIdx.x;;) {
+        if (A.next) {
+            if (tid == 0) s_idx = atomicAdd(A.next + which, 1u);
+            __syncthreads();
+            it = s_idx;
+            __syncthreads();
+        }
+        if (it >= count) break;
+        process(A.order ? A.order[first + it] : first + it);
+        if (!A.next) break;
+    }
 }
 
 // Spill bucketing: per-region record counts, their exclusive scan (one
@@ -1371,18 +1387,34 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
     if (n_regions == 0) return TFBS_OK;
     if (!a.order || !side) n_big = 0;
     n_big = std::min(n_big, n_regions);
+    // persistent grids (a.next): the workgroups of each shape that fit the device at once
+    static int n_cu = 0, per_small = 0, per_big = 0;
+    if (!n_cu) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_small, key_fast_kernel<KfSmall>, KfSmall::kBlock, 0) !=
+                hipSuccess || per_small <= 0)
+            per_small = 2;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_big, key_fast_kernel<KfBig>, KfBig::kBlock, 0) !=
+                hipSuccess || per_big <= 0)
+            per_big = 1;
+        (void)hipGetLastError();
+    }
+    auto grid = [&](uint32_t n, int per) { return a.next ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
     hipError_t e = hipSuccess;
     if (n_big) {  // the regions of many haplotypes (order[0, n_big)) beside the others, on a side stream
         if ((e = hipEventRecord(fork, stream)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(n_big), dim3(KfBig::kBlock), 0, side, a, 0u);
+            hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, side, a, 0u,
+                               n_big, 1u);
             e = hipEventRecord(join, side);
         }
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel (big): ") + hipGetErrorString(e));
     }
     if (n_regions > n_big)
-        hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(n_regions - n_big), dim3(KfSmall::kBlock), 0, stream, a,
-                           n_big);
+        hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(grid(n_regions - n_big, per_small)), dim3(KfSmall::kBlock), 0,
+                           stream, a, n_big, n_regions - n_big, 0u);
     if (n_big && (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess)
         return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
     // the regions it left: a fixed grid over the list (no host round trip)
