@@ -809,7 +809,7 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
 // asm_ctr: [0, 2) the scan's overflow counters (copied), 2 regions left to key_asm,
 // 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
-// give-up reasons, 16 / 17 key_fast_kernel's region counters; the spill buckets after.
+// give-up reasons, [16, 24) spare; the spill buckets after.
 constexpr size_t kAsmCtrWords = 24;
 
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
@@ -867,7 +867,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.report_src = mfma ? ctx->over.p : nullptr;  // (copied by the list pass: no report launch)
     a.report = ctx->asm_ctr.p;
     a.order = ctx->asm_order_n == nr ? ctx->asm_order.p : nullptr;
-    a.next = ctx->kf_persistent ? ctx->asm_ctr.p + 16 : nullptr;
+    a.persist = ctx->kf_persistent ? 1u : 0u;
     if (ctx->kf_prof_on && nr) {
         if ((rc = ctx->kf_prof.ensure((size_t)nr * 16))) return rc;
         HIP_TRY(hipMemsetAsync(ctx->kf_prof.p, 0, (size_t)nr * 128, ctx->stream));
@@ -911,7 +911,7 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
     std::sort(tot.begin(), tot.end());
     if (!tot.empty()) {
         auto pct = [&](double f) { return tot[std::min(tot.size() - 1, (size_t)(f * tot.size()))].first; };
-        fprintf(stderr, "[kf prof] total cycles p50 %.0f p90 %.0f p99 %.0f max %.0f; slowest regions (cycles U rows chunks "
+        fprintf(stderr, "[kf prof] total ticks p50 %.0f p90 %.0f p99 %.0f max %.0f; slowest regions (ticks U rows chunks "
                         "corrections refs):", pct(0.5), pct(0.9), pct(0.99), tot.back().first);
         for (size_t i = tot.size(); i-- > 0 && i + 6 > tot.size();) {
             const uint64_t *p = &h[(size_t)tot[i].second * 16];
@@ -921,9 +921,22 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
         }
         fprintf(stderr, "\n");
     }
+    uint64_t t_lo = UINT64_MAX, t_hi = 0;
+    double busy = 0;
+    for (uint32_t r = 0; r < nr; r++) {
+        const uint64_t *p = &h[(size_t)r * 16];
+        if (!p[6]) continue;
+        t_lo = std::min(t_lo, p[0]);
+        t_hi = std::max(t_hi, p[6]);
+        busy += (double)(p[6] - p[0]);
+    }
+    if (t_hi > t_lo)
+        fprintf(stderr, "[kf prof] span %.1f us (first region start to last end, 100 MHz ticks), region-time %.1f us: "
+                        "%.0f regions in flight on average\n",
+                (t_hi - t_lo) / 100.0, busy / 100.0, busy / (double)(t_hi - t_lo));
     const double d = n ? n : 1;
     fprintf(stderr,
-            "[kf prof] regions %u of %u cycles/region: descr+hitn %.0f refs %.0f dirty %.0f lists %.0f keys %.0f "
+            "[kf prof] regions %u of %u ticks/region: descr+hitn %.0f refs %.0f dirty %.0f lists %.0f keys %.0f "
             "chunks %.0f (max total %.0f); per region: U %.1f entries %.1f dirty-refs %.1f corrections %.1f rows "
             "%.1f chunks %.2f in-LDS %.2f refs %.1f\n",
             n, nr, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, ph[5] / d, mx, sz[0] / d, sz[1] / d,

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <string>
 
 #include "keys.hpp"
@@ -502,7 +504,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 }
 
 template <class C>
-__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count, uint32_t which) {
+__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count) {
     constexpr int kFBlock = C::kBlock;
     constexpr uint32_t kFWaves = C::kWaves, kFHapLds = C::kHapLds, kFCor = C::kCor, kFRefs = C::kRefs,
                        kFCnt = C::kCnt, kFRuns = C::kRuns, kFRows = C::kRows, kFLists = C::kLists;
@@ -518,14 +520,13 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     __shared__ uint32_t s_w[kFWaves];
     __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena, s_ndirty;
     __shared__ unsigned long long s_vbase, s_obase;
-    __shared__ uint32_t s_idx;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     auto process = [&](const uint32_t r) {  // one region (every exit is workgroup-uniform)
-    // TFBS_KF_PROF: phase clocks 0-7, then sizes (U, entries, dirty reference hits, rows, chunks)
+    // TFBS_KF_PROF: phase times 0-7 (wall_clock64: 100 MHz), then sizes (U, entries, dirty reference hits, rows, chunks)
     auto stamp = [&](uint32_t k, uint64_t v) {
         if (A.prof && tid == 0) A.prof[16 * (size_t)r + k] = v;
     };
-    stamp(0, clock64());
+    stamp(0, wall_clock64());
     const DevRegion rg = A.regions[r];
     const uint32_t U = rg.hap_count, n_inner = rg.n_inner, K = A.n_slots * n_inner;
     const uint64_t ko = (uint64_t)rg.inner_off * A.n_slots;
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         s_loff[tid] = loff;
     }
     if (lists_staged && tid == 0) s_loff[nl] = n_ent;
-    stamp(1, clock64());
+    stamp(1, wall_clock64());
     const uint32_t run0 = s_run0, nruns = s_run0 == kFNone ? 0u : s_run1 - s_run0;
     if (nruns >= 65536) return give_up(2);
 #pragma unroll
@@ -669,7 +670,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         if (tid < nref) s_ref[rank] = mine;
         __syncthreads();
     }
-    stamp(2, clock64());
+    stamp(2, wall_clock64());
     const uint32_t rpl = nref <= 1 ? 1u : nref >= 64 ? 64u : 1u << (32 - __clz(nref - 1));  // hits per lane group
     const uint32_t hpw = 64 / rpl;                                                         // haplotypes per wave
     auto each_dirty = [&](auto &&f) {
@@ -757,7 +758,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     }
     __syncthreads();
     if (!in_lds && s_arena == kFNone) return give_up(4);  // the host grows the arena for the next call
-    stamp(3, clock64());
+    stamp(3, wall_clock64());
     uint32_t *const cor = in_lds ? s_cor : A.cor_arena + s_arena;
     if (!in_lds && dirty_listed)
         for (uint32_t e = tid; e < nD; e += kFBlock) cor[e] = s_cor[kFCor - 1 - e];
@@ -822,7 +823,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     const uint32_t nw = (K + 31) / 32;
     for (uint32_t w = tid; w < nw; w += kFBlock) s_bits[w] = 0;
     __syncthreads();
-    stamp(4, clock64());
+    stamp(4, wall_clock64());
     // the corrections: [0, nA) and, listed at the top of s_cor, [kFCor - nB, kFCor)
     const uint32_t nA = s_ncor, nB = in_lds && dirty_listed ? nD : 0u, ncor = nA + nB;  // (nA <= need)
     auto cor_at = [&](uint32_t e) -> uint32_t & { return e < nA ? cor[e] : s_cor[kFCor - nB + (e - nA)]; };
@@ -860,7 +861,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
             }
         }
     }
-    stamp(5, clock64());
+    stamp(5, wall_clock64());
     auto row_of = [&](uint32_t j) { return s_rbase[j >> 5] + __popc(s_bits[j >> 5] & ((1u << (j & 31)) - 1u)); };
     // the counter block: LDS chunks of rows x U, or -- when that would take more than
     // 32 chunks (hundreds of haplotypes and keys: each chunk re-reads every
@@ -965,7 +966,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
             for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = cnt[rr * U + l];
         }
     }
-    stamp(6, clock64());
+    stamp(6, wall_clock64());
     stamp(8, U);
     stamp(9, n_ent);
     stamp(10, nD);
@@ -975,19 +976,23 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     stamp(14, in_lds);
     stamp(15, nref);
     };
-    // regions [first, first + count) in A.order's order: taken from the counter
-    // A.next[which] by a grid of a few workgroups per CU (no workgroup launch per
-    // region, the last ones free as soon as the counter runs out), or one per workgroup
-    for (uint32_t it = blockIdx.x;;) {
-        if (A.next) {
-            if (tid == 0) s_idx = atomicAdd(A.next + which, 1u);
-            __syncthreads();
-            it = s_idx;
-            __syncthreads();
-        }
-        if (it >= count) break;
-        process(A.order ? A.order[first + it] : first + it);
-        if (!A.next) break;
+    // regions [first, first + count) in A.order's order (most haplotypes first): with
+    // A.persist a grid of a few workgroups per CU deals them out in snake order --
+    // workgroup w takes k G + w in even rounds, k G + G - 1 - w in odd ones, so the
+    // big regions of a round are paired with small ones of the next -- and reads the
+    // next region's id while it works on this one; else one region per workgroup
+    const uint32_t G = gridDim.x, w = blockIdx.x;
+    auto index = [&](uint32_t k) { return k * G + ((k & 1u) ? G - 1 - w : w); };
+    auto region = [&](uint32_t i) { return A.order ? A.order[first + i] : first + i; };
+    uint32_t i = w, r = w < count ? region(w) : 0u;
+    for (uint32_t k = 0; i < count;) {
+        const uint32_t in = A.persist ? index(k + 1) : count;
+        const uint32_t rn = in < count ? region(in) : 0u;  // (in flight while this region runs)
+        process(r);
+        if (!A.persist) break;
+        k++;
+        i = in;
+        r = rn;
     }
 }
 
@@ -1382,12 +1387,19 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream) {
     return TFBS_OK;
 }
 
+static size_t key_fast_lds_bytes(bool big) {
+    hipFuncAttributes fa{};
+    const hipError_t e = big ? hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(key_fast_kernel<KfBig>))
+                             : hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(key_fast_kernel<KfSmall>));
+    return e == hipSuccess ? fa.sharedSizeBytes : 0;
+}
+
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
                     hipEvent_t fork, hipEvent_t join) {
     if (n_regions == 0) return TFBS_OK;
     if (!a.order || !side) n_big = 0;
     n_big = std::min(n_big, n_regions);
-    // persistent grids (a.next): the workgroups of each shape that fit the device at once
+    // persistent grids (a.persist): the workgroups of each shape that fit the device at once
     static int n_cu = 0, per_small = 0, per_big = 0;
     if (!n_cu) {
         int dev = 0;
@@ -1400,21 +1412,25 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
                 hipSuccess || per_big <= 0)
             per_big = 1;
         (void)hipGetLastError();
+        if (getenv("TFBS_KF_PROF"))
+            fprintf(stderr, "[kf prof] CUs %d, workgroups per CU: %d (%d threads, %zu B LDS), %d (%d threads, %zu B LDS)\n",
+                    n_cu, per_small, KfSmall::kBlock, key_fast_lds_bytes(false), per_big, KfBig::kBlock,
+                    key_fast_lds_bytes(true));
     }
-    auto grid = [&](uint32_t n, int per) { return a.next ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
+    auto grid = [&](uint32_t n, int per) { return a.persist ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
     hipError_t e = hipSuccess;
     if (n_big) {  // the regions of many haplotypes (order[0, n_big)) beside the others, on a side stream
         if ((e = hipEventRecord(fork, stream)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, side, a, 0u,
-                               n_big, 1u);
+                               n_big);
             e = hipEventRecord(join, side);
         }
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel (big): ") + hipGetErrorString(e));
     }
     if (n_regions > n_big)
         hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(grid(n_regions - n_big, per_small)), dim3(KfSmall::kBlock), 0,
-                           stream, a, n_big, n_regions - n_big, 0u);
+                           stream, a, n_big, n_regions - n_big);
     if (n_big && (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess)
         return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
     // the regions it left: a fixed grid over the list (no host round trip)
