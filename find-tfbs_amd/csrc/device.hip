@@ -809,7 +809,8 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
 // asm_ctr: [0, 2) the scan's overflow counters (copied), 2 regions left to key_asm,
 // 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
-// give-up reasons, [16, 24) spare; the spill buckets after.
+// give-up reasons, 16 / 17 key_fast_kernel's region counters, [18, 24) spare; the
+// spill buckets after.
 constexpr size_t kAsmCtrWords = 24;
 
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
@@ -868,6 +869,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     a.report = ctx->asm_ctr.p;
     a.order = ctx->asm_order_n == nr ? ctx->asm_order.p : nullptr;
     a.persist = ctx->kf_persistent ? 1u : 0u;
+    a.next = ctx->asm_ctr.p + 16;
     if (ctx->kf_prof_on && nr) {
         if ((rc = ctx->kf_prof.ensure((size_t)nr * 16))) return rc;
         HIP_TRY(hipMemsetAsync(ctx->kf_prof.p, 0, (size_t)nr * 128, ctx->stream));
@@ -895,7 +897,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
 static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
     std::vector<uint64_t> h((size_t)nr * 16);
     HIP_TRY(hipMemcpy(h.data(), ctx->kf_prof.p, h.size() * 8, hipMemcpyDeviceToHost));
-    double ph[6] = {0, 0, 0, 0, 0, 0}, sz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mx = 0;
+    double ph[6] = {0, 0, 0, 0, 0, 0}, sz[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mx = 0, at = 0;
     uint32_t n = 0;
     for (uint32_t r = 0; r < nr; r++) {
         const uint64_t *p = &h[(size_t)r * 16];
@@ -903,6 +905,7 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
         n++;
         for (int k = 0; k < 6; k++) ph[k] += (double)(p[k + 1] - p[k]);
         mx = std::max(mx, (double)(p[6] - p[0]));
+        at += (double)p[7];
         for (int k = 0; k < 8; k++) sz[k] += (double)p[8 + k];
     }
     std::vector<std::pair<double, uint32_t>> tot;  // (cycles, region)
@@ -937,9 +940,9 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
     const double d = n ? n : 1;
     fprintf(stderr,
             "[kf prof] regions %u of %u ticks/region: descr+hitn %.0f refs %.0f dirty %.0f lists %.0f keys %.0f "
-            "chunks %.0f (max total %.0f); per region: U %.1f entries %.1f dirty-refs %.1f corrections %.1f rows "
+            "chunks %.0f (of which var-list atomics %.0f) (max total %.0f); per region: U %.1f entries %.1f dirty-refs %.1f corrections %.1f rows "
             "%.1f chunks %.2f in-LDS %.2f refs %.1f\n",
-            n, nr, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, ph[5] / d, mx, sz[0] / d, sz[1] / d,
+            n, nr, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, ph[5] / d, at / d, mx, sz[0] / d, sz[1] / d,
             sz[2] / d, sz[3] / d, sz[4] / d, sz[5] / d, sz[6] / d, sz[7] / d);
     return TFBS_OK;
 }

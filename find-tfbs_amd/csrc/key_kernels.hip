@@ -449,7 +449,7 @@ struct KfShape {
 };
 constexpr int kFB = TFBS_KF_BLOCK;
 #ifdef TFBS_KF_LDS4  // (A/B: ~39 KB, four regions per CU)
-using KfSmall = KfShape<kFB, 2 * kFB, 13 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
+using KfSmall = KfShape<kFB, 2 * kFB, 14 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
 #else
 using KfSmall = KfShape<kFB, 4 * kFB, 16 * kFB, kFB, 16 * kFB, 2 * kFB, kFB>;
 #endif
@@ -504,7 +504,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
 }
 
 template <class C>
-__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count) {
+__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count, uint32_t which) {
     constexpr int kFBlock = C::kBlock;
     constexpr uint32_t kFWaves = C::kWaves, kFHapLds = C::kHapLds, kFCor = C::kCor, kFRefs = C::kRefs,
                        kFCnt = C::kCnt, kFRuns = C::kRuns, kFRows = C::kRows, kFLists = C::kLists;
@@ -518,7 +518,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     __shared__ uint32_t s_rkey[kFRows], s_rr[kFRows];  // per row of a chunk: its key; R(key), then its varying slot
     __shared__ uint32_t s_loff[kFLists + 1], s_lidx[kFLists];
     __shared__ uint32_t s_w[kFWaves];
-    __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena, s_ndirty;
+    __shared__ uint32_t s_ncor, s_nref, s_run0, s_run1, s_nvar, s_arena, s_ndirty, s_lmax;
     __shared__ unsigned long long s_vbase, s_obase;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     auto process = [&](const uint32_t r) {  // one region (every exit is workgroup-uniform)
@@ -547,13 +547,13 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     const uint32_t hb = rg.hap_begin;
     const bool refs_on = A.mfma && rg.ref_hap != UINT32_MAX;
     if (tid == 0) {
-        s_ncor = s_nref = s_run1 = s_ndirty = 0;
+        s_ncor = s_nref = s_run1 = s_ndirty = s_lmax = 0;
         s_run0 = kFNone;
     }
     __syncthreads();
     // descriptors: which haplotypes reuse the reference's windows, and their runs
     constexpr uint32_t kPer = kFMaxU / kFBlock;
-    uint32_t roff[kPer], rn[kPer];
+    uint32_t roff[kPer], rn[kPer], lmax = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kPer; q++) {
         const uint32_t l = tid + q * kFBlock;
@@ -561,6 +561,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         rn[q] = 0;
         if (l < U) {
             const DevHap &h = A.haps[hb + l];
+            lmax = max(lmax, h.len);
             if (h.flags & HAP_DEDUP) {
                 roff[q] = h.drun_off;
                 rn[q] = h.n_druns;
@@ -602,6 +603,8 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     }
     uint32_t n_ent = 0;
     const uint32_t loff = block_excl_scan<kFWaves>(lcnt, s_w, n_ent);  // (barriers: s_run0 / s_run1 are final)
+    if (tid == 0 && rg.ref_hap != UINT32_MAX) lmax = max(lmax, A.haps[rg.ref_hap].len);  // (R's haplotype)
+    if (lmax) atomicMax(&s_lmax, lmax);
     const bool lists_staged = nl <= kFLists;  // one list per thread: its offset and index kept for the list pass
     if (lists_staged && tid < nl) {
         s_lidx[tid] = lidx;
@@ -719,6 +722,15 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     // inclusive scan of the lanes' counts) when the wave calls together, else per lane
     auto slots = [&](uint32_t c, bool uniform, uint32_t *ctr) -> uint32_t {
         if (!uniform) return atomicAdd(ctr, c);
+        if (!__ballot(c > 1)) {  // (one entry per lane at most: a ballot prefix)
+            const uint64_t m = __ballot(c != 0);
+            if (!m) return 0;
+            const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+            return (uint32_t)__shfl((int)base, (int)leader) +
+                   __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+        }
         uint32_t x = c;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -867,9 +879,17 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     // 32 chunks (hundreds of haplotypes and keys: each chunk re-reads every
     // correction and costs a few barriers) -- chunks of kFRows rows in a share of
     // the arena (global atomics)
-    uint32_t rows_per = min(kFCnt / U, kFRows);
+    // u16 counters in LDS (two per word) when no count can reach 2^16: a key's count
+    // on a haplotype is at most its 2 strands' windows (< 2 x length); the -1
+    // corrections never take a count below 0 (a haplotype's dirty reference hits on
+    // a key are some of its base R), so a packed pair never borrows or carries
+    const bool half = 2 * (s_lmax + 64) < 65536 && A.cor_lds != 0;
+    uint32_t rows_per = min((half ? 2 : 1) * kFCnt / U, kFRows);
     uint32_t *cnt = s_cnt;
+    uint16_t *const cnt16 = reinterpret_cast<uint16_t *>(s_cnt);
+    bool h16 = half;
     if ((T + rows_per - 1) / rows_per > 32 || A.cor_lds == 0) {  // (cor_lds 0: the tests' all-global path)
+        h16 = false;
         rows_per = min(T, kFRows);
         if (tid == 0) {
             s_arena = kFNone;
@@ -895,6 +915,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     uint32_t dedup_bits = 0;  // bit i: haplotype lane + 64 i takes the reference's counts as its base
     for (uint32_t i = 0, l = lane; l < U; i++, l += 64)
         if (hap_info(l) != kFNone) dedup_bits |= 1u << i;
+    uint64_t t_atomics = 0;  // (TFBS_KF_PROF)
     for (uint32_t t0 = 0; t0 < T; t0 += rows_per) {
         const uint32_t nrow = min(rows_per, T - t0);
         __syncthreads();  // s_rbase / cor rows written, the previous chunk's readers done
@@ -922,24 +943,31 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {  // the base of every haplotype
             const uint32_t j = s_rkey[rr], R = s_rr[rr];
             const bool dense = A.any_dense && !A.slot_mfma[j / n_inner];
-            for (uint32_t i = 0, l = lane; l < U; i++, l += 64)
-                cnt[rr * U + l] = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
-                                        : ((dedup_bits >> i) & 1u ? R : 0u);
+            for (uint32_t i = 0, l = lane; l < U; i++, l += 64) {
+                const uint32_t v = dense ? A.counts[dense_base + (uint64_t)j * rg.count_stride + l]
+                                         : ((dedup_bits >> i) & 1u ? R : 0u);
+                if (h16) cnt16[rr * U + l] = (uint16_t)v;
+                else cnt[rr * U + l] = v;
+            }
         }
         __syncthreads();
         for (uint32_t e = tid; e < ncor; e += kFBlock) {
             const uint32_t c = cor_at(e);
             const uint32_t t = cor_key(c) - t0;  // (its row)
-            if (t < nrow) atomicAdd(&cnt[t * U + cor_hap(c)], cor_neg(c) ? 0xFFFFFFFFu : 1u);
+            if (t < nrow) {
+                const uint32_t x = t * U + cor_hap(c);
+                if (h16) atomicAdd(&cnt[x >> 1], (cor_neg(c) ? 0xFFFFFFFFu : 1u) << (16 * (x & 1u)));
+                else atomicAdd(&cnt[x], cor_neg(c) ? 0xFFFFFFFFu : 1u);
+            }
         }
         __syncthreads();
+        auto count_at = [&](uint32_t x) -> uint32_t { return h16 ? (uint32_t)cnt16[x] : cnt[x]; };
         // classify: one wave per row
         for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {
-            const uint32_t *col = cnt + rr * U;
-            const uint32_t c0 = col[0];
+            const uint32_t c0 = count_at(rr * U);
             uint32_t any = 0, diff = 0;
             for (uint32_t l = lane; l < U; l += 64) {
-                const uint32_t c = col[l];
+                const uint32_t c = count_at(rr * U + l);
                 any |= c;
                 diff |= c ^ c0;
             }
@@ -952,21 +980,24 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
             }
         }
         __syncthreads();
+        const uint64_t ta = A.prof ? wall_clock64() : 0;
         if (tid == 0 && s_nvar) {  // the chunk's share of the compact lists
             s_vbase = atomicAdd(A.var_tot, (unsigned long long)s_nvar);
             s_obase = atomicAdd(A.var_tot + 1, (unsigned long long)s_nvar * U);
         }
         __syncthreads();
+        if (A.prof) t_atomics += wall_clock64() - ta;
         for (uint32_t rr = wave; rr < nrow; rr += kFWaves) {
             const uint32_t slot = s_rr[rr];
             if (slot == kFNone) continue;
             const uint64_t vi = s_vbase + slot, off = s_obase + (uint64_t)slot * U;
             if (vi >= A.var_keys_cap || off + U > A.var_cap) continue;  // the host grows the lists and reruns
             if (lane == 0) A.var_keys[vi] = DevVarKey{r, s_rkey[rr], off};
-            for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = cnt[rr * U + l];
+            for (uint32_t l = lane; l < U; l += 64) A.var_counts[off + l] = count_at(rr * U + l);
         }
     }
     stamp(6, wall_clock64());
+    stamp(7, t_atomics);
     stamp(8, U);
     stamp(9, n_ent);
     stamp(10, nD);
@@ -977,22 +1008,26 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     stamp(15, nref);
     };
     // regions [first, first + count) in A.order's order (most haplotypes first): with
-    // A.persist a grid of a few workgroups per CU deals them out in snake order --
-    // workgroup w takes k G + w in even rounds, k G + G - 1 - w in odd ones, so the
-    // big regions of a round are paired with small ones of the next -- and reads the
-    // next region's id while it works on this one; else one region per workgroup
-    const uint32_t G = gridDim.x, w = blockIdx.x;
-    auto index = [&](uint32_t k) { return k * G + ((k & 1u) ? G - 1 - w : w); };
-    auto region = [&](uint32_t i) { return A.order ? A.order[first + i] : first + i; };
-    uint32_t i = w, r = w < count ? region(w) : 0u;
-    for (uint32_t k = 0; i < count;) {
-        const uint32_t in = A.persist ? index(k + 1) : count;
-        const uint32_t rn = in < count ? region(in) : 0u;  // (in flight while this region runs)
-        process(r);
+    // A.persist a grid of a few workgroups per CU takes them from the counter
+    // A.next[which] -- the ticket for the next region is taken as this one starts, so
+    // its latency hides behind the region's first loads --, else one per workgroup
+    __shared__ uint32_t s_tk;
+    uint32_t i = blockIdx.x;
+    if (A.persist) {
+        if (tid == 0) s_tk = atomicAdd(A.next + which, 1u);
+        __syncthreads();
+        i = s_tk;
+        __syncthreads();
+    }
+    while (i < count) {
+        uint32_t tk = 0;
+        if (A.persist && tid == 0) tk = atomicAdd(A.next + which, 1u);
+        process(A.order ? A.order[first + i] : first + i);
         if (!A.persist) break;
-        k++;
-        i = in;
-        r = rn;
+        if (tid == 0) s_tk = tk;
+        __syncthreads();
+        i = s_tk;
+        __syncthreads();
     }
 }
 
@@ -1423,14 +1458,14 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
         if ((e = hipEventRecord(fork, stream)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
         if (e == hipSuccess) {
             hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, side, a, 0u,
-                               n_big);
+                               n_big, 1u);
             e = hipEventRecord(join, side);
         }
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel (big): ") + hipGetErrorString(e));
     }
     if (n_regions > n_big)
         hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(grid(n_regions - n_big, per_small)), dim3(KfSmall::kBlock), 0,
-                           stream, a, n_big, n_regions - n_big);
+                           stream, a, n_big, n_regions - n_big, 0u);
     if (n_big && (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess)
         return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
     // the regions it left: a fixed grid over the list (no host round trip)

@@ -66,9 +66,11 @@ struct AsmArgs {
     // key_fast_kernel: workgroup b takes region order[b] (regions by distinct haplotypes,
     // most first: the longest regions start first and do not trail the launch), or b
     const uint32_t *order;
-    // key_fast_kernel: a persistent grid (a few workgroups per CU, each region list
-    // dealt out in snake order), else one region per workgroup
+    // key_fast_kernel: a persistent grid (a few workgroups per CU taking regions from
+    // the counters next[0] / next[1] of the two shapes, zeroed before the launch),
+    // else one region per workgroup
     uint32_t persist;
+    uint32_t *next;
     uint64_t *prof;  // debug (TFBS_KF_PROF): key_fast_kernel's phase clocks and sizes, 16 per region, or null
 };
 
