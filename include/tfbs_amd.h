@@ -237,7 +237,8 @@ uint64_t tfbs_batch_num_scan_windows(const tfbs_batch *b);
 uint64_t tfbs_batch_num_scan_cell_ops(const tfbs_batch *b);
 /* Packed bytes the scan reads from HBM per launch (sequence + masks + positions + metadata). */
 uint64_t tfbs_batch_input_bytes(const tfbs_batch *b);
-/* Bytes of hit counts the scan writes. */
+/* Bytes of the dense u32 counts (the LUT / generic kernels' slots, and the debug
+   download tfbs_batch_download fills); the matrix-core path writes sparse hit lists. */
 uint64_t tfbs_batch_output_bytes(const tfbs_batch *b);
 
 /* Copies the packed batch into ctx device memory (H2D). */
