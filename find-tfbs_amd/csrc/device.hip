@@ -892,6 +892,18 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
 // Waits for the enqueued assembly and checks its lists: a scan overflow list that
 // dropped entries means a rescan with larger lists (and a new assembly), a full
 // varying-key list a new assembly with larger ones.
+static uint64_t t_lo_all(const std::vector<uint64_t> &h, uint32_t nr) {
+    uint64_t t = UINT64_MAX;
+    for (uint32_t r = 0; r < nr; r++)
+        if (h[(size_t)r * 16 + 6]) t = std::min(t, h[(size_t)r * 16]);
+    return t;
+}
+static uint64_t t_hi_all(const std::vector<uint64_t> &h, uint32_t nr) {
+    uint64_t t = 0;
+    for (uint32_t r = 0; r < nr; r++) t = std::max(t, h[(size_t)r * 16 + 6]);
+    return t;
+}
+
 // TFBS_KF_PROF: key_fast_kernel's mean phase cycles and sizes over the regions it
 // finished (debug; synchronises).
 static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
@@ -933,10 +945,38 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
         t_hi = std::max(t_hi, p[6]);
         busy += (double)(p[6] - p[0]);
     }
+    {  // per workgroup: its regions in start order -> gaps between them, late start, early end
+        std::vector<std::pair<uint64_t, uint32_t>> ev;  // (workgroup, start) -> region
+        for (uint32_t r = 0; r < nr; r++)
+            if (h[(size_t)r * 16 + 6]) ev.push_back({(h[(size_t)r * 16 + 14] << 40) | (h[(size_t)r * 16] & ((1ull << 40) - 1)), r});
+        std::sort(ev.begin(), ev.end());
+        double gap = 0, late = 0, early_end = 0;
+        uint32_t n_gap = 0, n_wg = 0;
+        for (size_t i = 0; i < ev.size(); i++) {
+            const uint64_t *p = &h[(size_t)ev[i].second * 16];
+            const bool first = i == 0 || (ev[i - 1].first >> 40) != (ev[i].first >> 40);
+            const bool last = i + 1 == ev.size() || (ev[i + 1].first >> 40) != (ev[i].first >> 40);
+            if (first) {
+                n_wg++;
+                late += (double)(p[0] - t_lo_all(h, nr));
+            } else {
+                gap += (double)(p[0] - h[(size_t)ev[i - 1].second * 16 + 6]);
+                n_gap++;
+            }
+            if (last) early_end += (double)(t_hi_all(h, nr) - p[6]);
+        }
+        if (n_wg)
+            fprintf(stderr, "[kf prof] %u workgroups: mean gap between a workgroup's regions %.1f us (%u gaps), first "
+                            "region start after the kernel's first %.1f us, last end before the kernel's last %.1f us\n",
+                    n_wg, n_gap ? gap / n_gap / 100.0 : 0.0, n_gap, late / n_wg / 100.0, early_end / n_wg / 100.0);
+    }
+    uint32_t early = 0;  // regions started in the first 10 us: the workgroups resident at the start
+    for (uint32_t r = 0; r < nr; r++)
+        if (h[(size_t)r * 16 + 6] && h[(size_t)r * 16] < t_lo + 1000) early++;
     if (t_hi > t_lo)
         fprintf(stderr, "[kf prof] span %.1f us (first region start to last end, 100 MHz ticks), region-time %.1f us: "
-                        "%.0f regions in flight on average\n",
-                (t_hi - t_lo) / 100.0, busy / 100.0, busy / (double)(t_hi - t_lo));
+                        "%.0f regions in flight on average; %u regions started in the first 10 us\n",
+                (t_hi - t_lo) / 100.0, busy / 100.0, busy / (double)(t_hi - t_lo), early);
     const double d = n ? n : 1;
     fprintf(stderr,
             "[kf prof] regions %u of %u ticks/region: descr+hitn %.0f refs %.0f dirty %.0f lists %.0f keys %.0f "

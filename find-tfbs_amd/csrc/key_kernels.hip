@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     stamp(11, ncor);
     stamp(12, T);
     stamp(13, (T + rows_per - 1) / rows_per);
-    stamp(14, in_lds);
+    stamp(14, blockIdx.x | (which << 24));  // (the workgroup: its timeline in the report)
     stamp(15, nref);
     };
     // regions [first, first + count) in A.order's order (most haplotypes first): with

@@ -393,6 +393,31 @@ def test_reference_window_reuse_vs_oracle(tmp_path, monkeypatch, thr, fast_max_u
         _compare(ps, n_samples, beds, regions)
 
 
+def test_long_region_vs_oracle(tmp_path, monkeypatch):
+    """A 33 kb merged region next to a short one, 40 samples, 60 SNVs each with
+    random carriers, against the oracle: a count of the long region could pass 2^16,
+    so the key assembly keeps its LDS counters u32 there (packed u16 in the other)."""
+    monkeypatch.setenv("TFBS_MFMA", "1")
+    ps, _ = synth_patterns(tmp_path, 6, 3, 91, thr=1e-3)
+    lmax = ps.max_length
+    rnd = random.Random(7)
+    n_samples = 40
+    H = 2 * n_samples
+    regions, ranges = [], []
+    for (s, e) in ((5000, 5000 + 33000), (60000, 60200)):
+        es = s - lmax + 1
+        n = e - s + 2 * lmax - 1
+        ref = "".join(rnd.choice("ACGT") for _ in range(n))
+        recs = []
+        for q in sorted(rnd.sample(range(n), 60)):
+            alt = rnd.choice([c for c in "ACGT" if c != ref[q]])
+            recs.append(("car", es + q, ref[q], alt, sorted(rnd.sample(range(H), rnd.randint(1, 12)))))
+        regions.append({"merged": (s, e), "ref": ref, "records": recs})
+        ranges.append((s, e))
+    b = _compare(ps, n_samples, [("synthetic.bed", ranges)], regions)
+    assert b.num_haplotypes > 20
+
+
 def test_multi_bed_duplicate_and_nested_inner_peaks(tmp_path):
     """Several bed sources, duplicate ranges (double count), a range that is never selected
     (strictly inside a 3-way merge, bed.rs:77/89), empty ranges, Ns in the reference."""
