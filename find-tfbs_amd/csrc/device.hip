@@ -739,7 +739,9 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
         if ((rc = ctx->asm_order.put(order, ctx->stream))) return rc;
         ctx->asm_order_n = (uint32_t)order.size();
         ctx->asm_order_big = 0;
-        while (ctx->asm_order_big < order.size() && B.regions[order[ctx->asm_order_big]].hap_count > key_fast_big_u())
+        static const int big_u = env_int("TFBS_KF_BIGU", (int)key_fast_big_u());  // (0: every region on one shape)
+        while (big_u > 0 && ctx->asm_order_big < order.size() &&
+               B.regions[order[ctx->asm_order_big]].hap_count > (uint32_t)big_u)
             ctx->asm_order_big++;
     }
     if ((rc = build_lists(ctx, (uint32_t)B.haps.size()))) return rc;
@@ -946,16 +948,16 @@ static int kf_prof_report(tfbs_ctx *ctx, uint32_t nr) {
         busy += (double)(p[6] - p[0]);
     }
     {  // per workgroup: its regions in start order -> gaps between them, late start, early end
-        std::vector<std::pair<uint64_t, uint32_t>> ev;  // (workgroup, start) -> region
+        std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> ev;  // ((workgroup, start), region)
         for (uint32_t r = 0; r < nr; r++)
-            if (h[(size_t)r * 16 + 6]) ev.push_back({(h[(size_t)r * 16 + 14] << 40) | (h[(size_t)r * 16] & ((1ull << 40) - 1)), r});
+            if (h[(size_t)r * 16 + 6]) ev.push_back({{h[(size_t)r * 16 + 14], h[(size_t)r * 16]}, r});
         std::sort(ev.begin(), ev.end());
         double gap = 0, late = 0, early_end = 0;
         uint32_t n_gap = 0, n_wg = 0;
         for (size_t i = 0; i < ev.size(); i++) {
             const uint64_t *p = &h[(size_t)ev[i].second * 16];
-            const bool first = i == 0 || (ev[i - 1].first >> 40) != (ev[i].first >> 40);
-            const bool last = i + 1 == ev.size() || (ev[i + 1].first >> 40) != (ev[i].first >> 40);
+            const bool first = i == 0 || ev[i - 1].first.first != ev[i].first.first;
+            const bool last = i + 1 == ev.size() || ev[i + 1].first.first != ev[i].first.first;
             if (first) {
                 n_wg++;
                 late += (double)(p[0] - t_lo_all(h, nr));

@@ -1454,20 +1454,24 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
     }
     auto grid = [&](uint32_t n, int per) { return a.persist ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
     hipError_t e = hipSuccess;
-    if (n_big) {  // the regions of many haplotypes (order[0, n_big)) beside the others, on a side stream
+    // two shapes at once: the regions of many haplotypes (order[0, n_big), whole-CU
+    // workgroups) go first on `stream` -- queued ahead, they take their CUs before the
+    // others fill every CU -- and the rest on `side`, forked before and joined after
+    const bool two = n_big && n_regions > n_big;
+    if (two) {
         if ((e = hipEventRecord(fork, stream)) == hipSuccess) e = hipStreamWaitEvent(side, fork, 0);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, side, a, 0u,
-                               n_big, 1u);
-            e = hipEventRecord(join, side);
-        }
-        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel (big): ") + hipGetErrorString(e));
+        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel fork: ") + hipGetErrorString(e));
     }
+    if (n_big)
+        hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, stream, a, 0u,
+                           n_big, 1u);
     if (n_regions > n_big)
         hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(grid(n_regions - n_big, per_small)), dim3(KfSmall::kBlock), 0,
-                           stream, a, n_big, n_regions - n_big, 0u);
-    if (n_big && (e = hipStreamWaitEvent(stream, join, 0)) != hipSuccess)
-        return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
+                           two ? side : stream, a, n_big, n_regions - n_big, 0u);
+    if (two) {
+        if ((e = hipEventRecord(join, side)) == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
+        if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
+    }
     // the regions it left: a fixed grid over the list (no host round trip)
     hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
                        (const uint32_t *)a.redo, (const uint32_t *)a.redo_n);

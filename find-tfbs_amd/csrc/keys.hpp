@@ -81,8 +81,8 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 // appends the others to a.redo, which key_asm_kernel then works through (a fixed
 // grid looping over the list).  *a.redo_n, *a.cor_used and a.var_tot must be zero.
 // a.order lists the regions with the n_big of more than key_fast_big_u() distinct
-// haplotypes first: those take the 1 024-thread kernel on `side` (forked from and
-// joined back into `stream` with the two events) beside the others.
+// haplotypes first: those take the 1 024-thread kernel on `stream`, queued ahead of
+// the others' on `side` (forked from and joined back into `stream` with the events).
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
                     hipEvent_t fork, hipEvent_t join);
 uint32_t key_fast_big_u();
