@@ -431,8 +431,8 @@ constexpr uint32_t kFMaxU = 2048;     // distinct haplotypes (11 bits of a corre
 constexpr uint32_t kFKeyWords = 512;  // touched-key bitmap: keys <= 16384
 constexpr uint32_t kFBatch = 8;       // hit-list entries each thread has in flight
 constexpr uint32_t kFNone = 0xFFFFFFFFu;
-// Two shapes of the kernel: the common one (TFBS_KF_BLOCK threads, ~51 KB of LDS,
-// three regions per CU) and one for regions of many distinct haplotypes (1 024
+// Two shapes of the kernel: the common one (TFBS_KF_BLOCK threads, ~40 KB of LDS,
+// four regions per CU) and one for regions of many distinct haplotypes (1 024
 // threads and ~154 KB of LDS: a whole CU, counter chunks of 24 Ki u32 -- 17 rows of
 // 1 400 haplotypes instead of 2, which sent such a region's counters to the
 // global arena).  HAP_LDS: haplotypes whose reuse descriptor sits in LDS (the
@@ -448,10 +448,10 @@ struct KfShape {
                   "key_fast_kernel's per-thread shares");
 };
 constexpr int kFB = TFBS_KF_BLOCK;
-#ifdef TFBS_KF_LDS4  // (A/B: ~39 KB, four regions per CU)
-using KfSmall = KfShape<kFB, 2 * kFB, 14 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
-#else
+#ifdef TFBS_KF_LDS3  // (A/B: the round-4 start's ~51 KB shape, three regions per CU)
 using KfSmall = KfShape<kFB, 4 * kFB, 16 * kFB, kFB, 16 * kFB, 2 * kFB, kFB>;
+#else  // ~40 KB: four regions per CU
+using KfSmall = KfShape<kFB, 2 * kFB, 14 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
 #endif
 using KfBig = KfShape<1024, 2048, 8192, 256, 24576, 1024, 256>;
 constexpr uint32_t kFBigU = 384;  // regions of more distinct haplotypes take KfBig
