@@ -50,11 +50,21 @@ struct RefWindow {
 };
 
 // haplotype.rs:94-156.  The recursion of next_chunk is a loop with the same case order.
-static int patch_window(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const RefWindow &ref,
+// (Diffs already inside [rs, re] and in Diff order -- a group's bits over the sorted
+// distinct records -- are used as they are: no copy, no sort.)
+static int patch_window(uint64_t rs, uint64_t re, const std::vector<const Record *> &diffs_in, const RefWindow &ref,
                         std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
-    diffs.erase(std::remove_if(diffs.begin(), diffs.end(), [&](const Record *d) { return d->pos < rs || d->pos > re; }),
-                diffs.end());
-    std::stable_sort(diffs.begin(), diffs.end(), diff_less);
+    bool as_is = true;
+    for (size_t i = 0; i < diffs_in.size() && as_is; i++)
+        as_is = diffs_in[i]->pos >= rs && diffs_in[i]->pos <= re && (i == 0 || !diff_less(diffs_in[i], diffs_in[i - 1]));
+    std::vector<const Record *> sorted;
+    if (!as_is) {
+        sorted = diffs_in;
+        sorted.erase(std::remove_if(sorted.begin(), sorted.end(), [&](const Record *d) { return d->pos < rs || d->pos > re; }),
+                     sorted.end());
+        std::stable_sort(sorted.begin(), sorted.end(), diff_less);
+    }
+    const std::vector<const Record *> &diffs = as_is ? diffs_in : sorted;
     uint64_t at = rs;
     size_t k = 0;
     for (;;) {
@@ -96,8 +106,66 @@ static int patch_window(uint64_t rs, uint64_t re, std::vector<const Record *> di
 int patch(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const uint8_t *ref, uint64_t ref_start,
           size_t n_ref, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
     RefWindow w{ref, ref_start, n_ref};
-    return patch_window(rs, re, std::move(diffs), w, nucs, pos);
+    return patch_window(rs, re, diffs, w, nucs, pos);
 }
+
+// load_haplotypes' HashMap<(nucs, pos), group> insert (haplotype.rs:84): the
+// patched sequences of a region by a hash of their bases (8 at a time) and of their
+// runs of consecutive positions, in a flat open-addressing table; a sequence equal
+// to an earlier one gives that entry the later group (HashMap::insert replaces the
+// value), else it is appended to dist.
+namespace {
+struct SeqTable {
+    std::vector<uint64_t> key;  // hash, 0 = empty
+    std::vector<uint32_t> idx;
+    uint32_t mask = 0;
+    explicit SeqTable(size_t n) {
+        size_t c = 16;
+        while (c < 2 * n) c *= 2;
+        key.assign(c, 0);
+        idx.assign(c, 0);
+        mask = (uint32_t)c - 1;
+    }
+    static uint64_t hash(const Distinct &d, uint64_t es) {
+        auto mix = [](uint64_t h, uint64_t v) {
+            h ^= v * 0x9E3779B97F4A7C15ull;
+            h ^= h >> 29;
+            return h * 0xBF58476D1CE4E5B9ull;
+        };
+        const size_t n = d.nuc.size();
+        uint64_t h = mix(0x243F6A8885A308D3ull, n);
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t x;
+            memcpy(&x, d.nuc.data() + i, 8);
+            h = mix(h, x);
+        }
+        for (; i < n; i++) h = mix(h, d.nuc[i] | 0x100u);
+        for (size_t a = 0; a < n;) {  // positions as (first, length) runs
+            size_t b = a + 1;
+            while (b < n && d.pos[b] == d.pos[b - 1] + 1) b++;
+            h = mix(h, ((d.pos[a] - es) << 24) ^ (uint64_t)(b - a));
+            a = b;
+        }
+        return h | 1;  // (never 0: the empty mark)
+    }
+    void insert(std::vector<Distinct> &dist, Distinct &&d, uint64_t es) {
+        const uint64_t h = hash(d, es);
+        for (uint32_t s = (uint32_t)(h ^ (h >> 32)) & mask;; s = (s + 1) & mask) {
+            if (!key[s]) {
+                key[s] = h;
+                idx[s] = (uint32_t)dist.size();
+                dist.push_back(std::move(d));
+                return;
+            }
+            if (key[s] == h && dist[idx[s]].nuc == d.nuc && dist[idx[s]].pos == d.pos) {
+                dist[idx[s]].group = d.group;
+                return;
+            }
+        }
+    }
+};
+}  // namespace
 
 uint64_t Batch::device_bytes() const {
     return words.size() * 4ull + nmask.size() * 4ull + posrel.size() * 4ull + druns.size() * 4ull +
@@ -290,7 +358,7 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     // ---- load_haplotypes: patch each group, dedup by (nucs, pos) sequence; later group wins
     std::vector<Distinct> &dist = out.dist;
     dist.clear();
-    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    SeqTable table(groups.size());
     RefWindow ref{I.ref.data(), R.es, I.ref.size()};
     for (uint32_t g = 0; g < groups.size(); g++) {
         uint32_t rep = order[groups[g].first];
@@ -305,24 +373,7 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
         int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos);
         if (rc) return rc;
         d.group = (int32_t)g;
-        uint64_t h = 1469598103934665603ull;
-        for (size_t i = 0; i < d.nuc.size(); i++) {
-            h = (h ^ d.nuc[i]) * 1099511628211ull;
-            h = (h ^ (d.pos[i] - R.es)) * 1099511628211ull;
-        }
-        auto &bucket = by_hash[h];
-        bool replaced = false;
-        for (uint32_t idx : bucket) {
-            if (dist[idx].nuc == d.nuc && dist[idx].pos == d.pos) {
-                dist[idx].group = (int32_t)g;  // HashMap::insert replaces the value
-                replaced = true;
-                break;
-            }
-        }
-        if (!replaced) {
-            bucket.push_back((uint32_t)dist.size());
-            dist.push_back(std::move(d));
-        }
+        table.insert(dist, std::move(d), R.es);
     }
     // membership and carrier counts
     std::vector<uint32_t> &carriers = out.carriers;
@@ -504,7 +555,7 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
     inner_keys(I.inner, R);
     out.dev_grouped = true;
     std::vector<Distinct> &dist = out.dist;
-    std::unordered_map<uint64_t, std::vector<uint32_t>> by_hash;
+    SeqTable table(G);
     RefWindow ref{I.ref.data(), R.es, I.ref.size()};
     std::vector<const Record *> diffs;
     for (uint32_t g = 0; g < G; g++) {
@@ -515,23 +566,7 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
         d.pos.reserve(R.ee - R.es + 16);
         if (int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos)) return rc;
         d.group = (int32_t)g;
-        uint64_t h = 1469598103934665603ull;
-        for (size_t i = 0; i < d.nuc.size(); i++) {
-            h = (h ^ d.nuc[i]) * 1099511628211ull;
-            h = (h ^ (d.pos[i] - R.es)) * 1099511628211ull;
-        }
-        auto &bucket = by_hash[h];
-        bool replaced = false;
-        for (uint32_t idx : bucket)
-            if (dist[idx].nuc == d.nuc && dist[idx].pos == d.pos) {
-                dist[idx].group = (int32_t)g;  // HashMap::insert replaces the value
-                replaced = true;
-                break;
-            }
-        if (!replaced) {
-            bucket.push_back((uint32_t)dist.size());
-            dist.push_back(std::move(d));
-        }
+        table.insert(dist, std::move(d), R.es);
     }
     std::vector<uint32_t> &carriers = out.carriers;
     carriers.assign(dist.size(), 0);
