@@ -1434,24 +1434,30 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
     if (n_regions == 0) return TFBS_OK;
     if (!a.order || !side) n_big = 0;
     n_big = std::min(n_big, n_regions);
-    // persistent grids (a.persist): the workgroups of each shape that fit the device at once
-    static int n_cu = 0, per_small = 0, per_big = 0;
-    if (!n_cu) {
-        int dev = 0;
+    // persistent grids (a.persist): the workgroups of each shape that fit the device at
+    // once (a function-local static: initialised once, thread-safe, for every ctx)
+    struct Fit {
+        int n_cu = 256, per_small = 2, per_big = 1;
+    };
+    static const Fit fit = [] {
+        Fit f;
+        int dev = 0, v = 0;
         (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0) n_cu = 256;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_small, key_fast_kernel<KfSmall>, KfSmall::kBlock, 0) !=
-                hipSuccess || per_small <= 0)
-            per_small = 2;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_big, key_fast_kernel<KfBig>, KfBig::kBlock, 0) !=
-                hipSuccess || per_big <= 0)
-            per_big = 1;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) f.n_cu = v;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, key_fast_kernel<KfSmall>, KfSmall::kBlock, 0) ==
+                hipSuccess && v > 0)
+            f.per_small = v;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, key_fast_kernel<KfBig>, KfBig::kBlock, 0) == hipSuccess &&
+            v > 0)
+            f.per_big = v;
         (void)hipGetLastError();
         if (getenv("TFBS_KF_PROF"))
             fprintf(stderr, "[kf prof] CUs %d, workgroups per CU: %d (%d threads, %zu B LDS), %d (%d threads, %zu B LDS)\n",
-                    n_cu, per_small, KfSmall::kBlock, key_fast_lds_bytes(false), per_big, KfBig::kBlock,
+                    f.n_cu, f.per_small, KfSmall::kBlock, key_fast_lds_bytes(false), f.per_big, KfBig::kBlock,
                     key_fast_lds_bytes(true));
-    }
+        return f;
+    }();
+    const int n_cu = fit.n_cu, per_small = fit.per_small, per_big = fit.per_big;
     auto grid = [&](uint32_t n, int per) { return a.persist ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
     hipError_t e = hipSuccess;
     // two shapes at once: the regions of many haplotypes (order[0, n_big), whole-CU
