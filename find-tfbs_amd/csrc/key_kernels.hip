@@ -744,15 +744,36 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     };
     // pairwise mode lists the dirty corrections while counting them, at the top of
     // s_cor downwards (the first kFCor); the walk lists them in a second pass
-    uint32_t nd = 0;
+    // (a wave of at most 64 pairwise steps keeps a bit per step and lists its
+    // corrections after the pass: one slot reservation for the wave, no atomic per step)
+    const uint32_t n_p = (nref + rpl - 1) / rpl;
+    const uint32_t n_l0 = U > wave * hpw ? (U - wave * hpw + kFWaves * hpw - 1) / (kFWaves * hpw) : 0u;
+    const bool stepbits = pairwise && n_l0 * n_p <= 64;
+    uint32_t nd = 0, it = 0;
+    uint64_t dm = 0;  // steps whose pair is dirty
     each_dirty([&](uint32_t l, const uint4 &q, bool dirty, bool uniform) {
         const uint32_t c = dirty ? __popc(q.w) : 0u;
         nd += c;
         if (!uniform) return;
+        if (stepbits) {
+            if (c) dm |= 1ull << it;
+            it++;
+            return;
+        }
         uint32_t at = slots(c, true, &s_ndirty);
         for (uint32_t m = q.w; c && m; m &= m - 1, at++)
             if (at < kFCor) s_cor[kFCor - 1 - at] = cor_entry(q.x + __builtin_ctz(m), l, 1);
     });
+    if (stepbits && nref) {
+        uint32_t at = slots(nd, true, &s_ndirty);
+        for (uint64_t m = dm; m; m &= m - 1) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(m);
+            const uint32_t l = wave * hpw + (k / n_p) * kFWaves * hpw + lane / rpl;
+            const uint4 q = s_ref[(k % n_p) * rpl + lane % rpl];
+            for (uint32_t b = q.w; b; b &= b - 1, at++)
+                if (at < kFCor) s_cor[kFCor - 1 - at] = cor_entry(q.x + __builtin_ctz(b), l, 1);
+        }
+    }
     uint32_t nD = 0;
     (void)block_excl_scan<kFWaves>(nd, s_w, nD);
     const bool dirty_listed = pairwise && nD <= kFCor;
