@@ -134,6 +134,8 @@ struct tfbs_ctx {
     // matrix-core window lists per depth class (ScanArgs::wlist), built at upload
     DevBuf<uint64_t> wl_off[2], wl_tmp;
     DevBuf<uint32_t> wl[2];
+    DevBuf<uint16_t> wl16[2];  // the narrow groups' window lists
+    DevBuf<uint8_t> gnarrow;   // per haplotype group of mfma_hpb: every haplotype <= kWlNarrowLen bases
     uint64_t wl_entries[2] = {0, 0};
     double wl_seconds = 0;                // the last build's wall time
     DevBuf<DevRegion> regions;
@@ -241,7 +243,7 @@ static int env_int(const char *name, int dflt) {
 
 // The matrix-core window lists of the haplotypes just put on the device (one
 // per depth class the plan has; scan.hpp build_window_lists).
-static int build_lists(tfbs_ctx *ctx, uint32_t n_haps) {
+static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t> &narrow) {
     const Plan &P = ctx->plan;
     if (P.m_supers.empty()) return TFBS_OK;
     const auto t0 = std::chrono::steady_clock::now();
@@ -256,23 +258,28 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps) {
     if ((rc = ctx->wl_tmp.ensure(scan_tmp_words((size_t)n_haps + 1))) ||
         (rc = ctx->druns.ensure(std::max<size_t>(ctx->druns.n, 1))))
         return rc;
+    if ((rc = ctx->gnarrow.put(narrow, ctx->stream))) return rc;
     WindowListBufs bufs{};
     for (int c = 0; c < 2; c++) {
         bufs.off[c] = lmin[c] ? ctx->wl_off[c].p : nullptr;
         bufs.list[c] = nullptr;
+        bufs.list16[c] = nullptr;
     }
+    bufs.gnarrow = narrow.empty() ? nullptr : ctx->gnarrow.p;
     bufs.scan_tmp = ctx->wl_tmp.p;
-    auto ensure = [](void *x, int c, uint64_t n, uint32_t **p) {
+    auto ensure = [](void *x, int c, uint64_t n, uint32_t **p, uint16_t **p16) {
         tfbs_ctx *cx = static_cast<tfbs_ctx *>(x);
         if (int e = cx->wl[c].ensure(n)) return e;
+        if (int e = cx->wl16[c].ensure(n)) return e;
         *p = cx->wl[c].p;
+        *p16 = cx->wl16[c].p;
         return TFBS_OK;
     };
     if ((rc = build_window_lists(ctx->haps.p, n_haps, ctx->druns.p, lmin, ctx->mfma_hpb, 1, bufs, ctx->wl_entries,
                                  ctx->stream, ensure, ctx)))
         return rc;
     for (int c = 0; c < 2; c++)
-        if (!lmin[c]) ctx->wl_off[c].release(), ctx->wl[c].release();
+        if (!lmin[c]) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->wl_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return TFBS_OK;
@@ -323,6 +330,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             (rc = ctx->spill_boff.ensure(nr + 1)))
             return rc;
         m.dedup = 1;
+        m.gnarrow = ctx->gnarrow.n ? ctx->gnarrow.p : nullptr;
         m.druns = ctx->druns.p;
         m.n_regions = ctx->n_regions;
         m.ref_hits = ctx->ref_hits.p;
@@ -334,6 +342,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.cand_over_cap = ctx->cand_over_cap;
         for (int c = 0; c < 2; c++) {
             m.wlist[c] = ctx->wl[c].p;
+            m.wlist16[c] = ctx->wl16[c].p;
             m.wlist_off[c] = ctx->wl_off[c].p;
         }
         HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
@@ -524,7 +533,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (ctx->asm_t1) (void)hipEventDestroy(ctx->asm_t1);
     ctx->words.release(); ctx->nmask.release(); ctx->counts.release(); ctx->posrel.release();
     ctx->druns.release(); ctx->wl_tmp.release();
-    for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release();
+    for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
+    ctx->gnarrow.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->asm_ctr.release(); ctx->key_flags.release();
     ctx->asm_redo.release(); ctx->cor_arena.release();
@@ -744,7 +754,10 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
                B.regions[order[ctx->asm_order_big]].hap_count > (uint32_t)big_u)
             ctx->asm_order_big++;
     }
-    if ((rc = build_lists(ctx, (uint32_t)B.haps.size()))) return rc;
+    std::vector<uint8_t> narrow((B.haps.size() + ctx->mfma_hpb - 1) / ctx->mfma_hpb, 1);  // (alive until the sync)
+    for (size_t h = 0; h < B.haps.size(); h++)
+        if (B.haps[h].len > kWlNarrowLen) narrow[h / ctx->mfma_hpb] = 0;
+    if ((rc = build_lists(ctx, (uint32_t)B.haps.size(), narrow))) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->counts_live = dense;
     ctx->resident = b;
@@ -1606,7 +1619,7 @@ int tfbs_matches(tfbs_ctx *ctx, const uint8_t *nucs, const uint64_t *pos, size_t
         (rc = ctx->posrel.put(posrel, ctx->stream)) || (rc = ctx->haps.put(haps, ctx->stream)) ||
         (rc = ctx->regions.put(regions, ctx->stream)) || (rc = ctx->inner.put(inner, ctx->stream)) ||
         (rc = ctx->counts.ensure(std::max<uint64_t>(P.pats.size(), 1))) || (rc = ctx->druns.ensure(1)) ||
-        (rc = build_lists(ctx, 1)))
+        (rc = build_lists(ctx, 1, std::vector<uint8_t>{(uint8_t)(n <= kWlNarrowLen)})))
         return rc;
     ctx->counts_live = true;
     ctx->resident = nullptr;

@@ -57,8 +57,13 @@ struct ScanArgs {
     // matrix-core window lists (build_window_lists), per depth class (2, 4): the
     // windows the scan reads, haplotype-major, entry = window << 6 | the haplotype's
     // index in its group of haps_per_block (<= 64); haplotype h's entries start at
-    // wlist_off[c][h] (n_haps + 1 offsets, relative to this launch's haps)
+    // wlist_off[c][h] (n_haps + 1 offsets, relative to this launch's haps); a
+    // narrow group (gnarrow[g], relative to this launch's groups: every haplotype of
+    // at most kWlNarrowLen bases, so window << 6 | haplotype fits 16 bits) has its
+    // entries at the same offsets of wlist16[c] instead (half the bytes to read)
     const uint32_t *wlist[2];
+    const uint16_t *wlist16[2];
+    const uint8_t *gnarrow;
     const uint64_t *wlist_off[2];
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
     // != 0 scans only their dirty windows (the lists); the HAP_REF haplotypes' hits
@@ -121,16 +126,20 @@ constexpr uint32_t kMMaxHapsPerBlock = 64;  // 6 bits of a window list entry
 // all windows [0, len - lmin + 1) of a haplotype, only the dirty ones of a
 // HAP_DEDUP haplotype when dedup (tfbs_internal.hpp); off[c] gets n_haps + 1
 // offsets, list[c] (grown with ensure_list) the entries.  Synchronises `stream`.
+constexpr uint32_t kWlNarrowLen = 1024;  // haplotypes of a narrow group: windows < 2^10
 struct WindowListBufs {
     uint64_t *off[2];      // n_haps + 1 each
     uint64_t *scan_tmp;    // >= scan_tmp_words(n_haps + 1)
     uint32_t *list[2];
+    uint16_t *list16[2];   // the narrow groups' entries (gnarrow: one flag per group of hpb)
+    const uint8_t *gnarrow;
     uint64_t list_cap[2];  // entries
 };
 size_t scan_tmp_words(size_t n);
 int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
                        uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
-                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p), void *ensure_ctx);
+                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
+                       void *ensure_ctx);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach
 // the waves per SIMD its registers allow.
 void mfma_depth_budgets(uint32_t out[9]);

@@ -172,6 +172,15 @@ __shared__ uint4 s_hd[kMMaxHapsPerBlock];  // the group's haplotypes: LaneHap
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 
+// What the firing path of a round needs: the group's window list (wl, nw
+// entries) for the drain, the first global tile and haplotype of the workgroup.
+struct GroupCtx {
+    const uint32_t *wl;
+    const uint16_t *wl16;  // a narrow group's list (16-bit entries), else null
+    uint32_t nw, tile0, h0;
+    __device__ __forceinline__ uint32_t at(uint32_t q) const { return wl16 ? (uint32_t)wl16[q] : wl[q]; }
+};
+
 // Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
 // one load per column of the strand's blocks of 8 (zero-padded), all issued
 // before the first is summed (the rescoring runs where no accumulator is
@@ -293,8 +302,9 @@ __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
            (size_t)wave * wave_cand_cap(A);
 }
 
-__device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *wl, uint32_t nw, uint32_t tile0,
-                                            uint32_t h0, uint32_t n, uint32_t wave, uint32_t lane, uint32_t &cn) {
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const GroupCtx &G, uint32_t n, uint32_t wave,
+                                            uint32_t lane, uint32_t &cn) {
+    const uint32_t nw = G.nw, tile0 = G.tile0, h0 = G.h0;
     uint2 *list = cand_list(A, wave);
     const uint32_t cap = wave_cand_cap(A);
     for (uint32_t e0 = 0; e0 < n; e0 += 64) {
@@ -332,7 +342,7 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const uint32_t *w
             if (have) {
                 const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-                const uint32_t we = wl[q], hl = we & (kMMaxHapsPerBlock - 1), i = we >> 6, g = g0 + (b >> 4);
+                const uint32_t we = G.at(q), hl = we & (kMMaxHapsPerBlock - 1), i = we >> 6, g = g0 + (b >> 4);
                 if (slot < cap) {
                     list[slot] = make_uint2(g | (hl << 24), i);
                 } else {  // rescored after the scan (no rescoring code, whose loads would stay
@@ -478,12 +488,6 @@ __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, con
     for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
 }
 
-// What the firing path of a round needs: the group's window list (wl, nw
-// entries) for the drain, the first global tile and haplotype of the workgroup.
-struct GroupCtx {
-    const uint32_t *wl;
-    uint32_t nw, tile0, h0;
-};
 
 // The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
 // ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
@@ -515,7 +519,7 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             // accumulator is live across a drain)
             if (f0) {
                 if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                    drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
+                    drain_queue(A, G, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x0 = coarse_test(c0);
@@ -525,7 +529,7 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             }
             if (f1) {
                 if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                    drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
+                    drain_queue(A, G, qn, wave, lane, cn);
                     qn = 0;
                     round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
                     x1 = coarse_test(c1);
@@ -542,7 +546,7 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             const uint64_t f0 = __ballot(x0 != 0);
             if (__builtin_expect(f0 == 0, 1)) continue;
             if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                drain_queue(A, G.wl, G.nw, G.tile0, G.h0, qn, wave, lane, cn);
+                drain_queue(A, G, qn, wave, lane, cn);
                 qn = 0;
                 tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
                 x0 = coarse_test(c0);
@@ -603,6 +607,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     const uint64_t e0 = A.wlist_off[NK > 2][h0];
     GroupCtx G;
     G.wl = A.wlist[NK > 2] + e0;
+    G.wl16 = (A.gnarrow && A.gnarrow[hg]) ? A.wlist16[NK > 2] + e0 : nullptr;
     G.nw = (uint32_t)(A.wlist_off[NK > 2][h1] - e0);
     G.tile0 = S.tile0;
     G.h0 = h0;
@@ -621,8 +626,8 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     // lane l scores window row l & 31 of each tile
     auto entries = [&](uint32_t p, uint32_t &ea, uint32_t &eb) {
         const uint32_t q = kMWindows * 2 * p + (lane & 31);
-        ea = G.wl[min(q, G.nw - 1)];
-        eb = G.wl[min(q + kMWindows, G.nw - 1)];
+        ea = G.at(min(q, G.nw - 1));
+        eb = G.at(min(q + kMWindows, G.nw - 1));
     };
     uint32_t p = next_pair(), ea = 0, eb = 0;
     if (p < npair) entries(p, ea, eb);
@@ -636,7 +641,7 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
         p = pn;
     }
-    drain_queue(A, G.wl, G.nw, G.tile0, h0, qn, wave, lane, cn);  // the wave's last entries
+    drain_queue(A, G, qn, wave, lane, cn);  // the wave's last entries
     rescore_list(A, words, h0, wave, lane, cn);
 }
 
@@ -737,13 +742,18 @@ __global__ __launch_bounds__(256) void wl_count_kernel(const DevHap *__restrict_
 __global__ __launch_bounds__(256) void wl_fill_kernel(const DevHap *__restrict__ haps, uint32_t n,
                                                       const uint32_t *__restrict__ druns, uint32_t lmin, uint32_t S,
                                                       uint32_t dedup, uint32_t hpb, const uint64_t *__restrict__ off,
-                                                      uint32_t *__restrict__ list) {
+                                                      uint32_t *__restrict__ list, uint16_t *__restrict__ list16,
+                                                      const uint8_t *__restrict__ gnarrow) {
     const uint32_t h = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (h >= n) return;
     uint64_t at = off[h];
     const uint32_t hl = h % hpb;
+    const bool narrow = gnarrow && gnarrow[h / hpb];
     for_windows(haps[h], druns, lmin, S, dedup, [&](uint32_t lo, uint32_t hi) {
-        for (uint32_t w = lo + lane; w < hi; w += 64) list[at + (w - lo)] = (w << 6) | hl;
+        for (uint32_t w = lo + lane; w < hi; w += 64) {
+            if (narrow) list16[at + (w - lo)] = (uint16_t)((w << 6) | hl);
+            else list[at + (w - lo)] = (w << 6) | hl;
+        }
         at += hi - lo;
     });
 }
@@ -832,7 +842,8 @@ size_t scan_tmp_words(size_t n) {
 
 int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
                        uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
-                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p), void *ensure_ctx) {
+                       int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
+                       void *ensure_ctx) {
     for (int c = 0; c < 2; c++) {
         total[c] = 0;
         if (!lmin[c]) continue;
@@ -843,10 +854,11 @@ int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *drun
         hipError_t e = hipMemcpyAsync(&total[c], bufs.off[c] + n_haps, 8, hipMemcpyDeviceToHost, stream);
         if (e == hipSuccess) e = hipStreamSynchronize(stream);
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("window list size: ") + hipGetErrorString(e));
-        if (int rc = ensure_list(ensure_ctx, c, std::max<uint64_t>(total[c], 1), &bufs.list[c])) return rc;
+        if (int rc = ensure_list(ensure_ctx, c, std::max<uint64_t>(total[c], 1), &bufs.list[c], &bufs.list16[c]))
+            return rc;
         if (n_haps)
             hipLaunchKernelGGL(wl_fill_kernel, dim3((n_haps + 3) / 4), dim3(256), 0, stream, haps, n_haps, druns,
-                               lmin[c], S, dedup, hpb, bufs.off[c], bufs.list[c]);
+                               lmin[c], S, dedup, hpb, bufs.off[c], bufs.list[c], bufs.list16[c], bufs.gnarrow);
         e = hipGetLastError();
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("wl_fill_kernel: ") + hipGetErrorString(e));
     }
@@ -911,6 +923,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.haps = a0.haps + h0;
             a.hap_base = a0.hap_base + h0;
             for (int c = 0; c < 2; c++) a.wlist_off[c] = a0.wlist_off[c] ? a0.wlist_off[c] + h0 : nullptr;
+            a.gnarrow = a0.gnarrow ? a0.gnarrow + g0 : nullptr;
             a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
             a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
             a.region_base = region;
