@@ -136,6 +136,7 @@ struct tfbs_ctx {
     DevBuf<uint32_t> wl[2];
     DevBuf<uint16_t> wl16[2];  // the narrow groups' window lists
     DevBuf<uint8_t> gnarrow;   // per haplotype group of mfma_hpb: every haplotype <= kWlNarrowLen bases
+    DevBuf<uint4> hd;          // the matrix-core scan's compact haplotype descriptors
     uint64_t wl_entries[2] = {0, 0};
     double wl_seconds = 0;                // the last build's wall time
     DevBuf<DevRegion> regions;
@@ -266,6 +267,8 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
         bufs.list16[c] = nullptr;
     }
     bufs.gnarrow = narrow.empty() ? nullptr : ctx->gnarrow.p;
+    if ((rc = ctx->hd.ensure(std::max<uint32_t>(n_haps, 1)))) return rc;
+    bufs.hd = ctx->hd.p;
     bufs.scan_tmp = ctx->wl_tmp.p;
     auto ensure = [](void *x, int c, uint64_t n, uint32_t **p, uint16_t **p16) {
         tfbs_ctx *cx = static_cast<tfbs_ctx *>(x);
@@ -331,6 +334,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             return rc;
         m.dedup = 1;
         m.gnarrow = ctx->gnarrow.n ? ctx->gnarrow.p : nullptr;
+        m.hd = ctx->hd.p;
         m.druns = ctx->druns.p;
         m.n_regions = ctx->n_regions;
         m.ref_hits = ctx->ref_hits.p;
@@ -535,6 +539,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->druns.release(); ctx->wl_tmp.release();
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
     ctx->gnarrow.release();
+    ctx->hd.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->asm_ctr.release(); ctx->key_flags.release();
     ctx->asm_redo.release(); ctx->cor_arena.release();

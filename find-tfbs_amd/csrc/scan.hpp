@@ -63,6 +63,7 @@ struct ScanArgs {
     // entries at the same offsets of wlist16[c] instead (half the bytes to read)
     const uint32_t *wlist[2];
     const uint16_t *wlist16[2];
+    const uint4 *hd;  // matrix-core scan: per haplotype (word_off, len, flags, nmask_off) of haps (build_window_lists)
     const uint8_t *gnarrow;
     const uint64_t *wlist_off[2];
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
@@ -133,6 +134,7 @@ struct WindowListBufs {
     uint32_t *list[2];
     uint16_t *list16[2];   // the narrow groups' entries (gnarrow: one flag per group of hpb)
     const uint8_t *gnarrow;
+    uint4 *hd;             // n_haps compact descriptors (ScanArgs::hd), written here
     uint64_t list_cap[2];  // entries
 };
 size_t scan_tmp_words(size_t n);

@@ -669,17 +669,14 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
             for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
             tab[k] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
         }
-        if (threadIdx.x < hn) {
-            const DevHap &h = A.haps[h0 + threadIdx.x];
-            s_hd[threadIdx.x] = make_uint4(h.word_off, h.len, h.flags, h.nmask_off);
-        }
+        if (threadIdx.x < hn) s_hd[threadIdx.x] = A.hd[h0 + threadIdx.x];  // (16 of DevHap's 48 bytes)
     }
     const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     const uint32_t *words = A.words;
     if (STAGED) {
-        const uint32_t hl = h0 + hn - 1;
-        const uint32_t wbeg = A.haps[h0].word_off;
-        const uint32_t wend = A.haps[hl].word_off + (A.haps[hl].len + 15) / 16 + 3;
+        const uint4 f = A.hd[h0], l = A.hd[h0 + hn - 1];
+        const uint32_t wbeg = f.x;
+        const uint32_t wend = l.x + (l.y + 15) / 16 + 3;
         uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max) / 4;
         for (uint32_t i = threadIdx.x; i < wend - wbeg; i += kMBlock) s_words[i] = A.words[wbeg + i];
         words = s_words - wbeg;
@@ -756,6 +753,16 @@ __global__ __launch_bounds__(256) void wl_fill_kernel(const DevHap *__restrict__
         }
         at += hi - lo;
     });
+}
+
+// The scan's compact haplotype descriptors (ScanArgs::hd): word offset, length,
+// flags, N-mask offset of every DevHap.
+__global__ __launch_bounds__(256) void hd_kernel(const DevHap *__restrict__ haps, uint32_t n, uint4 *__restrict__ hd) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h < n) {
+        const DevHap x = haps[h];
+        hd[h] = make_uint4(x.word_off, x.len, x.flags, x.nmask_off);
+    }
 }
 
 // In-place exclusive scan of u64 values, 4096 per workgroup; sums[b] = tile b's total.
@@ -844,6 +851,8 @@ int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *drun
                        uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
                        int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
                        void *ensure_ctx) {
+    if (n_haps && bufs.hd) hipLaunchKernelGGL(hd_kernel, dim3((n_haps + 255) / 256), dim3(256), 0, stream, haps, n_haps,
+                                             bufs.hd);
     for (int c = 0; c < 2; c++) {
         total[c] = 0;
         if (!lmin[c]) continue;
@@ -921,6 +930,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.msupers = a0.msupers + s0;
             a.n_msupers = ns;
             a.haps = a0.haps + h0;
+            a.hd = a0.hd + h0;
             a.hap_base = a0.hap_base + h0;
             for (int c = 0; c < 2; c++) a.wlist_off[c] = a0.wlist_off[c] ? a0.wlist_off[c] + h0 : nullptr;
             a.gnarrow = a0.gnarrow ? a0.gnarrow + g0 : nullptr;
