@@ -829,8 +829,8 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
 // asm_ctr: [0, 2) the scan's overflow counters (copied), 2 regions left to key_asm,
 // 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
-// give-up reasons, 16 / 17 key_fast_kernel's region counters, [18, 24) spare; the
-// spill buckets after.
+// give-up reasons, 16 / 17 key_fast_kernel's region counters, 18 post_scan_kernel's
+// finished workgroups, [19, 24) spare; the spill buckets after.
 constexpr size_t kAsmCtrWords = 24;
 
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
@@ -858,16 +858,12 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     // the assembly's counters and the spill buckets' (at asm_ctr + kAsmCtrWords): one memset
     HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0,
                            (kAsmCtrWords + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4, ctx->stream));
-    if (mfma && post) {
-        if (!ctx->post_done) {  // (once per scan: the rescoring appends spill records)
-            const int f = launch_post_scan(ctx->last_margs, ctx->stream);
-            if (f < 0) return f;
-            ctx->post_done = true;
-        }
-        if ((rc = launch_spill_buckets(ctx->over.p, ctx->spill_cap, ctx->spill.p, std::max<uint32_t>(1, nr),
-                                       ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p, ctx->stream,
-                                       true)))
+    if (mfma && post) {  // overflow candidates rescored (once per scan: they append spill records) + spill buckets
+        if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18, std::max<uint32_t>(1, nr),
+                                    ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p,
+                                    ctx->stream)))
             return rc;
+        ctx->post_done = true;
     }
     AsmArgs a = asm_args(ctx, B, 0);
     a.key_first = ctx->key_first.p;

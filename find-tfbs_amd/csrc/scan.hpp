@@ -120,6 +120,10 @@ int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, u
                 const hipStream_t *streams, uint32_t n_streams, HitSrc *srcs, uint32_t *n_srcs);
 // Rescores the candidates past the waves' lists (after launch_mfma on the same stream).
 int launch_post_scan(const ScanArgs &a, hipStream_t stream);
+// The same (when cand) and the spill records' buckets by region (boff[0 .. n_regions],
+// sorted) in one launch; *done and bcnt[0 .. n_regions] must be zero.
+int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
+                      uint32_t *sorted, hipStream_t stream);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
 constexpr uint32_t kMMaxHapsPerBlock = 64;  // 6 bits of a window list entry
 // Builds the window lists of every haplotype of the batch for the depth classes

@@ -825,6 +825,80 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_dept
 
 }  // namespace
 
+// The scan's post-processing in one launch: every workgroup rescores its share of
+// the overflow candidates (cand_over_kernel's work, when `cand`), then the last
+// workgroup to finish -- the one whose ticket on *done (zeroed before) is the
+// grid's last -- buckets the spill records by region (a histogram, an exclusive
+// scan into boff, a scatter into sorted; bcnt n_regions + 1 zeroed before) on its
+// own: spills are rare, and no records (the usual case) costs one counter read.
+constexpr uint32_t kPostBlock = 256;
+__global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint32_t cand, uint32_t *done,
+                                                              uint32_t n_regions, uint32_t *__restrict__ bcnt,
+                                                              uint32_t *__restrict__ boff,
+                                                              uint32_t *__restrict__ sorted) {
+    __shared__ uint32_t s_last, s_sum[kPostBlock];
+    const uint32_t tid = threadIdx.x;
+    if (cand) {
+        const uint32_t n = min(A.over[1], A.cand_over_cap);
+        for (uint32_t k = blockIdx.x * kPostBlock + tid; k < n; k += gridDim.x * kPostBlock) {
+            const uint32_t hap = A.cand_over[3 * (size_t)k], g = A.cand_over[3 * (size_t)k + 1];
+            const DevHap hp = A.haps[hap];
+            uint32_t key0 = 0;
+            for (uint32_t m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0); m;
+                 m &= m - 1)
+                spill_record(A, hp.region, hap, key0 + __builtin_ctz(m));
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();  // (release: this workgroup's spill records)
+        s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // (acquire: every workgroup's records)
+    const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
+    if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
+    for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
+    __threadfence_block();
+    __syncthreads();
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 <= n_regions; b0 += kPostBlock) {  // boff[0 .. n_regions]: exclusive prefix
+        const uint32_t i = b0 + tid;
+        const uint32_t v = i < n_regions ? bcnt[i] : 0u;
+        s_sum[tid] = v;
+        __syncthreads();
+        for (uint32_t o = 1; o < kPostBlock; o <<= 1) {
+            const uint32_t t = tid >= o ? s_sum[tid - o] : 0u;
+            __syncthreads();
+            s_sum[tid] += t;
+            __syncthreads();
+        }
+        if (i <= n_regions) boff[i] = carry + s_sum[tid] - v;
+        if (i < n_regions) bcnt[i] = 0;  // the scatter's fill counters
+        carry += s_sum[kPostBlock - 1];
+        __syncthreads();
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t e = tid; e < n; e += kPostBlock) {
+        const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
+        const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
+        sorted[3 * (size_t)at] = A.spill[3 * (size_t)e];
+        sorted[3 * (size_t)at + 1] = A.spill[3 * (size_t)e + 1];
+        sorted[3 * (size_t)at + 2] = A.spill[3 * (size_t)e + 2];
+    }
+}
+
+int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
+                      uint32_t *sorted, hipStream_t stream) {
+    hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? 256 : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
+                       n_regions, bcnt, boff, sorted);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("post_scan_kernel launch: ") + hipGetErrorString(e));
+    return TFBS_OK;
+}
+
 int launch_post_scan(const ScanArgs &a, hipStream_t stream) {
     hipLaunchKernelGGL(cand_over_kernel, dim3(256), dim3(256), 0, stream, a);
     const hipError_t e = hipGetLastError();
