@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -980,7 +981,9 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
         s0 = s1;
     }
     for (size_t gi = 0; gi < groups.size(); gi++) {
-        const uint32_t s0 = groups[groups.size() - 1 - gi].first, s1 = groups[groups.size() - 1 - gi].second;
+        static const bool shallow_first = getenv("TFBS_SCAN_SHALLOW_FIRST") && atoi(getenv("TFBS_SCAN_SHALLOW_FIRST"));
+        const size_t gk = shallow_first ? gi : groups.size() - 1 - gi;  // (A/B: the launch order of the depths)
+        const uint32_t s0 = groups[gk].first, s1 = groups[gk].second;
         const hipStream_t stream = streams[gi % n_streams];
         const uint32_t nk = supers[s0].nk;
         size_t img_bytes = 0;
