@@ -861,7 +861,7 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
     if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
     for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
-    __threadfence_block();
+    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
     uint32_t carry = 0;
     for (uint32_t b0 = 0; b0 <= n_regions; b0 += kPostBlock) {  // boff[0 .. n_regions]: exclusive prefix
@@ -880,7 +880,7 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
         carry += s_sum[kPostBlock - 1];
         __syncthreads();
     }
-    __threadfence_block();
+    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
     for (uint32_t e = tid; e < n; e += kPostBlock) {
         const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
