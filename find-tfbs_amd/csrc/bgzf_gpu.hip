@@ -124,6 +124,7 @@ struct Stage {
     uint32_t cum[kStCum];
     uint32_t crc_tab[256];
     uint32_t crc_ops[kCrcOps * 32];
+    uint32_t crc_slice[768];  // slice-by-4 tables 1-3 (bgzf_wave_kernel)
 };
 
 // the block kernel's stage, at file scope so that every access compiles to LDS
@@ -1012,6 +1013,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     {
         for (uint32_t i = tid; i < 256; i += kWv) S.crc_tab[i] = A.crc_tab[i];
         for (uint32_t i = tid; i < kCrcOps * 32; i += kWv) S.crc_ops[i] = A.crc_ops[i];
+        for (uint32_t i = tid; i < 768; i += kWv) S.crc_slice[i] = A.crc_slice[i];
         for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
         for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
         const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
@@ -1121,55 +1123,87 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         uint32_t crc = 0;
         if (q1 - q0 == 64 && (q0 & 63) == 0) {  // a whole padded slice: dword reads, no bank conflicts
             const uint32_t *w = reinterpret_cast<const uint32_t *>(g_text) + (txt_at((uint32_t)q0) >> 2);
-            for (uint32_t i = 0; i < 16; i++) {
-                const uint32_t x = w[i];
-                crc = crc_byte(S.crc_tab, crc, x & 0xFFu);
-                crc = crc_byte(S.crc_tab, crc, (x >> 8) & 0xFFu);
-                crc = crc_byte(S.crc_tab, crc, (x >> 16) & 0xFFu);
-                crc = crc_byte(S.crc_tab, crc, x >> 24);
+            for (uint32_t i = 0; i < 16; i++) {  // slice-by-4: four independent table reads per dword
+                const uint32_t x = w[i] ^ crc;
+                crc = S.crc_slice[512 + (x & 0xFFu)] ^ S.crc_slice[256 + ((x >> 8) & 0xFFu)] ^
+                      S.crc_slice[(x >> 16) & 0xFFu] ^ S.crc_tab[x >> 24];
             }
         } else {
             for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[txt_at((uint32_t)q)]);
         }
-        {
-            const uint32_t *M = A.crc_ops64 + 32 * (kWv - 1 - tid);
+        // CRC(a b) = x^(8 |b|) CRC(a) ^ CRC(b): thread t's bytes precede t + 1's and every
+        // slice after the first non-empty one holds 64 bytes, so a binary tree over the
+        // threads shifts by 64 x 2^k bytes at level k (operator k + 6, in LDS: the same
+        // columns for every lane); 6 levels in the wave, 4 over the waves' results, then
+        // the init term (a full block's precomputed)
+        auto apply = [&](const uint32_t *M, uint32_t x) {
             uint32_t r = 0;
-            for (uint32_t i = 0; i < 32; i++) r ^= ((crc >> i) & 1u) ? M[i] : 0u;
-            crc = r;
+#pragma unroll
+            for (uint32_t i = 0; i < 32; i++) r ^= ((x >> i) & 1u) ? M[i] : 0u;
+            return r;
+        };
+#pragma unroll
+        for (uint32_t k = 0; k < 6; k++) {
+            const uint32_t other = (uint32_t)__shfl_down((int)crc, 1u << k);
+            const uint32_t c2 = apply(S.crc_ops + 32 * (k + 6), crc) ^ other;
+            if ((lane & ((2u << k) - 1u)) == 0) crc = c2;
         }
-        for (int dd = 32; dd; dd >>= 1) crc ^= (uint32_t)__shfl_xor((int)crc, dd);
-        __syncthreads();
         if (lane == 0) g_red[wave] = crc;
+        __syncthreads();
+        if (wave == 0) {
+            crc = lane < kWv / 64 ? g_red[lane] : 0u;
+#pragma unroll
+            for (uint32_t k = 6; k < 10; k++) {
+                const uint32_t other = (uint32_t)__shfl_down((int)crc, 1u << (k - 6));
+                const uint32_t c2 = apply(S.crc_ops + 32 * (k + 6), crc) ^ other;
+                if ((lane & ((2u << (k - 6)) - 1u)) == 0) crc = c2;
+            }
+            if (lane == 0)
+                g_red[0] = crc ^ (n == kBgzfRaw ? A.crc_full : crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n)) ^ 0xFFFFFFFFu;
+        }
         __syncthreads();
     }
     stamp(4);
+    // the block (header, deflate data, CRC32, ISIZE) in aligned 16-byte stores, every
+    // thread its share: inside the deflate data a dword is two bit-buffer words
+    // funnelled (block byte 18 = bit-buffer byte 0), the few dwords around it byte by byte
     uint8_t *out = A.out + (size_t)blockIdx.x * kBgzfMax;
     const uint32_t clen = stored ? 5 + n : dbytes;
     const uint32_t bsize = 18 + clen + 8;
-    if (stored) {  // BFINAL = 1, BTYPE = 00, LEN, NLEN, the bytes
-        for (uint32_t i = tid; i < n; i += kWv) out[23 + i] = g_text[txt_at(i)];
-        if (tid == 0) {
-            out[18] = 1;
-            out[19] = (uint8_t)n;
-            out[20] = (uint8_t)(n >> 8);
-            out[21] = (uint8_t)~n;
-            out[22] = (uint8_t)(~n >> 8);
+    const uint32_t crc32 = g_red[0];
+    auto byte_at = [&](uint32_t p) -> uint32_t {
+        if (p < 16) {
+            constexpr uint32_t h0 = 0x04088b1fu, h2 = 0x0006ff00u, h3 = 0x00024342u;
+            const uint32_t w = (p >> 2) == 0 ? h0 : (p >> 2) == 2 ? h2 : (p >> 2) == 3 ? h3 : 0u;
+            return (w >> (8 * (p & 3))) & 0xFFu;
         }
-    } else {
-        const uint8_t *src = reinterpret_cast<const uint8_t *>(g_bits);
-        for (uint32_t i = tid; i < dbytes; i += kWv) out[18 + i] = src[i];
+        if (p < 18) return ((bsize - 1) >> (8 * (p - 16))) & 0xFFu;
+        if (p < 18 + clen) {
+            if (!stored) return (g_bits[(p - 18) >> 2] >> (8 * ((p - 18) & 3))) & 0xFFu;
+            if (p >= 23) return g_text[txt_at(p - 23)];
+            const uint32_t len = n | ((~n & 0xFFFFu) << 16);  // LEN, NLEN after BFINAL = 1, BTYPE = 00
+            return p == 18 ? 1u : (len >> (8 * (p - 19))) & 0xFFu;
+        }
+        if (p < 22 + clen) return (crc32 >> (8 * (p - 18 - clen))) & 0xFFu;
+        if (p < bsize) return (n >> (8 * (p - 22 - clen))) & 0xFFu;
+        return 0u;
+    };
+    const uint32_t n16 = (bsize + 15) / 16;
+    for (uint32_t c = tid; c < n16; c += kWv) {
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t p = 16 * c + 4 * k;
+            if (!stored && p >= 20 && p + 4 <= 18 + clen) {
+                const uint32_t j = (p - 18) >> 2;  // p - 18 = 4 j + 2
+                w[k] = (g_bits[j] >> 16) | (g_bits[j + 1] << 16);
+            } else {
+                w[k] = byte_at(p) | byte_at(p + 1) << 8 | byte_at(p + 2) << 16 | byte_at(p + 3) << 24;
+            }
+        }
+        reinterpret_cast<uint4 *>(out)[c] = uint4{w[0], w[1], w[2], w[3]};
     }
-    if (tid == 0) {
-        uint32_t x = 0;
-        for (uint32_t w = 0; w < kWv / 64; w++) x ^= g_red[w];
-        const uint32_t crc32 = x ^ crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n) ^ 0xFFFFFFFFu;
-        const uint8_t hdr[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43, 2, 0,
-                                 (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
-        for (int i = 0; i < 18; i++) out[i] = hdr[i];
-        for (int i = 0; i < 4; i++) out[18 + clen + i] = (uint8_t)(crc32 >> (8 * i));
-        for (int i = 0; i < 4; i++) out[18 + clen + 4 + i] = (uint8_t)(n >> (8 * i));
-        A.out_len[blockIdx.x] = bsize;
-    }
+    if (tid == 0) A.out_len[blockIdx.x] = bsize;
     stamp(5);
     if (pf && tid == 0) {
         pf[6] = n_items;
@@ -1212,7 +1246,7 @@ __global__ __launch_bounds__(256) void bgzf_compact_kernel(const uint8_t *__rest
 
 }  // namespace
 
-void bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *ops64) {
+uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice) {
     for (uint32_t i = 0; i < 256; i++) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
@@ -1230,19 +1264,25 @@ void bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *ops64) {
                 if ((v >> j) & 1u) r ^= ops[32 * (k - 1) + j];
             ops[32 * k + i] = r;
         }
-    // shifts by 64 k bytes, k < kWv: identity, then each the one before composed with 64 bytes
-    for (uint32_t i = 0; i < 32; i++) ops64[i] = 1u << i;
-    const uint32_t *M64 = ops + 32 * 6;
-    for (uint32_t k = 1; k < (uint32_t)kWv; k++)
-        for (uint32_t i = 0; i < 32; i++) {
-            uint32_t v = ops64[32 * (k - 1) + i], r = 0;
-            for (uint32_t j = 0; j < 32; j++)
-                if ((v >> j) & 1u) r ^= M64[j];
-            ops64[32 * k + i] = r;
+    // slice-by-4: table k gives the CRC of a byte followed by k zero bytes
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = tab[i];
+        for (uint32_t k = 0; k < 3; k++) {
+            c = tab[c & 0xFFu] ^ (c >> 8);
+            slice[256 * k + i] = c;
         }
+    }
+    // x^(8 kBgzfRaw) on 0xFFFFFFFF: the operators of kBgzfRaw's set bits in turn
+    uint32_t v = 0xFFFFFFFFu;
+    for (uint32_t k = 0, n = kBgzfRaw; n; k++, n >>= 1)
+        if (n & 1u) {
+            uint32_t r = 0;
+            for (uint32_t j = 0; j < 32; j++)
+                if ((v >> j) & 1u) r ^= ops[32 * k + j];
+            v = r;
+        }
+    return v;
 }
-
-uint32_t bgzf_crc_ops64_count() { return (uint32_t)kWv; }
 
 int launch_row_cum(const BgArgs &a, hipStream_t stream) {
     if (a.n_rows == 0) return TFBS_OK;

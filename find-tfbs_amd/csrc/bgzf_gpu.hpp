@@ -27,15 +27,17 @@ struct BgArgs {
     uint32_t *out_len;          // the blocks' sizes
     const uint32_t *crc_tab;    // CRC32 byte table
     const uint32_t *crc_ops;    // kBgzfOps x 32 columns
-    const uint32_t *crc_ops64;  // bgzf_crc_ops64_count() x 32 columns: shifts by 64 k bytes
+    const uint32_t *crc_slice;  // slice-by-4 tables 1-3 (3 x 256; table 0 is crc_tab)
+    uint32_t crc_full;          // x^(8 kBgzfRaw) applied to 0xFFFFFFFF (a full block's CRC init term)
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
     uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 16 words of phase clocks and counts
 };
 size_t bgzf_plan_bytes();
 
-// CRC32 table and the x^(8 * 2^k) operators (host side, uploaded once).
-uint32_t bgzf_crc_ops64_count();
-void bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *ops64);
+// CRC32 table, the x^(8 * 2^k) operators and the slice-by-4 tables 1-3 (host side,
+// uploaded once: 256 + 32 kBgzfOps + 768 words); returns crc_full.
+constexpr size_t kBgzfCrcWords = 256 + 32 * kBgzfOps + 768;
+uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice);
 // Per row: its genotype text offsets every 64 samples.
 int launch_row_cum(const BgArgs &a, hipStream_t stream);
 // Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a

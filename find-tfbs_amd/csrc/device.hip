@@ -184,6 +184,7 @@ struct tfbs_ctx {
     DevBuf<uint8_t> bg_tok_len, bg_plans;
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
+    uint32_t bg_crc_full = 0;         // bgzf_crc_tables' full-block CRC init term
     DevBuf<uint64_t> kf_prof;         // TFBS_KF_PROF: key_fast_kernel phase clocks and sizes per region
     DevBuf<uint32_t> asm_order;       // the resident batch's regions by distinct haplotypes, most first
     uint32_t asm_order_n = 0;         // regions asm_order holds (0: none)
@@ -1426,10 +1427,11 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
             if ((rc = pp.drain_oldest(ctx, fd))) return rc;
         return TFBS_OK;
     }
-    if (!ctx->bg_crc.n) {  // CRC32 byte table and shift operators, once per ctx
-        std::vector<uint32_t> t(256 + 32 * kBgzfOps + 32 * tfbs::bgzf_crc_ops64_count());
-        tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
+    if (!ctx->bg_crc.n) {  // CRC32 byte table, shift operators and slice tables, once per ctx
+        std::vector<uint32_t> t(tfbs::kBgzfCrcWords);
+        ctx->bg_crc_full = tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
         if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
+        HIP_TRY(hipStreamSynchronize(ctx->stream));  // (t goes out of scope)
     }
     heads.assign(plan.heads.begin(), plan.heads.end());
     if ((rc = ctx->bg_rows.put(plan.rows, ctx->stream)) || (rc = ctx->bg_heads.put(heads, ctx->stream)) ||
@@ -1449,7 +1451,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.text_bytes = plan.text_bytes;
     a.crc_tab = ctx->bg_crc.p;
     a.crc_ops = ctx->bg_crc.p + 256;
-    a.crc_ops64 = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
+    a.crc_slice = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
+    a.crc_full = ctx->bg_crc_full;
     if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
     // blocks per launch (512 MiB of block slots); TFBS_BGZF_BATCH_BLOCKS=n: smaller
     // launches, so one call cycles the kBgSlots slots (the tests' path)

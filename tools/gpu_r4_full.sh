@@ -11,3 +11,8 @@ TFBS_KF_PROF=1 timeout -k 10 300 python3 bench.py --steps 2 --warmup 1 --no-cpu 
 grep "kf prof" $O/kf.err | tail -4 | cut -c1-300
 bash tools/trace_e2e.sh ${T}_e2e_c3 || exit 1
 bash tools/trace_e2e.sh ${T}_e2e_c5 --workload C5 || exit 1
+# A/B of the depth launches' order (shallow class first)
+for v in 0 1; do
+  TFBS_SCAN_SHALLOW_FIRST=$v timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --no-cpu --no-e2e > $O/order_$v.json 2> $O/order_$v.err || { echo "order $v failed"; exit 1; }
+  echo "shallow_first=$v $(grep -o '"ms_per_step": [0-9.]*' $O/order_$v.json) $(grep -o '"step_device_ms": {[^}]*}' $O/order_$v.json)"
+done
