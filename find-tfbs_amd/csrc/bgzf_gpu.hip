@@ -741,6 +741,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // items, so all counts arrive (items go to the waves round-robin, in order).
 // Then item i's end is published.
 __device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_t lane) {
+#ifdef BG_PROBE_NOPLACE  // (timing probe: no look-back, wrong offsets)
+    if (total != 0xFFFFFFFFu) return 64 * 128 * (i & 3);
+#endif
     if (lane == 0) __hip_atomic_store(&g_agg[i], total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     uint32_t acc = 3;  // BFINAL + BTYPE before item 0
     for (int32_t hi = (int32_t)i; hi > 0;) {
@@ -873,7 +876,11 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     // 8-bit codes and a row's first 8 samples: sample by sample
     uint32_t dist = 0;
     const bool want = full && !run && t >= 3;
+#ifdef BG_PROBE_NOLB
+    const bool packed = false && want;
+#else
     const bool packed = want && v.R.width <= 4 && s >= kLookback;
+#endif
     uint32_t kk = 0, P = 0;
     if (packed) {
         const uint32_t w = v.R.width, bit0 = (s - kLookback) * w, a = (uint32_t)(v.cbase + (int32_t)(bit0 >> 3));
@@ -923,7 +930,11 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         if ((r == 1 || r == 2) && Lr >= 3 && a <= Lr - 3 && Lr - 3 < b) m2 = 3;
     }
     // the text's bytes (for the CRC)
-    if (full) {  // its dwords, ORed (neighbouring texts share edge dwords)
+#ifdef BG_PROBE_NOTEXT
+    if (false) {
+#else
+    if (full) {
+#endif  // its dwords, ORed (neighbouring texts share edge dwords)
         const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
         const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
         uint32_t prev = 0;
@@ -975,6 +986,9 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     }
     const uint32_t base = wv_place(i, wave_sum(nb), lane);
     const uint32_t off = base + wave_excl_sum(nb, lane);
+#ifdef BG_PROBE_NOBITS
+    if (off == 0xFFFFFFFFu)
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < 4; k++) {
         if (!__ballot(bn > 32 * k)) break;
