@@ -1079,40 +1079,50 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
             g_tlitn[k] = (uint8_t)(nb <= 128 ? nb : kNoTokLit);
         }
     }
-    // the block's items in stream order: per row its head, its groups, its newline
+    // the block's items in stream order: per row its head, its groups, its newline;
+    // counted per row, offsets by a wave scan, then one wave per row writes them (its
+    // lanes the groups: a row holds up to kStCum of them)
     const Ctx<true> C{A, b0};
-    uint32_t my_items = 0;
-    if (tid < S.P.n_rows) {
-        const DevRow R = S.rows[tid];
-        const bool head = R.head_len && R.text_off < e && R.text_off + R.head_len > b0;
-        const uint64_t nl = R.text_off + R.head_len + R.geno_len;
-        uint32_t groups = 0;
+    auto row_items = [&](uint32_t r, bool &head, bool &nl, uint32_t &groups, uint32_t &k_st) {
+        const DevRow &R = S.rows[r];
+        head = R.head_len && R.text_off < e && R.text_off + R.head_len > b0;
+        const uint64_t q = R.text_off + R.head_len + R.geno_len;
+        nl = q >= b0 && q < e;
+        groups = 0;
+        k_st = 0;
         for (uint32_t k = 0; k < S.P.n_st; k++)
-            if (S.P.st[k].row == S.P.r_first + tid) groups = S.P.st[k].ncum - 1;
-        my_items = (head ? 1u : 0u) + groups + ((nl >= b0 && nl < e) ? 1u : 0u);
-        g_ioff[tid] = my_items;
+            if (S.P.st[k].row == S.P.r_first + r) {
+                groups = S.P.st[k].ncum - 1;
+                k_st = k;
+            }
+    };
+    if (tid < S.P.n_rows) {
+        bool head, nl;
+        uint32_t groups, k_st;
+        row_items(tid, head, nl, groups, k_st);
+        g_ioff[tid] = (head ? 1u : 0u) + groups + (nl ? 1u : 0u);
     }
     __syncthreads();
-    if (tid == 0) {
-        uint32_t at = 0;
-        for (uint32_t i = 0; i < S.P.n_rows; i++) {
-            const uint32_t c = g_ioff[i];
-            g_ioff[i] = at;
-            at += c;
+    if (wave == 0) {
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < S.P.n_rows; c0 += 64) {
+            const bool in = c0 + lane < S.P.n_rows;
+            const uint32_t x = in ? g_ioff[c0 + lane] : 0u, inc = wave_incl_sum(x);
+            if (in) g_ioff[c0 + lane] = carry + inc - x;
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
         }
-        g_ioff[kWvItems] = at;
+        if (lane == 0) g_ioff[kWvItems] = carry;
     }
     __syncthreads();
-    if (tid < S.P.n_rows) {
-        const DevRow R = S.rows[tid];
-        uint32_t at = g_ioff[tid];
-        if (R.head_len && R.text_off < e && R.text_off + R.head_len > b0) g_item[at++] = (IT_HEAD << 30) | (tid << 23);
-        for (uint32_t k = 0; k < S.P.n_st; k++)
-            if (S.P.st[k].row == S.P.r_first + tid)
-                for (uint32_t q = 0; q + 1 < S.P.st[k].ncum; q++)
-                    g_item[at++] = (IT_GROUP << 30) | (tid << 23) | (k << 20) | (S.P.st[k].g_lo + q);
-        const uint64_t nl = R.text_off + R.head_len + R.geno_len;
-        if (nl >= b0 && nl < e) g_item[at++] = (IT_NL << 30) | (tid << 23);
+    for (uint32_t r = wave; r < S.P.n_rows; r += kWv / 64) {
+        bool head, nl;
+        uint32_t groups, k_st;
+        row_items(r, head, nl, groups, k_st);
+        const uint32_t at = g_ioff[r] + (head ? 1u : 0u);
+        if (head && lane == 0) g_item[at - 1] = (IT_HEAD << 30) | (r << 23);
+        for (uint32_t q = lane; q < groups; q += 64)
+            g_item[at + q] = (IT_GROUP << 30) | (r << 23) | (k_st << 20) | (S.P.st[k_st].g_lo + q);
+        if (nl && lane == 0) g_item[at + groups] = (IT_NL << 30) | (r << 23);
     }
     __syncthreads();
     const uint32_t n_items = g_ioff[kWvItems];
