@@ -1029,22 +1029,19 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     stamp(15, nref);
     };
     // regions [first, first + count) in A.order's order (most haplotypes first): with
-    // A.persist a grid of a few workgroups per CU takes them from the counter
-    // A.next[which] -- the ticket for the next region is taken as this one starts, so
-    // its latency hides behind the region's first loads --, else one per workgroup
+    // A.persist a grid of a few workgroups per CU takes them -- its first region by
+    // workgroup index, the next ones from the counter A.next[which] (gridDim.x + ticket),
+    // the ticket for the next region taken as this one starts, so that its latency hides
+    // behind the region's first loads --, else one per workgroup.  A grid with one
+    // workgroup per region takes no ticket (1 000 tickets at once cost microseconds).
     __shared__ uint32_t s_tk;
+    const bool tickets = A.persist && gridDim.x < count;
     uint32_t i = blockIdx.x;
-    if (A.persist) {
-        if (tid == 0) s_tk = atomicAdd(A.next + which, 1u);
-        __syncthreads();
-        i = s_tk;
-        __syncthreads();
-    }
     while (i < count) {
         uint32_t tk = 0;
-        if (A.persist && tid == 0) tk = atomicAdd(A.next + which, 1u);
+        if (tickets && tid == 0) tk = gridDim.x + atomicAdd(A.next + which, 1u);
         process(A.order ? A.order[first + i] : first + i);
-        if (!A.persist) break;
+        if (!tickets) break;
         if (tid == 0) s_tk = tk;
         __syncthreads();
         i = s_tk;
