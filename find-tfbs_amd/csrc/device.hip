@@ -110,6 +110,7 @@ struct tfbs_ctx {
     uint32_t *over_host = nullptr;       // pinned [spill records, candidates past the lists]
     hipEvent_t over_ev = nullptr;
     bool over_pending = false;
+    bool over_copied = false;  // the last scan's overflow counters copied to over_host
     bool post_done = false;              // the last scan's overflow candidates were rescored (launch_post_scan)
     HitSrc srcs_host[kMaxHitSrcs] = {};
     HitSrc srcs_dev[kMaxHitSrcs] = {};   // what srcs holds (copied from here: stable while the copy runs)
@@ -159,6 +160,7 @@ struct tfbs_ctx {
     bool var_cap_forced = false;     // TFBS_VAR_CAP applied (tfbs_batch_reduce)
     Batch *var_owner = nullptr;      // the batch whose varying counts are only in var_counts (device)
     uint32_t *asm_host = nullptr;  // asm_ctr copied back (pinned)
+    bool asm_ctr_zeroed = false;   // launch_scan zeroed asm_ctr (for the scan's first assembly)
     hipEvent_t asm_ev = nullptr, asm_t0 = nullptr, asm_t1 = nullptr;
     const Batch *asm_batch = nullptr;    // the batch the enqueued assembly is for
     int asm_state = 0;                   // 0 none, 1 enqueued, 2 complete (checked)
@@ -289,6 +291,22 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
     return TFBS_OK;
 }
 
+// asm_ctr's counter words (layout at enqueue_assembly), the spill buckets after them
+constexpr size_t kAsmCtrWords = 24;
+
+// The scan's counters (reference hits per region, the overflow pair) and the
+// assembly's (asm_ctr) zeroed in one launch at the scan's start, instead of three
+// memsets on either side of it (C2 is launch-bound).
+__global__ void zero3_kernel(uint32_t *__restrict__ a, uint32_t na, uint32_t *__restrict__ b, uint32_t nb,
+                             uint32_t *__restrict__ c, uint32_t nc) {
+    const uint32_t s = gridDim.x * blockDim.x;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < na || k < nb || k < nc; k += s) {
+        if (k < na) a[k] = 0;
+        if (k < nb) b[k] = 0;
+        if (k < nc) c[k] = 0;
+    }
+}
+
 static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits, uint32_t hits_wpp) {
     const Plan &P = ctx->plan;
     if (n_haps == 0) return 0;
@@ -350,8 +368,14 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             m.wlist16[c] = ctx->wl16[c].p;
             m.wlist_off[c] = ctx->wl_off[c].p;
         }
-        HIP_TRY(hipMemsetAsync(ctx->ref_count.p, 0, (size_t)nr * 4, ctx->stream));
-        HIP_TRY(hipMemsetAsync(ctx->over.p, 0, 8, ctx->stream));
+        {
+            const uint32_t na = (uint32_t)(kAsmCtrWords + nr + 1);
+            if ((rc = ctx->asm_ctr.ensure(na))) return rc;
+            hipLaunchKernelGGL(zero3_kernel, dim3(std::min<uint32_t>(256, (std::max(na, nr) + 255) / 256)), dim3(256), 0,
+                               ctx->stream, ctx->ref_count.p, nr, ctx->over.p, 2u, ctx->asm_ctr.p, na);
+            HIP_TRY(hipGetLastError());
+            ctx->asm_ctr_zeroed = true;  // (for this scan's first assembly)
+        }
         HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         // one stream per depth launch (launch_mfma: one per K depth), side streams
         // forked and joined only when there is more than one (small batches: no
@@ -386,11 +410,10 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
                                    ctx->stream));
             ctx->srcs_on_dev = true;
         }
-        // the overflow counters, for the check before the results are read
-        if (!ctx->over_host) HIP_TRY(hipHostMalloc((void **)&ctx->over_host, 8, hipHostMallocDefault));
-        HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipEventRecord(ctx->over_ev, ctx->stream));
+        // the overflow counters are checked before the results are read: by the
+        // assembly's list pass, or by check_overflow (which copies them back first)
         ctx->over_pending = true;
+        ctx->over_copied = false;
     }
     if (!P.fast_tiles.empty()) {
         ScanArgs f = a;
@@ -428,6 +451,12 @@ static int check_overflow(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hi
     };
     for (int round = 0; ctx->over_pending; round++) {
         if (round == 8) return tfbs::fail(TFBS_E_NOMEM, "scan overflow lists still full after 8 rescans");
+        if (!ctx->over_copied) {  // (the scan's counters: nothing after it on the stream changes them)
+            if (!ctx->over_host) HIP_TRY(hipHostMalloc((void **)&ctx->over_host, 8, hipHostMallocDefault));
+            HIP_TRY(hipMemcpyAsync(ctx->over_host, ctx->over.p, 8, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipEventRecord(ctx->over_ev, ctx->stream));
+            ctx->over_copied = true;
+        }
         HIP_TRY(hipEventSynchronize(ctx->over_ev));
         uint32_t nspill = ctx->over_host[0];
         const uint32_t ncand = ctx->over_host[1];
@@ -832,7 +861,6 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
 // give-up reasons, 16 / 17 key_fast_kernel's region counters, 18 post_scan_kernel's
 // finished workgroups, [19, 24) spare; the spill buckets after.
-constexpr size_t kAsmCtrWords = 24;
 
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     int rc;
@@ -856,9 +884,13 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
     HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
     const bool mfma = !ctx->plan.m_supers.empty();
-    // the assembly's counters and the spill buckets' (at asm_ctr + kAsmCtrWords): one memset
-    HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0,
-                           (kAsmCtrWords + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4, ctx->stream));
+    // the assembly's counters and the spill buckets' (at asm_ctr + kAsmCtrWords): zeroed
+    // by the scan for its first assembly, else one memset
+    if (!(mfma && post && ctx->asm_ctr_zeroed && ctx->n_regions == nr))
+        HIP_TRY(hipMemsetAsync(ctx->asm_ctr.p, 0,
+                               (kAsmCtrWords + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4,
+                               ctx->stream));
+    ctx->asm_ctr_zeroed = false;
     if (mfma && post) {  // overflow candidates rescored (once per scan: they append spill records) + spill buckets
         if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18, std::max<uint32_t>(1, nr),
                                     ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p,
