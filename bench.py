@@ -388,19 +388,24 @@ def main():
             dist.barrier()
 
     barrier()
-    kernel_ms, mfma_ms, asm_ms = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # the scan's launches (HIP events)
-        mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
-        asm_ms.append(L.tfbs_ctx_last_assemble_ms(sc.h))  # the assembly's launches
     T.check(L.tfbs_ctx_sync(sc.h))
     if dist is not None:
         import torch
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
+    # the steps' device times (HIP events), read after further steps outside the timed
+    # loop: reading them syncs on each step's events, which is not part of a step
+    kernel_ms, mfma_ms, asm_ms = [], [], []
+    for _ in range(min(args.steps, 10)):
+        step()
+        kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # the scan's launches (HIP events)
+        mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
+        asm_ms.append(L.tfbs_ctx_last_assemble_ms(sc.h))  # the assembly's launches
+    T.check(L.tfbs_ctx_sync(sc.h))
 
     # the dense download, for reference (the run flow uses the key reduction)
     t_dense = time.perf_counter()
