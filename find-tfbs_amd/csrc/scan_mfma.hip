@@ -833,6 +833,8 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_dept
 // scan into boff, a scatter into sorted; bcnt n_regions + 1 zeroed before) on its
 // own: spills are rare, and no records (the usual case) costs one counter read.
 constexpr uint32_t kPostBlock = 256;
+constexpr uint32_t kPostSerial = 8192;  // spill records the last workgroup scatters itself
+
 __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint32_t cand, uint32_t *done,
                                                               uint32_t n_regions, uint32_t *__restrict__ bcnt,
                                                               uint32_t *__restrict__ boff,
@@ -840,14 +842,37 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     __shared__ uint32_t s_last, s_sum[kPostBlock];
     const uint32_t tid = threadIdx.x;
     if (cand) {
-        const uint32_t n = min(A.over[1], A.cand_over_cap);
-        for (uint32_t k = blockIdx.x * kPostBlock + tid; k < n; k += gridDim.x * kPostBlock) {
-            const uint32_t hap = A.cand_over[3 * (size_t)k], g = A.cand_over[3 * (size_t)k + 1];
-            const DevHap hp = A.haps[hap];
-            uint32_t key0 = 0;
-            for (uint32_t m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0); m;
-                 m &= m - 1)
-                spill_record(A, hp.region, hap, key0 + __builtin_ctz(m));
+        // the hits' spill records get their slots one atomic per wave (C5: ~120 000
+        // records through one counter, one atomic each, took ~1 ms); the loop is
+        // wave-uniform for the wave sum
+        const uint32_t n = min(A.over[1], A.cand_over_cap), lane = tid & 63;
+        for (uint32_t k0 = blockIdx.x * kPostBlock; k0 < n; k0 += gridDim.x * kPostBlock) {
+            const uint32_t k = k0 + tid;
+            uint32_t m = 0, key0 = 0, region = 0, hap = 0;
+            if (k < n) {
+                hap = A.cand_over[3 * (size_t)k];
+                const uint32_t g = A.cand_over[3 * (size_t)k + 1];
+                const DevHap hp = A.haps[hap];
+                region = hp.region;
+                m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0);
+            }
+            const uint32_t c = (uint32_t)__builtin_popcount(m);
+            uint32_t inc = c;
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+                if (lane >= o) inc += t;
+            }
+            const uint32_t total = (uint32_t)__shfl((int)inc, 63);
+            uint32_t base = 0;
+            if (lane == 0 && total) base = atomicAdd(A.over, total);
+            uint32_t at = (uint32_t)__shfl((int)base, 0) + inc - c;
+            for (; m; m &= m - 1, at++)
+                if (at < A.spill_cap) {
+                    A.spill[3 * (size_t)at] = region;
+                    A.spill[3 * (size_t)at + 1] = hap;
+                    A.spill[3 * (size_t)at + 2] = key0 + __builtin_ctz(m);
+                }
         }
     }
     __syncthreads();
@@ -863,11 +888,14 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
     __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 <= n_regions; b0 += kPostBlock) {  // boff[0 .. n_regions]: exclusive prefix
-        const uint32_t i = b0 + tid;
-        const uint32_t v = i < n_regions ? bcnt[i] : 0u;
-        s_sum[tid] = v;
+    {  // boff[0 .. n_regions]: exclusive prefix -- each thread a run of consecutive buckets,
+       // one block scan of the runs' sums (not one per 256 buckets: 10 000 regions took
+       // 40 scans of 16 barriers)
+        const uint32_t per = (n_regions + kPostBlock) / kPostBlock;  // ceil((n_regions + 1) / kPostBlock)
+        const uint32_t i0 = min(tid * per, n_regions + 1), i1 = min(i0 + per, n_regions + 1);
+        uint32_t mine = 0;
+        for (uint32_t i = i0; i < i1; i++) mine += i < n_regions ? bcnt[i] : 0u;
+        s_sum[tid] = mine;
         __syncthreads();
         for (uint32_t o = 1; o < kPostBlock; o <<= 1) {
             const uint32_t t = tid >= o ? s_sum[tid - o] : 0u;
@@ -875,14 +903,35 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
             s_sum[tid] += t;
             __syncthreads();
         }
-        if (i <= n_regions) boff[i] = carry + s_sum[tid] - v;
-        if (i < n_regions) bcnt[i] = 0;  // the scatter's fill counters
-        carry += s_sum[kPostBlock - 1];
-        __syncthreads();
+        uint32_t at = s_sum[tid] - mine;
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t v = i < n_regions ? bcnt[i] : 0u;
+            boff[i] = at;
+            at += v;
+            if (i < n_regions) bcnt[i] = 0;  // the scatter's fill counters
+        }
     }
     __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
+    if (n > kPostSerial) return;  // spill_scatter_wide_kernel's
     for (uint32_t e = tid; e < n; e += kPostBlock) {
+        const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
+        const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
+        sorted[3 * (size_t)at] = A.spill[3 * (size_t)e];
+        sorted[3 * (size_t)at + 1] = A.spill[3 * (size_t)e + 1];
+        sorted[3 * (size_t)at + 2] = A.spill[3 * (size_t)e + 2];
+    }
+}
+
+// The scatter of more than kPostSerial spill records, over the whole grid: each
+// record's slot is a returning atomic, whose latency one workgroup's 256 threads
+// cannot hide (C5's ~120 000 records took ~1 ms in post_scan_kernel's last workgroup).
+__global__ __launch_bounds__(256) void spill_scatter_wide_kernel(ScanArgs A, const uint32_t *__restrict__ boff,
+                                                                 uint32_t *__restrict__ bcnt,
+                                                                 uint32_t *__restrict__ sorted) {
+    const uint32_t n = min(A.over[0], A.spill_cap);
+    if (n <= kPostSerial) return;  // (post_scan_kernel scattered them)
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < n; e += gridDim.x * 256) {
         const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
         const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
         sorted[3 * (size_t)at] = A.spill[3 * (size_t)e];
@@ -893,8 +942,12 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
 
 int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
                       uint32_t *sorted, hipStream_t stream) {
+    // (256 workgroups: 1 024 cost C2 14 us in dispatch and finish tickets and did not
+    // speed up C5's rescoring; the wide scatter's 128 exit at once when there is nothing
+    // for them)
     hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? 256 : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
                        n_regions, bcnt, boff, sorted);
+    hipLaunchKernelGGL(spill_scatter_wide_kernel, dim3(128), dim3(256), 0, stream, a, boff, bcnt, sorted);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("post_scan_kernel launch: ") + hipGetErrorString(e));
     return TFBS_OK;
