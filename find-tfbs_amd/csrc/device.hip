@@ -859,8 +859,8 @@ int tfbs_batch_download(tfbs_ctx *ctx, tfbs_batch *b) {
 // shapes; TFBS_VAR_CAP=n starts at n keys and 4 n counts -- the regrow path's test).
 // asm_ctr: [0, 2) the scan's overflow counters (copied), 2 regions left to key_asm,
 // 3 arena words used, [4, 8) the varying keys' and counts' u64 totals, [8, 16) debug
-// give-up reasons, 16 / 17 key_fast_kernel's region counters, 18 post_scan_kernel's
-// finished workgroups, [19, 24) spare; the spill buckets after.
+// give-up reasons, 16 / 17 key_fast_kernel's region counters, 18 / 19 post_scan_kernel's and
+// spill_hist_wide_kernel's finished workgroups, [20, 24) spare; the spill buckets after.
 
 static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     int rc;

@@ -833,7 +833,34 @@ MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_dept
 // scan into boff, a scatter into sorted; bcnt n_regions + 1 zeroed before) on its
 // own: spills are rare, and no records (the usual case) costs one counter read.
 constexpr uint32_t kPostBlock = 256;
-constexpr uint32_t kPostSerial = 8192;  // spill records the last workgroup scatters itself
+constexpr uint32_t kPostSerial = 8192;  // spill records the last workgroup buckets itself
+
+// boff[0 .. n_regions]: the exclusive prefix of the bucket counts (one workgroup of
+// kPostBlock threads) -- each thread a run of consecutive buckets, one block scan of
+// the runs' sums (not one per 256 buckets: 10 000 regions took 40 scans of 16
+// barriers); the counts are zeroed for the scatter's fill counters
+__device__ void spill_bucket_offsets(uint32_t tid, uint32_t n_regions, uint32_t *__restrict__ bcnt,
+                                     uint32_t *__restrict__ boff, uint32_t *s_sum) {
+    const uint32_t per = (n_regions + kPostBlock) / kPostBlock;  // ceil((n_regions + 1) / kPostBlock)
+    const uint32_t i0 = min(tid * per, n_regions + 1), i1 = min(i0 + per, n_regions + 1);
+    uint32_t mine = 0;
+    for (uint32_t i = i0; i < i1; i++) mine += i < n_regions ? bcnt[i] : 0u;
+    s_sum[tid] = mine;
+    __syncthreads();
+    for (uint32_t o = 1; o < kPostBlock; o <<= 1) {
+        const uint32_t t = tid >= o ? s_sum[tid - o] : 0u;
+        __syncthreads();
+        s_sum[tid] += t;
+        __syncthreads();
+    }
+    uint32_t at = s_sum[tid] - mine;
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint32_t v = i < n_regions ? bcnt[i] : 0u;
+        boff[i] = at;
+        at += v;
+        if (i < n_regions) bcnt[i] = 0;
+    }
+}
 
 __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint32_t cand, uint32_t *done,
                                                               uint32_t n_regions, uint32_t *__restrict__ bcnt,
@@ -885,35 +912,13 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     __threadfence();  // (acquire: every workgroup's records)
     const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
     if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
+    if (n > kPostSerial) return;  // spill_hist_wide_kernel + spill_scatter_wide_kernel's
     for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
     __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
-    {  // boff[0 .. n_regions]: exclusive prefix -- each thread a run of consecutive buckets,
-       // one block scan of the runs' sums (not one per 256 buckets: 10 000 regions took
-       // 40 scans of 16 barriers)
-        const uint32_t per = (n_regions + kPostBlock) / kPostBlock;  // ceil((n_regions + 1) / kPostBlock)
-        const uint32_t i0 = min(tid * per, n_regions + 1), i1 = min(i0 + per, n_regions + 1);
-        uint32_t mine = 0;
-        for (uint32_t i = i0; i < i1; i++) mine += i < n_regions ? bcnt[i] : 0u;
-        s_sum[tid] = mine;
-        __syncthreads();
-        for (uint32_t o = 1; o < kPostBlock; o <<= 1) {
-            const uint32_t t = tid >= o ? s_sum[tid - o] : 0u;
-            __syncthreads();
-            s_sum[tid] += t;
-            __syncthreads();
-        }
-        uint32_t at = s_sum[tid] - mine;
-        for (uint32_t i = i0; i < i1; i++) {
-            const uint32_t v = i < n_regions ? bcnt[i] : 0u;
-            boff[i] = at;
-            at += v;
-            if (i < n_regions) bcnt[i] = 0;  // the scatter's fill counters
-        }
-    }
+    spill_bucket_offsets(tid, n_regions, bcnt, boff, s_sum);
     __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
-    if (n > kPostSerial) return;  // spill_scatter_wide_kernel's
     for (uint32_t e = tid; e < n; e += kPostBlock) {
         const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
         const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
@@ -923,9 +928,29 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     }
 }
 
-// The scatter of more than kPostSerial spill records, over the whole grid: each
-// record's slot is a returning atomic, whose latency one workgroup's 256 threads
-// cannot hide (C5's ~120 000 records took ~1 ms in post_scan_kernel's last workgroup).
+// More than kPostSerial spill records: their bucket counts over the whole grid, then
+// the last workgroup (finish ticket) the offsets; the scatter below, also over the
+// grid (C5's ~120 000 records took ~1 ms in post_scan_kernel's last workgroup).
+__global__ __launch_bounds__(kPostBlock) void spill_hist_wide_kernel(ScanArgs A, uint32_t *done, uint32_t n_regions,
+                                                                     uint32_t *__restrict__ bcnt,
+                                                                     uint32_t *__restrict__ boff) {
+    __shared__ uint32_t s_last, s_sum[kPostBlock];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t n = min(A.over[0], A.spill_cap);
+    if (n <= kPostSerial) return;  // (uniform: post_scan_kernel bucketed them)
+    for (uint32_t e = blockIdx.x * kPostBlock + tid; e < n; e += gridDim.x * kPostBlock)
+        atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
+    __syncthreads();
+    if (tid == 0) {
+        __threadfence();  // (release: this workgroup's counts)
+        s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();  // (acquire: every workgroup's counts)
+    spill_bucket_offsets(tid, n_regions, bcnt, boff, s_sum);
+}
+
 __global__ __launch_bounds__(256) void spill_scatter_wide_kernel(ScanArgs A, const uint32_t *__restrict__ boff,
                                                                  uint32_t *__restrict__ bcnt,
                                                                  uint32_t *__restrict__ sorted) {
@@ -947,6 +972,8 @@ int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_r
     // for them)
     hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? 256 : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
                        n_regions, bcnt, boff, sorted);
+    hipLaunchKernelGGL(spill_hist_wide_kernel, dim3(128), dim3(kPostBlock), 0, stream, a, done + 1, n_regions, bcnt,
+                       boff);
     hipLaunchKernelGGL(spill_scatter_wide_kernel, dim3(128), dim3(256), 0, stream, a, boff, bcnt, sorted);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("post_scan_kernel launch: ") + hipGetErrorString(e));
