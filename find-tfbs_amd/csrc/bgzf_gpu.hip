@@ -1034,9 +1034,10 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
         for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
         for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
+        __syncthreads();  // (S.rows: the staged rows' descriptors from LDS below, not a second global read)
         for (uint32_t k = 0; k < S.P.n_st; k++) {
             const StRow T = S.P.st[k];
-            const DevRow R = A.rows[T.row];
+            const DevRow R = S.rows[T.row - S.P.r_first];
             const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
             for (uint32_t i = tid; i < nb; i += kWv) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
             for (uint32_t i = tid; i < R.nv; i += kWv) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
