@@ -10,8 +10,10 @@ Regions are 201 bp merged BED rows of a synthetic chromosome with Poisson(20)
 variant sites and carrier counts ~ 1/k; PWMs are synthetic HOCOMOCO-format
 matrices with exact 1e-4 thresholds, both strands.  The host reduces every
 region to its distinct haplotypes and packs them into HBM (untimed, as the
-reference builds them before scanning); one timed step = one tfbs_scan over
-every distinct haplotype x pattern window of the rank's batch.
+reference builds them before scanning); one timed step = tfbs_scan (every
+distinct haplotype x pattern window of the rank's batch) + tfbs_batch_assemble +
+tfbs_batch_assemble_wait (every region's keyed counts: reference-window reuse
+resolved, classified, varying counts compacted; the host checks every list).
 
 Multi-GPU (one rank per GPU; `--gpus N` without WORLD_SIZE starts torchrun with
 N ranks itself, before anything touches a GPU): weak scaling, no collective on
@@ -28,12 +30,14 @@ the data path; a barrier + max-over-ranks bracket the timed region.
                           of the P shards of a block are the unsharded run's
                           (the host merges disjoint pattern_id keys)
 
-Besides the scan-only `value` the line carries an end-to-end leg over the same
-batch (host prep + upload + scan + device key reduction + row formatting), the
-roofline of the dominant kernel (HIP events around its launches on the ctx
-stream; traffic from the rocprofv3 PMC passes of the same bench command,
-tools/profile_round.sh) and the CPU baseline (the oracle, scan-only and
-end-to-end, 1 thread and the box's share of threads).
+Besides `value` the line carries an end-to-end leg over the same batch (host
+prep + upload + scan + device key reduction + device per-sample encoding + the
+VCF rows as BGZF blocks made on the GPU), the roofline of the dominant kernel
+(HIP events around its launches on the ctx stream; traffic, the rocprofv3 MFMA
+phase and the SQ instruction mix from the PMC passes and kernel trace of the
+same bench command, tools/profile_round.sh, used only when they profiled this
+same library build) and the CPU baseline (the oracle, scan-only and end-to-end,
+1 thread and the box's share of threads).
 """
 import argparse
 import ctypes
@@ -105,9 +109,23 @@ def workload_key(args):
             "threshold": args.threshold}
 
 
-def pmc_traffic(args, path):
-    """HBM bytes per step of the dominant kernel's launches from the PMC passes of this
-    same bench configuration (tools/pmc_traffic.py), or (None, reason)."""
+def library_sha256():
+    """SHA-256 of the product library this process loads (find-tfbs_amd/_capi.LIB_PATH)."""
+    import hashlib
+    import tfbs_pkg
+
+    path = tfbs_pkg.load()._capi.LIB_PATH
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def pmc_profile(args, path):
+    """The PMC passes and kernel trace of this same bench configuration AND library build
+    (profiles/pmc_traffic_<workload>.json, tools/pmc_traffic.py: stamped with the profiled
+    library's SHA-256), or (None, reason): a profile of another build is refused."""
     f = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % args.workload)
     if not os.path.exists(f):
         return None, "no %s" % os.path.relpath(f, ROOT)
@@ -117,7 +135,10 @@ def pmc_traffic(args, path):
         return None, "unreadable %s" % os.path.relpath(f, ROOT)
     if pm.get("config") != workload_key(args) or pm.get("scan_path") != path:
         return None, "%s is for another configuration" % os.path.relpath(f, ROOT)
-    return pm["hbm_bytes_per_step"], "%s (%s)" % (os.path.relpath(f, ROOT), pm.get("source", ""))
+    if pm.get("library_sha256") != library_sha256():
+        return None, "%s profiled another library build (sha256 %s)" % (os.path.relpath(f, ROOT),
+                                                                       str(pm.get("library_sha256"))[:12])
+    return pm, "%s (%s)" % (os.path.relpath(f, ROOT), pm.get("source", ""))
 
 
 def cpu_baseline(T, ps, args, budget_s):
@@ -433,7 +454,8 @@ def main():
         mms = sum(mfma_ms) / len(mfma_ms)
         ams = sum(asm_ms) / len(asm_ms)
         path = "mfma" if mms > 0 else "lut"
-        traffic, traffic_src = pmc_traffic(args, path)
+        prof, traffic_src = pmc_profile(args, path)
+        traffic = prof["hbm_bytes_per_step"] if prof else None
         pattern_bytes = 0
         for p in ps.to_list():
             pattern_bytes += ((len(p) + 15) // 16) * 1536 + 16 * len(p) + 24
@@ -446,10 +468,17 @@ def main():
         cell_tops = scan_cells / (kms / 1e3) / 1e12
         if mms > 0:  # the matrix-core kernel scored every strand of this workload
             mops = MFMA_OPS_PER_CELL * scan_cells / (mms / 1e3) / 1e12
+            rp = prof.get("rocprof_phase_ms") if prof else None
             roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TFLOP/s",
                     "frac": mops / MFMA_F6_PEAK_TOPS, "traffic": traffic,
                     "kernel": "scan_mfma_kernel<staged, K depth> (one launch per K depth, 4 streams)",
                     "kernel_ms": mms,
+                    # the same figure on the rocprofv3 kernel trace's MFMA phase (same library build)
+                    "rocprof_phase_ms": rp,
+                    "frac_rocprof": (MFMA_OPS_PER_CELL * scan_cells / (rp / 1e3) / 1e12 / MFMA_F6_PEAK_TOPS
+                                     if rp else None),
+                    "traffic_per_algorithmic_byte": traffic / alg_bytes if traffic else None,
+                    "sq": prof.get("sq") if prof else None,
                     "note": "achieved = 8 ops per (window, strand, column) cell of the FP4 one-hot x FP6 "
                             "bound-digit GEMM x %.4g cells the scan reads (of %.4g: reference-window reuse) / "
                             "the MFMA phase's HIP-event time (first launch to last, joined on the ctx stream; "

@@ -471,6 +471,21 @@ class RegionBatch:
         check(lib().tfbs_batch_region_key_digest_sum(self.h, region, C.byref(d)))
         return d.value
 
+    def region_digests(self, r0=0, r1=None, min_maf=0, threads=16, keys=True, rows=True):
+        """tfbs_batch_region_digests over regions [r0, r1): numpy uint64 arrays (keys, rows,
+        n_rows) -- the canonical sketch of each region's count_matches_by_sample vectors and
+        XXH64 of its rows without POS, comparable with the oracle's orc_job_digests (None for
+        a digest not asked for)."""
+        import numpy as np
+        r1 = self.num_regions if r1 is None else r1
+        n = max(1, r1 - r0)
+        k, r, c = (np.zeros(n, dtype=np.uint64) for _ in range(3))
+        p = C.POINTER(C.c_uint64)
+        ptr = lambda a, on: a.ctypes.data_as(p) if on else None
+        check(lib().tfbs_batch_region_digests(self.h, r0, r1, min_maf, threads, ptr(k, keys), ptr(r, rows),
+                                              ptr(c, rows)))
+        return (k[:r1 - r0] if keys else None), (r[:r1 - r0] if rows else None), (c[:r1 - r0] if rows else None)
+
     def input_digest(self, region):
         """tfbs_batch_region_input_digest: what the host prep packed for the region."""
         d = C.c_uint64()

@@ -123,6 +123,7 @@ SIGNATURES = [
     ("tfbs_batch_region_digest", C.c_int, [vp, C.c_size_t, u64p]),
     ("tfbs_batch_region_key_digest_sum", C.c_int, [vp, C.c_size_t, u64p]),
     ("tfbs_batch_region_input_digest", C.c_int, [vp, C.c_size_t, u64p]),
+    ("tfbs_batch_region_digests", C.c_int, [vp, C.c_size_t, C.c_size_t, C.c_uint32, C.c_uint32, u64p, u64p, u64p]),
     ("tfbs_batch_region_stats", C.c_int, [vp, C.c_size_t, u32p, u32p]),
     ("tfbs_batch_format_rows", C.c_int, [vp, C.c_char_p, C.c_uint32, C.c_uint32, C.c_size_t, C.c_size_t, u64p,
                                          u64p]),

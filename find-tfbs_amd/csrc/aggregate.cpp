@@ -747,6 +747,135 @@ int tfbs_batch_region_input_digest(const tfbs_batch *b, size_t region, uint64_t 
     return TFBS_OK;
 }
 
+namespace {
+// XXH64 (the published xxHash 64-bit algorithm), streaming: the row digest of
+// tfbs_batch_region_digests.
+struct Xxh64 {
+    static constexpr uint64_t P1 = 0x9E3779B185EBCA87ull, P2 = 0xC2B2AE3D27D4EB4Full, P3 = 0x165667B19E3779F9ull,
+                              P4 = 0x85EBCA77C2B2AE63ull, P5 = 0x27D4EB2F165667C5ull;
+    uint64_t v[4] = {P1 + P2, P2, 0, 0 - P1}, total = 0;
+    uint8_t buf[32];
+    size_t nbuf = 0;
+    static uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+    static uint64_t rd64(const uint8_t *p) {
+        uint64_t x;
+        memcpy(&x, p, 8);
+        return x;
+    }
+    static uint64_t round(uint64_t acc, uint64_t in) { return rotl(acc + in * P2, 31) * P1; }
+    void stripe(const uint8_t *p) {
+        for (int k = 0; k < 4; k++) v[k] = round(v[k], rd64(p + 8 * k));
+    }
+    void update(const void *data, size_t n) {
+        const uint8_t *p = static_cast<const uint8_t *>(data);
+        total += n;
+        if (nbuf) {
+            const size_t take = std::min(32 - nbuf, n);
+            memcpy(buf + nbuf, p, take);
+            nbuf += take;
+            p += take;
+            n -= take;
+            if (nbuf < 32) return;
+            stripe(buf);
+            nbuf = 0;
+        }
+        for (; n >= 32; p += 32, n -= 32) stripe(p);
+        memcpy(buf, p, n);
+        nbuf = n;
+    }
+    uint64_t digest() const {
+        uint64_t h = total >= 32 ? rotl(v[0], 1) + rotl(v[1], 7) + rotl(v[2], 12) + rotl(v[3], 18) : P5;
+        if (total >= 32)
+            for (int k = 0; k < 4; k++) h = (h ^ round(0, v[k])) * P1 + P4;
+        h += total;
+        const uint8_t *p = buf;
+        size_t n = nbuf;
+        for (; n >= 8; p += 8, n -= 8) h = rotl(h ^ round(0, rd64(p)), 27) * P1 + P4;
+        if (n >= 4) {
+            uint32_t x;
+            memcpy(&x, p, 4);
+            h = rotl(h ^ (uint64_t)x * P1, 23) * P2 + P3;
+            p += 4;
+            n -= 4;
+        }
+        for (; n > 0; p++, n--) h = rotl(h ^ (uint64_t)*p * P5, 11) * P1;
+        h ^= h >> 33;
+        h *= P2;
+        h ^= h >> 29;
+        h *= P3;
+        return h ^ (h >> 32);
+    }
+};
+
+uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+}  // namespace
+
+int tfbs_batch_region_digests(const tfbs_batch *b, size_t r0, size_t r1, uint32_t min_maf, uint32_t threads,
+                              uint64_t *keys, uint64_t *rows, uint64_t *n_rows) {
+    if (!b || (!keys && !rows)) return tfbs::fail(TFBS_E_ARG, "null argument");
+    const Batch &B = b->b;
+    if (r1 > B.rh.size() || r0 > r1) return tfbs::fail(TFBS_E_ARG, "bad region range");
+    if (!tfbs::have_counts(B)) return tfbs::fail(TFBS_E_STATE, "counts not downloaded");
+    if (int rc = tfbs::host_counts(B)) return rc;  // the varying counts on the host
+    if (!B.keep_membership && B.n_samples) return tfbs::fail(TFBS_E_STATE, "batch created without membership");
+    const uint32_t H = 2 * B.n_samples;
+    std::vector<uint64_t> w(H);
+    for (uint32_t h = 0; h < H; h++) w[h] = splitmix64(h);
+    std::atomic<size_t> next(r0);
+    auto work = [&]() {
+        std::string rr;
+        std::vector<uint64_t> W;
+        for (size_t j; (j = next.fetch_add(1)) < r1;) {
+            const tfbs::RegionH &R = B.rh[j];
+            uint64_t sum = 0;
+            Xxh64 x;
+            uint64_t nr = 0;
+            if (R.hap_count && keys) {
+                const auto ks = tfbs::region_keys(B, R);
+                if (!ks.empty()) {  // W[l]: the sketch weights of distinct haplotype l's carriers
+                    tfbs::Membership M(B, R, H);
+                    W.assign(R.hap_count, 0);
+                    for (uint32_t h = 0; h < H; h++) W[M.local[h]] += w[h];
+                }
+                for (const auto &k : ks) {
+                    uint64_t S = 0;
+                    for (uint32_t l = 0; l < R.hap_count; l++)
+                        S += (uint64_t)tfbs::count_of(B, R, l, k.slot, k.ik->slot) * k.ik->mult * W[l];
+                    uint64_t h = 0x2545F4914F6CDD1Dull;
+                    h = mix64(h, k.ik->bed);
+                    h = mix64(h, k.ik->s);
+                    h = mix64(h, k.ik->e);
+                    h = mix64(h, B.slot_pid[k.slot]);
+                    h = mix64(h, S);
+                    sum += h;
+                }
+            }
+            if (R.hap_count && rows) {
+                auto take = [&](std::string &head, const char *tail, size_t n) {
+                    x.update(head.data(), head.size());
+                    x.update(tail, n);
+                    x.update("\n", 1);
+                    head.clear();
+                };
+                nr = tfbs::region_rows_each<true>(B, R, min_maf, rr, take);
+            }
+            if (keys) keys[j - r0] = sum;
+            if (rows) rows[j - r0] = x.digest();
+            if (n_rows) n_rows[j - r0] = nr;
+        }
+    };
+    std::vector<std::thread> ts;
+    for (uint32_t t = 1; t < threads && t < r1 - r0; t++) ts.emplace_back(work);
+    work();
+    for (auto &t : ts) t.join();
+    return TFBS_OK;
+}
+
 int tfbs_batch_rows(const tfbs_batch *b, const char *chromosome, uint32_t min_maf, uint32_t *fake, char **text,
                     size_t *len) {
     if (!b || !chromosome || !fake || !text || !len) return tfbs::fail(TFBS_E_ARG, "null argument");

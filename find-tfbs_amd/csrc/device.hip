@@ -188,6 +188,7 @@ struct tfbs_ctx {
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
     uint32_t bg_crc_full = 0;         // bgzf_crc_tables' full-block CRC init term
     DevBuf<uint64_t> kf_prof;         // TFBS_KF_PROF: key_fast_kernel phase clocks and sizes per region
+    DevBuf<unsigned long long> scan_prof;  // TFBS_SCAN_PROF=<file>: scan_mfma_kernel's per-wave stamps (prof builds)
     DevBuf<uint32_t> asm_order;       // the resident batch's regions by distinct haplotypes, most first
     uint32_t asm_order_n = 0;         // regions asm_order holds (0: none)
     uint32_t asm_order_big = 0;       // the first of them with more than key_fast_big_u() haplotypes
@@ -363,6 +364,12 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.spill_cap = ctx->spill_cap;
         m.cand_over = ctx->cand_over.p;
         m.cand_over_cap = ctx->cand_over_cap;
+        static const char *prof_path = getenv("TFBS_SCAN_PROF");
+        if (prof_path && *prof_path) {
+            if ((rc = ctx->scan_prof.ensure(n_wg * kMBlockWaves * kScanProfWords))) return rc;
+            HIP_TRY(hipMemsetAsync(ctx->scan_prof.p, 0, ctx->scan_prof.n * 8, ctx->stream));
+            m.prof = ctx->scan_prof.p;
+        }
         for (int c = 0; c < 2; c++) {
             m.wlist[c] = ctx->wl[c].p;
             m.wlist16[c] = ctx->wl16[c].p;
@@ -400,6 +407,22 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
+        if (m.prof) {  // (profiling runs only) the stamps, appended to the file: launches, then the waves
+            std::vector<unsigned long long> h(ctx->scan_prof.n);
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            HIP_TRY(hipMemcpy(h.data(), ctx->scan_prof.p, h.size() * 8, hipMemcpyDeviceToHost));
+            if (FILE *f = fopen(prof_path, "ab")) {
+                unsigned long long hdr[2] = {ctx->n_srcs, h.size()};
+                fwrite(hdr, 8, 2, f);
+                for (uint32_t i = 0; i < ctx->n_srcs; i++) {
+                    const HitSrc &q = ctx->srcs_host[i];
+                    unsigned long long v[5] = {q.wg_base, q.ns, q.g0, q.ng, i};  // launches: deepest class first
+                    fwrite(v, 8, 5, f);
+                }
+                fwrite(h.data(), 8, h.size(), f);
+                fclose(f);
+            }
+        }
         ctx->last_margs = m;  // the overflow candidates are rescored when the results are read (check_overflow)
         ctx->post_done = false;
         if ((rc = ctx->srcs.ensure(kMaxHitSrcs))) return rc;

@@ -19,6 +19,8 @@
 // download).
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -900,11 +902,14 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     // 32 chunks (hundreds of haplotypes and keys: each chunk re-reads every
     // correction and costs a few barriers) -- chunks of kFRows rows in a share of
     // the arena (global atomics)
-    // u16 counters in LDS (two per word) when no count can reach 2^16: a key's count
-    // on a haplotype is at most its 2 strands' windows (< 2 x length); the -1
-    // corrections never take a count below 0 (a haplotype's dirty reference hits on
-    // a key are some of its base R), so a packed pair never borrows or carries
-    const bool half = 2 * (s_lmax + 64) < 65536 && A.cor_lds != 0;
+    // u16 counters in LDS (two per word) when no count can reach 2^16, also while the
+    // corrections land: a key's count on a haplotype is at most its 2 strands'
+    // windows (< 2 x length), but the unordered atomics can add every +1 (own hits,
+    // < 2 x length) to the base R (< 2 x length) before any -1, so the bound is
+    // 4 x length; the -1 corrections never take a count below 0 (a haplotype's
+    // dirty reference hits on a key are some of its base R), so a packed pair
+    // never borrows or carries
+    const bool half = 4 * (s_lmax + 64) < 65536 && A.cor_lds != 0;
     uint32_t rows_per = min((half ? 2 : 1) * kFCnt / U, kFRows);
     uint32_t *cnt = s_cnt;
     uint16_t *const cnt16 = reinterpret_cast<uint16_t *>(s_cnt);
@@ -1453,14 +1458,20 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
     if (!a.order || !side) n_big = 0;
     n_big = std::min(n_big, n_regions);
     // persistent grids (a.persist): the workgroups of each shape that fit the device at
-    // once (a function-local static: initialised once, thread-safe, for every ctx)
+    // once, queried once per device (the calling thread's current device: the ctx's),
+    // thread-safe for contexts on several threads
     struct Fit {
         int n_cu = 256, per_small = 2, per_big = 1;
     };
-    static const Fit fit = [] {
-        Fit f;
-        int dev = 0, v = 0;
-        (void)hipGetDevice(&dev);
+    constexpr int kMaxDev = 64;
+    static std::once_flag once[kMaxDev];
+    static Fit fits[kMaxDev];
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    dev = std::min(std::max(dev, 0), kMaxDev - 1);
+    std::call_once(once[dev], [dev] {
+        Fit &f = fits[dev];
+        int v = 0;
         if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) f.n_cu = v;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, key_fast_kernel<KfSmall>, KfSmall::kBlock, 0) ==
                 hipSuccess && v > 0)
@@ -1470,11 +1481,11 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
             f.per_big = v;
         (void)hipGetLastError();
         if (getenv("TFBS_KF_PROF"))
-            fprintf(stderr, "[kf prof] CUs %d, workgroups per CU: %d (%d threads, %zu B LDS), %d (%d threads, %zu B LDS)\n",
-                    f.n_cu, f.per_small, KfSmall::kBlock, key_fast_lds_bytes(false), f.per_big, KfBig::kBlock,
+            fprintf(stderr, "[kf prof] device %d: CUs %d, workgroups per CU: %d (%d threads, %zu B LDS), %d (%d threads, %zu B LDS)\n",
+                    dev, f.n_cu, f.per_small, KfSmall::kBlock, key_fast_lds_bytes(false), f.per_big, KfBig::kBlock,
                     key_fast_lds_bytes(true));
-        return f;
-    }();
+    });
+    const Fit &fit = fits[dev];
     const int n_cu = fit.n_cu, per_small = fit.per_small, per_big = fit.per_big;
     auto grid = [&](uint32_t n, int per) { return a.persist ? std::min<uint32_t>(n, (uint32_t)(n_cu * per)) : n; };
     hipError_t e = hipSuccess;

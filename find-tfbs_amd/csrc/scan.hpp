@@ -88,7 +88,12 @@ struct ScanArgs {
     // rescored by a kernel after the scan (launch_post_scan)
     uint32_t *cand_over;
     uint32_t cand_over_cap;
+    // TFBS_SCAN_PROF builds of scan_mfma.hip (tools/variant_build.sh): per wave of
+    // workgroup region_base + blockIdx.x, kScanProfWords clock stamps and counts
+    // (tools/scan_prof.py); null otherwise
+    unsigned long long *prof;
 };
+constexpr uint32_t kScanProfWords = 8;
 constexpr uint32_t kRefPerRegion = 64;
 constexpr uint32_t kMBlockWaves = 8;  // waves per matrix-core workgroup (hit list parts per workgroup)
 constexpr uint32_t kCandWords = 2;  // candidate list entry: strand | haplotype in the group << 24, window

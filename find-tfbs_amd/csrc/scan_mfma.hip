@@ -600,6 +600,17 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 // handed to the waves two at a time from an LDS counter -- the waves finish
 // together however the windows fall -- and the next pair's list entries are
 // loaded while the current pair is scored.
+#ifdef TFBS_SCAN_PROF
+// per wave: [0] s_memtime at the kernel's start, [1] after the staging barrier, [2]
+// after the scan loop, [3] after the last drain, [4] after the rescoring, [5] / [6]
+// s_memrealtime (100 MHz, one clock for the chip) at the start and the end, [7] pairs
+// scored | candidates << 32
+#define SCAN_STAMP(k, v) \
+    do { if (A.prof && lane == 0) A.prof[((size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave) * kScanProfWords + (k)] = (v); } while (0)
+#else
+#define SCAN_STAMP(k, v) do { } while (0)
+#endif
+
 template <int NK>
 __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                            const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
@@ -632,7 +643,13 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     };
     uint32_t p = next_pair(), ea = 0, eb = 0;
     if (p < npair) entries(p, ea, eb);
+#ifdef TFBS_SCAN_PROF
+    uint32_t n_pairs = 0;
+#endif
     while (p < npair) {
+#ifdef TFBS_SCAN_PROF
+        n_pairs++;
+#endif
         const uint32_t pn = next_pair();
         const bool two = 2 * p + 1 < ntile;
         v4i a0[NK], a1[NK];
@@ -642,8 +659,15 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
         p = pn;
     }
+    SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
     drain_queue(A, G, qn, wave, lane, cn);  // the wave's last entries
+    SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
     rescore_list(A, words, h0, wave, lane, cn);
+    SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
+    SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
+#ifdef TFBS_SCAN_PROF
+    SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
+#endif
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD (two workgroups per CU).
@@ -651,6 +675,9 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
 // workgroup's haplotypes, copied once so that every window read is an LDS read.
 template <bool STAGED, int NK>
 __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(ScanArgs A) {
+#ifdef TFBS_SCAN_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime(), r_start = __builtin_amdgcn_s_memrealtime();
+#endif
     int32_t *smem = s_mdyn;
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
@@ -685,6 +712,11 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     __syncthreads();
     // the wave index is uniform: keep every group-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef TFBS_SCAN_PROF
+    SCAN_STAMP(0, t_start);
+    SCAN_STAMP(5, r_start);
+    SCAN_STAMP(1, __builtin_amdgcn_s_memtime());
+#endif
     scan_super<NK>(A, S, s_img, words, hg, lane, wave);
 }
 

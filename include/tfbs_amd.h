@@ -337,6 +337,18 @@ int tfbs_batch_region_key_digest_sum(const tfbs_batch *b, size_t region, uint64_
  * haplotypes' bases / N masks / positions, carriers, membership): equal for the
  * same region built in any batch or shard. */
 int tfbs_batch_region_input_digest(const tfbs_batch *b, size_t region, uint64_t *digest);
+/* Canonical per-region digests of regions [r0, r1) (the full-size golden files of
+ * tests/golden/, made by the oracle's orc_job_digests; no reference counterpart):
+ * keys[i] = the sum over the region's keys of a hash of (bed index, start, end,
+ * pattern_id, S) with S = sum over samples s of L[s] w(2s) + R[s] w(2s + 1) mod 2^64
+ * (w = splitmix64; count_matches_by_sample's vectors, main.rs:500-534, as a linear
+ * sketch computed from the distinct haplotypes' counts and the membership);
+ * rows[i] = XXH64 (seed 0) of the region's rows with their "<chr>\t<POS>\t"
+ * prefix removed (main.rs:415-429), n_rows[i] their number.  Regions run on
+ * `threads` host threads; keys or rows (with n_rows) may be null to skip that digest.
+ * Needs the counts (download or reduce) and the membership. */
+int tfbs_batch_region_digests(const tfbs_batch *b, size_t r0, size_t r1, uint32_t min_maf, uint32_t threads,
+                              uint64_t *keys, uint64_t *rows, uint64_t *n_rows);
 /* Distinct haplotypes (number_of_haplotypes, main.rs:97-130) and records (variant_count) of a region. */
 int tfbs_batch_region_stats(const tfbs_batch *b, size_t region, uint32_t *n_haplotypes, uint32_t *n_variants);
 /* Formats the rows of regions [r0, r1) (main.rs:415-429) on `threads` host threads and

@@ -1151,3 +1151,121 @@ int orc_job_key(const orc_job *j, int i, int *bed, uint64_t *s, uint64_t *e, int
 void orc_job_stats(const orc_job *j, int *nhap, int *nvar, uint64_t *nmatch) {
     *nhap = j->last_haplotypes; *nvar = j->last_variants; *nmatch = j->last_matches;
 }
+
+/* ------------------------------------------------------------------------- */
+/* Region digests for the full-size golden files (tests/golden/               */
+/* make_fullsize_digests.py): not part of the reference, a canonical summary  */
+/* of one region's count_matches_by_sample map and rows that the product      */
+/* computes from its own representation (tfbs_batch_region_digests).          */
+/* ------------------------------------------------------------------------- */
+/* XXH64 (the published xxHash 64-bit algorithm), streaming. */
+#define XP1 0x9E3779B185EBCA87ull
+#define XP2 0xC2B2AE3D27D4EB4Full
+#define XP3 0x165667B19E3779F9ull
+#define XP4 0x85EBCA77C2B2AE63ull
+#define XP5 0x27D4EB2F165667C5ull
+typedef struct { uint64_t v[4], total; uint8_t buf[32]; int nbuf; uint64_t seed; } xxh64_state;
+static uint64_t xrotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static uint64_t xrd64(const uint8_t *p) { uint64_t x; memcpy(&x, p, 8); return x; }
+static uint32_t xrd32(const uint8_t *p) { uint32_t x; memcpy(&x, p, 4); return x; }
+static uint64_t xround(uint64_t acc, uint64_t in) { acc += in * XP2; acc = xrotl(acc, 31); return acc * XP1; }
+static uint64_t xmerge(uint64_t h, uint64_t v) { h ^= xround(0, v); return h * XP1 + XP4; }
+static void xxh64_init(xxh64_state *s, uint64_t seed) {
+    s->v[0] = seed + XP1 + XP2; s->v[1] = seed + XP2; s->v[2] = seed; s->v[3] = seed - XP1;
+    s->total = 0; s->nbuf = 0; s->seed = seed;
+}
+static void xxh64_update(xxh64_state *s, const void *data, size_t n) {
+    const uint8_t *p = (const uint8_t *)data;
+    s->total += n;
+    if (s->nbuf) {
+        size_t take = 32 - (size_t)s->nbuf < n ? 32 - (size_t)s->nbuf : n;
+        memcpy(s->buf + s->nbuf, p, take);
+        s->nbuf += (int)take; p += take; n -= take;
+        if (s->nbuf < 32) return;
+        for (int k = 0; k < 4; k++) s->v[k] = xround(s->v[k], xrd64(s->buf + 8 * k));
+        s->nbuf = 0;
+    }
+    for (; n >= 32; p += 32, n -= 32)
+        for (int k = 0; k < 4; k++) s->v[k] = xround(s->v[k], xrd64(p + 8 * k));
+    memcpy(s->buf, p, n);
+    s->nbuf = (int)n;
+}
+static uint64_t xxh64_digest(const xxh64_state *s) {
+    uint64_t h;
+    if (s->total >= 32) {
+        h = xrotl(s->v[0], 1) + xrotl(s->v[1], 7) + xrotl(s->v[2], 12) + xrotl(s->v[3], 18);
+        for (int k = 0; k < 4; k++) h = xmerge(h, s->v[k]);
+    } else {
+        h = s->seed + XP5;
+    }
+    h += s->total;
+    const uint8_t *p = s->buf;
+    int n = s->nbuf;
+    for (; n >= 8; p += 8, n -= 8) { h ^= xround(0, xrd64(p)); h = xrotl(h, 27) * XP1 + XP4; }
+    if (n >= 4) { h ^= (uint64_t)xrd32(p) * XP1; h = xrotl(h, 23) * XP2 + XP3; p += 4; n -= 4; }
+    for (; n > 0; p++, n--) { h ^= (uint64_t)(*p) * XP5; h = xrotl(h, 11) * XP1; }
+    h ^= h >> 33; h *= XP2; h ^= h >> 29; h *= XP3; h ^= h >> 32;
+    return h;
+}
+uint64_t orc_xxh64(const void *data, size_t n, uint64_t seed) {
+    xxh64_state s;
+    xxh64_init(&s, seed);
+    xxh64_update(&s, data, n);
+    return xxh64_digest(&s);
+}
+
+/* The per-haplotype weight of the key sketch: splitmix64's output for h. */
+static uint64_t sketch_weight(uint64_t h) {
+    uint64_t z = h + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static uint64_t dmix(uint64_t h, uint64_t x) {
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
+}
+
+/* Digests of the last region (orc_region_end): keys = the sum over its keys of
+ * dmix(bed index, start, end, pattern_id, S, starting at 0x2545F4914F6CDD1D) with
+ * S = sum over samples s of L[s] w(2s) + R[s] w(2s + 1) mod 2^64 (w = splitmix64):
+ * order-free, a linear sketch of count_matches_by_sample's vectors (main.rs:500-534);
+ * rows = XXH64 (seed 0) of the rows emitted since the last orc_job_clear_rows with
+ * each row's POS field removed (every row's text after "<chr>\t<POS>\t", '\n'
+ * included), *n_rows their number. */
+void orc_job_digests(const orc_job *j, uint64_t *keys, uint64_t *rows, uint64_t *n_rows) {
+    uint64_t sum = 0;
+    uint64_t *w = (uint64_t *)malloc(sizeof(uint64_t) * (2 * (size_t)j->nsamp + 1));
+    for (uint64_t h = 0; h < 2 * (uint64_t)j->nsamp; h++) w[h] = sketch_weight(h);
+    for (int i = 0; i < j->keys.n; i++) {
+        const orc_key *q = &j->keys.k[i];
+        uint64_t S = 0;
+        for (int s = 0; s < j->nsamp; s++) S += (uint64_t)q->l[s] * w[2 * s] + (uint64_t)q->r[s] * w[2 * s + 1];
+        uint64_t h = 0x2545F4914F6CDD1Dull;
+        h = dmix(h, (uint64_t)q->bed);
+        h = dmix(h, q->s);
+        h = dmix(h, q->e);
+        h = dmix(h, q->pid);
+        h = dmix(h, S);
+        sum += h;
+    }
+    free(w);
+    *keys = sum;
+    xxh64_state st;
+    xxh64_init(&st, 0);
+    uint64_t nr = 0;
+    const char *p = j->rows.p, *end = j->rows.p ? j->rows.p + j->rows.n : NULL;
+    while (p && p < end) {
+        const char *nl = memchr(p, '\n', (size_t)(end - p));
+        const char *stop = nl ? nl + 1 : end;
+        const char *t1 = memchr(p, '\t', (size_t)(stop - p));
+        const char *t2 = t1 ? memchr(t1 + 1, '\t', (size_t)(stop - t1 - 1)) : NULL;
+        const char *body = t2 ? t2 + 1 : p;
+        xxh64_update(&st, body, (size_t)(stop - body));
+        nr++;
+        p = stop;
+    }
+    *rows = xxh64_digest(&st);
+    *n_rows = nr;
+}

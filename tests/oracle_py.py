@@ -81,6 +81,9 @@ def lib():
         L.orc_job_stats.argtypes = [C.c_void_p, intp, intp, u64p]
         L.orc_job_set_scan_only.argtypes = [C.c_void_p, C.c_int]
         L.orc_job_phase_seconds.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.orc_job_digests.argtypes = [C.c_void_p, u64p, u64p, u64p]
+        L.orc_xxh64.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64]
+        L.orc_xxh64.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -322,6 +325,14 @@ class Job:
 
     def clear_rows(self):
         self.L.orc_job_clear_rows(self.h)
+
+    def digests(self):
+        """(keys, rows, n_rows) digests of the last region (orc_job_digests): the order-free
+        sketch of its count_matches_by_sample map and XXH64 of its rows without POS (the
+        rows since the last clear_rows)."""
+        k, r, n = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self.L.orc_job_digests(self.h, C.byref(k), C.byref(r), C.byref(n))
+        return k.value, r.value, n.value
 
     def stats(self):
         a, b, c = C.c_int(), C.c_int(), C.c_uint64()

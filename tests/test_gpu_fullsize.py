@@ -4,13 +4,14 @@ The batch the bench times is scanned here exactly as bench.py builds it (same
 generator, seeds, PWM sets and thresholds), and checked three ways:
 
 * against the oracle (oracle/tfbs_oracle.c, the C restatement of main.rs:94-154,
-  500-534 and 439-498): every region of C2, and for C3/C5 >= 1 000 regions (a
-  deterministic spread: first, last, the last haplotype group, evenly spaced
-  ones; the 50 with the most distinct haplotypes and the 50 with the most
-  variant records -- C5's indel-dense ones --; every region with N runs) key
-  by key -- the per-sample L/R vectors of count_matches_by_sample -- and row by
-  row (POS aside: the oracle numbers rows over its own region subset), in full
-  on 100 of them and through xxh3 digests of the same on the rest;
+  500-534 and 439-498): every region of C3 and C5 (10 000 each) and a spread of
+  1 000+ C4 regions through the oracle's committed per-region digests
+  (tests/golden/fullsize_<W>.npz, tests/golden/make_fullsize_digests.py: a linear
+  sketch of count_matches_by_sample's per-sample L/R vectors and XXH64 of the row
+  text without POS); every region of C2, and ~125 C3/C5 regions (a spread, the
+  10 with the most distinct haplotypes, the 10 with the most variant records --
+  C5's indel-dense ones --, every region with N runs) against the live oracle key
+  by key and row by row (POS aside: the oracle numbers rows over its own subset);
 * the device per-sample encoding (tfbs_batch_encode: the rows formatted from
   per-sample codes) against the oracle on the same regions;
 * device key reduction (the run flow's tfbs_batch_reduce) against the dense
@@ -19,7 +20,8 @@ generator, seeds, PWM sets and thresholds), and checked three ways:
 * C4: 100 000 regions scanned as one batch (a 28 GB count matrix: u64 count
   offsets) and as 8 static region shards of 12 500 (the multi-GPU partition,
   SURVEY.md 8(e)), run one after the other on this GPU: identical digests for
-  every region, and the oracle on a spread of regions of every shard.
+  every region, the golden oracle digests on the spread and the live oracle on
+  a few regions of every shard.
 
 C2/C3 carry no N in the reference (the generator draws ACGT only); the C3
 batch gets extra regions whose reference holds N runs (appended after the
@@ -33,7 +35,7 @@ import pytest
 import xxhash
 
 import oracle_py as O
-from helpers import T, pattern_dicts
+from helpers import GOLD, T, pattern_dicts
 
 pytestmark = pytest.mark.gpu
 
@@ -187,16 +189,30 @@ def _digests(b):
     return [b.digest(r) for r in range(b.num_regions)]
 
 
-def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0, build_device=None):
-    """n_check regions spread over the batch (all of them if n_check >= its size), the
-    n_top regions with the most distinct haplotypes and the n_top with the most
-    variant records, and the n_extra_n regions with N runs, against the oracle:
-    key by key and row by row on a 100-region subset, by xxh3 digests of the same
-    (count_matches_by_sample vectors of every key after the key reduction, row
-    text after the device encoding) on all of them.  build_device: the batch is
-    grouped there as bench.py builds it (SNV-only regions' haplotypes grouped on
-    the GPU); the 100-region subset's rows are then also made as BGZF blocks on
-    the device (tfbs_batch_rows_bgzf), inflated and compared with the oracle's."""
+def _golden(name, cfg):
+    """The oracle's per-region digests of workload `name` (tests/golden/make_fullsize_digests.py)."""
+    g = np.load(os.path.join(GOLD, "fullsize_%s.npz" % name))
+    assert tuple(int(x) for x in g["config"]) == cfg, ("golden file for another configuration", name)
+    return g
+
+
+def _check_golden(label, want_idx, want, got):
+    bad = [int(i) for i, a, b in zip(want_idx, want, got) if a != b]
+    assert not bad, (label, len(bad), bad[:10])
+
+
+def _fullsize(tmp_path, cfg, n_full, golden=None, n_extra_n=0, n_top=0, build_device=None):
+    """Every region of the batch against the oracle's golden digests (golden: the workload
+    name; tests/golden/fullsize_<W>.npz, made by the oracle over the same generator): the
+    canonical sketch of count_matches_by_sample's per-sample vectors after the device key
+    reduction, and XXH64 of the row text after the device encoding (tfbs_batch_region_digests
+    vs orc_job_digests).  Besides, against the live oracle key by key and row by row: ~n_full
+    regions spread over the batch, the n_top regions with the most distinct haplotypes and
+    the n_top with the most variant records (C5's indel-dense ones), and the n_extra_n regions
+    with N runs appended after the generator's.  build_device: the batch is grouped there as
+    bench.py builds it; those regions' rows are then also made as BGZF blocks on the device
+    (tfbs_batch_rows_bgzf), inflated and compared with the oracle's.  Without golden digests
+    (C2) every region is checked live."""
     n_samples, n_regions, _, _, indel, seed = cfg
     ps = _patterns(tmp_path, cfg)
     lmax = ps.max_length
@@ -208,58 +224,65 @@ def _fullsize(tmp_path, cfg, n_check, n_extra_n=0, n_top=0, build_device=None):
     extra = _n_regions(seed, n_regions, n_extra_n, n_samples, lmax, indel) if n_extra_n else []
     _append_regions(b, extra)
     assert b.num_regions == n_regions + n_extra_n
+    g = _golden(golden, cfg) if golden else None
+    if g is not None:
+        assert list(g["regions"]) == list(range(n_regions))
     sc = T.Scanner(ps)
     try:
         # the run flow's path: device key reduction
         b.scan(sc, reduce=True)
         reduced = _digests(b)
-        check = set(_spread(n_regions, n_check) if n_check < n_regions else range(n_regions))
+        n_golden = 0
+        if g is not None:  # every region's keys vs the oracle
+            keys, _, _ = b.region_digests(0, n_regions, threads=THREADS, rows=False)
+            _check_golden("keys", range(n_regions), g["keys"], keys)
+            n_golden = n_regions
+        full = set(_spread(n_regions, n_full) if n_full < n_regions else range(n_regions))
         if n_top:
             st = [b.region_stats(i) for i in range(n_regions)]
-            check |= set(sorted(range(n_regions), key=lambda i: -st[i][0])[:n_top])
-            check |= set(sorted(range(n_regions), key=lambda i: -st[i][1])[:n_top])
-        check = sorted(check)
-        full = set(check) if len(check) <= 100 else {check[i] for i in _spread(len(check), 100)}
-        jobs = _synth_jobs(seed, check, n_samples, lmax, indel)
+            full |= set(sorted(range(n_regions), key=lambda i: -st[i][0])[:n_top])
+            full |= set(sorted(range(n_regions), key=lambda i: -st[i][1])[:n_top])
+        jobs = _synth_jobs(seed, sorted(full), n_samples, lmax, indel)
         jobs += [(n_regions + k, r["merged"], r["ref"], r["records"]) for k, r in enumerate(extra)]
-        full |= {n_regions + k for k in range(len(extra))}
-        ref = _oracle_regions(ps, n_samples, seed, indel, [j for j in jobs if j[0] in full])
-        dig = _oracle_regions(ps, n_samples, seed, indel, [j for j in jobs if j[0] not in full], digest=True)
-        # the device key reduction: every checked region's keys (rows in full on the subset)
-        n_full = _check_vs_oracle(b, ref, "reduce")
-        _check_vs_oracle(b, dig, "reduce", digest=True, rows=False)
+        ref = _oracle_regions(ps, n_samples, seed, indel, jobs)
+        # the device key reduction: every checked region's keys and rows in full
+        n_full_rows = _check_vs_oracle(b, ref, "reduce")
         # the device per-sample encoding (f1) the run flow formats rows from, 2 000
-        # regions at a time: every checked region's rows
+        # regions at a time: every region's row digest, the live regions' text
         n_enc = n_rows = n_bgzf = 0
         for r0 in range(0, b.num_regions, 2000):
             r1 = min(b.num_regions, r0 + 2000)
             b.encode(sc, r0, r1)
             n_enc += _check_vs_oracle(b, {i: ref[i] for i in ref if r0 <= i < r1}, "encode", keys=False)
-            n_rows += _check_vs_oracle(b, {i: dig[i] for i in dig if r0 <= i < r1}, "encode", digest=True, keys=False)
-            if build_device is not None:  # the device BGZF writer's rows of the subset vs the oracle's
+            if g is not None and r0 < n_regions:
+                e1 = min(r1, n_regions)
+                _, rows, nr = b.region_digests(r0, e1, threads=THREADS, keys=False)
+                _check_golden("rows", range(r0, e1), g["rows"][r0:e1], rows)
+                _check_golden("n_rows", range(r0, e1), g["n_rows"][r0:e1], nr)
+                n_rows += int(nr.sum())
+            if build_device is not None:  # the device BGZF writer's rows of the live regions vs the oracle's
                 import gzip
                 for i in sorted(x for x in ref if r0 <= x < r1):
                     data, _, nr, _ = b.rows_bgzf(sc, "chr1", 0, 1, i, i + 1)
                     got = _strip_pos(gzip.decompress(data).decode()) if data else []
                     assert got == ref[i][1], ("bgzf", i)
                     n_bgzf += nr
-        assert n_enc == n_full
+        assert n_enc == n_full_rows
         if build_device is not None:
-            assert n_bgzf == n_full
-        n_rows += n_enc
+            assert n_bgzf == n_full_rows
         # dense download over the same batch, rescanned
         b.scan(sc, upload=False, download=True)
         assert _digests(b) == reduced
         _check_vs_oracle(b, {i: ref[i] for i in list(ref)[:24]}, "dense")
     finally:
         sc.close()
-    return b, n_rows, len(ref) + len(dig)
+    return b, n_rows + n_full_rows, n_golden, len(ref)
 
 
 def test_c2_full_vs_oracle(tmp_path):
-    """C2 in full: 1 000 samples x 1 000 regions x 10 PWMs, every region vs the oracle."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C2, C2[1])
-    assert n_checked == C2[1] and n_rows > 100
+    """C2 in full: 1 000 samples x 1 000 regions x 10 PWMs, every region vs the live oracle."""
+    b, n_rows, _, n_live = _fullsize(tmp_path, C2, C2[1])
+    assert n_live == C2[1] and n_rows > 100
 
 
 def test_c3_full_batch_vs_oracle(tmp_path):
@@ -267,16 +290,16 @@ def test_c3_full_batch_vs_oracle(tmp_path):
     ~1.18 M distinct haplotypes, one batch, SNV-only regions grouped on the GPU), plus
     6 regions with N runs at its end (built on the host); the device BGZF rows of the
     100-region subset against the oracle's."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C3, 1000, n_extra_n=6, n_top=50, build_device=0)
-    assert n_checked >= 1000 and n_rows > 0
+    b, n_rows, n_golden, n_live = _fullsize(tmp_path, C3, 100, "C3", n_extra_n=6, n_top=10, build_device=0)
+    assert n_golden == C3[1] and n_live >= 100 and n_rows > 300_000
     assert b.num_haplotypes > 1_000_000
 
 
 def test_c5_full_batch_vs_oracle(tmp_path):
     """C5: C3 with 30 % indels (non-affine positions, variable-length haplotypes) and
     PWMs of length 25-30 (K depth 2 of the matrix-core kernel)."""
-    b, n_rows, n_checked = _fullsize(tmp_path, C5, 1000, n_extra_n=4, n_top=50, build_device=0)
-    assert n_checked >= 1000 and n_rows > 0
+    b, n_rows, n_golden, n_live = _fullsize(tmp_path, C5, 100, "C5", n_extra_n=4, n_top=10, build_device=0)
+    assert n_golden == C5[1] and n_live >= 100 and n_rows > 0
 
 
 def test_c4_shards_equal_unsharded(tmp_path):
@@ -294,13 +317,21 @@ def test_c4_shards_equal_unsharded(tmp_path):
         want = _digests(whole)
         del whole
         n_shards = 8
-        got, checked = [], 0
+        g = _golden("C4", C4)
+        gidx = [int(i) for i in g["regions"]]
+        got, checked, n_golden = [], 0, 0
         for k in range(n_shards):
             r0, r1 = k * n_regions // n_shards, (k + 1) * n_regions // n_shards
             b = T.RegionBatch(ps, n_samples)
             b.synth_fill(seed, r0, r1 - r0, indel)
             b.scan(sc, reduce=True)
             got += _digests(b)
+            sel = [q for q, i in enumerate(gidx) if r0 <= i < r1]
+            with cf.ThreadPoolExecutor(THREADS) as ex:  # one region per call (ctypes drops the GIL)
+                dg = list(ex.map(lambda q: b.region_digests(gidx[q] - r0, gidx[q] - r0 + 1, threads=1), sel))
+            for name, f in (("keys", 0), ("rows", 1), ("n_rows", 2)):
+                _check_golden("C4 " + name, [gidx[q] for q in sel], g[name][sel], [d[f][0] for d in dg])
+            n_golden += len(sel)
             local = [0, (r1 - r0) // 2, r1 - r0 - 1] + list(range(3, r1 - r0, (r1 - r0) // 5))
             jobs = [(i, m, rf, rc) for (i, m, rf, rc) in _synth_jobs(seed, [r0 + i for i in local], n_samples, lmax,
                                                                       indel)]
@@ -312,7 +343,7 @@ def test_c4_shards_equal_unsharded(tmp_path):
         assert len(got) == len(want)
         bad = [i for i in range(n_regions) if got[i] != want[i]]
         assert not bad, bad[:10]
-        assert checked >= 40
+        assert checked >= 40 and n_golden == len(gidx) >= 1000
     finally:
         sc.close()
 

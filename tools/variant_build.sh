@@ -12,8 +12,10 @@ for spec in "$@"; do
   [ -z "$file" ] && file=find-tfbs_amd/csrc/$src.hip
   d=find-tfbs_amd/lib/probe$name
   mkdir -p $d
+  flags=""
+  [ "$src" = scan_mfma ] && flags="-mllvm -amdgpu-mfma-vgpr-form -ffinite-math-only"  # as the Makefile
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter --offload-arch=gfx950 -munsafe-fp-atomics \
-    -Ifind-tfbs_amd/csrc $extra -x hip -c $file -o $d/$src.o
+    $flags -Ifind-tfbs_amd/csrc $extra -x hip -c $file -o $d/$src.o
   objs=$(ls find-tfbs_amd/lib/obj/*.o | grep -v "/$src.o")
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $d/libtfbs_amd.so $objs $d/$src.o -lz -lpthread
 done
