@@ -787,6 +787,9 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         uint32_t n;
         bool has_n, affine, dedup = false;
         uint32_t r0 = 0, rn = 0;  // HAP_DEDUP: its diff runs (a, b), ascending, merged: rruns[j][r0 .. r0 + rn)
+        // and the same in the reference's columns (rruns[j][q0 .. q0 + qn)), q0 = r0 when
+        // both are the same list (every column at its reference column: no indel)
+        uint32_t q0 = 0, qn = 0;
     };
     std::vector<std::vector<HapInfo>> info(nr);
     std::vector<std::vector<uint32_t>> rruns(nr);  // per region, its haplotypes' diff runs
@@ -818,30 +821,29 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             h.affine = true;
             for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
         }
-        // reference-window reuse: a window whose bases and positions are the
-        // reference window's has its hits.  Per haplotype, the runs of columns that
-        // differ from the reference -- another base, another position (past an
-        // indel), or past the end of either sequence -- are recorded; the scan reads
-        // only the windows that meet one (haplotypes and reference of up to
-        // kDedupMaxWindows bases, at most kMaxDiffRuns runs).
+        // reference-window reuse: a window whose bases equal those of the reference
+        // window that starts at its first base's position has that window's score and
+        // match range (pattern.rs:151-156: the range is [pos_i, pos_i + L - 1]), so its
+        // hit (or none) is the reference's.  A haplotype's *segments* are maximal runs of
+        // columns equal to the reference column at their position with consecutive
+        // positions (one shift each: 0 before an indel, the indel's length after it),
+        // their reference ranges ascending and disjoint; a window inside one segment is
+        // the reference window shifted by the segment's shift.  The columns outside the
+        // segments form the haplotype's diff runs (in its own columns: the windows the
+        // scan reads, tfbs_internal.hpp), those outside the segments' reference ranges
+        // the same runs in the reference's columns (the reference hits the key assembly
+        // passes on); two segments that touch get a boundary run (a, a - 1), which meets
+        // exactly the windows spanning both.  Haplotypes and reference of up to
+        // kDedupMaxWindows bases, at most kMaxDiffRuns runs of either kind.
         const int32_t ref = rb.R.ref_local >= 0 ? rb.R.ref_local : (rb.helper ? (int32_t)rb.n_haps() - 1 : -1);
         if (!B.dedup || ref < 0) return;
         std::vector<uint32_t> &rv = rruns[j];
-        auto start = [&](HapInfo &h) { h.r0 = (uint32_t)rv.size(); };
-        auto add = [&](HapInfo &h, uint32_t p, uint32_t e) {  // columns p .. e, appended in ascending order
-            if (rv.size() > h.r0 && (rv.back() == kRunToEnd || rv.back() + 1 >= p)) {
+        auto add = [&](uint32_t r0, uint32_t p, uint32_t e) {  // columns p .. e (e = p - 1: a boundary), ascending
+            if (rv.size() > r0 && (rv.back() == kRunToEnd || rv.back() + 1 >= p)) {
                 rv.back() = std::max(rv.back(), e);
             } else {
                 rv.push_back(p);
                 rv.push_back(e);
-            }
-        };
-        auto finish = [&](HapInfo &h) {
-            h.rn = (uint32_t)rv.size() - h.r0;
-            h.dedup = h.rn / 2 <= kMaxDiffRuns;
-            if (!h.dedup) {
-                rv.resize(h.r0);
-                h.rn = 0;
             }
         };
         if (rb.dev) {  // every haplotype has the reference's length: its SNV columns differ
@@ -849,27 +851,77 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             for (size_t i = 0; i < rb.masks.size(); i++) {
                 if ((int32_t)i == ref) continue;
                 HapInfo &h = info[j][i];
-                start(h);
+                h.r0 = h.q0 = (uint32_t)rv.size();
                 for (uint64_t x = rb.masks[i]; x; x &= x - 1) {
                     const uint32_t p = rb.snv_rel[__builtin_ctzll(x)];
-                    add(h, p, p);
+                    add(h.r0, p, p);
                 }
-                finish(h);
+                h.rn = h.qn = (uint32_t)rv.size() - h.r0;
+                h.dedup = h.rn / 2 <= kMaxDiffRuns;
+                if (!h.dedup) rv.resize(h.r0), h.rn = h.qn = 0;
             }
             return;
         }
         const std::vector<uint8_t> &rn = rb.dist[ref].nuc;
-        if (rn.size() > kDedupMaxWindows) return;
+        const uint32_t m = (uint32_t)rn.size();
+        if (m > kDedupMaxWindows) return;
+        struct Seg {
+            uint32_t a, b, qa;  // columns [a, b) at reference columns [qa, qa + b - a)
+        };
+        std::vector<Seg> segs;
         for (size_t i = 0; i < rb.dist.size(); i++) {
             HapInfo &h = info[j][i];
             if ((int32_t)i == ref || h.n > kDedupMaxWindows) continue;
             const Distinct &d = rb.dist[i];
-            start(h);
-            const uint32_t nmin = std::min<uint32_t>(h.n, (uint32_t)rn.size());
-            for (uint32_t p = 0; p < nmin; p++)
-                if (d.nuc[p] != rn[p] || d.pos[p] != rb.R.es + p) add(h, p, p);
-            if (h.n != rn.size()) add(h, nmin, kRunToEnd);  // columns past the shorter sequence differ
-            finish(h);
+            segs.clear();
+            uint32_t qend = 0;  // the last segment's reference end (exclusive)
+            bool open = false;
+            for (uint32_t p = 0; p < h.n; p++) {
+                const int64_t q = (int64_t)d.pos[p] - (int64_t)rb.R.es;
+                const bool ok = q >= 0 && q < (int64_t)m && d.nuc[p] == rn[(size_t)q];
+                if (open && ok && d.pos[p] == d.pos[p - 1] + 1) continue;  // the segment goes on
+                if (open) {
+                    segs.back().b = p;
+                    qend = segs.back().qa + (p - segs.back().a);
+                    open = false;
+                }
+                if (ok && (segs.empty() || (uint32_t)q >= qend)) {
+                    segs.push_back({p, h.n, (uint32_t)q});
+                    open = true;
+                }
+            }
+            // the haplotype's own columns: outside the segments, and where two touch
+            h.r0 = (uint32_t)rv.size();
+            uint32_t at = 0;
+            for (size_t k = 0; k < segs.size(); k++) {
+                if (segs[k].a > at) add(h.r0, at, segs[k].a - 1);
+                else if (k) add(h.r0, at, at - 1);
+                at = segs[k].b;
+            }
+            if (at < h.n || segs.empty()) add(h.r0, at, kRunToEnd);
+            h.rn = (uint32_t)rv.size() - h.r0;
+            bool shifted = false;  // some segment off its own column: a separate reference-column list
+            for (const Seg &g : segs) shifted = shifted || g.qa != g.a;
+            if (h.n != m) shifted = true;
+            if (!shifted) {
+                h.q0 = h.r0;
+                h.qn = h.rn;
+            } else {  // the reference's columns: outside the segments' ranges, and where two touch
+                h.q0 = (uint32_t)rv.size();
+                uint32_t qa = 0;
+                for (size_t k = 0; k < segs.size(); k++) {
+                    if (segs[k].qa > qa) add(h.q0, qa, segs[k].qa - 1);
+                    else if (k) add(h.q0, qa, qa - 1);
+                    qa = segs[k].qa + (segs[k].b - segs[k].a);
+                }
+                if (qa < m || segs.empty()) add(h.q0, qa, kRunToEnd);
+                h.qn = (uint32_t)rv.size() - h.q0;
+            }
+            h.dedup = h.rn / 2 <= kMaxDiffRuns && h.qn / 2 <= kMaxDiffRuns;
+            if (!h.dedup) {
+                rv.resize(h.r0);
+                h.rn = h.qn = 0;
+            }
         }
     });
     // serial layout: region / haplotype / word / mask / position offsets
@@ -890,7 +942,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if (h.has_n) cur.nmask += (h.n + 31) / 32 + 2;
             if (!h.affine) cur.pos += h.n;
             cur.count += (uint64_t)B.n_slots * n_inner;
-            cur.runs += h.rn;
+            cur.runs += h.rn + (h.q0 != h.r0 ? h.qn : 0);
         }
     }
     const uint32_t region0 = (uint32_t)B.rh.size();
@@ -989,6 +1041,13 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 hm.n_druns = h.rn / 2;
                 std::copy(rruns[j].begin() + h.r0, rruns[j].begin() + h.r0 + h.rn, B.druns.begin() + runs);
                 runs += h.rn;
+                hm.rrun_off = hm.drun_off;
+                hm.n_rruns = h.qn / 2;
+                if (h.q0 != h.r0) {  // (an indel haplotype) its runs in the reference's columns follow
+                    hm.rrun_off = (uint32_t)(runs / 2);
+                    std::copy(rruns[j].begin() + h.q0, rruns[j].begin() + h.q0 + h.qn, B.druns.begin() + runs);
+                    runs += h.qn;
+                }
             }
             B.haps[o.hap + i] = hm;
             B.hap_carriers[o.hap + i] = rb.carriers[i];

@@ -120,7 +120,9 @@ struct tfbs_ctx {
     DevBuf<HitSrc> srcs;
     bool debug_over = false;  // TFBS_DEBUG_OVER: print the overflow lists' fill after each check
     uint32_t n_regions = 0;                // of the resident batch
-    uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP)
+    uint32_t cand_cap = 1024;            // per scan workgroup (TFBS_CAND_CAP), per super tile it scans
+    bool mfma_merged = true;             // TFBS_SCAN_MERGED=0: one launch per depth class (a workgroup per super tile)
+    uint32_t scan_cand_cap = 1024;       // the last scan's list entries per workgroup (ScanArgs::cand_cap)
     DevBuf<DevMSuper> m_supers;
     bool mfma = true;             // int8 matrix-core path for eligible strands (TFBS_MFMA=0: LUT only)
     uint32_t mfma_lds = 44 * 1024;  // LDS image budget of one MFMA super tile
@@ -137,7 +139,7 @@ struct tfbs_ctx {
     DevBuf<uint32_t> wl[2];
     DevBuf<uint16_t> wl16[2];  // the narrow groups' window lists
     DevBuf<uint8_t> gnarrow;   // per haplotype group of mfma_hpb: every haplotype <= kWlNarrowLen bases
-    DevBuf<uint4> hd;          // the matrix-core scan's compact haplotype descriptors
+    DevBuf<uint4> hd, hd2;     // the matrix-core scan's compact haplotype descriptors
     uint64_t wl_entries[2] = {0, 0};
     double wl_seconds = 0;                // the last build's wall time
     DevBuf<DevRegion> regions;
@@ -271,8 +273,10 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
         bufs.list16[c] = nullptr;
     }
     bufs.gnarrow = narrow.empty() ? nullptr : ctx->gnarrow.p;
-    if ((rc = ctx->hd.ensure(std::max<uint32_t>(n_haps, 1)))) return rc;
+    if ((rc = ctx->hd.ensure(std::max<uint32_t>(n_haps, 1))) || (rc = ctx->hd2.ensure(std::max<uint32_t>(n_haps, 1))))
+        return rc;
     bufs.hd = ctx->hd.p;
+    bufs.hd2 = ctx->hd2.p;
     bufs.scan_tmp = ctx->wl_tmp.p;
     auto ensure = [](void *x, int c, uint64_t n, uint32_t **p, uint16_t **p16) {
         tfbs_ctx *cx = static_cast<tfbs_ctx *>(x);
@@ -335,14 +339,21 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.mweights = ctx->m_weights.p;
         m.mmeta = ctx->m_meta.p;
         m.haps_per_block = ctx->mfma_hpb;
-        // one candidate list and one hit list per scan workgroup (super tile x haplotype group)
-        const uint64_t n_wg = (uint64_t)P.m_supers.size() * ((n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb);
+        // one candidate list and one hit list per scan workgroup (super tile x haplotype
+        // group; merged: one workgroup per group scans every super tile, its lists hold
+        // their candidates)
+        const uint64_t n_groups = (n_haps + ctx->mfma_hpb - 1) / ctx->mfma_hpb;
+        const uint64_t n_wg = ctx->mfma_merged ? n_groups : (uint64_t)P.m_supers.size() * n_groups;
+        const uint32_t cand_cap = ctx->mfma_merged
+                                      ? (uint32_t)std::min<uint64_t>(1u << 16, (uint64_t)ctx->cand_cap * P.m_supers.size())
+                                      : ctx->cand_cap;
         int rc;
-        if ((rc = ctx->cands.ensure(n_wg * ctx->cand_cap * kCandWords)) ||
-            (rc = ctx->hitl.ensure(n_wg * ctx->cand_cap * 2)) || (rc = ctx->hitn.ensure(n_wg * (kMBlockWaves))))
+        if ((rc = ctx->cands.ensure(n_wg * cand_cap * kCandWords)) || (rc = ctx->hitl.ensure(n_wg * cand_cap * 2)) ||
+            (rc = ctx->hitn.ensure(n_wg * (kMBlockWaves))))
             return rc;
         m.cands = ctx->cands.p;
-        m.cand_cap = ctx->cand_cap;
+        m.cand_cap = cand_cap;
+        ctx->scan_cand_cap = cand_cap;
         m.hitl = ctx->hitl.p;
         m.hitn = ctx->hitn.p;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
@@ -355,6 +366,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.dedup = 1;
         m.gnarrow = ctx->gnarrow.n ? ctx->gnarrow.p : nullptr;
         m.hd = ctx->hd.p;
+        m.hd2 = ctx->hd2.p;
         m.druns = ctx->druns.p;
         m.n_regions = ctx->n_regions;
         m.ref_hits = ctx->ref_hits.p;
@@ -390,6 +402,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         int n_depths = 0;
         for (size_t k = 0; k < P.m_supers.size(); k++)
             n_depths += (k == 0 || P.m_supers[k].nk != P.m_supers[k - 1].nk) ? 1 : 0;
+        if (ctx->mfma_merged) n_depths = 1;  // one launch
         const int n_side = std::min(n_depths - 1, (int)tfbs_ctx::kSide);
         hipStream_t streams[tfbs_ctx::kSide + 1] = {ctx->stream};
         if (n_side > 0) HIP_TRY(hipEventRecord(ctx->fork, ctx->stream));
@@ -397,8 +410,11 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             HIP_TRY(hipStreamWaitEvent(ctx->side[i], ctx->fork, 0));
             streams[i + 1] = ctx->side[i];
         }
-        const int n = launch_mfma(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words, n_haps,
-                                  streams, (uint32_t)n_side + 1, ctx->srcs_host, &ctx->n_srcs);
+        const int n = ctx->mfma_merged
+                          ? launch_mfma_all(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words,
+                                            n_haps, ctx->stream, ctx->srcs_host, &ctx->n_srcs)
+                          : launch_mfma(m, P.m_supers.data(), (uint32_t)P.m_supers.size(), ctx->mfma_group_words,
+                                        n_haps, streams, (uint32_t)n_side + 1, ctx->srcs_host, &ctx->n_srcs);
         if (n < 0) return n;
         for (int i = 0; i < n_side; i++) {
             HIP_TRY(hipEventRecord(ctx->join[i], ctx->side[i]));
@@ -536,7 +552,7 @@ static AsmArgs asm_args(tfbs_ctx *ctx, const Batch &B, int mode) {
     a.hpb = ctx->mfma_hpb;
     a.hitl = ctx->hitl.p;
     a.hitn = ctx->hitn.p;
-    a.cand_cap = ctx->cand_cap;
+    a.cand_cap = ctx->scan_cand_cap;
     a.srcs = ctx->srcs.p;
     a.mfma = ctx->plan.m_supers.empty() ? 0 : 1;
     a.n_srcs = a.mfma ? ctx->n_srcs : 0;
@@ -593,6 +609,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
     ctx->gnarrow.release();
     ctx->hd.release();
+    ctx->hd2.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
     ctx->key_first.release(); ctx->var_counts.release(); ctx->asm_ctr.release(); ctx->key_flags.release();
     ctx->asm_redo.release(); ctx->cor_arena.release();
@@ -649,6 +666,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->mfma_lds = (uint32_t)std::min(144, std::max(8, env_int("TFBS_MFMA_LDS_KB", 44))) * 1024u;
     ctx->mfma_hpb = (uint32_t)std::min((int)kMMaxHapsPerBlock, std::max(4, env_int("TFBS_MFMA_HAPS_PER_BLOCK", 64)));  // 6 bits in a window list entry
     ctx->cand_cap = (uint32_t)std::min(1 << 16, std::max(64, env_int("TFBS_CAND_CAP", 1024)));
+    ctx->mfma_merged = env_int("TFBS_SCAN_MERGED", 1) != 0;
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;

@@ -153,19 +153,19 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
     uint32_t run0 = 0, run1 = 0;
     for (uint32_t l = 0; l < U; l++)  // uniform: the first and last HAP_DEDUP haplotype's runs
         if (A.haps[hb + l].flags & HAP_DEDUP) {
-            run0 = A.haps[hb + l].drun_off;
+            run0 = A.haps[hb + l].rrun_off;
             break;
         }
     for (uint32_t l = U; l-- > 0;)
         if (A.haps[hb + l].flags & HAP_DEDUP) {
-            run1 = A.haps[hb + l].drun_off + A.haps[hb + l].n_druns;
+            run1 = A.haps[hb + l].rrun_off + A.haps[hb + l].n_rruns;
             break;
         }
     const bool lds_haps = U <= kAsmHaps && run1 - run0 <= kAsmRuns;
     if (lds_haps) {
         for (uint32_t l = tid; l < U; l += kAsmBlock) {
             const DevHap h = A.haps[hb + l];
-            s_rh[l] = (h.flags & HAP_DEDUP) ? (h.drun_off - run0) | (h.n_druns << 16) : 0xFFFFFFFFu;
+            s_rh[l] = (h.flags & HAP_DEDUP) ? (h.rrun_off - run0) | (h.n_rruns << 16) : 0xFFFFFFFFu;
         }
         for (uint32_t k = tid; k < run1 - run0; k += kAsmBlock)
             s_run[k] = make_uint2(A.druns[2 * (run0 + k)], A.druns[2 * (run0 + k) + 1]);
@@ -301,8 +301,9 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
                 if (t < nrow) atomicAdd(&cnt[t * U + l], 1u);
             });
             // reference hits: +1 to every HAP_DEDUP haplotype for which the hit's
-            // window is not dirty (its strand columns have the reference's bases and
-            // positions: the scan lists no hit there; tfbs_internal.hpp run_meets, span L)
+            // window is not dirty (in the reference's columns: the haplotype has the
+            // window's bases from its start position on, the scan lists no hit there;
+            // tfbs_internal.hpp run_meets, span L)
             auto dirty = [&](uint32_t l, uint32_t L, uint32_t w) {
                 const uint32_t S = L;
                 if (lds_haps) {
@@ -314,7 +315,7 @@ __global__ __launch_bounds__(kAsmBlock) void key_asm_kernel(AsmArgs A, const uin
                 }
                 const DevHap &h = A.haps[hb + l];
                 if (!(h.flags & HAP_DEDUP)) return true;
-                for (uint32_t k = h.drun_off; k < h.drun_off + h.n_druns; k++)
+                for (uint32_t k = h.rrun_off; k < h.rrun_off + h.n_rruns; k++)
                     if (run_meets(A.druns[2 * k], A.druns[2 * k + 1], w, S)) return true;
                 return false;
             };
@@ -564,11 +565,11 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
         if (l < U) {
             const DevHap &h = A.haps[hb + l];
             lmax = max(lmax, h.len);
-            if (h.flags & HAP_DEDUP) {
-                roff[q] = h.drun_off;
-                rn[q] = h.n_druns;
-                atomicMin(&s_run0, h.drun_off);
-                atomicMax(&s_run1, h.drun_off + h.n_druns);
+            if (h.flags & HAP_DEDUP) {  // its runs in the reference's columns
+                roff[q] = h.rrun_off;
+                rn[q] = h.n_rruns;
+                atomicMin(&s_run0, h.rrun_off);
+                atomicMax(&s_run1, h.rrun_off + h.n_rruns);
             }
         }
     }
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t
     auto hap_info = [&](uint32_t l) -> uint32_t {  // s_hap's entry of any haplotype
         if (l < kFHapLds) return s_hap[l];
         const DevHap &h = A.haps[hb + l];
-        return (h.flags & HAP_DEDUP) ? (h.drun_off - run0) | (h.n_druns << 16) : kFNone;
+        return (h.flags & HAP_DEDUP) ? (h.rrun_off - run0) | (h.n_rruns << 16) : kFNone;
     };
     // the runs in LDS when they fit, else read from global memory (L2)
     const uint2 *const runs = nruns <= kFRuns ? s_run : reinterpret_cast<const uint2 *>(A.druns) + run0;

@@ -63,7 +63,8 @@ struct ScanArgs {
     // entries at the same offsets of wlist16[c] instead (half the bytes to read)
     const uint32_t *wlist[2];
     const uint16_t *wlist16[2];
-    const uint4 *hd;  // matrix-core scan: per haplotype (word_off, len, flags, nmask_off) of haps (build_window_lists)
+    const uint4 *hd;   // matrix-core scan: per haplotype (word_off, len, flags, nmask_off) of haps (build_window_lists)
+    const uint4 *hd2;  // and (region, pos_off, drun_off, n_druns): the rescoring's
     const uint8_t *gnarrow;
     const uint64_t *wlist_off[2];
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
@@ -123,6 +124,10 @@ constexpr int kMaxHitSrcs = 64;
 // HitSrc per launch (*n_srcs of kMaxHitSrcs).
 int launch_mfma(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
                 const hipStream_t *streams, uint32_t n_streams, HitSrc *srcs, uint32_t *n_srcs);
+// The same in one launch on `stream`: one workgroup per haplotype group scans it
+// against every super tile in turn (scan_mfma_all_kernel); one HitSrc with ns = 1.
+int launch_mfma_all(const ScanArgs &a, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words, uint32_t n_haps,
+                    hipStream_t stream, HitSrc *srcs, uint32_t *n_srcs);
 // Rescores the candidates past the waves' lists (after launch_mfma on the same stream).
 int launch_post_scan(const ScanArgs &a, hipStream_t stream);
 // The same (when cand) and the spill records' buckets by region (boff[0 .. n_regions],
@@ -144,6 +149,7 @@ struct WindowListBufs {
     uint16_t *list16[2];   // the narrow groups' entries (gnarrow: one flag per group of hpb)
     const uint8_t *gnarrow;
     uint4 *hd;             // n_haps compact descriptors (ScanArgs::hd), written here
+    uint4 *hd2;            // and ScanArgs::hd2
     uint64_t list_cap[2];  // entries
 };
 size_t scan_tmp_words(size_t n);

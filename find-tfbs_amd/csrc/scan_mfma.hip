@@ -169,7 +169,8 @@ constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue];
 __shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint32_t s_hnext;  // the workgroup's next pair of window tiles (scan_super)
-__shared__ uint4 s_hd[kMMaxHapsPerBlock];  // the group's haplotypes: LaneHap
+__shared__ uint4 s_hd[kMMaxHapsPerBlock];   // the group's haplotypes: LaneHap
+__shared__ uint4 s_hd2[kMMaxHapsPerBlock];  // and (region, pos_off, drun_off, n_druns) for the rescoring
 extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot table | image | words
 
 
@@ -182,11 +183,23 @@ struct GroupCtx {
     __device__ __forceinline__ uint32_t at(uint32_t q) const { return wl16 ? (uint32_t)wl16[q] : wl[q]; }
 };
 
+// What the rescoring reads of a haplotype: DevHap's fields, from the scan
+// workgroup's LDS descriptors (s_hd, s_hd2) or from a DevHap.
+struct CandHap {
+    uint32_t word_off, len, flags, nmask_off, region, pos_off, drun_off, n_druns;
+    __device__ __forceinline__ static CandHap of(const DevHap &h) {
+        return CandHap{h.word_off, h.len, h.flags, h.nmask_off, h.region, h.pos_off, h.drun_off, h.n_druns};
+    }
+    __device__ __forceinline__ static CandHap of(const uint4 &a, const uint4 &b) {
+        return CandHap{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    }
+};
+
 // Exact score of window i of haplotype hp for a strand of length L (i + L <= len):
 // one load per column of the strand's blocks of 8 (zero-padded), all issued
 // before the first is summed (the rescoring runs where no accumulator is
 // live), N columns masked out.
-__device__ __forceinline__ int32_t exact_score(const uint32_t *words, const DevHap &hp, uint32_t i, uint32_t L,
+__device__ __forceinline__ int32_t exact_score(const uint32_t *words, const CandHap &hp, uint32_t i, uint32_t L,
                                                const int32_t *wt, uint32_t live) {
     const uint32_t *w = words + hp.word_off + (i >> 4);
     const uint32_t sh = 2 * (i & 15);
@@ -232,7 +245,7 @@ __device__ __forceinline__ void spill_record(const ScanArgs &A, uint32_t head, u
 // haplotypes) has no counts of its own.  The loads are issued in three
 // dependent rounds (strand fields | weights, region, position, N mask | inner
 // ranges).
-__device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uint32_t *words, const DevHap &hp,
+__device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uint32_t *words, const CandHap &hp,
                                                     uint32_t hap, uint32_t g, uint32_t i, uint32_t *key0) {
     const int32_t *meta = A.mmeta + (size_t)(g >> 6) * kGMetaInts;
     const uint32_t sn = g & 63u;
@@ -379,7 +392,8 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
         if (k < n) {
             const uint2 c = list[k];
             hap = h0 + (c.x >> 24);
-            mask = score_candidate(A, words, A.haps[hap], hap, c.x & 0xFFFFFFu, c.y, &key0);
+            const uint32_t hl = c.x >> 24;  // the haplotype's descriptors, staged in LDS
+            mask = score_candidate(A, words, CandHap::of(s_hd[hl], s_hd2[hl]), hap, c.x & 0xFFFFFFu, c.y, &key0);
         }
         uint64_t act;
         while ((act = __ballot(mask != 0)) != 0) {
@@ -389,7 +403,7 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
                 const uint32_t key = key0 + __builtin_ctz(mask);
                 mask &= mask - 1;
                 if (at < cap) out[at] = make_uint2(A.hap_base + hap, key);
-                else spill_record(A, A.haps[hap].region, A.hap_base + hap, key);
+                else spill_record(A, s_hd2[hap - h0].x, A.hap_base + hap, key);
             }
             hn += (uint32_t)__popcll(act);
         }
@@ -602,7 +616,7 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 // loaded while the current pair is scored.
 #ifdef TFBS_SCAN_PROF
 // per wave: [0] s_memtime at the kernel's start, [1] after the staging barrier, [2]
-// after the scan loop, [3] after the last drain, [4] after the rescoring, [5] / [6]
+// after the scan loops and their drains, [3] (the same), [4] after the rescoring, [5] / [6]
 // s_memrealtime (100 MHz, one clock for the chip) at the start and the end, [7] pairs
 // scored | candidates << 32
 #define SCAN_STAMP(k, v) \
@@ -611,9 +625,14 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 #define SCAN_STAMP(k, v) do { } while (0)
 #endif
 
+// One super tile's window pairs over the group's list of its depth class, then the
+// wave's last queue entries drained into its candidate list (qn, cn: the wave's
+// queued entries and listed candidates, carried over super tiles).  Returns the
+// pairs this wave scored.
 template <int NK>
-__device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S, const char *s_img,
-                                           const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave) {
+__device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper &S, const char *s_img,
+                                              const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave,
+                                              uint32_t &qn, uint32_t &cn) {
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t h1 = min(h0 + A.haps_per_block, A.n_haps);
     const uint64_t e0 = A.wlist_off[NK > 2][h0];
@@ -629,7 +648,6 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
     const int sa = lane < 32 ? kScaleA0 : kScaleA1;
     const char *tab = s_img - kMOnehotBytes;
-    uint32_t qn = 0, cn = 0;  // the wave's queued entries, listed candidates
     auto next_pair = [&]() {
         uint32_t p = 0;
         if (lane == 0) p = atomicAdd(&s_hnext, 1u);
@@ -641,15 +659,10 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         ea = G.at(min(q, G.nw - 1));
         eb = G.at(min(q + kMWindows, G.nw - 1));
     };
-    uint32_t p = next_pair(), ea = 0, eb = 0;
+    uint32_t p = next_pair(), ea = 0, eb = 0, n_pairs = 0;
     if (p < npair) entries(p, ea, eb);
-#ifdef TFBS_SCAN_PROF
-    uint32_t n_pairs = 0;
-#endif
     while (p < npair) {
-#ifdef TFBS_SCAN_PROF
         n_pairs++;
-#endif
         const uint32_t pn = next_pair();
         const bool two = 2 * p + 1 < ntile;
         v4i a0[NK], a1[NK];
@@ -659,15 +672,68 @@ __device__ __forceinline__ void scan_super(const ScanArgs &A, const DevMSuper &S
         scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
         p = pn;
     }
-    SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
-    drain_queue(A, G, qn, wave, lane, cn);  // the wave's last entries
-    SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
-    rescore_list(A, words, h0, wave, lane, cn);
-    SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
-    SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
-#ifdef TFBS_SCAN_PROF
-    SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
-#endif
+    drain_queue(A, G, qn, wave, lane, cn);  // the queue's entries refer to this super tile and list
+    qn = 0;
+    return n_pairs;
+}
+
+// LDS staging of a workgroup: every load of a chunk issued before its LDS stores
+// (one memory round trip per chunk: a load-store loop waited for each load in turn,
+// ~8k cycles per workgroup).
+__device__ __forceinline__ void stage_image(const ScanArgs &A, const DevMSuper &S, uint4 *dst) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
+    const uint32_t n16 = S.img_bytes / 16;
+    constexpr uint32_t kU = 6;  // 48 KiB per chunk: a default-budget image in one
+    for (uint32_t b = 0; b < n16; b += kU * kMBlock) {
+        uint4 v[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t i = b + u * kMBlock + threadIdx.x;
+            if (i < n16) v[u] = src[i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t i = b + u * kMBlock + threadIdx.x;
+            if (i < n16) dst[kMOnehotBytes / 16 + i] = v[u];
+        }
+    }
+}
+
+// The one-hot table (4-mer code -> 64 bits, column t (16 bits) holds FP4 1.0 (0x2)
+// in the nibble of its base), the group's descriptors and (STAGED) its packed
+// words after the image budget; returns the words' base for DevHap::word_off.
+template <bool STAGED>
+__device__ __forceinline__ const uint32_t *stage_group(const ScanArgs &A, int32_t *smem, uint32_t h0, uint32_t hn) {
+    uint2 *tab = reinterpret_cast<uint2 *>(smem);
+    for (uint32_t k = threadIdx.x; k < 256; k += kMBlock) {
+        uint32_t h[4];
+        for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
+        tab[k] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+    }
+    if (threadIdx.x < hn) {  // (32 of DevHap's 48 bytes)
+        s_hd[threadIdx.x] = A.hd[h0 + threadIdx.x];
+        s_hd2[threadIdx.x] = A.hd2[h0 + threadIdx.x];
+    }
+    if (!STAGED) return A.words;
+    const uint4 f = A.hd[h0], l = A.hd[h0 + hn - 1];
+    const uint32_t wbeg = f.x;
+    const uint32_t wend = l.x + (l.y + 15) / 16 + 3;
+    uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max) / 4;
+    constexpr uint32_t kU = 4;
+    for (uint32_t b = 0; b < wend - wbeg; b += kU * kMBlock) {
+        uint32_t v[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t i = b + u * kMBlock + threadIdx.x;
+            if (i < wend - wbeg) v[u] = A.words[wbeg + i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t i = b + u * kMBlock + threadIdx.x;
+            if (i < wend - wbeg) s_words[i] = v[u];
+        }
+    }
+    return s_words - wbeg;
 }
 
 // Grid: n_msupers x ceil(n_haps / haps_per_block), 4 waves per SIMD (two workgroups per CU).
@@ -682,34 +748,13 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
     const DevMSuper S = A.msupers[sidx];
-    uint4 *dst = reinterpret_cast<uint4 *>(smem);
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hn = min(h0 + A.haps_per_block, A.n_haps) - h0;
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
-        for (uint32_t i = threadIdx.x; i < S.img_bytes / 16; i += kMBlock) dst[kMOnehotBytes / 16 + i] = src[i];
-        // one-hot table: 4-mer code -> 64 bits, column t (16 bits) holds FP4
-        // 1.0 (0x2) in the nibble of its base
-        uint2 *tab = reinterpret_cast<uint2 *>(smem);
-        if (threadIdx.x == 0) s_hnext = 0;
-        for (uint32_t k = threadIdx.x; k < 256; k += kMBlock) {
-            uint32_t h[4];
-            for (int t = 0; t < 4; t++) h[t] = 2u << (4 * ((k >> (2 * t)) & 3));
-            tab[k] = make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
-        }
-        if (threadIdx.x < hn) s_hd[threadIdx.x] = A.hd[h0 + threadIdx.x];  // (16 of DevHap's 48 bytes)
-    }
-    const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
-    const uint32_t *words = A.words;
-    if (STAGED) {
-        const uint4 f = A.hd[h0], l = A.hd[h0 + hn - 1];
-        const uint32_t wbeg = f.x;
-        const uint32_t wend = l.x + (l.y + 15) / 16 + 3;
-        uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max) / 4;
-        for (uint32_t i = threadIdx.x; i < wend - wbeg; i += kMBlock) s_words[i] = A.words[wbeg + i];
-        words = s_words - wbeg;
-    }
+    stage_image(A, S, reinterpret_cast<uint4 *>(smem));
+    if (threadIdx.x == 0) s_hnext = 0;
+    const uint32_t *words = stage_group<STAGED>(A, smem, h0, hn);
     __syncthreads();
+    const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     // the wave index is uniform: keep every group-level value in SGPRs
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef TFBS_SCAN_PROF
@@ -717,7 +762,63 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     SCAN_STAMP(5, r_start);
     SCAN_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
-    scan_super<NK>(A, S, s_img, words, hg, lane, wave);
+    uint32_t qn = 0, cn = 0;
+    const uint32_t n_pairs = scan_loop<NK>(A, S, s_img, words, hg, lane, wave, qn, cn);
+    (void)n_pairs;
+    SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
+    SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
+    rescore_list(A, words, h0, wave, lane, cn);
+    SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
+    SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
+    SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
+}
+
+// One workgroup per haplotype group for EVERY super tile (the depth classes in
+// turn): the group's words, descriptors and one-hot table are staged once, each
+// super tile's image in turn (a barrier on either side), and the wave rescores its
+// candidates of all of them once at the end -- the per-workgroup costs (staging,
+// the rescoring's dependent loads) are paid once per group instead of once per
+// super tile.  LDS: one-hot table | the largest image | (STAGED) words.
+template <bool STAGED>
+__global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
+#ifdef TFBS_SCAN_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime(), r_start = __builtin_amdgcn_s_memrealtime();
+#endif
+    int32_t *smem = s_mdyn;
+    const uint32_t hg = blockIdx.x;
+    const uint32_t h0 = hg * A.haps_per_block;
+    const uint32_t hn = min(h0 + A.haps_per_block, A.n_haps) - h0;
+    const uint32_t *words = stage_group<STAGED>(A, smem, h0, hn);
+    const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
+    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t qn = 0, cn = 0, n_pairs = 0;
+#ifdef TFBS_SCAN_PROF
+    bool first = true;
+#endif
+    for (uint32_t si = 0; si < A.n_msupers; si++) {
+        const DevMSuper S = A.msupers[si];
+        __syncthreads();  // the previous image's readers are done
+        stage_image(A, S, reinterpret_cast<uint4 *>(smem));
+        if (threadIdx.x == 0) s_hnext = 0;
+        __syncthreads();
+#ifdef TFBS_SCAN_PROF
+        if (first) {
+            SCAN_STAMP(0, t_start);
+            SCAN_STAMP(5, r_start);
+            SCAN_STAMP(1, __builtin_amdgcn_s_memtime());
+            first = false;
+        }
+#endif
+        n_pairs += S.nk > 2 ? scan_loop<4>(A, S, s_img, words, hg, lane, wave, qn, cn)
+                            : scan_loop<2>(A, S, s_img, words, hg, lane, wave, qn, cn);
+    }
+    (void)n_pairs;
+    SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
+    SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
+    rescore_list(A, words, h0, wave, lane, cn);
+    SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
+    SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
+    SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
 }
 
 // Candidates past the waves' list regions (drain_queue), one per thread; their
@@ -728,7 +829,7 @@ __global__ __launch_bounds__(256) void cand_over_kernel(ScanArgs A) {
         const uint32_t hap = A.cand_over[3 * (size_t)k], g = A.cand_over[3 * (size_t)k + 1];
         const DevHap hp = A.haps[hap];
         uint32_t key0 = 0;
-        for (uint32_t m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0); m;
+        for (uint32_t m = score_candidate(A, A.words, CandHap::of(hp), hap, g, A.cand_over[3 * (size_t)k + 2], &key0); m;
              m &= m - 1)
             spill_record(A, hp.region, hap, key0 + __builtin_ctz(m));
     }
@@ -790,11 +891,13 @@ __global__ __launch_bounds__(256) void wl_fill_kernel(const DevHap *__restrict__
 
 // The scan's compact haplotype descriptors (ScanArgs::hd): word offset, length,
 // flags, N-mask offset of every DevHap.
-__global__ __launch_bounds__(256) void hd_kernel(const DevHap *__restrict__ haps, uint32_t n, uint4 *__restrict__ hd) {
+__global__ __launch_bounds__(256) void hd_kernel(const DevHap *__restrict__ haps, uint32_t n, uint4 *__restrict__ hd,
+                                                  uint4 *__restrict__ hd2) {
     const uint32_t h = blockIdx.x * 256 + threadIdx.x;
     if (h < n) {
         const DevHap x = haps[h];
         hd[h] = make_uint4(x.word_off, x.len, x.flags, x.nmask_off);
+        hd2[h] = make_uint4(x.region, x.pos_off, x.drun_off, x.n_druns);
     }
 }
 
@@ -855,6 +958,7 @@ template <int NK> MfmaKernel mfma_nk(bool staged) {
 MfmaKernel mfma_variant(bool staged, uint32_t nk) {  // depth classes (mfma_depth_class)
     return nk <= 2 ? mfma_nk<2>(staged) : mfma_nk<4>(staged);
 }
+MfmaKernel mfma_all_variant(bool staged) { return staged ? scan_mfma_all_kernel<true> : scan_mfma_all_kernel<false>; }
 
 }  // namespace
 
@@ -913,7 +1017,7 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
                 const uint32_t g = A.cand_over[3 * (size_t)k + 1];
                 const DevHap hp = A.haps[hap];
                 region = hp.region;
-                m = score_candidate(A, A.words, hp, hap, g, A.cand_over[3 * (size_t)k + 2], &key0);
+                m = score_candidate(A, A.words, CandHap::of(hp), hap, g, A.cand_over[3 * (size_t)k + 2], &key0);
             }
             const uint32_t c = (uint32_t)__builtin_popcount(m);
             uint32_t inc = c;
@@ -1039,7 +1143,7 @@ int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *drun
                        int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
                        void *ensure_ctx) {
     if (n_haps && bufs.hd) hipLaunchKernelGGL(hd_kernel, dim3((n_haps + 255) / 256), dim3(256), 0, stream, haps, n_haps,
-                                             bufs.hd);
+                                             bufs.hd, bufs.hd2);
     for (int c = 0; c < 2; c++) {
         total[c] = 0;
         if (!lmin[c]) continue;
@@ -1065,9 +1169,57 @@ size_t mfma_lds_fixed() { return kMOnehotBytes; }
 
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
-    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hd) + 256;  // table, staged words, queues
+    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hd) + sizeof(s_hd2) +
+                             256;  // table, staged words, queues
     // workgroups per CU = 4 SIMDs x waves per SIMD / waves per workgroup
     for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / (4 * waves[nk] / (kMBlock / 64)) - reserve;
+}
+
+int launch_mfma_all(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words,
+                    uint32_t n_haps, hipStream_t stream, HitSrc *srcs, uint32_t *n_srcs) {
+    *n_srcs = 0;
+    if (n_haps == 0 || n_supers == 0) return 0;
+    const uint32_t hpb = a0.haps_per_block;
+    const DevMSuper &last = supers[n_supers - 1];
+    if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > kMMaxHapsPerBlock)
+        return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 64 haplotypes per workgroup");
+    const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
+    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);
+    size_t img_bytes = 0;
+    for (uint32_t k = 0; k < n_supers; k++) img_bytes = std::max<size_t>(img_bytes, supers[k].img_bytes);
+    const size_t base = kMOnehotBytes + img_bytes;
+    const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
+    const bool staged = staged_bytes + static_lds <= kMStagedMax;
+    const size_t lds = staged ? staged_bytes : base;
+    const MfmaKernel kern = mfma_all_variant(staged);
+    hipError_t e = hipSuccess;
+    if (lds > 64 * 1024)
+        e = hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("MFMA LDS attribute: ") + hipGetErrorString(e));
+    int launches = 0;
+    const uint64_t max_hg = (1ull << 31) - 1;
+    for (uint64_t g0 = 0; g0 < n_hg; g0 += max_hg) {
+        const uint32_t ng = (uint32_t)std::min<uint64_t>(max_hg, n_hg - g0);
+        const uint32_t h0 = (uint32_t)(g0 * hpb);
+        ScanArgs a = a0;
+        a.haps = a0.haps + h0;
+        a.hd = a0.hd + h0;
+        a.hd2 = a0.hd2 + h0;
+        a.hap_base = a0.hap_base + h0;
+        for (int c = 0; c < 2; c++) a.wlist_off[c] = a0.wlist_off[c] ? a0.wlist_off[c] + h0 : nullptr;
+        a.gnarrow = a0.gnarrow ? a0.gnarrow + g0 : nullptr;
+        a.n_haps = std::min<uint32_t>(n_haps - h0, ng * hpb);
+        a.hits = a0.hits ? a0.hits + (size_t)h0 * a0.n_patterns_total * a0.hits_wpp : nullptr;
+        a.region_base = (uint32_t)g0;
+        if (*n_srcs >= (uint32_t)kMaxHitSrcs) return fail(TFBS_E_ARG, "matrix-core scan: too many launches");
+        srcs[(*n_srcs)++] = HitSrc{(uint32_t)g0, 1, (uint32_t)g0, ng};
+        a.mimg_max = (uint32_t)img_bytes;
+        hipLaunchKernelGGL(kern, dim3(ng), dim3(kMBlock), lds, stream, a);
+        launches++;
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("scan_mfma_all_kernel launch: ") + hipGetErrorString(e));
+    return launches;
 }
 
 int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, uint32_t group_words,
@@ -1080,7 +1232,8 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
     if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > kMMaxHapsPerBlock)
         return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 64 haplotypes per workgroup");
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd);  // queues, descriptors
+    const size_t static_lds =
+        sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);  // queues, descriptors
     uint32_t region = 0;
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is
@@ -1120,6 +1273,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
             a.n_msupers = ns;
             a.haps = a0.haps + h0;
             a.hd = a0.hd + h0;
+            a.hd2 = a0.hd2 + h0;
             a.hap_base = a0.hap_base + h0;
             for (int c = 0; c < 2; c++) a.wlist_off[c] = a0.wlist_off[c] ? a0.wlist_off[c] + h0 : nullptr;
             a.gnarrow = a0.gnarrow ? a0.gnarrow + g0 : nullptr;

@@ -135,14 +135,17 @@ constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 
 // HAP_REF: the region's reference haplotype (the reference group's, or a
 // helper with no carriers after the region's distinct haplotypes); its
 // matrix-core hits are listed for the reference-window reuse.  HAP_DEDUP: a
-// haplotype of at most kDedupMaxWindows bases whose columns differing from the
-// reference's -- another base or N, another position (past an indel), past the
-// end of either sequence -- form at most kMaxDiffRuns runs (diff runs [a, b],
-// inclusive, ascending, at DevHap::drun_off of the batch's run array).  Window i
-// of a strand of length L is *dirty* iff some run meets its columns [i, i + L -
-// 1]; every other window has the reference window's bases and positions, so its
-// hit (or none) is the reference's, which the key assembly adds
-// (key_kernels.hip).  The matrix-core scan reads the windows dirty for the span
+// haplotype of at most kDedupMaxWindows bases whose columns outside its
+// *segments* (runs of columns equal to the reference column at their position,
+// positions consecutive: the reference shifted by the indels before them;
+// batch.cpp commit_regions) form at most kMaxDiffRuns runs (diff runs [a, b],
+// inclusive, ascending, at DevHap::drun_off of the batch's run array; a run
+// [a, a - 1] marks two touching segments).  Window i of a strand of length L is
+// *dirty* iff some run meets its columns [i, i + L - 1]; every other window lies
+// in one segment and has the bases and the start position of the reference
+// window at i + its shift, so its hit (or none) is that window's, which the key
+// assembly adds (key_kernels.hip, with the runs in the reference's columns:
+// DevHap::rrun_off).  The matrix-core scan reads the windows dirty for the span
 // S = 8 nk of their depth class (S >= L: a superset; the window list,
 // scan_mfma.hip) and lists only the hits of windows dirty for the strand's L.
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
@@ -160,7 +163,10 @@ struct DevHap {
     uint64_t count_off;  // counts[count_off + (slot * n_inner + k) * DevRegion::count_stride]
     uint32_t drun_off;   // HAP_DEDUP: its diff runs, (a, b) u32 pairs at druns + 2 drun_off
     uint32_t n_druns;
-    uint32_t pad[2];
+    // HAP_DEDUP: the same runs in the reference's columns (the reference hits it
+    // takes: key_kernels.hip); = drun_off / n_druns unless it has an indel
+    uint32_t rrun_off;
+    uint32_t n_rruns;
 };
 
 // Window w of span S (a strand's L, or a depth class's 8 nk) is dirty for a

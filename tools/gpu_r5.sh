@@ -20,14 +20,37 @@ for st in "$@"; do
       w=${st#bench_}
       timeout -k 10 400 python3 bench.py --workload $w --no-cpu > $O/bench_$w.json 2> $O/bench_$w.err || { tail -20 $O/bench_$w.err; exit 1; }
       python3 -c "import json;d=json.load(open('$O/bench_$w.json'));print('$w', d['ms_per_step'], d['step_device_ms'], d['roofline']['frac'], d['end_to_end']['regions_per_s'])" ;;
-    sprof_*)
-      w=${st#sprof_}
-      rm -f /tmp/scan_$w.prof
-      TFBS_LIB=find-tfbs_amd/lib/probesprof/libtfbs_amd.so TFBS_SCAN_PROF=/tmp/scan_$w.prof timeout -k 10 300 python3 bench.py --workload $w --steps 1 --warmup 0 --no-cpu --no-e2e > $O/sprof_$w.json 2> $O/sprof_$w.err || { tail -20 $O/sprof_$w.err; exit 1; }
-      python3 tools/scan_prof.py /tmp/scan_$w.prof $O/scan_prof_$w.json > /dev/null || exit 1
+    sprof_*)  # sprof_<W>[:VAR=VAL]: the probesprof build's per-wave phase stamps (env VAR=VAL)
+      spec=${st#sprof_}; w=${spec%%:*}; envv=""; [ "$spec" != "$w" ] && envv=${spec#*:}
+      tag=$w${envv:+_${envv//=/}}
+      rm -f /tmp/scan_$tag.prof
+      env $envv TFBS_LIB=find-tfbs_amd/lib/probesprof/libtfbs_amd.so TFBS_SCAN_PROF=/tmp/scan_$tag.prof timeout -k 10 300 python3 bench.py --workload $w --steps 1 --warmup 0 --no-cpu --no-e2e > $O/sprof_$tag.json 2> $O/sprof_$tag.err || { tail -20 $O/sprof_$tag.err; exit 1; }
+      python3 tools/scan_prof.py /tmp/scan_$tag.prof $O/scan_prof_$tag.json > /dev/null || exit 1
       python3 -c "
-import json;d=json.load(open('$O/scan_prof_$w.json'))
-for l in d['launches']: print(l['launch'], l['workgroups'], {k:round(v,3) for k,v in l['phase_share'].items()}, l['pairs_per_wave'], round(l['cycles_per_pair_in_loop']), l['span_us'], l['tail_us'])" ;;
+import json;d=json.load(open('$O/scan_prof_$tag.json'))
+for l in d['launches']: print('$tag', l['launch'], l['workgroups'], {k:round(v) for k,v in l['phase_cycles_mean_per_wave'].items()}, l['pairs_per_wave']['mean'], round(l['cycles_per_pair_in_loop']), l['candidates_per_wave']['mean'], l['span_us'], l['tail_us'])" ;;
+    pmc_*)  # pmc_<W>[:<variant>]: one SQ counter pass over the MFMA phase (variant: a probe name or e.VAR=VAL)
+      spec=${st#pmc_}; w=${spec%%:*}; v=base; [ "$spec" != "$w" ] && v=${spec#*:}
+      unset TFBS_LIB; envv=""
+      case $v in base) ;; e.*) envv=${v#e.} ;; *) export TFBS_LIB=find-tfbs_amd/lib/probe$v/libtfbs_amd.so ;; esac
+      d=$O/pmc_${w}_${v//=/}
+      env $envv timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $d -o pmc -- python3 bench.py --workload $w --steps 2 --warmup 0 --no-cpu --no-e2e > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
+      unset TFBS_LIB
+      python3 tools/pmc_summary.py $d > /dev/null || exit 1
+      python3 -c "
+import json;q=json.load(open('$d/pmc_summary.json'));m=q['SQ_INSTS_MFMA']
+print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA %.2f conflicts/LDS %.2f mfma_busy_cycles %.3g' % (m, q['SQ_INSTS_VALU']/m, q['SQ_INSTS_SALU']/m, q['SQ_INSTS_LDS']/m, q['SQ_LDS_BANK_CONFLICT']/q['SQ_INSTS_LDS'], q['SQ_VALU_MFMA_BUSY_CYCLES']))" ;;
+    ab_*)  # ab_<W>:<probe>,<probe>: bench.py steps of the in-tree build and probe builds, interleaved twice
+      spec=${st#ab_}; w=${spec%%:*}; libs=${spec#*:}
+      for rep in 1 2; do
+        for lib in base ${libs//,/ }; do
+          unset TFBS_LIB; envv=""
+          case $lib in base) ;; e.*) envv=${lib#e.} ;; *) export TFBS_LIB=find-tfbs_amd/lib/probe$lib/libtfbs_amd.so ;; esac
+          env $envv timeout -k 10 300 python3 bench.py --workload $w --no-cpu --no-e2e --steps 10 > $O/ab_${w}_${lib}_$rep.json 2> $O/ab_${w}_${lib}_$rep.err || { tail -20 $O/ab_${w}_${lib}_$rep.err; exit 1; }
+          python3 -c "import json;d=json.load(open('$O/ab_${w}_${lib}_$rep.json'));print('$w $lib rep$rep ms/step %.3f' % d['ms_per_step'], {k: round(v, 3) for k, v in d['step_device_ms'].items()}, 'scanned %.3g' % d['config']['scanned_windows_per_step'])"
+        done
+      done
+      unset TFBS_LIB ;;
     prof_*)
       w=${st#prof_}
       bash tools/profile_round.sh ${T}_prof_$w --workload $w || exit 1 ;;
