@@ -83,6 +83,7 @@ struct Shard {
     std::string err;
     size_t regions = 0;
     double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0;
+    double t_bcf = 0, t_build = 0;  // of t_prep: BCF fetch + decode + record ids, add_regions
 };
 
 struct RunSetup {
@@ -90,6 +91,10 @@ struct RunSetup {
     std::string chrom;
     tfbs_patterns *pp;
     std::vector<std::pair<std::string, std::vector<std::pair<uint64_t, uint64_t>>>> beds;
+    // per bed source: its peaks' indices by start, and the longest peak's span (the
+    // inner peaks of a merged region by binary search, not a pass over every peak)
+    std::vector<std::vector<uint32_t>> by_start;
+    std::vector<uint64_t> max_span;
     std::vector<std::pair<uint64_t, uint64_t>> merged;
     std::vector<size_t> sel;
     size_t per_batch;
@@ -125,7 +130,8 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     }
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
     std::vector<const BcfRecord *> recs;
-    auto prepare = [&](size_t g, BatchPtr &bp, std::string &err) -> int {
+    auto clock = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    auto prepare = [&](size_t g, BatchPtr &bp, std::string &err, double &t_bcf, double &t_build) -> int {
         const size_t b0 = g * S.per_batch, b1 = std::min(S.merged.size(), b0 + S.per_batch);
         tfbs_batch *bb = nullptr;
         int rc = tfbs_batch_create(S.pp, (uint32_t)S.sel.size(), 1, &bb);
@@ -154,18 +160,30 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                 }
                 in.ref[i] = (uint8_t)c;
             }
-            // select_inner_peaks (main.rs:62-72): p.overlaps(merged)
-            for (size_t bi = 0; bi < S.beds.size(); bi++)
-                for (auto &p : S.beds[bi].second) {
+            // select_inner_peaks (main.rs:62-72): p.overlaps(merged), in file order; only
+            // peaks starting in [m.first - the longest span, m.second] can overlap
+            for (size_t bi = 0; bi < S.beds.size(); bi++) {
+                const auto &pk = S.beds[bi].second;
+                const auto &ord = S.by_start[bi];
+                const uint64_t lo = m.first >= S.max_span[bi] ? m.first - S.max_span[bi] : 0;
+                auto it = std::lower_bound(ord.begin(), ord.end(), lo,
+                                           [&](uint32_t i, uint64_t v) { return pk[i].first < v; });
+                std::vector<uint32_t> hit;
+                for (; it != ord.end() && pk[*it].first <= m.second; ++it) {
+                    const auto &p = pk[*it];
                     const bool ov = (m.first >= p.first && m.first <= p.second) ||
                                     (m.second >= p.first && m.second <= p.second);
-                    if (ov) in.inner.push_back({(uint32_t)bi, {p.first, p.second}});
+                    if (ov) hit.push_back(*it);
                 }
+                std::sort(hit.begin(), hit.end());
+                for (uint32_t i : hit) in.inner.push_back({(uint32_t)bi, {pk[i].first, pk[i].second}});
+            }
             // load_diffs (haplotype.rs:78-80): name2rid(chrom).unwrap() panics on an unknown contig
             if (rid < 0) {
                 err = "chromosome " + S.chrom + " not in the BCF header";
                 return TFBS_E_ARG;
             }
+            const double tb = clock();
             if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
             for (const BcfRecord *br : recs) {
                 Record rec;
@@ -174,9 +192,12 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                 if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
+            t_bcf += clock() - tb;
             ins.push_back(std::move(in));
         }
+        const double tb = clock();
         rc = add_regions(B, ins, sh.threads);
+        t_build += clock() - tb;
         if (rc) return err = tfbs_last_error(), rc;
         return TFBS_OK;
     };
@@ -184,19 +205,19 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     BatchPtr cur(nullptr, tfbs_batch_destroy);
     std::string err;
     double t0 = now();
-    if ((rc = prepare(sh.batches[0], cur, err))) return fail(rc, err);
+    if ((rc = prepare(sh.batches[0], cur, err, sh.t_bcf, sh.t_build))) return fail(rc, err);
     sh.t_prep += now() - t0;
     for (size_t bi = 0; bi < sh.batches.size(); bi++) {
         const size_t g = sh.batches[bi];
         BatchPtr next(nullptr, tfbs_batch_destroy);
         std::string nerr;
         int nrc = TFBS_OK;
-        double nprep = 0;
+        double nprep = 0, nbcf = 0, nbuild = 0;
         std::thread helper;
         if (bi + 1 < sh.batches.size())
             helper = std::thread([&, bi] {
                 const double t0 = now();
-                nrc = prepare(sh.batches[bi + 1], next, nerr);
+                nrc = prepare(sh.batches[bi + 1], next, nerr, nbcf, nbuild);
                 nprep = now() - t0;
             });
         // join the helper on every exit path
@@ -228,6 +249,8 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
         if (helper.joinable()) helper.join();
         sh.t_wait += now() - t0;
         sh.t_prep += nprep;
+        sh.t_bcf += nbcf;
+        sh.t_build += nbuild;
         if (nrc) return fail(nrc, nerr);
         cur = std::move(next);
     }
@@ -375,6 +398,17 @@ int tfbs_run(const tfbs_run_args *a) {
         if (!replaced) S.beds.push_back({bn, kept});
     }
     S.merged = merge_ranges(all);
+    for (auto &b : S.beds) {
+        std::vector<uint32_t> ord(b.second.size());
+        uint64_t span = 0;
+        for (uint32_t i = 0; i < ord.size(); i++) {
+            ord[i] = i;
+            if (b.second[i].second >= b.second[i].first) span = std::max(span, b.second[i].second - b.second[i].first);
+        }
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return b.second[x].first < b.second[y].first; });
+        S.by_start.push_back(std::move(ord));
+        S.max_span.push_back(span);
+    }
 
     // BCF header + samples (main.rs:255, 293-314)
     std::vector<std::string> sample_names;
@@ -538,9 +572,10 @@ int tfbs_run(const tfbs_run_args *a) {
         for (size_t k = 0; k < n_sh; k++)
             fprintf(stderr,
                     "tfbs_run_timing {\"shard\": %zu, \"device\": %d, \"regions\": %zu, \"batches\": %zu, "
-                    "\"prep_s\": %.4f, \"prep_wait_s\": %.4f, \"gpu_s\": %.4f, \"rows_s\": %.4f, "
-                    "\"ordered_write_s\": %.4f, \"close_s\": %.4f, \"loop_s\": %.4f}\n",
+                    "\"prep_s\": %.4f, \"prep_bcf_s\": %.4f, \"prep_build_s\": %.4f, \"prep_wait_s\": %.4f, "
+                    "\"gpu_s\": %.4f, \"rows_s\": %.4f, \"ordered_write_s\": %.4f, \"close_s\": %.4f, \"loop_s\": %.4f}\n",
                     k, shards[k].device, shards[k].regions, shards[k].batches.size(), shards[k].t_prep,
+                    shards[k].t_bcf, shards[k].t_build,
                     shards[k].t_wait, shards[k].t_gpu, shards[k].t_rows, t_write, t_close, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +

@@ -59,6 +59,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 constexpr int kMBlock = 512;          // 8 waves (two per SIMD) share one super tile image
 static_assert(kMBlock / 64 == kMBlockWaves, "hit list parts per workgroup");
 constexpr int kMOnehotBytes = 2048;   // LDS: one-hot table (4-mer -> 4 x 16 bits of FP4), image, words
+constexpr uint32_t kMChunkBytes = 1536;  // one K chunk's B fragments of a 64-strand tile (dwords 0-3 | 4-5)
 constexpr uint32_t kMStagedMax = 80 * 1024;  // LDS per workgroup at 2 workgroups per CU (160 KiB)
 // waves per SIMD the depth kernels' registers allow (see mfma_depth_budgets)
 constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
@@ -419,6 +420,14 @@ __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
     uint32_t u[16];
 #pragma unroll
     for (int r = 0; r < 16; r++) u[r] = __float_as_uint(acc[r]);
+#ifdef TFBS_OR_TREE  // a tree of depth 3 (the compiler chains the ORs: depth 8); the empty
+                     // asm only hides the partial ORs from reassociation (no instruction)
+    uint32_t p[5] = {u[0] | u[1] | u[2], u[3] | u[4] | u[5], u[6] | u[7] | u[8], u[9] | u[10] | u[11],
+                     u[12] | u[13] | u[14]};
+#pragma unroll
+    for (int k = 0; k < 5; k++) asm volatile("" : "+v"(p[k]));
+    return ((p[0] | p[1] | p[2]) | (p[3] | p[4] | u[15])) & kTestMask;
+#endif
     const uint32_t x = (u[0] | u[1] | u[2]) | (u[3] | u[4] | u[5]) | (u[6] | u[7] | u[8]) | (u[9] | u[10] | u[11]) |
                        (u[12] | u[13] | u[14]) | u[15];
     return x & kTestMask;
@@ -464,9 +473,10 @@ __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, co
     }
 }
 
-#ifndef TFBS_BPREFETCH
+#ifndef TFBS_BPREFETCH  // (unused by the tight loop, which always prefetches)
 #define TFBS_BPREFETCH 1
 #endif
+
 // The same with chunk 0's B fragment already loaded (f0: read during the round
 // before, so the round's first MFMAs do not wait for LDS); chunks 1.. are read
 // before the first MFMA is issued.
@@ -513,45 +523,47 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
                                              uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
     if (two) {
-#if TFBS_BPREFETCH
-        BFrag pf;  // the next round's chunk-0 B fragment, read while this round's MFMAs run
+        // a pointer loop (3 scalar instructions per round) and one vector compare for
+        // both tests; the next round's chunk-0 B fragment is read unconditionally (past
+        // the last tile: the image area is padded by kMChunkBytes, the value unused)
+        const char *tile = img;
+        const char *const end = img + (te - tb) * kTB;
+        uint32_t ti = tb;
+        BFrag pf;
         load_frag0(img, lane, pf);
-#endif
-        for (uint32_t ti = tb; ti < te; ti++) {
-            const char *tile = img + (ti - tb) * kTB;
+        do {
             v16f c0, c1;
-#if TFBS_BPREFETCH
             round_scores_pf<D, NK>(tile, lane, pf, a0, a1, cb, sa, c0, c1);
-            load_frag0(ti + 1 < te ? tile + kTB : tile, lane, pf);
-#else
-            round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-#endif
+            load_frag0(tile + kTB, lane, pf);
             uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
-            const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-            if (__builtin_expect((f0 | f1) == 0, 1)) continue;  // one branch for both tests
-            // cold: queue the firing tiles; a tile whose entries do not fit
-            // drains the queue first and its round is scored again (no
-            // accumulator is live across a drain)
-            if (f0) {
-                if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                    drain_queue(A, G, qn, wave, lane, cn);
-                    qn = 0;
-                    round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                    x0 = coarse_test(c0);
-                    x1 = coarse_test(c1);
+            if (__builtin_expect(__ballot((x0 | x1) != 0) != 0, 0)) {
+                // cold: queue the firing tiles; a tile whose entries do not fit
+                // drains the queue first and its round is scored again (no
+                // accumulator is live across a drain)
+                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
+                if (f0) {
+                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x0 = coarse_test(c0);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
                 }
-                queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
-            }
-            if (f1) {
-                if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                    drain_queue(A, G, qn, wave, lane, cn);
-                    qn = 0;
-                    round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                    x1 = coarse_test(c1);
+                if (f1) {
+                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
                 }
-                queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
             }
-        }
+            tile += kTB;
+            ti++;
+        } while (tile != end);
     } else {
         for (uint32_t ti = tb; ti < te; ti++) {
             const char *tile = img + (ti - tb) * kTB;
@@ -677,26 +689,12 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
     return n_pairs;
 }
 
-// LDS staging of a workgroup: every load of a chunk issued before its LDS stores
-// (one memory round trip per chunk: a load-store loop waited for each load in turn,
-// ~8k cycles per workgroup).
+// LDS staging of a workgroup (a plain copy loop: batching all loads before the
+// stores was slower, 2.84 -> 3.10 ms per C3 step).
 __device__ __forceinline__ void stage_image(const ScanArgs &A, const DevMSuper &S, uint4 *dst) {
     const uint4 *src = reinterpret_cast<const uint4 *>(A.mimage + S.img_off / 4);
     const uint32_t n16 = S.img_bytes / 16;
-    constexpr uint32_t kU = 6;  // 48 KiB per chunk: a default-budget image in one
-    for (uint32_t b = 0; b < n16; b += kU * kMBlock) {
-        uint4 v[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t i = b + u * kMBlock + threadIdx.x;
-            if (i < n16) v[u] = src[i];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t i = b + u * kMBlock + threadIdx.x;
-            if (i < n16) dst[kMOnehotBytes / 16 + i] = v[u];
-        }
-    }
+    for (uint32_t i = threadIdx.x; i < n16; i += kMBlock) dst[kMOnehotBytes / 16 + i] = src[i];
 }
 
 // The one-hot table (4-mer code -> 64 bits, column t (16 bits) holds FP4 1.0 (0x2)
@@ -718,21 +716,8 @@ __device__ __forceinline__ const uint32_t *stage_group(const ScanArgs &A, int32_
     const uint4 f = A.hd[h0], l = A.hd[h0 + hn - 1];
     const uint32_t wbeg = f.x;
     const uint32_t wend = l.x + (l.y + 15) / 16 + 3;
-    uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max) / 4;
-    constexpr uint32_t kU = 4;
-    for (uint32_t b = 0; b < wend - wbeg; b += kU * kMBlock) {
-        uint32_t v[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t i = b + u * kMBlock + threadIdx.x;
-            if (i < wend - wbeg) v[u] = A.words[wbeg + i];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t i = b + u * kMBlock + threadIdx.x;
-            if (i < wend - wbeg) s_words[i] = v[u];
-        }
-    }
+    uint32_t *s_words = reinterpret_cast<uint32_t *>(smem) + (kMOnehotBytes + A.mimg_max + kMChunkBytes) / 4;
+    for (uint32_t i = threadIdx.x; i < wend - wbeg; i += kMBlock) s_words[i] = A.words[wbeg + i];
     return s_words - wbeg;
 }
 
@@ -1187,7 +1172,7 @@ int launch_mfma_all(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supe
     const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);
     size_t img_bytes = 0;
     for (uint32_t k = 0; k < n_supers; k++) img_bytes = std::max<size_t>(img_bytes, supers[k].img_bytes);
-    const size_t base = kMOnehotBytes + img_bytes;
+    const size_t base = kMOnehotBytes + img_bytes + kMChunkBytes;  // (the padding: scan_segment's B prefetch)
     const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
     const bool staged = staged_bytes + static_lds <= kMStagedMax;
     const size_t lds = staged ? staged_bytes : base;
@@ -1255,7 +1240,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
         for (uint32_t k = s0; k < s1; k++) img_bytes = std::max<size_t>(img_bytes, supers[k].img_bytes);
         const uint32_t ns = s1 - s0;
         // stage the group's words in LDS when they fit beside the image at 4 workgroups per CU
-        const size_t base = kMOnehotBytes + img_bytes;
+        const size_t base = kMOnehotBytes + img_bytes + kMChunkBytes;  // (the padding: scan_segment's B prefetch)
         const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
         const bool staged = staged_bytes + static_lds <= kMStagedMax;
         const size_t lds = staged ? staged_bytes : base;

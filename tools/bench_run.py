@@ -43,7 +43,7 @@ def main():
     T = tfbs_pkg.load()
     work = tempfile.mkdtemp(prefix="tfbs_run_")
     t = time.perf_counter()
-    d = synth_dataset.make_dataset(work, a.samples, a.regions, a.pwms, a.length_config, a.seed)
+    d = synth_dataset.make_dataset(work, a.samples, a.regions, a.pwms, a.length_config, a.seed, keep_gt=False)
     t_gen = time.perf_counter() - t
     out = os.path.join(work, "out.vcf.gz")
     t = time.perf_counter()

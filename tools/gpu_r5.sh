@@ -51,6 +51,11 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
         done
       done
       unset TFBS_LIB ;;
+    run_*)  # run_<regions>[:<devices>]: tools/bench_run.py at 50 000 samples (BCF decode in the clock)
+      spec=${st#run_}; n=${spec%%:*}; dv=""; [ "$spec" != "$n" ] && dv="--devices ${spec#*:}"
+      tag=run_${n}${dv:+_$(echo ${spec#*:} | tr , _)}
+      timeout -k 10 900 python3 -u tools/bench_run.py --samples 50000 --regions $n $dv --oracle-seconds 0 > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }
+      grep tfbs_run_timing $O/$tag.err; python3 -c "import json;d=json.load(open('$O/$tag.json'));print('$tag', {k: d[k] for k in ('run_s','regions_per_s','bcf_decode_alone_s','dataset_gen_s','rows','records')})" ;;
     prof_*)
       w=${st#prof_}
       bash tools/profile_round.sh ${T}_prof_$w --workload $w || exit 1 ;;

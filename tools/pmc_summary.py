@@ -23,7 +23,7 @@ def last_phase(rows):
         names[int(r["Dispatch_Id"])] = r["Kernel_Name"]
     run, best = [], []
     for d in sorted(names):
-        if "scan_mfma_kernel" in names[d]:
+        if re.search(r"scan_mfma(_all)?_kernel", names[d]):
             run.append(d)
         else:
             if run:
@@ -57,7 +57,7 @@ def main():
             if d in take:
                 out[r["Counter_Name"]] = out.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         for d in sorted(take):
-            m = re.search(r"scan_mfma_kernel<[^>]*>", names[d])
+            m = re.search(r"scan_mfma(_all)?_kernel<[^>]*>", names[d])
             k = m.group(0) if m else names[d].split("(")[0][-60:]
             kern[k] = kern.get(k, 0) + 1
         out["_dispatches"] = len(take)

@@ -113,7 +113,50 @@ def bcf_record(chrom, pos0, ref, alt, gt_pairs):
     return struct.pack("<II", len(shared), len(indiv)) + shared + indiv
 
 
-def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0, index=True):
+class BgzfStream:
+    """BGZF framing written as the data comes (fixed BGZF_BLOCK-byte blocks, so a
+    record's uncompressed offset u lies in block u // BGZF_BLOCK, as csi_index assumes),
+    the blocks deflated on a thread pool (zlib drops the GIL); block_offsets receives
+    each block's compressed file offset."""
+
+    def __init__(self, f, level=6, threads=16):
+        import concurrent.futures as cf
+        self.f, self.level, self.pending, self.size = f, level, bytearray(), 0
+        self.block_offsets, self.pos = [], 0
+        self.ex = cf.ThreadPoolExecutor(threads)
+        self.threads = threads
+
+    def _blocks(self, chunks):
+        def one(chunk):
+            co = zlib.compressobj(self.level, zlib.DEFLATED, -15)
+            comp = co.compress(chunk) + co.flush()
+            return (struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, len(comp) + 25) + comp +
+                    struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk)))
+        for b in self.ex.map(one, chunks):
+            self.block_offsets.append(self.pos)
+            self.f.write(b)
+            self.pos += len(b)
+
+    def write(self, data):
+        self.pending += data
+        self.size += len(data)
+        n = len(self.pending) // BGZF_BLOCK
+        if n >= 4 * self.threads:
+            self._blocks([bytes(self.pending[i * BGZF_BLOCK:(i + 1) * BGZF_BLOCK]) for i in range(n)])
+            del self.pending[:n * BGZF_BLOCK]
+
+    def close(self):
+        n = (len(self.pending) + BGZF_BLOCK - 1) // BGZF_BLOCK
+        self._blocks([bytes(self.pending[i * BGZF_BLOCK:(i + 1) * BGZF_BLOCK]) for i in range(n)])
+        self.f.write(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+        self.ex.shutdown()
+
+
+def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0, index=True,
+                 keep_gt=True, level=6):
+    """keep_gt=False: the returned records carry no GT arrays (large runs: the BCF is
+    streamed out region by region, records of a region sorted; regions are 400 bp
+    apart and their extended windows do not overlap, so the file is sorted)."""
     import tfbs_pkg
     T = tfbs_pkg.load()
     os.makedirs(out, exist_ok=True)
@@ -125,22 +168,46 @@ def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, se
     regions, records = [], []
     chrom_len = 1000 + 400 * n_regions + 1000
     seq = bytearray(b"A" * chrom_len)
-    for j in range(n_regions):
-        r = T.SynthRegion(seed, j, n_samples, lmax, indel_pct)
-        s, e = r.merged
-        regions.append((s, e))
-        es = r.ext_start
-        seq[es:es + len(r.ref)] = r.ref.encode()
-        for pos, ref, alt, car in r.records:
-            gt = np.empty((n_samples, 2), dtype=np.int8)
-            gt[:, 0] = 2
-            gt[:, 1] = 3
-            car = np.asarray(car, dtype=np.int64)
-            car = car[car < H]
-            gt[car[car % 2 == 0] // 2, 0] = 4
-            gt[car[car % 2 == 1] // 2, 1] = 5
-            records.append({"chrom": "chr1", "pos0": pos, "rlen": len(ref), "alleles": [ref, alt], "gt": gt})
-    records.sort(key=lambda x: x["pos0"])
+    header = ("##fileformat=VCFv4.2\n##FILTER=<ID=PASS,Description=\"All filters passed\">\n"
+              "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+              "##contig=<ID=chr1,length=%d>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t%s\n"
+              % (chrom_len, "\t".join(samples))).encode() + b"\0"
+    bcf = os.path.join(out, "genotypes.bcf")
+    spans = []
+    last_pos = -1
+    with open(bcf, "wb") as f:
+        z = BgzfStream(f, level)
+        z.write(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+        for j in range(n_regions):
+            r = T.SynthRegion(seed, j, n_samples, lmax, indel_pct)
+            s, e = r.merged
+            regions.append((s, e))
+            es = r.ext_start
+            seq[es:es + len(r.ref)] = r.ref.encode()
+            recs = []
+            for pos, ref, alt, car in r.records:
+                gt = np.empty((n_samples, 2), dtype=np.int8)
+                gt[:, 0] = 2
+                gt[:, 1] = 3
+                car = np.asarray(car, dtype=np.int64)
+                car = car[car < H]
+                gt[car[car % 2 == 0] // 2, 0] = 4
+                gt[car[car % 2 == 1] // 2, 1] = 5
+                recs.append({"chrom": "chr1", "pos0": pos, "rlen": len(ref), "alleles": [ref, alt], "gt": gt})
+            recs.sort(key=lambda x: x["pos0"])
+            for rec in recs:
+                assert rec["pos0"] >= last_pos, "records out of order across regions"
+                last_pos = rec["pos0"]
+                u0 = z.size
+                z.write(bcf_record(0, rec["pos0"], rec["alleles"][0], rec["alleles"][1], rec["gt"]))
+                spans.append((rec["pos0"], rec["rlen"], u0, z.size))
+                if not keep_gt:
+                    rec = {k: v for k, v in rec.items() if k != "gt"}
+                records.append(rec)
+        z.close()
+    if index:
+        with open(bcf + ".csi", "wb") as f:
+            f.write(csi_index(spans, z.block_offsets, chrom_len))
     # FASTA + .fai
     fa = os.path.join(out, "genome.fa")
     with open(fa, "w") as f:
@@ -156,24 +223,6 @@ def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, se
             f.write("chr1\t%d\t%d\n" % (s, e))
     with open(os.path.join(out, "samples"), "w") as f:
         f.write("\n".join(samples) + "\n")
-    # BCF
-    header = ("##fileformat=VCFv4.2\n##FILTER=<ID=PASS,Description=\"All filters passed\">\n"
-              "##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
-              "##contig=<ID=chr1,length=%d>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t%s\n"
-              % (chrom_len, "\t".join(samples))).encode() + b"\0"
-    body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
-    spans = []
-    for rec in records:
-        u0 = len(body)
-        body += bcf_record(0, rec["pos0"], rec["alleles"][0], rec["alleles"][1], rec["gt"])
-        spans.append((rec["pos0"], rec["rlen"], u0, len(body)))
-    bcf = os.path.join(out, "genotypes.bcf")
-    offs = []
-    with open(bcf, "wb") as f:
-        f.write(bgzf_blocks(body, offs))
-    if index:
-        with open(bcf + ".csi", "wb") as f:
-            f.write(csi_index(spans, offs, chrom_len))
     return {"dir": out, "fasta": fa, "bed": bed, "bcf": bcf, "samples": samples, "names": names,
             "pwm_file": os.path.join(out, "pwms.txt"), "thr_dir": os.path.join(out, "thr"),
             "records": records, "regions": regions}

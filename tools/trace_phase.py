@@ -21,7 +21,7 @@ def main():
     rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Dispatch_Id"]))
     steps, cur = [], []
     for r in rows:
-        if "scan_mfma_kernel" in r["Kernel_Name"]:
+        if re.search(r"scan_mfma(_all)?_kernel", r["Kernel_Name"]):
             cur.append(r)
         elif cur:
             steps.append(cur)
@@ -36,8 +36,8 @@ def main():
         busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in st)
         out_steps.append({"dispatches": len(st), "phase_ms": (t1 - t0) / 1e6, "sum_of_kernel_ms": busy / 1e6})
         for r in st:
-            m = re.search(r"scan_mfma_kernel<(true|false), (\d+)>", r["Kernel_Name"])
-            key = "scan_mfma_kernel<%s, %s>" % (m.group(1), m.group(2)) if m else r["Kernel_Name"][:60]
+            m = re.search(r"scan_mfma(_all)?_kernel<[^>]*>", r["Kernel_Name"])
+            key = m.group(0) if m else r["Kernel_Name"][:60]
             per_kernel.setdefault(key, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
     timed = out_steps[1:] if len(out_steps) > 1 else out_steps  # the first step is the warmup
     out = {"source": sys.argv[1], "steps": out_steps,
