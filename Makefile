@@ -8,7 +8,7 @@ LIBDIR := $(PKG)/lib
 OBJDIR := $(PKG)/lib/obj
 JOBS ?= 8
 
-HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/plan.cpp $(SRC)/mfma.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/run.cpp
+HOST_SRCS := $(SRC)/patterns.cpp $(SRC)/plan.cpp $(SRC)/mfma.cpp $(SRC)/batch.cpp $(SRC)/aggregate.cpp $(SRC)/synth.cpp $(SRC)/io.cpp $(SRC)/inflate.cpp $(SRC)/run.cpp
 HIP_SRCS := $(SRC)/device.hip $(SRC)/scan_kernels.hip $(SRC)/scan_mfma.hip $(SRC)/key_kernels.hip $(SRC)/bgzf_gpu.hip $(SRC)/build_gpu.hip
 HDRS := $(wildcard $(SRC)/*.hpp) include/tfbs_amd.h
 HOST_OBJS := $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))

@@ -133,6 +133,7 @@ SIGNATURES = [
                                            C.c_size_t]),
     ("tfbs_run", C.c_int, [C.c_void_p]),
     ("tfbs_bcf_open", C.c_int, [C.c_char_p, C.POINTER(vp)]),
+    ("tfbs_inflate_raw", C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t]),
     ("tfbs_bcf_close", None, [vp]),
     ("tfbs_bcf_select", C.c_int, [vp, C.POINTER(C.c_size_t), C.c_size_t]),
     ("tfbs_bcf_num_samples", C.c_size_t, [vp]),

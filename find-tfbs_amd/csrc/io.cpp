@@ -18,6 +18,7 @@
 #include <map>
 #include <sstream>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <vector>
 
@@ -410,10 +411,15 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
 
 Bcf::~Bcf() {
     if (f) fclose(f);
+    if (getenv("TFBS_BCF_TIMING"))
+        fprintf(stderr, "tfbs_bcf_timing {\"read_s\": %.4f, \"inflate_s\": %.4f, \"erase_s\": %.4f, \"scan_s\": %.4f, "
+                        "\"decode_s\": %.4f, \"inflated_bytes\": %llu}\n",
+                t_read, t_inflate, t_erase, t_scan, t_decode, (unsigned long long)n_inflated);
 }
 
 int Bcf::open(const std::string &p, uint32_t nthreads) {
     path = p;
+    use_fast_inflate = !(getenv("TFBS_BCF_ZLIB") && atoi(getenv("TFBS_BCF_ZLIB")));
     threads = nthreads ? nthreads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     if (const char *e = getenv("TFBS_BCF_CHUNK_KB")) chunk = std::max<size_t>(1, (size_t)atoll(e)) << 10;
     int rc = rewind();
@@ -460,9 +466,19 @@ int Bcf::rewind() {
         std::string raw;
         int rc = read_file(path, raw);
         if (rc) return rc;
-        if ((rc = bgzf_inflate(raw, dbuf))) return rc;
+        std::string all;
+        if ((rc = bgzf_inflate(raw, all))) return rc;
+        dbuf.assign(all);
         in_eof = true;
     }
+    // the header in small reads (a full chunk inflates hundreds of MB of records
+    // that a fetch's seek would then inflate again)
+    const size_t big = chunk;
+    chunk = std::min<size_t>(big, 256u << 10);
+    struct Restore {
+        size_t &c, v;
+        ~Restore() { c = v; }
+    } restore{chunk, big};
     while (dbuf.size() < 9 && !in_eof)
         if (int rc = inflate_more()) return rc;
     if (dbuf.size() < 9 || memcmp(dbuf.data(), "BCF\2", 4) != 0) return fail(TFBS_E_PARSE, "not a BCF2 file: " + path);
@@ -570,16 +586,25 @@ int Bcf::seek(int contig, uint64_t voff) {
 
 // Read up to `chunk` compressed bytes, inflate every complete BGZF block in
 // parallel and append the output to dbuf.
+static double bcf_now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int Bcf::inflate_more() {
     if (in_eof) return TFBS_OK;
+    double t0 = bcf_now();
     if (doff) {
-        dbuf.erase(0, doff);
+        dbuf.erase_front(doff);
         doff = 0;
     }
+    double t1 = bcf_now();
+    t_erase += t1 - t0;
     const size_t have = cbuf.size();
     cbuf.resize(have + chunk);
     const size_t got = fread(&cbuf[have], 1, chunk, f);
     cbuf.resize(have + got);
+    t0 = bcf_now();
+    t_read += t0 - t1;
     const bool file_end = got < chunk;
     struct Blk {
         size_t off, len, out, isize;
@@ -610,11 +635,12 @@ int Bcf::inflate_more() {
         o += bsize;
     }
     if (file_end && o < cbuf.size() && blks.empty()) return fail(TFBS_E_PARSE, "truncated BGZF file " + path);
-    dbuf.resize(out);
+    dbuf.resize_uninit(out);
     std::vector<int> bad(blks.size(), 0);
     par_for(blks.size(), blks.size() >= 4 ? threads : 1, [&](size_t i) {
         const Blk &b = blks[i];
         if (!b.isize) return;
+        if (use_fast_inflate && inflate_raw_fast(c + b.off, b.len, (uint8_t *)&dbuf[b.out], b.isize) == 0) return;
         z_stream zs;
         memset(&zs, 0, sizeof zs);
         if (inflateInit2(&zs, -15) != Z_OK) {
@@ -629,6 +655,8 @@ int Bcf::inflate_more() {
         bad[i] = rc != Z_STREAM_END || zs.total_out != b.isize;
         inflateEnd(&zs);
     });
+    t_inflate += bcf_now() - t0;
+    for (const Blk &b : blks) n_inflated += b.isize;
     for (int x : bad)
         if (x) return fail(TFBS_E_IO, "corrupt BGZF data in " + path);
     cbuf.erase(0, o);
@@ -641,6 +669,7 @@ int Bcf::inflate_more() {
 // over (a later contig follows them) the stream is done.
 int Bcf::fill() {
     std::vector<size_t> offs;
+    const double ts = bcf_now();
     for (;;) {
         size_t o = doff;
         const unsigned char *d = (const unsigned char *)dbuf.data();
@@ -677,6 +706,8 @@ int Bcf::fill() {
         }
         if (int rc = inflate_more()) return rc;
     }
+    const double td = bcf_now();
+    t_scan += td - ts;
     const size_t base = win.size();
     win.resize(base + offs.size());
     std::vector<int> rcs(offs.size(), TFBS_OK);
@@ -687,6 +718,7 @@ int Bcf::fill() {
         int32_t chrom;
         rcs[i] = decode_bcf_record(p, end, samples.size(), gt_key, s, carriers_mode, win[base + i], chrom);
     });
+    t_decode += bcf_now() - td;
     for (size_t i = 0; i < rcs.size(); i++)
         if (rcs[i]) {  // decode again on this thread for the (thread-local) error message
             const unsigned char *p = (const unsigned char *)dbuf.data() + offs[i];

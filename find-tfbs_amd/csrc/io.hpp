@@ -4,6 +4,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -65,6 +67,46 @@ struct BcfRecord {
 // would rewind, or whose first record lies beyond what has been read, seeks
 // to the index's chunk start instead (IndexedReader::fetch's seek); the
 // sweep itself is unchanged.
+// Raw DEFLATE (RFC 1951) of in[0, in_len) into exactly out_len bytes (inflate.cpp);
+// 0 on success, nonzero when it cannot decode the stream exactly (the caller then
+// inflates with zlib).
+int inflate_raw_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_len);
+
+// A byte buffer that grows without zero-filling and drops consumed bytes from the
+// front by moving only what is left (the reader's inflated stream: hundreds of MB
+// per round, of which std::string's resize zero-filled and erase moved everything).
+class RawBuf {
+  public:
+    const char *data() const { return p.get(); }
+    char *data() { return p.get(); }
+    size_t size() const { return n; }
+    void clear() { n = 0; }
+    char &operator[](size_t i) { return p[i]; }
+    void resize_uninit(size_t m) {
+        if (m > cap) {
+            const size_t c = std::max(m, cap + cap / 2);
+            std::unique_ptr<char[]> q(new char[c]);
+            if (n) memcpy(q.get(), p.get(), n);
+            p = std::move(q);
+            cap = c;
+        }
+        n = m;
+    }
+    void erase_front(size_t k) {
+        k = std::min(k, n);
+        if (k < n) memmove(p.get(), p.get() + k, n - k);
+        n -= k;
+    }
+    void assign(const std::string &s) {
+        resize_uninit(s.size());
+        if (!s.empty()) memcpy(p.get(), s.data(), s.size());
+    }
+
+  private:
+    std::unique_ptr<char[]> p;
+    size_t n = 0, cap = 0;
+};
+
 class Bcf {
   public:
     int open(const std::string &path, uint32_t threads = 0);
@@ -97,8 +139,14 @@ class Bcf {
     FILE *f = nullptr;
     uint32_t threads = 1;
     size_t chunk = 8u << 20;            // compressed bytes read per inflate round
+    bool use_fast_inflate = true;       // inflate_raw_fast, zlib where it fails (TFBS_BCF_ZLIB=1: zlib only)
+    // TFBS_BCF_TIMING: seconds per phase (printed when the reader closes); scan_s
+    // includes the inflate rounds a fill needs
+    double t_read = 0, t_inflate = 0, t_erase = 0, t_scan = 0, t_decode = 0;
+    uint64_t n_inflated = 0;
     bool bgzf = true, in_eof = false, done = false, seen = false;
-    std::string cbuf, dbuf;             // compressed tail not yet inflated; inflated bytes from doff on
+    std::string cbuf;                   // compressed tail not yet inflated
+    RawBuf dbuf;                        // inflated bytes from doff on
     size_t doff = 0;
     int gt_key = -1;
     std::vector<size_t> sel;

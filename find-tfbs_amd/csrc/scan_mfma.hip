@@ -514,6 +514,68 @@ __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, con
 }
 
 
+#ifndef TFBS_PIPE
+#define TFBS_PIPE 1
+#endif
+// A tile's coarse test and, when it fires, its queue entries; the queue is
+// drained first when they may not fit (acc stays live across the drain).
+__device__ __forceinline__ void test_tile(const ScanArgs &A, const GroupCtx &G, const v16f &acc, uint32_t ti, uint32_t t,
+                                          uint32_t lane, uint32_t wave, uint32_t &qn, uint32_t &cn) {
+    const uint32_t x = coarse_test(acc);
+    const uint64_t f = __ballot(x != 0);
+    if (__builtin_expect(f != 0, 0)) {
+        if (qn + (uint32_t)__popcll(f) > kMQueue) {
+            drain_queue(A, G, qn, wave, lane, cn);
+            qn = 0;
+        }
+        queue_tile(acc, x, f, ti, t, lane, wave, qn);
+    }
+}
+
+// One window tile's chain of D MFMAs against a strand tile (B fragments f).
+template <int D, int NK>
+__device__ __forceinline__ v16f tile_chain(const v4i (&a)[NK], const BFrag (&f)[D], const v16f &cb, int sa) {
+    v16f c = mfma_chunk(a[0], f[0], cb, sa);
+#pragma unroll
+    for (int kc = 1; kc < D; kc++) c = mfma_chunk(a[kc], f[kc], c, sa);
+    return c;
+}
+
+// The software-pipelined form of scan_segment's two-tile rounds: per strand tile,
+// window tile ta's chain goes into X while the previous tile's window tile ta + 1
+// (Y, pending) is tested, then ta + 1's chain into Y while X is tested -- each
+// test's VALU work and its branch overlap the next chain's MFMAs instead of
+// waiting for the chain before them.  Y stays pending across segments (*pend:
+// the global tile of the pending Y; none at a pair's start) and is tested by the
+// caller at the pair's end.
+template <int D, int NK>
+__device__ __forceinline__ void scan_segment_pipe(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
+                                                  const GroupCtx &G, uint32_t lane, uint32_t wave,
+                                                  const v4i (&a0)[NK], const v4i (&a1)[NK], uint32_t ta,
+                                                  const v16f &cb, int sa, uint32_t &qn, uint32_t &cn, v16f &X,
+                                                  v16f &Y, bool &pend, uint32_t &pend_ti) {
+    constexpr uint32_t kTB = mfma_tile_bytes(D);
+    const char *tile = img;
+    BFrag pf;
+    load_frag0(img, lane, pf);
+    for (uint32_t ti = tb; ti < te; ti++, tile += kTB) {
+        BFrag f[D];
+        f[0] = pf;
+#pragma unroll
+        for (int kc = 1; kc < D; kc++) {
+            f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
+            f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
+        }
+        load_frag0(tile + kTB, lane, pf);  // (past the last tile: the padded image area, unused)
+        X = tile_chain<D, NK>(a0, f, cb, sa);
+        if (pend) test_tile(A, G, Y, pend_ti, ta + 1, lane, wave, qn, cn);
+        Y = tile_chain<D, NK>(a1, f, cb, sa);
+        test_tile(A, G, X, ti, ta, lane, wave, qn, cn);
+        pend = true;
+        pend_ti = ti;
+    }
+}
+
 // The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
 // ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
 template <int D, int NK>
@@ -591,6 +653,29 @@ __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, 
                                           bool two, uint32_t ta, const v16f &cb, int sa, uint32_t &qn, uint32_t &cn) {
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
+#if TFBS_PIPE
+    if (two) {
+        v16f X, Y;
+        bool pend = false;
+        uint32_t pend_ti = 0;
+#define TFBS_PSEGMENT(D)                                                                                         \
+        if (D <= NK && D + 1 >= NK) {                                                                            \
+            const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                 \
+            if (te > tb)                                                                                         \
+                scan_segment_pipe<(D <= NK ? D : 1), NK>(A, img, tb, te, G, lane, wave, a0, a1, ta, cb, sa, qn, cn, X, \
+                                                         Y, pend, pend_ti);                                        \
+            img += (te - tb) * mfma_tile_bytes(D);                                                               \
+            tb = te;                                                                                             \
+        }
+        TFBS_PSEGMENT(1)
+        TFBS_PSEGMENT(2)
+        TFBS_PSEGMENT(3)
+        TFBS_PSEGMENT(4)
+#undef TFBS_PSEGMENT
+        if (pend) test_tile(A, G, Y, pend_ti, ta + 1, lane, wave, qn, cn);
+        return;
+    }
+#endif
 #define TFBS_SEGMENT(D)                                                                                          \
     if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
         const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \

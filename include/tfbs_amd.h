@@ -430,6 +430,11 @@ int tfbs_bcf_record(const tfbs_bcf *b, size_t i, uint64_t *pos, uint32_t *rlen, 
  * selected sample), found on the reader's threads while decoding, instead of raw GT (tfbs_bcf_record
  * then returns gt NULL).  tfbs_run reads its BCF this way. */
 int tfbs_bcf_set_carriers_mode(tfbs_bcf *b, int on);
+/* The BCF reader's raw DEFLATE decoder (RFC 1951; BGZF blocks, htslib's bgzf.c
+ * reads them with zlib): in_len bytes into exactly out_len bytes.  TFBS_OK, or
+ * TFBS_E_PARSE for a stream it does not decode exactly (the reader then inflates
+ * that block with zlib).  Exported for its tests. */
+int tfbs_inflate_raw(const void *in, size_t in_len, void *out, size_t out_len);
 /* Record i of the last fetch in carriers mode: ascending carrier ids and the ploidy check
  * (TFBS_OK, or TFBS_E_PLOIDY when a selected sample's GT does not hold 2 alleles,
  * haplotype.rs:24-26); 0 ids for a record that is not bi-allelic. */

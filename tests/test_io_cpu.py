@@ -251,3 +251,57 @@ def test_bcf_carriers_mode_matches_raw_gt(tmp_path, sel):
                 n_bad += bad
                 n_car += len(ids)
     assert n_car > 50 and (n_bad > 0 or sel is not None)
+
+
+def test_inflate_raw_matches_zlib():
+    """tfbs_inflate_raw (the BCF reader's DEFLATE decoder, inflate.cpp) == zlib on raw
+    streams of every block type (stored, fixed, dynamic), every zlib level and strategy,
+    sizes around its copy steps, short periods (the GT columns' 2-byte runs) and random
+    bytes; truncated or corrupted streams fail or decode, never overrun."""
+    import ctypes as C
+    import random
+    import zlib
+
+    L = T.lib()
+
+    def fast(comp, n):
+        out = C.create_string_buffer(max(n, 1) + 16)
+        return L.tfbs_inflate_raw(comp, len(comp), out, n), out.raw[:n]
+
+    rnd = random.Random(7)
+    checked = 0
+    for trial in range(600):
+        kind = trial % 6
+        n = rnd.choice([0, 1, 2, 7, 8, 9, 15, 16, 17, 63, 64, 65, 1000, 4096, 20000, 65280])
+        if kind == 0:
+            data = bytes(rnd.randrange(256) for _ in range(n))
+        elif kind == 1:
+            data = bytes(rnd.choice(b"ACGT") for _ in range(n))
+        elif kind == 2:
+            data = (b"\x02\x03" * (n // 2 + 1))[:n]
+        elif kind == 3:
+            d = bytearray((b"\x02\x03" * (n // 2 + 1))[:n])
+            for _ in range(n // 50 + 1):
+                if n:
+                    d[rnd.randrange(n)] = rnd.choice([4, 5])
+            data = bytes(d)
+        elif kind == 4:
+            data = bytes(rnd.randrange(3) for _ in range(n))
+        else:
+            per = rnd.randint(1, 40)
+            pat = bytes(rnd.randrange(256) for _ in range(per))
+            data = (pat * (n // per + 1))[:n]
+        for level in (0, 1, 6, 9):
+            for strat in (zlib.Z_DEFAULT_STRATEGY, zlib.Z_FIXED, zlib.Z_HUFFMAN_ONLY, zlib.Z_RLE):
+                co = zlib.compressobj(level, zlib.DEFLATED, -15, 9, strat)
+                comp = co.compress(data) + co.flush()
+                rc, out = fast(comp, len(data))
+                assert rc == 0 and out == data, (trial, kind, n, level, strat)
+                checked += 1
+                if trial % 20 == 0 and len(comp) > 4:
+                    rc, out = fast(comp[:len(comp) // 2], len(data))
+                    assert rc != 0 or out == data
+                    bad = bytearray(comp)
+                    bad[len(bad) // 2] ^= 0x55
+                    fast(bytes(bad), len(data))
+    assert checked == 600 * 16

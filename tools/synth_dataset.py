@@ -179,6 +179,8 @@ def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, se
         z = BgzfStream(f, level)
         z.write(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
         for j in range(n_regions):
+            if j and j % 1000 == 0:  # progress for long runs (stderr)
+                print("synth_dataset: %d / %d regions" % (j, n_regions), file=sys.stderr, flush=True)
             r = T.SynthRegion(seed, j, n_samples, lmax, indel_pct)
             s, e = r.merged
             regions.append((s, e))
