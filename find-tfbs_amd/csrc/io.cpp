@@ -8,6 +8,7 @@
 // 0-based half-open [beg, end) the way htslib's region iterator does
 // (pos < end && pos + rlen > beg).  GT values are kept raw (BCF2 encoding
 // (allele + 1) << 1 | phased) with vector_end normalised to INT32_MIN + 1.
+#include <immintrin.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -306,16 +307,9 @@ static void gt8_carriers(const int8_t *g, size_t ns, const std::vector<size_t> *
     for (; j < 2 * ns; j += 2) one(j / 2, g[j], g[j + 1]);
 }
 
-static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, size_t ns, int gt_key,
-                             const std::vector<size_t> *sel, bool carriers, BcfRecord &r, int32_t &chrom) {
-    uint32_t l_shared, l_indiv;
-    memcpy(&l_shared, p, 4);
-    memcpy(&l_indiv, p + 4, 4);
-    p += 8;
-    if ((size_t)(end - p) < (size_t)l_shared + l_indiv) return fail(TFBS_E_PARSE, "truncated BCF record");
-    Cur sh{p, p + l_shared};
-    Cur in{p + l_shared, p + l_shared + l_indiv};
-    p += l_shared + l_indiv;
+// The shared part of a record (CHROM .. ALT; INFO is not read): position, rlen, REF,
+// ALT; n_allele and n_fmt for the per-sample part.
+static int decode_shared(Cur sh, BcfRecord &r, int32_t &chrom, uint32_t &n_allele, uint32_t &n_fmt) {
     int32_t pos, rlen;
     uint32_t nai, nfs;
     if (!sh.need(24)) return fail(TFBS_E_PARSE, "short BCF record");
@@ -327,8 +321,8 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
     sh.p += 24;
     r.pos = (uint64_t)(int64_t)pos;
     r.rlen = (uint32_t)std::max(rlen, 0);
-    const uint32_t n_allele = nai >> 16;
-    const uint32_t n_fmt = nfs >> 24;
+    n_allele = nai >> 16;
+    n_fmt = nfs >> 24;
     r.n_alleles = n_allele;
     r.ref.clear();
     r.alt.clear();
@@ -344,6 +338,44 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         if (a == 0) r.ref = al;
         else if (a == 1) r.alt = al;
     }
+    return TFBS_OK;
+}
+
+// Carriers mode: the carriers of a bi-allelic record's GT payload g (vt, vn as typed,
+// ns samples of the file), after r.gt_status was set from vn.
+static void gt_carriers(const unsigned char *g, int vt, uint32_t vn, size_t ns, const std::vector<size_t> *sel,
+                        BcfRecord &r) {
+    if (vt == 1 && vn == 2) {
+        gt8_carriers((const int8_t *)g, ns, sel, r.carriers, r.gt_status);
+        return;
+    }
+    if (vn < 2) return;
+    const size_t sz = type_size(vt), nk = sel ? sel->size() : ns;  // wider ints: the first two values of every sample
+    const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
+    for (size_t k = 0; k < nk; k++) {
+        const size_t s = sel ? (*sel)[k] : k;
+        Cur c{g + sz * vn * s, g + sz * vn * (s + 1)};
+        int64_t a = 0, b = 0;
+        read_int(c, vt, a);
+        read_int(c, vt, b);
+        if (a == ve || b == ve) r.gt_status = TFBS_E_PLOIDY;
+        if (a == 4) r.carriers.push_back((uint32_t)(2 * k));
+        if (b == 5) r.carriers.push_back((uint32_t)(2 * k + 1));
+    }
+}
+
+static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, size_t ns, int gt_key,
+                             const std::vector<size_t> *sel, bool carriers, BcfRecord &r, int32_t &chrom) {
+    uint32_t l_shared, l_indiv;
+    memcpy(&l_shared, p, 4);
+    memcpy(&l_indiv, p + 4, 4);
+    p += 8;
+    if ((size_t)(end - p) < (size_t)l_shared + l_indiv) return fail(TFBS_E_PARSE, "truncated BCF record");
+    Cur sh{p, p + l_shared};
+    Cur in{p + l_shared, p + l_shared + l_indiv};
+    p += l_shared + l_indiv;
+    uint32_t n_allele, n_fmt;
+    if (int rc = decode_shared(sh, r, chrom, n_allele, n_fmt)) return rc;
     const size_t nk = sel ? sel->size() : ns;
     r.carriers.clear();
     r.gt_status = TFBS_OK;
@@ -366,21 +398,7 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
         if (carriers) {
             if (key == gt_key && n_allele == 2 && nk && vt >= 1 && vt <= 3) {
                 r.gt_status = vn >= 2 ? TFBS_OK : TFBS_E_PLOIDY;  // one value per sample: glen 1
-                if (vt == 1 && vn == 2) {
-                    gt8_carriers((const int8_t *)in.p, ns, sel, r.carriers, r.gt_status);
-                } else if (vn >= 2) {  // wider ints: the first two values of every sample
-                    const int64_t ve = vt == 1 ? -127 : vt == 2 ? -32767 : (int64_t)INT32_MIN + 1;
-                    for (size_t k = 0; k < nk; k++) {
-                        const size_t s = sel ? (*sel)[k] : k;
-                        Cur c{in.p + sz * vn * s, in.p + sz * vn * (s + 1)};
-                        int64_t a = 0, b = 0;
-                        read_int(c, vt, a);
-                        read_int(c, vt, b);
-                        if (a == ve || b == ve) r.gt_status = TFBS_E_PLOIDY;
-                        if (a == 4) r.carriers.push_back((uint32_t)(2 * k));
-                        if (b == 5) r.carriers.push_back((uint32_t)(2 * k + 1));
-                    }
-                }
+                gt_carriers(in.p, vt, vn, ns, sel, r);
             }
         } else if (key == gt_key && vt == 1 && vn == 2) {  // the common diploid int8 layout
             const int8_t *g = (const int8_t *)in.p;
@@ -421,7 +439,9 @@ int Bcf::open(const std::string &p, uint32_t nthreads) {
     path = p;
     use_fast_inflate = !(getenv("TFBS_BCF_ZLIB") && atoi(getenv("TFBS_BCF_ZLIB")));
     threads = nthreads ? nthreads : std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (const char *e = getenv("TFBS_BCF_THREADS")) threads = std::max(1, atoi(e));
     if (const char *e = getenv("TFBS_BCF_CHUNK_KB")) chunk = std::max<size_t>(1, (size_t)atoll(e)) << 10;
+    condense = !(getenv("TFBS_BCF_CONDENSED") && atoi(getenv("TFBS_BCF_CONDENSED")) == 0);
     int rc = rewind();
     if (rc) return rc;
     if ((rc = load_csi())) return rc;
@@ -456,6 +476,8 @@ int Bcf::rewind() {
     dbuf.clear();
     doff = 0;
     in_eof = done = seen = false;
+    cmode = false;
+    cblk.clear();
     win.clear();
     last_beg = last_pos = 0;
     unsigned char m[4] = {0, 0, 0, 0};
@@ -573,10 +595,19 @@ int Bcf::seek(int contig, uint64_t voff) {
     dbuf.clear();
     doff = 0;
     in_eof = done = seen = false;
+    cmode = false;
+    cblk.clear();
     win.clear();
     last_pos = 0;
     cur = contig;
     const size_t u = (size_t)(voff & 0xFFFF);
+    // the condensed stream takes over after the block at voff: read it in a small round
+    const size_t big = chunk;
+    if (condensed()) chunk = std::min<size_t>(big, 256u << 10);
+    struct Restore {
+        size_t &c, v;
+        ~Restore() { c = v; }
+    } restore{chunk, big};
     while (dbuf.size() < u && !in_eof)
         if (int rc = inflate_more()) return rc;
     if (dbuf.size() < u) return fail(TFBS_E_PARSE, "CSI offset past the end of " + path);
@@ -588,6 +619,55 @@ int Bcf::seek(int contig, uint64_t voff) {
 // parallel and append the output to dbuf.
 static double bcf_now() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// The complete BGZF blocks at the start of c: their deflate data and inflated sizes
+// (out: offset of a block's bytes after the blocks before it); used = bytes they take.
+struct BgzfSpan {
+    size_t off, len, out, isize;
+};
+static int bgzf_spans(const std::string &cb, const std::string &path, std::vector<BgzfSpan> &blks, size_t &used) {
+    size_t o = 0, out = 0;
+    const unsigned char *c = (const unsigned char *)cb.data();
+    while (o + 18 <= cb.size()) {
+        if (c[o] != 0x1f || c[o + 1] != 0x8b || c[o + 2] != 8 || !(c[o + 3] & 4))
+            return fail(TFBS_E_PARSE, "corrupt BGZF block header in " + path);
+        const size_t xlen = c[o + 10] | (c[o + 11] << 8);
+        size_t bsize = 0;
+        for (size_t x = o + 12; x + 4 <= o + 12 + xlen && x + 4 <= cb.size();) {
+            const size_t slen = c[x + 2] | (c[x + 3] << 8);
+            if (c[x] == 'B' && c[x + 1] == 'C' && slen == 2 && x + 6 <= cb.size()) bsize = (c[x + 4] | (c[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (!bsize) {
+            if (o + 12 + xlen <= cb.size()) return fail(TFBS_E_PARSE, "BGZF block without BSIZE in " + path);
+            break;
+        }
+        if (o + bsize > cb.size()) break;
+        if (bsize < 12 + xlen + 8) return fail(TFBS_E_PARSE, "corrupt BGZF block size in " + path);
+        uint32_t isize;
+        memcpy(&isize, c + o + bsize - 4, 4);
+        blks.push_back({o + 12 + xlen, bsize - 12 - xlen - 8, out, isize});
+        out += isize;
+        o += bsize;
+    }
+    used = o;
+    return TFBS_OK;
+}
+
+// zlib's raw inflate of exactly isize bytes (where inflate_raw_fast declines)
+static bool inflate_zlib(const unsigned char *in, size_t len, uint8_t *out, size_t isize) {
+    z_stream zs;
+    memset(&zs, 0, sizeof zs);
+    if (inflateInit2(&zs, -15) != Z_OK) return false;
+    zs.next_in = (Bytef *)in;
+    zs.avail_in = (uInt)len;
+    zs.next_out = (Bytef *)out;
+    zs.avail_out = (uInt)isize;
+    const int rc = inflate(&zs, Z_FINISH);
+    const bool ok = rc == Z_STREAM_END && zs.total_out == isize;
+    inflateEnd(&zs);
+    return ok;
 }
 
 int Bcf::inflate_more() {
@@ -606,57 +686,23 @@ int Bcf::inflate_more() {
     t0 = bcf_now();
     t_read += t0 - t1;
     const bool file_end = got < chunk;
-    struct Blk {
-        size_t off, len, out, isize;
-    };
-    std::vector<Blk> blks;
-    size_t o = 0, out = dbuf.size();
-    const unsigned char *c = (const unsigned char *)cbuf.data();
-    while (o + 18 <= cbuf.size()) {
-        if (c[o] != 0x1f || c[o + 1] != 0x8b || c[o + 2] != 8 || !(c[o + 3] & 4))
-            return fail(TFBS_E_PARSE, "corrupt BGZF block header in " + path);
-        const size_t xlen = c[o + 10] | (c[o + 11] << 8);
-        size_t bsize = 0;
-        for (size_t x = o + 12; x + 4 <= o + 12 + xlen && x + 4 <= cbuf.size();) {
-            const size_t slen = c[x + 2] | (c[x + 3] << 8);
-            if (c[x] == 'B' && c[x + 1] == 'C' && slen == 2 && x + 6 <= cbuf.size()) bsize = (c[x + 4] | (c[x + 5] << 8)) + 1;
-            x += 4 + slen;
-        }
-        if (!bsize) {
-            if (o + 12 + xlen <= cbuf.size()) return fail(TFBS_E_PARSE, "BGZF block without BSIZE in " + path);
-            break;
-        }
-        if (o + bsize > cbuf.size()) break;
-        if (bsize < 12 + xlen + 8) return fail(TFBS_E_PARSE, "corrupt BGZF block size in " + path);
-        uint32_t isize;
-        memcpy(&isize, c + o + bsize - 4, 4);
-        blks.push_back({o + 12 + xlen, bsize - 12 - xlen - 8, out, isize});
-        out += isize;
-        o += bsize;
-    }
+    std::vector<BgzfSpan> blks;
+    size_t o = 0;
+    if (int rc = bgzf_spans(cbuf, path, blks, o)) return rc;
     if (file_end && o < cbuf.size() && blks.empty()) return fail(TFBS_E_PARSE, "truncated BGZF file " + path);
-    dbuf.resize_uninit(out);
+    const size_t out0 = dbuf.size();
+    dbuf.resize_uninit(out0 + (blks.empty() ? 0 : blks.back().out + blks.back().isize));
+    const unsigned char *c = (const unsigned char *)cbuf.data();
     std::vector<int> bad(blks.size(), 0);
     par_for(blks.size(), blks.size() >= 4 ? threads : 1, [&](size_t i) {
-        const Blk &b = blks[i];
+        const BgzfSpan &b = blks[i];
         if (!b.isize) return;
-        if (use_fast_inflate && inflate_raw_fast(c + b.off, b.len, (uint8_t *)&dbuf[b.out], b.isize) == 0) return;
-        z_stream zs;
-        memset(&zs, 0, sizeof zs);
-        if (inflateInit2(&zs, -15) != Z_OK) {
-            bad[i] = 1;
-            return;
-        }
-        zs.next_in = (Bytef *)(c + b.off);
-        zs.avail_in = (uInt)b.len;
-        zs.next_out = (Bytef *)&dbuf[b.out];
-        zs.avail_out = (uInt)b.isize;
-        const int rc = inflate(&zs, Z_FINISH);
-        bad[i] = rc != Z_STREAM_END || zs.total_out != b.isize;
-        inflateEnd(&zs);
+        uint8_t *dst = (uint8_t *)&dbuf[out0 + b.out];
+        if (use_fast_inflate && inflate_raw_fast(c + b.off, b.len, dst, b.isize) == 0) return;
+        bad[i] = !inflate_zlib(c + b.off, b.len, dst, b.isize);
     });
     t_inflate += bcf_now() - t0;
-    for (const Blk &b : blks) n_inflated += b.isize;
+    for (const BgzfSpan &b : blks) n_inflated += b.isize;
     for (int x : bad)
         if (x) return fail(TFBS_E_IO, "corrupt BGZF data in " + path);
     cbuf.erase(0, o);
@@ -729,6 +775,346 @@ int Bcf::fill() {
     return TFBS_OK;
 }
 
+// ---------------------------------------------------------------------------
+// The condensed stream (carriers mode): CBlock per inflated BGZF block.
+uint8_t CBlock::at(uint32_t off) const {
+    if (!raw.empty()) return raw[off];
+    auto it = std::lower_bound(ex.begin(), ex.end(), off << 8);
+    if (it != ex.end() && (*it >> 8) == off) return (uint8_t)*it;
+    const uint8_t c = bg[off >> 6];
+    return c < 2 ? (uint8_t)(2 + ((off ^ c) & 1)) : c;
+}
+
+void CBlock::read(uint32_t off, uint32_t m, uint8_t *dst) const {
+    if (!raw.empty()) {
+        memcpy(dst, raw.data() + off, m);
+        return;
+    }
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t q = off + i;
+        const uint8_t c = bg[q >> 6];
+        dst[i] = c < 2 ? (uint8_t)(2 + ((q ^ c) & 1)) : c;
+    }
+    for (auto it = std::lower_bound(ex.begin(), ex.end(), off << 8); it != ex.end() && (*it >> 8) < off + m; ++it)
+        dst[(*it >> 8) - off] = (uint8_t)*it;
+}
+
+// Per 64-byte line of d (full lines only): the bytes that match the alternating
+// backgrounds -- code 0: 2 at even offsets, 3 at odd ones; code 1: the other way
+// round -- as bit masks m[2 l], m[2 l + 1].
+__attribute__((target("avx2"))) static inline void line_masks_avx2(const uint8_t *d, uint32_t nl, uint64_t *m) {
+    const __m256i p0 = _mm256_set1_epi16(0x0302), p1 = _mm256_set1_epi16(0x0203);
+    for (uint32_t l = 0; l < nl; l++) {
+        const __m256i a = _mm256_loadu_si256((const __m256i *)(d + 64ull * l)),
+                      b = _mm256_loadu_si256((const __m256i *)(d + 64ull * l + 32));
+        m[2 * l] = (uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, p0)) |
+                   ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, p0)) << 32);
+        m[2 * l + 1] = (uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(a, p1)) |
+                       ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(b, p1)) << 32);
+    }
+}
+static inline void line_masks_sse2(const uint8_t *d, uint32_t nl, uint64_t *m) {
+    const __m128i p0 = _mm_set1_epi16(0x0302), p1 = _mm_set1_epi16(0x0203);
+    for (uint32_t l = 0; l < nl; l++) {
+        uint64_t r0 = 0, r1 = 0;
+        for (int k = 0; k < 4; k++) {
+            const __m128i x = _mm_loadu_si128((const __m128i *)(d + 64ull * l + 16 * k));
+            r0 |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, p0)) << (16 * k);
+            r1 |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(x, p1)) << (16 * k);
+        }
+        m[2 * l] = r0;
+        m[2 * l + 1] = r1;
+    }
+}
+
+// Condense n inflated bytes d into b: per line the background code with the most
+// matching bytes (a line that matches an alternating one whole is decided by the
+// masks alone), then the other bytes as exceptions; ex, mk: the thread's scratch.
+// (Compiled twice: with AVX2 + POPCNT where the CPU has them, and plain x86-64.)
+template <bool kAvx2>
+static inline __attribute__((always_inline)) void condense_body(const uint8_t *d, uint32_t n, CBlock &b,
+                                                                std::vector<uint32_t> &ex, std::vector<uint64_t> &mk) {
+    b.n = n;
+    b.raw.clear();
+    const uint32_t nl = (n + 63) / 64, nfull = n / 64, lim = n / 16;
+    b.bg.resize(nl);
+    if (mk.size() < 2ull * nl) mk.resize(2ull * nl);
+    if (ex.size() < (size_t)lim + 64) ex.resize((size_t)lim + 64);
+    if (kAvx2) line_masks_avx2(d, nfull, mk.data());
+    else line_masks_sse2(d, nfull, mk.data());
+    uint8_t *bg = b.bg.data();
+    uint32_t *e = ex.data(), *const e_lim = ex.data() + lim;
+    for (uint32_t l = 0; l < nl; l++) {
+        const uint8_t *p = d + 64ull * l;
+        const uint32_t m = std::min<uint32_t>(64, n - 64 * l);
+        const uint64_t valid = m == 64 ? ~0ull : (1ull << m) - 1;
+        uint64_t ok[4];
+        if (l < nfull) {
+            ok[0] = mk[2 * l];
+            ok[1] = mk[2 * l + 1];
+            if (ok[0] == ~0ull || ok[1] == ~0ull) {
+                bg[l] = ok[0] == ~0ull ? 0 : 1;
+                continue;
+            }
+        } else {
+            ok[0] = ok[1] = 0;
+            for (uint32_t i = 0; i < m; i++) {
+                ok[0] |= (uint64_t)(p[i] == 2 + (i & 1)) << i;
+                ok[1] |= (uint64_t)(p[i] == 3 - (i & 1)) << i;
+            }
+        }
+        // the constant backgrounds from the alternating masks: a byte equal to 2 at an
+        // even offset matches code 0 there, at an odd offset code 1
+        const uint64_t even = 0x5555555555555555ull;
+        ok[2] = (ok[0] & even) | (ok[1] & ~even);
+        ok[3] = (ok[1] & even) | (ok[0] & ~even);
+        int best = 0, bc = __builtin_popcountll(ok[0] & valid);
+        for (int c = 1; c < 4; c++) {
+            const int k = __builtin_popcountll(ok[c] & valid);
+            if (k > bc) bc = k, best = c;
+        }
+        bg[l] = (uint8_t)best;
+        for (uint64_t miss = valid & ~ok[best]; miss; miss &= miss - 1) {
+            const uint32_t i = (uint32_t)__builtin_ctzll(miss);
+            *e++ = ((64 * l + i) << 8) | p[i];
+        }
+        if (e > e_lim) {  // not GT-like: keep the bytes
+            b.raw.assign(d, d + n);
+            b.bg.clear();
+            b.bg.shrink_to_fit();
+            b.ex.clear();
+            return;
+        }
+    }
+    b.ex.assign(ex.data(), e);
+}
+__attribute__((target("avx2,popcnt,bmi"))) static void condense_avx2(const uint8_t *d, uint32_t n, CBlock &b,
+                                                                     std::vector<uint32_t> &ex,
+                                                                     std::vector<uint64_t> &mk) {
+    condense_body<true>(d, n, b, ex, mk);
+}
+static void condense_block(const uint8_t *d, uint32_t n, CBlock &b, std::vector<uint32_t> &ex,
+                           std::vector<uint64_t> &mk) {
+    static const bool avx2 = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("popcnt");
+    if (avx2) condense_avx2(d, n, b, ex, mk);
+    else condense_body<false>(d, n, b, ex, mk);
+}
+
+size_t Bcf::sblock(uint64_t o) const {
+    size_t lo = 0, hi = cblk.size();  // the last block with a0 <= o
+    while (hi - lo > 1) {
+        const size_t mid = (lo + hi) / 2;
+        if (cblk[mid].a0 <= o) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+void Bcf::sread(uint64_t o, size_t n, uint8_t *dst) const {
+    for (size_t bi = sblock(o); n; bi++) {
+        const CBlock &b = cblk[bi];
+        const uint32_t off = (uint32_t)(o - b.a0), m = (uint32_t)std::min<uint64_t>(n, b.n - off);
+        b.read(off, m, dst);
+        dst += m;
+        o += m;
+        n -= m;
+    }
+}
+
+// Read a chunk of compressed bytes, inflate its complete BGZF blocks on the reader's
+// threads, each into a thread-local buffer that is condensed at once, and append them.
+int Bcf::inflate_condensed() {
+    if (in_eof) return TFBS_OK;
+    double t0 = bcf_now();
+    size_t k = 0;  // the blocks wholly before the next record are done with
+    while (k < cblk.size() && cblk[k].a0 + cblk[k].n <= spos) k++;
+    if (k) cblk.erase(cblk.begin(), cblk.begin() + (long)k);
+    const size_t have = cbuf.size();
+    cbuf.resize(have + chunk);
+    const size_t got = fread(&cbuf[have], 1, chunk, f);
+    cbuf.resize(have + got);
+    double t1 = bcf_now();
+    t_read += t1 - t0;
+    const bool file_end = got < chunk;
+    std::vector<BgzfSpan> blks;
+    size_t used = 0;
+    if (int rc = bgzf_spans(cbuf, path, blks, used)) return rc;
+    if (file_end && used < cbuf.size() && blks.empty()) return fail(TFBS_E_PARSE, "truncated BGZF file " + path);
+    std::vector<size_t> nz;  // (empty blocks -- the EOF marker -- add nothing)
+    for (size_t i = 0; i < blks.size(); i++)
+        if (blks[i].isize) nz.push_back(i);
+    const size_t base = cblk.size();
+    cblk.resize(base + nz.size());
+    for (size_t j = 0; j < nz.size(); j++) {
+        cblk[base + j].a0 = send;
+        send += blks[nz[j]].isize;
+        n_inflated += blks[nz[j]].isize;
+    }
+    std::vector<int> bad(nz.size(), 0);
+    const unsigned char *c = (const unsigned char *)cbuf.data();
+    par_for(nz.size(), nz.size() >= 4 ? threads : 1, [&](size_t j) {
+        thread_local std::vector<uint8_t> buf;
+        thread_local std::vector<uint32_t> ex;
+        thread_local std::vector<uint64_t> mk;
+        const BgzfSpan &s = blks[nz[j]];
+        if (buf.size() < s.isize) buf.resize(s.isize);
+        if (!(use_fast_inflate && inflate_raw_fast(c + s.off, s.len, buf.data(), s.isize) == 0) &&
+            !inflate_zlib(c + s.off, s.len, buf.data(), s.isize)) {
+            bad[j] = 1;
+            return;
+        }
+        condense_block(buf.data(), (uint32_t)s.isize, cblk[base + j], ex, mk);
+    });
+    t_inflate += bcf_now() - t1;
+    for (int x : bad)
+        if (x) return fail(TFBS_E_IO, "corrupt BGZF data in " + path);
+    cbuf.erase(0, used);
+    if (file_end && cbuf.empty()) in_eof = true;
+    return TFBS_OK;
+}
+
+// fill() over the condensed stream.  The bytes already inflated (the header round,
+// a seek) start it as one kept block.
+int Bcf::fill_condensed() {
+    if (!cmode) {
+        cblk.clear();
+        spos = send = 0;
+        if (dbuf.size() > doff) {
+            CBlock b;
+            b.n = (uint32_t)(dbuf.size() - doff);
+            b.raw.assign(dbuf.data() + doff, dbuf.data() + dbuf.size());
+            send = b.n;
+            cblk.push_back(std::move(b));
+        }
+        dbuf.clear();
+        doff = 0;
+        cmode = true;
+    }
+    std::vector<uint64_t> offs;
+    const double ts = bcf_now();
+    for (;;) {
+        uint64_t o = spos;
+        while (o + 8 <= send) {
+            uint8_t h[16];
+            sread(o, 8, h);
+            uint32_t ls, li;
+            memcpy(&ls, h, 4);
+            memcpy(&li, h + 4, 4);
+            const uint64_t n = 8 + (uint64_t)ls + li;
+            if (o + n > send) break;
+            if (ls < 24) return fail(TFBS_E_PARSE, "short BCF record");
+            sread(o + 8, 8, h + 8);
+            int32_t chrom, pos;
+            memcpy(&chrom, h + 8, 4);
+            memcpy(&pos, h + 12, 4);
+            if (chrom < 0 || (size_t)chrom >= contigs.size()) return fail(TFBS_E_PARSE, "BCF record with unknown contig");
+            if (chrom == cur) {
+                const uint64_t p = (uint64_t)(int64_t)pos;
+                if (seen && p < last_pos)
+                    return fail(TFBS_E_PARSE, "BCF records are not sorted by position (an indexed BCF is): " + path);
+                seen = true;
+                last_pos = p;
+                offs.push_back(o);
+            } else if (seen) {
+                done = true;
+                break;
+            }
+            o += n;
+        }
+        spos = o;
+        if (done || !offs.empty()) break;
+        if (in_eof) {
+            if (spos + 8 <= send) return fail(TFBS_E_PARSE, "truncated BCF record");
+            done = true;
+            break;
+        }
+        if (int rc = inflate_condensed()) return rc;
+    }
+    const double td = bcf_now();
+    t_scan += td - ts;
+    const size_t base = win.size();
+    win.resize(base + offs.size());
+    std::vector<int> rcs(offs.size(), TFBS_OK);
+    par_for(offs.size(), offs.size() >= 64 ? threads : 1,
+            [&](size_t i) { rcs[i] = decode_condensed(offs[i], win[base + i]); });
+    t_decode += bcf_now() - td;
+    for (size_t i = 0; i < rcs.size(); i++)
+        if (rcs[i]) {
+            BcfRecord r;  // again on this thread for the (thread-local) error message
+            return decode_condensed(offs[i], r);
+        }
+    return TFBS_OK;
+}
+
+// decode_bcf_record in carriers mode over the condensed stream: the shared part and
+// the FORMAT descriptors are read back; an int8 diploid GT payload of all samples is
+// not: its carriers are the differing bytes of its blocks (a background byte, 2 or
+// 3, is allele 0 in either slot), or a kept block's bytes.
+int Bcf::decode_condensed(uint64_t o, BcfRecord &r) const {
+    uint8_t h[8];
+    sread(o, 8, h);
+    uint32_t ls, li;
+    memcpy(&ls, h, 4);
+    memcpy(&li, h + 4, 4);
+    thread_local std::vector<uint8_t> sh, gbuf;
+    sh.resize(ls);
+    sread(o + 8, ls, sh.data());
+    int32_t chrom;
+    uint32_t n_allele, n_fmt;
+    if (int rc = decode_shared(Cur{sh.data(), sh.data() + ls}, r, chrom, n_allele, n_fmt)) return rc;
+    const std::vector<size_t> *sel_p = all_samples ? nullptr : &sel;
+    const size_t ns = samples.size(), nk = sel_p ? sel_p->size() : ns;
+    r.carriers.clear();
+    r.gt.clear();
+    r.gt_status = (n_allele == 2 && nk) ? TFBS_E_PLOIDY : TFBS_OK;  // (no GT field: every GT is empty)
+    uint64_t ip = o + 8 + ls;
+    const uint64_t ie = ip + li;
+    for (uint32_t f = 0; f < n_fmt; f++) {
+        uint8_t tb[24];
+        const size_t m = (size_t)std::min<uint64_t>(sizeof tb, ie - ip);
+        sread(ip, m, tb);
+        Cur in{tb, tb + m};
+        int kt, vt;
+        uint32_t kn, vn;
+        int64_t key;
+        if (!typed(in, kt, kn) || kn != 1 || !read_int(in, kt, key)) return fail(TFBS_E_PARSE, "bad FORMAT key");
+        if (!typed(in, vt, vn)) return fail(TFBS_E_PARSE, "bad FORMAT type");
+        ip += (uint64_t)(in.p - tb);
+        const uint64_t payload = (uint64_t)type_size(vt) * vn * ns;
+        if (ie - ip < payload) return fail(TFBS_E_PARSE, "truncated FORMAT data");
+        if (key == gt_key && n_allele == 2 && nk && vt >= 1 && vt <= 3) {
+            r.gt_status = vn >= 2 ? TFBS_OK : TFBS_E_PLOIDY;  // one value per sample: glen 1
+            if (vt == 1 && vn == 2 && !sel_p) {
+                const uint64_t g0 = ip, g1 = ip + payload;
+                for (size_t bi = sblock(g0); bi < cblk.size() && cblk[bi].a0 < g1; bi++) {
+                    const CBlock &b = cblk[bi];
+                    const uint32_t lo = (uint32_t)(std::max(g0, b.a0) - b.a0),
+                                   hi = (uint32_t)(std::min<uint64_t>(g1, b.a0 + b.n) - b.a0);
+                    auto one = [&](uint32_t off, int8_t v) {
+                        const uint64_t q = b.a0 + off - g0;
+                        if (v == -127) r.gt_status = TFBS_E_PLOIDY;
+                        if (v == (q & 1 ? 5 : 4)) r.carriers.push_back((uint32_t)q);  // 2 k + slot
+                    };
+                    if (!b.raw.empty()) {
+                        for (uint32_t off = lo; off < hi; off++)
+                            if ((b.raw[off] & 0xFE) != 2) one(off, (int8_t)b.raw[off]);
+                    } else {
+                        for (auto it = std::lower_bound(b.ex.begin(), b.ex.end(), lo << 8);
+                             it != b.ex.end() && (*it >> 8) < hi; ++it)
+                            one(*it >> 8, (int8_t)(uint8_t)*it);
+                    }
+                }
+            } else if (vn >= 2) {
+                gbuf.resize(payload);
+                sread(ip, payload, gbuf.data());
+                gt_carriers(gbuf.data(), vt, vn, ns, sel_p, r);
+            }
+        }
+        ip += payload;
+    }
+    return TFBS_OK;
+}
+
 int Bcf::contig_index(const std::string &name) const {
     for (size_t i = 0; i < contigs.size(); i++)
         if (contigs[i] == name) return (int)i;
@@ -767,7 +1153,7 @@ int Bcf::fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfReco
         win.erase(std::remove_if(win.begin(), win.end(), [&](const BcfRecord &r) { return r.pos + r.rlen <= beg; }),
                   win.end());
     while (!done && (win.empty() || win.back().pos < end))
-        if (int rc = fill()) return rc;
+        if (int rc = condensed() ? fill_condensed() : fill()) return rc;
     for (const BcfRecord &r : win) {
         if (r.pos >= end) break;
         if (r.pos + r.rlen > beg) out.push_back(&r);

@@ -107,6 +107,22 @@ class RawBuf {
     size_t n = 0, cap = 0;
 };
 
+// One inflated BGZF block of a carriers-mode stream, condensed (Bcf::fill_condensed):
+// GT columns are nearly all 0|0 -- bytes 2 and 3 -- so a block is kept as a background
+// code per 64-byte line (0: 2 at even offsets and 3 at odd ones, 1: the other way
+// round, 2: all 2, 3: all 3) and the bytes that differ from it, (offset << 8 | byte)
+// ascending; a block with more than 1/16 of its bytes differing keeps its bytes
+// (`raw`).  Exact: every byte can be read back.
+struct CBlock {
+    uint64_t a0 = 0;              // offset of its first byte in the condensed stream
+    uint32_t n = 0;               // its bytes (> 0)
+    std::vector<uint8_t> raw;     // dense block; empty when condensed
+    std::vector<uint8_t> bg;      // per 64-byte line: its background code
+    std::vector<uint32_t> ex;     // the bytes that differ from the background
+    uint8_t at(uint32_t off) const;
+    void read(uint32_t off, uint32_t n, uint8_t *dst) const;
+};
+
 class Bcf {
   public:
     int open(const std::string &path, uint32_t threads = 0);
@@ -127,6 +143,15 @@ class Bcf {
     int rewind();
     int inflate_more();
     int fill();
+    // carriers mode over the condensed stream: BGZF blocks inflated and condensed on
+    // the reader's threads (CBlock: the inflated bytes never reach memory in full),
+    // record boundaries found serially, records decoded in parallel
+    int fill_condensed();
+    bool condensed() const { return carriers_mode && condense && bgzf; }
+    int inflate_condensed();
+    void sread(uint64_t o, size_t n, uint8_t *dst) const;  // bytes [o, o + n) of the condensed stream
+    size_t sblock(uint64_t o) const;                       // the block holding byte o
+    int decode_condensed(uint64_t o, BcfRecord &r) const;
     int load_csi();
     // virtual offset to start reading for records with pos + rlen > beg on
     // `contig` (the smallest chunk start of the CSI bins ending after beg);
@@ -152,6 +177,10 @@ class Bcf {
     std::vector<size_t> sel;
     bool all_samples = true;
     bool carriers_mode = false;
+    bool condense = true;               // carriers mode reads the condensed stream (TFBS_BCF_CONDENSED=0: off)
+    bool cmode = false;                 // the stream is condensed from spos on (reset by rewind / seek)
+    std::vector<CBlock> cblk;           // condensed blocks, in stream order (consumed ones dropped)
+    uint64_t spos = 0, send = 0;        // next record / end of the condensed stream
     int cur = -1;                       // contig of the window
     uint64_t last_beg = 0, last_pos = 0;
     std::vector<BcfRecord> win;         // window of decoded records of contig `cur`, file order

@@ -271,6 +271,10 @@ struct Ordered {
         std::string bodies;    // row bodies (host rows)
     };
     std::vector<Item> items;
+    size_t written = 0;  // batches the writer has written out
+    // at most kAhead batches past the one being written hold their blocks (memory
+    // files of hundreds of MB at 50 000 samples): a shard waits before making more
+    static constexpr size_t kAhead = 4;
     bool failed = false;
     int first_rc = TFBS_OK;  // the failure that stopped the others
     std::string first_err;
@@ -297,6 +301,16 @@ struct Ordered {
             first_err = err;
         }
         failed = true;
+        cv.notify_all();
+    }
+    bool room(size_t g) {  // waits until batch g may hold its blocks; false if a shard failed
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return failed || g < written + kAhead; });
+        return !failed;
+    }
+    void done(size_t g) {
+        std::lock_guard<std::mutex> l(mu);
+        written = g + 1;
         cv.notify_all();
     }
     bool take(size_t g, Item &it) {  // waits for batch g; false if a shard failed
@@ -501,6 +515,7 @@ int tfbs_run(const tfbs_run_args *a) {
                 const size_t n = bb->b.rh.size();
                 Ordered::Item it;
                 if (device_rows) {  // BGZF blocks into a memory file; the POS base from the chain
+                    if (!ord.room(g)) return tfbs::fail(TFBS_E_STATE, "another device's shard failed");
                     it.fd = memfd_create("tfbs_rows", MFD_CLOEXEC);
                     if (it.fd < 0) return tfbs::fail(TFBS_E_IO, std::string("memfd_create: ") + strerror(errno));
                     uint32_t fk = 0;
@@ -540,6 +555,7 @@ int tfbs_run(const tfbs_run_args *a) {
                     ord.abort(rc, tfbs_last_error());
                     return;
                 }
+                ord.done(g);
             }
         });
         auto run_one = [&](size_t k) {

@@ -253,6 +253,78 @@ def test_bcf_carriers_mode_matches_raw_gt(tmp_path, sel):
     assert n_car > 50 and (n_bad > 0 or sel is not None)
 
 
+@pytest.mark.parametrize("chunk_kb", [None, 1, 7])
+def test_bcf_condensed_stream_matches_dense(tmp_path, monkeypatch, chunk_kb):
+    """Carriers mode reads the condensed stream (io.hpp CBlock: per 64-byte line a
+    background code -- alternating 2/3 either way round, all 2, all 3 -- plus the
+    differing bytes; blocks that are not GT-like kept whole).  Against the dense
+    stream (TFBS_BCF_CONDENSED=0) on a file built to hit every case: phased 0|0,
+    unphased 0/0 (constant background), both mixed within a line, common variants
+    (blocks kept whole), random bytes, vector_end (ploidy), GT payloads spanning
+    several BGZF blocks and read chunks, odd-length shared parts (the alternation's
+    parity flips between records), multi-allelic records, a sample selection (the
+    payload read back) and a CSI seek (the condensed stream restarting mid-file)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import struct
+
+    import numpy as np
+    import synth_dataset
+    if chunk_kb:
+        monkeypatch.setenv("TFBS_BCF_CHUNK_KB", str(chunk_kb))
+    ns = 23000  # 46 000 GT bytes: payloads cross BGZF blocks
+    header = ("##fileformat=VCFv4.2\n##FORMAT=<ID=GT,Number=1,Type=String,Description=\"Genotype\">\n"
+              "##contig=<ID=chr1,length=1000000>\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\t" +
+              "\t".join("S%d" % i for i in range(ns)) + "\n").encode() + b"\0"
+    body = bytearray(b"BCF\2\2" + struct.pack("<I", len(header)) + header)
+    rnd = np.random.default_rng(11)
+    spans = []
+    for j, pos in enumerate(range(100, 100 + 40 * 3001, 3001)):
+        kind = j % 8
+        g = np.full((ns, 2), [2, 3], dtype=np.int8)                       # 0|0
+        if kind == 1:
+            g[:] = 2                                                      # 0/0 0/0: constant 2
+        elif kind == 2:
+            g[: ns // 2] = 2                                              # both backgrounds in one record
+            g[ns // 3: ns // 3 + 5] = [[3, 3]]                            # and all-3 runs
+        elif kind == 3:
+            k = rnd.random(ns) < 0.3                                      # a common variant: kept blocks
+            g[k, 0] = 4
+        elif kind == 4:
+            g[:] = rnd.integers(-128, 128, size=(ns, 2))                  # noise
+        f = rnd.random(ns) < 0.01
+        g[f, 0] = rnd.choice([4, 5, 2, 3], size=f.sum())
+        g[f, 1] = rnd.choice([4, 5, 2, 3], size=f.sum())
+        if kind == 5:
+            g[rnd.integers(ns), rnd.integers(2)] = -127                   # vector_end
+        ref, alt = ("A", "C") if kind != 6 else ("ACG", "A")
+        if kind == 7:
+            ref, alt = "AT", "A"                                          # odd-length alleles: parity flips
+        u0 = len(body)
+        body += synth_dataset.bcf_record(0, pos, ref, alt + "T" * (j % 3), g)
+        spans.append((pos, len(ref), u0, len(body)))
+    path = str(tmp_path / "mix.bcf")
+    offs = []
+    open(path, "wb").write(synth_dataset.bgzf_blocks(bytes(body), offs))
+    open(path + ".csi", "wb").write(synth_dataset.csi_index(spans, offs, 1000000))
+
+    def read(condensed, sel=None, queries=((0, 10 ** 9),)):
+        monkeypatch.setenv("TFBS_BCF_CONDENSED", "1" if condensed else "0")
+        r = T.BcfReader(path)
+        if sel is not None:
+            r.select(sel)
+        r.set_carriers_mode(True)
+        return [[(c["pos0"], c["ref"], c["alt"], c["carriers"], c["gt_status"]) for c in r.fetch("chr1", b, e)]
+                for b, e in queries]
+
+    qs = ((0, 500), (450, 9000), (50000, 60000), (90000, 91000), (20000, 33000), (100000, 10 ** 9))
+    for sel in (None, [5, 3, 22999, 0, 41, 41, 12000]):
+        want, got = read(False, sel, qs), read(True, sel, qs)
+        assert got == want
+        assert sum(len(q) for q in want) > 12
+        assert sum(len(c[3]) for q in want for c in q) > (1000 if sel is None else 0)
+        assert any(c[4] != 0 for q in want for c in q) or sel is not None
+
+
 def test_inflate_raw_matches_zlib():
     """tfbs_inflate_raw (the BCF reader's DEFLATE decoder, inflate.cpp) == zlib on raw
     streams of every block type (stored, fixed, dynamic), every zlib level and strategy,
