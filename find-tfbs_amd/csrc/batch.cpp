@@ -141,12 +141,9 @@ struct SeqTable {
             h = mix(h, x);
         }
         for (; i < n; i++) h = mix(h, d.nuc[i] | 0x100u);
-        for (size_t a = 0; a < n;) {  // positions as (first, length) runs
-            size_t b = a + 1;
-            while (b < n && d.pos[b] == d.pos[b - 1] + 1) b++;
-            h = mix(h, ((d.pos[a] - es) << 24) ^ (uint64_t)(b - a));
-            a = b;
-        }
+        uint64_t ps = 0;  // positions: their offsets from the affine ones, weighted (no branches)
+        for (size_t p = 0; p < n; p++) ps += (d.pos[p] - es - p) * (2 * p + 1);
+        h = mix(h, ps);
         return h | 1;  // (never 0: the empty mark)
     }
     void insert(std::vector<Distinct> &dist, Distinct &&d, uint64_t es) {
@@ -555,6 +552,7 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
     inner_keys(I.inner, R);
     out.dev_grouped = true;
     std::vector<Distinct> &dist = out.dist;
+    dist.reserve(G + 2);
     SeqTable table(G);
     RefWindow ref{I.ref.data(), R.es, I.ref.size()};
     std::vector<const Record *> diffs;
@@ -779,6 +777,21 @@ static uint64_t dirty_windows(const uint32_t *runs, size_t nruns, uint32_t S, ui
     return n;
 }
 
+// 16 base codes (0-3; N = 4 as 0) as one packed word, 2 bits each, base 0 lowest
+static inline uint32_t pack16(const uint8_t *p) {
+    auto half = [](uint64_t x) {
+        x &= 0x0303030303030303ull;
+        x = (x | (x >> 6)) & 0x000F000F000F000Full;
+        x = (x | (x >> 12)) & 0x000000FF000000FFull;
+        x = (x | (x >> 24)) & 0xFFFFull;
+        return (uint32_t)x;
+    };
+    uint64_t lo, hi;
+    memcpy(&lo, p, 8);
+    memcpy(&hi, p + 8, 8);
+    return half(lo) | (half(hi) << 16);
+}
+
 void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads) {
     const size_t nr = built.size();
     if (!nr) return;
@@ -817,9 +830,10 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             const Distinct &d = rb.dist[i];
             HapInfo &h = info[j][i];
             h.n = (uint32_t)d.nuc.size();
-            h.has_n = std::find(d.nuc.begin(), d.nuc.end(), (uint8_t)4) != d.nuc.end();
-            h.affine = true;
-            for (uint32_t p = 0; p < h.n && h.affine; p++) h.affine = d.pos[p] == rb.R.es + p;
+            h.has_n = h.n && memchr(d.nuc.data(), 4, h.n) != nullptr;
+            uint64_t off = 0;  // (no early exit: the loop vectorises)
+            for (uint32_t p = 0; p < h.n; p++) off |= d.pos[p] ^ (rb.R.es + p);
+            h.affine = off == 0;
         }
         // reference-window reuse: a window whose bases equal those of the reference
         // window that starts at its first base's position has that window's score and
@@ -877,6 +891,20 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             uint32_t qend = 0;  // the last segment's reference end (exclusive)
             bool open = false;
             for (uint32_t p = 0; p < h.n; p++) {
+                if (open) {  // 8 columns at a time while the segment goes on (consecutive
+                    // positions, bases equal to the reference's at them)
+                    for (;;) {
+                        const uint64_t at = d.pos[p - 1] + 1, qq = at - rb.R.es;
+                        if (p + 8 > h.n || qq + 8 > m) break;
+                        uint64_t x, y, off = 0;
+                        memcpy(&x, d.nuc.data() + p, 8);
+                        memcpy(&y, rn.data() + qq, 8);
+                        for (uint32_t k = 0; k < 8; k++) off |= d.pos[p + k] ^ (at + k);
+                        if (x != y || off) break;
+                        p += 8;
+                    }
+                    if (p >= h.n) break;
+                }
                 const int64_t q = (int64_t)d.pos[p] - (int64_t)rb.R.es;
                 const bool ok = q >= 0 && q < (int64_t)m && d.nuc[p] == rn[(size_t)q];
                 if (open && ok && d.pos[p] == d.pos[p - 1] + 1) continue;  // the segment goes on
@@ -1011,10 +1039,9 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 }
             } else {
                 const Distinct &d = rb.dist[i];
-                for (uint32_t p = 0; p < n; p++) {
-                    const uint32_t c = d.nuc[p] == 4 ? 0u : d.nuc[p];  // N packs as A (masked by the N bits)
-                    w[p / 16] |= c << (2 * (p % 16));
-                }
+                uint32_t p = 0;  // N (4) packs as A (masked by the N bits): the low two bits
+                for (; p + 16 <= n; p += 16) w[p / 16] = pack16(d.nuc.data() + p);
+                for (; p < n; p++) w[p / 16] |= (uint32_t)(d.nuc[p] & 3u) << (2 * (p % 16));
             }
             word += (n + 15) / 16 + 3;
             if (h.has_n) {

@@ -31,10 +31,20 @@ struct Table {
     int bits = 0;
 };
 
+struct Rev8 {
+    uint8_t r[256];
+    Rev8() {
+        for (int x = 0; x < 256; x++) {
+            int y = 0;
+            for (int i = 0; i < 8; i++) y |= ((x >> i) & 1) << (7 - i);
+            r[x] = (uint8_t)y;
+        }
+    }
+};
+const Rev8 kRev8;
+// the low n (<= 16) bits of x reversed
 inline uint32_t rev_bits(uint32_t x, int n) {
-    uint32_t r = 0;
-    for (int i = 0; i < n; i++, x >>= 1) r = (r << 1) | (x & 1u);
-    return r;
+    return (((uint32_t)kRev8.r[x & 0xFF] << 8) | kRev8.r[(x >> 8) & 0xFF]) >> (16 - n);
 }
 
 // Canonical Huffman code of lens[0..n) (0: unused) into t; false if over-subscribed.
@@ -56,26 +66,32 @@ bool build(Table &t, const uint8_t *lens, int n, int main_bits) {
     const uint32_t msize = 1u << main_bits;
     for (uint32_t i = 0; i < msize; i++) t.e[i] = 0;  // len 0: invalid code
     uint32_t sub_at = msize;
-    // longest code among the codes sharing each main-table prefix (for sub-table sizes)
-    int sub_len[1 << kLitBits] = {0};
-    int nx[16];
-    memcpy(nx, next, sizeof nx);
-    for (int s = 0; s < n; s++) {
-        const int l = lens[s];
-        if (l > main_bits) {
-            const uint32_t r = rev_bits((uint32_t)nx[l], l);
-            const uint32_t pre = r & (msize - 1);
-            if (l - main_bits > sub_len[pre]) sub_len[pre] = l - main_bits;
+    // longest code among the codes sharing each main-table prefix (for sub-table sizes;
+    // only when some code is longer than the main table's index)
+    bool longer = false;
+    for (int l = main_bits + 1; l < 16; l++) longer = longer || count[l];
+    if (longer) {
+        uint8_t sub_len[1 << kLitBits];
+        memset(sub_len, 0, msize);
+        int nx[16];
+        memcpy(nx, next, sizeof nx);
+        for (int s = 0; s < n; s++) {
+            const int l = lens[s];
+            if (l > main_bits) {
+                const uint32_t r = rev_bits((uint32_t)nx[l], l);
+                const uint32_t pre = r & (msize - 1);
+                if (l - main_bits > sub_len[pre]) sub_len[pre] = (uint8_t)(l - main_bits);
+            }
+            if (l) nx[l]++;
         }
-        if (l) nx[l]++;
+        for (uint32_t pre = 0; pre < msize; pre++)
+            if (sub_len[pre]) {
+                if (sub_at + (1u << sub_len[pre]) > sizeof(t.e) / sizeof(t.e[0])) return false;
+                t.e[pre] = (sub_at << 16) | 16u | (uint32_t)sub_len[pre];
+                for (uint32_t k = 0; k < (1u << sub_len[pre]); k++) t.e[sub_at + k] = 0;
+                sub_at += 1u << sub_len[pre];
+            }
     }
-    for (uint32_t pre = 0; pre < msize; pre++)
-        if (sub_len[pre]) {
-            if (sub_at + (1u << sub_len[pre]) > sizeof(t.e) / sizeof(t.e[0])) return false;
-            t.e[pre] = (sub_at << 16) | 16u | (uint32_t)sub_len[pre];
-            for (uint32_t k = 0; k < (1u << sub_len[pre]); k++) t.e[sub_at + k] = 0;
-            sub_at += 1u << sub_len[pre];
-        }
     for (int s = 0; s < n; s++) {
         const int l = lens[s];
         if (!l) continue;
