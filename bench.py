@@ -73,7 +73,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--regions", type=int, default=None, help="regions per GPU (workload default)")
     ap.add_argument("--samples", type=int, default=None)
@@ -393,7 +393,12 @@ def main():
     # region's keys assembled -- reference-window reuse resolved per haplotype --,
     # classified and the varying keys' counts compacted; tfbs_batch_assemble_wait:
     # the host waits and checks every list, rescanning if one overflowed)
+    # (tfbs_step: the same three calls in one; from the third step alike on, the scan's
+    # and the assembly's launches replay as one hipGraph)
     def step():
+        T.check(L.tfbs_step(sc.h, batch.h))
+
+    def step_plain():
         T.check(L.tfbs_scan(sc.h, batch.h))
         T.check(L.tfbs_batch_assemble(sc.h, batch.h))
         T.check(L.tfbs_batch_assemble_wait(sc.h, batch.h))
@@ -422,7 +427,7 @@ def main():
     # loop: reading them syncs on each step's events, which is not part of a step
     kernel_ms, mfma_ms, asm_ms = [], [], []
     for _ in range(min(args.steps, 10)):
-        step()
+        step_plain()  # (graph steps carry no timing events)
         kernel_ms.append(L.tfbs_ctx_last_scan_ms(sc.h))  # the scan's launches (HIP events)
         mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
         asm_ms.append(L.tfbs_ctx_last_assemble_ms(sc.h))  # the assembly's launches

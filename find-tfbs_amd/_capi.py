@@ -109,6 +109,7 @@ SIGNATURES = [
     ("tfbs_batch_reduce", C.c_int, [vp, vp]),
     ("tfbs_batch_assemble", C.c_int, [vp, vp]),
     ("tfbs_batch_assemble_wait", C.c_int, [vp, vp]),
+    ("tfbs_step", C.c_int, [vp, vp]),
     ("tfbs_ctx_last_assemble_ms", C.c_float, [vp]),
     ("tfbs_batch_encode", C.c_int, [vp, vp, C.c_size_t, C.c_size_t]),
     ("tfbs_batch_encode_flags", C.c_int, [vp, vp, C.c_size_t, C.c_size_t, C.c_int]),

@@ -212,6 +212,15 @@ struct tfbs_ctx {
     float last_ms = 0.f;
     int last_launches = 0;
     bool timing_pending = false;
+    // tfbs_step: one step's scan and assembly launches captured as a hipGraph and
+    // replayed while the resident batch and every buffer they use stay as captured
+    hipGraph_t step_graph = nullptr;
+    hipGraphExec_t step_exec = nullptr;
+    uint64_t step_sig = 0;       // step_signature() of the graph (or of the last plain step)
+    bool step_sig_seen = false;  // the last plain step had step_sig: the next one is captured
+    bool capturing = false;      // the timing events and asm_ev are left out of a capture
+    uint64_t upload_gen = 0;     // tfbs_batch_upload calls (a new batch image: a new graph)
+    bool step_graphs = true;     // TFBS_STEP_GRAPH=0: plain launches
 };
 
 namespace tfbs {
@@ -395,7 +404,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             HIP_TRY(hipGetLastError());
             ctx->asm_ctr_zeroed = true;  // (for this scan's first assembly)
         }
-        HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
+        if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         // one stream per depth launch (launch_mfma: one per K depth), side streams
         // forked and joined only when there is more than one (small batches: no
         // cross-stream waits)
@@ -420,7 +429,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             HIP_TRY(hipEventRecord(ctx->join[i], ctx->side[i]));
             HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->join[i], 0));
         }
-        HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
+        if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->evk1, ctx->stream));
         ctx->kernel_timed = true;
         launches += n;
         if (m.prof) {  // (profiling runs only) the stamps, appended to the file: launches, then the waves
@@ -643,6 +652,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
         if (ctx->side[i]) (void)hipStreamDestroy(ctx->side[i]);
         if (ctx->join[i]) (void)hipEventDestroy(ctx->join[i]);
     }
+    if (ctx->step_exec) (void)hipGraphExecDestroy(ctx->step_exec);
+    if (ctx->step_graph) (void)hipGraphDestroy(ctx->step_graph);
     if (ctx->fork) (void)hipEventDestroy(ctx->fork);
     if (ctx->kf_fork) (void)hipEventDestroy(ctx->kf_fork);
     if (ctx->kf_join) (void)hipEventDestroy(ctx->kf_join);
@@ -670,6 +681,8 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;
+    ctx->step_graphs = env_int("TFBS_STEP_GRAPH", 1) != 0 && !getenv("TFBS_SCAN_PROF") && !ctx->kf_prof_on &&
+                       !ctx->debug_over;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
     ctx->key_cor_lds = (uint32_t)std::max(0, env_int("TFBS_KEY_COR_LDS", 1 << 30));
     ctx->cor_cap = (uint32_t)std::max(1, env_int("TFBS_KEY_COR_CAP", 1 << 22));
@@ -837,6 +850,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->counts_live = dense;
     ctx->resident = b;
+    ctx->upload_gen++;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     ctx->n_regions = (uint32_t)B.regions.size();
     ctx->over_pending = false;
@@ -849,7 +863,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
     if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not uploaded to this ctx");
     HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+    if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
     ctx->kernel_timed = false;
     // asynchronous: the overflow lists are checked (and the scan redone if one
     // overflowed) when its results are read (tfbs_batch_reduce / download)
@@ -857,7 +871,7 @@ int tfbs_scan(tfbs_ctx *ctx, tfbs_batch *b) {
     if (n < 0) return n;
     ctx->scanned = true;
     ctx->asm_state = 0;
-    HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+    if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
     ctx->last_launches = n;
     ctx->timing_pending = true;
     b->b.counts_valid = b->b.reduced = false;
@@ -923,7 +937,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
         ctx->var_cap = std::max<uint64_t>(ctx->var_cap, std::min<uint64_t>(B.n_counts / 16, 1ull << 28));
     }
     if ((rc = ctx->var_keys.ensure(ctx->var_keys_cap)) || (rc = ctx->var_counts.ensure(ctx->var_cap))) return rc;
-    HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
+    if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->asm_t0, ctx->stream));
     const bool mfma = !ctx->plan.m_supers.empty();
     // the assembly's counters and the spill buckets' (at asm_ctr + kAsmCtrWords): zeroed
     // by the scan for its first assembly, else one memset
@@ -969,9 +983,9 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
                               ctx->kf_join)) ||
         (nr == 0 && (rc = launch_asm_report(a.report_src, ctx->asm_ctr.p, ctx->stream))))
         return rc;
-    HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
+    if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
     HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->asm_ctr.p, 64, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
+    if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
     ctx->over_pending = false;  // the assembly's check covers this scan's overflow lists
     ctx->asm_batch = &B;
     ctx->asm_state = 1;
@@ -1153,6 +1167,126 @@ int tfbs_batch_assemble(tfbs_ctx *ctx, tfbs_batch *b) {
         ctx->var_owner = nullptr;
     }
     return enqueue_assembly(ctx, B, true);
+}
+
+}  // extern "C"
+
+// What a step's launches depend on besides the batch image: the resident batch and
+// its upload, every buffer's address and every list capacity the scan and the
+// assembly pass to their kernels.  A step whose signature equals the captured
+// graph's replays it.
+static uint64_t step_signature(const tfbs_ctx *ctx, const tfbs_batch *b) {
+    uint64_t h = 0x9E3779B97F4A7C15ull;
+    auto mix = [&](uint64_t v) {
+        h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+        h *= 0xBF58476D1CE4E5B9ull;
+    };
+    auto buf = [&](const auto &d) {
+        mix((uint64_t)(uintptr_t)d.p);
+        mix(d.n);
+    };
+    mix((uint64_t)(uintptr_t)b);
+    mix((uint64_t)(uintptr_t)ctx->resident);
+    mix(ctx->upload_gen);
+    buf(ctx->cands); buf(ctx->hitl); buf(ctx->hitn); buf(ctx->ref_hits); buf(ctx->ref_count); buf(ctx->spill);
+    buf(ctx->over); buf(ctx->spill_sorted); buf(ctx->spill_bcnt); buf(ctx->spill_boff); buf(ctx->cand_over);
+    buf(ctx->srcs); buf(ctx->words); buf(ctx->nmask); buf(ctx->counts); buf(ctx->posrel); buf(ctx->inner);
+    buf(ctx->haps); buf(ctx->druns); buf(ctx->gnarrow); buf(ctx->hd); buf(ctx->hd2); buf(ctx->regions);
+    buf(ctx->hits); buf(ctx->asm_scratch); buf(ctx->key_first); buf(ctx->var_counts); buf(ctx->asm_redo);
+    buf(ctx->asm_ctr); buf(ctx->cor_arena); buf(ctx->key_flags); buf(ctx->var_keys); buf(ctx->asm_order);
+    for (int c = 0; c < 2; c++) {
+        buf(ctx->wl_off[c]);
+        buf(ctx->wl[c]);
+        buf(ctx->wl16[c]);
+    }
+    for (uint64_t v : {(uint64_t)ctx->spill_cap, (uint64_t)ctx->cand_over_cap, (uint64_t)ctx->cand_cap,
+                       (uint64_t)ctx->scan_cand_cap, (uint64_t)ctx->var_keys_cap, ctx->var_cap,
+                       (uint64_t)ctx->cor_cap, (uint64_t)ctx->n_regions, (uint64_t)ctx->asm_order_n,
+                       (uint64_t)ctx->asm_order_big, (uint64_t)ctx->n_srcs, (uint64_t)ctx->srcs_on_dev,
+                       (uint64_t)ctx->counts_live, (uint64_t)ctx->mfma_group_words,
+                       (uint64_t)(uintptr_t)ctx->var_owner})
+        mix(v);
+    return h;
+}
+
+// The host state a step leaves (tfbs_scan + tfbs_batch_assemble), set after a replay.
+static void step_state(tfbs_ctx *ctx, Batch &B) {
+    ctx->scanned = true;
+    ctx->kernel_timed = false;  // (no timing events in a graph: the timing queries keep the last plain step's)
+    ctx->timing_pending = false;
+    ctx->asm_timed = false;
+    ctx->asm_ctr_zeroed = false;
+    ctx->post_done = true;
+    ctx->over_pending = false;
+    ctx->over_copied = false;
+    ctx->asm_batch = &B;
+    ctx->asm_state = 1;
+    B.counts_valid = B.reduced = false;
+    B.enc_r0 = B.enc_r1 = 0;
+}
+
+extern "C" {
+
+int tfbs_step(tfbs_ctx *ctx, tfbs_batch *b) {
+    if (!ctx || !b) return tfbs::fail(TFBS_E_ARG, "null argument");
+    if (ctx->resident != b) return tfbs::fail(TFBS_E_STATE, "batch not uploaded to this ctx");
+    HIP_TRY(hipSetDevice(ctx->device));
+    Batch &B = b->b;
+    auto plain = [&]() -> int {
+        int rc;
+        if ((rc = tfbs_scan(ctx, b)) || (rc = tfbs_batch_assemble(ctx, b))) return rc;
+        return TFBS_OK;
+    };
+    auto drop = [&]() {
+        if (ctx->step_exec) (void)hipGraphExecDestroy(ctx->step_exec);
+        if (ctx->step_graph) (void)hipGraphDestroy(ctx->step_graph);
+        ctx->step_exec = nullptr;
+        ctx->step_graph = nullptr;
+    };
+    // (another batch's varying counts in var_counts: tfbs_batch_assemble hands them over first)
+    const bool eligible = ctx->step_graphs && (!ctx->var_owner || ctx->var_owner == &B);
+    const uint64_t sig = step_signature(ctx, b);
+    int rc;
+    if (eligible && ctx->step_exec && sig == ctx->step_sig) {  // replay
+        HIP_TRY(hipGraphLaunch(ctx->step_exec, ctx->stream));
+        HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
+        step_state(ctx, B);
+        ctx->last_launches = 1;
+        return assembly_wait(ctx, B);
+    }
+    drop();
+    if (eligible && ctx->step_sig_seen && sig == ctx->step_sig) {  // the second step alike: capture it
+        hipGraph_t g = nullptr;
+        HIP_TRY(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed));
+        ctx->capturing = true;
+        rc = plain();
+        ctx->capturing = false;
+        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        hipGraphExec_t x = nullptr;
+        const bool ok = !rc && e == hipSuccess && g && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) == hipSuccess;
+        const uint64_t after = step_signature(ctx, b);  // (a buffer that moved while capturing: no graph)
+        if (ok && after == sig) {
+            ctx->step_graph = g;
+            ctx->step_exec = x;
+            ctx->step_sig = sig;
+            HIP_TRY(hipGraphLaunch(ctx->step_exec, ctx->stream));
+            HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
+            step_state(ctx, B);
+            ctx->last_launches = 1;
+            return assembly_wait(ctx, B);
+        }
+        (void)hipGetLastError();
+        if (x) (void)hipGraphExecDestroy(x);
+        if (g) (void)hipGraphDestroy(g);
+        ctx->step_sig_seen = false;  // nothing ran: the step again, plainly
+        if ((rc = plain())) return rc;
+        return assembly_wait(ctx, B);
+    }
+    if ((rc = plain())) return rc;
+    rc = assembly_wait(ctx, B);
+    ctx->step_sig = step_signature(ctx, b);  // (after the wait: a rescan's regrown lists count)
+    ctx->step_sig_seen = ctx->step_sig == sig;
+    return rc;
 }
 
 int tfbs_batch_assemble_wait(tfbs_ctx *ctx, tfbs_batch *b) {

@@ -514,9 +514,13 @@ __device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, con
 }
 
 
-#ifndef TFBS_PIPE
-#define TFBS_PIPE 1
+#ifndef TFBS_PIPE  // (tried: no gain over the tight loop, profiles/r05/ab_scan_variants.txt)
+#define TFBS_PIPE 0
 #endif
+#ifndef TFBS_BPF2
+#define TFBS_BPF2 0
+#endif
+#if TFBS_PIPE
 // A tile's coarse test and, when it fires, its queue entries; the queue is
 // drained first when they may not fit (acc stays live across the drain).
 __device__ __forceinline__ void test_tile(const ScanArgs &A, const GroupCtx &G, const v16f &acc, uint32_t ti, uint32_t t,
@@ -576,6 +580,8 @@ __device__ __forceinline__ void scan_segment_pipe(const ScanArgs &A, const char 
     }
 }
 
+#endif
+
 // The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
 // ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
 template <int D, int NK>
@@ -584,6 +590,55 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
                                              const v4i (&a1)[NK], bool two, uint32_t ta, const v16f &cb, int sa,
                                              uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
+#if TFBS_BPF2
+    if (two && D == 2) {
+        // depth 2: both chunks' B fragments of the next strand tile are read during the
+        // round before (two register sets, the loop unrolled by two), so no round waits
+        // for LDS between its MFMAs
+        const char *tile = img;
+        uint32_t ti = tb;
+        BFrag p[2], q[2];
+        load_frags<2>(img, lane, p);
+        auto one = [&](const BFrag (&f)[2], BFrag (&nx)[2]) {
+            if (ti + 1 < te) load_frags<2>(tile + kTB, lane, nx);
+            v16f c0 = mfma_chunk(a0[0], f[0], cb, sa);
+            v16f c1 = mfma_chunk(a1[0], f[0], cb, sa);
+            c0 = mfma_chunk(a0[1], f[1], c0, sa);
+            c1 = mfma_chunk(a1[1], f[1], c1, sa);
+            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
+            if (__builtin_expect(__ballot((x0 | x1) != 0) != 0, 0)) {
+                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
+                if (f0) {
+                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x0 = coarse_test(c0);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
+                }
+                if (f1) {
+                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
+                }
+            }
+            tile += kTB;
+            ti++;
+        };
+        while (ti + 1 < te) {
+            one(p, q);
+            one(q, p);
+        }
+        if (ti < te) one(p, q);
+        return;
+    }
+#endif
     if (two) {
         // a pointer loop (3 scalar instructions per round) and one vector compare for
         // both tests; the next round's chunk-0 B fragment is read unconditionally (past

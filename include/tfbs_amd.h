@@ -277,6 +277,12 @@ int tfbs_batch_reduce(tfbs_ctx *ctx, tfbs_batch *b);
  * tfbs_batch_assemble_wait. */
 int tfbs_batch_assemble(tfbs_ctx *ctx, tfbs_batch *b);
 int tfbs_batch_assemble_wait(tfbs_ctx *ctx, tfbs_batch *b);
+/* One step of the resident batch: tfbs_scan + tfbs_batch_assemble +
+ * tfbs_batch_assemble_wait, same results.  From the third step alike on (same
+ * batch, no buffer regrown), the scan's and the assembly's launches run as one
+ * hipGraph captured on the third (TFBS_STEP_GRAPH=0: never); graph steps leave
+ * the timing queries (tfbs_ctx_last_scan_ms, ...) at the last plain step's. */
+int tfbs_step(tfbs_ctx *ctx, tfbs_batch *b);
 /* Device time (ms, HIP events on the ctx stream) of the last assembly, -1 if none ran. */
 float tfbs_ctx_last_assemble_ms(const tfbs_ctx *ctx);
 /* counts_as_genotypes' per-sample half on the device (main.rs:439-534, SURVEY.md

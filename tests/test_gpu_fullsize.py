@@ -392,3 +392,39 @@ def test_c4_region_x_pwm_shards_sum_to_unsharded(tmp_path):
     assert not bad, bad[:10]
     assert [sorted(x) for x in got_rows] == want_rows
     assert sum(len(x) for x in want_rows) > 200
+
+
+@pytest.mark.parametrize("cfg", [C2, (2000, 300, 40, 3, 30, 7)], ids=["C2", "indels"])
+def test_step_graph_replays_equal_plain_steps(tmp_path, cfg):
+    """tfbs_step (bench.py's step: scan + assembly + wait; from the third step alike on
+    one hipGraph replay of the scan's and the assembly's launches) gives exactly the
+    keys of plain tfbs_scan + tfbs_batch_reduce, after several replays, on C2 and on a
+    batch with indels; a new upload of another batch does not replay the old graph."""
+    n_samples, n_regions, _, _, indel, seed = cfg
+    ps = _patterns(tmp_path, cfg)
+    sc = T.Scanner(ps)
+    L = T.lib()
+    try:
+        b = T.RegionBatch(ps, n_samples, keep_membership=False)
+        b.synth_fill(seed, 0, n_regions, indel)
+        b.scan(sc, reduce=True)
+        want = _digests(b)
+        for _ in range(6):
+            T.check(L.tfbs_step(sc.h, b.h))
+        T.check(L.tfbs_batch_reduce(sc.h, b.h))
+        assert _digests(b) == want
+        b2 = T.RegionBatch(ps, n_samples, keep_membership=False)
+        b2.synth_fill(seed + 1, 0, n_regions // 2, indel)
+        b2.scan(sc, reduce=True)
+        want2 = _digests(b2)
+        for _ in range(5):
+            T.check(L.tfbs_step(sc.h, b2.h))
+        T.check(L.tfbs_batch_reduce(sc.h, b2.h))
+        assert _digests(b2) == want2
+        T.check(L.tfbs_batch_upload(sc.h, b.h))  # back to the first batch: a new image, a new graph
+        for _ in range(4):
+            T.check(L.tfbs_step(sc.h, b.h))
+        T.check(L.tfbs_batch_reduce(sc.h, b.h))
+        assert _digests(b) == want
+    finally:
+        del sc
