@@ -163,6 +163,10 @@ int BgzfWriter::raw_fd() {
     if (fflush(f) != 0) return fail(TFBS_E_IO, "write failed");
     return fileno(f);
 }
+int BgzfWriter::seek_to(uint64_t at) {
+    if (fflush(f) != 0 || fseeko(f, (off_t)at, SEEK_SET) != 0) return fail(TFBS_E_IO, "seek failed");
+    return TFBS_OK;
+}
 // like BGzWriter::flush: ends the block (an empty block if nothing is buffered)
 int BgzfWriter::flush() {
     ends.push_back(raw.size());
@@ -1086,6 +1090,19 @@ int Bcf::decode_condensed(uint64_t o, BcfRecord &r) const {
             r.gt_status = vn >= 2 ? TFBS_OK : TFBS_E_PLOIDY;  // one value per sample: glen 1
             if (vt == 1 && vn == 2 && !sel_p) {
                 const uint64_t g0 = ip, g1 = ip + payload;
+                size_t most = 0;  // (at most one carrier per differing byte: one allocation)
+                for (size_t bi = sblock(g0); bi < cblk.size() && cblk[bi].a0 < g1; bi++) {
+                    const CBlock &b = cblk[bi];
+                    if (!b.raw.empty()) {
+                        most += b.n;
+                        continue;
+                    }
+                    const uint32_t lo = (uint32_t)(std::max(g0, b.a0) - b.a0),
+                                   hi = (uint32_t)(std::min<uint64_t>(g1, b.a0 + b.n) - b.a0);
+                    most += (size_t)(std::lower_bound(b.ex.begin(), b.ex.end(), hi << 8) -
+                                     std::lower_bound(b.ex.begin(), b.ex.end(), lo << 8));
+                }
+                r.carriers.reserve(std::min<size_t>(most, 2 * ns));
                 for (size_t bi = sblock(g0); bi < cblk.size() && cblk[bi].a0 < g1; bi++) {
                     const CBlock &b = cblk[bi];
                     const uint32_t lo = (uint32_t)(std::max(g0, b.a0) - b.a0),

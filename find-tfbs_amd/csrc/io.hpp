@@ -27,6 +27,8 @@ class BgzfWriter {
     // if it holds anything, is ended and written, the stream flushed; returns the
     // file descriptor to append the blocks to (or < 0 with the error set).
     int raw_fd();
+    // after blocks were written to raw_fd() at explicit offsets: the stream goes on at `at`
+    int seek_to(uint64_t at);
     int flush();
     int close();
     ~BgzfWriter();

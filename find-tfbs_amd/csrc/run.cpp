@@ -9,7 +9,6 @@
 // interleaving / HashMap order); rows within a region are sorted (D2); the
 // POS counter is therefore deterministic.
 #include <sys/mman.h>
-#include <sys/sendfile.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -18,6 +17,7 @@
 #include <mutex>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -271,14 +271,21 @@ struct Ordered {
         std::string bodies;    // row bodies (host rows)
     };
     std::vector<Item> items;
-    size_t written = 0;  // batches the writer has written out
-    // at most kAhead batches past the one being written hold their blocks (memory
+    size_t written = 0;  // batches [0, written) are written out
+    // at most kAhead batches past the first unwritten one hold their blocks (memory
     // files of hundreds of MB at 50 000 samples): a shard waits before making more
-    static constexpr size_t kAhead = 4;
+    static constexpr size_t kAhead = 6;
+    // device rows: batch g's blocks go to [off[g], off[g] + size[g]) of the output, known
+    // once every batch before it is submitted, so the writer threads copy several
+    // batches at once (positioned writes); done[g]: batch g is in the output
+    std::vector<uint64_t> size;
+    std::vector<int64_t> off;
+    std::vector<uint8_t> done_;
+    size_t sized = 0;  // off[0 .. sized] known
     bool failed = false;
     int first_rc = TFBS_OK;  // the failure that stopped the others
     std::string first_err;
-    explicit Ordered(size_t n) : base(n + 1, -1), items(n) { base[0] = 1; }
+    explicit Ordered(size_t n) : base(n + 1, -1), items(n), size(n, 0), off(n + 1, -1), done_(n, 0) { base[0] = 1; }
     int chain(size_t g, uint64_t n_rows, uint32_t *fake) {
         std::unique_lock<std::mutex> l(mu);
         cv.wait(l, [&] { return failed || base[g] >= 0; });
@@ -288,10 +295,40 @@ struct Ordered {
         cv.notify_all();
         return TFBS_OK;
     }
-    void submit(size_t g, Item &&it) {
+    void submit(size_t g, Item &&it, uint64_t bytes = 0) {
         std::lock_guard<std::mutex> l(mu);
         items[g] = std::move(it);
         items[g].ready = true;
+        size[g] = bytes;
+        while (off[sized] >= 0 && sized < items.size() && items[sized].ready) {
+            off[sized + 1] = off[sized] + (int64_t)size[sized];
+            sized++;
+        }
+        cv.notify_all();
+    }
+    // the output offset of batch 0 (after the header); then offsets follow the sizes
+    void start(int64_t at) {
+        std::lock_guard<std::mutex> l(mu);
+        off[0] = at;
+        while (sized < items.size() && items[sized].ready) {
+            off[sized + 1] = off[sized] + (int64_t)size[sized];
+            sized++;
+        }
+        cv.notify_all();
+    }
+    // waits until batch g is submitted and placed; false if a shard failed
+    bool placed(size_t g, Item &it, int64_t &at) {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return failed || (items[g].ready && off[g] >= 0); });
+        if (failed) return false;
+        it = std::move(items[g]);
+        at = off[g];
+        return true;
+    }
+    void finished(size_t g) {  // batch g is in the output
+        std::lock_guard<std::mutex> l(mu);
+        done_[g] = 1;
+        while (written < done_.size() && done_[written]) written++;
         cv.notify_all();
     }
     void abort(int rc, const std::string &err) {
@@ -308,11 +345,6 @@ struct Ordered {
         cv.wait(l, [&] { return failed || g < written + kAhead; });
         return !failed;
     }
-    void done(size_t g) {
-        std::lock_guard<std::mutex> l(mu);
-        written = g + 1;
-        cv.notify_all();
-    }
     bool take(size_t g, Item &it) {  // waits for batch g; false if a shard failed
         std::unique_lock<std::mutex> l(mu);
         cv.wait(l, [&] { return failed || items[g].ready; });
@@ -322,17 +354,22 @@ struct Ordered {
     }
 };
 
-int copy_fd(int src, int dst) {  // a memory file's bytes to dst
-    off_t off = 0;
-    const off_t n = lseek(src, 0, SEEK_END);
-    if (n < 0) return tfbs::fail(TFBS_E_IO, std::string("lseek: ") + strerror(errno));
-    while (off < n) {
-        const ssize_t w = sendfile(dst, src, &off, (size_t)std::min<off_t>(n - off, 1 << 30));
-        if (w < 0) {
-            if (errno == EINTR) continue;
-            return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
+// A memory file's n bytes to dst at offset at, through the thread's 8 MiB buffer
+// (a mapping's page faults made it ~0.7 GB/s per thread).
+int copy_fd_at(int src, uint64_t n, int dst, uint64_t at) {
+    thread_local std::vector<char> buf;
+    if (buf.empty()) buf.resize(8u << 20);
+    for (uint64_t k = 0; k < n;) {
+        const ssize_t r = pread(src, buf.data(), (size_t)std::min<uint64_t>(n - k, buf.size()), (off_t)k);
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) return tfbs::fail(TFBS_E_IO, std::string("read: ") + (r < 0 ? strerror(errno) : "short read"));
+        for (ssize_t q = 0; q < r;) {
+            const ssize_t w = pwrite(dst, buf.data() + q, (size_t)(r - q), (off_t)(at + k + (uint64_t)q));
+            if (w < 0 && errno == EINTR) continue;
+            if (w <= 0) return tfbs::fail(TFBS_E_IO, std::string("write: ") + (w < 0 ? strerror(errno) : "short write"));
+            q += w;
         }
-        if (w == 0) return tfbs::fail(TFBS_E_IO, "write: short copy");
+        k += (uint64_t)r;
     }
     return TFBS_OK;
 }
@@ -526,6 +563,13 @@ int tfbs_run(const tfbs_run_args *a) {
                         close(it.fd);
                         return rc;
                     }
+                    const off_t end = lseek(it.fd, 0, SEEK_END);
+                    if (end < 0) {
+                        close(it.fd);
+                        return tfbs::fail(TFBS_E_IO, std::string("lseek: ") + strerror(errno));
+                    }
+                    ord.submit(g, std::move(it), (uint64_t)end);
+                    return TFBS_OK;
                 } else if (int rc = tfbs::batch_row_bodies(bb->b, S.a->min_maf, it.bodies, threads)) {
                     return rc;
                 }
@@ -533,31 +577,50 @@ int tfbs_run(const tfbs_run_args *a) {
                 return TFBS_OK;
             }
         };
-        std::thread writer([&] {  // batches in order: blocks copied, bodies prefixed with POS and deflated
-            const int out_fd = gpu_bgzf ? w.raw_fd() : 0;
-            if (out_fd < 0) {
-                ord.abort(out_fd, tfbs_last_error());
-                return;
-            }
-            for (size_t g = 0; g < n_batches; g++) {
+        // device rows: kWriters threads copy the batches' memory files to their places in
+        // the output (positioned writes: several batches at once); host rows: one thread
+        // prefixes the bodies with POS and deflates them in batch order
+        constexpr int kWriters = 4;
+        int out_fd = -1;
+        int64_t out_at = 0;
+        if (gpu_bgzf) {
+            out_fd = w.raw_fd();
+            if (out_fd < 0) return out_fd;
+            out_at = (int64_t)lseek(out_fd, 0, SEEK_END);
+            if (out_at < 0) return fail(TFBS_E_IO, std::string("lseek: ") + strerror(errno));
+            ord.start(out_at);
+        }
+        std::atomic<size_t> next_w(0);
+        std::mutex tw_mu;
+        auto writer_fn = [&] {
+            for (;;) {
+                const size_t g = gpu_bgzf ? next_w.fetch_add(1) : next_w.load();
+                if (g >= n_batches) return;
                 Ordered::Item it;
-                if (!ord.take(g, it)) return;
+                int64_t at = 0;
+                if (gpu_bgzf ? !ord.placed(g, it, at) : !ord.take(g, it)) return;
                 const double t0 = now();
                 int rc;
                 if (it.fd >= 0) {
-                    rc = copy_fd(it.fd, out_fd);
+                    rc = copy_fd_at(it.fd, ord.size[g], out_fd, (uint64_t)at);
                     close(it.fd);
                 } else {
                     rc = write_prefixed(w, chr, it.bodies.data(), it.bodies.size(), &fake);
+                    next_w.store(g + 1);
                 }
-                t_write += now() - t0;
+                {
+                    std::lock_guard<std::mutex> l(tw_mu);
+                    t_write += now() - t0;
+                }
                 if (rc) {
                     ord.abort(rc, tfbs_last_error());
                     return;
                 }
-                ord.done(g);
+                ord.finished(g);
             }
-        });
+        };
+        std::vector<std::thread> writers;
+        for (int k = 0; k < (gpu_bgzf ? kWriters : 1); k++) writers.emplace_back(writer_fn);
         auto run_one = [&](size_t k) {
             Many m{gpu_bgzf, S, ord, shards[k].threads};
             shards[k].rc = run_shard(S, shards[k], m);
@@ -570,7 +633,10 @@ int tfbs_run(const tfbs_run_args *a) {
         for (size_t k = 1; k < n_sh; k++) ts.emplace_back(run_one, k);
         run_one(0);
         for (auto &t : ts) t.join();
-        writer.join();
+        for (auto &t : writers) t.join();
+        if (gpu_bgzf && !ord.failed) {  // the stream continues after the last batch's blocks
+            if (int rc2 = w.seek_to((uint64_t)ord.off[n_batches])) return rc2;
+        }
         {  // memory files a failed run left behind
             std::lock_guard<std::mutex> l(ord.mu);
             for (auto &it : ord.items)
