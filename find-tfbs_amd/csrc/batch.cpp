@@ -803,6 +803,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
         // and the same in the reference's columns (rruns[j][q0 .. q0 + qn)), q0 = r0 when
         // both are the same list (every column at its reference column: no indel)
         uint32_t q0 = 0, qn = 0;
+        bool rsep = false;  // the reference-column runs are a list of their own (an indel haplotype)
     };
     std::vector<std::vector<HapInfo>> info(nr);
     std::vector<std::vector<uint32_t>> rruns(nr);  // per region, its haplotypes' diff runs
@@ -935,6 +936,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 h.q0 = h.r0;
                 h.qn = h.rn;
             } else {  // the reference's columns: outside the segments' ranges, and where two touch
+                h.rsep = true;  // (q0 == r0 when the haplotype's own list is empty: the flag tells)
                 h.q0 = (uint32_t)rv.size();
                 uint32_t qa = 0;
                 for (size_t k = 0; k < segs.size(); k++) {
@@ -949,6 +951,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if (!h.dedup) {
                 rv.resize(h.r0);
                 h.rn = h.qn = 0;
+                h.rsep = false;
             }
         }
     });
@@ -970,7 +973,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             if (h.has_n) cur.nmask += (h.n + 31) / 32 + 2;
             if (!h.affine) cur.pos += h.n;
             cur.count += (uint64_t)B.n_slots * n_inner;
-            cur.runs += h.rn + (h.q0 != h.r0 ? h.qn : 0);
+            cur.runs += h.rn + (h.rsep ? h.qn : 0);
         }
     }
     const uint32_t region0 = (uint32_t)B.rh.size();
@@ -1070,7 +1073,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 runs += h.rn;
                 hm.rrun_off = hm.drun_off;
                 hm.n_rruns = h.qn / 2;
-                if (h.q0 != h.r0) {  // (an indel haplotype) its runs in the reference's columns follow
+                if (h.rsep) {  // (an indel haplotype) its runs in the reference's columns follow
                     hm.rrun_off = (uint32_t)(runs / 2);
                     std::copy(rruns[j].begin() + h.q0, rruns[j].begin() + h.q0 + h.qn, B.druns.begin() + runs);
                     runs += h.qn;

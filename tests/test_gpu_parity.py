@@ -328,6 +328,46 @@ def test_dense_hits_vs_oracle(tmp_path, monkeypatch, thr):
     assert b.num_haplotypes > n_regions
 
 
+@pytest.mark.parametrize("thr", [1e-3, 0.05])
+def test_reuse_indel_haplotypes_without_own_runs_vs_oracle(tmp_path, monkeypatch, thr):
+    """Reference-window reuse across indels when a haplotype's own columns hold no diff
+    run but the reference's do: a deletion running to the window's last base (the
+    haplotype is a prefix of the reference: one segment, no run in its columns, the
+    reference's columns past it a run to the end), alone or with SNVs carried by other
+    haplotypes, one region per case and several in one batch (so a missing run list
+    cannot borrow a neighbour's).  Found by the C5 full-size golden digests: the
+    haplotype's reference-column runs were not stored when its own list was empty."""
+    monkeypatch.setenv("TFBS_MFMA", "1")
+    ps, _ = synth_patterns(tmp_path, 12, 5, 83, thr=thr)
+    n_samples = 40
+    H = 2 * n_samples
+    rnd = random.Random(9)
+    regions, ranges = [], []
+    for j in range(8):
+        r = T.SynthRegion(41, j, n_samples, ps.max_length, 0)
+        s, e = r.merged
+        es = s - ps.max_length + 1
+        ref = r.ref
+        recs = []
+        q = len(ref) - 2 - j  # the deletion's first base; it runs to the last base
+        dele = list(range(0, H, 3))
+        recs.append(("car", es + q, ref[q:], ref[q], dele))
+        if j % 2:  # SNVs carried by other haplotypes (their own runs come first in the run array)
+            for t in (5, 40, 77):
+                alt = "ACGT"[("ACGT".index(ref[t]) + 1) % 4]
+                recs.append(("car", es + t, ref[t], alt, sorted(rnd.sample([h for h in range(H) if h % 3], 9))))
+        if j == 4:  # an insertion at the end too
+            recs.append(("car", es + len(ref) - 1, ref[-1], ref[-1] + "AC", list(range(1, H, 7))))
+        recs.sort(key=lambda x: x[1])
+        regions.append({"merged": (s, e), "ref": ref, "records": recs})
+        ranges.append((s, e))
+    beds = [("synthetic.bed", ranges)]
+    b = _compare(ps, n_samples, beds, regions)
+    assert b.num_scan_windows < b.num_windows
+    for k in range(len(regions)):  # one region per batch
+        _compare(ps, n_samples, [("synthetic.bed", [ranges[k]])], [regions[k]])
+
+
 @pytest.mark.parametrize("thr,fast_max_u,cor", [(1e-3, None, None), (0.05, None, None), (1e-3, "0", None),
                                                 (0.05, "40", None), (0.05, None, ("0", None)),
                                                 (1e-3, None, ("16", "200"))])
