@@ -987,6 +987,13 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     B.regions.resize(region0 + nr);
     B.n_counts = cur.count;
     std::vector<uint64_t> win(nr, 0), eff(nr, 0), cells(nr, 0), swin(nr, 0), scells(nr, 0);
+    // the window lists' span per depth class: its longest strand (build_window_lists)
+    uint32_t class_lmax[2] = {0, 0};
+    for (const auto &lc : B.pwm_len_hist)
+        if (lc.first <= (uint32_t)(kMMaxChunks * kMChunkCols)) {
+            uint32_t &m = class_lmax[mfma_depth_class((lc.first + kMChunkCols - 1) / kMChunkCols) > 2];
+            m = std::max(m, lc.first);
+        }
     par([&](size_t j) {
         RegionBuilt &rb = built[j];
         RegionH &R = rb.R;
@@ -1088,7 +1095,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                     const uint64_t nw = n - lc.first + 1;
                     uint64_t sw = nw;  // windows the scan reads
                     if (h.dedup && lc.first <= (uint32_t)(kMMaxChunks * kMChunkCols)) {
-                        const uint32_t span = kMChunkCols * mfma_depth_class((lc.first + kMChunkCols - 1) / kMChunkCols);
+                        const uint32_t span = class_lmax[mfma_depth_class((lc.first + kMChunkCols - 1) / kMChunkCols) > 2];
                         sw = dirty_windows(rruns[j].data() + h.r0, h.rn, span, (uint32_t)nw);
                     }
                     r_swin += sw * lc.second;

@@ -263,10 +263,11 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
     const Plan &P = ctx->plan;
     if (P.m_supers.empty()) return TFBS_OK;
     const auto t0 = std::chrono::steady_clock::now();
-    uint32_t lmin[2] = {0, 0};
+    uint32_t lmin[2] = {0, 0}, span[2] = {0, 0};  // per depth class: shortest and longest strand
     for (const DevMSuper &S : P.m_supers) {
         uint32_t &l = lmin[S.nk > 2 ? 1 : 0];
         l = l ? std::min(l, S.lmin) : S.lmin;
+        span[S.nk > 2 ? 1 : 0] = std::max(span[S.nk > 2 ? 1 : 0], S.lmax);
     }
     int rc;
     for (int c = 0; c < 2; c++)
@@ -295,7 +296,7 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
         *p16 = cx->wl16[c].p;
         return TFBS_OK;
     };
-    if ((rc = build_window_lists(ctx->haps.p, n_haps, ctx->druns.p, lmin, ctx->mfma_hpb, 1, bufs, ctx->wl_entries,
+    if ((rc = build_window_lists(ctx->haps.p, n_haps, ctx->druns.p, lmin, span, ctx->mfma_hpb, 1, bufs, ctx->wl_entries,
                                  ctx->stream, ensure, ctx)))
         return rc;
     for (int c = 0; c < 2; c++)

@@ -206,14 +206,15 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
     // strand's reads stay in the buffer
     plan->m_weights.resize(plan->m_weights.size() + 4 * 32, 0);
 
-    struct TileSrc { size_t first, count; uint32_t nk, lmin; };
+    struct TileSrc { size_t first, count; uint32_t nk, lmin, lmax; };
     std::vector<TileSrc> tiles;
     for (size_t s = 0; s < strands.size(); s += kMStrands) {
-        TileSrc t{s, std::min<size_t>(kMStrands, strands.size() - s), 0, UINT32_MAX};
+        TileSrc t{s, std::min<size_t>(kMStrands, strands.size() - s), 0, UINT32_MAX, 0};
         for (size_t k = 0; k < t.count; k++) {
             const Pat &p = P.pats[strands[s + k].first];
             t.nk = std::max<uint32_t>(t.nk, (p.len + kMChunkCols - 1) / kMChunkCols);
             t.lmin = std::min(t.lmin, p.len);
+            t.lmax = std::max(t.lmax, p.len);
         }
         tiles.push_back(t);
     }
@@ -267,6 +268,7 @@ void build_mfma_tiles(const Patterns &P, const std::vector<SlotGroup> &groups, c
         for (uint32_t k = 0; k < count; b_off += mfma_tile_bytes(tiles[ti + k].nk), k++) {
             const TileSrc &t = tiles[ti + k];
             S.lmin = std::min(S.lmin, t.lmin);
+            S.lmax = std::max(S.lmax, t.lmax);
             const size_t g0 = plan->m_meta.size();
             plan->m_meta.resize(g0 + kGMetaInts, 0);
             int32_t *gm = &plan->m_meta[g0];

@@ -139,7 +139,8 @@ constexpr uint32_t kMMaxHapsPerBlock = 64;  // 6 bits of a window list entry
 // Builds the window lists of every haplotype of the batch for the depth classes
 // c (0: class 2, 1: class 4) with lmin[c] != 0 (the class's shortest strand):
 // all windows [0, len - lmin + 1) of a haplotype, only the dirty ones of a
-// HAP_DEDUP haplotype when dedup (tfbs_internal.hpp); off[c] gets n_haps + 1
+// HAP_DEDUP haplotype when dedup -- a run meeting the window's first span[c]
+// columns, span[c] the class's longest strand (tfbs_internal.hpp) --; off[c] gets n_haps + 1
 // offsets, list[c] (grown with ensure_list) the entries.  Synchronises `stream`.
 constexpr uint32_t kWlNarrowLen = 1024;  // haplotypes of a narrow group: windows < 2^10
 struct WindowListBufs {
@@ -154,7 +155,7 @@ struct WindowListBufs {
 };
 size_t scan_tmp_words(size_t n);
 int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
-                       uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
+                       const uint32_t span[2], uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
                        int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
                        void *ensure_ctx);
 // Super tile image budgets per K depth (1-8) that let each depth's kernel reach

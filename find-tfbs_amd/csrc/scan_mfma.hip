@@ -1264,7 +1264,7 @@ size_t scan_tmp_words(size_t n) {
 }
 
 int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
-                       uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
+                       const uint32_t span[2], uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
                        int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),
                        void *ensure_ctx) {
     if (n_haps && bufs.hd) hipLaunchKernelGGL(hd_kernel, dim3((n_haps + 255) / 256), dim3(256), 0, stream, haps, n_haps,
@@ -1272,7 +1272,7 @@ int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *drun
     for (int c = 0; c < 2; c++) {
         total[c] = 0;
         if (!lmin[c]) continue;
-        const uint32_t S = kMChunkCols * (c ? 4 : 2);
+        const uint32_t S = span[c] ? span[c] : kMChunkCols * (c ? 4 : 2);  // the windows dirty for the longest strand
         hipLaunchKernelGGL(wl_count_kernel, dim3(n_haps / 256 + 1), dim3(256), 0, stream, haps, n_haps, druns, lmin[c],
                            S, dedup, bufs.off[c]);
         if (int rc = exclusive_scan(bufs.off[c], (uint64_t)n_haps + 1, bufs.scan_tmp, stream)) return rc;

@@ -128,7 +128,8 @@ struct DevMSuper {
     uint32_t tile0;     // global index of tile 0 (Plan::m_meta)
     uint32_t acc0;
     uint32_t seg;       // depth segment ends, one byte per depth
-    uint32_t pad[3];
+    uint32_t lmax;      // longest strand
+    uint32_t pad[2];
 };
 constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 4u; }
 
