@@ -290,8 +290,10 @@ float tfbs_ctx_last_assemble_ms(const tfbs_ctx *ctx);
  * per key v[s] = C[hap(2s)] + C[hap(2s+1)] over the samples, min / max, the
  * sorted distinct values with their sample counts, and one u8 code per sample;
  * rows of these regions are then formatted from the codes (no per-sample
- * count gather on the host).  Keys whose region has > 255 distinct haplotypes,
- * > 255 distinct totals or a total range >= 65536 keep the host path. */
+ * count gather on the host).  Keys whose region has > 65 535 distinct haplotypes
+ * (u16 membership) or > 8 192 distinct (left, right) haplotype pairs (the LDS pair
+ * table, pair_table_kernel), or with > 255 distinct totals or a total range >= 65 536,
+ * keep the host path (tfbs_internal.hpp kEncMax*). */
 int tfbs_batch_encode(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1);
 /* tfbs_batch_encode with flags: TFBS_ENC_DEVICE_CODES keeps the per-sample codes on
  * the device only (for tfbs_batch_rows_bgzf; host row functions then take their
