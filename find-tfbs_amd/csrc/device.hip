@@ -139,6 +139,7 @@ struct tfbs_ctx {
     DevBuf<uint32_t> wl[2];
     DevBuf<uint16_t> wl16[2];  // the narrow groups' window lists
     DevBuf<uint8_t> gnarrow;   // per haplotype group of mfma_hpb: every haplotype <= kWlNarrowLen bases
+    bool wl_any_narrow = false, wl_any_wide = false;  // the resident batch has narrow / other groups
     DevBuf<uint4> hd, hd2;     // the matrix-core scan's compact haplotype descriptors
     uint64_t wl_entries[2] = {0, 0};
     double wl_seconds = 0;                // the last build's wall time
@@ -288,10 +289,15 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
     bufs.hd = ctx->hd.p;
     bufs.hd2 = ctx->hd2.p;
     bufs.scan_tmp = ctx->wl_tmp.p;
+    // a group's entries are all in one of the two lists (16-bit: a narrow group), both
+    // indexed by the same offsets: a list no group uses gets no room
+    ctx->wl_any_narrow = ctx->wl_any_wide = false;
+    for (uint8_t g : narrow) (g ? ctx->wl_any_narrow : ctx->wl_any_wide) = true;
+    if (narrow.empty()) ctx->wl_any_wide = true;
     auto ensure = [](void *x, int c, uint64_t n, uint32_t **p, uint16_t **p16) {
         tfbs_ctx *cx = static_cast<tfbs_ctx *>(x);
-        if (int e = cx->wl[c].ensure(n)) return e;
-        if (int e = cx->wl16[c].ensure(n)) return e;
+        if (int e = cx->wl[c].ensure(cx->wl_any_wide ? n : 1)) return e;
+        if (int e = cx->wl16[c].ensure(cx->wl_any_narrow ? n : 1)) return e;
         *p = cx->wl[c].p;
         *p16 = cx->wl16[c].p;
         return TFBS_OK;
