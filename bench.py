@@ -476,7 +476,7 @@ def main():
             rp = prof.get("rocprof_phase_ms") if prof else None
             roof = {"bound": "mfma", "achieved": mops, "peak": MFMA_F6_PEAK_TOPS, "unit": "TFLOP/s",
                     "frac": mops / MFMA_F6_PEAK_TOPS, "traffic": traffic,
-                    "kernel": "scan_mfma_kernel<staged, K depth> (one launch per K depth, 4 streams)",
+                    "kernel": "scan_mfma_all_kernel<staged> (one launch: a workgroup per group of 64 haplotypes over every super tile; TFBS_SCAN_MERGED=0: scan_mfma_kernel<staged, K depth>, one launch per depth class)",
                     "kernel_ms": mms,
                     # the same figure on the rocprofv3 kernel trace's MFMA phase (same library build)
                     "rocprof_phase_ms": rp,
