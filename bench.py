@@ -537,9 +537,10 @@ def main():
                           "region's reference window take the reference window's hits in the assembly (reference-"
                           "window reuse, exact; TFBS_DEDUP=0 scans them all); scanned_windows_per_s counts the "
                           "windows the kernels read",
-            "step": "tfbs_scan + tfbs_batch_assemble + tfbs_batch_assemble_wait (host sync and list check "
-                    "every step): scan kernels, overflow rescoring, spill bucketing, key assembly + "
-                    "classification + varying-count compaction of every region of the batch",
+            "step": "tfbs_step = tfbs_scan + tfbs_batch_assemble + tfbs_batch_assemble_wait (host sync and "
+                    "list check every step; from the third step alike the launches replay as one hipGraph): "
+                    "scan kernels, overflow rescoring, spill bucketing, key assembly + classification + "
+                    "varying-count compaction of every region of the batch",
             "step_device_ms": {"scan": kms, "mfma_phase": mms, "assemble": ams},
             "ranks": {"world_size": world, "backend": args.dist_backend if dist is not None else None,
                       "ms_per_step": per_rank_ms},
