@@ -222,6 +222,14 @@ struct tfbs_ctx {
     bool capturing = false;      // the timing events and asm_ev are left out of a capture
     uint64_t upload_gen = 0;     // tfbs_batch_upload calls (a new batch image: a new graph)
     bool step_graphs = true;     // TFBS_STEP_GRAPH=0: plain launches
+    // lean assemblies: the wide spill bucketing and the leftover key pass are left out
+    // when the batch's last assembly needed neither (C2 is launch-bound); the kernels
+    // flag what they could not do and the wait reruns the assembly in full.
+    // TFBS_ASM_LEAN: 0 never, 1 predicted (default), 2 always (the tests' rerun path)
+    int asm_lean_mode = 1;
+    uint32_t prev_spill = UINT32_MAX, prev_redo = UINT32_MAX;  // the last checked assembly's (unknown: max)
+    bool asm_wide = true, asm_leftover = true;                 // what the enqueued assembly launched
+    bool asm_full = false;                                     // (a rerun: everything)
 };
 
 namespace tfbs {
@@ -688,6 +696,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->debug_over = env_int("TFBS_DEBUG_OVER", 0) != 0;
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;
+    ctx->asm_lean_mode = env_int("TFBS_ASM_LEAN", 1);
     ctx->step_graphs = env_int("TFBS_STEP_GRAPH", 1) != 0 && !getenv("TFBS_SCAN_PROF") && !ctx->kf_prof_on &&
                        !ctx->debug_over;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
@@ -858,6 +867,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->counts_live = dense;
     ctx->resident = b;
     ctx->upload_gen++;
+    ctx->prev_spill = ctx->prev_redo = UINT32_MAX;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     ctx->n_regions = (uint32_t)B.regions.size();
     ctx->over_pending = false;
@@ -932,7 +942,7 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
         (rc = ctx->key_flags.ensure(std::max<uint64_t>(n_keys, 1))) || (rc = ctx->asm_ctr.ensure(kAsmCtrWords + (size_t)std::max<uint32_t>(1, nr) + 1)) ||
         (rc = ctx->asm_redo.ensure((size_t)nr + 1)) || (rc = ctx->cor_arena.ensure(ctx->cor_cap)))
         return rc;
-    if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 64, hipHostMallocDefault));
+    if (!ctx->asm_host) HIP_TRY(hipHostMalloc((void **)&ctx->asm_host, 4 * kAsmCtrWords, hipHostMallocDefault));
     if (const int vc = env_int("TFBS_VAR_CAP", 0); vc > 0) {
         if (!ctx->var_cap_forced) {
             ctx->var_keys_cap = (uint32_t)vc;
@@ -953,10 +963,16 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
                                (kAsmCtrWords + (mfma && post ? (size_t)std::max<uint32_t>(1, nr) + 1 : 0)) * 4,
                                ctx->stream));
     ctx->asm_ctr_zeroed = false;
+    // lean (see tfbs_ctx): left out what the batch's last checked assembly did not need
+    const bool lean = mfma && post && !ctx->asm_full && ctx->asm_lean_mode != 0;
+    ctx->asm_wide = !(lean && (ctx->asm_lean_mode == 2 || ctx->prev_spill <= kPostSerial));
+    ctx->asm_leftover = !(lean && (ctx->asm_lean_mode == 2 || ctx->prev_redo == 0));
     if (mfma && post) {  // overflow candidates rescored (once per scan: they append spill records) + spill buckets
+        // (without the leftover pass post_scan_kernel copies the overflow counters to
+        // asm_ctr[0, 2); asm_ctr[20]: set when the records needed the wide kernels)
         if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18, std::max<uint32_t>(1, nr),
                                     ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p,
-                                    ctx->stream)))
+                                    ctx->stream, ctx->asm_wide, ctx->asm_ctr.p, ctx->asm_ctr.p + 20)))
             return rc;
         ctx->post_done = true;
     }
@@ -987,11 +1003,11 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
         a.prof = ctx->kf_prof.p;
     }
     if ((rc = launch_key_fast(a, nr, a.order ? ctx->asm_order_big : 0, ctx->stream, ctx->side[0], ctx->kf_fork,
-                              ctx->kf_join)) ||
+                              ctx->kf_join, ctx->asm_leftover)) ||
         (nr == 0 && (rc = launch_asm_report(a.report_src, ctx->asm_ctr.p, ctx->stream))))
         return rc;
     if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->asm_t1, ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->asm_ctr.p, 64, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->asm_host, ctx->asm_ctr.p, 4 * kAsmCtrWords, hipMemcpyDeviceToHost, ctx->stream));
     if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->asm_ev, ctx->stream));
     ctx->over_pending = false;  // the assembly's check covers this scan's overflow lists
     ctx->asm_batch = &B;
@@ -1133,6 +1149,15 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
                     (unsigned long long)nk, ctx->var_keys_cap, (unsigned long long)nc,
                     (unsigned long long)ctx->var_cap);
         int rc;
+        // a lean assembly that needed what it left out (more spill records than post_scan_kernel
+        // buckets, or regions key_fast_kernel gave up): again with everything
+        if ((!ctx->asm_wide && ctx->asm_host[20]) || (!ctx->asm_leftover && ctx->asm_host[2])) {
+            ctx->asm_full = true;
+            rc = enqueue_assembly(ctx, B, true);
+            ctx->asm_full = false;
+            if (rc) return rc;
+            continue;
+        }
         if (ctx->asm_host[3] > ctx->cor_cap)  // regions that found the arena full went to key_asm_kernel: larger next time
             ctx->cor_cap = (uint32_t)std::min<uint64_t>((uint64_t)ctx->asm_host[3] * 5 / 4, 1u << 30);
         if (nspill > ctx->spill_cap || ncand > ctx->cand_over_cap) {
@@ -1151,6 +1176,8 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
             continue;
         }
         ctx->asm_state = 2;
+        ctx->prev_spill = nspill;
+        ctx->prev_redo = ctx->asm_host[2];
         if (ctx->kf_prof_on && (rc = kf_prof_report(ctx, (uint32_t)B.regions.size()))) return rc;
     }
     return TFBS_OK;
@@ -1211,7 +1238,8 @@ static uint64_t step_signature(const tfbs_ctx *ctx, const tfbs_batch *b) {
                        (uint64_t)ctx->cor_cap, (uint64_t)ctx->n_regions, (uint64_t)ctx->asm_order_n,
                        (uint64_t)ctx->asm_order_big, (uint64_t)ctx->n_srcs, (uint64_t)ctx->srcs_on_dev,
                        (uint64_t)ctx->counts_live, (uint64_t)ctx->mfma_group_words,
-                       (uint64_t)(uintptr_t)ctx->var_owner})
+                       (uint64_t)(uintptr_t)ctx->var_owner, (uint64_t)ctx->asm_lean_mode,
+                       (uint64_t)(ctx->prev_spill <= kPostSerial), (uint64_t)(ctx->prev_redo == 0)})
         mix(v);
     return h;
 }

@@ -1454,7 +1454,7 @@ static size_t key_fast_lds_bytes(bool big) {
 }
 
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
-                    hipEvent_t fork, hipEvent_t join) {
+                    hipEvent_t fork, hipEvent_t join, bool leftover) {
     if (n_regions == 0) return TFBS_OK;
     if (!a.order || !side) n_big = 0;
     n_big = std::min(n_big, n_regions);
@@ -1509,8 +1509,9 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));
     }
     // the regions it left: a fixed grid over the list (no host round trip)
-    hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
-                       (const uint32_t *)a.redo, (const uint32_t *)a.redo_n);
+    if (leftover)
+        hipLaunchKernelGGL(key_asm_kernel, dim3(std::min<uint32_t>(n_regions, 256)), dim3(kAsmBlock), 0, stream, a,
+                           (const uint32_t *)a.redo, (const uint32_t *)a.redo_n);
     e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;

@@ -83,8 +83,10 @@ int launch_key_asm(const AsmArgs &a, uint32_t n_regions, hipStream_t stream);
 // a.order lists the regions with the n_big of more than key_fast_big_u() distinct
 // haplotypes first: those take the 1 024-thread kernel on `stream`, queued ahead of
 // the others' on `side` (forked from and joined back into `stream` with the events).
+// leftover: also key_asm_kernel over the regions key_fast_kernel gave up (left out when the
+// batch's last assembly had none: the host reruns the assembly if this one did)
 int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStream_t stream, hipStream_t side,
-                    hipEvent_t fork, hipEvent_t join);
+                    hipEvent_t fork, hipEvent_t join, bool leftover = true);
 uint32_t key_fast_big_u();
 // ctr[0], ctr[1] = over[0], over[1] (the scan's overflow counters next to the
 // assembly's, for one copy back).

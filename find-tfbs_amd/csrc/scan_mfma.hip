@@ -1094,7 +1094,6 @@ MfmaKernel mfma_all_variant(bool staged) { return staged ? scan_mfma_all_kernel<
 // scan into boff, a scatter into sorted; bcnt n_regions + 1 zeroed before) on its
 // own: spills are rare, and no records (the usual case) costs one counter read.
 constexpr uint32_t kPostBlock = 256;
-constexpr uint32_t kPostSerial = 8192;  // spill records the last workgroup buckets itself
 
 // boff[0 .. n_regions]: the exclusive prefix of the bucket counts (one workgroup of
 // kPostBlock threads) -- each thread a run of consecutive buckets, one block scan of
@@ -1123,10 +1122,17 @@ __device__ void spill_bucket_offsets(uint32_t tid, uint32_t n_regions, uint32_t 
     }
 }
 
+// report (optional): the final overflow counters copied there by the last workgroup (the
+// assembly's check, when its leftover pass -- which copies them otherwise -- is not
+// launched); need_wide (optional: the wide kernels are not launched): set when the
+// records are too many for the last workgroup, so that the host reruns the assembly
+// with them.
 __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint32_t cand, uint32_t *done,
                                                               uint32_t n_regions, uint32_t *__restrict__ bcnt,
                                                               uint32_t *__restrict__ boff,
-                                                              uint32_t *__restrict__ sorted) {
+                                                              uint32_t *__restrict__ sorted,
+                                                              uint32_t *__restrict__ report,
+                                                              uint32_t *__restrict__ need_wide) {
     __shared__ uint32_t s_last, s_sum[kPostBlock];
     const uint32_t tid = threadIdx.x;
     if (cand) {
@@ -1171,9 +1177,13 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     __syncthreads();
     if (!s_last) return;
     __threadfence();  // (acquire: every workgroup's records)
+    if (report && tid < 2) report[tid] = __atomic_load_n(A.over + tid, __ATOMIC_RELAXED);
     const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
     if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
-    if (n > kPostSerial) return;  // spill_hist_wide_kernel + spill_scatter_wide_kernel's
+    if (n > kPostSerial) {  // spill_hist_wide_kernel + spill_scatter_wide_kernel's
+        if (need_wide && tid == 0) *need_wide = 1u;
+        return;
+    }
     for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
     __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
     __syncthreads();
@@ -1227,15 +1237,17 @@ __global__ __launch_bounds__(256) void spill_scatter_wide_kernel(ScanArgs A, con
 }
 
 int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
-                      uint32_t *sorted, hipStream_t stream) {
+                      uint32_t *sorted, hipStream_t stream, bool wide, uint32_t *report, uint32_t *need_wide) {
     // (256 workgroups: 1 024 cost C2 14 us in dispatch and finish tickets and did not
     // speed up C5's rescoring; the wide scatter's 128 exit at once when there is nothing
-    // for them)
+    // for them -- and are left out when the batch's last assembly did not need them)
     hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? 256 : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
-                       n_regions, bcnt, boff, sorted);
-    hipLaunchKernelGGL(spill_hist_wide_kernel, dim3(128), dim3(kPostBlock), 0, stream, a, done + 1, n_regions, bcnt,
-                       boff);
-    hipLaunchKernelGGL(spill_scatter_wide_kernel, dim3(128), dim3(256), 0, stream, a, boff, bcnt, sorted);
+                       n_regions, bcnt, boff, sorted, report, wide ? nullptr : need_wide);
+    if (wide) {
+        hipLaunchKernelGGL(spill_hist_wide_kernel, dim3(128), dim3(kPostBlock), 0, stream, a, done + 1, n_regions, bcnt,
+                           boff);
+        hipLaunchKernelGGL(spill_scatter_wide_kernel, dim3(128), dim3(256), 0, stream, a, boff, bcnt, sorted);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("post_scan_kernel launch: ") + hipGetErrorString(e));
     return TFBS_OK;
