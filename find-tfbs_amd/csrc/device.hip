@@ -228,6 +228,7 @@ struct tfbs_ctx {
     // TFBS_ASM_LEAN: 0 never, 1 predicted (default), 2 always (the tests' rerun path)
     int asm_lean_mode = 1;
     uint32_t prev_spill = UINT32_MAX, prev_redo = UINT32_MAX;  // the last checked assembly's (unknown: max)
+    uint32_t prev_cand = UINT32_MAX;                           // and its scan's candidates past the lists
     bool asm_wide = true, asm_leftover = true;                 // what the enqueued assembly launched
     bool asm_full = false;                                     // (a rerun: everything)
 };
@@ -867,7 +868,7 @@ int tfbs_batch_upload(tfbs_ctx *ctx, tfbs_batch *b) {
     ctx->counts_live = dense;
     ctx->resident = b;
     ctx->upload_gen++;
-    ctx->prev_spill = ctx->prev_redo = UINT32_MAX;
+    ctx->prev_spill = ctx->prev_redo = ctx->prev_cand = UINT32_MAX;
     ctx->mfma_group_words = mfma_group_words(B.haps.data(), (uint32_t)B.haps.size(), ctx->mfma_hpb);
     ctx->n_regions = (uint32_t)B.regions.size();
     ctx->over_pending = false;
@@ -972,7 +973,8 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
         // asm_ctr[0, 2); asm_ctr[20]: set when the records needed the wide kernels)
         if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18, std::max<uint32_t>(1, nr),
                                     ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p,
-                                    ctx->stream, ctx->asm_wide, ctx->asm_ctr.p, ctx->asm_ctr.p + 20)))
+                                    ctx->stream, ctx->asm_wide, ctx->asm_ctr.p, ctx->asm_ctr.p + 20,
+                                    lean && ctx->prev_cand == 0 ? 1u : 256u)))
             return rc;
         ctx->post_done = true;
     }
@@ -1178,6 +1180,7 @@ static int assembly_wait(tfbs_ctx *ctx, Batch &B) {
         ctx->asm_state = 2;
         ctx->prev_spill = nspill;
         ctx->prev_redo = ctx->asm_host[2];
+        ctx->prev_cand = ncand;
         if (ctx->kf_prof_on && (rc = kf_prof_report(ctx, (uint32_t)B.regions.size()))) return rc;
     }
     return TFBS_OK;
@@ -1239,7 +1242,8 @@ static uint64_t step_signature(const tfbs_ctx *ctx, const tfbs_batch *b) {
                        (uint64_t)ctx->asm_order_big, (uint64_t)ctx->n_srcs, (uint64_t)ctx->srcs_on_dev,
                        (uint64_t)ctx->counts_live, (uint64_t)ctx->mfma_group_words,
                        (uint64_t)(uintptr_t)ctx->var_owner, (uint64_t)ctx->asm_lean_mode,
-                       (uint64_t)(ctx->prev_spill <= kPostSerial), (uint64_t)(ctx->prev_redo == 0)})
+                       (uint64_t)(ctx->prev_spill <= kPostSerial), (uint64_t)(ctx->prev_redo == 0),
+                       (uint64_t)(ctx->prev_cand == 0)})
         mix(v);
     return h;
 }

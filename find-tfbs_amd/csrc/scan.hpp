@@ -133,11 +133,13 @@ int launch_post_scan(const ScanArgs &a, hipStream_t stream);
 // The same (when cand) and the spill records' buckets by region (boff[0 .. n_regions],
 // sorted) in one launch; *done and bcnt[0 .. n_regions] must be zero.
 // wide: also the grid-wide spill bucketing (more than kPostSerial records); report /
-// need_wide: post_scan_kernel's optional outputs (see there)
+// need_wide: post_scan_kernel's optional outputs (see there); cand_grid: the rescoring's
+// workgroups (1 when the batch's last scan had no candidate past the lists: the same
+// result, without 256 workgroups' dispatch and tickets)
 constexpr uint32_t kPostSerial = 8192;  // spill records post_scan_kernel's last workgroup buckets itself
 int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
                       uint32_t *sorted, hipStream_t stream, bool wide = true, uint32_t *report = nullptr,
-                      uint32_t *need_wide = nullptr);
+                      uint32_t *need_wide = nullptr, uint32_t cand_grid = 256);
 uint32_t mfma_group_words(const DevHap *haps, uint32_t n_haps, uint32_t hpb);
 constexpr uint32_t kMMaxHapsPerBlock = 64;  // 6 bits of a window list entry
 // Builds the window lists of every haplotype of the batch for the depth classes

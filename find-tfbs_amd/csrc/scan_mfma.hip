@@ -1237,11 +1237,12 @@ __global__ __launch_bounds__(256) void spill_scatter_wide_kernel(ScanArgs A, con
 }
 
 int launch_post_fused(const ScanArgs &a, bool cand, uint32_t *done, uint32_t n_regions, uint32_t *bcnt, uint32_t *boff,
-                      uint32_t *sorted, hipStream_t stream, bool wide, uint32_t *report, uint32_t *need_wide) {
+                      uint32_t *sorted, hipStream_t stream, bool wide, uint32_t *report, uint32_t *need_wide,
+                      uint32_t cand_grid) {
     // (256 workgroups: 1 024 cost C2 14 us in dispatch and finish tickets and did not
     // speed up C5's rescoring; the wide scatter's 128 exit at once when there is nothing
     // for them -- and are left out when the batch's last assembly did not need them)
-    hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? 256 : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
+    hipLaunchKernelGGL(post_scan_kernel, dim3(cand ? cand_grid : 1), dim3(kPostBlock), 0, stream, a, cand ? 1u : 0u, done,
                        n_regions, bcnt, boff, sorted, report, wide ? nullptr : need_wide);
     if (wide) {
         hipLaunchKernelGGL(spill_hist_wide_kernel, dim3(128), dim3(kPostBlock), 0, stream, a, done + 1, n_regions, bcnt,

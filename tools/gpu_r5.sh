@@ -56,6 +56,18 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
       tag=run_${n}${dv:+_$(echo ${spec#*:} | tr , _)}
       timeout -k 10 900 python3 -u tools/bench_run.py --samples 50000 --regions $n $dv --oracle-seconds 0 > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }
       grep tfbs_run_timing $O/$tag.err; python3 -c "import json;d=json.load(open('$O/$tag.json'));print('$tag', {k: d[k] for k in ('run_s','regions_per_s','bcf_decode_alone_s','dataset_gen_s','rows','records')})" ;;
+    bgzf_*)  # bgzf_<regions>[:<probe>,...]: tools/bgzf_only.py per build, phase clocks (TFBS_BGZF_PROF) then timing
+      spec=${st#bgzf_}; n=${spec%%:*}; libs=""; [ "$spec" != "$n" ] && libs=${spec#*:}
+      for rep in 1 2; do
+        for lib in base ${libs//,/ }; do
+          unset TFBS_LIB; [ $lib = base ] || export TFBS_LIB=find-tfbs_amd/lib/probe$lib/libtfbs_amd.so
+          TFBS_BGZF_PROF=1 timeout -k 10 300 python3 tools/bgzf_only.py $n > $O/bgzf_${lib}_prof_$rep.txt 2>&1 || { tail -20 $O/bgzf_${lib}_prof_$rep.txt; exit 1; }
+          grep "bgzf prof" $O/bgzf_${lib}_prof_$rep.txt | tail -1
+          timeout -k 10 300 python3 tools/bgzf_only.py $n > $O/bgzf_${lib}_$rep.txt 2>&1 || { tail -20 $O/bgzf_${lib}_$rep.txt; exit 1; }
+          echo "$lib rep$rep $(tail -1 $O/bgzf_${lib}_$rep.txt)"
+        done
+      done
+      unset TFBS_LIB ;;
     prof_*)
       w=${st#prof_}
       bash tools/profile_round.sh ${T}_prof_$w --workload $w || exit 1 ;;
