@@ -17,6 +17,7 @@
 // block that would not shrink is stored (BTYPE 00).
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <string>
 
 #include "bgzf_gpu.hpp"
@@ -106,6 +107,8 @@ struct StRow {
     uint32_t tok_at;       // Stage::tlen / text slot of token 0
     uint32_t g_lo, ncum;   // cum entries [g_lo, g_lo + ncum) at cum_at
     uint32_t cum_at;
+    uint32_t tok, nv, width, cum_off;  // the row's (DevRow): its staging reads them from the plan
+    uint64_t code_off;
 };
 
 struct BlockPlan {
@@ -488,13 +491,16 @@ __global__ __launch_bounds__(256) void bgzf_plan_kernel(BgArgs A, uint32_t n_blo
         const uint32_t s_lo = (g_lo ? g_lo - 1 : 0) * kCumGroup, s_hi = min(A.n_samples, (g_hi + 1) * kCumGroup);
         const uint32_t cb0 = s_lo * R.width / 8, cb1 = (s_hi * R.width + 7) / 8;
         const uint32_t ncum = g_hi - g_lo + 2;
-        if (n == kStRows || code_used + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok ||
+        // (the codes at the source's offset mod 4: bgzf_wave_kernel copies dwords)
+        const uint32_t code_at = ((code_used + 3) & ~3u) + (uint32_t)((R.code_off + cb0) & 3u);
+        if (n == kStRows || code_at + (cb1 - cb0) > kStCodes || tok_used + R.nv > kStTok ||
             cum_used + ncum > kStCum) {
             all = false;
             break;
         }
-        P.st[n] = StRow{r, s_lo, s_hi, cb0, code_used, tok_used, g_lo, ncum, cum_used};
-        code_used += cb1 - cb0;
+        P.st[n] = StRow{r, s_lo, s_hi, cb0, code_at, tok_used, g_lo, ncum, cum_used, R.tok, R.nv, R.width, R.cum_off,
+                        R.code_off};
+        code_used = code_at + (cb1 - cb0);
         tok_used += R.nv;
         cum_used += ncum;
         n++;
@@ -638,8 +644,13 @@ __shared__ uint32_t g_red[kWv / 64];
 __shared__ uint32_t g_pub[kWvItems];  // item i's end bit + 1 (0: not yet known; wv_place)
 __shared__ uint32_t g_agg[kWvItems];  // item i's bit count + 1 (0: not yet known; wv_place)
 // TFBS_BGZF_PROF counts: wv_place's waits; items all-run, with look-back matches,
-// with whole-token literals, with byte literals; heads; newlines
-__shared__ uint32_t g_pstat[8];
+// with whole-token literals, with byte literals; heads; newlines; other groups; then
+// wave-cycles of run groups' counts, of deferred emits, -, of other groups' counts, of
+// byte-literal groups, -; other groups on the serial look-back
+__shared__ uint32_t g_pstat[16];
+__device__ __forceinline__ void wv_pcycles(const BgArgs &A, uint32_t lane, uint32_t k, uint64_t t0) {
+    if (A.prof && lane == 0) atomicAdd(&g_pstat[k], (uint32_t)(clock64() - t0));
+}
 
 // A lane's bit stream: symbols gathered in a register, ORed into g_bits 32 bits at
 // a time (two LDS atomics at most per 32 bits, not per symbol)
@@ -740,11 +751,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 // Every item publishes its count before it looks back and waits only on lower
 // items, so all counts arrive (items go to the waves round-robin, in order).
 // Then item i's end is published.
-__device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_t lane) {
+__device__ __forceinline__ void wv_publish(uint32_t i, uint32_t total, uint32_t lane) {
+    if (lane == 0) __hip_atomic_store(&g_agg[i], total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t wv_lookback(uint32_t i, uint32_t total, uint32_t lane) {
 #ifdef BG_PROBE_NOPLACE  // (timing probe: no look-back, wrong offsets)
     if (total != 0xFFFFFFFFu) return 64 * 128 * (i & 3);
 #endif
-    if (lane == 0) __hip_atomic_store(&g_agg[i], total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     uint32_t acc = 3;  // BFINAL + BTYPE before item 0
     for (int32_t hi = (int32_t)i; hi > 0;) {
         const int32_t j = hi - 1 - (int32_t)lane;
@@ -771,13 +784,67 @@ __device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_
     if (lane == 0) __hip_atomic_store(&g_pub[i], acc + total + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return acc;
 }
+__device__ __forceinline__ uint32_t wv_place(uint32_t i, uint32_t total, uint32_t lane) {
+    wv_publish(i, total, lane);
+    return wv_lookback(i, total, lane);
+}
 
-// Item i of the block (all lanes of a wave together), in one pass: its bytes into
-// g_text, its bit count, its first bit (wv_place), its symbols.
+// A lane's symbols as up to 4 words (LSB first, bn bits) at stream bit off: at most
+// two LDS ORs each (bits past the buffer: the block is stored)
+__device__ __forceinline__ void wv_words(uint32_t off, const uint32_t (&bw)[4], uint32_t bn) {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        if (!__ballot(bn > 32 * k)) break;
+        if (bn > 32 * k) {
+            const uint32_t o = off + 32 * k, w = o >> 5, sh = o & 31, nk = min(bn - 32 * k, 32u);
+            if (w <= kBitWords) atomicOr(&g_bits[w], bw[k] << sh);
+            if (sh + nk > 32 && w < kBitWords) atomicOr(&g_bits[w + 1], bw[k] >> (32 - sh));
+        }
+    }
+}
+
+// A group item whose symbols wait for their place: its bit count (wave-uniform) and
+// each lane's symbol words.  A wave counts its next item before it places this one,
+// so that the look-back's wait overlaps that work (wv_emit).
+struct Pend {
+    uint32_t i;  // the item (~0u: none)
+    uint32_t total;
+    uint32_t bw[4], bn;
+};
+__device__ __forceinline__ void wv_emit(const BgArgs &A, const Pend &p, uint32_t lane) {
+    const uint64_t pt0 = A.prof ? clock64() : 0;
+    const uint32_t base = wv_lookback(p.i, p.total, lane);
+#ifdef BG_PROBE_NOBITS
+    if (base == 0xFFFFFFFFu)
+#endif
+    wv_words(base + wave_excl_sum(p.bn, lane), p.bw, p.bn);
+    wv_pcycles(A, lane, 9, pt0);
+}
+
+// A whole text at block byte rel (>= 0, inside the block) into g_text: its dwords,
+// ORed (neighbouring texts share edge dwords; the staged text's bytes past its length
+// are zero)
+__device__ __forceinline__ void wv_text_or(int32_t rel, uint32_t t, const uint4 &tx) {
+    const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
+    const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
+    uint32_t prev = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 5; j++) {
+        const uint32_t dw = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
+        prev = T[j];
+        if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), dw);
+    }
+}
+
+// Item i of the block (all lanes of a wave together): its bytes into g_text, its bit
+// count; then a group's symbols go to *out (placed by wv_emit), the other items' (and
+// groups with byte literals) are placed (wv_place) and written at once (out->i = ~0u).
 // v / vkey: the wave's last item's row view and its key (item bits 20-31), kept
 // across the wave's items (consecutive ones are mostly groups of one row).
 __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane,
-                        RowView &v, uint32_t &vkey) {
+                        RowView &v, uint32_t &vkey, Pend &out) {
+    const uint64_t pt0 = A.prof ? clock64() : 0;
+    out.i = ~0u;
     const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_item[i]);
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
     // the item's row as wave-uniform values (SGPRs: its arithmetic is scalar)
@@ -846,21 +913,52 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const uint32_t g = item & 0xFFFFFu, N = A.n_samples;
     const uint32_t s = g * kCumGroup + lane;
     const bool valid = s < N;
+    // the sample's code and the one before's, then its text (one round of LDS reads each)
     uint32_t c = 0, t = 0;
-    if (valid) {
-        c = C.code(v, s);
-        t = C.tlen(v, c);
-    }
-    const uint4 tx = C.ttext(v, c);
-    // the text's first byte relative to the block start (may be negative at its edge)
+    const uint32_t prevc = valid && s > 0 ? C.code(v, s - 1) : 0xFFFFFFFFu;
+    if (valid) c = C.code(v, s);
     const uint32_t cum_g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_st.cum[v.cum_at + g - v.g_lo]);
+    const int32_t n = (int32_t)(e - b0);
+    if (valid) t = C.tlen(v, c);
+    const uint4 tx = C.ttext(v, c);
+#ifndef BG_NO_RUN_GROUPS
+    // a group of 64 samples of one text that the sample before it also has, inside the
+    // block (most groups): one run, so its symbols follow from the run's length alone --
+    // the same symbols as the general path below makes for it (its texts all run, the
+    // run starting at lane 0): 258-byte matches at distance t, then the remainder r
+    // (r = 1, 2: the last whole match gives 3 - r bytes to a final 3-byte match)
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+    if (g > 0 && g * kCumGroup + kCumGroup <= N && __ballot(c == c0) == ~0ull &&
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)prevc) == c0) {
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
+        const int32_t rel0 = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0);
+        if (t0 >= 1 && rel0 >= (int32_t)t0 && rel0 + (int32_t)(kCumGroup * t0) <= n) {
+            wv_text_or(rel0 + (int32_t)(lane * t0), t0, tx);
+            const uint32_t Lr = kCumGroup * t0, nfull = Lr / 258, r = Lr % 258;
+            const bool split = r == 1 || r == 2;
+            const uint32_t n258 = split ? nfull - 1 : nfull;
+            const uint2 M = match_code(258, t0);
+            const uint2 X = split ? match_code(255 + r, t0) : (r ? match_code(r, t0) : uint2{0, 0});
+            const uint2 Y = split ? match_code(3, t0) : uint2{0, 0};
+            if (A.prof && lane == 0) atomicAdd(&g_pstat[1], 1u);
+            const uint2 sym = lane < n258 ? M : (lane == n258 ? X : (lane == n258 + 1 ? Y : uint2{0, 0}));
+            out.total = n258 * M.y + X.y + Y.y;
+            out.bw[0] = sym.x;
+            out.bw[1] = out.bw[2] = out.bw[3] = 0;
+            out.bn = sym.y;  // (lane k's symbol starts after lanes 0 .. k - 1's)
+            wv_publish(i, out.total, lane);
+            out.i = i;
+            wv_pcycles(A, lane, 8, pt0);
+            return;
+        }
+    }
+#endif
+    // the text's first byte relative to the block start (may be negative at its edge)
     const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0) +
                         (int32_t)wave_excl_sum(t, lane);
-    const int32_t n = (int32_t)(e - b0);
     const int32_t lo = max(rel, 0), hi = min(rel + (int32_t)t, n);
     const bool in = valid && hi > lo;
     const bool full = in && rel >= 0 && rel + (int32_t)t <= n;
-    const uint32_t prevc = valid && s > 0 ? C.code(v, s - 1) : 0xFFFFFFFFu;
     const bool run = full && prevc == c && rel >= (int32_t)t && t >= 1;
     // the wave's runs: a run's first and last texts
     const uint64_t rm = __ballot(run);
@@ -934,16 +1032,8 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     if (false) {
 #else
     if (full) {
-#endif  // its dwords, ORed (neighbouring texts share edge dwords)
-        const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
-        const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
-        uint32_t prev = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < 5; j++) {
-            const uint32_t dw = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
-            prev = T[j];
-            if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), dw);
-        }
+#endif
+        wv_text_or(rel, t, tx);
     } else if (in) {
         for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
     }
@@ -976,33 +1066,35 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         for (int32_t q = lo; q < hi; q++) nb += lit_bits(Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     if (A.prof) {
         const bool all_run = __ballot(run) == ~0ull, lb = __ballot(dist != 0) != 0,
-                   wl = __ballot(!runm && !dist && whole_lit) != 0;
+                   wl = __ballot(!runm && !dist && whole_lit) != 0, ser = __ballot(want && !packed) != 0;
         if (lane == 0) {
+            atomicAdd(&g_pstat[7], 1u);
+            if (ser) atomicAdd(&g_pstat[14], 1u);
             if (all_run) atomicAdd(&g_pstat[1], 1u);
             if (lb) atomicAdd(&g_pstat[2], 1u);
             if (wl) atomicAdd(&g_pstat[3], 1u);
             if (any_bytes) atomicAdd(&g_pstat[4], 1u);
         }
     }
-    const uint32_t base = wv_place(i, wave_sum(nb), lane);
-    const uint32_t off = base + wave_excl_sum(nb, lane);
-#ifdef BG_PROBE_NOBITS
-    if (off == 0xFFFFFFFFu)
-#endif
+    const uint32_t total = wave_sum(nb);
+    if (!any_bytes) {  // (nb == bn)
+        wv_publish(i, total, lane);
+        out.total = total;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        if (!__ballot(bn > 32 * k)) break;
-        if (bn > 32 * k) {
-            const uint32_t o = off + 32 * k, w = o >> 5, sh = o & 31, nk = min(bn - 32 * k, 32u);
-            if (w <= kBitWords) atomicOr(&g_bits[w], bw[k] << sh);
-            if (sh + nk > 32 && w < kBitWords) atomicOr(&g_bits[w + 1], bw[k] >> (32 - sh));
-        }
+        for (uint32_t k = 0; k < 4; k++) out.bw[k] = bw[k];
+        out.bn = bn;
+        out.i = i;
+        wv_pcycles(A, lane, 11, pt0);
+        return;
     }
-    if (any_bytes && by_byte) {
+    const uint32_t off = wv_place(i, total, lane) + wave_excl_sum(nb, lane);
+    wv_words(off, bw, bn);
+    if (by_byte) {
         LaneBits o{0, 0, off};
         for (int32_t q = lo; q < hi; q++) wv_lit(o, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
         o.finish();
     }
+    wv_pcycles(A, lane, 12, pt0);
 }
 
 __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
@@ -1012,61 +1104,126 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     const uint32_t n = (uint32_t)min((uint64_t)kBgzfRaw, A.text_bytes - b0);
     const uint64_t e = b0 + n;
     // phase clocks (TFBS_BGZF_PROF): start, staged, items listed, items done, CRC, end
-    uint64_t *const pf = A.prof ? A.prof + 16 * (size_t)blockIdx.x : nullptr;
+    uint64_t *const pf = A.prof ? A.prof + 32 * (size_t)blockIdx.x : nullptr;
     auto stamp = [&](int k) {
         if (pf && tid == 0) pf[k] = clock64();
     };
     stamp(0);
-    if (tid < 8) g_pstat[tid] = 0;
+    if (tid < 16) g_pstat[tid] = 0;
     {
         const uint32_t *src = reinterpret_cast<const uint32_t *>(reinterpret_cast<const BlockPlan *>(A.plans) + blockIdx.x);
         for (uint32_t i = tid; i < sizeof(BlockPlan) / 4; i += kWv) reinterpret_cast<uint32_t *>(&S.P)[i] = src[i];
     }
     __syncthreads();
     if (!S.P.all) return;  // (uniform) bgzf_block_kernel's block
+    // the block's reads as one flat list of segments -- the CRC tables, the rows'
+    // descriptors, per staged row its codes (dwords from the aligned-down source: the
+    // plan put code_at at the same offset mod 4), token texts, token lengths (bytes) and
+    // group offsets --, every thread issuing its loads before its stores (a loop per
+    // segment waited on one load per segment).  The list lives in g_item (listed later):
+    // [0, 64) source low words, [64, 128) high words, [128, 192) Stage byte offset (bit
+    // 31: a byte segment), [192, 256) the segments' inclusive end in units.
+    for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
+    for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
+    for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
+    if (wave == 0) {
+        static_assert(4 + 4 * kStRows <= 64 && 256 <= kWvItems, "the segment list");
+        uint64_t src = 0;
+        uint32_t dst = 0, nu = 0;
+        if (lane == 0) {
+            src = (uint64_t)A.crc_tab;
+            dst = offsetof(Stage, crc_tab);
+            nu = 256;
+        } else if (lane == 1) {
+            src = (uint64_t)A.crc_ops;
+            dst = offsetof(Stage, crc_ops);
+            nu = kCrcOps * 32;
+        } else if (lane == 2) {
+            src = (uint64_t)A.crc_slice;
+            dst = offsetof(Stage, crc_slice);
+            nu = 768;
+        } else if (lane == 3) {
+            src = (uint64_t)(A.rows + S.P.r_first);
+            dst = offsetof(Stage, rows);
+            nu = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
+        } else if (lane < 4 + 4 * S.P.n_st) {
+            const uint32_t k = (lane - 4) >> 2, m = (lane - 4) & 3;
+            const StRow &T = S.P.st[k];
+            if (m == 0) {
+                const uint64_t a = T.code_off + T.cfirst;
+                const uint32_t lead = (uint32_t)(a & 3u), nb = (T.s_hi * T.width + 7) / 8 - T.cfirst;
+                src = (uint64_t)(A.codes + (a - lead));
+                dst = (uint32_t)offsetof(Stage, codes) + T.code_at - lead;
+                nu = (lead + nb + 3) / 4;
+            } else if (m == 1) {
+                src = (uint64_t)(A.tok_text + (size_t)T.tok * kRowTokBytes);
+                dst = (uint32_t)offsetof(Stage, text) + T.tok_at * kRowTokBytes;
+                nu = T.nv * (kRowTokBytes / 4);
+            } else if (m == 2) {
+                src = (uint64_t)(A.tok_len + T.tok);
+                dst = ((uint32_t)offsetof(Stage, tlen) + T.tok_at) | 0x80000000u;
+                nu = T.nv;
+            } else {
+                src = (uint64_t)(A.cum + T.cum_off + T.g_lo);
+                dst = (uint32_t)offsetof(Stage, cum) + 4 * T.cum_at;
+                nu = T.ncum;
+            }
+        }
+        g_item[lane] = (uint32_t)src;
+        g_item[64 + lane] = (uint32_t)(src >> 32);
+        g_item[128 + lane] = dst;
+        g_item[192 + lane] = wave_incl_sum(nu);  // (lanes past the list: the total)
+    }
+    __syncthreads();
     {
-        for (uint32_t i = tid; i < 256; i += kWv) S.crc_tab[i] = A.crc_tab[i];
-        for (uint32_t i = tid; i < kCrcOps * 32; i += kWv) S.crc_ops[i] = A.crc_ops[i];
-        for (uint32_t i = tid; i < 768; i += kWv) S.crc_slice[i] = A.crc_slice[i];
-        for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-        for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
-        const uint32_t nd = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(A.rows + S.P.r_first);
-        for (uint32_t i = tid; i < nd; i += kWv) reinterpret_cast<uint32_t *>(S.rows)[i] = src[i];
-        for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
-        __syncthreads();  // (S.rows: the staged rows' descriptors from LDS below, not a second global read)
-        for (uint32_t k = 0; k < S.P.n_st; k++) {
-            const StRow T = S.P.st[k];
-            const DevRow R = S.rows[T.row - S.P.r_first];
-            const uint32_t nb = (T.s_hi * R.width + 7) / 8 - T.cfirst;
-            for (uint32_t i = tid; i < nb; i += kWv) S.codes[T.code_at + i] = A.codes[R.code_off + T.cfirst + i];
-            for (uint32_t i = tid; i < R.nv; i += kWv) S.tlen[T.tok_at + i] = A.tok_len[R.tok + i];
-            for (uint32_t i = tid; i < R.nv * kRowTokBytes; i += kWv)
-                S.text[T.tok_at * kRowTokBytes + i] = (uint8_t)A.tok_text[(size_t)R.tok * kRowTokBytes + i];
-            for (uint32_t i = tid; i < T.ncum; i += kWv) S.cum[T.cum_at + i] = A.cum[R.cum_off + T.g_lo + i];
+        uint8_t *const sb = reinterpret_cast<uint8_t *>(&g_st);
+        const uint32_t total = g_item[192 + 63];
+        for (uint32_t u0 = tid; u0 < total; u0 += 4 * kWv) {
+            uint32_t val[4], at[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                const uint32_t u = u0 + j * kWv;
+                at[j] = ~0u;
+                val[j] = 0;
+                if (u < total) {
+                    uint32_t k = 0;  // the first segment ending past u
+#pragma unroll
+                    for (uint32_t b = 32; b; b >>= 1)
+                        if (g_item[192 + k + b - 1] <= u) k += b;
+                    const uint32_t idx = u - (k ? g_item[192 + k - 1] : 0u), d = g_item[128 + k];
+                    const uint64_t src = (uint64_t)g_item[k] | ((uint64_t)g_item[64 + k] << 32);
+                    if (d >> 31) {
+                        val[j] = *reinterpret_cast<const uint8_t *>(src + idx);
+                        at[j] = d + idx;
+                    } else {
+                        val[j] = *reinterpret_cast<const uint32_t *>(src + 4 * (uint64_t)idx);
+                        at[j] = d + 4 * idx;
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < 4; j++) {
+                if (at[j] == ~0u) continue;
+                if (at[j] >> 31) sb[at[j] & 0x7FFFFFFFu] = (uint8_t)val[j];
+                else *reinterpret_cast<uint32_t *>(sb + at[j]) = val[j];
+            }
         }
     }
     __syncthreads();
     stamp(1);
-    // the staged tokens' literal codes (bytes past a text's length zeroed: the text's
-    // dwords are ORed into g_text whole)
+    // the staged tokens' literal codes (tok_lit_kernel zeroed the texts' bytes past their
+    // length: the wave ORs whole text dwords into g_text), on the upper waves (the lower
+    // ones list the items meanwhile)
     {
         uint32_t tok_end = 0;
-        for (uint32_t k = 0; k < S.P.n_st; k++) tok_end = max(tok_end, S.P.st[k].tok_at + S.rows[S.P.st[k].row - S.P.r_first].nv);
-        for (uint32_t k = tid; k < tok_end; k += kWv) {
-            uint4 &tx = reinterpret_cast<uint4 *>(S.text)[k];
-            const uint32_t t = S.tlen[k];
-            uint32_t w[4] = {tx.x, tx.y, tx.z, tx.w};
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int32_t keep = (int32_t)t - 4 * j;  // bytes of dword j inside the text
-                w[j] &= keep >= 4 ? ~0u : (keep <= 0 ? 0u : (1u << (8 * keep)) - 1u);
-            }
-            tx = uint4{w[0], w[1], w[2], w[3]};
+        for (uint32_t k = 0; k < S.P.n_st; k++) tok_end = max(tok_end, S.P.st[k].tok_at + S.P.st[k].nv);
+        for (uint32_t k = (tid + kWv / 2) % kWv; k < tok_end; k += kWv) {
+            const uint4 tx = reinterpret_cast<const uint4 *>(S.text)[k];
+            const uint32_t t = S.tlen[k], w[4] = {tx.x, tx.y, tx.z, tx.w};
             uint64_t lo = 0, hi = 0;
             uint32_t nb = 0;
             for (uint32_t i = 0; i < t && nb <= 128; i++) {
-                const uint32_t b = (w[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+                const uint32_t b = (w[(i >> 2) & 3u] >> (8 * (i & 3))) & 0xFFu;
                 const uint32_t code = b < 144 ? rev(0x30 + b, 8) : rev(0x190 + b - 144, 9), n = b < 144 ? 8u : 9u;
                 if (nb < 64) {
                     lo |= (uint64_t)code << nb;
@@ -1133,17 +1290,37 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     {
         RowView v{};
         uint32_t vkey = ~0u;
-        for (uint32_t i = wave; i < n_items; i += kWv / 64) wv_item(A, C, b0, e, i, lane, v, vkey);
+        Pend pend{~0u, 0, {0, 0, 0, 0}, 0};
+        for (uint32_t i = wave; i < n_items; i += kWv / 64) {
+            Pend cur;
+            wv_item(A, C, b0, e, i, lane, v, vkey, cur);
+#ifdef BG_NO_DEFER  // (timing probe: each group placed at once)
+            if (cur.i != ~0u) wv_emit(A, cur, lane);
+            continue;
+#endif
+            if (pend.i != ~0u) wv_emit(A, pend, lane);
+            pend = cur;
+        }
+        if (pend.i != ~0u) wv_emit(A, pend, lane);
     }
     __syncthreads();
     stamp(3);
     const uint32_t total_bits = g_pub[n_items - 1] - 1 + 7;  // BFINAL + BTYPE, symbols, end of block
     const uint32_t dbytes = (total_bits + 7) / 8;
     const bool stored = dbytes > 4 * kBitWords;
-    // the CRC32 of the block's bytes: 64 per thread counted from the block's end (so
-    // that thread t's CRC shifts by 64 (kWv - 1 - t) bytes: one operator of the
-    // table), XORed
+    // the CRC32 of the block's bytes: 64 per thread counted from the block's end, so
+    // that thread t's CRC shifts by 64 (kWv - 1 - t) = 64 (63 - lane) + 4096 (15 - wave)
+    // bytes: each lane applies its lane operator (x^(8 * 64 (63 - lane)), a column per
+    // register from the table, coalesced), the wave XORs and applies its wave operator
+    // (x^(8 * 4096 (15 - wave)); the tables' reads issued before the slice), then wave 0
+    // XORs the waves' (CRC(a b) = x^(8 |b|) CRC(a) ^ CRC(b)) and the init term (a full
+    // block's precomputed)
     {
+        uint32_t col[32], wcol[32];
+#pragma unroll
+        for (uint32_t i = 0; i < 32; i++) col[i] = A.crc_lane[i * 64 + lane];
+#pragma unroll
+        for (uint32_t i = 0; i < 32; i++) wcol[i] = A.crc_lane[64 * 32 + 32 * wave + i];
         const int32_t q1 = (int32_t)n - 64 * (kWv - 1 - (int32_t)tid), q0 = max(0, q1 - 64);
         uint32_t crc = 0;
         if (q1 - q0 == 64 && (q0 & 63) == 0) {  // a whole padded slice: dword reads, no bank conflicts
@@ -1156,35 +1333,22 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         } else {
             for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[txt_at((uint32_t)q)]);
         }
-        // CRC(a b) = x^(8 |b|) CRC(a) ^ CRC(b): thread t's bytes precede t + 1's and every
-        // slice after the first non-empty one holds 64 bytes, so a binary tree over the
-        // threads shifts by 64 x 2^k bytes at level k (operator k + 6, in LDS: the same
-        // columns for every lane); 6 levels in the wave, 4 over the waves' results, then
-        // the init term (a full block's precomputed)
-        auto apply = [&](const uint32_t *M, uint32_t x) {
-            uint32_t r = 0;
+        uint32_t r = 0;
 #pragma unroll
-            for (uint32_t i = 0; i < 32; i++) r ^= ((x >> i) & 1u) ? M[i] : 0u;
-            return r;
-        };
+        for (uint32_t i = 0; i < 32; i++) r ^= ((crc >> i) & 1u) ? col[i] : 0u;
 #pragma unroll
-        for (uint32_t k = 0; k < 6; k++) {
-            const uint32_t other = (uint32_t)__shfl_down((int)crc, 1u << k);
-            const uint32_t c2 = apply(S.crc_ops + 32 * (k + 6), crc) ^ other;
-            if ((lane & ((2u << k) - 1u)) == 0) crc = c2;
-        }
-        if (lane == 0) g_red[wave] = crc;
+        for (uint32_t o = 32; o; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, (int)o);
+        uint32_t rw = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 32; i++) rw ^= ((r >> i) & 1u) ? wcol[i] : 0u;
+        if (lane == 0) g_red[wave] = rw;
         __syncthreads();
         if (wave == 0) {
-            crc = lane < kWv / 64 ? g_red[lane] : 0u;
+            r = lane < kWv / 64 ? g_red[lane] : 0u;
 #pragma unroll
-            for (uint32_t k = 6; k < 10; k++) {
-                const uint32_t other = (uint32_t)__shfl_down((int)crc, 1u << (k - 6));
-                const uint32_t c2 = apply(S.crc_ops + 32 * (k + 6), crc) ^ other;
-                if ((lane & ((2u << (k - 6)) - 1u)) == 0) crc = c2;
-            }
+            for (uint32_t o = 8; o; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, (int)o);
             if (lane == 0)
-                g_red[0] = crc ^ (n == kBgzfRaw ? A.crc_full : crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n)) ^ 0xFFFFFFFFu;
+                g_red[0] = r ^ (n == kBgzfRaw ? A.crc_full : crc_shift_lds(S.crc_ops, 0xFFFFFFFFu, n)) ^ 0xFFFFFFFFu;
         }
         __syncthreads();
     }
@@ -1232,7 +1396,21 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     stamp(5);
     if (pf && tid == 0) {
         pf[6] = n_items;
-        for (int k = 0; k < 8; k++) pf[8 + k] = g_pstat[k];
+        for (int k = 0; k < 16; k++) pf[8 + k] = g_pstat[k];
+    }
+}
+
+// Per token of the launch's rows: its text's bytes past its length zeroed (the wave
+// kernel ORs whole text dwords into the block's bytes).
+__global__ __launch_bounds__(256) void tok_mask_kernel(uint32_t *__restrict__ text, const uint8_t *__restrict__ len,
+                                                       uint32_t n_tok) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n_tok) return;
+    const uint32_t t = len[k];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int32_t keep = (int32_t)t - 4 * j;  // bytes of dword j inside the text
+        if (keep < 4) text[4 * k + j] &= keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
     }
 }
 
@@ -1271,7 +1449,7 @@ __global__ __launch_bounds__(256) void bgzf_compact_kernel(const uint8_t *__rest
 
 }  // namespace
 
-uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice) {
+uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice, uint32_t *lane) {
     for (uint32_t i = 0; i < 256; i++) {
         uint32_t c = i;
         for (int k = 0; k < 8; k++) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
@@ -1297,16 +1475,33 @@ uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice) {
             slice[256 * k + i] = c;
         }
     }
-    // x^(8 kBgzfRaw) on 0xFFFFFFFF: the operators of kBgzfRaw's set bits in turn
-    uint32_t v = 0xFFFFFFFFu;
-    for (uint32_t k = 0, n = kBgzfRaw; n; k++, n >>= 1)
-        if (n & 1u) {
-            uint32_t r = 0;
-            for (uint32_t j = 0; j < 32; j++)
-                if ((v >> j) & 1u) r ^= ops[32 * k + j];
-            v = r;
-        }
-    return v;
+    // x^(8 n) on v: the operators of n's set bits in turn
+    auto shift = [&](uint32_t v, uint32_t n) {
+        for (uint32_t k = 0; n; k++, n >>= 1)
+            if (n & 1u) {
+                uint32_t r = 0;
+                for (uint32_t j = 0; j < 32; j++)
+                    if ((v >> j) & 1u) r ^= ops[32 * k + j];
+                v = r;
+            }
+        return v;
+    };
+    // bgzf_wave_kernel's lane operators x^(8 * 64 (63 - l)), column i of lane l at
+    // [64 i + l], then its wave operators x^(8 * 4096 (15 - w)), column i at [2048 + 32 w + i]
+    for (uint32_t l = 0; l < 64; l++)
+        for (uint32_t i = 0; i < 32; i++) lane[64 * i + l] = shift(1u << i, 64 * (63 - l));
+    for (uint32_t w = 0; w < 16; w++)
+        for (uint32_t i = 0; i < 32; i++) lane[64 * 32 + 32 * w + i] = shift(1u << i, 4096 * (15 - w));
+    return shift(0xFFFFFFFFu, kBgzfRaw);  // (on 0xFFFFFFFF: a full block's init term)
+}
+
+int launch_tok_mask(const BgArgs &a, uint32_t n_tok, hipStream_t stream) {
+    if (n_tok == 0) return TFBS_OK;
+    hipLaunchKernelGGL(tok_mask_kernel, dim3((n_tok + 255) / 256), dim3(256), 0, stream,
+                       reinterpret_cast<uint32_t *>(const_cast<char *>(a.tok_text)), a.tok_len, n_tok);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("tok_mask_kernel: ") + hipGetErrorString(e));
+    return TFBS_OK;
 }
 
 int launch_row_cum(const BgArgs &a, hipStream_t stream) {

@@ -16,7 +16,7 @@ struct BgArgs {
     const DevRow *rows;
     uint32_t n_rows;
     const char *heads;
-    const char *tok_text;       // kRowTokBytes per token slot
+    const char *tok_text;       // kRowTokBytes per token slot (bytes past the length zeroed: launch_tok_mask)
     const uint8_t *tok_len;
     const uint8_t *codes;       // the encoded keys' packed codes (tfbs_batch_encode's compact buffer)
     uint32_t *cum;              // per row (DevRow::cum_off): (n_samples + 63) / 64 + 1 genotype text offsets
@@ -28,16 +28,20 @@ struct BgArgs {
     const uint32_t *crc_tab;    // CRC32 byte table
     const uint32_t *crc_ops;    // kBgzfOps x 32 columns
     const uint32_t *crc_slice;  // slice-by-4 tables 1-3 (3 x 256; table 0 is crc_tab)
+    const uint32_t *crc_lane;   // bgzf_wave_kernel's lane and wave shift operators (bgzf_crc_tables)
     uint32_t crc_full;          // x^(8 kBgzfRaw) applied to 0xFFFFFFFF (a full block's CRC init term)
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
-    uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 16 words of phase clocks and counts
+    uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 32 words of phase clocks and counts
 };
 size_t bgzf_plan_bytes();
 
-// CRC32 table, the x^(8 * 2^k) operators and the slice-by-4 tables 1-3 (host side,
-// uploaded once: 256 + 32 kBgzfOps + 768 words); returns crc_full.
-constexpr size_t kBgzfCrcWords = 256 + 32 * kBgzfOps + 768;
-uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice);
+// CRC32 table, the x^(8 * 2^k) operators, the slice-by-4 tables 1-3 and the wave
+// kernel's lane and wave operators (host side, uploaded once: 256 + 32 kBgzfOps + 768 +
+// 32 x 64 + 32 x 16 words); returns crc_full.
+constexpr size_t kBgzfCrcWords = 256 + 32 * kBgzfOps + 768 + 32 * 64 + 32 * 16;
+uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice, uint32_t *lane);
+// Per token: the text's bytes past its length zeroed.
+int launch_tok_mask(const BgArgs &a, uint32_t n_tok, hipStream_t stream);
 // Per row: its genotype text offsets every 64 samples.
 int launch_row_cum(const BgArgs &a, hipStream_t stream);
 // Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a

@@ -1568,7 +1568,7 @@ int tfbs_batch_encode_flags(tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, 
         }
         const uint64_t total = B.enc_code_off[nk];
         if ((rc = ctx->enc_off.put(B.enc_code_off, ctx->stream)) ||
-            (rc = ctx->enc_packed.ensure(std::max<uint64_t>(total, 1))) ||
+            (rc = ctx->enc_packed.ensure(total + 16)) ||  // (the BGZF staging reads whole dwords)
             (!(flags & TFBS_ENC_DEVICE_CODES) && (rc = B.enc_codes.reserve(total))))
             return rc;
         if ((rc = launch_code_compact(ctx->enc_codes.p, (uint32_t)nk, N, ctx->enc_off.p, ctx->enc_packed.p,
@@ -1632,18 +1632,18 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
 
 // TFBS_BGZF_PROF: the launch's bgzf_wave_kernel phase clocks (debug; synchronises).
 static int bgzf_prof_report(tfbs_ctx *ctx, uint32_t nb) {
-    std::vector<uint64_t> h((size_t)nb * 16);
+    std::vector<uint64_t> h((size_t)nb * 32);
     HIP_TRY(hipMemcpyAsync(h.data(), ctx->bg_prof.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    double ph[5] = {0, 0, 0, 0, 0}, items = 0, st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    double ph[5] = {0, 0, 0, 0, 0}, items = 0, st[16] = {};
     uint32_t nw = 0;
     for (uint32_t b = 0; b < nb; b++) {
-        const uint64_t *p = &h[(size_t)b * 16];
+        const uint64_t *p = &h[(size_t)b * 32];
         if (!p[5]) continue;  // a bgzf_block_kernel block
         nw++;
         for (int k = 0; k < 5; k++) ph[k] += (double)(p[k + 1] - p[k]);
         items += (double)p[6];
-        for (int k = 0; k < 8; k++) st[k] += (double)p[8 + k];
+        for (int k = 0; k < 16; k++) st[k] += (double)p[8 + k];
     }
     const double d = nw ? nw : 1;
     fprintf(stderr,
@@ -1651,6 +1651,12 @@ static int bgzf_prof_report(tfbs_ctx *ctx, uint32_t nb) {
             "items %.1f spins %.1f all-run %.1f look-back %.1f token-lit %.1f byte-lit %.1f heads %.1f newlines %.1f\n",
             nb, nw, ph[0] / d, ph[1] / d, ph[2] / d, ph[3] / d, ph[4] / d, items / d, st[0] / d, st[1] / d, st[2] / d,
             st[3] / d, st[4] / d, st[5] / d, st[6] / d);
+    // wave-cycles per block: counting run groups / other groups, the deferred emits, the
+    // groups with byte literals; other groups, those on the sample-by-sample look-back
+    fprintf(stderr,
+            "[bgzf prof] item cycles/block: count run groups %.0f, other groups %.0f; emit %.0f; byte-literal groups "
+            "%.0f; other groups %.1f, on the serial look-back %.1f\n",
+            st[8] / d, st[11] / d, st[9] / d, st[12] / d, st[7] / d, st[14] / d);
     return TFBS_OK;
 }
 
@@ -1675,7 +1681,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     }
     if (!ctx->bg_crc.n) {  // CRC32 byte table, shift operators and slice tables, once per ctx
         std::vector<uint32_t> t(tfbs::kBgzfCrcWords);
-        ctx->bg_crc_full = tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps);
+        ctx->bg_crc_full = tfbs::bgzf_crc_tables(t.data(), t.data() + 256, t.data() + 256 + 32 * kBgzfOps,
+                                                 t.data() + 256 + 32 * kBgzfOps + 768);
         if ((rc = ctx->bg_crc.put(t, ctx->stream))) return rc;
         HIP_TRY(hipStreamSynchronize(ctx->stream));  // (t goes out of scope)
     }
@@ -1698,8 +1705,11 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.crc_tab = ctx->bg_crc.p;
     a.crc_ops = ctx->bg_crc.p + 256;
     a.crc_slice = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
+    a.crc_lane = ctx->bg_crc.p + 256 + 32 * kBgzfOps + 768;
     a.crc_full = ctx->bg_crc_full;
-    if ((rc = tfbs::launch_row_cum(a, ctx->stream))) return rc;
+    if ((rc = tfbs::launch_tok_mask(a, (uint32_t)plan.tok_len.size(), ctx->stream)) ||
+        (rc = tfbs::launch_row_cum(a, ctx->stream)))
+        return rc;
     // blocks per launch (512 MiB of block slots); TFBS_BGZF_BATCH_BLOCKS=n: smaller
     // launches, so one call cycles the kBgSlots slots (the tests' path)
     const uint64_t kBatchBlocks = (uint64_t)std::max(1, env_int("TFBS_BGZF_BATCH_BLOCKS", 8192));
@@ -1727,8 +1737,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
         a.out_len = ctx->bg_out_len[k].p;
         static const bool prof = env_int("TFBS_BGZF_PROF", 0) != 0;
         if (prof) {
-            if ((rc = ctx->bg_prof.ensure((size_t)nb * 16))) return rc;
-            HIP_TRY(hipMemsetAsync(ctx->bg_prof.p, 0, (size_t)nb * 128, ctx->stream));
+            if ((rc = ctx->bg_prof.ensure((size_t)nb * 32))) return rc;
+            HIP_TRY(hipMemsetAsync(ctx->bg_prof.p, 0, (size_t)nb * 256, ctx->stream));
             a.prof = ctx->bg_prof.p;
         }
         if ((rc = tfbs::launch_bgzf_blocks(a, nb, ctx->stream)) || (prof && (rc = bgzf_prof_report(ctx, nb))) ||

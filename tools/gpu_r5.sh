@@ -68,6 +68,18 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
         done
       done
       unset TFBS_LIB ;;
+    bpmc_*)  # bpmc_<regions>[:<probe>]: two SQ counter passes over tools/bgzf_only.py (bgzf_wave_kernel's last dispatch)
+      spec=${st#bpmc_}; n=${spec%%:*}; v=base; [ "$spec" != "$n" ] && v=${spec#*:}
+      unset TFBS_LIB; [ $v = base ] || export TFBS_LIB=find-tfbs_amd/lib/probe$v/libtfbs_amd.so
+      for pass in a b; do
+        d=$O/bpmc_${v}_$pass
+        if [ $pass = a ]; then c="SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAVES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
+        else c="SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SALU SQ_INSTS_VMEM_RD"; fi
+        timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $d -o pmc -- python3 tools/bgzf_only.py $n > $d.log 2>&1 || { tail -20 $d.log; exit 1; }
+        python3 tools/pmc_summary.py $d bgzf_wave_kernel > /dev/null || exit 1
+        python3 -c "import json;q=json.load(open('$d/pmc_summary_bgzf_wave_kernel.json'));print('$v $pass', {k: v for k, v in q.items() if not k.startswith('_')})"
+      done
+      unset TFBS_LIB ;;
     prof_*)
       w=${st#prof_}
       bash tools/profile_round.sh ${T}_prof_$w --workload $w || exit 1 ;;
