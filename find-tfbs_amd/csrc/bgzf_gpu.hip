@@ -625,7 +625,10 @@ __global__ __launch_bounds__(kBgBlock) void bgzf_block_kernel(BgArgs A) {
 constexpr int kWv = 1024;             // threads
 constexpr uint32_t kWvItems = 768;    // heads, groups, newlines of a block (<= 2 kStRowDesc + kStCum)
 static_assert(kWvItems >= 2 * kStRowDesc + kStCum, "a block's items");
-enum : uint32_t { IT_HEAD = 0u, IT_GROUP = 1u, IT_NL = 2u };
+// items: a row's head, a 64-sample group, a newline, or a run of 1-15 groups (item
+// bits: kind 30-31, row 23-29, staged row 20-22, run groups 16-19, group 0-15)
+enum : uint32_t { IT_HEAD = 0u, IT_GROUP = 1u, IT_NL = 2u, IT_RUN = 3u };
+constexpr uint32_t kRunGroups = 15;
 
 __shared__ uint32_t g_bits[kBitWords + 1];
 // the block's bytes, 4 bytes of padding after every 64 (so that the CRC's 64-byte
@@ -821,6 +824,14 @@ __device__ __forceinline__ void wv_emit(const BgArgs &A, const Pend &p, uint32_t
     wv_pcycles(A, lane, 9, pt0);
 }
 
+// One byte of the block at q into g_text: ORed into its dword (a byte store racing
+// another wave's OR of a neighbouring text's edge dword loses one of them: every
+// g_text write is an OR)
+__device__ __forceinline__ void wv_text_byte(uint32_t q, uint32_t b) {
+    const uint32_t a = txt_at(q);
+    atomicOr(reinterpret_cast<uint32_t *>(g_text + (a & ~3u)), b << (8 * (a & 3u)));
+}
+
 // A whole text at block byte rel (>= 0, inside the block) into g_text: its dwords,
 // ORed (neighbouring texts share edge dwords; the staged text's bytes past its length
 // are zero)
@@ -863,7 +874,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         v.R.cum_off = u32(R.cum_off);
         v.R.nv = u32(R.nv);
         v.mask = (1u << v.R.width) - 1u;
-        if (kind == IT_GROUP) {  // its staged codes, tokens and group offsets (item bits 20-22)
+        if (kind == IT_GROUP || kind == IT_RUN) {  // its staged codes, tokens and group offsets (item bits 20-22)
             const StRow &T = g_st.P.st[(item >> 20) & 7u];
             v.cbase = (int32_t)u32(T.code_at) - (int32_t)u32(T.cfirst);
             v.tok_at = u32(T.tok_at);
@@ -879,7 +890,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     if (kind == IT_NL) {
         const uint32_t base = wv_place(i, 8, lane);
         if (lane == 0) {
-            g_text[txt_at((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0))] = '\n';
+            wv_text_byte((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0), '\n');
             LaneBits o{0, 0, base};
             wv_lit(o, '\n');
             o.finish();
@@ -893,7 +904,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
             const uint64_t q = q0 + lane;
             const bool in = q < he;
             const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
-            if (in) g_text[txt_at((uint32_t)(q - b0))] = (uint8_t)b;
+            if (in) wv_text_byte((uint32_t)(q - b0), b);
             total += wave_sum(in ? lit_bits(b) : 0u);
         }
         uint32_t at = wv_place(i, total, lane);
@@ -909,8 +920,38 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         }
         return;
     }
+    if (kind == IT_RUN) {
+        // G groups of 64 samples of one text that the sample before them also has, inside
+        // the block (bgzf_wave_kernel's listing): one run of 64 G texts, so its symbols
+        // follow from the run's length alone: 258-byte matches at distance t, then the
+        // remainder r (r = 1, 2: the last whole match gives 3 - r bytes to a final 3-byte
+        // match); at most 59 + 2 symbols (G <= 15, t <= 16), a lane each
+        const uint32_t g = item & 0xFFFFu, G = (item >> 16) & 15u;
+        const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)C.code(v, g * kCumGroup));
+        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)C.tlen(v, c0));
+        const uint4 tx = C.ttext(v, c0);
+        const uint32_t cum_g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_st.cum[v.cum_at + g - v.g_lo]);
+        const int32_t rel0 = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0);
+        for (uint32_t j = 0; j < G; j++) wv_text_or(rel0 + (int32_t)((kCumGroup * j + lane) * t0), t0, tx);
+        const uint32_t Lr = kCumGroup * G * t0, nfull = Lr / 258, r = Lr % 258;
+        const bool split = r == 1 || r == 2;
+        const uint32_t n258 = split ? nfull - 1 : nfull;
+        const uint2 M = match_code(258, t0);
+        const uint2 X = split ? match_code(255 + r, t0) : (r ? match_code(r, t0) : uint2{0, 0});
+        const uint2 Y = split ? match_code(3, t0) : uint2{0, 0};
+        if (A.prof && lane == 0) atomicAdd(&g_pstat[1], G);
+        const uint2 sym = lane < n258 ? M : (lane == n258 ? X : (lane == n258 + 1 ? Y : uint2{0, 0}));
+        out.total = n258 * M.y + X.y + Y.y;
+        out.bw[0] = sym.x;
+        out.bw[1] = out.bw[2] = out.bw[3] = 0;
+        out.bn = sym.y;  // (lane k's symbol starts after lanes 0 .. k - 1's)
+        wv_publish(i, out.total, lane);
+        out.i = i;
+        wv_pcycles(A, lane, 8, pt0);
+        return;
+    }
     // a 64-sample group
-    const uint32_t g = item & 0xFFFFFu, N = A.n_samples;
+    const uint32_t g = item & 0xFFFFu, N = A.n_samples;
     const uint32_t s = g * kCumGroup + lane;
     const bool valid = s < N;
     // the sample's code and the one before's, then its text (one round of LDS reads each)
@@ -921,38 +962,6 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const int32_t n = (int32_t)(e - b0);
     if (valid) t = C.tlen(v, c);
     const uint4 tx = C.ttext(v, c);
-#ifndef BG_NO_RUN_GROUPS
-    // a group of 64 samples of one text that the sample before it also has, inside the
-    // block (most groups): one run, so its symbols follow from the run's length alone --
-    // the same symbols as the general path below makes for it (its texts all run, the
-    // run starting at lane 0): 258-byte matches at distance t, then the remainder r
-    // (r = 1, 2: the last whole match gives 3 - r bytes to a final 3-byte match)
-    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-    if (g > 0 && g * kCumGroup + kCumGroup <= N && __ballot(c == c0) == ~0ull &&
-        (uint32_t)__builtin_amdgcn_readfirstlane((int)prevc) == c0) {
-        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-        const int32_t rel0 = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0);
-        if (t0 >= 1 && rel0 >= (int32_t)t0 && rel0 + (int32_t)(kCumGroup * t0) <= n) {
-            wv_text_or(rel0 + (int32_t)(lane * t0), t0, tx);
-            const uint32_t Lr = kCumGroup * t0, nfull = Lr / 258, r = Lr % 258;
-            const bool split = r == 1 || r == 2;
-            const uint32_t n258 = split ? nfull - 1 : nfull;
-            const uint2 M = match_code(258, t0);
-            const uint2 X = split ? match_code(255 + r, t0) : (r ? match_code(r, t0) : uint2{0, 0});
-            const uint2 Y = split ? match_code(3, t0) : uint2{0, 0};
-            if (A.prof && lane == 0) atomicAdd(&g_pstat[1], 1u);
-            const uint2 sym = lane < n258 ? M : (lane == n258 ? X : (lane == n258 + 1 ? Y : uint2{0, 0}));
-            out.total = n258 * M.y + X.y + Y.y;
-            out.bw[0] = sym.x;
-            out.bw[1] = out.bw[2] = out.bw[3] = 0;
-            out.bn = sym.y;  // (lane k's symbol starts after lanes 0 .. k - 1's)
-            wv_publish(i, out.total, lane);
-            out.i = i;
-            wv_pcycles(A, lane, 8, pt0);
-            return;
-        }
-    }
-#endif
     // the text's first byte relative to the block start (may be negative at its edge)
     const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0) +
                         (int32_t)wave_excl_sum(t, lane);
@@ -1035,7 +1044,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
 #endif
         wv_text_or(rel, t, tx);
     } else if (in) {
-        for (int32_t q = lo; q < hi; q++) g_text[txt_at((uint32_t)q)] = (uint8_t)Ctx<true>::byte_of(tx, (uint32_t)(q - rel));
+        for (int32_t q = lo; q < hi; q++) wv_text_byte((uint32_t)q, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
     // its bits, its place in the block's stream, its symbols: a match or two, or a
     // whole token's literal codes, as up to 4 words (LSB first) that go into the
@@ -1124,7 +1133,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     // [0, 64) source low words, [64, 128) high words, [128, 192) Stage byte offset (bit
     // 31: a byte segment), [192, 256) the segments' inclusive end in units.
     for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-    for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
+    for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = 0;
     for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
     if (wave == 0) {
         static_assert(4 + 4 * kStRows <= 64 && 256 <= kWvItems, "the segment list");
@@ -1254,11 +1263,62 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
                 k_st = k;
             }
     };
-    if (tid < S.P.n_rows) {
+    // a group is part of a run when its 64 samples and the one before have one code and
+    // its texts lie inside the block with the text before; up to kRunGroups consecutive
+    // run groups of a row make one IT_RUN item (each starting a new run: the symbols
+    // depend on the run's length only).  A thread per staged group (Stage::cum's index,
+    // the lower waves; the upper ones make the literal codes) tests its packed codes as
+    // whole dwords against the code's byte pattern into g_agg; then one wave per row
+    // turns the flags into items: per group in g_agg bit 0 an item starts here, bit 1 a
+    // run, bits 2-5 the run's groups (cleared before the items).
+    if (tid < kStCum) {
+        bool run = false;
+        for (uint32_t k = 0; k < S.P.n_st; k++) {
+            const StRow &T = S.P.st[k];
+            if (tid < T.cum_at || tid + 1 >= T.cum_at + T.ncum) continue;  // (ncum - 1 groups)
+            const uint32_t g = T.g_lo + tid - T.cum_at, w = T.width;
+            if (g == 0 || g * kCumGroup + kCumGroup > A.n_samples) break;
+            const uint32_t a = T.code_at - T.cfirst + ((g * kCumGroup * w) >> 3);  // (a whole byte)
+            const uint32_t *dw = reinterpret_cast<const uint32_t *>(S.codes) + (a >> 2), sh = 8 * (a & 3u);
+            const uint32_t c = S.codes[a] & ((1u << w) - 1u);
+            const uint32_t pat = (w == 8 ? c : (w == 4 ? c * 0x11u : (w == 2 ? c * 0x55u : (c ? 0xFFu : 0u)))) * 0x01010101u;
+            bool same = ((uint32_t)S.codes[a - 1] >> (8 - w)) == c;  // the sample before
+#pragma unroll
+            for (uint32_t j = 0; j < 16; j++)  // the 2 w dwords of the group's codes
+                if (j < 2 * w) same = same && (uint32_t)((((uint64_t)dw[j + 1] << 32) | dw[j]) >> sh) == pat;
+            const DevRow &R = S.rows[T.row - S.P.r_first];
+            const uint32_t t = S.tlen[T.tok_at + c];
+            const int64_t rel0 = (int64_t)(R.text_off + R.head_len + S.cum[tid]) - (int64_t)b0;
+            run = same && t >= 1 && rel0 >= (int64_t)t && rel0 + kCumGroup * t <= (int64_t)(e - b0);
+            break;
+        }
+        g_agg[tid] = run ? 1u : 0u;
+    }
+    __syncthreads();
+    for (uint32_t r = wave; r < S.P.n_rows; r += kWv / 64) {
         bool head, nl;
         uint32_t groups, k_st;
-        row_items(tid, head, nl, groups, k_st);
-        g_ioff[tid] = (head ? 1u : 0u) + groups + (nl ? 1u : 0u);
+        row_items(r, head, nl, groups, k_st);
+        uint32_t cnt = (head ? 1u : 0u) + (nl ? 1u : 0u);
+        if (groups) {
+            const uint32_t cum_at = S.P.st[k_st].cum_at;
+            for (uint32_t q0 = 0; q0 < groups; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                const bool in = q < groups;
+                const bool run = in && g_agg[cum_at + q] != 0;
+                const uint64_t rb = __ballot(run);
+                const bool link = run && lane > 0 && ((rb >> (lane - 1)) & 1u);  // (a window starts its own item)
+                const uint64_t nl_mask = ~__ballot(link) | 1ull, below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                const uint32_t first = 63u - (uint32_t)__builtin_clzll(nl_mask & below);  // the chain's start lane
+                const bool start = in && (!link || (lane - first) % kRunGroups == 0);
+                const uint64_t sm = __ballot(start);
+                const uint64_t after = lane == 63 ? 0ull : (sm & ~below);
+                const uint32_t next = min(after ? (uint32_t)__builtin_ctzll(after) : 64u, groups - q0);
+                if (in) g_agg[cum_at + q] = start ? (1u | (run ? 2u : 0u) | ((next - lane) << 2)) : 0u;
+                cnt += (uint32_t)__builtin_popcountll(sm);
+            }
+        }
+        if (lane == 0) g_ioff[r] = cnt;
     }
     __syncthreads();
     if (wave == 0) {
@@ -1276,12 +1336,24 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         bool head, nl;
         uint32_t groups, k_st;
         row_items(r, head, nl, groups, k_st);
-        const uint32_t at = g_ioff[r] + (head ? 1u : 0u);
+        uint32_t at = g_ioff[r] + (head ? 1u : 0u);
         if (head && lane == 0) g_item[at - 1] = (IT_HEAD << 30) | (r << 23);
-        for (uint32_t q = lane; q < groups; q += 64)
-            g_item[at + q] = (IT_GROUP << 30) | (r << 23) | (k_st << 20) | (S.P.st[k_st].g_lo + q);
-        if (nl && lane == 0) g_item[at + groups] = (IT_NL << 30) | (r << 23);
+        const StRow &T = S.P.st[k_st];
+        for (uint32_t q0 = 0; q0 < groups; q0 += 64) {
+            const uint32_t q = q0 + lane;
+            const uint32_t f = q < groups ? g_agg[T.cum_at + q] : 0u;
+            const uint64_t sm = __ballot(f & 1u);
+            if (f & 1u) {
+                const uint32_t k = at + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1ull));
+                g_item[k] = ((f & 2u) ? (IT_RUN << 30) | (((f >> 2) & 15u) << 16) : (IT_GROUP << 30)) | (r << 23) |
+                            (k_st << 20) | (T.g_lo + q);
+            }
+            at += (uint32_t)__builtin_popcountll(sm);
+        }
+        if (nl && lane == 0) g_item[at] = (IT_NL << 30) | (r << 23);
     }
+    __syncthreads();
+    for (uint32_t i = tid; i < kWvItems; i += kWv) g_agg[i] = 0;  // (the flags: wv_publish's counts next)
     __syncthreads();
     const uint32_t n_items = g_ioff[kWvItems];
     stamp(2);
@@ -1307,7 +1379,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     stamp(3);
     const uint32_t total_bits = g_pub[n_items - 1] - 1 + 7;  // BFINAL + BTYPE, symbols, end of block
     const uint32_t dbytes = (total_bits + 7) / 8;
-    const bool stored = dbytes > 4 * kBitWords;
+    const bool stored = dbytes > 4 * kBitWords || A.stored;
     // the CRC32 of the block's bytes: 64 per thread counted from the block's end, so
     // that thread t's CRC shifts by 64 (kWv - 1 - t) = 64 (63 - lane) + 4096 (15 - wave)
     // bytes: each lane applies its lane operator (x^(8 * 64 (63 - lane)), a column per

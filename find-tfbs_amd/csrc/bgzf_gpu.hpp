@@ -32,6 +32,7 @@ struct BgArgs {
     uint32_t crc_full;          // x^(8 kBgzfRaw) applied to 0xFFFFFFFF (a full block's CRC init term)
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
     uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 32 words of phase clocks and counts
+    uint32_t stored;            // TFBS_BGZF_STORED=1 (debug): bgzf_wave_kernel's blocks stored, its text as it is
 };
 size_t bgzf_plan_bytes();
 

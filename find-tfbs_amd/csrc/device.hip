@@ -1707,6 +1707,7 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.crc_slice = ctx->bg_crc.p + 256 + 32 * kBgzfOps;
     a.crc_lane = ctx->bg_crc.p + 256 + 32 * kBgzfOps + 768;
     a.crc_full = ctx->bg_crc_full;
+    a.stored = env_int("TFBS_BGZF_STORED", 0) != 0 ? 1u : 0u;
     if ((rc = tfbs::launch_tok_mask(a, (uint32_t)plan.tok_len.size(), ctx->stream)) ||
         (rc = tfbs::launch_row_cum(a, ctx->stream)))
         return rc;
