@@ -859,8 +859,10 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const uint32_t item = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_item[i]);
     const uint32_t kind = item >> 30, d = (item >> 23) & 0x7Fu;
     // the item's row as wave-uniform values (SGPRs: its arithmetic is scalar)
-    if ((item >> 20) != vkey) {
-        vkey = item >> 20;
+    // (the key: row, staged row, and whether the item reads the row's staged groups --
+    // runs and groups of one row share it)
+    if ((((item >> 20) & 0x3FFu) | ((kind & 1u) << 10)) != vkey) {
+        vkey = ((item >> 20) & 0x3FFu) | ((kind & 1u) << 10);
         const DevRow &R = g_st.rows[d];
         auto u32 = [](uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); };
         auto u64 = [&](uint64_t x) { return (uint64_t)u32((uint32_t)x) | ((uint64_t)u32((uint32_t)(x >> 32)) << 32); };
@@ -874,7 +876,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         v.R.cum_off = u32(R.cum_off);
         v.R.nv = u32(R.nv);
         v.mask = (1u << v.R.width) - 1u;
-        if (kind == IT_GROUP || kind == IT_RUN) {  // its staged codes, tokens and group offsets (item bits 20-22)
+        if (kind & 1u) {  // IT_GROUP, IT_RUN: its staged codes, tokens and group offsets (item bits 20-22)
             const StRow &T = g_st.P.st[(item >> 20) & 7u];
             v.cbase = (int32_t)u32(T.code_at) - (int32_t)u32(T.cfirst);
             v.tok_at = u32(T.tok_at);
@@ -962,6 +964,8 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     const int32_t n = (int32_t)(e - b0);
     if (valid) t = C.tlen(v, c);
     const uint4 tx = C.ttext(v, c);
+    const uint32_t tlitn = g_tlitn[v.tok_at + c];  // (loaded with the text)
+    const uint4 tlit = g_tlit[v.tok_at + c];
     // the text's first byte relative to the block start (may be negative at its edge)
     const int32_t rel = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0) +
                         (int32_t)wave_excl_sum(t, lane);
@@ -1006,7 +1010,9 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
             acc = (uint32_t)(rel - rsrc);
         } else {  // sample s - kk is in the group before
             acc = 0;
-            for (uint32_t k = 1; k <= kk; k++) acc += C.tlen(v, (P >> ((kLookback - k) * v.R.width)) & v.mask);
+#pragma unroll
+            for (uint32_t k = 1; k <= kLookback; k++)  // (all loads at once)
+                acc += k <= kk ? C.tlen(v, (P >> ((kLookback - k) * v.R.width)) & v.mask) : 0u;
         }
         if (rel >= (int32_t)acc) dist = acc;
     } else if (want && !packed) {
@@ -1050,7 +1056,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     // whole token's literal codes, as up to 4 words (LSB first) that go into the
     // stream with at most two LDS ORs each; texts cut by the block's edges and tokens
     // of more than 128 bits of literals go byte by byte (rare)
-    const uint32_t tn = in ? g_tlitn[v.tok_at + c] : 0u;
+    const uint32_t tn = in ? tlitn : 0u;
     const bool whole_lit = full && tn != kNoTokLit;
     const bool by_byte = in && !runm && !dist && !whole_lit;
     uint32_t bw[4] = {0, 0, 0, 0}, bn = 0;
@@ -1062,7 +1068,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         bw[1] = (uint32_t)(x >> 32);
         bn = a.y + b.y;
     } else if (whole_lit) {
-        const uint4 L = g_tlit[v.tok_at + c];
+        const uint4 L = tlit;
         bw[0] = L.x;
         bw[1] = L.y;
         bw[2] = L.z;
