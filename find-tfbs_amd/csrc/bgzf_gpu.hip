@@ -1394,11 +1394,14 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     // XORs the waves' (CRC(a b) = x^(8 |b|) CRC(a) ^ CRC(b)) and the init term (a full
     // block's precomputed)
     {
-        uint32_t col[32], wcol[32];
+        // (the lane table, 2 048 words, goes to LDS over the codes -- dead: the items are
+        // done -- two words per thread; the wave's columns are wave-uniform: scalar loads)
+        const uint32_t lt0 = A.crc_lane[tid], lt1 = A.crc_lane[kWv + tid];
+        typedef const __attribute__((address_space(4))) uint32_t *ConstPtr;
+        const ConstPtr W = (ConstPtr)(uintptr_t)(A.crc_lane + 64 * 32 + 32 * __builtin_amdgcn_readfirstlane((int)wave));
+        uint32_t wcol[32];
 #pragma unroll
-        for (uint32_t i = 0; i < 32; i++) col[i] = A.crc_lane[i * 64 + lane];
-#pragma unroll
-        for (uint32_t i = 0; i < 32; i++) wcol[i] = A.crc_lane[64 * 32 + 32 * wave + i];
+        for (uint32_t i = 0; i < 32; i++) wcol[i] = W[i];
         const int32_t q1 = (int32_t)n - 64 * (kWv - 1 - (int32_t)tid), q0 = max(0, q1 - 64);
         uint32_t crc = 0;
         if (q1 - q0 == 64 && (q0 & 63) == 0) {  // a whole padded slice: dword reads, no bank conflicts
@@ -1411,9 +1414,13 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         } else {
             for (int32_t q = q0; q < q1; q++) crc = crc_byte(S.crc_tab, crc, g_text[txt_at((uint32_t)q)]);
         }
+        uint32_t *const lt = reinterpret_cast<uint32_t *>(S.codes);
+        lt[tid] = lt0;
+        lt[kWv + tid] = lt1;
+        __syncthreads();
         uint32_t r = 0;
 #pragma unroll
-        for (uint32_t i = 0; i < 32; i++) r ^= ((crc >> i) & 1u) ? col[i] : 0u;
+        for (uint32_t i = 0; i < 32; i++) r ^= ((crc >> i) & 1u) ? lt[i * 64 + lane] : 0u;
 #pragma unroll
         for (uint32_t o = 32; o; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, (int)o);
         uint32_t rw = 0;
