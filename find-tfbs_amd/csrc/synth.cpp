@@ -325,6 +325,17 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
     const uint64_t chunk = 64ull * T;
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_fill = now();
+    std::vector<tfbs::RegionBuilt> prev;  // the last chunk built, committed during the next build
+    bool have_prev = false, prev_first = false;
+    const char *ov = getenv("TFBS_PREP_OVERLAP");  // 0: never (A/B)
+    const bool overlap = !(ov && *ov && atoi(ov) == 0);
+    uint64_t prev_n = 0;
+    auto commit = [&] {
+        tfbs::commit_regions(B, prev, T);
+        if (prev_first && prev_n < count)  // the rest of the regions will look alike: room for them now
+            tfbs::reserve_batch(B, 1.15 * (double)(B.rh.size() + count - prev_n) / (double)std::max<size_t>(B.rh.size(), 1));
+        prev.clear();
+    };
     for (uint64_t c0 = first; c0 < first + count; c0 += chunk) {
         const uint64_t n = std::min<uint64_t>(chunk, first + count - c0);
         // phase 1: the synthetic inputs (what a BCF / FASTA reader would hand over)
@@ -367,14 +378,35 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
             for (auto &t : ts) t.join();
         }
         // phase 2: load_diffs / group / patch / dedup / pack (build_regions: on the
-        // device grouper where the region qualifies), then the commit
+        // device grouper where the region qualifies), while the previous chunk's regions
+        // are committed on another thread when its build mostly waited on the device
+        // (SNV-only regions, patched from the masks: at most a quarter built or patched
+        // on the host -- otherwise the two compete for the host threads).  build_regions
+        // and commit_regions touch disjoint batch fields; the generation above ran alone,
+        // so the overlap hides only build and commit time behind each other.
         const double t_build = now();
+        std::thread committer;
+        if (have_prev) committer = std::thread([&] { commit(); });
         std::vector<tfbs::RegionBuilt> built;
-        if (int rc = tfbs::build_regions(B, ins, T, built, &B.prep_s[1])) return rc;
-        tfbs::commit_regions(B, built, T);
-        if (c0 == first && n < count)  // the rest of the regions will look alike: room for them now
-            tfbs::reserve_batch(B, 1.15 * (double)(B.rh.size() + count - n) / (double)std::max<size_t>(B.rh.size(), 1));
+        const int rc = tfbs::build_regions(B, ins, T, built, &B.prep_s[1]);
+        if (committer.joinable()) committer.join();
+        if (rc) return rc;
+        uint64_t heavy = 0;
+        for (const tfbs::RegionBuilt &r : built) heavy += !r.dev || r.dev_grouped;
+        prev = std::move(built);
+        prev_first = c0 == first;
+        prev_n = n;
+        have_prev = true;
+        if (!overlap || 4 * heavy > n) {  // (a host-bound build: committed now, as it is built)
+            commit();
+            have_prev = false;
+        }
         B.prep_s[2] += now() - t_build;
+    }
+    if (have_prev) {
+        const double t = now();
+        commit();
+        B.prep_s[2] += now() - t;
     }
     B.prep_s[3] += now() - t_fill;
     return TFBS_OK;
