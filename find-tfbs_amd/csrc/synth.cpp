@@ -379,11 +379,11 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
         }
         // phase 2: load_diffs / group / patch / dedup / pack (build_regions: on the
         // device grouper where the region qualifies), while the previous chunk's regions
-        // are committed on another thread when its build mostly waited on the device
-        // (SNV-only regions, patched from the masks: at most a quarter built or patched
-        // on the host -- otherwise the two compete for the host threads).  build_regions
-        // and commit_regions touch disjoint batch fields; the generation above ran alone,
-        // so the overlap hides only build and commit time behind each other.
+        // are committed on another thread (the build waits on the device and neither
+        // keeps 16 threads busy throughout: C3 0.22 -> 0.16 s, C5 0.79 -> 0.72 s on one
+        // box).  build_regions and commit_regions touch disjoint batch fields; the
+        // generation above ran alone, so the overlap hides only build and commit time
+        // behind each other.
         const double t_build = now();
         std::thread committer;
         if (have_prev) committer = std::thread([&] { commit(); });
@@ -391,13 +391,11 @@ int tfbs_synth_fill_batch(tfbs_batch *b, uint64_t seed, uint64_t first, uint64_t
         const int rc = tfbs::build_regions(B, ins, T, built, &B.prep_s[1]);
         if (committer.joinable()) committer.join();
         if (rc) return rc;
-        uint64_t heavy = 0;
-        for (const tfbs::RegionBuilt &r : built) heavy += !r.dev || r.dev_grouped;
         prev = std::move(built);
         prev_first = c0 == first;
         prev_n = n;
         have_prev = true;
-        if (!overlap || 4 * heavy > n) {  // (a host-bound build: committed now, as it is built)
+        if (!overlap) {  // (TFBS_PREP_OVERLAP=0: committed as it is built)
             commit();
             have_prev = false;
         }
