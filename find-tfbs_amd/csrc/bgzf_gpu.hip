@@ -1139,7 +1139,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     // [0, 64) source low words, [64, 128) high words, [128, 192) Stage byte offset (bit
     // 31: a byte segment), [192, 256) the segments' inclusive end in units.
     for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
-    for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = 0;
+    for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
     for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
     if (wave == 0) {
         static_assert(4 + 4 * kStRows <= 64 && 256 <= kWvItems, "the segment list");
@@ -1274,9 +1274,13 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     // run groups of a row make one IT_RUN item (each starting a new run: the symbols
     // depend on the run's length only).  A thread per staged group (Stage::cum's index,
     // the lower waves; the upper ones make the literal codes) tests its packed codes as
-    // whole dwords against the code's byte pattern into g_agg; then one wave per row
-    // turns the flags into items: per group in g_agg bit 0 an item starts here, bit 1 a
-    // run, bits 2-5 the run's groups (cleared before the items).
+    // whole dwords against the code's byte pattern; then each wave takes a contiguous
+    // share of the rows, turns their groups' flags into items and counts them, and after
+    // one barrier writes them from its share's offset (the waves' counts before it).
+    // The flags live in g_ioff[kFlags + Stage::cum index]: bit 0 an item starts here,
+    // bit 1 a run, bits 2-5 the run's groups; g_ioff[0, 16) the waves' counts.
+    constexpr uint32_t kFlags = kWv / 64;
+    static_assert(kFlags + kStCum <= kWvItems, "the listing's flags");
     if (tid < kStCum) {
         bool run = false;
         for (uint32_t k = 0; k < S.P.n_st; k++) {
@@ -1298,20 +1302,23 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
             run = same && t >= 1 && rel0 >= (int64_t)t && rel0 + kCumGroup * t <= (int64_t)(e - b0);
             break;
         }
-        g_agg[tid] = run ? 1u : 0u;
+        g_ioff[kFlags + tid] = run ? 1u : 0u;
     }
     __syncthreads();
-    for (uint32_t r = wave; r < S.P.n_rows; r += kWv / 64) {
-        bool head, nl;
-        uint32_t groups, k_st;
-        row_items(r, head, nl, groups, k_st);
-        uint32_t cnt = (head ? 1u : 0u) + (nl ? 1u : 0u);
-        if (groups) {
-            const uint32_t cum_at = S.P.st[k_st].cum_at;
+    stamp(7);
+    const uint32_t r_lo = wave * S.P.n_rows / (kWv / 64), r_hi = (wave + 1) * S.P.n_rows / (kWv / 64);
+    {
+        uint32_t cnt = 0;
+        for (uint32_t r = r_lo; r < r_hi; r++) {
+            bool head, nl;
+            uint32_t groups, k_st;
+            row_items(r, head, nl, groups, k_st);
+            cnt += (head ? 1u : 0u) + (nl ? 1u : 0u);
+            const uint32_t *const fl = g_ioff + kFlags + S.P.st[k_st].cum_at;
             for (uint32_t q0 = 0; q0 < groups; q0 += 64) {
                 const uint32_t q = q0 + lane;
                 const bool in = q < groups;
-                const bool run = in && g_agg[cum_at + q] != 0;
+                const bool run = in && fl[q] != 0;
                 const uint64_t rb = __ballot(run);
                 const bool link = run && lane > 0 && ((rb >> (lane - 1)) & 1u);  // (a window starts its own item)
                 const uint64_t nl_mask = ~__ballot(link) | 1ull, below = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
@@ -1320,46 +1327,42 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
                 const uint64_t sm = __ballot(start);
                 const uint64_t after = lane == 63 ? 0ull : (sm & ~below);
                 const uint32_t next = min(after ? (uint32_t)__builtin_ctzll(after) : 64u, groups - q0);
-                if (in) g_agg[cum_at + q] = start ? (1u | (run ? 2u : 0u) | ((next - lane) << 2)) : 0u;
+                if (in) const_cast<uint32_t *>(fl)[q] = start ? (1u | (run ? 2u : 0u) | ((next - lane) << 2)) : 0u;
                 cnt += (uint32_t)__builtin_popcountll(sm);
             }
         }
-        if (lane == 0) g_ioff[r] = cnt;
+        if (lane == 0) g_ioff[wave] = cnt;
     }
     __syncthreads();
-    if (wave == 0) {
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < S.P.n_rows; c0 += 64) {
-            const bool in = c0 + lane < S.P.n_rows;
-            const uint32_t x = in ? g_ioff[c0 + lane] : 0u, inc = wave_incl_sum(x);
-            if (in) g_ioff[c0 + lane] = carry + inc - x;
-            carry += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+    {
+        const uint32_t x = lane < kWv / 64 ? g_ioff[lane] : 0u;
+        uint32_t at = wave_sum(lane < wave ? x : 0u);  // the waves' items before this one's rows
+        if (wave == 0) {
+            const uint32_t total = wave_sum(x);
+            if (lane == 0) g_ioff[kWvItems] = total;
         }
-        if (lane == 0) g_ioff[kWvItems] = carry;
-    }
-    __syncthreads();
-    for (uint32_t r = wave; r < S.P.n_rows; r += kWv / 64) {
-        bool head, nl;
-        uint32_t groups, k_st;
-        row_items(r, head, nl, groups, k_st);
-        uint32_t at = g_ioff[r] + (head ? 1u : 0u);
-        if (head && lane == 0) g_item[at - 1] = (IT_HEAD << 30) | (r << 23);
-        const StRow &T = S.P.st[k_st];
-        for (uint32_t q0 = 0; q0 < groups; q0 += 64) {
-            const uint32_t q = q0 + lane;
-            const uint32_t f = q < groups ? g_agg[T.cum_at + q] : 0u;
-            const uint64_t sm = __ballot(f & 1u);
-            if (f & 1u) {
-                const uint32_t k = at + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1ull));
-                g_item[k] = ((f & 2u) ? (IT_RUN << 30) | (((f >> 2) & 15u) << 16) : (IT_GROUP << 30)) | (r << 23) |
-                            (k_st << 20) | (T.g_lo + q);
+        for (uint32_t r = r_lo; r < r_hi; r++) {
+            bool head, nl;
+            uint32_t groups, k_st;
+            row_items(r, head, nl, groups, k_st);
+            if (head && lane == 0) g_item[at] = (IT_HEAD << 30) | (r << 23);
+            at += head ? 1u : 0u;
+            const StRow &T = S.P.st[k_st];
+            for (uint32_t q0 = 0; q0 < groups; q0 += 64) {
+                const uint32_t q = q0 + lane;
+                const uint32_t f = q < groups ? g_ioff[kFlags + T.cum_at + q] : 0u;
+                const uint64_t sm = __ballot(f & 1u);
+                if (f & 1u) {
+                    const uint32_t k = at + (uint32_t)__builtin_popcountll(sm & ((1ull << lane) - 1ull));
+                    g_item[k] = ((f & 2u) ? (IT_RUN << 30) | (((f >> 2) & 15u) << 16) : (IT_GROUP << 30)) | (r << 23) |
+                                (k_st << 20) | (T.g_lo + q);
+                }
+                at += (uint32_t)__builtin_popcountll(sm);
             }
-            at += (uint32_t)__builtin_popcountll(sm);
+            if (nl && lane == 0) g_item[at] = (IT_NL << 30) | (r << 23);
+            at += nl ? 1u : 0u;
         }
-        if (nl && lane == 0) g_item[at] = (IT_NL << 30) | (r << 23);
     }
-    __syncthreads();
-    for (uint32_t i = tid; i < kWvItems; i += kWv) g_agg[i] = 0;  // (the flags: wv_publish's counts next)
     __syncthreads();
     const uint32_t n_items = g_ioff[kWvItems];
     stamp(2);

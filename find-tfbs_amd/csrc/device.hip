@@ -1635,13 +1635,14 @@ static int bgzf_prof_report(tfbs_ctx *ctx, uint32_t nb) {
     std::vector<uint64_t> h((size_t)nb * 32);
     HIP_TRY(hipMemcpyAsync(h.data(), ctx->bg_prof.p, h.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    double ph[5] = {0, 0, 0, 0, 0}, items = 0, st[16] = {};
+    double ph[5] = {0, 0, 0, 0, 0}, items = 0, st[16] = {}, list_a = 0;
     uint32_t nw = 0;
     for (uint32_t b = 0; b < nb; b++) {
         const uint64_t *p = &h[(size_t)b * 32];
         if (!p[5]) continue;  // a bgzf_block_kernel block
         nw++;
         for (int k = 0; k < 5; k++) ph[k] += (double)(p[k + 1] - p[k]);
+        if (p[7]) list_a += (double)(p[7] - p[1]);
         items += (double)p[6];
         for (int k = 0; k < 16; k++) st[k] += (double)p[8 + k];
     }
@@ -1655,8 +1656,8 @@ static int bgzf_prof_report(tfbs_ctx *ctx, uint32_t nb) {
     // groups with byte literals; other groups, those on the sample-by-sample look-back
     fprintf(stderr,
             "[bgzf prof] item cycles/block: count run groups %.0f, other groups %.0f; emit %.0f; byte-literal groups "
-            "%.0f; other groups %.1f, on the serial look-back %.1f\n",
-            st[8] / d, st[11] / d, st[9] / d, st[12] / d, st[7] / d, st[14] / d);
+            "%.0f; other groups %.1f, on the serial look-back %.1f; listing: literal codes and run tests %.0f\n",
+            st[8] / d, st[11] / d, st[9] / d, st[12] / d, st[7] / d, st[14] / d, list_a / d);
     return TFBS_OK;
 }
 
