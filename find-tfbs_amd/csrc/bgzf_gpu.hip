@@ -1133,16 +1133,18 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     if (!S.P.all) return;  // (uniform) bgzf_block_kernel's block
     // the block's reads as one flat list of segments -- the CRC tables, the rows'
     // descriptors, per staged row its codes (dwords from the aligned-down source: the
-    // plan put code_at at the same offset mod 4), token texts, token lengths (bytes) and
-    // group offsets --, every thread issuing its loads before its stores (a loop per
-    // segment waited on one load per segment).  The list lives in g_item (listed later):
-    // [0, 64) source low words, [64, 128) high words, [128, 192) Stage byte offset (bit
-    // 31: a byte segment), [192, 256) the segments' inclusive end in units.
+    // plan put code_at at the same offset mod 4), token texts, token lengths (bytes),
+    // group offsets and the tokens' literal codes and bit counts (bytes; tok_lit_kernel)
+    // --, every thread issuing its loads before its stores (a loop per segment waited on
+    // one load per segment).  The list lives in g_item (listed later): [0, 64) source
+    // low words, [64, 128) high words, [128, 192) destination: byte offset into g_st /
+    // g_tlit / g_tlitn (bits 29-30), bit 31: a byte segment; [192, 256) the segments'
+    // inclusive end in units.
     for (uint32_t i = tid; i <= kBitWords; i += kWv) g_bits[i] = i ? 0u : 0x3u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
     for (uint32_t i = tid; i < kWvItems; i += kWv) g_pub[i] = g_agg[i] = 0;
     for (uint32_t i = tid; i < sizeof(g_text) / 16; i += kWv) reinterpret_cast<uint4 *>(g_text)[i] = uint4{0, 0, 0, 0};
     if (wave == 0) {
-        static_assert(4 + 4 * kStRows <= 64 && 256 <= kWvItems, "the segment list");
+        static_assert(4 + 6 * kStRows <= 64 && 256 <= kWvItems, "the segment list");
         uint64_t src = 0;
         uint32_t dst = 0, nu = 0;
         if (lane == 0) {
@@ -1161,8 +1163,8 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
             src = (uint64_t)(A.rows + S.P.r_first);
             dst = offsetof(Stage, rows);
             nu = S.P.n_rows * (uint32_t)(sizeof(DevRow) / 4);
-        } else if (lane < 4 + 4 * S.P.n_st) {
-            const uint32_t k = (lane - 4) >> 2, m = (lane - 4) & 3;
+        } else if (lane < 4 + 6 * S.P.n_st) {
+            const uint32_t k = (lane - 4) / 6, m = (lane - 4) % 6;
             const StRow &T = S.P.st[k];
             if (m == 0) {
                 const uint64_t a = T.code_off + T.cfirst;
@@ -1178,10 +1180,18 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
                 src = (uint64_t)(A.tok_len + T.tok);
                 dst = ((uint32_t)offsetof(Stage, tlen) + T.tok_at) | 0x80000000u;
                 nu = T.nv;
-            } else {
+            } else if (m == 3) {
                 src = (uint64_t)(A.cum + T.cum_off + T.g_lo);
                 dst = (uint32_t)offsetof(Stage, cum) + 4 * T.cum_at;
                 nu = T.ncum;
+            } else if (m == 4) {
+                src = (uint64_t)(A.tok_lit + T.tok);
+                dst = (1u << 29) | (16 * T.tok_at);
+                nu = T.nv * 4;
+            } else {
+                src = (uint64_t)(A.tok_litn + T.tok);
+                dst = 0x80000000u | (2u << 29) | T.tok_at;
+                nu = T.nv;
             }
         }
         g_item[lane] = (uint32_t)src;
@@ -1192,6 +1202,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     __syncthreads();
     {
         uint8_t *const sb = reinterpret_cast<uint8_t *>(&g_st);
+        uint8_t *const sl = reinterpret_cast<uint8_t *>(g_tlit);
         const uint32_t total = g_item[192 + 63];
         for (uint32_t u0 = tid; u0 < total; u0 += 4 * kWv) {
             uint32_t val[4], at[4];
@@ -1219,39 +1230,14 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
 #pragma unroll
             for (uint32_t j = 0; j < 4; j++) {
                 if (at[j] == ~0u) continue;
-                if (at[j] >> 31) sb[at[j] & 0x7FFFFFFFu] = (uint8_t)val[j];
-                else *reinterpret_cast<uint32_t *>(sb + at[j]) = val[j];
+                const uint32_t o = at[j] & 0x1FFFFFFFu, base = (at[j] >> 29) & 3u;
+                if (at[j] >> 31) (base == 2 ? g_tlitn : sb)[o] = (uint8_t)val[j];
+                else *reinterpret_cast<uint32_t *>((base == 1 ? sl : sb) + o) = val[j];
             }
         }
     }
     __syncthreads();
     stamp(1);
-    // the staged tokens' literal codes (tok_lit_kernel zeroed the texts' bytes past their
-    // length: the wave ORs whole text dwords into g_text), on the upper waves (the lower
-    // ones list the items meanwhile)
-    {
-        uint32_t tok_end = 0;
-        for (uint32_t k = 0; k < S.P.n_st; k++) tok_end = max(tok_end, S.P.st[k].tok_at + S.P.st[k].nv);
-        for (uint32_t k = (tid + kWv / 2) % kWv; k < tok_end; k += kWv) {
-            const uint4 tx = reinterpret_cast<const uint4 *>(S.text)[k];
-            const uint32_t t = S.tlen[k], w[4] = {tx.x, tx.y, tx.z, tx.w};
-            uint64_t lo = 0, hi = 0;
-            uint32_t nb = 0;
-            for (uint32_t i = 0; i < t && nb <= 128; i++) {
-                const uint32_t b = (w[(i >> 2) & 3u] >> (8 * (i & 3))) & 0xFFu;
-                const uint32_t code = b < 144 ? rev(0x30 + b, 8) : rev(0x190 + b - 144, 9), n = b < 144 ? 8u : 9u;
-                if (nb < 64) {
-                    lo |= (uint64_t)code << nb;
-                    if (nb + n > 64) hi |= (uint64_t)code >> (64 - nb);
-                } else {
-                    hi |= (uint64_t)code << (nb - 64);
-                }
-                nb += n;
-            }
-            g_tlit[k] = uint4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-            g_tlitn[k] = (uint8_t)(nb <= 128 ? nb : kNoTokLit);
-        }
-    }
     // the block's items in stream order: per row its head, its groups, its newline;
     // counted per row, offsets by a wave scan, then one wave per row writes them (its
     // lanes the groups: a row holds up to kStCum of them)
@@ -1489,17 +1475,36 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
 }
 
 // Per token of the launch's rows: its text's bytes past its length zeroed (the wave
-// kernel ORs whole text dwords into the block's bytes).
-__global__ __launch_bounds__(256) void tok_mask_kernel(uint32_t *__restrict__ text, const uint8_t *__restrict__ len,
-                                                       uint32_t n_tok) {
+// kernel ORs whole text dwords into the block's bytes) and its fixed-Huffman literal
+// codes, LSB first, with their bit count (kNoTokLit: more than 128 bits), which the
+// wave kernel stages with the texts.
+__global__ __launch_bounds__(256) void tok_lit_kernel(uint32_t *__restrict__ text, const uint8_t *__restrict__ len,
+                                                      uint32_t n_tok, uint4 *__restrict__ lit, uint8_t *__restrict__ litn) {
     const uint32_t k = blockIdx.x * 256 + threadIdx.x;
     if (k >= n_tok) return;
     const uint32_t t = len[k];
+    uint32_t w[4];
 #pragma unroll
     for (int j = 0; j < 4; j++) {
         const int32_t keep = (int32_t)t - 4 * j;  // bytes of dword j inside the text
-        if (keep < 4) text[4 * k + j] &= keep <= 0 ? 0u : (1u << (8 * keep)) - 1u;
+        w[j] = text[4 * k + j] & (keep >= 4 ? ~0u : (keep <= 0 ? 0u : (1u << (8 * keep)) - 1u));
+        text[4 * k + j] = w[j];
     }
+    uint64_t lo = 0, hi = 0;
+    uint32_t nb = 0;
+    for (uint32_t i = 0; i < t && nb <= 128; i++) {
+        const uint32_t b = (w[(i >> 2) & 3u] >> (8 * (i & 3))) & 0xFFu;
+        const uint32_t code = b < 144 ? rev(0x30 + b, 8) : rev(0x190 + b - 144, 9), n = b < 144 ? 8u : 9u;
+        if (nb < 64) {
+            lo |= (uint64_t)code << nb;
+            if (nb + n > 64) hi |= (uint64_t)code >> (64 - nb);
+        } else {
+            hi |= (uint64_t)code << (nb - 64);
+        }
+        nb += n;
+    }
+    lit[k] = uint4{(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    litn[k] = (uint8_t)(nb <= 128 ? nb : kNoTokLit);
 }
 
 // off[i] = the sizes of blocks before i, off[nb] = their total (one workgroup).
@@ -1583,12 +1588,13 @@ uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice, uint32_t
     return shift(0xFFFFFFFFu, kBgzfRaw);  // (on 0xFFFFFFFF: a full block's init term)
 }
 
-int launch_tok_mask(const BgArgs &a, uint32_t n_tok, hipStream_t stream) {
+int launch_tok_lit(const BgArgs &a, uint32_t n_tok, hipStream_t stream) {
     if (n_tok == 0) return TFBS_OK;
-    hipLaunchKernelGGL(tok_mask_kernel, dim3((n_tok + 255) / 256), dim3(256), 0, stream,
-                       reinterpret_cast<uint32_t *>(const_cast<char *>(a.tok_text)), a.tok_len, n_tok);
+    hipLaunchKernelGGL(tok_lit_kernel, dim3((n_tok + 255) / 256), dim3(256), 0, stream,
+                       reinterpret_cast<uint32_t *>(const_cast<char *>(a.tok_text)), a.tok_len, n_tok, a.tok_lit,
+                       a.tok_litn);
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("tok_mask_kernel: ") + hipGetErrorString(e));
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("tok_lit_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 

@@ -16,8 +16,10 @@ struct BgArgs {
     const DevRow *rows;
     uint32_t n_rows;
     const char *heads;
-    const char *tok_text;       // kRowTokBytes per token slot (bytes past the length zeroed: launch_tok_mask)
+    const char *tok_text;       // kRowTokBytes per token slot (bytes past the length zeroed: launch_tok_lit)
     const uint8_t *tok_len;
+    uint4 *tok_lit;             // per token its literal codes (launch_tok_lit)
+    uint8_t *tok_litn;          // and their bit count
     const uint8_t *codes;       // the encoded keys' packed codes (tfbs_batch_encode's compact buffer)
     uint32_t *cum;              // per row (DevRow::cum_off): (n_samples + 63) / 64 + 1 genotype text offsets
     uint32_t n_samples;
@@ -41,8 +43,8 @@ size_t bgzf_plan_bytes();
 // 32 x 64 + 32 x 16 words); returns crc_full.
 constexpr size_t kBgzfCrcWords = 256 + 32 * kBgzfOps + 768 + 32 * 64 + 32 * 16;
 uint32_t bgzf_crc_tables(uint32_t *tab, uint32_t *ops, uint32_t *slice, uint32_t *lane);
-// Per token: the text's bytes past its length zeroed.
-int launch_tok_mask(const BgArgs &a, uint32_t n_tok, hipStream_t stream);
+// Per token: the text's bytes past its length zeroed, its literal codes (tok_lit, tok_litn).
+int launch_tok_lit(const BgArgs &a, uint32_t n_tok, hipStream_t stream);
 // Per row: its genotype text offsets every 64 samples.
 int launch_row_cum(const BgArgs &a, hipStream_t stream);
 // Blocks [a.block0, a.block0 + n_blocks) of the stream, one workgroup each (after a

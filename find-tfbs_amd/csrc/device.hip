@@ -186,7 +186,8 @@ struct tfbs_ctx {
     // device BGZF rows (tfbs_batch_rows_bgzf)
     DevBuf<DevRow> bg_rows;
     DevBuf<char> bg_heads, bg_tok_text;
-    DevBuf<uint8_t> bg_tok_len, bg_plans;
+    DevBuf<uint8_t> bg_tok_len, bg_plans, bg_tok_litn;
+    DevBuf<uint4> bg_tok_lit;
     DevBuf<uint32_t> bg_cum, bg_crc;  // bg_crc: byte table | shift operators
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
     uint32_t bg_crc_full = 0;         // bgzf_crc_tables' full-block CRC init term
@@ -646,6 +647,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->enc_vals.release(); ctx->enc_hist.release(); ctx->enc_packed.release(); ctx->enc_off.release();
     ctx->enc_vals_c.release(); ctx->enc_hist_c.release(); ctx->enc_val_off.release();
     ctx->bg_rows.release(); ctx->bg_heads.release(); ctx->bg_tok_text.release(); ctx->bg_tok_len.release();
+    ctx->bg_tok_lit.release(); ctx->bg_tok_litn.release();
     ctx->bg_cum.release(); ctx->bg_crc.release(); ctx->bg_plans.release(); ctx->bg_prof.release(); ctx->kf_prof.release(); ctx->asm_order.release();
     for (int k = 0; k < tfbs_ctx::kBgSlots; k++) {
         ctx->bg_out[k].release(); ctx->bg_packed[k].release(); ctx->bg_out_len[k].release(); ctx->bg_off[k].release();
@@ -1691,6 +1693,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     if ((rc = ctx->bg_rows.put(plan.rows, ctx->stream)) || (rc = ctx->bg_heads.put(heads, ctx->stream)) ||
         (rc = ctx->bg_tok_text.put(plan.tok_text, ctx->stream)) ||
         (rc = ctx->bg_tok_len.put(plan.tok_len, ctx->stream)) ||
+        (rc = ctx->bg_tok_lit.ensure(std::max<size_t>(plan.tok_len.size(), 1))) ||
+        (rc = ctx->bg_tok_litn.ensure(std::max<size_t>(plan.tok_len.size(), 1))) ||
         (rc = ctx->bg_cum.ensure(std::max<size_t>(plan.rows.size() * (ng + 1), 1))))
         return rc;
     tfbs::BgArgs a{};
@@ -1699,6 +1703,8 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.heads = ctx->bg_heads.p;
     a.tok_text = ctx->bg_tok_text.p;
     a.tok_len = ctx->bg_tok_len.p;
+    a.tok_lit = ctx->bg_tok_lit.p;
+    a.tok_litn = ctx->bg_tok_litn.p;
     a.codes = ctx->enc_packed.p;
     a.cum = ctx->bg_cum.p;
     a.n_samples = N;
@@ -1709,7 +1715,7 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.crc_lane = ctx->bg_crc.p + 256 + 32 * kBgzfOps + 768;
     a.crc_full = ctx->bg_crc_full;
     a.stored = env_int("TFBS_BGZF_STORED", 0) != 0 ? 1u : 0u;
-    if ((rc = tfbs::launch_tok_mask(a, (uint32_t)plan.tok_len.size(), ctx->stream)) ||
+    if ((rc = tfbs::launch_tok_lit(a, (uint32_t)plan.tok_len.size(), ctx->stream)) ||
         (rc = tfbs::launch_row_cum(a, ctx->stream)))
         return rc;
     // blocks per launch (512 MiB of block slots); TFBS_BGZF_BATCH_BLOCKS=n: smaller
