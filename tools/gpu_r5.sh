@@ -80,6 +80,15 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
         python3 -c "import json;q=json.load(open('$d/pmc_summary_bgzf_wave_kernel.json'));print('$v $pass', {k: v for k, v in q.items() if not k.startswith('_')})"
       done
       unset TFBS_LIB ;;
+    kfpmc_*)  # kfpmc_<W>: key_fast_kernel's phase clocks (TFBS_KF_PROF, the slowest regions = the tail) and two SQ passes
+      w=${st#kfpmc_}; d=$O/kf_$w; mkdir -p $d
+      TFBS_KF_PROF=1 timeout -k 10 300 python3 bench.py --workload $w --steps 1 --warmup 0 --no-cpu --no-e2e > $d/bench.json 2> $d/kf_prof.err || { tail -20 $d/kf_prof.err; exit 1; }
+      grep "kf prof" $d/kf_prof.err > $d/kf_prof.txt; head -3 $d/kf_prof.txt | cut -c1-300
+      for pass in stall1:"SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_WAVE_CYCLES" stall2:"SQ_ACTIVE_INST_MISC SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_SALU SQ_INSTS_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVES"; do
+        name=${pass%%:*}; counters=${pass#*:}
+        timeout -s KILL 120 rocprofv3 --pmc $counters --output-format csv -d $d/pmc_$name -o pmc -- python3 bench.py --workload $w --steps 2 --warmup 0 --no-cpu --no-e2e > $d/pmc_$name.log 2>&1 || { tail -20 $d/pmc_$name.log; exit 1; }
+        python3 tools/pmc_summary.py $d/pmc_$name key_fast_kernel > /dev/null || exit 1
+      done ;;
     prof_*)
       w=${st#prof_}
       bash tools/profile_round.sh ${T}_prof_$w --workload $w || exit 1 ;;
