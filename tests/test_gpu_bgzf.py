@@ -135,3 +135,18 @@ def test_bgzf_many_pieces_one_call(tmp_path, monkeypatch, batch_blocks):
     blocks = _members(data)
     assert len(blocks) > 3 * 2 * 3  # several launches per slot when batch_blocks is 2
     assert want.count("\n") > 500
+
+
+def test_bgzf_stored_blocks_inflate_to_rows(tmp_path, monkeypatch):
+    """TFBS_BGZF_STORED=1: every wave-kernel block is stored (BTYPE 00) with the block's
+    text as the kernel assembled it for the CRC -- the path incompressible blocks take --
+    so the members inflate (and pass gzip's CRC check) to exactly the host rows."""
+    monkeypatch.setenv("TFBS_BGZF_STORED", "1")
+    ps, _ = synth_patterns(tmp_path, 40, 3, 106, thr=1e-4)
+    n_regions = 12
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
+    regions = make_regions_synth(17, 0, n_regions, 5000, ps.max_length, 10)
+    want, data = _compare(ps, 5000, beds, regions)
+    blocks = _members(data)
+    assert len(blocks) > 2
+    assert sum(b[0] for b in blocks) > len(want)  # stored: no smaller than the text
