@@ -556,8 +556,9 @@ def main():
                 "windows_per_s": tot_windows / e2e_max,
                 "seconds": e2e_max,
                 "note": "one pass over the rank's batch: haplotype reconstruction (load_diffs/group on the GPU "
-                        "for SNV-only regions, else on the host; patch/dedup/pack on %d host threads; the "
-                        "synthetic records are generated before, as for the CPU baseline) + upload "
+                        "for SNV-only regions, else on the host; patch/dedup/pack on %d host threads, a chunk's "
+                        "layout commit overlapping the next chunk's build; the synthetic records are generated "
+                        "before each chunk, outside the clock, as for the CPU baseline) + upload "
                         "+ scan + device key reduction + device "
                         "per-sample encoding + the VCF rows as BGZF blocks made on the GPU and written out (%d rows, "
                         "%.3g bytes of text deflated to %.3g bytes, to /dev/null)" % (
