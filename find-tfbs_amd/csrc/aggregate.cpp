@@ -8,6 +8,7 @@
 // (main.rs:439-498) and the row format (main.rs:415-429) follow.
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -482,19 +483,38 @@ int build_row_parts(const Batch &B, size_t r0, size_t r1, uint32_t min_maf, uint
 
 int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std::string &chrom, uint32_t *fake,
                     RowPlan &plan) {
-    // serially: POS, offsets in the stream, token slots
+    // serially: POS, offsets in the stream, token slots (sized first: one allocation each)
     plan = RowPlan();
     const std::string chr = strip_chr(chrom);
+    const size_t q0 = std::max(r0, P.r0), q1 = std::min(r1, P.r0 + P.parts.size());
+    size_t n_rows = 0, head_bytes = 0, n_tok = 0;
+    for (size_t r = q0; r < q1; r++)
+        for (const RowPart &p : P.parts[r - P.r0]) {
+            n_rows++;
+            head_bytes += chr.size() + 12 + p.head.size();  // ("\t<POS>\t": at most 12 bytes)
+            if (p.e != UINT32_MAX) n_tok += p.nv;
+        }
+    plan.rows.reserve(n_rows);
+    plan.heads.reserve(head_bytes);
+    plan.tok_len.reserve(n_tok);
+    plan.tok_text.reserve(n_tok * kRowTokBytes);
     uint64_t at = 0;
-    char pos[32];
-    for (size_t r = std::max(r0, P.r0); r < std::min(r1, P.r0 + P.parts.size()); r++)
+    char pos[16];
+    for (size_t r = q0; r < q1; r++) {
         for (RowPart &p : P.parts[r - P.r0]) {
             DevRow d{};
             d.head_off = (uint32_t)plan.heads.size();
-            const int m = snprintf(pos, sizeof pos, "\t%u\t", *fake);
-            (*fake)++;
+            // "\t<POS>\t" (the fake position, decimal)
+            char *e = pos + sizeof pos;
+            *--e = '\t';
+            uint32_t v = (*fake)++;
+            do {
+                *--e = (char)('0' + v % 10);
+                v /= 10;
+            } while (v);
+            *--e = '\t';
             plan.heads += chr;
-            plan.heads.append(pos, (size_t)m);
+            plan.heads.append(e, (size_t)(pos + sizeof pos - e));
             plan.heads += p.head;
             if (plan.heads.size() >= UINT32_MAX) return fail(TFBS_E_NOMEM, "row heads past 4 GiB in one call");
             d.head_len = (uint32_t)(plan.heads.size() - d.head_off);
@@ -510,8 +530,9 @@ int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std
             }
             at += d.head_len + d.geno_len + 1;
             plan.rows.push_back(d);
-            std::string().swap(p.head);
         }
+        std::vector<RowPart>().swap(P.parts[r - P.r0]);  // (the region's parts are done)
+    }
     plan.text_bytes = at;
     plan.n_rows = plan.rows.size();
     return TFBS_OK;
@@ -519,9 +540,22 @@ int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std
 
 int build_row_plan(const Batch &B, size_t r0, size_t r1, const std::string &chrom, uint32_t min_maf,
                    uint32_t *fake, uint32_t threads, RowPlan &plan) {
+    static const bool prof = getenv("TFBS_PLAN_PROF") != nullptr;  // (debug: the two halves' seconds)
+    static std::atomic<uint64_t> t_parts(0), t_plan(0), calls(0);
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    const auto t0 = now();
     std::shared_ptr<RowParts> P;
     if (int rc = build_row_parts(B, r0, r1, min_maf, threads, P, nullptr)) return rc;
-    return plan_from_parts(B, *P, r0, r1, chrom, fake, plan);
+    const auto t1 = now();
+    const int rc = plan_from_parts(B, *P, r0, r1, chrom, fake, plan);
+    if (prof) {
+        t_parts += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+        t_plan += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(now() - t1).count();
+        if (++calls % 40 == 0)
+            fprintf(stderr, "[plan prof] %llu plans: parts %.3f s, from parts %.3f s\n", (unsigned long long)calls.load(),
+                    t_parts.load() * 1e-6, t_plan.load() * 1e-6);
+    }
+    return rc;
 }
 
 size_t region_rows(const Batch &B, const RegionH &R, uint32_t min_maf, std::string &out) {
