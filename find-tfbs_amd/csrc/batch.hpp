@@ -229,6 +229,15 @@ struct RegionBuilt {
 int build_region(const Batch &B, RegionInput &&in, RegionBuilt &out);
 // Builds regions (on the device grouper where they qualify, see batch.cpp),
 // `threads` host threads; *build_s (optional) += the host threads' seconds.
+//
+// Field ownership (tfbs_synth_fill_batch runs build_regions of chunk k + 1 while
+// commit_regions of chunk k runs on another thread, TFBS_PREP_OVERLAP): build_regions
+// writes only grouper, memb_allocs and the dev_ / host_ / patched_regions counters;
+// commit_regions writes rh, regions, inner, haps, words, nmask, posrel, druns,
+// hap_carriers, windows and the other scan / count totals.  Both only read the
+// batch's configuration (n_samples, dedup, dev_patch, the patterns).  A field written
+// by both would be a data race: keep the two sets disjoint
+// (tests/test_capi_cpu.py::test_prep_overlap_same_batch checks the digests).
 int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std::vector<RegionBuilt> &built,
                   double *build_s);
 // The region's nonref_id / nonref_local (fetched from the device if grouped there).

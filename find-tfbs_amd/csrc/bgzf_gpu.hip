@@ -827,15 +827,29 @@ __device__ __forceinline__ void wv_emit(const BgArgs &A, const Pend &p, uint32_t
 // One byte of the block at q into g_text: ORed into its dword (a byte store racing
 // another wave's OR of a neighbouring text's edge dword loses one of them: every
 // g_text write is an OR)
-__device__ __forceinline__ void wv_text_byte(uint32_t q, uint32_t b) {
+// CHECK (TFBS_BGZF_CHECK, debug): the OR returns the dword's old value, and a write
+// meeting bits already set -- a byte written twice, or a text's zero padding that is
+// not zero -- is counted in A.check (the host fails the call).
+template <bool CHECK>
+__device__ __forceinline__ void wv_text_put(const BgArgs &A, uint32_t a4, uint32_t v) {
+    uint32_t *w = reinterpret_cast<uint32_t *>(g_text + a4);
+    if (CHECK) {
+        if (atomicOr(w, v) & v) atomicAdd(A.check, 1u);
+    } else {
+        atomicOr(w, v);
+    }
+}
+template <bool CHECK>
+__device__ __forceinline__ void wv_text_byte(const BgArgs &A, uint32_t q, uint32_t b) {
     const uint32_t a = txt_at(q);
-    atomicOr(reinterpret_cast<uint32_t *>(g_text + (a & ~3u)), b << (8 * (a & 3u)));
+    wv_text_put<CHECK>(A, a & ~3u, b << (8 * (a & 3u)));
 }
 
 // A whole text at block byte rel (>= 0, inside the block) into g_text: its dwords,
 // ORed (neighbouring texts share edge dwords; the staged text's bytes past its length
 // are zero)
-__device__ __forceinline__ void wv_text_or(int32_t rel, uint32_t t, const uint4 &tx) {
+template <bool CHECK>
+__device__ __forceinline__ void wv_text_or(const BgArgs &A, int32_t rel, uint32_t t, const uint4 &tx) {
     const uint32_t a8 = 8 * ((uint32_t)rel & 3u), k0 = (uint32_t)rel >> 2, k1 = (uint32_t)(rel + (int32_t)t - 1) >> 2;
     const uint32_t T[5] = {tx.x, tx.y, tx.z, tx.w, 0u};
     uint32_t prev = 0;
@@ -843,7 +857,7 @@ __device__ __forceinline__ void wv_text_or(int32_t rel, uint32_t t, const uint4 
     for (uint32_t j = 0; j < 5; j++) {
         const uint32_t dw = (uint32_t)(((((uint64_t)T[j]) << 32) | prev) >> (32 - a8));
         prev = T[j];
-        if (k0 + j <= k1) atomicOr(reinterpret_cast<uint32_t *>(g_text + txt_at(4 * (k0 + j))), dw);
+        if (k0 + j <= k1) wv_text_put<CHECK>(A, txt_at(4 * (k0 + j)), dw);
     }
 }
 
@@ -852,6 +866,7 @@ __device__ __forceinline__ void wv_text_or(int32_t rel, uint32_t t, const uint4 
 // groups with byte literals) are placed (wv_place) and written at once (out->i = ~0u).
 // v / vkey: the wave's last item's row view and its key (item bits 20-31), kept
 // across the wave's items (consecutive ones are mostly groups of one row).
+template <bool CHECK>
 __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64_t e, uint32_t i, uint32_t lane,
                         RowView &v, uint32_t &vkey, Pend &out) {
     const uint64_t pt0 = A.prof ? clock64() : 0;
@@ -892,7 +907,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     if (kind == IT_NL) {
         const uint32_t base = wv_place(i, 8, lane);
         if (lane == 0) {
-            wv_text_byte((uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0), '\n');
+            wv_text_byte<CHECK>(A, (uint32_t)(v.R.text_off + v.R.head_len + v.R.geno_len - b0), '\n');
             LaneBits o{0, 0, base};
             wv_lit(o, '\n');
             o.finish();
@@ -906,7 +921,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
             const uint64_t q = q0 + lane;
             const bool in = q < he;
             const uint32_t b = in ? (uint8_t)A.heads[v.R.head_off + (q - v.R.text_off)] : 0u;
-            if (in) wv_text_byte((uint32_t)(q - b0), b);
+            if (in) wv_text_byte<CHECK>(A, (uint32_t)(q - b0), b);
             total += wave_sum(in ? lit_bits(b) : 0u);
         }
         uint32_t at = wv_place(i, total, lane);
@@ -934,7 +949,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
         const uint4 tx = C.ttext(v, c0);
         const uint32_t cum_g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g_st.cum[v.cum_at + g - v.g_lo]);
         const int32_t rel0 = (int32_t)((int64_t)(v.R.text_off + v.R.head_len + cum_g) - (int64_t)b0);
-        for (uint32_t j = 0; j < G; j++) wv_text_or(rel0 + (int32_t)((kCumGroup * j + lane) * t0), t0, tx);
+        for (uint32_t j = 0; j < G; j++) wv_text_or<CHECK>(A, rel0 + (int32_t)((kCumGroup * j + lane) * t0), t0, tx);
         const uint32_t Lr = kCumGroup * G * t0, nfull = Lr / 258, r = Lr % 258;
         const bool split = r == 1 || r == 2;
         const uint32_t n258 = split ? nfull - 1 : nfull;
@@ -1048,9 +1063,9 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
 #else
     if (full) {
 #endif
-        wv_text_or(rel, t, tx);
+        wv_text_or<CHECK>(A, rel, t, tx);
     } else if (in) {
-        for (int32_t q = lo; q < hi; q++) wv_text_byte((uint32_t)q, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
+        for (int32_t q = lo; q < hi; q++) wv_text_byte<CHECK>(A, (uint32_t)q, Ctx<true>::byte_of(tx, (uint32_t)(q - rel)));
     }
     // its bits, its place in the block's stream, its symbols: a match or two, or a
     // whole token's literal codes, as up to 4 words (LSB first) that go into the
@@ -1112,6 +1127,7 @@ __device__ void wv_item(const BgArgs &A, const Ctx<true> &C, uint64_t b0, uint64
     wv_pcycles(A, lane, 12, pt0);
 }
 
+template <bool CHECK>
 __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
     Stage &S = g_st;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1360,7 +1376,7 @@ __global__ __launch_bounds__(kWv) void bgzf_wave_kernel(BgArgs A) {
         Pend pend{~0u, 0, {0, 0, 0, 0}, 0};
         for (uint32_t i = wave; i < n_items; i += kWv / 64) {
             Pend cur;
-            wv_item(A, C, b0, e, i, lane, v, vkey, cur);
+            wv_item<CHECK>(A, C, b0, e, i, lane, v, vkey, cur);
 #ifdef BG_NO_DEFER  // (timing probe: each group placed at once)
             if (cur.i != ~0u) wv_emit(A, cur, lane);
             continue;
@@ -1611,7 +1627,10 @@ size_t bgzf_plan_bytes() { return sizeof(BlockPlan); }
 int launch_bgzf_blocks(const BgArgs &a, uint32_t n_blocks, hipStream_t stream) {
     if (n_blocks == 0) return TFBS_OK;
     hipLaunchKernelGGL(bgzf_plan_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, stream, a, n_blocks);
-    hipLaunchKernelGGL(bgzf_wave_kernel, dim3(n_blocks), dim3(kWv), 0, stream, a);
+    if (a.check)
+        hipLaunchKernelGGL(bgzf_wave_kernel<true>, dim3(n_blocks), dim3(kWv), 0, stream, a);
+    else
+        hipLaunchKernelGGL(bgzf_wave_kernel<false>, dim3(n_blocks), dim3(kWv), 0, stream, a);
     hipLaunchKernelGGL(bgzf_block_kernel, dim3(n_blocks), dim3(kBgBlock), 0, stream, a);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("bgzf_block_kernel: ") + hipGetErrorString(e));

@@ -35,6 +35,10 @@ struct BgArgs {
     void *plans;                // per block of the launch: bgzf_plan_bytes() of scratch
     uint64_t *prof;             // optional (TFBS_BGZF_PROF): per block 32 words of phase clocks and counts
     uint32_t stored;            // TFBS_BGZF_STORED=1 (debug): bgzf_wave_kernel's blocks stored, its text as it is
+    // TFBS_BGZF_CHECK=1 (debug): the checked bgzf_wave_kernel, which counts here every
+    // block-text write that meets bits already set (the text is zeroed per block and
+    // every byte written once, by an LDS OR: the invariant behind its race fix)
+    uint32_t *check;
 };
 size_t bgzf_plan_bytes();
 

@@ -192,6 +192,7 @@ struct tfbs_ctx {
     DevBuf<uint64_t> bg_prof;         // TFBS_BGZF_PROF: bgzf_wave_kernel phase clocks
     uint32_t bg_crc_full = 0;         // bgzf_crc_tables' full-block CRC init term
     DevBuf<uint64_t> kf_prof;         // TFBS_KF_PROF: key_fast_kernel phase clocks and sizes per region
+    DevBuf<uint32_t> bg_check;  // TFBS_BGZF_CHECK=1: the checked BGZF wave kernel's violation count
     DevBuf<unsigned long long> scan_prof;  // TFBS_SCAN_PROF=<file>: scan_mfma_kernel's per-wave stamps (prof builds)
     DevBuf<uint32_t> asm_order;       // the resident batch's regions by distinct haplotypes, most first
     uint32_t asm_order_n = 0;         // regions asm_order holds (0: none)
@@ -1715,6 +1716,12 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
     a.crc_lane = ctx->bg_crc.p + 256 + 32 * kBgzfOps + 768;
     a.crc_full = ctx->bg_crc_full;
     a.stored = env_int("TFBS_BGZF_STORED", 0) != 0 ? 1u : 0u;
+    const bool bg_check = env_int("TFBS_BGZF_CHECK", 0) != 0;  // (debug: checked every launch, synchronously)
+    if (bg_check) {
+        if ((rc = ctx->bg_check.ensure(1))) return rc;
+        HIP_TRY(hipMemsetAsync(ctx->bg_check.p, 0, 4, ctx->stream));
+        a.check = ctx->bg_check.p;
+    }
     if ((rc = tfbs::launch_tok_lit(a, (uint32_t)plan.tok_len.size(), ctx->stream)) ||
         (rc = tfbs::launch_row_cum(a, ctx->stream)))
         return rc;
@@ -1753,6 +1760,14 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
             (rc = tfbs::launch_bgzf_compact(ctx->bg_out[k].p, ctx->bg_out_len[k].p, ctx->bg_off[k].p, nb,
                                             ctx->bg_packed[k].p, ctx->stream)))
             return rc;
+        if (bg_check) {
+            uint32_t bad = 0;
+            HIP_TRY(hipMemcpyAsync(&bad, ctx->bg_check.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(hipStreamSynchronize(ctx->stream));
+            if (bad)
+                return fail(TFBS_E_STATE, "bgzf_wave_kernel: " + std::to_string(bad) +
+                                                 " block-text writes met bits already set (TFBS_BGZF_CHECK)");
+        }
         HIP_TRY(hipMemcpyAsync(ctx->bg_total_host + k, ctx->bg_off[k].p + nb, 8, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(hipEventRecord(ctx->bg_done[k], ctx->stream));
         pp.pending[pp.n_pending++] = k;

@@ -47,16 +47,26 @@ inline uint32_t rev_bits(uint32_t x, int n) {
     return (((uint32_t)kRev8.r[x & 0xFF] << 8) | kRev8.r[(x >> 8) & 0xFF]) >> (16 - n);
 }
 
-// Canonical Huffman code of lens[0..n) (0: unused) into t; false if over-subscribed.
-bool build(Table &t, const uint8_t *lens, int n, int main_bits) {
+// How build() treats an incomplete code (fewer codes than its lengths allow), as
+// zlib's inflate_table does: a dynamic block's code-length code must be complete,
+// its literal/length and distance codes too unless they hold a single code of
+// length 1 (or none at all); the fixed distance code (30 of 32) is incomplete.
+enum Incomplete { kRejectIncomplete, kSingleCode, kAllowIncomplete };
+
+// Canonical Huffman code of lens[0..n) (0: unused) into t; false if over-subscribed
+// or incomplete where `inc` forbids it.
+bool build(Table &t, const uint8_t *lens, int n, int main_bits, Incomplete inc) {
     int count[16] = {0};
     for (int i = 0; i < n; i++) count[lens[i]]++;
     count[0] = 0;
-    int left = 1;
+    int left = 1, max_len = 0;
     for (int l = 1; l < 16; l++) {
         left = (left << 1) - count[l];
         if (left < 0) return false;
+        if (count[l]) max_len = l;
     }
+    if (left > 0 && max_len > 0 && inc != kAllowIncomplete && (inc == kRejectIncomplete || max_len != 1))
+        return false;  // zlib: "invalid code lengths set" / "invalid literal/lengths set"
     int next[16] = {0};
     for (int l = 1, code = 0; l < 16; l++) {
         code = (code + count[l - 1]) << 1;
@@ -163,10 +173,10 @@ struct FixedTables {
         for (int i = 144; i < 256; i++) l[i] = 9;
         for (int i = 256; i < 280; i++) l[i] = 7;
         for (int i = 280; i < 288; i++) l[i] = 8;
-        build(lit, l, 288, kLitBits);
+        build(lit, l, 288, kLitBits, kAllowIncomplete);
         uint8_t d[30];
         for (int i = 0; i < 30; i++) d[i] = 5;
-        build(dist, d, 30, kDistBits);
+        build(dist, d, 30, kDistBits, kAllowIncomplete);
     }
 };
 
@@ -207,7 +217,7 @@ int inflate_raw_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_
                 uint8_t cl[19] = {0};
                 for (int i = 0; i < hclen; i++) cl[ord[i]] = (uint8_t)b.get(3);
                 Table ct;
-                if (!build(ct, cl, 19, 7)) return -1;
+                if (!build(ct, cl, 19, 7, kRejectIncomplete)) return -1;
                 uint8_t lens[288 + 32];
                 int n = 0;
                 while (n < hlit + hdist) {
@@ -233,7 +243,8 @@ int inflate_raw_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_
                     }
                 }
                 if (!lens[256]) return -1;
-                if (!build(dyn_lit, lens, hlit, kLitBits) || !build(dyn_dist, lens + hlit, hdist, kDistBits)) return -1;
+                if (!build(dyn_lit, lens, hlit, kLitBits, kSingleCode) || !build(dyn_dist, lens + hlit, hdist, kDistBits, kSingleCode))
+                    return -1;
                 lt = &dyn_lit;
                 dt = &dyn_dist;
             }

@@ -322,6 +322,7 @@ struct Ordered {
         cv.wait(l, [&] { return failed || (items[g].ready && off[g] >= 0); });
         if (failed) return false;
         it = std::move(items[g]);
+        items[g].fd = -1;  // the writer owns (and closes) the memory file now
         at = off[g];
         return true;
     }
@@ -350,6 +351,7 @@ struct Ordered {
         cv.wait(l, [&] { return failed || items[g].ready; });
         if (failed) return false;
         it = std::move(items[g]);
+        items[g].fd = -1;  // the writer owns (and closes) the memory file now
         return true;
     }
 };
@@ -637,7 +639,7 @@ int tfbs_run(const tfbs_run_args *a) {
         if (gpu_bgzf && !ord.failed) {  // the stream continues after the last batch's blocks
             if (int rc2 = w.seek_to((uint64_t)ord.off[n_batches])) return rc2;
         }
-        {  // memory files a failed run left behind
+        {  // memory files no writer took (a failed run); taken ones were handed over (fd -1 here)
             std::lock_guard<std::mutex> l(ord.mu);
             for (auto &it : ord.items)
                 if (it.fd >= 0) close(it.fd);

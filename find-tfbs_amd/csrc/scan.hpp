@@ -94,7 +94,7 @@ struct ScanArgs {
     // (tools/scan_prof.py); null otherwise
     unsigned long long *prof;
 };
-constexpr uint32_t kScanProfWords = 8;
+constexpr uint32_t kScanProfWords = 16;
 constexpr uint32_t kRefPerRegion = 64;
 constexpr uint32_t kMBlockWaves = 8;  // waves per matrix-core workgroup (hit list parts per workgroup)
 constexpr uint32_t kCandWords = 2;  // candidate list entry: strand | haplotype in the group << 24, window

@@ -428,8 +428,20 @@ __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
     for (int k = 0; k < 5; k++) asm volatile("" : "+v"(p[k]));
     return ((p[0] | p[1] | p[2]) | (p[3] | p[4] | u[15])) & kTestMask;
 #endif
+#if defined(TFBS_AB_NOTEST) || defined(TFBS_AB_NOFIRE)
+    // timing ablations (wrong results): an opaque zero ends the test; NOTEST reads one
+    // accumulator (the MFMAs stay live), NOFIRE keeps the whole test and never fires
+    uint32_t z;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(z));
+#ifdef TFBS_AB_NOTEST
+    return u[15] & z;
+#endif
+#endif
     const uint32_t x = (u[0] | u[1] | u[2]) | (u[3] | u[4] | u[5]) | (u[6] | u[7] | u[8]) | (u[9] | u[10] | u[11]) |
                        (u[12] | u[13] | u[14]) | u[15];
+#ifdef TFBS_AB_NOFIRE
+    return x & kTestMask & z;
+#endif
     return x & kTestMask;
 }
 
@@ -582,6 +594,19 @@ __device__ __forceinline__ void scan_segment_pipe(const ScanArgs &A, const char 
 
 #endif
 
+#ifdef TFBS_ROUND_PROF
+// Per-round clock split (profiling builds only, TFBS_SCAN_PROF words 8-15): per wave,
+// shader cycles from a two-tile round's top to its first MFMA's issue (the chunk-0 B
+// fragment and the matrix pipe), first to last MFMA issued, last MFMA to the test's
+// decision, the firing path; rounds, fired rounds; the super tiles' restaging; the
+// pairs' own work (next pair, list entries, A fragments).  s_memtime between
+// scheduling barriers: the stamps order the round but add their own latency.
+__shared__ unsigned long long s_rprof[kMBlock / 64][8];
+#define RPROF_T() ({ __builtin_amdgcn_sched_barrier(0); const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+                     __builtin_amdgcn_sched_barrier(0); t_; })
+#define RPROF_ADD(wave, k, v) do { if ((threadIdx.x & 63) == 0) s_rprof[wave][k] += (v); } while (0)
+#endif
+
 // The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
 // ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
 template <int D, int NK>
@@ -590,6 +615,77 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
                                              const v4i (&a1)[NK], bool two, uint32_t ta, const v16f &cb, int sa,
                                              uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
+#ifdef TFBS_ROUND_PROF
+    if (two) {
+        const char *tile = img;
+        const char *const end = img + (te - tb) * kTB;
+        uint32_t ti = tb;
+        BFrag pf;
+        load_frag0(img, lane, pf);
+        unsigned long long pb = 0, pm = 0, pt = 0, pfi = 0, nr = 0, nf = 0;
+        do {
+            const unsigned long long t0 = RPROF_T();
+            BFrag f[D];
+            f[0] = pf;
+#pragma unroll
+            for (int kc = 1; kc < D; kc++) {
+                f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
+                f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
+            }
+            v16f c0 = mfma_chunk(a0[0], f[0], cb, sa);
+            const unsigned long long t1 = RPROF_T();
+            v16f c1 = mfma_chunk(a1[0], f[0], cb, sa);
+#pragma unroll
+            for (int kc = 1; kc < D; kc++) {
+                c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+                c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+            }
+            const unsigned long long t2 = RPROF_T();
+            load_frag0(tile + kTB, lane, pf);
+            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
+            const bool any = __ballot((x0 | x1) != 0) != 0;
+            const unsigned long long t3 = RPROF_T();
+            if (__builtin_expect(any, 0)) {
+                nf++;
+                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
+                if (f0) {
+                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x0 = coarse_test(c0);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
+                }
+                if (f1) {
+                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
+                        drain_queue(A, G, qn, wave, lane, cn);
+                        qn = 0;
+                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
+                        x1 = coarse_test(c1);
+                    }
+                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
+                }
+            }
+            const unsigned long long t4 = RPROF_T();
+            pb += t1 - t0;
+            pm += t2 - t1;
+            pt += t3 - t2;
+            pfi += t4 - t3;
+            nr++;
+            tile += kTB;
+            ti++;
+        } while (tile != end);
+        RPROF_ADD(wave, 0, pb);
+        RPROF_ADD(wave, 1, pm);
+        RPROF_ADD(wave, 2, pt);
+        RPROF_ADD(wave, 3, pfi);
+        RPROF_ADD(wave, 4, nr);
+        RPROF_ADD(wave, 5, nf);
+        return;
+    }
+#endif
 #if TFBS_BPF2
     if (two && D == 2) {
         // depth 2: both chunks' B fragments of the next strand tile are read during the
@@ -815,12 +911,22 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
     if (p < npair) entries(p, ea, eb);
     while (p < npair) {
         n_pairs++;
+#ifdef TFBS_ROUND_PROF
+        const unsigned long long tp0 = RPROF_T();
+#endif
         const uint32_t pn = next_pair();
         const bool two = 2 * p + 1 < ntile;
         v4i a0[NK], a1[NK];
         entry_onehot<NK>(A, words, ea, tab, a0);
         entry_onehot<NK>(A, words, eb, tab, a1);  // (a copy of the last window when !two: unused)
         if (pn < npair) entries(pn, ea, eb);      // in flight while this pair is scored
+#ifdef TFBS_ROUND_PROF
+        // the A fragments awaited here (their LDS reads), so that the pair's first
+        // round does not carry them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long tp1 = RPROF_T();
+        RPROF_ADD(wave, 7, tp1 - tp0);
+#endif
         scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
         p = pn;
     }
@@ -920,12 +1026,24 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
 #ifdef TFBS_SCAN_PROF
     bool first = true;
 #endif
+#ifdef TFBS_ROUND_PROF
+    if (threadIdx.x < kMBlockWaves * 8) (&s_rprof[0][0])[threadIdx.x] = 0;
+#endif
     for (uint32_t si = 0; si < A.n_msupers; si++) {
         const DevMSuper S = A.msupers[si];
+#ifdef TFBS_ROUND_PROF
+        const unsigned long long ts0 = RPROF_T();
+#endif
         __syncthreads();  // the previous image's readers are done
+#ifdef TFBS_AB_NORESTAGE  // timing ablation (wrong results): the first image only
+        if (si == 0)
+#endif
         stage_image(A, S, reinterpret_cast<uint4 *>(smem));
         if (threadIdx.x == 0) s_hnext = 0;
         __syncthreads();
+#ifdef TFBS_ROUND_PROF
+        if (si) RPROF_ADD(wave, 6, RPROF_T() - ts0);
+#endif
 #ifdef TFBS_SCAN_PROF
         if (first) {
             SCAN_STAMP(0, t_start);
@@ -940,10 +1058,15 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
     (void)n_pairs;
     SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
+#ifndef TFBS_AB_NORESCORE  // timing ablation (wrong results): no rescoring
     rescore_list(A, words, h0, wave, lane, cn);
+#endif
     SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
     SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
+#ifdef TFBS_ROUND_PROF
+    for (int k = 0; k < 8; k++) SCAN_STAMP(8 + k, s_rprof[wave][k]);
+#endif
 }
 
 // Candidates past the waves' list regions (drain_queue), one per thread; their
@@ -1328,7 +1451,9 @@ int launch_mfma_all(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supe
     const size_t base = kMOnehotBytes + img_bytes + kMChunkBytes;  // (the padding: scan_segment's B prefetch)
     const size_t staged_bytes = base + ((size_t)group_words * 4 + 15) / 16 * 16;
     const bool staged = staged_bytes + static_lds <= kMStagedMax;
-    const size_t lds = staged ? staged_bytes : base;
+    // (TFBS_SCAN_LDS_MIN: an occupancy A/B -- more LDS per workgroup, fewer per CU)
+    static const size_t lds_min = getenv("TFBS_SCAN_LDS_MIN") ? (size_t)atol(getenv("TFBS_SCAN_LDS_MIN")) : 0;
+    const size_t lds = std::max(staged ? staged_bytes : base, lds_min);
     const MfmaKernel kern = mfma_all_variant(staged);
     hipError_t e = hipSuccess;
     if (lds > 64 * 1024)

@@ -147,8 +147,9 @@ constexpr inline uint32_t mfma_depth_class(uint32_t nk) { return nk <= 2 ? 2u : 
 // window at i + its shift, so its hit (or none) is that window's, which the key
 // assembly adds (key_kernels.hip, with the runs in the reference's columns:
 // DevHap::rrun_off).  The matrix-core scan reads the windows dirty for the span
-// S = 8 nk of their depth class (S >= L: a superset; the window list,
-// scan_mfma.hip) and lists only the hits of windows dirty for the strand's L.
+// S = the longest strand of their depth class (DevMSuper::lmax, or 8 nk when the
+// class's span is not given; S >= L: a superset; the window list, scan_mfma.hip)
+// and lists only the hits of windows dirty for the strand's L.
 enum HapFlags : uint32_t { HAP_HAS_N = 1u, HAP_HAS_POS = 2u, HAP_REF = 4u, HAP_DEDUP = 8u };
 constexpr uint32_t kDedupMaxWindows = 1024;  // longest HAP_DEDUP haplotype (and reference)
 constexpr uint32_t kMaxDiffRuns = 16;        // diff runs of a HAP_DEDUP haplotype
@@ -170,7 +171,7 @@ struct DevHap {
     uint32_t n_rruns;
 };
 
-// Window w of span S (a strand's L, or a depth class's 8 nk) is dirty for a
+// Window w of span S (a strand's L, or a depth class's longest strand) is dirty for a
 // haplotype with diff runs r (HAP_DEDUP): some run meets its columns [w, w + S - 1].
 inline constexpr bool run_meets(uint32_t a, uint32_t b, uint32_t w, uint32_t S) { return a <= w + S - 1 && b >= w; }
 

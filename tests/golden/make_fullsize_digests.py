@@ -3,7 +3,7 @@
 TEST INFRASTRUCTURE: runs the CPU oracle (oracle/tfbs_oracle.c, the C restatement of
 main.rs:94-154, 395-534 and haplotype.rs:13-156) over the same synthetic regions bench.py
 times (the product's deterministic generator, SURVEY.md 8(d): C3 and C5 in full, 10 000
-regions each; C4 a spread of 1 000+ of its 100 000) and writes per region
+regions each; C4 a spread of 10 000+ of its 100 000, 1 250+ per shard of 12 500) and writes per region
 
   keys[i]   the oracle's orc_job_digests key sketch (count_matches_by_sample vectors),
   rows[i]   XXH64 of the region's rows without POS,
@@ -49,7 +49,7 @@ def spread(n, count):
 
 def region_indices(name):
     n = WORKLOADS[name][1]
-    return spread(n, 1000) if name == "C4" else list(range(n))
+    return spread(n, 10000) if name == "C4" else list(range(n))
 
 
 def golden_path(name):

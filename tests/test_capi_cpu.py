@@ -252,3 +252,23 @@ def test_mfma_bound_eligibility():
     assert ps.mfma_bound(0, "AA")["eligible"] == 0
     assert ps.mfma_bound(1, "AAA")["eligible"] == 1
     assert ps.mfma_bound(2, "A" * 33)["eligible"] == 0
+
+
+@pytest.mark.parametrize("indel", [0, 30])
+def test_prep_overlap_same_batch(tmp_path, indel, monkeypatch):
+    """tfbs_synth_fill_batch commits chunk k while it builds chunk k + 1 (build_regions and
+    commit_regions on two threads, disjoint Batch fields: batch.hpp).  The packed batch must
+    not depend on it: every region's input digest and stats with the overlap on equal the
+    serial order's (TFBS_PREP_OVERLAP=0).  Two host threads make 128-region chunks, so 300
+    regions take three chunks and two overlapped commits."""
+    ps, _ = synth_patterns(str(tmp_path), 12, 3, 5)
+    monkeypatch.setenv("TFBS_HOST_THREADS", "2")
+    got = {}
+    for ov in ("0", "1"):
+        monkeypatch.setenv("TFBS_PREP_OVERLAP", ov)
+        b = T.RegionBatch(ps, 400, keep_membership=True)
+        b.synth_fill(7, 0, 300, indel)
+        got[ov] = (b.num_regions, b.num_windows, b.num_effective_windows,
+                   [(b.region_stats(r), b.input_digest(r)) for r in range(b.num_regions)])
+    assert got["0"][0] == 300
+    assert got["0"] == got["1"]

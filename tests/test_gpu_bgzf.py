@@ -118,6 +118,33 @@ def test_bgzf_c3_regions_vs_host_rows(tmp_path):
     assert len(data) * 8 < len(want)
 
 
+def test_bgzf_text_writes_meet_zeroed_lds(tmp_path, monkeypatch):
+    """TFBS_BGZF_CHECK=1: the checked bgzf_wave_kernel counts every block-text LDS write
+    (always an OR, fc3b823) that meets bits already set -- a byte written twice, or a
+    staged text's zero padding that is not zero.  On the C3 generator's rows (runs,
+    look-back matches, literals, 50 000 samples) and on a small indel set the count stays
+    0 (the call fails otherwise) and the blocks inflate to the host rows."""
+    monkeypatch.setenv("TFBS_BGZF_CHECK", "1")
+    names = T.synth_write_pwms(str(tmp_path), 600, 3, 3)
+    ps = T.parse_pwm_files(os.path.join(str(tmp_path), "pwms.txt"), os.path.join(str(tmp_path), "thr"), 1e-4, names)
+    b = T.RegionBatch(ps, 50000)
+    b.synth_fill(3, 200, 60, 0)
+    sc = T.Scanner(ps)
+    try:
+        b.scan(sc, reduce=True)
+        want, _ = b.rows("chr1")
+        got, _, _ = _device_rows(b, sc, "chr1", chunk=64)
+    finally:
+        sc.close()
+    assert got == want
+    (tmp_path / "small").mkdir()
+    ps2, _ = synth_patterns(tmp_path / "small", 40, 3, 107, thr=1e-3)
+    n_regions = 40
+    beds = [("synthetic.bed", [(1000 + 400 * j, 1200 + 400 * j) for j in range(n_regions)])]
+    regions = make_regions_synth(19, 0, n_regions, 3000, ps2.max_length, 20)
+    _compare(ps2, 3000, beds, regions)
+
+
 @pytest.mark.parametrize("batch_blocks", [None, "2"])
 def test_bgzf_many_pieces_one_call(tmp_path, monkeypatch, batch_blocks):
     """One call over 640 regions (the run flow's batches are 512): 8 pieces, the host

@@ -377,3 +377,76 @@ def test_inflate_raw_matches_zlib():
                     bad[len(bad) // 2] ^= 0x55
                     fast(bytes(bad), len(data))
     assert checked == 600 * 16
+
+
+def _dynamic_block(lit_lens, dist_lens, symbols):
+    """A raw DEFLATE stream of one final dynamic block with the given literal/length and
+    distance code lengths (written one by one through a complete code-length code:
+    lengths 0 -> '0', 1 -> '10', 2 -> '11') and the literal symbols (< 256) then EOB."""
+    bits = []
+
+    def put(v, n):  # LSB first
+        bits.extend((v >> i) & 1 for i in range(n))
+
+    def code(c, n):  # Huffman codes MSB first
+        bits.extend((c >> (n - 1 - i)) & 1 for i in range(n))
+
+    def canon(lens):  # RFC 1951 3.2.2
+        count = [sum(1 for x in lens if x == ln) if ln else 0 for ln in range(16)]
+        codes, nxt, c = {}, {}, 0
+        for ln in range(1, 16):
+            c = (c + count[ln - 1]) << 1
+            nxt[ln] = c
+        for s, ln in enumerate(lens):
+            if ln:
+                codes[s] = (nxt[ln], ln)
+                nxt[ln] += 1
+        return codes
+
+    put(1, 1)
+    put(2, 2)
+    put(len(lit_lens) - 257, 5)
+    put(len(dist_lens) - 1, 5)
+    order = [16, 17, 18, 0, 8, 7, 9, 6, 10, 5, 11, 4, 12, 3, 13, 2, 14, 1, 15]
+    cl = [0] * 19
+    cl[0], cl[1], cl[2] = 1, 2, 2
+    put(18 - 4, 4)
+    for k in range(18):
+        put(cl[order[k]], 3)
+    cc = canon(cl)
+    for ln in list(lit_lens) + list(dist_lens):
+        code(*cc[ln])
+    lc = canon(lit_lens)
+    for s in list(symbols) + [256]:
+        code(*lc[s])
+    while len(bits) % 8:
+        bits.append(0)
+    return bytes(sum(bits[i + j] << j for j in range(8)) for i in range(0, len(bits), 8))
+
+
+def test_inflate_raw_rejects_incomplete_codes():
+    """A dynamic block whose literal/length code is incomplete (two codes of length 2)
+    is refused, as zlib refuses it ('invalid literal/lengths set'), even though every
+    symbol the stream uses has a code and the output length matches; a single distance
+    code of length 1 (zlib's allowed incomplete case) and complete codes still decode."""
+    import ctypes as C
+    import zlib
+
+    L = T.lib()
+
+    def fast(comp, n):
+        out = C.create_string_buffer(max(n, 1) + 16)
+        return L.tfbs_inflate_raw(comp, len(comp), out, n), out.raw[:n]
+
+    lit = [0] * 257
+    lit[65], lit[256] = 2, 2  # incomplete: 2 of 4 codes of length 2
+    bad = _dynamic_block(lit, [1], [65] * 4)
+    with pytest.raises(zlib.error):
+        zlib.decompressobj(-15).decompress(bad)
+    rc, _ = fast(bad, 4)
+    assert rc != 0
+    lit[66], lit[67] = 2, 2  # complete; the one distance code of length 1 stays allowed
+    good = _dynamic_block(lit, [1], [65, 66, 67, 65])
+    assert zlib.decompressobj(-15).decompress(good) == b"ABCA"
+    rc, out = fast(good, 4)
+    assert rc == 0 and out == b"ABCA"

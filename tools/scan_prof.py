@@ -23,7 +23,7 @@ def read(path):
         i += 2
         srcs = raw[i:i + 5 * n_srcs].reshape(n_srcs, 5)
         i += 5 * n_srcs
-        scans.append((srcs, raw[i:i + n].reshape(-1, 8, 8)))
+        scans.append((srcs, raw[i:i + n].reshape(-1, 8, 16)))
         i += n
     return scans
 
@@ -62,6 +62,18 @@ def main():
             "tail_us": {"after_90pct_end": float(span - ends[int(0.9 * (len(ends) - 1))]),
                         "after_99pct_end": float(span - ends[int(0.99 * (len(ends) - 1))])},
         }
+        if w[:, :, 12].sum() > 0:  # TFBS_ROUND_PROF build: the two-tile rounds' clock split
+            rb, rm, rt, rf, nr, nf, rs, pp = (w[:, :, 8 + k][live].sum() for k in range(8))
+            loop = ph["loop"][live].sum()
+            rec["round_split"] = {
+                "rounds_per_wave": float(nr / live.sum()), "fired_share": float(nf / max(1, nr)),
+                "cycles_per_round": {"to_first_mfma": float(rb / nr), "first_to_last_mfma": float(rm / nr),
+                                     "last_mfma_to_test": float(rt / nr), "firing_path": float(rf / nr)},
+                "loop_share": {"to_first_mfma": float(rb / loop), "first_to_last_mfma": float(rm / loop),
+                               "last_mfma_to_test": float(rt / loop), "firing_path": float(rf / loop),
+                               "restaging": float(rs / loop), "pair_setup": float(pp / loop),
+                               "other": float(1 - (rb + rm + rt + rf + rs + pp) / loop)},
+            }
         out["launches"].append(rec)
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
