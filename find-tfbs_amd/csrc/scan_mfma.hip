@@ -1,43 +1,42 @@
-// Matrix-core scan (gfx950 v_mfma_scale_f32_32x32x64_f8f6f4, FP4 x FP6) for
+// Matrix-core scan (gfx950 v_mfma_scale_f32_32x32x64_f8f6f4, FP6 x FP4) for
 // strands with L <= 32 (mfma.cpp).
 //
 // matches (pattern.rs:141-171) scores every window i of a haplotype with
-// sum_j w[j][nuc(i + j)] (N = 0, pattern.rs:119-135).  For 32 consecutive
-// windows x a set of strands that is a GEMM: A[window][k] = one-hot of the
-// window's bases (all zero for N), B[k][strand] = the strand's weights.  The
-// kernel runs it on FP6 digits q <= 0 of an upper bound (score <= C + s Q,
-// mfma.cpp) with the one-hot in FP4, at the matrix cores' FP4/FP6 rate.  U = 8 Q
-// > T0 is necessary for a hit; those candidate windows are rescored exactly
-// from the strand's integer weights.
+// sum_j w[j][nuc(i + j)] (N = 0, pattern.rs:119-135).  For 32 windows x a set of
+// strands that is a GEMM: the strands' weights times the windows' one-hot bases
+// (all zero for N).  The kernel runs it on FP6 digits q <= 0 of an upper bound
+// (score <= C + s Q, mfma.cpp) with the one-hot in FP4, at the matrix cores'
+// FP4/FP6 rate.  U = 8 Q > T0 is necessary for a hit; those candidate windows are
+// rescored exactly from the strand's integer weights.
 //
-//  * Two strands per GEMM column: the K chunk of 64 holds 8 columns of strand
-//    2n (K block 0) and of strand 2n + 1 (K block 1); the A fragment carries the
-//    window's one-hot in both blocks, block 1 with scale 2^11, B scale 2^3
-//    (digits x 8 = integers), and the accumulator starts at 2^23 + (1023 - T0)
-//    (1 + 2^11).  Every output is an integer in [2^23, 2^24) (exact in f32) whose
-//    mantissa holds V = U + 1023 - T0 of strand 2n in bits 0-10 and of strand
-//    2n + 1 in bits 11-21, each in [0, 2048) (mfma.cpp clips the digits so);
-//    U > T0 iff the field's top bit (10 or 21) is set.  One OR tree over a
-//    lane's 16 outputs (v_or3 + v_bitop3) tests 32 (window, strand) pairs.
+//  * Two strands per GEMM row: the K chunk of 64 holds 8 columns of strand 2n (K
+//    block 0) and of strand 2n + 1 (K block 1); A = the digits (scale 2^3: digits x 8
+//    = integers; block 1 2^14: the field one up), B = the window's one-hot in both
+//    blocks, and the accumulator starts at 2^23 + (1023 - T0) (1 + 2^11).  Every
+//    output is an integer in [2^23, 2^24) (exact in f32) whose mantissa holds V = U +
+//    1023 - T0 of strand 2n in bits 0-10 and of strand 2n + 1 in bits 11-21, each in
+//    [0, 2048) (mfma.cpp clips the digits so); U > T0 iff the field's top bit (10 or
+//    21) is set.  One OR tree over a lane's 16 outputs (v_or3 + v_bitop3) tests 32
+//    (window, strand) pairs.
 //  * A workgroup (8 waves) stages one super tile (tiles of 64 strands of equal
 //    K depth), the one-hot table, its group's haplotype descriptors and packed
-//    words in LDS.  Every B fragment is one conflict-free ds_read_b128 +
+//    words in LDS.  Every digit fragment is one conflict-free ds_read_b128 +
 //    ds_read_b64 per lane and feeds two window tiles.
 //  * Window tiles come from the group's window list (build_window_lists): 32
 //    listed windows of any of the group's haplotypes per tile, lane l & 31 its
 //    own (haplotype, window), so reference-window reuse leaves no holes.
-//  * C layout: lane l holds column l & 31 (strands 2 (l & 31), + 1) and windows
-//    (r & 3) + 8 (r >> 2) + 4 (l >> 5), r < 16.  A firing lane (rare) appends
-//    the fields' top bits of its 16 outputs (16 bytes) to the wave's LDS queue;
-//    drain_queue decodes them (through the window list) into (haplotype,
-//    strand, window) candidates in the
-//    wave's region of a global (L2-resident) list, and when the wave has
-//    scanned it rescores those exactly, one per lane (pattern.rs:125-151),
-//    applies the inner-range overlap test (range.rs:18-21 as main.rs:503 uses
-//    it) and appends one (haplotype, key) pair per hit and overlapped range to
-//    its part of the workgroup's hit list (no count matrix, no atomics: the
-//    key assembly, key_kernels.hip, counts them per region); a full wave list
-//    spills to a launch-wide list rescored by cand_over_kernel after the scan.
+//  * C layout: lane l holds column l & 31 -- the window of its own list entry --
+//    and strand pairs (r & 3) + 8 (r >> 2) + 4 (l >> 5), r < 16.  A firing lane
+//    (a candidate among its 32 strands) queues a self-contained record (its
+//    fields' top bits, its window's list entry, the strand tile) in LDS; the wave
+//    decodes its records in batches into (haplotype, strand, window) candidates
+//    (drain_queue: no global load); when the wave has scanned
+//    it rescores those exactly, one per lane (pattern.rs:125-151), applies the
+//    inner-range overlap test (range.rs:18-21 as main.rs:503 uses it) and appends
+//    one (haplotype, key) pair per hit and overlapped range to its part of the
+//    workgroup's hit list (no count matrix, no atomics: the key assembly,
+//    key_kernels.hip, counts them per region); a full wave list spills to a
+//    launch-wide list rescored after the scan.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -66,7 +65,8 @@ constexpr uint32_t kMfmaRegWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 constexpr int kMfmaMinWaves[kMMaxChunks + 1] = {4, 4, 4, 4, 4};
 constexpr uint32_t kTestMask = (1u << (kMFieldBits - 1)) | (1u << (2 * kMFieldBits - 1));  // the fields' top bits
 constexpr uint32_t kQueueBits = 0x20200404u;  // those bits after queue_tile's byte permute (outputs 2j, 2j + 1)
-constexpr int kScaleA0 = 127, kScaleA1 = 127 + kMFieldBits, kScaleB = 130;  // e8m0: 1, 2^11, 2^3
+// e8m0 scales: the digits x 8 (K block 0), x 2^(3 + 11) (block 1: the field one up); the one-hot x 1
+constexpr int kScaleD0 = 130, kScaleD1 = 130 + kMFieldBits, kScaleOnehot = 127;
 
 // A lane's haplotype (the group's descriptors are staged in LDS, s_hd).
 struct LaneHap {
@@ -150,25 +150,36 @@ __device__ __forceinline__ void load_frags(const char *tile, uint32_t lane, BFra
     }
 }
 
-// One chunk: FP4 one-hot (A) x FP6 digits (B), f32 accumulate; sa: the lane's
-// A scale (2^11 for the pair's second strand), B digits x 8
+// One chunk: FP6 digits (A: rows = the tile's 32 strand pairs) x FP4 one-hot (B:
+// columns = the tile's 32 windows), f32 accumulate; sa: the lane's A scale (digits x 8,
+// x 2^14 for the pair's second strand, K block 1), B scale 1.  (A and B have the same
+// lane layout -- lane l: row / column l & 31, K block l >> 5 -- so the image and the
+// one-hot serve either operand; with the windows as columns a lane's 16 outputs are 16
+// strand pairs of ONE window, the window of its own list entry.)
 __device__ __forceinline__ v16f mfma_chunk(const v4i &a, const BFrag &f, const v16f &acc, int sa) {
-    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v8i{a[0], a[1], a[2], a[3], 0, 0, 0, 0},
-                                                           v8i{f.b[0], f.b[1], f.b[2], f.b[3], f.c.x, f.c.y, 0, 0},
-                                                           acc, 4 /* A: FP4 e2m1 */, 2 /* B: FP6 e2m3 */, 0, sa, 0,
-                                                           kScaleB);
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(v8i{f.b[0], f.b[1], f.b[2], f.b[3], f.c.x, f.c.y, 0, 0},
+                                                           v8i{a[0], a[1], a[2], a[3], 0, 0, 0, 0}, acc,
+                                                           2 /* A: FP6 e2m3 */, 4 /* B: FP4 e2m1 */, 0, sa, 0,
+                                                           kScaleOnehot);
 }
 
-// Candidate handling.  A tile test that fires (about one in four) appends one
-// entry per firing lane to the wave's queue in LDS: bytes 1-2 of its 16 outputs
-// (the fields' top bits; 8 v_perm, 32 bytes; see drain_queue) and a descriptor
-// (bits 0-5 the lane, 6-11 the strand tile, 32-63 the window tile: its index
-// in the group's window list).  A tile whose entries do not fit drains the
-// queue (drain_queue) and its round is scored again, so no accumulator is live
-// across a drain.
-constexpr uint32_t kMQueue = 88;  // entries per wave (>= one tile's 64)
+// Candidate handling.  A firing lane (its window passed the coarse test for some
+// strand of the tile; ~40 % of the rounds have one) appends one record to its wave's
+// LDS queue (queue_tile): the fields' top bits of its 16 outputs (8 v_perm + 4
+// v_bitop3, 16 bytes), its own list entry (the window: s_went) and the tile's first
+// global strand | the lane.  The wave decodes its records in batches, one record per
+// lane (drain_queue, no global load), into (strand | haplotype in group << 24,
+// window) candidates: the first kWaveCands in LDS (s_cand), then the wave's region of
+// the global list (A.cands), then the launch-wide overflow list (cand_over_kernel /
+// post_scan_kernel).  A tile whose records do not fit drains the queue first and its
+// round is scored again (no accumulator live across a drain).  The wave rescores its
+// candidates after the scan (rescore_list).
+constexpr uint32_t kMQueue = 64;      // records per wave (>= one tile's 64 firing lanes)
+constexpr uint32_t kWaveCands = 48;   // LDS candidates per wave (C3: 66 mean; the rest in the global list)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue];
-__shared__ uint64_t s_qmeta[kMBlock / 64][kMQueue];
+__shared__ uint2 s_qmeta[kMBlock / 64][kMQueue];
+__shared__ uint2 s_cand[kMBlock / 64][kWaveCands];
+__shared__ uint32_t s_went[kMBlock / 64][64];  // per wave: the current pair's list entries (tile a | tile b)
 __shared__ uint32_t s_hnext;  // the workgroup's next pair of window tiles (scan_super)
 __shared__ uint4 s_hd[kMMaxHapsPerBlock];   // the group's haplotypes: LaneHap
 __shared__ uint4 s_hd2[kMMaxHapsPerBlock];  // and (region, pos_off, drun_off, n_druns) for the rescoring
@@ -302,77 +313,14 @@ __device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uin
     return mask;
 }
 
-// Drains the wave's first n queue entries, one entry per lane per pass: the
-// candidate bits of both strands of the entry's column are gathered into one
-// mask and each candidate (window row of a tile of the group's window list wl,
-// nw entries; rows past nw are the last tile's padding) is appended to the
-// wave's region of the candidate list (2 dwords: global strand | haplotype in
-// the group << 24, window), one candidate per lane per round; the wave rescores
-// its list when it has scanned (rescore_list).  A full region (dense hits)
-// spills to A.cand_over (cand_over_kernel).
-// h0: the workgroup's first haplotype; tile0: the super tile's first global tile.
+// The hit lists' room per wave (A.cand_cap per workgroup), and the candidates': the
+// LDS list's (at most kWaveCands) followed by the wave's region of the global list
+// (TFBS_CAND_CAP makes all of them small in the spill tests).
 __device__ __forceinline__ uint32_t wave_cand_cap(const ScanArgs &A) { return A.cand_cap / (kMBlock / 64); }
+__device__ __forceinline__ uint32_t wave_lds_cap(const ScanArgs &A) { return min(wave_cand_cap(A), kWaveCands); }
 __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
     return reinterpret_cast<uint2 *>(A.cands) + (size_t)(A.region_base + blockIdx.x) * A.cand_cap +
            (size_t)wave * wave_cand_cap(A);
-}
-
-__device__ __forceinline__ void drain_queue(const ScanArgs &A, const GroupCtx &G, uint32_t n, uint32_t wave,
-                                            uint32_t lane, uint32_t &cn) {
-    const uint32_t nw = G.nw, tile0 = G.tile0, h0 = G.h0;
-    uint2 *list = cand_list(A, wave);
-    const uint32_t cap = wave_cand_cap(A);
-    for (uint32_t e0 = 0; e0 < n; e0 += 64) {
-        const uint32_t e = e0 + lane;
-        uint32_t m = 0, g0 = 0, q0 = 0;
-        if (e < n) {
-            const uint4 d = s_qdata[wave][e];
-            const uint64_t q = s_qmeta[wave][e];
-            const uint32_t src = (uint32_t)q & 63u, ti = ((uint32_t)q >> 6) & 63u;
-            q0 = ((uint32_t)(q >> 32) << 5) + 4 * (src >> 5);  // the list position of the lane's row 0
-            g0 = (tile0 + ti) * kMStrands + 2 * (src & 31u);
-            // dword k (queue_tile): the first strand's top bits of outputs 4k, 4k+1,
-            // 4k+2, 4k+3 at 2, 10, 3, 11, the second's at 21, 29, 22, 30.  m bit
-            // b: strand b >> 4, output 4 (b >> 1 & 3) + 2 (b & 1) + (b >> 3 & 1)
-            const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
-            uint32_t lo = (dd[0] >> 2) & 0x303u, hi = (dd[0] >> 21) & 0x303u;
-#pragma unroll
-            for (int k = 1; k < 4; k++) {
-                lo |= (dd[k] << (2 * k - 2)) & (0x303u << (2 * k));
-                hi |= (dd[k] >> (21 - 2 * k)) & (0x303u << (2 * k));
-            }
-            m = lo | (hi << 16);
-        }
-        while (__ballot(m != 0) != 0) {
-            bool have = m != 0;
-            uint32_t b = 0, q = 0;
-            if (have) {
-                b = __builtin_ctz(m);
-                m &= m - 1;
-                const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
-                q = q0 + (r & 3) + 8 * (r >> 2);
-                have = q < nw;  // the last tile's padding rows repeat an earlier window
-            }
-            const uint64_t act = __ballot(have);
-            if (have) {
-                const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
-                const uint32_t we = G.at(q), hl = we & (kMMaxHapsPerBlock - 1), i = we >> 6, g = g0 + (b >> 4);
-                if (slot < cap) {
-                    list[slot] = make_uint2(g | (hl << 24), i);
-                } else {  // rescored after the scan (no rescoring code, whose loads would stay
-                          // pending, in the scan loop)
-                    const uint32_t o = atomicAdd(A.over + 1, 1u);
-                    if (o < A.cand_over_cap) {
-                        A.cand_over[3 * (size_t)o] = A.hap_base + h0 + hl;  // batch index
-                        A.cand_over[3 * (size_t)o + 1] = g;
-                        A.cand_over[3 * (size_t)o + 2] = i;
-                    }
-                }
-            }
-            cn += (uint32_t)__popcll(act);
-        }
-    }
 }
 
 // The wave's listed candidates, one per lane (after its scan: no accumulator
@@ -385,13 +333,13 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
     const size_t part = (size_t)(A.region_base + blockIdx.x) * A.cand_cap + (size_t)wave * cap;
     uint2 *out = reinterpret_cast<uint2 *>(A.hitl) + part;
     uint32_t hn = 0;  // wave-uniform
-    const uint32_t n = min(cn, cap);
-    const uint2 *list = cand_list(A, wave);
+    const uint32_t lcap = wave_lds_cap(A), n = min(cn, lcap + cap);
+    const uint2 *glist = cand_list(A, wave);
     for (uint32_t k0 = 0; k0 < n; k0 += 64) {
         const uint32_t k = k0 + lane;
         uint32_t mask = 0, key0 = 0, hap = 0;
         if (k < n) {
-            const uint2 c = list[k];
+            const uint2 c = k < lcap ? s_cand[wave][k] : glist[k - lcap];
             hap = h0 + (c.x >> 24);
             const uint32_t hl = c.x >> 24;  // the haplotype's descriptors, staged in LDS
             mask = score_candidate(A, words, CandHap::of(s_hd[hl], s_hd2[hl]), hap, c.x & 0xFFFFFFu, c.y, &key0);
@@ -445,56 +393,120 @@ __device__ __forceinline__ uint32_t coarse_test(const v16f &acc) {
     return x & kTestMask;
 }
 
-// A firing tile (x: the lane's coarse test, fired = its ballot; the queue has
-// room; t: its index in the group's window list): each firing lane queues bytes
-// 1-2 of its outputs (the fields' top bits); qn (wave-uniform) counts the wave's
-// queued entries.
-__device__ __forceinline__ void queue_tile(const v16f &acc, uint32_t x, uint64_t fired, uint32_t ti, uint32_t t,
-                                           uint32_t lane, uint32_t wave, uint32_t &qn) {
-    const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(fired >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fired, qn));
-    if (x) {
-        // bytes 1, 1', 2, 2' of outputs 2j, 2j + 1: top bits at 2, 10, 21, 29;
-        // dword k keeps those of j = 2k and, one bit up, of j = 2k + 1
-        uint32_t d[8];
+// The same tile's candidates decoded at once when the queue is full (rare): the
+// lane's mask as drain_queue builds it, each candidate listed as drain_queue lists it.
+__device__ __forceinline__ uint32_t record_mask(const uint32_t (&dd)[4]) {
+    // dword k (queue_tile): the first strand's top bits of outputs 4k, 4k+1, 4k+2,
+    // 4k+3 at 2, 10, 3, 11, the second's at 21, 29, 22, 30.  m bit b: strand b >> 4,
+    // output 4 (b >> 1 & 3) + 2 (b & 1) + (b >> 3 & 1)
+    uint32_t lo = (dd[0] >> 2) & 0x303u, hi = (dd[0] >> 21) & 0x303u;
 #pragma unroll
-        for (int j = 0; j < 8; j++)
-            d[j] = __builtin_amdgcn_perm(__float_as_uint(acc[2 * j + 1]), __float_as_uint(acc[2 * j]), 0x06020501u);
-        uint32_t x[4];
+    for (int k = 1; k < 4; k++) {
+        lo |= (dd[k] << (2 * k - 2)) & (0x303u << (2 * k));
+        hi |= (dd[k] >> (21 - 2 * k)) & (0x303u << (2 * k));
+    }
+    return lo | (hi << 16);
+}
+// bytes 1, 1', 2, 2' of outputs 2j, 2j + 1: top bits at 2, 10, 21, 29; dword k keeps
+// those of j = 2k and, one bit up, of j = 2k + 1
+__device__ __forceinline__ void record_bits(const v16f &acc, uint32_t (&x)[4]) {
+    uint32_t d[8];
 #pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = __builtin_amdgcn_bitop3_b32(d[2 * k], d[2 * k + 1] << 1, kQueueBits, 0xe4);  // M ? d[2k] : d[2k+1] << 1
+    for (int j = 0; j < 8; j++)
+        d[j] = __builtin_amdgcn_perm(__float_as_uint(acc[2 * j + 1]), __float_as_uint(acc[2 * j]), 0x06020501u);
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = __builtin_amdgcn_bitop3_b32(d[2 * k], d[2 * k + 1] << 1, kQueueBits, 0xe4);  // M ? d[2k] : d[2k+1] << 1
+}
+// Lists the candidates of mask m (bit b: strand b >> 4 of output r(b)) of a record
+// whose tile's first global strand | lane is gl and whose window entry is ent; one
+// per lane per pass.
+__device__ __forceinline__ void list_mask(const ScanArgs &A, const GroupCtx &G, uint32_t wave, uint32_t m, uint32_t gl,
+                                          uint32_t ent, uint32_t &cn) {
+    const uint32_t lcap = wave_lds_cap(A), cap = lcap + wave_cand_cap(A);
+    uint2 *glist = cand_list(A, wave);
+    const uint32_t hl = ent & (kMMaxHapsPerBlock - 1), i = ent >> 6;
+    const uint32_t gbase = (gl & ~63u) + 8 * ((gl >> 5) & 1u);  // the tile's first strand; lanes 32-63: pairs + 4
+    uint64_t act;
+    while ((act = __ballot(m != 0)) != 0) {
+        if (m) {
+            const uint32_t b = __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t r = 4 * ((b >> 1) & 3u) + 2 * (b & 1u) + ((b >> 3) & 1u);
+            const uint32_t g = gbase + 2 * ((r & 3u) + 8 * (r >> 2)) + (b >> 4);
+            const uint32_t slot = cn + __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0));
+            const uint2 c = make_uint2(g | (hl << 24), i);
+            if (slot < lcap) {
+                s_cand[wave][slot] = c;
+            } else if (slot < cap) {
+                glist[slot - lcap] = c;
+            } else {  // rescored after the scan (cand_over_kernel / post_scan_kernel)
+                const uint32_t o = atomicAdd(A.over + 1, 1u);
+                if (o < A.cand_over_cap) {
+                    A.cand_over[3 * (size_t)o] = A.hap_base + G.h0 + hl;  // batch index
+                    A.cand_over[3 * (size_t)o + 1] = g;
+                    A.cand_over[3 * (size_t)o + 2] = i;
+                }
+            }
+        }
+        cn += (uint32_t)__popcll(act);
+    }
+}
+
+// Decodes the wave's first n queue records, one per lane per pass: the record's
+// candidate bits (both strands of its 16 outputs) gathered into one mask, each
+// candidate listed (one per lane per round; cn: the wave's count, uniform).
+__device__ __forceinline__ void drain_queue(const ScanArgs &A, const GroupCtx &G, uint32_t n, uint32_t wave,
+                                            uint32_t lane, uint32_t &cn) {
+    for (uint32_t e0 = 0; e0 < n; e0 += 64) {
+        const uint32_t e = e0 + lane;
+        uint32_t m = 0, ent = 0, gl = 0;
+        if (e < n) {
+            const uint4 d = s_qdata[wave][e];
+            const uint2 q = s_qmeta[wave][e];
+            ent = q.x;
+            gl = q.y;
+            const uint32_t dd[4] = {d.x, d.y, d.z, d.w};
+            m = record_mask(dd);
+        }
+        list_mask(A, G, wave, m, gl, ent, cn);
+    }
+}
+
+// A firing tile (x: the lane's coarse test; q: the lane's list position, rows past
+// the list's nw entries being the last tile's padding; the queue has room for the
+// tile's records): each firing lane queues one record -- bytes 1-2 of its outputs
+// (the fields' top bits), its list entry (window row lane & 31 of window tile
+// `which`, s_went) and g0 | lane (g0: the strand tile's first global strand) --;
+// qn (uniform) counts the wave's records.
+__device__ __forceinline__ void queue_tile(const ScanArgs &A, const GroupCtx &G, const v16f &acc, bool mine, uint64_t f,
+                                           uint32_t g0, uint32_t which, uint32_t lane, uint32_t wave, uint32_t &qn,
+                                           uint32_t &cn) {
+    const uint32_t nf = (uint32_t)__popcll(f);
+    uint32_t ent = 0, x[4] = {0, 0, 0, 0};
+    if (mine) {
+        ent = s_went[wave][which * 32 + (lane & 31)];
+        record_bits(acc, x);
+    }
+    if (__builtin_expect(qn + nf > kMQueue, 0)) {  // the queue is full (dense hits): decoded first
+        drain_queue(A, G, qn, wave, lane, cn);
+        qn = 0;
+    }
+    if (mine) {
+        const uint32_t at = __builtin_amdgcn_mbcnt_hi((uint32_t)(f >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)f, qn));
         s_qdata[wave][at] = uint4{x[0], x[1], x[2], x[3]};
-        s_qmeta[wave][at] = (uint64_t)(lane | (ti << 6)) | ((uint64_t)t << 32);
+        s_qmeta[wave][at] = make_uint2(ent, g0 | lane);
     }
-    qn += (uint32_t)__popcll(fired);
+    qn += nf;
 }
 
-// The accumulators of one round: a strand tile of depth D (its image at
-// `tile`) x the window tiles a0, a1 (one B fragment read feeds both MFMAs),
-// starting from the field biases cb.
-template <int D, int NK>
-__device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v4i (&a1)[NK],
-                                             const v16f &cb, int sa, v16f &c0, v16f &c1) {
-    BFrag f[D];
-    load_frags<D>(tile, lane, f);
-    c0 = cb;
-    c1 = cb;
-#pragma unroll
-    for (int kc = 0; kc < D; kc++) {
-        c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
-        c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
-    }
-}
-
-#ifndef TFBS_BPREFETCH  // (unused by the tight loop, which always prefetches)
-#define TFBS_BPREFETCH 1
-#endif
-
-// The same with chunk 0's B fragment already loaded (f0: read during the round
-// before, so the round's first MFMAs do not wait for LDS); chunks 1.. are read
-// before the first MFMA is issued.
-template <int D, int NK>
-__device__ __forceinline__ void round_scores_pf(const char *tile, uint32_t lane, const BFrag &f0, const v4i (&a0)[NK],
-                                                const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
+// One round's chains with chunk 0's B fragment already loaded (f0: read during the
+// round before, so the round's first MFMAs do not wait for LDS); chunks 1.. are read
+// before the first MFMA is issued.  a1 / c1: the pair's second window tile (TWO).
+template <int D, int NK, bool TWO>
+__device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, const BFrag &f0, const v4i (&a0)[NK],
+                                             const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
+#ifndef TFBS_B_JIT
     BFrag f[D];
     f[0] = f0;
 #pragma unroll
@@ -503,96 +515,35 @@ __device__ __forceinline__ void round_scores_pf(const char *tile, uint32_t lane,
         f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
     }
     c0 = cb;
-    c1 = cb;
+    if (TWO) c1 = cb;
 #pragma unroll
     for (int kc = 0; kc < D; kc++) {
         c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
-        c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+        if (TWO) c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
     }
+#else
+    // chunk kc + 1's fragment read while chunk kc's MFMAs issue: two fragments live
+    // instead of D (depth 3-4 rounds hold 12-24 fewer VGPRs)
+    BFrag cur = f0;
+    c0 = cb;
+    if (TWO) c1 = cb;
+#pragma unroll
+    for (int kc = 0; kc < D; kc++) {
+        BFrag nx;
+        if (kc + 1 < D) {
+            nx.b = *reinterpret_cast<const v4i *>(tile + (kc + 1) * 1536 + lane * 16);
+            nx.c = *reinterpret_cast<const int2 *>(tile + (kc + 1) * 1536 + 1024 + lane * 8);
+        }
+        c0 = mfma_chunk(a0[kc], cur, c0, sa);
+        if (TWO) c1 = mfma_chunk(a1[kc], cur, c1, sa);
+        if (kc + 1 < D) cur = nx;
+    }
+#endif
 }
 __device__ __forceinline__ void load_frag0(const char *tile, uint32_t lane, BFrag &f) {
     f.b = *reinterpret_cast<const v4i *>(tile + lane * 16);
     f.c = *reinterpret_cast<const int2 *>(tile + 1024 + lane * 8);
 }
-
-template <int D, int NK>
-__device__ __forceinline__ void tile_scores(const char *tile, uint32_t lane, const v4i (&a0)[NK], const v16f &cb,
-                                            int sa, v16f &c0) {
-    BFrag f[D];
-    load_frags<D>(tile, lane, f);
-    c0 = cb;
-#pragma unroll
-    for (int kc = 0; kc < D; kc++) c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
-}
-
-
-#ifndef TFBS_PIPE  // (tried: no gain over the tight loop, profiles/r05/ab_scan_variants.txt)
-#define TFBS_PIPE 0
-#endif
-#ifndef TFBS_BPF2
-#define TFBS_BPF2 0
-#endif
-#if TFBS_PIPE
-// A tile's coarse test and, when it fires, its queue entries; the queue is
-// drained first when they may not fit (acc stays live across the drain).
-__device__ __forceinline__ void test_tile(const ScanArgs &A, const GroupCtx &G, const v16f &acc, uint32_t ti, uint32_t t,
-                                          uint32_t lane, uint32_t wave, uint32_t &qn, uint32_t &cn) {
-    const uint32_t x = coarse_test(acc);
-    const uint64_t f = __ballot(x != 0);
-    if (__builtin_expect(f != 0, 0)) {
-        if (qn + (uint32_t)__popcll(f) > kMQueue) {
-            drain_queue(A, G, qn, wave, lane, cn);
-            qn = 0;
-        }
-        queue_tile(acc, x, f, ti, t, lane, wave, qn);
-    }
-}
-
-// One window tile's chain of D MFMAs against a strand tile (B fragments f).
-template <int D, int NK>
-__device__ __forceinline__ v16f tile_chain(const v4i (&a)[NK], const BFrag (&f)[D], const v16f &cb, int sa) {
-    v16f c = mfma_chunk(a[0], f[0], cb, sa);
-#pragma unroll
-    for (int kc = 1; kc < D; kc++) c = mfma_chunk(a[kc], f[kc], c, sa);
-    return c;
-}
-
-// The software-pipelined form of scan_segment's two-tile rounds: per strand tile,
-// window tile ta's chain goes into X while the previous tile's window tile ta + 1
-// (Y, pending) is tested, then ta + 1's chain into Y while X is tested -- each
-// test's VALU work and its branch overlap the next chain's MFMAs instead of
-// waiting for the chain before them.  Y stays pending across segments (*pend:
-// the global tile of the pending Y; none at a pair's start) and is tested by the
-// caller at the pair's end.
-template <int D, int NK>
-__device__ __forceinline__ void scan_segment_pipe(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
-                                                  const GroupCtx &G, uint32_t lane, uint32_t wave,
-                                                  const v4i (&a0)[NK], const v4i (&a1)[NK], uint32_t ta,
-                                                  const v16f &cb, int sa, uint32_t &qn, uint32_t &cn, v16f &X,
-                                                  v16f &Y, bool &pend, uint32_t &pend_ti) {
-    constexpr uint32_t kTB = mfma_tile_bytes(D);
-    const char *tile = img;
-    BFrag pf;
-    load_frag0(img, lane, pf);
-    for (uint32_t ti = tb; ti < te; ti++, tile += kTB) {
-        BFrag f[D];
-        f[0] = pf;
-#pragma unroll
-        for (int kc = 1; kc < D; kc++) {
-            f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
-            f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
-        }
-        load_frag0(tile + kTB, lane, pf);  // (past the last tile: the padded image area, unused)
-        X = tile_chain<D, NK>(a0, f, cb, sa);
-        if (pend) test_tile(A, G, Y, pend_ti, ta + 1, lane, wave, qn, cn);
-        Y = tile_chain<D, NK>(a1, f, cb, sa);
-        test_tile(A, G, X, ti, ta, lane, wave, qn, cn);
-        pend = true;
-        pend_ti = ti;
-    }
-}
-
-#endif
 
 #ifdef TFBS_ROUND_PROF
 // Per-round clock split (profiling builds only, TFBS_SCAN_PROF words 8-15): per wave,
@@ -607,231 +558,104 @@ __shared__ unsigned long long s_rprof[kMBlock / 64][8];
 #define RPROF_ADD(wave, k, v) do { if ((threadIdx.x & 63) == 0) s_rprof[wave][k] += (v); } while (0)
 #endif
 
-// The strand tiles of depth D, [tb, te) (images from `img`), x window tiles
-// ta (A fragments a0) and, if two, ta + 1 (a1) of the group's list.
-template <int D, int NK>
+// The strand tiles of depth D, [tb, te) (images from `img`), x window tiles ta (A
+// fragments a0) and, if TWO, ta + 1 (a1) of the group's list: per strand tile one
+// round (D chunks x the window tiles), the coarse test of both tiles with one vector
+// compare, the firing path (queue_tile) only when some lane fired.  A pointer loop (3
+// scalar instructions per round); the next round's chunk-0 B fragment is read
+// unconditionally (past the last tile: the image area is padded by kMChunkBytes, the
+// value unused).
+template <int D, int NK, bool TWO>
 __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
                                              const GroupCtx &G, uint32_t lane, uint32_t wave, const v4i (&a0)[NK],
-                                             const v4i (&a1)[NK], bool two, uint32_t ta, const v16f &cb, int sa,
-                                             uint32_t &qn, uint32_t &cn) {
+                                             const v4i (&a1)[NK], uint32_t ta, const v16f &cb, int sa, uint32_t &qn,
+                                             uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
+    const char *tile = img;
+    const char *const end = img + (te - tb) * kTB;
+    uint32_t g0 = (G.tile0 + tb) * kMStrands;  // the tile's first global strand
+    const uint32_t q0 = kMWindows * ta + (lane & 31);  // the lane's list positions (tile a; tile b: + 32)
+    BFrag pf;
+    load_frag0(img, lane, pf);
 #ifdef TFBS_ROUND_PROF
-    if (two) {
-        const char *tile = img;
-        const char *const end = img + (te - tb) * kTB;
-        uint32_t ti = tb;
-        BFrag pf;
-        load_frag0(img, lane, pf);
-        unsigned long long pb = 0, pm = 0, pt = 0, pfi = 0, nr = 0, nf = 0;
-        do {
-            const unsigned long long t0 = RPROF_T();
-            BFrag f[D];
-            f[0] = pf;
+    unsigned long long pb = 0, pm = 0, pt = 0, pfi = 0, nr = 0, nf = 0;
+#endif
+    do {
+#ifdef TFBS_ROUND_PROF
+        const unsigned long long t0 = RPROF_T();
+        BFrag f[D];
+        f[0] = pf;
 #pragma unroll
-            for (int kc = 1; kc < D; kc++) {
-                f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
-                f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
-            }
-            v16f c0 = mfma_chunk(a0[0], f[0], cb, sa);
-            const unsigned long long t1 = RPROF_T();
-            v16f c1 = mfma_chunk(a1[0], f[0], cb, sa);
+        for (int kc = 1; kc < D; kc++) {
+            f[kc].b = *reinterpret_cast<const v4i *>(tile + kc * 1536 + lane * 16);
+            f[kc].c = *reinterpret_cast<const int2 *>(tile + kc * 1536 + 1024 + lane * 8);
+        }
+        v16f c0 = mfma_chunk(a0[0], f[0], cb, sa), c1;
+        const unsigned long long t1 = RPROF_T();
+        if (TWO) c1 = mfma_chunk(a1[0], f[0], cb, sa);
 #pragma unroll
-            for (int kc = 1; kc < D; kc++) {
-                c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
-                c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
-            }
-            const unsigned long long t2 = RPROF_T();
-            load_frag0(tile + kTB, lane, pf);
-            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
-            const bool any = __ballot((x0 | x1) != 0) != 0;
-            const unsigned long long t3 = RPROF_T();
-            if (__builtin_expect(any, 0)) {
-                nf++;
-                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-                if (f0) {
-                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x0 = coarse_test(c0);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
-                }
-                if (f1) {
-                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
-                }
-            }
-            const unsigned long long t4 = RPROF_T();
-            pb += t1 - t0;
-            pm += t2 - t1;
-            pt += t3 - t2;
-            pfi += t4 - t3;
-            nr++;
-            tile += kTB;
-            ti++;
-        } while (tile != end);
+        for (int kc = 1; kc < D; kc++) {
+            c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
+            if (TWO) c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
+        }
+        const unsigned long long t2 = RPROF_T();
+#else
+        v16f c0, c1;
+        round_scores<D, NK, TWO>(tile, lane, pf, a0, a1, cb, sa, c0, c1);
+#endif
+        load_frag0(tile + kTB, lane, pf);
+        const uint32_t x0 = coarse_test(c0), x1 = TWO ? coarse_test(c1) : 0u;
+        const bool fired = __ballot((x0 | x1) != 0) != 0;
+#ifdef TFBS_ROUND_PROF
+        const unsigned long long t3 = RPROF_T();
+#endif
+        if (__builtin_expect(fired, 0)) {
+#ifdef TFBS_ROUND_PROF
+            nf++;
+#endif
+            // cold: queue the firing lanes' records (padding rows left out), or list
+            // a tile's candidates at once when the queue is full
+            const bool m0 = x0 != 0 && q0 < G.nw, m1 = TWO && x1 != 0 && q0 + kMWindows < G.nw;
+            const uint64_t f0 = __ballot(m0), f1 = __ballot(m1);
+            if (f0) queue_tile(A, G, c0, m0, f0, g0, 0, lane, wave, qn, cn);
+            if (TWO && f1) queue_tile(A, G, c1, m1, f1, g0, 1, lane, wave, qn, cn);
+        }
+#ifdef TFBS_ROUND_PROF
+        const unsigned long long t4 = RPROF_T();
+        pb += t1 - t0;
+        pm += t2 - t1;
+        pt += t3 - t2;
+        pfi += t4 - t3;
+        nr++;
+#endif
+        tile += kTB;
+        g0 += kMStrands;
+    } while (tile != end);
+#ifdef TFBS_ROUND_PROF
+    if (TWO) {
         RPROF_ADD(wave, 0, pb);
         RPROF_ADD(wave, 1, pm);
         RPROF_ADD(wave, 2, pt);
         RPROF_ADD(wave, 3, pfi);
         RPROF_ADD(wave, 4, nr);
         RPROF_ADD(wave, 5, nf);
-        return;
     }
 #endif
-#if TFBS_BPF2
-    if (two && D == 2) {
-        // depth 2: both chunks' B fragments of the next strand tile are read during the
-        // round before (two register sets, the loop unrolled by two), so no round waits
-        // for LDS between its MFMAs
-        const char *tile = img;
-        uint32_t ti = tb;
-        BFrag p[2], q[2];
-        load_frags<2>(img, lane, p);
-        auto one = [&](const BFrag (&f)[2], BFrag (&nx)[2]) {
-            if (ti + 1 < te) load_frags<2>(tile + kTB, lane, nx);
-            v16f c0 = mfma_chunk(a0[0], f[0], cb, sa);
-            v16f c1 = mfma_chunk(a1[0], f[0], cb, sa);
-            c0 = mfma_chunk(a0[1], f[1], c0, sa);
-            c1 = mfma_chunk(a1[1], f[1], c1, sa);
-            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
-            if (__builtin_expect(__ballot((x0 | x1) != 0) != 0, 0)) {
-                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-                if (f0) {
-                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x0 = coarse_test(c0);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
-                }
-                if (f1) {
-                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
-                }
-            }
-            tile += kTB;
-            ti++;
-        };
-        while (ti + 1 < te) {
-            one(p, q);
-            one(q, p);
-        }
-        if (ti < te) one(p, q);
-        return;
-    }
-#endif
-    if (two) {
-        // a pointer loop (3 scalar instructions per round) and one vector compare for
-        // both tests; the next round's chunk-0 B fragment is read unconditionally (past
-        // the last tile: the image area is padded by kMChunkBytes, the value unused)
-        const char *tile = img;
-        const char *const end = img + (te - tb) * kTB;
-        uint32_t ti = tb;
-        BFrag pf;
-        load_frag0(img, lane, pf);
-        do {
-            v16f c0, c1;
-            round_scores_pf<D, NK>(tile, lane, pf, a0, a1, cb, sa, c0, c1);
-            load_frag0(tile + kTB, lane, pf);
-            uint32_t x0 = coarse_test(c0), x1 = coarse_test(c1);
-            if (__builtin_expect(__ballot((x0 | x1) != 0) != 0, 0)) {
-                // cold: queue the firing tiles; a tile whose entries do not fit
-                // drains the queue first and its round is scored again (no
-                // accumulator is live across a drain)
-                const uint64_t f0 = __ballot(x0 != 0), f1 = __ballot(x1 != 0);
-                if (f0) {
-                    if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x0 = coarse_test(c0);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
-                }
-                if (f1) {
-                    if (qn + (uint32_t)__popcll(f1) > kMQueue) {
-                        drain_queue(A, G, qn, wave, lane, cn);
-                        qn = 0;
-                        round_scores<D, NK>(tile, lane, a0, a1, cb, sa, c0, c1);
-                        x1 = coarse_test(c1);
-                    }
-                    queue_tile(c1, x1, f1, ti, ta + 1, lane, wave, qn);
-                }
-            }
-            tile += kTB;
-            ti++;
-        } while (tile != end);
-    } else {
-        for (uint32_t ti = tb; ti < te; ti++) {
-            const char *tile = img + (ti - tb) * kTB;
-            v16f c0;
-            tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
-            uint32_t x0 = coarse_test(c0);
-            const uint64_t f0 = __ballot(x0 != 0);
-            if (__builtin_expect(f0 == 0, 1)) continue;
-            if (qn + (uint32_t)__popcll(f0) > kMQueue) {
-                drain_queue(A, G, qn, wave, lane, cn);
-                qn = 0;
-                tile_scores<D, NK>(tile, lane, a0, cb, sa, c0);
-                x0 = coarse_test(c0);
-            }
-            queue_tile(c0, x0, f0, ti, ta, lane, wave, qn);
-        }
-    }
 }
 
 // One step: every strand tile of the super tile (depth segments 1..NK, byte
-// d - 1 of seg = the end of depth d) x the window tiles ta and, if two, ta + 1.
-template <int NK>
+// d - 1 of seg = the end of depth d) x the window tiles ta and, if TWO, ta + 1.
+template <int NK, bool TWO>
 __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const GroupCtx &G,
                                           uint32_t lane, uint32_t wave, const v4i (&a0)[NK], const v4i (&a1)[NK],
-                                          bool two, uint32_t ta, const v16f &cb, int sa, uint32_t &qn, uint32_t &cn) {
+                                          uint32_t ta, const v16f &cb, int sa, uint32_t &qn, uint32_t &cn) {
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
-#if TFBS_PIPE
-    if (two) {
-        v16f X, Y;
-        bool pend = false;
-        uint32_t pend_ti = 0;
-#define TFBS_PSEGMENT(D)                                                                                         \
-        if (D <= NK && D + 1 >= NK) {                                                                            \
-            const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                 \
-            if (te > tb)                                                                                         \
-                scan_segment_pipe<(D <= NK ? D : 1), NK>(A, img, tb, te, G, lane, wave, a0, a1, ta, cb, sa, qn, cn, X, \
-                                                         Y, pend, pend_ti);                                        \
-            img += (te - tb) * mfma_tile_bytes(D);                                                               \
-            tb = te;                                                                                             \
-        }
-        TFBS_PSEGMENT(1)
-        TFBS_PSEGMENT(2)
-        TFBS_PSEGMENT(3)
-        TFBS_PSEGMENT(4)
-#undef TFBS_PSEGMENT
-        if (pend) test_tile(A, G, Y, pend_ti, ta + 1, lane, wave, qn, cn);
-        return;
-    }
-#endif
 #define TFBS_SEGMENT(D)                                                                                          \
     if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
         const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \
         if (te > tb)                                                                                             \
-            scan_segment<(D <= NK ? D : 1), NK>(A, img, tb, te, G, lane, wave, a0, a1, two, ta, cb, sa, qn, cn); \
+            scan_segment<(D <= NK ? D : 1), NK, TWO>(A, img, tb, te, G, lane, wave, a0, a1, ta, cb, sa, qn, cn); \
         img += (te - tb) * mfma_tile_bytes(D);                                                                   \
         tb = te;                                                                                                 \
     }
@@ -864,9 +688,9 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 // loaded while the current pair is scored.
 #ifdef TFBS_SCAN_PROF
 // per wave: [0] s_memtime at the kernel's start, [1] after the staging barrier, [2]
-// after the scan loops and their drains, [3] (the same), [4] after the rescoring, [5] / [6]
+// after the scan loops, [3] (the same), [4] after the rescoring, [5] / [6]
 // s_memrealtime (100 MHz, one clock for the chip) at the start and the end, [7] pairs
-// scored | candidates << 32
+// scored | candidates << 32; [8, 16) TFBS_ROUND_PROF's split
 #define SCAN_STAMP(k, v) \
     do { if (A.prof && lane == 0) A.prof[((size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave) * kScanProfWords + (k)] = (v); } while (0)
 #else
@@ -874,9 +698,8 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 #endif
 
 // One super tile's window pairs over the group's list of its depth class, then the
-// wave's last queue entries drained into its candidate list (qn, cn: the wave's
-// queued entries and listed candidates, carried over super tiles).  Returns the
-// pairs this wave scored.
+// wave's last queue records decoded (qn, cn: the wave's queued records and listed
+// candidates, carried over super tiles).  Returns the pairs this wave scored.
 template <int NK>
 __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper &S, const char *s_img,
                                               const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave,
@@ -894,7 +717,7 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
     const float a0f = __uint_as_float(S.acc0);
     v16f cb = {a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f};
     asm volatile("" : "+v"(cb));  // kept in VGPRs: every round's MFMAs read it (no per-round copies)
-    const int sa = lane < 32 ? kScaleA0 : kScaleA1;
+    const int sa = lane < 32 ? kScaleD0 : kScaleD1;
     const char *tab = s_img - kMOnehotBytes;
     auto next_pair = [&]() {
         uint32_t p = 0;
@@ -919,6 +742,7 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
         v4i a0[NK], a1[NK];
         entry_onehot<NK>(A, words, ea, tab, a0);
         entry_onehot<NK>(A, words, eb, tab, a1);  // (a copy of the last window when !two: unused)
+        s_went[wave][lane] = lane < 32 ? ea : eb;  // the firing path's windows (queue_tile)
         if (pn < npair) entries(pn, ea, eb);      // in flight while this pair is scored
 #ifdef TFBS_ROUND_PROF
         // the A fragments awaited here (their LDS reads), so that the pair's first
@@ -927,10 +751,11 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
         const unsigned long long tp1 = RPROF_T();
         RPROF_ADD(wave, 7, tp1 - tp0);
 #endif
-        scan_step<NK>(A, s_img, S.seg, G, lane, wave, a0, a1, two, 2 * p, cb, sa, qn, cn);
+        if (two) scan_step<NK, true>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, cb, sa, qn, cn);
+        else scan_step<NK, false>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, cb, sa, qn, cn);
         p = pn;
     }
-    drain_queue(A, G, qn, wave, lane, cn);  // the queue's entries refer to this super tile and list
+    drain_queue(A, G, qn, wave, lane, cn);  // (the records are self-contained: a drain per super tile)
     qn = 0;
     return n_pairs;
 }
@@ -1069,7 +894,7 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
 #endif
 }
 
-// Candidates past the waves' list regions (drain_queue), one per thread; their
+// Candidates past the waves' lists (drain_queue), one per thread; their
 // hits go to the spill list.
 __global__ __launch_bounds__(256) void cand_over_kernel(ScanArgs A) {
     const uint32_t n = min(A.over[1], A.cand_over_cap);
@@ -1430,7 +1255,7 @@ size_t mfma_lds_fixed() { return kMOnehotBytes; }
 
 void mfma_depth_budgets(uint32_t out[9]) {
     const uint32_t *waves = kMfmaRegWaves;
-    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hd) + sizeof(s_hd2) +
+    const uint32_t reserve = kMOnehotBytes + 4096 + sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_cand) + sizeof(s_went) + sizeof(s_hd) + sizeof(s_hd2) +
                              256;  // table, staged words, queues
     // workgroups per CU = 4 SIMDs x waves per SIMD / waves per workgroup
     for (int nk = 1; nk <= kMMaxChunks; nk++) out[nk] = (160 * 1024) / (4 * waves[nk] / (kMBlock / 64)) - reserve;
@@ -1445,7 +1270,7 @@ int launch_mfma_all(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supe
     if ((uint64_t)(last.tile0 + last.tile_count) * kMStrands > (1u << 24) || hpb > kMMaxHapsPerBlock)
         return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 64 haplotypes per workgroup");
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
-    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);
+    const size_t static_lds = sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_cand) + sizeof(s_went) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);
     size_t img_bytes = 0;
     for (uint32_t k = 0; k < n_supers; k++) img_bytes = std::max<size_t>(img_bytes, supers[k].img_bytes);
     const size_t base = kMOnehotBytes + img_bytes + kMChunkBytes;  // (the padding: scan_segment's B prefetch)
@@ -1496,7 +1321,7 @@ int launch_mfma(const ScanArgs &a0, const DevMSuper *supers, uint32_t n_supers, 
         return fail(TFBS_E_ARG, "matrix-core scan: more than 2^24 strands or 64 haplotypes per workgroup");
     const uint32_t n_hg = (n_haps + hpb - 1) / hpb;
     const size_t static_lds =
-        sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);  // queues, descriptors
+        sizeof(s_qdata) + sizeof(s_qmeta) + sizeof(s_cand) + sizeof(s_went) + sizeof(s_hnext) + sizeof(s_hd) + sizeof(s_hd2);  // queues, descriptors
     uint32_t region = 0;
     int launches = 0;
     // one launch per K depth (super tiles come sorted by depth): each kernel is

@@ -107,6 +107,9 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
         python3 -c "import json;q=json.load(open('$d/pmc_summary.json'));print('$w $v $name', {k: '%.4g' % v for k, v in q.items() if not k.startswith('_')})"
       done
       unset TFBS_LIB ;;
+    probe_scale)
+      /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/probe/f4f6_scale.hip -o /tmp/f4f6_scale 2>/dev/null || exit 1
+      timeout -k 10 60 /tmp/f4f6_scale > $O/probe_scale.txt 2>&1; rc=$?; cat $O/probe_scale.txt; [ $rc -eq 0 ] || exit $rc ;;
     probe_chain)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-mfma-vgpr-form tools/probe/f4f6_chain.hip -o /tmp/f4f6_chain || exit 1
       timeout -k 10 120 /tmp/f4f6_chain > $O/probe_chain.txt 2>&1 || exit 1

@@ -29,6 +29,19 @@ __global__ void k(const uint32_t *a, const uint32_t *b, const int *sa, const int
     for (int r = 0; r < 16; r++) out[l * 16 + r] = d[r];
 }
 
+// The scan's operand order since round 6: A = FP6 digits (rows), B = FP4 one-hot (columns).
+__global__ void k_swapped(const uint32_t *a, const uint32_t *b, const int *sa, const int *sb, const float *cin,
+                          float *out) {
+    const int l = threadIdx.x;
+    v8i va = {0, 0, 0, 0, 0, 0, 0, 0}, vb = va;
+    for (int i = 0; i < 4; i++) va[i] = a[l * 4 + i];
+    for (int i = 0; i < 6; i++) vb[i] = b[l * 6 + i];
+    v16f c;
+    for (int r = 0; r < 16; r++) c[r] = cin[l * 16 + r];
+    const v16f d = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vb, va, c, 2, 4, 0, sb[l], 0, sa[l]);
+    for (int r = 0; r < 16; r++) out[l * 16 + r] = d[r];
+}
+
 static double fp4(uint32_t x) {
     const double mag[8] = {0, 0.5, 1, 1.5, 2, 3, 4, 6};
     return (x & 8 ? -1.0 : 1.0) * mag[x & 7];
@@ -55,7 +68,8 @@ int main() {
     hipMalloc(&dc, 64 * 16 * 4);
     hipMalloc(&dout, 64 * 16 * 4);
     int fails = 0;
-    for (int trial = 0; trial < 4; trial++) {
+    for (int trial = 0; trial < 8; trial++) {
+        const bool swapped = trial >= 4;  // trials 4-7: digits as A (rows), one-hot as B (columns)
         std::vector<uint32_t> a(64 * 4 + 1, 0), b(64 * 6 + 1, 0);
         std::vector<int> sa(64), sb(64);
         std::vector<float> cin(64 * 16);
@@ -69,7 +83,7 @@ int main() {
                     if ((code >> q) & 1) b[l * 6 + (pos + q) / 32] |= 1u << ((pos + q) % 32);
             }
         for (int l = 0; l < 64; l++) {
-            if (trial == 0) {
+            if (trial % 4 == 0) {
                 sa[l] = l < 32 ? 127 : 138;  // the packed layout: block 1 scaled by 2^11
                 sb[l] = 130;                 // digits x 8: integer units
             } else {
@@ -79,32 +93,37 @@ int main() {
         }
         for (int l = 0; l < 64; l++)
             for (int r = 0; r < 16; r++)
-                cin[l * 16 + r] = trial == 0 ? (float)(8388608 + (rng() % 2000) + 2048 * (rng() % 2000)) : 0.0f;
+                cin[l * 16 + r] = trial % 4 == 0 ? (float)(8388608 + (rng() % 2000) + 2048 * (rng() % 2000)) : 0.0f;
         hipMemcpy(da, a.data(), a.size() * 4, hipMemcpyHostToDevice);
         hipMemcpy(db, b.data(), b.size() * 4, hipMemcpyHostToDevice);
         hipMemcpy(dsa, sa.data(), 64 * 4, hipMemcpyHostToDevice);
         hipMemcpy(dsb, sb.data(), 64 * 4, hipMemcpyHostToDevice);
         hipMemcpy(dc, cin.data(), cin.size() * 4, hipMemcpyHostToDevice);
-        hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, da, db, dsa, dsb, dc, dout);
+        if (swapped)
+            hipLaunchKernelGGL(k_swapped, dim3(1), dim3(64), 0, 0, da, db, dsa, dsb, dc, dout);
+        else
+            hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, da, db, dsa, dsb, dc, dout);
         std::vector<float> out(64 * 16);
         hipMemcpy(out.data(), dout, out.size() * 4, hipMemcpyDeviceToHost);
         int ok = 0;
         for (int l = 0; l < 64; l++)
             for (int r = 0; r < 16; r++) {
+                // swapped: row i = the digits' lane (strand pair), column j = the one-hot's (window)
                 const int i = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), j = l & 31;
                 double c = cin[l * 16 + r];
                 for (int kk = 0; kk < 64; kk++) {
-                    const int la = i + 32 * (kk >> 5), lb = j + 32 * (kk >> 5);  // hypothesis (1)
+                    const int la = (swapped ? j : i) + 32 * (kk >> 5), lb = (swapped ? i : j) + 32 * (kk >> 5);  // hypothesis (1)
                     const double av = fp4(bits(&a[la * 4], 4 * (kk & 31), 4)) * std::ldexp(1.0, sa[la] - 127);
                     const double bv = fp6(bits(&b[lb * 6], 6 * (kk & 31), 6)) * std::ldexp(1.0, sb[lb] - 127);
                     c += av * bv;
                 }
-                const double tol = trial == 0 ? 0.0 : 1e-5 * std::max(1.0, std::fabs(c));  // trial 0 must be exact
+                const double tol = trial % 4 == 0 ? 0.0 : 1e-5 * std::max(1.0, std::fabs(c));  // trial 0 must be exact
                 if (std::fabs((double)out[l * 16 + r] - c) <= tol) ok++;
                 else if (fails++ < 8)
                     printf("trial %d lane %d r %d: got %.3f want %.3f\n", trial, l, r, out[l * 16 + r], c);
             }
-        printf("trial %d (%s): %d/1024 outputs exact\n", trial, trial == 0 ? "packed scales" : "random scales", ok);
+        printf("trial %d (%s%s): %d/1024 outputs exact\n", trial, trial % 4 == 0 ? "packed scales" : "random scales",
+               swapped ? ", FP6 A x FP4 B" : "", ok);
     }
     printf(fails ? "FAIL\n" : "PASS\n");
     return fails ? 1 : 0;
