@@ -5,7 +5,7 @@ generator, seeds, PWM sets and thresholds), and checked three ways:
 
 * against the oracle (oracle/tfbs_oracle.c, the C restatement of main.rs:94-154,
   500-534 and 439-498): every region of C3 and C5 (10 000 each) and a spread of
-  1 000+ C4 regions through the oracle's committed per-region digests
+  10 000+ C4 regions (1 250+ per shard) through the oracle's committed per-region digests
   (tests/golden/fullsize_<W>.npz, tests/golden/make_fullsize_digests.py: a linear
   sketch of count_matches_by_sample's per-sample L/R vectors and XXH64 of the row
   text without POS); every region of C2, and ~125 C3/C5 regions (a spread, the
