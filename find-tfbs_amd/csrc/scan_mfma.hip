@@ -603,6 +603,9 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
         v16f c0, c1;
         round_scores<D, NK, TWO>(tile, lane, pf, a0, a1, cb, sa, c0, c1);
 #endif
+#ifdef TFBS_NO_READ2
+        asm volatile("" ::: "memory");  // (A/B) no ds_read2 merged with the round's reads: no v_mov copies
+#endif
         load_frag0(tile + kTB, lane, pf);
         const uint32_t x0 = coarse_test(c0), x1 = TWO ? coarse_test(c1) : 0u;
         const bool fired = __ballot((x0 | x1) != 0) != 0;
@@ -847,6 +850,9 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
     const uint32_t *words = stage_group<STAGED>(A, smem, h0, hn);
     const char *s_img = reinterpret_cast<const char *>(smem) + kMOnehotBytes;
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#ifdef TFBS_SETPRIO
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);  // (A/B) the workgroup's second half wins issue ties
+#endif
     uint32_t qn = 0, cn = 0, n_pairs = 0;
 #ifdef TFBS_SCAN_PROF
     bool first = true;

@@ -659,3 +659,39 @@ def test_reduce_zero_samples_after_keys(tmp_path):
             assert empty.region_rows(r, "chr1")[0] == ""
     finally:
         sc.close()
+
+
+@pytest.mark.parametrize("mfma", ["0", "1"])
+def test_ds_ties_at_the_fifth_decimal_vs_oracle(monkeypatch, mfma):
+    """counts_as_genotypes' DS = {:.4} of the f32 2 (x - lo) / (hi - lo) (main.rs:439-498):
+    with hi - lo = 64 (a multiple of 32) a sample at x - lo odd lands exactly on a 5th
+    decimal 5 (1/32 = 0.03125 -> '0.0312', 63/32 = 1.96875 -> '1.9688': ties to even, as
+    Rust >= 1.67 and printf('%.4f') print them).  A one-column 'A' PWM hits
+    every A of the inner range; per-sample counts are set by A->C SNVs on either
+    haplotype: 2 a0 (both reference), 2 (a0 - 32) (32 SNVs on both), 2 a0 - 1 and
+    2 (a0 - 32) + 1 (one SNV / 31 SNVs on one side) and a spread of others.  Device keys,
+    rows (dense, device reduction, device encoding) == the oracle's, and the tie texts
+    are in the rows."""
+    monkeypatch.setenv("TFBS_MFMA", mfma)
+    ps = T.PatternSet.from_patterns([T.Pattern.PWM([T.Weight(1000, 0, 0, 0)], "A1", 0, 999, 0)])
+    n = 12
+    s0, e0 = 2000, 2199  # inner = merged: 200 bases, ext = the same (L_max 1)
+    rnd = random.Random(5)
+    ref = "".join(rnd.choice("AACGT") for _ in range(e0 - s0 + 1))
+    a_pos = [s0 + i for i, c in enumerate(ref) if c == "A"]
+    assert len(a_pos) > 64
+    # haplotype h carries the SNVs at a_pos[:k_h]
+    k = {0: 0, 1: 0, 2: 32, 3: 32, 4: 1, 5: 0, 6: 31, 7: 32}
+    for s in range(4, n):
+        k[2 * s], k[2 * s + 1] = rnd.randint(0, 32), rnd.randint(0, 32)
+    recs = []
+    for j, p in enumerate(a_pos[:32]):
+        car = sorted(h for h in range(2 * n) if k.get(h, 0) > j)
+        if car:
+            recs.append(("car", p, "A", "C", car))
+    regions = [{"merged": (s0, e0), "ref": ref, "records": recs}]
+    beds = [("ties.bed", [(s0, e0)])]
+    _compare(ps, n, beds, regions)
+    okeys, orows, _ = run_oracle(ps, n, beds, regions)
+    row = [r for r in orows.split("\n") if r][0].split("\t")
+    assert "1|1:1.9688" in row and "0|0:0.0312" in row, row[9:]

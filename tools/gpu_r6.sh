@@ -14,6 +14,9 @@ for st in "$@"; do
     tests)
       timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread --durations=20 > $O/gpu_tests.log 2>&1
       rc=$?; tail -25 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
+    k_*)  # k_<expr>: the GPU tests selected by pytest -k <expr>
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "${st#k_}" > $O/gpu_tests_k.log 2>&1
+      rc=$?; tail -15 $O/gpu_tests_k.log; [ $rc -eq 0 ] || exit $rc ;;
     tests_nofull)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread --durations=15 -k "not (c3_full or c5_full or c4_shards)" > $O/gpu_tests.log 2>&1
       rc=$?; tail -20 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc ;;
