@@ -139,6 +139,8 @@ struct tfbs_ctx {
     DevBuf<uint32_t> wl[2];
     DevBuf<uint16_t> wl16[2];  // the narrow groups' window lists
     DevBuf<uint8_t> gnarrow;   // per haplotype group of mfma_hpb: every haplotype <= kWlNarrowLen bases
+    DevBuf<uint32_t> gorder;   // the merged scan's group order (most work first; TFBS_SCAN_LPT=0: none)
+    DevBuf<uint32_t> gcost;    // (its per-group work estimates)
     bool wl_any_narrow = false, wl_any_wide = false;  // the resident batch has narrow / other groups
     DevBuf<uint4> hd, hd2;     // the matrix-core scan's compact haplotype descriptors
     uint64_t wl_entries[2] = {0, 0};
@@ -318,6 +320,33 @@ static int build_lists(tfbs_ctx *ctx, uint32_t n_haps, const std::vector<uint8_t
         return rc;
     for (int c = 0; c < 2; c++)
         if (!lmin[c]) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
+    // The merged scan's workgroup order: groups by descending work (window pairs x the
+    // per-pair MFMAs + rounds of each depth class's super tiles), so that the launch
+    // ends on its smallest groups instead of a late large one (LPT).
+    ctx->gorder.release();
+    if (env_int("TFBS_SCAN_LPT", 1) && n_haps) {
+        uint32_t w[2] = {0, 0};
+        for (const DevMSuper &S : P.m_supers) {
+            uint32_t prev = 0;
+            for (uint32_t d = 1; d <= 4; d++) {
+                const uint32_t e = (S.seg >> (8 * (d - 1))) & 255u;
+                if (e > prev) w[S.nk > 2 ? 1 : 0] += (e - prev) * (2 * d + 1);
+                prev = std::max(prev, e);
+            }
+        }
+        const uint32_t hpb = ctx->mfma_hpb, ng = (n_haps + hpb - 1) / hpb;
+        if ((rc = ctx->gcost.ensure(ng)) ||
+            (rc = group_costs(lmin[0] ? ctx->wl_off[0].p : nullptr, lmin[1] ? ctx->wl_off[1].p : nullptr, n_haps, hpb,
+                              w[0], w[1], ctx->gcost.p, ctx->stream)))
+            return rc;
+        std::vector<uint32_t> cost(ng), order(ng);
+        HIP_TRY(hipMemcpyAsync(cost.data(), ctx->gcost.p, (size_t)ng * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        for (uint32_t g = 0; g < ng; g++) order[g] = g;
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        if ((rc = ctx->gorder.put(order, ctx->stream))) return rc;
+        HIP_TRY(hipStreamSynchronize(ctx->stream));  // (order is copied from the host's stack)
+    }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     ctx->wl_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return TFBS_OK;
@@ -392,6 +421,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             return rc;
         m.dedup = 1;
         m.gnarrow = ctx->gnarrow.n ? ctx->gnarrow.p : nullptr;
+        m.gorder = ctx->mfma_merged && ctx->gorder.n ? ctx->gorder.p : nullptr;
         m.hd = ctx->hd.p;
         m.hd2 = ctx->hd2.p;
         m.druns = ctx->druns.p;
@@ -635,6 +665,8 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->druns.release(); ctx->wl_tmp.release();
     for (int c = 0; c < 2; c++) ctx->wl_off[c].release(), ctx->wl[c].release(), ctx->wl16[c].release();
     ctx->gnarrow.release();
+    ctx->gorder.release();
+    ctx->gcost.release();
     ctx->hd.release();
     ctx->hd2.release();
     ctx->inner.release(); ctx->haps.release(); ctx->regions.release(); ctx->hits.release(); ctx->asm_scratch.release();
@@ -1231,7 +1263,7 @@ static uint64_t step_signature(const tfbs_ctx *ctx, const tfbs_batch *b) {
     buf(ctx->cands); buf(ctx->hitl); buf(ctx->hitn); buf(ctx->ref_hits); buf(ctx->ref_count); buf(ctx->spill);
     buf(ctx->over); buf(ctx->spill_sorted); buf(ctx->spill_bcnt); buf(ctx->spill_boff); buf(ctx->cand_over);
     buf(ctx->srcs); buf(ctx->words); buf(ctx->nmask); buf(ctx->counts); buf(ctx->posrel); buf(ctx->inner);
-    buf(ctx->haps); buf(ctx->druns); buf(ctx->gnarrow); buf(ctx->hd); buf(ctx->hd2); buf(ctx->regions);
+    buf(ctx->haps); buf(ctx->druns); buf(ctx->gnarrow); buf(ctx->gorder); buf(ctx->hd); buf(ctx->hd2); buf(ctx->regions);
     buf(ctx->hits); buf(ctx->asm_scratch); buf(ctx->key_first); buf(ctx->var_counts); buf(ctx->asm_redo);
     buf(ctx->asm_ctr); buf(ctx->cor_arena); buf(ctx->key_flags); buf(ctx->var_keys); buf(ctx->asm_order);
     for (int c = 0; c < 2; c++) {

@@ -66,6 +66,9 @@ struct ScanArgs {
     const uint4 *hd;   // matrix-core scan: per haplotype (word_off, len, flags, nmask_off) of haps (build_window_lists)
     const uint4 *hd2;  // and (region, pos_off, drun_off, n_druns): the rescoring's
     const uint8_t *gnarrow;
+    // scan_mfma_all_kernel: workgroup b scans haplotype group gorder[b] (the groups in
+    // descending order of work, so the launch ends on the small ones); null: group b
+    const uint32_t *gorder;
     const uint64_t *wlist_off[2];
     // reference-window reuse (HAP_DEDUP haplotypes, tfbs_internal.hpp): dedup
     // != 0 scans only their dirty windows (the lists); the HAP_REF haplotypes' hits
@@ -160,6 +163,11 @@ struct WindowListBufs {
     uint64_t list_cap[2];  // entries
 };
 size_t scan_tmp_words(size_t n);
+// Per haplotype group of hpb (n_groups): the window tiles of its lists, cost[g] =
+// pairs of class 2 x w[0] + pairs of class 4 x w[1] (w: the per-pair work of each
+// depth class's super tiles), for the scan's workgroup order.
+int group_costs(const uint64_t *off0, const uint64_t *off1, uint32_t n_haps, uint32_t hpb, uint32_t w0, uint32_t w1,
+                uint32_t *cost, hipStream_t stream);
 int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *druns, const uint32_t lmin[2],
                        const uint32_t span[2], uint32_t hpb, uint32_t dedup, WindowListBufs &bufs, uint64_t total[2], hipStream_t stream,
                        int (*ensure_list)(void *ctx, int c, uint64_t n, uint32_t **p, uint16_t **p16),

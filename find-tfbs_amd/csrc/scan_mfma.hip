@@ -191,7 +191,7 @@ extern __shared__ __attribute__((aligned(16))) int32_t s_mdyn[];  // one-hot tab
 struct GroupCtx {
     const uint32_t *wl;
     const uint16_t *wl16;  // a narrow group's list (16-bit entries), else null
-    uint32_t nw, tile0, h0;
+    uint32_t nw, tile0, h0, slot;
     __device__ __forceinline__ uint32_t at(uint32_t q) const { return wl16 ? (uint32_t)wl16[q] : wl[q]; }
 };
 
@@ -318,8 +318,11 @@ __device__ __forceinline__ uint32_t score_candidate(const ScanArgs &A, const uin
 // (TFBS_CAND_CAP makes all of them small in the spill tests).
 __device__ __forceinline__ uint32_t wave_cand_cap(const ScanArgs &A) { return A.cand_cap / (kMBlock / 64); }
 __device__ __forceinline__ uint32_t wave_lds_cap(const ScanArgs &A) { return min(wave_cand_cap(A), kWaveCands); }
-__device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
-    return reinterpret_cast<uint2 *>(A.cands) + (size_t)(A.region_base + blockIdx.x) * A.cand_cap +
+// slot: the workgroup's place in the per-workgroup lists (region_base + its
+// haplotype group in the merged kernel's ordered launch, ScanArgs::gorder; else +
+// its index).
+__device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t slot, uint32_t wave) {
+    return reinterpret_cast<uint2 *>(A.cands) + (size_t)slot * A.cand_cap +
            (size_t)wave * wave_cand_cap(A);
 }
 
@@ -327,14 +330,14 @@ __device__ __forceinline__ uint2 *cand_list(const ScanArgs &A, uint32_t wave) {
 // is live, and the other waves keep the matrix cores busy); each hit's
 // (haplotype, key) pairs are appended to the wave's part of the workgroup's hit
 // list in lane order (ballot prefix: no atomics), the excess spilled.
-__device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *words, uint32_t h0, uint32_t wave,
+__device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *words, uint32_t h0, uint32_t slot, uint32_t wave,
                                              uint32_t lane, uint32_t cn) {
     const uint32_t cap = wave_cand_cap(A);
-    const size_t part = (size_t)(A.region_base + blockIdx.x) * A.cand_cap + (size_t)wave * cap;
+    const size_t part = (size_t)slot * A.cand_cap + (size_t)wave * cap;
     uint2 *out = reinterpret_cast<uint2 *>(A.hitl) + part;
     uint32_t hn = 0;  // wave-uniform
     const uint32_t lcap = wave_lds_cap(A), n = min(cn, lcap + cap);
-    const uint2 *glist = cand_list(A, wave);
+    const uint2 *glist = cand_list(A, slot, wave);
     for (uint32_t k0 = 0; k0 < n; k0 += 64) {
         const uint32_t k = k0 + lane;
         uint32_t mask = 0, key0 = 0, hap = 0;
@@ -357,7 +360,7 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
             hn += (uint32_t)__popcll(act);
         }
     }
-    if (lane == 0) A.hitn[(size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave] = min(hn, cap);
+    if (lane == 0) A.hitn[(size_t)slot * kMBlockWaves + wave] = min(hn, cap);
 }
 
 // Coarse test of one tile: OR of the lane's 16 outputs, the fields' top bits
@@ -423,7 +426,7 @@ __device__ __forceinline__ void record_bits(const v16f &acc, uint32_t (&x)[4]) {
 __device__ __forceinline__ void list_mask(const ScanArgs &A, const GroupCtx &G, uint32_t wave, uint32_t m, uint32_t gl,
                                           uint32_t ent, uint32_t &cn) {
     const uint32_t lcap = wave_lds_cap(A), cap = lcap + wave_cand_cap(A);
-    uint2 *glist = cand_list(A, wave);
+    uint2 *glist = cand_list(A, G.slot, wave);
     const uint32_t hl = ent & (kMMaxHapsPerBlock - 1), i = ent >> 6;
     const uint32_t gbase = (gl & ~63u) + 8 * ((gl >> 5) & 1u);  // the tile's first strand; lanes 32-63: pairs + 4
     uint64_t act;
@@ -695,7 +698,7 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 // s_memrealtime (100 MHz, one clock for the chip) at the start and the end, [7] pairs
 // scored | candidates << 32; [8, 16) TFBS_ROUND_PROF's split
 #define SCAN_STAMP(k, v) \
-    do { if (A.prof && lane == 0) A.prof[((size_t)(A.region_base + blockIdx.x) * kMBlockWaves + wave) * kScanProfWords + (k)] = (v); } while (0)
+    do { if (A.prof && lane == 0) A.prof[((size_t)slot * kMBlockWaves + wave) * kScanProfWords + (k)] = (v); } while (0)
 #else
 #define SCAN_STAMP(k, v) do { } while (0)
 #endif
@@ -705,8 +708,8 @@ __device__ __forceinline__ void entry_onehot(const ScanArgs &A, const uint32_t *
 // candidates, carried over super tiles).  Returns the pairs this wave scored.
 template <int NK>
 __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper &S, const char *s_img,
-                                              const uint32_t *words, uint32_t hg, uint32_t lane, uint32_t wave,
-                                              uint32_t &qn, uint32_t &cn) {
+                                              const uint32_t *words, uint32_t hg, uint32_t slot, uint32_t lane,
+                                              uint32_t wave, uint32_t &qn, uint32_t &cn) {
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t h1 = min(h0 + A.haps_per_block, A.n_haps);
     const uint64_t e0 = A.wlist_off[NK > 2][h0];
@@ -716,6 +719,7 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
     G.nw = (uint32_t)(A.wlist_off[NK > 2][h1] - e0);
     G.tile0 = S.tile0;
     G.h0 = h0;
+    G.slot = slot;
     const uint32_t ntile = (G.nw + kMWindows - 1) / kMWindows, npair = (ntile + 1) / 2;
     const float a0f = __uint_as_float(S.acc0);
     v16f cb = {a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f, a0f};
@@ -806,6 +810,7 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     int32_t *smem = s_mdyn;
     const uint32_t sidx = blockIdx.x % A.n_msupers;
     const uint32_t hg = blockIdx.x / A.n_msupers;
+    const uint32_t slot = A.region_base + blockIdx.x;
     const DevMSuper S = A.msupers[sidx];
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hn = min(h0 + A.haps_per_block, A.n_haps) - h0;
@@ -822,11 +827,11 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
     SCAN_STAMP(1, __builtin_amdgcn_s_memtime());
 #endif
     uint32_t qn = 0, cn = 0;
-    const uint32_t n_pairs = scan_loop<NK>(A, S, s_img, words, hg, lane, wave, qn, cn);
+    const uint32_t n_pairs = scan_loop<NK>(A, S, s_img, words, hg, slot, lane, wave, qn, cn);
     (void)n_pairs;
     SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
-    rescore_list(A, words, h0, wave, lane, cn);
+    rescore_list(A, words, h0, slot, wave, lane, cn);
     SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
     SCAN_STAMP(7, (unsigned long long)n_pairs | ((unsigned long long)cn << 32));
@@ -844,7 +849,8 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
     const unsigned long long t_start = __builtin_amdgcn_s_memtime(), r_start = __builtin_amdgcn_s_memrealtime();
 #endif
     int32_t *smem = s_mdyn;
-    const uint32_t hg = blockIdx.x;
+    const uint32_t hg = A.gorder ? A.gorder[blockIdx.x] : blockIdx.x;  // (its lists and stamps at slot hg)
+    const uint32_t slot = A.region_base + hg;
     const uint32_t h0 = hg * A.haps_per_block;
     const uint32_t hn = min(h0 + A.haps_per_block, A.n_haps) - h0;
     const uint32_t *words = stage_group<STAGED>(A, smem, h0, hn);
@@ -883,14 +889,14 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
             first = false;
         }
 #endif
-        n_pairs += S.nk > 2 ? scan_loop<4>(A, S, s_img, words, hg, lane, wave, qn, cn)
-                            : scan_loop<2>(A, S, s_img, words, hg, lane, wave, qn, cn);
+        n_pairs += S.nk > 2 ? scan_loop<4>(A, S, s_img, words, hg, slot, lane, wave, qn, cn)
+                            : scan_loop<2>(A, S, s_img, words, hg, slot, lane, wave, qn, cn);
     }
     (void)n_pairs;
     SCAN_STAMP(2, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(3, __builtin_amdgcn_s_memtime());
 #ifndef TFBS_AB_NORESCORE  // timing ablation (wrong results): no rescoring
-    rescore_list(A, words, h0, wave, lane, cn);
+    rescore_list(A, words, h0, slot, wave, lane, cn);
 #endif
     SCAN_STAMP(4, __builtin_amdgcn_s_memtime());
     SCAN_STAMP(6, __builtin_amdgcn_s_memrealtime());
@@ -966,6 +972,19 @@ __global__ __launch_bounds__(256) void wl_fill_kernel(const DevHap *__restrict__
         }
         at += hi - lo;
     });
+}
+
+__global__ __launch_bounds__(256) void group_cost_kernel(const uint64_t *__restrict__ off0,
+                                                         const uint64_t *__restrict__ off1, uint32_t n_haps, uint32_t hpb,
+                                                         uint32_t n_groups, uint32_t w0, uint32_t w1,
+                                                         uint32_t *__restrict__ cost) {
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= n_groups) return;
+    const uint32_t h0 = g * hpb, h1 = min(h0 + hpb, n_haps);
+    uint64_t c = 0;
+    if (off0) c += (off0[h1] - off0[h0] + 2 * kMWindows - 1) / (2 * kMWindows) * w0;
+    if (off1) c += (off1[h1] - off1[h0] + 2 * kMWindows - 1) / (2 * kMWindows) * w1;
+    cost[g] = (uint32_t)min<uint64_t>(c, 0xFFFFFFFFu);
 }
 
 // The scan's compact haplotype descriptors (ScanArgs::hd): word offset, length,
@@ -1254,6 +1273,17 @@ int build_window_lists(const DevHap *haps, uint32_t n_haps, const uint32_t *drun
         e = hipGetLastError();
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("wl_fill_kernel: ") + hipGetErrorString(e));
     }
+    return TFBS_OK;
+}
+
+int group_costs(const uint64_t *off0, const uint64_t *off1, uint32_t n_haps, uint32_t hpb, uint32_t w0, uint32_t w1,
+                uint32_t *cost, hipStream_t stream) {
+    const uint32_t ng = (n_haps + hpb - 1) / hpb;
+    if (ng == 0) return TFBS_OK;
+    hipLaunchKernelGGL(group_cost_kernel, dim3((ng + 255) / 256), dim3(256), 0, stream, off0, off1, n_haps, hpb, ng, w0,
+                       w1, cost);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("group_cost_kernel: ") + hipGetErrorString(e));
     return TFBS_OK;
 }
 
