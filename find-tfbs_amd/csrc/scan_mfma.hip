@@ -509,7 +509,30 @@ __device__ __forceinline__ void queue_tile(const ScanArgs &A, const GroupCtx &G,
 template <int D, int NK, bool TWO>
 __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, const BFrag &f0, const v4i (&a0)[NK],
                                              const v4i (&a1)[NK], const v16f &cb, int sa, v16f &c0, v16f &c1) {
-#ifndef TFBS_B_JIT
+#ifndef TFBS_B_ALL
+    if (D >= 3) {
+        // depth 3-4 (the class whose A fragments take 32 VGPRs): chunk kc + 1's
+        // fragment read as chunk kc's MFMAs issue, a scheduling barrier between the
+        // chunks -- two fragments live instead of D (no scratch spill in the merged
+        // kernel)
+        BFrag cur = f0;
+        c0 = cb;
+        if (TWO) c1 = cb;
+#pragma unroll
+        for (int kc = 0; kc < D; kc++) {
+            BFrag nx;
+            if (kc + 1 < D) {
+                nx.b = *reinterpret_cast<const v4i *>(tile + (kc + 1) * 1536 + lane * 16);
+                nx.c = *reinterpret_cast<const int2 *>(tile + (kc + 1) * 1536 + 1024 + lane * 8);
+            }
+            c0 = mfma_chunk(a0[kc], cur, c0, sa);
+            if (TWO) c1 = mfma_chunk(a1[kc], cur, c1, sa);
+            __builtin_amdgcn_sched_barrier(0);
+            if (kc + 1 < D) cur = nx;
+        }
+        return;
+    }
+#endif
     BFrag f[D];
     f[0] = f0;
 #pragma unroll
@@ -524,24 +547,6 @@ __device__ __forceinline__ void round_scores(const char *tile, uint32_t lane, co
         c0 = mfma_chunk(a0[kc], f[kc], c0, sa);
         if (TWO) c1 = mfma_chunk(a1[kc], f[kc], c1, sa);
     }
-#else
-    // chunk kc + 1's fragment read while chunk kc's MFMAs issue: two fragments live
-    // instead of D (depth 3-4 rounds hold 12-24 fewer VGPRs)
-    BFrag cur = f0;
-    c0 = cb;
-    if (TWO) c1 = cb;
-#pragma unroll
-    for (int kc = 0; kc < D; kc++) {
-        BFrag nx;
-        if (kc + 1 < D) {
-            nx.b = *reinterpret_cast<const v4i *>(tile + (kc + 1) * 1536 + lane * 16);
-            nx.c = *reinterpret_cast<const int2 *>(tile + (kc + 1) * 1536 + 1024 + lane * 8);
-        }
-        c0 = mfma_chunk(a0[kc], cur, c0, sa);
-        if (TWO) c1 = mfma_chunk(a1[kc], cur, c1, sa);
-        if (kc + 1 < D) cur = nx;
-    }
-#endif
 }
 __device__ __forceinline__ void load_frag0(const char *tile, uint32_t lane, BFrag &f) {
     f.b = *reinterpret_cast<const v4i *>(tile + lane * 16);
