@@ -1156,12 +1156,11 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
     const tfbs::Patterns &P = tfbs::patterns_of(p);
     if (P.pats.empty()) return tfbs::fail(TFBS_E_NOPATTERN, "no pattern");  // main.rs:238
     if ((uint64_t)n_samples * 2 > 0xFFFFFFF0ull) return tfbs::fail(TFBS_E_ARG, "too many samples");
-    tfbs::Plan plan;  // only its slot order is used (independent of the tile options)
-    tfbs::PlanOptions opt;
-    opt.tile_blocks = 1u << 30;
-    int rc = P.build_plan(opt, &plan);
+    std::vector<uint16_t> slot_pid;
+    bool zero_len_panics = false;
+    int rc = P.slot_order(slot_pid, zero_len_panics);
     if (rc) return rc;
-    if (plan.zero_len_panics)
+    if (zero_len_panics)
         return tfbs::fail(TFBS_E_ZEROLEN, "length-0 PWM with negative min_score (pattern.rs:150-156)");
     auto *b = new tfbs_batch();
     Batch &B = b->b;
@@ -1174,12 +1173,12 @@ int tfbs_batch_create(const tfbs_patterns *p, uint32_t n_samples, int keep_membe
         const char *w = getenv("TFBS_DEV_PATCH");  // 0: only SNV-only regions are grouped on the device
         B.dev_patch = !(w && *w && atoi(w) == 0);
     }
-    B.slot_pid = plan.slot_pid;
+    B.slot_pid = std::move(slot_pid);
     B.slots_by_pid.resize(B.slot_pid.size());
     std::iota(B.slots_by_pid.begin(), B.slots_by_pid.end(), 0u);
     std::sort(B.slots_by_pid.begin(), B.slots_by_pid.end(),
               [&](uint32_t a, uint32_t b) { return B.slot_pid[a] < B.slot_pid[b]; });
-    B.n_slots = (uint32_t)plan.slot_pid.size();
+    B.n_slots = (uint32_t)B.slot_pid.size();
     std::map<uint32_t, uint32_t> lens;
     for (auto &q : P.pats)
         if (q.kind == TFBS_KIND_PWM && q.len > 0) lens[q.len]++;

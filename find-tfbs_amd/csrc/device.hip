@@ -211,6 +211,7 @@ struct tfbs_ctx {
     hipEvent_t bg_done[kBgSlots] = {}, bg_copied[kBgSlots] = {};
     hipStream_t copy_stream = nullptr;
     double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
+    double drain_s[3] = {0, 0, 0};        // of rows_s[1]: bgzf_drain's waits for the blocks, the copy back, the write
     uint64_t rows_text_last = 0;          // the last call's uncompressed row bytes
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
@@ -1638,9 +1639,48 @@ struct BgPipe {
     }
 };
 
+// n bytes to fd at its offset, which moves past them.  A large write goes out as
+// positioned pieces on a few threads (a page-cache copy runs ~2-3 GB/s per thread:
+// one thread made the rows' write the run flow's longest host step); a descriptor
+// without an offset (a pipe) takes plain writes.
+static int write_out(int fd, const char *p, uint64_t n) {
+    auto seq = [](int fd, const char *p, uint64_t n, int64_t at) -> int {  // at < 0: write()
+        for (uint64_t o = 0; o < n;) {
+            const size_t m = (size_t)std::min<uint64_t>(n - o, 1u << 30);
+            const ssize_t w = at < 0 ? ::write(fd, p + o, m) : ::pwrite(fd, p + o, m, (off_t)(at + (int64_t)o));
+            if (w < 0) {
+                if (errno == EINTR) continue;
+                return errno ? errno : EIO;
+            }
+            o += (uint64_t)w;
+        }
+        return 0;
+    };
+    constexpr uint64_t kPiece = 32u << 20;
+    const off_t at = n >= 2 * kPiece ? lseek(fd, 0, SEEK_CUR) : (off_t)-1;
+    int err = 0;
+    if (at < 0) {
+        err = seq(fd, p, n, -1);
+    } else {
+        const uint32_t T = (uint32_t)std::min<uint64_t>(4, n / kPiece);
+        std::vector<int> errs(T, 0);
+        std::vector<std::thread> ts;
+        for (uint32_t t = 1; t < T; t++)
+            ts.emplace_back([&, t] { errs[t] = seq(fd, p + n * t / T, n * (t + 1) / T - n * t / T, at + (int64_t)(n * t / T)); });
+        errs[0] = seq(fd, p, n / T, at);
+        for (auto &x : ts) x.join();
+        for (int e : errs) err = err ? err : e;
+        if (!err && lseek(fd, at + (off_t)n, SEEK_SET) < 0) err = errno;
+    }
+    return err ? tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(err)) : TFBS_OK;
+}
+
 // The launched batch in slot k: its packed blocks back (copy stream) and to fd.
 int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
+    auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = now();
     HIP_TRY(hipEventSynchronize(ctx->bg_done[k]));
+    const double t1 = now();
     const uint64_t total = ctx->bg_total_host[k];
     int r;
     if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
@@ -1648,14 +1688,11 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
         HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost, ctx->copy_stream));
     HIP_TRY(hipEventRecord(ctx->bg_copied[k], ctx->copy_stream));
     HIP_TRY(hipEventSynchronize(ctx->bg_copied[k]));
-    for (uint64_t at = 0; at < total;) {  // the blocks to the file as they are
-        const ssize_t w = ::write(fd, ctx->bg_host[k].p + at, (size_t)std::min<uint64_t>(total - at, 1u << 30));
-        if (w < 0) {
-            if (errno == EINTR) continue;
-            return tfbs::fail(TFBS_E_IO, std::string("write: ") + strerror(errno));
-        }
-        at += (uint64_t)w;
-    }
+    const double t2 = now();
+    if ((r = write_out(fd, reinterpret_cast<const char *>(ctx->bg_host[k].p), total))) return r;  // the blocks as they are
+    ctx->drain_s[0] += t1 - t0;
+    ctx->drain_s[1] += t2 - t1;
+    ctx->drain_s[2] += now() - t2;
     written += total;
     return TFBS_OK;
 }
@@ -1813,6 +1850,10 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
 }  // extern "C"
 
 namespace tfbs {
+
+void rows_bgzf_drain_seconds(const ::tfbs_ctx *ctx, double out[3]) {
+    for (int i = 0; i < 3; i++) out[i] = ctx ? ctx->drain_s[i] : 0.0;
+}
 
 // tfbs_batch_rows_bgzf; pos_base (optional): the POS base is asked for once the
 // call's rows are counted (every piece's row parts built first).

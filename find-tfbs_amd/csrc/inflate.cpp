@@ -53,9 +53,28 @@ inline uint32_t rev_bits(uint32_t x, int n) {
 // length 1 (or none at all); the fixed distance code (30 of 32) is incomplete.
 enum Incomplete { kRejectIncomplete, kSingleCode, kAllowIncomplete };
 
+// Entry payloads (bits 8-31) of the literal/length and distance codes: a literal's
+// byte, a length's or distance's base with its extra-bit count, end of block, or a
+// symbol the format reserves (286-287, 30-31).  One lookup then gives the whole
+// length or distance: base + the extra bits that follow the code.
+constexpr uint32_t kLit = 1u << 12, kEob = 1u << 13, kBad = 1u << 14;
+struct Payloads {
+    uint32_t lit[288], dist[32];
+    Payloads() {
+        for (int s = 0; s < 288; s++)
+            lit[s] = s < 256    ? ((uint32_t)s << 16) | kLit
+                     : s == 256 ? kEob
+                     : s < 286  ? ((uint32_t)kLenBase[s - 257] << 16) | ((uint32_t)kLenExtra[s - 257] << 8)
+                                : kBad;
+        for (int s = 0; s < 32; s++)
+            dist[s] = s < 30 ? ((uint32_t)kDistBase[s] << 16) | ((uint32_t)kDistExtra[s] << 8) : kBad;
+    }
+};
+const Payloads kPay;
+
 // Canonical Huffman code of lens[0..n) (0: unused) into t; false if over-subscribed
-// or incomplete where `inc` forbids it.
-bool build(Table &t, const uint8_t *lens, int n, int main_bits, Incomplete inc) {
+// or incomplete where `inc` forbids it.  Entries carry pay[s] (nullptr: the symbol).
+bool build(Table &t, const uint8_t *lens, int n, int main_bits, Incomplete inc, const uint32_t *pay = nullptr) {
     int count[16] = {0};
     for (int i = 0; i < n; i++) count[lens[i]]++;
     count[0] = 0;
@@ -106,13 +125,14 @@ bool build(Table &t, const uint8_t *lens, int n, int main_bits, Incomplete inc) 
         const int l = lens[s];
         if (!l) continue;
         const uint32_t r = rev_bits((uint32_t)next[l]++, l);
+        const uint32_t ent = (pay ? pay[s] : (uint32_t)s << 16) | (uint32_t)l;
         if (l <= main_bits) {
-            for (uint32_t k = r; k < msize; k += 1u << l) t.e[k] = ((uint32_t)s << 16) | (uint32_t)l;
+            for (uint32_t k = r; k < msize; k += 1u << l) t.e[k] = ent;
         } else {
             const uint32_t link = t.e[r & (msize - 1)];
             const uint32_t base = link >> 16, sb = link & 15u;
             const int rest = l - main_bits;
-            for (uint32_t k = r >> main_bits; k < (1u << sb); k += 1u << rest) t.e[base + k] = ((uint32_t)s << 16) | (uint32_t)l;
+            for (uint32_t k = r >> main_bits; k < (1u << sb); k += 1u << rest) t.e[base + k] = ent;
         }
     }
     return true;
@@ -165,6 +185,14 @@ inline int decode(const Table &t, Bits &b) {
     return (int)(e >> 16);
 }
 
+// t's entry for the code at the bottom of buf (>= 15 bits there), the sub-table
+// link followed; bits 0-3 the code's length (0: no such code)
+inline uint32_t lookup(const Table &t, uint64_t buf) {
+    uint32_t e = t.e[buf & ((1u << t.bits) - 1u)];
+    if (__builtin_expect(e & 16u, 0)) e = t.e[(e >> 16) + ((uint32_t)(buf >> t.bits) & ((1u << (e & 15u)) - 1u))];
+    return e;
+}
+
 struct FixedTables {
     Table lit, dist;
     FixedTables() {
@@ -173,10 +201,10 @@ struct FixedTables {
         for (int i = 144; i < 256; i++) l[i] = 9;
         for (int i = 256; i < 280; i++) l[i] = 7;
         for (int i = 280; i < 288; i++) l[i] = 8;
-        build(lit, l, 288, kLitBits, kAllowIncomplete);
+        build(lit, l, 288, kLitBits, kAllowIncomplete, kPay.lit);
         uint8_t d[30];
         for (int i = 0; i < 30; i++) d[i] = 5;
-        build(dist, d, 30, kDistBits, kAllowIncomplete);
+        build(dist, d, 30, kDistBits, kAllowIncomplete, kPay.dist);
     }
 };
 
@@ -243,28 +271,39 @@ int inflate_raw_fast(const uint8_t *in, size_t in_len, uint8_t *out, size_t out_
                     }
                 }
                 if (!lens[256]) return -1;
-                if (!build(dyn_lit, lens, hlit, kLitBits, kSingleCode) || !build(dyn_dist, lens + hlit, hdist, kDistBits, kSingleCode))
+                if (!build(dyn_lit, lens, hlit, kLitBits, kSingleCode, kPay.lit) ||
+                    !build(dyn_dist, lens + hlit, hdist, kDistBits, kSingleCode, kPay.dist))
                     return -1;
                 lt = &dyn_lit;
                 dt = &dyn_dist;
             }
             for (;;) {
-                if (b.n < 48) b.refill();
-                const int sym = decode(*lt, b);
-                if (sym < 0) return -1;
-                if (sym < 256) {
+                // one refill per symbol (>= 56 bits): a length code with its extra bits
+                // (<= 20) and a distance code with its (<= 28) fit
+                b.refill();
+                const uint32_t e = lookup(*lt, b.buf);
+                const int l = (int)(e & 15u);
+                if (!l) return -1;
+                if (e & kLit) {
                     if (o >= out_len) return -1;
-                    out[o++] = (uint8_t)sym;
+                    b.drop(l);
+                    out[o++] = (uint8_t)(e >> 16);
                     continue;
                 }
-                if (sym == 256) break;
-                const int li = sym - 257;
-                if (li >= 29) return -1;
-                const uint32_t len = kLenBase[li] + b.get(kLenExtra[li]);
-                if (b.n < 32) b.refill();
-                const int ds = decode(*dt, b);
-                if (ds < 0 || ds >= 30) return -1;
-                const uint32_t dist = kDistBase[ds] + b.get(kDistExtra[ds]);
+                if (e & (kEob | kBad)) {
+                    if (e & kBad) return -1;
+                    b.drop(l);
+                    break;
+                }
+                const int lx = (int)((e >> 8) & 15u);
+                const uint32_t len = (e >> 16) + ((uint32_t)(b.buf >> l) & ((1u << lx) - 1u));
+                b.drop(l + lx);
+                const uint32_t de = lookup(*dt, b.buf);
+                const int dl = (int)(de & 15u);
+                if (!dl || (de & kBad)) return -1;
+                const int dx = (int)((de >> 8) & 15u);
+                const uint32_t dist = (de >> 16) + ((uint32_t)(b.buf >> dl) & ((1u << dx) - 1u));
+                b.drop(dl + dx);
                 if (dist > o || o + len > out_len) return -1;
                 uint8_t *dst = out + o;
                 const uint8_t *src = dst - dist;

@@ -12,6 +12,7 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -35,11 +36,17 @@ template <class F> static void par_for(size_t n, uint32_t threads, F fn) {
         for (size_t i = 0; i < n; i++) fn(i);
         return;
     }
+    // items taken in small grains from a shared counter: a thread the scheduler holds
+    // back (the run flow's other stages share the cores) leaves its share to the others
+    const size_t grain = std::max<size_t>(1, n / (T * 16));
+    std::atomic<size_t> next(0);
+    auto work = [&] {
+        for (size_t i0; (i0 = next.fetch_add(grain)) < n;)
+            for (size_t i = i0; i < std::min(n, i0 + grain); i++) fn(i);
+    };
     std::vector<std::thread> ts;
-    for (size_t t = 0; t < T; t++)
-        ts.emplace_back([&, t] {
-            for (size_t i = t * n / T; i < (t + 1) * n / T; i++) fn(i);
-        });
+    for (size_t t = 1; t < T; t++) ts.emplace_back(work);
+    work();
     for (auto &x : ts) x.join();
 }
 
@@ -432,11 +439,12 @@ static int decode_bcf_record(const unsigned char *&p, const unsigned char *end, 
 }
 
 Bcf::~Bcf() {
+    discard_ahead();
     if (f) fclose(f);
     if (getenv("TFBS_BCF_TIMING"))
         fprintf(stderr, "tfbs_bcf_timing {\"read_s\": %.4f, \"inflate_s\": %.4f, \"erase_s\": %.4f, \"scan_s\": %.4f, "
-                        "\"decode_s\": %.4f, \"inflated_bytes\": %llu}\n",
-                t_read, t_inflate, t_erase, t_scan, t_decode, (unsigned long long)n_inflated);
+                        "\"decode_s\": %.4f, \"ahead_wait_s\": %.4f, \"inflated_bytes\": %llu}\n",
+                t_read, t_inflate, t_erase, t_scan, t_decode, t_ahead_wait, (unsigned long long)n_inflated);
 }
 
 int Bcf::open(const std::string &p, uint32_t nthreads) {
@@ -446,6 +454,7 @@ int Bcf::open(const std::string &p, uint32_t nthreads) {
     if (const char *e = getenv("TFBS_BCF_THREADS")) threads = std::max(1, atoi(e));
     if (const char *e = getenv("TFBS_BCF_CHUNK_KB")) chunk = std::max<size_t>(1, (size_t)atoll(e)) << 10;
     condense = !(getenv("TFBS_BCF_CONDENSED") && atoi(getenv("TFBS_BCF_CONDENSED")) == 0);
+    read_ahead = !(getenv("TFBS_BCF_READAHEAD") && atoi(getenv("TFBS_BCF_READAHEAD")) == 0);
     int rc = rewind();
     if (rc) return rc;
     if ((rc = load_csi())) return rc;
@@ -473,6 +482,7 @@ int Bcf::select(const std::vector<size_t> &s) {
 
 // (Re)start at the first record: header parsed again, window emptied.
 int Bcf::rewind() {
+    discard_ahead();
     if (f) fclose(f);
     f = fopen(path.c_str(), "rb");
     if (!f) return fail(TFBS_E_IO, "Could not open file " + path);
@@ -594,6 +604,7 @@ uint64_t Bcf::csi_start(int contig, uint64_t beg) const {
 
 // Restart the stream at virtual offset voff (block at voff >> 16, byte voff & 0xFFFF of it).
 int Bcf::seek(int contig, uint64_t voff) {
+    discard_ahead();
     if (fseeko(f, (off_t)(voff >> 16), SEEK_SET) != 0) return fail(TFBS_E_IO, "seek failed in " + path);
     cbuf.clear();
     dbuf.clear();
@@ -915,7 +926,15 @@ size_t Bcf::sblock(uint64_t o) const {
 }
 
 void Bcf::sread(uint64_t o, size_t n, uint8_t *dst) const {
-    for (size_t bi = sblock(o); n; bi++) {
+    size_t hint = sblock(o);
+    sread_from(hint, o, n, dst);
+}
+
+void Bcf::sread_from(size_t &hint, uint64_t o, size_t n, uint8_t *dst) const {
+    size_t bi = hint < cblk.size() && cblk[hint].a0 <= o ? hint : sblock(o);
+    while (bi + 1 < cblk.size() && cblk[bi].a0 + cblk[bi].n <= o) bi++;
+    hint = bi;
+    for (; n; bi++) {
         const CBlock &b = cblk[bi];
         const uint32_t off = (uint32_t)(o - b.a0), m = (uint32_t)std::min<uint64_t>(n, b.n - off);
         b.read(off, m, dst);
@@ -925,20 +944,17 @@ void Bcf::sread(uint64_t o, size_t n, uint8_t *dst) const {
     }
 }
 
-// Read a chunk of compressed bytes, inflate its complete BGZF blocks on the reader's
-// threads, each into a thread-local buffer that is condensed at once, and append them.
-int Bcf::inflate_condensed() {
-    if (in_eof) return TFBS_OK;
+// Read a chunk of compressed bytes and inflate its complete BGZF blocks on the reader's
+// threads, each into a thread-local buffer that is condensed at once.
+int Bcf::condense_chunk(std::vector<CBlock> &out, bool &eof, double &tr, double &ti) {
+    out.clear();
     double t0 = bcf_now();
-    size_t k = 0;  // the blocks wholly before the next record are done with
-    while (k < cblk.size() && cblk[k].a0 + cblk[k].n <= spos) k++;
-    if (k) cblk.erase(cblk.begin(), cblk.begin() + (long)k);
     const size_t have = cbuf.size();
     cbuf.resize(have + chunk);
     const size_t got = fread(&cbuf[have], 1, chunk, f);
     cbuf.resize(have + got);
     double t1 = bcf_now();
-    t_read += t1 - t0;
+    tr += t1 - t0;
     const bool file_end = got < chunk;
     std::vector<BgzfSpan> blks;
     size_t used = 0;
@@ -947,13 +963,7 @@ int Bcf::inflate_condensed() {
     std::vector<size_t> nz;  // (empty blocks -- the EOF marker -- add nothing)
     for (size_t i = 0; i < blks.size(); i++)
         if (blks[i].isize) nz.push_back(i);
-    const size_t base = cblk.size();
-    cblk.resize(base + nz.size());
-    for (size_t j = 0; j < nz.size(); j++) {
-        cblk[base + j].a0 = send;
-        send += blks[nz[j]].isize;
-        n_inflated += blks[nz[j]].isize;
-    }
+    out.resize(nz.size());
     std::vector<int> bad(nz.size(), 0);
     const unsigned char *c = (const unsigned char *)cbuf.data();
     par_for(nz.size(), nz.size() >= 4 ? threads : 1, [&](size_t j) {
@@ -967,13 +977,64 @@ int Bcf::inflate_condensed() {
             bad[j] = 1;
             return;
         }
-        condense_block(buf.data(), (uint32_t)s.isize, cblk[base + j], ex, mk);
+        condense_block(buf.data(), (uint32_t)s.isize, out[j], ex, mk);
     });
-    t_inflate += bcf_now() - t1;
+    ti += bcf_now() - t1;
     for (int x : bad)
         if (x) return fail(TFBS_E_IO, "corrupt BGZF data in " + path);
     cbuf.erase(0, used);
-    if (file_end && cbuf.empty()) in_eof = true;
+    eof = file_end && cbuf.empty();
+    return TFBS_OK;
+}
+
+void Bcf::discard_ahead() {
+    if (ahead.th.joinable()) ahead.th.join();
+    ahead.blk.clear();
+    ahead.rc = TFBS_OK;
+}
+
+// The next chunk's condensed blocks onto the stream: the read-ahead's (waited for), or
+// read here; then the read-ahead of the one after starts.
+int Bcf::inflate_condensed() {
+    if (in_eof) return TFBS_OK;
+    size_t k = 0;  // the blocks wholly before the next record are done with
+    while (k < cblk.size() && cblk[k].a0 + cblk[k].n <= spos) k++;
+    if (k) cblk.erase(cblk.begin(), cblk.begin() + (long)k);
+    std::vector<CBlock> got;
+    bool eof = false;
+    if (ahead.th.joinable()) {
+        const double t0 = bcf_now();
+        ahead.th.join();
+        t_ahead_wait += bcf_now() - t0;
+        t_read += ahead.tr;
+        t_inflate += ahead.ti;
+        ahead.tr = ahead.ti = 0;
+        if (ahead.rc) {
+            const int rc = ahead.rc;
+            ahead.rc = TFBS_OK;
+            return fail(rc, ahead.err);
+        }
+        got.swap(ahead.blk);
+        eof = ahead.eof;
+    } else if (int rc = condense_chunk(got, eof, t_read, t_inflate)) {
+        return rc;
+    }
+    const size_t base = cblk.size();
+    cblk.reserve(base + got.size());
+    for (CBlock &b : got) {
+        b.a0 = send;
+        send += b.n;
+        n_inflated += b.n;
+        cblk.push_back(std::move(b));
+    }
+    if (eof) {
+        in_eof = true;
+    } else if (read_ahead) {
+        ahead.th = std::thread([this] {
+            ahead.rc = condense_chunk(ahead.blk, ahead.eof, ahead.tr, ahead.ti);
+            if (ahead.rc) ahead.err = tfbs_last_error();
+        });
+    }
     return TFBS_OK;
 }
 
@@ -996,18 +1057,18 @@ int Bcf::fill_condensed() {
     }
     std::vector<uint64_t> offs;
     const double ts = bcf_now();
+    size_t hint = 0;
     for (;;) {
         uint64_t o = spos;
         while (o + 8 <= send) {
-            uint8_t h[16];
-            sread(o, 8, h);
+            uint8_t h[16];  // the lengths, CHROM and POS in one read
+            sread_from(hint, o, (size_t)std::min<uint64_t>(16, send - o), h);
             uint32_t ls, li;
             memcpy(&ls, h, 4);
             memcpy(&li, h + 4, 4);
             const uint64_t n = 8 + (uint64_t)ls + li;
             if (o + n > send) break;
             if (ls < 24) return fail(TFBS_E_PARSE, "short BCF record");
-            sread(o + 8, 8, h + 8);
             int32_t chrom, pos;
             memcpy(&chrom, h + 8, 4);
             memcpy(&pos, h + 12, 4);

@@ -7,6 +7,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace tfbs {
@@ -140,6 +141,11 @@ class Bcf {
     std::vector<std::string> samples, contigs;
 
     bool indexed() const { return !csi.empty(); }
+    // seconds so far in file reads, inflate + condense, record boundary scans (with the
+    // inflate rounds they wait for: of them, waits for the read-ahead), decodes
+    void phase_seconds(double &read, double &inflate, double &scan, double &ahead_wait, double &decode) const {
+        read = t_read, inflate = t_inflate, scan = t_scan, ahead_wait = t_ahead_wait, decode = t_decode;
+    }
 
   private:
     int rewind();
@@ -151,7 +157,26 @@ class Bcf {
     int fill_condensed();
     bool condensed() const { return carriers_mode && condense && bgzf; }
     int inflate_condensed();
+    // the next `chunk` compressed bytes' complete BGZF blocks, inflated and condensed
+    // on the reader's threads (a0 unset); reads f and cbuf only
+    int condense_chunk(std::vector<CBlock> &out, bool &eof, double &tr, double &ti);
+    // read-ahead (TFBS_BCF_READAHEAD=0: off): once a chunk is in, the next one is read
+    // and condensed on a background thread while the caller scans, decodes and does
+    // its own work; inflate_condensed takes it over, seek/rewind discard it
+    struct Ahead {
+        std::thread th;
+        std::vector<CBlock> blk;
+        bool eof = false;
+        int rc = 0;
+        std::string err;
+        double tr = 0, ti = 0;
+    } ahead;
+    bool read_ahead = true;
+    double t_ahead_wait = 0;  // (of t_scan) waiting for the read-ahead to finish
+    void discard_ahead();
     void sread(uint64_t o, size_t n, uint8_t *dst) const;  // bytes [o, o + n) of the condensed stream
+    // sread with the block search from *hint on (a walk in stream order)
+    void sread_from(size_t &hint, uint64_t o, size_t n, uint8_t *dst) const;
     size_t sblock(uint64_t o) const;                       // the block holding byte o
     int decode_condensed(uint64_t o, BcfRecord &r) const;
     int load_csi();

@@ -453,6 +453,10 @@ struct KfShape {
 constexpr int kFB = TFBS_KF_BLOCK;
 #ifdef TFBS_KF_LDS3  // (A/B: the round-4 start's ~51 KB shape, three regions per CU)
 using KfSmall = KfShape<kFB, 4 * kFB, 16 * kFB, kFB, 16 * kFB, 2 * kFB, kFB>;
+#elif defined(TFBS_KF_LDS6)  // (A/B: ~26 KB, six regions per CU)
+using KfSmall = KfShape<kFB, 2 * kFB, 7 * kFB, kFB, 6 * kFB, kFB, kFB / 2>;
+#elif defined(TFBS_KF_LDS8)  // (A/B: ~19 KB, eight regions per CU)
+using KfSmall = KfShape<kFB, kFB, 4 * kFB, kFB / 2, 4 * kFB, kFB / 2, kFB / 2>;
 #else  // ~40 KB: four regions per CU
 using KfSmall = KfShape<kFB, 2 * kFB, 14 * kFB, kFB, 12 * kFB, kFB, kFB / 2>;
 #endif
@@ -506,8 +510,12 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *s_w, u
     return pre + x - v;
 }
 
+#ifndef TFBS_KF_WAVES
+#define TFBS_KF_WAVES 1
+#endif
 template <class C>
-__global__ __launch_bounds__(C::kBlock) void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count, uint32_t which) {
+__global__ __launch_bounds__(C::kBlock) __attribute__((amdgpu_waves_per_eu(C::kBlock == 1024 ? 1 : TFBS_KF_WAVES)))
+void key_fast_kernel(AsmArgs A, uint32_t first, uint32_t count, uint32_t which) {
     constexpr int kFBlock = C::kBlock;
     constexpr uint32_t kFWaves = C::kWaves, kFHapLds = C::kHapLds, kFCor = C::kCor, kFRefs = C::kRefs,
                        kFCnt = C::kCnt, kFRuns = C::kRuns, kFRows = C::kRows, kFLists = C::kLists;

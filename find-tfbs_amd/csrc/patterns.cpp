@@ -109,6 +109,25 @@ int parse_threshold_file(const std::string &path, float thr, int32_t *out) {
 void Patterns::add(const Pat &p) {
     pats.push_back(p);
     names[p.pattern_id] = p.name;  // main.rs:239-250 HashMap insert: last wins
+    slot_cache = std::make_shared<SlotCache>();  // (a copy keeps the old set's)
+}
+
+int Patterns::slot_order(std::vector<uint16_t> &slot_pid, bool &zero_len_panics) const {
+    std::lock_guard<std::mutex> l(slot_cache->mu);
+    SlotCache &c = *slot_cache;
+    if (!c.built) {
+        Plan plan;  // only its slot order is used (independent of the tile options)
+        PlanOptions opt;
+        opt.tile_blocks = 1u << 30;
+        c.rc = build_plan(opt, &plan);
+        c.slot_pid = std::move(plan.slot_pid);
+        c.zero_len_panics = plan.zero_len_panics;
+        c.built = true;
+    }
+    if (c.rc) return c.rc;
+    slot_pid = c.slot_pid;
+    zero_len_panics = c.zero_len_panics;
+    return 0;
 }
 
 uint32_t Patterns::max_length() const {

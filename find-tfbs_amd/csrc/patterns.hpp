@@ -3,6 +3,8 @@
 
 #include <cstdint>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,6 +59,19 @@ struct Patterns {
     void add(const Pat &p);
     uint32_t max_length() const;
     int build_plan(const PlanOptions &opt, Plan *plan) const;
+    // the plan's slot order (slot -> pattern id) and zero_len_panics, built once per
+    // pattern set and shared by every batch made from it (tfbs_batch_create)
+    int slot_order(std::vector<uint16_t> &slot_pid, bool &zero_len_panics) const;
+
+  private:
+    struct SlotCache {
+        std::mutex mu;
+        bool built = false;
+        int rc = 0;
+        std::vector<uint16_t> slot_pid;
+        bool zero_len_panics = false;
+    };
+    std::shared_ptr<SlotCache> slot_cache = std::make_shared<SlotCache>();
 };
 
 struct SlotGroup {  // the strands of one pattern_id and its count slot

@@ -63,5 +63,8 @@ int plan_from_parts(const Batch &B, RowParts &P, size_t r0, size_t r1, const std
 int rows_bgzf_chained(::tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, const char *chromosome,
                       uint32_t min_maf, uint32_t *fake_position, int fd, uint64_t *bytes, uint64_t *n_rows,
                       const std::function<int(uint64_t, uint32_t *)> &pos_base);
+// Seconds the ctx's BGZF row calls spent draining: waiting for the device's blocks,
+// for their copy back, and writing them out.
+void rows_bgzf_drain_seconds(const ::tfbs_ctx *ctx, double out[3]);
 
 }  // namespace tfbs

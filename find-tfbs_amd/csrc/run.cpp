@@ -70,11 +70,12 @@ bool in_path(const char *prog) {
 }
 
 // One device's share of the run: batches of merged regions (global batch g =
-// regions [g per_batch, (g + 1) per_batch)), processed in the two-stage pipeline
-// (a helper thread prepares the next batch -- FASTA windows, BCF records,
-// load_diffs, distinct haplotypes, grouped on the device where the region is
-// SNV-only -- while this one is scanned, reduced and encoded on the device) with
-// its own readers and ctx; out(g, ctx, batch) emits each batch's rows.
+// regions [g per_batch, (g + 1) per_batch)), processed in a three-stage pipeline
+// (one thread fetches batch g + 2's inputs -- FASTA windows, inner peaks, BCF
+// records with their carriers (load_diffs) --, another builds batch g + 1's
+// distinct haplotypes, grouped on the device where it can, while batch g is
+// scanned, reduced and encoded on the device) with its own readers and ctx;
+// out(g, ctx, batch) emits each batch's rows.
 struct Shard {
     std::vector<size_t> batches;  // global batch indices, ascending
     int device = 0;
@@ -83,7 +84,14 @@ struct Shard {
     std::string err;
     size_t regions = 0;
     double t_prep = 0, t_wait = 0, t_gpu = 0, t_rows = 0;
-    double t_bcf = 0, t_build = 0;  // of t_prep: BCF fetch + decode + record ids, add_regions
+    double t_bcf = 0, t_build = 0;  // of t_prep (fetch + build stages): BCF fetch + decode + record ids, add_regions
+    double t_fasta = 0, t_ids = 0;   // of t_prep: FASTA + inner peaks; of t_bcf: make_record_ids
+    // the BCF reader's own phases (of t_bcf): file reads, inflate + condense, record
+    // boundary scan, record decode
+    double b_read = 0, b_inflate = 0, b_scan = 0, b_wait = 0, b_decode = 0;
+    double t_create = 0;                 // of t_prep: tfbs_batch_create
+    double rows_plan = 0, rows_dev = 0;  // of t_rows: host row plans, device blocks + copy back + write
+    double drain[3] = {0, 0, 0};         // of rows_dev: waits for the device's blocks, their copy back, the writes
 };
 
 struct RunSetup {
@@ -131,17 +139,42 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
     std::vector<const BcfRecord *> recs;
     auto clock = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    auto prepare = [&](size_t g, BatchPtr &bp, std::string &err, double &t_bcf, double &t_build) -> int {
+    struct BcfPhases {
+        Bcf &b;
+        Shard &sh;
+        ~BcfPhases() { b.phase_seconds(sh.b_read, sh.b_inflate, sh.b_scan, sh.b_wait, sh.b_decode); }
+    } bcf_phases{bcf, sh};
+    // The shard's batches go through three stages at once: batch g + 2's inputs are
+    // fetched (FASTA, inner peaks, the BCF's records with their carriers -- the reader
+    // inflating ahead on its own thread) while batch g + 1 is built (add_regions:
+    // distinct haplotypes, grouped on the device where it can) and batch g is
+    // scanned, reduced and encoded on the device and its rows written here.
+    struct Pending {
+        BatchPtr bp{nullptr, tfbs_batch_destroy};
+        std::vector<RegionInput> ins;
+    };
+    struct Times {
+        double fetch = 0, build = 0, bcf = 0, ids = 0, fasta = 0, create = 0;
+    };
+    auto fetch = [&](size_t g, Pending &p, std::string &err, Times &t) -> int {
+        const double t_in = clock();
+        struct Done {
+            double &acc, t0;
+            ~Done() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - t0; }
+        } done{t.fetch, t_in};
         const size_t b0 = g * S.per_batch, b1 = std::min(S.merged.size(), b0 + S.per_batch);
         tfbs_batch *bb = nullptr;
         int rc = tfbs_batch_create(S.pp, (uint32_t)S.sel.size(), 1, &bb);
+        t.create += clock() - t_in;
         if (rc) return err = tfbs_last_error(), rc;
-        bp = BatchPtr(bb, tfbs_batch_destroy);
+        p.bp = BatchPtr(bb, tfbs_batch_destroy);
         Batch &B = bb->b;
         B.grouper = grouper;
         for (auto &b : S.beds) B.beds.push_back(b.first);
-        std::vector<RegionInput> ins;
+        p.ins.clear();
+        p.ins.reserve(b1 - b0);
         for (size_t r = b0; r < b1; r++) {
+            const double tf = clock();
             const auto &m = S.merged[r];
             RegionInput in;
             in.R.ms = m.first;
@@ -170,9 +203,9 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                                            [&](uint32_t i, uint64_t v) { return pk[i].first < v; });
                 std::vector<uint32_t> hit;
                 for (; it != ord.end() && pk[*it].first <= m.second; ++it) {
-                    const auto &p = pk[*it];
-                    const bool ov = (m.first >= p.first && m.first <= p.second) ||
-                                    (m.second >= p.first && m.second <= p.second);
+                    const auto &q = pk[*it];
+                    const bool ov = (m.first >= q.first && m.first <= q.second) ||
+                                    (m.second >= q.first && m.second <= q.second);
                     if (ov) hit.push_back(*it);
                 }
                 std::sort(hit.begin(), hit.end());
@@ -184,7 +217,9 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                 return TFBS_E_ARG;
             }
             const double tb = clock();
+            t.fasta += tb - tf;
             if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
+            const double ti = clock();
             for (const BcfRecord *br : recs) {
                 Record rec;
                 rc = make_record_ids(br->pos, br->n_alleles, br->ref.c_str(),
@@ -192,44 +227,58 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                 if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
-            t_bcf += clock() - tb;
-            ins.push_back(std::move(in));
+            const double te = clock();
+            t.ids += te - ti;
+            t.bcf += te - tb;
+            p.ins.push_back(std::move(in));
         }
-        const double tb = clock();
-        rc = add_regions(B, ins, sh.threads);
-        t_build += clock() - tb;
-        if (rc) return err = tfbs_last_error(), rc;
         return TFBS_OK;
     };
+    auto build = [&](Pending &p, std::string &err, Times &t) -> int {
+        const double tb = clock();
+        const int rc = add_regions(p.bp->b, p.ins, sh.threads);
+        std::vector<RegionInput>().swap(p.ins);
+        t.build += clock() - tb;
+        return rc ? (err = tfbs_last_error(), rc) : TFBS_OK;
+    };
+    auto account = [&](const Times &t) {
+        sh.t_prep += t.fetch + t.build;
+        sh.t_bcf += t.bcf;
+        sh.t_build += t.build;
+        sh.t_fasta += t.fasta;
+        sh.t_ids += t.ids;
+        sh.t_create += t.create;
+    };
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    BatchPtr cur(nullptr, tfbs_batch_destroy);
+    const size_t nb = sh.batches.size();
+    Pending cur, nxt, nxt2;
     std::string err;
-    double t0 = now();
-    if ((rc = prepare(sh.batches[0], cur, err, sh.t_bcf, sh.t_build))) return fail(rc, err);
-    sh.t_prep += now() - t0;
-    for (size_t bi = 0; bi < sh.batches.size(); bi++) {
+    {
+        Times t;
+        if ((rc = fetch(sh.batches[0], cur, err, t)) || (rc = build(cur, err, t)) ||
+            (nb > 1 && (rc = fetch(sh.batches[1], nxt, err, t))))
+            return fail(rc, err);
+        account(t);
+    }
+    for (size_t bi = 0; bi < nb; bi++) {
         const size_t g = sh.batches[bi];
-        BatchPtr next(nullptr, tfbs_batch_destroy);
-        std::string nerr;
-        int nrc = TFBS_OK;
-        double nprep = 0, nbcf = 0, nbuild = 0;
-        std::thread helper;
-        if (bi + 1 < sh.batches.size())
-            helper = std::thread([&, bi] {
-                const double t0 = now();
-                nrc = prepare(sh.batches[bi + 1], next, nerr, nbcf, nbuild);
-                nprep = now() - t0;
-            });
-        // join the helper on every exit path
+        Times ta, tb;
+        std::string ea, eb;
+        int ra = TFBS_OK, rb = TFBS_OK;
+        std::thread th_fetch, th_build;
+        if (bi + 2 < nb) th_fetch = std::thread([&, bi] { ra = fetch(sh.batches[bi + 2], nxt2, ea, ta); });
+        if (bi + 1 < nb) th_build = std::thread([&] { rb = build(nxt, eb, tb); });
+        // join the helpers on every exit path
         struct Joiner {
-            std::thread &t;
+            std::thread &a, &b;
             ~Joiner() {
-                if (t.joinable()) t.join();
+                if (a.joinable()) a.join();
+                if (b.joinable()) b.join();
             }
-        } joiner{helper};
-        tfbs_batch *bb = cur.get();
+        } joiner{th_fetch, th_build};
+        tfbs_batch *bb = cur.bp.get();
         Batch &B = bb->b;
-        t0 = now();
+        double t0 = now();
         if ((rc = tfbs_batch_upload(ctx, bb)) || (rc = tfbs_scan(ctx, bb)) || (rc = tfbs_batch_assemble(ctx, bb)) ||
             (rc = tfbs_batch_reduce(ctx, bb)) ||
             (rc = tfbs_batch_encode_flags(ctx, bb, 0, B.rh.size(), out.device_rows ? TFBS_ENC_DEVICE_CODES : 0)))
@@ -246,14 +295,20 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
                         B.rh[r].hap_count, B.rh[r].n_variants);
         }
         t0 = now();
-        if (helper.joinable()) helper.join();
+        if (th_fetch.joinable()) th_fetch.join();
+        if (th_build.joinable()) th_build.join();
         sh.t_wait += now() - t0;
-        sh.t_prep += nprep;
-        sh.t_bcf += nbcf;
-        sh.t_build += nbuild;
-        if (nrc) return fail(nrc, nerr);
-        cur = std::move(next);
+        account(ta);
+        account(tb);
+        if (rb) return fail(rb, eb);
+        if (ra) return fail(ra, ea);
+        cur = std::move(nxt);
+        nxt = std::move(nxt2);
+        nxt2 = Pending();
     }
+    double rs[2];
+    if (tfbs_ctx_rows_bgzf_seconds(ctx, rs) == TFBS_OK) sh.rows_plan = rs[0], sh.rows_dev = rs[1];
+    rows_bgzf_drain_seconds(ctx, sh.drain);
     return TFBS_OK;
 }
 
@@ -656,10 +711,15 @@ int tfbs_run(const tfbs_run_args *a) {
         for (size_t k = 0; k < n_sh; k++)
             fprintf(stderr,
                     "tfbs_run_timing {\"shard\": %zu, \"device\": %d, \"regions\": %zu, \"batches\": %zu, "
-                    "\"prep_s\": %.4f, \"prep_bcf_s\": %.4f, \"prep_build_s\": %.4f, \"prep_wait_s\": %.4f, "
+                    "\"prep_s\": %.4f, \"prep_bcf_s\": %.4f, \"prep_build_s\": %.4f, \"prep_fasta_s\": %.4f, "
+                    "\"prep_ids_s\": %.4f, \"bcf_read_s\": %.4f, \"bcf_inflate_s\": %.4f, \"bcf_scan_s\": %.4f, "
+                    "\"bcf_ahead_wait_s\": %.4f, \"bcf_decode_s\": %.4f, \"prep_create_s\": %.4f, \"rows_plan_s\": %.4f, \"rows_dev_s\": %.4f, "
+                    "\"drain_gpu_s\": %.4f, \"drain_copy_s\": %.4f, \"drain_write_s\": %.4f, \"prep_wait_s\": %.4f, "
                     "\"gpu_s\": %.4f, \"rows_s\": %.4f, \"ordered_write_s\": %.4f, \"close_s\": %.4f, \"loop_s\": %.4f}\n",
                     k, shards[k].device, shards[k].regions, shards[k].batches.size(), shards[k].t_prep,
-                    shards[k].t_bcf, shards[k].t_build,
+                    shards[k].t_bcf, shards[k].t_build, shards[k].t_fasta, shards[k].t_ids, shards[k].b_read,
+                    shards[k].b_inflate, shards[k].b_scan, shards[k].b_wait, shards[k].b_decode, shards[k].t_create, shards[k].rows_plan,
+                    shards[k].rows_dev, shards[k].drain[0], shards[k].drain[1], shards[k].drain[2],
                     shards[k].t_wait, shards[k].t_gpu, shards[k].t_rows, t_write, t_close, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +

@@ -253,8 +253,9 @@ def test_bcf_carriers_mode_matches_raw_gt(tmp_path, sel):
     assert n_car > 50 and (n_bad > 0 or sel is not None)
 
 
+@pytest.mark.parametrize("readahead", [0, 1])
 @pytest.mark.parametrize("chunk_kb", [None, 1, 7])
-def test_bcf_condensed_stream_matches_dense(tmp_path, monkeypatch, chunk_kb):
+def test_bcf_condensed_stream_matches_dense(tmp_path, monkeypatch, chunk_kb, readahead):
     """Carriers mode reads the condensed stream (io.hpp CBlock: per 64-byte line a
     background code -- alternating 2/3 either way round, all 2, all 3 -- plus the
     differing bytes; blocks that are not GT-like kept whole).  Against the dense
@@ -263,7 +264,10 @@ def test_bcf_condensed_stream_matches_dense(tmp_path, monkeypatch, chunk_kb):
     (blocks kept whole), random bytes, vector_end (ploidy), GT payloads spanning
     several BGZF blocks and read chunks, odd-length shared parts (the alternation's
     parity flips between records), multi-allelic records, a sample selection (the
-    payload read back) and a CSI seek (the condensed stream restarting mid-file)."""
+    payload read back) and a CSI seek (the condensed stream restarting mid-file); with
+    and without the read-ahead (the next chunk condensed on a background thread, dropped
+    by a seek)."""
+    monkeypatch.setenv("TFBS_BCF_READAHEAD", str(readahead))
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import struct
 
