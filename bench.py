@@ -432,6 +432,15 @@ def main():
         mfma_ms.append(L.tfbs_ctx_last_mfma_ms(sc.h))   # the matrix-core kernel alone (-1: none ran)
         asm_ms.append(L.tfbs_ctx_last_assemble_ms(sc.h))  # the assembly's launches
     T.check(L.tfbs_ctx_sync(sc.h))
+    # the last step's list counters (device atomics, one per wave): candidates, the part
+    # of them in the waves' global lists, hit-list pairs, spill records, overflow
+    lc = (ctypes.c_uint64 * 5)()
+    T.check(L.tfbs_ctx_scan_counters(sc.h, lc))
+    list_counters = {"candidates": lc[2], "candidates_global": lc[3], "hit_pairs": lc[4], "spill_records": lc[0],
+                     "candidates_overflow": lc[1],
+                     # bytes the scan writes to its lists: 8 per global candidate and per hit pair,
+                     # 12 per spill / overflow record, 4 per wave's hit count
+                     "list_bytes": 8 * (lc[3] + lc[4]) + 12 * (lc[0] + lc[1])}
 
     # the dense download, for reference (the run flow uses the key reduction)
     t_dense = time.perf_counter()
@@ -483,6 +492,13 @@ def main():
                     "frac_rocprof": (MFMA_OPS_PER_CELL * scan_cells / (rp / 1e3) / 1e12 / MFMA_F6_PEAK_TOPS
                                      if rp else None),
                     "traffic_per_algorithmic_byte": traffic / alg_bytes if traffic else None,
+                    "frac_source": "frac: HIP events on the ctx stream around the MFMA phase (this run); "
+                                   "frac_rocprof: the same phase on the rocprofv3 kernel trace of this build "
+                                   "(profiles/pmc_traffic_<W>.json)",
+                    "list_counters": list_counters,
+                    "write_per_list_byte": (prof["write_bytes"] / list_counters["list_bytes"]
+                                            if prof and prof.get("write_bytes") and list_counters["list_bytes"]
+                                            else None),
                     "sq": prof.get("sq") if prof else None,
                     "note": "achieved = 8 ops per (window, strand, column) cell of the FP4 one-hot x FP6 "
                             "bound-digit GEMM x %.4g cells the scan reads (of %.4g: reference-window reuse) / "

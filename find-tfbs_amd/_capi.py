@@ -78,6 +78,7 @@ SIGNATURES = [
     ("tfbs_ctx_last_scan_launches", C.c_int, [vp]),
     ("tfbs_ctx_last_mfma_ms", C.c_float, [vp]),
     ("tfbs_ctx_window_lists", C.c_int, [vp, C.POINTER(C.c_uint64), C.POINTER(C.c_double)]),
+    ("tfbs_ctx_scan_counters", C.c_int, [vp, C.POINTER(C.c_uint64)]),
     ("tfbs_matches", C.c_int, [vp, u8p, u64p, C.c_size_t, u32p, u64p, u64p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("tfbs_patch_haplotype", C.c_int, [C.c_uint64, C.c_uint64, C.c_size_t, u64p, u8p, u32p, u8p, u32p, u8p, u64p,
                                        C.c_size_t, u8p, u64p, C.c_size_t, C.POINTER(C.c_size_t)]),

@@ -9,6 +9,9 @@
 #include <atomic>
 #include <cerrno>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -212,6 +215,25 @@ struct tfbs_ctx {
     hipStream_t copy_stream = nullptr;
     double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
     double drain_s[3] = {0, 0, 0};        // of rows_s[1]: bgzf_drain's waits for the blocks, the copy back, the write
+    // rows_set_async (the run flow's one-device path): a drained slot's blocks are
+    // written by this ctx's writer thread, in order, while the caller goes on; the slot's
+    // host buffer is reused once its write is done (rows_flush: every write done)
+    struct RowsWriter {
+        std::thread th;
+        std::mutex mu;
+        std::condition_variable cv;
+        struct Job {
+            int fd, k;
+            uint64_t n;
+        };
+        std::deque<Job> q;
+        bool busy[3] = {false, false, false};
+        bool stop = false;
+        int rc = 0;
+        std::string err;
+        double write_s = 0;
+    } rw;
+    bool rows_async = false;
     uint64_t rows_text_last = 0;          // the last call's uncompressed row bytes
     const tfbs_batch *resident = nullptr;
     bool scanned = false;                 // the resident batch has been scanned (its lists exist)
@@ -415,7 +437,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
         m.hitn = ctx->hitn.p;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
         if ((rc = ctx->ref_count.ensure(nr)) || (rc = ctx->ref_hits.ensure((size_t)nr * kRefPerRegion * 2)) ||
-            (rc = ctx->over.ensure(2)) || (rc = ctx->spill.ensure((size_t)ctx->spill_cap * 3)) ||
+            (rc = ctx->over.ensure(5)) || (rc = ctx->spill.ensure((size_t)ctx->spill_cap * 3)) ||
             (rc = ctx->cand_over.ensure((size_t)ctx->cand_over_cap * 3)) ||
             (rc = ctx->spill_sorted.ensure((size_t)ctx->spill_cap * 3)) || (rc = ctx->spill_bcnt.ensure(nr + 1)) ||
             (rc = ctx->spill_boff.ensure(nr + 1)))
@@ -449,7 +471,7 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             const uint32_t na = (uint32_t)(kAsmCtrWords + nr + 1);
             if ((rc = ctx->asm_ctr.ensure(na))) return rc;
             hipLaunchKernelGGL(zero3_kernel, dim3(std::min<uint32_t>(256, (std::max(na, nr) + 255) / 256)), dim3(256), 0,
-                               ctx->stream, ctx->ref_count.p, nr, ctx->over.p, 2u, ctx->asm_ctr.p, na);
+                               ctx->stream, ctx->ref_count.p, nr, ctx->over.p, 5u, ctx->asm_ctr.p, na);
             HIP_TRY(hipGetLastError());
             ctx->asm_ctr_zeroed = true;  // (for this scan's first assembly)
         }
@@ -645,6 +667,14 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->rw.th.joinable()) {  // the writes still queued go out first
+        {
+            std::lock_guard<std::mutex> l(ctx->rw.mu);
+            ctx->rw.stop = true;
+        }
+        ctx->rw.cv.notify_all();
+        ctx->rw.th.join();
+    }
     if (ctx->var_owner) {  // its varying counts to the host before var_counts goes
         (void)tfbs::ensure_host_var_counts(*ctx->var_owner);
         std::lock_guard<std::mutex> g(ctx->var_owner->var_mu);
@@ -842,6 +872,18 @@ int tfbs_ctx_rows_bgzf_seconds(const tfbs_ctx *ctx, double *out) {
     if (!ctx || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
     out[0] = ctx->rows_s[0];
     out[1] = ctx->rows_s[1];
+    return TFBS_OK;
+}
+
+int tfbs_ctx_scan_counters(tfbs_ctx *ctx, uint64_t out[5]) {
+    if (!ctx || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
+    for (int i = 0; i < 5; i++) out[i] = 0;
+    if (!ctx->over.p || ctx->over.n < 5) return TFBS_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    uint32_t h[5];
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(h, ctx->over.p, sizeof h, hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; i++) out[i] = h[i];
     return TFBS_OK;
 }
 
@@ -1676,6 +1718,56 @@ static int write_out(int fd, const char *p, uint64_t n) {
 }
 
 // The launched batch in slot k: its packed blocks back (copy stream) and to fd.
+static_assert(tfbs_ctx::kBgSlots == 3, "RowsWriter::busy has a flag per slot");
+
+// The writer thread of rows_set_async: slot writes in queue order.
+static void rows_writer_loop(tfbs_ctx *ctx) {
+    auto &w = ctx->rw;
+    for (;;) {
+        tfbs_ctx::RowsWriter::Job j;
+        {
+            std::unique_lock<std::mutex> l(w.mu);
+            w.cv.wait(l, [&] { return w.stop || !w.q.empty(); });
+            if (w.q.empty()) return;  // (stop with nothing queued)
+            j = w.q.front();
+            w.q.pop_front();
+        }
+        const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        int rc = TFBS_OK;
+        std::string err;
+        {
+            std::lock_guard<std::mutex> l(w.mu);
+            rc = w.rc;  // (after a failed write the rest are dropped)
+        }
+        if (!rc && (rc = write_out(j.fd, reinterpret_cast<const char *>(ctx->bg_host[j.k].p), j.n))) err = tfbs_last_error();
+        const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        {
+            std::lock_guard<std::mutex> l(w.mu);
+            w.busy[j.k] = false;
+            w.write_s += t1 - t0;
+            if (rc && !w.rc) {
+                w.rc = rc;
+                w.err = err;
+            }
+        }
+        w.cv.notify_all();
+    }
+}
+
+// Waits until slot k's host buffer is free (async writes), or every queued write is
+// done (k < 0); the writer's first failure, if any.
+static int rows_wait(tfbs_ctx *ctx, int k) {
+    auto &w = ctx->rw;
+    std::unique_lock<std::mutex> l(w.mu);
+    w.cv.wait(l, [&] {
+        if (k >= 0) return !w.busy[k];
+        for (bool b : w.busy)
+            if (b) return false;
+        return w.q.empty();
+    });
+    return w.rc ? tfbs::fail(w.rc, w.err) : TFBS_OK;
+}
+
 int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
     auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t0 = now();
@@ -1683,17 +1775,28 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
     const double t1 = now();
     const uint64_t total = ctx->bg_total_host[k];
     int r;
+    if (ctx->rw.th.joinable() && (r = rows_wait(ctx, k))) return r;  // slot k's last write is out
     if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
     if (total)
         HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost, ctx->copy_stream));
     HIP_TRY(hipEventRecord(ctx->bg_copied[k], ctx->copy_stream));
     HIP_TRY(hipEventSynchronize(ctx->bg_copied[k]));
     const double t2 = now();
-    if ((r = write_out(fd, reinterpret_cast<const char *>(ctx->bg_host[k].p), total))) return r;  // the blocks as they are
     ctx->drain_s[0] += t1 - t0;
     ctx->drain_s[1] += t2 - t1;
-    ctx->drain_s[2] += now() - t2;
     written += total;
+    if (ctx->rows_async) {  // the writer thread takes it (in order)
+        if (!ctx->rw.th.joinable()) ctx->rw.th = std::thread(rows_writer_loop, ctx);
+        {
+            std::lock_guard<std::mutex> l(ctx->rw.mu);
+            ctx->rw.busy[k] = true;
+            ctx->rw.q.push_back({fd, k, total});
+        }
+        ctx->rw.cv.notify_all();
+        return TFBS_OK;
+    }
+    if ((r = write_out(fd, reinterpret_cast<const char *>(ctx->bg_host[k].p), total))) return r;  // the blocks as they are
+    ctx->drain_s[2] += now() - t2;
     return TFBS_OK;
 }
 
@@ -1853,6 +1956,16 @@ namespace tfbs {
 
 void rows_bgzf_drain_seconds(const ::tfbs_ctx *ctx, double out[3]) {
     for (int i = 0; i < 3; i++) out[i] = ctx ? ctx->drain_s[i] : 0.0;
+    if (ctx) out[2] += const_cast<::tfbs_ctx *>(ctx)->rw.write_s;  // (read after rows_flush)
+}
+
+void rows_set_async(::tfbs_ctx *ctx, bool on) {
+    if (ctx) ctx->rows_async = on;
+}
+
+int rows_flush(::tfbs_ctx *ctx) {
+    if (!ctx || !ctx->rw.th.joinable()) return TFBS_OK;
+    return rows_wait(ctx, -1);
 }
 
 // tfbs_batch_rows_bgzf; pos_base (optional): the POS base is asked for once the

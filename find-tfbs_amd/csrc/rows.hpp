@@ -66,5 +66,10 @@ int rows_bgzf_chained(::tfbs_ctx *ctx, tfbs_batch *b, size_t r0, size_t r1, cons
 // Seconds the ctx's BGZF row calls spent draining: waiting for the device's blocks,
 // for their copy back, and writing them out.
 void rows_bgzf_drain_seconds(const ::tfbs_ctx *ctx, double out[3]);
+// on: the ctx's BGZF row calls return before their last blocks are written (a writer
+// thread writes them in order; the fd must stay open and untouched until rows_flush,
+// which waits for every write and returns the first failure)
+void rows_set_async(::tfbs_ctx *ctx, bool on);
+int rows_flush(::tfbs_ctx *ctx);
 
 }  // namespace tfbs

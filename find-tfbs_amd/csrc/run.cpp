@@ -128,6 +128,9 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
         return rc;
     }
     std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
+    // one device writing straight to the output: its rows' writes go out on the ctx's
+    // writer thread while the next batch runs (flushed below, joined by the ctx's destroy)
+    if (out.device_rows && out.async_rows) rows_set_async(ctx, true);
     // SNV-only regions grouped on this device (haplotype.rs:16-88 on the GPU), one
     // grouper for the shard's batches (its membership rows recycled batch to batch);
     // TFBS_RUN_BUILD_DEVICE=0: every region on the host
@@ -306,6 +309,7 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
         nxt = std::move(nxt2);
         nxt2 = Pending();
     }
+    if ((rc = rows_flush(ctx))) return rc;
     double rs[2];
     if (tfbs_ctx_rows_bgzf_seconds(ctx, rs) == TFBS_OK) sh.rows_plan = rs[0], sh.rows_dev = rs[1];
     rows_bgzf_drain_seconds(ctx, sh.drain);
@@ -578,6 +582,7 @@ int tfbs_run(const tfbs_run_args *a) {
     if (n_sh == 1) {  // one device: its batches in order, straight to the output
         struct One {
             bool device_rows;
+            bool async_rows;  // (straight to the output file: writes may trail the call)
             const RunSetup &S;
             tfbs::BgzfWriter &w;
             const std::string &chr;
@@ -595,13 +600,15 @@ int tfbs_run(const tfbs_run_args *a) {
                 if (int rc = tfbs::batch_row_bodies(bb->b, S.a->min_maf, bodies, std::max(1u, S.a->threads))) return rc;
                 return write_prefixed(w, chr, bodies.data(), bodies.size(), &fake);
             }
-        } one{gpu_bgzf, S, w, chr, fake, t_write};
+        } one{gpu_bgzf, !(getenv("TFBS_RUN_ASYNC_WRITE") && atoi(getenv("TFBS_RUN_ASYNC_WRITE")) == 0), S, w, chr, fake,
+              t_write};
         shards[0].rc = run_shard(S, shards[0], one);
         if (shards[0].rc) shards[0].err = tfbs_last_error();
     } else {  // several: each batch's output to the ordered writer
         Ordered ord(n_batches);
         struct Many {
             bool device_rows;
+            bool async_rows;  // false: each batch's memory file is complete when submitted
             const RunSetup &S;
             Ordered &ord;
             uint32_t threads;
@@ -679,7 +686,7 @@ int tfbs_run(const tfbs_run_args *a) {
         std::vector<std::thread> writers;
         for (int k = 0; k < (gpu_bgzf ? kWriters : 1); k++) writers.emplace_back(writer_fn);
         auto run_one = [&](size_t k) {
-            Many m{gpu_bgzf, S, ord, shards[k].threads};
+            Many m{gpu_bgzf, false, S, ord, shards[k].threads};
             shards[k].rc = run_shard(S, shards[k], m);
             if (shards[k].rc) {
                 shards[k].err = tfbs_last_error();

@@ -86,7 +86,8 @@ struct ScanArgs {
     // key), kind 1 a reference hit (strand, window) -- counted at over[0] (of
     // spill_cap), bucketed by region after the scan (launch_spill_buckets)
     uint32_t *spill;
-    uint32_t *over;  // [0] spill records, [1] candidates past a wave's list
+    uint32_t *over;  // [0] spill records, [1] candidates past a wave's list; counters: [2] candidates,
+                     // [3] of them in the waves' global lists, [4] hit-list pairs
     uint32_t spill_cap;
     // candidates past a wave's list region: (haplotype, strand, window) triples,
     // rescored by a kernel after the scan (launch_post_scan)

@@ -360,7 +360,13 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
             hn += (uint32_t)__popcll(act);
         }
     }
-    if (lane == 0) A.hitn[(size_t)slot * kMBlockWaves + wave] = min(hn, cap);
+    if (lane == 0) {
+        A.hitn[(size_t)slot * kMBlockWaves + wave] = min(hn, cap);
+        // the step's list counters (tfbs_ctx_scan_counters): one vector atomic each per wave
+        atomicAdd(A.over + 2, cn);
+        atomicAdd(A.over + 3, cn > lcap ? min(cn, lcap + cap) - lcap : 0u);
+        atomicAdd(A.over + 4, min(hn, cap));
+    }
 }
 
 // Coarse test of one tile: OR of the lane's 16 outputs, the fields' top bits

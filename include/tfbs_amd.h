@@ -144,6 +144,11 @@ float tfbs_ctx_last_mfma_ms(const tfbs_ctx *ctx);
  * entries[c] = windows depth class c (0: strands of 1-2 K chunks, 1: 3-4) reads,
  * *seconds = the build's wall time.  Zeros before an upload or without MFMA strands. */
 int tfbs_ctx_window_lists(const tfbs_ctx *ctx, uint64_t entries[2], double *seconds);
+/* The last matrix-core scan's list counters (waits for it): out[0] spill records,
+ * out[1] candidates past the waves' lists (rescored by post_scan_kernel), out[2]
+ * candidates found, out[3] of them written to the waves' global lists (past the
+ * LDS ones), out[4] (haplotype, key) pairs in the hit lists.  Zeros without one. */
+int tfbs_ctx_scan_counters(tfbs_ctx *ctx, uint64_t out[5]);
 
 /* Replaces matches() (pattern.rs:141-171) for ONE haplotype against every
  * pattern, on the GPU.  nucs are codes 0..4, pos the NucleotidePos.pos values.

@@ -110,6 +110,11 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
         python3 -c "import json;q=json.load(open('$d/pmc_summary.json'));print('$w $v $name', {k: '%.4g' % v for k, v in q.items() if not k.startswith('_')})"
       done
       unset TFBS_LIB ;;
+    tl_*)  # tl_<W>: kernel + memory-copy trace of bench.py (graph-replayed steps), the last steps' timelines
+      w=${st#tl_}
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d $O/tl_$w -o tl --output-format csv -- python3 bench.py --workload $w --steps 12 --warmup 3 --no-cpu --no-e2e > $O/tl_$w.json 2> $O/tl_$w.err || { tail -20 $O/tl_$w.err; exit 1; }
+      kt=$(find $O/tl_$w -name '*kernel_trace.csv' | head -1); mt=$(find $O/tl_$w -name '*memory_copy_trace.csv' | head -1)
+      python3 tools/step_timeline.py $kt $mt 3 > $O/tl_$w.txt; cat $O/tl_$w.txt | head -60 ;;
     probe_scale)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 tools/probe/f4f6_scale.hip -o /tmp/f4f6_scale 2>/dev/null || exit 1
       timeout -k 10 60 /tmp/f4f6_scale > $O/probe_scale.txt 2>&1; rc=$?; cat $O/probe_scale.txt; [ $rc -eq 0 ] || exit $rc ;;
