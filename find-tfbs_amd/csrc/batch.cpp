@@ -1308,8 +1308,9 @@ int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const c
     return TFBS_OK;
 }
 
-int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
-                    const std::vector<uint32_t> &carriers, int gt_status, Record &r) {
+template <class V>
+static int record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt, V &&carriers, int gt_status,
+                      Record &r) {
     if (n_alleles < 2 || !alt) return fail(TFBS_E_ALLELES, "record with one allele (haplotype.rs:22)");
     if (!ref) return fail(TFBS_E_ARG, "null argument");
     r = Record();
@@ -1320,9 +1321,17 @@ int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const cha
     if (rc) return rc;
     if (n_alleles == 2) {
         if (gt_status) return fail(gt_status, "Inconsistent number of alleles");
-        r.carriers = carriers;
+        r.carriers = std::forward<V>(carriers);
     }
     return TFBS_OK;
+}
+int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                    const std::vector<uint32_t> &carriers, int gt_status, Record &r) {
+    return record_ids(pos, n_alleles, ref, alt, carriers, gt_status, r);
+}
+int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                    std::vector<uint32_t> &&carriers, int gt_status, Record &r) {
+    return record_ids(pos, n_alleles, ref, alt, std::move(carriers), gt_status, r);
 }
 
 // Builds regions on up to `threads` host threads, commits them in order.

@@ -260,6 +260,8 @@ int make_record_gt(uint32_t n_samples, uint64_t pos, uint32_t n_alleles, const c
 // make_record_gt would (after the allele count and the REF / ALT bases).
 int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
                     const std::vector<uint32_t> &carriers, int gt_status, Record &r);
+int make_record_ids(uint64_t pos, uint32_t n_alleles, const char *ref, const char *alt,
+                    std::vector<uint32_t> &&carriers, int gt_status, Record &r);  // (carriers moved in)
 
 // haplotype.rs:94-156 over a reference window given as codes for positions
 // [ref_start, ref_start + n_ref).  Diffs are pointers to records.

@@ -102,6 +102,7 @@ struct tfbs_ctx {
     DevBuf<uint8_t> slot_mfma;           // Plan::slot_mfma
     DevBuf<uint32_t> cands;              // matrix-core candidate lists (scan.hpp)
     DevBuf<uint32_t> hitl, hitn;         // matrix-core hit lists (scan.hpp)
+    DevBuf<uint32_t> candn;              // per wave: candidates found (tfbs_ctx_scan_counters)
     DevBuf<uint32_t> ref_hits, ref_count;  // reference-window reuse (scan.hpp)
     DevBuf<uint32_t> spill, over;        // spill records, [0] their count, [1] candidates past the wave lists
     uint32_t spill_cap = 1u << 16;
@@ -216,8 +217,10 @@ struct tfbs_ctx {
     double rows_s[2] = {0, 0};            // tfbs_batch_rows_bgzf seconds: row plan (host), the rest
     double drain_s[3] = {0, 0, 0};        // of rows_s[1]: bgzf_drain's waits for the blocks, the copy back, the write
     // rows_set_async (the run flow's one-device path): a drained slot's blocks are
-    // written by this ctx's writer thread, in order, while the caller goes on; the slot's
-    // host buffer is reused once its write is done (rows_flush: every write done)
+    // copied back and written by this ctx's writer thread, in order, while the caller
+    // goes on; the slot's device buffers are reused once its copy is enqueued (the
+    // stream waits for bg_copied), its host buffer once its write is done (rows_flush:
+    // every write done)
     struct RowsWriter {
         std::thread th;
         std::mutex mu;
@@ -227,11 +230,12 @@ struct tfbs_ctx {
             uint64_t n;
         };
         std::deque<Job> q;
-        bool busy[3] = {false, false, false};
+        bool busy[3] = {false, false, false};      // a job of the slot is queued or running
+        bool recorded[3] = {false, false, false};  // its copy back is enqueued (bg_copied[k] recorded)
         bool stop = false;
         int rc = 0;
         std::string err;
-        double write_s = 0;
+        double copy_s = 0, write_s = 0;
     } rw;
     bool rows_async = false;
     uint64_t rows_text_last = 0;          // the last call's uncompressed row bytes
@@ -258,6 +262,9 @@ struct tfbs_ctx {
     uint32_t prev_cand = UINT32_MAX;                           // and its scan's candidates past the lists
     bool asm_wide = true, asm_leftover = true;                 // what the enqueued assembly launched
     bool asm_full = false;                                     // (a rerun: everything)
+    // fused post-scan (ScanArgs::post_done): tfbs_step allows it for its lean steps
+    // (TFBS_POST_FUSE=0: never); post_fused: the last scan did it (its assembly skips the launch)
+    bool post_fuse_env = true, post_fuse_ok = false, post_fused = false;
 };
 
 namespace tfbs {
@@ -428,16 +435,17 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
                                       : ctx->cand_cap;
         int rc;
         if ((rc = ctx->cands.ensure(n_wg * cand_cap * kCandWords)) || (rc = ctx->hitl.ensure(n_wg * cand_cap * 2)) ||
-            (rc = ctx->hitn.ensure(n_wg * (kMBlockWaves))))
+            (rc = ctx->hitn.ensure(n_wg * (kMBlockWaves))) || (rc = ctx->candn.ensure(n_wg * (kMBlockWaves))))
             return rc;
         m.cands = ctx->cands.p;
         m.cand_cap = cand_cap;
         ctx->scan_cand_cap = cand_cap;
         m.hitl = ctx->hitl.p;
         m.hitn = ctx->hitn.p;
+        m.candn = ctx->candn.p;
         const uint32_t nr = std::max<uint32_t>(1, ctx->n_regions);
         if ((rc = ctx->ref_count.ensure(nr)) || (rc = ctx->ref_hits.ensure((size_t)nr * kRefPerRegion * 2)) ||
-            (rc = ctx->over.ensure(5)) || (rc = ctx->spill.ensure((size_t)ctx->spill_cap * 3)) ||
+            (rc = ctx->over.ensure(2)) || (rc = ctx->spill.ensure((size_t)ctx->spill_cap * 3)) ||
             (rc = ctx->cand_over.ensure((size_t)ctx->cand_over_cap * 3)) ||
             (rc = ctx->spill_sorted.ensure((size_t)ctx->spill_cap * 3)) || (rc = ctx->spill_bcnt.ensure(nr + 1)) ||
             (rc = ctx->spill_boff.ensure(nr + 1)))
@@ -471,9 +479,25 @@ static int launch_scan(tfbs_ctx *ctx, uint32_t n_haps, unsigned long long *hits,
             const uint32_t na = (uint32_t)(kAsmCtrWords + nr + 1);
             if ((rc = ctx->asm_ctr.ensure(na))) return rc;
             hipLaunchKernelGGL(zero3_kernel, dim3(std::min<uint32_t>(256, (std::max(na, nr) + 255) / 256)), dim3(256), 0,
-                               ctx->stream, ctx->ref_count.p, nr, ctx->over.p, 5u, ctx->asm_ctr.p, na);
+                               ctx->stream, ctx->ref_count.p, nr, ctx->over.p, 2u, ctx->asm_ctr.p, na);
             HIP_TRY(hipGetLastError());
             ctx->asm_ctr_zeroed = true;  // (for this scan's first assembly)
+        }
+        // the post-scan work in the scan's last workgroup when the assembly that follows
+        // (tfbs_step) would launch it lean: neither the grid-wide bucketing nor overflow
+        // candidates last time (it handles both anyway: too many spill records set
+        // need_wide, and the assembly reruns with the wide kernels)
+        ctx->post_fused = ctx->post_fuse_ok && ctx->post_fuse_env && ctx->mfma_merged && ctx->asm_lean_mode != 0 &&
+                          !ctx->asm_full && (ctx->asm_lean_mode == 2 || ctx->prev_spill <= kPostSerial) &&
+                          ctx->prev_cand == 0;
+        if (ctx->post_fused) {
+            m.post_done = ctx->asm_ctr.p + 21;
+            m.post_regions = nr;
+            m.post_bcnt = ctx->asm_ctr.p + kAsmCtrWords;
+            m.post_boff = ctx->spill_boff.p;
+            m.post_sorted = ctx->spill_sorted.p;
+            m.post_report = ctx->asm_ctr.p;
+            m.post_need_wide = ctx->asm_ctr.p + 20;
         }
         if (!ctx->capturing) HIP_TRY(hipEventRecord(ctx->evk0, ctx->stream));
         // one stream per depth launch (launch_mfma: one per K depth), side streams
@@ -684,7 +708,7 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     ctx->fast_units.release(); ctx->gen_pats.release(); ctx->fast_tiles.release(); ctx->gen_tiles.release();
     ctx->lut.release(); ctx->wfull.release(); ctx->gen_w.release(); ctx->slot_mfma.release();
     ctx->m_image.release(); ctx->m_weights.release(); ctx->m_meta.release(); ctx->m_supers.release();
-    ctx->cands.release(); ctx->hitl.release(); ctx->hitn.release(); ctx->cand_over.release(); ctx->ref_hits.release();
+    ctx->cands.release(); ctx->hitl.release(); ctx->hitn.release(); ctx->candn.release(); ctx->cand_over.release(); ctx->ref_hits.release();
     ctx->ref_count.release(); ctx->spill.release(); ctx->over.release(); ctx->spill_sorted.release();
     ctx->spill_bcnt.release(); ctx->spill_boff.release(); ctx->srcs.release();
     if (ctx->over_host) (void)hipHostFree(ctx->over_host);
@@ -764,6 +788,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;
     ctx->asm_lean_mode = env_int("TFBS_ASM_LEAN", 1);
+    ctx->post_fuse_env = env_int("TFBS_POST_FUSE", 1) != 0;
     ctx->step_graphs = env_int("TFBS_STEP_GRAPH", 1) != 0 && !getenv("TFBS_SCAN_PROF") && !ctx->kf_prof_on &&
                        !ctx->debug_over;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));
@@ -878,12 +903,23 @@ int tfbs_ctx_rows_bgzf_seconds(const tfbs_ctx *ctx, double *out) {
 int tfbs_ctx_scan_counters(tfbs_ctx *ctx, uint64_t out[5]) {
     if (!ctx || !out) return tfbs::fail(TFBS_E_ARG, "null argument");
     for (int i = 0; i < 5; i++) out[i] = 0;
-    if (!ctx->over.p || ctx->over.n < 5) return TFBS_OK;
+    if (!ctx->over.p || !ctx->candn.p || !ctx->hitn.p || !ctx->scan_cand_cap) return TFBS_OK;
     HIP_TRY(hipSetDevice(ctx->device));
-    uint32_t h[5];
+    const size_t nw = std::min(ctx->hitn.n, ctx->candn.n);
+    std::vector<uint32_t> hn(nw), cn(nw);
+    uint32_t ov[2];
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipMemcpy(h, ctx->over.p, sizeof h, hipMemcpyDeviceToHost));
-    for (int i = 0; i < 5; i++) out[i] = h[i];
+    HIP_TRY(hipMemcpy(hn.data(), ctx->hitn.p, nw * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(cn.data(), ctx->candn.p, nw * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ov, ctx->over.p, sizeof ov, hipMemcpyDeviceToHost));
+    const uint64_t cap = ctx->scan_cand_cap / kMBlockWaves, lcap = std::min<uint64_t>(cap, kMWaveCands);
+    out[0] = ov[0];
+    out[1] = ov[1];
+    for (size_t i = 0; i < nw; i++) {  // (the waves of every workgroup the last scan launched)
+        out[2] += cn[i];
+        out[3] += cn[i] > lcap ? std::min<uint64_t>(cn[i], lcap + cap) - lcap : 0;
+        out[4] += hn[i];
+    }
     return TFBS_OK;
 }
 
@@ -1049,13 +1085,17 @@ static int enqueue_assembly(tfbs_ctx *ctx, Batch &B, bool post) {
     if (mfma && post) {  // overflow candidates rescored (once per scan: they append spill records) + spill buckets
         // (without the leftover pass post_scan_kernel copies the overflow counters to
         // asm_ctr[0, 2); asm_ctr[20]: set when the records needed the wide kernels)
-        if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18, std::max<uint32_t>(1, nr),
-                                    ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p, ctx->spill_sorted.p,
-                                    ctx->stream, ctx->asm_wide, ctx->asm_ctr.p, ctx->asm_ctr.p + 20,
-                                    lean && ctx->prev_cand == 0 ? 1u : 256u)))
+        if (ctx->post_fused) {  // the scan's last workgroup did it (lean: no wide kernels)
+            ctx->asm_wide = false;
+        } else if ((rc = launch_post_fused(ctx->last_margs, !ctx->post_done, ctx->asm_ctr.p + 18,
+                                           std::max<uint32_t>(1, nr), ctx->asm_ctr.p + kAsmCtrWords, ctx->spill_boff.p,
+                                           ctx->spill_sorted.p, ctx->stream, ctx->asm_wide, ctx->asm_ctr.p,
+                                           ctx->asm_ctr.p + 20, lean && ctx->prev_cand == 0 ? 1u : 256u))) {
             return rc;
+        }
         ctx->post_done = true;
     }
+    ctx->post_fused = false;
     AsmArgs a = asm_args(ctx, B, 0);
     a.key_first = ctx->key_first.p;
     a.key_flags = ctx->key_flags.p;
@@ -1303,7 +1343,7 @@ static uint64_t step_signature(const tfbs_ctx *ctx, const tfbs_batch *b) {
     mix((uint64_t)(uintptr_t)b);
     mix((uint64_t)(uintptr_t)ctx->resident);
     mix(ctx->upload_gen);
-    buf(ctx->cands); buf(ctx->hitl); buf(ctx->hitn); buf(ctx->ref_hits); buf(ctx->ref_count); buf(ctx->spill);
+    buf(ctx->cands); buf(ctx->hitl); buf(ctx->hitn); buf(ctx->candn); buf(ctx->ref_hits); buf(ctx->ref_count); buf(ctx->spill);
     buf(ctx->over); buf(ctx->spill_sorted); buf(ctx->spill_bcnt); buf(ctx->spill_boff); buf(ctx->cand_over);
     buf(ctx->srcs); buf(ctx->words); buf(ctx->nmask); buf(ctx->counts); buf(ctx->posrel); buf(ctx->inner);
     buf(ctx->haps); buf(ctx->druns); buf(ctx->gnarrow); buf(ctx->gorder); buf(ctx->hd); buf(ctx->hd2); buf(ctx->regions);
@@ -1351,7 +1391,10 @@ int tfbs_step(tfbs_ctx *ctx, tfbs_batch *b) {
     Batch &B = b->b;
     auto plain = [&]() -> int {
         int rc;
-        if ((rc = tfbs_scan(ctx, b)) || (rc = tfbs_batch_assemble(ctx, b))) return rc;
+        ctx->post_fuse_ok = true;  // (the assembly follows the scan at once)
+        rc = tfbs_scan(ctx, b);
+        ctx->post_fuse_ok = false;
+        if (rc || (rc = tfbs_batch_assemble(ctx, b))) return rc;
         return TFBS_OK;
     };
     auto drop = [&]() {
@@ -1739,12 +1782,34 @@ static void rows_writer_loop(tfbs_ctx *ctx) {
             std::lock_guard<std::mutex> l(w.mu);
             rc = w.rc;  // (after a failed write the rest are dropped)
         }
+        // the copy back (the main thread waits for its event to be recorded before it
+        // launches into the slot again), then the write; TFBS_ROWS_WRITER_DELAY_US: a
+        // pause first (tests: the caller runs ahead of the copies)
+        const int delay_us = env_int("TFBS_ROWS_WRITER_DELAY_US", 0);
+        if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
+        hipError_t he = hipSetDevice(ctx->device);
+        if (!rc && (rc = ctx->bg_host[j.k].reserve(std::max<uint64_t>(j.n, 1)))) err = tfbs_last_error();
+        if (!rc && he == hipSuccess && j.n)
+            he = hipMemcpyAsync(ctx->bg_host[j.k].p, ctx->bg_packed[j.k].p, j.n, hipMemcpyDeviceToHost, ctx->copy_stream);
+        if (he == hipSuccess) he = hipEventRecord(ctx->bg_copied[j.k], ctx->copy_stream);
+        {
+            std::lock_guard<std::mutex> l(w.mu);
+            w.recorded[j.k] = true;  // (also on failure: the stream's wait must not block)
+        }
+        w.cv.notify_all();
+        if (he == hipSuccess) he = hipEventSynchronize(ctx->bg_copied[j.k]);
+        if (!rc && he != hipSuccess) {
+            rc = TFBS_E_HIP;
+            err = std::string("rows copy back: ") + hipGetErrorString(he);
+        }
+        const double tc = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
         if (!rc && (rc = write_out(j.fd, reinterpret_cast<const char *>(ctx->bg_host[j.k].p), j.n))) err = tfbs_last_error();
         const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
         {
             std::lock_guard<std::mutex> l(w.mu);
             w.busy[j.k] = false;
-            w.write_s += t1 - t0;
+            w.copy_s += tc - t0;
+            w.write_s += t1 - tc;
             if (rc && !w.rc) {
                 w.rc = rc;
                 w.err = err;
@@ -1754,13 +1819,13 @@ static void rows_writer_loop(tfbs_ctx *ctx) {
     }
 }
 
-// Waits until slot k's host buffer is free (async writes), or every queued write is
-// done (k < 0); the writer's first failure, if any.
-static int rows_wait(tfbs_ctx *ctx, int k) {
+// Waits until slot k's last job is done (k >= 0), until its copy back is enqueued
+// (recorded), or until every queued job is done (k < 0); the writer's first failure.
+static int rows_wait(tfbs_ctx *ctx, int k, bool recorded = false) {
     auto &w = ctx->rw;
     std::unique_lock<std::mutex> l(w.mu);
     w.cv.wait(l, [&] {
-        if (k >= 0) return !w.busy[k];
+        if (k >= 0) return !w.busy[k] || (recorded && w.recorded[k]);
         for (bool b : w.busy)
             if (b) return false;
         return w.q.empty();
@@ -1775,7 +1840,20 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
     const double t1 = now();
     const uint64_t total = ctx->bg_total_host[k];
     int r;
-    if (ctx->rw.th.joinable() && (r = rows_wait(ctx, k))) return r;  // slot k's last write is out
+    if (ctx->rows_async) {  // the writer thread copies it back and writes it (in order)
+        if (!ctx->rw.th.joinable()) ctx->rw.th = std::thread(rows_writer_loop, ctx);
+        if ((r = rows_wait(ctx, k))) return r;  // slot k's last job is done (its host buffer free)
+        {
+            std::lock_guard<std::mutex> l(ctx->rw.mu);
+            ctx->rw.busy[k] = true;
+            ctx->rw.recorded[k] = false;
+            ctx->rw.q.push_back({fd, k, total});
+        }
+        ctx->rw.cv.notify_all();
+        ctx->drain_s[0] += t1 - t0;
+        written += total;
+        return TFBS_OK;
+    }
     if ((r = ctx->bg_host[k].reserve(std::max<uint64_t>(total, 1)))) return r;
     if (total)
         HIP_TRY(hipMemcpyAsync(ctx->bg_host[k].p, ctx->bg_packed[k].p, total, hipMemcpyDeviceToHost, ctx->copy_stream));
@@ -1785,16 +1863,6 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
     ctx->drain_s[0] += t1 - t0;
     ctx->drain_s[1] += t2 - t1;
     written += total;
-    if (ctx->rows_async) {  // the writer thread takes it (in order)
-        if (!ctx->rw.th.joinable()) ctx->rw.th = std::thread(rows_writer_loop, ctx);
-        {
-            std::lock_guard<std::mutex> l(ctx->rw.mu);
-            ctx->rw.busy[k] = true;
-            ctx->rw.q.push_back({fd, k, total});
-        }
-        ctx->rw.cv.notify_all();
-        return TFBS_OK;
-    }
     if ((r = write_out(fd, reinterpret_cast<const char *>(ctx->bg_host[k].p), total))) return r;  // the blocks as they are
     ctx->drain_s[2] += now() - t2;
     return TFBS_OK;
@@ -1912,12 +1980,25 @@ int rows_bgzf_device(tfbs_ctx *ctx, const Batch &B, tfbs::RowPlan &plan, std::ve
         const int k = (int)(pp.next % tfbs_ctx::kBgSlots);
         const uint64_t b0 = i * kBatchBlocks;
         const uint32_t nb = (uint32_t)std::min(kBatchBlocks, n_blocks - b0);
+        if (ctx->rw.th.joinable()) {
+            // async rows: slot k's last copy back -- of this call or of an earlier one, which
+            // returned before its copies ran -- must be enqueued by the writer thread before
+            // the stream may wait for it (below), and done before the slot's buffers grow
+            // (a reallocation under a pending copy sent zeros to the file)
+            const bool grows = ctx->bg_out[k].cap < (size_t)nb * kBgzfMax || ctx->bg_packed[k].cap < (size_t)nb * kBgzfMax ||
+                               ctx->bg_out_len[k].cap < nb || ctx->bg_off[k].cap < (size_t)nb + 1;
+            if ((rc = rows_wait(ctx, k, !grows))) return rc;
+        }
         if ((rc = ctx->bg_out[k].ensure((size_t)nb * kBgzfMax)) || (rc = ctx->bg_out_len[k].ensure(nb)) ||
             (rc = ctx->bg_off[k].ensure(nb + 1)) || (rc = ctx->bg_packed[k].ensure((size_t)nb * kBgzfMax)) ||
             (rc = ctx->bg_plans.ensure((size_t)nb * tfbs::bgzf_plan_bytes())))
             return rc;
         // slot k's packed blocks were copied back (kBgSlots batches ago) before they are overwritten
-        if (pp.next >= (uint64_t)tfbs_ctx::kBgSlots) HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+        if (ctx->rw.th.joinable()) {  // (waited for above)
+            HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+        } else if (pp.next >= (uint64_t)tfbs_ctx::kBgSlots) {  // (an earlier call's copies are done)
+            HIP_TRY(hipStreamWaitEvent(ctx->stream, ctx->bg_copied[k], 0));
+        }
         a.plans = ctx->bg_plans.p;
         a.block0 = b0;
         a.out = ctx->bg_out[k].p;
@@ -1956,7 +2037,10 @@ namespace tfbs {
 
 void rows_bgzf_drain_seconds(const ::tfbs_ctx *ctx, double out[3]) {
     for (int i = 0; i < 3; i++) out[i] = ctx ? ctx->drain_s[i] : 0.0;
-    if (ctx) out[2] += const_cast<::tfbs_ctx *>(ctx)->rw.write_s;  // (read after rows_flush)
+    if (ctx) {  // (the writer thread's, read after rows_flush)
+        out[1] += ctx->rw.copy_s;
+        out[2] += ctx->rw.write_s;
+    }
 }
 
 void rows_set_async(::tfbs_ctx *ctx, bool on) {

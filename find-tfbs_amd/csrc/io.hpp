@@ -137,6 +137,13 @@ class Bcf {
     // records with pos < end && pos + rlen > beg, in file order; pointers stay
     // valid until the next fetch
     int fetch(int contig, uint64_t beg, uint64_t end, std::vector<const BcfRecord *> &out);
+    // The records of the last fetch that no later fetch from beg_next on can return
+    // (pos + rlen <= beg_next): their carriers may be moved out (the run flow's fetch
+    // stage, which knows its next region), the others are copied.
+    bool dropped_before(const BcfRecord *r, uint64_t beg_next) const { return r->pos + r->rlen <= beg_next; }
+    std::vector<uint32_t> take_carriers(const BcfRecord *r) {
+        return std::move(const_cast<BcfRecord *>(r)->carriers);  // (r is one of this reader's window)
+    }
     ~Bcf();
     std::vector<std::string> samples, contigs;
 

@@ -92,6 +92,7 @@ struct Shard {
     double t_create = 0;                 // of t_prep: tfbs_batch_create
     double rows_plan = 0, rows_dev = 0;  // of t_rows: host row plans, device blocks + copy back + write
     double drain[3] = {0, 0, 0};         // of rows_dev: waits for the device's blocks, their copy back, the writes
+    double t_setup = 0, t_boot = 0, t_end = 0;  // readers + ctx + grouper; the first batches' stages; flush + ctx release
 };
 
 struct RunSetup {
@@ -113,6 +114,7 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     using namespace tfbs;
     const tfbs_run_args *a = S.a;
     if (sh.batches.empty()) return TFBS_OK;
+    const double t_in = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
     Bcf bcf;
     int rc = bcf.open(a->bcf, sh.threads);
     if (rc) return rc;
@@ -121,24 +123,45 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     const int rid = bcf.contig_index(S.chrom);
     Fasta fasta;
     if ((rc = fasta.open(a->reference))) return rc;
+    // The device side -- the ctx (plan tables, streams) and the grouper that groups
+    // SNV-only regions on this device (haplotype.rs:16-88 on the GPU; one for the
+    // shard's batches, its membership rows recycled batch to batch; TFBS_RUN_BUILD_DEVICE=0:
+    // every region on the host) -- is made on a helper thread while the first batch's
+    // inputs are fetched.
     tfbs_ctx *ctx = nullptr;
-    if ((rc = tfbs_ctx_create(sh.device, S.pp, &ctx))) return rc;
-    if ((rc = tfbs_ctx_set_host_threads(ctx, sh.threads))) {
-        tfbs_ctx_destroy(ctx);
-        return rc;
-    }
-    std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(ctx, tfbs_ctx_destroy);
-    // one device writing straight to the output: its rows' writes go out on the ctx's
-    // writer thread while the next batch runs (flushed below, joined by the ctx's destroy)
-    if (out.device_rows && out.async_rows) rows_set_async(ctx, true);
-    // SNV-only regions grouped on this device (haplotype.rs:16-88 on the GPU), one
-    // grouper for the shard's batches (its membership rows recycled batch to batch);
-    // TFBS_RUN_BUILD_DEVICE=0: every region on the host
     std::shared_ptr<DevGrouper> grouper;
-    if (!(getenv("TFBS_RUN_BUILD_DEVICE") && atoi(getenv("TFBS_RUN_BUILD_DEVICE")) == 0)) {
-        grouper.reset(make_gpu_grouper(sh.device));
-        if (!grouper) return TFBS_E_NODEVICE;
-    }
+    int dev_rc = TFBS_OK;
+    std::string dev_err;
+    std::thread dev_setup([&] {
+        int r = tfbs_ctx_create(sh.device, S.pp, &ctx);
+        if (!r) r = tfbs_ctx_set_host_threads(ctx, sh.threads);
+        if (!r && !(getenv("TFBS_RUN_BUILD_DEVICE") && atoi(getenv("TFBS_RUN_BUILD_DEVICE")) == 0)) {
+            grouper.reset(make_gpu_grouper(sh.device));
+            if (!grouper) r = fail(TFBS_E_NODEVICE, "no device for the grouper");
+        }
+        if (r) dev_err = tfbs_last_error();
+        dev_rc = r;
+    });
+    struct DevGuard {  // every exit: the helper joined, a ctx not handed to cguard released
+        std::thread &t;
+        tfbs_ctx *&c;
+        bool owned = false;
+        ~DevGuard() {
+            if (t.joinable()) t.join();
+            if (!owned && c) tfbs_ctx_destroy(c);
+        }
+    } dev_guard{dev_setup, ctx};
+    std::unique_ptr<tfbs_ctx, void (*)(tfbs_ctx *)> cguard(nullptr, tfbs_ctx_destroy);
+    auto dev_ready = [&]() -> int {
+        dev_setup.join();
+        if (dev_rc) return fail(dev_rc, dev_err);
+        cguard.reset(ctx);
+        dev_guard.owned = true;
+        // one device writing straight to the output: its rows' writes go out on the ctx's
+        // writer thread while the next batch runs (flushed below, joined by the ctx's destroy)
+        if (out.device_rows && out.async_rows) rows_set_async(ctx, true);
+        return TFBS_OK;
+    };
     using BatchPtr = std::unique_ptr<tfbs_batch, void (*)(tfbs_batch *)>;
     std::vector<const BcfRecord *> recs;
     auto clock = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
@@ -172,7 +195,6 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
         if (rc) return err = tfbs_last_error(), rc;
         p.bp = BatchPtr(bb, tfbs_batch_destroy);
         Batch &B = bb->b;
-        B.grouper = grouper;
         for (auto &b : S.beds) B.beds.push_back(b.first);
         p.ins.clear();
         p.ins.reserve(b1 - b0);
@@ -223,10 +245,20 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
             t.fasta += tb - tf;
             if ((rc = bcf.fetch(rid, in.R.es, in.R.ee + 1, recs))) return err = tfbs_last_error(), rc;
             const double ti = clock();
+            // the next region of the batch starts at beg_next: a record it cannot return
+            // gives its carriers away instead of a copy
+            uint64_t beg_next = 0, ee_next = 0;
+            const bool has_next =
+                r + 1 < b1 && tfbs_batch_region_ext(bb, S.merged[r + 1].first, S.merged[r + 1].second, &beg_next,
+                                                    &ee_next) == TFBS_OK;
             for (const BcfRecord *br : recs) {
                 Record rec;
-                rc = make_record_ids(br->pos, br->n_alleles, br->ref.c_str(),
-                                     br->n_alleles >= 2 ? br->alt.c_str() : nullptr, br->carriers, br->gt_status, rec);
+                const char *alt = br->n_alleles >= 2 ? br->alt.c_str() : nullptr;
+                rc = has_next && bcf.dropped_before(br, beg_next)
+                         ? make_record_ids(br->pos, br->n_alleles, br->ref.c_str(), alt, bcf.take_carriers(br),
+                                           br->gt_status, rec)
+                         : make_record_ids(br->pos, br->n_alleles, br->ref.c_str(), alt, br->carriers, br->gt_status,
+                                           rec);
                 if (rc) return err = tfbs_last_error(), rc;
                 in.recs.push_back(std::move(rec));
             }
@@ -239,6 +271,7 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     };
     auto build = [&](Pending &p, std::string &err, Times &t) -> int {
         const double tb = clock();
+        p.bp->b.grouper = grouper;
         const int rc = add_regions(p.bp->b, p.ins, sh.threads);
         std::vector<RegionInput>().swap(p.ins);
         t.build += clock() - tb;
@@ -258,9 +291,15 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
     std::string err;
     {
         Times t;
-        if ((rc = fetch(sh.batches[0], cur, err, t)) || (rc = build(cur, err, t)) ||
-            (nb > 1 && (rc = fetch(sh.batches[1], nxt, err, t))))
-            return fail(rc, err);
+        if ((rc = fetch(sh.batches[0], cur, err, t))) return fail(rc, err);
+        if ((rc = dev_ready())) return rc;
+        sh.t_setup = now() - t_in;  // (readers, the first fetch, the device side: the longer)
+        const double tb0 = now();
+        struct Boot {
+            double &acc, t0;
+            ~Boot() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - t0; }
+        } boot{sh.t_boot, tb0};
+        if ((rc = build(cur, err, t)) || (nb > 1 && (rc = fetch(sh.batches[1], nxt, err, t)))) return fail(rc, err);
         account(t);
     }
     for (size_t bi = 0; bi < nb; bi++) {
@@ -309,6 +348,11 @@ int run_shard(const RunSetup &S, Shard &sh, Out &&out) {
         nxt = std::move(nxt2);
         nxt2 = Pending();
     }
+    const double te = now();
+    struct End {  // the flush and the ctx's release (cguard, after this)
+        double &acc, t0;
+        ~End() { acc += std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count() - t0; }
+    } end_t{sh.t_end, te};
     if ((rc = rows_flush(ctx))) return rc;
     double rs[2];
     if (tfbs_ctx_rows_bgzf_seconds(ctx, rs) == TFBS_OK) sh.rows_plan = rs[0], sh.rows_dev = rs[1];
@@ -721,12 +765,14 @@ int tfbs_run(const tfbs_run_args *a) {
                     "\"prep_s\": %.4f, \"prep_bcf_s\": %.4f, \"prep_build_s\": %.4f, \"prep_fasta_s\": %.4f, "
                     "\"prep_ids_s\": %.4f, \"bcf_read_s\": %.4f, \"bcf_inflate_s\": %.4f, \"bcf_scan_s\": %.4f, "
                     "\"bcf_ahead_wait_s\": %.4f, \"bcf_decode_s\": %.4f, \"prep_create_s\": %.4f, \"rows_plan_s\": %.4f, \"rows_dev_s\": %.4f, "
-                    "\"drain_gpu_s\": %.4f, \"drain_copy_s\": %.4f, \"drain_write_s\": %.4f, \"prep_wait_s\": %.4f, "
+                    "\"drain_gpu_s\": %.4f, \"drain_copy_s\": %.4f, \"drain_write_s\": %.4f, \"setup_s\": %.4f, \"boot_s\": %.4f, "
+                    "\"end_s\": %.4f, \"prep_wait_s\": %.4f, "
                     "\"gpu_s\": %.4f, \"rows_s\": %.4f, \"ordered_write_s\": %.4f, \"close_s\": %.4f, \"loop_s\": %.4f}\n",
                     k, shards[k].device, shards[k].regions, shards[k].batches.size(), shards[k].t_prep,
                     shards[k].t_bcf, shards[k].t_build, shards[k].t_fasta, shards[k].t_ids, shards[k].b_read,
                     shards[k].b_inflate, shards[k].b_scan, shards[k].b_wait, shards[k].b_decode, shards[k].t_create, shards[k].rows_plan,
                     shards[k].rows_dev, shards[k].drain[0], shards[k].drain[1], shards[k].drain[2],
+                    shards[k].t_setup, shards[k].t_boot, shards[k].t_end,
                     shards[k].t_wait, shards[k].t_gpu, shards[k].t_rows, t_write, t_close, now() - t_start);
     if (a->tabix) {
         const std::string cmd = "zcat '" + part + "' | bgzip > '" + out + "'; tabix -f -p vcf '" + out + "'; rm '" +

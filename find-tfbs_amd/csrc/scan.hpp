@@ -54,6 +54,7 @@ struct ScanArgs {
     // wave]; the excess goes to the spill list
     uint32_t *hitl;
     uint32_t *hitn;
+    uint32_t *candn;  // per wave (as hitn): the candidates it found (tfbs_ctx_scan_counters; no atomics)
     // matrix-core window lists (build_window_lists), per depth class (2, 4): the
     // windows the scan reads, haplotype-major, entry = window << 6 | the haplotype's
     // index in its group of haps_per_block (<= 64); haplotype h's entries start at
@@ -86,13 +87,20 @@ struct ScanArgs {
     // key), kind 1 a reference hit (strand, window) -- counted at over[0] (of
     // spill_cap), bucketed by region after the scan (launch_spill_buckets)
     uint32_t *spill;
-    uint32_t *over;  // [0] spill records, [1] candidates past a wave's list; counters: [2] candidates,
-                     // [3] of them in the waves' global lists, [4] hit-list pairs
+    uint32_t *over;  // [0] spill records, [1] candidates past a wave's list
     uint32_t spill_cap;
     // candidates past a wave's list region: (haplotype, strand, window) triples,
     // rescored by a kernel after the scan (launch_post_scan)
     uint32_t *cand_over;
     uint32_t cand_over_cap;
+    // fused post-scan (tfbs_step's lean steps): scan_mfma_all_kernel's last workgroup to
+    // finish (ticket post_done) does post_scan_kernel's work -- the overflow candidates'
+    // rescoring, the overflow counters to post_report, the spill records bucketed by
+    // region (post_need_wide set when they are too many) -- instead of a launch after
+    // the scan; post_done null: no fusion
+    uint32_t *post_done;
+    uint32_t post_regions;
+    uint32_t *post_bcnt, *post_boff, *post_sorted, *post_report, *post_need_wide;
     // TFBS_SCAN_PROF builds of scan_mfma.hip (tools/variant_build.sh): per wave of
     // workgroup region_base + blockIdx.x, kScanProfWords clock stamps and counts
     // (tools/scan_prof.py); null otherwise
@@ -121,6 +129,7 @@ struct HitSrc {
     uint32_t wg_base, ns, g0, ng;
 };
 constexpr int kMaxHitSrcs = 64;
+constexpr uint32_t kMWaveCands = 48;  // a scan wave's candidates kept in LDS before its global list
 // Matrix-core scan (scan_mfma.hip): sparse hits (hitl / hitn / spill), no counts.
 // group_words: the most packed words any haplotype group of haps_per_block spans.
 // One launch per K depth, spread round-robin over `streams` (deepest first);

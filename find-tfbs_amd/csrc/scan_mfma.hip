@@ -175,7 +175,7 @@ __device__ __forceinline__ v16f mfma_chunk(const v4i &a, const BFrag &f, const v
 // round is scored again (no accumulator live across a drain).  The wave rescores its
 // candidates after the scan (rescore_list).
 constexpr uint32_t kMQueue = 64;      // records per wave (>= one tile's 64 firing lanes)
-constexpr uint32_t kWaveCands = 48;   // LDS candidates per wave (C3: 66 mean; the rest in the global list)
+constexpr uint32_t kWaveCands = kMWaveCands;  // LDS candidates per wave (C3: 66 mean; the rest in the global list)
 __shared__ uint4 s_qdata[kMBlock / 64][kMQueue];
 __shared__ uint2 s_qmeta[kMBlock / 64][kMQueue];
 __shared__ uint2 s_cand[kMBlock / 64][kWaveCands];
@@ -362,10 +362,9 @@ __device__ __forceinline__ void rescore_list(const ScanArgs &A, const uint32_t *
     }
     if (lane == 0) {
         A.hitn[(size_t)slot * kMBlockWaves + wave] = min(hn, cap);
-        // the step's list counters (tfbs_ctx_scan_counters): one vector atomic each per wave
-        atomicAdd(A.over + 2, cn);
-        atomicAdd(A.over + 3, cn > lcap ? min(cn, lcap + cap) - lcap : 0u);
-        atomicAdd(A.over + 4, min(hn, cap));
+        // (the list counters: per-wave stores summed on the host -- one atomic per wave on a
+        // shared counter serialises at L2, ~10 ns each, and doubled the C3 step)
+        A.candn[(size_t)slot * kMBlockWaves + wave] = cn;
     }
 }
 
@@ -854,6 +853,15 @@ __global__ __launch_bounds__(kMBlock, kMfmaMinWaves[NK]) void scan_mfma_kernel(S
 // candidates of all of them once at the end -- the per-workgroup costs (staging,
 // the rescoring's dependent loads) are paid once per group instead of once per
 // super tile.  LDS: one-hot table | the largest image | (STAGED) words.
+}  // namespace
+// post_scan_kernel's work by one workgroup of NT threads (defined below); s_sum: NT + 1
+// words of LDS
+template <uint32_t NT>
+__device__ void post_one_block(const ScanArgs &A, uint32_t tid, uint32_t n_regions, uint32_t *__restrict__ bcnt,
+                               uint32_t *__restrict__ boff, uint32_t *__restrict__ sorted,
+                               uint32_t *__restrict__ report, uint32_t *__restrict__ need_wide, uint32_t *s_sum);
+namespace {
+
 template <bool STAGED>
 __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
 #ifdef TFBS_SCAN_PROF
@@ -915,6 +923,20 @@ __global__ __launch_bounds__(kMBlock, 4) void scan_mfma_all_kernel(ScanArgs A) {
 #ifdef TFBS_ROUND_PROF
     for (int k = 0; k < 8; k++) SCAN_STAMP(8 + k, s_rprof[wave][k]);
 #endif
+    if (A.post_done) {  // fused post-scan: the last workgroup to finish does it
+        __syncthreads();  // every wave's lists and spill records are written
+        uint32_t *s_t = reinterpret_cast<uint32_t *>(&s_qdata[0][0]);  // (the queues are empty now)
+        if (threadIdx.x == 0) {
+            __threadfence();  // (release: this workgroup's records)
+            s_t[0] = atomicAdd(A.post_done, 1u) == gridDim.x - 1 ? 1u : 0u;
+        }
+        __syncthreads();
+        if (s_t[0]) {
+            __threadfence();  // (acquire: every workgroup's records)
+            post_one_block<kMBlock>(A, threadIdx.x, A.post_regions, A.post_bcnt, A.post_boff, A.post_sorted,
+                                    A.post_report, A.post_need_wide, s_t + 4);
+        }
+    }
 }
 
 // Candidates past the waves' lists (drain_queue), one per thread; their
@@ -1083,15 +1105,16 @@ constexpr uint32_t kPostBlock = 256;
 // kPostBlock threads) -- each thread a run of consecutive buckets, one block scan of
 // the runs' sums (not one per 256 buckets: 10 000 regions took 40 scans of 16
 // barriers); the counts are zeroed for the scatter's fill counters
+template <uint32_t NT = kPostBlock>
 __device__ void spill_bucket_offsets(uint32_t tid, uint32_t n_regions, uint32_t *__restrict__ bcnt,
                                      uint32_t *__restrict__ boff, uint32_t *s_sum) {
-    const uint32_t per = (n_regions + kPostBlock) / kPostBlock;  // ceil((n_regions + 1) / kPostBlock)
+    const uint32_t per = (n_regions + NT) / NT;  // ceil((n_regions + 1) / NT)
     const uint32_t i0 = min(tid * per, n_regions + 1), i1 = min(i0 + per, n_regions + 1);
     uint32_t mine = 0;
     for (uint32_t i = i0; i < i1; i++) mine += i < n_regions ? bcnt[i] : 0u;
     s_sum[tid] = mine;
     __syncthreads();
-    for (uint32_t o = 1; o < kPostBlock; o <<= 1) {
+    for (uint32_t o = 1; o < NT; o <<= 1) {
         const uint32_t t = tid >= o ? s_sum[tid - o] : 0u;
         __syncthreads();
         s_sum[tid] += t;
@@ -1111,6 +1134,83 @@ __device__ void spill_bucket_offsets(uint32_t tid, uint32_t n_regions, uint32_t 
 // launched); need_wide (optional: the wide kernels are not launched): set when the
 // records are too many for the last workgroup, so that the host reruns the assembly
 // with them.
+// The overflow candidates' rescoring, block blk of nblk (NT threads): the hits' spill
+// records get their slots one atomic per wave (C5: ~120 000 records through one
+// counter, one atomic each, took ~1 ms); the loop is wave-uniform for the wave sum.
+template <uint32_t NT>
+__device__ void post_candidates(const ScanArgs &A, uint32_t tid, uint32_t blk, uint32_t nblk) {
+    const uint32_t n = min(A.over[1], A.cand_over_cap), lane = tid & 63;
+    for (uint32_t k0 = blk * NT; k0 < n; k0 += nblk * NT) {
+        const uint32_t k = k0 + tid;
+        uint32_t m = 0, key0 = 0, region = 0, hap = 0;
+        if (k < n) {
+            hap = A.cand_over[3 * (size_t)k];
+            const uint32_t g = A.cand_over[3 * (size_t)k + 1];
+            const DevHap hp = A.haps[hap];
+            region = hp.region;
+            m = score_candidate(A, A.words, CandHap::of(hp), hap, g, A.cand_over[3 * (size_t)k + 2], &key0);
+        }
+        const uint32_t c = (uint32_t)__builtin_popcount(m);
+        uint32_t inc = c;
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
+            if (lane >= o) inc += t;
+        }
+        const uint32_t total = (uint32_t)__shfl((int)inc, 63);
+        uint32_t base = 0;
+        if (lane == 0 && total) base = atomicAdd(A.over, total);
+        uint32_t at = (uint32_t)__shfl((int)base, 0) + inc - c;
+        for (; m; m &= m - 1, at++)
+            if (at < A.spill_cap) {
+                A.spill[3 * (size_t)at] = region;
+                A.spill[3 * (size_t)at + 1] = hap;
+                A.spill[3 * (size_t)at + 2] = key0 + __builtin_ctz(m);
+            }
+    }
+}
+
+// The last workgroup's part (every workgroup's spill records visible): the overflow
+// counters to report, then the records bucketed by region when they are few.
+template <uint32_t NT>
+__device__ void post_buckets(const ScanArgs &A, uint32_t tid, uint32_t n_regions, uint32_t *__restrict__ bcnt,
+                             uint32_t *__restrict__ boff, uint32_t *__restrict__ sorted,
+                             uint32_t *__restrict__ report, uint32_t *__restrict__ need_wide, uint32_t *s_sum) {
+    if (report && tid < 2) report[tid] = __atomic_load_n(A.over + tid, __ATOMIC_RELAXED);
+    const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
+    if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
+    if (n > kPostSerial) {  // spill_hist_wide_kernel + spill_scatter_wide_kernel's
+        if (need_wide && tid == 0) *need_wide = 1u;
+        return;
+    }
+    for (uint32_t e = tid; e < n; e += NT) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
+    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
+    __syncthreads();
+    spill_bucket_offsets<NT>(tid, n_regions, bcnt, boff, s_sum);
+    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
+    __syncthreads();
+    for (uint32_t e = tid; e < n; e += NT) {
+        const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
+        const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
+        sorted[3 * (size_t)at] = A.spill[3 * (size_t)e];
+        sorted[3 * (size_t)at + 1] = A.spill[3 * (size_t)e + 1];
+        sorted[3 * (size_t)at + 2] = A.spill[3 * (size_t)e + 2];
+    }
+}
+
+template <uint32_t NT>
+__device__ void post_one_block(const ScanArgs &A, uint32_t tid, uint32_t n_regions, uint32_t *__restrict__ bcnt,
+                               uint32_t *__restrict__ boff, uint32_t *__restrict__ sorted,
+                               uint32_t *__restrict__ report, uint32_t *__restrict__ need_wide, uint32_t *s_sum) {
+    post_candidates<NT>(A, tid, 0, 1);
+    __threadfence();  // (its spill records, for the whole block)
+    __syncthreads();
+    post_buckets<NT>(A, tid, n_regions, bcnt, boff, sorted, report, need_wide, s_sum);
+}
+// (the merged scan kernel's tail, instantiated above this definition)
+template __device__ void post_one_block<kMBlock>(const ScanArgs &, uint32_t, uint32_t, uint32_t *, uint32_t *,
+                                                 uint32_t *, uint32_t *, uint32_t *, uint32_t *);
+
 __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint32_t cand, uint32_t *done,
                                                               uint32_t n_regions, uint32_t *__restrict__ bcnt,
                                                               uint32_t *__restrict__ boff,
@@ -1119,40 +1219,7 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
                                                               uint32_t *__restrict__ need_wide) {
     __shared__ uint32_t s_last, s_sum[kPostBlock];
     const uint32_t tid = threadIdx.x;
-    if (cand) {
-        // the hits' spill records get their slots one atomic per wave (C5: ~120 000
-        // records through one counter, one atomic each, took ~1 ms); the loop is
-        // wave-uniform for the wave sum
-        const uint32_t n = min(A.over[1], A.cand_over_cap), lane = tid & 63;
-        for (uint32_t k0 = blockIdx.x * kPostBlock; k0 < n; k0 += gridDim.x * kPostBlock) {
-            const uint32_t k = k0 + tid;
-            uint32_t m = 0, key0 = 0, region = 0, hap = 0;
-            if (k < n) {
-                hap = A.cand_over[3 * (size_t)k];
-                const uint32_t g = A.cand_over[3 * (size_t)k + 1];
-                const DevHap hp = A.haps[hap];
-                region = hp.region;
-                m = score_candidate(A, A.words, CandHap::of(hp), hap, g, A.cand_over[3 * (size_t)k + 2], &key0);
-            }
-            const uint32_t c = (uint32_t)__builtin_popcount(m);
-            uint32_t inc = c;
-#pragma unroll
-            for (uint32_t o = 1; o < 64; o <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)inc, o);
-                if (lane >= o) inc += t;
-            }
-            const uint32_t total = (uint32_t)__shfl((int)inc, 63);
-            uint32_t base = 0;
-            if (lane == 0 && total) base = atomicAdd(A.over, total);
-            uint32_t at = (uint32_t)__shfl((int)base, 0) + inc - c;
-            for (; m; m &= m - 1, at++)
-                if (at < A.spill_cap) {
-                    A.spill[3 * (size_t)at] = region;
-                    A.spill[3 * (size_t)at + 1] = hap;
-                    A.spill[3 * (size_t)at + 2] = key0 + __builtin_ctz(m);
-                }
-        }
-    }
+    if (cand) post_candidates<kPostBlock>(A, tid, blockIdx.x, gridDim.x);
     __syncthreads();
     if (tid == 0) {
         __threadfence();  // (release: this workgroup's spill records)
@@ -1161,26 +1228,7 @@ __global__ __launch_bounds__(kPostBlock) void post_scan_kernel(ScanArgs A, uint3
     __syncthreads();
     if (!s_last) return;
     __threadfence();  // (acquire: every workgroup's records)
-    if (report && tid < 2) report[tid] = __atomic_load_n(A.over + tid, __ATOMIC_RELAXED);
-    const uint32_t n = min(__atomic_load_n(A.over, __ATOMIC_RELAXED), A.spill_cap);
-    if (n == 0) return;  // no records: the readers skip the buckets (AsmArgs::spill_count)
-    if (n > kPostSerial) {  // spill_hist_wide_kernel + spill_scatter_wide_kernel's
-        if (need_wide && tid == 0) *need_wide = 1u;
-        return;
-    }
-    for (uint32_t e = tid; e < n; e += kPostBlock) atomicAdd(&bcnt[A.spill[3 * (size_t)e] & 0x7FFFFFFFu], 1u);
-    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
-    __syncthreads();
-    spill_bucket_offsets(tid, n_regions, bcnt, boff, s_sum);
-    __threadfence();  // (the counters' atomics and boff's stores seen by every thread of the block)
-    __syncthreads();
-    for (uint32_t e = tid; e < n; e += kPostBlock) {
-        const uint32_t r = A.spill[3 * (size_t)e] & 0x7FFFFFFFu;
-        const uint32_t at = boff[r] + atomicAdd(&bcnt[r], 1u);
-        sorted[3 * (size_t)at] = A.spill[3 * (size_t)e];
-        sorted[3 * (size_t)at + 1] = A.spill[3 * (size_t)e + 1];
-        sorted[3 * (size_t)at + 2] = A.spill[3 * (size_t)e + 2];
-    }
+    post_buckets<kPostBlock>(A, tid, n_regions, bcnt, boff, sorted, report, need_wide, s_sum);
 }
 
 // More than kPostSerial spill records: their bucket counts over the whole grid, then

@@ -618,6 +618,32 @@ def test_run_devices_shards_same_text(tmp_path, index):
     assert want.count("\n") > 10
 
 
+def test_run_async_rows_writer_same_text(tmp_path, monkeypatch):
+    """The one-device run flow hands each drained slot of BGZF blocks to the ctx's writer
+    thread (copy back + write, in order) and goes on with the next batch.  With the
+    writer held back (TFBS_ROWS_WRITER_DELAY_US) and two blocks per launch (every call
+    cycles the three slots, so the next call's launches meet slots whose copies have
+    not run yet, and a slot that held a one-block remainder grows under them) the output
+    equals the synchronous writes' (TFBS_RUN_ASYNC_WRITE=0)."""
+    import gzip
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path / "data"), n_samples=2000, n_regions=30, n_pwms=10,
+                                   length_config=2, seed=21, indel_pct=10)
+    args = ("chr1", d["bcf"], [d["bed"]], d["fasta"], None, d["pwm_file"], d["thr_dir"], 2e-3, d["names"])
+    monkeypatch.setenv("TFBS_BGZF_BATCH_BLOCKS", "2")
+    texts = []
+    for asyn, delay in ((0, 0), (1, 0), (1, 3000)):
+        monkeypatch.setenv("TFBS_RUN_ASYNC_WRITE", str(asyn))
+        monkeypatch.setenv("TFBS_ROWS_WRITER_DELAY_US", str(delay))
+        out = tmp_path / ("async%d.vcf.gz" % len(texts))
+        T.run(*args, str(out), threads=4, regions_per_batch=3)
+        texts.append(gzip.open(str(out), "rt").read())
+    assert texts[1] == texts[0] and texts[2] == texts[0]
+    assert texts[0].count("\n") > 20
+
+
 def test_cli_gpus_and_devices(tmp_path):
     """--gpus N / --devices LIST on the command line: same text as one device."""
     import gzip
