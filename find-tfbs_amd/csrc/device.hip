@@ -788,7 +788,7 @@ int tfbs_ctx_create(int device, const tfbs_patterns *p, tfbs_ctx **out) {
     ctx->kf_prof_on = env_int("TFBS_KF_PROF", 0) != 0;
     ctx->kf_persistent = env_int("TFBS_KF_PERSIST", 1) != 0;
     ctx->asm_lean_mode = env_int("TFBS_ASM_LEAN", 1);
-    ctx->post_fuse_env = env_int("TFBS_POST_FUSE", 1) != 0;
+    ctx->post_fuse_env = env_int("TFBS_POST_FUSE", 0) != 0;  // (measured: C2 0.083 vs 0.068 ms -- a ticket atomic per scan workgroup)
     ctx->step_graphs = env_int("TFBS_STEP_GRAPH", 1) != 0 && !getenv("TFBS_SCAN_PROF") && !ctx->kf_prof_on &&
                        !ctx->debug_over;
     ctx->key_fast_max_u = (uint32_t)std::max(0, env_int("TFBS_KEY_FAST_MAXU", 1 << 30));

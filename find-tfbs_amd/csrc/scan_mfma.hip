@@ -488,12 +488,16 @@ __device__ __forceinline__ void drain_queue(const ScanArgs &A, const GroupCtx &G
 // `which`, s_went) and g0 | lane (g0: the strand tile's first global strand) --;
 // qn (uniform) counts the wave's records.
 __device__ __forceinline__ void queue_tile(const ScanArgs &A, const GroupCtx &G, const v16f &acc, bool mine, uint64_t f,
-                                           uint32_t g0, uint32_t which, uint32_t lane, uint32_t wave, uint32_t &qn,
-                                           uint32_t &cn) {
+                                           uint32_t g0, uint32_t went, uint32_t which, uint32_t lane, uint32_t wave,
+                                           uint32_t &qn, uint32_t &cn) {
     const uint32_t nf = (uint32_t)__popcll(f);
     uint32_t ent = 0, x[4] = {0, 0, 0, 0};
     if (mine) {
+#ifdef TFBS_WENT_LDS  // (A/B: the round-6 first version's LDS copy of the pair's entries)
         ent = s_went[wave][which * 32 + (lane & 31)];
+#else
+        ent = went;  // the lane's own entry of tile `which` (lanes l and l + 32 load the same)
+#endif
         record_bits(acc, x);
     }
     if (__builtin_expect(qn + nf > kMQueue, 0)) {  // the queue is full (dense hits): decoded first
@@ -581,8 +585,8 @@ __shared__ unsigned long long s_rprof[kMBlock / 64][8];
 template <int D, int NK, bool TWO>
 __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img, uint32_t tb, uint32_t te,
                                              const GroupCtx &G, uint32_t lane, uint32_t wave, const v4i (&a0)[NK],
-                                             const v4i (&a1)[NK], uint32_t ta, const v16f &cb, int sa, uint32_t &qn,
-                                             uint32_t &cn) {
+                                             const v4i (&a1)[NK], uint32_t ta, uint32_t e0, uint32_t e1, const v16f &cb,
+                                             int sa, uint32_t &qn, uint32_t &cn) {
     constexpr uint32_t kTB = mfma_tile_bytes(D);
     const char *tile = img;
     const char *const end = img + (te - tb) * kTB;
@@ -633,8 +637,8 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
             // a tile's candidates at once when the queue is full
             const bool m0 = x0 != 0 && q0 < G.nw, m1 = TWO && x1 != 0 && q0 + kMWindows < G.nw;
             const uint64_t f0 = __ballot(m0), f1 = __ballot(m1);
-            if (f0) queue_tile(A, G, c0, m0, f0, g0, 0, lane, wave, qn, cn);
-            if (TWO && f1) queue_tile(A, G, c1, m1, f1, g0, 1, lane, wave, qn, cn);
+            if (f0) queue_tile(A, G, c0, m0, f0, g0, e0, 0, lane, wave, qn, cn);
+            if (TWO && f1) queue_tile(A, G, c1, m1, f1, g0, e1, 1, lane, wave, qn, cn);
         }
 #ifdef TFBS_ROUND_PROF
         const unsigned long long t4 = RPROF_T();
@@ -664,14 +668,15 @@ __device__ __forceinline__ void scan_segment(const ScanArgs &A, const char *img,
 template <int NK, bool TWO>
 __device__ __forceinline__ void scan_step(const ScanArgs &A, const char *s_img, uint32_t seg, const GroupCtx &G,
                                           uint32_t lane, uint32_t wave, const v4i (&a0)[NK], const v4i (&a1)[NK],
-                                          uint32_t ta, const v16f &cb, int sa, uint32_t &qn, uint32_t &cn) {
+                                          uint32_t ta, uint32_t e0, uint32_t e1, const v16f &cb, int sa, uint32_t &qn,
+                                          uint32_t &cn) {
     uint32_t tb = NK > 2 ? (seg >> 8) & 255u : 0;  // class 4 starts at depth 3 (no tile of depth 1-2)
     const char *img = s_img;
 #define TFBS_SEGMENT(D)                                                                                          \
     if (D <= NK && D + 1 >= NK) { /* a class holds depths NK - 1 and NK (mfma_depth_class) */                  \
         const uint32_t te = (seg >> (8 * (D - 1))) & 255u;                                                     \
         if (te > tb)                                                                                             \
-            scan_segment<(D <= NK ? D : 1), NK, TWO>(A, img, tb, te, G, lane, wave, a0, a1, ta, cb, sa, qn, cn); \
+            scan_segment<(D <= NK ? D : 1), NK, TWO>(A, img, tb, te, G, lane, wave, a0, a1, ta, e0, e1, cb, sa, qn, cn); \
         img += (te - tb) * mfma_tile_bytes(D);                                                                   \
         tb = te;                                                                                                 \
     }
@@ -759,7 +764,10 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
         v4i a0[NK], a1[NK];
         entry_onehot<NK>(A, words, ea, tab, a0);
         entry_onehot<NK>(A, words, eb, tab, a1);  // (a copy of the last window when !two: unused)
+#ifdef TFBS_WENT_LDS
         s_went[wave][lane] = lane < 32 ? ea : eb;  // the firing path's windows (queue_tile)
+#endif
+        const uint32_t e0 = ea, e1 = eb;          // (the firing path's entries: the lane's own)
         if (pn < npair) entries(pn, ea, eb);      // in flight while this pair is scored
 #ifdef TFBS_ROUND_PROF
         // the A fragments awaited here (their LDS reads), so that the pair's first
@@ -768,8 +776,8 @@ __device__ __forceinline__ uint32_t scan_loop(const ScanArgs &A, const DevMSuper
         const unsigned long long tp1 = RPROF_T();
         RPROF_ADD(wave, 7, tp1 - tp0);
 #endif
-        if (two) scan_step<NK, true>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, cb, sa, qn, cn);
-        else scan_step<NK, false>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, cb, sa, qn, cn);
+        if (two) scan_step<NK, true>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, e0, e1, cb, sa, qn, cn);
+        else scan_step<NK, false>(A, s_img, S.seg, G, lane, wave, a0, a1, 2 * p, e0, e1, cb, sa, qn, cn);
         p = pn;
     }
     drain_queue(A, G, qn, wave, lane, cn);  // (the records are self-contained: a drain per super tile)
