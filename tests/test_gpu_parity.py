@@ -590,6 +590,33 @@ def test_run_flow_on_synthetic_bcf_vs_oracle(tmp_path, indel, per_batch, subset,
 
 
 @pytest.mark.parametrize("index", [True, False])
+def test_run_flow_fetch_edges_vs_oracle(tmp_path, index):
+    """The fetch window's edges (parity unpinned by the reference's
+    fixtures): per region an SNV at ext.end (fetched and patched), one at ext.end + 1
+    (outside the half-open fetch(ext.start, ext.end + 1), haplotype.rs:78-79) and a
+    deletion starting left of ext.start that reaches into the window (fetched: its
+    carriers form their own groups; not patched: patch_haplotype keeps diffs with
+    ext.start <= pos, haplotype.rs:95-96).  The product's rows equal the oracle's,
+    which restates htslib's overlap rule (pos < end and pos + rlen > beg); with and
+    without the CSI index."""
+    import gzip
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import synth_dataset
+    d = synth_dataset.make_dataset(str(tmp_path / "data"), n_samples=60, n_regions=12, n_pwms=10,
+                                   length_config=2, seed=13, indel_pct=10, index=index, edges=True)
+    out = tmp_path / "edges.vcf.gz"
+    T.run("chr1", d["bcf"], [d["bed"]], d["fasta"], None, d["pwm_file"], d["thr_dir"], 2e-3, d["names"], str(out),
+          threads=4, regions_per_batch=5)
+    got = gzip.open(str(out), "rt").read()
+    recs = [dict(r, gt=r["gt"].astype(int).tolist()) for r in d["records"]]
+    want = O.run("chr1", recs, [d["bed"]], d["fasta"], d["samples"], d["samples"], d["pwm_file"], d["thr_dir"], 2e-3,
+                 d["names"])
+    assert got == want
+    assert got.count("\n") > 10
+
+
+@pytest.mark.parametrize("index", [True, False])
 def test_run_devices_shards_same_text(tmp_path, index):
     """Multi-device run flow: the merged regions cut into one block per
     listed device, each with its own BCF reader (CSI seek to its block, or a sweep from

@@ -153,10 +153,15 @@ class BgzfStream:
 
 
 def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, seed=3, indel_pct=0, index=True,
-                 keep_gt=True, level=6):
+                 keep_gt=True, level=6, edges=False):
     """keep_gt=False: the returned records carry no GT arrays (large runs: the BCF is
     streamed out region by region, records of a region sorted; regions are 400 bp
-    apart and their extended windows do not overlap, so the file is sorted)."""
+    apart and their extended windows do not overlap, so the file is sorted).
+    edges=True: per region three more records at the fetch window's edges (SURVEY.md
+    8(c), the cases no reference fixture pins): an SNV at the window's last base
+    (pos0 = ext.end), one just past it (pos0 = ext.end + 1: outside the half-open
+    fetch(ext.start, ext.end + 1)), and a 3-base deletion starting two bases left of
+    ext.start that reaches into the window (fetched, left out of the patch)."""
     import tfbs_pkg
     T = tfbs_pkg.load()
     os.makedirs(out, exist_ok=True)
@@ -187,7 +192,18 @@ def make_dataset(out, n_samples=200, n_regions=20, n_pwms=8, length_config=2, se
             es = r.ext_start
             seq[es:es + len(r.ref)] = r.ref.encode()
             recs = []
-            for pos, ref, alt, car in r.records:
+            extra = []
+            if edges:
+                ee = es + len(r.ref) - 1  # ext.end (inclusive)
+                erng = np.random.default_rng(seed * 7919 + j)
+                for p0, rl in ((ee, 1), (ee + 1, 1), (es - 2, 4)):
+                    if p0 < 0:
+                        continue
+                    ref_b = bytes(seq[p0:p0 + rl]).decode()
+                    alt_b = ref_b[0] if rl > 1 else "ACGT"[("ACGT".index(ref_b) + 1 + int(erng.integers(3))) % 4]
+                    car = np.sort(erng.choice(H, size=max(1, H // 5), replace=False))
+                    extra.append((p0, ref_b, alt_b, car.tolist()))
+            for pos, ref, alt, car in list(r.records) + extra:
                 gt = np.empty((n_samples, 2), dtype=np.int8)
                 gt[:, 0] = 2
                 gt[:, 1] = 3
