@@ -93,6 +93,9 @@ struct DevGrouper {
     virtual void recycle(std::vector<void *> &allocs) = 0;
 };
 DevGrouper *make_gpu_grouper(int device);  // build_gpu.hip
+// The HIP runtime and these devices' contexts initialised (0.1-0.4 s in a fresh process):
+// tfbs_run starts it on a thread before it parses its inputs.  build_gpu.hip
+void warm_devices(const std::vector<int> &devices);
 
 struct Batch {
     const Patterns *pats = nullptr;

@@ -320,6 +320,14 @@ struct GpuGrouper final : DevGrouper {
 
 }  // namespace
 
+void warm_devices(const std::vector<int> &devices) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return;
+    for (int d : devices)
+        if (d >= 0 && d < n && hipSetDevice(d) == hipSuccess) (void)hipFree(nullptr);  // (creates the device's context)
+    (void)hipGetLastError();
+}
+
 DevGrouper *make_gpu_grouper(int device) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {

@@ -229,7 +229,9 @@ struct tfbs_ctx {
             int fd, k;
             uint64_t n;
         };
-        std::deque<Job> q;
+        std::deque<Job> q, wq;                     // to copy back; copied, to write (in order)
+        std::thread th2;                           // the writes (th: the copies back)
+        bool copier_done = false;
         bool busy[3] = {false, false, false};      // a job of the slot is queued or running
         bool recorded[3] = {false, false, false};  // its copy back is enqueued (bg_copied[k] recorded)
         bool stop = false;
@@ -691,13 +693,14 @@ void tfbs_ctx_destroy(tfbs_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->rw.th.joinable()) {  // the writes still queued go out first
+    if (ctx->rw.th.joinable()) {  // the jobs still queued go out first
         {
             std::lock_guard<std::mutex> l(ctx->rw.mu);
             ctx->rw.stop = true;
         }
         ctx->rw.cv.notify_all();
         ctx->rw.th.join();
+        if (ctx->rw.th2.joinable()) ctx->rw.th2.join();
     }
     if (ctx->var_owner) {  // its varying counts to the host before var_counts goes
         (void)tfbs::ensure_host_var_counts(*ctx->var_owner);
@@ -1763,15 +1766,23 @@ static int write_out(int fd, const char *p, uint64_t n) {
 // The launched batch in slot k: its packed blocks back (copy stream) and to fd.
 static_assert(tfbs_ctx::kBgSlots == 3, "RowsWriter::busy has a flag per slot");
 
-// The writer thread of rows_set_async: slot writes in queue order.
-static void rows_writer_loop(tfbs_ctx *ctx) {
+// The threads of rows_set_async: the copier takes the drained slots in order, copies
+// each back (the main thread waits for its event to be recorded before it launches
+// into the slot again) and hands it to the writer, which writes them in order -- a
+// slot's copy overlaps the previous slot's write.  TFBS_ROWS_WRITER_DELAY_US: a pause
+// before each copy (tests: the caller runs ahead of the copies).
+static void rows_copier_loop(tfbs_ctx *ctx) {
     auto &w = ctx->rw;
     for (;;) {
         tfbs_ctx::RowsWriter::Job j;
         {
             std::unique_lock<std::mutex> l(w.mu);
             w.cv.wait(l, [&] { return w.stop || !w.q.empty(); });
-            if (w.q.empty()) return;  // (stop with nothing queued)
+            if (w.q.empty()) {  // (stop with nothing queued)
+                w.copier_done = true;
+                w.cv.notify_all();
+                return;
+            }
             j = w.q.front();
             w.q.pop_front();
         }
@@ -1780,11 +1791,8 @@ static void rows_writer_loop(tfbs_ctx *ctx) {
         std::string err;
         {
             std::lock_guard<std::mutex> l(w.mu);
-            rc = w.rc;  // (after a failed write the rest are dropped)
+            rc = w.rc;  // (after a failure the rest are dropped)
         }
-        // the copy back (the main thread waits for its event to be recorded before it
-        // launches into the slot again), then the write; TFBS_ROWS_WRITER_DELAY_US: a
-        // pause first (tests: the caller runs ahead of the copies)
         const int delay_us = env_int("TFBS_ROWS_WRITER_DELAY_US", 0);
         if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
         hipError_t he = hipSetDevice(ctx->device);
@@ -1802,14 +1810,41 @@ static void rows_writer_loop(tfbs_ctx *ctx) {
             rc = TFBS_E_HIP;
             err = std::string("rows copy back: ") + hipGetErrorString(he);
         }
-        const double tc = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        {
+            std::lock_guard<std::mutex> l(w.mu);
+            w.copy_s += t1 - t0;
+            if (rc && !w.rc) {
+                w.rc = rc;
+                w.err = err;
+            }
+            w.wq.push_back(j);
+        }
+        w.cv.notify_all();
+    }
+}
+
+static void rows_writer_loop(tfbs_ctx *ctx) {
+    auto &w = ctx->rw;
+    for (;;) {
+        tfbs_ctx::RowsWriter::Job j;
+        int rc;
+        {
+            std::unique_lock<std::mutex> l(w.mu);
+            w.cv.wait(l, [&] { return !w.wq.empty() || (w.stop && w.copier_done); });
+            if (w.wq.empty()) return;
+            j = w.wq.front();
+            w.wq.pop_front();
+            rc = w.rc;
+        }
+        const double t0 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        std::string err;
         if (!rc && (rc = write_out(j.fd, reinterpret_cast<const char *>(ctx->bg_host[j.k].p), j.n))) err = tfbs_last_error();
         const double t1 = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
         {
             std::lock_guard<std::mutex> l(w.mu);
             w.busy[j.k] = false;
-            w.copy_s += tc - t0;
-            w.write_s += t1 - tc;
+            w.write_s += t1 - t0;
             if (rc && !w.rc) {
                 w.rc = rc;
                 w.err = err;
@@ -1828,7 +1863,7 @@ static int rows_wait(tfbs_ctx *ctx, int k, bool recorded = false) {
         if (k >= 0) return !w.busy[k] || (recorded && w.recorded[k]);
         for (bool b : w.busy)
             if (b) return false;
-        return w.q.empty();
+        return w.q.empty() && w.wq.empty();
     });
     return w.rc ? tfbs::fail(w.rc, w.err) : TFBS_OK;
 }
@@ -1841,7 +1876,10 @@ int bgzf_drain(tfbs_ctx *ctx, int k, int fd, uint64_t &written) {
     const uint64_t total = ctx->bg_total_host[k];
     int r;
     if (ctx->rows_async) {  // the writer thread copies it back and writes it (in order)
-        if (!ctx->rw.th.joinable()) ctx->rw.th = std::thread(rows_writer_loop, ctx);
+        if (!ctx->rw.th.joinable()) {
+            ctx->rw.th = std::thread(rows_copier_loop, ctx);
+            ctx->rw.th2 = std::thread(rows_writer_loop, ctx);
+        }
         if ((r = rows_wait(ctx, k))) return r;  // slot k's last job is done (its host buffer free)
         {
             std::lock_guard<std::mutex> l(ctx->rw.mu);

@@ -1509,19 +1509,9 @@ int launch_key_fast(const AsmArgs &a, uint32_t n_regions, uint32_t n_big, hipStr
     if (n_big)
         hipLaunchKernelGGL(key_fast_kernel<KfBig>, dim3(grid(n_big, per_big)), dim3(KfBig::kBlock), 0, stream, a, 0u,
                            n_big, 1u);
-    if (n_regions > n_big) {
-        // the small shape's persistent grid leaves out the CUs the big shape's
-        // workgroups hold (TFBS_KF_EXCLUDE_BIG=1): a workgroup queued behind them would
-        // start its first region -- by index, one of the larger -- only when they end
-        uint32_t gs = grid(n_regions - n_big, per_small);
-        static const bool exclude = getenv("TFBS_KF_EXCLUDE_BIG") && atoi(getenv("TFBS_KF_EXCLUDE_BIG")) != 0;
-        if (exclude && a.persist && n_big) {
-            const uint32_t held = std::min<uint32_t>(grid(n_big, per_big), (uint32_t)n_cu);
-            gs = std::min(gs, std::max<uint32_t>(1, ((uint32_t)n_cu - held) * (uint32_t)per_small));
-        }
-        hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(gs), dim3(KfSmall::kBlock), 0, two ? side : stream, a, n_big,
-                           n_regions - n_big, 0u);
-    }
+    if (n_regions > n_big)
+        hipLaunchKernelGGL(key_fast_kernel<KfSmall>, dim3(grid(n_regions - n_big, per_small)), dim3(KfSmall::kBlock), 0,
+                           two ? side : stream, a, n_big, n_regions - n_big, 0u);
     if (two) {
         if ((e = hipEventRecord(join, side)) == hipSuccess) e = hipStreamWaitEvent(stream, join, 0);
         if (e != hipSuccess) return fail(TFBS_E_HIP, std::string("key_fast_kernel join: ") + hipGetErrorString(e));

@@ -524,6 +524,14 @@ int tfbs_run(const tfbs_run_args *a) {
     S.chrom = a->chromosome;
     if (a->tabix && (!in_path("bgzip") || !in_path("tabix")))
         return fail(TFBS_E_IO, "bgzip/tabix cannot be found in PATH");  // main.rs:220-223
+    // the HIP runtime's start-up overlaps the PWM / BED / BCF-header parsing below
+    std::thread warm([a] { warm_devices(parse_devices(a)); });
+    struct Joined {
+        std::thread &t;
+        ~Joined() {
+            if (t.joinable()) t.join();
+        }
+    } warm_join{warm};
 
     // patterns (main.rs:237-250)
     int rc = tfbs_patterns_from_files(a->pwm_file, a->pwm_threshold_dir, a->pwm_threshold, a->pwm_names,

@@ -56,6 +56,15 @@ def main():
     del r
     devices = [int(x) for x in a.devices.split(",")] if a.devices else None
     os.environ["TFBS_RUN_TIMING"] = "1"  # per-shard phase seconds on stderr
+    # the process's first device use (HIP runtime, the device's context and code objects:
+    # 0.1-0.6 s, the most on a fresh box) timed apart: a context made and released on
+    # each device before the run's clock -- tfbs_run warms the runtime itself too, so the
+    # run alone does not depend on it; both rates are in the line
+    t = time.perf_counter()
+    warm_ps = T.parse_pwm_files(d["pwm_file"], d["thr_dir"], a.threshold, d["names"])
+    for dev in sorted(set(devices or [0])):
+        T.Scanner(warm_ps, device=dev).close()
+    t_warm = time.perf_counter() - t
     t = time.perf_counter()
     T.run("chr1", d["bcf"], [d["bed"]], d["fasta"], None, d["pwm_file"], d["thr_dir"], a.threshold, d["names"], out,
           threads=a.threads, regions_per_batch=a.regions_per_batch, devices=devices)
@@ -71,6 +80,7 @@ def main():
                     "threshold %g" % (a.samples, a.regions, a.pwms, a.threshold),
         "devices": a.devices or "0", "records": n_rec, "rows": rows, "bcf_bytes": os.path.getsize(d["bcf"]),
         "vcf_gz_bytes": os.path.getsize(out), "run_s": t_run, "regions_per_s": a.regions / t_run,
+        "device_warmup_s": t_warm, "regions_per_s_with_device_warmup": a.regions / (t_run + t_warm),
         "bcf_decode_alone_s": t_bcf, "dataset_gen_s": t_gen, "threads": a.threads,
         "regions_per_batch": a.regions_per_batch}
     if a.oracle_seconds > 0:  # the oracle's end-to-end leg on the same generator (bench.py's CPU baseline)

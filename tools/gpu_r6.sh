@@ -59,7 +59,7 @@ print('$w $v', q['_kernels'], 'MFMA %.3g VALU/MFMA %.2f SALU/MFMA %.2f LDS/MFMA 
       spec=${st#run_}; n=${spec%%:*}; dv=""; [ "$spec" != "$n" ] && dv="--devices ${spec#*:}"
       tag=run_${n}${dv:+_$(echo ${spec#*:} | tr , _)}
       timeout -k 10 900 python3 -u tools/bench_run.py --samples 50000 --regions $n $dv --oracle-seconds 0 > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; exit 1; }
-      grep tfbs_run_timing $O/$tag.err; python3 -c "import json;d=json.load(open('$O/$tag.json'));print('$tag', {k: d[k] for k in ('run_s','regions_per_s','bcf_decode_alone_s','dataset_gen_s','rows','records')})" ;;
+      grep tfbs_run_timing $O/$tag.err; python3 -c "import json;d=json.load(open('$O/$tag.json'));print('$tag', {k: d.get(k) for k in ('run_s','regions_per_s','device_warmup_s','regions_per_s_with_device_warmup','bcf_decode_alone_s','dataset_gen_s','rows','records')})" ;;
     bgzf_*)  # bgzf_<regions>[:<probe>,...]: tools/bgzf_only.py per build, phase clocks (TFBS_BGZF_PROF) then timing
       spec=${st#bgzf_}; n=${spec%%:*}; libs=""; [ "$spec" != "$n" ] && libs=${spec#*:}
       for rep in 1 2; do

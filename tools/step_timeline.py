@@ -12,8 +12,8 @@ import sys
 
 
 def short(n):
-    n = re.sub(r"\(.*", "", n)
     n = re.sub(r"tfbs::|\(anonymous namespace\)::|void ", "", n)
+    n = re.sub(r"\(.*", "", n)
     return n[:48]
 
 
