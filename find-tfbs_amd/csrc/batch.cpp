@@ -980,8 +980,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
     B.haps.resize(cur.hap);
     B.hap_carriers.resize(cur.hap);
     B.inner.resize(cur.inner);
-    B.words.resize(cur.word, 0u);
-    B.nmask.resize(cur.nmask, 0u);
+    B.words.resize(cur.word);  // (uninitialised: every word is written below, pads and tails zeroed)
+    B.nmask.resize(cur.nmask);  // (the same)
     B.posrel.resize(cur.pos);
     B.druns.resize(cur.runs);
     B.regions.resize(region0 + nr);
@@ -1041,6 +1041,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             hm.len = n;
             hm.region = region0 + (uint32_t)j;
             uint32_t *w = B.words.data() + word;
+            std::fill(w + n / 16, w + (n + 15) / 16 + 3, 0u);  // the partial last word and the 3 pads
             if (rb.dev) {  // the reference's words, the SNVs' bases written over
                 std::copy(refw.begin(), refw.end(), w);
                 for (uint64_t x = rb.masks[i]; x; x &= x - 1) {
@@ -1059,6 +1060,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 hm.flags |= HAP_HAS_N;
                 hm.nmask_off = (uint32_t)nmask;
                 uint32_t *m = B.nmask.data() + nmask;
+                std::fill(m, m + (n + 31) / 32 + 2, 0u);
                 for (uint32_t p = 0; p < n; p++)
                     if (d.nuc[p] == 4) m[p / 32] |= 1u << (p % 32);
                 nmask += (n + 31) / 32 + 2;

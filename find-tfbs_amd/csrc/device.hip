@@ -63,7 +63,8 @@ struct DevBuf {
         cap = c;
         return TFBS_OK;
     }
-    int put(const std::vector<T> &v, hipStream_t s) {
+    template <class Alloc>
+    int put(const std::vector<T, Alloc> &v, hipStream_t s) {
         int rc = ensure(v.size());
         if (rc) return rc;
         if (!v.empty()) HIP_TRY(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s));
