@@ -652,6 +652,29 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
         work();
         for (auto &t : ts) t.join();
     };
+    // TFBS_BUILD_PROF: the phases' wall seconds, summed over the calls (debug)
+    static const bool prof = getenv("TFBS_BUILD_PROF") != nullptr;
+    double tp[6] = {0, 0, 0, 0, 0, 0};  // prepare, staging, device grouping, finish, host fallback, (calls)
+    double tq = now();
+    auto lap = [&](int k) {
+        if (!prof) return;
+        const double t = now();
+        tp[k] += t - tq;
+        tq = t;
+    };
+    struct Report {
+        const double *tp;
+        ~Report() {
+            static std::mutex m;
+            static double acc[6];
+            if (!getenv("TFBS_BUILD_PROF")) return;
+            std::lock_guard<std::mutex> g(m);
+            for (int k = 0; k < 5; k++) acc[k] += tp[k];
+            acc[5] += 1;
+            fprintf(stderr, "[build prof] calls %.0f: prepare %.3f staging %.3f grouping %.3f finish %.3f host %.3f s\n",
+                    acc[5], acc[0], acc[1], acc[2], acc[3], acc[4]);
+        }
+    } report{tp};
     // 1: SNV-only, grouped and patched from the masks; 3: grouped on the device,
     // patched on the host (mask_finish); 2: device overflow -> build_region
     par(n, [&](size_t j) {
@@ -695,6 +718,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
                     off += (uint32_t)u[q]->carriers.size();
                 }
             }
+            lap(0);
             uint32_t *car = B.grouper->carriers(ncar);
             if (!car) return fail(TFBS_E_NOMEM, "device grouping staging");
             par(c1 - c0, [&](size_t k) {
@@ -704,8 +728,10 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
                     memcpy(car + g.off, u[q]->carriers.data(), (size_t)g.n * 4);
                 }
             });
+            lap(1);
             GroupOut go;
             if (int rc = B.grouper->group(ncar, recs, regs, H, go)) return rc;
+            lap(2);
             if (go.memb_alloc) B.memb_allocs.push_back(go.memb_alloc);
             par(c1 - c0, [&](size_t c) {
                 const size_t j = dj[c0 + c];
@@ -721,6 +747,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
                                          go.counts.data() + go.first[c], go.n_groups[c], go.memb[c]);
             });
             c0 = c1;
+            lap(3);
         }
         std::vector<size_t> hj;
         for (size_t j = 0; j < n; j++)
@@ -730,6 +757,7 @@ int build_regions(Batch &B, std::vector<RegionInput> &ins, uint32_t threads, std
             built[j] = RegionBuilt();
             rcs[j] = build_region(B, std::move(ins[j]), built[j]);
         });
+        lap(4);
     }
     for (size_t j = 0; j < n; j++) {
         if (rcs[j]) return rcs[j];
