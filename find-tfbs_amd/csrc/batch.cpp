@@ -36,14 +36,12 @@ struct RefWindow {
     uint64_t start;
     size_t n;
     // haplotype.rs:90-92 get(): bases with pos in [s, e]
-    void get(uint64_t s, uint64_t e, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) const {
+    void get(uint64_t s, uint64_t e, std::vector<uint8_t> &nucs, PosRuns &pos) const {
         if (n == 0 || e < s) return;
         const uint64_t lo = std::max(s, start), hi = std::min(e, start + n - 1);
         if (hi < lo) return;
         nucs.insert(nucs.end(), nuc + (lo - start), nuc + (hi - start) + 1);
-        const size_t k = pos.size();
-        pos.resize(k + (hi - lo + 1));
-        for (uint64_t p = lo; p <= hi; p++) pos[k + (p - lo)] = p;
+        pos.push_range(lo, hi);
     }
     // haplotype.rs:119-125: the base at pos, N if absent
     uint8_t at(uint64_t p) const { return (p >= start && p - start < n) ? nuc[p - start] : 4; }
@@ -53,7 +51,7 @@ struct RefWindow {
 // (Diffs already inside [rs, re] and in Diff order -- a group's bits over the sorted
 // distinct records -- are used as they are: no copy, no sort.)
 static int patch_window(uint64_t rs, uint64_t re, const std::vector<const Record *> &diffs_in, const RefWindow &ref,
-                        std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
+                        std::vector<uint8_t> &nucs, PosRuns &pos) {
     bool as_is = true;
     for (size_t i = 0; i < diffs_in.size() && as_is; i++)
         as_is = diffs_in[i]->pos >= rs && diffs_in[i]->pos <= re && (i == 0 || !diff_less(diffs_in[i], diffs_in[i - 1]));
@@ -83,13 +81,13 @@ static int patch_window(uint64_t rs, uint64_t re, const std::vector<const Record
                                 std::to_string(at));
             for (uint8_t a : d->alt) {
                 nucs.push_back(a);
-                pos.push_back(at);
+                pos.push(at);
             }
             at += 1;
             k++;
         } else if (d->pos == at && d->alt.size() == 1) {  // deletion
             nucs.push_back(d->alt[0]);
-            pos.push_back(at);
+            pos.push(at);
             at += d->ref.size();
             k++;
         } else if (d->pos == at) {
@@ -106,7 +104,11 @@ static int patch_window(uint64_t rs, uint64_t re, const std::vector<const Record
 int patch(uint64_t rs, uint64_t re, std::vector<const Record *> diffs, const uint8_t *ref, uint64_t ref_start,
           size_t n_ref, std::vector<uint8_t> &nucs, std::vector<uint64_t> &pos) {
     RefWindow w{ref, ref_start, n_ref};
-    return patch_window(rs, re, diffs, w, nucs, pos);
+    PosRuns runs;
+    const int rc = patch_window(rs, re, diffs, w, nucs, runs);
+    pos.resize(runs.n);
+    runs.expand(pos.data(), [](uint64_t p) { return p; });
+    return rc;
 }
 
 // load_haplotypes' HashMap<(nucs, pos), group> insert (haplotype.rs:84): the
@@ -141,8 +143,13 @@ struct SeqTable {
             h = mix(h, x);
         }
         for (; i < n; i++) h = mix(h, d.nuc[i] | 0x100u);
-        uint64_t ps = 0;  // positions: their offsets from the affine ones, weighted (no branches)
-        for (size_t p = 0; p < n; p++) ps += (d.pos[p] - es - p) * (2 * p + 1);
+        // positions: their offsets from the affine ones, weighted by 2i + 1 (sum over
+        // a run [a, b) of the run's constant offset x (b^2 - a^2), mod 2^64)
+        uint64_t ps = 0;
+        for (size_t k = 0; k < d.pos.r.size(); k++) {
+            const uint64_t a = d.pos.r[k].at, b = d.pos.end(k);
+            ps += (d.pos.r[k].p - es - a) * (b * b - a * a);
+        }
         h = mix(h, ps);
         return h | 1;  // (never 0: the empty mark)
     }
@@ -366,7 +373,6 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
             for (uint32_t t = span_b[rep]; t < span_e[rep]; t++) diffs.push_back(uniq[hd[t].second]);
         Distinct d;
         d.nuc.reserve(R.ee - R.es + 16);
-        d.pos.reserve(R.ee - R.es + 16);
         int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos);
         if (rc) return rc;
         d.group = (int32_t)g;
@@ -391,8 +397,7 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     if (covered < H) {  // haplotypes_with_reference_genome is non-empty (main.rs:129)
         Distinct d;
         d.nuc = I.ref;
-        d.pos.resize(I.ref.size());
-        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.pos = PosRuns::affine(R.es, I.ref.size());
         d.group = -1;
         R.ref_local = (int32_t)dist.size();
         dist.push_back(std::move(d));
@@ -410,8 +415,7 @@ int build_region(const Batch &B, RegionInput &&I, RegionBuilt &out) {
     if (B.dedup && R.ref_local < 0 && reusable && fits(I.ref.size())) {
         Distinct d;
         d.nuc = I.ref;
-        d.pos.resize(I.ref.size());
-        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.pos = PosRuns::affine(R.es, I.ref.size());
         d.group = -2;
         dist.push_back(std::move(d));
         carriers.push_back(0);
@@ -561,7 +565,6 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
         for (uint64_t x = masks[g]; x; x &= x - 1) diffs.push_back(uniq[__builtin_ctzll(x)]);
         Distinct d;
         d.nuc.reserve(R.ee - R.es + 16);
-        d.pos.reserve(R.ee - R.es + 16);
         if (int rc = patch_window(R.es, R.ee, diffs, ref, d.nuc, d.pos)) return rc;
         d.group = (int32_t)g;
         table.insert(dist, std::move(d), R.es);
@@ -578,8 +581,7 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
     if (covered < H) {
         Distinct d;
         d.nuc = I.ref;
-        d.pos.resize(I.ref.size());
-        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.pos = PosRuns::affine(R.es, I.ref.size());
         d.group = -1;
         R.ref_local = (int32_t)dist.size();
         dist.push_back(std::move(d));
@@ -592,8 +594,7 @@ static int mask_finish(const Batch &B, RegionInput &I, RegionBuilt &out, const s
     if (B.dedup && R.ref_local < 0 && reusable && fits(I.ref.size())) {
         Distinct d;
         d.nuc = I.ref;
-        d.pos.resize(I.ref.size());
-        for (size_t i = 0; i < d.pos.size(); i++) d.pos[i] = R.es + i;
+        d.pos = PosRuns::affine(R.es, I.ref.size());
         d.group = -2;
         dist.push_back(std::move(d));
         carriers.push_back(0);
@@ -860,9 +861,7 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             HapInfo &h = info[j][i];
             h.n = (uint32_t)d.nuc.size();
             h.has_n = h.n && memchr(d.nuc.data(), 4, h.n) != nullptr;
-            uint64_t off = 0;  // (no early exit: the loop vectorises)
-            for (uint32_t p = 0; p < h.n; p++) off |= d.pos[p] ^ (rb.R.es + p);
-            h.affine = off == 0;
+            h.affine = d.pos.is_affine(rb.R.es);
         }
         // reference-window reuse: a window whose bases equal those of the reference
         // window that starts at its first base's position has that window's score and
@@ -912,10 +911,13 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
             uint32_t a, b, qa;  // columns [a, b) at reference columns [qa, qa + b - a)
         };
         std::vector<Seg> segs;
+        std::vector<uint64_t> dpos;  // the haplotype's positions, expanded from its runs
         for (size_t i = 0; i < rb.dist.size(); i++) {
             HapInfo &h = info[j][i];
             if ((int32_t)i == ref || h.n > kDedupMaxWindows) continue;
             const Distinct &d = rb.dist[i];
+            dpos.resize(h.n);
+            d.pos.expand(dpos.data(), [](uint64_t p) { return p; });
             segs.clear();
             uint32_t qend = 0;  // the last segment's reference end (exclusive)
             bool open = false;
@@ -923,20 +925,20 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 if (open) {  // 8 columns at a time while the segment goes on (consecutive
                     // positions, bases equal to the reference's at them)
                     for (;;) {
-                        const uint64_t at = d.pos[p - 1] + 1, qq = at - rb.R.es;
+                        const uint64_t at = dpos[p - 1] + 1, qq = at - rb.R.es;
                         if (p + 8 > h.n || qq + 8 > m) break;
                         uint64_t x, y, off = 0;
                         memcpy(&x, d.nuc.data() + p, 8);
                         memcpy(&y, rn.data() + qq, 8);
-                        for (uint32_t k = 0; k < 8; k++) off |= d.pos[p + k] ^ (at + k);
+                        for (uint32_t k = 0; k < 8; k++) off |= dpos[p + k] ^ (at + k);
                         if (x != y || off) break;
                         p += 8;
                     }
                     if (p >= h.n) break;
                 }
-                const int64_t q = (int64_t)d.pos[p] - (int64_t)rb.R.es;
+                const int64_t q = (int64_t)dpos[p] - (int64_t)rb.R.es;
                 const bool ok = q >= 0 && q < (int64_t)m && d.nuc[p] == rn[(size_t)q];
-                if (open && ok && d.pos[p] == d.pos[p - 1] + 1) continue;  // the segment goes on
+                if (open && ok && dpos[p] == dpos[p - 1] + 1) continue;  // the segment goes on
                 if (open) {
                     segs.back().b = p;
                     qend = segs.back().qa + (p - segs.back().a);
@@ -1097,7 +1099,8 @@ void commit_regions(Batch &B, std::vector<RegionBuilt> &built, uint32_t threads)
                 const Distinct &d = rb.dist[i];
                 hm.flags |= HAP_HAS_POS;
                 hm.pos_off = (uint32_t)pos;
-                for (uint32_t p = 0; p < n; p++) B.posrel[pos + p] = (int32_t)(d.pos[p] - R.es);
+                const uint64_t es = R.es;
+                d.pos.expand(B.posrel.data() + pos, [es](uint64_t p) { return (int32_t)(p - es); });
                 pos += n;
             }
             hm.count_off = count + i;  // key-major: [key][haplotype]

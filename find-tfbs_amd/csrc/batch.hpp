@@ -230,9 +230,47 @@ struct RegionInput {  // one merged region as the reader hands it over
     std::vector<std::pair<uint32_t, std::pair<uint64_t, uint64_t>>> inner;  // (bed, (s, e))
 };
 
+// A haplotype's positions (haplotype.rs's pos vector) as maximal runs of consecutive
+// positions: run k covers bases [r[k].at, r[k + 1].at) (the last to n) at positions
+// r[k].p, r[k].p + 1, ...  One run unless an indel breaks it, so a distinct haplotype
+// holds ~1 byte per base instead of 9 (the batch build's first-touch page faults were
+// most of a cold C5 build).  The runs are canonical (each starts where the previous
+// one's positions stop being consecutive), so equal runs <=> equal position vectors.
+struct PosRun {
+    uint32_t at;
+    uint64_t p;
+    bool operator==(const PosRun &o) const { return at == o.at && p == o.p; }
+};
+struct PosRuns {
+    std::vector<PosRun> r;
+    uint32_t n = 0;  // positions
+    bool extends(uint64_t p) const { return n && r.back().p + (n - r.back().at) == p; }
+    void push(uint64_t p) {  // one position
+        if (!extends(p)) r.push_back({n, p});
+        n++;
+    }
+    void push_range(uint64_t lo, uint64_t hi) {  // positions lo ..= hi
+        if (!extends(lo)) r.push_back({n, lo});
+        n += (uint32_t)(hi - lo + 1);
+    }
+    static PosRuns affine(uint64_t start, size_t count) {  // start, start + 1, ...
+        PosRuns x;
+        if (count) x.push_range(start, start + count - 1);
+        return x;
+    }
+    bool is_affine(uint64_t start) const { return n == 0 || (r.size() == 1 && r[0].p == start); }
+    uint32_t end(size_t k) const { return k + 1 < r.size() ? r[k + 1].at : n; }
+    template <class T, class F>
+    void expand(T *out, F &&f) const {  // out[i] = f(position of base i)
+        for (size_t k = 0; k < r.size(); k++)
+            for (uint32_t i = r[k].at, e = end(k); i < e; i++) out[i] = f(r[k].p + (i - r[k].at));
+    }
+    bool operator==(const PosRuns &o) const { return n == o.n && r == o.r; }
+};
+
 struct Distinct {  // one distinct haplotype (a key of load_haplotypes' HashMap)
     std::vector<uint8_t> nuc;
-    std::vector<uint64_t> pos;
+    PosRuns pos;
     int32_t group;
 };
 

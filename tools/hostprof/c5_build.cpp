@@ -130,9 +130,29 @@ int main(int argc, char **argv) {
         auto t1 = std::chrono::steady_clock::now();
         commit_regions(bb->b, built, T);
         auto t2 = std::chrono::steady_clock::now();
+        size_t bytes = 0;
+        for (const RegionBuilt &rb : built)
+            for (const Distinct &d : rb.dist) bytes += d.nuc.capacity() + d.pos.r.capacity() * sizeof(PosRun);
+        printf("rep %d: build %.3f s (less the grouper), commit %.3f s, the distinct haplotypes' sequences %.1f MB\n",
+               rep, std::chrono::duration<double>(t1 - t0).count() - gr->secs,
+               std::chrono::duration<double>(t2 - t1).count(), bytes / 1e6);
         best_b = std::min(best_b, std::chrono::duration<double>(t1 - t0).count() - gr->secs);
         best_c = std::min(best_c, std::chrono::duration<double>(t2 - t1).count());
         gsec = gr->secs;
+        if (rep == 0) {  // a digest of the committed batch image (words, N masks, positions, runs, descriptors)
+            uint64_t h = 1469598103934665603ull;
+            auto mixb = [&](const void *p, size_t n) {
+                const uint8_t *c = (const uint8_t *)p;
+                for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+            };
+            mixb(bb->b.words.data(), bb->b.words.size() * 4);
+            mixb(bb->b.nmask.data(), bb->b.nmask.size() * 4);
+            mixb(bb->b.posrel.data(), bb->b.posrel.size() * 4);
+            mixb(bb->b.druns.data(), bb->b.druns.size() * 4);
+            mixb(bb->b.haps.data(), bb->b.haps.size() * sizeof(bb->b.haps[0]));
+            printf("batch image digest %016llx (words %zu, posrel %zu, druns %zu)\n", (unsigned long long)h,
+                   (size_t)bb->b.words.size(), (size_t)bb->b.posrel.size(), (size_t)bb->b.druns.size());
+        }
         haps = bb->b.haps.size();
         patched = bb->b.patched_regions;
         tfbs_batch_destroy(bb);
