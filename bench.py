@@ -42,6 +42,7 @@ same library build) and the CPU baseline (the oracle, scan-only and end-to-end,
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import tempfile
@@ -72,7 +73,10 @@ WORKLOADS = {  # samples, regions per GPU, pwms, length config, indel %, seed
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: as many as fill --min-seconds, at least 5, from the warmup's pace)")
+    ap.add_argument("--min-seconds", type=float, default=5.0,
+                    help="without --steps: the timed loop's length to aim for (long enough for a GPU-busy sampler)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     ap.add_argument("--regions", type=int, default=None, help="regions per GPU (workload default)")
@@ -406,6 +410,19 @@ def main():
     for _ in range(args.warmup):
         step()
     T.check(L.tfbs_ctx_sync(sc.h))
+    if args.steps is None:  # K from the pace of a few more untimed steps (every rank the same K: the max)
+        t = time.perf_counter()
+        for _ in range(3):
+            step()
+        T.check(L.tfbs_ctx_sync(sc.h))
+        pace = (time.perf_counter() - t) / 3
+        k = max(5, min(100000, int(math.ceil(args.min_seconds / max(pace, 1e-6)))))
+        if dist is not None:
+            import torch
+            kt = torch.tensor([k], dtype=torch.int64, device=rdev)
+            dist.all_reduce(kt, op=dist.ReduceOp.MAX)
+            k = int(kt.item())
+        args.steps = k
 
     def barrier():
         if dist is not None:
