@@ -273,14 +273,23 @@ struct tfbs_ctx {
 namespace tfbs {
 int PinnedBytes::reserve(size_t n) {
     if (n <= cap) return TFBS_OK;
+    // geometric with headroom (page-locking is slow: ~5 ms per 20 MB; the BGZF slots' batches
+    // vary 2x in size, and each regrowth stalled the GPU between a batch and its copy back).
+    // (The old capacity is read before release() clears it: until round 6 it was read after,
+    // so every growth was to the exact size.)
+    size_t want = std::max<size_t>({n + n / 2, 2 * cap, (size_t)1 << 20});
     release();
-    const size_t want = std::max<size_t>({n, cap + cap / 2, (size_t)1 << 20});  // geometric: page-locking is slow
-    if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) == hipSuccess) {
-        pinned = true;
-    } else {  // page-locked memory exhausted: pageable memory (slower copies, same results)
+    if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
+        want = n;  // the exact size, then pageable memory
+        if (hipHostMalloc((void **)&p, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            p = nullptr;
+        }
+    }
+    pinned = p != nullptr;
+    if (!pinned) {  // page-locked memory exhausted: pageable memory (slower copies, same results)
         p = static_cast<uint8_t *>(malloc(want));
-        pinned = false;
         if (!p) return tfbs::fail(TFBS_E_NOMEM, "host staging buffer");
     }
     cap = want;
